@@ -1,0 +1,99 @@
+// mirror.h — the ClusterSnapshot mirror: host journal + device SoA rows.
+//
+// Host side keeps the authoritative rows (so Fork/Revert/Commit are O(changes),
+// DeltaClusterSnapshot semantics, CA/simulator/clustersnapshot/delta.go:43-475);
+// device rows are re-synchronised lazily (dirty rows only) before a kernel reads them.
+#pragma once
+#include "casim_internal.h"
+#include <array>
+
+namespace casim {
+
+enum { J_FORK = 1, J_ADD_NODE, J_ADD_POD, J_REMOVE_POD };
+
+struct JournalEntry {
+    int32_t kind, node, pod, slot;
+    uint64_t ports[CA_PORT_WORDS];
+};
+
+struct NodeRow {
+    ca_node_spec spec;
+    int64_t req_cpu = 0, req_mem = 0, req_eph = 0;
+    int64_t req_scalar[CA_MAX_SCALAR] = {0};
+    int64_t npods = 0;
+    uint64_t ports[CA_PORT_WORDS] = {0};
+    std::vector<int32_t> pods;   // NodeInfo.Pods order
+};
+
+struct PodRow {
+    ca_pod_spec spec;            // selector indices re-based on the mirror tables
+    int32_t node = -1;
+};
+
+struct ca_mirror_impl;
+
+// Device pod table: hot rows + full records + selector tables.
+struct DevPodTable {
+    DevBuf hot, spec, terms, reqs, names;
+    int32_t n_pods = 0, n_terms = 0, n_reqs = 0, n_names = 0;
+    int upload(const ca_pod_spec* pods, int32_t n, const ca_selector_term* terms, int32_t nt,
+               const ca_selector_req* reqs, int32_t nr, const int32_t* names, int32_t nn, hipStream_t st);
+};
+
+struct Stats {
+    int32_t rounds = 0;
+    float kernel_ms = 0, sort_ms = 0, total_ms = 0;
+};
+
+}  // namespace casim
+
+struct ca_mirror {
+    int32_t device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+
+    std::vector<casim::NodeRow> nodes;
+    std::vector<casim::PodRow> pods;
+    std::vector<ca_selector_term> terms;
+    std::vector<ca_selector_req> reqs;
+    std::vector<int32_t> pf_names;
+    std::vector<casim::JournalEntry> journal;
+    int32_t depth = 0;
+
+    // device rows
+    casim::DevBuf d_hot, d_ext, d_static;
+    size_t d_cap = 0;                      // rows allocated
+    size_t d_rows = 0;                     // rows valid on device
+    std::vector<int32_t> dirty_rows;       // rows whose dynamic part changed
+    std::vector<uint8_t> dirty_flag;
+    bool static_dirty = true;              // static/ext columns need a full upload
+    bool all_dirty = true;
+
+    // device pod table (mirror pods), appended lazily
+    casim::DevPodTable d_pods;
+    size_t d_pods_synced = 0;              // pods whose records are on device
+    size_t d_terms_synced = 0;
+
+    // scratch
+    casim::DevBuf d_scratch0, d_scratch1, d_scratch2, d_scratch3;
+    casim::DevBuf d_mask;                  // per-node match mask
+    std::vector<uint8_t> h_scratch;
+    casim::Stats sweep_stats;
+
+    int sync_nodes();                      // push dirty rows to the device
+    int sync_pods();                       // push new pod records to the device
+    void mark_dirty(int32_t node);
+    void node_apply(int32_t node, const ca_pod_spec& p, int sign);
+    void add_pod_to_node(int32_t pod, int32_t node);
+    int32_t store_pod(const ca_pod_table* t, int32_t idx, int32_t node);
+    void journal_push(int32_t kind, int32_t node, int32_t pod, int32_t slot, const uint64_t* ports);
+    void fill_hot(int32_t i, casim::NodeHot& h) const;
+    void fill_ext(int32_t i, casim::NodeExt& e) const;
+    void fill_static(int32_t i, casim::NodeStatic& s) const;
+};
+
+struct ca_podset {
+    ca_mirror* m = nullptr;
+    casim::DevPodTable t;
+    std::vector<ca_pod_spec> h_pods;   // host copy (flags, used for classification)
+};

@@ -1,0 +1,694 @@
+// mirror.hip — ClusterSnapshot mirror (host journal + device SoA), the C-ABI entry
+// points for the snapshot data plane, and the single-pod predicate kernels
+// (FitsAnyNode scan, CheckPredicates, dense feasibility matrix).
+//
+// Reference: CA/simulator/clustersnapshot/delta.go:43-475 (fork/revert/commit),
+// SF/types.go:602-692 (AddPod/RemovePod/update), CA/simulator/predicatechecker/
+// schedulerbased.go:83-185 (FitsAnyNodeMatching, CheckPredicates).
+#include "mirror.h"
+#include "device_filters.h"
+
+#include <cstring>
+#include <mutex>
+#include <algorithm>
+
+namespace casim {
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& s) { g_last_error = s; }
+
+int DevBuf::reserve(size_t need) {
+    if (need <= bytes) return CA_OK;
+    release();
+    size_t sz = std::max<size_t>(need, 256);
+    if (hipMalloc(&ptr, sz) != hipSuccess) { ptr = nullptr; bytes = 0; set_last_error("hipMalloc failed"); return CA_EDEVICE; }
+    bytes = sz;
+    return CA_OK;
+}
+
+int DevBuf::reserve_keep(size_t need, hipStream_t st) {
+    if (need <= bytes) return CA_OK;
+    size_t sz = std::max<size_t>(need, bytes * 2);
+    void* p = nullptr;
+    if (hipMalloc(&p, sz) != hipSuccess) { set_last_error("hipMalloc failed"); return CA_EDEVICE; }
+    if (ptr && bytes) {
+        if (hipMemcpyAsync(p, ptr, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess) return CA_EDEVICE;
+        if (hipStreamSynchronize(st) != hipSuccess) return CA_EDEVICE;
+        (void)hipFree(ptr);
+    }
+    ptr = p;
+    bytes = sz;
+    return CA_OK;
+}
+
+void DevBuf::release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+}
+
+int DevPodTable::upload(const ca_pod_spec* pods, int32_t n, const ca_selector_term* tms, int32_t nt,
+                        const ca_selector_req* rqs, int32_t nr, const int32_t* nms, int32_t nn,
+                        hipStream_t st) {
+    std::vector<PodHot> h((size_t)n);
+    for (int32_t i = 0; i < n; i++) {
+        h[i].cpu = pods[i].req_milli_cpu;
+        h[i].mem = pods[i].req_memory;
+        h[i].eph = pods[i].req_ephemeral;
+        h[i].flags = pod_dev_flags(pods[i]);
+        h[i].spec = i;
+    }
+    int rc;
+    if ((rc = hot.reserve(sizeof(PodHot) * (size_t)(n + 1))) != CA_OK) return rc;
+    if ((rc = spec.reserve(sizeof(ca_pod_spec) * (size_t)(n + 1))) != CA_OK) return rc;
+    if ((rc = terms.reserve(sizeof(ca_selector_term) * (size_t)(nt + 1))) != CA_OK) return rc;
+    if ((rc = reqs.reserve(sizeof(ca_selector_req) * (size_t)(nr + 1))) != CA_OK) return rc;
+    if ((rc = names.reserve(sizeof(int32_t) * (size_t)(nn + 1))) != CA_OK) return rc;
+    if (n) CA_HIP_CHECK(hipMemcpyAsync(hot.ptr, h.data(), sizeof(PodHot) * n, hipMemcpyHostToDevice, st));
+    if (n) CA_HIP_CHECK(hipMemcpyAsync(spec.ptr, pods, sizeof(ca_pod_spec) * n, hipMemcpyHostToDevice, st));
+    if (nt) CA_HIP_CHECK(hipMemcpyAsync(terms.ptr, tms, sizeof(ca_selector_term) * nt, hipMemcpyHostToDevice, st));
+    if (nr) CA_HIP_CHECK(hipMemcpyAsync(reqs.ptr, rqs, sizeof(ca_selector_req) * nr, hipMemcpyHostToDevice, st));
+    if (nn) CA_HIP_CHECK(hipMemcpyAsync(names.ptr, nms, sizeof(int32_t) * nn, hipMemcpyHostToDevice, st));
+    CA_HIP_CHECK(hipStreamSynchronize(st));
+    n_pods = n; n_terms = nt; n_reqs = nr; n_names = nn;
+    return CA_OK;
+}
+
+}  // namespace casim
+
+using namespace casim;
+
+// ---------------------------------------------------------------------------
+// host row algebra (NodeInfo.update SF/types.go:672-692)
+// ---------------------------------------------------------------------------
+void ca_mirror::mark_dirty(int32_t node) {
+    if ((size_t)node >= dirty_flag.size()) dirty_flag.resize(nodes.size(), 0);
+    if (!dirty_flag[node]) {
+        dirty_flag[node] = 1;
+        dirty_rows.push_back(node);
+    }
+}
+
+void ca_mirror::node_apply(int32_t node, const ca_pod_spec& p, int sign) {
+    NodeRow& nd = nodes[node];
+    if (sign > 0) {
+        nd.req_cpu = wadd(nd.req_cpu, p.req_milli_cpu);
+        nd.req_mem = wadd(nd.req_mem, p.req_memory);
+        nd.req_eph = wadd(nd.req_eph, p.req_ephemeral);
+        for (int i = 0; i < CA_MAX_SCALAR; i++) nd.req_scalar[i] = wadd(nd.req_scalar[i], p.req_scalar[i]);
+        for (int w = 0; w < CA_PORT_WORDS; w++) nd.ports[w] |= p.port_use[w];
+    } else {
+        nd.req_cpu = wsub(nd.req_cpu, p.req_milli_cpu);
+        nd.req_mem = wsub(nd.req_mem, p.req_memory);
+        nd.req_eph = wsub(nd.req_eph, p.req_ephemeral);
+        for (int i = 0; i < CA_MAX_SCALAR; i++) nd.req_scalar[i] = wsub(nd.req_scalar[i], p.req_scalar[i]);
+        // HostPortInfo.Remove deletes the triple (set semantics, SF/types.go:863-880)
+        for (int w = 0; w < CA_PORT_WORDS; w++) nd.ports[w] &= ~p.port_use[w];
+    }
+    nd.npods += sign;
+    mark_dirty(node);
+}
+
+void ca_mirror::journal_push(int32_t kind, int32_t node, int32_t pod, int32_t slot, const uint64_t* ports) {
+    if (depth == 0 && kind != J_FORK) return;
+    JournalEntry e;
+    std::memset(&e, 0, sizeof e);
+    e.kind = kind; e.node = node; e.pod = pod; e.slot = slot;
+    if (ports) std::memcpy(e.ports, ports, sizeof e.ports);
+    journal.push_back(e);
+}
+
+void ca_mirror::add_pod_to_node(int32_t pod, int32_t node) {
+    uint64_t before[CA_PORT_WORDS];
+    std::memcpy(before, nodes[node].ports, sizeof before);
+    node_apply(node, pods[pod].spec, +1);
+    nodes[node].pods.push_back(pod);
+    pods[pod].node = node;
+    journal_push(J_ADD_POD, node, pod, (int32_t)nodes[node].pods.size() - 1, before);
+}
+
+int32_t ca_mirror::store_pod(const ca_pod_table* t, int32_t idx, int32_t node) {
+    PodRow row;
+    row.spec = t->pods[idx];
+    row.node = node;
+    if (row.spec.aff_term_count > 0) {
+        int32_t first = (int32_t)terms.size();
+        for (int32_t k = 0; k < row.spec.aff_term_count; k++) {
+            ca_selector_term tm = t->terms[row.spec.aff_term_first + k];
+            int32_t rfirst = (int32_t)reqs.size();
+            for (int32_t r = 0; r < tm.count; r++) reqs.push_back(t->reqs[tm.first + r]);
+            tm.first = rfirst;
+            terms.push_back(tm);
+        }
+        row.spec.aff_term_first = first;
+    }
+    if ((row.spec.flags & CA_POD_PREFILTER_NAMES) && row.spec.prefilter_count > 0) {
+        int32_t first = (int32_t)pf_names.size();
+        for (int32_t k = 0; k < row.spec.prefilter_count; k++)
+            pf_names.push_back(t->prefilter_names[row.spec.prefilter_first + k]);
+        row.spec.prefilter_first = first;
+    }
+    pods.push_back(row);
+    return (int32_t)pods.size() - 1;
+}
+
+void ca_mirror::fill_hot(int32_t i, NodeHot& h) const {
+    const NodeRow& nd = nodes[i];
+    h.cpu = wsub(nd.spec.alloc_milli_cpu, nd.req_cpu);
+    h.mem = wsub(nd.spec.alloc_memory, nd.req_mem);
+    h.eph = wsub(nd.spec.alloc_ephemeral, nd.req_eph);
+    h.pods = clamp_i32(nd.spec.alloc_pods - nd.npods);
+    uint32_t f = NF_VALID;
+    if (nd.spec.flags & CA_NODE_UNSCHEDULABLE) f |= NF_UNSCHED;
+    if (nd.spec.taints) f |= NF_TAINTS;
+    bool ports = false;
+    for (int w = 0; w < CA_PORT_WORDS; w++) ports |= nd.ports[w] != 0;
+    if (ports) f |= NF_PORTS;
+    bool sc = false;
+    for (int k = 0; k < CA_MAX_SCALAR; k++) sc |= nd.spec.alloc_scalar[k] != 0 || nd.req_scalar[k] != 0;
+    if (sc) f |= NF_SCALAR;
+    h.flags = f;
+}
+
+void ca_mirror::fill_ext(int32_t i, NodeExt& e) const {
+    const NodeRow& nd = nodes[i];
+    for (int k = 0; k < CA_MAX_SCALAR; k++) e.scalar[k] = wsub(nd.spec.alloc_scalar[k], nd.req_scalar[k]);
+    for (int w = 0; w < CA_PORT_WORDS; w++) e.ports[w] = nd.ports[w];
+}
+
+void ca_mirror::fill_static(int32_t i, NodeStatic& s) const {
+    const ca_node_spec& n = nodes[i].spec;
+    std::memset(&s, 0, sizeof s);
+    s.taints = n.taints;
+    for (int w = 0; w < CA_LABEL_WORDS; w++) s.labels[w] = n.label_pairs[w];
+    s.keys = n.label_keys;
+    for (int k = 0; k < CA_MAX_INT_KEYS; k++) s.ints[k] = n.int_label[k];
+    s.int_valid = n.int_label_valid;
+    s.name_id = n.name_id;
+}
+
+int ca_mirror::sync_nodes() {
+    const size_t n = nodes.size();
+    int rc;
+    if (n > d_cap) {
+        size_t cap = std::max<size_t>(n, std::max<size_t>(1024, d_cap * 2));
+        if ((rc = d_hot.reserve(sizeof(NodeHot) * cap)) != CA_OK) return rc;
+        if ((rc = d_ext.reserve(sizeof(NodeExt) * cap)) != CA_OK) return rc;
+        if ((rc = d_static.reserve(sizeof(NodeStatic) * cap)) != CA_OK) return rc;
+        d_cap = cap;
+        all_dirty = true;
+        static_dirty = true;
+    }
+    if (n > d_rows) {
+        // new rows (AddNode): upload them fully
+        for (size_t i = d_rows; i < n; i++) mark_dirty((int32_t)i);
+        static_dirty = true;
+    }
+    if (all_dirty || dirty_rows.size() > 64) {
+        std::vector<NodeHot> h(n);
+        std::vector<NodeExt> e(n);
+        for (size_t i = 0; i < n; i++) { fill_hot((int32_t)i, h[i]); fill_ext((int32_t)i, e[i]); }
+        if (n) CA_HIP_CHECK(hipMemcpyAsync(d_hot.ptr, h.data(), sizeof(NodeHot) * n, hipMemcpyHostToDevice, stream));
+        if (n) CA_HIP_CHECK(hipMemcpyAsync(d_ext.ptr, e.data(), sizeof(NodeExt) * n, hipMemcpyHostToDevice, stream));
+        CA_HIP_CHECK(hipStreamSynchronize(stream));
+    } else if (!dirty_rows.empty()) {
+        for (int32_t r : dirty_rows) {
+            NodeHot h; NodeExt e;
+            fill_hot(r, h); fill_ext(r, e);
+            CA_HIP_CHECK(hipMemcpyAsync(d_hot.as<NodeHot>() + r, &h, sizeof h, hipMemcpyHostToDevice, stream));
+            CA_HIP_CHECK(hipMemcpyAsync(d_ext.as<NodeExt>() + r, &e, sizeof e, hipMemcpyHostToDevice, stream));
+            CA_HIP_CHECK(hipStreamSynchronize(stream));   // h/e are stack temporaries
+        }
+    }
+    if (static_dirty && n) {
+        std::vector<NodeStatic> s(n);
+        for (size_t i = 0; i < n; i++) fill_static((int32_t)i, s[i]);
+        CA_HIP_CHECK(hipMemcpyAsync(d_static.ptr, s.data(), sizeof(NodeStatic) * n, hipMemcpyHostToDevice, stream));
+        CA_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+    for (int32_t r : dirty_rows) if ((size_t)r < dirty_flag.size()) dirty_flag[r] = 0;
+    dirty_rows.clear();
+    all_dirty = false;
+    static_dirty = false;
+    d_rows = n;
+    return CA_OK;
+}
+
+int ca_mirror::sync_pods() {
+    if (d_pods_synced == pods.size() && d_terms_synced == terms.size()) return CA_OK;
+    std::vector<ca_pod_spec> specs(pods.size());
+    for (size_t i = 0; i < pods.size(); i++) specs[i] = pods[i].spec;
+    int rc = d_pods.upload(specs.data(), (int32_t)specs.size(), terms.data(), (int32_t)terms.size(),
+                           reqs.data(), (int32_t)reqs.size(), pf_names.data(), (int32_t)pf_names.size(), stream);
+    if (rc != CA_OK) return rc;
+    d_pods_synced = pods.size();
+    d_terms_synced = terms.size();
+    return CA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// kernels: FitsAnyNodeMatching scan, CheckPredicates, feasibility matrix
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_fits_scan(
+    const NodeHot* __restrict__ hot, const NodeExt* __restrict__ ext, const NodeStatic* __restrict__ st,
+    int32_t n, const PodHot* __restrict__ ph, const ca_pod_spec* __restrict__ specs,
+    const ca_selector_term* __restrict__ terms, const ca_selector_req* __restrict__ reqs,
+    const int32_t* __restrict__ names, int32_t pod, int64_t L, int32_t kind, int32_t lo, int32_t hi,
+    int32_t exclude, const uint8_t* __restrict__ mask, unsigned long long* __restrict__ out_fit,
+    unsigned long long* __restrict__ out_vis) {
+    const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);   // rotated offset
+    const PodHot p = ph[pod];
+    bool vis = false, fit = false;
+    if (i < n) {
+        const int32_t pos = (int32_t)((L + i) % n);                       // schedulerbased.go:115
+        bool m = pos != exclude;
+        if (kind == CA_MATCH_RANGE) m = m && pos >= lo && pos < hi;
+        else if (kind == CA_MATCH_MASK) m = m && mask[pos] != 0;
+        if (m) {
+            const NodeHot h = hot[pos];
+            bool pf_ok = true;
+            if (p.flags & PF_PREFILTER_NAMES) {                            // :120
+                const ca_pod_spec& s = specs[p.spec];
+                const int32_t nm = st[pos].name_id;
+                pf_ok = false;
+                for (int32_t k = 0; k < s.prefilter_count; k++) pf_ok |= names[s.prefilter_first + k] == nm;
+            }
+            if (pf_ok && !(h.flags & NF_UNSCHED)) {                        // :125
+                vis = true;
+                uint32_t reasons;
+                fit = dev_full_filters(specs[p.spec], p, terms, reqs, h, ext + pos, st + pos, false, &reasons)
+                      == CA_PLUGIN_NONE;
+            }
+        }
+    }
+    const unsigned long long bf = __ballot(fit), bv = __ballot(vis);
+    const int32_t w = i >> 6;
+    if ((threadIdx.x & 63) == 0 && (int64_t)w * 64 < n) { out_fit[w] = bf; out_vis[w] = bv; }
+}
+
+__global__ void k_check_one(const NodeHot* __restrict__ hot, const NodeExt* __restrict__ ext,
+                            const NodeStatic* __restrict__ st, const PodHot* __restrict__ ph,
+                            const ca_pod_spec* __restrict__ specs, const ca_selector_term* __restrict__ terms,
+                            const ca_selector_req* __restrict__ reqs, int32_t pod, int32_t node,
+                            ca_pred_result* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    const PodHot p = ph[pod];
+    ca_pred_result r;
+    r.type = CA_PRED_OK; r.plugin = 0; r.reasons = 0; r.taint = 0;
+    uint32_t reasons = 0;
+    const int plugin = dev_full_filters(specs[p.spec], p, terms, reqs, hot[node], ext + node, st + node, true, &reasons);
+    if (plugin != CA_PLUGIN_NONE) {
+        r.type = CA_PRED_NOT_SCHEDULABLE;
+        r.plugin = plugin;
+        r.reasons = reasons;
+        if (plugin == CA_PLUGIN_TAINT_TOLERATION) {
+            const uint64_t u = st[node].taints & ~specs[p.spec].tolerated_taints;
+            r.taint = (int32_t)__builtin_ctzll(u);
+        }
+    }
+    *out = r;
+}
+
+// Dense pods x nodes feasibility (CheckPredicates semantics, PreFilter failure -> 0).
+// One thread per (pod, node); nodes on the fast axis for coalesced node rows.
+__global__ void __launch_bounds__(256) k_fits_matrix(
+    const NodeHot* __restrict__ hot, const NodeExt* __restrict__ ext, const NodeStatic* __restrict__ st,
+    int32_t n, const PodHot* __restrict__ ph, const ca_pod_spec* __restrict__ specs,
+    const ca_selector_term* __restrict__ terms, const ca_selector_req* __restrict__ reqs,
+    int32_t n_pods, uint8_t* __restrict__ out) {
+    const int32_t node = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int32_t pod = (int32_t)blockIdx.y;
+    if (node >= n || pod >= n_pods) return;
+    const PodHot p = ph[pod];
+    uint8_t ok = 0;
+    if (!(p.flags & PF_PREFILTER_FAIL)) {
+        uint32_t reasons;
+        ok = dev_full_filters(specs[p.spec], p, terms, reqs, hot[node], ext + node, st + node, true, &reasons)
+             == CA_PLUGIN_NONE;
+    }
+    out[(size_t)pod * n + node] = ok;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int ca_abi_version(void) { return CASIM_ABI_VERSION; }
+
+int ca_abi_struct_sizes(int32_t* out, int32_t cap) {
+    const int32_t s[] = {(int32_t)sizeof(ca_node_spec), (int32_t)sizeof(ca_pod_spec),
+                         (int32_t)sizeof(ca_selector_req), (int32_t)sizeof(ca_selector_term),
+                         (int32_t)sizeof(ca_pod_table), (int32_t)sizeof(ca_match_spec),
+                         (int32_t)sizeof(ca_pred_result), (int32_t)sizeof(ca_template),
+                         (int32_t)sizeof(ca_limiter), (int32_t)sizeof(ca_estimate_result),
+                         (int32_t)sizeof(ca_removal_result)};
+    const int32_t n = (int32_t)(sizeof s / sizeof s[0]);
+    for (int32_t i = 0; i < n && i < cap; i++) out[i] = s[i];
+    return n;
+}
+
+int ca_device_count(int32_t* out) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) { *out = 0; set_last_error(hipGetErrorString(e)); return CA_EDEVICE; }
+    *out = n;
+    return CA_OK;
+}
+
+const char* ca_status_string(int status) {
+    switch (status) {
+    case CA_OK: return "ok";
+    case CA_EINVAL: return "invalid argument";
+    case CA_ENOTFOUND: return "not found";
+    case CA_EEXISTS: return "already exists";
+    case CA_EDEVICE: return g_last_error.empty() ? "device error" : g_last_error.c_str();
+    case CA_ECAPACITY: return "capacity exceeded";
+    case CA_EUNSUPPORTED: return "unsupported by the kernels";
+    case CA_ESTATE: return "invalid fork state";
+    default: return "unknown status";
+    }
+}
+
+int ca_mirror_create(int32_t device, ca_mirror** out) {
+    if (!out) return CA_EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) { set_last_error("no HIP device"); return CA_EDEVICE; }
+    if (device < 0 || device >= n) return CA_EINVAL;
+    CA_HIP_CHECK(hipSetDevice(device));
+    ca_mirror* m = new ca_mirror();
+    m->device = device;
+    if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&m->ev0) != hipSuccess || hipEventCreate(&m->ev1) != hipSuccess ||
+        hipEventCreate(&m->ev2) != hipSuccess) {
+        delete m;
+        set_last_error("stream/event creation failed");
+        return CA_EDEVICE;
+    }
+    *out = m;
+    return CA_OK;
+}
+
+int ca_mirror_destroy(ca_mirror* m) {
+    if (!m) return CA_EINVAL;
+    (void)hipSetDevice(m->device);
+    (void)hipStreamSynchronize(m->stream);
+    (void)hipEventDestroy(m->ev0); (void)hipEventDestroy(m->ev1); (void)hipEventDestroy(m->ev2);
+    (void)hipStreamDestroy(m->stream);
+    delete m;
+    return CA_OK;
+}
+
+int ca_mirror_clear(ca_mirror* m) {
+    if (!m) return CA_EINVAL;
+    m->nodes.clear(); m->pods.clear(); m->terms.clear(); m->reqs.clear(); m->pf_names.clear();
+    m->journal.clear(); m->depth = 0;
+    m->dirty_rows.clear(); m->dirty_flag.clear();
+    m->all_dirty = true; m->static_dirty = true; m->d_rows = 0;
+    m->d_pods_synced = 0; m->d_terms_synced = 0;
+    return CA_OK;
+}
+
+int ca_mirror_add_nodes(ca_mirror* m, const ca_node_spec* nodes, int32_t n, int32_t* out_first_pos) {
+    if (!m || (n > 0 && !nodes) || n < 0) return CA_EINVAL;
+    if (out_first_pos) *out_first_pos = (int32_t)m->nodes.size();
+    for (int32_t i = 0; i < n; i++) {
+        NodeRow r;
+        r.spec = nodes[i];
+        m->nodes.push_back(std::move(r));
+        m->journal_push(J_ADD_NODE, (int32_t)m->nodes.size() - 1, -1, -1, nullptr);
+    }
+    m->static_dirty = true;
+    return CA_OK;
+}
+
+int ca_mirror_add_pods(ca_mirror* m, const ca_pod_table* t, const int32_t* pod_idx,
+                       const int32_t* node_pos, int32_t n, int32_t* out_ids) {
+    if (!m || !t || n < 0) return CA_EINVAL;
+    for (int32_t i = 0; i < n; i++) {
+        if (node_pos[i] < 0 || (size_t)node_pos[i] >= m->nodes.size()) return CA_ENOTFOUND;
+        if (pod_idx[i] < 0 || pod_idx[i] >= t->n_pods) return CA_EINVAL;
+        int32_t id = m->store_pod(t, pod_idx[i], node_pos[i]);
+        m->add_pod_to_node(id, node_pos[i]);
+        if (out_ids) out_ids[i] = id;
+    }
+    return CA_OK;
+}
+
+int ca_mirror_remove_pod(ca_mirror* m, int32_t pod_id) {
+    if (!m) return CA_EINVAL;
+    if (pod_id < 0 || (size_t)pod_id >= m->pods.size() || m->pods[pod_id].node < 0) return CA_ENOTFOUND;
+    const int32_t node = m->pods[pod_id].node;
+    NodeRow& nd = m->nodes[node];
+    int32_t slot = -1;
+    for (size_t i = 0; i < nd.pods.size(); i++) if (nd.pods[i] == pod_id) { slot = (int32_t)i; break; }
+    if (slot < 0) return CA_ENOTFOUND;
+    uint64_t before[CA_PORT_WORDS];
+    std::memcpy(before, nd.ports, sizeof before);
+    nd.pods[slot] = nd.pods.back();          // swap-with-last (SF/types.go:660-663)
+    nd.pods.pop_back();
+    m->node_apply(node, m->pods[pod_id].spec, -1);
+    m->pods[pod_id].node = -1;
+    m->journal_push(J_REMOVE_POD, node, pod_id, slot, before);
+    return CA_OK;
+}
+
+int ca_mirror_fork(ca_mirror* m) {
+    if (!m) return CA_EINVAL;
+    m->depth++;
+    m->journal_push(J_FORK, -1, -1, -1, nullptr);
+    return CA_OK;
+}
+
+int ca_mirror_revert(ca_mirror* m) {
+    if (!m) return CA_EINVAL;
+    if (m->depth == 0) return CA_ESTATE;
+    while (!m->journal.empty()) {
+        JournalEntry e = m->journal.back();
+        m->journal.pop_back();
+        if (e.kind == J_FORK) break;
+        if (e.kind == J_ADD_NODE) {
+            m->nodes.pop_back();
+            if (m->d_rows > m->nodes.size()) m->d_rows = m->nodes.size();
+            if (m->dirty_flag.size() > m->nodes.size()) m->dirty_flag.resize(m->nodes.size());
+            m->dirty_rows.erase(std::remove_if(m->dirty_rows.begin(), m->dirty_rows.end(),
+                                               [&](int32_t r) { return (size_t)r >= m->nodes.size(); }),
+                                m->dirty_rows.end());
+            m->static_dirty = true;
+        } else if (e.kind == J_ADD_POD) {
+            m->node_apply(e.node, m->pods[e.pod].spec, -1);
+            std::memcpy(m->nodes[e.node].ports, e.ports, sizeof e.ports);
+            m->nodes[e.node].pods.pop_back();
+            m->pods[e.pod].node = -1;
+        } else if (e.kind == J_REMOVE_POD) {
+            NodeRow& nd = m->nodes[e.node];
+            m->node_apply(e.node, m->pods[e.pod].spec, +1);
+            std::memcpy(nd.ports, e.ports, sizeof e.ports);
+            nd.pods.push_back(nd.pods[e.slot]);
+            nd.pods[e.slot] = e.pod;
+            m->pods[e.pod].node = e.node;
+        }
+    }
+    m->depth--;
+    return CA_OK;
+}
+
+int ca_mirror_commit(ca_mirror* m) {
+    if (!m) return CA_EINVAL;
+    if (m->depth == 0) return CA_ESTATE;
+    int64_t i = (int64_t)m->journal.size() - 1;
+    while (i >= 0 && m->journal[i].kind != J_FORK) i--;
+    if (i < 0) return CA_ESTATE;
+    m->depth--;
+    if (m->depth == 0) m->journal.clear();
+    else m->journal.erase(m->journal.begin() + i);
+    return CA_OK;
+}
+
+int ca_mirror_node_count(const ca_mirror* m, int32_t* out) {
+    if (!m || !out) return CA_EINVAL;
+    *out = (int32_t)m->nodes.size();
+    return CA_OK;
+}
+
+int ca_mirror_pod_node(const ca_mirror* m, int32_t pod_id, int32_t* out_node_pos) {
+    if (!m || !out_node_pos) return CA_EINVAL;
+    if (pod_id < 0 || (size_t)pod_id >= m->pods.size()) return CA_ENOTFOUND;
+    *out_node_pos = m->pods[pod_id].node;
+    return CA_OK;
+}
+
+int ca_mirror_node_pods(const ca_mirror* m, int32_t node_pos, int32_t* out_ids, int32_t cap, int32_t* out_n) {
+    if (!m || !out_n) return CA_EINVAL;
+    if (node_pos < 0 || (size_t)node_pos >= m->nodes.size()) return CA_ENOTFOUND;
+    const auto& v = m->nodes[node_pos].pods;
+    *out_n = (int32_t)v.size();
+    if ((int32_t)v.size() > cap) return CA_ECAPACITY;
+    for (size_t i = 0; i < v.size(); i++) out_ids[i] = v[i];
+    return CA_OK;
+}
+
+int ca_podset_create(ca_mirror* m, const ca_pod_table* t, ca_podset** out) {
+    if (!m || !t || !out || t->n_pods < 0) return CA_EINVAL;
+    CA_HIP_CHECK(hipSetDevice(m->device));
+    ca_podset* s = new ca_podset();
+    s->m = m;
+    s->h_pods.assign(t->pods, t->pods + t->n_pods);
+    int rc = s->t.upload(t->pods, t->n_pods, t->terms, t->n_terms, t->reqs, t->n_reqs, t->prefilter_names,
+                         t->n_prefilter_names, m->stream);
+    if (rc != CA_OK) { delete s; return rc; }
+    *out = s;
+    return CA_OK;
+}
+
+int ca_podset_destroy(ca_podset* s) {
+    if (!s) return CA_EINVAL;
+    delete s;
+    return CA_OK;
+}
+
+int ca_fits_any_node(ca_mirror* m, const ca_pod_table* t, int32_t pod, const ca_match_spec* match,
+                     int32_t* last_index, int32_t* out_node, int32_t* out_prefilter_failed, uint64_t* evals) {
+    if (!m || !t || !last_index || !out_node || pod < 0 || pod >= t->n_pods) return CA_EINVAL;
+    CA_HIP_CHECK(hipSetDevice(m->device));
+    *out_node = -1;
+    if (out_prefilter_failed) *out_prefilter_failed = 0;
+    const ca_pod_spec& ps = t->pods[pod];
+    if (ps.flags & CA_POD_PREFILTER_FAIL) {                 // schedulerbased.go:109-112
+        if (out_prefilter_failed) *out_prefilter_failed = 1;
+        return CA_OK;
+    }
+    const int32_t n = (int32_t)m->nodes.size();
+    if (n == 0) return CA_OK;
+    int rc;
+    if ((rc = m->sync_nodes()) != CA_OK) return rc;
+    // single-pod table on device (pod record + its selector tables)
+    ca_pod_spec one = ps;
+    std::vector<ca_selector_term> tms;
+    std::vector<ca_selector_req> rqs;
+    std::vector<int32_t> nms;
+    if (one.aff_term_count > 0) {
+        for (int32_t k = 0; k < one.aff_term_count; k++) {
+            ca_selector_term tm = t->terms[one.aff_term_first + k];
+            int32_t rf = (int32_t)rqs.size();
+            for (int32_t r = 0; r < tm.count; r++) rqs.push_back(t->reqs[tm.first + r]);
+            tm.first = rf;
+            tms.push_back(tm);
+        }
+        one.aff_term_first = 0;
+    }
+    if ((one.flags & CA_POD_PREFILTER_NAMES) && one.prefilter_count > 0) {
+        for (int32_t k = 0; k < one.prefilter_count; k++) nms.push_back(t->prefilter_names[one.prefilter_first + k]);
+        one.prefilter_first = 0;
+    }
+    DevPodTable dp;
+    if ((rc = dp.upload(&one, 1, tms.data(), (int32_t)tms.size(), rqs.data(), (int32_t)rqs.size(), nms.data(),
+                        (int32_t)nms.size(), m->stream)) != CA_OK)
+        return rc;
+    const int32_t kind = match ? match->kind : CA_MATCH_ALL;
+    const uint8_t* dmask = nullptr;
+    if (kind == CA_MATCH_MASK) {
+        if (!match->mask) return CA_EINVAL;
+        if ((rc = m->d_mask.reserve((size_t)n)) != CA_OK) return rc;
+        CA_HIP_CHECK(hipMemcpyAsync(m->d_mask.ptr, match->mask, (size_t)n, hipMemcpyHostToDevice, m->stream));
+        dmask = m->d_mask.as<uint8_t>();
+    }
+    const int32_t words = (n + 63) / 64;
+    if ((rc = m->d_scratch0.reserve(sizeof(unsigned long long) * 2 * (size_t)words)) != CA_OK) return rc;
+    unsigned long long* dfit = m->d_scratch0.as<unsigned long long>();
+    unsigned long long* dvis = dfit + words;
+    const int64_t L = *last_index;
+    hipLaunchKernelGGL(k_fits_scan, dim3((n + 255) / 256), dim3(256), 0, m->stream, m->d_hot.as<NodeHot>(),
+                       m->d_ext.as<NodeExt>(), m->d_static.as<NodeStatic>(), n, dp.hot.as<PodHot>(),
+                       dp.spec.as<ca_pod_spec>(), dp.terms.as<ca_selector_term>(), dp.reqs.as<ca_selector_req>(),
+                       dp.names.as<int32_t>(), 0, L, kind, match ? match->lo : 0, match ? match->hi : 0,
+                       match ? match->exclude : -1, dmask, dfit, dvis);
+    CA_HIP_CHECK(hipGetLastError());
+    std::vector<unsigned long long> h((size_t)words * 2);
+    CA_HIP_CHECK(hipMemcpyAsync(h.data(), dfit, sizeof(unsigned long long) * 2 * words, hipMemcpyDeviceToHost, m->stream));
+    CA_HIP_CHECK(hipStreamSynchronize(m->stream));
+    // first fit in rotated order; evals = visited nodes up to and including it
+    uint64_t ev = 0;
+    for (int32_t w = 0; w < words; w++) {
+        const unsigned long long f = h[w], v = h[words + w];
+        if (f) {
+            const int b = __builtin_ctzll(f);
+            const unsigned long long below = (b == 63) ? ~0ull : ((2ull << b) - 1);
+            ev += (uint64_t)__builtin_popcountll(v & below);
+            const int64_t i = (int64_t)w * 64 + b;
+            *out_node = (int32_t)((L + i) % n);
+            *last_index = (int32_t)((L + i + 1) % n);     // schedulerbased.go:131
+            if (evals) *evals += ev;
+            return CA_OK;
+        }
+        ev += (uint64_t)__builtin_popcountll(v);
+    }
+    if (evals) *evals += ev;
+    return CA_OK;
+}
+
+int ca_check_predicates(ca_mirror* m, const ca_pod_table* t, int32_t pod, int32_t node_pos, ca_pred_result* out) {
+    if (!m || !t || !out || pod < 0 || pod >= t->n_pods) return CA_EINVAL;
+    std::memset(out, 0, sizeof *out);
+    if (node_pos < 0 || (size_t)node_pos >= m->nodes.size()) {   // schedulerbased.go:143-147
+        out->type = CA_PRED_INTERNAL;
+        return CA_OK;
+    }
+    const ca_pod_spec& ps = t->pods[pod];
+    if (ps.flags & CA_POD_PREFILTER_FAIL) {                       // :153-161
+        out->type = CA_PRED_INTERNAL;
+        out->plugin = CA_PLUGIN_NODE_AFFINITY;
+        return CA_OK;
+    }
+    CA_HIP_CHECK(hipSetDevice(m->device));
+    int rc;
+    if ((rc = m->sync_nodes()) != CA_OK) return rc;
+    ca_pod_spec one = ps;
+    std::vector<ca_selector_term> tms;
+    std::vector<ca_selector_req> rqs;
+    if (one.aff_term_count > 0) {
+        for (int32_t k = 0; k < one.aff_term_count; k++) {
+            ca_selector_term tm = t->terms[one.aff_term_first + k];
+            int32_t rf = (int32_t)rqs.size();
+            for (int32_t r = 0; r < tm.count; r++) rqs.push_back(t->reqs[tm.first + r]);
+            tm.first = rf;
+            tms.push_back(tm);
+        }
+        one.aff_term_first = 0;
+    }
+    DevPodTable dp;
+    if ((rc = dp.upload(&one, 1, tms.data(), (int32_t)tms.size(), rqs.data(), (int32_t)rqs.size(), nullptr, 0,
+                        m->stream)) != CA_OK)
+        return rc;
+    if ((rc = m->d_scratch1.reserve(sizeof(ca_pred_result))) != CA_OK) return rc;
+    hipLaunchKernelGGL(k_check_one, dim3(1), dim3(64), 0, m->stream, m->d_hot.as<NodeHot>(), m->d_ext.as<NodeExt>(),
+                       m->d_static.as<NodeStatic>(), dp.hot.as<PodHot>(), dp.spec.as<ca_pod_spec>(),
+                       dp.terms.as<ca_selector_term>(), dp.reqs.as<ca_selector_req>(), 0, node_pos,
+                       m->d_scratch1.as<ca_pred_result>());
+    CA_HIP_CHECK(hipGetLastError());
+    CA_HIP_CHECK(hipMemcpyAsync(out, m->d_scratch1.ptr, sizeof(ca_pred_result), hipMemcpyDeviceToHost, m->stream));
+    CA_HIP_CHECK(hipStreamSynchronize(m->stream));
+    return CA_OK;
+}
+
+int ca_fits_matrix(ca_mirror* m, const ca_podset* s, uint8_t* out) {
+    if (!m || !s || !out) return CA_EINVAL;
+    CA_HIP_CHECK(hipSetDevice(m->device));
+    int rc;
+    if ((rc = m->sync_nodes()) != CA_OK) return rc;
+    const int32_t n = (int32_t)m->nodes.size();
+    const int32_t P = s->t.n_pods;
+    if (n == 0 || P == 0) return CA_OK;
+    const size_t bytes = (size_t)n * (size_t)P;
+    if ((rc = m->d_scratch2.reserve(bytes)) != CA_OK) return rc;
+    hipLaunchKernelGGL(k_fits_matrix, dim3((n + 255) / 256, P), dim3(256), 0, m->stream, m->d_hot.as<NodeHot>(),
+                       m->d_ext.as<NodeExt>(), m->d_static.as<NodeStatic>(), n, s->t.hot.as<PodHot>(),
+                       s->t.spec.as<ca_pod_spec>(), s->t.terms.as<ca_selector_term>(), s->t.reqs.as<ca_selector_req>(),
+                       P, m->d_scratch2.as<uint8_t>());
+    CA_HIP_CHECK(hipGetLastError());
+    CA_HIP_CHECK(hipMemcpyAsync(out, m->d_scratch2.ptr, bytes, hipMemcpyDeviceToHost, m->stream));
+    CA_HIP_CHECK(hipStreamSynchronize(m->stream));
+    return CA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,300 @@
+"""Loader and thin object wrapper of ``libcasim.so`` (the MI355X product path).
+
+There is no fallback: if the in-tree library is missing, or no HIP device is
+visible, every constructor raises.  The wrapper only marshals numpy arrays into
+the C ABI of ``include/casim.h``; all simulation work happens in the library.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import abi
+from .abi import ptr
+
+_LIB = None
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libcasim.so")
+
+
+class CasimError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        self.status = status
+        super().__init__(f"{what}: status {status} ({_status_string(status)})")
+
+
+def _status_string(status: int) -> str:
+    try:
+        return load().ca_status_string(status).decode()
+    except Exception:  # pragma: no cover - only while the library is unusable
+        return "?"
+
+
+def load() -> C.CDLL:
+    """Load the in-tree libcasim.so (raises if it was not built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libcasim.so not built: {LIB_PATH} missing (run __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    vp, i32, p = C.c_void_p, C.c_int32, C.POINTER
+    sigs = {
+        "ca_abi_version": ([], C.c_int),
+        "ca_abi_struct_sizes": ([p(i32), i32], C.c_int),
+        "ca_device_count": ([p(i32)], C.c_int),
+        "ca_status_string": ([C.c_int], C.c_char_p),
+        "ca_mirror_create": ([i32, p(vp)], C.c_int),
+        "ca_mirror_destroy": ([vp], C.c_int),
+        "ca_mirror_clear": ([vp], C.c_int),
+        "ca_mirror_add_nodes": ([vp, vp, i32, p(i32)], C.c_int),
+        "ca_mirror_add_pods": ([vp, vp, vp, vp, i32, vp], C.c_int),
+        "ca_mirror_remove_pod": ([vp, i32], C.c_int),
+        "ca_mirror_fork": ([vp], C.c_int),
+        "ca_mirror_revert": ([vp], C.c_int),
+        "ca_mirror_commit": ([vp], C.c_int),
+        "ca_mirror_node_count": ([vp, p(i32)], C.c_int),
+        "ca_mirror_pod_node": ([vp, i32, p(i32)], C.c_int),
+        "ca_mirror_node_pods": ([vp, i32, vp, i32, p(i32)], C.c_int),
+        "ca_podset_create": ([vp, vp, p(vp)], C.c_int),
+        "ca_podset_destroy": ([vp], C.c_int),
+        "ca_fits_any_node": ([vp, vp, i32, vp, p(i32), p(i32), p(i32), p(C.c_uint64)], C.c_int),
+        "ca_check_predicates": ([vp, vp, i32, i32, vp], C.c_int),
+        "ca_fits_matrix": ([vp, vp, vp], C.c_int),
+        "ca_estimate_batch": ([vp, vp, vp, vp, vp, i32, vp, p(i32), vp, vp, vp], C.c_int),
+        "ca_estimate_plan_create": ([vp, vp, vp, vp, vp, i32, p(vp)], C.c_int),
+        "ca_estimate_plan_run": ([vp, vp, p(i32), vp, vp, vp], C.c_int),
+        "ca_estimate_plan_destroy": ([vp], C.c_int),
+        "ca_estimate_plan_stats": ([vp, p(i32), p(C.c_float), p(C.c_float), p(C.c_float)], C.c_int),
+        "ca_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, p(i32), vp, vp], C.c_int),
+        "ca_removal_stats": ([vp, p(i32), p(C.c_float), p(C.c_float)], C.c_int),
+    }
+    for name, (args, res) in sigs.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+    _LIB = lib
+    return lib
+
+
+def _check(status: int, what: str) -> None:
+    if status != abi.CA_OK:
+        raise CasimError(status, what)
+
+
+def exported_symbols() -> list[str]:
+    return [
+        "ca_abi_version", "ca_abi_struct_sizes", "ca_device_count", "ca_status_string", "ca_mirror_create",
+        "ca_mirror_destroy", "ca_mirror_clear", "ca_mirror_add_nodes", "ca_mirror_add_pods", "ca_mirror_remove_pod",
+        "ca_mirror_fork", "ca_mirror_revert", "ca_mirror_commit", "ca_mirror_node_count", "ca_mirror_pod_node",
+        "ca_mirror_node_pods", "ca_podset_create", "ca_podset_destroy", "ca_fits_any_node", "ca_check_predicates",
+        "ca_fits_matrix", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
+        "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_find_nodes_to_remove", "ca_removal_stats",
+    ]
+
+
+def device_count() -> int:
+    n = C.c_int32(0)
+    st = load().ca_device_count(C.byref(n))
+    return n.value if st == abi.CA_OK else 0
+
+
+@dataclass
+class EstimateOutput:
+    results: np.ndarray          # ESTIMATE_RESULT_DTYPE [G]
+    sched_pod: np.ndarray        # int32 [total], CSR by group_off
+    sched_node: np.ndarray       # int32 [total]
+    last_index: int
+
+
+@dataclass
+class RemovalOutput:
+    results: np.ndarray          # REMOVAL_RESULT_DTYPE [C]
+    dest: np.ndarray             # int32 [M]
+    hints: np.ndarray            # int32 [pods]
+    last_index: int
+
+
+class Mirror:
+    """A ``ca_mirror``: the HBM-resident ClusterSnapshot data plane."""
+
+    backend_name = "native"
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = C.c_void_p()
+        _check(self.lib.ca_mirror_create(device, C.byref(h)), "ca_mirror_create")
+        self.h = h
+        self._keep: list = []
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.ca_mirror_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- snapshot data plane --------------------------------------------------
+    def clear(self) -> None:
+        _check(self.lib.ca_mirror_clear(self.h), "ca_mirror_clear")
+
+    def add_nodes(self, nodes: np.ndarray) -> int:
+        nodes = np.ascontiguousarray(nodes, dtype=abi.NODE_DTYPE)
+        first = C.c_int32(0)
+        _check(self.lib.ca_mirror_add_nodes(self.h, ptr(nodes), len(nodes), C.byref(first)), "ca_mirror_add_nodes")
+        return first.value
+
+    def add_pods(self, table: abi.PodTable, idx, node_pos) -> np.ndarray:
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        node_pos = np.ascontiguousarray(node_pos, dtype=np.int32)
+        out = np.zeros(len(idx), np.int32)
+        _check(self.lib.ca_mirror_add_pods(self.h, table.ref, ptr(idx), ptr(node_pos), len(idx), ptr(out)),
+               "ca_mirror_add_pods")
+        return out
+
+    def remove_pod(self, pod_id: int) -> None:
+        _check(self.lib.ca_mirror_remove_pod(self.h, pod_id), "ca_mirror_remove_pod")
+
+    def fork(self) -> None:
+        _check(self.lib.ca_mirror_fork(self.h), "ca_mirror_fork")
+
+    def revert(self) -> None:
+        _check(self.lib.ca_mirror_revert(self.h), "ca_mirror_revert")
+
+    def commit(self) -> None:
+        _check(self.lib.ca_mirror_commit(self.h), "ca_mirror_commit")
+
+    def node_count(self) -> int:
+        n = C.c_int32(0)
+        _check(self.lib.ca_mirror_node_count(self.h, C.byref(n)), "ca_mirror_node_count")
+        return n.value
+
+    def pod_node(self, pod_id: int) -> int:
+        n = C.c_int32(0)
+        _check(self.lib.ca_mirror_pod_node(self.h, pod_id, C.byref(n)), "ca_mirror_pod_node")
+        return n.value
+
+    def node_pods(self, node: int) -> list[int]:
+        cap = 256
+        while True:
+            out = np.zeros(cap, np.int32)
+            n = C.c_int32(0)
+            st = self.lib.ca_mirror_node_pods(self.h, node, ptr(out), cap, C.byref(n))
+            if st == abi.CA_ECAPACITY:
+                cap = n.value
+                continue
+            _check(st, "ca_mirror_node_pods")
+            return out[: n.value].tolist()
+
+    # -- predicate checker ----------------------------------------------------
+    def fits_any_node(self, table: abi.PodTable, pod: int, match=None, last_index: int = 0):
+        ms, mask = abi.match_spec(*(match or ()))
+        li = C.c_int32(last_index)
+        out = C.c_int32(-1)
+        pf = C.c_int32(0)
+        ev = C.c_uint64(0)
+        _check(self.lib.ca_fits_any_node(self.h, table.ref, pod, C.byref(ms), C.byref(li), C.byref(out),
+                                         C.byref(pf), C.byref(ev)), "ca_fits_any_node")
+        del mask
+        return out.value, li.value, pf.value, ev.value
+
+    def check_predicates(self, table: abi.PodTable, pod: int, node: int):
+        r = abi.PredResultC()
+        _check(self.lib.ca_check_predicates(self.h, table.ref, pod, node, C.byref(r)), "ca_check_predicates")
+        return r.type, r.plugin, r.reasons, r.taint
+
+    def fits_matrix(self, table: abi.PodTable) -> np.ndarray:
+        s = C.c_void_p()
+        _check(self.lib.ca_podset_create(self.h, table.ref, C.byref(s)), "ca_podset_create")
+        try:
+            out = np.zeros((len(table), self.node_count()), np.uint8)
+            _check(self.lib.ca_fits_matrix(self.h, s, ptr(out)), "ca_fits_matrix")
+        finally:
+            self.lib.ca_podset_destroy(s)
+        return out
+
+    # -- estimator ------------------------------------------------------------
+    def estimate(self, table: abi.PodTable, group_off, pod_idx, templates: np.ndarray, max_nodes: int,
+                 last_index: int = 0) -> EstimateOutput:
+        with EstimatePlan(self, table, group_off, pod_idx, templates) as plan:
+            return plan.run(max_nodes, last_index)
+
+    # -- removal simulator ----------------------------------------------------
+    def find_nodes_to_remove(self, candidates, dest_mask, cand_status, move_off, move_pods, hints,
+                             last_index: int = 0) -> RemovalOutput:
+        cand = np.ascontiguousarray(candidates, dtype=np.int32)
+        mask = np.ascontiguousarray(dest_mask, dtype=np.uint8)
+        status = np.ascontiguousarray(cand_status if cand_status is not None else np.zeros(len(cand)), dtype=np.int32)
+        off = np.ascontiguousarray(move_off, dtype=np.int32)
+        moves = np.ascontiguousarray(move_pods, dtype=np.int32)
+        hints = np.array(hints, dtype=np.int32, copy=True)
+        res = np.zeros(len(cand), abi.REMOVAL_RESULT_DTYPE)
+        dest = np.full(max(len(moves), 1), -1, np.int32)
+        li = C.c_int32(last_index)
+        _check(self.lib.ca_find_nodes_to_remove(self.h, ptr(cand), len(cand), ptr(mask), ptr(status), ptr(off),
+                                                ptr(moves), ptr(hints), C.byref(li), ptr(res), ptr(dest)),
+               "ca_find_nodes_to_remove")
+        return RemovalOutput(res, dest[: len(moves)], hints, li.value)
+
+    def removal_stats(self) -> dict:
+        r, k, t = C.c_int32(0), C.c_float(0), C.c_float(0)
+        self.lib.ca_removal_stats(self.h, C.byref(r), C.byref(k), C.byref(t))
+        return {"rounds": r.value, "kernel_ms": k.value, "total_ms": t.value}
+
+
+class EstimatePlan:
+    """``ca_estimate_plan``: device-resident groups for repeated Estimate batches."""
+
+    def __init__(self, mirror: Mirror, table: abi.PodTable, group_off, pod_idx, templates: np.ndarray):
+        self.m = mirror
+        self.lib = mirror.lib
+        self.group_off = np.ascontiguousarray(group_off, dtype=np.int32)
+        self.pod_idx = np.ascontiguousarray(pod_idx, dtype=np.int32)
+        self.templates = np.ascontiguousarray(templates, dtype=abi.TEMPLATE_DTYPE)
+        self.G = len(self.templates)
+        self.total = int(self.group_off[-1]) if len(self.group_off) else 0
+        s = C.c_void_p()
+        _check(self.lib.ca_podset_create(mirror.h, table.ref, C.byref(s)), "ca_podset_create")
+        self.podset = s
+        p = C.c_void_p()
+        st = self.lib.ca_estimate_plan_create(mirror.h, s, ptr(self.group_off), ptr(self.pod_idx),
+                                              ptr(self.templates), self.G, C.byref(p))
+        if st != abi.CA_OK:
+            self.lib.ca_podset_destroy(s)
+            raise CasimError(st, "ca_estimate_plan_create")
+        self.h = p
+        self.sched_pod = np.full(max(self.total, 1), -1, np.int32)
+        self.sched_node = np.full(max(self.total, 1), -1, np.int32)
+        self.results = np.zeros(self.G, abi.ESTIMATE_RESULT_DTYPE)
+
+    def run(self, max_nodes: int, last_index: int = 0, want_nodes: bool = True) -> EstimateOutput:
+        lim = abi.LimiterC(max_nodes, 0)
+        li = C.c_int32(last_index)
+        _check(self.lib.ca_estimate_plan_run(self.h, C.byref(lim), C.byref(li), ptr(self.results),
+                                             ptr(self.sched_pod), ptr(self.sched_node) if want_nodes else None),
+               "ca_estimate_plan_run")
+        return EstimateOutput(self.results.copy(), self.sched_pod[: self.total].copy(),
+                              self.sched_node[: self.total].copy(), li.value)
+
+    def stats(self) -> dict:
+        r, a, b, c = C.c_int32(0), C.c_float(0), C.c_float(0), C.c_float(0)
+        self.lib.ca_estimate_plan_stats(self.h, C.byref(r), C.byref(a), C.byref(b), C.byref(c))
+        return {"rounds": r.value, "chain_ms": a.value, "sort_ms": b.value, "total_ms": c.value}
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.ca_estimate_plan_destroy(self.h)
+            self.lib.ca_podset_destroy(self.podset)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

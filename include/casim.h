@@ -1,0 +1,338 @@
+/*
+ * casim.h — C ABI of the MI355X scheduling-simulation library (libcasim.so).
+ *
+ * This is the drop-in boundary for cluster-autoscaler's scheduling-simulation
+ * hot path.  A Go shim (cgo) or any C caller binds these entry points; no torch
+ * or C++ types appear in any signature.  Every struct is plain-old-data with
+ * fixed-size members so cgo can pass Go-allocated arrays of them directly.
+ *
+ * Reference interfaces replaced (CA/ = cluster-autoscaler/ in the reference):
+ *   ClusterSnapshot data plane   CA/simulator/clustersnapshot/clustersnapshot.go:29-55
+ *                                (DeltaClusterSnapshot CA/simulator/clustersnapshot/delta.go:43-475)
+ *       -> ca_mirror_* (create/add_nodes/add_pods/remove_pod/fork/revert/commit/clear)
+ *   PredicateChecker.FitsAnyNode / FitsAnyNodeMatching
+ *                                CA/simulator/predicatechecker/interface.go:27-31,
+ *                                CA/simulator/predicatechecker/schedulerbased.go:83-136
+ *       -> ca_fits_any_node (closure nodeMatches -> ca_match_spec; lastIndex explicit in/out)
+ *   PredicateChecker.CheckPredicates  schedulerbased.go:139-185, error.go:24-107
+ *       -> ca_check_predicates (PredicateError -> ca_pred_result)
+ *   Estimator.Estimate           CA/estimator/estimator.go:40-42,
+ *                                CA/estimator/binpacking_estimator.go:65-193
+ *   EstimationLimiter            CA/estimator/estimator.go:63-74, threshold_based_limiter.go:27-64
+ *       -> ca_estimate_batch (one call = Estimate for every node group of one ScaleUp,
+ *          CA/core/scaleup/orchestrator/orchestrator.go:139-178, :487-488)
+ *   RemovalSimulator.FindNodesToRemove  CA/simulator/cluster.go:116-139 (+ SimulateNodeRemoval
+ *                                :145-184, findPlaceFor :220-254, HintingSimulator.TrySchedulePods
+ *                                CA/simulator/scheduling/hinting_simulator.go:58-125)
+ *       -> ca_find_nodes_to_remove (legacy canPersist=false semantics)
+ *
+ * Node order.  Every node index in this ABI is a POSITION in the mirror's node
+ * list.  The list is the canonical order of SURVEY.md fact 2: nodes in
+ * ca_mirror_add_nodes order; nodes added in a fork are appended.  The caller
+ * passes nodes in the order its own ClusterSnapshot.NodeInfos().List() returned
+ * (the rotating scan of FitsAnyNodeMatching walks that order).
+ *
+ * Threading.  One mirror per caller thread; calls on one handle are serialised
+ * by the caller (the reference checker is not thread-safe either,
+ * schedulerbased.go:43,105-106).  No pointer passed in is retained after a call
+ * returns.
+ */
+#ifndef CASIM_H
+#define CASIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CASIM_ABI_VERSION 1
+
+/* ---- status codes (int return of every entry point) -------------------- */
+#define CA_OK            0
+#define CA_EINVAL        1  /* malformed argument                                    */
+#define CA_ENOTFOUND     2  /* node/pod not in the mirror (clustersnapshot.go:58 ErrNodeNotFound) */
+#define CA_EEXISTS       3  /* object already present                                */
+#define CA_EDEVICE       4  /* HIP runtime failure                                   */
+#define CA_ECAPACITY     5  /* a fixed-width intern table (labels/ports/...) overflowed */
+#define CA_EUNSUPPORTED  6  /* input needs a plugin the kernels do not implement:
+                               the caller routes it to the Go scheduler framework      */
+#define CA_ESTATE        7  /* fork/revert/commit misuse                              */
+
+/* ---- fixed widths of interned bitsets (host interning) -- */
+#define CA_MAX_SCALAR    8   /* extended / hugepage / attachable-volume resources   */
+#define CA_LABEL_WORDS   4   /* 256 interned (key,value) label pairs                  */
+#define CA_PORT_WORDS    2   /* 128 interned (hostIP,protocol,hostPort) triples        */
+#define CA_MAX_INT_KEYS  4   /* label keys referenced by Gt/Lt requirements           */
+/* taint classes: 64 (one u64); label keys for Exists/DoesNotExist: 64 (one u64) */
+
+/* ---- node flags ---------------------------------------------------------- */
+#define CA_NODE_UNSCHEDULABLE   0x1u  /* node.Spec.Unschedulable                       */
+
+/* ---- pod flags ----------------------------------------------------------- */
+#define CA_POD_HAS_SCALAR_KEYS        0x001u /* len(podRequest.ScalarResources) != 0 (fit.go:267-272) */
+#define CA_POD_HAS_NONTPU_SCALAR_KEYS 0x002u /* same after tpu.ClearTPURequests (tpu.go:57-79)        */
+#define CA_POD_TOLERATES_UNSCHED      0x004u /* tolerates node.kubernetes.io/unschedulable:NoSchedule
+                                                (node_unschedulable.go:61-75)                         */
+#define CA_POD_AFFINITY_FILTER        0x008u /* NodeAffinity PreFilter did not Skip (node_affinity.go:91-99):
+                                                pod has nodeSelector or required node affinity        */
+#define CA_POD_PREFILTER_FAIL         0x010u /* NodeAffinity PreFilter UnschedulableAndUnresolvable
+                                                (empty matchFields intersection, node_affinity.go:125-127) */
+#define CA_POD_PREFILTER_NAMES        0x020u /* PreFilterResult.NodeNames set (node_affinity.go:129-133) */
+#define CA_POD_DAEMONSET              0x040u /* owned by a DaemonSet (similar_pods.go:94)            */
+#define CA_POD_HOSTNAME_DEPENDENT     0x080u /* selector/affinity/nodeName refer to node identity:
+                                                not evaluable once per template in ca_estimate_batch  */
+
+/* ---- selector requirement ops (labels/selector.go:223-267, nodeaffinity.go:297-324) */
+#define CA_OP_IN            1  /* node has key with value in set:  node.pairs & req.pairs != 0   */
+#define CA_OP_NOTIN         2  /* !(node.pairs & req.pairs)                                       */
+#define CA_OP_EXISTS        3  /* node.label_keys bit key                                          */
+#define CA_OP_DOESNOTEXIST  4
+#define CA_OP_GT            5  /* int label key `key` present, parses as int64, value >  bound     */
+#define CA_OP_LT            6  /*                                                 value <  bound     */
+#define CA_OP_FIELD_EQ      7  /* matchFields metadata.name In [v]   -> node.name_id == key         */
+#define CA_OP_FIELD_NE      8  /* matchFields metadata.name NotIn [v] -> node.name_id != key        */
+#define CA_OP_FALSE         9  /* term never matches (parse error, unsupported field key)          */
+
+/* ---- plugins (default_plugins.go:33-53 filter order) ---------------------- */
+#define CA_PLUGIN_NONE               0
+#define CA_PLUGIN_NODE_UNSCHEDULABLE 1
+#define CA_PLUGIN_NODE_NAME          2
+#define CA_PLUGIN_TAINT_TOLERATION   3
+#define CA_PLUGIN_NODE_AFFINITY      4
+#define CA_PLUGIN_NODE_PORTS         5
+#define CA_PLUGIN_NODE_RESOURCES_FIT 6
+
+/* ---- predicate result types (error.go:27-32) ----------------------------- */
+#define CA_PRED_OK              0
+#define CA_PRED_NOT_SCHEDULABLE 1  /* NotSchedulablePredicateError */
+#define CA_PRED_INTERNAL        2  /* InternalPredicateError       */
+
+/* reason bits of NodeResourcesFit (fit.go:256-329), in the reference's append order */
+#define CA_REASON_TOO_MANY_PODS   0x1u
+#define CA_REASON_INSUFF_CPU      0x2u
+#define CA_REASON_INSUFF_MEMORY   0x4u
+#define CA_REASON_INSUFF_EPHEMERAL 0x8u
+#define CA_REASON_INSUFF_SCALAR0  0x100u /* bit (8+i): "Insufficient <scalar resource i>" */
+
+/* ---- match spec: the data form of the nodeMatches closure ---------------- */
+#define CA_MATCH_ALL   0  /* FitsAnyNode (schedulerbased.go:83-87)                                */
+#define CA_MATCH_RANGE 1  /* positions [lo,hi): nodes added since a fork (binpacking_estimator.go:91-93) */
+#define CA_MATCH_MASK  2  /* mask[pos] != 0 (destinations, cluster.go:221-223)                     */
+
+/* UnremovableReason values (cluster.go:58-90) used by ca_find_nodes_to_remove */
+#define CA_UNREMOVABLE_NONE              0
+#define CA_UNREMOVABLE_NO_PLACE          13 /* NoPlaceToMovePods */
+#define CA_UNREMOVABLE_BLOCKED_BY_POD    14 /* BlockedByPod      */
+#define CA_UNREMOVABLE_UNEXPECTED_ERROR  15 /* UnexpectedError   */
+
+/* ------------------------------------------------------------------------- */
+
+/* One node (NodeInfo.node + NodeInfo.Allocatable, SF/types.go:381-441, :791-796). */
+typedef struct ca_node_spec {
+    int64_t  alloc_milli_cpu;                 /* Allocatable.MilliCPU                    */
+    int64_t  alloc_memory;                    /* Allocatable.Memory                      */
+    int64_t  alloc_ephemeral;                 /* Allocatable.EphemeralStorage            */
+    int64_t  alloc_pods;                      /* Allocatable.AllowedPodNumber            */
+    int64_t  alloc_scalar[CA_MAX_SCALAR];     /* Allocatable.ScalarResources[interned i] */
+    uint64_t taints;                          /* NoSchedule/NoExecute taint classes      */
+    uint64_t label_pairs[CA_LABEL_WORDS];     /* interned (key,value) pairs on the node  */
+    uint64_t label_keys;                      /* interned keys present                   */
+    int64_t  int_label[CA_MAX_INT_KEYS];      /* int64 value of Gt/Lt key i              */
+    uint32_t int_label_valid;                 /* bit i: key i present and ParseInt ok    */
+    uint32_t flags;                           /* CA_NODE_*                               */
+    int32_t  name_id;                         /* unique interned node name               */
+    int32_t  reserved;
+} ca_node_spec;
+
+/* One pod (requests per computePodResourceRequest fit.go:160-176 == calculateResource
+ * SF/types.go:726-757; scoring sums per calculatePodScore binpacking_estimator.go:164-193). */
+typedef struct ca_pod_spec {
+    int64_t  req_milli_cpu;                   /* max(sum containers, init) + overhead   */
+    int64_t  req_memory;
+    int64_t  req_ephemeral;
+    int64_t  req_scalar[CA_MAX_SCALAR];
+    int64_t  score_milli_cpu;                 /* containers-only cpu sum, MilliValue()   */
+    int64_t  score_memory;                    /* containers-only memory sum, Value()     */
+    uint64_t tolerated_taints;                /* bit t: some toleration tolerates class t */
+    uint64_t port_conflict[CA_PORT_WORDS];    /* triples that conflict with wanted ports
+                                                 (HostPortInfo.CheckConflict SF/types.go:887-921) */
+    uint64_t port_use[CA_PORT_WORDS];         /* triples the pod occupies once placed    */
+    uint64_t node_selector[CA_LABEL_WORDS];   /* spec.nodeSelector pairs (AND)           */
+    int32_t  aff_term_first;                  /* required node affinity terms (ORed)     */
+    int32_t  aff_term_count;                  /* -1: none; 0: present but no terms       */
+    int32_t  prefilter_first;                 /* PreFilter NodeNames (node name ids)     */
+    int32_t  prefilter_count;
+    int32_t  node_name_id;                    /* spec.nodeName; -1 empty                 */
+    uint32_t flags;                           /* CA_POD_*                                */
+    int32_t  similar_class;                   /* SimilarPodsScheduling key, -1 none      */
+    uint32_t tpu_scalar_mask;                 /* scalar indices cleared by ClearTPURequests */
+} ca_pod_spec;
+
+typedef struct ca_selector_req {
+    int32_t  op;                              /* CA_OP_*                                 */
+    int32_t  key;                             /* key id / int key id / name id           */
+    int64_t  bound;                           /* Gt/Lt integer                           */
+    uint64_t pairs[CA_LABEL_WORDS];           /* In/NotIn value pairs of `key`           */
+} ca_selector_req;
+
+typedef struct ca_selector_term {
+    int32_t first;                            /* into ca_pod_table.reqs                  */
+    int32_t count;                            /* 0 is never emitted (empty terms dropped, nodeaffinity.go:83-85) */
+} ca_selector_term;
+
+/* A set of pods plus the side tables their records index into. */
+typedef struct ca_pod_table {
+    const ca_pod_spec*      pods;
+    int32_t                 n_pods;
+    int32_t                 n_terms;
+    const ca_selector_term* terms;
+    const ca_selector_req*  reqs;
+    int32_t                 n_reqs;
+    int32_t                 n_prefilter_names;
+    const int32_t*          prefilter_names;
+} ca_pod_table;
+
+typedef struct ca_match_spec {
+    int32_t        kind;                      /* CA_MATCH_*                              */
+    int32_t        lo, hi;                    /* CA_MATCH_RANGE                          */
+    int32_t        exclude;                   /* position never matched, -1 none         */
+    const uint8_t* mask;                      /* CA_MATCH_MASK, length = node count      */
+} ca_match_spec;
+
+typedef struct ca_pred_result {
+    int32_t  type;                            /* CA_PRED_*                               */
+    int32_t  plugin;                          /* CA_PLUGIN_* that failed                 */
+    uint32_t reasons;                         /* CA_REASON_* (NodeResourcesFit)          */
+    int32_t  taint;                           /* lowest untolerated taint class          */
+} ca_pred_result;
+
+/* Node-group template for Estimate: NodeInfo template (orchestrator.go:444-491) and the
+ * aggregate of its pods (DaemonSets), copied onto every new node (scheduler.go:73-91). */
+typedef struct ca_template {
+    ca_node_spec node;
+    int64_t  used_milli_cpu;
+    int64_t  used_memory;
+    int64_t  used_ephemeral;
+    int64_t  used_scalar[CA_MAX_SCALAR];
+    int64_t  used_pods;
+    uint64_t used_ports[CA_PORT_WORDS];
+} ca_template;
+
+/* thresholdBasedEstimationLimiter (threshold_based_limiter.go:27-64).  Duration must be 0
+ * for a deterministic result; the kernels implement the node cap only. */
+typedef struct ca_limiter {
+    int32_t max_nodes;                        /* 0 = unlimited                           */
+    int32_t reserved;
+} ca_limiter;
+
+typedef struct ca_estimate_result {
+    int32_t  node_count;                      /* len(newNodesWithPods)                   */
+    int32_t  n_scheduled;                     /* len(scheduledPods)                      */
+    int32_t  nodes_added;                     /* new nodes created (incl. empty ones)    */
+    int32_t  last_index_in;                   /* lastIndex the group started from        */
+    int32_t  last_index_out;                  /* lastIndex after the group               */
+    int32_t  status;                          /* CA_OK or CA_EUNSUPPORTED                */
+    uint64_t evals;                           /* filter-chain evaluations performed      */
+} ca_estimate_result;
+
+typedef struct ca_removal_result {
+    int32_t  removable;                       /* 1: NodeToBeRemoved, 0: UnremovableNode  */
+    int32_t  reason;                          /* CA_UNREMOVABLE_*                        */
+    int32_t  n_placed;                        /* pods placed before success/failure      */
+    int32_t  last_index_in;
+    uint64_t evals;
+} ca_removal_result;
+
+typedef struct ca_mirror ca_mirror;
+typedef struct ca_podset ca_podset;
+
+/* ---- library ---------------------------------------------------------------- */
+int ca_abi_version(void);
+/* sizes of every ABI struct, in declaration order, for binding checks */
+int ca_abi_struct_sizes(int32_t* out, int32_t cap);
+int ca_device_count(int32_t* out);
+const char* ca_status_string(int status);
+
+/* ---- mirror: the SoA ClusterSnapshot data plane in HBM ---------------------- */
+int ca_mirror_create(int32_t device, ca_mirror** out);
+int ca_mirror_destroy(ca_mirror* m);
+int ca_mirror_clear(ca_mirror* m);                                   /* Clear()          */
+int ca_mirror_add_nodes(ca_mirror* m, const ca_node_spec* nodes, int32_t n,
+                        int32_t* out_first_pos);                     /* AddNode*         */
+/* Scheduled pods: AddPod(pod, nodeName) for each (t->pods[pod_idx[i]], node_pos[i]); the
+ * mirror keeps a copy of each record and of its selector terms.  out_ids receive mirror
+ * pod ids (stable for the mirror's lifetime). */
+int ca_mirror_add_pods(ca_mirror* m, const ca_pod_table* t, const int32_t* pod_idx,
+                       const int32_t* node_pos, int32_t n, int32_t* out_ids);
+int ca_mirror_remove_pod(ca_mirror* m, int32_t pod_id);              /* RemovePod        */
+int ca_mirror_fork(ca_mirror* m);                                    /* Fork             */
+int ca_mirror_revert(ca_mirror* m);                                  /* Revert           */
+int ca_mirror_commit(ca_mirror* m);                                  /* Commit           */
+int ca_mirror_node_count(const ca_mirror* m, int32_t* out);
+int ca_mirror_pod_node(const ca_mirror* m, int32_t pod_id, int32_t* out_node_pos);
+/* node pods in NodeInfo.Pods order (ids), returns count in *out_n (CA_ECAPACITY if cap short) */
+int ca_mirror_node_pods(const ca_mirror* m, int32_t node_pos, int32_t* out_ids, int32_t cap,
+                        int32_t* out_n);
+
+/* ---- device-resident pod sets (pending pods for Estimate) ------------------ */
+int ca_podset_create(ca_mirror* m, const ca_pod_table* t, ca_podset** out);
+int ca_podset_destroy(ca_podset* s);
+
+/* ---- predicate checker ------------------------------------------------------- */
+/* FitsAnyNodeMatching: *out_node = position or -1.  *out_prefilter_failed = 1 when the
+ * PreFilter failed (the reference returns an error without scanning).  *last_index is
+ * updated exactly as schedulerbased.go:131.  evals (may be NULL) accumulates
+ * RunFilterPlugins calls. */
+int ca_fits_any_node(ca_mirror* m, const ca_pod_table* t, int32_t pod, const ca_match_spec* match,
+                     int32_t* last_index, int32_t* out_node, int32_t* out_prefilter_failed,
+                     uint64_t* evals);
+int ca_check_predicates(ca_mirror* m, const ca_pod_table* t, int32_t pod, int32_t node_pos,
+                        ca_pred_result* out);
+/* Dense feasibility: out[p*n_nodes + n] = 1 iff RunFilterPlugins(pod p, node n) succeeds
+ * (CheckPredicates semantics, PreFilter failure -> 0). */
+int ca_fits_matrix(ca_mirror* m, const ca_podset* s, uint8_t* out);
+
+/* ---- estimator ---------------------------------------------------------------- */
+/* Estimate() for G node groups in order, sharing lastIndex as the reference's single
+ * checker does.  Group g's pods are pod_idx[group_off[g] .. group_off[g+1])
+ * (indices into the pod set, in the order Estimate receives them).  Outputs:
+ * results[g]; sched_pod/sched_node[group_off[g] + i] = i-th scheduled pod (pod set index)
+ * and the new-node ordinal it went to (sched_node may be NULL).  Ties of the float64
+ * score are broken by position in the group's list (stable order). */
+int ca_estimate_batch(ca_mirror* m, const ca_podset* s,
+                      const int32_t* group_off, const int32_t* pod_idx,
+                      const ca_template* templates, int32_t n_groups,
+                      const ca_limiter* limiter, int32_t* last_index,
+                      ca_estimate_result* results, int32_t* sched_pod, int32_t* sched_node);
+
+/* Prepared form for repeated calls (bench): uploads group lists/templates once. */
+typedef struct ca_estimate_plan ca_estimate_plan;
+int ca_estimate_plan_create(ca_mirror* m, const ca_podset* s, const int32_t* group_off,
+                            const int32_t* pod_idx, const ca_template* templates,
+                            int32_t n_groups, ca_estimate_plan** out);
+int ca_estimate_plan_run(ca_estimate_plan* p, const ca_limiter* limiter, int32_t* last_index,
+                         ca_estimate_result* results, int32_t* sched_pod, int32_t* sched_node);
+int ca_estimate_plan_destroy(ca_estimate_plan* p);
+/* statistics of the last run: speculation rounds, kernel time of the chain kernel (ms) */
+int ca_estimate_plan_stats(const ca_estimate_plan* p, int32_t* rounds, float* chain_ms,
+                           float* sort_ms, float* total_ms);
+
+/* ---- removal simulator ------------------------------------------------------- */
+/* FindNodesToRemove(candidates, destinations) with legacy semantics (canPersist=false).
+ * cand_status[c] != 0 carries the host-side GetPodsToMove verdict (drain.go:50-90):
+ * CA_UNREMOVABLE_BLOCKED_BY_POD / _UNEXPECTED_ERROR.  Pods to move for candidate c are
+ * move_pods[move_off[c] .. move_off[c+1]) (mirror pod ids, NodeInfo.Pods order).
+ * hints[pod_id]: hinted node position or -1 (Hints.Get), updated in place (Hints.Set).
+ * out_dest[move_off[c]+i] = destination of the i-th moved pod or -1. */
+int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t n_candidates,
+                            const uint8_t* dest_mask, const int32_t* cand_status,
+                            const int32_t* move_off, const int32_t* move_pods,
+                            int32_t* hints, int32_t* last_index,
+                            ca_removal_result* results, int32_t* out_dest);
+int ca_removal_stats(const ca_mirror* m, int32_t* rounds, float* kernel_ms, float* total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CASIM_H */

@@ -225,14 +225,23 @@ __device__ inline int32_t wave_max32(int32_t v) {
     return v;
 }
 
-struct ChainSmem {
-    int64_t* cpu; int64_t* mem; int64_t* eph; int32_t* pods; uint8_t* used;
-    uint64_t* ports;      // [kcap][CA_PORT_WORDS]   (use_ports)
-    int64_t* scalar;      // [CA_MAX_SCALAR][kcap]  (use_scalar)
-    int64_t* scpu; int64_t* smem; int64_t* seph; int32_t* spods;   // block summaries
+// New-node row in LDS: free resources of one template copy (32 B, two ds_read_b128).
+struct alignas(16) NodeRec {
+    int64_t cpu, mem, eph;
+    int32_t pods;      // free pod slots
+    int32_t used;      // newNodesWithPods membership
 };
+static_assert(sizeof(NodeRec) == 32, "NodeRec");
 
-// One wavefront per node group.  New-node rows live in LDS (kcap rows).
+// NodeResourcesFit on a row (fit.go:256-300), branch-free so all loads issue together.
+__device__ inline bool rec_fits(const NodeRec& r, int64_t pcpu, int64_t pmem, int64_t peph, bool zero) {
+    const bool res = (pcpu <= r.cpu) & (pmem <= r.mem) & (peph <= r.eph);
+    return (r.pods >= 1) & (zero | res);
+}
+
+// One wavefront per node group.  LDS: NodeRec rows[kcap], block summaries[kcap/64]
+// (per-dimension maxima over a 64-row block, allowed to be stale-high), and the
+// optional port / scalar columns.
 __global__ void __launch_bounds__(64) k_ffd_chain(
     const GroupMeta* __restrict__ groups, const StreamPod* __restrict__ stream, const ca_template* __restrict__ tmpls,
     const ca_pod_spec* __restrict__ specs, const PodHot* __restrict__ ph, const int32_t* __restrict__ lin_arr,
@@ -254,46 +263,51 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
         return;
     }
     const int nb_cap = (kcap + 63) >> 6;
-    // carve LDS
-    ChainSmem S;
-    unsigned char* p = smem_raw;
-    S.cpu = (int64_t*)p; p += 8 * (size_t)kcap;
-    S.mem = (int64_t*)p; p += 8 * (size_t)kcap;
-    S.eph = (int64_t*)p; p += 8 * (size_t)kcap;
-    S.scpu = (int64_t*)p; p += 8 * (size_t)nb_cap;
-    S.smem = (int64_t*)p; p += 8 * (size_t)nb_cap;
-    S.seph = (int64_t*)p; p += 8 * (size_t)nb_cap;
-    S.ports = (uint64_t*)p; if (use_ports) p += 8 * CA_PORT_WORDS * (size_t)kcap;
-    S.scalar = (int64_t*)p; if (use_scalar) p += 8 * CA_MAX_SCALAR * (size_t)kcap;
-    S.pods = (int32_t*)p; p += 4 * (size_t)kcap;
-    S.spods = (int32_t*)p; p += 4 * (size_t)nb_cap;
-    S.used = (uint8_t*)p;
+    NodeRec* R = reinterpret_cast<NodeRec*>(smem_raw);
+    NodeRec* SUM = R + kcap;
+    uint64_t* PORTS = reinterpret_cast<uint64_t*>(SUM + nb_cap);               // [kcap][CA_PORT_WORDS]
+    int64_t* SC = reinterpret_cast<int64_t*>(PORTS + (use_ports ? (size_t)CA_PORT_WORDS * kcap : 0));  // [8][kcap]
 
     const ca_template& tp = tmpls[gm.tmpl];
-    const int64_t tcpu = gm.tcpu, tmem = gm.tmem, teph = gm.teph;
-    const int32_t tpods = gm.tpods;
+    NodeRec trec;                 // a fresh template copy
+    trec.cpu = gm.tcpu; trec.mem = gm.tmem; trec.eph = gm.teph; trec.pods = gm.tpods; trec.used = 0;
 
     int32_t k = 0;              // new nodes so far
     int32_t granted = 0;        // limiter.nodes
     int32_t last_node = -1;     // lastNodeName
-    int64_t L = lin;            // the checker's lastIndex
+    int32_t L = lin;            // the checker's lastIndex
     int32_t nsched = 0;
     uint64_t evals = 0;
     bool first_success = false, sensitive = false;
 
     const int32_t P = gm.count;
     const StreamPod* gs = stream + gm.off;
-    StreamPod cur;               // this lane's prefetched stream entry
+    // Stream double buffer: lane l holds entry (window + l) in `cur` and (window + 64 + l)
+    // in `nxt`; the next window is requested 64 steps before it is read.  Outputs are
+    // kept in lanes (lane i = i-th placement of the window) and stored once per window,
+    // before the prefetch, so no step waits on a store (vmcnt counts both).
+    StreamPod cur = {}, nxt = {};
     if (lane < P) cur = gs[lane];
+    if (64 + lane < P) nxt = gs[64 + lane];
+    int32_t out_pod = -1, out_node = -1;
+    int32_t flushed = 0;         // placements already stored
 
     for (int32_t step = 0; step < P; step++) {
         const int sl = step & 63;
         if (sl == 0 && step > 0) {
-            if (step + lane < P) cur = gs[step + lane];
+            const int32_t pend = nsched - flushed;
+            if (lane < pend) {
+                sched_pod[gm.off + flushed + lane] = out_pod;
+                if (sched_node) sched_node[gm.off + flushed + lane] = out_node;
+            }
+            flushed = nsched;
+            cur = nxt;
+            if (step + 64 + lane < P) nxt = gs[step + 64 + lane];
         }
         const int64_t pcpu = rl64(cur.cpu, sl), pmem = rl64(cur.mem, sl), peph = rl64(cur.eph, sl);
         const int32_t pidx = rl32(cur.pod, sl);
         const uint32_t sf = (uint32_t)rl32((int32_t)cur.flags, sl);
+        const bool zero = (sf & SF_ZERO) != 0;
 
         // rare per-pod data (ports / scalars) from the full record
         uint64_t pconf[CA_PORT_WORDS] = {0, 0}, puse[CA_PORT_WORDS] = {0, 0};
@@ -304,69 +318,72 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
             for (int w = 0; w < CA_PORT_WORDS; w++) { pconf[w] = s.port_conflict[w]; puse[w] = s.port_use[w]; }
             for (int i = 0; i < CA_MAX_SCALAR; i++) psc[i] = s.req_scalar[i];
         }
-        const bool zero = (sf & SF_ZERO) != 0;
 
         // ---- FitsAnyNodeMatching(newNodeNames) (binpacking_estimator.go:91-93) ----
         int32_t found = -1;
         if ((sf & SF_EVAL) && k > 0) {
             if (sf & SF_FA_OK) {
-                const int64_t len = (int64_t)n_base + k;
-                const int64_t s0 = L % len;
-                const int32_t j0 = s0 > n_base ? (int32_t)(s0 - n_base) : 0;   // first new node visited
+                const int32_t len = n_base + k;
+                int32_t s0 = L;                                                // (lastIndex+i) % len at i = 0
+                if (s0 >= len) s0 = (int32_t)((uint32_t)s0 % (uint32_t)len);   // only for a caller-supplied L
+                const int32_t j0 = s0 > n_base ? s0 - n_base : 0;              // first new node visited
                 const int32_t nb = (k + 63) >> 6;
                 const int32_t b0 = j0 >> 6;
+                const bool lower_part = (j0 & 63) != 0;    // block b0 is visited twice (>= j0, then < j0)
                 for (int32_t rbase = 0; rbase <= nb && found < 0; rbase += 64) {
+                    // visit order: rotated block r -> block (b0 + r) mod nb; r == nb is b0's lower part
                     const int32_t rb = rbase + lane;
-                    bool adm = false;
-                    if (rb <= nb && !(rb == nb && (j0 & 63) == 0)) {
-                        const int32_t b = rb < nb ? (b0 + rb) % nb : b0;
-                        adm = S.spods[b] >= 1;
-                        if (!zero) adm = adm && S.scpu[b] >= pcpu && S.smem[b] >= pmem && S.seph[b] >= peph;
-                    }
+                    int32_t b = rb < nb ? b0 + rb : b0;
+                    if (b >= nb) b -= nb;
+                    const bool rb_ok = (rb < nb) | ((rb == nb) & lower_part);
+                    const NodeRec sr = SUM[rb_ok ? b : 0];
+                    const bool adm = rb_ok & rec_fits(sr, pcpu, pmem, peph, zero);
                     uint64_t amask = __ballot(adm);
                     while (amask && found < 0) {
                         const int l = __builtin_ctzll(amask);
                         amask &= amask - 1;
                         const int32_t r = rbase + l;
-                        const int32_t b = r < nb ? (b0 + r) % nb : b0;
-                        const int32_t j = (b << 6) + lane;
-                        bool valid = j < k;
-                        if (r == 0) valid = valid && j >= j0;
-                        if (r == nb) valid = valid && j < j0;
-                        bool fit = false;
-                        if (valid) {
-                            fit = S.pods[j] >= 1;
-                            if (!zero) fit = fit && pcpu <= S.cpu[j] && pmem <= S.mem[j] && peph <= S.eph[j];
-                            if (fit && (sf & SF_SCALAR)) {
-                                for (int i = 0; i < CA_MAX_SCALAR; i++)
-                                    if (psc[i] != 0 && psc[i] > S.scalar[(size_t)i * kcap + j]) fit = false;
-                            }
-                            if (fit && (sf & SF_PORTS)) {
-                                uint64_t c = 0;
-                                for (int w = 0; w < CA_PORT_WORDS; w++) c |= S.ports[(size_t)j * CA_PORT_WORDS + w] & pconf[w];
-                                fit = c == 0;
-                            }
+                        int32_t bb = r < nb ? b0 + r : b0;
+                        if (bb >= nb) bb -= nb;
+                        const int32_t j = (bb << 6) + lane;
+                        const bool valid = (j < k) & ((r != 0) | (j >= j0)) & ((r != nb) | (j < j0));
+                        const NodeRec nr = R[j < k ? j : 0];
+                        bool fit = valid & rec_fits(nr, pcpu, pmem, peph, zero);
+                        if (sf & SF_SCALAR) {
+                            for (int i = 0; i < CA_MAX_SCALAR; i++)
+                                fit = fit & !((psc[i] != 0) & (j < k) && psc[i] > SC[(size_t)i * kcap + (j < k ? j : 0)]);
+                        }
+                        if (sf & SF_PORTS) {
+                            uint64_t c = 0;
+                            for (int w = 0; w < CA_PORT_WORDS; w++) c |= PORTS[(size_t)(j < k ? j : 0) * CA_PORT_WORDS + w] & pconf[w];
+                            fit = fit & (c == 0);
                         }
                         const uint64_t fmask = __ballot(fit);
                         if (fmask) {
-                            found = (b << 6) + __builtin_ctzll(fmask);
+                            found = (bb << 6) + __builtin_ctzll(fmask);
                         } else {
-                            // refresh the block summary exactly (all rows of block b)
-                            const int32_t jj = (b << 6) + lane;
-                            const bool in = jj < k;
-                            const int64_t mc = wave_max64(in ? S.cpu[jj] : INT64_MIN);
-                            const int64_t mm = wave_max64(in ? S.mem[jj] : INT64_MIN);
-                            const int64_t me = wave_max64(in ? S.eph[jj] : INT64_MIN);
-                            const int32_t mp = wave_max32(in ? S.pods[jj] : INT32_MIN);
-                            if (lane == 0) { S.scpu[b] = mc; S.smem[b] = mm; S.seph[b] = me; S.spods[b] = mp; }
+                            // no row of the visited part fits: tighten the block summary
+                            // to the exact per-dimension maxima of the whole block
+                            const bool in = j < k;
+                            const int64_t mc = wave_max64(in ? nr.cpu : INT64_MIN);
+                            const int64_t mm = wave_max64(in ? nr.mem : INT64_MIN);
+                            const int64_t me = wave_max64(in ? nr.eph : INT64_MIN);
+                            const int32_t mp = wave_max32(in ? nr.pods : INT32_MIN);
+                            if (lane == 0) {
+                                NodeRec sm;
+                                sm.cpu = mc; sm.mem = mm; sm.eph = me; sm.pods = mp; sm.used = 0;
+                                SUM[bb] = sm;
+                            }
                         }
                     }
                 }
                 if (found >= 0) {
-                    const int32_t off = (found - j0 + k) % k;
+                    int32_t off = found - j0;                                  // rotated offset among new nodes
+                    if (off < 0) off += k;
                     evals += (uint64_t)off + 1;
                     if (!first_success) { first_success = true; sensitive = k >= 2; }
-                    L = ((int64_t)n_base + found + 1) % len;                       // schedulerbased.go:131
+                    L = n_base + found + 1;                                    // schedulerbased.go:131
+                    if (L >= len) L -= len;
                 } else {
                     evals += (uint64_t)k;
                 }
@@ -378,26 +395,24 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
             // PermissionToAddNode (threshold_based_limiter.go:46-56), before the empty-node skip
             if (max_nodes > 0 && granted >= max_nodes) break;
             granted++;
-            if (last_node >= 0 && !S.used[last_node]) continue;               // :114-116
+            if (last_node >= 0 && !R[last_node].used) continue;               // :114-116
             if (k >= kcap) { res.status = CA_ECAPACITY; break; }
             // addNewNodeToSnapshot: a template copy (:146-159)
             const int32_t nn = k;
             if (lane == 0) {
-                S.cpu[nn] = tcpu; S.mem[nn] = tmem; S.eph[nn] = teph; S.pods[nn] = tpods; S.used[nn] = 0;
-                const int32_t b = nn >> 6;
-                S.scpu[b] = tcpu; S.smem[b] = tmem; S.seph[b] = teph; S.spods[b] = tpods;
+                R[nn] = trec;
+                SUM[nn >> 6] = trec;   // a fresh copy is the largest a row can be
             }
-            if (use_ports && lane < CA_PORT_WORDS) S.ports[(size_t)nn * CA_PORT_WORDS + lane] = tp.used_ports[lane];
+            if (use_ports && lane < CA_PORT_WORDS) PORTS[(size_t)nn * CA_PORT_WORDS + lane] = tp.used_ports[lane];
             if (use_scalar && lane < CA_MAX_SCALAR)
-                S.scalar[(size_t)lane * kcap + nn] = wsub(tp.node.alloc_scalar[lane], tp.used_scalar[lane]);
+                SC[(size_t)lane * kcap + nn] = wsub(tp.node.alloc_scalar[lane], tp.used_scalar[lane]);
             k++;
             last_node = nn;
             // CheckPredicates(pod, newNode) (:132-134)
             if (sf & SF_CP_EVAL) evals++;
             bool ok = (sf & SF_CP_OK) != 0;
             if (ok) {
-                ok = tpods >= 1;
-                if (!zero) ok = ok && pcpu <= tcpu && pmem <= tmem && peph <= teph;
+                ok = rec_fits(trec, pcpu, pmem, peph, zero);
                 if (ok && (sf & SF_SCALAR)) {
                     for (int i = 0; i < CA_MAX_SCALAR; i++)
                         if (psc[i] != 0 && psc[i] > wsub(tp.node.alloc_scalar[i], tp.used_scalar[i])) ok = false;
@@ -413,35 +428,43 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
         }
         // AddPod(pod, node) (:96 / :135) — NodeInfo.update on the new-node row
         if (lane == 0) {
-            S.cpu[found] = wsub(S.cpu[found], pcpu);
-            S.mem[found] = wsub(S.mem[found], pmem);
-            S.eph[found] = wsub(S.eph[found], peph);
-            S.pods[found] -= 1;
-            S.used[found] = 1;
-            sched_pod[gm.off + nsched] = pidx;
-            if (sched_node) sched_node[gm.off + nsched] = found;
+            NodeRec r = R[found];
+            r.cpu = wsub(r.cpu, pcpu);
+            r.mem = wsub(r.mem, pmem);
+            r.eph = wsub(r.eph, peph);
+            r.pods -= 1;
+            r.used = 1;
+            R[found] = r;
         }
+        if (lane == nsched - flushed) { out_pod = pidx; out_node = found; }
         if (sf & SF_SCALAR) {
             if (lane < CA_MAX_SCALAR) {
                 const size_t ix = (size_t)lane * kcap + found;
-                S.scalar[ix] = wsub(S.scalar[ix], psc[lane]);
+                SC[ix] = wsub(SC[ix], psc[lane]);
             }
         }
         if (sf & SF_PORTS) {
-            if (lane < CA_PORT_WORDS) S.ports[(size_t)found * CA_PORT_WORDS + lane] |= puse[lane];
+            if (lane < CA_PORT_WORDS) PORTS[(size_t)found * CA_PORT_WORDS + lane] |= puse[lane];
         }
         nsched++;
         __builtin_amdgcn_wave_barrier();
     }
+    {
+        const int32_t pend = nsched - flushed;
+        if (lane < pend) {
+            sched_pod[gm.off + flushed + lane] = out_pod;
+            if (sched_node) sched_node[gm.off + flushed + lane] = out_node;
+        }
+    }
     // newNodesWithPods
     int32_t cnt = 0;
-    for (int32_t j = lane; j < k; j += 64) cnt += S.used[j];
+    for (int32_t j = lane; j < k; j += 64) cnt += R[j].used;
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
     if (lane == 0) {
         res.node_count = cnt;
         res.n_sched = nsched;
         res.nodes_added = k;
-        res.lout = (int32_t)L;
+        res.lout = L;
         res.sensitive = sensitive ? 1 : 0;
         res.had_success = first_success ? 1 : 0;
         res.evals = evals;
@@ -529,10 +552,9 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
 
 size_t chain_lds_bytes(int32_t kcap, bool use_ports, bool use_scalar) {
     const size_t nb = (size_t)((kcap + 63) >> 6);
-    size_t b = 24 * (size_t)kcap + 24 * nb;
+    size_t b = 32 * ((size_t)kcap + nb);
     if (use_ports) b += 8 * CA_PORT_WORDS * (size_t)kcap;
     if (use_scalar) b += 8 * CA_MAX_SCALAR * (size_t)kcap;
-    b += 4 * (size_t)kcap + 4 * nb + (size_t)kcap;
     return (b + 15) & ~(size_t)15;
 }
 
@@ -552,6 +574,10 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     const size_t lds = chain_lds_bytes(kcap, p->use_ports, p->use_scalar);
     if (lds > 160 * 1024) return CA_EUNSUPPORTED;   // HBM-backed variant is future work
     CA_HIP_CHECK(hipMemsetAsync(p->d_unsup.ptr, 0, sizeof(uint32_t) * G, st));
+    if (p->total > 0) {   // entries past n_scheduled read back as -1
+        CA_HIP_CHECK(hipMemsetAsync(p->d_sched_pod.ptr, 0xFF, sizeof(int32_t) * p->total, st));
+        CA_HIP_CHECK(hipMemsetAsync(p->d_sched_node.ptr, 0xFF, sizeof(int32_t) * p->total, st));
+    }
     CA_HIP_CHECK(hipEventRecord(m->ev0, st));
     // 1-3: score, sort, stream
     if (p->total > 0) {
@@ -579,6 +605,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     std::vector<uint8_t> need(G, 1);
     std::vector<ChainOut> outs(G);
     std::vector<uint8_t> accepted(G, 0);
+    std::vector<int32_t> true_lin(G, *last_index);
     int32_t rounds = 0;
     float chain_ms = 0;
     for (;;) {
@@ -612,6 +639,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         std::fill(need.begin(), need.end(), 0);
         for (int32_t g = 0; g < G; g++) {
             const ChainOut& o = outs[g];
+            true_lin[g] = (int32_t)cur;     // exact once the walk converged (known stays true)
             const bool insensitive = o.status != CA_OK || !o.sensitive;
             if (known && (o.lin == cur || insensitive)) {
                 accepted[g] = 1;
@@ -653,8 +681,8 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         r.node_count = o.node_count;
         r.n_scheduled = o.n_sched;
         r.nodes_added = o.nodes_added;
-        r.last_index_in = o.lin;
-        r.last_index_out = o.status == CA_OK && o.had_success ? o.lout : o.lin;
+        r.last_index_in = true_lin[g];
+        r.last_index_out = o.status == CA_OK && o.had_success ? o.lout : true_lin[g];
         r.status = o.status;
         r.evals = o.evals;
     }

@@ -260,7 +260,8 @@ __global__ void __launch_bounds__(256) k_fits_scan(
     const PodHot p = ph[pod];
     bool vis = false, fit = false;
     if (i < n) {
-        const int32_t pos = (int32_t)((L + i) % n);                       // schedulerbased.go:115
+        int32_t pos = (int32_t)L + i;                                      // schedulerbased.go:115
+        if (pos >= n) pos -= n;
         bool m = pos != exclude;
         if (kind == CA_MATCH_RANGE) m = m && pos >= lo && pos < hi;
         else if (kind == CA_MATCH_MASK) m = m && mask[pos] != 0;
@@ -597,7 +598,7 @@ int ca_fits_any_node(ca_mirror* m, const ca_pod_table* t, int32_t pod, const ca_
     if ((rc = m->d_scratch0.reserve(sizeof(unsigned long long) * 2 * (size_t)words)) != CA_OK) return rc;
     unsigned long long* dfit = m->d_scratch0.as<unsigned long long>();
     unsigned long long* dvis = dfit + words;
-    const int64_t L = *last_index;
+    const int64_t L = (int64_t)((uint32_t)*last_index % (uint32_t)n);   // (lastIndex+i)%len
     hipLaunchKernelGGL(k_fits_scan, dim3((n + 255) / 256), dim3(256), 0, m->stream, m->d_hot.as<NodeHot>(),
                        m->d_ext.as<NodeExt>(), m->d_static.as<NodeStatic>(), n, dp.hot.as<PodHot>(),
                        dp.spec.as<ca_pod_spec>(), dp.terms.as<ca_selector_term>(), dp.reqs.as<ca_selector_req>(),

@@ -5,21 +5,30 @@
 // (TrySchedulePods, hints), CA/utils/tpu/tpu.go:57-79 (ClearTPURequests).
 //
 // Every candidate is simulated on a fork that is reverted afterwards, so candidates
-// share no snapshot state: one wavefront per candidate keeps its placements in an
-// LDS overlay over the read-only base rows.  The only coupling is the checker's
-// lastIndex; the host driver runs all candidates from guessed
-// lastIndex values and re-runs the ones whose guess was wrong until every
-// candidate's input equals its predecessor's output.
+// share no snapshot state; the only coupling is the checker's lastIndex.
+// Two kernels:
+//   k_sweep_table  one wavefront per candidate, one lastIndex per LANE: lane w runs the
+//                  candidate from L = window_start + w and reports where lastIndex ends.
+//                  The host composes these 64-wide tables along the candidate order to
+//                  find every candidate's exact input lastIndex (re-centring the windows
+//                  that missed).
+//   k_sweep        one wavefront per candidate at its exact lastIndex: 64-node chunks of
+//                  the rotating scan with an LDS overlay of the candidate's placements;
+//                  produces every output (removable, destinations, hints, evals).
 #include "mirror.h"
 #include "device_filters.h"
 
 #include <cstring>
+#include <cstdlib>
 #include <algorithm>
 #include <chrono>
 
 namespace casim {
 
-constexpr int OV_CAP = 128;   // distinct destination nodes per candidate
+constexpr int OV_CAP = 128;     // distinct destination nodes per candidate (k_sweep)
+constexpr int TB_MAXP = 128;    // moved pods per candidate handled by k_sweep_table
+constexpr int TB_SCAN = 512;    // per-lane scan bound in k_sweep_table (longer: exact kernel)
+constexpr int32_t TB_UNKNOWN = -1;
 
 struct alignas(16) SweepOut {
     int32_t removable, reason, n_placed, lin;
@@ -43,6 +52,7 @@ __device__ inline int64_t rl64s(int64_t v, int lane) {
     const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), lane);
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
+__device__ inline int32_t rl32s(int32_t v, int lane) { return (int32_t)__builtin_amdgcn_readlane((uint32_t)v, lane); }
 
 // moved-pod semantics: Spec.NodeName cleared (cluster.go:235-240), TPU requests
 // cleared (tpu.go:57-79)
@@ -54,11 +64,16 @@ __device__ inline uint32_t moved_flags(uint32_t f) {
     return m;
 }
 
-// Evaluate the filter chain for one node with the candidate's overlay applied.
-// All lanes hold the same (pod, node) — used for the hint check.
-__device__ inline bool eval_node_uniform(const ca_pod_spec& s, const PodHot& p, const int64_t* psc,
-                                         const ca_selector_term* terms, const ca_selector_req* reqs,
-                                         NodeHot h, NodeExt e, const NodeStatic* st_row, bool apply_unsched) {
+// Resource part of NodeResourcesFit on a row, branch-free (fit.go:256-300).
+__device__ inline bool hot_fits(const PodHot& p, const NodeHot& h) {
+    const bool res = (p.cpu <= h.cpu) & (p.mem <= h.mem) & (p.eph <= h.eph);
+    return (h.pods >= 1) & (((p.flags & PF_ALL_ZERO) != 0) | res);
+}
+
+// Full filter chain on a (possibly overlay-adjusted) row; per lane.
+__device__ inline bool eval_node(const ca_pod_spec& s, const PodHot& p, const int64_t* psc,
+                                 const ca_selector_term* terms, const ca_selector_req* reqs,
+                                 const NodeHot& h, const NodeExt& e, const NodeStatic* st_row, bool apply_unsched) {
     if (apply_unsched && (h.flags & NF_UNSCHED) && !(p.flags & PF_TOL_UNSCHED)) return false;
     const bool need_static = (p.flags & (PF_NODE_NAME | PF_AFFINITY)) ||
                              ((h.flags & NF_TAINTS) && !(p.flags & PF_TAINT_MASK_ALL));
@@ -74,6 +89,25 @@ __device__ inline bool eval_node_uniform(const ca_pod_spec& s, const PodHot& p, 
     return dev_fit_reasons(p.cpu, p.mem, p.eph, p.flags, psc, h.cpu, h.mem, h.eph, h.pods, e.scalar) == 0;
 }
 
+// static filters only where the pod needs them (taints / affinity / names)
+__device__ inline bool static_ok(const ca_pod_spec& s, const PodHot& p, const ca_selector_term* terms,
+                                 const ca_selector_req* reqs, const NodeHot& h, const NodeStatic* st_row) {
+    const bool need_static = (p.flags & (PF_NODE_NAME | PF_AFFINITY)) ||
+                             ((h.flags & NF_TAINTS) && !(p.flags & PF_TAINT_MASK_ALL));
+    if (!need_static) return true;
+    const NodeStatic ns = *st_row;
+    return dev_static_filters(s, p.flags, terms, reqs, ns, false) == CA_PLUGIN_NONE;
+}
+
+__device__ inline bool in_prefilter(const ca_pod_spec& s, const int32_t* names, int32_t name_id) {
+    bool ok = false;
+    for (int32_t k = 0; k < s.prefilter_count; k++) ok |= names[s.prefilter_first + k] == name_id;
+    return ok;
+}
+
+// ---------------------------------------------------------------------------
+// exact kernel: one wavefront per candidate at its exact lastIndex
+// ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) k_sweep(
     const NodeHot* __restrict__ hot, const NodeExt* __restrict__ ext, const NodeStatic* __restrict__ st, int32_t n,
     const uint8_t* __restrict__ dest_mask, const int32_t* __restrict__ cands, const int32_t* __restrict__ cand_status,
@@ -92,29 +126,50 @@ __global__ void __launch_bounds__(64) k_sweep(
     res.fa_success = 0; res.status = CA_OK; res.pad = 0; res.evals = 0; res.pad2 = 0;
     const int32_t node = cands[c];
     const int32_t mo = move_off[c], mn = move_off[c + 1] - mo;
-    for (int32_t i = lane; i < mn; i += 64) { out_dest[mo + i] = -1; hint_set[mo + i] = -1; }
     if (node < 0 || node >= n || !dest_mask[node]) {                          // cluster.go:157-160
+        for (int32_t i = lane; i < mn; i += 64) { out_dest[mo + i] = -1; hint_set[mo + i] = -1; }
         res.reason = CA_UNREMOVABLE_UNEXPECTED_ERROR;
         if (lane == 0) outs[c] = res;
         return;
     }
     if (cand_status[c] != 0) {                                                 // :162-169
+        for (int32_t i = lane; i < mn; i += 64) { out_dest[mo + i] = -1; hint_set[mo + i] = -1; }
         res.reason = cand_status[c];
         if (lane == 0) outs[c] = res;
         return;
     }
     int32_t npl = 0;          // overlay entries
-    int64_t L = lin;
+    int32_t L = lin;
+    if (n > 0 && L >= n) L = (int32_t)((uint32_t)L % (uint32_t)n);
     uint64_t evals = 0;
     bool fa_success = false;
     int32_t placed = 0;
     bool failed = false;
+    // lane i holds moved pod (batch + i): id, record, hint; outputs kept in lanes and
+    // stored once per batch (no per-pod store for a later load to wait behind)
+    int32_t my_id = -1, my_hint = -1, my_dest = -1, my_hset = -1;
+    PodHot my_p = {};
 
     for (int32_t i = 0; i < mn; i++) {
+        const int sl = i & 63;
+        if (sl == 0) {
+            if (i > 0) {   // flush the previous batch's outputs
+                out_dest[mo + i - 64 + lane] = my_dest;
+                hint_set[mo + i - 64 + lane] = my_hset;
+            }
+            my_dest = -1; my_hset = -1;
+            if (i + lane < mn) {
+                my_id = move_pods[mo + i + lane];
+                my_p = ph[my_id];
+                my_hint = hints[my_id];
+            }
+        }
         __syncthreads();
-        const int32_t id = move_pods[mo + i];
-        PodHot p = ph[id];
-        p.flags = moved_flags(p.flags);
+        PodHot p;
+        p.cpu = rl64s(my_p.cpu, sl); p.mem = rl64s(my_p.mem, sl); p.eph = rl64s(my_p.eph, sl);
+        p.flags = moved_flags((uint32_t)rl32s((int32_t)my_p.flags, sl));
+        p.spec = rl32s(my_p.spec, sl);
+        const int32_t h = rl32s(my_hint, sl);
         const ca_pod_spec& s = specs[p.spec];
         int64_t psc[CA_MAX_SCALAR];
         for (int k = 0; k < CA_MAX_SCALAR; k++) psc[k] = 0;
@@ -124,7 +179,6 @@ __global__ void __launch_bounds__(64) k_sweep(
         int32_t target = -1;
 
         // ---- findNodeWithHints (hinting_simulator.go:91-108) ----
-        const int32_t h = hints[id];
         if (h >= 0 && h < n && !pre_fail) {
             evals++;
             NodeHot nh = hot[h];
@@ -149,8 +203,8 @@ __global__ void __launch_bounds__(64) k_sweep(
                     }
                 }
             }
-            if (eval_node_uniform(s, p, psc, terms, reqs, nh, ne, st + h, true)) {
-                if (lane == 0) hint_set[mo + i] = h;                          // :95
+            if (eval_node(s, p, psc, terms, reqs, nh, ne, st + h, true)) {
+                if (lane == sl) my_hset = h;                                    // :95
                 if (h != node && dest_mask[h]) target = h;                      // :102
             }
         }
@@ -158,28 +212,24 @@ __global__ void __launch_bounds__(64) k_sweep(
         if (target < 0 && !pre_fail) {
             for (int32_t base = 0; base < n; base += 64) {
                 const int32_t off = base + lane;
-                const int32_t pos = (int32_t)((L + off) % n);
-                bool vis = false;
-                NodeHot nh;
-                if (off < n && pos != node && dest_mask[pos]) {
-                    nh = hot[pos];
-                    bool pf_ok = true;
-                    if (p.flags & PF_PREFILTER_NAMES) {
-                        const int32_t nm = st[pos].name_id;
-                        pf_ok = false;
-                        for (int32_t k = 0; k < s.prefilter_count; k++) pf_ok |= names[s.prefilter_first + k] == nm;
-                    }
-                    vis = pf_ok && !(nh.flags & NF_UNSCHED);
-                }
+                int32_t pos = L + off;                                        // (lastIndex+i) % len
+                if (pos >= n) pos -= n;
+                const int32_t rp = off < n ? pos : 0;
+                const uint8_t dm = dest_mask[rp];                             // both loads issue together
+                NodeHot nh = hot[rp];
+                bool vis = (off < n) & (pos != node) & (dm != 0) & !(nh.flags & NF_UNSCHED);
+                if (vis && (p.flags & PF_PREFILTER_NAMES)) vis = in_prefilter(s, names, st[pos].name_id);
                 // overlay entries inside this chunk
                 bool ov_here = false;
                 int32_t ov_slot = -1;
+                int32_t st0 = L + base;                                        // chunk start position
+                if (st0 >= n) st0 -= n;
                 for (int32_t q0 = 0; q0 < npl; q0 += 64) {
                     const int32_t q = q0 + lane;
                     bool in = false;
                     int32_t d = 0;
                     if (q < npl) {
-                        d = (int32_t)(((int64_t)ov.node[q] - (L + base)) % n);
+                        d = ov.node[q] - st0;
                         if (d < 0) d += n;
                         in = d < 64;
                     }
@@ -193,31 +243,18 @@ __global__ void __launch_bounds__(64) k_sweep(
                 }
                 bool fit = false;
                 if (vis) {
-                    NodeExt ne;
                     const bool need_ext = (p.flags & (PF_PORTS | PF_SCALAR_REQ)) || ov_here;
-                    if (need_ext) ne = ext[pos];
-                    if (ov_here) {
-                        nh.cpu = wsub(nh.cpu, ov.cpu[ov_slot]); nh.mem = wsub(nh.mem, ov.mem[ov_slot]);
-                        nh.eph = wsub(nh.eph, ov.eph[ov_slot]); nh.pods -= ov.pods[ov_slot];
-                        for (int w = 0; w < CA_PORT_WORDS; w++) ne.ports[w] |= ov.ports[ov_slot][w];
-                        for (int k = 0; k < CA_MAX_SCALAR; k++) ne.scalar[k] = wsub(ne.scalar[k], ov.scalar[ov_slot][k]);
-                    }
                     if (!need_ext) {
-                        // resource-only fast path: one 32-B row
-                        const bool need_static = (p.flags & (PF_NODE_NAME | PF_AFFINITY)) ||
-                                                 ((nh.flags & NF_TAINTS) && !(p.flags & PF_TAINT_MASK_ALL));
-                        fit = true;
-                        if (need_static) {
-                            const NodeStatic ns = st[pos];
-                            fit = dev_static_filters(s, p.flags, terms, reqs, ns, false) == CA_PLUGIN_NONE;
-                        }
-                        if (fit) {
-                            fit = nh.pods >= 1;
-                            if (!(p.flags & PF_ALL_ZERO))
-                                fit = fit && p.cpu <= nh.cpu && p.mem <= nh.mem && p.eph <= nh.eph;
-                        }
+                        fit = hot_fits(p, nh) && static_ok(s, p, terms, reqs, nh, st + pos);
                     } else {
-                        fit = eval_node_uniform(s, p, psc, terms, reqs, nh, ne, st + pos, false);
+                        NodeExt ne = ext[pos];
+                        if (ov_here) {
+                            nh.cpu = wsub(nh.cpu, ov.cpu[ov_slot]); nh.mem = wsub(nh.mem, ov.mem[ov_slot]);
+                            nh.eph = wsub(nh.eph, ov.eph[ov_slot]); nh.pods -= ov.pods[ov_slot];
+                            for (int w = 0; w < CA_PORT_WORDS; w++) ne.ports[w] |= ov.ports[ov_slot][w];
+                            for (int k = 0; k < CA_MAX_SCALAR; k++) ne.scalar[k] = wsub(ne.scalar[k], ov.scalar[ov_slot][k]);
+                        }
+                        fit = eval_node(s, p, psc, terms, reqs, nh, ne, st + pos, false);
                     }
                 }
                 const uint64_t fm = __ballot(fit), vm = __ballot(vis);
@@ -226,10 +263,12 @@ __global__ void __launch_bounds__(64) k_sweep(
                     const uint64_t below = (f == 63) ? ~0ull : ((2ull << f) - 1);
                     evals += (uint64_t)__popcll(vm & below);
                     const int32_t foff = base + f;
-                    target = (int32_t)((L + foff) % n);
-                    L = (L + foff + 1) % n;                                    // schedulerbased.go:131
+                    target = L + foff;
+                    if (target >= n) target -= n;
+                    L = target + 1;                                            // schedulerbased.go:131
+                    if (L >= n) L -= n;
                     fa_success = true;
-                    if (lane == 0) hint_set[mo + i] = target;                  // :123
+                    if (lane == sl) my_hset = target;                          // :123
                     break;
                 }
                 evals += (uint64_t)__popcll(vm);
@@ -259,24 +298,127 @@ __global__ void __launch_bounds__(64) k_sweep(
             ov.pods[slot] += 1;
             for (int w = 0; w < CA_PORT_WORDS; w++) ov.ports[slot][w] |= s.port_use[w];
             for (int k = 0; k < CA_MAX_SCALAR; k++) ov.scalar[slot][k] = wadd(ov.scalar[slot][k], psc[k]);
-            out_dest[mo + i] = target;
         }
+        if (lane == sl) my_dest = target;
         placed++;
+    }
+    if (mn > 0) {
+        // the batch that was being processed (the last one, or the one that failed)
+        const int32_t bi = failed ? (placed >> 6) << 6 : ((mn - 1) >> 6) << 6;
+        if (bi + lane < mn) { out_dest[mo + bi + lane] = my_dest; hint_set[mo + bi + lane] = my_hset; }
+        // batches after it were never loaded
+        for (int32_t i = bi + 64 + lane; i < mn; i += 64) { out_dest[mo + i] = -1; hint_set[mo + i] = -1; }
     }
     if (lane == 0) {
         res.n_placed = placed;
         if (!failed && placed == mn) { res.removable = 1; res.reason = CA_UNREMOVABLE_NONE; }
         else res.reason = CA_UNREMOVABLE_NO_PLACE;
-        res.lout = (int32_t)L;
+        res.lout = L;
         res.fa_success = fa_success ? 1 : 0;
         res.evals = evals;
         outs[c] = res;
     }
 }
 
+// ---------------------------------------------------------------------------
+// table kernel: lane w simulates the candidate from lastIndex = wstart + w.
+// A lane's placements all lie in the cyclic interval its scans have passed
+// ([L_start, L_cur)); a scan that would re-enter it (a full turn of the ring: a
+// NoPlace failure or a revisit) is left to the exact kernel, as are candidates with
+// hints or port/scalar pods.  Scans longer than TB_SCAN are left to it too.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_sweep_table(
+    const NodeHot* __restrict__ hot, const NodeStatic* __restrict__ st, int32_t n,
+    const uint8_t* __restrict__ dest_mask, const int32_t* __restrict__ cands, const int32_t* __restrict__ move_off,
+    const int32_t* __restrict__ move_pods, const PodHot* __restrict__ ph, const ca_pod_spec* __restrict__ specs,
+    const ca_selector_term* __restrict__ terms, const ca_selector_req* __restrict__ reqs,
+    const int32_t* __restrict__ names, const int32_t* __restrict__ hints, const int32_t* __restrict__ todo,
+    const int32_t* __restrict__ wstart, int32_t* __restrict__ table) {
+    const int t = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int32_t c = todo[t];
+    const int32_t node = cands[c];
+    const int32_t mo = move_off[c], mn = move_off[c + 1] - mo;
+    int32_t Ls = wstart[t] + lane;
+    if (Ls >= n) Ls -= n;
+    int32_t Lcur = Ls;
+    int32_t adv = 0;              // positions passed since Ls
+    bool unknown = mn > TB_MAXP;
+    // candidates with hints / ports / scalars go to the exact kernel
+    for (int32_t i = lane; i < mn; i += 64) {
+        const int32_t id = move_pods[mo + i];
+        const uint32_t f = moved_flags(ph[id].flags);
+        if ((hints[id] >= 0) | ((f & (PF_PORTS | PF_SCALAR_REQ)) != 0)) unknown = true;
+    }
+    unknown = __ballot(unknown) != 0;
+    if (!unknown) {
+        // lane-parallel prefetch of the moved pods' records (batch of 64)
+        int32_t my_id = -1;
+        PodHot my_p = {};
+        for (int32_t i = 0; i < mn; i++) {
+            const int sl = i & 63;
+            if (sl == 0 && i + lane < mn) { my_id = move_pods[mo + i + lane]; my_p = ph[my_id]; }
+            PodHot p;
+            p.cpu = rl64s(my_p.cpu, sl); p.mem = rl64s(my_p.mem, sl); p.eph = rl64s(my_p.eph, sl);
+            p.flags = moved_flags((uint32_t)rl32s((int32_t)my_p.flags, sl));
+            p.spec = rl32s(my_p.spec, sl);
+            if (p.flags & PF_PREFILTER_FAIL) break;                            // FitsAnyNode error: stop
+            const ca_pod_spec& s = specs[p.spec];
+            // lane-private rotating scan from this lane's lastIndex
+            int32_t steps = 0;
+            int32_t pos = Lcur;
+            bool lane_unknown = false;
+            while (!unknown) {
+                if (adv + steps >= n || steps >= TB_SCAN) { lane_unknown = true; break; }
+                const NodeHot nh = hot[pos];
+                const uint8_t dm = dest_mask[pos];
+                bool vis = (pos != node) & (dm != 0) & !(nh.flags & NF_UNSCHED);
+                if (vis && (p.flags & PF_PREFILTER_NAMES)) vis = in_prefilter(s, names, st[pos].name_id);
+                if (vis && hot_fits(p, nh) && static_ok(s, p, terms, reqs, nh, st + pos)) break;
+                steps++;
+                pos++;
+                if (pos >= n) pos = 0;
+            }
+            if (lane_unknown) unknown = true;
+            if (__ballot(!unknown) == 0) break;          // every lane handed over
+            if (!unknown) {
+                adv += steps + 1;
+                Lcur = pos + 1;
+                if (Lcur >= n) Lcur = 0;
+            }
+        }
+    }
+    table[(size_t)t * 64 + lane] = unknown ? TB_UNKNOWN : Lcur;
+}
+
 }  // namespace casim
 
 using namespace casim;
+
+namespace {
+
+inline int32_t wrap(int64_t v, int32_t n) {
+    if (n <= 0) return 0;
+    int64_t r = v % n;
+    if (r < 0) r += n;
+    return (int32_t)r;
+}
+
+int launch_exact(ca_mirror* m, hipStream_t st, int32_t C, int32_t n, DevBuf& d_mask, DevBuf& d_c, DevBuf& d_status,
+                 DevBuf& d_off, DevBuf& d_moves, DevBuf& d_hints, DevBuf& d_lin, DevBuf& d_need, DevBuf& d_dest,
+                 DevBuf& d_hset, DevBuf& d_out) {
+    hipLaunchKernelGGL(k_sweep, dim3(C), dim3(64), 0, st, m->d_hot.as<NodeHot>(), m->d_ext.as<NodeExt>(),
+                       m->d_static.as<NodeStatic>(), n, d_mask.as<uint8_t>(), d_c.as<int32_t>(),
+                       d_status.as<int32_t>(), d_off.as<int32_t>(), d_moves.as<int32_t>(),
+                       m->d_pods.hot.as<PodHot>(), m->d_pods.spec.as<ca_pod_spec>(),
+                       m->d_pods.terms.as<ca_selector_term>(), m->d_pods.reqs.as<ca_selector_req>(),
+                       m->d_pods.names.as<int32_t>(), d_hints.as<int32_t>(), d_lin.as<int32_t>(),
+                       d_need.as<uint8_t>(), d_dest.as<int32_t>(), d_hset.as<int32_t>(), d_out.as<SweepOut>());
+    CA_HIP_CHECK(hipGetLastError());
+    return CA_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -321,13 +463,23 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     int rc;
     if ((rc = m->sync_nodes()) != CA_OK) return rc;
     if ((rc = m->sync_pods()) != CA_OK) return rc;
-    // per-call inputs
     std::vector<int32_t> status((size_t)C, 0);
     if (cand_status) std::copy(cand_status, cand_status + C, status.begin());
     const size_t hint_n = std::max<size_t>(m->pods.size(), 1);
     std::vector<int32_t> h_hints(hint_n, -1);
     if (hints) std::copy(hints, hints + m->pods.size(), h_hints.begin());
-    DevBuf d_c, d_status, d_off, d_moves, d_hints, d_lin, d_need, d_dest, d_hset, d_out, d_mask;
+
+    // candidates whose simulation can move lastIndex: valid, not blocked, pods to move
+    std::vector<int32_t> sens;
+    for (int32_t c = 0; c < C; c++) {
+        const int32_t nd = candidates[c];
+        if (nd < 0 || nd >= n || !dest_mask[nd] || status[c] != 0) continue;
+        if (move_off[c + 1] - move_off[c] == 0) continue;
+        sens.push_back(c);
+    }
+    const int32_t S = (int32_t)sens.size();
+
+    DevBuf d_c, d_status, d_off, d_moves, d_hints, d_lin, d_need, d_dest, d_hset, d_out, d_mask, d_todo, d_ws, d_tab;
     if ((rc = d_c.reserve(sizeof(int32_t) * C)) != CA_OK) return rc;
     if ((rc = d_status.reserve(sizeof(int32_t) * C)) != CA_OK) return rc;
     if ((rc = d_off.reserve(sizeof(int32_t) * (C + 1))) != CA_OK) return rc;
@@ -339,6 +491,9 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     if ((rc = d_hset.reserve(sizeof(int32_t) * std::max(M, 1))) != CA_OK) return rc;
     if ((rc = d_out.reserve(sizeof(SweepOut) * C)) != CA_OK) return rc;
     if ((rc = d_mask.reserve((size_t)std::max(n, 1))) != CA_OK) return rc;
+    if ((rc = d_todo.reserve(sizeof(int32_t) * std::max(S, 1))) != CA_OK) return rc;
+    if ((rc = d_ws.reserve(sizeof(int32_t) * std::max(S, 1))) != CA_OK) return rc;
+    if ((rc = d_tab.reserve(sizeof(int32_t) * 64 * (size_t)std::max(S, 1))) != CA_OK) return rc;
     CA_HIP_CHECK(hipMemcpyAsync(d_c.ptr, candidates, sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
     CA_HIP_CHECK(hipMemcpyAsync(d_status.ptr, status.data(), sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
     CA_HIP_CHECK(hipMemcpyAsync(d_off.ptr, move_off, sizeof(int32_t) * (C + 1), hipMemcpyHostToDevice, st));
@@ -346,81 +501,174 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     CA_HIP_CHECK(hipMemcpyAsync(d_hints.ptr, h_hints.data(), sizeof(int32_t) * hint_n, hipMemcpyHostToDevice, st));
     if (n) CA_HIP_CHECK(hipMemcpyAsync(d_mask.ptr, dest_mask, (size_t)n, hipMemcpyHostToDevice, st));
 
-    std::vector<int32_t> lin((size_t)C, *last_index);
-    std::vector<uint8_t> need((size_t)C, 1);
-    std::vector<SweepOut> outs((size_t)C), fresh((size_t)C);
-    int32_t rounds = 0;
+    // ---- 1. every candidate's input lastIndex ----
+    std::vector<int32_t> exact_lin((size_t)C, 0), exact_lout((size_t)C, 0);
+    std::vector<int32_t> ws((size_t)S, 0);          // window start per sensitive candidate
+    std::vector<int32_t> tab((size_t)S * 64, TB_UNKNOWN);
+    std::vector<uint8_t> have((size_t)S, 0);        // table row computed for ws
+    std::vector<int32_t> todo, todo_ws;
+    std::vector<uint8_t> need1((size_t)C, 0);
+    std::vector<int32_t> lin1((size_t)C, 0);
+    int32_t rounds = 0, exact_runs = 0;
     float kms = 0;
-    int32_t first_unconfirmed = 0;
-    int64_t cur_true = *last_index;
-    for (;;) {
-        rounds++;
-        CA_HIP_CHECK(hipMemcpyAsync(d_lin.ptr, lin.data(), sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
-        CA_HIP_CHECK(hipMemcpyAsync(d_need.ptr, need.data(), (size_t)C, hipMemcpyHostToDevice, st));
-        CA_HIP_CHECK(hipEventRecord(m->ev0, st));
-        hipLaunchKernelGGL(k_sweep, dim3(C), dim3(64), 0, st, m->d_hot.as<NodeHot>(), m->d_ext.as<NodeExt>(),
-                           m->d_static.as<NodeStatic>(), n, d_mask.as<uint8_t>(), d_c.as<int32_t>(),
-                           d_status.as<int32_t>(), d_off.as<int32_t>(), d_moves.as<int32_t>(),
-                           m->d_pods.hot.as<PodHot>(), m->d_pods.spec.as<ca_pod_spec>(),
-                           m->d_pods.terms.as<ca_selector_term>(), m->d_pods.reqs.as<ca_selector_req>(),
-                           m->d_pods.names.as<int32_t>(), d_hints.as<int32_t>(), d_lin.as<int32_t>(),
-                           d_need.as<uint8_t>(), d_dest.as<int32_t>(), d_hset.as<int32_t>(), d_out.as<SweepOut>());
-        CA_HIP_CHECK(hipGetLastError());
-        CA_HIP_CHECK(hipEventRecord(m->ev1, st));
-        CA_HIP_CHECK(hipMemcpyAsync(fresh.data(), d_out.ptr, sizeof(SweepOut) * C, hipMemcpyDeviceToHost, st));
-        CA_HIP_CHECK(hipStreamSynchronize(st));
-        float ms = 0;
-        (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
-        kms += ms;
-        for (int32_t c = 0; c < C; c++) if (need[c]) outs[c] = fresh[c];
-        // confirm the exact prefix
-        int32_t c = first_unconfirmed;
-        for (; c < C; c++) {
-            const SweepOut& o = outs[c];
-            const bool insensitive = !o.fa_success;          // no FitsAnyNode placement: L untouched
-            if (o.lin != cur_true && !insensitive) break;
-            if (o.fa_success) cur_true = o.lout;
+    const int64_t L0 = wrap(*last_index, n);
+    {   // initial guesses: every moved pod advances lastIndex by at least one position
+        int64_t g = L0;
+        for (int32_t k = 0; k < S; k++) {
+            ws[k] = wrap(g - 32, n);
+            g += move_off[sens[k] + 1] - move_off[sens[k]];
         }
-        first_unconfirmed = c;
-        if (c == C) break;
-        // new guesses: exact lastIndex for the first unconfirmed candidate, then the
-        // lastIndex advance each later candidate showed on its last run
-        std::fill(need.begin(), need.end(), 0);
-        int64_t guess = cur_true;
-        for (int32_t k = c; k < C; k++) {
-            const SweepOut& o = outs[k];
-            if (o.fa_success) {
-                if (o.lin != (int32_t)guess) { need[k] = 1; lin[k] = (int32_t)guess; }
-                int64_t adv = ((int64_t)o.lout - (int64_t)o.lin) % n;
-                if (adv < 0) adv += n;
-                guess = (guess + adv) % n;
+    }
+    SweepOut one;
+    int32_t k0 = 0;               // first sensitive candidate not yet resolved
+    int64_t cur = L0;             // exact lastIndex before sens[k0]
+    while (k0 < S) {
+        todo.clear(); todo_ws.clear();
+        for (int32_t k = k0; k < S; k++) if (!have[k]) { todo.push_back(sens[k]); todo_ws.push_back(ws[k]); }
+        if (!todo.empty()) {
+            rounds++;
+            const int32_t T = (int32_t)todo.size();
+            CA_HIP_CHECK(hipMemcpyAsync(d_todo.ptr, todo.data(), sizeof(int32_t) * T, hipMemcpyHostToDevice, st));
+            CA_HIP_CHECK(hipMemcpyAsync(d_ws.ptr, todo_ws.data(), sizeof(int32_t) * T, hipMemcpyHostToDevice, st));
+            CA_HIP_CHECK(hipEventRecord(m->ev0, st));
+            hipLaunchKernelGGL(k_sweep_table, dim3(T), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
+                               m->d_static.as<NodeStatic>(), n, d_mask.as<uint8_t>(), d_c.as<int32_t>(),
+                               d_off.as<int32_t>(), d_moves.as<int32_t>(), m->d_pods.hot.as<PodHot>(),
+                               m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
+                               m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
+                               d_hints.as<int32_t>(), d_todo.as<int32_t>(), d_ws.as<int32_t>(), d_tab.as<int32_t>());
+            CA_HIP_CHECK(hipGetLastError());
+            CA_HIP_CHECK(hipEventRecord(m->ev1, st));
+            std::vector<int32_t> rows((size_t)T * 64);
+            CA_HIP_CHECK(hipMemcpyAsync(rows.data(), d_tab.ptr, sizeof(int32_t) * 64 * T, hipMemcpyDeviceToHost, st));
+            CA_HIP_CHECK(hipStreamSynchronize(st));
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
+            kms += ms;
+            int32_t ti = 0;
+            for (int32_t k = k0; k < S; k++) {
+                if (have[k]) continue;
+                std::copy(rows.begin() + (size_t)ti * 64, rows.begin() + (size_t)ti * 64 + 64, tab.begin() + (size_t)k * 64);
+                have[k] = 1;
+                ti++;
             }
         }
-        need[c] = 1;
-        lin[c] = (int32_t)cur_true;
-        if (rounds > C + 2) { set_last_error("sweep speculation did not converge"); return CA_EDEVICE; }
+        // walk the exact chain as far as the windows reach
+        for (; k0 < S; k0++) {
+            const int32_t c = sens[k0];
+            const int32_t w = wrap(cur - ws[k0], n);
+            if (w >= 64) break;
+            int32_t v = tab[(size_t)k0 * 64 + w];
+            if (v == TB_UNKNOWN) {
+                // hints / ports / long scans: exact kernel at the exact lastIndex
+                need1[c] = 1;
+                lin1[c] = (int32_t)cur;
+                CA_HIP_CHECK(hipMemcpyAsync(d_lin.ptr, lin1.data(), sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
+                CA_HIP_CHECK(hipMemcpyAsync(d_need.ptr, need1.data(), (size_t)C, hipMemcpyHostToDevice, st));
+                if ((rc = launch_exact(m, st, C, n, d_mask, d_c, d_status, d_off, d_moves, d_hints, d_lin, d_need,
+                                       d_dest, d_hset, d_out)) != CA_OK)
+                    return rc;
+                CA_HIP_CHECK(hipMemcpyAsync(&one, d_out.as<SweepOut>() + c, sizeof(SweepOut), hipMemcpyDeviceToHost, st));
+                CA_HIP_CHECK(hipStreamSynchronize(st));
+                need1[c] = 0;
+                exact_runs++;
+                v = one.fa_success ? one.lout : (int32_t)cur;
+            }
+            exact_lin[c] = (int32_t)cur;
+            exact_lout[c] = v;
+            cur = v;
+        }
+        if (k0 >= S) break;
+        // re-centre the windows from k0 on: follow the tables where the estimate falls
+        // inside a window, otherwise shift the nearest known entry
+        int64_t est = cur;
+        for (int32_t k = k0; k < S; k++) {
+            const int32_t w = wrap(est - ws[k], n);
+            const int32_t v = w < 64 ? tab[(size_t)k * 64 + w] : TB_UNKNOWN;
+            if (w < 64 && v != TB_UNKNOWN) { est = v; continue; }
+            int64_t next = est + (move_off[sens[k] + 1] - move_off[sens[k]]);
+            int best = -1;
+            for (int q = 0; q < 64; q++) {
+                if (tab[(size_t)k * 64 + q] == TB_UNKNOWN) continue;
+                if (best < 0 || std::abs(q - 32) < std::abs(best - 32)) best = q;
+            }
+            if (best >= 0) {
+                const int64_t from = (int64_t)ws[k] + best;
+                next = est + wrap(tab[(size_t)k * 64 + best] - from, n);
+            }
+            if (w >= 64) { ws[k] = wrap(est - 32, n); have[k] = 0; }
+            est = wrap(next, n);
+        }
+        if (rounds > S + 4) { set_last_error("sweep speculation did not converge"); return CA_EDEVICE; }
     }
-    *last_index = (int32_t)cur_true;
+    {   // candidates that cannot move lastIndex see the running value
+        int64_t run = L0;
+        int32_t k = 0;
+        for (int32_t c = 0; c < C; c++) {
+            if (k < S && sens[k] == c) {
+                run = exact_lout[c];
+                k++;
+                continue;
+            }
+            exact_lin[c] = (int32_t)run;
+        }
+    }
+    // ---- 2. exact pass at the exact lastIndex: every output ----
+    std::vector<uint8_t> need((size_t)C, 1);
+    CA_HIP_CHECK(hipMemcpyAsync(d_lin.ptr, exact_lin.data(), sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
+    CA_HIP_CHECK(hipMemcpyAsync(d_need.ptr, need.data(), (size_t)C, hipMemcpyHostToDevice, st));
+    CA_HIP_CHECK(hipEventRecord(m->ev0, st));
+    if ((rc = launch_exact(m, st, C, n, d_mask, d_c, d_status, d_off, d_moves, d_hints, d_lin, d_need, d_dest, d_hset,
+                           d_out)) != CA_OK)
+        return rc;
+    CA_HIP_CHECK(hipEventRecord(m->ev1, st));
+    std::vector<SweepOut> outs((size_t)C);
     std::vector<int32_t> hset((size_t)std::max(M, 1));
+    CA_HIP_CHECK(hipMemcpyAsync(outs.data(), d_out.ptr, sizeof(SweepOut) * C, hipMemcpyDeviceToHost, st));
     if (M) {
         CA_HIP_CHECK(hipMemcpyAsync(out_dest, d_dest.ptr, sizeof(int32_t) * M, hipMemcpyDeviceToHost, st));
         CA_HIP_CHECK(hipMemcpyAsync(hset.data(), d_hset.ptr, sizeof(int32_t) * M, hipMemcpyDeviceToHost, st));
     }
     CA_HIP_CHECK(hipStreamSynchronize(st));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
+    kms += ms;
+    // the exact pass must reproduce the chain it was given
+    int64_t Lrun = L0;
     for (int32_t c = 0; c < C; c++) {
         const SweepOut& o = outs[c];
         if (o.status != CA_OK) { set_last_error("overlay capacity exceeded"); return o.status; }
+        if (o.lin != exact_lin[c] || exact_lin[c] != Lrun) {
+            if (getenv("CASIM_DEBUG")) {
+                fprintf(stderr, "chain mismatch at candidate %d: o.lin=%d exact_lin=%d Lrun=%ld\n", c, o.lin,
+                        exact_lin[c], (long)Lrun);
+                for (int32_t q = std::max(0, c - 3); q <= c && q < C; q++) {
+                    int32_t k = (int32_t)(std::find(sens.begin(), sens.end(), q) - sens.begin());
+                    fprintf(stderr, "  cand %d sens=%d lin=%d lout=%d fa=%d placed=%d mn=%d", q, k < S, outs[q].lin,
+                            outs[q].lout, outs[q].fa_success, outs[q].n_placed, move_off[q + 1] - move_off[q]);
+                    if (k < S) {
+                        const int32_t w = wrap(exact_lin[q] - ws[k], n);
+                        fprintf(stderr, " ws=%d w=%d tab=%d", ws[k], w, w < 64 ? tab[(size_t)k * 64 + w] : -9);
+                    }
+                    fprintf(stderr, "\n");
+                }
+            }
+            set_last_error("sweep lastIndex chain mismatch");
+            return CA_EDEVICE;
+        }
         ca_removal_result& r = results[c];
         r.removable = o.removable;
         r.reason = o.reason;
         r.n_placed = o.n_placed;
-        r.last_index_in = o.lin;
+        r.last_index_in = (int32_t)Lrun;
         r.evals = o.evals;
+        if (o.fa_success) Lrun = o.lout;
     }
+    *last_index = (int32_t)Lrun;
     if (hints) {
         for (int32_t i = 0; i < M; i++) if (hset[i] >= 0) hints[move_pods[i]] = hset[i];
     }
-    m->sweep_stats.rounds = rounds;
+    m->sweep_stats.rounds = rounds + exact_runs + 1;
     m->sweep_stats.kernel_ms = kms;
     m->sweep_stats.total_ms =
         std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_start).count();

@@ -1,0 +1,490 @@
+"""Host-side interning: API objects -> ``casim.h`` records (the cgo shim's job).
+
+Taints, label pairs/keys, Gt/Lt keys, host-port triples, scalar resources and
+node names are mapped to small integer ids so the kernels evaluate the filter
+chain with bit operations.  The universes are built from
+every object the simulation will see, so one encoding serves the whole call:
+
+  taint classes   NoSchedule/NoExecute (key,value,effect) on nodes/templates
+                  (helpers.go:78-101 filters on these effects)
+  label pairs     (key,value) referenced by nodeSelector / In / NotIn
+  label keys      keys referenced by Exists / DoesNotExist
+  int keys        keys referenced by Gt / Lt (node value parsed like strconv.ParseInt)
+  port triples    (hostIP,protocol,hostPort) of pod ports, sanitised like
+                  HostPortInfo.sanitize (SF/types.go:923-931)
+  scalar names    IsScalarResourceName (scheduler/util/utils.go:158-161)
+"""
+from __future__ import annotations
+
+import re
+from fractions import Fraction
+from typing import Iterable, Optional
+
+import numpy as np
+
+from . import abi
+from .k8s import Node, Pod, Quantity, Taint, Toleration
+
+TPU_PREFIX = "cloud-tpus.google.com/"           # CA/utils/tpu/tpu.go:27
+HOSTNAME_KEY = "kubernetes.io/hostname"
+UNSCHED_TAINT = Taint("node.kubernetes.io/unschedulable", "", "NoSchedule")
+NATIVE = {"cpu", "memory", "pods", "ephemeral-storage"}
+
+_NAME_RE = re.compile(r"^([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9]$")
+_DNS1123 = re.compile(r"^[a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*$")
+_INT64 = re.compile(r"^[+-]?[0-9]+$")
+
+
+class InternCapacityError(RuntimeError):
+    """An intern universe exceeded the fixed ABI width (CA_ECAPACITY)."""
+
+
+def is_qualified_name(s: str) -> bool:
+    """validation.IsQualifiedName (apimachinery/pkg/util/validation)."""
+    parts = s.split("/")
+    if len(parts) == 1:
+        name = parts[0]
+    elif len(parts) == 2:
+        prefix, name = parts
+        if not prefix or len(prefix) > 253 or not _DNS1123.match(prefix):
+            return False
+    else:
+        return False
+    return 0 < len(name) <= 63 and bool(_NAME_RE.match(name))
+
+
+def is_valid_label_value(v: str) -> bool:
+    return v == "" or (len(v) <= 63 and bool(_NAME_RE.match(v)))
+
+
+def parse_int64(s: str) -> Optional[int]:
+    """strconv.ParseInt(s, 10, 64): optional sign, decimal digits, range-checked."""
+    if not _INT64.match(s):
+        return None
+    v = int(s)
+    if v < -(1 << 63) or v > (1 << 63) - 1:
+        return None
+    return v
+
+
+def is_scalar_resource(name: str) -> bool:
+    """IsScalarResourceName: extended | hugepages- | prefixed native | attachable-volumes-."""
+    if name in NATIVE:
+        return False
+    if name.startswith("hugepages-") or name.startswith("attachable-volumes-"):
+        return True
+    if "kubernetes.io/" in name:                    # IsPrefixedNativeResource
+        return True
+    if "/" not in name or name.startswith("requests."):
+        return False
+    return is_qualified_name("requests." + name)    # IsExtendedResourceName
+
+
+def tolerates(t: Toleration, taint: Taint) -> bool:
+    """Toleration.ToleratesTaint (core/v1/toleration.go:38-57)."""
+    if t.effect and t.effect != taint.effect:
+        return False
+    if t.key and t.key != taint.key:
+        return False
+    if t.operator in ("", "Equal"):
+        return t.value == taint.value
+    if t.operator == "Exists":
+        return True
+    return False
+
+
+def _q(v) -> Quantity:
+    return v if isinstance(v, Quantity) else Quantity(v)
+
+
+class PodRequest:
+    """computePodResourceRequest / calculateResource (fit.go:160-176, SF/types.go:726-757)."""
+
+    def __init__(self, pod: Pod, drop_tpu: bool = False):
+        self.cpu = 0
+        self.mem = 0
+        self.eph = 0
+        self.scalar: dict[str, int] = {}
+
+        def add(rl: dict, skip_tpu: bool):
+            for name, q in rl.items():
+                q = _q(q)
+                if skip_tpu and name.startswith(TPU_PREFIX):
+                    continue
+                if name == "cpu":
+                    self.cpu += q.milli_value()
+                elif name == "memory":
+                    self.mem += q.value()
+                elif name == "ephemeral-storage":
+                    self.eph += q.value()
+                elif name != "pods" and is_scalar_resource(name):
+                    self.scalar[name] = self.scalar.get(name, 0) + q.value()
+
+        for c in pod.containers:
+            add(c.requests, drop_tpu)
+        for c in pod.init_containers:          # SetMaxResource
+            for name, q in c.requests.items():
+                q = _q(q)
+                if name == "cpu":
+                    self.cpu = max(self.cpu, q.milli_value())
+                elif name == "memory":
+                    self.mem = max(self.mem, q.value())
+                elif name == "ephemeral-storage":
+                    self.eph = max(self.eph, q.value())
+                elif name != "pods" and is_scalar_resource(name):
+                    self.scalar[name] = max(self.scalar.get(name, 0), q.value())
+        if pod.overhead is not None:
+            add(pod.overhead, False)
+
+
+def score_sums(pod: Pod) -> tuple[int, int]:
+    """calculatePodScore sums (binpacking_estimator.go:168-178): Quantity sums, then MilliValue/Value."""
+    c = Fraction(0)
+    m = Fraction(0)
+    for ct in pod.containers:
+        if "cpu" in ct.requests:
+            c += _q(ct.requests["cpu"]).v
+        if "memory" in ct.requests:
+            m += _q(ct.requests["memory"]).v
+    return Quantity(c).milli_value(), Quantity(m).value()
+
+
+def _sanitize_port(ip: str, proto: str) -> tuple[str, str]:
+    return (ip or "0.0.0.0", proto or "TCP")
+
+
+def pod_ports(pod: Pod) -> list[tuple[str, str, int]]:
+    out = []
+    for c in pod.containers:
+        for p in c.ports:
+            if p.host_port > 0:                  # HostPortInfo.Add ignores port <= 0
+                ip, proto = _sanitize_port(p.host_ip, p.protocol)
+                out.append((ip, proto, p.host_port))
+    return out
+
+
+class _Universe:
+    def __init__(self, cap: int, what: str):
+        self.ids: dict = {}
+        self.cap = cap
+        self.what = what
+
+    def get(self, key, create: bool = True) -> Optional[int]:
+        i = self.ids.get(key)
+        if i is None and create:
+            if len(self.ids) >= self.cap:
+                raise InternCapacityError(f"{self.what}: more than {self.cap} interned values")
+            i = self.ids[key] = len(self.ids)
+        return i
+
+    def __len__(self) -> int:
+        return len(self.ids)
+
+
+def _bits(ids: Iterable[int], words: int) -> np.ndarray:
+    out = np.zeros(words, np.uint64)
+    for i in ids:
+        out[i >> 6] |= np.uint64(1) << np.uint64(i & 63)
+    return out
+
+
+class Interner:
+    """Builds the intern universes from every node, template and pod of a simulation."""
+
+    def __init__(self, nodes: Iterable[Node] = (), pods: Iterable[Pod] = (), templates: Iterable = ()):
+        self.taints = _Universe(64, "taint classes")
+        self.pairs = _Universe(abi.CA_LABEL_WORDS * 64, "label pairs")
+        self.keys = _Universe(64, "label keys")
+        self.int_keys = _Universe(abi.CA_MAX_INT_KEYS, "Gt/Lt label keys")
+        self.ports = _Universe(abi.CA_PORT_WORDS * 64, "host port triples")
+        self.scalars = _Universe(abi.CA_MAX_SCALAR, "scalar resources")
+        self.names: dict[str, int] = {}
+        self.classes: dict = {}
+        self.observe(nodes, pods, templates)
+
+    # -- universes -----------------------------------------------------------
+    def observe(self, nodes: Iterable[Node] = (), pods: Iterable[Pod] = (), templates: Iterable = ()) -> None:
+        for n in list(nodes) + [t[0] if isinstance(t, tuple) else t for t in templates]:
+            self.name_id(n.name)
+            for t in n.taints:
+                if t.effect in ("NoSchedule", "NoExecute"):
+                    self.taints.get((t.key, t.value, t.effect))
+            for r in n.allocatable:
+                if is_scalar_resource(r):
+                    self.scalars.get(r)
+        tpods = []
+        for t in templates:
+            if isinstance(t, tuple):
+                tpods.extend(t[1])
+        for p in list(pods) + tpods:
+            for c in p.containers + p.init_containers:
+                for r in c.requests:
+                    if is_scalar_resource(r):
+                        self.scalars.get(r)
+            for r in (p.overhead or {}):
+                if is_scalar_resource(r):
+                    self.scalars.get(r)
+            for k, v in (p.node_selector or {}).items():
+                self.pairs.get((k, v))
+            if p.affinity is not None and p.affinity.required_terms:
+                for term in p.affinity.required_terms:
+                    for r in term.match_expressions:
+                        if r.operator in ("In", "NotIn"):
+                            for v in r.values:
+                                self.pairs.get((r.key, v))
+                        elif r.operator in ("Exists", "DoesNotExist"):
+                            self.keys.get(r.key)
+                        elif r.operator in ("Gt", "Lt"):
+                            self.int_keys.get(r.key)
+            for trip in pod_ports(p):
+                self.ports.get(trip)
+            if p.node_name:
+                self.name_id(p.node_name)
+
+    def name_id(self, name: str) -> int:
+        i = self.names.get(name)
+        if i is None:
+            i = self.names[name] = len(self.names)
+        return i
+
+    # -- nodes ----------------------------------------------------------------
+    def encode_node(self, n: Node, out: Optional[np.ndarray] = None, name_id: Optional[int] = None) -> np.ndarray:
+        rec = out if out is not None else abi.empty_nodes(1)[0]
+        a = n.allocatable
+        rec["alloc_milli_cpu"] = _q(a["cpu"]).milli_value() if "cpu" in a else 0
+        rec["alloc_memory"] = _q(a["memory"]).value() if "memory" in a else 0
+        rec["alloc_ephemeral"] = _q(a["ephemeral-storage"]).value() if "ephemeral-storage" in a else 0
+        rec["alloc_pods"] = _q(a["pods"]).value() if "pods" in a else 0
+        sc = np.zeros(abi.CA_MAX_SCALAR, np.int64)
+        for r, q in a.items():
+            if is_scalar_resource(r):
+                sc[self.scalars.get(r)] += _q(q).value()
+        rec["alloc_scalar"] = sc
+        taint_ids = [self.taints.get((t.key, t.value, t.effect)) for t in n.taints
+                     if t.effect in ("NoSchedule", "NoExecute")]
+        rec["taints"] = int(_bits(taint_ids, 1)[0])
+        pair_ids = [i for i in (self.pairs.get((k, v), create=False) for k, v in n.labels.items()) if i is not None]
+        rec["label_pairs"] = _bits(pair_ids, abi.CA_LABEL_WORDS)
+        key_ids = [i for i in (self.keys.get(k, create=False) for k in n.labels) if i is not None]
+        rec["label_keys"] = int(_bits(key_ids, 1)[0])
+        ints = np.zeros(abi.CA_MAX_INT_KEYS, np.int64)
+        valid = 0
+        for k, i in self.int_keys.ids.items():
+            if k in n.labels:
+                v = parse_int64(n.labels[k])
+                if v is not None:
+                    ints[i] = v
+                    valid |= 1 << i
+        rec["int_label"] = ints
+        rec["int_label_valid"] = valid
+        rec["flags"] = abi.CA_NODE_UNSCHEDULABLE if n.unschedulable else 0
+        rec["name_id"] = self.name_id(n.name) if name_id is None else name_id
+        return rec
+
+    def encode_nodes(self, nodes: list[Node]) -> np.ndarray:
+        out = abi.empty_nodes(len(nodes))
+        for i, n in enumerate(nodes):
+            self.encode_node(n, out[i])
+        return out
+
+    def encode_template(self, node: Node, pods: list[Pod]) -> np.ndarray:
+        """ca_template of a node group (template NodeInfo + its pods, scheduler.go:73-91)."""
+        t = np.zeros(1, abi.TEMPLATE_DTYPE)[0]
+        self.encode_node(node, t["node"], name_id=-1000 - self.name_id(node.name))
+        sc = np.zeros(abi.CA_MAX_SCALAR, np.int64)
+        cpu = mem = eph = 0
+        ports = []
+        for p in pods:
+            r = PodRequest(p)
+            cpu += r.cpu
+            mem += r.mem
+            eph += r.eph
+            for name, v in r.scalar.items():
+                sc[self.scalars.get(name)] += v
+            ports += [self.ports.get(x) for x in pod_ports(p)]
+        t["used_milli_cpu"] = cpu
+        t["used_memory"] = mem
+        t["used_ephemeral"] = eph
+        t["used_scalar"] = sc
+        t["used_pods"] = len(pods)
+        t["used_ports"] = _bits(ports, abi.CA_PORT_WORDS)
+        return t
+
+    # -- pods -----------------------------------------------------------------
+    def similar_class(self, pod: Pod) -> int:
+        """SimilarPodsScheduling key: controller UID + labels + spec equality (similar_pods.go:30-111)."""
+        ref = pod.controller_ref()
+        if ref is None:
+            return -1
+        key = (ref.uid, repr(sorted(pod.labels.items())), repr((pod.containers, pod.init_containers, pod.overhead,
+                                                                 pod.node_selector, pod.affinity, pod.tolerations,
+                                                                 pod.volumes, pod.topology_spread)))
+        return self.classes.setdefault(key, len(self.classes))
+
+    def encode_pods(self, pods: list[Pod]) -> abi.PodTable:
+        recs = abi.empty_pods(len(pods))
+        terms: list = []
+        reqs: list = []
+        names: list = []
+        for i, p in enumerate(pods):
+            self._encode_pod(p, recs[i], terms, reqs, names)
+        t = np.zeros(len(terms), abi.TERM_DTYPE)
+        for i, (f, c) in enumerate(terms):
+            t[i] = (f, c)
+        r = np.zeros(len(reqs), abi.REQ_DTYPE)
+        for i, (op, key, bound, pairs) in enumerate(reqs):
+            r[i]["op"] = op
+            r[i]["key"] = key
+            r[i]["bound"] = bound
+            r[i]["pairs"] = pairs
+        return abi.PodTable(recs, t, r, np.array(names, np.int32))
+
+    def _encode_pod(self, p: Pod, rec, terms: list, reqs: list, names: list) -> None:
+        flags = 0
+        r = PodRequest(p)
+        rec["req_milli_cpu"] = r.cpu
+        rec["req_memory"] = r.mem
+        rec["req_ephemeral"] = r.eph
+        sc = np.zeros(abi.CA_MAX_SCALAR, np.int64)
+        tpu_mask = 0
+        for name, v in r.scalar.items():
+            i = self.scalars.get(name)
+            sc[i] = v
+            if name.startswith(TPU_PREFIX):
+                tpu_mask |= 1 << i
+        rec["req_scalar"] = sc
+        if r.scalar:
+            flags |= abi.CA_POD_HAS_SCALAR_KEYS
+        if PodRequest(p, drop_tpu=True).scalar:
+            flags |= abi.CA_POD_HAS_NONTPU_SCALAR_KEYS
+        rec["tpu_scalar_mask"] = tpu_mask
+        sc_cpu, sc_mem = score_sums(p)
+        rec["score_milli_cpu"] = sc_cpu
+        rec["score_memory"] = sc_mem
+        # tolerations
+        tol = 0
+        for (k, v, e), i in self.taints.ids.items():
+            taint = Taint(k, v, e)
+            if any(tolerates(t, taint) for t in p.tolerations):
+                tol |= 1 << i
+        rec["tolerated_taints"] = tol
+        if any(tolerates(t, UNSCHED_TAINT) for t in p.tolerations):
+            flags |= abi.CA_POD_TOLERATES_UNSCHED
+        # ports
+        conflict, use = [], []
+        for (ip, proto, port) in pod_ports(p):
+            use.append(self.ports.get((ip, proto, port)))
+            for (ip2, proto2, port2), j in self.ports.ids.items():
+                if proto2 != proto or port2 != port:
+                    continue
+                if ip == "0.0.0.0" or ip2 == "0.0.0.0" or ip2 == ip:   # HostPortInfo.CheckConflict
+                    conflict.append(j)
+        rec["port_conflict"] = _bits(conflict, abi.CA_PORT_WORDS)
+        rec["port_use"] = _bits(use, abi.CA_PORT_WORDS)
+        # node name
+        rec["node_name_id"] = self.name_id(p.node_name) if p.node_name else -1
+        hostname_dep = bool(p.node_name)
+        # NodeAffinity PreFilter / Filter (node_affinity.go:91-170)
+        required = p.affinity.required_terms if p.affinity is not None else None
+        if p.node_selector is not None or required is not None:
+            flags |= abi.CA_POD_AFFINITY_FILTER
+        sel = []
+        for k, v in (p.node_selector or {}).items():
+            sel.append(self.pairs.get((k, v)))
+            if k == HOSTNAME_KEY:
+                hostname_dep = True
+        rec["node_selector"] = _bits(sel, abi.CA_LABEL_WORDS)
+        if required is None:
+            rec["aff_term_first"] = 0
+            rec["aff_term_count"] = -1
+        else:
+            first = len(terms)
+            for term in required:
+                if not term.match_expressions and not term.match_fields:
+                    continue                                   # empty term matches nothing (nodeaffinity.go:83-85)
+                rfirst = len(reqs)
+                self._compile_term(term, reqs)
+                terms.append((rfirst, len(reqs) - rfirst))
+                if term.match_fields or any(r.key == HOSTNAME_KEY for r in term.match_expressions):
+                    hostname_dep = True
+            rec["aff_term_first"] = first
+            rec["aff_term_count"] = len(terms) - first
+            pf = self._prefilter_names(required)
+            if pf == "fail":
+                flags |= abi.CA_POD_PREFILTER_FAIL
+            elif pf is not None:
+                flags |= abi.CA_POD_PREFILTER_NAMES
+                rec["prefilter_first"] = len(names)
+                rec["prefilter_count"] = len(pf)
+                names.extend(pf)
+        if hostname_dep:
+            flags |= abi.CA_POD_HOSTNAME_DEPENDENT
+        ref = p.controller_ref()
+        if ref is not None and ref.kind == "DaemonSet":
+            flags |= abi.CA_POD_DAEMONSET
+        rec["flags"] = flags
+        rec["similar_class"] = self.similar_class(p)
+
+    def _compile_term(self, term, reqs: list) -> None:
+        """nodeSelectorTerm -> requirement rows; a parse error makes the term never match."""
+        zero = np.zeros(abi.CA_LABEL_WORDS, np.uint64)
+        rows = []
+        bad = False
+        for r in term.match_expressions:            # nodeSelectorRequirementsAsSelector (:223-260)
+            if not is_qualified_name(r.key) or any(not is_valid_label_value(v) for v in r.values):
+                bad = True
+                continue
+            if r.operator in ("In", "NotIn"):
+                if not r.values:
+                    bad = True
+                    continue
+                bits = _bits([self.pairs.get((r.key, v)) for v in r.values], abi.CA_LABEL_WORDS)
+                rows.append((abi.CA_OP_IN if r.operator == "In" else abi.CA_OP_NOTIN, 0, 0, bits))
+            elif r.operator in ("Exists", "DoesNotExist"):
+                if r.values:
+                    bad = True
+                    continue
+                rows.append((abi.CA_OP_EXISTS if r.operator == "Exists" else abi.CA_OP_DOESNOTEXIST,
+                             self.keys.get(r.key), 0, zero))
+            elif r.operator in ("Gt", "Lt"):
+                v = parse_int64(r.values[0]) if len(r.values) == 1 else None
+                if v is None:
+                    bad = True
+                    continue
+                rows.append((abi.CA_OP_GT if r.operator == "Gt" else abi.CA_OP_LT, self.int_keys.get(r.key), v, zero))
+            else:
+                bad = True
+        for r in term.match_fields:                 # nodeSelectorRequirementsAsFieldSelector (:263-293)
+            if r.operator not in ("In", "NotIn") or len(r.values) != 1:
+                bad = True
+                continue
+            v = r.values[0]
+            if r.key == "metadata.name":
+                nid = self.name_id(v)
+                rows.append((abi.CA_OP_FIELD_EQ if r.operator == "In" else abi.CA_OP_FIELD_NE, nid, 0, zero))
+            else:
+                # fields.Set.Get(missing) == "": In [v] matches iff v == "", NotIn iff v != ""
+                ok = (v == "") if r.operator == "In" else (v != "")
+                if not ok:
+                    bad = True
+        if bad:
+            rows = [(abi.CA_OP_FALSE, 0, 0, zero)]
+        reqs.extend(rows)
+
+    def _prefilter_names(self, required: list):
+        """NodeAffinity.PreFilter NodeNames (node_affinity.go:106-135): None == all nodes."""
+        if not required:
+            return None
+        union = None
+        for term in required:
+            tn = None
+            for r in term.match_fields:
+                if r.key == "metadata.name" and r.operator == "In":
+                    s = set(r.values)
+                    tn = s if tn is None else tn & s
+            if tn is None:
+                return None
+            if not tn:
+                return "fail"
+            union = tn if union is None else union | tn
+        return sorted(self.name_id(n) for n in union)

@@ -29,6 +29,9 @@ def cmp_est(name, w):
         st = plan.stats()
     ok = (np.array_equal(ro.results, rg.results) and np.array_equal(ro.sched_pod, rg.sched_pod)
           and np.array_equal(ro.sched_node, rg.sched_node) and ro.last_index == rg.last_index)
+    if not ok:
+        print(" results eq", np.array_equal(ro.results, rg.results), "sp eq", np.array_equal(ro.sched_pod, rg.sched_pod),
+              "sn eq", np.array_equal(ro.sched_node, rg.sched_node), "L", ro.last_index, rg.last_index)
     ev = int(ro.results["evals"].sum())
     print(f"{name}: parity={ok} oracle={to*1e3:.1f}ms gpu={tg*1e3:.2f}ms stats={st} evals={ev} "
           f"L={ro.last_index}/{rg.last_index}", flush=True)
@@ -36,6 +39,23 @@ def cmp_est(name, w):
         bad = np.nonzero(ro.results != rg.results)[0][:5]
         print(" oracle", ro.results[bad])
         print(" gpu   ", rg.results[bad])
+        pods = w.table.pods
+        for g in range(len(w.templates)):
+            a, b = w.group_off[g], w.group_off[g + 1]
+            n = ro.results[g]["n_scheduled"]
+            so, sg = ro.sched_pod[a:a + n], rg.sched_pod[a:a + n]
+            no, ng = ro.sched_node[a:a + n], rg.sched_node[a:a + n]
+            if np.array_equal(so, sg) and np.array_equal(no, ng):
+                continue
+            d = int(np.nonzero((so != sg) | (no != ng))[0][0])
+            t = w.templates[g]["node"]
+            def score(pi):
+                p = pods[pi]
+                return p["score_milli_cpu"] / t["alloc_milli_cpu"] + p["score_memory"] / t["alloc_memory"]
+            print(f" group {g} first diff at {d}/{n}: oracle pod {so[d]} node {no[d]} score {score(so[d])!r} | "
+                  f"gpu pod {sg[d]} node {ng[d]} score {score(sg[d])!r}; prev oracle {so[max(d-3,0):d+3]} "
+                  f"gpu {sg[max(d-3,0):d+3]} nodes o {no[max(d-3,0):d+3]} g {ng[max(d-3,0):d+3]}")
+            break
     return ok
 
 

@@ -63,9 +63,9 @@ CA_REASON_INSUFF_SCALAR0 = 0x100
 CA_MATCH_ALL, CA_MATCH_RANGE, CA_MATCH_MASK = 0, 1, 2
 
 CA_UNREMOVABLE_NONE = 0
-CA_UNREMOVABLE_NO_PLACE = 13
-CA_UNREMOVABLE_BLOCKED_BY_POD = 14
-CA_UNREMOVABLE_UNEXPECTED_ERROR = 15
+CA_UNREMOVABLE_NO_PLACE = 12
+CA_UNREMOVABLE_BLOCKED_BY_POD = 13
+CA_UNREMOVABLE_UNEXPECTED_ERROR = 14
 
 # --------------------------------------------------------------------------
 # record dtypes (C layout: align=True)

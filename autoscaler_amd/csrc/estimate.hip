@@ -688,6 +688,16 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     }
     float sort_ms = 0;
     (void)hipEventElapsedTime(&sort_ms, m->ev0, m->ev1);
+    // batch-level lastIndex dependence: the first group with a FitsAnyNode success decides
+    p->stats.lin_sensitive = 0;
+    p->stats.had_success = 0;
+    for (int32_t g = 0; g < G; g++) {
+        const ChainOut& o = outs[g];
+        if (o.status != CA_OK || !o.had_success) continue;
+        p->stats.lin_sensitive = o.sensitive;
+        p->stats.had_success = 1;
+        break;
+    }
     p->stats.rounds = rounds;
     p->stats.kernel_ms = chain_ms;
     p->stats.sort_ms = sort_ms;
@@ -728,6 +738,13 @@ int ca_estimate_plan_stats(const ca_estimate_plan* p, int32_t* rounds, float* ch
     if (chain_ms) *chain_ms = p->stats.kernel_ms;
     if (sort_ms) *sort_ms = p->stats.sort_ms;
     if (total_ms) *total_ms = p->stats.total_ms;
+    return CA_OK;
+}
+
+int ca_estimate_plan_chain_info(const ca_estimate_plan* p, int32_t* lin_sensitive, int32_t* had_success) {
+    if (!p) return CA_EINVAL;
+    if (lin_sensitive) *lin_sensitive = p->stats.lin_sensitive;
+    if (had_success) *had_success = p->stats.had_success;
     return CA_OK;
 }
 

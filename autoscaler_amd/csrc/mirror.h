@@ -43,6 +43,8 @@ struct DevPodTable {
 struct Stats {
     int32_t rounds = 0;
     float kernel_ms = 0, sort_ms = 0, total_ms = 0;
+    int32_t lin_sensitive = 0;    // batch output depends on the input lastIndex
+    int32_t had_success = 0;      // some FitsAnyNode call of the batch succeeded
 };
 
 }  // namespace casim

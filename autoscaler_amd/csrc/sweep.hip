@@ -511,7 +511,7 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     std::vector<int32_t> lin1((size_t)C, 0);
     int32_t rounds = 0, exact_runs = 0;
     float kms = 0;
-    const int64_t L0 = wrap(*last_index, n);
+    const int64_t L0 = *last_index;               // raw until the first placement (Go keeps the int)
     {   // initial guesses: every moved pod advances lastIndex by at least one position
         int64_t g = L0;
         for (int32_t k = 0; k < S; k++) {

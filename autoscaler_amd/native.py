@@ -68,6 +68,7 @@ def load() -> C.CDLL:
         "ca_estimate_plan_run": ([vp, vp, p(i32), vp, vp, vp], C.c_int),
         "ca_estimate_plan_destroy": ([vp], C.c_int),
         "ca_estimate_plan_stats": ([vp, p(i32), p(C.c_float), p(C.c_float), p(C.c_float)], C.c_int),
+        "ca_estimate_plan_chain_info": ([vp, p(i32), p(i32)], C.c_int),
         "ca_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, p(i32), vp, vp], C.c_int),
         "ca_removal_stats": ([vp, p(i32), p(C.c_float), p(C.c_float)], C.c_int),
     }
@@ -91,7 +92,8 @@ def exported_symbols() -> list[str]:
         "ca_mirror_fork", "ca_mirror_revert", "ca_mirror_commit", "ca_mirror_node_count", "ca_mirror_pod_node",
         "ca_mirror_node_pods", "ca_podset_create", "ca_podset_destroy", "ca_fits_any_node", "ca_check_predicates",
         "ca_fits_matrix", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
-        "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_find_nodes_to_remove", "ca_removal_stats",
+        "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_find_nodes_to_remove",
+        "ca_removal_stats",
     ]
 
 
@@ -285,7 +287,10 @@ class EstimatePlan:
     def stats(self) -> dict:
         r, a, b, c = C.c_int32(0), C.c_float(0), C.c_float(0), C.c_float(0)
         self.lib.ca_estimate_plan_stats(self.h, C.byref(r), C.byref(a), C.byref(b), C.byref(c))
-        return {"rounds": r.value, "chain_ms": a.value, "sort_ms": b.value, "total_ms": c.value}
+        sens, succ = C.c_int32(0), C.c_int32(0)
+        self.lib.ca_estimate_plan_chain_info(self.h, C.byref(sens), C.byref(succ))
+        return {"rounds": r.value, "chain_ms": a.value, "sort_ms": b.value, "total_ms": c.value,
+                "lin_sensitive": sens.value, "had_success": succ.value}
 
     def close(self) -> None:
         if self.h:

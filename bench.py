@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json's metric on its C2 configuration.
+
+One step = one Estimate batch: BinpackingNodeEstimator.Estimate for every node
+group of a scale-up (CA/core/scaleup/orchestrator/orchestrator.go:139-178), i.e. the
+C2 workload of SURVEY.md §8d: 50k heterogeneous pending pods x 100 node-group
+templates, resource-fit only, maxNodes = 1000 (the --max-nodes-per-scaleup
+default), 1000 existing nodes, inputs resident in HBM.  The step runs the device
+sort, the per-group First-Fit-Decreasing chains and the lastIndex fix-up, and
+copies every group's result (count, scheduled pods, node assignment) to the host.
+
+value = filter-chain evaluations the reference algorithm performs in that batch
+(every RunFilterPlugins call, counted exactly) / wall time.  With --gpus N each
+rank runs its own batch of 100 groups (weak scaling: N x 100 groups); the ranks'
+batches are chained through the checker's lastIndex with one RCCL all_gather of a
+4-int record per rank per step.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "pod×node predicate evals/sec; Estimate() latency, 50k pods × 100 node groups"
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E (MI355X_MICROARCH.md, chip table)
+BYTES_PER_EVAL = 64              # node record read per resource-only evaluation
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pods", type=int, default=50_000)
+    ap.add_argument("--groups", type=int, default=100)
+    ap.add_argument("--existing", type=int, default=1000)
+    ap.add_argument("--max-nodes", type=int, default=1000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-groups", type=int, default=100, help="groups in the bounded CPU-baseline sample")
+    return ap.parse_args()
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")           # RCCL on ROCm
+
+    from autoscaler_amd import native
+    from autoscaler_amd import workloads as W
+
+    # rank r owns node groups [100 r, 100 r + 100) of the job (seeded per rank)
+    w = W.c2(n_pods=args.pods, n_groups=args.groups, n_existing=args.existing, max_nodes=args.max_nodes,
+             seed=42 + rank)
+    mirror = native.Mirror(local)
+    W.load_estimate(mirror, w)
+    plan = native.EstimatePlan(mirror, w.table, w.group_off, w.pod_idx, w.templates)
+    L0 = 0
+
+    def step():
+        """One batch on this rank + the lastIndex chain across ranks."""
+        out = plan.run(w.max_nodes, L0)
+        st = plan.stats()
+        if dist is None:
+            return out, st, 0
+        lin = L0
+        extra = 0
+        while True:
+            rec = torch.tensor([lin, out.last_index, st["lin_sensitive"], st["had_success"]], dtype=torch.int64,
+                               device=f"cuda:{local}")
+            gathered = [torch.empty_like(rec) for _ in range(world)]
+            dist.all_gather(gathered, rec)
+            recs = torch.stack(gathered).cpu().tolist()
+            cur = L0
+            rerun = -1
+            for r, (l_in, l_out, sens, succ) in enumerate(recs):
+                if l_in != cur and sens:
+                    rerun = r
+                    break
+                cur = l_out if succ else cur
+            if rerun < 0:
+                return out, st, extra
+            if rerun == rank:                       # exact input for the first stale shard
+                lin = cur
+                out = plan.run(w.max_nodes, lin)
+                st = plan.stats()
+                extra += 1
+
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evals = 0
+    chain_ms = []
+    sort_ms = []
+    rounds = []
+    for _ in range(args.steps):
+        out, st, extra = step()
+        evals += int(out.results["evals"].sum())
+        chain_ms.append(st["chain_ms"] / max(st["rounds"], 1))
+        sort_ms.append(st["sort_ms"])
+        rounds.append(st["rounds"] + extra)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed, float(evals)], dtype=torch.float64, device=f"cuda:{local}")
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax[0])
+        total_evals = int(tsum[1])
+    else:
+        total_evals = evals
+    evals_per_step = evals / args.steps                         # this rank's batch
+    kernel_ms = float(np.mean(chain_ms))
+    achieved = BYTES_PER_EVAL * evals_per_step / (kernel_ms / 1e3) / 1e9
+
+    result = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import pyoracle                                       # CPU baseline leg only
+            o = pyoracle.OracleState()
+            W.load_estimate(o, w)
+            g = min(args.cpu_groups, args.groups)
+            off = w.group_off[: g + 1]
+            c0 = time.perf_counter()
+            ro = o.estimate(w.table, off, w.pod_idx[: off[-1]], w.templates[:g], w.max_nodes, L0)
+            cpu_s = time.perf_counter() - c0
+            cpu_evals = int(ro.results["evals"].sum())
+            cpu = {"value": cpu_evals / cpu_s, "unit": "evals/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle/casim_oracle.c Estimate of {g} of the {args.groups} C2 groups (one batch, "
+                             f"{cpu_evals} evals in {cpu_s:.2f} s) on 1 thread of {cpu_model()}",
+                   "estimate_ms": cpu_s * 1e3}
+        ms = elapsed / args.steps * 1e3
+        result = {
+            "metric": METRIC,
+            "value": total_evals / elapsed,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic: seeded C2 generator (autoscaler_amd/workloads.py), 64-shape pod catalog",
+            "config": {
+                "workload": "C2: heterogeneous pending pods x node-group templates, resource-fit only "
+                            "(BASELINE.json configs[1]); one step = Estimate() for every group",
+                "pods": args.pods, "groups_per_gpu": args.groups, "existing_nodes": args.existing,
+                "max_nodes_per_scaleup": args.max_nodes,
+                "parallelism": f"groups sharded over {world} GPU(s), lastIndex chained by all_gather",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "kernel": "k_ffd_chain", "kernel_ms": kernel_ms,
+                "bytes_per_unit": BYTES_PER_EVAL, "units_per_launch": evals_per_step,
+            },
+            "cpu_baseline": cpu,
+            "extra": {
+                "estimate_latency_ms": ms,
+                "sort_ms": float(np.mean(sort_ms)),
+                "chain_kernel_ms": kernel_ms,
+                "speculation_rounds": float(np.mean(rounds)),
+                "evals_per_step": total_evals / args.steps,
+                "speedup_vs_cpu_baseline": (total_evals / elapsed) / cpu["value"] if cpu else None,
+            },
+        }
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    plan.close()
+    mirror.close()
+    return result
+
+
+if __name__ == "__main__":
+    main()

@@ -122,9 +122,9 @@ extern "C" {
 
 /* UnremovableReason values (cluster.go:58-90) used by ca_find_nodes_to_remove */
 #define CA_UNREMOVABLE_NONE              0
-#define CA_UNREMOVABLE_NO_PLACE          13 /* NoPlaceToMovePods */
-#define CA_UNREMOVABLE_BLOCKED_BY_POD    14 /* BlockedByPod      */
-#define CA_UNREMOVABLE_UNEXPECTED_ERROR  15 /* UnexpectedError   */
+#define CA_UNREMOVABLE_NO_PLACE          12 /* NoPlaceToMovePods */
+#define CA_UNREMOVABLE_BLOCKED_BY_POD    13 /* BlockedByPod      */
+#define CA_UNREMOVABLE_UNEXPECTED_ERROR  14 /* UnexpectedError   */
 
 /* ------------------------------------------------------------------------- */
 
@@ -317,6 +317,11 @@ int ca_estimate_plan_destroy(ca_estimate_plan* p);
 /* statistics of the last run: speculation rounds, kernel time of the chain kernel (ms) */
 int ca_estimate_plan_stats(const ca_estimate_plan* p, int32_t* rounds, float* chain_ms,
                            float* sort_ms, float* total_ms);
+/* Whether the last run's outputs depend on the lastIndex it started from (then a caller
+ * that ran the batch from a guessed lastIndex must re-run it from the true one), and
+ * whether any FitsAnyNode call succeeded (if not, lastIndex passed through unchanged).
+ * Used to chain batches sharded across GPUs. */
+int ca_estimate_plan_chain_info(const ca_estimate_plan* p, int32_t* lin_sensitive, int32_t* had_success);
 
 /* ---- removal simulator ------------------------------------------------------- */
 /* FindNodesToRemove(candidates, destinations) with legacy semantics (canPersist=false).

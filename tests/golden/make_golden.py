@@ -1,0 +1,182 @@
+"""Writes tests/golden/reference_cases.json: the known-answer tests of the reference.
+
+The reference is Go (no toolchain in this container), so its tests
+cannot be executed here.  Each case below transcribes one table row of a
+reference test — its inputs (node/pod builders with the same arguments) and the
+expected values the test asserts — with the file:line it comes from.  Quantities
+are in the reference's units: cpu in millicores, memory in bytes, and the
+estimator tests' makeNode/makePods memory in MiB (converted here).
+
+Run:  python tests/golden/make_golden.py
+"""
+import json
+import os
+
+MIB = 1024 * 1024
+EST = "CA/estimator/binpacking_estimator_test.go"
+SCH = "CA/simulator/predicatechecker/schedulerbased_test.go"
+CLU = "CA/simulator/cluster_test.go"
+HNT = "CA/simulator/scheduling/hinting_simulator_test.go"
+
+
+def est_node(cpu, mem_mib, name, zone):
+    """makeNode (binpacking_estimator_test.go:83-103): pods 10, hostname + zone labels."""
+    return {"name": name, "cpu": cpu, "mem": mem_mib * MIB, "pods": 10,
+            "labels": {"kubernetes.io/hostname": name, "topology.kubernetes.io/zone": zone}}
+
+
+def est_pods(cpu, mem_mib, hostport, count):
+    """makePods (binpacking_estimator_test.go:35-81): one pod object repeated."""
+    p = {"name": "estimatee", "ns": "universe", "cpu": cpu, "mem": mem_mib * MIB, "labels": {"app": "estimatee"}}
+    if hostport:
+        p["hostport"] = hostport
+    return {"repeat": count, "pod": p}
+
+
+def test_node(name, cpu, mem, **kw):
+    """BuildTestNode (utils/test/test_utils.go:179-210): pods 100."""
+    d = {"name": name, "cpu": cpu, "mem": mem, "pods": 100}
+    d.update(kw)
+    return d
+
+
+def test_pod(name, cpu, mem, **kw):
+    """BuildTestPod (utils/test/test_utils.go:36-68): UID = name, namespace default."""
+    d = {"name": name, "cpu": cpu, "mem": mem}
+    d.update(kw)
+    return d
+
+
+cases = []
+
+# ---- estimator: TestBinpackingEstimate -------------------------------------
+for name, line, cpu, mem, pods, max_nodes, en, ep in [
+    ("simple resource-based binpacking", "114-120", 350 * 3 - 50, 2 * 1000, est_pods(350, 1000, 0, 10), 0, 5, 10),
+    ("pods-per-node bound binpacking", "121-127", 10000, 20000, est_pods(10, 100, 0, 20), 0, 2, 20),
+    ("hostport conflict forces pod-per-node", "128-134", 1000, 5000, est_pods(200, 1000, 5555, 8), 0, 8, 8),
+    ("limiter cuts binpacking", "135-142", 1000, 5000, est_pods(500, 1000, 0, 20), 5, 5, 10),
+]:
+    cases.append({
+        "id": f"estimate/{name}", "source": f"{EST}:{line},164-186", "kind": "estimate",
+        "nodes": [est_node(100, 100, "oldnode", "zone-jupiter")],
+        "template": est_node(cpu, mem, "template", "zone-mars"),
+        "pods": pods, "max_nodes": max_nodes,
+        "expect": {"node_count": en, "pod_count": ep},
+    })
+# the two topology-spread rows (:143-158) need PodTopologySpread: out of kernel scope
+for name, line in [("hostname topology spreading with maxSkew=2 forces 2 pods/node", "143-150"),
+                   ("zonal topology spreading with maxSkew=2 only allows 2 pods to schedule", "151-158")]:
+    cases.append({"id": f"estimate/{name}", "source": f"{EST}:{line}", "kind": "unsupported",
+                  "reason": "PodTopologySpread DoNotSchedule constraint (SURVEY §8a A12): routed to the Go path"})
+
+# ---- predicate checker: TestCheckPredicate ------------------------------------
+n1000 = test_node("n1000", 1000, 2000000)
+for name, line, sched, pod, err in [
+    ("other pod - insuficient cpu", "44-50", [test_pod("p450", 450, 500000)], test_pod("p600", 600, 500000), True),
+    ("other pod - ok", "51-57", [test_pod("p450", 450, 500000)], test_pod("p500", 500, 500000), False),
+    ("empty - insuficient cpu", "58-64", [], test_pod("p8000", 8000, 0), True),
+    ("empty - ok", "65-71", [], test_pod("p600", 600, 500000), False),
+]:
+    expect = {"error": err}
+    if err:
+        expect.update({"type": 0, "message": "Insufficient cpu",
+                       "verbose_contains": "Insufficient cpu; predicateName=NodeResourcesFit"})
+    cases.append({"id": f"check_predicates/{name}", "source": f"{SCH}:{line},73-91", "kind": "check_predicates",
+                  "nodes": [dict(n1000, scheduled=sched)], "pod": pod, "node": "n1000", "expect": expect})
+
+cases.append({
+    "id": "check_predicates/debug info (taints)", "source": f"{SCH}:127-157", "kind": "check_predicates",
+    "nodes": [test_node("n1", 1000, 2000000, taints=[["SomeTaint", "WhyNot?", "NoSchedule"],
+                                                     ["RandomTaint", "JustBecause", "NoExecute"]])],
+    "pod": test_pod("p1", 0, 0), "node": "n1",
+    "expect": {"error": True, "message": "node(s) had untolerated taint {SomeTaint: WhyNot?}",
+               "verbose_contains": "RandomTaint"},
+})
+
+# ---- predicate checker: TestFitsAnyNode ----------------------------------------
+cases.append({
+    "id": "fits_any_node/TestFitsAnyNode", "source": f"{SCH}:96-125", "kind": "fits_any_node",
+    "nodes": [test_node("n1000", 1000, 2000000), test_node("n2000", 2000, 2000000)],
+    "sequence": [
+        {"pod": test_pod("p900", 900, 1000), "expect": ["n1000", "n2000"]},
+        {"pod": test_pod("p1900", 1900, 1000), "expect": ["n2000"]},
+        {"pod": test_pod("p2100", 2100, 1000), "expect": None},
+    ],
+})
+
+# ---- removal simulator: TestFindNodesToRemove -----------------------------------
+nodes = {"n1": test_node("n1", 1000, 2000000), "n2": test_node("n2", 1000, 2000000),
+         "n3": test_node("n3", 1000, 2000000), "n4": test_node("n4", 1000, 2000000)}
+pods = {
+    "p1": test_pod("p1", 100, 100000, owner=["ReplicaSet", "rs"], node="n2"),
+    "p2": test_pod("p2", 100, 100000, owner=["ReplicaSet", "rs"], node="n2"),
+    "p3": test_pod("p3", 100, 100000, node="n3"),
+    "p4": test_pod("p4", 1000, 100000, node="n4"),
+}
+for name, line, ps, cands, alln, to_remove, unremovable in [
+    ("just an empty node, should be removed", "151-159", [], ["n1"], ["n1"], [["n1", []]], []),
+    ("just a drainable node, but nowhere for pods to go to", "160-168", ["p1", "p2"], ["n2"], ["n2"], [],
+     [["n2", "NoPlaceToMovePods", None, None]]),
+    ("drainable node, and a mostly empty node that can take its pods", "169-177", ["p1", "p2", "p3"], ["n2", "n3"],
+     ["n2", "n3"], [["n2", ["p1", "p2"]]], [["n3", "BlockedByPod", "p3", "NotReplicated"]]),
+    ("drainable node, and a full node that cannot fit anymore pods", "178-186", ["p1", "p2", "p4"], ["n2"],
+     ["n2", "n4"], [], [["n2", "NoPlaceToMovePods", None, None]]),
+    ("4 nodes, 1 empty, 1 drainable", "187-195", ["p1", "p2", "p3", "p4"], ["n1", "n2"], ["n1", "n2", "n4", "n3"],
+     [["n1", []], ["n2", ["p1", "p2"]]], []),
+]:
+    cases.append({
+        "id": f"find_nodes_to_remove/{name}", "source": f"{CLU}:{line},198-216", "kind": "find_nodes_to_remove",
+        "nodes": [nodes[n] for n in alln], "pods": [pods[p] for p in ps], "candidates": cands,
+        "listers": {"ReplicaSet": [["default", "rs", 5]]},
+        "delete_options": [True, True, 0],
+        "expect": {"to_remove": to_remove, "unremovable": unremovable},
+    })
+
+cases.append({
+    "id": "find_empty_nodes/TestFindEmptyNodes", "source": f"{CLU}:39-65", "kind": "find_empty_nodes",
+    "nodes": [test_node(f"n{i}", 1000, 2000000) for i in range(4)],
+    "pods": [test_pod("p1", 300, 500000, node="n1"),
+             test_pod("p2", 300, 500000, node="n2", annotations={"kubernetes.io/config.mirror": ""})],
+    "candidates": ["n0", "n1", "n2", "n3"],
+    "expect": {"empty": ["n0", "n2", "n3"]},
+})
+
+# ---- hinting simulator: TestTrySchedulePods / TestPodSchedulesOnHintedNode -------
+two = [test_node("n1", 1000, 2000000), test_node("n2", 1000, 2000000)]
+p1 = test_pod("p1", 300, 500000, node="n1")
+for name, line, new, acc, want in [
+    ("two new pods, two nodes", "44-62", [test_pod("p2", 800, 500000), test_pod("p3", 500, 500000)], None,
+     [["p2", "n2"], ["p3", "n1"]]),
+    ("three new pods, two nodes, no fit", "63-82",
+     [test_pod("p2", 800, 500000), test_pod("p3", 500, 500000), test_pod("p4", 700, 500000)], None,
+     [["p2", "n2"], ["p3", "n1"]]),
+    ("no new pods, two nodes", "83-94", [], None, []),
+    ("two nodes, but only one acceptable", "95-112", [test_pod("p2", 500, 500000), test_pod("p3", 500, 500000)],
+     ["n2"], [["p2", "n2"], ["p3", "n2"]]),
+    ("two nodes, but only one acceptable, no fit", "113-129",
+     [test_pod("p2", 500, 500000), test_pod("p3", 500, 500000)], ["n1"], [["p2", "n1"]]),
+]:
+    cases.append({
+        "id": f"try_schedule_pods/{name}", "source": f"{HNT}:{line},132-157", "kind": "try_schedule_pods",
+        "nodes": two, "pods": [p1], "new_pods": new, "acceptable": acc, "hints": {},
+        "expect": {"statuses": want},
+    })
+for name, line, pn in [
+    ("single hint", "166-170", {"p1": "n2"}),
+    ("all on one node", "171-179", {"p1": "n2", "p2": "n2", "p3": "n2"}),
+    ("spread across nodes", "180-188", {"p1": "n1", "p2": "n2", "p3": "n3"}),
+    ("lots of pods", "189-203", {"p1": "n1", "p2": "n1", "p3": "n1", "p4": "n2", "p5": "n2", "p6": "n2",
+                                 "p7": "n3", "p8": "n3", "p9": "n3"}),
+]:
+    cases.append({
+        "id": f"hinted/{name}", "source": f"{HNT}:{line},205-232", "kind": "try_schedule_pods",
+        "nodes": [test_node(n, 9999, 9999) for n in ("n1", "n2", "n3")], "pods": [],
+        "new_pods": [test_pod(p, 1, 1) for p in pn], "acceptable": None, "hints": pn,
+        "expect": {"statuses": [[p, n] for p, n in pn.items()]},
+    })
+
+if __name__ == "__main__":
+    out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_cases.json")
+    with open(out, "w") as f:
+        json.dump({"generated_by": "tests/golden/make_golden.py", "cases": cases}, f, indent=1)
+    print(f"wrote {len(cases)} cases to {out}")

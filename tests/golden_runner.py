@@ -1,0 +1,144 @@
+"""Runs the reference's known-answer cases (tests/golden/reference_cases.json) through
+the host facade over a given mirror backend (libcasim or the oracle)."""
+from __future__ import annotations
+
+import json
+import os
+
+from autoscaler_amd import k8s
+from autoscaler_amd.clustersnapshot import ClusterSnapshot, NodeInfo
+from autoscaler_amd.drain import ListerRegistry, NodeDeleteOptions
+from autoscaler_amd.estimator import BinpackingNodeEstimator, ThresholdBasedEstimationLimiter
+from autoscaler_amd.predicatechecker import SchedulerBasedPredicateChecker
+from autoscaler_amd.simulator import HintingSimulator, RemovalSimulator
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+REASONS = {"NoPlaceToMovePods": 12, "BlockedByPod": 13, "UnexpectedError": 14}
+BLOCK = {"NotReplicated": 3, "UnmovableKubeSystemPod": 6, "ControllerNotFound": 1}
+
+
+def load_cases() -> list:
+    with open(os.path.join(HERE, "golden", "reference_cases.json")) as f:
+        return json.load(f)["cases"]
+
+
+def build_node(d: dict) -> k8s.Node:
+    n = k8s.build_test_node(d["name"], d["cpu"], d["mem"], d.get("pods", 100))
+    n.labels.update(d.get("labels", {}))
+    n.taints = [k8s.Taint(*t) for t in d.get("taints", [])]
+    if d.get("gpu"):
+        k8s.add_gpus_to_node(n, d["gpu"])
+    n.unschedulable = d.get("unschedulable", False)
+    return n
+
+
+def build_pod(d: dict) -> k8s.Pod:
+    p = k8s.build_test_pod(d["name"], d["cpu"], d["mem"])
+    p.namespace = d.get("ns", p.namespace)
+    if "ns" in d:
+        p.uid = ""
+    p.labels.update(d.get("labels", {}))
+    p.annotations.update(d.get("annotations", {}))
+    if d.get("hostport"):
+        p.containers[0].ports.append(k8s.ContainerPort(host_port=d["hostport"]))
+    if d.get("owner"):
+        kind, name = d["owner"]
+        p.owner_refs = [k8s.OwnerReference(kind, name, name)]
+    if d.get("node"):
+        p.node_name = d["node"]
+    return p
+
+
+def expand_pods(spec) -> list:
+    if isinstance(spec, dict) and "repeat" in spec:
+        one = build_pod(spec["pod"])
+        return [one] * spec["repeat"]
+    return [build_pod(d) for d in spec]
+
+
+def run_case(case: dict, make_backend):
+    """Returns a list of mismatch strings (empty == pass)."""
+    kind = case["kind"]
+    errs = []
+    snap = ClusterSnapshot(make_backend())
+    checker = SchedulerBasedPredicateChecker()
+    if kind == "estimate":
+        snap.AddNodes([build_node(n) for n in case["nodes"]])
+        tmpl = build_node(case["template"])
+        pods = expand_pods(case["pods"])
+        est = BinpackingNodeEstimator(checker, snap, ThresholdBasedEstimationLimiter(case["max_nodes"]))
+        count, scheduled = est.Estimate(pods, NodeInfo(tmpl, []), None)
+        e = case["expect"]
+        if count != e["node_count"]:
+            errs.append(f"node count {count} != {e['node_count']}")
+        if len(scheduled) != e["pod_count"]:
+            errs.append(f"pod count {len(scheduled)} != {e['pod_count']}")
+    elif kind == "check_predicates":
+        for nd in case["nodes"]:
+            snap.AddNodeWithPods(build_node(nd), [build_pod(p) for p in nd.get("scheduled", [])])
+        err = checker.CheckPredicates(snap, build_pod(case["pod"]), case["node"])
+        e = case["expect"]
+        if (err is not None) != e["error"]:
+            errs.append(f"error={err!r}, expected error={e['error']}")
+        elif err is not None:
+            if "type" in e and err.ErrorType() != e["type"]:
+                errs.append(f"type {err.ErrorType()} != {e['type']}")
+            if err.Message() != e["message"]:
+                errs.append(f"message {err.Message()!r} != {e['message']!r}")
+            if e["verbose_contains"] not in err.VerboseMessage():
+                errs.append(f"verbose {err.VerboseMessage()!r} lacks {e['verbose_contains']!r}")
+    elif kind == "fits_any_node":
+        snap.AddNodes([build_node(n) for n in case["nodes"]])
+        for step in case["sequence"]:
+            name, err = checker.FitsAnyNode(snap, build_pod(step["pod"]))
+            if step["expect"] is None:
+                if err is None:
+                    errs.append(f"{step['pod']['name']}: expected error, got {name}")
+            elif err is not None or name not in step["expect"]:
+                errs.append(f"{step['pod']['name']}: got {name!r}/{err}, expected one of {step['expect']}")
+    elif kind == "find_nodes_to_remove":
+        nodes = [build_node(n) for n in case["nodes"]]
+        snap.AddNodes(nodes)
+        for pd in case["pods"]:
+            snap.AddPod(build_pod(pd), pd["node"])
+        listers = ListerRegistry({k: {(ns, n): r for ns, n, r in v} for k, v in case["listers"].items()})
+        opts = NodeDeleteOptions(*case["delete_options"])
+        rs = RemovalSimulator(listers, snap, checker, None, opts, False)
+        to_remove, unremovable = rs.FindNodesToRemove(case["candidates"], [n.name for n in nodes], 0.0, [])
+        got_tr = [[t.node.name, [p.name for p in t.pods_to_reschedule]] for t in to_remove]
+        if got_tr != case["expect"]["to_remove"]:
+            errs.append(f"toRemove {got_tr} != {case['expect']['to_remove']}")
+        got_un = [[u.node.name, {v: k for k, v in REASONS.items()}.get(u.reason, u.reason),
+                   u.blocking_pod.pod.name if u.blocking_pod else None,
+                   {v: k for k, v in BLOCK.items()}.get(u.blocking_pod.reason) if u.blocking_pod else None]
+                  for u in unremovable]
+        if got_un != case["expect"]["unremovable"]:
+            errs.append(f"unremovable {got_un} != {case['expect']['unremovable']}")
+    elif kind == "find_empty_nodes":
+        snap.AddNodes([build_node(n) for n in case["nodes"]])
+        for pd in case["pods"]:
+            snap.AddPod(build_pod(pd), pd["node"])
+        rs = RemovalSimulator(None, snap, checker, None, NodeDeleteOptions(), False)
+        got = rs.FindEmptyNodesToRemove(case["candidates"])
+        if got != case["expect"]["empty"]:
+            errs.append(f"empty {got} != {case['expect']['empty']}")
+    elif kind == "try_schedule_pods":
+        snap.AddNodes([build_node(n) for n in case["nodes"]])
+        for pd in case["pods"]:
+            snap.AddPod(build_pod(pd), pd["node"])
+        sim = HintingSimulator(checker)
+        new = [build_pod(p) for p in case["new_pods"]]
+        for p in new:
+            if p.name in case["hints"]:
+                sim.hints.Set(p.uid, case["hints"][p.name])
+        acc = case["acceptable"]
+        fn = None if acc is None else (lambda ni, acc=acc: ni.node.name in acc)
+        statuses, _, _ = sim.TrySchedulePods(snap, new, fn, False)
+        got = [[s.pod.name, s.node_name] for s in statuses]
+        if got != case["expect"]["statuses"]:
+            errs.append(f"statuses {got} != {case['expect']['statuses']}")
+        placed = sum(len(ni.pods) for ni in snap.List())
+        if placed != len(case["pods"]) + len(got):
+            errs.append(f"snapshot holds {placed} pods")
+    return errs

@@ -1,0 +1,311 @@
+"""HIP path (libcasim.so through the C ABI) vs the CPU restatement: bit-exact.
+
+Parity is exact equality of every output: node counts, scheduled pods and their
+node ordinals, removable sets, destinations, hints, lastIndex and the number of
+filter evaluations.  Sizes are chosen so the oracle finishes in seconds; the
+full-size workloads are also checked through size-independent properties.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from autoscaler_amd import abi, native
+from autoscaler_amd import workloads as W
+from autoscaler_amd.clustersnapshot import ClusterSnapshot, NodeInfo
+from autoscaler_amd.intern import Interner
+from autoscaler_amd.predicatechecker import SchedulerBasedPredicateChecker
+from golden_runner import load_cases, run_case
+from randgen import rand_cluster, rand_node, rand_pod
+
+pytestmark = pytest.mark.gpu
+
+CASES = [c for c in load_cases() if c["kind"] != "unsupported"]
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    import pyoracle
+    pyoracle.build()
+    return pyoracle
+
+
+def _mirror():
+    return native.Mirror(0)
+
+
+# --------------------------------------------------------------------------
+# the reference's own known-answer tests
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("case", CASES, ids=[c["id"] for c in CASES])
+def test_reference_case_on_gpu(case):
+    errs = run_case(case, _mirror)
+    assert not errs, f"{case['source']}: {errs}"
+
+
+# --------------------------------------------------------------------------
+# predicate checker: random clusters
+# --------------------------------------------------------------------------
+def _both(oracle, nodes, scheduled):
+    snaps = []
+    for b in (oracle.OracleState(), _mirror()):
+        s = ClusterSnapshot(b)
+        s.AddNodes(nodes)
+        for p, n in scheduled:
+            s.AddPod(p, n)
+        snaps.append(s)
+    return snaps
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_check_predicates_random(seed, oracle):
+    rng, nodes, scheduled, pending = rand_cluster(seed, n_nodes=10, n_pods=30)
+    so, sg = _both(oracle, nodes, scheduled)
+    table_o = so.encode(pending)
+    table_g = sg.encode(pending)
+    for i in range(len(pending)):
+        for pos in range(len(nodes)):
+            assert so.backend.check_predicates(table_o, i, pos) == sg.backend.check_predicates(table_g, i, pos), \
+                (seed, i, pos)
+    # dense feasibility matrix == CheckPredicates verdicts
+    mat = sg.backend.fits_matrix(table_g)
+    for i in range(len(pending)):
+        for pos in range(len(nodes)):
+            t = so.backend.check_predicates(table_o, i, pos)[0]
+            assert mat[i, pos] == (1 if t == abi.CA_PRED_OK else 0)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fits_any_node_random(seed, oracle):
+    rng, nodes, scheduled, pending = rand_cluster(seed, n_nodes=12, n_pods=40)
+    so, sg = _both(oracle, nodes, scheduled)
+    to, tg = so.encode(pending), sg.encode(pending)
+    L = 0
+    for i in range(len(pending)):
+        kind = rng.choice([abi.CA_MATCH_ALL, abi.CA_MATCH_RANGE, abi.CA_MATCH_MASK])
+        mask = np.array([rng.random() < 0.7 for _ in nodes], np.uint8)
+        lo, hi = sorted(rng.sample(range(len(nodes) + 1), 2))
+        match = (kind, lo, hi, rng.choice([-1, rng.randrange(len(nodes))]), mask if kind == abi.CA_MATCH_MASK else None)
+        if rng.random() < 0.2:
+            L = rng.randrange(0, 1000)
+        ro = so.backend.fits_any_node(to, i, match, L)
+        rg = sg.backend.fits_any_node(tg, i, match, L)
+        assert ro == rg, (seed, i, ro, rg)
+        L = ro[1]
+        if ro[0] >= 0 and rng.random() < 0.5:       # place it: the state moves on
+            for s, t in ((so, to), (sg, tg)):
+                s.backend.add_pods(t, [i], [ro[0]])
+
+
+# --------------------------------------------------------------------------
+# estimator
+# --------------------------------------------------------------------------
+def _estimate_inputs(seed, n_groups=6, n_pods=80):
+    rng = random.Random(seed)
+    nodes = [rand_node(rng, f"e{i}") for i in range(rng.randint(0, 5))]
+    pods = [rand_pod(rng, f"q{i}", small=rng.random() < 0.5) for i in range(n_pods)]
+    for p in pods:            # Estimate inputs never carry nodeName / matchFields in these runs
+        p.node_name = ""
+        if p.affinity is not None and p.affinity.required_terms:
+            for t in p.affinity.required_terms:
+                t.match_fields = []
+    templates = []
+    for g in range(n_groups):
+        t = rand_node(rng, f"tmpl{g}", big=rng.random() < 0.5)
+        ds = [rand_pod(rng, f"ds{g}-{j}", small=True) for j in range(rng.randint(0, 2))]
+        for d in ds:
+            d.affinity = None
+            d.node_selector = None
+        templates.append((t, ds))
+    groups = []
+    for g in range(n_groups):
+        sel = [p for p in pods if rng.random() < 0.6]
+        groups.append(sel)
+    return rng, nodes, pods, templates, groups
+
+
+def _encode_estimate(nodes, pods, templates, groups):
+    it = Interner(nodes, pods, templates)
+    table = it.encode_pods(pods)
+    node_recs = it.encode_nodes(nodes)
+    tm = np.zeros(len(templates), abi.TEMPLATE_DTYPE)
+    for g, (t, ds) in enumerate(templates):
+        tm[g] = it.encode_template(t, ds)
+    idx = {id(p): i for i, p in enumerate(pods)}
+    off = [0]
+    pod_idx = []
+    for sel in groups:
+        pod_idx.extend(idx[id(p)] for p in sel)
+        off.append(len(pod_idx))
+    return table, node_recs, tm, np.array(off, np.int32), np.array(pod_idx, np.int32)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_estimate_random(seed, oracle):
+    rng, nodes, pods, templates, groups = _estimate_inputs(seed)
+    table, node_recs, tm, off, pod_idx = _encode_estimate(nodes, pods, templates, groups)
+    max_nodes = rng.choice([0, 0, 3, 10])
+    L0 = rng.choice([0, 0, 1, 7, 123])
+    outs = []
+    for b in (oracle.OracleState(), _mirror()):
+        b.clear()
+        if len(node_recs):
+            b.add_nodes(node_recs)
+        outs.append(b.estimate(table, off, pod_idx, tm, max_nodes, L0))
+    o, g = outs
+    assert np.array_equal(o.results, g.results), (seed, o.results, g.results)
+    for k in range(len(groups)):
+        n = int(o.results[k]["n_scheduled"])
+        a = off[k]
+        assert np.array_equal(o.sched_pod[a:a + n], g.sched_pod[a:a + n]), (seed, k)
+        assert np.array_equal(o.sched_node[a:a + n], g.sched_node[a:a + n]), (seed, k)
+    assert o.last_index == g.last_index
+
+
+@pytest.mark.parametrize("name,w", [
+    ("C1", W.c1()),
+    ("C2-small", W.c2(n_pods=4000, n_groups=12, n_existing=50)),
+    ("C2-unlimited", W.c2(n_pods=1500, n_groups=8, n_existing=20, max_nodes=0)),
+    ("C2-medium", W.c2(n_pods=20000, n_groups=20, n_existing=300)),
+])
+def test_estimate_workloads(name, w, oracle):
+    outs = []
+    for b in (oracle.OracleState(), _mirror()):
+        W.load_estimate(b, w)
+        outs.append(b.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, 5))
+    o, g = outs
+    assert np.array_equal(o.results, g.results)
+    assert np.array_equal(o.sched_pod, g.sched_pod)
+    assert np.array_equal(o.sched_node, g.sched_node)
+    assert o.last_index == g.last_index
+    if name == "C1":
+        assert int(g.results[0]["node_count"]) == 125 and int(g.results[0]["n_scheduled"]) == 1000
+
+
+def test_estimate_full_c2_properties():
+    """Full-size C2 (50k pods x 100 groups): every new node's placements fit the template
+    (capacity conservation), scheduled pods are distinct members of their group, counts agree."""
+    w = W.c2()
+    m = _mirror()
+    W.load_estimate(m, w)
+    out = m.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, 0)
+    pods = w.table.pods
+    for g in range(len(w.templates)):
+        r = out.results[g]
+        n = int(r["n_scheduled"])
+        a = w.group_off[g]
+        sp, sn = out.sched_pod[a:a + n], out.sched_node[a:a + n]
+        assert len(set(sp.tolist())) == n
+        assert set(sp.tolist()) <= set(w.pod_idx[a:w.group_off[g + 1]].tolist())
+        t = w.templates[g]
+        free_cpu = t["node"]["alloc_milli_cpu"] - t["used_milli_cpu"]
+        free_mem = t["node"]["alloc_memory"] - t["used_memory"]
+        cpu = np.bincount(sn, weights=pods["req_milli_cpu"][sp], minlength=int(r["nodes_added"]))
+        mem = np.bincount(sn, weights=pods["req_memory"][sp].astype(np.float64), minlength=int(r["nodes_added"]))
+        assert (cpu <= free_cpu).all() and (mem <= free_mem * (1 + 1e-12)).all()
+        assert int(r["node_count"]) == len(set(sn.tolist()))
+        assert int(r["nodes_added"]) <= w.max_nodes
+
+
+# --------------------------------------------------------------------------
+# removal sweep
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("seed", range(12))
+def test_sweep_random(seed, oracle):
+    rng, nodes, scheduled, pending = rand_cluster(seed, n_nodes=14, n_pods=40, pods_per_node=4)
+    it = Interner(nodes, [p for p, _ in scheduled])
+    node_recs = it.encode_nodes(nodes)
+    table = it.encode_pods([p for p, _ in scheduled])
+    pos = {n.name: i for i, n in enumerate(nodes)}
+    node_of = np.array([pos[n] for _, n in scheduled], np.int32)
+    C = len(nodes)
+    cands = np.array(rng.sample(range(C), rng.randint(1, C)), np.int32)
+    mask = np.array([rng.random() < 0.85 for _ in nodes], np.uint8)
+    status = np.array([rng.choice([0, 0, 0, abi.CA_UNREMOVABLE_BLOCKED_BY_POD]) for _ in cands], np.int32)
+    off, moves = [0], []
+    for c in cands:
+        ids = [i for i in range(len(scheduled)) if node_of[i] == c and rng.random() < 0.9]
+        moves.extend(ids)
+        off.append(len(moves))
+    hints = np.array([rng.choice([-1, -1, rng.randrange(C)]) for _ in scheduled], np.int32)
+    L0 = rng.randrange(0, 3 * C)
+    outs = []
+    for b in (oracle.OracleState(), _mirror()):
+        b.clear()
+        b.add_nodes(node_recs)
+        b.add_pods(table, np.arange(len(scheduled), dtype=np.int32), node_of)
+        outs.append(b.find_nodes_to_remove(cands, mask, status, np.array(off, np.int32), np.array(moves, np.int32),
+                                           hints, L0))
+    o, g = outs
+    assert np.array_equal(o.results, g.results), (seed, o.results, g.results)
+    assert np.array_equal(o.dest, g.dest), seed
+    assert np.array_equal(o.hints, g.hints), seed
+    assert o.last_index == g.last_index
+
+
+@pytest.mark.parametrize("n_nodes", [300, 1500, 5000])
+def test_sweep_workload(n_nodes, oracle):
+    w = W.c3(n_nodes=n_nodes)
+    hints = np.full(len(w.table), -1, np.int32)
+    outs = []
+    for b in (oracle.OracleState(), _mirror()):
+        W.load_sweep(b, w)
+        outs.append(b.find_nodes_to_remove(w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods,
+                                           hints, 0))
+    o, g = outs
+    assert np.array_equal(o.results, g.results)
+    assert np.array_equal(o.dest, g.dest)
+    assert np.array_equal(o.hints, g.hints)
+    assert o.last_index == g.last_index
+
+
+def test_sweep_with_hints_second_loop(oracle):
+    """A second FindNodesToRemove with the hints of the first (the next loop's case)."""
+    w = W.c3(n_nodes=400)
+    outs = []
+    for b in (oracle.OracleState(), _mirror()):
+        W.load_sweep(b, w)
+        h = np.full(len(w.table), -1, np.int32)
+        r1 = b.find_nodes_to_remove(w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods, h, 0)
+        r2 = b.find_nodes_to_remove(w.candidates[::-1].copy(), w.dest_mask, w.cand_status[::-1].copy(),
+                                    *_reverse_moves(w), r1.hints, r1.last_index)
+        outs.append((r1, r2))
+    (o1, o2), (g1, g2) = outs
+    for o, g in ((o1, g1), (o2, g2)):
+        assert np.array_equal(o.results, g.results)
+        assert np.array_equal(o.dest, g.dest)
+        assert np.array_equal(o.hints, g.hints)
+        assert o.last_index == g.last_index
+
+
+def _reverse_moves(w):
+    C = len(w.candidates)
+    off, moves = [0], []
+    for c in reversed(range(C)):
+        moves.extend(w.move_pods[w.move_off[c]:w.move_off[c + 1]].tolist())
+        off.append(len(moves))
+    return np.array(off, np.int32), np.array(moves, np.int32)
+
+
+def test_fork_revert_commit_parity(oracle):
+    rng, nodes, scheduled, pending = rand_cluster(3, n_nodes=6, n_pods=20)
+    so, sg = _both(oracle, nodes, scheduled)
+    to, tg = so.encode(pending), sg.encode(pending)
+    ops = []
+    for step in range(60):
+        op = rng.choice(["fork", "add", "add", "revert", "commit", "fits"])
+        ops.append(op)
+        for s, t in ((so, to), (sg, tg)):
+            b = s.backend
+            if op == "fork":
+                b.fork()
+            elif op == "add":
+                b.add_pods(t, [step % len(pending)], [step % len(nodes)])
+            elif op in ("revert", "commit"):
+                try:
+                    getattr(b, op)()
+                except Exception:
+                    pass
+        if op == "fits":
+            assert so.backend.fits_any_node(to, step % len(pending), None, step) == \
+                sg.backend.fits_any_node(tg, step % len(pending), None, step), ops

@@ -23,6 +23,7 @@
 #include <cstring>
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 
 namespace casim {
 
@@ -48,9 +49,15 @@ static_assert(sizeof(SortItem) == 16, "SortItem");
 struct alignas(16) StreamPod {
     int64_t cpu, mem, eph;
     int32_t pod;      // pod set index
-    uint32_t flags;   // SF_*
+    uint32_t flags;   // SF_* | SF_HEAD | SF_BATCH
 };
 static_assert(sizeof(StreamPod) == 32, "StreamPod");
+
+// stream-only bits (k_emit_stream)
+enum : uint32_t {
+    SF_HEAD  = 0x100u,   // first pod of a run of identical consecutive pods
+    SF_BATCH = 0x200u,   // run-batchable: resource-only (no ports / scalars), requests >= 0
+};
 
 struct alignas(16) GroupMeta {
     int64_t tcpu, tmem, teph;      // template free (alloc - template pods)
@@ -59,8 +66,11 @@ struct alignas(16) GroupMeta {
     int32_t count;                 // pods in the group
     int32_t tmpl;                  // template index
     uint32_t tflags;               // NF_* of the template
-    int32_t pad;
+    int32_t moff;                  // offset of the group's 64-pod head masks
+    int32_t toff;                  // offset of the group's 1024-pod tile counters
+    int32_t pad[3];
 };
+static_assert(sizeof(GroupMeta) == 64, "GroupMeta");
 
 struct alignas(16) ChainOut {
     int32_t node_count, n_sched, nodes_added, lin;
@@ -184,21 +194,39 @@ __global__ void __launch_bounds__(256) k_merge_runs(const GroupMeta* __restrict_
     dst[gm.off + start + (i - run * width) + rank] = me;
 }
 
-// 3. gather the stream ---------------------------------------------------------
+// 3. gather the stream + run heads -------------------------------------------
+// A run is a maximal sequence of consecutive sorted pods that behave identically on
+// every new node: equal requests and equal SF_* bits, resource-only.  heads[] holds
+// one 64-bit mask per 64 stream positions (bit set = a run starts there; positions
+// past the group end are heads).
+__device__ inline bool batchable(const PodHot& p, uint32_t sf) {
+    return !(sf & (SF_PORTS | SF_SCALAR | SF_UNSUP)) && p.cpu >= 0 && p.mem >= 0 && p.eph >= 0;
+}
+
 __global__ void __launch_bounds__(256) k_emit_stream(const GroupMeta* __restrict__ groups, const SortItem* __restrict__ src,
                                                     const int32_t* __restrict__ pod_idx, const PodHot* __restrict__ ph,
-                                                    StreamPod* __restrict__ out) {
+                                                    StreamPod* __restrict__ out, uint64_t* __restrict__ heads) {
     const GroupMeta gm = groups[blockIdx.y];
     const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (i >= gm.count) return;
-    const SortItem it = src[gm.off + i];
-    const int32_t pidx = pod_idx[gm.off + (int32_t)it.pos];
-    const PodHot p = ph[pidx];
-    StreamPod sp;
-    sp.cpu = p.cpu; sp.mem = p.mem; sp.eph = p.eph;
-    sp.pod = pidx;
-    sp.flags = it.flags;
-    out[gm.off + i] = sp;
+    bool head = true;
+    if (i < gm.count) {
+        const SortItem it = src[gm.off + i];
+        const int32_t pidx = pod_idx[gm.off + (int32_t)it.pos];
+        const PodHot p = ph[pidx];
+        const bool bat = batchable(p, it.flags);
+        if (i > 0 && bat) {
+            const SortItem pv = src[gm.off + i - 1];
+            const PodHot q = ph[pod_idx[gm.off + (int32_t)pv.pos]];
+            head = !(pv.flags == it.flags && q.cpu == p.cpu && q.mem == p.mem && q.eph == p.eph);
+        }
+        StreamPod sp;
+        sp.cpu = p.cpu; sp.mem = p.mem; sp.eph = p.eph;
+        sp.pod = pidx;
+        sp.flags = it.flags | (head ? SF_HEAD : 0u) | (bat ? SF_BATCH : 0u);
+        out[gm.off + i] = sp;
+    }
+    const uint64_t hb = __ballot(head);
+    if ((threadIdx.x & 63) == 0 && i < gm.count) heads[gm.moff + (i >> 6)] = hb;
 }
 
 // 4. the First-Fit-Decreasing chain -------------------------------------------
@@ -224,6 +252,13 @@ __device__ inline int32_t wave_max32(int32_t v) {
     }
     return v;
 }
+__device__ inline int64_t wave_sum64(int64_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ inline int32_t mbcnt(uint64_t m) {
+    return (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 
 // New-node row in LDS: free resources of one template copy (32 B, two ds_read_b128).
 struct alignas(16) NodeRec {
@@ -239,15 +274,66 @@ __device__ inline bool rec_fits(const NodeRec& r, int64_t pcpu, int64_t pmem, in
     return (r.pods >= 1) & (zero | res);
 }
 
+// How many copies of a resource-only pod (requests >= 0) fit a row one after another:
+// copy m+1 fits iff pods >= m+1 and (all-zero or every req <= free - m*req), so the
+// count is min(pods, floor(free/req)) over the requested dimensions (fit.go:256-300;
+// a zero request passes iff free >= 0).  Capped at `cap`.
+__device__ inline int32_t dim_copies(int64_t free_, int64_t req, int32_t cap) {
+    if (free_ < 0) return 0;
+    if (req == 0) return cap;
+    const int64_t q = free_ / req;
+    return q < (int64_t)cap ? (int32_t)q : cap;
+}
+__device__ inline int32_t rec_copies(const NodeRec& r, int64_t pcpu, int64_t pmem, int64_t peph, bool zero, int32_t cap) {
+    int32_t c = r.pods < cap ? r.pods : cap;
+    if (c <= 0) return 0;
+    if (!zero) {
+        c = min(c, dim_copies(r.cpu, pcpu, c));
+        c = min(c, dim_copies(r.mem, pmem, c));
+        c = min(c, dim_copies(r.eph, peph, c));
+    }
+    return c;
+}
+
+// first run head strictly after `pos` (positions >= P count as heads)
+__device__ inline int32_t run_end(const uint64_t* __restrict__ hm, int32_t pos, int32_t P, int lane) {
+    int32_t c = pos >> 6;
+    const int32_t nc = (P + 63) >> 6;
+    const int sh = (pos & 63) + 1;
+    uint64_t m = hm[c];
+    m = sh >= 64 ? 0ull : (m >> sh) << sh;
+    if (m) return min(P, (c << 6) + __builtin_ctzll(m));
+    for (c = c + 1; c < nc; c += 64) {
+        const int32_t cc = c + lane;
+        const uint64_t v = cc < nc ? hm[cc] : 0ull;
+        const uint64_t b = __ballot(v != 0);
+        if (b) {
+            const int l = __builtin_ctzll(b);
+            return min(P, ((c + l) << 6) + __builtin_ctzll((uint64_t)rl64((int64_t)v, l)));
+        }
+    }
+    return P;
+}
+
 // One wavefront per node group.  LDS: NodeRec rows[kcap], block summaries[kcap/64]
-// (per-dimension maxima over a 64-row block, allowed to be stale-high), and the
-// optional port / scalar columns.
+// (per-dimension maxima over a 64-row block, allowed to be stale-high), the per-run
+// scratch CAPA/ALIVE[kcap], and the optional port / scalar columns.
+//
+// The sequential loop of binpacking_estimator.go:86-141 runs pod by pod, except that a
+// run of identical resource-only pods (SF_BATCH) is placed in closed form: the rotating
+// first fit of schedulerbased.go:114-131 with identical pods visits the nodes that still
+// have room in rotated order, one pod per node per revolution, so revolution r serves
+// the nodes with c_j >= r copies left, and the run costs O(k/64) wave steps plus one
+// step per node it opens instead of one k-node scan per pod.  Evals are exact: the t-th
+// placement's scan ends at unwrapped position (rev-1)*k + rank, so a batch costs
+// (r_last-1)*k + rank(last)+1 filter calls.  assign[pos] receives the new-node index of
+// every placed stream position (-1 = not scheduled).
 __global__ void __launch_bounds__(64) k_ffd_chain(
-    const GroupMeta* __restrict__ groups, const StreamPod* __restrict__ stream, const ca_template* __restrict__ tmpls,
-    const ca_pod_spec* __restrict__ specs, const PodHot* __restrict__ ph, const int32_t* __restrict__ lin_arr,
-    const uint8_t* __restrict__ need, const uint32_t* __restrict__ group_unsup, int32_t n_base, int32_t max_nodes,
-    int32_t kcap, int32_t use_ports, int32_t use_scalar, int32_t* __restrict__ sched_pod,
-    int32_t* __restrict__ sched_node, ChainOut* __restrict__ outs) {
+    const GroupMeta* __restrict__ groups, const StreamPod* __restrict__ stream, const uint64_t* __restrict__ heads,
+    const ca_template* __restrict__ tmpls, const ca_pod_spec* __restrict__ specs, const PodHot* __restrict__ ph,
+    const int32_t* __restrict__ lin_arr, const uint8_t* __restrict__ need, const uint32_t* __restrict__ group_unsup,
+    int32_t n_base, int32_t max_nodes, int32_t kcap, int32_t use_ports, int32_t use_scalar, int32_t batch_runs,
+    int32_t* __restrict__ assign, ChainOut* __restrict__ outs) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int g = blockIdx.x;
     if (!need[g]) return;
@@ -265,7 +351,9 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
     const int nb_cap = (kcap + 63) >> 6;
     NodeRec* R = reinterpret_cast<NodeRec*>(smem_raw);
     NodeRec* SUM = R + kcap;
-    uint64_t* PORTS = reinterpret_cast<uint64_t*>(SUM + nb_cap);               // [kcap][CA_PORT_WORDS]
+    int32_t* CAPA = reinterpret_cast<int32_t*>(SUM + nb_cap);                   // [kcap]
+    int32_t* ALIVE = CAPA + kcap;                                               // [kcap]
+    uint64_t* PORTS = reinterpret_cast<uint64_t*>(ALIVE + kcap);                // [kcap][CA_PORT_WORDS]
     int64_t* SC = reinterpret_cast<int64_t*>(PORTS + (use_ports ? (size_t)CA_PORT_WORDS * kcap : 0));  // [8][kcap]
 
     const ca_template& tp = tmpls[gm.tmpl];
@@ -282,33 +370,271 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
 
     const int32_t P = gm.count;
     const StreamPod* gs = stream + gm.off;
-    // Stream double buffer: lane l holds entry (window + l) in `cur` and (window + 64 + l)
-    // in `nxt`; the next window is requested 64 steps before it is read.  Outputs are
-    // kept in lanes (lane i = i-th placement of the window) and stored once per window,
-    // before the prefetch, so no step waits on a store (vmcnt counts both).
+    const uint64_t* hm = heads + gm.moff;
+    int32_t* ga = assign + gm.off;
+    // Stream double buffer: lane l holds entry (wbase + l) in `cur` and (wbase + 64 + l)
+    // in `nxt`.  Single-pod placements are kept in the lane of their stream position and
+    // stored when the window moves on, so no step waits on a store (vmcnt counts both).
+    int32_t wbase = 0;
     StreamPod cur = {}, nxt = {};
     if (lane < P) cur = gs[lane];
     if (64 + lane < P) nxt = gs[64 + lane];
-    int32_t out_pod = -1, out_node = -1;
-    int32_t flushed = 0;         // placements already stored
+    int32_t out_node = -1;
+    bool pend = false;
+    bool stop = false;
 
-    for (int32_t step = 0; step < P; step++) {
-        const int sl = step & 63;
-        if (sl == 0 && step > 0) {
-            const int32_t pend = nsched - flushed;
-            if (lane < pend) {
-                sched_pod[gm.off + flushed + lane] = out_pod;
-                if (sched_node) sched_node[gm.off + flushed + lane] = out_node;
-            }
-            flushed = nsched;
-            cur = nxt;
-            if (step + 64 + lane < P) nxt = gs[step + 64 + lane];
+    // add a template copy as new node k (addNewNodeToSnapshot, :146-159)
+    auto open_node = [&]() -> int32_t {
+        const int32_t nn = k;
+        if (lane == 0) {
+            R[nn] = trec;
+            SUM[nn >> 6] = trec;   // a fresh copy is the largest a row can be
         }
+        if (use_ports && lane < CA_PORT_WORDS) PORTS[(size_t)nn * CA_PORT_WORDS + lane] = tp.used_ports[lane];
+        if (use_scalar && lane < CA_MAX_SCALAR)
+            SC[(size_t)lane * kcap + nn] = wsub(tp.node.alloc_scalar[lane], tp.used_scalar[lane]);
+        k++;
+        last_node = nn;
+        return nn;
+    };
+    auto note_success = [&]() {
+        if (!first_success) { first_success = true; sensitive = k >= 2; }
+    };
+
+    int32_t pos = 0;
+    while (pos < P && !stop) {
+        if (pos >= wbase + 64) {
+            if (pend) ga[wbase + lane] = out_node;
+            pend = false;
+            if (pos < wbase + 128) {
+                cur = nxt;
+                wbase += 64;
+            } else {
+                wbase = pos & ~63;
+                cur = StreamPod{};
+                if (wbase + lane < P) cur = gs[wbase + lane];
+            }
+            nxt = StreamPod{};
+            if (wbase + 64 + lane < P) nxt = gs[wbase + 64 + lane];
+        }
+        const int sl = pos - wbase;
         const int64_t pcpu = rl64(cur.cpu, sl), pmem = rl64(cur.mem, sl), peph = rl64(cur.eph, sl);
         const int32_t pidx = rl32(cur.pod, sl);
         const uint32_t sf = (uint32_t)rl32((int32_t)cur.flags, sl);
         const bool zero = (sf & SF_ZERO) != 0;
 
+        // ---------------- a run of identical resource-only pods ----------------
+        if (batch_runs && (sf & (SF_BATCH | SF_HEAD)) == (SF_BATCH | SF_HEAD)) {
+            const int32_t e = run_end(hm, pos, P, lane);
+            if (e - pos >= 2) {
+                const int32_t RN = e - pos;
+                const uint64_t kev = (sf & SF_EVAL) ? 1u : 0u;
+                int32_t done = 0;
+                bool exhausted = false;          // every row but last_node has no room left
+                while (done < RN) {
+                    const int32_t rem = RN - done;
+                    const int32_t len = n_base + k;
+                    int32_t placed = 0;
+                    if ((sf & SF_FA_OK) && k > 0) {
+                        int32_t s0 = L;
+                        if (s0 >= len) s0 = (int32_t)((uint32_t)s0 % (uint32_t)len);
+                        const int32_t j0 = s0 > n_base ? s0 - n_base : 0;   // first new node visited
+                        int32_t one = -1, n_one = 0, nalive = 0;
+                        int64_t S = 0;
+                        if (exhausted) {
+                            const int32_t c = rec_copies(R[last_node], pcpu, pmem, peph, zero, rem);
+                            if (c > 0) { one = last_node; n_one = c; nalive = 1; }
+                        } else {
+                            int32_t na = 0, a1 = -1;
+                            for (int32_t j = lane; j < k; j += 64) {
+                                const int32_t c = rec_copies(R[j], pcpu, pmem, peph, zero, rem);
+                                CAPA[j] = c;
+                                S += c;
+                                if (c > 0) { na++; a1 = j; }
+                            }
+                            S = wave_sum64(S);
+                            nalive = (int32_t)wave_sum64(na);
+                            a1 = wave_max32(a1);
+                            if (nalive == 1) { one = a1; n_one = (int32_t)min(S, (int64_t)rem); }
+                        }
+                        if (nalive == 1) {
+                            // every remaining copy goes to the one row with room
+                            int32_t rho = one - j0;
+                            if (rho < 0) rho += k;
+                            evals += (uint64_t)rho + 1 + (uint64_t)(n_one - 1) * (uint64_t)k;
+                            if (lane == 0) {
+                                NodeRec r = R[one];
+                                r.cpu -= (int64_t)n_one * pcpu;
+                                r.mem -= (int64_t)n_one * pmem;
+                                r.eph -= (int64_t)n_one * peph;
+                                r.pods -= n_one;
+                                r.used = 1;
+                                R[one] = r;
+                            }
+                            for (int32_t t = lane; t < n_one; t += 64) ga[pos + done + t] = one;
+                            L = n_base + one + 1;
+                            if (L >= len) L -= len;
+                            note_success();
+                            placed = n_one;
+                        } else if (nalive > 1) {
+                            const int32_t n = (int32_t)min(S, (int64_t)rem);
+                            __builtin_amdgcn_wave_barrier();
+                            // revolution 1: rows with room, in rotated order from j0
+                            int32_t na = 0;
+                            for (int32_t b = 0; b < k; b += 64) {
+                                const int32_t rr = b + lane;
+                                int32_t j = j0 + rr;
+                                if (j >= k) j -= k;
+                                const bool keep = rr < k && CAPA[rr < k ? j : 0] >= 1;
+                                const uint64_t bm = __ballot(keep);
+                                if (keep) ALIVE[na + mbcnt(bm)] = j;
+                                na += __builtin_popcountll(bm);
+                            }
+                            __builtin_amdgcn_wave_barrier();
+                            int32_t got = 0, r = 1, last = -1;
+                            for (;;) {
+                                const int32_t m = min(na, n - got);
+                                for (int32_t i = lane; i < m; i += 64) ga[pos + done + got + i] = ALIVE[i];
+                                last = ALIVE[m - 1];
+                                got += m;
+                                if (got == n) break;
+                                // revolution r+1 serves the rows with at least r+1 copies
+                                int32_t nn2 = 0;
+                                for (int32_t b = 0; b < na; b += 64) {
+                                    const int32_t i = b + lane;
+                                    const int32_t j = i < na ? ALIVE[i] : 0;
+                                    const bool keep = i < na && CAPA[j] >= r + 1;
+                                    const uint64_t bm = __ballot(keep);
+                                    __builtin_amdgcn_wave_barrier();
+                                    if (keep) ALIVE[nn2 + mbcnt(bm)] = j;
+                                    nn2 += __builtin_popcountll(bm);
+                                    __builtin_amdgcn_wave_barrier();
+                                }
+                                na = nn2;
+                                r++;
+                            }
+                            int32_t rl = last - j0;
+                            if (rl < 0) rl += k;
+                            evals += (uint64_t)(r - 1) * (uint64_t)k + (uint64_t)rl + 1;
+                            for (int32_t j = lane; j < k; j += 64) {
+                                const int32_t c = CAPA[j];
+                                int32_t rj = j - j0;
+                                if (rj < 0) rj += k;
+                                const int32_t nj = min(c, r - 1) + ((c >= r && rj <= rl) ? 1 : 0);
+                                if (nj > 0) {
+                                    NodeRec q = R[j];
+                                    q.cpu -= (int64_t)nj * pcpu;
+                                    q.mem -= (int64_t)nj * pmem;
+                                    q.eph -= (int64_t)nj * peph;
+                                    q.pods -= nj;
+                                    q.used = 1;
+                                    R[j] = q;
+                                }
+                            }
+                            __builtin_amdgcn_wave_barrier();
+                            L = n_base + last + 1;
+                            if (L >= len) L -= len;
+                            note_success();
+                            placed = n;
+                        }
+                    }
+                    nsched += placed;
+                    done += placed;
+                    if (done == RN) break;
+                    exhausted = true;
+                    // the next pod of the run fails FitsAnyNode: every new node visited
+                    evals += kev * (uint64_t)k;
+                    if (max_nodes > 0 && granted >= max_nodes) { stop = true; break; }
+                    granted++;
+                    if (last_node >= 0 && !R[last_node].used) {
+                        // :114-116 — and every later pod of the run repeats this pod's fate
+                        done++;
+                        const int32_t q = RN - done;
+                        if (max_nodes > 0 && q > max_nodes - granted) {
+                            const int32_t allowed = max_nodes - granted;
+                            evals += (uint64_t)(allowed + 1) * kev * (uint64_t)k;
+                            granted = max_nodes;
+                            stop = true;
+                            break;
+                        }
+                        evals += (uint64_t)q * kev * (uint64_t)k;
+                        granted += q;
+                        done = RN;
+                        break;
+                    }
+                    if (k >= kcap) { res.status = CA_ECAPACITY; stop = true; break; }
+                    const int32_t rem2 = RN - done;
+                    if (!((sf & SF_CP_OK) && rec_fits(trec, pcpu, pmem, peph, zero))) {
+                        // CheckPredicates on the new node fails: it stays empty and the
+                        // next pod of the run takes the empty-node skip above
+                        open_node();
+                        if (sf & SF_CP_EVAL) evals++;
+                        done++;
+                        continue;
+                    }
+                    // Every row is full for this pod, so each remaining pod group opens a
+                    // fresh template copy: pod 1 by CheckPredicates (:132-135), the next
+                    // ct-1 by FitsAnyNode, whose scan ends at the new (last) row, so after
+                    // the first one lastIndex wraps to 0 and each costs k evals.  A
+                    // node's opening pod first fails FitsAnyNode over the k rows before it
+                    // and takes one limiter grant.  Closed form over n_open nodes.
+                    const int32_t ct = (sf & SF_FA_OK) ? rec_copies(trec, pcpu, pmem, peph, zero, rem2) : 1;
+                    int32_t n_open = (rem2 + ct - 1) / ct;
+                    if (max_nodes > 0) n_open = min(n_open, 1 + (max_nodes - granted));
+                    n_open = min(n_open, kcap - k);
+                    const int32_t k0 = k;
+                    const int32_t placed2 = min(rem2, n_open * ct);
+                    const int32_t len0 = n_base + k0 + 1;
+                    int32_t s00 = L;
+                    if (s00 >= len0) s00 = (int32_t)((uint32_t)s00 % (uint32_t)len0);
+                    const int32_t j00 = s00 > n_base ? s00 - n_base : 0;
+                    uint64_t ev = 0;
+                    for (int32_t i = lane; i < n_open; i += 64) {
+                        const int32_t pi = (i == n_open - 1) ? placed2 - i * ct : ct;
+                        if (i > 0) ev += kev * (uint64_t)(k0 + i);
+                        if (sf & SF_CP_EVAL) ev += 1;
+                        if (pi >= 2) {
+                            const int32_t j0i = i == 0 ? j00 : 0;
+                            ev += (uint64_t)(k0 + i - j0i + 1) + (uint64_t)(pi - 2) * (uint64_t)(k0 + i + 1);
+                        }
+                        NodeRec r = trec;
+                        r.cpu -= (int64_t)pi * pcpu;
+                        r.mem -= (int64_t)pi * pmem;
+                        r.eph -= (int64_t)pi * peph;
+                        r.pods -= pi;
+                        r.used = 1;
+                        R[k0 + i] = r;
+                    }
+                    evals += (uint64_t)wave_sum64((int64_t)ev);
+                    for (int32_t b = (k0 >> 6) + lane; b <= ((k0 + n_open - 1) >> 6); b += 64) SUM[b] = trec;
+                    if (use_ports) {
+                        for (int32_t i = lane; i < n_open * CA_PORT_WORDS; i += 64)
+                            PORTS[(size_t)k0 * CA_PORT_WORDS + i] = tp.used_ports[i % CA_PORT_WORDS];
+                    }
+                    if (use_scalar) {
+                        for (int32_t i = lane; i < n_open * CA_MAX_SCALAR; i += 64) {
+                            const int32_t sc = i / n_open, node = k0 + i % n_open;
+                            SC[(size_t)sc * kcap + node] = wsub(tp.node.alloc_scalar[sc], tp.used_scalar[sc]);
+                        }
+                    }
+                    for (int32_t t = lane; t < placed2; t += 64) ga[pos + done + t] = k0 + t / ct;
+                    if (ct >= 2 && placed2 >= 2) {
+                        if (!first_success) { first_success = true; sensitive = k0 + 1 >= 2; }
+                        L = 0;       // n_base + (last row) + 1 == len
+                    }
+                    k = k0 + n_open;
+                    last_node = k - 1;
+                    granted += n_open - 1;
+                    nsched += placed2;
+                    done += placed2;
+                    __builtin_amdgcn_wave_barrier();
+                }
+                pos = e;
+                continue;
+            }
+        }
+
+        // ---------------- one pod ----------------
         // rare per-pod data (ports / scalars) from the full record
         uint64_t pconf[CA_PORT_WORDS] = {0, 0}, puse[CA_PORT_WORDS] = {0, 0};
         int64_t psc[CA_MAX_SCALAR];
@@ -318,6 +644,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
             for (int w = 0; w < CA_PORT_WORDS; w++) { pconf[w] = s.port_conflict[w]; puse[w] = s.port_use[w]; }
             for (int i = 0; i < CA_MAX_SCALAR; i++) psc[i] = s.req_scalar[i];
         }
+        pos++;
 
         // ---- FitsAnyNodeMatching(newNodeNames) (binpacking_estimator.go:91-93) ----
         int32_t found = -1;
@@ -381,7 +708,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                     int32_t off = found - j0;                                  // rotated offset among new nodes
                     if (off < 0) off += k;
                     evals += (uint64_t)off + 1;
-                    if (!first_success) { first_success = true; sensitive = k >= 2; }
+                    note_success();
                     L = n_base + found + 1;                                    // schedulerbased.go:131
                     if (L >= len) L -= len;
                 } else {
@@ -397,17 +724,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
             granted++;
             if (last_node >= 0 && !R[last_node].used) continue;               // :114-116
             if (k >= kcap) { res.status = CA_ECAPACITY; break; }
-            // addNewNodeToSnapshot: a template copy (:146-159)
-            const int32_t nn = k;
-            if (lane == 0) {
-                R[nn] = trec;
-                SUM[nn >> 6] = trec;   // a fresh copy is the largest a row can be
-            }
-            if (use_ports && lane < CA_PORT_WORDS) PORTS[(size_t)nn * CA_PORT_WORDS + lane] = tp.used_ports[lane];
-            if (use_scalar && lane < CA_MAX_SCALAR)
-                SC[(size_t)lane * kcap + nn] = wsub(tp.node.alloc_scalar[lane], tp.used_scalar[lane]);
-            k++;
-            last_node = nn;
+            const int32_t nn = open_node();
             // CheckPredicates(pod, newNode) (:132-134)
             if (sf & SF_CP_EVAL) evals++;
             bool ok = (sf & SF_CP_OK) != 0;
@@ -436,7 +753,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
             r.used = 1;
             R[found] = r;
         }
-        if (lane == nsched - flushed) { out_pod = pidx; out_node = found; }
+        if (lane == sl) { out_node = found; pend = true; }
         if (sf & SF_SCALAR) {
             if (lane < CA_MAX_SCALAR) {
                 const size_t ix = (size_t)lane * kcap + found;
@@ -449,13 +766,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
         nsched++;
         __builtin_amdgcn_wave_barrier();
     }
-    {
-        const int32_t pend = nsched - flushed;
-        if (lane < pend) {
-            sched_pod[gm.off + flushed + lane] = out_pod;
-            if (sched_node) sched_node[gm.off + flushed + lane] = out_node;
-        }
-    }
+    if (pend) ga[wbase + lane] = out_node;
     // newNodesWithPods
     int32_t cnt = 0;
     for (int32_t j = lane; j < k; j += 64) cnt += R[j].used;
@@ -469,6 +780,65 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
         res.had_success = first_success ? 1 : 0;
         res.evals = evals;
         outs[g] = res;
+    }
+}
+
+// 5. scheduled pods in processing order: compact assign[] per group ------------
+// (binpacking_estimator.go:143 returns the scheduled pods in the order they were placed,
+// which is stream order.)  Two passes over 1024-position tiles: count, then scatter.
+constexpr int CTILE = 1024;
+
+__global__ void __launch_bounds__(256) k_tile_count(const GroupMeta* __restrict__ groups, const int32_t* __restrict__ assign,
+                                                   int32_t* __restrict__ tcount) {
+    const GroupMeta gm = groups[blockIdx.y];
+    const int32_t base = (int32_t)blockIdx.x * CTILE;
+    if (base >= gm.count) return;
+    __shared__ int32_t wsum[4];
+    int32_t c = 0;
+    for (int t = threadIdx.x; t < CTILE; t += 256) {
+        const int32_t i = base + t;
+        c += (i < gm.count && assign[gm.off + i] >= 0) ? 1 : 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) tcount[gm.toff + blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+__global__ void __launch_bounds__(CTILE) k_tile_scatter(const GroupMeta* __restrict__ groups, const int32_t* __restrict__ assign,
+                                                      const StreamPod* __restrict__ stream, const int32_t* __restrict__ tcount,
+                                                      int32_t* __restrict__ sched_pod, int32_t* __restrict__ sched_node) {
+    const GroupMeta gm = groups[blockIdx.y];
+    const int32_t base = (int32_t)blockIdx.x * CTILE;
+    if (base >= gm.count) return;
+    __shared__ int32_t wsum[CTILE / 64];
+    __shared__ int32_t prefix, total;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (w == 0) {   // tiles before this one, and the group's scheduled count
+        const int32_t nt = (gm.count + CTILE - 1) / CTILE;
+        int32_t s = 0, a = 0;
+        for (int32_t t = lane; t < nt; t += 64) {
+            const int32_t c = tcount[gm.toff + t];
+            a += c;
+            if (t < (int32_t)blockIdx.x) s += c;
+        }
+        for (int o = 32; o > 0; o >>= 1) { s += __shfl_xor(s, o, 64); a += __shfl_xor(a, o, 64); }
+        if (lane == 0) { prefix = s; total = a; }
+    }
+    const int32_t i = base + (int32_t)threadIdx.x;
+    const int32_t a = i < gm.count ? assign[gm.off + i] : -1;
+    const uint64_t bm = __ballot(a >= 0);
+    if (lane == 0) wsum[w] = __builtin_popcountll(bm);
+    __syncthreads();
+    if (a >= 0) {
+        int32_t o = prefix + mbcnt(bm);
+        for (int v = 0; v < w; v++) o += wsum[v];
+        sched_pod[gm.off + o] = stream[gm.off + i].pod;
+        if (sched_node) sched_node[gm.off + o] = a;
+    }
+    if (i < gm.count && i >= total) {     // entries past n_scheduled read back as -1
+        sched_pod[gm.off + i] = -1;
+        if (sched_node) sched_node[gm.off + i] = -1;
     }
 }
 
@@ -486,9 +856,18 @@ struct ca_estimate_plan {
     std::vector<ca_template> h_tmpl;
     std::vector<GroupMeta> h_meta;
     bool use_ports = false, use_scalar = false;
-    DevBuf d_meta, d_pod_idx, d_tmpl, d_sortA, d_sortB, d_stream, d_unsup, d_lin, d_need, d_out, d_sched_pod,
-        d_sched_node;
+    int32_t n_masks = 0, n_tiles = 0;
+    DevBuf d_meta, d_pod_idx, d_tmpl, d_sortA, d_sortB, d_stream, d_heads, d_assign, d_tcount, d_unsup, d_lin, d_need,
+        d_out, d_sched_pod, d_sched_node;
     Stats stats;
+    // per-phase device timings of the last run (ms): score, merge, emit, chain (all
+    // rounds), compact, d2h; and the host wall time of the call
+    enum { EV_START, EV_SCORE, EV_MERGE, EV_EMIT, EV_CHAIN0, EV_CHAIN1, EV_COMPACT, EV_D2H, EV_N };
+    hipEvent_t ev[EV_N] = {};
+    float t_ms[7] = {};
+    ~ca_estimate_plan() {
+        for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+    }
 };
 
 namespace {
@@ -496,12 +875,15 @@ namespace {
 int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const int32_t* group_off,
                  const int32_t* pod_idx, const ca_template* templates, int32_t G) {
     p->m = m; p->s = s; p->G = G;
+    for (auto& e : p->ev) CA_HIP_CHECK(hipEventCreate(&e));
     p->h_off.assign(group_off, group_off + G + 1);
     p->h_tmpl.assign(templates, templates + G);
     p->total = group_off[G] - group_off[0];
     if (group_off[0] != 0) return CA_EINVAL;
     p->h_meta.resize(G);
     p->max_count = 0;
+    p->n_masks = 0;
+    p->n_tiles = 0;
     for (int32_t g = 0; g < G; g++) {
         const int32_t c = group_off[g + 1] - group_off[g];
         if (c < 0) return CA_EINVAL;
@@ -515,7 +897,11 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
         gm.count = c;
         gm.tmpl = g;
         gm.tflags = t.node.flags;
-        gm.pad = 0;
+        gm.moff = p->n_masks;
+        gm.toff = p->n_tiles;
+        gm.pad[0] = gm.pad[1] = gm.pad[2] = 0;
+        p->n_masks += (c + 63) / 64;
+        p->n_tiles += (c + CTILE - 1) / CTILE;
         p->max_count = std::max(p->max_count, c);
         for (int w = 0; w < CA_PORT_WORDS; w++) if (t.used_ports[w]) p->use_ports = true;
         for (int i = 0; i < CA_MAX_SCALAR; i++)
@@ -537,6 +923,9 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     if ((rc = p->d_sortA.reserve(sizeof(SortItem) * tot)) != CA_OK) return rc;
     if ((rc = p->d_sortB.reserve(sizeof(SortItem) * tot)) != CA_OK) return rc;
     if ((rc = p->d_stream.reserve(sizeof(StreamPod) * tot)) != CA_OK) return rc;
+    if ((rc = p->d_heads.reserve(sizeof(uint64_t) * (size_t)std::max(p->n_masks, 1))) != CA_OK) return rc;
+    if ((rc = p->d_assign.reserve(sizeof(int32_t) * tot)) != CA_OK) return rc;
+    if ((rc = p->d_tcount.reserve(sizeof(int32_t) * (size_t)std::max(p->n_tiles, 1))) != CA_OK) return rc;
     if ((rc = p->d_unsup.reserve(sizeof(uint32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
     if ((rc = p->d_lin.reserve(sizeof(int32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
     if ((rc = p->d_need.reserve((size_t)std::max(G, 1))) != CA_OK) return rc;
@@ -552,7 +941,7 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
 
 size_t chain_lds_bytes(int32_t kcap, bool use_ports, bool use_scalar) {
     const size_t nb = (size_t)((kcap + 63) >> 6);
-    size_t b = 32 * ((size_t)kcap + nb);
+    size_t b = 32 * ((size_t)kcap + nb) + 8 * (size_t)kcap;   // rows, summaries, CAPA + ALIVE
     if (use_ports) b += 8 * CA_PORT_WORDS * (size_t)kcap;
     if (use_scalar) b += 8 * CA_MAX_SCALAR * (size_t)kcap;
     return (b + 15) & ~(size_t)15;
@@ -575,10 +964,11 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     if (lds > 160 * 1024) return CA_EUNSUPPORTED;   // HBM-backed variant is future work
     CA_HIP_CHECK(hipMemsetAsync(p->d_unsup.ptr, 0, sizeof(uint32_t) * G, st));
     if (p->total > 0) {   // entries past n_scheduled read back as -1
-        CA_HIP_CHECK(hipMemsetAsync(p->d_sched_pod.ptr, 0xFF, sizeof(int32_t) * p->total, st));
-        CA_HIP_CHECK(hipMemsetAsync(p->d_sched_node.ptr, 0xFF, sizeof(int32_t) * p->total, st));
+        CA_HIP_CHECK(hipMemsetAsync(p->d_assign.ptr, 0xFF, sizeof(int32_t) * p->total, st));
     }
-    CA_HIP_CHECK(hipEventRecord(m->ev0, st));
+    const char* rb_env = getenv("CASIM_RUN_BATCH");
+    const int32_t batch_runs = (rb_env && rb_env[0] == '0') ? 0 : 1;
+    CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_START], st));
     // 1-3: score, sort, stream
     if (p->total > 0) {
         const int32_t tiles = (p->max_count + TILE - 1) / TILE;
@@ -587,6 +977,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                            p->s->t.spec.as<ca_pod_spec>(), p->s->t.terms.as<ca_selector_term>(),
                            p->s->t.reqs.as<ca_selector_req>(), p->d_sortA.as<SortItem>(), p->d_unsup.as<uint32_t>());
         CA_HIP_CHECK(hipGetLastError());
+        CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], st));
         SortItem* a = p->d_sortA.as<SortItem>();
         SortItem* b = p->d_sortB.as<SortItem>();
         const int32_t blocks = (p->max_count + 255) / 256;
@@ -595,11 +986,13 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             CA_HIP_CHECK(hipGetLastError());
             std::swap(a, b);
         }
+        CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], st));
         hipLaunchKernelGGL(k_emit_stream, dim3(blocks, G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(), a,
-                           p->d_pod_idx.as<int32_t>(), p->s->t.hot.as<PodHot>(), p->d_stream.as<StreamPod>());
+                           p->d_pod_idx.as<int32_t>(), p->s->t.hot.as<PodHot>(), p->d_stream.as<StreamPod>(),
+                           p->d_heads.as<uint64_t>());
         CA_HIP_CHECK(hipGetLastError());
     }
-    CA_HIP_CHECK(hipEventRecord(m->ev1, st));
+    CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_EMIT], st));
     // 4-5: chains with lastIndex speculation
     std::vector<int32_t> lin(G, *last_index);
     std::vector<uint8_t> need(G, 1);
@@ -612,24 +1005,21 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         rounds++;
         CA_HIP_CHECK(hipMemcpyAsync(p->d_lin.ptr, lin.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
         CA_HIP_CHECK(hipMemcpyAsync(p->d_need.ptr, need.data(), G, hipMemcpyHostToDevice, st));
-        CA_HIP_CHECK(hipEventRecord(m->ev2, st));
+        CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN0], st));
         CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_ffd_chain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL(k_ffd_chain, dim3(G), dim3(64), lds, st, p->d_meta.as<GroupMeta>(),
-                           p->d_stream.as<StreamPod>(), p->d_tmpl.as<ca_template>(), p->s->t.spec.as<ca_pod_spec>(),
-                           p->s->t.hot.as<PodHot>(), p->d_lin.as<int32_t>(), p->d_need.as<uint8_t>(),
-                           p->d_unsup.as<uint32_t>(), n_base, lim->max_nodes, kcap, p->use_ports ? 1 : 0,
-                           p->use_scalar ? 1 : 0, p->d_sched_pod.as<int32_t>(), p->d_sched_node.as<int32_t>(),
+                           p->d_stream.as<StreamPod>(), p->d_heads.as<uint64_t>(), p->d_tmpl.as<ca_template>(),
+                           p->s->t.spec.as<ca_pod_spec>(), p->s->t.hot.as<PodHot>(), p->d_lin.as<int32_t>(),
+                           p->d_need.as<uint8_t>(), p->d_unsup.as<uint32_t>(), n_base, lim->max_nodes, kcap,
+                           p->use_ports ? 1 : 0, p->use_scalar ? 1 : 0, batch_runs, p->d_assign.as<int32_t>(),
                            p->d_out.as<ChainOut>());
         CA_HIP_CHECK(hipGetLastError());
-        hipEvent_t evc;
-        CA_HIP_CHECK(hipEventCreate(&evc));
-        CA_HIP_CHECK(hipEventRecord(evc, st));
+        CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN1], st));
         std::vector<ChainOut> fresh(G);
         CA_HIP_CHECK(hipMemcpyAsync(fresh.data(), p->d_out.ptr, sizeof(ChainOut) * G, hipMemcpyDeviceToHost, st));
         CA_HIP_CHECK(hipStreamSynchronize(st));
         float ms = 0;
-        (void)hipEventElapsedTime(&ms, m->ev2, evc);
-        (void)hipEventDestroy(evc);
+        (void)hipEventElapsedTime(&ms, p->ev[ca_estimate_plan::EV_CHAIN0], p->ev[ca_estimate_plan::EV_CHAIN1]);
         chain_ms += ms;
         for (int32_t g = 0; g < G; g++) if (need[g]) outs[g] = fresh[g];
         // walk the lastIndex chain
@@ -668,12 +1058,24 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         }
         if (rounds > G + 2) { set_last_error("estimate speculation did not converge"); return CA_EDEVICE; }
     }
-    // results
+    // results: compact the per-position assignments into processing order
+    if (p->total > 0) {
+        const int32_t tiles = (p->max_count + CTILE - 1) / CTILE;
+        hipLaunchKernelGGL(k_tile_count, dim3(tiles, G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(),
+                           p->d_assign.as<int32_t>(), p->d_tcount.as<int32_t>());
+        CA_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_tile_scatter, dim3(tiles, G), dim3(CTILE), 0, st, p->d_meta.as<GroupMeta>(),
+                           p->d_assign.as<int32_t>(), p->d_stream.as<StreamPod>(), p->d_tcount.as<int32_t>(),
+                           p->d_sched_pod.as<int32_t>(), sched_node ? p->d_sched_node.as<int32_t>() : nullptr);
+        CA_HIP_CHECK(hipGetLastError());
+    }
+    CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_COMPACT], st));
     CA_HIP_CHECK(hipMemcpyAsync(sched_pod, p->d_sched_pod.ptr, sizeof(int32_t) * std::max(p->total, 0),
                                 hipMemcpyDeviceToHost, st));
     if (sched_node)
         CA_HIP_CHECK(hipMemcpyAsync(sched_node, p->d_sched_node.ptr, sizeof(int32_t) * std::max(p->total, 0),
                                     hipMemcpyDeviceToHost, st));
+    CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_D2H], st));
     CA_HIP_CHECK(hipStreamSynchronize(st));
     for (int32_t g = 0; g < G; g++) {
         const ChainOut& o = outs[g];
@@ -687,7 +1089,18 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         r.evals = o.evals;
     }
     float sort_ms = 0;
-    (void)hipEventElapsedTime(&sort_ms, m->ev0, m->ev1);
+    {
+        using P = ca_estimate_plan;
+        auto el = [&](int a, int b) { float v = 0; (void)hipEventElapsedTime(&v, p->ev[a], p->ev[b]); return v; };
+        const bool any = p->total > 0;
+        p->t_ms[0] = any ? el(P::EV_START, P::EV_SCORE) : 0;
+        p->t_ms[1] = any ? el(P::EV_SCORE, P::EV_MERGE) : 0;
+        p->t_ms[2] = any ? el(P::EV_MERGE, P::EV_EMIT) : 0;
+        p->t_ms[3] = chain_ms;
+        p->t_ms[4] = el(P::EV_CHAIN1, P::EV_COMPACT);
+        p->t_ms[5] = el(P::EV_COMPACT, P::EV_D2H);
+        sort_ms = el(P::EV_START, P::EV_EMIT);
+    }
     // batch-level lastIndex dependence: the first group with a FitsAnyNode success decides
     p->stats.lin_sensitive = 0;
     p->stats.had_success = 0;
@@ -702,6 +1115,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     p->stats.kernel_ms = chain_ms;
     p->stats.sort_ms = sort_ms;
     p->stats.total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    p->t_ms[6] = p->stats.total_ms;
     return CA_OK;
 }
 
@@ -739,6 +1153,13 @@ int ca_estimate_plan_stats(const ca_estimate_plan* p, int32_t* rounds, float* ch
     if (sort_ms) *sort_ms = p->stats.sort_ms;
     if (total_ms) *total_ms = p->stats.total_ms;
     return CA_OK;
+}
+
+int ca_estimate_plan_timings(const ca_estimate_plan* p, float* out, int32_t cap) {
+    if (!p || (cap > 0 && !out)) return CA_EINVAL;
+    const int32_t n = 7;
+    for (int32_t i = 0; i < n && i < cap; i++) out[i] = p->t_ms[i];
+    return n;
 }
 
 int ca_estimate_plan_chain_info(const ca_estimate_plan* p, int32_t* lin_sensitive, int32_t* had_success) {

@@ -357,6 +357,21 @@ int ca_device_count(int32_t* out) {
     return CA_OK;
 }
 
+int ca_host_alloc(size_t bytes, void** out) {
+    if (!out) return CA_EINVAL;
+    *out = nullptr;
+    hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
+    if (e != hipSuccess) { set_last_error(hipGetErrorString(e)); return CA_EDEVICE; }
+    return CA_OK;
+}
+
+int ca_host_free(void* p) {
+    if (!p) return CA_OK;
+    hipError_t e = hipHostFree(p);
+    if (e != hipSuccess) { set_last_error(hipGetErrorString(e)); return CA_EDEVICE; }
+    return CA_OK;
+}
+
 const char* ca_status_string(int status) {
     switch (status) {
     case CA_OK: return "ok";

@@ -46,6 +46,8 @@ def load() -> C.CDLL:
         "ca_abi_struct_sizes": ([p(i32), i32], C.c_int),
         "ca_device_count": ([p(i32)], C.c_int),
         "ca_status_string": ([C.c_int], C.c_char_p),
+        "ca_host_alloc": ([C.c_size_t, p(vp)], C.c_int),
+        "ca_host_free": ([vp], C.c_int),
         "ca_mirror_create": ([i32, p(vp)], C.c_int),
         "ca_mirror_destroy": ([vp], C.c_int),
         "ca_mirror_clear": ([vp], C.c_int),
@@ -69,6 +71,7 @@ def load() -> C.CDLL:
         "ca_estimate_plan_destroy": ([vp], C.c_int),
         "ca_estimate_plan_stats": ([vp, p(i32), p(C.c_float), p(C.c_float), p(C.c_float)], C.c_int),
         "ca_estimate_plan_chain_info": ([vp, p(i32), p(i32)], C.c_int),
+        "ca_estimate_plan_timings": ([vp, p(C.c_float), i32], C.c_int),
         "ca_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, p(i32), vp, vp], C.c_int),
         "ca_removal_stats": ([vp, p(i32), p(C.c_float), p(C.c_float)], C.c_int),
     }
@@ -87,12 +90,13 @@ def _check(status: int, what: str) -> None:
 
 def exported_symbols() -> list[str]:
     return [
-        "ca_abi_version", "ca_abi_struct_sizes", "ca_device_count", "ca_status_string", "ca_mirror_create",
+        "ca_abi_version", "ca_abi_struct_sizes", "ca_device_count", "ca_status_string", "ca_host_alloc",
+        "ca_host_free", "ca_mirror_create",
         "ca_mirror_destroy", "ca_mirror_clear", "ca_mirror_add_nodes", "ca_mirror_add_pods", "ca_mirror_remove_pod",
         "ca_mirror_fork", "ca_mirror_revert", "ca_mirror_commit", "ca_mirror_node_count", "ca_mirror_pod_node",
         "ca_mirror_node_pods", "ca_podset_create", "ca_podset_destroy", "ca_fits_any_node", "ca_check_predicates",
         "ca_fits_matrix", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
-        "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_find_nodes_to_remove",
+        "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_estimate_plan_timings", "ca_find_nodes_to_remove",
         "ca_removal_stats",
     ]
 
@@ -250,6 +254,25 @@ class Mirror:
         return {"rounds": r.value, "kernel_ms": k.value, "total_ms": t.value}
 
 
+class PinnedArray:
+    """A numpy array over ca_host_alloc (page-locked) memory."""
+
+    def __init__(self, lib, n: int, dtype):
+        self.lib = lib
+        dt = np.dtype(dtype)
+        p = C.c_void_p()
+        _check(lib.ca_host_alloc(max(n, 1) * dt.itemsize, C.byref(p)), "ca_host_alloc")
+        self.p = p
+        buf = (C.c_char * (max(n, 1) * dt.itemsize)).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=dt, count=n)
+
+    def close(self) -> None:
+        if self.p:
+            self.array = None
+            self.lib.ca_host_free(self.p)
+            self.p = None
+
+
 class EstimatePlan:
     """``ca_estimate_plan``: device-resident groups for repeated Estimate batches."""
 
@@ -271,32 +294,43 @@ class EstimatePlan:
             self.lib.ca_podset_destroy(s)
             raise CasimError(st, "ca_estimate_plan_create")
         self.h = p
-        self.sched_pod = np.full(max(self.total, 1), -1, np.int32)
-        self.sched_node = np.full(max(self.total, 1), -1, np.int32)
+        n = max(self.total, 1)
+        self._pinned = PinnedArray(self.lib, 2 * n, np.int32)     # sched_pod | sched_node
+        self.sched_pod = self._pinned.array[:n]
+        self.sched_node = self._pinned.array[n:]
         self.results = np.zeros(self.G, abi.ESTIMATE_RESULT_DTYPE)
 
-    def run(self, max_nodes: int, last_index: int = 0, want_nodes: bool = True) -> EstimateOutput:
+    def run(self, max_nodes: int, last_index: int = 0, want_nodes: bool = True, copy: bool = True) -> EstimateOutput:
+        """One Estimate batch.  With copy=False the returned arrays are views of the plan's
+        page-locked result buffers, overwritten by the next run."""
         lim = abi.LimiterC(max_nodes, 0)
         li = C.c_int32(last_index)
         _check(self.lib.ca_estimate_plan_run(self.h, C.byref(lim), C.byref(li), ptr(self.results),
                                              ptr(self.sched_pod), ptr(self.sched_node) if want_nodes else None),
                "ca_estimate_plan_run")
-        return EstimateOutput(self.results.copy(), self.sched_pod[: self.total].copy(),
-                              self.sched_node[: self.total].copy(), li.value)
+        f = (lambda a: a.copy()) if copy else (lambda a: a)
+        return EstimateOutput(f(self.results), f(self.sched_pod[: self.total]), f(self.sched_node[: self.total]),
+                              li.value)
 
     def stats(self) -> dict:
         r, a, b, c = C.c_int32(0), C.c_float(0), C.c_float(0), C.c_float(0)
         self.lib.ca_estimate_plan_stats(self.h, C.byref(r), C.byref(a), C.byref(b), C.byref(c))
         sens, succ = C.c_int32(0), C.c_int32(0)
         self.lib.ca_estimate_plan_chain_info(self.h, C.byref(sens), C.byref(succ))
+        t = (C.c_float * 7)()
+        self.lib.ca_estimate_plan_timings(self.h, t, 7)
+        names = ("score_ms", "merge_ms", "emit_ms", "chain_ms", "compact_ms", "d2h_ms", "host_ms")
         return {"rounds": r.value, "chain_ms": a.value, "sort_ms": b.value, "total_ms": c.value,
-                "lin_sensitive": sens.value, "had_success": succ.value}
+                "lin_sensitive": sens.value, "had_success": succ.value,
+                "phases": {k: float(v) for k, v in zip(names, t)}}
 
     def close(self) -> None:
         if self.h:
             self.lib.ca_estimate_plan_destroy(self.h)
             self.lib.ca_podset_destroy(self.podset)
             self.h = None
+            self.sched_pod = self.sched_node = None
+            self._pinned.close()
 
     def __enter__(self):
         return self

@@ -34,6 +34,16 @@ METRIC = "pod×node predicate evals/sec; Estimate() latency, 50k pods × 100 nod
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E (MI355X_MICROARCH.md, chip table)
 BYTES_PER_EVAL = 64              # node record read per resource-only evaluation
 
+# Algorithmic HBM bytes per (pod, group) item of each Estimate phase:
+#   score   pod_idx 4 + PodHot 32 + score sums 16 + SortItem write 16
+#   merge   per pass: SortItem read 16 + write 16
+#   emit    SortItem 16 + pod_idx 4 + PodHot 32 + StreamPod write 32 + head bit
+#   chain   StreamPod read 32 + assign write 4
+#   compact assign read 2x4 + pod id 4 + sched_pod/sched_node writes 8
+PHASE_BYTES = {"score_ms": 68.0, "merge_ms": 32.0, "emit_ms": 84.125, "chain_ms": 36.0, "compact_ms": 20.0}
+PHASE_KERNEL = {"score_ms": "k_score_tiles", "merge_ms": "k_merge_runs", "emit_ms": "k_emit_stream",
+                "chain_ms": "k_ffd_chain", "compact_ms": "k_tile_count+k_tile_scatter"}
+
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -85,7 +95,7 @@ def main():
 
     def step():
         """One batch on this rank + the lastIndex chain across ranks."""
-        out = plan.run(w.max_nodes, L0)
+        out = plan.run(w.max_nodes, L0, copy=False)
         st = plan.stats()
         if dist is None:
             return out, st, 0
@@ -108,7 +118,7 @@ def main():
                 return out, st, extra
             if rerun == rank:                       # exact input for the first stale shard
                 lin = cur
-                out = plan.run(w.max_nodes, lin)
+                out = plan.run(w.max_nodes, lin, copy=False)
                 st = plan.stats()
                 extra += 1
 
@@ -122,12 +132,16 @@ def main():
     chain_ms = []
     sort_ms = []
     rounds = []
+    phases = []
     for _ in range(args.steps):
         out, st, extra = step()
         evals += int(out.results["evals"].sum())
         chain_ms.append(st["chain_ms"] / max(st["rounds"], 1))
         sort_ms.append(st["sort_ms"])
         rounds.append(st["rounds"] + extra)
+        ph = dict(st["phases"])
+        ph["chain_ms"] = ph["chain_ms"] / max(st["rounds"], 1)       # one launch
+        phases.append(ph)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -143,8 +157,18 @@ def main():
     else:
         total_evals = evals
     evals_per_step = evals / args.steps                         # this rank's batch
-    kernel_ms = float(np.mean(chain_ms))
-    achieved = BYTES_PER_EVAL * evals_per_step / (kernel_ms / 1e3) / 1e9
+    items = int(w.group_off[-1])                                # (pod, group) items per batch
+    n_merge = 0
+    width = 1024
+    while width < int(np.diff(w.group_off).max()):
+        n_merge += 1
+        width *= 2
+    ph_mean = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
+    # dominant kernel of the step (longest device phase), with its algorithmic bytes
+    dom = max(PHASE_BYTES, key=lambda k: ph_mean[k])
+    per_item = PHASE_BYTES[dom] * (n_merge if dom == "merge_ms" else 1)
+    kernel_ms = ph_mean[dom]
+    achieved = per_item * items / (kernel_ms / 1e3) / 1e9
 
     result = None
     if rank == 0:
@@ -188,14 +212,18 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                "kernel": "k_ffd_chain", "kernel_ms": kernel_ms,
-                "bytes_per_unit": BYTES_PER_EVAL, "units_per_launch": evals_per_step,
+                "kernel": PHASE_KERNEL[dom], "kernel_ms": kernel_ms,
+                "bytes_per_unit": per_item, "unit_of_work": "(pod, node group) item",
+                "units_per_launch": items,
             },
             "cpu_baseline": cpu,
             "extra": {
                 "estimate_latency_ms": ms,
                 "sort_ms": float(np.mean(sort_ms)),
-                "chain_kernel_ms": kernel_ms,
+                "phases_ms": ph_mean,
+                "chain_kernel_ms": ph_mean["chain_ms"],
+                "items_per_s": items * world * args.steps / elapsed,
+                "eval_equivalent_GBps": BYTES_PER_EVAL * evals_per_step / (ph_mean["chain_ms"] / 1e3) / 1e9,
                 "speculation_rounds": float(np.mean(rounds)),
                 "evals_per_step": total_evals / args.steps,
                 "speedup_vs_cpu_baseline": (total_evals / elapsed) / cpu["value"] if cpu else None,

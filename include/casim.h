@@ -40,6 +40,7 @@
 #ifndef CASIM_H
 #define CASIM_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -253,6 +254,11 @@ int ca_abi_version(void);
 int ca_abi_struct_sizes(int32_t* out, int32_t cap);
 int ca_device_count(int32_t* out);
 const char* ca_status_string(int status);
+/* Page-locked host memory for result buffers (sched_pod/sched_node/dest): results are
+ * DMA'd straight into it instead of through a pageable staging copy.  C memory, so a cgo
+ * caller may keep it across calls. */
+int ca_host_alloc(size_t bytes, void** out);
+int ca_host_free(void* p);
 
 /* ---- mirror: the SoA ClusterSnapshot data plane in HBM ---------------------- */
 int ca_mirror_create(int32_t device, ca_mirror** out);
@@ -321,6 +327,11 @@ int ca_estimate_plan_stats(const ca_estimate_plan* p, int32_t* rounds, float* ch
  * that ran the batch from a guessed lastIndex must re-run it from the true one), and
  * whether any FitsAnyNode call succeeded (if not, lastIndex passed through unchanged).
  * Used to chain batches sharded across GPUs. */
+/* Device time of each phase of the last run, in ms: [0] score+static predicates,
+ * [1] merge passes, [2] stream emission, [3] FFD chains (all speculation rounds),
+ * [4] result compaction, [5] D2H of the results; [6] host wall time of the call.
+ * Writes min(cap, 7) values; returns 7. */
+int ca_estimate_plan_timings(const ca_estimate_plan* p, float* out, int32_t cap);
 int ca_estimate_plan_chain_info(const ca_estimate_plan* p, int32_t* lin_sensitive, int32_t* had_success);
 
 /* ---- removal simulator ------------------------------------------------------- */

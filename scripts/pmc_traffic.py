@@ -1,0 +1,42 @@
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into per-kernel HBM bytes per
+launch (MI355X_MICROARCH.md, HBM section: FETCH_SIZE counts wide coalesced reads at half
+their bytes on gfx950, so it is doubled; WRITE_SIZE is exact for 16-B/lane stores)."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def load(root: str, counter: str) -> dict:
+    per = defaultdict(list)
+    for f in glob.glob(os.path.join(root, f"pmc_{counter}", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter:
+                continue
+            name = r["Kernel_Name"].split("(")[0]
+            per[(name, r.get("Dispatch_Id", r.get("Correlation_Id", "")))].append(float(r["Counter_Value"]))
+    out = defaultdict(list)
+    for (name, _), vals in per.items():
+        out[name].append(sum(vals))                 # sum over XCD/TCC instances of one dispatch
+    return out
+
+
+def main(root: str) -> None:
+    fetch = load(root, "FETCH_SIZE")
+    write = load(root, "WRITE_SIZE")
+    res = {}
+    for name in sorted(set(fetch) | set(write)):
+        f = fetch.get(name, [])
+        w = write.get(name, [])
+        fk = sum(f) / len(f) * 1024 * 2 if f else None     # KB -> bytes, x2 gfx950 read correction
+        wk = sum(w) / len(w) * 1024 if w else None
+        res[name] = {"launches": max(len(f), len(w)), "read_bytes_per_launch": fk, "write_bytes_per_launch": wk,
+                     "traffic_bytes_per_launch": (fk or 0) + (wk or 0)}
+    json.dump(res, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out")

@@ -162,13 +162,86 @@ def test_estimate_random(seed, oracle):
     assert o.last_index == g.last_index
 
 
+def _run_heavy_inputs(seed, n_groups=6):
+    """Pending pods drawn from a handful of shapes and repeated, so the sorted streams are
+    long runs of identical pods: the run-batched chain (closed-form revolutions, limiter
+    and empty-node skips inside a run) against the per-pod oracle."""
+    import copy
+    rng = random.Random(1000 + seed)
+    nodes = [rand_node(rng, f"e{i}") for i in range(rng.randint(0, 4))]
+    shapes = []
+    for s in range(rng.randint(1, 5)):
+        p = rand_pod(rng, f"shape{s}", small=rng.random() < 0.6)
+        p.node_name = ""
+        if p.affinity is not None:
+            for t in p.affinity.required_terms:
+                t.match_fields = []
+        if rng.random() < 0.7:
+            for c in p.containers:
+                c.ports = []
+        if rng.random() < 0.5:
+            p.affinity = None
+            p.node_selector = None
+        shapes.append(p)
+    pods = []
+    for s in shapes:
+        for r in range(rng.choice([1, 2, 7, 40, 150])):
+            q = copy.deepcopy(s)
+            q.name = f"{s.name}-{r}"
+            pods.append(q)
+    rng.shuffle(pods)
+    templates = []
+    for g in range(n_groups):
+        t = rand_node(rng, f"tmpl{g}", big=rng.random() < 0.5)
+        if rng.random() < 0.15:
+            t.allocatable["cpu"] = k8s_milli(rng.choice([100, 300]))     # template DS pods overcommit it
+        ds = [rand_pod(rng, f"ds{g}-{j}", small=True) for j in range(rng.randint(0, 2))]
+        for d in ds:
+            d.affinity = None
+            d.node_selector = None
+        templates.append((t, ds))
+    groups = [[p for p in pods if rng.random() < 0.8] for _ in range(n_groups)]
+    return rng, nodes, pods, templates, groups
+
+
+def k8s_milli(v):
+    from autoscaler_amd.k8s import Quantity
+    return Quantity.milli(v)
+
+
+@pytest.mark.parametrize("batch", ["1", "0"])
+@pytest.mark.parametrize("seed", range(24))
+def test_estimate_runs_random(seed, batch, oracle, monkeypatch):
+    monkeypatch.setenv("CASIM_RUN_BATCH", batch)
+    rng, nodes, pods, templates, groups = _run_heavy_inputs(seed)
+    table, node_recs, tm, off, pod_idx = _encode_estimate(nodes, pods, templates, groups)
+    max_nodes = rng.choice([0, 0, 1, 2, 5, 40])
+    L0 = rng.choice([0, 0, 1, 3, 7, 123])
+    outs = []
+    for b in (oracle.OracleState(), _mirror()):
+        b.clear()
+        if len(node_recs):
+            b.add_nodes(node_recs)
+        outs.append(b.estimate(table, off, pod_idx, tm, max_nodes, L0))
+    o, g = outs
+    assert np.array_equal(o.results, g.results), (seed, o.results, g.results)
+    for k in range(len(groups)):
+        n = int(o.results[k]["n_scheduled"])
+        a = off[k]
+        assert np.array_equal(o.sched_pod[a:a + n], g.sched_pod[a:a + n]), (seed, k)
+        assert np.array_equal(o.sched_node[a:a + n], g.sched_node[a:a + n]), (seed, k)
+    assert o.last_index == g.last_index
+
+
 @pytest.mark.parametrize("name,w", [
     ("C1", W.c1()),
     ("C2-small", W.c2(n_pods=4000, n_groups=12, n_existing=50)),
     ("C2-unlimited", W.c2(n_pods=1500, n_groups=8, n_existing=20, max_nodes=0)),
     ("C2-medium", W.c2(n_pods=20000, n_groups=20, n_existing=300)),
 ])
-def test_estimate_workloads(name, w, oracle):
+@pytest.mark.parametrize("batch", ["1", "0"])
+def test_estimate_workloads(name, w, batch, oracle, monkeypatch):
+    monkeypatch.setenv("CASIM_RUN_BATCH", batch)
     outs = []
     for b in (oracle.OracleState(), _mirror()):
         W.load_estimate(b, w)

@@ -200,6 +200,16 @@ struct DevBuf {
     template <class T> T* as() const { return static_cast<T*>(ptr); }
 };
 
+// A growable page-locked host buffer (DMA target for results / tables).
+struct HostBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    int reserve(size_t need);   // grows (content not preserved)
+    void release();
+    ~HostBuf() { release(); }
+    template <class T> T* as() const { return static_cast<T*>(ptr); }
+};
+
 // Convert int64 allowed pods - count into the int32 free-slot column.
 inline int32_t clamp_i32(int64_t v) {
     if (v > INT32_MAX) return INT32_MAX;

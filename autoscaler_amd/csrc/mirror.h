@@ -40,11 +40,20 @@ struct DevPodTable {
                const ca_selector_req* reqs, int32_t nr, const int32_t* names, int32_t nn, hipStream_t st);
 };
 
+// Per-mirror scratch of ca_find_nodes_to_remove, kept across calls (no per-call
+// hipMalloc); host staging is page-locked.
+struct SweepScratch {
+    DevBuf in, lin, need, dest, hset, out, todo, tab;
+    HostBuf h_in, h_tab, h_out, h_hset, h_dest, h_todo, h_lin;
+};
+
 struct Stats {
     int32_t rounds = 0;
     float kernel_ms = 0, sort_ms = 0, total_ms = 0;
     int32_t lin_sensitive = 0;    // batch output depends on the input lastIndex
     int32_t had_success = 0;      // some FitsAnyNode call of the batch succeeded
+    float exact_ms = 0;           // sweep: device time of the exact pass
+    float walk_ms = 0;            // sweep: host time up to the end of the exact pass
 };
 
 }  // namespace casim
@@ -81,6 +90,8 @@ struct ca_mirror {
     casim::DevBuf d_mask;                  // per-node match mask
     std::vector<uint8_t> h_scratch;
     casim::Stats sweep_stats;
+    casim::SweepScratch sw;
+    int64_t n_ext_pods = 0;                // pods stored with host ports / extended requests
 
     int sync_nodes();                      // push dirty rows to the device
     int sync_pods();                       // push new pod records to the device

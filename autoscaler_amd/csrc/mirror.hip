@@ -47,6 +47,23 @@ void DevBuf::release() {
     bytes = 0;
 }
 
+int HostBuf::reserve(size_t need) {
+    if (need <= bytes) return CA_OK;
+    release();
+    size_t sz = std::max<size_t>(need, 256);
+    if (hipHostMalloc(&ptr, sz, hipHostMallocDefault) != hipSuccess) {
+        ptr = nullptr; bytes = 0; set_last_error("hipHostMalloc failed"); return CA_EDEVICE;
+    }
+    bytes = sz;
+    return CA_OK;
+}
+
+void HostBuf::release() {
+    if (ptr) (void)hipHostFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+}
+
 int DevPodTable::upload(const ca_pod_spec* pods, int32_t n, const ca_selector_term* tms, int32_t nt,
                         const ca_selector_req* rqs, int32_t nr, const int32_t* nms, int32_t nn,
                         hipStream_t st) {
@@ -148,6 +165,7 @@ int32_t ca_mirror::store_pod(const ca_pod_table* t, int32_t idx, int32_t node) {
             pf_names.push_back(t->prefilter_names[row.spec.prefilter_first + k]);
         row.spec.prefilter_first = first;
     }
+    if (pod_dev_flags(row.spec) & (PF_PORTS | PF_SCALAR_REQ | PF_MOVED_SCALAR_REQ)) n_ext_pods++;
     pods.push_back(row);
     return (int32_t)pods.size() - 1;
 }
@@ -417,6 +435,7 @@ int ca_mirror_destroy(ca_mirror* m) {
 
 int ca_mirror_clear(ca_mirror* m) {
     if (!m) return CA_EINVAL;
+    m->n_ext_pods = 0;
     m->nodes.clear(); m->pods.clear(); m->terms.clear(); m->reqs.clear(); m->pf_names.clear();
     m->journal.clear(); m->depth = 0;
     m->dirty_rows.clear(); m->dirty_flag.clear();

@@ -42,6 +42,10 @@ struct OverlaySmem {
     int32_t node[OV_CAP];
     int32_t pods[OV_CAP];
     int64_t cpu[OV_CAP], mem[OV_CAP], eph[OV_CAP];
+};
+// port / extended-resource overlay columns: dynamic LDS, only when some pod of the
+// mirror has host ports or extended requests (keeps 4 KB of LDS per block otherwise)
+struct OverlayExt {
     uint64_t ports[OV_CAP][CA_PORT_WORDS];
     int64_t scalar[OV_CAP][CA_MAX_SCALAR];
 };
@@ -115,8 +119,10 @@ __global__ void __launch_bounds__(64) k_sweep(
     const ca_pod_spec* __restrict__ specs, const ca_selector_term* __restrict__ terms,
     const ca_selector_req* __restrict__ reqs, const int32_t* __restrict__ names, const int32_t* __restrict__ hints,
     const int32_t* __restrict__ lin_arr, const uint8_t* __restrict__ need, int32_t* __restrict__ out_dest,
-    int32_t* __restrict__ hint_set, SweepOut* __restrict__ outs) {
+    int32_t* __restrict__ hint_set, SweepOut* __restrict__ outs, int32_t use_ext) {
     __shared__ OverlaySmem ov;
+    extern __shared__ __attribute__((aligned(16))) unsigned char ovx_raw[];
+    OverlayExt& ox = *reinterpret_cast<OverlayExt*>(ovx_raw);
     const int c = blockIdx.x;
     if (!need[c]) return;
     const int lane = threadIdx.x;
@@ -150,6 +156,49 @@ __global__ void __launch_bounds__(64) k_sweep(
     int32_t my_id = -1, my_hint = -1, my_dest = -1, my_hset = -1;
     PodHot my_p = {};
 
+    const int32_t nb = (n + 63) >> 6;
+    // register block cache: raw hot row, base visibility, overlay delta per lane
+    int32_t ja = -1, jb = -1;
+    NodeHot Ah = {}, Bh = {};
+    bool Avis = false, Bvis = false;
+    int64_t Adc = 0, Adm = 0, Ade = 0, Bdc = 0, Bdm = 0, Bde = 0;
+    int32_t Adp = 0, Bdp = 0;
+    auto load_block = [&](int32_t j, NodeHot& h, bool& vis, int64_t& dc, int64_t& dmm, int64_t& de, int32_t& dp) {
+        const int32_t pos = j * 64 + lane;
+        const bool valid = pos < n;
+        h = NodeHot{};
+        uint8_t dm = 0;
+        if (valid) { h = hot[pos]; dm = dest_mask[pos]; }
+        dc = 0; dmm = 0; de = 0; dp = 0;
+        for (int32_t q0 = 0; q0 < npl; q0 += 64) {           // this candidate's placements in block j
+            const int32_t q = q0 + lane;
+            const int32_t d = q < npl ? ov.node[q] - j * 64 : -1;
+            uint64_t mm = __ballot(d >= 0 && d < 64);
+            while (mm) {
+                const int l = __builtin_ctzll(mm);
+                mm &= mm - 1;
+                const int32_t dl = __builtin_amdgcn_readlane(d, l);
+                const int32_t slot = q0 + l;
+                if (lane == dl) { dc = ov.cpu[slot]; dmm = ov.mem[slot]; de = ov.eph[slot]; dp = ov.pods[slot]; }
+            }
+        }
+        vis = valid & (pos != node) & (dm != 0);   // & !unschedulable: applied at use
+    };
+    // A = block of lastIndex, B = the next one (prefetched)
+    auto refill = [&]() {
+        const int32_t j = L >> 6;
+        if (j == ja) return;
+        if (j == jb) {
+            ja = jb; Ah = Bh; Avis = Bvis; Adc = Bdc; Adm = Bdm; Ade = Bde; Adp = Bdp;
+        } else {
+            ja = j;
+            load_block(ja, Ah, Avis, Adc, Adm, Ade, Adp);
+        }
+        jb = ja + 1 < nb ? ja + 1 : (nb > 1 ? 0 : -1);
+        if (jb == ja) jb = -1;
+        if (jb >= 0) load_block(jb, Bh, Bvis, Bdc, Bdm, Bde, Bdp);
+    };
+
     for (int32_t i = 0; i < mn; i++) {
         const int sl = i & 63;
         if (sl == 0) {
@@ -161,7 +210,7 @@ __global__ void __launch_bounds__(64) k_sweep(
             if (i + lane < mn) {
                 my_id = move_pods[mo + i + lane];
                 my_p = ph[my_id];
-                my_hint = hints[my_id];
+                my_hint = hints[mo + i + lane];
             }
         }
         __syncthreads();
@@ -178,6 +227,7 @@ __global__ void __launch_bounds__(64) k_sweep(
         const bool pre_fail = (p.flags & PF_PREFILTER_FAIL) != 0;
         int32_t target = -1;
 
+        if (n > 0) refill();
         // ---- findNodeWithHints (hinting_simulator.go:91-108) ----
         if (h >= 0 && h < n && !pre_fail) {
             evals++;
@@ -198,8 +248,10 @@ __global__ void __launch_bounds__(64) k_sweep(
                     if (ov.node[q] == h) {
                         nh.cpu = wsub(nh.cpu, ov.cpu[q]); nh.mem = wsub(nh.mem, ov.mem[q]);
                         nh.eph = wsub(nh.eph, ov.eph[q]); nh.pods -= ov.pods[q];
-                        for (int w = 0; w < CA_PORT_WORDS; w++) ne.ports[w] |= ov.ports[q][w];
-                        for (int k = 0; k < CA_MAX_SCALAR; k++) ne.scalar[k] = wsub(ne.scalar[k], ov.scalar[q][k]);
+                        if (use_ext) {
+                            for (int w = 0; w < CA_PORT_WORDS; w++) ne.ports[w] |= ox.ports[q][w];
+                            for (int k = 0; k < CA_MAX_SCALAR; k++) ne.scalar[k] = wsub(ne.scalar[k], ox.scalar[q][k]);
+                        }
                     }
                 }
             }
@@ -209,7 +261,10 @@ __global__ void __launch_bounds__(64) k_sweep(
             }
         }
         // ---- findNode -> FitsAnyNodeMatching(isCandidateNode) (:110-125) ----
-        if (target < 0 && !pre_fail) {
+        // slow path: pods with host ports / extended resources / PreFilter node names
+        // evaluate 64-node chunks straight from HBM with the overlay applied per chunk
+        const bool fast = !(p.flags & (PF_PORTS | PF_SCALAR_REQ | PF_PREFILTER_NAMES));
+        if (target < 0 && !pre_fail && !fast) {
             for (int32_t base = 0; base < n; base += 64) {
                 const int32_t off = base + lane;
                 int32_t pos = L + off;                                        // (lastIndex+i) % len
@@ -251,8 +306,11 @@ __global__ void __launch_bounds__(64) k_sweep(
                         if (ov_here) {
                             nh.cpu = wsub(nh.cpu, ov.cpu[ov_slot]); nh.mem = wsub(nh.mem, ov.mem[ov_slot]);
                             nh.eph = wsub(nh.eph, ov.eph[ov_slot]); nh.pods -= ov.pods[ov_slot];
-                            for (int w = 0; w < CA_PORT_WORDS; w++) ne.ports[w] |= ov.ports[ov_slot][w];
-                            for (int k = 0; k < CA_MAX_SCALAR; k++) ne.scalar[k] = wsub(ne.scalar[k], ov.scalar[ov_slot][k]);
+                            if (use_ext) {
+                                for (int w = 0; w < CA_PORT_WORDS; w++) ne.ports[w] |= ox.ports[ov_slot][w];
+                                for (int k = 0; k < CA_MAX_SCALAR; k++)
+                                    ne.scalar[k] = wsub(ne.scalar[k], ox.scalar[ov_slot][k]);
+                            }
                         }
                         fit = eval_node(s, p, psc, terms, reqs, nh, ne, st + pos, false);
                     }
@@ -265,6 +323,43 @@ __global__ void __launch_bounds__(64) k_sweep(
                     const int32_t foff = base + f;
                     target = L + foff;
                     if (target >= n) target -= n;
+                    L = target + 1;                                            // schedulerbased.go:131
+                    if (L >= n) L -= n;
+                    fa_success = true;
+                    if (lane == sl) my_hset = target;                          // :123
+                    break;
+                }
+                evals += (uint64_t)__popcll(vm);
+            }
+        }
+        // fast path: aligned 64-node blocks; the block holding lastIndex (A) and the next
+        // one (B) stay in registers with this candidate's overlay as per-lane deltas
+        if (target < 0 && !pre_fail && fast) {
+            const int32_t j0 = L >> 6, l0 = L & 63;
+            for (int32_t r = 0; r <= nb; r++) {
+                if (r == nb && l0 == 0) break;
+                int32_t j = j0 + r;
+                if (j >= nb) j -= nb;
+                NodeHot raw;
+                bool bvis;
+                int64_t dc, dmm, de;
+                int32_t dp;
+                if (j == ja) { raw = Ah; bvis = Avis; dc = Adc; dmm = Adm; de = Ade; dp = Adp; }
+                else if (j == jb) { raw = Bh; bvis = Bvis; dc = Bdc; dmm = Bdm; de = Bde; dp = Bdp; }
+                else load_block(j, raw, bvis, dc, dmm, de, dp);
+                const bool inr = (r == 0) ? lane >= l0 : (r == nb ? lane < l0 : true);
+                const bool vis = bvis & inr & !(raw.flags & NF_UNSCHED);
+                NodeHot eff = raw;
+                eff.cpu = wsub(raw.cpu, dc); eff.mem = wsub(raw.mem, dmm); eff.eph = wsub(raw.eph, de);
+                eff.pods = raw.pods - dp;
+                bool fit = vis && hot_fits(p, eff);
+                if (fit) fit = static_ok(s, p, terms, reqs, eff, st + (j * 64 + lane));
+                const uint64_t fm = __ballot(fit), vm = __ballot(vis);
+                if (fm) {
+                    const int f = __builtin_ctzll(fm);
+                    const uint64_t below = (f == 63) ? ~0ull : ((2ull << f) - 1);
+                    evals += (uint64_t)__popcll(vm & below);
+                    target = j * 64 + f;
                     L = target + 1;                                            // schedulerbased.go:131
                     if (L >= n) L -= n;
                     fa_success = true;
@@ -287,8 +382,10 @@ __global__ void __launch_bounds__(64) k_sweep(
             slot = npl++;
             if (lane == 0) {
                 ov.node[slot] = target; ov.pods[slot] = 0; ov.cpu[slot] = 0; ov.mem[slot] = 0; ov.eph[slot] = 0;
-                for (int w = 0; w < CA_PORT_WORDS; w++) ov.ports[slot][w] = 0;
-                for (int k = 0; k < CA_MAX_SCALAR; k++) ov.scalar[slot][k] = 0;
+                if (use_ext) {
+                    for (int w = 0; w < CA_PORT_WORDS; w++) ox.ports[slot][w] = 0;
+                    for (int k = 0; k < CA_MAX_SCALAR; k++) ox.scalar[slot][k] = 0;
+                }
             }
         }
         if (lane == 0) {
@@ -296,8 +393,14 @@ __global__ void __launch_bounds__(64) k_sweep(
             ov.mem[slot] = wadd(ov.mem[slot], p.mem);
             ov.eph[slot] = wadd(ov.eph[slot], p.eph);
             ov.pods[slot] += 1;
-            for (int w = 0; w < CA_PORT_WORDS; w++) ov.ports[slot][w] |= s.port_use[w];
-            for (int k = 0; k < CA_MAX_SCALAR; k++) ov.scalar[slot][k] = wadd(ov.scalar[slot][k], psc[k]);
+            if (use_ext) {
+                for (int w = 0; w < CA_PORT_WORDS; w++) ox.ports[slot][w] |= s.port_use[w];
+                for (int k = 0; k < CA_MAX_SCALAR; k++) ox.scalar[slot][k] = wadd(ox.scalar[slot][k], psc[k]);
+            }
+        }
+        if (lane == (target & 63)) {
+            if ((target >> 6) == ja) { Adc = wadd(Adc, p.cpu); Adm = wadd(Adm, p.mem); Ade = wadd(Ade, p.eph); Adp += 1; }
+            if ((target >> 6) == jb) { Bdc = wadd(Bdc, p.cpu); Bdm = wadd(Bdm, p.mem); Bde = wadd(Bde, p.eph); Bdp += 1; }
         }
         if (lane == sl) my_dest = target;
         placed++;
@@ -348,7 +451,7 @@ __global__ void __launch_bounds__(64) k_sweep_table(
     for (int32_t i = lane; i < mn; i += 64) {
         const int32_t id = move_pods[mo + i];
         const uint32_t f = moved_flags(ph[id].flags);
-        if ((hints[id] >= 0) | ((f & (PF_PORTS | PF_SCALAR_REQ)) != 0)) unknown = true;
+        if ((hints[mo + i] >= 0) | ((f & (PF_PORTS | PF_SCALAR_REQ)) != 0)) unknown = true;
     }
     unknown = __ballot(unknown) != 0;
     if (!unknown) {
@@ -404,16 +507,27 @@ inline int32_t wrap(int64_t v, int32_t n) {
     return (int32_t)r;
 }
 
-int launch_exact(ca_mirror* m, hipStream_t st, int32_t C, int32_t n, DevBuf& d_mask, DevBuf& d_c, DevBuf& d_status,
-                 DevBuf& d_off, DevBuf& d_moves, DevBuf& d_hints, DevBuf& d_lin, DevBuf& d_need, DevBuf& d_dest,
+// a typed view into the packed input buffer
+struct DevView {
+    void* ptr;
+    template <class T> T* as() const { return static_cast<T*>(ptr); }
+};
+
+int launch_exact(ca_mirror* m, hipStream_t st, int32_t C, int32_t n, DevView d_mask, DevView d_c, DevView d_status,
+                 DevView d_off, DevView d_moves, DevView d_hints, DevBuf& d_lin, DevBuf& d_need, DevBuf& d_dest,
                  DevBuf& d_hset, DevBuf& d_out) {
-    hipLaunchKernelGGL(k_sweep, dim3(C), dim3(64), 0, st, m->d_hot.as<NodeHot>(), m->d_ext.as<NodeExt>(),
+    const bool use_ext = m->n_ext_pods > 0;
+    const size_t dyn = use_ext ? sizeof(OverlayExt) : 0;
+    if (use_ext)
+        CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_sweep, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+    hipLaunchKernelGGL(k_sweep, dim3(C), dim3(64), dyn, st, m->d_hot.as<NodeHot>(), m->d_ext.as<NodeExt>(),
                        m->d_static.as<NodeStatic>(), n, d_mask.as<uint8_t>(), d_c.as<int32_t>(),
                        d_status.as<int32_t>(), d_off.as<int32_t>(), d_moves.as<int32_t>(),
                        m->d_pods.hot.as<PodHot>(), m->d_pods.spec.as<ca_pod_spec>(),
                        m->d_pods.terms.as<ca_selector_term>(), m->d_pods.reqs.as<ca_selector_req>(),
                        m->d_pods.names.as<int32_t>(), d_hints.as<int32_t>(), d_lin.as<int32_t>(),
-                       d_need.as<uint8_t>(), d_dest.as<int32_t>(), d_hset.as<int32_t>(), d_out.as<SweepOut>());
+                       d_need.as<uint8_t>(), d_dest.as<int32_t>(), d_hset.as<int32_t>(), d_out.as<SweepOut>(),
+                       use_ext ? 1 : 0);
     CA_HIP_CHECK(hipGetLastError());
     return CA_OK;
 }
@@ -428,17 +542,23 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     if (!m || (C > 0 && (!candidates || !dest_mask || !move_off || !results || !out_dest)) || !last_index || C < 0)
         return CA_EINVAL;
     const auto t_start = std::chrono::steady_clock::now();
+    const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
+    auto tmark = [&](const char* what) {
+        if (dbg_t)
+            fprintf(stderr, "[sweep] %-14s %8.3f ms\n", what,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
+    };
     CA_HIP_CHECK(hipSetDevice(m->device));
     hipStream_t st = m->stream;
     const int32_t n = (int32_t)m->nodes.size();
     if (C == 0) return CA_OK;
     const int32_t M = move_off[C] - move_off[0];
     if (move_off[0] != 0 || M < 0) return CA_EINVAL;
-    for (int32_t c = 0; c < C; c++) {
-        for (int32_t i = move_off[c]; i < move_off[c + 1]; i++) {
-            const int32_t id = move_pods[i];
-            if (id < 0 || (size_t)id >= m->pods.size()) return CA_EINVAL;
-        }
+    for (int32_t c = 0; c < C; c++)
+        if (move_off[c + 1] < move_off[c]) return CA_EINVAL;
+    for (int32_t i = 0; i < M; i++) {
+        const int32_t id = move_pods[i];
+        if (id < 0 || (size_t)id >= m->pods.size()) return CA_EINVAL;
     }
     // duplicate candidates share hints between their simulations: run them in
     // separate sequential segments (Hints.Set of one is seen by the next).
@@ -461,13 +581,13 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
         }
     }
     int rc;
+    tmark("validate");
     if ((rc = m->sync_nodes()) != CA_OK) return rc;
     if ((rc = m->sync_pods()) != CA_OK) return rc;
-    std::vector<int32_t> status((size_t)C, 0);
-    if (cand_status) std::copy(cand_status, cand_status + C, status.begin());
-    const size_t hint_n = std::max<size_t>(m->pods.size(), 1);
-    std::vector<int32_t> h_hints(hint_n, -1);
-    if (hints) std::copy(hints, hints + m->pods.size(), h_hints.begin());
+    tmark("sync");
+    const int32_t* status = cand_status;
+    std::vector<int32_t> zero_status;
+    if (!status) { zero_status.assign((size_t)C, 0); status = zero_status.data(); }
 
     // candidates whose simulation can move lastIndex: valid, not blocked, pods to move
     std::vector<int32_t> sens;
@@ -479,28 +599,44 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     }
     const int32_t S = (int32_t)sens.size();
 
-    DevBuf d_c, d_status, d_off, d_moves, d_hints, d_lin, d_need, d_dest, d_hset, d_out, d_mask, d_todo, d_ws, d_tab;
-    if ((rc = d_c.reserve(sizeof(int32_t) * C)) != CA_OK) return rc;
-    if ((rc = d_status.reserve(sizeof(int32_t) * C)) != CA_OK) return rc;
-    if ((rc = d_off.reserve(sizeof(int32_t) * (C + 1))) != CA_OK) return rc;
-    if ((rc = d_moves.reserve(sizeof(int32_t) * std::max(M, 1))) != CA_OK) return rc;
-    if ((rc = d_hints.reserve(sizeof(int32_t) * hint_n)) != CA_OK) return rc;
+    SweepScratch& sw = m->sw;
+    DevBuf &d_in = sw.in, &d_lin = sw.lin, &d_need = sw.need, &d_dest = sw.dest, &d_hset = sw.hset,
+           &d_out = sw.out, &d_todo = sw.todo, &d_tab = sw.tab;
+    // one page-locked staging area and one H2D copy for every per-call input:
+    // [cand C][status C][move_off C+1][move_pods M][hint per moved pod M][dest mask n bytes]
+    const size_t in_ints = (size_t)C * 3 + 1 + (size_t)M * 2;
+    const size_t in_bytes = sizeof(int32_t) * in_ints + (size_t)std::max(n, 1);
+    if ((rc = sw.h_in.reserve(in_bytes)) != CA_OK) return rc;
+    if ((rc = d_in.reserve(in_bytes)) != CA_OK) return rc;
+    if ((rc = sw.h_tab.reserve(sizeof(int32_t) * 64 * (size_t)std::max(S, 1))) != CA_OK) return rc;
+    if ((rc = sw.h_out.reserve(sizeof(SweepOut) * (size_t)C)) != CA_OK) return rc;
+    if ((rc = sw.h_hset.reserve(sizeof(int32_t) * (size_t)std::max(M, 1))) != CA_OK) return rc;
+    if ((rc = sw.h_dest.reserve(sizeof(int32_t) * (size_t)std::max(M, 1))) != CA_OK) return rc;
+    if ((rc = sw.h_todo.reserve(sizeof(int32_t) * 2 * (size_t)std::max(S, 1))) != CA_OK) return rc;
+    if ((rc = sw.h_lin.reserve((sizeof(int32_t) + 1) * (size_t)C)) != CA_OK) return rc;
     if ((rc = d_lin.reserve(sizeof(int32_t) * C)) != CA_OK) return rc;
     if ((rc = d_need.reserve((size_t)C)) != CA_OK) return rc;
     if ((rc = d_dest.reserve(sizeof(int32_t) * std::max(M, 1))) != CA_OK) return rc;
     if ((rc = d_hset.reserve(sizeof(int32_t) * std::max(M, 1))) != CA_OK) return rc;
     if ((rc = d_out.reserve(sizeof(SweepOut) * C)) != CA_OK) return rc;
-    if ((rc = d_mask.reserve((size_t)std::max(n, 1))) != CA_OK) return rc;
-    if ((rc = d_todo.reserve(sizeof(int32_t) * std::max(S, 1))) != CA_OK) return rc;
-    if ((rc = d_ws.reserve(sizeof(int32_t) * std::max(S, 1))) != CA_OK) return rc;
+    if ((rc = d_todo.reserve(sizeof(int32_t) * 2 * std::max(S, 1))) != CA_OK) return rc;
     if ((rc = d_tab.reserve(sizeof(int32_t) * 64 * (size_t)std::max(S, 1))) != CA_OK) return rc;
-    CA_HIP_CHECK(hipMemcpyAsync(d_c.ptr, candidates, sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
-    CA_HIP_CHECK(hipMemcpyAsync(d_status.ptr, status.data(), sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
-    CA_HIP_CHECK(hipMemcpyAsync(d_off.ptr, move_off, sizeof(int32_t) * (C + 1), hipMemcpyHostToDevice, st));
-    if (M) CA_HIP_CHECK(hipMemcpyAsync(d_moves.ptr, move_pods, sizeof(int32_t) * M, hipMemcpyHostToDevice, st));
-    CA_HIP_CHECK(hipMemcpyAsync(d_hints.ptr, h_hints.data(), sizeof(int32_t) * hint_n, hipMemcpyHostToDevice, st));
-    if (n) CA_HIP_CHECK(hipMemcpyAsync(d_mask.ptr, dest_mask, (size_t)n, hipMemcpyHostToDevice, st));
-
+    int32_t* hin = sw.h_in.as<int32_t>();
+    std::memcpy(hin, candidates, sizeof(int32_t) * C);
+    std::memcpy(hin + C, status, sizeof(int32_t) * C);
+    std::memcpy(hin + 2 * C, move_off, sizeof(int32_t) * (C + 1));
+    if (M) std::memcpy(hin + 3 * C + 1, move_pods, sizeof(int32_t) * M);
+    int32_t* hh = hin + 3 * C + 1 + M;
+    if (hints) for (int32_t i = 0; i < M; i++) hh[i] = hints[move_pods[i]];
+    else std::fill(hh, hh + M, -1);
+    std::memcpy(reinterpret_cast<uint8_t*>(hin + in_ints), dest_mask, (size_t)n);
+    CA_HIP_CHECK(hipMemcpyAsync(d_in.ptr, sw.h_in.ptr, in_bytes, hipMemcpyHostToDevice, st));
+    int32_t* const dptr = d_in.as<int32_t>();
+    DevView d_c{dptr}, d_status{dptr + C}, d_off{dptr + 2 * C}, d_moves{dptr + 3 * C + 1},
+        d_hints{dptr + 3 * C + 1 + M}, d_mask{dptr + in_ints};
+    int32_t* h_lin = sw.h_lin.as<int32_t>();
+    uint8_t* h_need = reinterpret_cast<uint8_t*>(h_lin + C);
+    tmark("upload");
     // ---- 1. every candidate's input lastIndex ----
     std::vector<int32_t> exact_lin((size_t)C, 0), exact_lout((size_t)C, 0);
     std::vector<int32_t> ws((size_t)S, 0);          // window start per sensitive candidate
@@ -528,27 +664,31 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
         if (!todo.empty()) {
             rounds++;
             const int32_t T = (int32_t)todo.size();
-            CA_HIP_CHECK(hipMemcpyAsync(d_todo.ptr, todo.data(), sizeof(int32_t) * T, hipMemcpyHostToDevice, st));
-            CA_HIP_CHECK(hipMemcpyAsync(d_ws.ptr, todo_ws.data(), sizeof(int32_t) * T, hipMemcpyHostToDevice, st));
+            int32_t* ht = sw.h_todo.as<int32_t>();
+            std::memcpy(ht, todo.data(), sizeof(int32_t) * T);
+            std::memcpy(ht + T, todo_ws.data(), sizeof(int32_t) * T);
+            CA_HIP_CHECK(hipMemcpyAsync(d_todo.ptr, ht, sizeof(int32_t) * 2 * T, hipMemcpyHostToDevice, st));
             CA_HIP_CHECK(hipEventRecord(m->ev0, st));
             hipLaunchKernelGGL(k_sweep_table, dim3(T), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
                                m->d_static.as<NodeStatic>(), n, d_mask.as<uint8_t>(), d_c.as<int32_t>(),
                                d_off.as<int32_t>(), d_moves.as<int32_t>(), m->d_pods.hot.as<PodHot>(),
                                m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
                                m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
-                               d_hints.as<int32_t>(), d_todo.as<int32_t>(), d_ws.as<int32_t>(), d_tab.as<int32_t>());
+                               d_hints.as<int32_t>(), d_todo.as<int32_t>(), d_todo.as<int32_t>() + T, d_tab.as<int32_t>());
             CA_HIP_CHECK(hipGetLastError());
             CA_HIP_CHECK(hipEventRecord(m->ev1, st));
-            std::vector<int32_t> rows((size_t)T * 64);
-            CA_HIP_CHECK(hipMemcpyAsync(rows.data(), d_tab.ptr, sizeof(int32_t) * 64 * T, hipMemcpyDeviceToHost, st));
+            const int32_t* rows = sw.h_tab.as<int32_t>();
+            CA_HIP_CHECK(hipMemcpyAsync(sw.h_tab.ptr, d_tab.ptr, sizeof(int32_t) * 64 * T, hipMemcpyDeviceToHost, st));
             CA_HIP_CHECK(hipStreamSynchronize(st));
             float ms = 0;
             (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
             kms += ms;
+            if (dbg_t) fprintf(stderr, "[sweep] table round %d: %d rows, kernel %.3f ms\n", rounds, T, ms);
+            tmark("table");
             int32_t ti = 0;
             for (int32_t k = k0; k < S; k++) {
                 if (have[k]) continue;
-                std::copy(rows.begin() + (size_t)ti * 64, rows.begin() + (size_t)ti * 64 + 64, tab.begin() + (size_t)k * 64);
+                std::copy(rows + (size_t)ti * 64, rows + (size_t)ti * 64 + 64, tab.begin() + (size_t)k * 64);
                 have[k] = 1;
                 ti++;
             }
@@ -563,8 +703,10 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
                 // hints / ports / long scans: exact kernel at the exact lastIndex
                 need1[c] = 1;
                 lin1[c] = (int32_t)cur;
-                CA_HIP_CHECK(hipMemcpyAsync(d_lin.ptr, lin1.data(), sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
-                CA_HIP_CHECK(hipMemcpyAsync(d_need.ptr, need1.data(), (size_t)C, hipMemcpyHostToDevice, st));
+                std::memcpy(h_lin, lin1.data(), sizeof(int32_t) * C);
+                std::memcpy(h_need, need1.data(), (size_t)C);
+                CA_HIP_CHECK(hipMemcpyAsync(d_lin.ptr, h_lin, sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
+                CA_HIP_CHECK(hipMemcpyAsync(d_need.ptr, h_need, (size_t)C, hipMemcpyHostToDevice, st));
                 if ((rc = launch_exact(m, st, C, n, d_mask, d_c, d_status, d_off, d_moves, d_hints, d_lin, d_need,
                                        d_dest, d_hset, d_out)) != CA_OK)
                     return rc;
@@ -587,10 +729,10 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
             const int32_t v = w < 64 ? tab[(size_t)k * 64 + w] : TB_UNKNOWN;
             if (w < 64 && v != TB_UNKNOWN) { est = v; continue; }
             int64_t next = est + (move_off[sens[k] + 1] - move_off[sens[k]]);
-            int best = -1;
-            for (int q = 0; q < 64; q++) {
-                if (tab[(size_t)k * 64 + q] == TB_UNKNOWN) continue;
-                if (best < 0 || std::abs(q - 32) < std::abs(best - 32)) best = q;
+            int best = -1;              // known entry nearest the window centre
+            for (int d = 0; d <= 32 && best < 0; d++) {
+                if (32 - d >= 0 && tab[(size_t)k * 64 + 32 - d] != TB_UNKNOWN) best = 32 - d;
+                else if (32 + d < 64 && tab[(size_t)k * 64 + 32 + d] != TB_UNKNOWN) best = 32 + d;
             }
             if (best >= 0) {
                 const int64_t from = (int64_t)ws[k] + best;
@@ -613,23 +755,29 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
             exact_lin[c] = (int32_t)run;
         }
     }
+    tmark("walk");
+    if (dbg_t) fprintf(stderr, "[sweep] exact fallbacks %d\n", exact_runs);
     // ---- 2. exact pass at the exact lastIndex: every output ----
-    std::vector<uint8_t> need((size_t)C, 1);
-    CA_HIP_CHECK(hipMemcpyAsync(d_lin.ptr, exact_lin.data(), sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
-    CA_HIP_CHECK(hipMemcpyAsync(d_need.ptr, need.data(), (size_t)C, hipMemcpyHostToDevice, st));
+    std::memcpy(h_lin, exact_lin.data(), sizeof(int32_t) * C);
+    std::memset(h_need, 1, (size_t)C);
+    CA_HIP_CHECK(hipMemcpyAsync(d_lin.ptr, h_lin, sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
+    CA_HIP_CHECK(hipMemcpyAsync(d_need.ptr, h_need, (size_t)C, hipMemcpyHostToDevice, st));
     CA_HIP_CHECK(hipEventRecord(m->ev0, st));
     if ((rc = launch_exact(m, st, C, n, d_mask, d_c, d_status, d_off, d_moves, d_hints, d_lin, d_need, d_dest, d_hset,
                            d_out)) != CA_OK)
         return rc;
     CA_HIP_CHECK(hipEventRecord(m->ev1, st));
-    std::vector<SweepOut> outs((size_t)C);
-    std::vector<int32_t> hset((size_t)std::max(M, 1));
-    CA_HIP_CHECK(hipMemcpyAsync(outs.data(), d_out.ptr, sizeof(SweepOut) * C, hipMemcpyDeviceToHost, st));
+    const SweepOut* outs = sw.h_out.as<SweepOut>();
+    const int32_t* hset = sw.h_hset.as<int32_t>();
+    CA_HIP_CHECK(hipMemcpyAsync(sw.h_out.ptr, d_out.ptr, sizeof(SweepOut) * C, hipMemcpyDeviceToHost, st));
     if (M) {
-        CA_HIP_CHECK(hipMemcpyAsync(out_dest, d_dest.ptr, sizeof(int32_t) * M, hipMemcpyDeviceToHost, st));
-        CA_HIP_CHECK(hipMemcpyAsync(hset.data(), d_hset.ptr, sizeof(int32_t) * M, hipMemcpyDeviceToHost, st));
+        CA_HIP_CHECK(hipMemcpyAsync(sw.h_dest.ptr, d_dest.ptr, sizeof(int32_t) * M, hipMemcpyDeviceToHost, st));
+        CA_HIP_CHECK(hipMemcpyAsync(sw.h_hset.ptr, d_hset.ptr, sizeof(int32_t) * M, hipMemcpyDeviceToHost, st));
     }
     CA_HIP_CHECK(hipStreamSynchronize(st));
+    const auto t_exact = std::chrono::steady_clock::now();
+    tmark("exact");
+    if (M) std::memcpy(out_dest, sw.h_dest.ptr, sizeof(int32_t) * M);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
     kms += ms;
@@ -668,11 +816,22 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     if (hints) {
         for (int32_t i = 0; i < M; i++) if (hset[i] >= 0) hints[move_pods[i]] = hset[i];
     }
+    tmark("done");
     m->sweep_stats.rounds = rounds + exact_runs + 1;
+    m->sweep_stats.exact_ms = ms;
+    m->sweep_stats.walk_ms = std::chrono::duration<float, std::milli>(t_exact - t_start).count();
     m->sweep_stats.kernel_ms = kms;
     m->sweep_stats.total_ms =
         std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     return CA_OK;
+}
+
+int ca_removal_timings(const ca_mirror* m, float* out, int32_t cap) {
+    if (!m || (cap > 0 && !out)) return CA_EINVAL;
+    const float t[4] = {m->sweep_stats.kernel_ms, m->sweep_stats.exact_ms, m->sweep_stats.walk_ms,
+                        m->sweep_stats.total_ms};
+    for (int32_t i = 0; i < 4 && i < cap; i++) out[i] = t[i];
+    return 4;
 }
 
 int ca_removal_stats(const ca_mirror* m, int32_t* rounds, float* kernel_ms, float* total_ms) {

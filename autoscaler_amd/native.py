@@ -74,6 +74,7 @@ def load() -> C.CDLL:
         "ca_estimate_plan_timings": ([vp, p(C.c_float), i32], C.c_int),
         "ca_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, p(i32), vp, vp], C.c_int),
         "ca_removal_stats": ([vp, p(i32), p(C.c_float), p(C.c_float)], C.c_int),
+        "ca_removal_timings": ([vp, p(C.c_float), i32], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(lib, name)
@@ -97,7 +98,7 @@ def exported_symbols() -> list[str]:
         "ca_mirror_node_pods", "ca_podset_create", "ca_podset_destroy", "ca_fits_any_node", "ca_check_predicates",
         "ca_fits_matrix", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
         "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_estimate_plan_timings", "ca_find_nodes_to_remove",
-        "ca_removal_stats",
+        "ca_removal_stats", "ca_removal_timings",
     ]
 
 
@@ -251,7 +252,10 @@ class Mirror:
     def removal_stats(self) -> dict:
         r, k, t = C.c_int32(0), C.c_float(0), C.c_float(0)
         self.lib.ca_removal_stats(self.h, C.byref(r), C.byref(k), C.byref(t))
-        return {"rounds": r.value, "kernel_ms": k.value, "total_ms": t.value}
+        tm = (C.c_float * 4)()
+        self.lib.ca_removal_timings(self.h, tm, 4)
+        return {"rounds": r.value, "kernel_ms": k.value, "total_ms": t.value, "exact_ms": float(tm[1]),
+                "walk_ms": float(tm[2])}
 
 
 class PinnedArray:

@@ -82,7 +82,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")           # RCCL on ROCm
 
-    from autoscaler_amd import native
+    from autoscaler_amd import native, shard
     from autoscaler_amd import workloads as W
 
     # rank r owns node groups [100 r, 100 r + 100) of the job (seeded per rank)
@@ -93,34 +93,20 @@ def main():
     plan = native.EstimatePlan(mirror, w.table, w.group_off, w.pod_idx, w.templates)
     L0 = 0
 
-    def step():
-        """One batch on this rank + the lastIndex chain across ranks."""
-        out = plan.run(w.max_nodes, L0, copy=False)
+    def run_block(lin):
+        out = plan.run(w.max_nodes, lin, copy=False)
         st = plan.stats()
+        return (out, st), out.last_index, st["lin_sensitive"], st["had_success"]
+
+    gather = shard.torch_all_gather(dist, f"cuda:{local}") if dist is not None else None
+
+    def step():
+        """One batch on this rank + the lastIndex chain across ranks (autoscaler_amd/shard.py)."""
         if dist is None:
+            (out, st), _, _, _ = run_block(L0)
             return out, st, 0
-        lin = L0
-        extra = 0
-        while True:
-            rec = torch.tensor([lin, out.last_index, st["lin_sensitive"], st["had_success"]], dtype=torch.int64,
-                               device=f"cuda:{local}")
-            gathered = [torch.empty_like(rec) for _ in range(world)]
-            dist.all_gather(gathered, rec)
-            recs = torch.stack(gathered).cpu().tolist()
-            cur = L0
-            rerun = -1
-            for r, (l_in, l_out, sens, succ) in enumerate(recs):
-                if l_in != cur and sens:
-                    rerun = r
-                    break
-                cur = l_out if succ else cur
-            if rerun < 0:
-                return out, st, extra
-            if rerun == rank:                       # exact input for the first stale shard
-                lin = cur
-                out = plan.run(w.max_nodes, lin, copy=False)
-                st = plan.stats()
-                extra += 1
+        (out, st), _, extra = shard.run_sharded(run_block, L0, gather, rank)
+        return out, st, extra
 
     for _ in range(args.warmup):
         step()

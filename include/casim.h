@@ -346,6 +346,9 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t n_c
                             const int32_t* move_off, const int32_t* move_pods,
                             int32_t* hints, int32_t* last_index,
                             ca_removal_result* results, int32_t* out_dest);
+/* [0] device time of all sweep kernels, [1] of the exact pass, [2] host time until the
+ * exact pass's results were on the host, [3] host wall time of the call (ms); returns 4. */
+int ca_removal_timings(const ca_mirror* m, float* out, int32_t cap);
 int ca_removal_stats(const ca_mirror* m, int32_t* rounds, float* kernel_ms, float* total_ms);
 
 #ifdef __cplusplus

@@ -1,0 +1,134 @@
+"""Multi-rank node-group sharding (autoscaler_amd/shard.py) over torch.distributed gloo,
+world_size 2, on CPU.  Each rank runs its contiguous block of node groups from the
+caller's lastIndex and the ranks fix up the lastIndex chain with one all_gather per
+round; the union of the ranks' results must equal one sequential Estimate over every
+group (the reference calls Estimate group after group with one shared checker,
+CA/core/scaleup/orchestrator/orchestrator.go:487-488).  The per-block Estimate here is
+the CPU restatement (test infrastructure), so the protocol is exercised without a GPU."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from autoscaler_amd.shard import run_sharded, walk
+
+
+def test_walk_accepts_and_flags():
+    # rank 1 ran from 0 but rank 0 moved lastIndex to 5 and rank 1 is sensitive
+    assert walk([[0, 5, 1, 1], [0, 9, 1, 1]], 0) == (1, 5)
+    # insensitive blocks are accepted whatever their input
+    assert walk([[0, 5, 1, 1], [0, 9, 0, 1]], 0) == (-1, 9)
+    # a block without a FitsAnyNode success passes lastIndex through
+    assert walk([[3, 3, 0, 0], [3, 7, 1, 1]], 3) == (-1, 7)
+
+
+def test_run_sharded_single_process_protocol():
+    """Two simulated ranks driven in lockstep: rank 1 must re-run from rank 0's output."""
+    calls = {0: [], 1: []}
+
+    def make_run(r):
+        def run(lin):
+            calls[r].append(lin)
+            return f"out{r}@{lin}", lin + 10 * (r + 1), 1, 1
+        return run
+
+    # lockstep all_gather for two "ranks" inside one process
+    import threading
+    barrier = threading.Barrier(2)
+    slots = [None, None]
+    results = {}
+
+    def gather_for(r):
+        def gather(rec):
+            slots[r] = list(rec)
+            barrier.wait()
+            out = [list(slots[0]), list(slots[1])]
+            barrier.wait()
+            return out
+        return gather
+
+    def worker(r):
+        results[r] = run_sharded(make_run(r), 4, gather_for(r), r)
+
+    ts = [threading.Thread(target=worker, args=(r,)) for r in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert calls[0] == [4]
+    assert calls[1] == [4, 14]                  # re-run from rank 0's lastIndex out
+    assert results[1][0] == "out1@14" and results[1][1] == 34 and results[0][1] == 34
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, seed, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "oracle"), os.path.join(root, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    import pyoracle
+    from autoscaler_amd import shard
+    from estgen import _encode_estimate, _estimate_inputs
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng, nodes, pods, templates, groups = _estimate_inputs(seed, n_groups=8, n_pods=60)
+        table, node_recs, tm, off, pod_idx = _encode_estimate(nodes, pods, templates, groups)
+        max_nodes = 0
+        L0 = 3
+        G = len(tm)
+        a, b = rank * G // world, (rank + 1) * G // world
+        off_blk = off[a:b + 1] - off[a]
+        idx_blk = pod_idx[off[a]:off[b]]
+
+        def run(lin):
+            o = pyoracle.OracleState()
+            if len(node_recs):
+                o.add_nodes(node_recs)
+            out = o.estimate(table, off_blk, idx_blk, tm[a:b], max_nodes, lin)
+            # conservative: every block counts as lastIndex-sensitive with a success
+            return out, out.last_index, 1, 1
+
+        out, final_L, reruns = shard.run_sharded(run, L0, shard.torch_all_gather(dist, "cpu"), rank)
+        # sequential reference over every group
+        o = pyoracle.OracleState()
+        if len(node_recs):
+            o.add_nodes(node_recs)
+        ref = o.estimate(table, off, pod_idx, tm, max_nodes, L0)
+        ok = np.array_equal(out.results, ref.results[a:b])
+        for g in range(a, b):
+            n = int(ref.results[g]["n_scheduled"])
+            s0, s1 = off[g] - off[a], off[g] - off[a] + n
+            ok &= np.array_equal(out.sched_pod[s0:s1], ref.sched_pod[off[g]:off[g] + n])
+            ok &= np.array_equal(out.sched_node[s0:s1], ref.sched_node[off[g]:off[g] + n])
+        ok &= final_L == ref.last_index
+        q.put((rank, bool(ok), reruns))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("seed", [0, 3, 7])
+def test_sharded_estimate_gloo_world2(seed, oracle_lib):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, seed, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    assert all(ok for _, ok, _ in res), res

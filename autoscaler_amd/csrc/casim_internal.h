@@ -108,6 +108,14 @@ inline uint32_t pod_dev_flags(const ca_pod_spec& p) {
 // TaintToleration, NodeAffinity — SF/runtime/framework.go:727-749 order.
 // Returns the failing plugin (CA_PLUGIN_*) or CA_PLUGIN_NONE.
 // ---------------------------------------------------------------------------
+// n.ints[k] without a dynamic register-array index (which would put the row in scratch)
+__host__ __device__ inline int64_t int_label_at(const NodeStatic& n, int32_t k) {
+    static_assert(CA_MAX_INT_KEYS == 4, "int_label_at");
+    const int64_t a = (k & 1) ? n.ints[1] : n.ints[0];
+    const int64_t b = (k & 1) ? n.ints[3] : n.ints[2];
+    return (k & 2) ? b : a;
+}
+
 __host__ __device__ inline bool dev_req_matches(const ca_selector_req& r, const NodeStatic& n) {
     switch (r.op) {
     case CA_OP_IN: {
@@ -122,8 +130,8 @@ __host__ __device__ inline bool dev_req_matches(const ca_selector_req& r, const 
     }
     case CA_OP_EXISTS: return (n.keys >> r.key) & 1u;
     case CA_OP_DOESNOTEXIST: return !((n.keys >> r.key) & 1u);
-    case CA_OP_GT: return ((n.int_valid >> r.key) & 1u) && n.ints[r.key] > r.bound;
-    case CA_OP_LT: return ((n.int_valid >> r.key) & 1u) && n.ints[r.key] < r.bound;
+    case CA_OP_GT: return ((n.int_valid >> r.key) & 1u) && int_label_at(n, r.key) > r.bound;
+    case CA_OP_LT: return ((n.int_valid >> r.key) & 1u) && int_label_at(n, r.key) < r.bound;
     case CA_OP_FIELD_EQ: return n.name_id == r.key;
     case CA_OP_FIELD_NE: return n.name_id != r.key;
     default: return false;

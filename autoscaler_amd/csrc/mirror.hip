@@ -51,7 +51,7 @@ int HostBuf::reserve(size_t need) {
     if (need <= bytes) return CA_OK;
     release();
     size_t sz = std::max<size_t>(need, 256);
-    if (hipHostMalloc(&ptr, sz, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc(&ptr, sz, hipHostMallocNonCoherent) != hipSuccess) {
         ptr = nullptr; bytes = 0; set_last_error("hipHostMalloc failed"); return CA_EDEVICE;
     }
     bytes = sz;
@@ -378,7 +378,7 @@ int ca_device_count(int32_t* out) {
 int ca_host_alloc(size_t bytes, void** out) {
     if (!out) return CA_EINVAL;
     *out = nullptr;
-    hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocNonCoherent);
     if (e != hipSuccess) { set_last_error(hipGetErrorString(e)); return CA_EDEVICE; }
     return CA_OK;
 }

@@ -436,7 +436,8 @@ __global__ void __launch_bounds__(64) k_sweep_table(
     const int32_t* __restrict__ move_pods, const PodHot* __restrict__ ph, const ca_pod_spec* __restrict__ specs,
     const ca_selector_term* __restrict__ terms, const ca_selector_req* __restrict__ reqs,
     const int32_t* __restrict__ names, const int32_t* __restrict__ hints, const int32_t* __restrict__ todo,
-    const int32_t* __restrict__ wstart, int32_t* __restrict__ table) {
+    const int32_t* __restrict__ wstart, const int32_t* __restrict__ row_of, int32_t* __restrict__ table,
+    int32_t stride) {
     const int t = blockIdx.x;
     const int lane = threadIdx.x;
     const int32_t c = todo[t];
@@ -491,7 +492,92 @@ __global__ void __launch_bounds__(64) k_sweep_table(
             }
         }
     }
-    table[(size_t)t * 64 + lane] = unknown ? TB_UNKNOWN : Lcur;
+    table[(size_t)lane * stride + (row_of ? row_of[t] : t)] = unknown ? TB_UNKNOWN : Lcur;
+}
+
+// ---------------------------------------------------------------------------
+// calibration for the first table round: thread i runs sensitive candidate i once,
+// from a rough guess g_i, and reports how far it moved lastIndex.  The advance barely
+// depends on the starting point (a placement lands on the first node with room), so
+// the prefix sum of these advances (k_sweep_est) centres the first windows within a
+// few positions of the true values.  Hints / ports / extended resources / long scans:
+// the advance falls back to the number of moved pods.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_sweep_calib(
+    const NodeHot* __restrict__ hot, const NodeStatic* __restrict__ st, int32_t n,
+    const uint8_t* __restrict__ dest_mask, const int32_t* __restrict__ cands, const int32_t* __restrict__ move_off,
+    const int32_t* __restrict__ move_pods, const PodHot* __restrict__ ph, const ca_pod_spec* __restrict__ specs,
+    const ca_selector_term* __restrict__ terms, const ca_selector_req* __restrict__ reqs,
+    const int32_t* __restrict__ names, const int32_t* __restrict__ hints, const int32_t* __restrict__ sens,
+    const int32_t* __restrict__ guess, int32_t S, int32_t* __restrict__ adv_out) {
+    const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= S || n <= 0) return;
+    const int32_t c = sens[i];
+    const int32_t node = cands[c];
+    const int32_t mo = move_off[c], mn = move_off[c + 1] - mo;
+    int32_t L = guess[i];
+    if (L >= n || L < 0) L = (int32_t)((uint32_t)L % (uint32_t)n);
+    int32_t adv = 0;
+    bool ok = mn <= TB_MAXP;
+    for (int32_t q = 0; q < mn && ok; q++) {
+        const PodHot p0 = ph[move_pods[mo + q]];
+        PodHot p = p0;
+        p.flags = moved_flags(p0.flags);
+        if ((hints[mo + q] >= 0) || (p.flags & (PF_PORTS | PF_SCALAR_REQ))) { ok = false; break; }
+        if (p.flags & PF_PREFILTER_FAIL) break;
+        const ca_pod_spec& sp = specs[p.spec];
+        int32_t steps = 0, pos = L;
+        for (;;) {
+            if (adv + steps >= n || steps >= TB_SCAN) { ok = false; break; }
+            const NodeHot nh = hot[pos];
+            bool vis = (pos != node) & (dest_mask[pos] != 0) & !(nh.flags & NF_UNSCHED);
+            if (vis && (p.flags & PF_PREFILTER_NAMES)) vis = in_prefilter(sp, names, st[pos].name_id);
+            if (vis && hot_fits(p, nh) && static_ok(sp, p, terms, reqs, nh, st + pos)) break;
+            steps++;
+            pos++;
+            if (pos >= n) pos = 0;
+        }
+        if (!ok) break;
+        adv += steps + 1;
+        L = pos + 1;
+        if (L >= n) L = 0;
+    }
+    adv_out[i] = ok ? adv : mn;
+}
+
+// est_k = L0 + sum_{i<k} adv_i (mod n); window start = est_k - 32.  One block.
+__global__ void __launch_bounds__(1024) k_sweep_est(const int32_t* __restrict__ adv, int32_t S, int64_t L0, int32_t n,
+                                                    int32_t* __restrict__ ws) {
+    __shared__ int64_t wtot[16];
+    __shared__ int64_t carry;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    for (int32_t base = 0; base < S; base += 1024) {
+        const int32_t k = base + tid;
+        const int64_t v = k < S ? adv[k] : 0;
+        int64_t x = v;                                   // inclusive scan in the wave
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wtot[w] = x;
+        __syncthreads();
+        int64_t pre = carry;
+        for (int q = 0; q < w; q++) pre += wtot[q];
+        if (k < S) {
+            int64_t e = (L0 + pre + x - v - 32) % n;       // exclusive prefix, window start
+            if (e < 0) e += n;
+            ws[k] = (int32_t)e;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int64_t t = 0;
+            for (int q = 0; q < 16; q++) t += wtot[q];
+            carry += t;
+        }
+        __syncthreads();
+    }
 }
 
 }  // namespace casim
@@ -502,6 +588,9 @@ namespace {
 
 inline int32_t wrap(int64_t v, int32_t n) {
     if (n <= 0) return 0;
+    if (v >= 0 && v < n) return (int32_t)v;            // the common case: no division
+    if (v >= n && v < 2 * (int64_t)n) return (int32_t)(v - n);
+    if (v < 0 && v >= -(int64_t)n) return (int32_t)(v + n);
     int64_t r = v % n;
     if (r < 0) r += n;
     return (int32_t)r;
@@ -514,8 +603,8 @@ struct DevView {
 };
 
 int launch_exact(ca_mirror* m, hipStream_t st, int32_t C, int32_t n, DevView d_mask, DevView d_c, DevView d_status,
-                 DevView d_off, DevView d_moves, DevView d_hints, DevBuf& d_lin, DevBuf& d_need, DevBuf& d_dest,
-                 DevBuf& d_hset, DevBuf& d_out) {
+                 DevView d_off, DevView d_moves, DevView d_hints, DevBuf& d_lin, DevBuf& d_need, DevView d_dest,
+                 DevView d_hset, DevView d_out) {
     const bool use_ext = m->n_ext_pods > 0;
     const size_t dyn = use_ext ? sizeof(OverlayExt) : 0;
     if (use_ext)
@@ -600,8 +689,14 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     const int32_t S = (int32_t)sens.size();
 
     SweepScratch& sw = m->sw;
-    DevBuf &d_in = sw.in, &d_lin = sw.lin, &d_need = sw.need, &d_dest = sw.dest, &d_hset = sw.hset,
-           &d_out = sw.out, &d_todo = sw.todo, &d_tab = sw.tab;
+    DevBuf &d_in = sw.in, &d_lin = sw.lin, &d_need = sw.need, &d_todo = sw.todo, &d_tab = sw.tab;
+    // outputs packed for one D2H: [SweepOut x C][dest M][hint set M]
+    const size_t out_bytes = sizeof(SweepOut) * (size_t)C + sizeof(int32_t) * 2 * (size_t)std::max(M, 1);
+    if ((rc = sw.out.reserve(out_bytes)) != CA_OK) return rc;
+    if ((rc = sw.h_out.reserve(out_bytes)) != CA_OK) return rc;
+    DevView d_out{sw.out.ptr};
+    DevView d_dest{sw.out.as<unsigned char>() + sizeof(SweepOut) * (size_t)C};
+    DevView d_hset{d_dest.as<int32_t>() + std::max(M, 1)};
     // one page-locked staging area and one H2D copy for every per-call input:
     // [cand C][status C][move_off C+1][move_pods M][hint per moved pod M][dest mask n bytes]
     const size_t in_ints = (size_t)C * 3 + 1 + (size_t)M * 2;
@@ -609,17 +704,11 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     if ((rc = sw.h_in.reserve(in_bytes)) != CA_OK) return rc;
     if ((rc = d_in.reserve(in_bytes)) != CA_OK) return rc;
     if ((rc = sw.h_tab.reserve(sizeof(int32_t) * 64 * (size_t)std::max(S, 1))) != CA_OK) return rc;
-    if ((rc = sw.h_out.reserve(sizeof(SweepOut) * (size_t)C)) != CA_OK) return rc;
-    if ((rc = sw.h_hset.reserve(sizeof(int32_t) * (size_t)std::max(M, 1))) != CA_OK) return rc;
-    if ((rc = sw.h_dest.reserve(sizeof(int32_t) * (size_t)std::max(M, 1))) != CA_OK) return rc;
-    if ((rc = sw.h_todo.reserve(sizeof(int32_t) * 2 * (size_t)std::max(S, 1))) != CA_OK) return rc;
+    if ((rc = sw.h_todo.reserve(sizeof(int32_t) * 4 * (size_t)std::max(S, 1))) != CA_OK) return rc;
     if ((rc = sw.h_lin.reserve((sizeof(int32_t) + 1) * (size_t)C)) != CA_OK) return rc;
     if ((rc = d_lin.reserve(sizeof(int32_t) * C)) != CA_OK) return rc;
     if ((rc = d_need.reserve((size_t)C)) != CA_OK) return rc;
-    if ((rc = d_dest.reserve(sizeof(int32_t) * std::max(M, 1))) != CA_OK) return rc;
-    if ((rc = d_hset.reserve(sizeof(int32_t) * std::max(M, 1))) != CA_OK) return rc;
-    if ((rc = d_out.reserve(sizeof(SweepOut) * C)) != CA_OK) return rc;
-    if ((rc = d_todo.reserve(sizeof(int32_t) * 2 * std::max(S, 1))) != CA_OK) return rc;
+    if ((rc = d_todo.reserve(sizeof(int32_t) * 4 * std::max(S, 1))) != CA_OK) return rc;
     if ((rc = d_tab.reserve(sizeof(int32_t) * 64 * (size_t)std::max(S, 1))) != CA_OK) return rc;
     int32_t* hin = sw.h_in.as<int32_t>();
     std::memcpy(hin, candidates, sizeof(int32_t) * C);
@@ -640,9 +729,9 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     // ---- 1. every candidate's input lastIndex ----
     std::vector<int32_t> exact_lin((size_t)C, 0), exact_lout((size_t)C, 0);
     std::vector<int32_t> ws((size_t)S, 0);          // window start per sensitive candidate
-    std::vector<int32_t> tab((size_t)S * 64, TB_UNKNOWN);
+    int32_t* const tab = sw.h_tab.as<int32_t>();    // [64][S], filled by the table rounds
     std::vector<uint8_t> have((size_t)S, 0);        // table row computed for ws
-    std::vector<int32_t> todo, todo_ws;
+    std::vector<int32_t> todo, todo_ws, todo_k;
     std::vector<uint8_t> need1((size_t)C, 0);
     std::vector<int32_t> lin1((size_t)C, 0);
     int32_t rounds = 0, exact_runs = 0;
@@ -655,50 +744,87 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
             g += move_off[sens[k] + 1] - move_off[sens[k]];
         }
     }
+    if (S > 0 && n > 0 && !getenv("CASIM_SWEEP_NO_CALIB")) {
+        // round 1 without a host round trip: calibrate the advances, centre the windows
+        // on their prefix sums, build every table row (DESIGN.md §4 sweep)
+        rounds++;
+        int32_t* ht = sw.h_todo.as<int32_t>();
+        for (int32_t k = 0; k < S; k++) { ht[k] = sens[k]; ht[S + k] = wrap((int64_t)ws[k] + 32, n); }
+        CA_HIP_CHECK(hipMemcpyAsync(d_todo.ptr, ht, sizeof(int32_t) * 2 * S, hipMemcpyHostToDevice, st));
+        int32_t* d_sens = d_todo.as<int32_t>();
+        int32_t* d_guess = d_sens + S;
+        int32_t* d_adv = d_sens + 2 * S;
+        int32_t* d_ws = d_sens + 3 * S;
+        CA_HIP_CHECK(hipEventRecord(m->ev0, st));
+        hipLaunchKernelGGL(k_sweep_calib, dim3((S + 63) / 64), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
+                           m->d_static.as<NodeStatic>(), n, d_mask.as<uint8_t>(), d_c.as<int32_t>(),
+                           d_off.as<int32_t>(), d_moves.as<int32_t>(), m->d_pods.hot.as<PodHot>(),
+                           m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
+                           m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
+                           d_hints.as<int32_t>(), d_sens, d_guess, S, d_adv);
+        CA_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_sweep_est, dim3(1), dim3(1024), 0, st, d_adv, S, (int64_t)L0, n, d_ws);
+        CA_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_sweep_table, dim3(S), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
+                           m->d_static.as<NodeStatic>(), n, d_mask.as<uint8_t>(), d_c.as<int32_t>(),
+                           d_off.as<int32_t>(), d_moves.as<int32_t>(), m->d_pods.hot.as<PodHot>(),
+                           m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
+                           m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
+                           d_hints.as<int32_t>(), d_sens, d_ws, (const int32_t*)nullptr, d_tab.as<int32_t>(), S);
+        CA_HIP_CHECK(hipGetLastError());
+        CA_HIP_CHECK(hipEventRecord(m->ev1, st));
+        CA_HIP_CHECK(hipMemcpyAsync(tab, d_tab.ptr, sizeof(int32_t) * 64 * (size_t)S, hipMemcpyDeviceToHost, st));
+        CA_HIP_CHECK(hipMemcpyAsync(ht, d_ws, sizeof(int32_t) * S, hipMemcpyDeviceToHost, st));
+        CA_HIP_CHECK(hipStreamSynchronize(st));
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
+        kms += ms;
+        for (int32_t k = 0; k < S; k++) { ws[k] = ht[k]; have[k] = 1; }
+        if (dbg_t) fprintf(stderr, "[sweep] calibrated table round: %d rows, kernels %.3f ms\n", S, ms);
+        tmark("table");
+    }
     SweepOut one;
     int32_t k0 = 0;               // first sensitive candidate not yet resolved
     int64_t cur = L0;             // exact lastIndex before sens[k0]
     while (k0 < S) {
-        todo.clear(); todo_ws.clear();
-        for (int32_t k = k0; k < S; k++) if (!have[k]) { todo.push_back(sens[k]); todo_ws.push_back(ws[k]); }
+        todo.clear(); todo_ws.clear(); todo_k.clear();
+        for (int32_t k = k0; k < S; k++)
+            if (!have[k]) { todo.push_back(sens[k]); todo_ws.push_back(ws[k]); todo_k.push_back(k); }
         if (!todo.empty()) {
             rounds++;
             const int32_t T = (int32_t)todo.size();
             int32_t* ht = sw.h_todo.as<int32_t>();
             std::memcpy(ht, todo.data(), sizeof(int32_t) * T);
             std::memcpy(ht + T, todo_ws.data(), sizeof(int32_t) * T);
-            CA_HIP_CHECK(hipMemcpyAsync(d_todo.ptr, ht, sizeof(int32_t) * 2 * T, hipMemcpyHostToDevice, st));
+            std::memcpy(ht + 2 * T, todo_k.data(), sizeof(int32_t) * T);
+            CA_HIP_CHECK(hipMemcpyAsync(d_todo.ptr, ht, sizeof(int32_t) * 3 * T, hipMemcpyHostToDevice, st));
             CA_HIP_CHECK(hipEventRecord(m->ev0, st));
             hipLaunchKernelGGL(k_sweep_table, dim3(T), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
                                m->d_static.as<NodeStatic>(), n, d_mask.as<uint8_t>(), d_c.as<int32_t>(),
                                d_off.as<int32_t>(), d_moves.as<int32_t>(), m->d_pods.hot.as<PodHot>(),
                                m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
                                m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
-                               d_hints.as<int32_t>(), d_todo.as<int32_t>(), d_todo.as<int32_t>() + T, d_tab.as<int32_t>());
+                               d_hints.as<int32_t>(), d_todo.as<int32_t>(), d_todo.as<int32_t>() + T,
+                               d_todo.as<int32_t>() + 2 * T, d_tab.as<int32_t>(), S);
             CA_HIP_CHECK(hipGetLastError());
             CA_HIP_CHECK(hipEventRecord(m->ev1, st));
-            const int32_t* rows = sw.h_tab.as<int32_t>();
-            CA_HIP_CHECK(hipMemcpyAsync(sw.h_tab.ptr, d_tab.ptr, sizeof(int32_t) * 64 * T, hipMemcpyDeviceToHost, st));
+            // the table is stored [lane][candidate] so the host walk, whose window offset
+            // stays near the centre, reads it nearly sequentially
+            CA_HIP_CHECK(hipMemcpyAsync(tab, d_tab.ptr, sizeof(int32_t) * 64 * (size_t)S, hipMemcpyDeviceToHost, st));
             CA_HIP_CHECK(hipStreamSynchronize(st));
             float ms = 0;
             (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
             kms += ms;
             if (dbg_t) fprintf(stderr, "[sweep] table round %d: %d rows, kernel %.3f ms\n", rounds, T, ms);
             tmark("table");
-            int32_t ti = 0;
-            for (int32_t k = k0; k < S; k++) {
-                if (have[k]) continue;
-                std::copy(rows + (size_t)ti * 64, rows + (size_t)ti * 64 + 64, tab.begin() + (size_t)k * 64);
-                have[k] = 1;
-                ti++;
-            }
+            for (int32_t k = k0; k < S; k++) have[k] = 1;
         }
         // walk the exact chain as far as the windows reach
         for (; k0 < S; k0++) {
             const int32_t c = sens[k0];
             const int32_t w = wrap(cur - ws[k0], n);
             if (w >= 64) break;
-            int32_t v = tab[(size_t)k0 * 64 + w];
+            int32_t v = tab[(size_t)(w) * S + k0];
             if (v == TB_UNKNOWN) {
                 // hints / ports / long scans: exact kernel at the exact lastIndex
                 need1[c] = 1;
@@ -726,17 +852,17 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
         int64_t est = cur;
         for (int32_t k = k0; k < S; k++) {
             const int32_t w = wrap(est - ws[k], n);
-            const int32_t v = w < 64 ? tab[(size_t)k * 64 + w] : TB_UNKNOWN;
+            const int32_t v = w < 64 ? tab[(size_t)(w) * S + k] : TB_UNKNOWN;
             if (w < 64 && v != TB_UNKNOWN) { est = v; continue; }
             int64_t next = est + (move_off[sens[k] + 1] - move_off[sens[k]]);
             int best = -1;              // known entry nearest the window centre
             for (int d = 0; d <= 32 && best < 0; d++) {
-                if (32 - d >= 0 && tab[(size_t)k * 64 + 32 - d] != TB_UNKNOWN) best = 32 - d;
-                else if (32 + d < 64 && tab[(size_t)k * 64 + 32 + d] != TB_UNKNOWN) best = 32 + d;
+                if (32 - d >= 0 && tab[(size_t)(32 - d) * S + k] != TB_UNKNOWN) best = 32 - d;
+                else if (32 + d < 64 && tab[(size_t)(32 + d) * S + k] != TB_UNKNOWN) best = 32 + d;
             }
             if (best >= 0) {
                 const int64_t from = (int64_t)ws[k] + best;
-                next = est + wrap(tab[(size_t)k * 64 + best] - from, n);
+                next = est + wrap(tab[(size_t)(best) * S + k] - from, n);
             }
             if (w >= 64) { ws[k] = wrap(est - 32, n); have[k] = 0; }
             est = wrap(next, n);
@@ -768,16 +894,13 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
         return rc;
     CA_HIP_CHECK(hipEventRecord(m->ev1, st));
     const SweepOut* outs = sw.h_out.as<SweepOut>();
-    const int32_t* hset = sw.h_hset.as<int32_t>();
-    CA_HIP_CHECK(hipMemcpyAsync(sw.h_out.ptr, d_out.ptr, sizeof(SweepOut) * C, hipMemcpyDeviceToHost, st));
-    if (M) {
-        CA_HIP_CHECK(hipMemcpyAsync(sw.h_dest.ptr, d_dest.ptr, sizeof(int32_t) * M, hipMemcpyDeviceToHost, st));
-        CA_HIP_CHECK(hipMemcpyAsync(sw.h_hset.ptr, d_hset.ptr, sizeof(int32_t) * M, hipMemcpyDeviceToHost, st));
-    }
+    const int32_t* h_dest = reinterpret_cast<const int32_t*>(outs + C);
+    const int32_t* hset = h_dest + std::max(M, 1);
+    CA_HIP_CHECK(hipMemcpyAsync(sw.h_out.ptr, sw.out.ptr, out_bytes, hipMemcpyDeviceToHost, st));
     CA_HIP_CHECK(hipStreamSynchronize(st));
     const auto t_exact = std::chrono::steady_clock::now();
     tmark("exact");
-    if (M) std::memcpy(out_dest, sw.h_dest.ptr, sizeof(int32_t) * M);
+    if (M) std::memcpy(out_dest, h_dest, sizeof(int32_t) * M);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
     kms += ms;
@@ -796,7 +919,7 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
                             outs[q].lout, outs[q].fa_success, outs[q].n_placed, move_off[q + 1] - move_off[q]);
                     if (k < S) {
                         const int32_t w = wrap(exact_lin[q] - ws[k], n);
-                        fprintf(stderr, " ws=%d w=%d tab=%d", ws[k], w, w < 64 ? tab[(size_t)k * 64 + w] : -9);
+                        fprintf(stderr, " ws=%d w=%d tab=%d", ws[k], w, w < 64 ? tab[(size_t)(w) * S + k] : -9);
                     }
                     fprintf(stderr, "\n");
                 }

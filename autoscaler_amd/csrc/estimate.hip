@@ -68,7 +68,9 @@ struct alignas(16) GroupMeta {
     uint32_t tflags;               // NF_* of the template
     int32_t moff;                  // offset of the group's 64-pod head masks
     int32_t toff;                  // offset of the group's 1024-pod tile counters
-    int32_t pad[3];
+    int32_t hoff;                  // offset of the group's radix histograms [256][rtiles]
+    int32_t rtiles;                // radix tiles of the group (bucket sort)
+    int32_t pad;
 };
 static_assert(sizeof(GroupMeta) == 64, "GroupMeta");
 
@@ -90,6 +92,40 @@ __device__ inline uint64_t ordered_bits(double d) {
 
 __device__ inline bool item_less(const SortItem& a, const SortItem& b) {
     return a.key < b.key || (a.key == b.key && a.pos < b.pos);
+}
+
+// SF_* bits of a pod against a group's template: the template-only part of the
+// filter chain (schedulerbased.go:107-129 PreFilter / Unschedulable skip, framework.go
+// order via dev_static_filters), evaluated once per (group, pod).  The full pod record
+// is read only when a static filter can matter.
+__device__ inline uint32_t static_sf(const PodHot& p, const ca_template& tp, bool tunsched,
+                                     const ca_pod_spec* __restrict__ specs, const ca_selector_term* __restrict__ terms,
+                                     const ca_selector_req* __restrict__ reqs) {
+    uint32_t sf = 0;
+    const bool pre_fail = (p.flags & PF_PREFILTER_FAIL) != 0;
+    bool static_ok = true;
+    if ((p.flags & (PF_NODE_NAME | PF_AFFINITY)) || (tp.node.taints && !(p.flags & PF_TAINT_MASK_ALL))) {
+        const ca_pod_spec& s = specs[p.spec];
+        if ((p.flags & (PF_NODE_NAME | PF_AFFINITY)) || (tp.node.taints & ~s.tolerated_taints)) {
+            NodeStatic ns;
+            ns.taints = tp.node.taints;
+            for (int w = 0; w < CA_LABEL_WORDS; w++) ns.labels[w] = tp.node.label_pairs[w];
+            ns.keys = tp.node.label_keys;
+            for (int k = 0; k < CA_MAX_INT_KEYS; k++) ns.ints[k] = tp.node.int_label[k];
+            ns.int_valid = tp.node.int_label_valid;
+            ns.name_id = tp.node.name_id;
+            static_ok = dev_static_filters(s, p.flags, terms, reqs, ns, false) == CA_PLUGIN_NONE;
+        }
+    }
+    if (!pre_fail && !tunsched) sf |= SF_EVAL;                           // schedulerbased.go:125
+    if ((sf & SF_EVAL) && static_ok) sf |= SF_FA_OK;
+    if (!pre_fail) sf |= SF_CP_EVAL;
+    if (!pre_fail && (!tunsched || (p.flags & PF_TOL_UNSCHED)) && static_ok) sf |= SF_CP_OK;
+    if (p.flags & PF_ALL_ZERO) sf |= SF_ZERO;
+    if (p.flags & PF_SCALAR_REQ) sf |= SF_SCALAR;
+    if (p.flags & PF_PORTS) sf |= SF_PORTS;
+    if (p.flags & PF_HOSTNAME_DEP) sf |= SF_UNSUP;
+    return sf;
 }
 
 // 1. score + static predicates + tile sort ----------------------------------
@@ -117,29 +153,8 @@ __global__ void __launch_bounds__(256) k_score_tiles(
             double score = 0.0;
             if (acpu > 0) score += (double)s.score_milli_cpu / (double)acpu;
             if (amem > 0) score += (double)s.score_memory / (double)amem;
-            uint32_t sf = 0;
-            const bool pre_fail = (p.flags & PF_PREFILTER_FAIL) != 0;
-            bool static_ok = true;
-            const bool need_static = (p.flags & (PF_NODE_NAME | PF_AFFINITY)) ||
-                                     (tp.node.taints & ~s.tolerated_taints);
-            if (need_static) {
-                NodeStatic ns;
-                ns.taints = tp.node.taints;
-                for (int w = 0; w < CA_LABEL_WORDS; w++) ns.labels[w] = tp.node.label_pairs[w];
-                ns.keys = tp.node.label_keys;
-                for (int k = 0; k < CA_MAX_INT_KEYS; k++) ns.ints[k] = tp.node.int_label[k];
-                ns.int_valid = tp.node.int_label_valid;
-                ns.name_id = tp.node.name_id;
-                static_ok = dev_static_filters(s, p.flags, terms, reqs, ns, false) == CA_PLUGIN_NONE;
-            }
-            if (!pre_fail && !tunsched) sf |= SF_EVAL;                           // schedulerbased.go:125
-            if ((sf & SF_EVAL) && static_ok) sf |= SF_FA_OK;
-            if (!pre_fail) sf |= SF_CP_EVAL;
-            if (!pre_fail && (!tunsched || (p.flags & PF_TOL_UNSCHED)) && static_ok) sf |= SF_CP_OK;
-            if (p.flags & PF_ALL_ZERO) sf |= SF_ZERO;
-            if (p.flags & PF_SCALAR_REQ) sf |= SF_SCALAR;
-            if (p.flags & PF_PORTS) sf |= SF_PORTS;
-            if (p.flags & PF_HOSTNAME_DEP) { sf |= SF_UNSUP; unsup = 1; }
+            const uint32_t sf = static_sf(p, tp, tunsched, specs, terms, reqs);
+            if (sf & SF_UNSUP) unsup = 1;
             it.key = ~ordered_bits(score);
             it.pos = (uint32_t)pos;
             it.flags = sf;
@@ -229,7 +244,252 @@ __global__ void __launch_bounds__(256) k_emit_stream(const GroupMeta* __restrict
     if ((threadIdx.x & 63) == 0 && i < gm.count) heads[gm.moff + (i >> 6)] = hb;
 }
 
+// 1'-3'. bucket sort over score classes ----------------------------------------
+// The sort key (score desc, list position asc) depends on a pod only through its
+// score class (ca_podset: equal score_milli_cpu and score_memory) and its position.  So
+// when the pod set has at most CLS_MAX classes, each group ranks its classes by score
+// (k_class_rank: dense rank, equal scores share a rank = the tie-by-position rule H2),
+// and its pod list — already in position order — is stably sorted by that rank with
+// 8-bit LSD counting passes (k_radix_hist / k_radix_scan / k_radix_scatter; ranks of
+// equal digits inside a wave by ballot multisplit).  k_emit_bucket then builds the
+// stream exactly as k_emit_stream does from the comparison sort.  Same output as
+// k_score_tiles + k_merge_runs + k_emit_stream, ~8 B of HBM per item and pass instead
+// of ~300.
+constexpr int CLS_MAX = 4096;
+constexpr int RT = 2048;               // items per radix tile
+constexpr int RTHREADS = 256;
+constexpr int RPT = RT / RTHREADS;     // items per thread
+constexpr int RCH = RT / 64 / (RTHREADS / 64);   // 64-item chunks per wave
+
+__global__ void __launch_bounds__(1024) k_class_rank(const GroupMeta* __restrict__ groups,
+                                                    const ca_template* __restrict__ tmpls,
+                                                    const int64_t* __restrict__ cls_sc, int32_t U, int32_t NP,
+                                                    int32_t* __restrict__ crank) {
+    __shared__ uint64_t key[CLS_MAX];
+    __shared__ uint32_t idx[CLS_MAX];
+    __shared__ int32_t sc[CLS_MAX];
+    const GroupMeta gm = groups[blockIdx.x];
+    const ca_template& tp = tmpls[gm.tmpl];
+    const int64_t acpu = tp.node.alloc_milli_cpu, amem = tp.node.alloc_memory;
+    for (int i = threadIdx.x; i < NP; i += blockDim.x) {
+        uint64_t k = ~0ull;
+        if (i < U) {
+            // calculatePodScore (binpacking_estimator.go:164-193), same float64 operations
+            double score = 0.0;
+            if (acpu > 0) score += (double)cls_sc[2 * i] / (double)acpu;
+            if (amem > 0) score += (double)cls_sc[2 * i + 1] / (double)amem;
+            k = ~ordered_bits(score);            // ascending key == descending score
+        }
+        key[i] = k;
+        idx[i] = (uint32_t)i;
+    }
+    __syncthreads();
+    for (int k = 2; k <= NP; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = threadIdx.x; t < NP; t += blockDim.x) {
+                const int ixj = t ^ j;
+                if (ixj > t) {
+                    const uint64_t a = key[t], b = key[ixj];
+                    const uint32_t ia = idx[t], ib = idx[ixj];
+                    const bool up = (t & k) == 0;
+                    const bool less_ba = b < a || (b == a && ib < ia);
+                    const bool less_ab = a < b || (a == b && ia < ib);
+                    if (up ? less_ba : less_ab) { key[t] = b; key[ixj] = a; idx[t] = ib; idx[ixj] = ia; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // dense rank: number of distinct keys before
+    for (int i = threadIdx.x; i < NP; i += blockDim.x) sc[i] = (i > 0 && key[i] != key[i - 1]) ? 1 : 0;
+    __syncthreads();
+    for (int o = 1; o < NP; o <<= 1) {
+        int32_t v[CLS_MAX / 1024];
+        int n = 0;
+        for (int i = threadIdx.x; i < NP; i += blockDim.x) v[n++] = (i >= o ? sc[i - o] : 0);
+        __syncthreads();
+        n = 0;
+        for (int i = threadIdx.x; i < NP; i += blockDim.x) sc[i] += v[n++];
+        __syncthreads();
+    }
+    for (int i = threadIdx.x; i < U; i += blockDim.x) crank[(size_t)blockIdx.x * U + idx[i]] = sc[i];
+}
+
+__device__ inline uint32_t item_digit(const GroupMeta& gm, const uint32_t* __restrict__ src, int32_t i,
+                                      const int32_t* __restrict__ pod_idx, const int32_t* __restrict__ pcls,
+                                      const int32_t* __restrict__ crank_g, int shift, uint32_t* pos_out) {
+    const uint32_t pos = src ? src[gm.off + i] : (uint32_t)i;
+    *pos_out = pos;
+    const int32_t pidx = pod_idx[gm.off + (int32_t)pos];
+    return ((uint32_t)crank_g[pcls[pidx]] >> shift) & 255u;
+}
+
+__global__ void __launch_bounds__(RTHREADS) k_radix_hist(const GroupMeta* __restrict__ groups,
+                                                        const uint32_t* __restrict__ src,
+                                                        const int32_t* __restrict__ pod_idx,
+                                                        const int32_t* __restrict__ pcls,
+                                                        const int32_t* __restrict__ crank, int32_t U, int shift,
+                                                        int32_t* __restrict__ hist) {
+    __shared__ int32_t h[256];
+    const GroupMeta gm = groups[blockIdx.y];
+    const int32_t t = (int32_t)blockIdx.x;
+    if (t >= gm.rtiles) return;
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int32_t* cr = crank + (size_t)blockIdx.y * U;
+    const int32_t base = t * RT;
+    for (int r = 0; r < RPT; r++) {
+        const int32_t i = base + r * RTHREADS + (int32_t)threadIdx.x;
+        if (i < gm.count) {
+            uint32_t pos;
+            atomicAdd(&h[item_digit(gm, src, i, pod_idx, pcls, cr, shift, &pos)], 1);
+        }
+    }
+    __syncthreads();
+    hist[gm.hoff + (int32_t)threadIdx.x * gm.rtiles + t] = h[threadIdx.x];
+}
+
+// exclusive scan of the group's [256][rtiles] histogram, digit-major
+__global__ void __launch_bounds__(256) k_radix_scan(const GroupMeta* __restrict__ groups, int32_t* __restrict__ hist) {
+    __shared__ int32_t wsum[4];
+    const GroupMeta gm = groups[blockIdx.x];
+    const int32_t n = 256 * gm.rtiles;
+    int32_t* h = hist + gm.hoff;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int32_t carry = 0;
+    for (int32_t b = 0; b < n; b += 256) {
+        const int32_t i = b + (int32_t)threadIdx.x;
+        const int32_t v = i < n ? h[i] : 0;
+        int32_t x = v;                                   // inclusive wave scan
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        int32_t pre = carry;
+        for (int q = 0; q < w; q++) pre += wsum[q];
+        const int32_t tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (i < n) h[i] = pre + x - v;
+        carry += tot;
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(RTHREADS) k_radix_scatter(const GroupMeta* __restrict__ groups,
+                                                           const uint32_t* __restrict__ src,
+                                                           const int32_t* __restrict__ pod_idx,
+                                                           const int32_t* __restrict__ pcls,
+                                                           const int32_t* __restrict__ crank, int32_t U, int shift,
+                                                           const int32_t* __restrict__ hist,
+                                                           uint32_t* __restrict__ dst) {
+    __shared__ int32_t wcnt[RTHREADS / 64][256];
+    const GroupMeta gm = groups[blockIdx.y];
+    const int32_t t = (int32_t)blockIdx.x;
+    if (t >= gm.rtiles) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int d = lane; d < 256; d += 64) wcnt[w][d] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const int32_t* cr = crank + (size_t)blockIdx.y * U;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t dg[RCH], pv[RCH];
+    int32_t rk[RCH];
+    const int32_t wbase = t * RT + w * (RCH * 64);       // wave w owns RCH consecutive chunks
+    for (int c = 0; c < RCH; c++) {
+        const int32_t i = wbase + c * 64 + lane;
+        const bool valid = i < gm.count;
+        uint32_t pos = 0, d = 0;
+        if (valid) d = item_digit(gm, src, i, pod_idx, pcls, cr, shift, &pos);
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < 8; b++) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const int32_t before = wcnt[w][valid ? d : 0];
+        const int32_t r = before + __builtin_popcountll(peers & lt);
+        __builtin_amdgcn_wave_barrier();
+        if (valid && (peers & lt) == 0) wcnt[w][d] = before + __builtin_popcountll(peers);
+        __builtin_amdgcn_wave_barrier();
+        dg[c] = valid ? d : 0xFFFFFFFFu;
+        pv[c] = pos;
+        rk[c] = r;
+    }
+    __syncthreads();
+    // offset of wave w inside each digit of the tile: the counts of waves before it
+    int32_t pre[RTHREADS / 64];
+    if (threadIdx.x < 256) {
+        int32_t acc = 0;
+        for (int q = 0; q < RTHREADS / 64; q++) { pre[q] = acc; acc += wcnt[q][threadIdx.x]; }
+    }
+    __syncthreads();
+    if (threadIdx.x < 256)
+        for (int q = 0; q < RTHREADS / 64; q++) wcnt[q][threadIdx.x] = pre[q] + hist[gm.hoff + (int32_t)threadIdx.x * gm.rtiles + t];
+    __syncthreads();
+    for (int c = 0; c < RCH; c++) {
+        if (dg[c] == 0xFFFFFFFFu) continue;
+        dst[gm.off + wcnt[w][dg[c]] + rk[c]] = pv[c];
+    }
+}
+
+// stream of one group from the bucket-sorted positions (same output as k_emit_stream)
+__global__ void __launch_bounds__(256) k_emit_bucket(const GroupMeta* __restrict__ groups,
+                                                    const uint32_t* __restrict__ sorted,
+                                                    const int32_t* __restrict__ pod_idx, const ca_template* __restrict__ tmpls,
+                                                    const PodHot* __restrict__ ph, const ca_pod_spec* __restrict__ specs,
+                                                    const ca_selector_term* __restrict__ terms,
+                                                    const ca_selector_req* __restrict__ reqs,
+                                                    StreamPod* __restrict__ out, uint64_t* __restrict__ heads,
+                                                    uint32_t* __restrict__ group_unsup) {
+    const GroupMeta gm = groups[blockIdx.y];
+    const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int lane = threadIdx.x & 63;
+    if ((int32_t)(blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) >= gm.count) return;   // whole wave past the end
+    const ca_template& tp = tmpls[gm.tmpl];
+    const bool tunsched = (tp.node.flags & CA_NODE_UNSCHEDULABLE) != 0;
+    const bool valid = i < gm.count;
+    PodHot p = {};
+    uint32_t sf = 0;
+    int32_t pidx = 0;
+    if (valid) {
+        pidx = pod_idx[gm.off + (int32_t)sorted[gm.off + i]];
+        p = ph[pidx];
+        sf = static_sf(p, tp, tunsched, specs, terms, reqs);
+    }
+    // the previous stream entry: lane - 1, or recomputed by lane 0
+    int64_t qc = __shfl_up(p.cpu, 1, 64), qm = __shfl_up(p.mem, 1, 64), qe = __shfl_up(p.eph, 1, 64);
+    uint32_t qf = __shfl_up(sf, 1, 64);
+    if (lane == 0 && valid && i > 0) {
+        const PodHot q = ph[pod_idx[gm.off + (int32_t)sorted[gm.off + i - 1]]];
+        qc = q.cpu; qm = q.mem; qe = q.eph;
+        qf = static_sf(q, tp, tunsched, specs, terms, reqs);
+    }
+    bool head = true;
+    if (valid) {
+        const bool bat = batchable(p, sf);
+        if (i > 0 && bat) head = !(qf == sf && qc == p.cpu && qm == p.mem && qe == p.eph);
+        StreamPod sp;
+        sp.cpu = p.cpu; sp.mem = p.mem; sp.eph = p.eph;
+        sp.pod = pidx;
+        sp.flags = sf | (head ? SF_HEAD : 0u) | (bat ? SF_BATCH : 0u);
+        out[gm.off + i] = sp;
+        if (sf & SF_UNSUP) atomicOr(&group_unsup[blockIdx.y], 1u);
+    }
+    const uint64_t hb = __ballot(head);
+    if (lane == 0) heads[gm.moff + (i >> 6)] = hb;
+}
+
 // 4. the First-Fit-Decreasing chain -------------------------------------------
+#ifdef CASIM_PROF   // section cycle counters of k_ffd_chain (profiling build only)
+__device__ unsigned long long g_chain_prof[1024][8];
+#define PROF_T(v) const uint64_t v = clock64()
+#define PROF_ADD(i, t) prof[i] += clock64() - (t)
+#define PROF_INC(i) prof[i]++
+#else
+#define PROF_T(v) (void)0
+#define PROF_ADD(i, t) (void)0
+#define PROF_INC(i) (void)0
+#endif
 __device__ inline int64_t rl64(int64_t v, int lane) {
     const uint64_t u = (uint64_t)v;
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, lane);
@@ -249,6 +509,13 @@ __device__ inline int32_t wave_max32(int32_t v) {
     for (int o = 32; o > 0; o >>= 1) {
         const int32_t x = __shfl_xor(v, o, 64);
         v = x > v ? x : v;
+    }
+    return v;
+}
+__device__ inline int32_t wave_min32(int32_t v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const int32_t x = __shfl_xor(v, o, 64);
+        v = x < v ? x : v;
     }
     return v;
 }
@@ -281,8 +548,15 @@ __device__ inline bool rec_fits(const NodeRec& r, int64_t pcpu, int64_t pmem, in
 __device__ inline int32_t dim_copies(int64_t free_, int64_t req, int32_t cap) {
     if (free_ < 0) return 0;
     if (req == 0) return cap;
-    const int64_t q = free_ / req;
-    return q < (int64_t)cap ? (int32_t)q : cap;
+    if (free_ < req) return 0;
+    // floor(free/req) capped at cap, without a 64-bit integer division: the float64
+    // quotient is within one of the exact one once capped, and one step each way fixes it.
+    const double qd = (double)free_ / (double)req;
+    uint64_t q = qd >= (double)cap ? (uint64_t)cap : (uint64_t)qd;
+    const uint64_t f = (uint64_t)free_, r = (uint64_t)req;     // both < 2^63: no wrap below
+    if (q * r > f) q--;
+    else if (q < (uint64_t)cap && (q + 1) * r <= f) q++;
+    return (int32_t)q;
 }
 __device__ inline int32_t rec_copies(const NodeRec& r, int64_t pcpu, int64_t pmem, int64_t peph, bool zero, int32_t cap) {
     int32_t c = r.pods < cap ? r.pods : cap;
@@ -337,6 +611,14 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int g = blockIdx.x;
     if (!need[g]) return;
+    const uint64_t t_begin = wall_clock64();      // diagnostics: ca_estimate_plan_group_ticks
+#ifdef CASIM_PROF
+    const uint64_t t_cyc0 = clock64();
+#endif
+    uint32_t n_single = 0;
+#ifdef CASIM_PROF
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     const int lane = threadIdx.x;
     const GroupMeta gm = groups[g];
     const int32_t lin = lin_arr[g];
@@ -425,8 +707,11 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
 
         // ---------------- a run of identical resource-only pods ----------------
         if (batch_runs && (sf & (SF_BATCH | SF_HEAD)) == (SF_BATCH | SF_HEAD)) {
+            PROF_T(t_re);
             const int32_t e = run_end(hm, pos, P, lane);
+            PROF_ADD(0, t_re);
             if (e - pos >= 2) {
+                PROF_INC(7);
                 const int32_t RN = e - pos;
                 const uint64_t kev = (sf & SF_EVAL) ? 1u : 0u;
                 int32_t done = 0;
@@ -445,6 +730,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                             const int32_t c = rec_copies(R[last_node], pcpu, pmem, peph, zero, rem);
                             if (c > 0) { one = last_node; n_one = c; nalive = 1; }
                         } else {
+                            PROF_T(t_ca);
                             int32_t na = 0, a1 = -1;
                             for (int32_t j = lane; j < k; j += 64) {
                                 const int32_t c = rec_copies(R[j], pcpu, pmem, peph, zero, rem);
@@ -456,6 +742,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                             nalive = (int32_t)wave_sum64(na);
                             a1 = wave_max32(a1);
                             if (nalive == 1) { one = a1; n_one = (int32_t)min(S, (int64_t)rem); }
+                            PROF_ADD(1, t_ca);
                         }
                         if (nalive == 1) {
                             // every remaining copy goes to the one row with room
@@ -478,41 +765,69 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                             placed = n_one;
                         } else if (nalive > 1) {
                             const int32_t n = (int32_t)min(S, (int64_t)rem);
+                            PROF_T(t_rv);
                             __builtin_amdgcn_wave_barrier();
                             // revolution 1: rows with room, in rotated order from j0
-                            int32_t na = 0;
+                            int32_t na = 0, cmin = INT32_MAX;
                             for (int32_t b = 0; b < k; b += 64) {
                                 const int32_t rr = b + lane;
                                 int32_t j = j0 + rr;
                                 if (j >= k) j -= k;
-                                const bool keep = rr < k && CAPA[rr < k ? j : 0] >= 1;
+                                const int32_t c = rr < k ? CAPA[j] : 0;
+                                const bool keep = c >= 1;
                                 const uint64_t bm = __ballot(keep);
-                                if (keep) ALIVE[na + mbcnt(bm)] = j;
+                                if (keep) { ALIVE[na + mbcnt(bm)] = j; cmin = min(cmin, c); }
                                 na += __builtin_popcountll(bm);
                             }
+                            cmin = wave_min32(cmin);
                             __builtin_amdgcn_wave_barrier();
+                            // Revolutions r..cmin serve the same alive list (no row runs out
+                            // before cmin), so the list is compacted once per distinct copy
+                            // level, and the placements of those revolutions are the list
+                            // repeated: placement t of the level goes to ALIVE[t % na].
                             int32_t got = 0, r = 1, last = -1;
+                            int32_t* gdst = ga + pos + done;
                             for (;;) {
-                                const int32_t m = min(na, n - got);
-                                for (int32_t i = lane; i < m; i += 64) ga[pos + done + got + i] = ALIVE[i];
-                                last = ALIVE[m - 1];
-                                got += m;
-                                if (got == n) break;
-                                // revolution r+1 serves the rows with at least r+1 copies
-                                int32_t nn2 = 0;
+                                const int64_t avail = (int64_t)(cmin - r + 1) * na;
+                                const bool fin = got + avail >= n;
+                                const int32_t cnt = fin ? n - got : (int32_t)avail;
+                                {
+                                    const int32_t st = 64 % na;
+                                    int32_t q = lane % na;
+                                    for (int32_t t = lane; t < cnt; t += 64) {
+                                        gdst[got + t] = ALIVE[q];
+                                        q += st;
+                                        if (q >= na) q -= na;
+                                    }
+                                }
+                                if (fin) {
+                                    r += (cnt - 1) / na;                    // revolution of the last placement
+                                    last = ALIVE[(cnt - 1) % na];
+                                    got = n;
+                                    PROF_INC(6);
+                                    break;
+                                }
+                                got += cnt;
+                                r = cmin + 1;
+                                // the rows with at least r copies stay
+                                int32_t nn2 = 0, cm2 = INT32_MAX;
                                 for (int32_t b = 0; b < na; b += 64) {
                                     const int32_t i = b + lane;
                                     const int32_t j = i < na ? ALIVE[i] : 0;
-                                    const bool keep = i < na && CAPA[j] >= r + 1;
+                                    const int32_t c = i < na ? CAPA[j] : 0;
+                                    const bool keep = c >= r;
                                     const uint64_t bm = __ballot(keep);
                                     __builtin_amdgcn_wave_barrier();
-                                    if (keep) ALIVE[nn2 + mbcnt(bm)] = j;
+                                    if (keep) { ALIVE[nn2 + mbcnt(bm)] = j; cm2 = min(cm2, c); }
                                     nn2 += __builtin_popcountll(bm);
                                     __builtin_amdgcn_wave_barrier();
                                 }
                                 na = nn2;
-                                r++;
+                                cmin = wave_min32(cm2);
+                                PROF_INC(6);
                             }
+                            PROF_ADD(2, t_rv);
+                            PROF_T(t_up);
                             int32_t rl = last - j0;
                             if (rl < 0) rl += k;
                             evals += (uint64_t)(r - 1) * (uint64_t)k + (uint64_t)rl + 1;
@@ -532,6 +847,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                                 }
                             }
                             __builtin_amdgcn_wave_barrier();
+                            PROF_ADD(3, t_up);
                             L = n_base + last + 1;
                             if (L >= len) L -= len;
                             note_success();
@@ -578,6 +894,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                     // the first one lastIndex wraps to 0 and each costs k evals.  A
                     // node's opening pod first fails FitsAnyNode over the k rows before it
                     // and takes one limiter grant.  Closed form over n_open nodes.
+                    PROF_T(t_op);
                     const int32_t ct = (sf & SF_FA_OK) ? rec_copies(trec, pcpu, pmem, peph, zero, rem2) : 1;
                     int32_t n_open = (rem2 + ct - 1) / ct;
                     if (max_nodes > 0) n_open = min(n_open, 1 + (max_nodes - granted));
@@ -628,6 +945,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                     nsched += placed2;
                     done += placed2;
                     __builtin_amdgcn_wave_barrier();
+                    PROF_ADD(4, t_op);
                 }
                 pos = e;
                 continue;
@@ -645,6 +963,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
             for (int i = 0; i < CA_MAX_SCALAR; i++) psc[i] = s.req_scalar[i];
         }
         pos++;
+        n_single++;
 
         // ---- FitsAnyNodeMatching(newNodeNames) (binpacking_estimator.go:91-93) ----
         int32_t found = -1;
@@ -779,7 +1098,12 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
         res.sensitive = sensitive ? 1 : 0;
         res.had_success = first_success ? 1 : 0;
         res.evals = evals;
+        res.pad = (uint64_t)(uint32_t)(wall_clock64() - t_begin) | ((uint64_t)n_single << 32);
         outs[g] = res;
+#ifdef CASIM_PROF
+        prof[5] = clock64() - t_cyc0;
+        if (g < 1024) for (int i = 0; i < 8; i++) g_chain_prof[g][i] = prof[i];
+#endif
     }
 }
 
@@ -858,13 +1182,16 @@ struct ca_estimate_plan {
     bool use_ports = false, use_scalar = false;
     int32_t n_masks = 0, n_tiles = 0;
     DevBuf d_meta, d_pod_idx, d_tmpl, d_sortA, d_sortB, d_stream, d_heads, d_assign, d_tcount, d_unsup, d_lin, d_need,
-        d_out, d_sched_pod, d_sched_node;
+        d_out, d_sched_pod, d_sched_node, d_crank, d_hist;
+    int32_t n_hist = 0, max_rtiles = 0;
+    bool bucket = false;           // bucket sort over score classes (podset has <= CLS_MAX classes)
     Stats stats;
     // per-phase device timings of the last run (ms): score, merge, emit, chain (all
     // rounds), compact, d2h; and the host wall time of the call
     enum { EV_START, EV_SCORE, EV_MERGE, EV_EMIT, EV_CHAIN0, EV_CHAIN1, EV_COMPACT, EV_D2H, EV_N };
     hipEvent_t ev[EV_N] = {};
     float t_ms[7] = {};
+    std::vector<uint64_t> diag;     // per group: chain ticks (100 MHz) | single-pod steps << 32
     ~ca_estimate_plan() {
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
     }
@@ -884,6 +1211,12 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     p->max_count = 0;
     p->n_masks = 0;
     p->n_tiles = 0;
+    p->n_hist = 0;
+    p->max_rtiles = 0;
+    {
+        const char* e = getenv("CASIM_SORT");      // "merge" forces the comparison sort (tests run both)
+        p->bucket = s->n_cls <= CLS_MAX && !(e && strcmp(e, "merge") == 0);
+    }
     for (int32_t g = 0; g < G; g++) {
         const int32_t c = group_off[g + 1] - group_off[g];
         if (c < 0) return CA_EINVAL;
@@ -899,7 +1232,11 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
         gm.tflags = t.node.flags;
         gm.moff = p->n_masks;
         gm.toff = p->n_tiles;
-        gm.pad[0] = gm.pad[1] = gm.pad[2] = 0;
+        gm.rtiles = (c + RT - 1) / RT;
+        gm.hoff = p->n_hist;
+        gm.pad = 0;
+        p->n_hist += 256 * gm.rtiles;
+        p->max_rtiles = std::max(p->max_rtiles, gm.rtiles);
         p->n_masks += (c + 63) / 64;
         p->n_tiles += (c + CTILE - 1) / CTILE;
         p->max_count = std::max(p->max_count, c);
@@ -932,6 +1269,11 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     if ((rc = p->d_out.reserve(sizeof(ChainOut) * (size_t)std::max(G, 1))) != CA_OK) return rc;
     if ((rc = p->d_sched_pod.reserve(sizeof(int32_t) * tot)) != CA_OK) return rc;
     if ((rc = p->d_sched_node.reserve(sizeof(int32_t) * tot)) != CA_OK) return rc;
+    if (p->bucket) {
+        if ((rc = p->d_crank.reserve(sizeof(int32_t) * (size_t)std::max(G, 1) * (size_t)std::max(s->n_cls, 1))) != CA_OK)
+            return rc;
+        if ((rc = p->d_hist.reserve(sizeof(int32_t) * (size_t)std::max(p->n_hist, 1))) != CA_OK) return rc;
+    }
     if (G) CA_HIP_CHECK(hipMemcpyAsync(p->d_meta.ptr, p->h_meta.data(), sizeof(GroupMeta) * G, hipMemcpyHostToDevice, st));
     if (p->total) CA_HIP_CHECK(hipMemcpyAsync(p->d_pod_idx.ptr, pod_idx, sizeof(int32_t) * p->total, hipMemcpyHostToDevice, st));
     if (G) CA_HIP_CHECK(hipMemcpyAsync(p->d_tmpl.ptr, templates, sizeof(ca_template) * G, hipMemcpyHostToDevice, st));
@@ -970,7 +1312,42 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     const int32_t batch_runs = (rb_env && rb_env[0] == '0') ? 0 : 1;
     CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_START], st));
     // 1-3: score, sort, stream
-    if (p->total > 0) {
+    if (p->total > 0 && p->bucket) {
+        const int32_t U = p->s->n_cls;
+        int32_t NP = 1;
+        while (NP < U) NP <<= 1;
+        int32_t* crank = p->d_crank.as<int32_t>();
+        const int32_t* pcls = p->s->d_cls.as<int32_t>();
+        hipLaunchKernelGGL(k_class_rank, dim3(G), dim3(1024), 0, st, p->d_meta.as<GroupMeta>(), p->d_tmpl.as<ca_template>(),
+                           p->s->d_cls_sc.as<int64_t>(), U, NP, crank);
+        CA_HIP_CHECK(hipGetLastError());
+        CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], st));
+        int32_t nb = 1, passes = 0;                       // buckets <= U: 8-bit digits
+        while (nb < U) { nb <<= 8; passes++; }
+        passes = std::max(passes, 1);
+        uint32_t* a = nullptr;                            // identity (position order)
+        uint32_t* bufs[2] = {p->d_sortA.as<uint32_t>(), p->d_sortB.as<uint32_t>()};
+        for (int ps = 0; ps < passes; ps++) {
+            uint32_t* b = bufs[ps & 1];
+            hipLaunchKernelGGL(k_radix_hist, dim3(p->max_rtiles, G), dim3(RTHREADS), 0, st, p->d_meta.as<GroupMeta>(), a,
+                               p->d_pod_idx.as<int32_t>(), pcls, crank, U, 8 * ps, p->d_hist.as<int32_t>());
+            CA_HIP_CHECK(hipGetLastError());
+            hipLaunchKernelGGL(k_radix_scan, dim3(G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(), p->d_hist.as<int32_t>());
+            CA_HIP_CHECK(hipGetLastError());
+            hipLaunchKernelGGL(k_radix_scatter, dim3(p->max_rtiles, G), dim3(RTHREADS), 0, st, p->d_meta.as<GroupMeta>(), a,
+                               p->d_pod_idx.as<int32_t>(), pcls, crank, U, 8 * ps, p->d_hist.as<int32_t>(), b);
+            CA_HIP_CHECK(hipGetLastError());
+            a = b;
+        }
+        CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], st));
+        const int32_t blocks = (p->max_count + 255) / 256;
+        hipLaunchKernelGGL(k_emit_bucket, dim3(blocks, G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(), a,
+                           p->d_pod_idx.as<int32_t>(), p->d_tmpl.as<ca_template>(), p->s->t.hot.as<PodHot>(),
+                           p->s->t.spec.as<ca_pod_spec>(), p->s->t.terms.as<ca_selector_term>(),
+                           p->s->t.reqs.as<ca_selector_req>(), p->d_stream.as<StreamPod>(), p->d_heads.as<uint64_t>(),
+                           p->d_unsup.as<uint32_t>());
+        CA_HIP_CHECK(hipGetLastError());
+    } else if (p->total > 0) {
         const int32_t tiles = (p->max_count + TILE - 1) / TILE;
         hipLaunchKernelGGL(k_score_tiles, dim3(tiles, G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(),
                            p->d_pod_idx.as<int32_t>(), p->d_tmpl.as<ca_template>(), p->s->t.hot.as<PodHot>(),
@@ -1022,6 +1399,10 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         (void)hipEventElapsedTime(&ms, p->ev[ca_estimate_plan::EV_CHAIN0], p->ev[ca_estimate_plan::EV_CHAIN1]);
         chain_ms += ms;
         for (int32_t g = 0; g < G; g++) if (need[g]) outs[g] = fresh[g];
+        if (rounds == 1) {
+            p->diag.resize(G);
+            for (int32_t g = 0; g < G; g++) p->diag[g] = fresh[g].pad;
+        }
         // walk the lastIndex chain
         int64_t cur = *last_index;
         bool known = true;
@@ -1162,6 +1543,13 @@ int ca_estimate_plan_timings(const ca_estimate_plan* p, float* out, int32_t cap)
     return n;
 }
 
+int ca_estimate_plan_group_ticks(const ca_estimate_plan* p, uint64_t* out, int32_t cap) {
+    if (!p || (cap > 0 && !out)) return CA_EINVAL;
+    const int32_t n = (int32_t)p->diag.size();
+    for (int32_t i = 0; i < n && i < cap; i++) out[i] = p->diag[i];
+    return n;
+}
+
 int ca_estimate_plan_chain_info(const ca_estimate_plan* p, int32_t* lin_sensitive, int32_t* had_success) {
     if (!p) return CA_EINVAL;
     if (lin_sensitive) *lin_sensitive = p->stats.lin_sensitive;
@@ -1179,5 +1567,13 @@ int ca_estimate_batch(ca_mirror* m, const ca_podset* s, const int32_t* group_off
     ca_estimate_plan_destroy(p);
     return rc;
 }
+
+#ifdef CASIM_PROF
+int ca_debug_chain_prof(uint64_t* out, int32_t n_groups) {
+    if (n_groups > 1024) n_groups = 1024;
+    CA_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_prof), sizeof(uint64_t) * 8 * (size_t)n_groups));
+    return CA_OK;
+}
+#endif
 
 }  // extern "C"

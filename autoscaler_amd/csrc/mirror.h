@@ -109,4 +109,10 @@ struct ca_podset {
     ca_mirror* m = nullptr;
     casim::DevPodTable t;
     std::vector<ca_pod_spec> h_pods;   // host copy (flags, used for classification)
+    // Score classes: pods with equal (score_milli_cpu, score_memory) — the only inputs of
+    // calculatePodScore (binpacking_estimator.go:164-193) — share a class, numbered in
+    // first-occurrence order.  d_cls[pod] = class, d_cls_sc[c] = {score_milli_cpu,
+    // score_memory}.  Used by the Estimate bucket sort (estimate.hip).
+    int32_t n_cls = 0;
+    casim::DevBuf d_cls, d_cls_sc;
 };

@@ -10,6 +10,7 @@
 
 #include <cstring>
 #include <mutex>
+#include <unordered_map>
 #include <algorithm>
 
 namespace casim {
@@ -572,6 +573,36 @@ int ca_podset_create(ca_mirror* m, const ca_pod_table* t, ca_podset** out) {
     int rc = s->t.upload(t->pods, t->n_pods, t->terms, t->n_terms, t->reqs, t->n_reqs, t->prefilter_names,
                          t->n_prefilter_names, m->stream);
     if (rc != CA_OK) { delete s; return rc; }
+    {   // score classes
+        struct PairHash {
+            size_t operator()(const std::pair<int64_t, int64_t>& k) const {
+                return std::hash<int64_t>()(k.first * 0x9E3779B97F4A7C15ll ^ k.second);
+            }
+        };
+        std::unordered_map<std::pair<int64_t, int64_t>, int32_t, PairHash> ids;
+        std::vector<int32_t> cls((size_t)t->n_pods);
+        std::vector<int64_t> sc;
+        for (int32_t i = 0; i < t->n_pods; i++) {
+            const auto key = std::make_pair(t->pods[i].score_milli_cpu, t->pods[i].score_memory);
+            auto it = ids.find(key);
+            if (it == ids.end()) {
+                it = ids.emplace(key, (int32_t)ids.size()).first;
+                sc.push_back(key.first);
+                sc.push_back(key.second);
+            }
+            cls[i] = it->second;
+        }
+        s->n_cls = (int32_t)ids.size();
+        if ((rc = s->d_cls.reserve(sizeof(int32_t) * (cls.size() + 1))) != CA_OK ||
+            (rc = s->d_cls_sc.reserve(sizeof(int64_t) * (sc.size() + 2))) != CA_OK) { delete s; return rc; }
+        if (!cls.empty())
+            CA_HIP_CHECK(hipMemcpyAsync(s->d_cls.ptr, cls.data(), sizeof(int32_t) * cls.size(), hipMemcpyHostToDevice,
+                                        m->stream));
+        if (!sc.empty())
+            CA_HIP_CHECK(hipMemcpyAsync(s->d_cls_sc.ptr, sc.data(), sizeof(int64_t) * sc.size(), hipMemcpyHostToDevice,
+                                        m->stream));
+        CA_HIP_CHECK(hipStreamSynchronize(m->stream));
+    }
     *out = s;
     return CA_OK;
 }

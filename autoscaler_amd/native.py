@@ -37,9 +37,10 @@ def load() -> C.CDLL:
     global _LIB
     if _LIB is not None:
         return _LIB
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError(f"libcasim.so not built: {LIB_PATH} missing (run __graft_entry__.build())")
-    lib = C.CDLL(LIB_PATH)
+    path = os.environ.get("CASIM_LIB_PATH", LIB_PATH)    # diagnostics builds only (Makefile: prof)
+    if not os.path.exists(path):
+        raise RuntimeError(f"libcasim.so not built: {path} missing (run __graft_entry__.build())")
+    lib = C.CDLL(path)
     vp, i32, p = C.c_void_p, C.c_int32, C.POINTER
     sigs = {
         "ca_abi_version": ([], C.c_int),
@@ -72,6 +73,7 @@ def load() -> C.CDLL:
         "ca_estimate_plan_stats": ([vp, p(i32), p(C.c_float), p(C.c_float), p(C.c_float)], C.c_int),
         "ca_estimate_plan_chain_info": ([vp, p(i32), p(i32)], C.c_int),
         "ca_estimate_plan_timings": ([vp, p(C.c_float), i32], C.c_int),
+        "ca_estimate_plan_group_ticks": ([vp, p(C.c_uint64), i32], C.c_int),
         "ca_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, p(i32), vp, vp], C.c_int),
         "ca_removal_stats": ([vp, p(i32), p(C.c_float), p(C.c_float)], C.c_int),
         "ca_removal_timings": ([vp, p(C.c_float), i32], C.c_int),
@@ -97,7 +99,8 @@ def exported_symbols() -> list[str]:
         "ca_mirror_fork", "ca_mirror_revert", "ca_mirror_commit", "ca_mirror_node_count", "ca_mirror_pod_node",
         "ca_mirror_node_pods", "ca_podset_create", "ca_podset_destroy", "ca_fits_any_node", "ca_check_predicates",
         "ca_fits_matrix", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
-        "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_estimate_plan_timings", "ca_find_nodes_to_remove",
+        "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_estimate_plan_timings",
+        "ca_estimate_plan_group_ticks", "ca_find_nodes_to_remove",
         "ca_removal_stats", "ca_removal_timings",
     ]
 
@@ -327,6 +330,14 @@ class EstimatePlan:
         return {"rounds": r.value, "chain_ms": a.value, "sort_ms": b.value, "total_ms": c.value,
                 "lin_sensitive": sens.value, "had_success": succ.value,
                 "phases": {k: float(v) for k, v in zip(names, t)}}
+
+    def group_ticks(self) -> np.ndarray:
+        """Per group of the last run: (chain device time in us, single-pod steps)."""
+        n = self.lib.ca_estimate_plan_group_ticks(self.h, None, 0)
+        a = np.zeros(max(n, 0), np.uint64)
+        if n > 0:
+            self.lib.ca_estimate_plan_group_ticks(self.h, a.ctypes.data_as(C.POINTER(C.c_uint64)), n)
+        return np.stack([(a & 0xFFFFFFFF).astype(np.float64) / 100.0, (a >> 32).astype(np.float64)], axis=1)
 
     def close(self) -> None:
         if self.h:

@@ -99,9 +99,14 @@ C2_MEM_PER_CORE = [2, 4, 8]
 
 
 def c2(n_pods: int = 50_000, n_groups: int = 100, n_existing: int = 1000, max_nodes: int = 1000,
-       seed: int = 42, pods_per_controller: int = 100) -> EstimateWorkload:
+       seed: int = 42, pods_per_controller: int = 100, n_random_shapes: int = 0) -> EstimateWorkload:
+    """C2.  n_random_shapes > 0 replaces the 64-shape catalog by that many
+    random (cpu, mem) shapes (test variant: many score classes, cross-shape ties allowed)."""
     rng = np.random.default_rng(seed)
     shapes = [(c, m) for c in C2_CPU for m in C2_MEM]
+    if n_random_shapes > 0:
+        shapes = list({(int(c), int(m) * MI) for c, m in zip(rng.integers(1, 8000, n_random_shapes),
+                                                                rng.integers(1, 32768, n_random_shapes))})
     n_ctrl = max(1, (n_pods + pods_per_controller - 1) // pods_per_controller)
     ctrl_shape = rng.integers(0, len(shapes), n_ctrl)
     shape_of_pod = np.repeat(ctrl_shape, pods_per_controller)[:n_pods]
@@ -128,10 +133,11 @@ def c2(n_pods: int = 50_000, n_groups: int = 100, n_existing: int = 1000, max_no
         offs.append(offs[-1] + len(sel))
         # H2 check: distinct shapes tying in float64 score for this template
         sc = {}
-        for (c, m) in shapes:
-            s = c / acpu + m / amem
-            sc.setdefault(s, set()).add((c, m))
-        ties += sum(1 for v in sc.values() if len(v) > 1)
+        if n_random_shapes <= 0:
+            for (c, m) in shapes:
+                s = c / acpu + m / amem
+                sc.setdefault(s, set()).add((c, m))
+            ties += sum(1 for v in sc.values() if len(v) > 1)
     pod_idx = np.concatenate(idx_parts) if idx_parts else np.zeros(0, np.int32)
     existing = abi.empty_nodes(n_existing)
     existing["alloc_milli_cpu"] = 16000

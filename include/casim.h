@@ -333,6 +333,10 @@ int ca_estimate_plan_stats(const ca_estimate_plan* p, int32_t* rounds, float* ch
  * Writes min(cap, 7) values; returns 7. */
 int ca_estimate_plan_timings(const ca_estimate_plan* p, float* out, int32_t cap);
 int ca_estimate_plan_chain_info(const ca_estimate_plan* p, int32_t* lin_sensitive, int32_t* had_success);
+/* Diagnostics of the last run's first chain launch, one entry per group: the chain's
+ * device wall-clock ticks (100 MHz) in bits 0-31, the number of single-pod steps (pods
+ * not placed by the closed-form run path) in bits 32-63.  Returns the group count. */
+int ca_estimate_plan_group_ticks(const ca_estimate_plan* p, uint64_t* out, int32_t cap);
 
 /* ---- removal simulator ------------------------------------------------------- */
 /* FindNodesToRemove(candidates, destinations) with legacy semantics (canPersist=false).

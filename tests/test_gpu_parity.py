@@ -101,8 +101,10 @@ def test_fits_any_node_random(seed, oracle):
 # --------------------------------------------------------------------------
 # estimator
 # --------------------------------------------------------------------------
+@pytest.mark.parametrize("sort", ["bucket", "merge"])
 @pytest.mark.parametrize("seed", range(16))
-def test_estimate_random(seed, oracle):
+def test_estimate_random(seed, sort, oracle, monkeypatch):
+    monkeypatch.setenv("CASIM_SORT", sort)
     rng, nodes, pods, templates, groups = _estimate_inputs(seed)
     table, node_recs, tm, off, pod_idx = _encode_estimate(nodes, pods, templates, groups)
     max_nodes = rng.choice([0, 0, 3, 10])
@@ -200,9 +202,10 @@ def test_estimate_runs_random(seed, batch, oracle, monkeypatch):
     ("C2-unlimited", W.c2(n_pods=1500, n_groups=8, n_existing=20, max_nodes=0)),
     ("C2-medium", W.c2(n_pods=20000, n_groups=20, n_existing=300)),
 ])
-@pytest.mark.parametrize("batch", ["1", "0"])
-def test_estimate_workloads(name, w, batch, oracle, monkeypatch):
+@pytest.mark.parametrize("batch,sort", [("1", "bucket"), ("0", "bucket"), ("1", "merge")])
+def test_estimate_workloads(name, w, batch, sort, oracle, monkeypatch):
     monkeypatch.setenv("CASIM_RUN_BATCH", batch)
+    monkeypatch.setenv("CASIM_SORT", sort)
     outs = []
     for b in (oracle.OracleState(), _mirror()):
         W.load_estimate(b, w)
@@ -214,6 +217,36 @@ def test_estimate_workloads(name, w, batch, oracle, monkeypatch):
     assert o.last_index == g.last_index
     if name == "C1":
         assert int(g.results[0]["node_count"]) == 125 and int(g.results[0]["n_scheduled"]) == 1000
+
+
+@pytest.mark.parametrize("shapes", [300, 3000, 6000])
+def test_estimate_many_score_classes(shapes, oracle):
+    """Random (cpu, mem) shapes: > 256 score classes take two radix passes, > 4096 take the
+    comparison sort; cross-shape score ties (H2) resolve by list position on both."""
+    w = W.c2(n_pods=8000, n_groups=10, n_existing=30, pods_per_controller=1, n_random_shapes=shapes, seed=shapes)
+    outs = []
+    for b in (oracle.OracleState(), _mirror()):
+        W.load_estimate(b, w)
+        outs.append(b.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, 3))
+    o, g = outs
+    assert np.array_equal(o.results, g.results)
+    assert np.array_equal(o.sched_pod, g.sched_pod)
+    assert np.array_equal(o.sched_node, g.sched_node)
+    assert o.last_index == g.last_index
+
+
+def test_estimate_full_c2_parity(oracle):
+    """BASELINE configs[1] at full size (50k pods x 100 groups): bit-exact vs the oracle."""
+    w = W.c2()
+    outs = []
+    for b in (oracle.OracleState(), _mirror()):
+        W.load_estimate(b, w)
+        outs.append(b.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, 0))
+    o, g = outs
+    assert np.array_equal(o.results, g.results)
+    assert np.array_equal(o.sched_pod, g.sched_pod)
+    assert np.array_equal(o.sched_node, g.sched_node)
+    assert o.last_index == g.last_index
 
 
 def test_estimate_full_c2_properties():

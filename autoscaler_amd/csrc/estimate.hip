@@ -67,7 +67,7 @@ struct alignas(16) GroupMeta {
     int32_t tmpl;                  // template index
     uint32_t tflags;               // NF_* of the template
     int32_t moff;                  // offset of the group's 64-pod head masks
-    int32_t toff;                  // offset of the group's 1024-pod tile counters
+    int32_t toff;                  // unused (was: compaction tile counters)
     int32_t hoff;                  // offset of the group's radix histograms [256][rtiles]
     int32_t rtiles;                // radix tiles of the group (bucket sort)
     int32_t pad;
@@ -78,9 +78,17 @@ struct alignas(16) ChainOut {
     int32_t node_count, n_sched, nodes_added, lin;
     int32_t lout, status, sensitive, had_success;
     uint64_t evals;
-    uint64_t pad;
+    uint64_t pad;        // diagnostics (ca_estimate_plan_group_ticks)
+    int32_t nseg;        // run-placement segments written to the group's segment list
+    int32_t pad2[3];
 };
-static_assert(sizeof(ChainOut) == 48, "ChainOut");
+static_assert(sizeof(ChainOut) == 64, "ChainOut");
+
+// A run placement: stream positions [src, src+len) were scheduled as outputs
+// [dst, dst+len) of the group (k_copy_segments fills sched_pod from them).
+struct alignas(16) Seg {
+    int32_t dst, src, len, pad;
+};
 
 constexpr int TILE = 1024;
 
@@ -220,7 +228,8 @@ __device__ inline bool batchable(const PodHot& p, uint32_t sf) {
 
 __global__ void __launch_bounds__(256) k_emit_stream(const GroupMeta* __restrict__ groups, const SortItem* __restrict__ src,
                                                     const int32_t* __restrict__ pod_idx, const PodHot* __restrict__ ph,
-                                                    StreamPod* __restrict__ out, uint64_t* __restrict__ heads) {
+                                                    StreamPod* __restrict__ out, int32_t* __restrict__ spod,
+                                                    uint64_t* __restrict__ heads) {
     const GroupMeta gm = groups[blockIdx.y];
     const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     bool head = true;
@@ -239,6 +248,7 @@ __global__ void __launch_bounds__(256) k_emit_stream(const GroupMeta* __restrict
         sp.pod = pidx;
         sp.flags = it.flags | (head ? SF_HEAD : 0u) | (bat ? SF_BATCH : 0u);
         out[gm.off + i] = sp;
+        spod[gm.off + i] = pidx;
     }
     const uint64_t hb = __ballot(head);
     if ((threadIdx.x & 63) == 0 && i < gm.count) heads[gm.moff + (i >> 6)] = hb;
@@ -439,8 +449,8 @@ __global__ void __launch_bounds__(256) k_emit_bucket(const GroupMeta* __restrict
                                                     const PodHot* __restrict__ ph, const ca_pod_spec* __restrict__ specs,
                                                     const ca_selector_term* __restrict__ terms,
                                                     const ca_selector_req* __restrict__ reqs,
-                                                    StreamPod* __restrict__ out, uint64_t* __restrict__ heads,
-                                                    uint32_t* __restrict__ group_unsup) {
+                                                    StreamPod* __restrict__ out, int32_t* __restrict__ spod,
+                                                    uint64_t* __restrict__ heads, uint32_t* __restrict__ group_unsup) {
     const GroupMeta gm = groups[blockIdx.y];
     const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     const int lane = threadIdx.x & 63;
@@ -473,6 +483,7 @@ __global__ void __launch_bounds__(256) k_emit_bucket(const GroupMeta* __restrict
         sp.pod = pidx;
         sp.flags = sf | (head ? SF_HEAD : 0u) | (bat ? SF_BATCH : 0u);
         out[gm.off + i] = sp;
+        spod[gm.off + i] = pidx;
         if (sf & SF_UNSUP) atomicOr(&group_unsup[blockIdx.y], 1u);
     }
     const uint64_t hb = __ballot(head);
@@ -607,7 +618,8 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
     const ca_template* __restrict__ tmpls, const ca_pod_spec* __restrict__ specs, const PodHot* __restrict__ ph,
     const int32_t* __restrict__ lin_arr, const uint8_t* __restrict__ need, const uint32_t* __restrict__ group_unsup,
     int32_t n_base, int32_t max_nodes, int32_t kcap, int32_t use_ports, int32_t use_scalar, int32_t batch_runs,
-    int32_t* __restrict__ assign, ChainOut* __restrict__ outs) {
+    int32_t* __restrict__ sched_pod, int32_t* __restrict__ sched_node, Seg* __restrict__ segs,
+    ChainOut* __restrict__ outs) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int g = blockIdx.x;
     if (!need[g]) return;
@@ -625,6 +637,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
     ChainOut res;
     res.node_count = 0; res.n_sched = 0; res.nodes_added = 0; res.lin = lin; res.lout = lin;
     res.status = CA_OK; res.sensitive = 0; res.had_success = 0; res.evals = 0; res.pad = 0;
+    res.nseg = 0; res.pad2[0] = res.pad2[1] = res.pad2[2] = 0;
     if (group_unsup[g]) {
         res.status = CA_EUNSUPPORTED;
         if (lane == 0) outs[g] = res;
@@ -653,7 +666,12 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
     const int32_t P = gm.count;
     const StreamPod* gs = stream + gm.off;
     const uint64_t* hm = heads + gm.moff;
-    int32_t* ga = assign + gm.off;
+    // outputs in processing order (binpacking_estimator.go:143): the i-th scheduled pod of
+    // the group and its new-node ordinal go to index i; placements happen in stream order
+    Seg* gseg = segs + gm.off;
+    int32_t nseg = 0;
+    int32_t* so_pod = sched_pod + gm.off;
+    int32_t* so_node = sched_node ? sched_node + gm.off : nullptr;
     // Stream double buffer: lane l holds entry (wbase + l) in `cur` and (wbase + 64 + l)
     // in `nxt`.  Single-pod placements are kept in the lane of their stream position and
     // stored when the window moves on, so no step waits on a store (vmcnt counts both).
@@ -661,7 +679,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
     StreamPod cur = {}, nxt = {};
     if (lane < P) cur = gs[lane];
     if (64 + lane < P) nxt = gs[64 + lane];
-    int32_t out_node = -1;
+    int32_t out_node = -1, out_idx = 0;
     bool pend = false;
     bool stop = false;
 
@@ -686,7 +704,10 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
     int32_t pos = 0;
     while (pos < P && !stop) {
         if (pos >= wbase + 64) {
-            if (pend) ga[wbase + lane] = out_node;
+            if (pend) {
+                so_pod[out_idx] = cur.pod;
+                if (so_node) so_node[out_idx] = out_node;
+            }
             pend = false;
             if (pos < wbase + 128) {
                 cur = nxt;
@@ -758,7 +779,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                                 r.used = 1;
                                 R[one] = r;
                             }
-                            for (int32_t t = lane; t < n_one; t += 64) ga[pos + done + t] = one;
+                            if (so_node) for (int32_t t = lane; t < n_one; t += 64) so_node[nsched + t] = one;
                             L = n_base + one + 1;
                             if (L >= len) L -= len;
                             note_success();
@@ -786,12 +807,12 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                             // level, and the placements of those revolutions are the list
                             // repeated: placement t of the level goes to ALIVE[t % na].
                             int32_t got = 0, r = 1, last = -1;
-                            int32_t* gdst = ga + pos + done;
+                            int32_t* gdst = so_node ? so_node + nsched : nullptr;
                             for (;;) {
                                 const int64_t avail = (int64_t)(cmin - r + 1) * na;
                                 const bool fin = got + avail >= n;
                                 const int32_t cnt = fin ? n - got : (int32_t)avail;
-                                {
+                                if (gdst) {
                                     const int32_t st = 64 % na;
                                     int32_t q = lane % na;
                                     for (int32_t t = lane; t < cnt; t += 64) {
@@ -854,6 +875,8 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                             placed = n;
                         }
                     }
+                    if (lane == 0 && placed > 0) gseg[nseg] = Seg{nsched, pos + done, placed, 0};
+                    nseg += placed > 0 ? 1 : 0;
                     nsched += placed;
                     done += placed;
                     if (done == RN) break;
@@ -934,7 +957,9 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                             SC[(size_t)sc * kcap + node] = wsub(tp.node.alloc_scalar[sc], tp.used_scalar[sc]);
                         }
                     }
-                    for (int32_t t = lane; t < placed2; t += 64) ga[pos + done + t] = k0 + t / ct;
+                    if (so_node) for (int32_t t = lane; t < placed2; t += 64) so_node[nsched + t] = k0 + t / ct;
+                    if (lane == 0 && placed2 > 0) gseg[nseg] = Seg{nsched, pos + done, placed2, 0};
+                    nseg += placed2 > 0 ? 1 : 0;
                     if (ct >= 2 && placed2 >= 2) {
                         if (!first_success) { first_success = true; sensitive = k0 + 1 >= 2; }
                         L = 0;       // n_base + (last row) + 1 == len
@@ -1072,7 +1097,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
             r.used = 1;
             R[found] = r;
         }
-        if (lane == sl) { out_node = found; pend = true; }
+        if (lane == sl) { out_node = found; out_idx = nsched; pend = true; }
         if (sf & SF_SCALAR) {
             if (lane < CA_MAX_SCALAR) {
                 const size_t ix = (size_t)lane * kcap + found;
@@ -1085,7 +1110,10 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
         nsched++;
         __builtin_amdgcn_wave_barrier();
     }
-    if (pend) ga[wbase + lane] = out_node;
+    if (pend) {
+        so_pod[out_idx] = cur.pod;
+        if (so_node) so_node[out_idx] = out_node;
+    }
     // newNodesWithPods
     int32_t cnt = 0;
     for (int32_t j = lane; j < k; j += 64) cnt += R[j].used;
@@ -1098,6 +1126,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
         res.sensitive = sensitive ? 1 : 0;
         res.had_success = first_success ? 1 : 0;
         res.evals = evals;
+        res.nseg = nseg;
         res.pad = (uint64_t)(uint32_t)(wall_clock64() - t_begin) | ((uint64_t)n_single << 32);
         outs[g] = res;
 #ifdef CASIM_PROF
@@ -1107,62 +1136,27 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
     }
 }
 
-// 5. scheduled pods in processing order: compact assign[] per group ------------
-// (binpacking_estimator.go:143 returns the scheduled pods in the order they were placed,
-// which is stream order.)  Two passes over 1024-position tiles: count, then scatter.
-constexpr int CTILE = 1024;
-
-__global__ void __launch_bounds__(256) k_tile_count(const GroupMeta* __restrict__ groups, const int32_t* __restrict__ assign,
-                                                   int32_t* __restrict__ tcount) {
+// 5. scheduled pods of the run placements: sched_pod[dst + t] = stream pod at src + t.
+// Output i of a group lies in the last segment with dst <= i, or was written directly
+// by the chain (single-pod placements).
+constexpr int CPY_PER_BLOCK = 2048;
+__global__ void __launch_bounds__(256) k_copy_segments(const GroupMeta* __restrict__ groups,
+                                                      const ChainOut* __restrict__ outs, const Seg* __restrict__ segs,
+                                                      const int32_t* __restrict__ spod, int32_t* __restrict__ sched_pod) {
     const GroupMeta gm = groups[blockIdx.y];
-    const int32_t base = (int32_t)blockIdx.x * CTILE;
-    if (base >= gm.count) return;
-    __shared__ int32_t wsum[4];
-    int32_t c = 0;
-    for (int t = threadIdx.x; t < CTILE; t += 256) {
-        const int32_t i = base + t;
-        c += (i < gm.count && assign[gm.off + i] >= 0) ? 1 : 0;
-    }
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) tcount[gm.toff + blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-}
-
-__global__ void __launch_bounds__(CTILE) k_tile_scatter(const GroupMeta* __restrict__ groups, const int32_t* __restrict__ assign,
-                                                      const StreamPod* __restrict__ stream, const int32_t* __restrict__ tcount,
-                                                      int32_t* __restrict__ sched_pod, int32_t* __restrict__ sched_node) {
-    const GroupMeta gm = groups[blockIdx.y];
-    const int32_t base = (int32_t)blockIdx.x * CTILE;
-    if (base >= gm.count) return;
-    __shared__ int32_t wsum[CTILE / 64];
-    __shared__ int32_t prefix, total;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (w == 0) {   // tiles before this one, and the group's scheduled count
-        const int32_t nt = (gm.count + CTILE - 1) / CTILE;
-        int32_t s = 0, a = 0;
-        for (int32_t t = lane; t < nt; t += 64) {
-            const int32_t c = tcount[gm.toff + t];
-            a += c;
-            if (t < (int32_t)blockIdx.x) s += c;
+    const ChainOut o = outs[blockIdx.y];
+    const int32_t base = (int32_t)blockIdx.x * CPY_PER_BLOCK;
+    if (o.status != CA_OK || base >= o.n_sched || o.nseg == 0) return;
+    const Seg* gs = segs + gm.off;
+    for (int32_t i = base + (int32_t)threadIdx.x; i < min(base + CPY_PER_BLOCK, o.n_sched); i += blockDim.x) {
+        int32_t lo = 0, hi = o.nseg;               // first segment with dst > i
+        while (lo < hi) {
+            const int32_t mid = (lo + hi) >> 1;
+            if (gs[mid].dst <= i) lo = mid + 1; else hi = mid;
         }
-        for (int o = 32; o > 0; o >>= 1) { s += __shfl_xor(s, o, 64); a += __shfl_xor(a, o, 64); }
-        if (lane == 0) { prefix = s; total = a; }
-    }
-    const int32_t i = base + (int32_t)threadIdx.x;
-    const int32_t a = i < gm.count ? assign[gm.off + i] : -1;
-    const uint64_t bm = __ballot(a >= 0);
-    if (lane == 0) wsum[w] = __builtin_popcountll(bm);
-    __syncthreads();
-    if (a >= 0) {
-        int32_t o = prefix + mbcnt(bm);
-        for (int v = 0; v < w; v++) o += wsum[v];
-        sched_pod[gm.off + o] = stream[gm.off + i].pod;
-        if (sched_node) sched_node[gm.off + o] = a;
-    }
-    if (i < gm.count && i >= total) {     // entries past n_scheduled read back as -1
-        sched_pod[gm.off + i] = -1;
-        if (sched_node) sched_node[gm.off + i] = -1;
+        if (lo == 0) continue;
+        const Seg sg = gs[lo - 1];
+        if (i < sg.dst + sg.len) sched_pod[gm.off + i] = spod[gm.off + sg.src + (i - sg.dst)];
     }
 }
 
@@ -1181,7 +1175,7 @@ struct ca_estimate_plan {
     std::vector<GroupMeta> h_meta;
     bool use_ports = false, use_scalar = false;
     int32_t n_masks = 0, n_tiles = 0;
-    DevBuf d_meta, d_pod_idx, d_tmpl, d_sortA, d_sortB, d_stream, d_heads, d_assign, d_tcount, d_unsup, d_lin, d_need,
+    DevBuf d_meta, d_pod_idx, d_tmpl, d_sortA, d_sortB, d_stream, d_spod, d_seg, d_heads, d_unsup, d_lin, d_need,
         d_out, d_sched_pod, d_sched_node, d_crank, d_hist;
     int32_t n_hist = 0, max_rtiles = 0;
     bool bucket = false;           // bucket sort over score classes (podset has <= CLS_MAX classes)
@@ -1238,7 +1232,6 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
         p->n_hist += 256 * gm.rtiles;
         p->max_rtiles = std::max(p->max_rtiles, gm.rtiles);
         p->n_masks += (c + 63) / 64;
-        p->n_tiles += (c + CTILE - 1) / CTILE;
         p->max_count = std::max(p->max_count, c);
         for (int w = 0; w < CA_PORT_WORDS; w++) if (t.used_ports[w]) p->use_ports = true;
         for (int i = 0; i < CA_MAX_SCALAR; i++)
@@ -1261,8 +1254,8 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     if ((rc = p->d_sortB.reserve(sizeof(SortItem) * tot)) != CA_OK) return rc;
     if ((rc = p->d_stream.reserve(sizeof(StreamPod) * tot)) != CA_OK) return rc;
     if ((rc = p->d_heads.reserve(sizeof(uint64_t) * (size_t)std::max(p->n_masks, 1))) != CA_OK) return rc;
-    if ((rc = p->d_assign.reserve(sizeof(int32_t) * tot)) != CA_OK) return rc;
-    if ((rc = p->d_tcount.reserve(sizeof(int32_t) * (size_t)std::max(p->n_tiles, 1))) != CA_OK) return rc;
+    if ((rc = p->d_spod.reserve(sizeof(int32_t) * tot)) != CA_OK) return rc;
+    if ((rc = p->d_seg.reserve(sizeof(Seg) * tot)) != CA_OK) return rc;
     if ((rc = p->d_unsup.reserve(sizeof(uint32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
     if ((rc = p->d_lin.reserve(sizeof(int32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
     if ((rc = p->d_need.reserve((size_t)std::max(G, 1))) != CA_OK) return rc;
@@ -1306,7 +1299,8 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     if (lds > 160 * 1024) return CA_EUNSUPPORTED;   // HBM-backed variant is future work
     CA_HIP_CHECK(hipMemsetAsync(p->d_unsup.ptr, 0, sizeof(uint32_t) * G, st));
     if (p->total > 0) {   // entries past n_scheduled read back as -1
-        CA_HIP_CHECK(hipMemsetAsync(p->d_assign.ptr, 0xFF, sizeof(int32_t) * p->total, st));
+        CA_HIP_CHECK(hipMemsetAsync(p->d_sched_pod.ptr, 0xFF, sizeof(int32_t) * p->total, st));
+        if (sched_node) CA_HIP_CHECK(hipMemsetAsync(p->d_sched_node.ptr, 0xFF, sizeof(int32_t) * p->total, st));
     }
     const char* rb_env = getenv("CASIM_RUN_BATCH");
     const int32_t batch_runs = (rb_env && rb_env[0] == '0') ? 0 : 1;
@@ -1344,8 +1338,8 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         hipLaunchKernelGGL(k_emit_bucket, dim3(blocks, G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(), a,
                            p->d_pod_idx.as<int32_t>(), p->d_tmpl.as<ca_template>(), p->s->t.hot.as<PodHot>(),
                            p->s->t.spec.as<ca_pod_spec>(), p->s->t.terms.as<ca_selector_term>(),
-                           p->s->t.reqs.as<ca_selector_req>(), p->d_stream.as<StreamPod>(), p->d_heads.as<uint64_t>(),
-                           p->d_unsup.as<uint32_t>());
+                           p->s->t.reqs.as<ca_selector_req>(), p->d_stream.as<StreamPod>(), p->d_spod.as<int32_t>(),
+                           p->d_heads.as<uint64_t>(), p->d_unsup.as<uint32_t>());
         CA_HIP_CHECK(hipGetLastError());
     } else if (p->total > 0) {
         const int32_t tiles = (p->max_count + TILE - 1) / TILE;
@@ -1366,7 +1360,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], st));
         hipLaunchKernelGGL(k_emit_stream, dim3(blocks, G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(), a,
                            p->d_pod_idx.as<int32_t>(), p->s->t.hot.as<PodHot>(), p->d_stream.as<StreamPod>(),
-                           p->d_heads.as<uint64_t>());
+                           p->d_spod.as<int32_t>(), p->d_heads.as<uint64_t>());
         CA_HIP_CHECK(hipGetLastError());
     }
     CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_EMIT], st));
@@ -1388,8 +1382,9 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                            p->d_stream.as<StreamPod>(), p->d_heads.as<uint64_t>(), p->d_tmpl.as<ca_template>(),
                            p->s->t.spec.as<ca_pod_spec>(), p->s->t.hot.as<PodHot>(), p->d_lin.as<int32_t>(),
                            p->d_need.as<uint8_t>(), p->d_unsup.as<uint32_t>(), n_base, lim->max_nodes, kcap,
-                           p->use_ports ? 1 : 0, p->use_scalar ? 1 : 0, batch_runs, p->d_assign.as<int32_t>(),
-                           p->d_out.as<ChainOut>());
+                           p->use_ports ? 1 : 0, p->use_scalar ? 1 : 0, batch_runs,
+                           p->d_sched_pod.as<int32_t>(), sched_node ? p->d_sched_node.as<int32_t>() : nullptr,
+                           p->d_seg.as<Seg>(), p->d_out.as<ChainOut>());
         CA_HIP_CHECK(hipGetLastError());
         CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN1], st));
         std::vector<ChainOut> fresh(G);
@@ -1439,15 +1434,11 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         }
         if (rounds > G + 2) { set_last_error("estimate speculation did not converge"); return CA_EDEVICE; }
     }
-    // results: compact the per-position assignments into processing order
+    // results: the chains wrote single placements directly; fill the run placements
     if (p->total > 0) {
-        const int32_t tiles = (p->max_count + CTILE - 1) / CTILE;
-        hipLaunchKernelGGL(k_tile_count, dim3(tiles, G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(),
-                           p->d_assign.as<int32_t>(), p->d_tcount.as<int32_t>());
-        CA_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(k_tile_scatter, dim3(tiles, G), dim3(CTILE), 0, st, p->d_meta.as<GroupMeta>(),
-                           p->d_assign.as<int32_t>(), p->d_stream.as<StreamPod>(), p->d_tcount.as<int32_t>(),
-                           p->d_sched_pod.as<int32_t>(), sched_node ? p->d_sched_node.as<int32_t>() : nullptr);
+        hipLaunchKernelGGL(k_copy_segments, dim3((p->max_count + CPY_PER_BLOCK - 1) / CPY_PER_BLOCK, G), dim3(256), 0, st,
+                           p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
+                           p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>());
         CA_HIP_CHECK(hipGetLastError());
     }
     CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_COMPACT], st));

@@ -7,7 +7,9 @@ C2 workload of SURVEY.md §8d: 50k heterogeneous pending pods x 100 node-group
 templates, resource-fit only, maxNodes = 1000 (the --max-nodes-per-scaleup
 default), 1000 existing nodes, inputs resident in HBM.  The step runs the device
 sort, the per-group First-Fit-Decreasing chains and the lastIndex fix-up, and
-copies every group's result (count, scheduled pods, node assignment) to the host.
+copies every group's result to the host: what Estimate returns (estimator.go:40-42) —
+the node count and the scheduled pods in placement order (the per-pod new-node
+ordinal, which Go does not return, stays on the device unless --with-nodes).
 
 value = filter-chain evaluations the reference algorithm performs in that batch
 (every RunFilterPlugins call, counted exactly) / wall time.  With --gpus N each
@@ -55,6 +57,9 @@ def parse():
     ap.add_argument("--existing", type=int, default=1000)
     ap.add_argument("--max-nodes", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--with-nodes", action="store_true",
+                    help="also copy each scheduled pod's new-node ordinal to the host (not part of Estimate's "
+                         "Go return value (int, []*Pod), estimator.go:40-42)")
     ap.add_argument("--cpu-groups", type=int, default=100, help="groups in the bounded CPU-baseline sample")
     return ap.parse_args()
 
@@ -94,7 +99,7 @@ def main():
     L0 = 0
 
     def run_block(lin):
-        out = plan.run(w.max_nodes, lin, copy=False)
+        out = plan.run(w.max_nodes, lin, want_nodes=args.with_nodes, copy=False)
         st = plan.stats()
         return (out, st), out.last_index, st["lin_sensitive"], st["had_success"]
 

@@ -509,31 +509,13 @@ __device__ inline int64_t rl64(int64_t v, int lane) {
 }
 __device__ inline int32_t rl32(int32_t v, int lane) { return (int32_t)__builtin_amdgcn_readlane((uint32_t)v, lane); }
 
-__device__ inline int64_t wave_max64(int64_t v) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const int64_t x = __shfl_xor(v, o, 64);
-        v = x > v ? x : v;
-    }
-    return v;
-}
-__device__ inline int32_t wave_max32(int32_t v) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const int32_t x = __shfl_xor(v, o, 64);
-        v = x > v ? x : v;
-    }
-    return v;
-}
-__device__ inline int32_t wave_min32(int32_t v) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const int32_t x = __shfl_xor(v, o, 64);
-        v = x < v ? x : v;
-    }
-    return v;
-}
-__device__ inline int64_t wave_sum64(int64_t v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
+// wavefront reductions (device-library DPP reductions; all 64 lanes active at every call site)
+extern "C" __device__ long long __ockl_wfred_add_i64(long long);
+extern "C" __device__ long long __ockl_wfred_max_i64(long long);
+__device__ inline int64_t wave_max64(int64_t v) { return __ockl_wfred_max_i64(v); }
+__device__ inline int32_t wave_max32(int32_t v) { return __ockl_wfred_max_i32(v); }
+__device__ inline int32_t wave_min32(int32_t v) { return __ockl_wfred_min_i32(v); }
+__device__ inline int64_t wave_sum64(int64_t v) { return __ockl_wfred_add_i64(v); }
 __device__ inline int32_t mbcnt(uint64_t m) {
     return (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -576,6 +558,41 @@ __device__ inline int32_t rec_copies(const NodeRec& r, int64_t pcpu, int64_t pme
         c = min(c, dim_copies(r.cpu, pcpu, c));
         c = min(c, dim_copies(r.mem, pmem, c));
         c = min(c, dim_copies(r.eph, peph, c));
+    }
+    return c;
+}
+
+// rec_copies for the rows of one run: the pod's reciprocals are computed once, each
+// quotient comes from float32 (rel. error < 2^-21, so within one of floor(free/req)
+// while the cap is <= 2^20) and one multiply-compare step each way makes it exact.
+struct RunDiv {
+    int64_t req[3];
+    float rcp[3];
+};
+__device__ inline RunDiv run_div(int64_t pcpu, int64_t pmem, int64_t peph) {
+    RunDiv d;
+    d.req[0] = pcpu; d.req[1] = pmem; d.req[2] = peph;
+    // req == 0: rcp = +inf, so the float quotient is inf (or NaN for free == 0) and
+    // fminf(., cap) gives cap — a zero request passes whenever free >= 0
+    for (int i = 0; i < 3; i++) d.rcp[i] = d.req[i] > 0 ? 1.0f / (float)d.req[i] : __builtin_inff();
+    return d;
+}
+// branch-free (no exec-mask juggling in the row loop)
+__device__ inline int32_t dim_copies_fast(int64_t free_, int64_t req, float rcp, int32_t cap) {
+    const uint64_t f = free_ < 0 ? 0ull : (uint64_t)free_, r = (uint64_t)req;
+    const float ff = (float)(uint32_t)(f >> 32) * 4294967296.0f + (float)(uint32_t)f;
+    uint32_t q = (uint32_t)fminf(ff * rcp, (float)cap);
+    const bool dn = (uint64_t)q * r > f;
+    const bool up = !dn && q < (uint32_t)cap && (uint64_t)(q + 1) * r <= f;
+    q = q - (dn ? 1u : 0u) + (up ? 1u : 0u);
+    return free_ < 0 ? 0 : (int32_t)q;
+}
+__device__ inline int32_t rec_copies_run(const NodeRec& r, const RunDiv& d, bool zero, int32_t cap) {
+    int32_t c = max(0, min(r.pods, cap));
+    if (!zero) {     // uniform
+        c = min(c, dim_copies_fast(r.cpu, d.req[0], d.rcp[0], max(c, 1)));
+        c = min(c, dim_copies_fast(r.mem, d.req[1], d.rcp[1], max(c, 1)));
+        c = min(c, dim_copies_fast(r.eph, d.req[2], d.rcp[2], max(c, 1)));
     }
     return c;
 }
@@ -753,11 +770,32 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                         } else {
                             PROF_T(t_ca);
                             int32_t na = 0, a1 = -1;
-                            for (int32_t j = lane; j < k; j += 64) {
-                                const int32_t c = rec_copies(R[j], pcpu, pmem, peph, zero, rem);
-                                CAPA[j] = c;
-                                S += c;
-                                if (c > 0) { na++; a1 = j; }
+                            if (rem <= (1 << 20)) {
+                                const RunDiv dv = run_div(pcpu, pmem, peph);
+                                int32_t j = lane;
+                                for (; j + 64 < k; j += 128) {          // two rows in flight
+                                    const NodeRec r0 = R[j], r1 = R[j + 64];
+                                    const int32_t c0 = rec_copies_run(r0, dv, zero, rem);
+                                    const int32_t c1 = rec_copies_run(r1, dv, zero, rem);
+                                    CAPA[j] = c0;
+                                    CAPA[j + 64] = c1;
+                                    S += c0 + c1;
+                                    if (c0 > 0) { na++; a1 = j; }
+                                    if (c1 > 0) { na++; a1 = j + 64; }
+                                }
+                                if (j < k) {
+                                    const int32_t c = rec_copies_run(R[j], dv, zero, rem);
+                                    CAPA[j] = c;
+                                    S += c;
+                                    if (c > 0) { na++; a1 = j; }
+                                }
+                            } else {
+                                for (int32_t j = lane; j < k; j += 64) {
+                                    const int32_t c = rec_copies(R[j], pcpu, pmem, peph, zero, rem);
+                                    CAPA[j] = c;
+                                    S += c;
+                                    if (c > 0) { na++; a1 = j; }
+                                }
                             }
                             S = wave_sum64(S);
                             nalive = (int32_t)wave_sum64(na);
@@ -1117,7 +1155,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
     // newNodesWithPods
     int32_t cnt = 0;
     for (int32_t j = lane; j < k; j += 64) cnt += R[j].used;
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    cnt = __ockl_wfred_add_i32(cnt);
     if (lane == 0) {
         res.node_count = cnt;
         res.n_sched = nsched;

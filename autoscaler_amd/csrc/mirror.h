@@ -43,8 +43,8 @@ struct DevPodTable {
 // Per-mirror scratch of ca_find_nodes_to_remove, kept across calls (no per-call
 // hipMalloc); host staging is page-locked.
 struct SweepScratch {
-    DevBuf in, lin, need, out, todo, tab;
-    HostBuf h_in, h_tab, h_out, h_todo, h_lin;
+    DevBuf in, lin, need, out, todo, tab, wl;
+    HostBuf h_in, h_tab, h_out, h_todo, h_lin, h_wl;
 };
 
 struct Stats {

@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(64) k_sweep(
     const ca_pod_spec* __restrict__ specs, const ca_selector_term* __restrict__ terms,
     const ca_selector_req* __restrict__ reqs, const int32_t* __restrict__ names, const int32_t* __restrict__ hints,
     const int32_t* __restrict__ lin_arr, const uint8_t* __restrict__ need, int32_t* __restrict__ out_dest,
-    int32_t* __restrict__ hint_set, SweepOut* __restrict__ outs, int32_t use_ext) {
+    int32_t* __restrict__ hint_set, SweepOut* __restrict__ outs, int32_t* __restrict__ walk_lout, int32_t use_ext) {
     __shared__ OverlaySmem ov;
     extern __shared__ __attribute__((aligned(16))) unsigned char ovx_raw[];
     OverlayExt& ox = *reinterpret_cast<OverlayExt*>(ovx_raw);
@@ -135,13 +135,13 @@ __global__ void __launch_bounds__(64) k_sweep(
     if (node < 0 || node >= n || !dest_mask[node]) {                          // cluster.go:157-160
         for (int32_t i = lane; i < mn; i += 64) { out_dest[mo + i] = -1; hint_set[mo + i] = -1; }
         res.reason = CA_UNREMOVABLE_UNEXPECTED_ERROR;
-        if (lane == 0) outs[c] = res;
+        if (lane == 0) { outs[c] = res; walk_lout[c] = -1; }
         return;
     }
     if (cand_status[c] != 0) {                                                 // :162-169
         for (int32_t i = lane; i < mn; i += 64) { out_dest[mo + i] = -1; hint_set[mo + i] = -1; }
         res.reason = cand_status[c];
-        if (lane == 0) outs[c] = res;
+        if (lane == 0) { outs[c] = res; walk_lout[c] = -1; }
         return;
     }
     int32_t npl = 0;          // overlay entries
@@ -155,6 +155,8 @@ __global__ void __launch_bounds__(64) k_sweep(
     // stored once per batch (no per-pod store for a later load to wait behind)
     int32_t my_id = -1, my_hint = -1, my_dest = -1, my_hset = -1;
     PodHot my_p = {};
+    NodeHot my_hh = {};           // the hinted node's row, prefetched with the batch
+    uint8_t my_hdm = 0;
 
     const int32_t nb = (n + 63) >> 6;
     // register block cache: raw hot row, base visibility, overlay delta per lane
@@ -211,6 +213,7 @@ __global__ void __launch_bounds__(64) k_sweep(
                 my_id = move_pods[mo + i + lane];
                 my_p = ph[my_id];
                 my_hint = hints[mo + i + lane];
+                if (my_hint >= 0 && my_hint < n) { my_hh = hot[my_hint]; my_hdm = dest_mask[my_hint]; }
             }
         }
         __syncthreads();
@@ -231,8 +234,12 @@ __global__ void __launch_bounds__(64) k_sweep(
         // ---- findNodeWithHints (hinting_simulator.go:91-108) ----
         if (h >= 0 && h < n && !pre_fail) {
             evals++;
-            NodeHot nh = hot[h];
-            NodeExt ne = ext[h];
+            NodeHot nh;
+            nh.cpu = rl64s(my_hh.cpu, sl); nh.mem = rl64s(my_hh.mem, sl); nh.eph = rl64s(my_hh.eph, sl);
+            nh.pods = rl32s(my_hh.pods, sl);
+            nh.flags = (uint32_t)rl32s((int32_t)my_hh.flags, sl);
+            NodeExt ne = {};                 // read only by the port / extended-resource checks
+            if (p.flags & (PF_PORTS | PF_SCALAR_REQ)) ne = ext[h];
             if (h == node) {
                 // the candidate with every moved pod removed (cluster.go:228-233)
                 for (int32_t q = 0; q < mn; q++) {
@@ -244,20 +251,24 @@ __global__ void __launch_bounds__(64) k_sweep(
                     for (int w = 0; w < CA_PORT_WORDS; w++) ne.ports[w] &= ~ms.port_use[w];
                 }
             } else {
-                for (int32_t q = 0; q < npl; q++) {
-                    if (ov.node[q] == h) {
-                        nh.cpu = wsub(nh.cpu, ov.cpu[q]); nh.mem = wsub(nh.mem, ov.mem[q]);
-                        nh.eph = wsub(nh.eph, ov.eph[q]); nh.pods -= ov.pods[q];
-                        if (use_ext) {
-                            for (int w = 0; w < CA_PORT_WORDS; w++) ne.ports[w] |= ox.ports[q][w];
-                            for (int k = 0; k < CA_MAX_SCALAR; k++) ne.scalar[k] = wsub(ne.scalar[k], ox.scalar[q][k]);
-                        }
+                // this candidate's placements on h (a node has at most one overlay slot)
+                int32_t q = -1;
+                for (int32_t q0 = 0; q0 < npl && q < 0; q0 += 64) {
+                    const uint64_t m = __ballot(q0 + lane < npl && ov.node[q0 + lane] == h);
+                    if (m) q = q0 + __builtin_ctzll(m);
+                }
+                if (q >= 0) {
+                    nh.cpu = wsub(nh.cpu, ov.cpu[q]); nh.mem = wsub(nh.mem, ov.mem[q]);
+                    nh.eph = wsub(nh.eph, ov.eph[q]); nh.pods -= ov.pods[q];
+                    if (use_ext) {
+                        for (int w = 0; w < CA_PORT_WORDS; w++) ne.ports[w] |= ox.ports[q][w];
+                        for (int k = 0; k < CA_MAX_SCALAR; k++) ne.scalar[k] = wsub(ne.scalar[k], ox.scalar[q][k]);
                     }
                 }
             }
             if (eval_node(s, p, psc, terms, reqs, nh, ne, st + h, true)) {
                 if (lane == sl) my_hset = h;                                    // :95
-                if (h != node && dest_mask[h]) target = h;                      // :102
+                if (h != node && rl32s((int32_t)my_hdm, sl) != 0) target = h;  // :102
             }
         }
         // ---- findNode -> FitsAnyNodeMatching(isCandidateNode) (:110-125) ----
@@ -420,6 +431,7 @@ __global__ void __launch_bounds__(64) k_sweep(
         res.fa_success = fa_success ? 1 : 0;
         res.evals = evals;
         outs[c] = res;
+        walk_lout[c] = fa_success ? L : -1;    // host walk: -1 = the result does not depend on lastIndex
     }
 }
 
@@ -496,58 +508,15 @@ __global__ void __launch_bounds__(64) k_sweep_table(
 }
 
 // ---------------------------------------------------------------------------
-// calibration for the first table round: thread i runs sensitive candidate i once,
-// from a rough guess g_i, and reports how far it moved lastIndex.  The advance barely
-// depends on the starting point (a placement lands on the first node with room), so
-// the prefix sum of these advances (k_sweep_est) centres the first windows within a
-// few positions of the true values.  Hints / ports / extended resources / long scans:
-// the advance falls back to the number of moved pods.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_sweep_calib(
-    const NodeHot* __restrict__ hot, const NodeStatic* __restrict__ st, int32_t n,
-    const uint8_t* __restrict__ dest_mask, const int32_t* __restrict__ cands, const int32_t* __restrict__ move_off,
-    const int32_t* __restrict__ move_pods, const PodHot* __restrict__ ph, const ca_pod_spec* __restrict__ specs,
-    const ca_selector_term* __restrict__ terms, const ca_selector_req* __restrict__ reqs,
-    const int32_t* __restrict__ names, const int32_t* __restrict__ hints, const int32_t* __restrict__ sens,
-    const int32_t* __restrict__ guess, int32_t S, int32_t* __restrict__ adv_out) {
-    const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (i >= S || n <= 0) return;
-    const int32_t c = sens[i];
-    const int32_t node = cands[c];
-    const int32_t mo = move_off[c], mn = move_off[c + 1] - mo;
-    int32_t L = guess[i];
-    if (L >= n || L < 0) L = (int32_t)((uint32_t)L % (uint32_t)n);
-    int32_t adv = 0;
-    bool ok = mn <= TB_MAXP;
-    for (int32_t q = 0; q < mn && ok; q++) {
-        const PodHot p0 = ph[move_pods[mo + q]];
-        PodHot p = p0;
-        p.flags = moved_flags(p0.flags);
-        if ((hints[mo + q] >= 0) || (p.flags & (PF_PORTS | PF_SCALAR_REQ))) { ok = false; break; }
-        if (p.flags & PF_PREFILTER_FAIL) break;
-        const ca_pod_spec& sp = specs[p.spec];
-        int32_t steps = 0, pos = L;
-        for (;;) {
-            if (adv + steps >= n || steps >= TB_SCAN) { ok = false; break; }
-            const NodeHot nh = hot[pos];
-            bool vis = (pos != node) & (dest_mask[pos] != 0) & !(nh.flags & NF_UNSCHED);
-            if (vis && (p.flags & PF_PREFILTER_NAMES)) vis = in_prefilter(sp, names, st[pos].name_id);
-            if (vis && hot_fits(p, nh) && static_ok(sp, p, terms, reqs, nh, st + pos)) break;
-            steps++;
-            pos++;
-            if (pos >= n) pos = 0;
-        }
-        if (!ok) break;
-        adv += steps + 1;
-        L = pos + 1;
-        if (L >= n) L = 0;
-    }
-    adv_out[i] = ok ? adv : mn;
-}
-
+// window estimate for the first table round.  The probe pass (k_sweep at rough
+// guesses) tells how far each candidate moved lastIndex; the advance barely depends on
+// the starting point (a placement lands on the first node with room), so the prefix sum
+// of the advances centres every window within a few positions of the true value.  A
+// candidate that made no successful scan does not move lastIndex at all (advance 0).
 // est_k = L0 + sum_{i<k} adv_i (mod n); window start = est_k - 32.  One block.
-__global__ void __launch_bounds__(1024) k_sweep_est(const int32_t* __restrict__ adv, int32_t S, int64_t L0, int32_t n,
-                                                    int32_t* __restrict__ ws) {
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_sweep_est(const SweepOut* __restrict__ probe, const int32_t* __restrict__ sens,
+                                                    int32_t S, int64_t L0, int32_t n, int32_t* __restrict__ ws) {
     __shared__ int64_t wtot[16];
     __shared__ int64_t carry;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -555,7 +524,15 @@ __global__ void __launch_bounds__(1024) k_sweep_est(const int32_t* __restrict__ 
     __syncthreads();
     for (int32_t base = 0; base < S; base += 1024) {
         const int32_t k = base + tid;
-        const int64_t v = k < S ? adv[k] : 0;
+        int64_t v = 0;
+        if (k < S) {
+            const SweepOut o = probe[sens[k]];
+            if (o.fa_success) {
+                int64_t d = ((int64_t)o.lout - (int64_t)o.lin) % n;
+                if (d < 0) d += n;
+                v = d;
+            }
+        }
         int64_t x = v;                                   // inclusive scan in the wave
         for (int o = 1; o < 64; o <<= 1) {
             const int64_t y = __shfl_up(x, o, 64);
@@ -604,7 +581,7 @@ struct DevView {
 
 int launch_exact(ca_mirror* m, hipStream_t st, int32_t C, int32_t n, DevView d_mask, DevView d_c, DevView d_status,
                  DevView d_off, DevView d_moves, DevView d_hints, DevBuf& d_lin, DevBuf& d_need, DevView d_dest,
-                 DevView d_hset, DevView d_out) {
+                 DevView d_hset, DevView d_out, DevBuf& d_wl) {
     const bool use_ext = m->n_ext_pods > 0;
     const size_t dyn = use_ext ? sizeof(OverlayExt) : 0;
     if (use_ext)
@@ -616,7 +593,7 @@ int launch_exact(ca_mirror* m, hipStream_t st, int32_t C, int32_t n, DevView d_m
                        m->d_pods.terms.as<ca_selector_term>(), m->d_pods.reqs.as<ca_selector_req>(),
                        m->d_pods.names.as<int32_t>(), d_hints.as<int32_t>(), d_lin.as<int32_t>(),
                        d_need.as<uint8_t>(), d_dest.as<int32_t>(), d_hset.as<int32_t>(), d_out.as<SweepOut>(),
-                       use_ext ? 1 : 0);
+                       d_wl.as<int32_t>(), use_ext ? 1 : 0);
     CA_HIP_CHECK(hipGetLastError());
     return CA_OK;
 }
@@ -689,7 +666,7 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     const int32_t S = (int32_t)sens.size();
 
     SweepScratch& sw = m->sw;
-    DevBuf &d_in = sw.in, &d_lin = sw.lin, &d_need = sw.need, &d_todo = sw.todo, &d_tab = sw.tab;
+    DevBuf &d_in = sw.in, &d_lin = sw.lin, &d_need = sw.need, &d_todo = sw.todo, &d_tab = sw.tab, &d_wl = sw.wl;
     // outputs packed for one D2H: [SweepOut x C][dest M][hint set M]
     const size_t out_bytes = sizeof(SweepOut) * (size_t)C + sizeof(int32_t) * 2 * (size_t)std::max(M, 1);
     if ((rc = sw.out.reserve(out_bytes)) != CA_OK) return rc;
@@ -726,44 +703,50 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     int32_t* h_lin = sw.h_lin.as<int32_t>();
     uint8_t* h_need = reinterpret_cast<uint8_t*>(h_lin + C);
     tmark("upload");
-    // ---- 1. every candidate's input lastIndex ----
-    std::vector<int32_t> exact_lin((size_t)C, 0), exact_lout((size_t)C, 0);
-    std::vector<int32_t> ws((size_t)S, 0);          // window start per sensitive candidate
-    int32_t* const tab = sw.h_tab.as<int32_t>();    // [64][S], filled by the table rounds
-    std::vector<uint8_t> have((size_t)S, 0);        // table row computed for ws
-    std::vector<int32_t> todo, todo_ws, todo_k;
-    std::vector<uint8_t> need1((size_t)C, 0);
-    std::vector<int32_t> lin1((size_t)C, 0);
-    int32_t rounds = 0, exact_runs = 0;
-    float kms = 0;
+    if ((rc = d_wl.reserve(sizeof(int32_t) * (size_t)C)) != CA_OK) return rc;
+    if ((rc = sw.h_wl.reserve(sizeof(int32_t) * (size_t)C)) != CA_OK) return rc;
+    int32_t* const h_wl = sw.h_wl.as<int32_t>();
+    // ---- 1. probe: every candidate once, at a rough guess of its lastIndex ----
+    // A candidate's outputs depend on its input lastIndex only from its first successful
+    // FitsAnyNode scan on (hint checks and failed full scans do not depend on it).  The
+    // probe's results are final for every candidate without a successful scan (steady
+    // state: the hints of the previous loop place every pod), and for the others its
+    // advances calibrate the table windows.
     const int64_t L0 = *last_index;               // raw until the first placement (Go keeps the int)
-    {   // initial guesses: every moved pod advances lastIndex by at least one position
+    std::vector<int32_t> guess((size_t)C, 0);
+    std::vector<int32_t> ws((size_t)S, 0);          // window start per sensitive candidate
+    {
         int64_t g = L0;
-        for (int32_t k = 0; k < S; k++) {
-            ws[k] = wrap(g - 32, n);
-            g += move_off[sens[k] + 1] - move_off[sens[k]];
+        int32_t k = 0;
+        for (int32_t c = 0; c < C; c++) {
+            guess[c] = wrap(g, n);
+            if (k < S && sens[k] == c) {
+                ws[k] = wrap(g - 32, n);
+                g += move_off[c + 1] - move_off[c];     // every moved pod advances it at most... a guess
+                k++;
+            }
         }
     }
-    if (S > 0 && n > 0 && !getenv("CASIM_SWEEP_NO_CALIB")) {
-        // round 1 without a host round trip: calibrate the advances, centre the windows
-        // on their prefix sums, build every table row (DESIGN.md §4 sweep)
+    std::memcpy(h_lin, guess.data(), sizeof(int32_t) * C);
+    std::memset(h_need, 1, (size_t)C);
+    CA_HIP_CHECK(hipMemcpyAsync(d_lin.ptr, h_lin, sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
+    CA_HIP_CHECK(hipMemcpyAsync(d_need.ptr, h_need, (size_t)C, hipMemcpyHostToDevice, st));
+    CA_HIP_CHECK(hipEventRecord(m->ev0, st));
+    if ((rc = launch_exact(m, st, C, n, d_mask, d_c, d_status, d_off, d_moves, d_hints, d_lin, d_need, d_dest, d_hset,
+                           d_out, d_wl)) != CA_OK)
+        return rc;
+    int32_t* const tab = sw.h_tab.as<int32_t>();    // [64][S], filled by the table rounds
+    int32_t rounds = 1, exact_runs = 0;
+    if (S > 0 && n > 0) {
+        // ---- 2. first table round, windows centred on the probe's advances ----
         rounds++;
         int32_t* ht = sw.h_todo.as<int32_t>();
-        for (int32_t k = 0; k < S; k++) { ht[k] = sens[k]; ht[S + k] = wrap((int64_t)ws[k] + 32, n); }
-        CA_HIP_CHECK(hipMemcpyAsync(d_todo.ptr, ht, sizeof(int32_t) * 2 * S, hipMemcpyHostToDevice, st));
+        std::memcpy(ht, sens.data(), sizeof(int32_t) * S);
+        CA_HIP_CHECK(hipMemcpyAsync(d_todo.ptr, ht, sizeof(int32_t) * S, hipMemcpyHostToDevice, st));
         int32_t* d_sens = d_todo.as<int32_t>();
-        int32_t* d_guess = d_sens + S;
-        int32_t* d_adv = d_sens + 2 * S;
-        int32_t* d_ws = d_sens + 3 * S;
-        CA_HIP_CHECK(hipEventRecord(m->ev0, st));
-        hipLaunchKernelGGL(k_sweep_calib, dim3((S + 63) / 64), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
-                           m->d_static.as<NodeStatic>(), n, d_mask.as<uint8_t>(), d_c.as<int32_t>(),
-                           d_off.as<int32_t>(), d_moves.as<int32_t>(), m->d_pods.hot.as<PodHot>(),
-                           m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
-                           m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
-                           d_hints.as<int32_t>(), d_sens, d_guess, S, d_adv);
-        CA_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(k_sweep_est, dim3(1), dim3(1024), 0, st, d_adv, S, (int64_t)L0, n, d_ws);
+        int32_t* d_ws = d_sens + S;
+        hipLaunchKernelGGL(k_sweep_est, dim3(1), dim3(1024), 0, st, d_out.as<SweepOut>(), d_sens, S, (int64_t)L0, n,
+                           d_ws);
         CA_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(k_sweep_table, dim3(S), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
                            m->d_static.as<NodeStatic>(), n, d_mask.as<uint8_t>(), d_c.as<int32_t>(),
@@ -775,21 +758,39 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
         CA_HIP_CHECK(hipEventRecord(m->ev1, st));
         CA_HIP_CHECK(hipMemcpyAsync(tab, d_tab.ptr, sizeof(int32_t) * 64 * (size_t)S, hipMemcpyDeviceToHost, st));
         CA_HIP_CHECK(hipMemcpyAsync(ht, d_ws, sizeof(int32_t) * S, hipMemcpyDeviceToHost, st));
+        CA_HIP_CHECK(hipMemcpyAsync(h_wl, d_wl.ptr, sizeof(int32_t) * C, hipMemcpyDeviceToHost, st));
         CA_HIP_CHECK(hipStreamSynchronize(st));
+        for (int32_t k = 0; k < S; k++) ws[k] = ht[k];
+    } else {
+        CA_HIP_CHECK(hipEventRecord(m->ev1, st));
+        CA_HIP_CHECK(hipMemcpyAsync(h_wl, d_wl.ptr, sizeof(int32_t) * C, hipMemcpyDeviceToHost, st));
+        CA_HIP_CHECK(hipStreamSynchronize(st));
+    }
+    float kms = 0;
+    {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
         kms += ms;
-        for (int32_t k = 0; k < S; k++) { ws[k] = ht[k]; have[k] = 1; }
-        if (dbg_t) fprintf(stderr, "[sweep] calibrated table round: %d rows, kernels %.3f ms\n", S, ms);
-        tmark("table");
+        if (dbg_t) fprintf(stderr, "[sweep] probe + table round: %d rows, kernels %.3f ms\n", S, ms);
+        tmark("probe+table");
     }
+    // ---- 3. walk the lastIndex chain ----
+    // final[c]: the probe's outputs for c are exact (insensitive, or probed at the true
+    // lastIndex, or re-run alone); the rest re-run in one exact pass at exact_lin.
+    std::vector<int32_t> exact_lin((size_t)C, 0), exact_lout((size_t)C, 0);
+    std::vector<uint8_t> final_((size_t)C, 1);
+    std::vector<uint8_t> have((size_t)S, 1);        // table row computed for ws
+    std::vector<int32_t> todo, todo_ws, todo_k;
+    std::vector<uint8_t> need1((size_t)C, 0);
+    std::vector<int32_t> lin1((size_t)C, 0);
     SweepOut one;
     int32_t k0 = 0;               // first sensitive candidate not yet resolved
     int64_t cur = L0;             // exact lastIndex before sens[k0]
+    auto insensitive = [&](int32_t k) { return h_wl[sens[k]] < 0; };
     while (k0 < S) {
         todo.clear(); todo_ws.clear(); todo_k.clear();
         for (int32_t k = k0; k < S; k++)
-            if (!have[k]) { todo.push_back(sens[k]); todo_ws.push_back(ws[k]); todo_k.push_back(k); }
+            if (!have[k] && !insensitive(k)) { todo.push_back(sens[k]); todo_ws.push_back(ws[k]); todo_k.push_back(k); }
         if (!todo.empty()) {
             rounds++;
             const int32_t T = (int32_t)todo.size();
@@ -817,16 +818,20 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
             kms += ms;
             if (dbg_t) fprintf(stderr, "[sweep] table round %d: %d rows, kernel %.3f ms\n", rounds, T, ms);
             tmark("table");
-            for (int32_t k = k0; k < S; k++) have[k] = 1;
         }
+        for (int32_t k = k0; k < S; k++) have[k] = 1;
         // walk the exact chain as far as the windows reach
         for (; k0 < S; k0++) {
             const int32_t c = sens[k0];
+            const int32_t wl = h_wl[c];
+            exact_lin[c] = (int32_t)cur;
+            if (wl < 0) { exact_lout[c] = (int32_t)cur; continue; }            // lastIndex passes through
+            if (wrap(cur, n) == guess[c]) { exact_lout[c] = wl; cur = wl; continue; }   // probed at the true value
             const int32_t w = wrap(cur - ws[k0], n);
             if (w >= 64) break;
             int32_t v = tab[(size_t)(w) * S + k0];
             if (v == TB_UNKNOWN) {
-                // hints / ports / long scans: exact kernel at the exact lastIndex
+                // hints / ports / long scans: exact kernel at the exact lastIndex, alone
                 need1[c] = 1;
                 lin1[c] = (int32_t)cur;
                 std::memcpy(h_lin, lin1.data(), sizeof(int32_t) * C);
@@ -834,15 +839,16 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
                 CA_HIP_CHECK(hipMemcpyAsync(d_lin.ptr, h_lin, sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
                 CA_HIP_CHECK(hipMemcpyAsync(d_need.ptr, h_need, (size_t)C, hipMemcpyHostToDevice, st));
                 if ((rc = launch_exact(m, st, C, n, d_mask, d_c, d_status, d_off, d_moves, d_hints, d_lin, d_need,
-                                       d_dest, d_hset, d_out)) != CA_OK)
+                                       d_dest, d_hset, d_out, d_wl)) != CA_OK)
                     return rc;
                 CA_HIP_CHECK(hipMemcpyAsync(&one, d_out.as<SweepOut>() + c, sizeof(SweepOut), hipMemcpyDeviceToHost, st));
                 CA_HIP_CHECK(hipStreamSynchronize(st));
                 need1[c] = 0;
                 exact_runs++;
                 v = one.fa_success ? one.lout : (int32_t)cur;
+            } else {
+                final_[c] = 0;                                                   // re-run at exact_lin
             }
-            exact_lin[c] = (int32_t)cur;
             exact_lout[c] = v;
             cur = v;
         }
@@ -851,6 +857,7 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
         // inside a window, otherwise shift the nearest known entry
         int64_t est = cur;
         for (int32_t k = k0; k < S; k++) {
+            if (insensitive(k)) continue;
             const int32_t w = wrap(est - ws[k], n);
             const int32_t v = w < 64 ? tab[(size_t)(w) * S + k] : TB_UNKNOWN;
             if (w < 64 && v != TB_UNKNOWN) { est = v; continue; }
@@ -869,29 +876,24 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
         }
         if (rounds > S + 4) { set_last_error("sweep speculation did not converge"); return CA_EDEVICE; }
     }
-    {   // candidates that cannot move lastIndex see the running value
-        int64_t run = L0;
-        int32_t k = 0;
-        for (int32_t c = 0; c < C; c++) {
-            if (k < S && sens[k] == c) {
-                run = exact_lout[c];
-                k++;
-                continue;
-            }
-            exact_lin[c] = (int32_t)run;
-        }
-    }
     tmark("walk");
     if (dbg_t) fprintf(stderr, "[sweep] exact fallbacks %d\n", exact_runs);
-    // ---- 2. exact pass at the exact lastIndex: every output ----
-    std::memcpy(h_lin, exact_lin.data(), sizeof(int32_t) * C);
-    std::memset(h_need, 1, (size_t)C);
-    CA_HIP_CHECK(hipMemcpyAsync(d_lin.ptr, h_lin, sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
-    CA_HIP_CHECK(hipMemcpyAsync(d_need.ptr, h_need, (size_t)C, hipMemcpyHostToDevice, st));
+    // ---- 4. exact pass for the candidates the probe did not settle ----
+    int32_t n_rerun = 0;
+    for (int32_t c = 0; c < C; c++) {
+        h_need[c] = final_[c] ? 0 : 1;
+        h_lin[c] = exact_lin[c];
+        n_rerun += final_[c] ? 0 : 1;
+    }
     CA_HIP_CHECK(hipEventRecord(m->ev0, st));
-    if ((rc = launch_exact(m, st, C, n, d_mask, d_c, d_status, d_off, d_moves, d_hints, d_lin, d_need, d_dest, d_hset,
-                           d_out)) != CA_OK)
-        return rc;
+    if (n_rerun > 0) {
+        rounds++;
+        CA_HIP_CHECK(hipMemcpyAsync(d_lin.ptr, h_lin, sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
+        CA_HIP_CHECK(hipMemcpyAsync(d_need.ptr, h_need, (size_t)C, hipMemcpyHostToDevice, st));
+        if ((rc = launch_exact(m, st, C, n, d_mask, d_c, d_status, d_off, d_moves, d_hints, d_lin, d_need, d_dest,
+                               d_hset, d_out, d_wl)) != CA_OK)
+            return rc;
+    }
     CA_HIP_CHECK(hipEventRecord(m->ev1, st));
     const SweepOut* outs = sw.h_out.as<SweepOut>();
     const int32_t* h_dest = reinterpret_cast<const int32_t*>(outs + C);
@@ -904,26 +906,16 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     float ms = 0;
     (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
     kms += ms;
-    // the exact pass must reproduce the chain it was given
+    // the outputs must reproduce the chain: each sensitive result was computed at the
+    // lastIndex the walk gives it, the others do not move it
     int64_t Lrun = L0;
     for (int32_t c = 0; c < C; c++) {
         const SweepOut& o = outs[c];
         if (o.status != CA_OK) { set_last_error("overlay capacity exceeded"); return o.status; }
-        if (o.lin != exact_lin[c] || exact_lin[c] != Lrun) {
-            if (getenv("CASIM_DEBUG")) {
-                fprintf(stderr, "chain mismatch at candidate %d: o.lin=%d exact_lin=%d Lrun=%ld\n", c, o.lin,
-                        exact_lin[c], (long)Lrun);
-                for (int32_t q = std::max(0, c - 3); q <= c && q < C; q++) {
-                    int32_t k = (int32_t)(std::find(sens.begin(), sens.end(), q) - sens.begin());
-                    fprintf(stderr, "  cand %d sens=%d lin=%d lout=%d fa=%d placed=%d mn=%d", q, k < S, outs[q].lin,
-                            outs[q].lout, outs[q].fa_success, outs[q].n_placed, move_off[q + 1] - move_off[q]);
-                    if (k < S) {
-                        const int32_t w = wrap(exact_lin[q] - ws[k], n);
-                        fprintf(stderr, " ws=%d w=%d tab=%d", ws[k], w, w < 64 ? tab[(size_t)(w) * S + k] : -9);
-                    }
-                    fprintf(stderr, "\n");
-                }
-            }
+        if (o.fa_success && wrap(o.lin, n) != wrap(Lrun, n)) {
+            if (getenv("CASIM_DEBUG"))
+                fprintf(stderr, "chain mismatch at candidate %d: o.lin=%d Lrun=%ld final=%d\n", c, o.lin, (long)Lrun,
+                        (int)final_[c]);
             set_last_error("sweep lastIndex chain mismatch");
             return CA_EDEVICE;
         }
@@ -940,7 +932,7 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
         for (int32_t i = 0; i < M; i++) if (hset[i] >= 0) hints[move_pods[i]] = hset[i];
     }
     tmark("done");
-    m->sweep_stats.rounds = rounds + exact_runs + 1;
+    m->sweep_stats.rounds = rounds + exact_runs;
     m->sweep_stats.exact_ms = ms;
     m->sweep_stats.walk_ms = std::chrono::duration<float, std::milli>(t_exact - t_start).count();
     m->sweep_stats.kernel_ms = kms;

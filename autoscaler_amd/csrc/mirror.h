@@ -91,6 +91,10 @@ struct ca_mirror {
     std::vector<uint8_t> h_scratch;
     casim::Stats sweep_stats;
     casim::SweepScratch sw;
+    // resident HintingSimulator hints (hints.go:29-72): node per mirror pod, -1 = none
+    casim::DevBuf d_pod_hints;
+    size_t d_hints_n = 0;
+    int ensure_pod_hints();                // grow to pods.size(), new entries -1
     int64_t n_ext_pods = 0;                // pods stored with host ports / extended requests
 
     int sync_nodes();                      // push dirty rows to the device

@@ -442,6 +442,39 @@ int ca_mirror_clear(ca_mirror* m) {
     m->dirty_rows.clear(); m->dirty_flag.clear();
     m->all_dirty = true; m->static_dirty = true; m->d_rows = 0;
     m->d_pods_synced = 0; m->d_terms_synced = 0;
+    m->d_hints_n = 0;
+    return CA_OK;
+}
+
+int ca_mirror::ensure_pod_hints() {
+    const size_t np = pods.size();
+    if (d_hints_n >= np) return CA_OK;
+    int rc = d_pod_hints.reserve_keep(sizeof(int32_t) * std::max<size_t>(np, 1), stream);
+    if (rc != CA_OK) return rc;
+    CA_HIP_CHECK(hipMemsetAsync(d_pod_hints.as<int32_t>() + d_hints_n, 0xFF, sizeof(int32_t) * (np - d_hints_n), stream));
+    d_hints_n = np;
+    return CA_OK;
+}
+
+int ca_mirror_set_hints(ca_mirror* m, const int32_t* hints, int32_t n_pods) {
+    if (!m || n_pods != (int32_t)m->pods.size() || (n_pods > 0 && !hints)) return CA_EINVAL;
+    CA_HIP_CHECK(hipSetDevice(m->device));
+    int rc = m->ensure_pod_hints();
+    if (rc != CA_OK) return rc;
+    if (n_pods) CA_HIP_CHECK(hipMemcpyAsync(m->d_pod_hints.ptr, hints, sizeof(int32_t) * n_pods, hipMemcpyHostToDevice,
+                                            m->stream));
+    CA_HIP_CHECK(hipStreamSynchronize(m->stream));
+    return CA_OK;
+}
+
+int ca_mirror_get_hints(ca_mirror* m, int32_t* hints, int32_t n_pods) {
+    if (!m || n_pods != (int32_t)m->pods.size() || (n_pods > 0 && !hints)) return CA_EINVAL;
+    CA_HIP_CHECK(hipSetDevice(m->device));
+    int rc = m->ensure_pod_hints();
+    if (rc != CA_OK) return rc;
+    if (n_pods) CA_HIP_CHECK(hipMemcpyAsync(hints, m->d_pod_hints.ptr, sizeof(int32_t) * n_pods, hipMemcpyDeviceToHost,
+                                            m->stream));
+    CA_HIP_CHECK(hipStreamSynchronize(m->stream));
     return CA_OK;
 }
 

@@ -125,6 +125,7 @@ __global__ void __launch_bounds__(64) k_sweep(
     OverlayExt& ox = *reinterpret_cast<OverlayExt*>(ovx_raw);
     const int c = blockIdx.x;
     if (!need[c]) return;
+    const uint64_t t_begin = wall_clock64();      // diagnostics: SweepOut.pad2 = device ticks (100 MHz)
     const int lane = threadIdx.x;
     const int32_t lin = lin_arr[c];
     SweepOut res;
@@ -217,6 +218,90 @@ __global__ void __launch_bounds__(64) k_sweep(
             }
         }
         __syncthreads();
+        if (sl == 0) {
+            // ---- the batch's leading pods placed on their hints, in bulk ----
+            // Pod i of a run whose earlier pods all went to their hinted nodes sees exactly
+            // those placements (plus the overlay so far) on its own hinted node, so the
+            // hint checks of the run are independent lane-parallel checks; the first pod
+            // whose check fails (or that cannot take this path) continues sequentially.
+            // The steady-state sweep (hints of the previous loop) is almost all such pods.
+            const int32_t bn = min(64, mn - i);
+            bool el = false;
+            PodHot q = my_p;
+            q.flags = moved_flags(my_p.flags);
+            if (lane < bn)
+                el = my_hint >= 0 && my_hint < n && my_hint != node && my_hdm != 0 &&
+                     !(q.flags & (PF_PREFILTER_FAIL | PF_PORTS | PF_SCALAR_REQ));
+            const uint64_t em = __ballot(el);
+            const int32_t lead = min(bn, em == ~0ull ? 64 : __builtin_ctzll(~em));
+            int32_t f = 0;
+            if (lead > 0) {
+                int64_t ac = 0, am = 0, ae = 0;
+                int32_t ap = 0;
+                for (int32_t j = 0; j + 1 < lead; j++) {          // earlier pods of the run, same node
+                    const int32_t hj = rl32s(my_hint, j);
+                    const int64_t cj = rl64s(my_p.cpu, j), mj = rl64s(my_p.mem, j), ej = rl64s(my_p.eph, j);
+                    if ((lane > j) & (lane < lead) & (my_hint == hj)) { ac += cj; am += mj; ae += ej; ap += 1; }
+                }
+                for (int32_t qq = 0; qq < npl; qq++) {              // this candidate's overlay so far
+                    const int32_t nd = ov.node[qq];
+                    if ((lane < lead) & (my_hint == nd)) {
+                        ac += ov.cpu[qq]; am += ov.mem[qq]; ae += ov.eph[qq]; ap += ov.pods[qq];
+                    }
+                }
+                bool fit = false;
+                if (lane < lead) {
+                    NodeHot nh = my_hh;
+                    nh.cpu = wsub(nh.cpu, ac); nh.mem = wsub(nh.mem, am); nh.eph = wsub(nh.eph, ae); nh.pods -= ap;
+                    const NodeExt ne = {};
+                    int64_t psc0[CA_MAX_SCALAR];
+                    for (int k = 0; k < CA_MAX_SCALAR; k++) psc0[k] = 0;
+                    fit = eval_node(specs[q.spec], q, psc0, terms, reqs, nh, ne, st + my_hint, true);
+                }
+                const uint64_t fm = __ballot(fit);
+                f = min(lead, fm == ~0ull ? 64 : __builtin_ctzll(~fm));
+                // AddPod of the run into the overlay, in order (:79)
+                for (int32_t j = 0; j < f; j++) {
+                    const int32_t hj = rl32s(my_hint, j);
+                    const int64_t cj = rl64s(my_p.cpu, j), mj = rl64s(my_p.mem, j), ej = rl64s(my_p.eph, j);
+                    int32_t slot = -1;
+                    for (int32_t q0 = 0; q0 < npl; q0 += 64) {
+                        const uint64_t mm = __ballot(q0 + lane < npl && ov.node[q0 + lane] == hj);
+                        if (mm) { slot = q0 + __builtin_ctzll(mm); break; }
+                    }
+                    if (slot < 0) {
+                        if (npl >= OV_CAP) { f = j; break; }            // the sequential path reports it
+                        slot = npl++;
+                        if (lane == 0) {
+                            ov.node[slot] = hj; ov.pods[slot] = 0; ov.cpu[slot] = 0; ov.mem[slot] = 0; ov.eph[slot] = 0;
+                            if (use_ext) {
+                                for (int w = 0; w < CA_PORT_WORDS; w++) ox.ports[slot][w] = 0;
+                                for (int k = 0; k < CA_MAX_SCALAR; k++) ox.scalar[slot][k] = 0;
+                            }
+                        }
+                    }
+                    if (lane == 0) {
+                        ov.cpu[slot] = wadd(ov.cpu[slot], cj);
+                        ov.mem[slot] = wadd(ov.mem[slot], mj);
+                        ov.eph[slot] = wadd(ov.eph[slot], ej);
+                        ov.pods[slot] += 1;
+                    }
+                    if (lane == (hj & 63)) {
+                        if ((hj >> 6) == ja) { Adc = wadd(Adc, cj); Adm = wadd(Adm, mj); Ade = wadd(Ade, ej); Adp += 1; }
+                        if ((hj >> 6) == jb) { Bdc = wadd(Bdc, cj); Bdm = wadd(Bdm, mj); Bde = wadd(Bde, ej); Bdp += 1; }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            if (f > 0) {
+                if (lane < f) { my_dest = my_hint; my_hset = my_hint; }      // hints.Set + isNodeAcceptable
+                evals += (uint64_t)f;
+                placed += f;
+                __syncthreads();
+                i += f - 1;
+                continue;
+            }
+        }
         PodHot p;
         p.cpu = rl64s(my_p.cpu, sl); p.mem = rl64s(my_p.mem, sl); p.eph = rl64s(my_p.eph, sl);
         p.flags = moved_flags((uint32_t)rl32s((int32_t)my_p.flags, sl));
@@ -430,6 +515,7 @@ __global__ void __launch_bounds__(64) k_sweep(
         res.lout = L;
         res.fa_success = fa_success ? 1 : 0;
         res.evals = evals;
+        res.pad2 = wall_clock64() - t_begin;
         outs[c] = res;
         walk_lout[c] = fa_success ? L : -1;    // host walk: -1 = the result does not depend on lastIndex
     }
@@ -557,11 +643,119 @@ __global__ void __launch_bounds__(1024) k_sweep_est(const SweepOut* __restrict__
     }
 }
 
+// ---------------------------------------------------------------------------
+// device walk of the lastIndex chain, replacing the host walk and its
+// round trip in the common case.  The chain is cut into chunks of WK sensitive
+// candidates.  k_walk_chunks: lane x of chunk j follows the chain through the chunk from
+// input ws[first] + x (the 64 values around the estimate), applying each candidate's map
+// (insensitive: identity; the probe's input: the probe's output; inside the candidate's
+// table window: the table; otherwise: stop), with the table rows staged in LDS; it
+// records every lane's trajectory.  k_walk_resolve: one thread chains the chunk maps
+// from the true input, then every candidate of the resolved prefix reads its exact
+// input and whether it needs the exact re-run from the trajectory of its chunk's true
+// lane.  A stop (input outside every window, or a row the table cannot simulate) hands
+// the rest of the chain to the host walk.
+// ---------------------------------------------------------------------------
+constexpr int WK = 64;
+constexpr int WALK_MAX_CHUNKS = 256;
+
+__global__ void __launch_bounds__(64) k_walk_chunks(const int32_t* __restrict__ sens, const int32_t* __restrict__ ws,
+                                                   const int32_t* __restrict__ guess, const int32_t* __restrict__ wl,
+                                                   const int32_t* __restrict__ tab, int32_t S, int32_t n,
+                                                   int32_t* __restrict__ cmap, int32_t* __restrict__ traj) {
+    __shared__ int32_t T[64][WK + 1];
+    __shared__ int32_t cws[WK], cg[WK], cwl[WK];
+    const int j = blockIdx.x, lane = threadIdx.x;
+    const int32_t k0 = j * WK, kn = min(WK, S - k0);
+    for (int w = 0; w < 64; w++) T[w][lane] = lane < kn ? tab[(size_t)w * S + k0 + lane] : TB_UNKNOWN;
+    if (lane < kn) {
+        const int32_t c = sens[k0 + lane];
+        cws[lane] = ws[k0 + lane];
+        cg[lane] = guess[c];
+        cwl[lane] = wl[c];
+    }
+    __syncthreads();
+    int32_t cur = (int32_t)(((int64_t)cws[0] + lane) % n);
+    int32_t stop = -1;
+    for (int kk = 0; kk < kn; kk++) {
+        int32_t enc = -1;
+        if (stop < 0) {
+            enc = cur * 2;                                  // lastIndex before candidate kk, re-run bit
+            const int32_t wlv = cwl[kk];
+            if (wlv >= 0) {
+                if (cur == cg[kk]) {
+                    cur = wlv;
+                } else {
+                    int32_t w = cur - cws[kk];
+                    if (w < 0) w += n;
+                    const int32_t v = w < 64 ? T[w][kk] : TB_UNKNOWN;
+                    if (v == TB_UNKNOWN) stop = kk;
+                    else { cur = v; enc |= 1; }
+                }
+            }
+        }
+        traj[((size_t)k0 + kk) * 64 + lane] = enc;
+    }
+    cmap[(size_t)j * 64 + lane] = stop >= 0 ? -1 - stop : cur;
+}
+
+// info[0] = first unresolved sensitive candidate (S: all), info[1] = lastIndex before it
+__global__ void __launch_bounds__(1024) k_walk_resolve(const int32_t* __restrict__ sens, const int32_t* __restrict__ ws,
+                                                      const int32_t* __restrict__ cmap, const int32_t* __restrict__ traj,
+                                                      int32_t S, int32_t n, int32_t L0n, int32_t* __restrict__ lin,
+                                                      uint8_t* __restrict__ need, int32_t* __restrict__ info) {
+    __shared__ int32_t cm[WALK_MAX_CHUNKS * 64];
+    __shared__ int32_t lane_of[WALK_MAX_CHUNKS];
+    __shared__ int32_t stop_k, cur_out;
+    const int32_t nch = (S + WK - 1) / WK;
+    for (int32_t i = threadIdx.x; i < nch * 64; i += blockDim.x) cm[i] = cmap[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t cur = L0n, sk = S;
+        for (int32_t j = 0; j < nch; j++) {
+            int32_t x = cur - ws[j * WK];
+            if (x < 0) x += n;
+            if (x >= 64) { sk = j * WK; break; }
+            lane_of[j] = x;
+            const int32_t r = cm[j * 64 + x];
+            if (r < 0) {
+                sk = j * WK + (-1 - r);
+                cur = traj[(size_t)sk * 64 + x] >> 1;
+                break;
+            }
+            cur = r;
+        }
+        stop_k = sk;
+        cur_out = cur;
+    }
+    __syncthreads();
+    const int32_t sk = stop_k;
+    for (int32_t k = threadIdx.x; k < sk; k += blockDim.x) {
+        const int32_t e = traj[(size_t)k * 64 + lane_of[k / WK]];
+        const int32_t c = sens[k];
+        lin[c] = e >> 1;
+        need[c] = (uint8_t)(e & 1);
+    }
+    if (threadIdx.x == 0) { info[0] = sk; info[1] = cur_out; }
+}
+
+// resident hints (per mirror pod): gather the moved pods' hints / apply the hint sets
+__global__ void k_hints_gather(const int32_t* __restrict__ pod_hints, const int32_t* __restrict__ moves, int32_t M,
+                               int32_t* __restrict__ hint_move) {
+    const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i < M) hint_move[i] = pod_hints[moves[i]];
+}
+__global__ void k_hints_apply(const int32_t* __restrict__ hset, const int32_t* __restrict__ moves, int32_t M,
+                              int32_t* __restrict__ pod_hints) {
+    const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i < M && hset[i] >= 0) pod_hints[moves[i]] = hset[i];
+}
+
 }  // namespace casim
 
 using namespace casim;
 
-namespace {
+namespace casim {
 
 inline int32_t wrap(int64_t v, int32_t n) {
     if (n <= 0) return 0;
@@ -579,26 +773,325 @@ struct DevView {
     template <class T> T* as() const { return static_cast<T*>(ptr); }
 };
 
-int launch_exact(ca_mirror* m, hipStream_t st, int32_t C, int32_t n, DevView d_mask, DevView d_c, DevView d_status,
-                 DevView d_off, DevView d_moves, DevView d_hints, DevBuf& d_lin, DevBuf& d_need, DevView d_dest,
-                 DevView d_hset, DevView d_out, DevBuf& d_wl) {
+// One FindNodesToRemove call: host copies (bookkeeping) and device views of the inputs.
+struct SweepCall {
+    int32_t C = 0, M = 0, n = 0;
+    const int32_t *cand = nullptr, *status = nullptr, *move_off = nullptr, *move_pods = nullptr;
+    const uint8_t* dest_mask = nullptr;
+    DevView d_c{}, d_status{}, d_off{}, d_moves{}, d_hints{}, d_mask{};
+};
+
+int launch_exact(ca_mirror* m, hipStream_t st, const SweepCall& in, const int32_t* d_lin, const uint8_t* d_need,
+                 DevView d_dest, DevView d_hset, DevView d_out, int32_t* d_wl) {
     const bool use_ext = m->n_ext_pods > 0;
     const size_t dyn = use_ext ? sizeof(OverlayExt) : 0;
     if (use_ext)
         CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_sweep, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-    hipLaunchKernelGGL(k_sweep, dim3(C), dim3(64), dyn, st, m->d_hot.as<NodeHot>(), m->d_ext.as<NodeExt>(),
-                       m->d_static.as<NodeStatic>(), n, d_mask.as<uint8_t>(), d_c.as<int32_t>(),
-                       d_status.as<int32_t>(), d_off.as<int32_t>(), d_moves.as<int32_t>(),
+    hipLaunchKernelGGL(k_sweep, dim3(in.C), dim3(64), dyn, st, m->d_hot.as<NodeHot>(), m->d_ext.as<NodeExt>(),
+                       m->d_static.as<NodeStatic>(), in.n, in.d_mask.as<uint8_t>(), in.d_c.as<int32_t>(),
+                       in.d_status.as<int32_t>(), in.d_off.as<int32_t>(), in.d_moves.as<int32_t>(),
                        m->d_pods.hot.as<PodHot>(), m->d_pods.spec.as<ca_pod_spec>(),
                        m->d_pods.terms.as<ca_selector_term>(), m->d_pods.reqs.as<ca_selector_req>(),
-                       m->d_pods.names.as<int32_t>(), d_hints.as<int32_t>(), d_lin.as<int32_t>(),
-                       d_need.as<uint8_t>(), d_dest.as<int32_t>(), d_hset.as<int32_t>(), d_out.as<SweepOut>(),
-                       d_wl.as<int32_t>(), use_ext ? 1 : 0);
+                       m->d_pods.names.as<int32_t>(), in.d_hints.as<int32_t>(), d_lin, d_need, d_dest.as<int32_t>(),
+                       d_hset.as<int32_t>(), d_out.as<SweepOut>(), d_wl, use_ext ? 1 : 0);
     CA_HIP_CHECK(hipGetLastError());
     return CA_OK;
 }
 
-}  // namespace
+// The sweep proper (DESIGN.md §4 sweep).  hints: per mirror pod, host (in/out; nullable);
+// d_pod_hints: the mirror's resident per-pod hints (used and updated instead when
+// non-null).  out_dest nullable.
+int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod_hints, int32_t* last_index,
+               ca_removal_result* results, int32_t* out_dest) {
+    const auto t_start = std::chrono::steady_clock::now();
+    const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
+    auto tmark = [&](const char* what) {
+        if (dbg_t)
+            fprintf(stderr, "[sweep] %-14s %8.3f ms\n", what,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
+    };
+    hipStream_t st = m->stream;
+    const int32_t C = in.C, M = in.M, n = in.n;
+    const int32_t *candidates = in.cand, *status = in.status, *move_off = in.move_off, *move_pods = in.move_pods;
+    int rc;
+    // candidates whose simulation can move lastIndex: valid, not blocked, pods to move
+    std::vector<int32_t> sens;
+    sens.reserve((size_t)C);
+    for (int32_t c = 0; c < C; c++) {
+        const int32_t nd = candidates[c];
+        if (nd < 0 || nd >= n || !in.dest_mask[nd] || status[c] != 0) continue;
+        if (move_off[c + 1] - move_off[c] == 0) continue;
+        sens.push_back(c);
+    }
+    const int32_t S = (int32_t)sens.size();
+    const int32_t nch = (S + WK - 1) / WK;
+    const bool dev_walk = S > 0 && n > 0 && nch <= WALK_MAX_CHUNKS && !getenv("CASIM_SWEEP_HOST_WALK");
+
+    SweepScratch& sw = m->sw;
+    // device scratch: [SweepOut C][walk lout C][info 2][dest M][hint set M] (one D2H; the
+    // per-pod part only when the caller wants destinations or host hints),
+    // [lin C][need C] (one H2D), [sens S][ws S], table [64][S], trajectories [S][64], chunk maps
+    const size_t out_bytes = sizeof(SweepOut) * (size_t)C + sizeof(int32_t) * (2 * (size_t)std::max(M, 1) + C + 2);
+    if ((rc = sw.out.reserve(out_bytes)) != CA_OK) return rc;
+    if ((rc = sw.h_out.reserve(out_bytes)) != CA_OK) return rc;
+    DevView d_out{sw.out.ptr};
+    int32_t* const d_wl = reinterpret_cast<int32_t*>(sw.out.as<unsigned char>() + sizeof(SweepOut) * (size_t)C);
+    int32_t* const d_info = d_wl + C;
+    DevView d_dest{d_info + 2};
+    DevView d_hset{d_dest.as<int32_t>() + std::max(M, 1)};
+    const SweepOut* outs = sw.h_out.as<SweepOut>();
+    const int32_t* h_wl = reinterpret_cast<const int32_t*>(outs + C);
+    const int32_t* h_info = h_wl + C;
+    const int32_t* h_dest = h_info + 2;
+    const int32_t* hset = h_dest + std::max(M, 1);
+    const size_t d2h_bytes = (out_dest || hints) ? out_bytes : sizeof(SweepOut) * (size_t)C + sizeof(int32_t) * (C + 2);
+    if ((rc = sw.lin.reserve((sizeof(int32_t) + 1) * (size_t)C)) != CA_OK) return rc;
+    if ((rc = sw.h_lin.reserve((sizeof(int32_t) + 1) * (size_t)C)) != CA_OK) return rc;
+    int32_t* const d_lin = sw.lin.as<int32_t>();
+    uint8_t* const d_need = reinterpret_cast<uint8_t*>(d_lin + C);
+    int32_t* const h_lin = sw.h_lin.as<int32_t>();
+    uint8_t* const h_need = reinterpret_cast<uint8_t*>(h_lin + C);
+    const size_t Sx = (size_t)std::max(S, 1);
+    if ((rc = sw.todo.reserve(sizeof(int32_t) * 4 * Sx)) != CA_OK) return rc;
+    if ((rc = sw.h_todo.reserve(sizeof(int32_t) * 4 * Sx)) != CA_OK) return rc;
+    if ((rc = sw.tab.reserve(sizeof(int32_t) * 64 * Sx)) != CA_OK) return rc;
+    if ((rc = sw.h_tab.reserve(sizeof(int32_t) * 64 * Sx)) != CA_OK) return rc;
+    if ((rc = sw.wl.reserve(sizeof(int32_t) * (64 * Sx + 64 * (size_t)std::max(nch, 1)))) != CA_OK) return rc;
+    int32_t* const d_traj = sw.wl.as<int32_t>();
+    int32_t* const d_cmap = d_traj + 64 * Sx;
+    int32_t* const tab = sw.h_tab.as<int32_t>();    // [64][S] host copy (host walk only)
+    int32_t* const ht = sw.h_todo.as<int32_t>();
+    int32_t* const d_sens = sw.todo.as<int32_t>();
+    int32_t* const d_ws = d_sens + S;
+
+    // ---- 1. probe: every candidate once, at a rough guess of its lastIndex ----
+    // A candidate's outputs depend on its input lastIndex only from its first successful
+    // FitsAnyNode scan on (hint checks and failed full scans do not depend on it).  The
+    // probe's results are final for every candidate without a successful scan (steady
+    // state: the hints of the previous loop place every pod), and for the others its
+    // advances calibrate the table windows.
+    const int64_t L0 = *last_index;               // raw until the first placement (Go keeps the int)
+    std::vector<int32_t> guess((size_t)C, 0);
+    {
+        int64_t g = L0;
+        int32_t k = 0;
+        for (int32_t c = 0; c < C; c++) {
+            guess[c] = wrap(g, n);
+            if (k < S && sens[k] == c) { g += move_off[c + 1] - move_off[c]; k++; }
+        }
+    }
+    std::memcpy(h_lin, guess.data(), sizeof(int32_t) * C);
+    std::memset(h_need, 1, (size_t)C);
+    CA_HIP_CHECK(hipMemcpyAsync(d_lin, h_lin, (sizeof(int32_t) + 1) * (size_t)C, hipMemcpyHostToDevice, st));
+    if (d_pod_hints && M > 0) {
+        hipLaunchKernelGGL(k_hints_gather, dim3((M + 255) / 256), dim3(256), 0, st, d_pod_hints,
+                           in.d_moves.as<int32_t>(), M, in.d_hints.as<int32_t>());
+        CA_HIP_CHECK(hipGetLastError());
+    }
+    CA_HIP_CHECK(hipEventRecord(m->ev0, st));
+    if ((rc = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl)) != CA_OK) return rc;
+    int32_t rounds = 1, exact_runs = 0;
+    if (S > 0 && n > 0) {
+        // ---- 2. first table round, windows centred on the probe's advances ----
+        rounds++;
+        std::memcpy(ht, sens.data(), sizeof(int32_t) * S);
+        CA_HIP_CHECK(hipMemcpyAsync(d_sens, ht, sizeof(int32_t) * S, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_sweep_est, dim3(1), dim3(1024), 0, st, d_out.as<SweepOut>(), d_sens, S, (int64_t)L0, n,
+                           d_ws);
+        CA_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_sweep_table, dim3(S), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
+                           m->d_static.as<NodeStatic>(), n, in.d_mask.as<uint8_t>(), in.d_c.as<int32_t>(),
+                           in.d_off.as<int32_t>(), in.d_moves.as<int32_t>(), m->d_pods.hot.as<PodHot>(),
+                           m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
+                           m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
+                           in.d_hints.as<int32_t>(), d_sens, d_ws, (const int32_t*)nullptr, sw.tab.as<int32_t>(), S);
+        CA_HIP_CHECK(hipGetLastError());
+    }
+    if (dev_walk) {
+        // ---- 3. device walk, then the exact pass at the exact lastIndex values ----
+        CA_HIP_CHECK(hipMemsetAsync(d_need, 0, (size_t)C, st));
+        hipLaunchKernelGGL(k_walk_chunks, dim3(nch), dim3(64), 0, st, d_sens, d_ws, d_lin, d_wl, sw.tab.as<int32_t>(),
+                           S, n, d_cmap, d_traj);
+        CA_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_walk_resolve, dim3(1), dim3(1024), 0, st, d_sens, d_ws, d_cmap, d_traj, S, n, wrap(L0, n),
+                           d_lin, d_need, d_info);
+        CA_HIP_CHECK(hipGetLastError());
+        if ((rc = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl)) != CA_OK) return rc;
+    }
+    CA_HIP_CHECK(hipEventRecord(m->ev1, st));
+    CA_HIP_CHECK(hipMemcpyAsync(sw.h_out.ptr, sw.out.ptr, d2h_bytes, hipMemcpyDeviceToHost, st));
+    CA_HIP_CHECK(hipStreamSynchronize(st));
+    float kms = 0;
+    {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
+        kms += ms;
+        if (dbg_t) fprintf(stderr, "[sweep] device pipeline: %d sensitive, kernels %.3f ms\n", S, ms);
+        tmark("device");
+    }
+    // ---- 4. host walk from where the device walk stopped (or of everything) ----
+    int32_t k0 = dev_walk ? h_info[0] : 0;         // first sensitive candidate not yet resolved
+    int64_t cur = dev_walk ? (int64_t)h_info[1] : L0;
+    if (dev_walk && k0 == 0) cur = L0;
+    if (k0 < S) {
+        std::vector<int32_t> ws((size_t)S, 0);
+        std::vector<int32_t> wlc((size_t)C, 0);
+        std::memcpy(wlc.data(), h_wl, sizeof(int32_t) * C);   // the probe's walk values (h_out is reused below)
+        CA_HIP_CHECK(hipMemcpyAsync(tab, sw.tab.ptr, sizeof(int32_t) * 64 * (size_t)S, hipMemcpyDeviceToHost, st));
+        CA_HIP_CHECK(hipMemcpyAsync(ht, d_ws, sizeof(int32_t) * S, hipMemcpyDeviceToHost, st));
+        CA_HIP_CHECK(hipStreamSynchronize(st));
+        for (int32_t k = 0; k < S; k++) ws[k] = ht[k];
+        // final[c] = 0: re-run at exact_lin in one exact pass
+        std::vector<int32_t> exact_lin((size_t)C, 0);
+        std::vector<uint8_t> final_((size_t)C, 1);
+        std::vector<uint8_t> have((size_t)S, 1);
+        std::vector<int32_t> todo, todo_ws, todo_k;
+        auto insensitive = [&](int32_t k) { return wlc[sens[k]] < 0; };
+        // the device walk's re-runs already happened: only candidates from k0 on remain
+        while (k0 < S) {
+            todo.clear(); todo_ws.clear(); todo_k.clear();
+            for (int32_t k = k0; k < S; k++)
+                if (!have[k] && !insensitive(k)) { todo.push_back(sens[k]); todo_ws.push_back(ws[k]); todo_k.push_back(k); }
+            if (!todo.empty()) {
+                rounds++;
+                const int32_t T = (int32_t)todo.size();
+                std::memcpy(ht, todo.data(), sizeof(int32_t) * T);
+                std::memcpy(ht + T, todo_ws.data(), sizeof(int32_t) * T);
+                std::memcpy(ht + 2 * T, todo_k.data(), sizeof(int32_t) * T);
+                CA_HIP_CHECK(hipMemcpyAsync(sw.todo.ptr, ht, sizeof(int32_t) * 3 * T, hipMemcpyHostToDevice, st));
+                CA_HIP_CHECK(hipEventRecord(m->ev0, st));
+                hipLaunchKernelGGL(k_sweep_table, dim3(T), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
+                                   m->d_static.as<NodeStatic>(), n, in.d_mask.as<uint8_t>(), in.d_c.as<int32_t>(),
+                                   in.d_off.as<int32_t>(), in.d_moves.as<int32_t>(), m->d_pods.hot.as<PodHot>(),
+                                   m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
+                                   m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
+                                   in.d_hints.as<int32_t>(), sw.todo.as<int32_t>(), sw.todo.as<int32_t>() + T,
+                                   sw.todo.as<int32_t>() + 2 * T, sw.tab.as<int32_t>(), S);
+                CA_HIP_CHECK(hipGetLastError());
+                CA_HIP_CHECK(hipEventRecord(m->ev1, st));
+                // the table is stored [lane][candidate] so the host walk, whose window offset
+                // stays near the centre, reads it nearly sequentially
+                CA_HIP_CHECK(hipMemcpyAsync(tab, sw.tab.ptr, sizeof(int32_t) * 64 * (size_t)S, hipMemcpyDeviceToHost, st));
+                CA_HIP_CHECK(hipStreamSynchronize(st));
+                float ms = 0;
+                (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
+                kms += ms;
+                if (dbg_t) fprintf(stderr, "[sweep] table round %d: %d rows, kernel %.3f ms\n", rounds, T, ms);
+                tmark("table");
+            }
+            for (int32_t k = k0; k < S; k++) have[k] = 1;
+            // walk the exact chain as far as the windows reach
+            for (; k0 < S; k0++) {
+                const int32_t c = sens[k0];
+                const int32_t wlv = wlc[c];
+                exact_lin[c] = (int32_t)cur;
+                if (wlv < 0) continue;                                             // lastIndex passes through
+                if (wrap(cur, n) == guess[c]) { cur = wlv; continue; }            // probed at the true value
+                const int32_t w = wrap(cur - ws[k0], n);
+                if (w >= 64) break;
+                int32_t v = tab[(size_t)(w) * S + k0];
+                if (v == TB_UNKNOWN) {
+                    // hints / ports / long scans: exact kernel at the exact lastIndex, alone
+                    std::memset(h_need, 0, (size_t)C);
+                    h_need[c] = 1;
+                    h_lin[c] = (int32_t)cur;
+                    CA_HIP_CHECK(hipMemcpyAsync(d_lin, h_lin, (sizeof(int32_t) + 1) * (size_t)C, hipMemcpyHostToDevice, st));
+                    if ((rc = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl)) != CA_OK) return rc;
+                    SweepOut one;
+                    CA_HIP_CHECK(hipMemcpyAsync(&one, d_out.as<SweepOut>() + c, sizeof(SweepOut), hipMemcpyDeviceToHost, st));
+                    CA_HIP_CHECK(hipStreamSynchronize(st));
+                    exact_runs++;
+                    v = one.fa_success ? one.lout : (int32_t)cur;
+                } else {
+                    final_[c] = 0;
+                }
+                cur = v;
+            }
+            if (k0 >= S) break;
+            // re-centre the windows from k0 on: follow the tables where the estimate falls
+            // inside a window, otherwise shift the nearest known entry
+            int64_t est = cur;
+            for (int32_t k = k0; k < S; k++) {
+                if (insensitive(k)) continue;
+                const int32_t w = wrap(est - ws[k], n);
+                const int32_t v = w < 64 ? tab[(size_t)(w) * S + k] : TB_UNKNOWN;
+                if (w < 64 && v != TB_UNKNOWN) { est = v; continue; }
+                int64_t next = est + (move_off[sens[k] + 1] - move_off[sens[k]]);
+                int best = -1;              // known entry nearest the window centre
+                for (int d = 0; d <= 32 && best < 0; d++) {
+                    if (32 - d >= 0 && tab[(size_t)(32 - d) * S + k] != TB_UNKNOWN) best = 32 - d;
+                    else if (32 + d < 64 && tab[(size_t)(32 + d) * S + k] != TB_UNKNOWN) best = 32 + d;
+                }
+                if (best >= 0) {
+                    const int64_t from = (int64_t)ws[k] + best;
+                    next = est + wrap(tab[(size_t)(best) * S + k] - from, n);
+                }
+                if (w >= 64) { ws[k] = wrap(est - 32, n); have[k] = 0; }
+                est = wrap(next, n);
+            }
+            if (rounds > S + 4) { set_last_error("sweep speculation did not converge"); return CA_EDEVICE; }
+        }
+        tmark("host walk");
+        // exact pass for the candidates the host walk resolved through the table
+        int32_t n_rerun = 0;
+        for (int32_t c = 0; c < C; c++) {
+            h_need[c] = final_[c] ? 0 : 1;
+            h_lin[c] = exact_lin[c];
+            n_rerun += final_[c] ? 0 : 1;
+        }
+        if (n_rerun > 0) {
+            rounds++;
+            CA_HIP_CHECK(hipMemcpyAsync(d_lin, h_lin, (sizeof(int32_t) + 1) * (size_t)C, hipMemcpyHostToDevice, st));
+            if ((rc = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl)) != CA_OK) return rc;
+        }
+        CA_HIP_CHECK(hipMemcpyAsync(sw.h_out.ptr, sw.out.ptr, d2h_bytes, hipMemcpyDeviceToHost, st));
+        CA_HIP_CHECK(hipStreamSynchronize(st));
+    }
+    if (dbg_t) fprintf(stderr, "[sweep] exact fallbacks %d, device walk %s (stopped at %d of %d)\n", exact_runs,
+                       dev_walk ? "on" : "off", dev_walk ? h_info[0] : 0, S);
+    if (d_pod_hints && M > 0) {
+        hipLaunchKernelGGL(k_hints_apply, dim3((M + 255) / 256), dim3(256), 0, st, d_hset.as<int32_t>(),
+                           in.d_moves.as<int32_t>(), M, d_pod_hints);
+        CA_HIP_CHECK(hipGetLastError());
+    }
+    const auto t_exact = std::chrono::steady_clock::now();
+    if (M && out_dest) std::memcpy(out_dest, h_dest, sizeof(int32_t) * M);
+    // the outputs must reproduce the chain: each result with a successful scan was
+    // computed at the lastIndex the chain gives it; the others do not move it
+    int64_t Lrun = L0;
+    for (int32_t c = 0; c < C; c++) {
+        const SweepOut& o = outs[c];
+        if (o.status != CA_OK) { set_last_error("overlay capacity exceeded"); return o.status; }
+        if (o.fa_success && wrap(o.lin, n) != wrap(Lrun, n)) {
+            if (getenv("CASIM_DEBUG"))
+                fprintf(stderr, "chain mismatch at candidate %d: o.lin=%d Lrun=%ld\n", c, o.lin, (long)Lrun);
+            set_last_error("sweep lastIndex chain mismatch");
+            return CA_EDEVICE;
+        }
+        ca_removal_result& r = results[c];
+        r.removable = o.removable;
+        r.reason = o.reason;
+        r.n_placed = o.n_placed;
+        r.last_index_in = (int32_t)Lrun;
+        r.evals = o.evals;
+        if (o.fa_success) Lrun = o.lout;
+    }
+    *last_index = (int32_t)Lrun;
+    if (hints) {
+        for (int32_t i = 0; i < M; i++) if (hset[i] >= 0) hints[move_pods[i]] = hset[i];
+    }
+    if (d_pod_hints) CA_HIP_CHECK(hipStreamSynchronize(st));
+    tmark("done");
+    m->sweep_stats.rounds = rounds + exact_runs;
+    m->sweep_stats.exact_ms = 0;
+    m->sweep_stats.walk_ms = std::chrono::duration<float, std::milli>(t_exact - t_start).count();
+    m->sweep_stats.kernel_ms = kms;
+    m->sweep_stats.total_ms =
+        std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    return CA_OK;
+}
+
+}  // namespace casim
 
 extern "C" {
 
@@ -607,13 +1100,6 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
                             int32_t* hints, int32_t* last_index, ca_removal_result* results, int32_t* out_dest) {
     if (!m || (C > 0 && (!candidates || !dest_mask || !move_off || !results || !out_dest)) || !last_index || C < 0)
         return CA_EINVAL;
-    const auto t_start = std::chrono::steady_clock::now();
-    const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
-    auto tmark = [&](const char* what) {
-        if (dbg_t)
-            fprintf(stderr, "[sweep] %-14s %8.3f ms\n", what,
-                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
-    };
     CA_HIP_CHECK(hipSetDevice(m->device));
     hipStream_t st = m->stream;
     const int32_t n = (int32_t)m->nodes.size();
@@ -622,10 +1108,6 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     if (move_off[0] != 0 || M < 0) return CA_EINVAL;
     for (int32_t c = 0; c < C; c++)
         if (move_off[c + 1] < move_off[c]) return CA_EINVAL;
-    for (int32_t i = 0; i < M; i++) {
-        const int32_t id = move_pods[i];
-        if (id < 0 || (size_t)id >= m->pods.size()) return CA_EINVAL;
-    }
     // duplicate candidates share hints between their simulations: run them in
     // separate sequential segments (Hints.Set of one is seen by the next).
     {
@@ -647,298 +1129,41 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
         }
     }
     int rc;
-    tmark("validate");
     if ((rc = m->sync_nodes()) != CA_OK) return rc;
     if ((rc = m->sync_pods()) != CA_OK) return rc;
-    tmark("sync");
     const int32_t* status = cand_status;
     std::vector<int32_t> zero_status;
     if (!status) { zero_status.assign((size_t)C, 0); status = zero_status.data(); }
-
-    // candidates whose simulation can move lastIndex: valid, not blocked, pods to move
-    std::vector<int32_t> sens;
-    for (int32_t c = 0; c < C; c++) {
-        const int32_t nd = candidates[c];
-        if (nd < 0 || nd >= n || !dest_mask[nd] || status[c] != 0) continue;
-        if (move_off[c + 1] - move_off[c] == 0) continue;
-        sens.push_back(c);
-    }
-    const int32_t S = (int32_t)sens.size();
-
-    SweepScratch& sw = m->sw;
-    DevBuf &d_in = sw.in, &d_lin = sw.lin, &d_need = sw.need, &d_todo = sw.todo, &d_tab = sw.tab, &d_wl = sw.wl;
-    // outputs packed for one D2H: [SweepOut x C][dest M][hint set M]
-    const size_t out_bytes = sizeof(SweepOut) * (size_t)C + sizeof(int32_t) * 2 * (size_t)std::max(M, 1);
-    if ((rc = sw.out.reserve(out_bytes)) != CA_OK) return rc;
-    if ((rc = sw.h_out.reserve(out_bytes)) != CA_OK) return rc;
-    DevView d_out{sw.out.ptr};
-    DevView d_dest{sw.out.as<unsigned char>() + sizeof(SweepOut) * (size_t)C};
-    DevView d_hset{d_dest.as<int32_t>() + std::max(M, 1)};
     // one page-locked staging area and one H2D copy for every per-call input:
     // [cand C][status C][move_off C+1][move_pods M][hint per moved pod M][dest mask n bytes]
+    SweepScratch& sw = m->sw;
     const size_t in_ints = (size_t)C * 3 + 1 + (size_t)M * 2;
     const size_t in_bytes = sizeof(int32_t) * in_ints + (size_t)std::max(n, 1);
     if ((rc = sw.h_in.reserve(in_bytes)) != CA_OK) return rc;
-    if ((rc = d_in.reserve(in_bytes)) != CA_OK) return rc;
-    if ((rc = sw.h_tab.reserve(sizeof(int32_t) * 64 * (size_t)std::max(S, 1))) != CA_OK) return rc;
-    if ((rc = sw.h_todo.reserve(sizeof(int32_t) * 4 * (size_t)std::max(S, 1))) != CA_OK) return rc;
-    if ((rc = sw.h_lin.reserve((sizeof(int32_t) + 1) * (size_t)C)) != CA_OK) return rc;
-    if ((rc = d_lin.reserve(sizeof(int32_t) * C)) != CA_OK) return rc;
-    if ((rc = d_need.reserve((size_t)C)) != CA_OK) return rc;
-    if ((rc = d_todo.reserve(sizeof(int32_t) * 4 * std::max(S, 1))) != CA_OK) return rc;
-    if ((rc = d_tab.reserve(sizeof(int32_t) * 64 * (size_t)std::max(S, 1))) != CA_OK) return rc;
+    if ((rc = sw.in.reserve(in_bytes)) != CA_OK) return rc;
     int32_t* hin = sw.h_in.as<int32_t>();
     std::memcpy(hin, candidates, sizeof(int32_t) * C);
     std::memcpy(hin + C, status, sizeof(int32_t) * C);
     std::memcpy(hin + 2 * C, move_off, sizeof(int32_t) * (C + 1));
-    if (M) std::memcpy(hin + 3 * C + 1, move_pods, sizeof(int32_t) * M);
-    int32_t* hh = hin + 3 * C + 1 + M;
-    if (hints) for (int32_t i = 0; i < M; i++) hh[i] = hints[move_pods[i]];
-    else std::fill(hh, hh + M, -1);
+    int32_t* hm = hin + 3 * C + 1;
+    int32_t* hh = hm + M;
+    const int32_t np = (int32_t)m->pods.size();
+    for (int32_t i = 0; i < M; i++) {             // validate, stage, gather the hints in one pass
+        const int32_t id = move_pods[i];
+        if (id < 0 || id >= np) return CA_EINVAL;
+        hm[i] = id;
+        hh[i] = hints ? hints[id] : -1;
+    }
     std::memcpy(reinterpret_cast<uint8_t*>(hin + in_ints), dest_mask, (size_t)n);
-    CA_HIP_CHECK(hipMemcpyAsync(d_in.ptr, sw.h_in.ptr, in_bytes, hipMemcpyHostToDevice, st));
-    int32_t* const dptr = d_in.as<int32_t>();
-    DevView d_c{dptr}, d_status{dptr + C}, d_off{dptr + 2 * C}, d_moves{dptr + 3 * C + 1},
-        d_hints{dptr + 3 * C + 1 + M}, d_mask{dptr + in_ints};
-    int32_t* h_lin = sw.h_lin.as<int32_t>();
-    uint8_t* h_need = reinterpret_cast<uint8_t*>(h_lin + C);
-    tmark("upload");
-    if ((rc = d_wl.reserve(sizeof(int32_t) * (size_t)C)) != CA_OK) return rc;
-    if ((rc = sw.h_wl.reserve(sizeof(int32_t) * (size_t)C)) != CA_OK) return rc;
-    int32_t* const h_wl = sw.h_wl.as<int32_t>();
-    // ---- 1. probe: every candidate once, at a rough guess of its lastIndex ----
-    // A candidate's outputs depend on its input lastIndex only from its first successful
-    // FitsAnyNode scan on (hint checks and failed full scans do not depend on it).  The
-    // probe's results are final for every candidate without a successful scan (steady
-    // state: the hints of the previous loop place every pod), and for the others its
-    // advances calibrate the table windows.
-    const int64_t L0 = *last_index;               // raw until the first placement (Go keeps the int)
-    std::vector<int32_t> guess((size_t)C, 0);
-    std::vector<int32_t> ws((size_t)S, 0);          // window start per sensitive candidate
-    {
-        int64_t g = L0;
-        int32_t k = 0;
-        for (int32_t c = 0; c < C; c++) {
-            guess[c] = wrap(g, n);
-            if (k < S && sens[k] == c) {
-                ws[k] = wrap(g - 32, n);
-                g += move_off[c + 1] - move_off[c];     // every moved pod advances it at most... a guess
-                k++;
-            }
-        }
-    }
-    std::memcpy(h_lin, guess.data(), sizeof(int32_t) * C);
-    std::memset(h_need, 1, (size_t)C);
-    CA_HIP_CHECK(hipMemcpyAsync(d_lin.ptr, h_lin, sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
-    CA_HIP_CHECK(hipMemcpyAsync(d_need.ptr, h_need, (size_t)C, hipMemcpyHostToDevice, st));
-    CA_HIP_CHECK(hipEventRecord(m->ev0, st));
-    if ((rc = launch_exact(m, st, C, n, d_mask, d_c, d_status, d_off, d_moves, d_hints, d_lin, d_need, d_dest, d_hset,
-                           d_out, d_wl)) != CA_OK)
-        return rc;
-    int32_t* const tab = sw.h_tab.as<int32_t>();    // [64][S], filled by the table rounds
-    int32_t rounds = 1, exact_runs = 0;
-    if (S > 0 && n > 0) {
-        // ---- 2. first table round, windows centred on the probe's advances ----
-        rounds++;
-        int32_t* ht = sw.h_todo.as<int32_t>();
-        std::memcpy(ht, sens.data(), sizeof(int32_t) * S);
-        CA_HIP_CHECK(hipMemcpyAsync(d_todo.ptr, ht, sizeof(int32_t) * S, hipMemcpyHostToDevice, st));
-        int32_t* d_sens = d_todo.as<int32_t>();
-        int32_t* d_ws = d_sens + S;
-        hipLaunchKernelGGL(k_sweep_est, dim3(1), dim3(1024), 0, st, d_out.as<SweepOut>(), d_sens, S, (int64_t)L0, n,
-                           d_ws);
-        CA_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(k_sweep_table, dim3(S), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
-                           m->d_static.as<NodeStatic>(), n, d_mask.as<uint8_t>(), d_c.as<int32_t>(),
-                           d_off.as<int32_t>(), d_moves.as<int32_t>(), m->d_pods.hot.as<PodHot>(),
-                           m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
-                           m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
-                           d_hints.as<int32_t>(), d_sens, d_ws, (const int32_t*)nullptr, d_tab.as<int32_t>(), S);
-        CA_HIP_CHECK(hipGetLastError());
-        CA_HIP_CHECK(hipEventRecord(m->ev1, st));
-        CA_HIP_CHECK(hipMemcpyAsync(tab, d_tab.ptr, sizeof(int32_t) * 64 * (size_t)S, hipMemcpyDeviceToHost, st));
-        CA_HIP_CHECK(hipMemcpyAsync(ht, d_ws, sizeof(int32_t) * S, hipMemcpyDeviceToHost, st));
-        CA_HIP_CHECK(hipMemcpyAsync(h_wl, d_wl.ptr, sizeof(int32_t) * C, hipMemcpyDeviceToHost, st));
-        CA_HIP_CHECK(hipStreamSynchronize(st));
-        for (int32_t k = 0; k < S; k++) ws[k] = ht[k];
-    } else {
-        CA_HIP_CHECK(hipEventRecord(m->ev1, st));
-        CA_HIP_CHECK(hipMemcpyAsync(h_wl, d_wl.ptr, sizeof(int32_t) * C, hipMemcpyDeviceToHost, st));
-        CA_HIP_CHECK(hipStreamSynchronize(st));
-    }
-    float kms = 0;
-    {
-        float ms = 0;
-        (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
-        kms += ms;
-        if (dbg_t) fprintf(stderr, "[sweep] probe + table round: %d rows, kernels %.3f ms\n", S, ms);
-        tmark("probe+table");
-    }
-    // ---- 3. walk the lastIndex chain ----
-    // final[c]: the probe's outputs for c are exact (insensitive, or probed at the true
-    // lastIndex, or re-run alone); the rest re-run in one exact pass at exact_lin.
-    std::vector<int32_t> exact_lin((size_t)C, 0), exact_lout((size_t)C, 0);
-    std::vector<uint8_t> final_((size_t)C, 1);
-    std::vector<uint8_t> have((size_t)S, 1);        // table row computed for ws
-    std::vector<int32_t> todo, todo_ws, todo_k;
-    std::vector<uint8_t> need1((size_t)C, 0);
-    std::vector<int32_t> lin1((size_t)C, 0);
-    SweepOut one;
-    int32_t k0 = 0;               // first sensitive candidate not yet resolved
-    int64_t cur = L0;             // exact lastIndex before sens[k0]
-    auto insensitive = [&](int32_t k) { return h_wl[sens[k]] < 0; };
-    while (k0 < S) {
-        todo.clear(); todo_ws.clear(); todo_k.clear();
-        for (int32_t k = k0; k < S; k++)
-            if (!have[k] && !insensitive(k)) { todo.push_back(sens[k]); todo_ws.push_back(ws[k]); todo_k.push_back(k); }
-        if (!todo.empty()) {
-            rounds++;
-            const int32_t T = (int32_t)todo.size();
-            int32_t* ht = sw.h_todo.as<int32_t>();
-            std::memcpy(ht, todo.data(), sizeof(int32_t) * T);
-            std::memcpy(ht + T, todo_ws.data(), sizeof(int32_t) * T);
-            std::memcpy(ht + 2 * T, todo_k.data(), sizeof(int32_t) * T);
-            CA_HIP_CHECK(hipMemcpyAsync(d_todo.ptr, ht, sizeof(int32_t) * 3 * T, hipMemcpyHostToDevice, st));
-            CA_HIP_CHECK(hipEventRecord(m->ev0, st));
-            hipLaunchKernelGGL(k_sweep_table, dim3(T), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
-                               m->d_static.as<NodeStatic>(), n, d_mask.as<uint8_t>(), d_c.as<int32_t>(),
-                               d_off.as<int32_t>(), d_moves.as<int32_t>(), m->d_pods.hot.as<PodHot>(),
-                               m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
-                               m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
-                               d_hints.as<int32_t>(), d_todo.as<int32_t>(), d_todo.as<int32_t>() + T,
-                               d_todo.as<int32_t>() + 2 * T, d_tab.as<int32_t>(), S);
-            CA_HIP_CHECK(hipGetLastError());
-            CA_HIP_CHECK(hipEventRecord(m->ev1, st));
-            // the table is stored [lane][candidate] so the host walk, whose window offset
-            // stays near the centre, reads it nearly sequentially
-            CA_HIP_CHECK(hipMemcpyAsync(tab, d_tab.ptr, sizeof(int32_t) * 64 * (size_t)S, hipMemcpyDeviceToHost, st));
-            CA_HIP_CHECK(hipStreamSynchronize(st));
-            float ms = 0;
-            (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
-            kms += ms;
-            if (dbg_t) fprintf(stderr, "[sweep] table round %d: %d rows, kernel %.3f ms\n", rounds, T, ms);
-            tmark("table");
-        }
-        for (int32_t k = k0; k < S; k++) have[k] = 1;
-        // walk the exact chain as far as the windows reach
-        for (; k0 < S; k0++) {
-            const int32_t c = sens[k0];
-            const int32_t wl = h_wl[c];
-            exact_lin[c] = (int32_t)cur;
-            if (wl < 0) { exact_lout[c] = (int32_t)cur; continue; }            // lastIndex passes through
-            if (wrap(cur, n) == guess[c]) { exact_lout[c] = wl; cur = wl; continue; }   // probed at the true value
-            const int32_t w = wrap(cur - ws[k0], n);
-            if (w >= 64) break;
-            int32_t v = tab[(size_t)(w) * S + k0];
-            if (v == TB_UNKNOWN) {
-                // hints / ports / long scans: exact kernel at the exact lastIndex, alone
-                need1[c] = 1;
-                lin1[c] = (int32_t)cur;
-                std::memcpy(h_lin, lin1.data(), sizeof(int32_t) * C);
-                std::memcpy(h_need, need1.data(), (size_t)C);
-                CA_HIP_CHECK(hipMemcpyAsync(d_lin.ptr, h_lin, sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
-                CA_HIP_CHECK(hipMemcpyAsync(d_need.ptr, h_need, (size_t)C, hipMemcpyHostToDevice, st));
-                if ((rc = launch_exact(m, st, C, n, d_mask, d_c, d_status, d_off, d_moves, d_hints, d_lin, d_need,
-                                       d_dest, d_hset, d_out, d_wl)) != CA_OK)
-                    return rc;
-                CA_HIP_CHECK(hipMemcpyAsync(&one, d_out.as<SweepOut>() + c, sizeof(SweepOut), hipMemcpyDeviceToHost, st));
-                CA_HIP_CHECK(hipStreamSynchronize(st));
-                need1[c] = 0;
-                exact_runs++;
-                v = one.fa_success ? one.lout : (int32_t)cur;
-            } else {
-                final_[c] = 0;                                                   // re-run at exact_lin
-            }
-            exact_lout[c] = v;
-            cur = v;
-        }
-        if (k0 >= S) break;
-        // re-centre the windows from k0 on: follow the tables where the estimate falls
-        // inside a window, otherwise shift the nearest known entry
-        int64_t est = cur;
-        for (int32_t k = k0; k < S; k++) {
-            if (insensitive(k)) continue;
-            const int32_t w = wrap(est - ws[k], n);
-            const int32_t v = w < 64 ? tab[(size_t)(w) * S + k] : TB_UNKNOWN;
-            if (w < 64 && v != TB_UNKNOWN) { est = v; continue; }
-            int64_t next = est + (move_off[sens[k] + 1] - move_off[sens[k]]);
-            int best = -1;              // known entry nearest the window centre
-            for (int d = 0; d <= 32 && best < 0; d++) {
-                if (32 - d >= 0 && tab[(size_t)(32 - d) * S + k] != TB_UNKNOWN) best = 32 - d;
-                else if (32 + d < 64 && tab[(size_t)(32 + d) * S + k] != TB_UNKNOWN) best = 32 + d;
-            }
-            if (best >= 0) {
-                const int64_t from = (int64_t)ws[k] + best;
-                next = est + wrap(tab[(size_t)(best) * S + k] - from, n);
-            }
-            if (w >= 64) { ws[k] = wrap(est - 32, n); have[k] = 0; }
-            est = wrap(next, n);
-        }
-        if (rounds > S + 4) { set_last_error("sweep speculation did not converge"); return CA_EDEVICE; }
-    }
-    tmark("walk");
-    if (dbg_t) fprintf(stderr, "[sweep] exact fallbacks %d\n", exact_runs);
-    // ---- 4. exact pass for the candidates the probe did not settle ----
-    int32_t n_rerun = 0;
-    for (int32_t c = 0; c < C; c++) {
-        h_need[c] = final_[c] ? 0 : 1;
-        h_lin[c] = exact_lin[c];
-        n_rerun += final_[c] ? 0 : 1;
-    }
-    CA_HIP_CHECK(hipEventRecord(m->ev0, st));
-    if (n_rerun > 0) {
-        rounds++;
-        CA_HIP_CHECK(hipMemcpyAsync(d_lin.ptr, h_lin, sizeof(int32_t) * C, hipMemcpyHostToDevice, st));
-        CA_HIP_CHECK(hipMemcpyAsync(d_need.ptr, h_need, (size_t)C, hipMemcpyHostToDevice, st));
-        if ((rc = launch_exact(m, st, C, n, d_mask, d_c, d_status, d_off, d_moves, d_hints, d_lin, d_need, d_dest,
-                               d_hset, d_out, d_wl)) != CA_OK)
-            return rc;
-    }
-    CA_HIP_CHECK(hipEventRecord(m->ev1, st));
-    const SweepOut* outs = sw.h_out.as<SweepOut>();
-    const int32_t* h_dest = reinterpret_cast<const int32_t*>(outs + C);
-    const int32_t* hset = h_dest + std::max(M, 1);
-    CA_HIP_CHECK(hipMemcpyAsync(sw.h_out.ptr, sw.out.ptr, out_bytes, hipMemcpyDeviceToHost, st));
-    CA_HIP_CHECK(hipStreamSynchronize(st));
-    const auto t_exact = std::chrono::steady_clock::now();
-    tmark("exact");
-    if (M) std::memcpy(out_dest, h_dest, sizeof(int32_t) * M);
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
-    kms += ms;
-    // the outputs must reproduce the chain: each sensitive result was computed at the
-    // lastIndex the walk gives it, the others do not move it
-    int64_t Lrun = L0;
-    for (int32_t c = 0; c < C; c++) {
-        const SweepOut& o = outs[c];
-        if (o.status != CA_OK) { set_last_error("overlay capacity exceeded"); return o.status; }
-        if (o.fa_success && wrap(o.lin, n) != wrap(Lrun, n)) {
-            if (getenv("CASIM_DEBUG"))
-                fprintf(stderr, "chain mismatch at candidate %d: o.lin=%d Lrun=%ld final=%d\n", c, o.lin, (long)Lrun,
-                        (int)final_[c]);
-            set_last_error("sweep lastIndex chain mismatch");
-            return CA_EDEVICE;
-        }
-        ca_removal_result& r = results[c];
-        r.removable = o.removable;
-        r.reason = o.reason;
-        r.n_placed = o.n_placed;
-        r.last_index_in = (int32_t)Lrun;
-        r.evals = o.evals;
-        if (o.fa_success) Lrun = o.lout;
-    }
-    *last_index = (int32_t)Lrun;
-    if (hints) {
-        for (int32_t i = 0; i < M; i++) if (hset[i] >= 0) hints[move_pods[i]] = hset[i];
-    }
-    tmark("done");
-    m->sweep_stats.rounds = rounds + exact_runs;
-    m->sweep_stats.exact_ms = ms;
-    m->sweep_stats.walk_ms = std::chrono::duration<float, std::milli>(t_exact - t_start).count();
-    m->sweep_stats.kernel_ms = kms;
-    m->sweep_stats.total_ms =
-        std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_start).count();
-    return CA_OK;
+    CA_HIP_CHECK(hipMemcpyAsync(sw.in.ptr, sw.h_in.ptr, in_bytes, hipMemcpyHostToDevice, st));
+    int32_t* const dptr = sw.in.as<int32_t>();
+    SweepCall in;
+    in.C = C; in.M = M; in.n = n;
+    in.cand = candidates; in.status = status; in.move_off = move_off; in.move_pods = move_pods; in.dest_mask = dest_mask;
+    in.d_c = DevView{dptr}; in.d_status = DevView{dptr + C}; in.d_off = DevView{dptr + 2 * C};
+    in.d_moves = DevView{dptr + 3 * C + 1}; in.d_hints = DevView{dptr + 3 * C + 1 + M};
+    in.d_mask = DevView{dptr + in_ints};
+    return sweep_core(m, in, hints, nullptr, last_index, results, out_dest);
 }
 
 int ca_removal_timings(const ca_mirror* m, float* out, int32_t cap) {
@@ -949,11 +1174,123 @@ int ca_removal_timings(const ca_mirror* m, float* out, int32_t cap) {
     return 4;
 }
 
+int ca_removal_candidate_ticks(const ca_mirror* m, uint64_t* out, int32_t C) {
+    if (!m || C < 0 || (C > 0 && !out)) return CA_EINVAL;
+    if (m->sw.h_out.bytes < sizeof(SweepOut) * (size_t)C) return CA_EINVAL;
+    const SweepOut* o = m->sw.h_out.as<SweepOut>();
+    for (int32_t c = 0; c < C; c++) out[c] = o[c].pad2;
+    return CA_OK;
+}
+
 int ca_removal_stats(const ca_mirror* m, int32_t* rounds, float* kernel_ms, float* total_ms) {
     if (!m) return CA_EINVAL;
     if (rounds) *rounds = m->sweep_stats.rounds;
     if (kernel_ms) *kernel_ms = m->sweep_stats.kernel_ms;
     if (total_ms) *total_ms = m->sweep_stats.total_ms;
+    return CA_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// removal plan: the call's inputs resident in HBM across runs (FindNodesToRemove is
+// called every loop with the same candidates while the cluster is stable)
+// ---------------------------------------------------------------------------
+struct ca_removal_plan {
+    ca_mirror* m = nullptr;
+    int32_t C = 0, M = 0, n = 0;
+    std::vector<int32_t> cand, status, off, moves;
+    std::vector<uint8_t> mask;
+    casim::DevBuf d_in;
+    casim::HostBuf h_hints;
+    casim::SweepCall call() {
+        casim::SweepCall in;
+        in.C = C; in.M = M; in.n = n;
+        in.cand = cand.data(); in.status = status.data(); in.move_off = off.data(); in.move_pods = moves.data();
+        in.dest_mask = mask.data();
+        int32_t* d = d_in.as<int32_t>();
+        const size_t in_ints = (size_t)C * 3 + 1 + (size_t)M * 2;
+        in.d_c = casim::DevView{d}; in.d_status = casim::DevView{d + C}; in.d_off = casim::DevView{d + 2 * C};
+        in.d_moves = casim::DevView{d + 3 * C + 1}; in.d_hints = casim::DevView{d + 3 * C + 1 + M};
+        in.d_mask = casim::DevView{d + in_ints};
+        return in;
+    }
+};
+
+extern "C" {
+
+int ca_removal_plan_create(ca_mirror* m, const int32_t* candidates, int32_t C, const uint8_t* dest_mask,
+                           const int32_t* cand_status, const int32_t* move_off, const int32_t* move_pods,
+                           ca_removal_plan** out) {
+    if (!m || !out || C < 0 || (C > 0 && (!candidates || !dest_mask || !move_off))) return CA_EINVAL;
+    CA_HIP_CHECK(hipSetDevice(m->device));
+    const int32_t n = (int32_t)m->nodes.size();
+    const int32_t M = C > 0 ? move_off[C] - move_off[0] : 0;
+    if (C > 0 && (move_off[0] != 0 || M < 0)) return CA_EINVAL;
+    std::vector<uint8_t> seen((size_t)std::max(n, 1), 0);
+    for (int32_t c = 0; c < C; c++) {
+        if (move_off[c + 1] < move_off[c]) return CA_EINVAL;
+        const int32_t nd = candidates[c];
+        if (nd >= 0 && nd < n) {
+            if (seen[nd]) return CA_EUNSUPPORTED;     // duplicates: ca_find_nodes_to_remove splits them
+            seen[nd] = 1;
+        }
+    }
+    const int32_t np = (int32_t)m->pods.size();
+    for (int32_t i = 0; i < M; i++) if (move_pods[i] < 0 || move_pods[i] >= np) return CA_EINVAL;
+    ca_removal_plan* p = new ca_removal_plan();
+    p->m = m; p->C = C; p->M = M; p->n = n;
+    p->cand.assign(candidates, candidates + C);
+    p->status = cand_status ? std::vector<int32_t>(cand_status, cand_status + C) : std::vector<int32_t>((size_t)C, 0);
+    p->off.assign(move_off, move_off + C + 1);
+    p->moves.assign(move_pods, move_pods + M);
+    p->mask.assign(dest_mask, dest_mask + n);
+    const size_t in_ints = (size_t)C * 3 + 1 + (size_t)M * 2;
+    std::vector<int32_t> h(in_ints + ((size_t)std::max(n, 1) + 3) / 4, 0);
+    std::copy(p->cand.begin(), p->cand.end(), h.begin());
+    std::copy(p->status.begin(), p->status.end(), h.begin() + C);
+    std::copy(p->off.begin(), p->off.end(), h.begin() + 2 * C);
+    std::copy(p->moves.begin(), p->moves.end(), h.begin() + 3 * C + 1);
+    std::fill(h.begin() + 3 * C + 1 + M, h.begin() + 3 * C + 1 + 2 * M, -1);
+    std::memcpy(h.data() + in_ints, p->mask.data(), (size_t)n);
+    int rc = p->d_in.reserve(sizeof(int32_t) * h.size());
+    if (rc != CA_OK) { delete p; return rc; }
+    if (hipMemcpy(p->d_in.ptr, h.data(), sizeof(int32_t) * h.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        delete p;
+        casim::set_last_error("plan upload failed");
+        return CA_EDEVICE;
+    }
+    *out = p;
+    return CA_OK;
+}
+
+int ca_removal_plan_run(ca_removal_plan* p, int32_t* hints, int32_t* last_index, ca_removal_result* results,
+                        int32_t* out_dest) {
+    if (!p || !last_index || (p->C > 0 && !results)) return CA_EINVAL;
+    ca_mirror* m = p->m;
+    CA_HIP_CHECK(hipSetDevice(m->device));
+    if (p->C == 0) return CA_OK;
+    if ((int32_t)m->nodes.size() != p->n) return CA_EINVAL;   // the plan's dest mask covers the node list
+    int rc;
+    if ((rc = m->sync_nodes()) != CA_OK) return rc;
+    if ((rc = m->sync_pods()) != CA_OK) return rc;
+    casim::SweepCall in = p->call();
+    int32_t* d_pod_hints = nullptr;
+    if (hints) {                    // caller-held hints: gather per moved pod, one H2D
+        if ((rc = p->h_hints.reserve(sizeof(int32_t) * (size_t)std::max(p->M, 1))) != CA_OK) return rc;
+        int32_t* hh = p->h_hints.as<int32_t>();
+        for (int32_t i = 0; i < p->M; i++) hh[i] = hints[p->moves[i]];
+        if (p->M) CA_HIP_CHECK(hipMemcpyAsync(in.d_hints.ptr, hh, sizeof(int32_t) * p->M, hipMemcpyHostToDevice, m->stream));
+    } else {                        // the mirror's resident hints
+        if ((rc = m->ensure_pod_hints()) != CA_OK) return rc;
+        d_pod_hints = m->d_pod_hints.as<int32_t>();
+    }
+    return casim::sweep_core(m, in, hints, d_pod_hints, last_index, results, out_dest);
+}
+
+int ca_removal_plan_destroy(ca_removal_plan* p) {
+    if (!p) return CA_EINVAL;
+    delete p;
     return CA_OK;
 }
 

@@ -76,6 +76,12 @@ def load() -> C.CDLL:
         "ca_estimate_plan_group_ticks": ([vp, p(C.c_uint64), i32], C.c_int),
         "ca_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, p(i32), vp, vp], C.c_int),
         "ca_removal_stats": ([vp, p(i32), p(C.c_float), p(C.c_float)], C.c_int),
+        "ca_removal_plan_create": ([vp, vp, i32, vp, vp, vp, vp, p(vp)], C.c_int),
+        "ca_removal_plan_run": ([vp, vp, p(i32), vp, vp], C.c_int),
+        "ca_removal_plan_destroy": ([vp], C.c_int),
+        "ca_mirror_set_hints": ([vp, vp, i32], C.c_int),
+        "ca_mirror_get_hints": ([vp, vp, i32], C.c_int),
+        "ca_removal_candidate_ticks": ([vp, p(C.c_uint64), i32], C.c_int),
         "ca_removal_timings": ([vp, p(C.c_float), i32], C.c_int),
     }
     for name, (args, res) in sigs.items():
@@ -101,7 +107,9 @@ def exported_symbols() -> list[str]:
         "ca_fits_matrix", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
         "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_estimate_plan_timings",
         "ca_estimate_plan_group_ticks", "ca_find_nodes_to_remove",
-        "ca_removal_stats", "ca_removal_timings",
+        "ca_removal_stats", "ca_removal_timings", "ca_removal_plan_create", "ca_removal_plan_run",
+        "ca_removal_plan_destroy", "ca_mirror_set_hints", "ca_mirror_get_hints",
+        "ca_removal_candidate_ticks",
     ]
 
 
@@ -252,6 +260,23 @@ class Mirror:
                "ca_find_nodes_to_remove")
         return RemovalOutput(res, dest[: len(moves)], hints, li.value)
 
+    def set_hints(self, hints) -> None:
+        """The mirror's resident HintingSimulator hints (node per mirror pod, -1 = none)."""
+        h = np.ascontiguousarray(hints, dtype=np.int32)
+        _check(self.lib.ca_mirror_set_hints(self.h, ptr(h), len(h)), "ca_mirror_set_hints")
+
+    def get_hints(self, n_pods: int) -> np.ndarray:
+        h = np.zeros(n_pods, np.int32)
+        _check(self.lib.ca_mirror_get_hints(self.h, ptr(h), n_pods), "ca_mirror_get_hints")
+        return h
+
+    def candidate_ticks(self, n_candidates: int) -> np.ndarray:
+        """Per candidate of the last sweep: device time of its simulation, us."""
+        a = np.zeros(n_candidates, np.uint64)
+        _check(self.lib.ca_removal_candidate_ticks(self.h, a.ctypes.data_as(C.POINTER(C.c_uint64)), n_candidates),
+               "ca_removal_candidate_ticks")
+        return a.astype(np.float64) / 100.0
+
     def removal_stats(self) -> dict:
         r, k, t = C.c_int32(0), C.c_float(0), C.c_float(0)
         self.lib.ca_removal_stats(self.h, C.byref(r), C.byref(k), C.byref(t))
@@ -259,6 +284,49 @@ class Mirror:
         self.lib.ca_removal_timings(self.h, tm, 4)
         return {"rounds": r.value, "kernel_ms": k.value, "total_ms": t.value, "exact_ms": float(tm[1]),
                 "walk_ms": float(tm[2])}
+
+
+class RemovalPlan:
+    """``ca_removal_plan``: FindNodesToRemove inputs resident in HBM for repeated sweeps."""
+
+    def __init__(self, mirror: Mirror, candidates, dest_mask, cand_status, move_off, move_pods):
+        self.m = mirror
+        self.lib = mirror.lib
+        self.cand = np.ascontiguousarray(candidates, dtype=np.int32)
+        mask = np.ascontiguousarray(dest_mask, dtype=np.uint8)
+        status = np.ascontiguousarray(cand_status if cand_status is not None else np.zeros(len(self.cand)),
+                                      dtype=np.int32)
+        off = np.ascontiguousarray(move_off, dtype=np.int32)
+        self.moves = np.ascontiguousarray(move_pods, dtype=np.int32)
+        p = C.c_void_p()
+        _check(self.lib.ca_removal_plan_create(mirror.h, ptr(self.cand), len(self.cand), ptr(mask), ptr(status),
+                                               ptr(off), ptr(self.moves), C.byref(p)), "ca_removal_plan_create")
+        self.h = p
+        self.results = np.zeros(len(self.cand), abi.REMOVAL_RESULT_DTYPE)
+        self._dest = PinnedArray(self.lib, max(len(self.moves), 1), np.int32)
+
+    def run(self, last_index: int = 0, hints=None, want_dest: bool = False) -> RemovalOutput:
+        """One sweep.  hints=None: the mirror's resident hints are used and updated
+        (Mirror.set_hints / get_hints); else a per-pod array, updated in place."""
+        h = None if hints is None else np.ascontiguousarray(hints, dtype=np.int32)
+        li = C.c_int32(last_index)
+        dest = self._dest.array if want_dest else None
+        _check(self.lib.ca_removal_plan_run(self.h, ptr(h) if h is not None else None, C.byref(li), ptr(self.results),
+                                            ptr(dest) if dest is not None else None), "ca_removal_plan_run")
+        return RemovalOutput(self.results.copy(), dest[: len(self.moves)].copy() if dest is not None else None, h,
+                             li.value)
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.ca_removal_plan_destroy(self.h)
+            self.h = None
+            self._dest.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
 
 class PinnedArray:

@@ -36,15 +36,18 @@ METRIC = "pod×node predicate evals/sec; Estimate() latency, 50k pods × 100 nod
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E (MI355X_MICROARCH.md, chip table)
 BYTES_PER_EVAL = 64              # node record read per resource-only evaluation
 
-# Algorithmic HBM bytes per (pod, group) item of each Estimate phase:
-#   score   pod_idx 4 + PodHot 32 + score sums 16 + SortItem write 16
-#   merge   per pass: SortItem read 16 + write 16
-#   emit    SortItem 16 + pod_idx 4 + PodHot 32 + StreamPod write 32 + head bit
-#   chain   StreamPod read 32 + assign write 4
-#   compact assign read 2x4 + pod id 4 + sched_pod/sched_node writes 8
-PHASE_BYTES = {"score_ms": 68.0, "merge_ms": 32.0, "emit_ms": 84.125, "chain_ms": 36.0, "compact_ms": 20.0}
-PHASE_KERNEL = {"score_ms": "k_score_tiles", "merge_ms": "k_merge_runs", "emit_ms": "k_emit_stream",
-                "chain_ms": "k_ffd_chain", "compact_ms": "k_tile_count+k_tile_scatter"}
+# Algorithmic HBM bytes per (pod, group) item of each Estimate phase,
+# bucket-sort path (score classes <= 4096):
+#   score   k_class_rank: per class, not per item (0)
+#   merge   k_radix_hist + k_radix_scatter, per 8-bit pass: 2 x (pod_idx 4 + class 4 + rank 4)
+#           + position write 4
+#   emit    k_emit_bucket: position 4 + pod_idx 4 + PodHot 32 + StreamPod write 32 + pod id 4
+#           + head bit
+#   chain   k_ffd_chain: StreamPod read 32 + result write 4
+#   compact k_copy_segments: pod id read 4 + sched_pod write 4
+PHASE_BYTES = {"score_ms": 0.0, "merge_ms": 28.0, "emit_ms": 76.125, "chain_ms": 36.0, "compact_ms": 8.0}
+PHASE_KERNEL = {"score_ms": "k_class_rank", "merge_ms": "k_radix_hist+k_radix_scan+k_radix_scatter",
+                "emit_ms": "k_emit_bucket", "chain_ms": "k_ffd_chain", "compact_ms": "k_copy_segments"}
 
 
 def parse():
@@ -61,6 +64,8 @@ def parse():
                     help="also copy each scheduled pod's new-node ordinal to the host (not part of Estimate's "
                          "Go return value (int, []*Pod), estimator.go:40-42)")
     ap.add_argument("--cpu-groups", type=int, default=100, help="groups in the bounded CPU-baseline sample")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the C3 scale-down sweep leg (N=1 only)")
+    ap.add_argument("--sweep-nodes", type=int, default=5000)
     return ap.parse_args()
 
 
@@ -73,6 +78,57 @@ def cpu_model() -> str:
     except OSError:
         pass
     return platform.processor() or "unknown"
+
+
+def sweep_leg(args, device: int, with_cpu: bool) -> dict:
+    """C3 (BASELINE configs[2]): FindNodesToRemove over a 5k-node cluster with
+    150k running pods, legacy semantics, inputs resident in HBM (ca_removal_plan) and the
+    HintingSimulator's hints resident in the mirror.  'fresh' = first loop (no hints),
+    'hinted' = a following loop (the previous loop's hints: the steady state)."""
+    from autoscaler_amd import native
+    from autoscaler_amd import workloads as W
+    w = W.c3(n_nodes=args.sweep_nodes)
+    m = native.Mirror(device)
+    W.load_sweep(m, w)
+    sweep_args = (w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods)
+    fresh_h = np.full(len(w.table), -1, np.int32)
+    out = {"workload": f"C3: {args.sweep_nodes} nodes, {len(w.table)} running pods, candidates = all nodes",
+           "inputs": "resident in HBM (removal plan); hints resident in the mirror"}
+    with native.RemovalPlan(m, *sweep_args) as plan:
+        runs = {}
+        for mode in ("fresh", "hinted"):
+            ts = []
+            for _ in range(max(args.steps, 5)):
+                if mode == "fresh":
+                    m.set_hints(fresh_h)
+                t = time.perf_counter()
+                r = plan.run(0)
+                ts.append(time.perf_counter() - t)
+            runs[mode] = (r, m.get_hints(len(w.table)))
+            out[f"{mode}_ms"] = float(np.median(ts) * 1e3)
+            out[f"{mode}_evals"] = int(r.results["evals"].sum())
+            out[f"{mode}_removable"] = int(r.results["removable"].sum())
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle                                           # CPU baseline leg only
+        o = pyoracle.OracleState()
+        W.load_sweep(o, w)
+        h = fresh_h
+        for mode in ("fresh", "hinted"):
+            t = time.perf_counter()
+            ro = o.find_nodes_to_remove(*sweep_args, h, 0)
+            cpu_ms = (time.perf_counter() - t) * 1e3
+            r, hg = runs[mode]
+            out[f"{mode}_cpu_ms"] = cpu_ms
+            out[f"{mode}_speedup"] = cpu_ms / out[f"{mode}_ms"]
+            out[f"{mode}_parity"] = bool(np.array_equal(ro.results, r.results) and ro.last_index == r.last_index
+                                         and np.array_equal(ro.hints, hg))
+            h = ro.hints
+        out["cpu_baseline"] = {"kind": "port", "cores": 1,
+                               "sample": f"oracle/casim_oracle.c FindNodesToRemove, same C3 sweep, 1 thread of "
+                                         f"{cpu_model()}"}
+    m.close()
+    return out
 
 
 def main():
@@ -149,11 +205,8 @@ def main():
         total_evals = evals
     evals_per_step = evals / args.steps                         # this rank's batch
     items = int(w.group_off[-1])                                # (pod, group) items per batch
-    n_merge = 0
-    width = 1024
-    while width < int(np.diff(w.group_off).max()):
-        n_merge += 1
-        width *= 2
+    n_cls = len(set(zip(w.table.pods["score_milli_cpu"].tolist(), w.table.pods["score_memory"].tolist())))
+    n_merge = 1 if n_cls <= 256 else 2                            # radix passes (8-bit digits)
     ph_mean = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
     # dominant kernel of the step (longest device phase), with its algorithmic bytes
     dom = max(PHASE_BYTES, key=lambda k: ph_mean[k])
@@ -220,6 +273,8 @@ def main():
                 "speedup_vs_cpu_baseline": (total_evals / elapsed) / cpu["value"] if cpu else None,
             },
         }
+        if world == 1 and not args.no_sweep:
+            result["extra"]["sweep"] = sweep_leg(args, local, not args.no_cpu_baseline)
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.barrier()

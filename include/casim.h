@@ -352,8 +352,27 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t n_c
                             ca_removal_result* results, int32_t* out_dest);
 /* [0] device time of all sweep kernels, [1] of the exact pass, [2] host time until the
  * exact pass's results were on the host, [3] host wall time of the call (ms); returns 4. */
+/* Removal plan: FindNodesToRemove's inputs (candidates, destination mask, host drain
+ * verdicts, pods to move) uploaded once and resident in HBM, for repeated sweeps over an
+ * unchanged candidate set (RunOnce calls FindNodesToRemove every loop, legacy.go:146).
+ * Duplicate candidates: CA_EUNSUPPORTED (use ca_find_nodes_to_remove).  run: hints are
+ * per mirror pod in/out as in ca_find_nodes_to_remove, or NULL to use and update the
+ * mirror's resident hint table (ca_mirror_set_hints/get_hints: the HintingSimulator's
+ * hints kept in HBM, hinting_simulator.go:32-43).  out_dest may be NULL. */
+typedef struct ca_removal_plan ca_removal_plan;
+int ca_removal_plan_create(ca_mirror* m, const int32_t* candidates, int32_t n_candidates,
+                           const uint8_t* dest_mask, const int32_t* cand_status,
+                           const int32_t* move_off, const int32_t* move_pods, ca_removal_plan** out);
+int ca_removal_plan_run(ca_removal_plan* p, int32_t* hints, int32_t* last_index,
+                        ca_removal_result* results, int32_t* out_dest);
+int ca_removal_plan_destroy(ca_removal_plan* p);
+int ca_mirror_set_hints(ca_mirror* m, const int32_t* hints, int32_t n_pods);
+int ca_mirror_get_hints(ca_mirror* m, int32_t* hints, int32_t n_pods);
 int ca_removal_timings(const ca_mirror* m, float* out, int32_t cap);
 int ca_removal_stats(const ca_mirror* m, int32_t* rounds, float* kernel_ms, float* total_ms);
+/* Diagnostics: device wall-clock ticks (100 MHz) each candidate's simulation took in the
+ * last sweep's last exact pass that ran it (0 for candidates it did not run). */
+int ca_removal_candidate_ticks(const ca_mirror* m, uint64_t* out, int32_t n_candidates);
 
 #ifdef __cplusplus
 }

@@ -36,3 +36,22 @@ for name, hints in (("fresh", np.full(len(w.table), -1, np.int32)), ("hinted", N
           f"removable={int(rg.results['removable'].sum())} evals={int(ro.results['evals'].sum())} "
           f"stats={g.removal_stats()}", flush=True)
     h_next = ro.hints
+
+# inputs resident in HBM (removal plan), hints resident in the mirror
+with native.RemovalPlan(g, *args) as plan:
+    fresh = np.full(len(w.table), -1, np.int32)
+    for name in ("plan-fresh", "plan-hinted"):
+        ts = []
+        for _ in range(9):
+            if name == "plan-fresh":
+                g.set_hints(fresh)
+            t = time.perf_counter()
+            r = plan.run(0)
+            ts.append(time.perf_counter() - t)
+        print(f"{name}: gpu={np.median(ts)*1e3:.3f}ms stats={g.removal_stats()}", flush=True)
+    t = g.candidate_ticks(len(w.candidates))
+    nz = t[t > 0]
+    mo = np.diff(w.move_off)
+    print(f"candidate us (last run): max {nz.max():.1f} p50 {np.median(nz):.1f} mean {nz.mean():.1f} n={len(nz)}; "
+          f"moved pods max {mo.max()} mean {mo.mean():.1f}; slowest: {np.argsort(-t)[:5].tolist()} "
+          f"{np.sort(t)[::-1][:5].round(1).tolist()} pods {mo[np.argsort(-t)[:5]].tolist()}")

@@ -310,8 +310,11 @@ def test_sweep_random(seed, oracle):
     assert o.last_index == g.last_index
 
 
+@pytest.mark.parametrize("walk", ["device", "host"])
 @pytest.mark.parametrize("n_nodes", [300, 1500, 5000])
-def test_sweep_workload(n_nodes, oracle):
+def test_sweep_workload(n_nodes, walk, oracle, monkeypatch):
+    if walk == "host":
+        monkeypatch.setenv("CASIM_SWEEP_HOST_WALK", "1")
     w = W.c3(n_nodes=n_nodes)
     hints = np.full(len(w.table), -1, np.int32)
     outs = []
@@ -324,6 +327,35 @@ def test_sweep_workload(n_nodes, oracle):
     assert np.array_equal(o.dest, g.dest)
     assert np.array_equal(o.hints, g.hints)
     assert o.last_index == g.last_index
+
+
+@pytest.mark.parametrize("n_nodes", [400, 5000])
+def test_removal_plan_resident_hints(n_nodes, oracle):
+    """The removal plan (inputs resident in HBM) over two loops: fresh hints, then the
+    hints the first loop left in the mirror's resident table — vs the oracle's two
+    FindNodesToRemove calls with caller-held hints."""
+    w = W.c3(n_nodes=n_nodes)
+    o = oracle.OracleState()
+    W.load_sweep(o, w)
+    args = (w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods)
+    o1 = o.find_nodes_to_remove(*args, np.full(len(w.table), -1, np.int32), 0)
+    o2 = o.find_nodes_to_remove(*args, o1.hints, o1.last_index)
+    m = _mirror()
+    W.load_sweep(m, w)
+    m.set_hints(np.full(len(w.table), -1, np.int32))
+    with native.RemovalPlan(m, *args) as plan:
+        g1 = plan.run(0)
+        assert np.array_equal(o1.results, g1.results) and o1.last_index == g1.last_index
+        assert np.array_equal(m.get_hints(len(w.table)), o1.hints)
+        g2 = plan.run(g1.last_index, want_dest=True)
+        assert np.array_equal(o2.results, g2.results) and o2.last_index == g2.last_index
+        assert np.array_equal(o2.dest, g2.dest)
+        assert np.array_equal(m.get_hints(len(w.table)), o2.hints)
+        # caller-held hints through the plan
+        h = o1.hints.copy()
+        g3 = plan.run(o1.last_index, hints=h, want_dest=True)
+        assert np.array_equal(o2.results, g3.results) and np.array_equal(o2.dest, g3.dest)
+        assert np.array_equal(h, o2.hints)
 
 
 def test_sweep_with_hints_second_loop(oracle):

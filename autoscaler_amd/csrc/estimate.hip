@@ -617,6 +617,94 @@ __device__ inline int32_t run_end(const uint64_t* __restrict__ hm, int32_t pos, 
     return P;
 }
 
+// Zero-copy results (page-locked sched_pod, no node ordinals): a finished group hands
+// its output range to k_publish in PCH-sized tickets, so the results of the groups
+// that finish early cross PCIe while the long chains still run.  Release at agent scope:
+// the L2s of the 8 XCDs are not coherent, the publisher may run on another XCD.
+constexpr int PCH = 4096;
+__device__ inline void push_tickets(int32_t g, int32_t count, int32_t nsub, int32_t* tickets, int32_t* qctl, int lane) {
+    __threadfence();
+    if (lane == 0) {
+        const int32_t nt = (count + PCH - 1) / PCH;
+        const int32_t base = atomicAdd(&qctl[1], nt);
+        for (int32_t i = 0; i < nt; i++)
+            __hip_atomic_store(&tickets[base + i], g * nsub + i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Publisher (second stream, concurrent with k_ffd_chain): block b claims the next ticket
+// in completion order, waits for it, and writes outputs [sub*PCH, +PCH) of its group
+// into the caller's page-locked buffer: single placements from the chain's sched_pod,
+// run placements from the stream via the group's segments, -1 past n_scheduled.
+// Every block exits once all `total` tickets are claimed; a ticket not pushed within
+// the deadline (a chain that died) sets qctl[2] and ends the block.
+__global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ groups, const ChainOut* __restrict__ outs,
+                                                const Seg* __restrict__ segs, const int32_t* __restrict__ spod,
+                                                const int32_t* __restrict__ sched_dev, int32_t* __restrict__ tickets,
+                                                int32_t* __restrict__ qctl, int32_t total, int32_t nsub,
+                                                int32_t* __restrict__ pub) {
+    __shared__ int32_t s_t, s_tk, s_seg0;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            s_t = atomicAdd(&qctl[0], 1);
+            int32_t tk = -1;
+            if (s_t < total) {
+                const uint64_t t0 = wall_clock64();
+                for (;;) {
+                    tk = __hip_atomic_load(&tickets[s_t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    if (tk >= 0) break;
+                    if (wall_clock64() - t0 > 20000000ull) { atomicExch(&qctl[2], 1); break; }   // 200 ms
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            s_tk = tk;
+        }
+        __syncthreads();
+        const int32_t t = s_t, tk = s_tk;
+        if (t >= total || tk < 0) return;
+        __threadfence();                                   // acquire for every thread of the block
+        const int32_t g = tk / nsub, sub = tk - g * nsub;
+        const GroupMeta gm = groups[g];
+        const ChainOut o = outs[g];
+        const Seg* gs = segs + gm.off;
+        const int32_t a = sub * PCH, b = min(gm.count, a + PCH);
+        const int32_t ns = o.status == CA_OK ? o.n_sched : 0;
+        const int32_t nseg = o.status == CA_OK ? o.nseg : 0;
+        if (threadIdx.x == 0) {                            // first segment ending after a
+            int32_t lo = 0, hi = nseg;
+            while (lo < hi) {
+                const int32_t mid = (lo + hi) >> 1;
+                const Seg sg = gs[mid];
+                if (sg.dst + sg.len <= a) lo = mid + 1; else hi = mid;
+            }
+            s_seg0 = lo;
+        }
+        __syncthreads();
+        int32_t at = a, q = s_seg0;
+        const int32_t end = min(b, ns);
+        while (at < end) {
+            int32_t lim = end, src_off = 0;
+            bool from_seg = false;
+            if (q < nseg) {
+                const Seg sg = gs[q];
+                if (sg.dst <= at) {                            // inside segment q
+                    from_seg = true;
+                    src_off = sg.src - sg.dst;
+                    lim = min(end, sg.dst + sg.len);
+                    q++;
+                } else {
+                    lim = min(end, sg.dst);                    // single placements before it
+                }
+            }
+            for (int32_t i = at + (int32_t)threadIdx.x; i < lim; i += blockDim.x)
+                pub[gm.off + i] = from_seg ? spod[gm.off + src_off + i] : sched_dev[gm.off + i];
+            at = lim;
+        }
+        for (int32_t i = max(a, ns) + (int32_t)threadIdx.x; i < b; i += blockDim.x) pub[gm.off + i] = -1;
+        __syncthreads();
+    }
+}
+
 // One wavefront per node group.  LDS: NodeRec rows[kcap], block summaries[kcap/64]
 // (per-dimension maxima over a 64-row block, allowed to be stale-high), the per-run
 // scratch CAPA/ALIVE[kcap], and the optional port / scalar columns.
@@ -636,11 +724,12 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
     const int32_t* __restrict__ lin_arr, const uint8_t* __restrict__ need, const uint32_t* __restrict__ group_unsup,
     int32_t n_base, int32_t max_nodes, int32_t kcap, int32_t use_ports, int32_t use_scalar, int32_t batch_runs,
     int32_t* __restrict__ sched_pod, int32_t* __restrict__ sched_node, Seg* __restrict__ segs,
-    ChainOut* __restrict__ outs) {
+    int32_t* __restrict__ tickets, int32_t* __restrict__ qctl, int32_t nsub, ChainOut* __restrict__ outs) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int g = blockIdx.x;
     if (!need[g]) return;
     const uint64_t t_begin = wall_clock64();      // diagnostics: ca_estimate_plan_group_ticks
+    __builtin_amdgcn_s_setprio(3);                // the chain is the critical path: win issue over k_publish
 #ifdef CASIM_PROF
     const uint64_t t_cyc0 = clock64();
 #endif
@@ -658,6 +747,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
     if (group_unsup[g]) {
         res.status = CA_EUNSUPPORTED;
         if (lane == 0) outs[g] = res;
+        if (tickets) push_tickets(g, gm.count, nsub, tickets, qctl, lane);
         return;
     }
     const int nb_cap = (kcap + 63) >> 6;
@@ -1167,6 +1257,9 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
         res.nseg = nseg;
         res.pad = (uint64_t)(uint32_t)(wall_clock64() - t_begin) | ((uint64_t)n_single << 32);
         outs[g] = res;
+    }
+    if (tickets) push_tickets(g, P, nsub, tickets, qctl, lane);
+    if (lane == 0) {
 #ifdef CASIM_PROF
         prof[5] = clock64() - t_cyc0;
         if (g < 1024) for (int i = 0; i < 8; i++) g_chain_prof[g][i] = prof[i];
@@ -1184,10 +1277,13 @@ __global__ void __launch_bounds__(256) k_copy_segments(const GroupMeta* __restri
     const GroupMeta gm = groups[blockIdx.y];
     const ChainOut o = outs[blockIdx.y];
     const int32_t base = (int32_t)blockIdx.x * CPY_PER_BLOCK;
-    if (o.status != CA_OK || base >= o.n_sched || o.nseg == 0) return;
+    if (base >= gm.count) return;
+    const int32_t ns = o.status == CA_OK ? o.n_sched : 0;
+    const int32_t nseg = o.status == CA_OK ? o.nseg : 0;
     const Seg* gs = segs + gm.off;
-    for (int32_t i = base + (int32_t)threadIdx.x; i < min(base + CPY_PER_BLOCK, o.n_sched); i += blockDim.x) {
-        int32_t lo = 0, hi = o.nseg;               // first segment with dst > i
+    for (int32_t i = base + (int32_t)threadIdx.x; i < min(base + CPY_PER_BLOCK, gm.count); i += blockDim.x) {
+        if (i >= ns) { sched_pod[gm.off + i] = -1; continue; }   // past n_scheduled (or a failed group)
+        int32_t lo = 0, hi = nseg;                 // first segment with dst > i
         while (lo < hi) {
             const int32_t mid = (lo + hi) >> 1;
             if (gs[mid].dst <= i) lo = mid + 1; else hi = mid;
@@ -1224,8 +1320,16 @@ struct ca_estimate_plan {
     hipEvent_t ev[EV_N] = {};
     float t_ms[7] = {};
     std::vector<uint64_t> diag;     // per group: chain ticks (100 MHz) | single-pod steps << 32
+    // zero-copy publishing (k_publish on its own stream, concurrent with the chains)
+    hipStream_t pub_stream = nullptr;
+    hipEvent_t ev_go = nullptr, ev_pub = nullptr;
+    DevBuf d_tickets, d_qctl;
+    int32_t n_tickets = 0, nsub = 0;
     ~ca_estimate_plan() {
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+        if (ev_go) (void)hipEventDestroy(ev_go);
+        if (ev_pub) (void)hipEventDestroy(ev_pub);
+        if (pub_stream) (void)hipStreamDestroy(pub_stream);
     }
 };
 
@@ -1235,6 +1339,9 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
                  const int32_t* pod_idx, const ca_template* templates, int32_t G) {
     p->m = m; p->s = s; p->G = G;
     for (auto& e : p->ev) CA_HIP_CHECK(hipEventCreate(&e));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_go, hipEventDisableTiming));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_pub, hipEventDisableTiming));
+    CA_HIP_CHECK(hipStreamCreateWithFlags(&p->pub_stream, hipStreamNonBlocking));
     p->h_off.assign(group_off, group_off + G + 1);
     p->h_tmpl.assign(templates, templates + G);
     p->total = group_off[G] - group_off[0];
@@ -1294,6 +1401,11 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     if ((rc = p->d_heads.reserve(sizeof(uint64_t) * (size_t)std::max(p->n_masks, 1))) != CA_OK) return rc;
     if ((rc = p->d_spod.reserve(sizeof(int32_t) * tot)) != CA_OK) return rc;
     if ((rc = p->d_seg.reserve(sizeof(Seg) * tot)) != CA_OK) return rc;
+    p->n_tickets = 0;
+    for (int32_t g = 0; g < G; g++) p->n_tickets += (p->h_meta[g].count + PCH - 1) / PCH;
+    p->nsub = std::max(1, (p->max_count + PCH - 1) / PCH);
+    if ((rc = p->d_tickets.reserve(sizeof(int32_t) * (size_t)std::max(p->n_tickets, 1))) != CA_OK) return rc;
+    if ((rc = p->d_qctl.reserve(sizeof(int32_t) * 4)) != CA_OK) return rc;
     if ((rc = p->d_unsup.reserve(sizeof(uint32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
     if ((rc = p->d_lin.reserve(sizeof(int32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
     if ((rc = p->d_need.reserve((size_t)std::max(G, 1))) != CA_OK) return rc;
@@ -1310,6 +1422,11 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     if (G) CA_HIP_CHECK(hipMemcpyAsync(p->d_tmpl.ptr, templates, sizeof(ca_template) * G, hipMemcpyHostToDevice, st));
     CA_HIP_CHECK(hipStreamSynchronize(st));
     return CA_OK;
+}
+
+int32_t pub_blocks() {
+    const char* e = getenv("CASIM_PUB_BLOCKS");
+    return e ? std::max(1, atoi(e)) : 16;
 }
 
 size_t chain_lds_bytes(int32_t kcap, bool use_ports, bool use_scalar) {
@@ -1336,7 +1453,18 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     const size_t lds = chain_lds_bytes(kcap, p->use_ports, p->use_scalar);
     if (lds > 160 * 1024) return CA_EUNSUPPORTED;   // HBM-backed variant is future work
     CA_HIP_CHECK(hipMemsetAsync(p->d_unsup.ptr, 0, sizeof(uint32_t) * G, st));
-    if (p->total > 0) {   // entries past n_scheduled read back as -1
+    // Zero-copy results: when the caller's sched_pod is page-locked (ca_host_alloc) and no
+    // node ordinals are wanted, the chains publish straight into it (k_ffd_chain epilogue).
+    int32_t* publish = nullptr;
+    if (!sched_node && p->total > 0 && (int64_t)G * p->nsub < INT32_MAX && !getenv("CASIM_NO_PUBLISH")) {
+        hipPointerAttribute_t attr;
+        if (hipPointerGetAttributes(&attr, sched_pod) == hipSuccess && attr.type == hipMemoryTypeHost &&
+            attr.devicePointer != nullptr)
+            publish = static_cast<int32_t*>(attr.devicePointer);
+        else
+            (void)hipGetLastError();
+    }
+    if (p->total > 0 && !publish) {   // entries past n_scheduled read back as -1
         CA_HIP_CHECK(hipMemsetAsync(p->d_sched_pod.ptr, 0xFF, sizeof(int32_t) * p->total, st));
         if (sched_node) CA_HIP_CHECK(hipMemsetAsync(p->d_sched_node.ptr, 0xFF, sizeof(int32_t) * p->total, st));
     }
@@ -1414,6 +1542,14 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         rounds++;
         CA_HIP_CHECK(hipMemcpyAsync(p->d_lin.ptr, lin.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
         CA_HIP_CHECK(hipMemcpyAsync(p->d_need.ptr, need.data(), G, hipMemcpyHostToDevice, st));
+        int32_t round_tickets = 0;
+        if (publish) {
+            for (int32_t g = 0; g < G; g++) if (need[g]) round_tickets += (p->h_meta[g].count + PCH - 1) / PCH;
+            if (rounds > 1) CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_pub, 0));   // previous publisher done
+            CA_HIP_CHECK(hipMemsetAsync(p->d_tickets.ptr, 0xFF, sizeof(int32_t) * (size_t)std::max(round_tickets, 1), st));
+            CA_HIP_CHECK(hipMemsetAsync(p->d_qctl.ptr, 0, sizeof(int32_t) * 4, st));
+            CA_HIP_CHECK(hipEventRecord(p->ev_go, st));
+        }
         CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN0], st));
         CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_ffd_chain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL(k_ffd_chain, dim3(G), dim3(64), lds, st, p->d_meta.as<GroupMeta>(),
@@ -1422,8 +1558,18 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                            p->d_need.as<uint8_t>(), p->d_unsup.as<uint32_t>(), n_base, lim->max_nodes, kcap,
                            p->use_ports ? 1 : 0, p->use_scalar ? 1 : 0, batch_runs,
                            p->d_sched_pod.as<int32_t>(), sched_node ? p->d_sched_node.as<int32_t>() : nullptr,
-                           p->d_seg.as<Seg>(), p->d_out.as<ChainOut>());
+                           p->d_seg.as<Seg>(), publish ? p->d_tickets.as<int32_t>() : nullptr,
+                           p->d_qctl.as<int32_t>(), p->nsub, p->d_out.as<ChainOut>());
         CA_HIP_CHECK(hipGetLastError());
+        if (publish && round_tickets > 0) {
+            CA_HIP_CHECK(hipStreamWaitEvent(p->pub_stream, p->ev_go, 0));
+            hipLaunchKernelGGL(k_publish, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, p->pub_stream,
+                               p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
+                               p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int32_t>(),
+                               p->d_qctl.as<int32_t>(), round_tickets, p->nsub, publish);
+            CA_HIP_CHECK(hipGetLastError());
+            CA_HIP_CHECK(hipEventRecord(p->ev_pub, p->pub_stream));
+        }
         CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN1], st));
         std::vector<ChainOut> fresh(G);
         CA_HIP_CHECK(hipMemcpyAsync(fresh.data(), p->d_out.ptr, sizeof(ChainOut) * G, hipMemcpyDeviceToHost, st));
@@ -1473,15 +1619,33 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         if (rounds > G + 2) { set_last_error("estimate speculation did not converge"); return CA_EDEVICE; }
     }
     // results: the chains wrote single placements directly; fill the run placements
-    if (p->total > 0) {
+    if (p->total > 0 && !publish) {
         hipLaunchKernelGGL(k_copy_segments, dim3((p->max_count + CPY_PER_BLOCK - 1) / CPY_PER_BLOCK, G), dim3(256), 0, st,
                            p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
                            p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>());
         CA_HIP_CHECK(hipGetLastError());
     }
     CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_COMPACT], st));
-    CA_HIP_CHECK(hipMemcpyAsync(sched_pod, p->d_sched_pod.ptr, sizeof(int32_t) * std::max(p->total, 0),
-                                hipMemcpyDeviceToHost, st));
+    if (publish) {
+        // the publisher of the last round wrote the results; a deadline hit (a chain that
+        // died) falls back to the device copy + D2H
+        int32_t qc[4] = {0, 0, 0, 0};
+        CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_pub, 0));
+        CA_HIP_CHECK(hipMemcpyAsync(qc, p->d_qctl.ptr, sizeof(qc), hipMemcpyDeviceToHost, st));
+        CA_HIP_CHECK(hipStreamSynchronize(st));
+        if (qc[2] != 0) {
+            set_last_error("estimate publisher missed a ticket; results copied instead");
+            hipLaunchKernelGGL(k_copy_segments, dim3((p->max_count + CPY_PER_BLOCK - 1) / CPY_PER_BLOCK, G), dim3(256), 0,
+                               st, p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
+                               p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>());
+            CA_HIP_CHECK(hipGetLastError());
+            CA_HIP_CHECK(hipMemcpyAsync(sched_pod, p->d_sched_pod.ptr, sizeof(int32_t) * std::max(p->total, 0),
+                                        hipMemcpyDeviceToHost, st));
+        }
+    } else {
+        CA_HIP_CHECK(hipMemcpyAsync(sched_pod, p->d_sched_pod.ptr, sizeof(int32_t) * std::max(p->total, 0),
+                                    hipMemcpyDeviceToHost, st));
+    }
     if (sched_node)
         CA_HIP_CHECK(hipMemcpyAsync(sched_node, p->d_sched_node.ptr, sizeof(int32_t) * std::max(p->total, 0),
                                     hipMemcpyDeviceToHost, st));

@@ -236,7 +236,8 @@ def test_estimate_many_score_classes(shapes, oracle):
 
 
 def test_estimate_full_c2_parity(oracle):
-    """BASELINE configs[1] at full size (50k pods x 100 groups): bit-exact vs the oracle."""
+    """BASELINE configs[1] at full size (50k pods x 100 groups): bit-exact vs the oracle,
+    through ca_estimate_batch and through a plan publishing into page-locked memory."""
     w = W.c2()
     outs = []
     for b in (oracle.OracleState(), _mirror()):
@@ -247,6 +248,43 @@ def test_estimate_full_c2_parity(oracle):
     assert np.array_equal(o.sched_pod, g.sched_pod)
     assert np.array_equal(o.sched_node, g.sched_node)
     assert o.last_index == g.last_index
+    m = _mirror()
+    W.load_estimate(m, w)
+    with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as plan:
+        for _ in range(2):
+            p = plan.run(w.max_nodes, 0, want_nodes=False)
+            assert np.array_equal(o.results, p.results)
+            assert np.array_equal(o.sched_pod, p.sched_pod)
+            assert o.last_index == p.last_index
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_estimate_plan_publish_random(seed, oracle):
+    """Zero-copy results (plan, page-locked sched_pod, no node ordinals) on random inputs,
+    including unsupported and capacity-limited groups."""
+    rng, nodes, pods, templates, groups = _run_heavy_inputs(seed)
+    table, node_recs, tm, off, pod_idx = _encode_estimate(nodes, pods, templates, groups)
+    max_nodes = rng.choice([0, 1, 5, 40])
+    L0 = rng.choice([0, 3, 123])
+    o = oracle.OracleState()
+    o.clear()
+    if len(node_recs):
+        o.add_nodes(node_recs)
+    ro = o.estimate(table, off, pod_idx, tm, max_nodes, L0)
+    m = _mirror()
+    if len(node_recs):
+        m.add_nodes(node_recs)
+    with native.EstimatePlan(m, table, off, pod_idx, tm) as plan:
+        g = plan.run(max_nodes, L0, want_nodes=False)
+    assert np.array_equal(ro.results, g.results)
+    for k in range(len(groups)):
+        if int(ro.results[k]["status"]) != 0:
+            continue
+        a, b = off[k], off[k + 1]
+        n = int(ro.results[k]["n_scheduled"])
+        assert np.array_equal(ro.sched_pod[a:a + n], g.sched_pod[a:a + n]), (seed, k)
+        assert (g.sched_pod[a + n:b] == -1).all()
+    assert ro.last_index == g.last_index
 
 
 def test_estimate_full_c2_properties():

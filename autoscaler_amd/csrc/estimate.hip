@@ -1273,7 +1273,8 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
 constexpr int CPY_PER_BLOCK = 2048;
 __global__ void __launch_bounds__(256) k_copy_segments(const GroupMeta* __restrict__ groups,
                                                       const ChainOut* __restrict__ outs, const Seg* __restrict__ segs,
-                                                      const int32_t* __restrict__ spod, int32_t* __restrict__ sched_pod) {
+                                                      const int32_t* __restrict__ spod, int32_t* __restrict__ sched_pod,
+                                                      int32_t* __restrict__ sched_node) {
     const GroupMeta gm = groups[blockIdx.y];
     const ChainOut o = outs[blockIdx.y];
     const int32_t base = (int32_t)blockIdx.x * CPY_PER_BLOCK;
@@ -1282,7 +1283,11 @@ __global__ void __launch_bounds__(256) k_copy_segments(const GroupMeta* __restri
     const int32_t nseg = o.status == CA_OK ? o.nseg : 0;
     const Seg* gs = segs + gm.off;
     for (int32_t i = base + (int32_t)threadIdx.x; i < min(base + CPY_PER_BLOCK, gm.count); i += blockDim.x) {
-        if (i >= ns) { sched_pod[gm.off + i] = -1; continue; }   // past n_scheduled (or a failed group)
+        if (i >= ns) {                             // past n_scheduled (or a failed group): also what
+            sched_pod[gm.off + i] = -1;            // an earlier speculation round of the group wrote
+            if (sched_node) sched_node[gm.off + i] = -1;
+            continue;
+        }
         int32_t lo = 0, hi = nseg;                 // first segment with dst > i
         while (lo < hi) {
             const int32_t mid = (lo + hi) >> 1;
@@ -1622,7 +1627,8 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     if (p->total > 0 && !publish) {
         hipLaunchKernelGGL(k_copy_segments, dim3((p->max_count + CPY_PER_BLOCK - 1) / CPY_PER_BLOCK, G), dim3(256), 0, st,
                            p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
-                           p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>());
+                           p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(),
+                           sched_node ? p->d_sched_node.as<int32_t>() : nullptr);
         CA_HIP_CHECK(hipGetLastError());
     }
     CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_COMPACT], st));
@@ -1637,7 +1643,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             set_last_error("estimate publisher missed a ticket; results copied instead");
             hipLaunchKernelGGL(k_copy_segments, dim3((p->max_count + CPY_PER_BLOCK - 1) / CPY_PER_BLOCK, G), dim3(256), 0,
                                st, p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
-                               p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>());
+                               p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), nullptr);
             CA_HIP_CHECK(hipGetLastError());
             CA_HIP_CHECK(hipMemcpyAsync(sched_pod, p->d_sched_pod.ptr, sizeof(int32_t) * std::max(p->total, 0),
                                         hipMemcpyDeviceToHost, st));

@@ -208,3 +208,234 @@ def load_sweep(backend, w: SweepWorkload) -> np.ndarray:
     backend.add_nodes(w.nodes)
     ids = backend.add_pods(w.table, np.arange(len(w.table), dtype=np.int32), w.pod_node)
     return ids
+
+
+# ---------------------------------------------------------------------------
+# C4: taint / toleration + node-affinity-heavy
+# ---------------------------------------------------------------------------
+C4_KEYS = 12            # label keys; key 0 is the integer key (Gt/Lt), keys 1..11 string keys
+C4_PAIRS = 64           # interned (key, value) pairs over keys 1..11
+C4_TAINT_CLASSES = 20
+
+
+class _C4Universe:
+    """Interned attribute universe shared by nodes, templates and pods."""
+
+    def __init__(self, rng):
+        # pair p belongs to string key pair_key[p] (1..11), values spread over the keys
+        self.pair_key = np.array([1 + (p % (C4_KEYS - 1)) for p in range(C4_PAIRS)], np.int64)
+        # taint class effects: 0 NoSchedule, 1 NoExecute, 2 PreferNoSchedule (not a filter)
+        self.taint_effect = rng.integers(0, 3, C4_TAINT_CLASSES)
+        self.filter_taints = np.nonzero(self.taint_effect != 2)[0]
+
+    def node_attrs(self, rng, n_taints: int):
+        """(taint mask, pair bitset word, key mask, int label) of one node / template."""
+        classes = rng.choice(C4_TAINT_CLASSES, size=n_taints, replace=False) if n_taints else np.zeros(0, int)
+        mask = 0
+        for c in classes:
+            if self.taint_effect[c] != 2:          # PreferNoSchedule is not interned for filtering
+                mask |= 1 << int(c)
+        pairs, keys = 0, 1                          # key 0 (integer) always present
+        for k in range(1, C4_KEYS):
+            if rng.random() < 0.75:
+                cand = np.nonzero(self.pair_key == k)[0]
+                pairs |= 1 << int(rng.choice(cand))
+                keys |= 1 << k
+        return mask, pairs, keys, int(rng.integers(0, 100))
+
+
+def _c4_pod_spec(rng, uni: _C4Universe, terms: list, reqs: list, anchor=None):
+    """Tolerations, nodeSelector and required node-affinity terms of one controller's pods.
+    anchor = (taints, pairs, keys, ival) of a node the pods must fit (sweep), or None."""
+    tol = 0
+    if rng.random() < 0.05:
+        tol = (1 << 64) - 1                        # a key-less Exists toleration: every taint
+    else:
+        for c in uni.filter_taints:
+            if rng.random() < 0.4:
+                tol |= 1 << int(c)
+        if anchor is not None:
+            tol |= anchor[0]
+    sel = 0
+    if rng.random() < 0.60:
+        if anchor is not None:
+            have = [p for p in range(C4_PAIRS) if (anchor[1] >> p) & 1]
+            pick = rng.choice(have, size=min(len(have), int(rng.integers(1, 4))), replace=False) if have else []
+        else:
+            pick = rng.choice(C4_PAIRS, size=int(rng.integers(1, 4)), replace=False)
+            # at most one pair per key (a selector with two values of one key matches nothing)
+            seen, keep = set(), []
+            for p in pick:
+                if uni.pair_key[p] not in seen:
+                    seen.add(uni.pair_key[p])
+                    keep.append(p)
+            pick = keep
+        for p in pick:
+            sel |= 1 << int(p)
+    first, count = 0, -1
+    if rng.random() < 0.20:
+        first, count = len(terms), 2
+        for t in range(2):
+            tf = len(reqs)
+            for e in range(2):
+                op = int(rng.choice([abi.CA_OP_IN, abi.CA_OP_NOTIN, abi.CA_OP_EXISTS, abi.CA_OP_GT]))
+                r = np.zeros(1, abi.REQ_DTYPE)[0]
+                r["op"] = op
+                if op == abi.CA_OP_GT:
+                    r["key"] = 0
+                    r["bound"] = int(rng.integers(0, 60))
+                    if anchor is not None and t == 0 and not anchor[3] > r["bound"]:
+                        r["bound"] = anchor[3] - 1
+                elif op == abi.CA_OP_EXISTS:
+                    k = int(rng.integers(1, C4_KEYS))
+                    if anchor is not None and t == 0:
+                        ks = [kk for kk in range(1, C4_KEYS) if (anchor[2] >> kk) & 1]
+                        k = int(rng.choice(ks)) if ks else 0
+                    r["key"] = k
+                else:
+                    k = int(rng.integers(1, C4_KEYS))
+                    vals = np.nonzero(uni.pair_key == k)[0]
+                    chosen = rng.choice(vals, size=min(len(vals), int(rng.integers(1, 3))), replace=False)
+                    word = 0
+                    for p in chosen:
+                        word |= 1 << int(p)
+                    if anchor is not None and t == 0:
+                        node_pairs_k = anchor[1] & sum(1 << int(p) for p in vals)
+                        if op == abi.CA_OP_IN:
+                            word |= node_pairs_k if node_pairs_k else 0
+                            if not node_pairs_k:
+                                r["op"] = abi.CA_OP_NOTIN
+                        else:
+                            word &= ~node_pairs_k
+                    r["key"] = k
+                    r["pairs"][0] = np.uint64(word & ((1 << 64) - 1))
+                reqs.append(r)
+            terms.append((tf, 2))
+    return tol, sel, first, count
+
+
+def _c4_static_ok(tol, sel, first, count, terms, reqs, node_taints, node_pairs, node_keys, ival) -> bool:
+    """Template-side static filters (TaintToleration, NodeAffinity) of one pod spec."""
+    if node_taints & ~tol & ((1 << 64) - 1):
+        return False
+    if (node_pairs & sel) != sel:
+        return False
+    if count < 0:
+        return True
+    for t in range(first, first + count):
+        tf, tc = terms[t]
+        ok = True
+        for r in reqs[tf:tf + tc]:
+            op, key, bound, word = int(r["op"]), int(r["key"]), int(r["bound"]), int(r["pairs"][0])
+            if op == abi.CA_OP_IN:
+                ok = (node_pairs & word) != 0
+            elif op == abi.CA_OP_NOTIN:
+                ok = (node_pairs & word) == 0
+            elif op == abi.CA_OP_EXISTS:
+                ok = bool((node_keys >> key) & 1)
+            elif op == abi.CA_OP_GT:
+                ok = ival > bound
+            if not ok:
+                break
+        if ok:
+            return True
+    return False
+
+
+def _c4_encode_spec(p, tol, sel, first, count):
+    p["tolerated_taints"] = np.uint64(tol & ((1 << 64) - 1))
+    p["node_selector"][:, 0] = np.uint64(sel)
+    p["aff_term_first"] = first
+    p["aff_term_count"] = count
+    if sel or count >= 0:
+        p["flags"] |= abi.CA_POD_AFFINITY_FILTER
+
+
+def _c4_node(rec, attrs):
+    taints, pairs, keys, ival = attrs
+    rec["taints"] = np.uint64(taints)
+    rec["label_pairs"][0] = np.uint64(pairs)
+    rec["label_keys"] = np.uint64(keys)
+    rec["int_label"][0] = ival
+    rec["int_label_valid"] = 1
+
+
+def c4(n_pods: int = 50_000, n_groups: int = 100, n_existing: int = 1000, max_nodes: int = 1000,
+       seed: int = 1234, pods_per_controller: int = 100) -> EstimateWorkload:
+    """C4 Estimate batch: C2 shapes and templates plus 20 taint classes (0-3 per template),
+    64 label pairs over 12 keys (one integer key), 60% of controllers with a nodeSelector of
+    1-3 pairs, 20% with 2 required terms x 2 expressions (In/NotIn/Exists/Gt), 5% tolerating
+    everything.  Group pod lists = the pods passing CheckPredicates on the template
+    (ComputeExpansionOption, orchestrator.go:455-481): resources and static filters."""
+    rng = np.random.default_rng(seed)
+    uni = _C4Universe(rng)
+    shapes = [(c, m) for c in C2_CPU for m in C2_MEM]
+    n_ctrl = max(1, (n_pods + pods_per_controller - 1) // pods_per_controller)
+    ctrl_shape = rng.integers(0, len(shapes), n_ctrl)
+    terms: list = []
+    reqs: list = []
+    ctrl_spec = [_c4_pod_spec(rng, uni, terms, reqs) for _ in range(n_ctrl)]
+    ctrl_of_pod = np.repeat(np.arange(n_ctrl), pods_per_controller)[:n_pods]
+    cpu = np.array([shapes[ctrl_shape[c]][0] for c in ctrl_of_pod], np.int64)
+    mem = np.array([shapes[ctrl_shape[c]][1] for c in ctrl_of_pod], np.int64)
+    pods = resource_pods(cpu, mem)
+    pods["similar_class"] = ctrl_of_pod
+    for c in range(n_ctrl):
+        sl = slice(c * pods_per_controller, min(n_pods, (c + 1) * pods_per_controller))
+        _c4_encode_spec(pods[sl], *ctrl_spec[c])
+    term_arr = np.array(terms, dtype=abi.TERM_DTYPE) if terms else np.zeros(0, abi.TERM_DTYPE)
+    req_arr = np.array(reqs, dtype=abi.REQ_DTYPE) if reqs else np.zeros(0, abi.REQ_DTYPE)
+    templates = np.zeros(n_groups, abi.TEMPLATE_DTYPE)
+    offs, parts = [0], []
+    for g in range(n_groups):
+        cores = C2_CORES[rng.integers(0, len(C2_CORES))]
+        mpc = C2_MEM_PER_CORE[rng.integers(0, len(C2_MEM_PER_CORE))]
+        acpu = cores * 1000 * 95 // 100
+        amem = cores * mpc * GI * 95 // 100
+        ds = int(rng.integers(0, 4))
+        templates[g] = make_template(acpu, amem, 110, ds, name_id=-1000 - g)[0]
+        attrs = uni.node_attrs(rng, int(rng.integers(0, 4)))
+        _c4_node(templates[g]["node"], attrs)
+        free_cpu, free_mem = acpu - ds * 100, amem - ds * 128 * MI
+        ok_ctrl = np.array([_c4_static_ok(*ctrl_spec[c], terms, reqs, *attrs) for c in range(n_ctrl)])
+        ok = ok_ctrl[ctrl_of_pod] & (cpu <= free_cpu) & (mem <= free_mem)
+        sel = np.nonzero(ok)[0].astype(np.int32)
+        parts.append(sel)
+        offs.append(offs[-1] + len(sel))
+    existing = abi.empty_nodes(n_existing)
+    existing["alloc_milli_cpu"] = 16000
+    existing["alloc_memory"] = 64 * GI
+    existing["alloc_pods"] = 110
+    existing["name_id"] = np.arange(n_existing)
+    for i in range(n_existing):
+        _c4_node(existing[i], uni.node_attrs(rng, int(rng.integers(0, 3))))
+    pod_idx = np.concatenate(parts).astype(np.int32) if parts else np.zeros(0, np.int32)
+    return EstimateWorkload("C4", abi.PodTable(pods, term_arr, req_arr), np.array(offs, np.int32), pod_idx,
+                            templates, n_existing, max_nodes, existing,
+                            {"seed": seed, "terms": len(term_arr), "reqs": len(req_arr)})
+
+
+def c4_sweep(n_nodes: int = 5000, pods_per_node: int = 30, seed: int = 4321) -> SweepWorkload:
+    """C3 with the C4 attributes: nodes carry 0-2 taint classes and labels, running pods
+    tolerate their node's taints (plus random others) and carry selectors / required terms
+    their node satisfies, so moving them is restricted by the static filters."""
+    w = c3(n_nodes=n_nodes, pods_per_node=pods_per_node, seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    uni = _C4Universe(rng)
+    attrs = [uni.node_attrs(rng, int(rng.integers(0, 3))) for _ in range(n_nodes)]
+    for i in range(n_nodes):
+        _c4_node(w.nodes[i], attrs[i])
+    terms: list = []
+    reqs: list = []
+    pods = w.table.pods
+    # one spec per (node, replica set) group of pods: controllers are per node here
+    for i in range(n_nodes):
+        for j in range(0, pods_per_node, 10):
+            spec = _c4_pod_spec(rng, uni, terms, reqs, anchor=attrs[i])
+            sl = slice(i * pods_per_node + j, i * pods_per_node + min(pods_per_node, j + 10))
+            _c4_encode_spec(pods[sl], *spec)
+    term_arr = np.array(terms, dtype=abi.TERM_DTYPE) if terms else np.zeros(0, abi.TERM_DTYPE)
+    req_arr = np.array(reqs, dtype=abi.REQ_DTYPE) if reqs else np.zeros(0, abi.REQ_DTYPE)
+    return SweepWorkload("C4-sweep", w.nodes, abi.PodTable(pods, term_arr, req_arr), w.pod_node, w.candidates,
+                         w.dest_mask, w.cand_status, w.move_off, w.move_pods,
+                         dict(w.meta, seed=seed, terms=len(term_arr)))

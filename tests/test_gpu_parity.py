@@ -287,6 +287,50 @@ def test_estimate_plan_publish_random(seed, oracle):
     assert ro.last_index == g.last_index
 
 
+@pytest.mark.parametrize("size", ["small", "full"])
+def test_estimate_c4_taints_affinity(size, oracle):
+    """C4 (taint/toleration + node-affinity heavy): static filters on the templates, per
+    group pod lists, bit-exact vs the oracle; the plan path publishes zero-copy."""
+    w = W.c4() if size == "full" else W.c4(n_pods=6000, n_groups=16, n_existing=60)
+    outs = []
+    for b in (oracle.OracleState(), _mirror()):
+        W.load_estimate(b, w)
+        outs.append(b.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, 7))
+    o, g = outs
+    assert np.array_equal(o.results, g.results)
+    assert np.array_equal(o.sched_pod, g.sched_pod)
+    assert np.array_equal(o.sched_node, g.sched_node)
+    assert o.last_index == g.last_index
+    m = _mirror()
+    W.load_estimate(m, w)
+    with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as plan:
+        p = plan.run(w.max_nodes, 7, want_nodes=False)
+    assert np.array_equal(o.results, p.results) and np.array_equal(o.sched_pod, p.sched_pod)
+
+
+@pytest.mark.parametrize("n_nodes", [800, 5000])
+def test_sweep_c4_taints_affinity(n_nodes, oracle):
+    """The sweep over a C4-attributed cluster (taints, labels, selectors, required terms):
+    two loops (fresh, then hinted), plan with resident hints vs the oracle."""
+    w = W.c4_sweep(n_nodes=n_nodes)
+    o = oracle.OracleState()
+    W.load_sweep(o, w)
+    args = (w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods)
+    o1 = o.find_nodes_to_remove(*args, np.full(len(w.table), -1, np.int32), 0)
+    o2 = o.find_nodes_to_remove(*args, o1.hints, o1.last_index)
+    m = _mirror()
+    W.load_sweep(m, w)
+    g1 = m.find_nodes_to_remove(*args, np.full(len(w.table), -1, np.int32), 0)
+    assert np.array_equal(o1.results, g1.results) and np.array_equal(o1.dest, g1.dest)
+    assert np.array_equal(o1.hints, g1.hints) and o1.last_index == g1.last_index
+    m.set_hints(o1.hints)
+    with native.RemovalPlan(m, *args) as plan:
+        g2 = plan.run(o1.last_index, want_dest=True)
+    assert np.array_equal(o2.results, g2.results) and np.array_equal(o2.dest, g2.dest)
+    assert o2.last_index == g2.last_index
+    assert np.array_equal(m.get_hints(len(w.table)), o2.hints)
+
+
 def test_estimate_full_c2_properties():
     """Full-size C2 (50k pods x 100 groups): every new node's placements fit the template
     (capacity conservation), scheduled pods are distinct members of their group, counts agree."""

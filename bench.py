@@ -65,6 +65,7 @@ def parse():
                          "Go return value (int, []*Pod), estimator.go:40-42)")
     ap.add_argument("--cpu-groups", type=int, default=100, help="groups in the bounded CPU-baseline sample")
     ap.add_argument("--no-sweep", action="store_true", help="skip the C3 scale-down sweep leg (N=1 only)")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 taint/affinity Estimate leg (N=1 only)")
     ap.add_argument("--sweep-nodes", type=int, default=5000)
     return ap.parse_args()
 
@@ -78,6 +79,45 @@ def cpu_model() -> str:
     except OSError:
         pass
     return platform.processor() or "unknown"
+
+
+def c4_leg(args, device: int, with_cpu: bool) -> dict:
+    """C4 (BASELINE configs[3]): the Estimate batch with taints (20 classes),
+    64 label pairs over 12 keys, nodeSelectors and required node-affinity terms; group pod
+    lists are the pods passing CheckPredicates on the template."""
+    from autoscaler_amd import native
+    from autoscaler_amd import workloads as W
+    w = W.c4(n_pods=args.pods, n_groups=args.groups, n_existing=args.existing, max_nodes=args.max_nodes)
+    m = native.Mirror(device)
+    W.load_estimate(m, w)
+    out = {"workload": f"C4: {args.pods} pods x {args.groups} groups, taints/labels/affinity, "
+                       f"{int(w.group_off[-1])} (pod, group) items"}
+    with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as plan:
+        for _ in range(2):
+            plan.run(w.max_nodes, 0, want_nodes=False, copy=False)
+        ts = []
+        for _ in range(max(args.steps, 5)):
+            t = time.perf_counter()
+            r = plan.run(w.max_nodes, 0, want_nodes=False, copy=False)
+            ts.append(time.perf_counter() - t)
+        ms = float(np.median(ts) * 1e3)
+        evals = int(r.results["evals"].sum())
+        out.update({"estimate_ms": ms, "evals": evals, "evals_per_s": evals / (ms / 1e3)})
+        res, sp = r.results.copy(), r.sched_pod.copy()
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle                                           # CPU baseline leg only
+        o = pyoracle.OracleState()
+        W.load_estimate(o, w)
+        t = time.perf_counter()
+        ro = o.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, 0)
+        cpu_ms = (time.perf_counter() - t) * 1e3
+        out.update({"cpu_ms": cpu_ms, "speedup": cpu_ms / ms,
+                    "parity": bool(np.array_equal(ro.results, res) and np.array_equal(ro.sched_pod, sp)),
+                    "cpu_baseline": {"kind": "port", "cores": 1,
+                                     "sample": f"oracle/casim_oracle.c, the same C4 batch, 1 thread of {cpu_model()}"}})
+    m.close()
+    return out
 
 
 def sweep_leg(args, device: int, with_cpu: bool) -> dict:
@@ -213,6 +253,16 @@ def main():
     per_item = PHASE_BYTES[dom] * (n_merge if dom == "merge_ms" else 1)
     kernel_ms = ph_mean[dom]
     achieved = per_item * items / (kernel_ms / 1e3) / 1e9
+    traffic, traffic_src = None, None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")      # rocprofv3 --pmc passes (scripts/gpu_round.sh pmc)
+    if os.path.exists(tf):
+        with open(tf) as f:
+            tj = json.load(f)
+        for name in PHASE_KERNEL[dom].split("+")[:1]:
+            rec = tj.get("kernels", {}).get(f"casim::{name}")
+            if rec:
+                traffic = rec["traffic_bytes_per_launch"]
+                traffic_src = f"profiles/pmc_traffic.json ({tj.get('source', '')})"
 
     result = None
     if rank == 0:
@@ -255,7 +305,8 @@ def main():
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per launch",
+                "traffic_source": traffic_src,
                 "kernel": PHASE_KERNEL[dom], "kernel_ms": kernel_ms,
                 "bytes_per_unit": per_item, "unit_of_work": "(pod, node group) item",
                 "units_per_launch": items,
@@ -275,6 +326,8 @@ def main():
         }
         if world == 1 and not args.no_sweep:
             result["extra"]["sweep"] = sweep_leg(args, local, not args.no_cpu_baseline)
+        if world == 1 and not args.no_c4:
+            result["extra"]["c4"] = c4_leg(args, local, not args.no_cpu_baseline)
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.barrier()

@@ -34,7 +34,9 @@ def main(root: str) -> None:
         wk = sum(w) / len(w) * 1024 if w else None
         res[name] = {"launches": max(len(f), len(w)), "read_bytes_per_launch": fk, "write_bytes_per_launch": wk,
                      "traffic_bytes_per_launch": (fk or 0) + (wk or 0)}
-    json.dump(res, sys.stdout, indent=1)
+    json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes over "
+                         "bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-sweep --no-c4; "
+                         "FETCH_SIZE x2 (gfx950 wide-read correction)", "kernels": res}, sys.stdout, indent=1)
     print()
 
 

@@ -568,14 +568,37 @@ __device__ inline int32_t rec_copies(const NodeRec& r, int64_t pcpu, int64_t pme
 struct RunDiv {
     int64_t req[3];
     float rcp[3];
+    double reqd[3], rcpd[3];
+    bool f64;          // every free value and request < 2^53: the float64 path is exact
 };
-__device__ inline RunDiv run_div(int64_t pcpu, int64_t pmem, int64_t peph) {
+// `bound` = the largest free value a row of the group can hold (the template copy's:
+// rows only lose resources), so one uniform test decides the path for every row.
+__device__ inline RunDiv run_div(int64_t pcpu, int64_t pmem, int64_t peph, int64_t bound) {
     RunDiv d;
     d.req[0] = pcpu; d.req[1] = pmem; d.req[2] = peph;
     // req == 0: rcp = +inf, so the float quotient is inf (or NaN for free == 0) and
     // fminf(., cap) gives cap — a zero request passes whenever free >= 0
     for (int i = 0; i < 3; i++) d.rcp[i] = d.req[i] > 0 ? 1.0f / (float)d.req[i] : __builtin_inff();
+    constexpr int64_t E53 = 1ll << 53;
+    d.f64 = bound < E53 && pcpu < E53 && pmem < E53 && peph < E53;
+    for (int i = 0; i < 3; i++) {
+        d.reqd[i] = (double)d.req[i];
+        d.rcpd[i] = d.req[i] > 0 ? 1.0 / d.reqd[i] : __builtin_inf();
+    }
     return d;
+}
+// floor(free/req) capped at cap with full-rate float64 ops only: below 2^53 the
+// conversions are exact, the quotient is within one of the exact floor, and
+// fma(-q, req, free) = free - q*req is an integer below 2^53 in magnitude, so it is
+// computed exactly and one step each way makes q exact (no 64-bit integer multiply).
+__device__ inline int32_t dim_copies_f64(int64_t free_, double rd, double rcpd, int32_t cap) {
+    const double fd = (double)(free_ < 0 ? 0 : free_);
+    const double cp = (double)cap;
+    double q = fmin(floor(fd * rcpd), cp);              // NaN (0 * inf) -> cap
+    const double t = fma(-q, rd, fd);
+    q += ((t >= rd) & (q < cp)) ? 1.0 : 0.0;
+    q -= (t < 0.0) ? 1.0 : 0.0;
+    return free_ < 0 ? 0 : (int32_t)q;
 }
 // branch-free (no exec-mask juggling in the row loop)
 __device__ inline int32_t dim_copies_fast(int64_t free_, int64_t req, float rcp, int32_t cap) {
@@ -589,7 +612,11 @@ __device__ inline int32_t dim_copies_fast(int64_t free_, int64_t req, float rcp,
 }
 __device__ inline int32_t rec_copies_run(const NodeRec& r, const RunDiv& d, bool zero, int32_t cap) {
     int32_t c = max(0, min(r.pods, cap));
-    if (!zero) {     // uniform
+    if (!zero && d.f64) {     // uniform
+        c = min(c, dim_copies_f64(r.cpu, d.reqd[0], d.rcpd[0], max(c, 1)));
+        c = min(c, dim_copies_f64(r.mem, d.reqd[1], d.rcpd[1], max(c, 1)));
+        c = min(c, dim_copies_f64(r.eph, d.reqd[2], d.rcpd[2], max(c, 1)));
+    } else if (!zero) {
         c = min(c, dim_copies_fast(r.cpu, d.req[0], d.rcp[0], max(c, 1)));
         c = min(c, dim_copies_fast(r.mem, d.req[1], d.rcp[1], max(c, 1)));
         c = min(c, dim_copies_fast(r.eph, d.req[2], d.rcp[2], max(c, 1)));
@@ -612,6 +639,34 @@ __device__ inline int32_t run_end(const uint64_t* __restrict__ hm, int32_t pos, 
         if (b) {
             const int l = __builtin_ctzll(b);
             return min(P, ((c + l) << 6) + __builtin_ctzll((uint64_t)rl64((int64_t)v, l)));
+        }
+    }
+    return P;
+}
+// run_end with the head words [pf_c, pf_c + 64) already in registers (lane l holds word
+// pf_c + l, 0 past the end; loaded when the previous run started), so finding a run's
+// end costs no global round trip unless the run is longer than the 4096 positions held.
+__device__ inline int32_t run_end_pf(const uint64_t* __restrict__ hm, int32_t pos, int32_t P, int lane,
+                                     int32_t pf_c, uint64_t pf_w) {
+    const int32_t c = pos >> 6;
+    if (c != pf_c) return run_end(hm, pos, P, lane);
+    const int sh = (pos & 63) + 1;
+    uint64_t m = (uint64_t)rl64((int64_t)pf_w, 0);
+    m = sh >= 64 ? 0ull : (m >> sh) << sh;
+    if (m) return min(P, (c << 6) + __builtin_ctzll(m));
+    const uint64_t b = __ballot((lane > 0) & (pf_w != 0ull));
+    if (b) {
+        const int l = __builtin_ctzll(b);
+        return min(P, ((c + l) << 6) + __builtin_ctzll((uint64_t)rl64((int64_t)pf_w, l)));
+    }
+    const int32_t nc = (P + 63) >> 6;
+    for (int32_t c2 = c + 64; c2 < nc; c2 += 64) {
+        const int32_t cc = c2 + lane;
+        const uint64_t v = cc < nc ? hm[cc] : 0ull;
+        const uint64_t b2 = __ballot(v != 0);
+        if (b2) {
+            const int l = __builtin_ctzll(b2);
+            return min(P, ((c2 + l) << 6) + __builtin_ctzll((uint64_t)rl64((int64_t)v, l)));
         }
     }
     return P;
@@ -789,6 +844,13 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
     int32_t out_node = -1, out_idx = 0;
     bool pend = false;
     bool stop = false;
+    // Prefetch for the next run head, issued when a run starts: the stream window at the
+    // run's end (pf_base, -1 none) and the head words from there (pf_hc, lane l holds word
+    // pf_hc + l), so the global latency overlaps the run's LDS work instead of following it.
+    int32_t pf_base = -1, pf_hc = -1;
+    StreamPod pf_cur = {}, pf_nxt = {};
+    uint64_t pf_hw = 0;
+    const int32_t nhc = (P + 63) >> 6;
 
     // add a template copy as new node k (addNewNodeToSnapshot, :146-159)
     auto open_node = [&]() -> int32_t {
@@ -819,13 +881,20 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
             if (pos < wbase + 128) {
                 cur = nxt;
                 wbase += 64;
+                nxt = StreamPod{};
+                if (wbase + 64 + lane < P) nxt = gs[wbase + 64 + lane];
+            } else if ((pos & ~63) == pf_base) {
+                wbase = pf_base;            // prefetched when the run that ends here started
+                cur = pf_cur;
+                nxt = pf_nxt;
             } else {
                 wbase = pos & ~63;
                 cur = StreamPod{};
                 if (wbase + lane < P) cur = gs[wbase + lane];
+                nxt = StreamPod{};
+                if (wbase + 64 + lane < P) nxt = gs[wbase + 64 + lane];
             }
-            nxt = StreamPod{};
-            if (wbase + 64 + lane < P) nxt = gs[wbase + 64 + lane];
+            pf_base = -1;
         }
         const int sl = pos - wbase;
         const int64_t pcpu = rl64(cur.cpu, sl), pmem = rl64(cur.mem, sl), peph = rl64(cur.eph, sl);
@@ -836,7 +905,19 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
         // ---------------- a run of identical resource-only pods ----------------
         if (batch_runs && (sf & (SF_BATCH | SF_HEAD)) == (SF_BATCH | SF_HEAD)) {
             PROF_T(t_re);
-            const int32_t e = run_end(hm, pos, P, lane);
+            const int32_t e = run_end_pf(hm, pos, P, lane, pf_hc, pf_hw);
+            if (e < P) {
+                const int32_t pb = e & ~63;
+                if (pb >= wbase + 128) {
+                    pf_base = pb;
+                    pf_cur = StreamPod{};
+                    if (pb + lane < P) pf_cur = gs[pb + lane];
+                    pf_nxt = StreamPod{};
+                    if (pb + 64 + lane < P) pf_nxt = gs[pb + 64 + lane];
+                }
+                pf_hc = e >> 6;
+                pf_hw = pf_hc + lane < nhc ? hm[pf_hc + lane] : 0ull;
+            }
             PROF_ADD(0, t_re);
             if (e - pos >= 2) {
                 PROF_INC(7);
@@ -861,7 +942,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                             PROF_T(t_ca);
                             int32_t na = 0, a1 = -1;
                             if (rem <= (1 << 20)) {
-                                const RunDiv dv = run_div(pcpu, pmem, peph);
+                                const RunDiv dv = run_div(pcpu, pmem, peph, max(trec.cpu, max(trec.mem, trec.eph)));
                                 int32_t j = lane;
                                 for (; j + 64 < k; j += 128) {          // two rows in flight
                                     const NodeRec r0 = R[j], r1 = R[j + 64];

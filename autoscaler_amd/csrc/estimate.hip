@@ -492,7 +492,8 @@ __global__ void __launch_bounds__(256) k_emit_bucket(const GroupMeta* __restrict
 
 // 4. the First-Fit-Decreasing chain -------------------------------------------
 #ifdef CASIM_PROF   // section cycle counters of k_ffd_chain (profiling build only)
-__device__ unsigned long long g_chain_prof[1024][8];
+constexpr int NPROF = 12;
+__device__ unsigned long long g_chain_prof[1024][NPROF];
 #define PROF_T(v) const uint64_t v = clock64()
 #define PROF_ADD(i, t) prof[i] += clock64() - (t)
 #define PROF_INC(i) prof[i]++
@@ -518,6 +519,130 @@ __device__ inline int32_t wave_min32(int32_t v) { return __ockl_wfred_min_i32(v)
 __device__ inline int64_t wave_sum64(int64_t v) { return __ockl_wfred_add_i64(v); }
 __device__ inline int32_t mbcnt(uint64_t m) {
     return (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// The chain workgroup: CW wavefronts, one per SIMD of the CU.  Every wave runs the same
+// sequential control flow on the same (uniform) state; the per-row loops over the
+// group's new nodes are split across the waves (row j -> thread j mod CT), so the
+// row work of a run — copy counts, revolution lists, row updates, opened rows — runs
+// on all four SIMDs.  Cross-wave reductions go through LDS, double-buffered by a parity
+// bit so that one barrier per reduction suffices (a wave cannot reach the next use of
+// a buffer before every wave has read it: that needs the barrier in between).
+// Barrier that orders LDS only.  __syncthreads() is also a workgroup fence for global
+// memory, i.e. an s_waitcnt vmcnt(0) before s_barrier: every barrier would wait for the
+// chain's result stores and the stream prefetch.  The waves of a chain workgroup share
+// state through LDS only (their global stores are write-only results, released once at
+// the end with __threadfence), so an LDS-scoped fence is all the barriers need.
+__device__ inline void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+constexpr int CW = 4;
+constexpr int CT = 64 * CW;
+constexpr int RED_N = 5;
+struct ChainRed {
+    int64_t v[2][CW][RED_N];
+    int32_t cnt[2][CW];
+    int32_t pick;          // a value one wave found, for every wave (barrier-ordered)
+};
+enum { R_SUM = 0, R_MAX = 1, R_MIN = 2 };
+extern "C" __device__ long long __ockl_wfred_min_i64(long long);
+template <int OP> __device__ inline int64_t wred(int64_t v) {
+    return OP == R_SUM ? __ockl_wfred_add_i64(v) : OP == R_MAX ? __ockl_wfred_max_i64(v) : __ockl_wfred_min_i64(v);
+}
+template <int OP> __device__ inline int64_t wcomb(int64_t a, int64_t b) {
+    return OP == R_SUM ? a + b : OP == R_MAX ? (a > b ? a : b) : (a < b ? a : b);
+}
+template <int OA, int OB, int OC>
+__device__ inline void blk_red3(ChainRed& cr, int& par, int wv, int lane, int64_t& a, int64_t& b, int64_t& c) {
+    a = wred<OA>(a); b = wred<OB>(b); c = wred<OC>(c);
+    if (lane == 0) { cr.v[par][wv][0] = a; cr.v[par][wv][1] = b; cr.v[par][wv][2] = c; }
+    lds_barrier();
+    a = cr.v[par][0][0]; b = cr.v[par][0][1]; c = cr.v[par][0][2];
+    for (int w = 1; w < CW; w++) {
+        a = wcomb<OA>(a, cr.v[par][w][0]); b = wcomb<OB>(b, cr.v[par][w][1]); c = wcomb<OC>(c, cr.v[par][w][2]);
+    }
+    par ^= 1;
+}
+// Five reductions with one barrier; the waves' partial values stay readable in
+// cr.v[par ^ 1] (the buffer just used) until the reduction after next.
+__device__ inline int64_t wred_rt(int op, int64_t v) {
+    return op == R_SUM ? wred<R_SUM>(v) : op == R_MAX ? wred<R_MAX>(v) : wred<R_MIN>(v);
+}
+__device__ inline int64_t wcomb_rt(int op, int64_t a, int64_t b) {
+    return op == R_SUM ? a + b : op == R_MAX ? (a > b ? a : b) : (a < b ? a : b);
+}
+__device__ inline void blk_red5(ChainRed& cr, int& par, int wv, int lane, int64_t (&x)[RED_N], const int (&op)[RED_N]) {
+    for (int i = 0; i < RED_N; i++) x[i] = wred_rt(op[i], x[i]);
+    if (lane == 0)
+        for (int i = 0; i < RED_N; i++) cr.v[par][wv][i] = x[i];
+    lds_barrier();
+    for (int i = 0; i < RED_N; i++) {
+        int64_t a = cr.v[par][0][i];
+        for (int w = 1; w < CW; w++) a = wcomb_rt(op[i], a, cr.v[par][w][i]);
+        x[i] = a;
+    }
+    par ^= 1;
+}
+// Cross-wave step only: x[] already reduced within each wave (wave-uniform).
+__device__ inline void blk_xchg5(ChainRed& cr, int& par, int wv, int lane, int64_t (&x)[RED_N], const int (&op)[RED_N]) {
+    if (lane == 0)
+        for (int i = 0; i < RED_N; i++) cr.v[par][wv][i] = x[i];
+    lds_barrier();
+    for (int i = 0; i < RED_N; i++) {
+        int64_t a = cr.v[par][0][i];
+        for (int w = 1; w < CW; w++) a = wcomb_rt(op[i], a, cr.v[par][w][i]);
+        x[i] = a;
+    }
+    par ^= 1;
+}
+__device__ inline int32_t hibit(uint64_t m) { return 63 - __builtin_clzll(m); }
+// lanes below `n` (n in [0, 64])
+__device__ inline uint64_t lanes_below(int32_t n) { return n >= 64 ? ~0ull : n <= 0 ? 0ull : ((1ull << n) - 1); }
+
+// Rows of the group split in contiguous 64-row-aligned ranges, one per wave, so that
+// per-wave counts in wave order are counts in row order.
+__device__ inline void wave_rows(int32_t k, int wv, int32_t& lo, int32_t& hi) {
+    const int32_t cpw = (((k + 63) >> 6) + CW - 1) / CW;      // 64-row chunks per wave
+    lo = min(k, wv * cpw * 64);
+    hi = min(k, lo + cpw * 64);
+}
+// Evals of opening n_open template copies for the rest of a run (closed form of the
+// per-node sum: node i's opening pod fails FitsAnyNode over the k0+i rows before it
+// (i > 0), passes CheckPredicates, and its next pi-2 pods scan k0+i+1 rows each, the
+// first of them from j00 on node 0).
+__device__ inline uint64_t open_evals(int32_t n_open, int32_t ct, int32_t placed2, int32_t k0, int32_t j00,
+                                      uint64_t kev, bool cp_eval) {
+    const uint64_t no = (uint64_t)n_open;
+    uint64_t ev = kev * ((no - 1) * (uint64_t)k0 + (no - 1) * no / 2);
+    if (cp_eval) ev += no;
+    const uint64_t m = no - 1;                   // full nodes, ct pods each
+    if (m > 0 && ct >= 2) ev += (uint64_t)(ct - 1) * (m * (uint64_t)(k0 + 1) + m * (m - 1) / 2) - (uint64_t)j00;
+    const int32_t i = n_open - 1;                // the last node
+    const int32_t pi = placed2 - i * ct;
+    if (pi >= 2) {
+        const int32_t j0i = i == 0 ? j00 : 0;
+        ev += (uint64_t)(k0 + i - j0i + 1) + (uint64_t)(pi - 2) * (uint64_t)(k0 + i + 1);
+    }
+    return ev;
+}
+
+// Ordered compaction step over the workgroup: thread t contributes `keep` for index
+// base + t; returns the thread's slot (exclusive prefix over the workgroup) and the total.
+__device__ inline int32_t blk_compact(ChainRed& cr, int& par, int wv, bool keep, int32_t& total) {
+    const uint64_t bm = __ballot(keep);
+    if ((threadIdx.x & 63) == 0) cr.cnt[par][wv] = __builtin_popcountll(bm);
+    lds_barrier();
+    int32_t before = 0;
+    total = 0;
+    for (int w = 0; w < CW; w++) {
+        const int32_t c = cr.cnt[par][w];
+        before += w < wv ? c : 0;
+        total += c;
+    }
+    par ^= 1;
+    return before + mbcnt(bm);
 }
 
 // New-node row in LDS: free resources of one template copy (32 B, two ds_read_b128).
@@ -613,9 +738,13 @@ __device__ inline int32_t dim_copies_fast(int64_t free_, int64_t req, float rcp,
 __device__ inline int32_t rec_copies_run(const NodeRec& r, const RunDiv& d, bool zero, int32_t cap) {
     int32_t c = max(0, min(r.pods, cap));
     if (!zero && d.f64) {     // uniform
-        c = min(c, dim_copies_f64(r.cpu, d.reqd[0], d.rcpd[0], max(c, 1)));
-        c = min(c, dim_copies_f64(r.mem, d.reqd[1], d.rcpd[1], max(c, 1)));
-        c = min(c, dim_copies_f64(r.eph, d.reqd[2], d.rcpd[2], max(c, 1)));
+        // independent per-dimension quotients (capped at the same c, min taken after);
+        // a zero request only needs free >= 0 (uniform skip of the division)
+        const int32_t cp = max(c, 1);
+        const int32_t q0 = d.req[0] ? dim_copies_f64(r.cpu, d.reqd[0], d.rcpd[0], cp) : (r.cpu < 0 ? 0 : cp);
+        const int32_t q1 = d.req[1] ? dim_copies_f64(r.mem, d.reqd[1], d.rcpd[1], cp) : (r.mem < 0 ? 0 : cp);
+        const int32_t q2 = d.req[2] ? dim_copies_f64(r.eph, d.reqd[2], d.rcpd[2], cp) : (r.eph < 0 ? 0 : cp);
+        c = min(c, min(q0, min(q1, q2)));
     } else if (!zero) {
         c = min(c, dim_copies_fast(r.cpu, d.req[0], d.rcp[0], max(c, 1)));
         c = min(c, dim_copies_fast(r.mem, d.req[1], d.rcp[1], max(c, 1)));
@@ -714,7 +843,7 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
             }
             s_tk = tk;
         }
-        __syncthreads();
+        lds_barrier();
         const int32_t t = s_t, tk = s_tk;
         if (t >= total || tk < 0) return;
         __threadfence();                                   // acquire for every thread of the block
@@ -734,7 +863,7 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
             }
             s_seg0 = lo;
         }
-        __syncthreads();
+        lds_barrier();
         int32_t at = a, q = s_seg0;
         const int32_t end = min(b, ns);
         while (at < end) {
@@ -756,7 +885,7 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
             at = lim;
         }
         for (int32_t i = max(a, ns) + (int32_t)threadIdx.x; i < b; i += blockDim.x) pub[gm.off + i] = -1;
-        __syncthreads();
+        lds_barrier();
     }
 }
 
@@ -773,7 +902,7 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
 // placement's scan ends at unwrapped position (rev-1)*k + rank, so a batch costs
 // (r_last-1)*k + rank(last)+1 filter calls.  assign[pos] receives the new-node index of
 // every placed stream position (-1 = not scheduled).
-__global__ void __launch_bounds__(64) k_ffd_chain(
+__global__ void __launch_bounds__(CT) k_ffd_chain(
     const GroupMeta* __restrict__ groups, const StreamPod* __restrict__ stream, const uint64_t* __restrict__ heads,
     const ca_template* __restrict__ tmpls, const ca_pod_spec* __restrict__ specs, const PodHot* __restrict__ ph,
     const int32_t* __restrict__ lin_arr, const uint8_t* __restrict__ need, const uint32_t* __restrict__ group_unsup,
@@ -790,9 +919,14 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
 #endif
     uint32_t n_single = 0;
 #ifdef CASIM_PROF
-    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t prof[NPROF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wv = tid >> 6;          // wave of the workgroup
+    const bool w0 = wv == 0;          // the wave that stores single-pod results
+    __shared__ ChainRed cred;
+    int par = 0;
     const GroupMeta gm = groups[g];
     const int32_t lin = lin_arr[g];
     ChainOut res;
@@ -801,8 +935,8 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
     res.nseg = 0; res.pad2[0] = res.pad2[1] = res.pad2[2] = 0;
     if (group_unsup[g]) {
         res.status = CA_EUNSUPPORTED;
-        if (lane == 0) outs[g] = res;
-        if (tickets) push_tickets(g, gm.count, nsub, tickets, qctl, lane);
+        if (tid == 0) outs[g] = res;
+        if (tickets && w0) push_tickets(g, gm.count, nsub, tickets, qctl, lane);
         return;
     }
     const int nb_cap = (kcap + 63) >> 6;
@@ -853,15 +987,16 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
     const int32_t nhc = (P + 63) >> 6;
 
     // add a template copy as new node k (addNewNodeToSnapshot, :146-159)
+    // (LDS writes by one thread; a barrier follows before any wave reads the row)
     auto open_node = [&]() -> int32_t {
         const int32_t nn = k;
-        if (lane == 0) {
+        if (tid == 0) {
             R[nn] = trec;
             SUM[nn >> 6] = trec;   // a fresh copy is the largest a row can be
         }
-        if (use_ports && lane < CA_PORT_WORDS) PORTS[(size_t)nn * CA_PORT_WORDS + lane] = tp.used_ports[lane];
-        if (use_scalar && lane < CA_MAX_SCALAR)
-            SC[(size_t)lane * kcap + nn] = wsub(tp.node.alloc_scalar[lane], tp.used_scalar[lane]);
+        if (use_ports && tid < CA_PORT_WORDS) PORTS[(size_t)nn * CA_PORT_WORDS + tid] = tp.used_ports[tid];
+        if (use_scalar && tid < CA_MAX_SCALAR)
+            SC[(size_t)tid * kcap + nn] = wsub(tp.node.alloc_scalar[tid], tp.used_scalar[tid]);
         k++;
         last_node = nn;
         return nn;
@@ -905,6 +1040,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
         // ---------------- a run of identical resource-only pods ----------------
         if (batch_runs && (sf & (SF_BATCH | SF_HEAD)) == (SF_BATCH | SF_HEAD)) {
             PROF_T(t_re);
+            PROF_T(t_run);
             const int32_t e = run_end_pf(hm, pos, P, lane, pf_hc, pf_hw);
             if (e < P) {
                 const int32_t pb = e & ~63;
@@ -921,10 +1057,15 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
             PROF_ADD(0, t_re);
             if (e - pos >= 2) {
                 PROF_INC(7);
+                PROF_T(t_pro);
                 const int32_t RN = e - pos;
                 const uint64_t kev = (sf & SF_EVAL) ? 1u : 0u;
+                // the pod's reciprocals, once per run (copy counts of every row, the last
+                // row and the template: fast path while the cap is <= 2^20)
+                const RunDiv dv = run_div(pcpu, pmem, peph, max(trec.cpu, max(trec.mem, trec.eph)));
                 int32_t done = 0;
                 bool exhausted = false;          // every row but last_node has no room left
+                PROF_ADD(8, t_pro);
                 while (done < RN) {
                     const int32_t rem = RN - done;
                     const int32_t len = n_base + k;
@@ -935,43 +1076,65 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                         const int32_t j0 = s0 > n_base ? s0 - n_base : 0;   // first new node visited
                         int32_t one = -1, n_one = 0, nalive = 0;
                         int64_t S = 0;
+                        int64_t lv_cmin = 0;      // revolution 1: fewest copies among rows with room
+                        int32_t lv_s = 0;         // ... and how many of them lie before j0
                         if (exhausted) {
-                            const int32_t c = rec_copies(R[last_node], pcpu, pmem, peph, zero, rem);
+                            PROF_T(t_ex);
+                            const NodeRec rl_ = R[last_node];
+                            const int32_t c = rem <= (1 << 20) ? rec_copies_run(rl_, dv, zero, rem)
+                                                               : rec_copies(rl_, pcpu, pmem, peph, zero, rem);
+                            lds_barrier();    // every wave has read the row before it changes
                             if (c > 0) { one = last_node; n_one = c; nalive = 1; }
+                            PROF_ADD(10, t_ex);
                         } else {
                             PROF_T(t_ca);
-                            int32_t na = 0, a1 = -1;
-                            if (rem <= (1 << 20)) {
-                                const RunDiv dv = run_div(pcpu, pmem, peph, max(trec.cpu, max(trec.mem, trec.eph)));
-                                int32_t j = lane;
-                                for (; j + 64 < k; j += 128) {          // two rows in flight
-                                    const NodeRec r0 = R[j], r1 = R[j + 64];
+                            // copies per row, and for revolution 1 (rows with room): count,
+                            // last such row, fewest copies, count below j0 (rotation split)
+                            int32_t lo, hi;
+                            wave_rows(k, wv, lo, hi);
+                            // counts, last row with room and the rotation split come from
+                            // ballots (scalar); only the copy sum and minimum need reductions
+                            int64_t s64 = 0;                          // copies (rem > 2^20 path)
+                            int32_t s32 = 0, cm = INT32_MAX;          // copies (<= 2^24 per lane), fewest
+                            int32_t na_w = 0, lt_w = 0, a1_w = -1;    // wave-uniform
+                            auto acc = [&](int32_t b, int32_t c, bool in) -> int32_t {   // row b + lane
+                                if (in) CAPA[b + lane] = c;
+                                const bool room = in && c > 0;
+                                cm = room ? min(cm, c) : cm;
+                                const uint64_t m = __ballot(room);
+                                na_w += __builtin_popcountll(m);
+                                lt_w += __builtin_popcountll(m & lanes_below(j0 - b));
+                                if (m) a1_w = b + hibit(m);
+                                return in ? c : 0;
+                            };
+                            const bool fast = rem <= (1 << 20);
+                            if (fast) {
+                                for (int32_t b = lo; b < hi; b += 128) {       // two rows in flight
+                                    const int32_t j = b + lane;
+                                    const bool in0 = j < hi, in1 = j + 64 < hi;
+                                    const NodeRec r0 = R[in0 ? j : 0], r1 = R[in1 ? j + 64 : 0];
                                     const int32_t c0 = rec_copies_run(r0, dv, zero, rem);
                                     const int32_t c1 = rec_copies_run(r1, dv, zero, rem);
-                                    CAPA[j] = c0;
-                                    CAPA[j + 64] = c1;
-                                    S += c0 + c1;
-                                    if (c0 > 0) { na++; a1 = j; }
-                                    if (c1 > 0) { na++; a1 = j + 64; }
-                                }
-                                if (j < k) {
-                                    const int32_t c = rec_copies_run(R[j], dv, zero, rem);
-                                    CAPA[j] = c;
-                                    S += c;
-                                    if (c > 0) { na++; a1 = j; }
+                                    s32 += acc(b, c0, in0);
+                                    s32 += acc(b + 64, c1, in1);
                                 }
                             } else {
-                                for (int32_t j = lane; j < k; j += 64) {
-                                    const int32_t c = rec_copies(R[j], pcpu, pmem, peph, zero, rem);
-                                    CAPA[j] = c;
-                                    S += c;
-                                    if (c > 0) { na++; a1 = j; }
+                                for (int32_t b = lo; b < hi; b += 64) {
+                                    const int32_t j = b + lane;
+                                    const bool in = j < hi;
+                                    s64 += acc(b, rec_copies(R[in ? j : 0], pcpu, pmem, peph, zero, rem), in);
                                 }
                             }
-                            S = wave_sum64(S);
-                            nalive = (int32_t)wave_sum64(na);
-                            a1 = wave_max32(a1);
-                            if (nalive == 1) { one = a1; n_one = (int32_t)min(S, (int64_t)rem); }
+                            int64_t x[RED_N];          // S, rows with room, last such row, fewest copies, rows < j0
+                            x[0] = fast ? (int64_t)__ockl_wfred_add_i32(s32) : wave_sum64(s64);
+                            x[1] = na_w; x[2] = a1_w; x[3] = wave_min32(cm); x[4] = lt_w;
+                            constexpr int OPS[RED_N] = {R_SUM, R_SUM, R_MAX, R_MIN, R_SUM};
+                            blk_xchg5(cred, par, wv, lane, x, OPS);     // + CAPA visible
+                            S = x[0];
+                            nalive = (int32_t)x[1];
+                            lv_cmin = x[3];
+                            lv_s = (int32_t)x[4];
+                            if (nalive == 1) { one = (int32_t)x[2]; n_one = (int32_t)min(S, (int64_t)rem); }
                             PROF_ADD(1, t_ca);
                         }
                         if (nalive == 1) {
@@ -979,7 +1142,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                             int32_t rho = one - j0;
                             if (rho < 0) rho += k;
                             evals += (uint64_t)rho + 1 + (uint64_t)(n_one - 1) * (uint64_t)k;
-                            if (lane == 0) {
+                            if (tid == 0) {
                                 NodeRec r = R[one];
                                 r.cpu -= (int64_t)n_one * pcpu;
                                 r.mem -= (int64_t)n_one * pmem;
@@ -988,7 +1151,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                                 r.used = 1;
                                 R[one] = r;
                             }
-                            if (so_node) for (int32_t t = lane; t < n_one; t += 64) so_node[nsched + t] = one;
+                            if (so_node) for (int32_t t = tid; t < n_one; t += CT) so_node[nsched + t] = one;
                             L = n_base + one + 1;
                             if (L >= len) L -= len;
                             note_success();
@@ -996,35 +1159,104 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                         } else if (nalive > 1) {
                             const int32_t n = (int32_t)min(S, (int64_t)rem);
                             PROF_T(t_rv);
-                            __builtin_amdgcn_wave_barrier();
+                            int32_t got = 0, r = 1, last = -1;
+                            int32_t* gdst = so_node ? so_node + nsched : nullptr;
+                            if (!gdst) {
+                            // Without node ordinals no placement list is needed: a level
+                            // (revolutions r..cmin, rows with >= r copies) is a count, and
+                            // only the last placement's row matters — the m-th row of its
+                            // revolution in rotated order, i.e. the t-th qualifying row in
+                            // row order, found from the waves' counts and one wave's ballots.
+                            int32_t lv_na = nalive;
+                            int lv_buf = par ^ 1;     // per-wave partial counts of this level (x[1])
+                            for (;;) {
+                                const int64_t avail = (lv_cmin - r + 1) * (int64_t)lv_na;
+                                if ((int64_t)got + avail >= n) {
+                                    const int32_t m0 = n - got;
+                                    r += (m0 - 1) / lv_na;
+                                    const int32_t m = (m0 - 1) % lv_na + 1;        // rank in rotated order
+                                    const int32_t hiN = lv_na - lv_s;              // qualifying rows >= j0
+                                    int32_t t = m <= hiN ? lv_s + m : m - hiN;     // rank in row order (1-based)
+                                    int w = 0;
+                                    for (; w < CW - 1; w++) {
+                                        const int32_t cw_ = (int32_t)cred.v[lv_buf][w][1];
+                                        if (t <= cw_) break;
+                                        t -= cw_;
+                                    }
+                                    if (wv == w) {
+                                        int32_t lo, hi;
+                                        wave_rows(k, wv, lo, hi);
+                                        for (int32_t b = lo; b < hi; b += 64) {
+                                            const int32_t j = b + lane;
+                                            const uint64_t bm = __ballot(j < hi && CAPA[j] >= r);
+                                            const int32_t pc = __builtin_popcountll(bm);
+                                            if (t <= pc) {
+                                                const bool hit = ((bm >> lane) & 1ull) && mbcnt(bm) == t - 1;
+                                                const uint64_t hm2 = __ballot(hit);
+                                                if (lane == 0) cred.pick = b + __builtin_ctzll(hm2);
+                                                break;
+                                            }
+                                            t -= pc;
+                                        }
+                                    }
+                                    lds_barrier();
+                                    last = cred.pick;
+                                    got = n;
+                                    PROF_INC(6);
+                                    break;
+                                }
+                                got += (int32_t)avail;
+                                r = (int32_t)lv_cmin + 1;
+                                // the next level: rows with at least r copies
+                                int32_t lo, hi;
+                                wave_rows(k, wv, lo, hi);
+                                int32_t cnt_w = 0, lt2 = 0, cm2 = INT32_MAX;
+                                for (int32_t b = lo; b < hi; b += 64) {
+                                    const int32_t j = b + lane;
+                                    const int32_t c = j < hi ? CAPA[j] : 0;
+                                    const bool q = c >= r;
+                                    cm2 = q ? min(cm2, c) : cm2;
+                                    const uint64_t m = __ballot(q);
+                                    cnt_w += __builtin_popcountll(m);
+                                    lt2 += __builtin_popcountll(m & lanes_below(j0 - b));
+                                }
+                                int64_t y[RED_N] = {0, cnt_w, 0, wave_min32(cm2), lt2};   // -, count, -, min, count < j0
+                                constexpr int OPS2[RED_N] = {R_SUM, R_SUM, R_SUM, R_MIN, R_SUM};
+                                blk_xchg5(cred, par, wv, lane, y, OPS2);
+                                lv_buf = par ^ 1;
+                                lv_na = (int32_t)y[1];
+                                lv_cmin = y[3];
+                                lv_s = (int32_t)y[4];
+                                PROF_INC(6);
+                            }
+                            } else {
                             // revolution 1: rows with room, in rotated order from j0
-                            int32_t na = 0, cmin = INT32_MAX;
-                            for (int32_t b = 0; b < k; b += 64) {
-                                const int32_t rr = b + lane;
+                            int32_t na = 0;
+                            int64_t cmin = INT32_MAX, z0 = 0, z1 = 0;
+                            for (int32_t b = 0; b < k; b += CT) {
+                                const int32_t rr = b + tid;
                                 int32_t j = j0 + rr;
                                 if (j >= k) j -= k;
                                 const int32_t c = rr < k ? CAPA[j] : 0;
                                 const bool keep = c >= 1;
-                                const uint64_t bm = __ballot(keep);
-                                if (keep) { ALIVE[na + mbcnt(bm)] = j; cmin = min(cmin, c); }
-                                na += __builtin_popcountll(bm);
+                                int32_t tot;
+                                const int32_t slot = blk_compact(cred, par, wv, keep, tot);
+                                if (keep) { ALIVE[na + slot] = j; cmin = min(cmin, (int64_t)c); }
+                                na += tot;
                             }
-                            cmin = wave_min32(cmin);
-                            __builtin_amdgcn_wave_barrier();
+                            blk_red3<R_MIN, R_SUM, R_SUM>(cred, par, wv, lane, cmin, z0, z1);   // + ALIVE visible
                             // Revolutions r..cmin serve the same alive list (no row runs out
                             // before cmin), so the list is compacted once per distinct copy
                             // level, and the placements of those revolutions are the list
                             // repeated: placement t of the level goes to ALIVE[t % na].
-                            int32_t got = 0, r = 1, last = -1;
-                            int32_t* gdst = so_node ? so_node + nsched : nullptr;
                             for (;;) {
                                 const int64_t avail = (int64_t)(cmin - r + 1) * na;
                                 const bool fin = got + avail >= n;
                                 const int32_t cnt = fin ? n - got : (int32_t)avail;
                                 if (gdst) {
-                                    const int32_t st = 64 % na;
-                                    int32_t q = lane % na;
-                                    for (int32_t t = lane; t < cnt; t += 64) {
+                                    const int32_t st = CT % na;
+                                    int32_t q = tid % na;
+                                    for (int32_t t = tid; t < cnt; t += CT) {
                                         gdst[got + t] = ALIVE[q];
                                         q += st;
                                         if (q >= na) q -= na;
@@ -1040,28 +1272,32 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                                 got += cnt;
                                 r = cmin + 1;
                                 // the rows with at least r copies stay
-                                int32_t nn2 = 0, cm2 = INT32_MAX;
-                                for (int32_t b = 0; b < na; b += 64) {
-                                    const int32_t i = b + lane;
+                                // (in place: a chunk's writes land below its end, and the
+                                // barrier in blk_compact orders them after the chunk's reads)
+                                int32_t nn2 = 0;
+                                int64_t cm2 = INT32_MAX;
+                                for (int32_t b = 0; b < na; b += CT) {
+                                    const int32_t i = b + tid;
                                     const int32_t j = i < na ? ALIVE[i] : 0;
                                     const int32_t c = i < na ? CAPA[j] : 0;
                                     const bool keep = c >= r;
-                                    const uint64_t bm = __ballot(keep);
-                                    __builtin_amdgcn_wave_barrier();
-                                    if (keep) { ALIVE[nn2 + mbcnt(bm)] = j; cm2 = min(cm2, c); }
-                                    nn2 += __builtin_popcountll(bm);
-                                    __builtin_amdgcn_wave_barrier();
+                                    int32_t tot;
+                                    const int32_t slot = blk_compact(cred, par, wv, keep, tot);
+                                    if (keep) { ALIVE[nn2 + slot] = j; cm2 = min(cm2, (int64_t)c); }
+                                    nn2 += tot;
                                 }
                                 na = nn2;
-                                cmin = wave_min32(cm2);
+                                blk_red3<R_MIN, R_SUM, R_SUM>(cred, par, wv, lane, cm2, z0, z1);   // + ALIVE visible
+                                cmin = cm2;
                                 PROF_INC(6);
+                            }
                             }
                             PROF_ADD(2, t_rv);
                             PROF_T(t_up);
                             int32_t rl = last - j0;
                             if (rl < 0) rl += k;
                             evals += (uint64_t)(r - 1) * (uint64_t)k + (uint64_t)rl + 1;
-                            for (int32_t j = lane; j < k; j += 64) {
+                            for (int32_t j = tid; j < k; j += CT) {     // rows owned per thread: no conflicts
                                 const int32_t c = CAPA[j];
                                 int32_t rj = j - j0;
                                 if (rj < 0) rj += k;
@@ -1076,7 +1312,6 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                                     R[j] = q;
                                 }
                             }
-                            __builtin_amdgcn_wave_barrier();
                             PROF_ADD(3, t_up);
                             L = n_base + last + 1;
                             if (L >= len) L -= len;
@@ -1084,7 +1319,9 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                             placed = n;
                         }
                     }
-                    if (lane == 0 && placed > 0) gseg[nseg] = Seg{nsched, pos + done, placed, 0};
+                    PROF_T(t_pb);
+                    lds_barrier();            // the run's row updates are visible to every wave
+                    if (tid == 0 && placed > 0) gseg[nseg] = Seg{nsched, pos + done, placed, 0};
                     nseg += placed > 0 ? 1 : 0;
                     nsched += placed;
                     done += placed;
@@ -1094,6 +1331,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                     evals += kev * (uint64_t)k;
                     if (max_nodes > 0 && granted >= max_nodes) { stop = true; break; }
                     granted++;
+                    PROF_ADD(9, t_pb);
                     if (last_node >= 0 && !R[last_node].used) {
                         // :114-116 — and every later pod of the run repeats this pod's fate
                         done++;
@@ -1118,6 +1356,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                         open_node();
                         if (sf & SF_CP_EVAL) evals++;
                         done++;
+                        lds_barrier();
                         continue;
                     }
                     // Every row is full for this pod, so each remaining pod group opens a
@@ -1127,7 +1366,9 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                     // node's opening pod first fails FitsAnyNode over the k rows before it
                     // and takes one limiter grant.  Closed form over n_open nodes.
                     PROF_T(t_op);
-                    const int32_t ct = (sf & SF_FA_OK) ? rec_copies(trec, pcpu, pmem, peph, zero, rem2) : 1;
+                    const int32_t ct = !(sf & SF_FA_OK) ? 1
+                                       : rem2 <= (1 << 20) ? rec_copies_run(trec, dv, zero, rem2)
+                                                           : rec_copies(trec, pcpu, pmem, peph, zero, rem2);
                     int32_t n_open = (rem2 + ct - 1) / ct;
                     if (max_nodes > 0) n_open = min(n_open, 1 + (max_nodes - granted));
                     n_open = min(n_open, kcap - k);
@@ -1137,15 +1378,8 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                     int32_t s00 = L;
                     if (s00 >= len0) s00 = (int32_t)((uint32_t)s00 % (uint32_t)len0);
                     const int32_t j00 = s00 > n_base ? s00 - n_base : 0;
-                    uint64_t ev = 0;
-                    for (int32_t i = lane; i < n_open; i += 64) {
+                    for (int32_t i = tid; i < n_open; i += CT) {
                         const int32_t pi = (i == n_open - 1) ? placed2 - i * ct : ct;
-                        if (i > 0) ev += kev * (uint64_t)(k0 + i);
-                        if (sf & SF_CP_EVAL) ev += 1;
-                        if (pi >= 2) {
-                            const int32_t j0i = i == 0 ? j00 : 0;
-                            ev += (uint64_t)(k0 + i - j0i + 1) + (uint64_t)(pi - 2) * (uint64_t)(k0 + i + 1);
-                        }
                         NodeRec r = trec;
                         r.cpu -= (int64_t)pi * pcpu;
                         r.mem -= (int64_t)pi * pmem;
@@ -1154,20 +1388,21 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                         r.used = 1;
                         R[k0 + i] = r;
                     }
-                    evals += (uint64_t)wave_sum64((int64_t)ev);
-                    for (int32_t b = (k0 >> 6) + lane; b <= ((k0 + n_open - 1) >> 6); b += 64) SUM[b] = trec;
+                    for (int32_t b = (k0 >> 6) + tid; b <= ((k0 + n_open - 1) >> 6); b += CT) SUM[b] = trec;
                     if (use_ports) {
-                        for (int32_t i = lane; i < n_open * CA_PORT_WORDS; i += 64)
+                        for (int32_t i = tid; i < n_open * CA_PORT_WORDS; i += CT)
                             PORTS[(size_t)k0 * CA_PORT_WORDS + i] = tp.used_ports[i % CA_PORT_WORDS];
                     }
                     if (use_scalar) {
-                        for (int32_t i = lane; i < n_open * CA_MAX_SCALAR; i += 64) {
+                        for (int32_t i = tid; i < n_open * CA_MAX_SCALAR; i += CT) {
                             const int32_t sc = i / n_open, node = k0 + i % n_open;
                             SC[(size_t)sc * kcap + node] = wsub(tp.node.alloc_scalar[sc], tp.used_scalar[sc]);
                         }
                     }
-                    if (so_node) for (int32_t t = lane; t < placed2; t += 64) so_node[nsched + t] = k0 + t / ct;
-                    if (lane == 0 && placed2 > 0) gseg[nseg] = Seg{nsched, pos + done, placed2, 0};
+                    lds_barrier();                                                  // new rows visible
+                    evals += open_evals(n_open, ct, placed2, k0, j00, kev, (sf & SF_CP_EVAL) != 0);
+                    if (so_node) for (int32_t t = tid; t < placed2; t += CT) so_node[nsched + t] = k0 + t / ct;
+                    if (tid == 0 && placed2 > 0) gseg[nseg] = Seg{nsched, pos + done, placed2, 0};
                     nseg += placed2 > 0 ? 1 : 0;
                     if (ct >= 2 && placed2 >= 2) {
                         if (!first_success) { first_success = true; sensitive = k0 + 1 >= 2; }
@@ -1178,10 +1413,10 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                     granted += n_open - 1;
                     nsched += placed2;
                     done += placed2;
-                    __builtin_amdgcn_wave_barrier();
                     PROF_ADD(4, t_op);
                 }
                 pos = e;
+                PROF_ADD(11, t_run);
                 continue;
             }
         }
@@ -1249,7 +1484,9 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                             const int64_t mm = wave_max64(in ? nr.mem : INT64_MIN);
                             const int64_t me = wave_max64(in ? nr.eph : INT64_MIN);
                             const int32_t mp = wave_max32(in ? nr.pods : INT32_MIN);
-                            if (lane == 0) {
+                            // (one writer; another wave may read either value of any field:
+                            // both bound every row of the block, so its `found` is the same)
+                            if (tid == 0) {
                                 NodeRec sm;
                                 sm.cpu = mc; sm.mem = mm; sm.eph = me; sm.pods = mp; sm.used = 0;
                                 SUM[bb] = sm;
@@ -1277,6 +1514,7 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
             granted++;
             if (last_node >= 0 && !R[last_node].used) continue;               // :114-116
             if (k >= kcap) { res.status = CA_ECAPACITY; break; }
+            lds_barrier();                    // every wave's scan is done before rows change
             const int32_t nn = open_node();
             // CheckPredicates(pod, newNode) (:132-134)
             if (sf & SF_CP_EVAL) evals++;
@@ -1293,11 +1531,12 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
                     ok = c == 0;
                 }
             }
-            if (!ok) continue;
+            if (!ok) { lds_barrier(); continue; }
             found = nn;
         }
+        lds_barrier();                        // every wave's scan is done before R[found] changes
         // AddPod(pod, node) (:96 / :135) — NodeInfo.update on the new-node row
-        if (lane == 0) {
+        if (tid == 0) {
             NodeRec r = R[found];
             r.cpu = wsub(r.cpu, pcpu);
             r.mem = wsub(r.mem, pmem);
@@ -1306,29 +1545,30 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
             r.used = 1;
             R[found] = r;
         }
-        if (lane == sl) { out_node = found; out_idx = nsched; pend = true; }
+        if (w0 && lane == sl) { out_node = found; out_idx = nsched; pend = true; }
         if (sf & SF_SCALAR) {
-            if (lane < CA_MAX_SCALAR) {
-                const size_t ix = (size_t)lane * kcap + found;
-                SC[ix] = wsub(SC[ix], psc[lane]);
+            if (tid < CA_MAX_SCALAR) {
+                const size_t ix = (size_t)tid * kcap + found;
+                SC[ix] = wsub(SC[ix], psc[tid]);
             }
         }
         if (sf & SF_PORTS) {
-            if (lane < CA_PORT_WORDS) PORTS[(size_t)found * CA_PORT_WORDS + lane] |= puse[lane];
+            if (tid < CA_PORT_WORDS) PORTS[(size_t)found * CA_PORT_WORDS + tid] |= puse[tid];
         }
         nsched++;
-        __builtin_amdgcn_wave_barrier();
+        lds_barrier();                        // the placement is visible to every wave
     }
     if (pend) {
         so_pod[out_idx] = cur.pod;
         if (so_node) so_node[out_idx] = out_node;
     }
     // newNodesWithPods
-    int32_t cnt = 0;
-    for (int32_t j = lane; j < k; j += 64) cnt += R[j].used;
-    cnt = __ockl_wfred_add_i32(cnt);
-    if (lane == 0) {
-        res.node_count = cnt;
+    lds_barrier();
+    int64_t cnt = 0, z0 = 0, z1 = 0;
+    for (int32_t j = tid; j < k; j += CT) cnt += R[j].used;
+    blk_red3<R_SUM, R_SUM, R_SUM>(cred, par, wv, lane, cnt, z0, z1);
+    if (tid == 0) {
+        res.node_count = (int32_t)cnt;
         res.n_sched = nsched;
         res.nodes_added = k;
         res.lout = L;
@@ -1339,13 +1579,32 @@ __global__ void __launch_bounds__(64) k_ffd_chain(
         res.pad = (uint64_t)(uint32_t)(wall_clock64() - t_begin) | ((uint64_t)n_single << 32);
         outs[g] = res;
     }
-    if (tickets) push_tickets(g, P, nsub, tickets, qctl, lane);
-    if (lane == 0) {
+    if (tickets) {
+        __threadfence();                        // every wave's result stores, before the release
+        __syncthreads();
+        if (w0) push_tickets(g, P, nsub, tickets, qctl, lane);
+    }
+    if (tid == 0) {
 #ifdef CASIM_PROF
         prof[5] = clock64() - t_cyc0;
-        if (g < 1024) for (int i = 0; i < 8; i++) g_chain_prof[g][i] = prof[i];
+        if (g < 1024) for (int i = 0; i < NPROF; i++) g_chain_prof[g][i] = prof[i];
 #endif
     }
+}
+
+// Round-1 state of a batch in one launch instead of five copies/fills on the critical
+// path: every group needed, every group from the caller's lastIndex, no unsupported
+// group yet, publisher tickets empty, queue counters zero.
+__global__ void __launch_bounds__(256) k_round_init(int32_t G, int32_t lin0, int32_t* __restrict__ lin,
+                                                   uint8_t* __restrict__ need, uint32_t* __restrict__ unsup,
+                                                   int32_t* __restrict__ tickets, int32_t n_tickets,
+                                                   int32_t* __restrict__ qctl) {
+    const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int32_t stride = (int32_t)(gridDim.x * blockDim.x);
+    for (int32_t g = i; g < G; g += stride) { lin[g] = lin0; need[g] = 1; unsup[g] = 0; }
+    if (tickets)
+        for (int32_t t = i; t < n_tickets; t += stride) tickets[t] = -1;
+    if (qctl && i < 4) qctl[i] = 0;
 }
 
 // 5. scheduled pods of the run placements: sched_pod[dst + t] = stream pod at src + t.
@@ -1537,8 +1796,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     int32_t kcap = lim->max_nodes > 0 ? std::min(lim->max_nodes, std::max(p->max_count, 1)) : std::max(p->max_count, 1);
     kcap = ((kcap + 63) / 64) * 64;
     const size_t lds = chain_lds_bytes(kcap, p->use_ports, p->use_scalar);
-    if (lds > 160 * 1024) return CA_EUNSUPPORTED;   // HBM-backed variant is future work
-    CA_HIP_CHECK(hipMemsetAsync(p->d_unsup.ptr, 0, sizeof(uint32_t) * G, st));
+    if (lds + sizeof(ChainRed) > 160 * 1024) return CA_EUNSUPPORTED;   // HBM-backed variant is future work
     // Zero-copy results: when the caller's sched_pod is page-locked (ca_host_alloc) and no
     // node ordinals are wanted, the chains publish straight into it (k_ffd_chain epilogue).
     int32_t* publish = nullptr;
@@ -1556,7 +1814,18 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     }
     const char* rb_env = getenv("CASIM_RUN_BATCH");
     const int32_t batch_runs = (rb_env && rb_env[0] == '0') ? 0 : 1;
+    int32_t tickets1 = 0;                               // publisher tickets of round 1 (every group)
+    if (publish)
+        for (int32_t g = 0; g < G; g++) tickets1 += (p->h_meta[g].count + PCH - 1) / PCH;
     CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_START], st));
+    {
+        const int32_t n = std::max(G, tickets1);
+        hipLaunchKernelGGL(k_round_init, dim3(std::min((n + 255) / 256, 64)), dim3(256), 0, st, G, *last_index,
+                           p->d_lin.as<int32_t>(), p->d_need.as<uint8_t>(), p->d_unsup.as<uint32_t>(),
+                           publish ? p->d_tickets.as<int32_t>() : nullptr, tickets1,
+                           publish ? p->d_qctl.as<int32_t>() : nullptr);
+        CA_HIP_CHECK(hipGetLastError());
+    }
     // 1-3: score, sort, stream
     if (p->total > 0 && p->bucket) {
         const int32_t U = p->s->n_cls;
@@ -1626,19 +1895,23 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     float chain_ms = 0;
     for (;;) {
         rounds++;
-        CA_HIP_CHECK(hipMemcpyAsync(p->d_lin.ptr, lin.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
-        CA_HIP_CHECK(hipMemcpyAsync(p->d_need.ptr, need.data(), G, hipMemcpyHostToDevice, st));
+        if (rounds > 1) {      // round 1's state came from k_round_init
+            CA_HIP_CHECK(hipMemcpyAsync(p->d_lin.ptr, lin.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
+            CA_HIP_CHECK(hipMemcpyAsync(p->d_need.ptr, need.data(), G, hipMemcpyHostToDevice, st));
+        }
         int32_t round_tickets = 0;
         if (publish) {
             for (int32_t g = 0; g < G; g++) if (need[g]) round_tickets += (p->h_meta[g].count + PCH - 1) / PCH;
-            if (rounds > 1) CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_pub, 0));   // previous publisher done
-            CA_HIP_CHECK(hipMemsetAsync(p->d_tickets.ptr, 0xFF, sizeof(int32_t) * (size_t)std::max(round_tickets, 1), st));
-            CA_HIP_CHECK(hipMemsetAsync(p->d_qctl.ptr, 0, sizeof(int32_t) * 4, st));
+            if (rounds > 1) {
+                CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_pub, 0));   // previous publisher done
+                CA_HIP_CHECK(hipMemsetAsync(p->d_tickets.ptr, 0xFF, sizeof(int32_t) * (size_t)std::max(round_tickets, 1), st));
+                CA_HIP_CHECK(hipMemsetAsync(p->d_qctl.ptr, 0, sizeof(int32_t) * 4, st));
+            }
             CA_HIP_CHECK(hipEventRecord(p->ev_go, st));
         }
         CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN0], st));
         CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_ffd_chain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(k_ffd_chain, dim3(G), dim3(64), lds, st, p->d_meta.as<GroupMeta>(),
+        hipLaunchKernelGGL(k_ffd_chain, dim3(G), dim3(CT), lds, st, p->d_meta.as<GroupMeta>(),
                            p->d_stream.as<StreamPod>(), p->d_heads.as<uint64_t>(), p->d_tmpl.as<ca_template>(),
                            p->s->t.spec.as<ca_pod_spec>(), p->s->t.hot.as<PodHot>(), p->d_lin.as<int32_t>(),
                            p->d_need.as<uint8_t>(), p->d_unsup.as<uint32_t>(), n_base, lim->max_nodes, kcap,
@@ -1851,7 +2124,7 @@ int ca_estimate_batch(ca_mirror* m, const ca_podset* s, const int32_t* group_off
 #ifdef CASIM_PROF
 int ca_debug_chain_prof(uint64_t* out, int32_t n_groups) {
     if (n_groups > 1024) n_groups = 1024;
-    CA_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_prof), sizeof(uint64_t) * 8 * (size_t)n_groups));
+    CA_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_prof), sizeof(uint64_t) * NPROF * (size_t)n_groups));
     return CA_OK;
 }
 #endif

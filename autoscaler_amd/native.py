@@ -239,9 +239,9 @@ class Mirror:
 
     # -- estimator ------------------------------------------------------------
     def estimate(self, table: abi.PodTable, group_off, pod_idx, templates: np.ndarray, max_nodes: int,
-                 last_index: int = 0) -> EstimateOutput:
+                 last_index: int = 0, want_nodes: bool = True) -> EstimateOutput:
         with EstimatePlan(self, table, group_off, pod_idx, templates) as plan:
-            return plan.run(max_nodes, last_index)
+            return plan.run(max_nodes, last_index, want_nodes=want_nodes)
 
     # -- removal simulator ----------------------------------------------------
     def find_nodes_to_remove(self, candidates, dest_mask, cand_status, move_off, move_pods, hints,

@@ -13,7 +13,7 @@ m = native.Mirror(0)
 W.load_estimate(m, w)
 plan = native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates)
 for _ in range(3):
-    out = plan.run(w.max_nodes, 0, copy=False)
+    out = plan.run(w.max_nodes, 0, want_nodes=False, copy=False)   # the bench configuration
 d = plan.group_ticks()
 r = out.results
 order = np.argsort(-d[:, 0])
@@ -28,8 +28,8 @@ if os.environ.get("CASIM_LIB_PATH", "").endswith("libcasim_prof.so"):
     import ctypes as C
     lib = native.load()
     G = len(w.templates)
-    buf = np.zeros((G, 8), np.uint64)
+    buf = np.zeros((G, 12), np.uint64)
     lib.ca_debug_chain_prof(buf.ctypes.data_as(C.POINTER(C.c_uint64)), G)
-    names = ["run_end", "capa", "revol", "update", "open", "total", "n_rev", "n_runs"]
+    names = ["run_end", "capa", "revol", "update", "open", "total", "n_rev", "n_runs", "prologue", "post_bar", "exhausted", "run_total"]
     for g in order[:6]:
         print(f"g{g:3d} " + " ".join(f"{n}={int(v)}" for n, v in zip(names, buf[g])))

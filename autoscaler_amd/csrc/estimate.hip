@@ -801,23 +801,41 @@ __device__ inline int32_t run_end_pf(const uint64_t* __restrict__ hm, int32_t po
     return P;
 }
 
-// Zero-copy results (page-locked sched_pod, no node ordinals): a finished group hands
-// its output range to k_publish in PCH-sized tickets, so the results of the groups
-// that finish early cross PCIe while the long chains still run.  Release at agent scope:
-// the L2s of the 8 XCDs are not coherent, the publisher may run on another XCD.
-constexpr int PCH = 4096;
-__device__ inline void push_tickets(int32_t g, int32_t count, int32_t nsub, int32_t* tickets, int32_t* qctl, int lane) {
+// Zero-copy results (page-locked sched_pod, no node ordinals): a group hands its output
+// range to k_publish in pch-sized chunks ("tickets") as soon as each chunk is final —
+// every output of [c*pch, (c+1)*pch) is scheduled — and the rest when it ends, so the
+// results cross PCIe while the chains still run, the long ones included.  Each ticket
+// carries the group's progress (segments written, pods scheduled) at its push.
+// Release at agent scope: the L2s of the 8 XCDs are not coherent, the publisher may run
+// on another XCD.  Called by one whole wavefront (the one that stores the results).
+constexpr int PCH = 4096;      // default chunk (CASIM_PUB_CHUNK overrides, for tests)
+__device__ inline void push_chunks(int32_t g, int32_t c0, int32_t c1, int32_t nsub, int32_t* tickets, int32_t* qctl,
+                                   int2* prog, int32_t nseg, int32_t nsched, int lane) {
     __threadfence();
-    if (lane == 0) {
-        const int32_t nt = (count + PCH - 1) / PCH;
-        const int32_t base = atomicAdd(&qctl[1], nt);
-        for (int32_t i = 0; i < nt; i++)
-            __hip_atomic_store(&tickets[base + i], g * nsub + i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0 && c1 > c0) {
+        for (int32_t c = c0; c < c1; c++) prog[g * nsub + c] = make_int2(nseg, nsched);
+        const int32_t base = atomicAdd(&qctl[1], c1 - c0);
+        for (int32_t i = 0; i < c1 - c0; i++)
+            __hip_atomic_store(&tickets[base + i], g * nsub + c0 + i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
+// Data the chains write while the publisher runs (progress records, segments) is read
+// with device-coherent loads: a uniform plain load may be served from the scalar cache,
+// which the acquire does not invalidate, so a line cached for an earlier chunk (or a
+// neighbouring group) could hand back entries written after it was filled.
+__device__ inline int32_t ld_coh(const int32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline Seg ld_seg(const Seg* p) {
+    const int32_t* q = reinterpret_cast<const int32_t*>(p);
+    Seg sg;
+    sg.dst = ld_coh(q); sg.src = ld_coh(q + 1); sg.len = ld_coh(q + 2); sg.pad = 0;
+    return sg;
+}
+
 // Publisher (second stream, concurrent with k_ffd_chain): block b claims the next ticket
-// in completion order, waits for it, and writes outputs [sub*PCH, +PCH) of its group
+// in completion order, waits for it, and writes outputs [sub*pch, +pch) of its group
 // into the caller's page-locked buffer: single placements from the chain's sched_pod,
 // run placements from the stream via the group's segments, -1 past n_scheduled.
 // Every block exits once all `total` tickets are claimed; a ticket not pushed within
@@ -826,6 +844,7 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
                                                 const Seg* __restrict__ segs, const int32_t* __restrict__ spod,
                                                 const int32_t* __restrict__ sched_dev, int32_t* __restrict__ tickets,
                                                 int32_t* __restrict__ qctl, int32_t total, int32_t nsub,
+                                                const int2* __restrict__ prog, int32_t pch,
                                                 int32_t* __restrict__ pub) {
     __shared__ int32_t s_t, s_tk, s_seg0;
     for (;;) {
@@ -849,16 +868,16 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
         __threadfence();                                   // acquire for every thread of the block
         const int32_t g = tk / nsub, sub = tk - g * nsub;
         const GroupMeta gm = groups[g];
-        const ChainOut o = outs[g];
         const Seg* gs = segs + gm.off;
-        const int32_t a = sub * PCH, b = min(gm.count, a + PCH);
-        const int32_t ns = o.status == CA_OK ? o.n_sched : 0;
-        const int32_t nseg = o.status == CA_OK ? o.nseg : 0;
+        const int32_t a = sub * pch, b = min(gm.count, a + pch);
+        const int32_t* pr = reinterpret_cast<const int32_t*>(prog + tk);   // the group's progress at the push
+        const int32_t nseg = ld_coh(pr);
+        const int32_t ns = ld_coh(pr + 1);
         if (threadIdx.x == 0) {                            // first segment ending after a
             int32_t lo = 0, hi = nseg;
             while (lo < hi) {
                 const int32_t mid = (lo + hi) >> 1;
-                const Seg sg = gs[mid];
+                const Seg sg = ld_seg(gs + mid);
                 if (sg.dst + sg.len <= a) lo = mid + 1; else hi = mid;
             }
             s_seg0 = lo;
@@ -870,7 +889,7 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
             int32_t lim = end, src_off = 0;
             bool from_seg = false;
             if (q < nseg) {
-                const Seg sg = gs[q];
+                const Seg sg = ld_seg(gs + q);
                 if (sg.dst <= at) {                            // inside segment q
                     from_seg = true;
                     src_off = sg.src - sg.dst;
@@ -908,7 +927,8 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     const int32_t* __restrict__ lin_arr, const uint8_t* __restrict__ need, const uint32_t* __restrict__ group_unsup,
     int32_t n_base, int32_t max_nodes, int32_t kcap, int32_t use_ports, int32_t use_scalar, int32_t batch_runs,
     int32_t* __restrict__ sched_pod, int32_t* __restrict__ sched_node, Seg* __restrict__ segs,
-    int32_t* __restrict__ tickets, int32_t* __restrict__ qctl, int32_t nsub, ChainOut* __restrict__ outs) {
+    int32_t* __restrict__ tickets, int32_t* __restrict__ qctl, int32_t nsub, int2* __restrict__ prog, int32_t pch,
+    ChainOut* __restrict__ outs) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int g = blockIdx.x;
     if (!need[g]) return;
@@ -936,7 +956,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     if (group_unsup[g]) {
         res.status = CA_EUNSUPPORTED;
         if (tid == 0) outs[g] = res;
-        if (tickets && w0) push_tickets(g, gm.count, nsub, tickets, qctl, lane);
+        if (tickets && w0) push_chunks(g, 0, (gm.count + pch - 1) / pch, nsub, tickets, qctl, prog, 0, 0, lane);
         return;
     }
     const int nb_cap = (kcap + 63) >> 6;
@@ -1003,6 +1023,20 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     };
     auto note_success = [&]() {
         if (!first_success) { first_success = true; sensitive = k >= 2; }
+    };
+    // publish the chunks whose outputs are all scheduled (wave 0 stores every result in
+    // publishing mode: segments by thread 0, single placements by its lanes)
+    int32_t tk_next = 0;
+    auto progress = [&]() {
+        if (!tickets || !w0) return;
+        const int32_t c1 = nsched / pch;
+        if (c1 <= tk_next) return;
+        if (pend) {                       // the pending single placement, stored now
+            so_pod[out_idx] = cur.pod;
+            pend = false;
+        }
+        push_chunks(g, tk_next, c1, nsub, tickets, qctl, prog, nseg, nsched, lane);
+        tk_next = c1;
     };
 
     int32_t pos = 0;
@@ -1325,6 +1359,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                     nseg += placed > 0 ? 1 : 0;
                     nsched += placed;
                     done += placed;
+                    progress();
                     if (done == RN) break;
                     exhausted = true;
                     // the next pod of the run fails FitsAnyNode: every new node visited
@@ -1413,6 +1448,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                     granted += n_open - 1;
                     nsched += placed2;
                     done += placed2;
+                    progress();
                     PROF_ADD(4, t_op);
                 }
                 pos = e;
@@ -1556,6 +1592,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
             if (tid < CA_PORT_WORDS) PORTS[(size_t)found * CA_PORT_WORDS + tid] |= puse[tid];
         }
         nsched++;
+        progress();
         lds_barrier();                        // the placement is visible to every wave
     }
     if (pend) {
@@ -1582,7 +1619,12 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     if (tickets) {
         __threadfence();                        // every wave's result stores, before the release
         __syncthreads();
-        if (w0) push_tickets(g, P, nsub, tickets, qctl, lane);
+        if (w0) {
+            const bool ok = res.status == CA_OK;
+            // a group that failed after publishing chunks: the host falls back to the copy
+            if (!ok && tk_next > 0 && lane == 0) atomicExch(&qctl[3], 1);
+            push_chunks(g, tk_next, (P + pch - 1) / pch, nsub, tickets, qctl, prog, ok ? nseg : 0, ok ? nsched : 0, lane);
+        }
     }
     if (tid == 0) {
 #ifdef CASIM_PROF
@@ -1669,7 +1711,11 @@ struct ca_estimate_plan {
     hipStream_t pub_stream = nullptr;
     hipEvent_t ev_go = nullptr, ev_pub = nullptr;
     DevBuf d_tickets, d_qctl;
-    int32_t n_tickets = 0, nsub = 0;
+    int32_t n_tickets = 0, nsub = 0, pch = PCH;
+    DevBuf d_prog;                 // progress record per ticket slot (segments, pods scheduled)
+    // page-locked landing buffers of the per-round readback (chain outputs + publisher
+    // counters): one small D2H each and one synchronisation per round
+    HostBuf h_out, h_qc;
     ~ca_estimate_plan() {
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (ev_go) (void)hipEventDestroy(ev_go);
@@ -1687,6 +1733,11 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_go, hipEventDisableTiming));
     CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_pub, hipEventDisableTiming));
     CA_HIP_CHECK(hipStreamCreateWithFlags(&p->pub_stream, hipStreamNonBlocking));
+    {
+        int rc0;
+        if ((rc0 = p->h_out.reserve(sizeof(ChainOut) * (size_t)std::max(G, 1))) != CA_OK) return rc0;
+        if ((rc0 = p->h_qc.reserve(sizeof(int32_t) * 4)) != CA_OK) return rc0;
+    }
     p->h_off.assign(group_off, group_off + G + 1);
     p->h_tmpl.assign(templates, templates + G);
     p->total = group_off[G] - group_off[0];
@@ -1746,10 +1797,15 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     if ((rc = p->d_heads.reserve(sizeof(uint64_t) * (size_t)std::max(p->n_masks, 1))) != CA_OK) return rc;
     if ((rc = p->d_spod.reserve(sizeof(int32_t) * tot)) != CA_OK) return rc;
     if ((rc = p->d_seg.reserve(sizeof(Seg) * tot)) != CA_OK) return rc;
+    p->pch = PCH;
+    if (const char* e = getenv("CASIM_PUB_CHUNK")) p->pch = std::max(1, atoi(e));
+    const int32_t pch = p->pch;
     p->n_tickets = 0;
-    for (int32_t g = 0; g < G; g++) p->n_tickets += (p->h_meta[g].count + PCH - 1) / PCH;
-    p->nsub = std::max(1, (p->max_count + PCH - 1) / PCH);
+    for (int32_t g = 0; g < G; g++) p->n_tickets += (p->h_meta[g].count + pch - 1) / pch;
+    p->nsub = std::max(1, (p->max_count + pch - 1) / pch);
     if ((rc = p->d_tickets.reserve(sizeof(int32_t) * (size_t)std::max(p->n_tickets, 1))) != CA_OK) return rc;
+    if ((int64_t)G * p->nsub < INT32_MAX &&
+        (rc = p->d_prog.reserve(sizeof(int2) * (size_t)G * (size_t)p->nsub)) != CA_OK) return rc;
     if ((rc = p->d_qctl.reserve(sizeof(int32_t) * 4)) != CA_OK) return rc;
     if ((rc = p->d_unsup.reserve(sizeof(uint32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
     if ((rc = p->d_lin.reserve(sizeof(int32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
@@ -1816,7 +1872,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     const int32_t batch_runs = (rb_env && rb_env[0] == '0') ? 0 : 1;
     int32_t tickets1 = 0;                               // publisher tickets of round 1 (every group)
     if (publish)
-        for (int32_t g = 0; g < G; g++) tickets1 += (p->h_meta[g].count + PCH - 1) / PCH;
+        for (int32_t g = 0; g < G; g++) tickets1 += (p->h_meta[g].count + p->pch - 1) / p->pch;
     CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_START], st));
     {
         const int32_t n = std::max(G, tickets1);
@@ -1901,11 +1957,11 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         }
         int32_t round_tickets = 0;
         if (publish) {
-            for (int32_t g = 0; g < G; g++) if (need[g]) round_tickets += (p->h_meta[g].count + PCH - 1) / PCH;
+            for (int32_t g = 0; g < G; g++) if (need[g]) round_tickets += (p->h_meta[g].count + p->pch - 1) / p->pch;
             if (rounds > 1) {
                 CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_pub, 0));   // previous publisher done
                 CA_HIP_CHECK(hipMemsetAsync(p->d_tickets.ptr, 0xFF, sizeof(int32_t) * (size_t)std::max(round_tickets, 1), st));
-                CA_HIP_CHECK(hipMemsetAsync(p->d_qctl.ptr, 0, sizeof(int32_t) * 4, st));
+                CA_HIP_CHECK(hipMemsetAsync(p->d_qctl.ptr, 0, sizeof(int32_t) * 3, st));   // [3] stays: sticky
             }
             CA_HIP_CHECK(hipEventRecord(p->ev_go, st));
         }
@@ -1918,20 +1974,27 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                            p->use_ports ? 1 : 0, p->use_scalar ? 1 : 0, batch_runs,
                            p->d_sched_pod.as<int32_t>(), sched_node ? p->d_sched_node.as<int32_t>() : nullptr,
                            p->d_seg.as<Seg>(), publish ? p->d_tickets.as<int32_t>() : nullptr,
-                           p->d_qctl.as<int32_t>(), p->nsub, p->d_out.as<ChainOut>());
+                           p->d_qctl.as<int32_t>(), p->nsub, p->d_prog.as<int2>(), p->pch, p->d_out.as<ChainOut>());
         CA_HIP_CHECK(hipGetLastError());
         if (publish && round_tickets > 0) {
             CA_HIP_CHECK(hipStreamWaitEvent(p->pub_stream, p->ev_go, 0));
             hipLaunchKernelGGL(k_publish, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, p->pub_stream,
                                p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
                                p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int32_t>(),
-                               p->d_qctl.as<int32_t>(), round_tickets, p->nsub, publish);
+                               p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
+                               publish);
             CA_HIP_CHECK(hipGetLastError());
             CA_HIP_CHECK(hipEventRecord(p->ev_pub, p->pub_stream));
         }
         CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN1], st));
-        std::vector<ChainOut> fresh(G);
-        CA_HIP_CHECK(hipMemcpyAsync(fresh.data(), p->d_out.ptr, sizeof(ChainOut) * G, hipMemcpyDeviceToHost, st));
+        // one readback per round: the chain outputs, and (publishing) the publisher's
+        // counters once it is done — the results are then already in the caller's buffer
+        if (publish) {
+            CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_pub, 0));
+            CA_HIP_CHECK(hipMemcpyAsync(p->h_qc.ptr, p->d_qctl.ptr, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, st));
+        }
+        const ChainOut* fresh = p->h_out.as<ChainOut>();
+        CA_HIP_CHECK(hipMemcpyAsync(p->h_out.ptr, p->d_out.ptr, sizeof(ChainOut) * G, hipMemcpyDeviceToHost, st));
         CA_HIP_CHECK(hipStreamSynchronize(st));
         float ms = 0;
         (void)hipEventElapsedTime(&ms, p->ev[ca_estimate_plan::EV_CHAIN0], p->ev[ca_estimate_plan::EV_CHAIN1]);
@@ -1989,11 +2052,8 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     if (publish) {
         // the publisher of the last round wrote the results; a deadline hit (a chain that
         // died) falls back to the device copy + D2H
-        int32_t qc[4] = {0, 0, 0, 0};
-        CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_pub, 0));
-        CA_HIP_CHECK(hipMemcpyAsync(qc, p->d_qctl.ptr, sizeof(qc), hipMemcpyDeviceToHost, st));
-        CA_HIP_CHECK(hipStreamSynchronize(st));
-        if (qc[2] != 0) {
+        const int32_t* qc = p->h_qc.as<int32_t>();      // read back with the last round's outputs
+        if (qc[2] != 0 || qc[3] != 0) {
             set_last_error("estimate publisher missed a ticket; results copied instead");
             hipLaunchKernelGGL(k_copy_segments, dim3((p->max_count + CPY_PER_BLOCK - 1) / CPY_PER_BLOCK, G), dim3(256), 0,
                                st, p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),

@@ -268,9 +268,12 @@ def test_estimate_full_c2_parity(oracle):
 
 
 @pytest.mark.parametrize("seed", range(8))
-def test_estimate_plan_publish_random(seed, oracle):
+@pytest.mark.parametrize("chunk", ["4096", "64"], ids=["chunk4096", "chunk64"])
+def test_estimate_plan_publish_random(seed, chunk, oracle, monkeypatch):
     """Zero-copy results (plan, page-locked sched_pod, no node ordinals) on random inputs,
-    including unsupported and capacity-limited groups."""
+    including unsupported and capacity-limited groups.  With 64-output chunks the chains
+    publish most chunks while they still run (progressive tickets)."""
+    monkeypatch.setenv("CASIM_PUB_CHUNK", chunk)
     rng, nodes, pods, templates, groups = _run_heavy_inputs(seed)
     table, node_recs, tm, off, pod_idx = _encode_estimate(nodes, pods, templates, groups)
     max_nodes = rng.choice([0, 1, 5, 40])

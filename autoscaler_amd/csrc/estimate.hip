@@ -1843,7 +1843,11 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     ca_mirror* m = p->m;
     hipStream_t st = m->stream;
     const int32_t G = p->G;
-    if (!lim || !last_index || !results || !sched_pod) return CA_EINVAL;
+    if (!lim || !last_index || !results) return CA_EINVAL;
+    // sched_pod == NULL: the scheduled pods stay in device memory (ca_estimate_plan_fetch /
+    // ca_estimate_plan_device_results); no node ordinals then
+    const bool to_host = sched_pod != nullptr;
+    if (!to_host && sched_node) return CA_EINVAL;
     const auto t_start = std::chrono::steady_clock::now();
     CA_HIP_CHECK(hipSetDevice(m->device));
     const int32_t n_base = (int32_t)m->nodes.size();
@@ -1856,7 +1860,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     // Zero-copy results: when the caller's sched_pod is page-locked (ca_host_alloc) and no
     // node ordinals are wanted, the chains publish straight into it (k_ffd_chain epilogue).
     int32_t* publish = nullptr;
-    if (!sched_node && p->total > 0 && (int64_t)G * p->nsub < INT32_MAX && !getenv("CASIM_NO_PUBLISH")) {
+    if (to_host && !sched_node && p->total > 0 && (int64_t)G * p->nsub < INT32_MAX && !getenv("CASIM_NO_PUBLISH")) {
         hipPointerAttribute_t attr;
         if (hipPointerGetAttributes(&attr, sched_pod) == hipSuccess && attr.type == hipMemoryTypeHost &&
             attr.devicePointer != nullptr)
@@ -1864,10 +1868,8 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         else
             (void)hipGetLastError();
     }
-    if (p->total > 0 && !publish) {   // entries past n_scheduled read back as -1
-        CA_HIP_CHECK(hipMemsetAsync(p->d_sched_pod.ptr, 0xFF, sizeof(int32_t) * p->total, st));
-        if (sched_node) CA_HIP_CHECK(hipMemsetAsync(p->d_sched_node.ptr, 0xFF, sizeof(int32_t) * p->total, st));
-    }
+    // (no fill of the result buffers: k_copy_segments writes every output the chains do
+    // not — run placements, and -1 past n_scheduled or for a failed group)
     const char* rb_env = getenv("CASIM_RUN_BATCH");
     const int32_t batch_runs = (rb_env && rb_env[0] == '0') ? 0 : 1;
     int32_t tickets1 = 0;                               // publisher tickets of round 1 (every group)
@@ -2062,7 +2064,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             CA_HIP_CHECK(hipMemcpyAsync(sched_pod, p->d_sched_pod.ptr, sizeof(int32_t) * std::max(p->total, 0),
                                         hipMemcpyDeviceToHost, st));
         }
-    } else {
+    } else if (to_host) {
         CA_HIP_CHECK(hipMemcpyAsync(sched_pod, p->d_sched_pod.ptr, sizeof(int32_t) * std::max(p->total, 0),
                                     hipMemcpyDeviceToHost, st));
     }
@@ -2125,6 +2127,20 @@ int ca_estimate_plan_create(ca_mirror* m, const ca_podset* s, const int32_t* gro
     int rc = plan_prepare(p, m, s, group_off, pod_idx, templates, n_groups);
     if (rc != CA_OK) { delete p; return rc; }
     *out = p;
+    return CA_OK;
+}
+
+int ca_estimate_plan_fetch(const ca_estimate_plan* p, int32_t* sched_pod) {
+    if (!p || !sched_pod) return CA_EINVAL;
+    CA_HIP_CHECK(hipSetDevice(p->m->device));
+    if (p->total > 0)
+        CA_HIP_CHECK(hipMemcpy(sched_pod, p->d_sched_pod.ptr, sizeof(int32_t) * (size_t)p->total, hipMemcpyDeviceToHost));
+    return CA_OK;
+}
+
+int ca_estimate_plan_device_results(const ca_estimate_plan* p, const int32_t** sched_pod_dev) {
+    if (!p || !sched_pod_dev) return CA_EINVAL;
+    *sched_pod_dev = p->d_sched_pod.as<int32_t>();
     return CA_OK;
 }
 

@@ -70,6 +70,8 @@ def load() -> C.CDLL:
         "ca_estimate_plan_create": ([vp, vp, vp, vp, vp, i32, p(vp)], C.c_int),
         "ca_estimate_plan_run": ([vp, vp, p(i32), vp, vp, vp], C.c_int),
         "ca_estimate_plan_destroy": ([vp], C.c_int),
+        "ca_estimate_plan_fetch": ([vp, vp], C.c_int),
+        "ca_estimate_plan_device_results": ([vp, p(vp)], C.c_int),
         "ca_estimate_plan_stats": ([vp, p(i32), p(C.c_float), p(C.c_float), p(C.c_float)], C.c_int),
         "ca_estimate_plan_chain_info": ([vp, p(i32), p(i32)], C.c_int),
         "ca_estimate_plan_timings": ([vp, p(C.c_float), i32], C.c_int),
@@ -106,7 +108,8 @@ def exported_symbols() -> list[str]:
         "ca_mirror_node_pods", "ca_podset_create", "ca_podset_destroy", "ca_fits_any_node", "ca_check_predicates",
         "ca_fits_matrix", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
         "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_estimate_plan_timings",
-        "ca_estimate_plan_group_ticks", "ca_find_nodes_to_remove",
+        "ca_estimate_plan_group_ticks", "ca_estimate_plan_fetch", "ca_estimate_plan_device_results",
+        "ca_find_nodes_to_remove",
         "ca_removal_stats", "ca_removal_timings", "ca_removal_plan_create", "ca_removal_plan_run",
         "ca_removal_plan_destroy", "ca_mirror_set_hints", "ca_mirror_get_hints",
         "ca_removal_candidate_ticks",
@@ -375,17 +378,30 @@ class EstimatePlan:
         self.sched_node = self._pinned.array[n:]
         self.results = np.zeros(self.G, abi.ESTIMATE_RESULT_DTYPE)
 
-    def run(self, max_nodes: int, last_index: int = 0, want_nodes: bool = True, copy: bool = True) -> EstimateOutput:
+    def run(self, max_nodes: int, last_index: int = 0, want_nodes: bool = True, copy: bool = True,
+            device_results: bool = False) -> EstimateOutput:
         """One Estimate batch.  With copy=False the returned arrays are views of the plan's
-        page-locked result buffers, overwritten by the next run."""
+        page-locked result buffers, overwritten by the next run.  With device_results=True
+        the scheduled pods stay in device memory (sched_pod/sched_node of the returned
+        output are None; fetch() copies them)."""
         lim = abi.LimiterC(max_nodes, 0)
         li = C.c_int32(last_index)
+        if device_results:
+            _check(self.lib.ca_estimate_plan_run(self.h, C.byref(lim), C.byref(li), ptr(self.results), None, None),
+                   "ca_estimate_plan_run")
+            return EstimateOutput(self.results.copy() if copy else self.results, None, None, li.value)
         _check(self.lib.ca_estimate_plan_run(self.h, C.byref(lim), C.byref(li), ptr(self.results),
                                              ptr(self.sched_pod), ptr(self.sched_node) if want_nodes else None),
                "ca_estimate_plan_run")
         f = (lambda a: a.copy()) if copy else (lambda a: a)
         return EstimateOutput(f(self.results), f(self.sched_pod[: self.total]), f(self.sched_node[: self.total]),
                               li.value)
+
+    def fetch(self) -> np.ndarray:
+        """The scheduled pods of the last run, copied from device memory."""
+        out = np.full(max(self.total, 1), -1, np.int32)
+        _check(self.lib.ca_estimate_plan_fetch(self.h, ptr(out)), "ca_estimate_plan_fetch")
+        return out[: self.total]
 
     def stats(self) -> dict:
         r, a, b, c = C.c_int32(0), C.c_float(0), C.c_float(0), C.c_float(0)

@@ -319,6 +319,12 @@ int ca_estimate_plan_create(ca_mirror* m, const ca_podset* s, const int32_t* gro
                             int32_t n_groups, ca_estimate_plan** out);
 int ca_estimate_plan_run(ca_estimate_plan* p, const ca_limiter* limiter, int32_t* last_index,
                          ca_estimate_result* results, int32_t* sched_pod, int32_t* sched_node);
+/* sched_pod == NULL (and sched_node == NULL) in ca_estimate_plan_run keeps the scheduled
+ * pods in device memory: results[] and last_index are returned as usual, the pod lists
+ * stay in the plan (same layout as sched_pod) until the next run.  Fetch them with
+ * ca_estimate_plan_fetch (one D2H), or hand the device pointer to a device consumer. */
+int ca_estimate_plan_fetch(const ca_estimate_plan* p, int32_t* sched_pod);
+int ca_estimate_plan_device_results(const ca_estimate_plan* p, const int32_t** sched_pod_dev);
 int ca_estimate_plan_destroy(ca_estimate_plan* p);
 /* statistics of the last run: speculation rounds, kernel time of the chain kernel (ms) */
 int ca_estimate_plan_stats(const ca_estimate_plan* p, int32_t* rounds, float* chain_ms,

@@ -265,6 +265,10 @@ def test_estimate_full_c2_parity(oracle):
             assert np.array_equal(o.results, p.results)
             assert np.array_equal(o.sched_pod, p.sched_pod)
             assert o.last_index == p.last_index
+            d = plan.run(w.max_nodes, 0, device_results=True)        # results left in HBM (bench)
+            assert np.array_equal(o.results, d.results)
+            assert o.last_index == d.last_index
+            assert np.array_equal(o.sched_pod, plan.fetch())
 
 
 @pytest.mark.parametrize("seed", range(8))
@@ -288,7 +292,10 @@ def test_estimate_plan_publish_random(seed, chunk, oracle, monkeypatch):
         m.add_nodes(node_recs)
     with native.EstimatePlan(m, table, off, pod_idx, tm) as plan:
         g = plan.run(max_nodes, L0, want_nodes=False)
+        d = plan.run(max_nodes, L0, device_results=True)
+        dp = plan.fetch()
     assert np.array_equal(ro.results, g.results)
+    assert np.array_equal(ro.results, d.results)
     for k in range(len(groups)):
         if int(ro.results[k]["status"]) != 0:
             continue
@@ -296,7 +303,9 @@ def test_estimate_plan_publish_random(seed, chunk, oracle, monkeypatch):
         n = int(ro.results[k]["n_scheduled"])
         assert np.array_equal(ro.sched_pod[a:a + n], g.sched_pod[a:a + n]), (seed, k)
         assert (g.sched_pod[a + n:b] == -1).all()
-    assert ro.last_index == g.last_index
+        assert np.array_equal(ro.sched_pod[a:a + n], dp[a:a + n]), (seed, k)
+        assert (dp[a + n:b] == -1).all()
+    assert ro.last_index == g.last_index == d.last_index
 
 
 @pytest.mark.parametrize("size", ["small", "full"])

@@ -22,6 +22,7 @@
 
 #include <cstring>
 #include <algorithm>
+#include <functional>
 #include <chrono>
 #include <cstdlib>
 
@@ -73,6 +74,9 @@ struct alignas(16) GroupMeta {
     int32_t pad;
 };
 static_assert(sizeof(GroupMeta) == 64, "GroupMeta");
+// Group handled by a block: the launch's group map (a subset of the batch, e.g. the
+// heavy groups launched first) or the block index itself.
+#define GSEL(b) (gmap ? gmap[(b)] : (int)(b))
 
 struct alignas(16) ChainOut {
     int32_t node_count, n_sched, nodes_added, lin;
@@ -274,11 +278,13 @@ constexpr int RCH = RT / 64 / (RTHREADS / 64);   // 64-item chunks per wave
 __global__ void __launch_bounds__(1024) k_class_rank(const GroupMeta* __restrict__ groups,
                                                     const ca_template* __restrict__ tmpls,
                                                     const int64_t* __restrict__ cls_sc, int32_t U, int32_t NP,
-                                                    int32_t* __restrict__ crank) {
+                                                    int32_t* __restrict__ crank,
+    const int32_t* __restrict__ gmap) {
     __shared__ uint64_t key[CLS_MAX];
     __shared__ uint32_t idx[CLS_MAX];
     __shared__ int32_t sc[CLS_MAX];
-    const GroupMeta gm = groups[blockIdx.x];
+    const int gi = GSEL(blockIdx.x);
+    const GroupMeta gm = groups[gi];
     const ca_template& tp = tmpls[gm.tmpl];
     const int64_t acpu = tp.node.alloc_milli_cpu, amem = tp.node.alloc_memory;
     for (int i = threadIdx.x; i < NP; i += blockDim.x) {
@@ -322,7 +328,7 @@ __global__ void __launch_bounds__(1024) k_class_rank(const GroupMeta* __restrict
         for (int i = threadIdx.x; i < NP; i += blockDim.x) sc[i] += v[n++];
         __syncthreads();
     }
-    for (int i = threadIdx.x; i < U; i += blockDim.x) crank[(size_t)blockIdx.x * U + idx[i]] = sc[i];
+    for (int i = threadIdx.x; i < U; i += blockDim.x) crank[(size_t)gi * U + idx[i]] = sc[i];
 }
 
 __device__ inline uint32_t item_digit(const GroupMeta& gm, const uint32_t* __restrict__ src, int32_t i,
@@ -339,14 +345,15 @@ __global__ void __launch_bounds__(RTHREADS) k_radix_hist(const GroupMeta* __rest
                                                         const int32_t* __restrict__ pod_idx,
                                                         const int32_t* __restrict__ pcls,
                                                         const int32_t* __restrict__ crank, int32_t U, int shift,
-                                                        int32_t* __restrict__ hist) {
+                                                        int32_t* __restrict__ hist, const int32_t* __restrict__ gmap) {
     __shared__ int32_t h[256];
-    const GroupMeta gm = groups[blockIdx.y];
+    const int gi = GSEL(blockIdx.y);
+    const GroupMeta gm = groups[gi];
     const int32_t t = (int32_t)blockIdx.x;
     if (t >= gm.rtiles) return;
     h[threadIdx.x] = 0;
     __syncthreads();
-    const int32_t* cr = crank + (size_t)blockIdx.y * U;
+    const int32_t* cr = crank + (size_t)gi * U;
     const int32_t base = t * RT;
     for (int r = 0; r < RPT; r++) {
         const int32_t i = base + r * RTHREADS + (int32_t)threadIdx.x;
@@ -359,30 +366,32 @@ __global__ void __launch_bounds__(RTHREADS) k_radix_hist(const GroupMeta* __rest
     hist[gm.hoff + (int32_t)threadIdx.x * gm.rtiles + t] = h[threadIdx.x];
 }
 
-// exclusive scan of the group's [256][rtiles] histogram, digit-major
-__global__ void __launch_bounds__(256) k_radix_scan(const GroupMeta* __restrict__ groups, int32_t* __restrict__ hist) {
+// exclusive scan of the group's [256][rtiles] histogram, digit-major: thread d owns
+// digit d's row (its tiles, contiguous), so the scan is one row sum per thread, one
+// block scan of the 256 row totals and one pass writing the row's prefixes — two
+// barriers instead of two per 256 entries.
+__global__ void __launch_bounds__(256) k_radix_scan(const GroupMeta* __restrict__ groups, int32_t* __restrict__ hist,
+                                                   const int32_t* __restrict__ gmap) {
     __shared__ int32_t wsum[4];
-    const GroupMeta gm = groups[blockIdx.x];
-    const int32_t n = 256 * gm.rtiles;
-    int32_t* h = hist + gm.hoff;
+    const GroupMeta gm = groups[GSEL(blockIdx.x)];
+    const int32_t nt = gm.rtiles;
+    int32_t* row = hist + gm.hoff + (int32_t)threadIdx.x * nt;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int32_t carry = 0;
-    for (int32_t b = 0; b < n; b += 256) {
-        const int32_t i = b + (int32_t)threadIdx.x;
-        const int32_t v = i < n ? h[i] : 0;
-        int32_t x = v;                                   // inclusive wave scan
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) wsum[w] = x;
-        __syncthreads();
-        int32_t pre = carry;
-        for (int q = 0; q < w; q++) pre += wsum[q];
-        const int32_t tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-        if (i < n) h[i] = pre + x - v;
-        carry += tot;
-        __syncthreads();
+    int32_t tot = 0;
+    for (int32_t j = 0; j < nt; j++) tot += row[j];
+    int32_t x = tot;                                     // inclusive wave scan of row totals
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int32_t pre = x - tot;
+    for (int q = 0; q < w; q++) pre += wsum[q];
+    for (int32_t j = 0; j < nt; j++) {
+        const int32_t v = row[j];
+        row[j] = pre;
+        pre += v;
     }
 }
 
@@ -392,15 +401,16 @@ __global__ void __launch_bounds__(RTHREADS) k_radix_scatter(const GroupMeta* __r
                                                            const int32_t* __restrict__ pcls,
                                                            const int32_t* __restrict__ crank, int32_t U, int shift,
                                                            const int32_t* __restrict__ hist,
-                                                           uint32_t* __restrict__ dst) {
+                                                           uint32_t* __restrict__ dst, const int32_t* __restrict__ gmap) {
     __shared__ int32_t wcnt[RTHREADS / 64][256];
-    const GroupMeta gm = groups[blockIdx.y];
+    const int gi = GSEL(blockIdx.y);
+    const GroupMeta gm = groups[gi];
     const int32_t t = (int32_t)blockIdx.x;
     if (t >= gm.rtiles) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int d = lane; d < 256; d += 64) wcnt[w][d] = 0;
     __builtin_amdgcn_wave_barrier();
-    const int32_t* cr = crank + (size_t)blockIdx.y * U;
+    const int32_t* cr = crank + (size_t)gi * U;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t dg[RCH], pv[RCH];
     int32_t rk[RCH];
@@ -450,8 +460,10 @@ __global__ void __launch_bounds__(256) k_emit_bucket(const GroupMeta* __restrict
                                                     const ca_selector_term* __restrict__ terms,
                                                     const ca_selector_req* __restrict__ reqs,
                                                     StreamPod* __restrict__ out, int32_t* __restrict__ spod,
-                                                    uint64_t* __restrict__ heads, uint32_t* __restrict__ group_unsup) {
-    const GroupMeta gm = groups[blockIdx.y];
+                                                    uint64_t* __restrict__ heads, uint32_t* __restrict__ group_unsup,
+                                                    const int32_t* __restrict__ gmap) {
+    const int gi = GSEL(blockIdx.y);
+    const GroupMeta gm = groups[gi];
     const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     const int lane = threadIdx.x & 63;
     if ((int32_t)(blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) >= gm.count) return;   // whole wave past the end
@@ -484,7 +496,7 @@ __global__ void __launch_bounds__(256) k_emit_bucket(const GroupMeta* __restrict
         sp.flags = sf | (head ? SF_HEAD : 0u) | (bat ? SF_BATCH : 0u);
         out[gm.off + i] = sp;
         spod[gm.off + i] = pidx;
-        if (sf & SF_UNSUP) atomicOr(&group_unsup[blockIdx.y], 1u);
+        if (sf & SF_UNSUP) atomicOr(&group_unsup[gi], 1u);
     }
     const uint64_t hb = __ballot(head);
     if (lane == 0) heads[gm.moff + (i >> 6)] = hb;
@@ -842,10 +854,10 @@ __device__ inline Seg ld_seg(const Seg* p) {
 // the deadline (a chain that died) sets qctl[2] and ends the block.
 __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ groups, const ChainOut* __restrict__ outs,
                                                 const Seg* __restrict__ segs, const int32_t* __restrict__ spod,
-                                                const int32_t* __restrict__ sched_dev, int32_t* __restrict__ tickets,
+                                                const int32_t* sched_dev, int32_t* __restrict__ tickets,
                                                 int32_t* __restrict__ qctl, int32_t total, int32_t nsub,
                                                 const int2* __restrict__ prog, int32_t pch,
-                                                int32_t* __restrict__ pub) {
+                                                int32_t* pub) {      // pub may alias sched_dev (device results)
     __shared__ int32_t s_t, s_tk, s_seg0;
     for (;;) {
         if (threadIdx.x == 0) {
@@ -928,9 +940,9 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     int32_t n_base, int32_t max_nodes, int32_t kcap, int32_t use_ports, int32_t use_scalar, int32_t batch_runs,
     int32_t* __restrict__ sched_pod, int32_t* __restrict__ sched_node, Seg* __restrict__ segs,
     int32_t* __restrict__ tickets, int32_t* __restrict__ qctl, int32_t nsub, int2* __restrict__ prog, int32_t pch,
-    ChainOut* __restrict__ outs) {
+    ChainOut* __restrict__ outs, const int32_t* __restrict__ gmap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int g = blockIdx.x;
+    const int g = GSEL(blockIdx.x);
     if (!need[g]) return;
     const uint64_t t_begin = wall_clock64();      // diagnostics: ca_estimate_plan_group_ticks
     __builtin_amdgcn_s_setprio(3);                // the chain is the critical path: win issue over k_publish
@@ -1651,7 +1663,9 @@ __global__ void __launch_bounds__(256) k_round_init(int32_t G, int32_t lin0, int
 
 // 5. scheduled pods of the run placements: sched_pod[dst + t] = stream pod at src + t.
 // Output i of a group lies in the last segment with dst <= i, or was written directly
-// by the chain (single-pod placements).
+// by the chain (single-pod placements).  One block per CPY_PER_BLOCK outputs: one
+// binary search for the first segment reaching the block's range, then the segments
+// of the range are copied in turn (coalesced reads of the stream's pod ids).
 constexpr int CPY_PER_BLOCK = 2048;
 __global__ void __launch_bounds__(256) k_copy_segments(const GroupMeta* __restrict__ groups,
                                                       const ChainOut* __restrict__ outs, const Seg* __restrict__ segs,
@@ -1661,23 +1675,32 @@ __global__ void __launch_bounds__(256) k_copy_segments(const GroupMeta* __restri
     const ChainOut o = outs[blockIdx.y];
     const int32_t base = (int32_t)blockIdx.x * CPY_PER_BLOCK;
     if (base >= gm.count) return;
+    const int32_t end = min(base + CPY_PER_BLOCK, gm.count);
     const int32_t ns = o.status == CA_OK ? o.n_sched : 0;
     const int32_t nseg = o.status == CA_OK ? o.nseg : 0;
     const Seg* gs = segs + gm.off;
-    for (int32_t i = base + (int32_t)threadIdx.x; i < min(base + CPY_PER_BLOCK, gm.count); i += blockDim.x) {
-        if (i >= ns) {                             // past n_scheduled (or a failed group): also what
-            sched_pod[gm.off + i] = -1;            // an earlier speculation round of the group wrote
-            if (sched_node) sched_node[gm.off + i] = -1;
-            continue;
-        }
-        int32_t lo = 0, hi = nseg;                 // first segment with dst > i
-        while (lo < hi) {
-            const int32_t mid = (lo + hi) >> 1;
-            if (gs[mid].dst <= i) lo = mid + 1; else hi = mid;
-        }
-        if (lo == 0) continue;
-        const Seg sg = gs[lo - 1];
-        if (i < sg.dst + sg.len) sched_pod[gm.off + i] = spod[gm.off + sg.src + (i - sg.dst)];
+    int32_t* sp = sched_pod + gm.off;
+    const int32_t* src = spod + gm.off;
+    // past n_scheduled (or a failed group): -1, also over what an earlier speculation
+    // round of the group wrote
+    for (int32_t i = max(base, ns) + (int32_t)threadIdx.x; i < end; i += blockDim.x) {
+        sp[i] = -1;
+        if (sched_node) sched_node[gm.off + i] = -1;
+    }
+    const int32_t lim = min(end, ns);
+    if (base >= lim) return;
+    int32_t lo = 0, hi = nseg;                     // first segment ending after base
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        const Seg sg = gs[mid];
+        if (sg.dst + sg.len <= base) lo = mid + 1; else hi = mid;
+    }
+    for (int32_t q = lo; q < nseg; q++) {
+        const Seg sg = gs[q];
+        if (sg.dst >= lim) break;
+        const int32_t a = max(base, sg.dst), b = min(lim, sg.dst + sg.len);
+        const int32_t off = sg.src - sg.dst;
+        for (int32_t i = a + (int32_t)threadIdx.x; i < b; i += blockDim.x) sp[i] = src[off + i];
     }
 }
 
@@ -1716,11 +1739,25 @@ struct ca_estimate_plan {
     // page-locked landing buffers of the per-round readback (chain outputs + publisher
     // counters): one small D2H each and one synchronisation per round
     HostBuf h_out, h_qc;
+    // Heavy groups first: the chains of the groups whose closed-form FFD
+    // runs longest start as soon as their own sort is done, while the other groups sort
+    // on a second, lower-priority stream.  demand[g] = template copies the group's pods
+    // need (max over cpu, memory, pod slots of sum / template free); the map
+    // [heavy..., rest...] is rebuilt when the limiter's max_nodes changes.
+    std::vector<double> demand;
+    hipStream_t st2 = nullptr;
+    hipEvent_t ev_init = nullptr, ev_b = nullptr, ev_rb = nullptr;
+    DevBuf d_gmap;
+    int32_t map_max_nodes = -1, n_heavy = 0;
     ~ca_estimate_plan() {
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (ev_go) (void)hipEventDestroy(ev_go);
         if (ev_pub) (void)hipEventDestroy(ev_pub);
         if (pub_stream) (void)hipStreamDestroy(pub_stream);
+        if (st2) (void)hipStreamDestroy(st2);
+        if (ev_init) (void)hipEventDestroy(ev_init);
+        if (ev_b) (void)hipEventDestroy(ev_b);
+        if (ev_rb) (void)hipEventDestroy(ev_rb);
     }
 };
 
@@ -1733,6 +1770,14 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_go, hipEventDisableTiming));
     CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_pub, hipEventDisableTiming));
     CA_HIP_CHECK(hipStreamCreateWithFlags(&p->pub_stream, hipStreamNonBlocking));
+    {
+        int lo = 0, hi = 0;                  // the light groups' stream at the lowest priority
+        CA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        CA_HIP_CHECK(hipStreamCreateWithPriority(&p->st2, hipStreamNonBlocking, lo));
+    }
+    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_init, hipEventDisableTiming));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_b, hipEventDisableTiming));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_rb, hipEventDisableTiming));
     {
         int rc0;
         if ((rc0 = p->h_out.reserve(sizeof(ChainOut) * (size_t)std::max(G, 1))) != CA_OK) return rc0;
@@ -1785,6 +1830,20 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
         if (f & PF_PORTS) p->use_ports = true;
         if (f & PF_SCALAR_REQ) p->use_scalar = true;
     }
+    p->demand.assign(G, 0.0);
+    for (int32_t g = 0; g < G; g++) {
+        const GroupMeta& gm = p->h_meta[g];
+        double c = 0, mm = 0;
+        for (int32_t i = gm.off; i < gm.off + gm.count; i++) {
+            const ca_pod_spec& ps = s->h_pods[pod_idx[i]];
+            c += (double)ps.req_milli_cpu;
+            mm += (double)ps.req_memory;
+        }
+        double d = gm.tpods > 0 ? (double)gm.count / gm.tpods : 0.0;
+        if (gm.tcpu > 0) d = std::max(d, c / (double)gm.tcpu);
+        if (gm.tmem > 0) d = std::max(d, mm / (double)gm.tmem);
+        p->demand[g] = d;
+    }
     hipStream_t st = m->stream;
     int rc;
     const size_t tot = (size_t)std::max(p->total, 1);
@@ -1827,7 +1886,7 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
 
 int32_t pub_blocks() {
     const char* e = getenv("CASIM_PUB_BLOCKS");
-    return e ? std::max(1, atoi(e)) : 16;
+    return e ? std::max(1, atoi(e)) : 32;        // scripts/pub_sweep.sh: 32 x 4096-output chunks on C2
 }
 
 size_t chain_lds_bytes(int32_t kcap, bool use_ports, bool use_scalar) {
@@ -1859,14 +1918,18 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     if (lds + sizeof(ChainRed) > 160 * 1024) return CA_EUNSUPPORTED;   // HBM-backed variant is future work
     // Zero-copy results: when the caller's sched_pod is page-locked (ca_host_alloc) and no
     // node ordinals are wanted, the chains publish straight into it (k_ffd_chain epilogue).
+    // (Device-resident results could use the same publisher into the plan's own buffer;
+    // measured on C2 it slows the chains more than k_copy_segments after them costs.)
     int32_t* publish = nullptr;
     if (to_host && !sched_node && p->total > 0 && (int64_t)G * p->nsub < INT32_MAX && !getenv("CASIM_NO_PUBLISH")) {
-        hipPointerAttribute_t attr;
-        if (hipPointerGetAttributes(&attr, sched_pod) == hipSuccess && attr.type == hipMemoryTypeHost &&
-            attr.devicePointer != nullptr)
-            publish = static_cast<int32_t*>(attr.devicePointer);
-        else
-            (void)hipGetLastError();
+        {
+            hipPointerAttribute_t attr;
+            if (hipPointerGetAttributes(&attr, sched_pod) == hipSuccess && attr.type == hipMemoryTypeHost &&
+                attr.devicePointer != nullptr)
+                publish = static_cast<int32_t*>(attr.devicePointer);
+            else
+                (void)hipGetLastError();
+        }
     }
     // (no fill of the result buffers: k_copy_segments writes every output the chains do
     // not — run placements, and -1 past n_scheduled or for a failed group)
@@ -1884,6 +1947,39 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                            publish ? p->d_qctl.as<int32_t>() : nullptr);
         CA_HIP_CHECK(hipGetLastError());
     }
+    // heavy groups first (bucket path): see ca_estimate_plan::demand
+    bool split = false;
+    const int32_t* gmapA = nullptr;
+    const int32_t* gmapB = nullptr;
+    if (p->total > 0 && p->bucket && G >= 8 && !getenv("CASIM_NO_SPLIT")) {
+        if (p->map_max_nodes != lim->max_nodes) {
+            // chain length ~ the template copies a group opens over the runs it gets
+            // through: `demand` below the limiter's cap, cap^2/demand above it (the
+            // limiter stops the group after ~cap/demand of its pods)
+            const double M = lim->max_nodes > 0 ? (double)lim->max_nodes : 0.0;
+            std::vector<double> cost(G);
+            double cmax = 0;
+            for (int32_t g = 0; g < G; g++) {
+                const double d = p->demand[g];
+                cost[g] = (M > 0 && d > M) ? M * M / d : d;
+                cmax = std::max(cmax, cost[g]);
+            }
+            std::vector<int32_t> map;
+            map.reserve(G);
+            for (int32_t g = 0; g < G; g++) if (cmax > 0 && cost[g] >= 0.7 * cmax) map.push_back(g);
+            p->n_heavy = (int32_t)map.size();
+            for (int32_t g = 0; g < G; g++) if (!(cmax > 0 && cost[g] >= 0.7 * cmax)) map.push_back(g);
+            int rc;
+            if ((rc = p->d_gmap.reserve(sizeof(int32_t) * (size_t)G)) != CA_OK) return rc;
+            CA_HIP_CHECK(hipMemcpy(p->d_gmap.ptr, map.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice));
+            p->map_max_nodes = lim->max_nodes;
+        }
+        split = p->n_heavy > 0 && p->n_heavy < G;
+        gmapA = p->d_gmap.as<int32_t>();
+        gmapB = gmapA + p->n_heavy;
+    }
+    const int32_t nA = split ? p->n_heavy : G, nB = split ? G - p->n_heavy : 0;
+    std::function<int()> sort_light;        // split: the light groups' sort, queued after the heavy chains
     // 1-3: score, sort, stream
     if (p->total > 0 && p->bucket) {
         const int32_t U = p->s->n_cls;
@@ -1891,35 +1987,53 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         while (NP < U) NP <<= 1;
         int32_t* crank = p->d_crank.as<int32_t>();
         const int32_t* pcls = p->s->d_cls.as<int32_t>();
-        hipLaunchKernelGGL(k_class_rank, dim3(G), dim3(1024), 0, st, p->d_meta.as<GroupMeta>(), p->d_tmpl.as<ca_template>(),
-                           p->s->d_cls_sc.as<int64_t>(), U, NP, crank);
-        CA_HIP_CHECK(hipGetLastError());
-        CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], st));
         int32_t nb = 1, passes = 0;                       // buckets <= U: 8-bit digits
         while (nb < U) { nb <<= 8; passes++; }
         passes = std::max(passes, 1);
-        uint32_t* a = nullptr;                            // identity (position order)
-        uint32_t* bufs[2] = {p->d_sortA.as<uint32_t>(), p->d_sortB.as<uint32_t>()};
-        for (int ps = 0; ps < passes; ps++) {
-            uint32_t* b = bufs[ps & 1];
-            hipLaunchKernelGGL(k_radix_hist, dim3(p->max_rtiles, G), dim3(RTHREADS), 0, st, p->d_meta.as<GroupMeta>(), a,
-                               p->d_pod_idx.as<int32_t>(), pcls, crank, U, 8 * ps, p->d_hist.as<int32_t>());
-            CA_HIP_CHECK(hipGetLastError());
-            hipLaunchKernelGGL(k_radix_scan, dim3(G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(), p->d_hist.as<int32_t>());
-            CA_HIP_CHECK(hipGetLastError());
-            hipLaunchKernelGGL(k_radix_scatter, dim3(p->max_rtiles, G), dim3(RTHREADS), 0, st, p->d_meta.as<GroupMeta>(), a,
-                               p->d_pod_idx.as<int32_t>(), pcls, crank, U, 8 * ps, p->d_hist.as<int32_t>(), b);
-            CA_HIP_CHECK(hipGetLastError());
-            a = b;
-        }
-        CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], st));
         const int32_t blocks = (p->max_count + 255) / 256;
-        hipLaunchKernelGGL(k_emit_bucket, dim3(blocks, G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(), a,
-                           p->d_pod_idx.as<int32_t>(), p->d_tmpl.as<ca_template>(), p->s->t.hot.as<PodHot>(),
-                           p->s->t.spec.as<ca_pod_spec>(), p->s->t.terms.as<ca_selector_term>(),
-                           p->s->t.reqs.as<ca_selector_req>(), p->d_stream.as<StreamPod>(), p->d_spod.as<int32_t>(),
-                           p->d_heads.as<uint64_t>(), p->d_unsup.as<uint32_t>());
-        CA_HIP_CHECK(hipGetLastError());
+        // class ranks, LSD radix passes, stream emission for `ng` groups (map `gm`)
+        // (by value: the light groups' call runs after this block's locals are gone)
+        auto sort_groups = [=](hipStream_t ss, const int32_t* gm, int32_t ng, bool events) -> int {
+            hipLaunchKernelGGL(k_class_rank, dim3(ng), dim3(1024), 0, ss, p->d_meta.as<GroupMeta>(),
+                               p->d_tmpl.as<ca_template>(), p->s->d_cls_sc.as<int64_t>(), U, NP, crank, gm);
+            CA_HIP_CHECK(hipGetLastError());
+            if (events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], ss));
+            uint32_t* a = nullptr;                        // identity (position order)
+            uint32_t* bufs[2] = {p->d_sortA.as<uint32_t>(), p->d_sortB.as<uint32_t>()};
+            for (int ps = 0; ps < passes; ps++) {
+                uint32_t* b = bufs[ps & 1];
+                hipLaunchKernelGGL(k_radix_hist, dim3(p->max_rtiles, ng), dim3(RTHREADS), 0, ss, p->d_meta.as<GroupMeta>(),
+                                   a, p->d_pod_idx.as<int32_t>(), pcls, crank, U, 8 * ps, p->d_hist.as<int32_t>(), gm);
+                CA_HIP_CHECK(hipGetLastError());
+                hipLaunchKernelGGL(k_radix_scan, dim3(ng), dim3(256), 0, ss, p->d_meta.as<GroupMeta>(),
+                                   p->d_hist.as<int32_t>(), gm);
+                CA_HIP_CHECK(hipGetLastError());
+                hipLaunchKernelGGL(k_radix_scatter, dim3(p->max_rtiles, ng), dim3(RTHREADS), 0, ss,
+                                   p->d_meta.as<GroupMeta>(), a, p->d_pod_idx.as<int32_t>(), pcls, crank, U, 8 * ps,
+                                   p->d_hist.as<int32_t>(), b, gm);
+                CA_HIP_CHECK(hipGetLastError());
+                a = b;
+            }
+            if (events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], ss));
+            hipLaunchKernelGGL(k_emit_bucket, dim3(blocks, ng), dim3(256), 0, ss, p->d_meta.as<GroupMeta>(), a,
+                               p->d_pod_idx.as<int32_t>(), p->d_tmpl.as<ca_template>(), p->s->t.hot.as<PodHot>(),
+                               p->s->t.spec.as<ca_pod_spec>(), p->s->t.terms.as<ca_selector_term>(),
+                               p->s->t.reqs.as<ca_selector_req>(), p->d_stream.as<StreamPod>(), p->d_spod.as<int32_t>(),
+                               p->d_heads.as<uint64_t>(), p->d_unsup.as<uint32_t>(), gm);
+            CA_HIP_CHECK(hipGetLastError());
+            return CA_OK;
+        };
+        int rc;
+        if (split) {     // the light groups are sorted right after the heavy chains are queued
+            CA_HIP_CHECK(hipEventRecord(p->ev_init, st));
+            if ((rc = sort_groups(st, gmapA, nA, true)) != CA_OK) return rc;
+            sort_light = [=]() -> int {
+                CA_HIP_CHECK(hipStreamWaitEvent(p->st2, p->ev_init, 0));
+                return sort_groups(p->st2, gmapB, nB, false);
+            };
+        } else if ((rc = sort_groups(st, nullptr, G, true)) != CA_OK) {
+            return rc;
+        }
     } else if (p->total > 0) {
         const int32_t tiles = (p->max_count + TILE - 1) / TILE;
         hipLaunchKernelGGL(k_score_tiles, dim3(tiles, G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(),
@@ -1969,15 +2083,29 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         }
         CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN0], st));
         CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_ffd_chain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(k_ffd_chain, dim3(G), dim3(CT), lds, st, p->d_meta.as<GroupMeta>(),
-                           p->d_stream.as<StreamPod>(), p->d_heads.as<uint64_t>(), p->d_tmpl.as<ca_template>(),
-                           p->s->t.spec.as<ca_pod_spec>(), p->s->t.hot.as<PodHot>(), p->d_lin.as<int32_t>(),
-                           p->d_need.as<uint8_t>(), p->d_unsup.as<uint32_t>(), n_base, lim->max_nodes, kcap,
-                           p->use_ports ? 1 : 0, p->use_scalar ? 1 : 0, batch_runs,
-                           p->d_sched_pod.as<int32_t>(), sched_node ? p->d_sched_node.as<int32_t>() : nullptr,
-                           p->d_seg.as<Seg>(), publish ? p->d_tickets.as<int32_t>() : nullptr,
-                           p->d_qctl.as<int32_t>(), p->nsub, p->d_prog.as<int2>(), p->pch, p->d_out.as<ChainOut>());
-        CA_HIP_CHECK(hipGetLastError());
+        auto chain = [&](hipStream_t ss, const int32_t* gm, int32_t ng) -> int {
+            hipLaunchKernelGGL(k_ffd_chain, dim3(ng), dim3(CT), lds, ss, p->d_meta.as<GroupMeta>(),
+                               p->d_stream.as<StreamPod>(), p->d_heads.as<uint64_t>(), p->d_tmpl.as<ca_template>(),
+                               p->s->t.spec.as<ca_pod_spec>(), p->s->t.hot.as<PodHot>(), p->d_lin.as<int32_t>(),
+                               p->d_need.as<uint8_t>(), p->d_unsup.as<uint32_t>(), n_base, lim->max_nodes, kcap,
+                               p->use_ports ? 1 : 0, p->use_scalar ? 1 : 0, batch_runs,
+                               p->d_sched_pod.as<int32_t>(), sched_node ? p->d_sched_node.as<int32_t>() : nullptr,
+                               p->d_seg.as<Seg>(), publish ? p->d_tickets.as<int32_t>() : nullptr,
+                               p->d_qctl.as<int32_t>(), p->nsub, p->d_prog.as<int2>(), p->pch, p->d_out.as<ChainOut>(),
+                               gm);
+            CA_HIP_CHECK(hipGetLastError());
+            return CA_OK;
+        };
+        int rc;
+        if (rounds == 1 && split) {         // heavy groups on st as soon as their sort is done
+            if ((rc = chain(st, gmapA, nA)) != CA_OK) return rc;
+            if ((rc = sort_light()) != CA_OK) return rc;
+            if ((rc = chain(p->st2, gmapB, nB)) != CA_OK) return rc;
+            CA_HIP_CHECK(hipEventRecord(p->ev_b, p->st2));
+            CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_b, 0));
+        } else if ((rc = chain(st, nullptr, G)) != CA_OK) {
+            return rc;
+        }
         if (publish && round_tickets > 0) {
             CA_HIP_CHECK(hipStreamWaitEvent(p->pub_stream, p->ev_go, 0));
             hipLaunchKernelGGL(k_publish, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, p->pub_stream,
@@ -1991,13 +2119,24 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN1], st));
         // one readback per round: the chain outputs, and (publishing) the publisher's
         // counters once it is done — the results are then already in the caller's buffer
+        const ChainOut* fresh = p->h_out.as<ChainOut>();
+        CA_HIP_CHECK(hipMemcpyAsync(p->h_out.ptr, p->d_out.ptr, sizeof(ChainOut) * G, hipMemcpyDeviceToHost, st));
         if (publish) {
             CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_pub, 0));
             CA_HIP_CHECK(hipMemcpyAsync(p->h_qc.ptr, p->d_qctl.ptr, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, st));
         }
-        const ChainOut* fresh = p->h_out.as<ChainOut>();
-        CA_HIP_CHECK(hipMemcpyAsync(p->h_out.ptr, p->d_out.ptr, sizeof(ChainOut) * G, hipMemcpyDeviceToHost, st));
-        CA_HIP_CHECK(hipStreamSynchronize(st));
+        CA_HIP_CHECK(hipEventRecord(p->ev_rb, st));
+        // results of this round, queued behind the readback: the device fills them while
+        // the host walks the lastIndex chain (a later round queues them again)
+        if (p->total > 0 && !publish) {
+            hipLaunchKernelGGL(k_copy_segments, dim3((p->max_count + CPY_PER_BLOCK - 1) / CPY_PER_BLOCK, G), dim3(256), 0,
+                               st, p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
+                               p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(),
+                               sched_node ? p->d_sched_node.as<int32_t>() : nullptr);
+            CA_HIP_CHECK(hipGetLastError());
+        }
+        CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_COMPACT], st));
+        CA_HIP_CHECK(hipEventSynchronize(p->ev_rb));
         float ms = 0;
         (void)hipEventElapsedTime(&ms, p->ev[ca_estimate_plan::EV_CHAIN0], p->ev[ca_estimate_plan::EV_CHAIN1]);
         chain_ms += ms;
@@ -2042,15 +2181,8 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         }
         if (rounds > G + 2) { set_last_error("estimate speculation did not converge"); return CA_EDEVICE; }
     }
-    // results: the chains wrote single placements directly; fill the run placements
-    if (p->total > 0 && !publish) {
-        hipLaunchKernelGGL(k_copy_segments, dim3((p->max_count + CPY_PER_BLOCK - 1) / CPY_PER_BLOCK, G), dim3(256), 0, st,
-                           p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
-                           p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(),
-                           sched_node ? p->d_sched_node.as<int32_t>() : nullptr);
-        CA_HIP_CHECK(hipGetLastError());
-    }
-    CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_COMPACT], st));
+    // results: the chains wrote single placements directly, the last round's
+    // k_copy_segments the run placements (or the publisher, into the caller's buffer)
     if (publish) {
         // the publisher of the last round wrote the results; a deadline hit (a chain that
         // died) falls back to the device copy + D2H
@@ -2061,8 +2193,9 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                st, p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
                                p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), nullptr);
             CA_HIP_CHECK(hipGetLastError());
-            CA_HIP_CHECK(hipMemcpyAsync(sched_pod, p->d_sched_pod.ptr, sizeof(int32_t) * std::max(p->total, 0),
-                                        hipMemcpyDeviceToHost, st));
+            if (to_host)
+                CA_HIP_CHECK(hipMemcpyAsync(sched_pod, p->d_sched_pod.ptr, sizeof(int32_t) * std::max(p->total, 0),
+                                            hipMemcpyDeviceToHost, st));
         }
     } else if (to_host) {
         CA_HIP_CHECK(hipMemcpyAsync(sched_pod, p->d_sched_pod.ptr, sizeof(int32_t) * std::max(p->total, 0),

@@ -415,6 +415,12 @@ class EstimatePlan:
                 "lin_sensitive": sens.value, "had_success": succ.value,
                 "phases": {k: float(v) for k, v in zip(names, t)}}
 
+    def chain_info(self) -> tuple:
+        """(lastIndex-sensitive, had a FitsAnyNode success) of the last run: one call."""
+        sens, succ = C.c_int32(0), C.c_int32(0)
+        self.lib.ca_estimate_plan_chain_info(self.h, C.byref(sens), C.byref(succ))
+        return sens.value, succ.value
+
     def group_ticks(self) -> np.ndarray:
         """Per group of the last run: (chain device time in us, single-pod steps)."""
         n = self.lib.ca_estimate_plan_group_ticks(self.h, None, 0)

@@ -201,18 +201,18 @@ def main():
             out = plan.run(w.max_nodes, lin, want_nodes=True, copy=False)
         else:
             out = plan.run(w.max_nodes, lin, copy=False, device_results=True)
-        st = plan.stats()
-        return (out, st), out.last_index, st["lin_sensitive"], st["had_success"]
+        sens, succ = plan.chain_info()
+        return out, out.last_index, sens, succ
 
     gather = shard.torch_all_gather(dist, f"cuda:{local}") if dist is not None else None
 
     def step():
         """One batch on this rank + the lastIndex chain across ranks (autoscaler_amd/shard.py)."""
         if dist is None:
-            (out, st), _, _, _ = run_block(L0)
-            return out, st, 0
-        (out, st), _, extra = shard.run_sharded(run_block, L0, gather, rank)
-        return out, st, extra
+            out = run_block(L0)[0]
+            return out, 0
+        out, _, extra = shard.run_sharded(run_block, L0, gather, rank)
+        return out, extra
 
     for _ in range(args.warmup):
         step()
@@ -221,23 +221,27 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     evals = 0
-    chain_ms = []
-    sort_ms = []
-    rounds = []
-    phases = []
+    extras = []
     for _ in range(args.steps):
-        out, st, extra = step()
+        out, extra = step()
         evals += int(out.results["evals"].sum())
-        chain_ms.append(st["chain_ms"] / max(st["rounds"], 1))
-        sort_ms.append(st["sort_ms"])
-        rounds.append(st["rounds"] + extra)
-        ph = dict(st["phases"])
-        ph["chain_ms"] = ph["chain_ms"] / max(st["rounds"], 1)       # one launch
-        phases.append(ph)
+        extras.append(extra)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # per-phase device times: the same steps again, untimed (reading them is host work
+    # that is not part of Estimate)
+    chain_ms, sort_ms, rounds, phases = [], [], [], []
+    for i in range(args.steps):
+        step()
+        st = plan.stats()
+        chain_ms.append(st["chain_ms"] / max(st["rounds"], 1))
+        sort_ms.append(st["sort_ms"])
+        rounds.append(st["rounds"] + extras[i])
+        ph = dict(st["phases"])
+        ph["chain_ms"] = ph["chain_ms"] / max(st["rounds"], 1)       # one launch
+        phases.append(ph)
     if dist is not None:
         t = torch.tensor([elapsed, float(evals)], dtype=torch.float64, device=f"cuda:{local}")
         tmax = t.clone()

@@ -205,6 +205,39 @@ def test_estimate_runs_random(seed, batch, nodes, oracle, monkeypatch):
     assert o.last_index == g.last_index
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_estimate_heavy_first_split(seed, oracle, monkeypatch):
+    """G >= 8 groups: the heavy groups sort and chain first on the main stream, the rest
+    on a second stream (plan map rebuilt when max_nodes changes); identical to the oracle
+    with and without the split, with and without node ordinals."""
+    rng, nodes, pods, templates, groups = _run_heavy_inputs(seed, n_groups=16)
+    table, node_recs, tm, off, pod_idx = _encode_estimate(nodes, pods, templates, groups)
+    o = oracle.OracleState()
+    m = _mirror()
+    for b in (o, m):
+        b.clear()
+        if len(node_recs):
+            b.add_nodes(node_recs)
+    for split in ("1", "0"):
+        if split == "0":
+            monkeypatch.setenv("CASIM_NO_SPLIT", "1")
+        with native.EstimatePlan(m, table, off, pod_idx, tm) as plan:
+            for max_nodes in (rng.choice([0, 3, 40]), rng.choice([1, 5, 100])):
+                L0 = rng.choice([0, 1, 7, 123])
+                ro = o.estimate(table, off, pod_idx, tm, max_nodes, L0)
+                for want in (True, False):
+                    g = plan.run(max_nodes, L0, want_nodes=want)
+                    assert np.array_equal(ro.results, g.results), (seed, split, max_nodes, want)
+                    assert ro.last_index == g.last_index
+                    for k in range(len(groups)):
+                        if int(ro.results[k]["status"]) != 0:
+                            continue
+                        a, n = off[k], int(ro.results[k]["n_scheduled"])
+                        assert np.array_equal(ro.sched_pod[a:a + n], g.sched_pod[a:a + n]), (seed, k)
+                        if want:
+                            assert np.array_equal(ro.sched_node[a:a + n], g.sched_node[a:a + n]), (seed, k)
+
+
 @pytest.mark.parametrize("name,w", [
     ("C1", W.c1()),
     ("C2-small", W.c2(n_pods=4000, n_groups=12, n_existing=50)),

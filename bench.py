@@ -270,7 +270,8 @@ def main():
         for name in PHASE_KERNEL[dom].split("+")[:1]:
             rec = tj.get("kernels", {}).get(f"casim::{name}")
             if rec:
-                traffic = rec["traffic_bytes_per_launch"]
+                # the phase's launches of one step together (heavy + light chain launches)
+                traffic = rec.get("traffic_bytes_per_step", rec["traffic_bytes_per_launch"])
                 traffic_src = f"profiles/pmc_traffic.json ({tj.get('source', '')})"
 
     # PCIe-inclusive: the same step with the scheduled pods streamed to the host
@@ -351,7 +352,8 @@ def main():
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per launch",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "traffic_unit": "HBM bytes per step of the phase (all its launches)",
                 "traffic_source": traffic_src,
                 "kernel": PHASE_KERNEL[dom], "kernel_ms": kernel_ms,
                 "bytes_per_unit": per_item, "unit_of_work": "(pod, node group) item",

@@ -30,11 +30,11 @@ fi
 if [[ "$STEP" == pmc ]]; then
   # HBM traffic: one counter per pass (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950)
   for c in FETCH_SIZE WRITE_SIZE; do
-    cd /tmp && timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$c" -o run \
-       --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-sweep --no-c4 \
+    cd /tmp && PMC_STEPS=3 timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$c" -o run \
+       --output-format csv -- python3 "$GRAFT_REPO_ROOT/scripts/pmc_step.py" \
        > "$GRAFT_REPO_ROOT/gpurun_out/pmc_$c.log" 2>&1 || { echo "PMC $c FAILED"; tail -20 "$GRAFT_REPO_ROOT/gpurun_out/pmc_$c.log"; exit 1; }
   done
   cd "$GRAFT_REPO_ROOT"
-  python3 scripts/pmc_traffic.py gpurun_out > gpurun_out/pmc_traffic.json && cat gpurun_out/pmc_traffic.json
+  python3 scripts/pmc_traffic.py gpurun_out 3 > gpurun_out/pmc_traffic.json && cat gpurun_out/pmc_traffic.json
 fi
 echo ROUND_OK

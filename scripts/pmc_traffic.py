@@ -23,7 +23,7 @@ def load(root: str, counter: str) -> dict:
     return out
 
 
-def main(root: str) -> None:
+def main(root: str, steps: int) -> None:
     fetch = load(root, "FETCH_SIZE")
     write = load(root, "WRITE_SIZE")
     res = {}
@@ -32,13 +32,17 @@ def main(root: str) -> None:
         w = write.get(name, [])
         fk = sum(f) / len(f) * 1024 * 2 if f else None     # KB -> bytes, x2 gfx950 read correction
         wk = sum(w) / len(w) * 1024 if w else None
-        res[name] = {"launches": max(len(f), len(w)), "read_bytes_per_launch": fk, "write_bytes_per_launch": wk,
-                     "traffic_bytes_per_launch": (fk or 0) + (wk or 0)}
-    json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes over "
-                         "bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-sweep --no-c4; "
-                         "FETCH_SIZE x2 (gfx950 wide-read correction)", "kernels": res}, sys.stdout, indent=1)
+        n = max(len(f), len(w))
+        res[name] = {"launches": n, "launches_per_step": n / steps,
+                     "read_bytes_per_launch": fk, "write_bytes_per_launch": wk,
+                     "traffic_bytes_per_launch": (fk or 0) + (wk or 0),
+                     "traffic_bytes_per_step": ((fk or 0) + (wk or 0)) * n / steps}
+    json.dump({"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes over "
+                         f"scripts/pmc_step.py ({steps} C2 Estimate steps, results in HBM); "
+                         "FETCH_SIZE x2 (gfx950 wide-read correction)", "steps": steps, "kernels": res},
+              sys.stdout, indent=1)
     print()
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out")
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out", int(sys.argv[2]) if len(sys.argv) > 2 else 3)

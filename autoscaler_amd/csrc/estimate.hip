@@ -1749,6 +1749,7 @@ struct ca_estimate_plan {
     hipEvent_t ev_init = nullptr, ev_b = nullptr, ev_rb = nullptr;
     DevBuf d_gmap;
     int32_t map_max_nodes = -1, n_heavy = 0;
+    int32_t map_source = 0;        // 1: demand model, 2: the chains' measured times (previous run)
     ~ca_estimate_plan() {
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (ev_go) (void)hipEventDestroy(ev_go);
@@ -1952,27 +1953,43 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     const int32_t* gmapA = nullptr;
     const int32_t* gmapB = nullptr;
     if (p->total > 0 && p->bucket && G >= 8 && !getenv("CASIM_NO_SPLIT")) {
+        // The heavy set: groups whose chain cost is within 60% of the largest, if that is
+        // at most half the batch (a flat distribution gains nothing from the split).
+        // First from the demand model, then once from the chain times the previous run
+        // measured (ChainOut ticks) with the same max_nodes — a scheduling choice only:
+        // every run computes everything.
+        auto build_map = [&](const std::vector<double>& cost) -> int {
+            double cmax = 0;
+            for (int32_t g = 0; g < G; g++) cmax = std::max(cmax, cost[g]);
+            std::vector<int32_t> map;
+            map.reserve(G);
+            for (int32_t g = 0; g < G; g++) if (cmax > 0 && cost[g] >= 0.6 * cmax) map.push_back(g);
+            p->n_heavy = (int32_t)map.size() * 2 <= G ? (int32_t)map.size() : 0;
+            for (int32_t g = 0; g < G; g++) if (!(cmax > 0 && cost[g] >= 0.6 * cmax)) map.push_back(g);
+            int rc;
+            if ((rc = p->d_gmap.reserve(sizeof(int32_t) * (size_t)G)) != CA_OK) return rc;
+            CA_HIP_CHECK(hipMemcpy(p->d_gmap.ptr, map.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice));
+            return CA_OK;
+        };
+        int rc;
         if (p->map_max_nodes != lim->max_nodes) {
             // chain length ~ the template copies a group opens over the runs it gets
             // through: `demand` below the limiter's cap, cap^2/demand above it (the
             // limiter stops the group after ~cap/demand of its pods)
             const double M = lim->max_nodes > 0 ? (double)lim->max_nodes : 0.0;
             std::vector<double> cost(G);
-            double cmax = 0;
             for (int32_t g = 0; g < G; g++) {
                 const double d = p->demand[g];
                 cost[g] = (M > 0 && d > M) ? M * M / d : d;
-                cmax = std::max(cmax, cost[g]);
             }
-            std::vector<int32_t> map;
-            map.reserve(G);
-            for (int32_t g = 0; g < G; g++) if (cmax > 0 && cost[g] >= 0.7 * cmax) map.push_back(g);
-            p->n_heavy = (int32_t)map.size();
-            for (int32_t g = 0; g < G; g++) if (!(cmax > 0 && cost[g] >= 0.7 * cmax)) map.push_back(g);
-            int rc;
-            if ((rc = p->d_gmap.reserve(sizeof(int32_t) * (size_t)G)) != CA_OK) return rc;
-            CA_HIP_CHECK(hipMemcpy(p->d_gmap.ptr, map.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice));
+            if ((rc = build_map(cost)) != CA_OK) return rc;
             p->map_max_nodes = lim->max_nodes;
+            p->map_source = 1;
+        } else if (p->map_source == 1 && (int32_t)p->diag.size() == G) {
+            std::vector<double> cost(G);
+            for (int32_t g = 0; g < G; g++) cost[g] = (double)(uint32_t)(p->diag[g] & 0xFFFFFFFFull);
+            if ((rc = build_map(cost)) != CA_OK) return rc;
+            p->map_source = 2;
         }
         split = p->n_heavy > 0 && p->n_heavy < G;
         gmapA = p->d_gmap.as<int32_t>();

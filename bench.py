@@ -96,16 +96,16 @@ def c4_leg(args, device: int, with_cpu: bool) -> dict:
                        f"{int(w.group_off[-1])} (pod, group) items"}
     with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as plan:
         for _ in range(2):
-            plan.run(w.max_nodes, 0, want_nodes=False, copy=False)
+            plan.run(w.max_nodes, 0, copy=False, device_results=True)
         ts = []
         for _ in range(max(args.steps, 5)):
             t = time.perf_counter()
-            r = plan.run(w.max_nodes, 0, want_nodes=False, copy=False)
+            r = plan.run(w.max_nodes, 0, copy=False, device_results=True)     # results in HBM, as the C2 line
             ts.append(time.perf_counter() - t)
         ms = float(np.median(ts) * 1e3)
         evals = int(r.results["evals"].sum())
         out.update({"estimate_ms": ms, "evals": evals, "evals_per_s": evals / (ms / 1e3)})
-        res, sp = r.results.copy(), r.sched_pod.copy()
+        res, sp = r.results.copy(), plan.fetch()
     if with_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle                                           # CPU baseline leg only

@@ -1124,6 +1124,9 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                         int64_t S = 0;
                         int64_t lv_cmin = 0;      // revolution 1: fewest copies among rows with room
                         int32_t lv_s = 0;         // ... and how many of them lie before j0
+                        // blocks of this wave's row range whose copy counts were computed
+                        // (bit i: rows [lo + 64 i, +64)); every other row has no room
+                        uint64_t adm_w = 0;
                         if (exhausted) {
                             PROF_T(t_ex);
                             const NodeRec rl_ = R[last_node];
@@ -1155,16 +1158,30 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                             };
                             const bool fast = rem <= (1 << 20);
                             if (fast) {
-                                for (int32_t b = lo; b < hi; b += 128) {       // two rows in flight
+                                // Block skip: a row has room for a copy iff the pod fits it
+                                // (rec_fits: compares only), so the float64 copy counts run
+                                // only for 64-row blocks where some row fits — in FFD most rows
+                                // are full for most later pods (C2: ~5% of rows have room per
+                                // pass).  The placement-list path (node ordinals) reads every
+                                // row's count, so it computes them all.  Two blocks in flight.
+                                const bool all = so_node != nullptr;
+                                for (int32_t b = lo; b < hi; b += 128) {
                                     const int32_t j = b + lane;
                                     const bool in0 = j < hi, in1 = j + 64 < hi;
                                     const NodeRec r0 = R[in0 ? j : 0], r1 = R[in1 ? j + 64 : 0];
-                                    const int32_t c0 = rec_copies_run(r0, dv, zero, rem);
-                                    const int32_t c1 = rec_copies_run(r1, dv, zero, rem);
-                                    s32 += acc(b, c0, in0);
-                                    s32 += acc(b + 64, c1, in1);
+                                    const uint64_t f0 = __ballot(in0 && (all || rec_fits(r0, pcpu, pmem, peph, zero)));
+                                    const uint64_t f1 = __ballot(in1 && (all || rec_fits(r1, pcpu, pmem, peph, zero)));
+                                    if (f0) {
+                                        adm_w |= 1ull << ((b - lo) >> 6);
+                                        s32 += acc(b, rec_copies_run(r0, dv, zero, rem), in0);
+                                    }
+                                    if (f1) {
+                                        adm_w |= 1ull << ((b + 64 - lo) >> 6);
+                                        s32 += acc(b + 64, rec_copies_run(r1, dv, zero, rem), in1);
+                                    }
                                 }
                             } else {
+                                adm_w = ~0ull;
                                 for (int32_t b = lo; b < hi; b += 64) {
                                     const int32_t j = b + lane;
                                     const bool in = j < hi;
@@ -1233,6 +1250,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                                         int32_t lo, hi;
                                         wave_rows(k, wv, lo, hi);
                                         for (int32_t b = lo; b < hi; b += 64) {
+                                            if (!((adm_w >> ((b - lo) >> 6)) & 1ull)) continue;
                                             const int32_t j = b + lane;
                                             const uint64_t bm = __ballot(j < hi && CAPA[j] >= r);
                                             const int32_t pc = __builtin_popcountll(bm);
@@ -1258,6 +1276,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                                 wave_rows(k, wv, lo, hi);
                                 int32_t cnt_w = 0, lt2 = 0, cm2 = INT32_MAX;
                                 for (int32_t b = lo; b < hi; b += 64) {
+                                    if (!((adm_w >> ((b - lo) >> 6)) & 1ull)) continue;
                                     const int32_t j = b + lane;
                                     const int32_t c = j < hi ? CAPA[j] : 0;
                                     const bool q = c >= r;
@@ -1343,19 +1362,25 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                             int32_t rl = last - j0;
                             if (rl < 0) rl += k;
                             evals += (uint64_t)(r - 1) * (uint64_t)k + (uint64_t)rl + 1;
-                            for (int32_t j = tid; j < k; j += CT) {     // rows owned per thread: no conflicts
-                                const int32_t c = CAPA[j];
-                                int32_t rj = j - j0;
-                                if (rj < 0) rj += k;
-                                const int32_t nj = min(c, r - 1) + ((c >= r && rj <= rl) ? 1 : 0);
-                                if (nj > 0) {
-                                    NodeRec q = R[j];
-                                    q.cpu -= (int64_t)nj * pcpu;
-                                    q.mem -= (int64_t)nj * pmem;
-                                    q.eph -= (int64_t)nj * peph;
-                                    q.pods -= nj;
-                                    q.used = 1;
-                                    R[j] = q;
+                            {   // the wave's own rows, blocks with counts only (others: no room)
+                                int32_t lo, hi;
+                                wave_rows(k, wv, lo, hi);
+                                for (int32_t b = lo; b < hi; b += 64) {
+                                    if (!((adm_w >> ((b - lo) >> 6)) & 1ull)) continue;
+                                    const int32_t j = b + lane;
+                                    const int32_t c = j < hi ? CAPA[j] : 0;
+                                    int32_t rj = j - j0;
+                                    if (rj < 0) rj += k;
+                                    const int32_t nj = min(c, r - 1) + ((c >= r && rj <= rl) ? 1 : 0);
+                                    if (nj > 0) {
+                                        NodeRec q = R[j];
+                                        q.cpu -= (int64_t)nj * pcpu;
+                                        q.mem -= (int64_t)nj * pmem;
+                                        q.eph -= (int64_t)nj * peph;
+                                        q.pods -= nj;
+                                        q.used = 1;
+                                        R[j] = q;
+                                    }
                                 }
                             }
                             PROF_ADD(3, t_up);

@@ -699,28 +699,24 @@ __device__ inline int32_t rec_copies(const NodeRec& r, int64_t pcpu, int64_t pme
     return c;
 }
 
-// rec_copies for the rows of one run: the pod's reciprocals are computed once, each
-// quotient comes from float32 (rel. error < 2^-21, so within one of floor(free/req)
-// while the cap is <= 2^20) and one multiply-compare step each way makes it exact.
+// rec_copies for the rows of one run: the pod's requests and reciprocals in float64,
+// computed once per run.  Exact while every free value and request is below 2^53 (a
+// template copy's free values bound every row of its group; checked once per run);
+// otherwise the exact integer rec_copies.
 struct RunDiv {
-    int64_t req[3];
-    float rcp[3];
     double reqd[3], rcpd[3];
-    bool f64;          // every free value and request < 2^53: the float64 path is exact
+    bool f64;
 };
-// `bound` = the largest free value a row of the group can hold (the template copy's:
-// rows only lose resources), so one uniform test decides the path for every row.
 __device__ inline RunDiv run_div(int64_t pcpu, int64_t pmem, int64_t peph, int64_t bound) {
     RunDiv d;
-    d.req[0] = pcpu; d.req[1] = pmem; d.req[2] = peph;
-    // req == 0: rcp = +inf, so the float quotient is inf (or NaN for free == 0) and
-    // fminf(., cap) gives cap — a zero request passes whenever free >= 0
-    for (int i = 0; i < 3; i++) d.rcp[i] = d.req[i] > 0 ? 1.0f / (float)d.req[i] : __builtin_inff();
     constexpr int64_t E53 = 1ll << 53;
     d.f64 = bound < E53 && pcpu < E53 && pmem < E53 && peph < E53;
+    const int64_t req[3] = {pcpu, pmem, peph};
     for (int i = 0; i < 3; i++) {
-        d.reqd[i] = (double)d.req[i];
-        d.rcpd[i] = d.req[i] > 0 ? 1.0 / d.reqd[i] : __builtin_inf();
+        d.reqd[i] = (double)req[i];
+        // req == 0: rcp = +inf, the quotient inf (NaN for free == 0) and fmin(., cap)
+        // gives cap — a zero request passes whenever free >= 0
+        d.rcpd[i] = req[i] > 0 ? 1.0 / d.reqd[i] : __builtin_inf();
     }
     return d;
 }
@@ -737,30 +733,18 @@ __device__ inline int32_t dim_copies_f64(int64_t free_, double rd, double rcpd, 
     q -= (t < 0.0) ? 1.0 : 0.0;
     return free_ < 0 ? 0 : (int32_t)q;
 }
-// branch-free (no exec-mask juggling in the row loop)
-__device__ inline int32_t dim_copies_fast(int64_t free_, int64_t req, float rcp, int32_t cap) {
-    const uint64_t f = free_ < 0 ? 0ull : (uint64_t)free_, r = (uint64_t)req;
-    const float ff = (float)(uint32_t)(f >> 32) * 4294967296.0f + (float)(uint32_t)f;
-    uint32_t q = (uint32_t)fminf(ff * rcp, (float)cap);
-    const bool dn = (uint64_t)q * r > f;
-    const bool up = !dn && q < (uint32_t)cap && (uint64_t)(q + 1) * r <= f;
-    q = q - (dn ? 1u : 0u) + (up ? 1u : 0u);
-    return free_ < 0 ? 0 : (int32_t)q;
-}
-__device__ inline int32_t rec_copies_run(const NodeRec& r, const RunDiv& d, bool zero, int32_t cap) {
+__device__ inline int32_t rec_copies_run(const NodeRec& r, const RunDiv& d, bool zero, int32_t cap,
+                                         int64_t pcpu, int64_t pmem, int64_t peph) {
+    if (!d.f64) return rec_copies(r, pcpu, pmem, peph, zero, cap);     // uniform
     int32_t c = max(0, min(r.pods, cap));
-    if (!zero && d.f64) {     // uniform
+    if (!zero) {     // uniform
         // independent per-dimension quotients (capped at the same c, min taken after);
         // a zero request only needs free >= 0 (uniform skip of the division)
         const int32_t cp = max(c, 1);
-        const int32_t q0 = d.req[0] ? dim_copies_f64(r.cpu, d.reqd[0], d.rcpd[0], cp) : (r.cpu < 0 ? 0 : cp);
-        const int32_t q1 = d.req[1] ? dim_copies_f64(r.mem, d.reqd[1], d.rcpd[1], cp) : (r.mem < 0 ? 0 : cp);
-        const int32_t q2 = d.req[2] ? dim_copies_f64(r.eph, d.reqd[2], d.rcpd[2], cp) : (r.eph < 0 ? 0 : cp);
+        const int32_t q0 = d.reqd[0] != 0.0 ? dim_copies_f64(r.cpu, d.reqd[0], d.rcpd[0], cp) : (r.cpu < 0 ? 0 : cp);
+        const int32_t q1 = d.reqd[1] != 0.0 ? dim_copies_f64(r.mem, d.reqd[1], d.rcpd[1], cp) : (r.mem < 0 ? 0 : cp);
+        const int32_t q2 = d.reqd[2] != 0.0 ? dim_copies_f64(r.eph, d.reqd[2], d.rcpd[2], cp) : (r.eph < 0 ? 0 : cp);
         c = min(c, min(q0, min(q1, q2)));
-    } else if (!zero) {
-        c = min(c, dim_copies_fast(r.cpu, d.req[0], d.rcp[0], max(c, 1)));
-        c = min(c, dim_copies_fast(r.mem, d.req[1], d.rcp[1], max(c, 1)));
-        c = min(c, dim_copies_fast(r.eph, d.req[2], d.rcp[2], max(c, 1)));
     }
     return c;
 }
@@ -1130,7 +1114,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                         if (exhausted) {
                             PROF_T(t_ex);
                             const NodeRec rl_ = R[last_node];
-                            const int32_t c = rem <= (1 << 20) ? rec_copies_run(rl_, dv, zero, rem)
+                            const int32_t c = rem <= (1 << 20) ? rec_copies_run(rl_, dv, zero, rem, pcpu, pmem, peph)
                                                                : rec_copies(rl_, pcpu, pmem, peph, zero, rem);
                             lds_barrier();    // every wave has read the row before it changes
                             if (c > 0) { one = last_node; n_one = c; nalive = 1; }
@@ -1173,11 +1157,11 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                                     const uint64_t f1 = __ballot(in1 && (all || rec_fits(r1, pcpu, pmem, peph, zero)));
                                     if (f0) {
                                         adm_w |= 1ull << ((b - lo) >> 6);
-                                        s32 += acc(b, rec_copies_run(r0, dv, zero, rem), in0);
+                                        s32 += acc(b, rec_copies_run(r0, dv, zero, rem, pcpu, pmem, peph), in0);
                                     }
                                     if (f1) {
                                         adm_w |= 1ull << ((b + 64 - lo) >> 6);
-                                        s32 += acc(b + 64, rec_copies_run(r1, dv, zero, rem), in1);
+                                        s32 += acc(b + 64, rec_copies_run(r1, dv, zero, rem, pcpu, pmem, peph), in1);
                                     }
                                 }
                             } else {
@@ -1439,7 +1423,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                     // and takes one limiter grant.  Closed form over n_open nodes.
                     PROF_T(t_op);
                     const int32_t ct = !(sf & SF_FA_OK) ? 1
-                                       : rem2 <= (1 << 20) ? rec_copies_run(trec, dv, zero, rem2)
+                                       : rem2 <= (1 << 20) ? rec_copies_run(trec, dv, zero, rem2, pcpu, pmem, peph)
                                                            : rec_copies(trec, pcpu, pmem, peph, zero, rem2);
                     int32_t n_open = (rem2 + ct - 1) / ct;
                     if (max_nodes > 0) n_open = min(n_open, 1 + (max_nodes - granted));

@@ -132,6 +132,9 @@ class PredResultC(C.Structure):
     _fields_ = [("type", C.c_int32), ("plugin", C.c_int32), ("reasons", C.c_uint32), ("taint", C.c_int32)]
 
 
+PRED_RESULT_DTYPE = np.dtype([("type", np.int32), ("plugin", np.int32), ("reasons", np.uint32), ("taint", np.int32)])
+
+
 class LimiterC(C.Structure):
     _fields_ = [("max_nodes", C.c_int32), ("reserved", C.c_int32)]
 

@@ -329,6 +329,41 @@ __global__ void k_check_one(const NodeHot* __restrict__ hot, const NodeExt* __re
     *out = r;
 }
 
+// ComputeExpansionOption's check (orchestrator.go:455-481) for every (node group, pod
+// equivalence group): CheckPredicates(sample pod, fresh copy of the group's template)
+// with the reference's result (schedulerbased.go:139-185; the PreFilter failure is an
+// internal error).  One thread per (template, sample); templates on the grid's y axis.
+__global__ void __launch_bounds__(256) k_check_templates(
+    const NodeHot* __restrict__ thot, const NodeExt* __restrict__ text, const NodeStatic* __restrict__ tst,
+    const int32_t* __restrict__ samples, int32_t n_samples, const PodHot* __restrict__ ph,
+    const ca_pod_spec* __restrict__ specs, const ca_selector_term* __restrict__ terms,
+    const ca_selector_req* __restrict__ reqs, ca_pred_result* __restrict__ out, uint8_t* __restrict__ out_ok) {
+    const int32_t e = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int32_t g = (int32_t)blockIdx.y;
+    if (e >= n_samples) return;
+    const PodHot p = ph[samples[e]];
+    ca_pred_result r;
+    r.type = CA_PRED_OK; r.plugin = 0; r.reasons = 0; r.taint = 0;
+    if (p.flags & PF_PREFILTER_FAIL) {
+        r.type = CA_PRED_INTERNAL;
+        r.plugin = CA_PLUGIN_NODE_AFFINITY;
+    } else {
+        uint32_t reasons = 0;
+        const int plugin = dev_full_filters(specs[p.spec], p, terms, reqs, thot[g], text + g, tst + g, true, &reasons);
+        if (plugin != CA_PLUGIN_NONE) {
+            r.type = CA_PRED_NOT_SCHEDULABLE;
+            r.plugin = plugin;
+            r.reasons = reasons;
+            if (plugin == CA_PLUGIN_TAINT_TOLERATION) {
+                const uint64_t u = tst[g].taints & ~specs[p.spec].tolerated_taints;
+                r.taint = (int32_t)__builtin_ctzll(u);
+            }
+        }
+    }
+    if (out) out[(size_t)g * n_samples + e] = r;
+    if (out_ok) out_ok[(size_t)g * n_samples + e] = r.type == CA_PRED_OK ? 1 : 0;
+}
+
 // Dense pods x nodes feasibility (CheckPredicates semantics, PreFilter failure -> 0).
 // One thread per (pod, node); nodes on the fast axis for coalesced node rows.
 __global__ void __launch_bounds__(256) k_fits_matrix(
@@ -786,6 +821,73 @@ int ca_fits_matrix(ca_mirror* m, const ca_podset* s, uint8_t* out) {
                        P, m->d_scratch2.as<uint8_t>());
     CA_HIP_CHECK(hipGetLastError());
     CA_HIP_CHECK(hipMemcpyAsync(out, m->d_scratch2.ptr, bytes, hipMemcpyDeviceToHost, m->stream));
+    CA_HIP_CHECK(hipStreamSynchronize(m->stream));
+    return CA_OK;
+}
+
+int ca_check_templates(ca_mirror* m, const ca_podset* s, const int32_t* samples, int32_t n_samples,
+                       const ca_template* templates, int32_t n_templates, ca_pred_result* out, uint8_t* out_ok) {
+    if (!m || !s || n_samples < 0 || n_templates < 0) return CA_EINVAL;
+    if (n_samples == 0 || n_templates == 0) return CA_OK;
+    if (!samples || !templates || (!out && !out_ok)) return CA_EINVAL;
+    for (int32_t e = 0; e < n_samples; e++)
+        if (samples[e] < 0 || samples[e] >= s->t.n_pods) return CA_EINVAL;
+    CA_HIP_CHECK(hipSetDevice(m->device));
+    // the test node: the template with its pods (NodeInfo of a fresh template copy)
+    std::vector<NodeHot> h(n_templates);
+    std::vector<NodeExt> x(n_templates);
+    std::vector<NodeStatic> st(n_templates);
+    for (int32_t g = 0; g < n_templates; g++) {
+        const ca_template& tp = templates[g];
+        const ca_node_spec& n = tp.node;
+        h[g].cpu = wsub(n.alloc_milli_cpu, tp.used_milli_cpu);
+        h[g].mem = wsub(n.alloc_memory, tp.used_memory);
+        h[g].eph = wsub(n.alloc_ephemeral, tp.used_ephemeral);
+        h[g].pods = clamp_i32(n.alloc_pods - tp.used_pods);
+        uint32_t f = NF_VALID;
+        if (n.flags & CA_NODE_UNSCHEDULABLE) f |= NF_UNSCHED;
+        if (n.taints) f |= NF_TAINTS;
+        bool ports = false, sc = false;
+        for (int w = 0; w < CA_PORT_WORDS; w++) { x[g].ports[w] = tp.used_ports[w]; ports |= tp.used_ports[w] != 0; }
+        for (int k = 0; k < CA_MAX_SCALAR; k++) {
+            x[g].scalar[k] = wsub(n.alloc_scalar[k], tp.used_scalar[k]);
+            sc |= n.alloc_scalar[k] != 0 || tp.used_scalar[k] != 0;
+        }
+        if (ports) f |= NF_PORTS;
+        if (sc) f |= NF_SCALAR;
+        h[g].flags = f;
+        std::memset(&st[g], 0, sizeof st[g]);
+        st[g].taints = n.taints;
+        for (int w = 0; w < CA_LABEL_WORDS; w++) st[g].labels[w] = n.label_pairs[w];
+        st[g].keys = n.label_keys;
+        for (int k = 0; k < CA_MAX_INT_KEYS; k++) st[g].ints[k] = n.int_label[k];
+        st[g].int_valid = n.int_label_valid;
+        st[g].name_id = n.name_id;
+    }
+    const size_t nh = sizeof(NodeHot) * n_templates, nx = sizeof(NodeExt) * n_templates,
+                 ns = sizeof(NodeStatic) * n_templates, nsm = sizeof(int32_t) * n_samples,
+                 no = out ? sizeof(ca_pred_result) * (size_t)n_templates * (size_t)n_samples : 0,
+                 nok = out_ok ? (size_t)n_templates * (size_t)n_samples : 0;
+    int rc;
+    if ((rc = m->d_scratch2.reserve(nh + nx + ns + nsm + no + nok + 64)) != CA_OK) return rc;
+    char* base = m->d_scratch2.as<char>();
+    NodeHot* dh = reinterpret_cast<NodeHot*>(base);
+    NodeExt* dx = reinterpret_cast<NodeExt*>(base + nh);
+    NodeStatic* ds = reinterpret_cast<NodeStatic*>(base + nh + nx);
+    int32_t* dsm = reinterpret_cast<int32_t*>(base + nh + nx + ns);
+    const size_t o_out = (nh + nx + ns + nsm + 15) & ~size_t(15);
+    ca_pred_result* dout = out ? reinterpret_cast<ca_pred_result*>(base + o_out) : nullptr;
+    uint8_t* dok = out_ok ? reinterpret_cast<uint8_t*>(base + o_out + no) : nullptr;
+    CA_HIP_CHECK(hipMemcpyAsync(dh, h.data(), nh, hipMemcpyHostToDevice, m->stream));
+    CA_HIP_CHECK(hipMemcpyAsync(dx, x.data(), nx, hipMemcpyHostToDevice, m->stream));
+    CA_HIP_CHECK(hipMemcpyAsync(ds, st.data(), ns, hipMemcpyHostToDevice, m->stream));
+    CA_HIP_CHECK(hipMemcpyAsync(dsm, samples, nsm, hipMemcpyHostToDevice, m->stream));
+    hipLaunchKernelGGL(k_check_templates, dim3((n_samples + 255) / 256, n_templates), dim3(256), 0, m->stream,
+                       dh, dx, ds, dsm, n_samples, s->t.hot.as<PodHot>(), s->t.spec.as<ca_pod_spec>(),
+                       s->t.terms.as<ca_selector_term>(), s->t.reqs.as<ca_selector_req>(), dout, dok);
+    CA_HIP_CHECK(hipGetLastError());
+    if (out) CA_HIP_CHECK(hipMemcpyAsync(out, dout, no, hipMemcpyDeviceToHost, m->stream));
+    if (out_ok) CA_HIP_CHECK(hipMemcpyAsync(out_ok, dok, nok, hipMemcpyDeviceToHost, m->stream));
     CA_HIP_CHECK(hipStreamSynchronize(m->stream));
     return CA_OK;
 }

@@ -66,6 +66,7 @@ def load() -> C.CDLL:
         "ca_fits_any_node": ([vp, vp, i32, vp, p(i32), p(i32), p(i32), p(C.c_uint64)], C.c_int),
         "ca_check_predicates": ([vp, vp, i32, i32, vp], C.c_int),
         "ca_fits_matrix": ([vp, vp, vp], C.c_int),
+        "ca_check_templates": ([vp, vp, vp, i32, vp, i32, vp, vp], C.c_int),
         "ca_estimate_batch": ([vp, vp, vp, vp, vp, i32, vp, p(i32), vp, vp, vp], C.c_int),
         "ca_estimate_plan_create": ([vp, vp, vp, vp, vp, i32, p(vp)], C.c_int),
         "ca_estimate_plan_run": ([vp, vp, p(i32), vp, vp, vp], C.c_int),
@@ -106,7 +107,7 @@ def exported_symbols() -> list[str]:
         "ca_mirror_destroy", "ca_mirror_clear", "ca_mirror_add_nodes", "ca_mirror_add_pods", "ca_mirror_remove_pod",
         "ca_mirror_fork", "ca_mirror_revert", "ca_mirror_commit", "ca_mirror_node_count", "ca_mirror_pod_node",
         "ca_mirror_node_pods", "ca_podset_create", "ca_podset_destroy", "ca_fits_any_node", "ca_check_predicates",
-        "ca_fits_matrix", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
+        "ca_fits_matrix", "ca_check_templates", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
         "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_estimate_plan_timings",
         "ca_estimate_plan_group_ticks", "ca_estimate_plan_fetch", "ca_estimate_plan_device_results",
         "ca_find_nodes_to_remove",
@@ -246,6 +247,30 @@ class Mirror:
         with EstimatePlan(self, table, group_off, pod_idx, templates) as plan:
             return plan.run(max_nodes, last_index, want_nodes=want_nodes)
 
+    def check_templates(self, table: abi.PodTable, samples, templates: np.ndarray, podset=None,
+                        verdict_only: bool = False, out=None) -> np.ndarray:
+        """ComputeExpansionOption's feasibility (orchestrator.go:455-481) for every (node
+        group, pod equivalence group): [G][E] ca_pred_result of CheckPredicates(sample pod,
+        a fresh copy of the template), or with verdict_only a [G][E] uint8 (1 = fits).
+        `podset`: a resident PodSet of `table` (else the table is uploaded for the call);
+        `out`: a caller buffer of the result shape (e.g. page-locked)."""
+        sm = np.ascontiguousarray(samples, dtype=np.int32)
+        tm = np.ascontiguousarray(templates, dtype=abi.TEMPLATE_DTYPE)
+        if out is None:
+            out = np.zeros((len(tm), len(sm)), np.uint8 if verdict_only else abi.PRED_RESULT_DTYPE)
+        own = podset is None
+        ps = PodSet(self, table) if own else podset
+        try:
+            full, ok = (None, out) if verdict_only else (out, None)
+            _check(self.lib.ca_check_templates(self.h, ps.h, ptr(sm), len(sm), ptr(tm), len(tm),
+                                               ptr(full) if full is not None else None,
+                                               ptr(ok) if ok is not None else None),
+                   "ca_check_templates")
+        finally:
+            if own:
+                ps.close()
+        return out
+
     # -- removal simulator ----------------------------------------------------
     def find_nodes_to_remove(self, candidates, dest_mask, cand_status, move_off, move_pods, hints,
                              last_index: int = 0) -> RemovalOutput:
@@ -349,6 +374,28 @@ class PinnedArray:
             self.array = None
             self.lib.ca_host_free(self.p)
             self.p = None
+
+
+class PodSet:
+    """A pod table resident in device memory (ca_podset): uploaded once, reused by calls."""
+
+    def __init__(self, mirror: "Mirror", table: abi.PodTable):
+        self.lib = mirror.lib
+        self.table = table                      # keeps the host arrays alive
+        h = C.c_void_p()
+        _check(self.lib.ca_podset_create(mirror.h, table.ref, C.byref(h)), "ca_podset_create")
+        self.h = h
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.ca_podset_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 class EstimatePlan:

@@ -68,6 +68,7 @@ def parse():
     ap.add_argument("--cpu-groups", type=int, default=100, help="groups in the bounded CPU-baseline sample")
     ap.add_argument("--no-sweep", action="store_true", help="skip the C3 scale-down sweep leg (N=1 only)")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 taint/affinity Estimate leg (N=1 only)")
+    ap.add_argument("--no-expansion", action="store_true", help="skip the expansion-option feasibility leg (N=1)")
     ap.add_argument("--sweep-nodes", type=int, default=5000)
     return ap.parse_args()
 
@@ -118,6 +119,67 @@ def c4_leg(args, device: int, with_cpu: bool) -> dict:
                     "parity": bool(np.array_equal(ro.results, res) and np.array_equal(ro.sched_pod, sp)),
                     "cpu_baseline": {"kind": "port", "cores": 1,
                                      "sample": f"oracle/casim_oracle.c, the same C4 batch, 1 thread of {cpu_model()}"}})
+    m.close()
+    return out
+
+
+def expansion_leg(args, device: int, with_cpu: bool) -> dict:
+    """ComputeExpansionOption's feasibility for every (node group, pod group) pair
+    (orchestrator.go:455-481) on the C4 attributes: CheckPredicates of
+    each pod group's sample on a fresh copy of each template (ca_check_templates).
+    'groups' = the distinct pod records (equivalence groups), 'all' = every pod its own
+    group (no controller: the worst case)."""
+    from autoscaler_amd import native
+    from autoscaler_amd import workloads as W
+    w = W.c4(n_pods=args.pods, n_groups=args.groups, n_existing=args.existing, max_nodes=args.max_nodes)
+    pods = w.table.pods
+    uniq = np.unique(pods.view(np.dtype((np.void, pods.dtype.itemsize))), return_index=True)[1].astype(np.int32)
+    m = native.Mirror(device)
+    W.load_estimate(m, w)
+    out = {"workload": f"C4 pods x {args.groups} node-group templates"}
+    podset = native.PodSet(m, w.table)                                      # pods resident in HBM
+    for name, samples in (("groups", np.sort(uniq)), ("all", np.arange(len(pods), dtype=np.int32))):
+        # the verdicts (which pod groups join which option) into page-locked memory, then
+        # the full results (failing plugin and reasons per pair: eg.SchedulingErrors)
+        pin = native.PinnedArray(m.lib, len(samples) * len(w.templates), np.uint8)
+        ok = pin.array.reshape(len(w.templates), len(samples))
+        rec = {"pod_groups": int(len(samples)), "pairs": int(len(samples) * len(w.templates))}
+        for mode in ("verdicts", "with_reasons"):
+            call = (lambda: m.check_templates(w.table, samples, w.templates, podset=podset, verdict_only=True,
+                                              out=ok)) if mode == "verdicts" else \
+                   (lambda: m.check_templates(w.table, samples, w.templates, podset=podset))
+            call()                                                         # warm-up
+            ts = []
+            for _ in range(max(args.steps, 5)):
+                t = time.perf_counter()
+                res = call()
+                ts.append(time.perf_counter() - t)
+            ms = float(np.median(ts) * 1e3)
+            rec[f"{mode}_ms"] = ms
+            rec[f"{mode}_pairs_per_s"] = len(samples) * len(w.templates) / (ms / 1e3)
+        rec["feasible_pairs"] = int((res["type"] == 0).sum())
+        rec["verdicts_match_results"] = bool(np.array_equal(ok.astype(bool), res["type"] == 0))
+        pin.close()
+        ms = rec["verdicts_ms"]
+        if with_cpu:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import pyoracle                                           # CPU baseline leg only
+            o = pyoracle.OracleState()
+            W.load_estimate(o, w)
+            t = time.perf_counter()
+            ro = o.check_templates(w.table, samples, w.templates)
+            cpu_ms = (time.perf_counter() - t) * 1e3
+            rec.update({"cpu_ms": cpu_ms, "speedup_verdicts": cpu_ms / ms,
+                        "speedup_with_reasons": cpu_ms / rec["with_reasons_ms"],
+                        "parity": bool(np.array_equal(ro, res))})
+        out[name] = rec
+    podset.close()
+    out["includes"] = ("host->device template rows, the matrix kernel, device->host results (1 B per pair into "
+                       "page-locked memory; 16 B per pair with reasons into pageable memory)")
+    if with_cpu:
+        out["cpu_baseline"] = {"kind": "port", "cores": 1,
+                               "sample": f"oracle/casim_oracle.c or_check_templates (fork, template copy, "
+                                         f"CheckPredicates, revert per node group), 1 thread of {cpu_model()}"}
     m.close()
     return out
 
@@ -379,6 +441,8 @@ def main():
             result["extra"]["sweep"] = sweep_leg(args, local, not args.no_cpu_baseline)
         if world == 1 and not args.no_c4:
             result["extra"]["c4"] = c4_leg(args, local, not args.no_cpu_baseline)
+        if world == 1 and not args.no_expansion:
+            result["extra"]["expansion"] = expansion_leg(args, local, not args.no_cpu_baseline)
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.barrier()

@@ -298,6 +298,17 @@ int ca_check_predicates(ca_mirror* m, const ca_pod_table* t, int32_t pod, int32_
 /* Dense feasibility: out[p*n_nodes + n] = 1 iff RunFilterPlugins(pod p, node n) succeeds
  * (CheckPredicates semantics, PreFilter failure -> 0). */
 int ca_fits_matrix(ca_mirror* m, const ca_podset* s, uint8_t* out);
+/* ComputeExpansionOption's feasibility check (CA/core/scaleup/orchestrator/
+ * orchestrator.go:455-481) for every (node group, pod equivalence group) at once:
+ * CheckPredicates(pod set entry samples[e], a fresh copy of templates[g] — the node
+ * with its template pods) as schedulerbased.go:139-185 returns it.
+ * out[g * n_samples + e]: type CA_PRED_OK when group e's pods join g's option (the
+ * failing plugin / reasons otherwise: eg.SchedulingErrors); out_ok[g * n_samples + e]:
+ * the same verdict as one byte (either output may be NULL).
+ * The snapshot is not modified (the reference forks, adds the test node, reverts). */
+int ca_check_templates(ca_mirror* m, const ca_podset* s, const int32_t* samples, int32_t n_samples,
+                       const ca_template* templates, int32_t n_templates, ca_pred_result* out,
+                       uint8_t* out_ok);
 
 /* ---- estimator ---------------------------------------------------------------- */
 /* Estimate() for G node groups in order, sharing lastIndex as the reference's single

@@ -516,6 +516,25 @@ static int32_t add_template_copy(or_state* s, const ca_template* tp) {
     return pos;
 }
 
+/* ComputeExpansionOption's feasibility check (CA/core/scaleup/orchestrator/
+ * orchestrator.go:455-481), per node group: Fork, AddNodeWithPods(template node,
+ * template pods), CheckPredicates(samplePod, node) for every equivalence group, Revert. */
+int or_check_templates(or_state* s, const ca_pod_table* t, const int32_t* samples, int32_t n_samples,
+                       const ca_template* templates, int32_t n_templates, ca_pred_result* out) {
+    for (int32_t e = 0; e < n_samples; e++)
+        if (samples[e] < 0 || samples[e] >= t->n_pods) return CA_EINVAL;
+    for (int32_t g = 0; g < n_templates; g++) {
+        or_fork(s);                                                           /* :454 */
+        const int32_t node = add_template_copy(s, &templates[g]);             /* :457-466 */
+        for (int32_t e = 0; e < n_samples; e++) {                             /* :468-480 */
+            pod_ctx c = table_ctx(t, samples[e]);
+            check_pred(s, &c, node, &out[(size_t)g * n_samples + e], NULL);
+        }
+        or_revert(s);                                                         /* :482 */
+    }
+    return CA_OK;
+}
+
 static int estimate_one(or_state* s, const ca_pod_table* t, const int32_t* pods, int32_t P,
                         const ca_template* tp, const ca_limiter* lim, int32_t* last_index,
                         ca_estimate_result* res, int32_t* sched_pod, int32_t* sched_node) {

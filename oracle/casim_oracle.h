@@ -47,6 +47,8 @@ int or_fits_any_node(or_state* s, const ca_pod_table* t, int32_t pod, const ca_m
                      uint64_t* evals);
 int or_check_predicates(or_state* s, const ca_pod_table* t, int32_t pod, int32_t node,
                         ca_pred_result* out);
+int or_check_templates(or_state* s, const ca_pod_table* t, const int32_t* samples, int32_t n_samples,
+                       const ca_template* templates, int32_t n_templates, ca_pred_result* out);
 int or_estimate(or_state* s, const ca_pod_table* t, const int32_t* group_off,
                 const int32_t* pod_idx, const ca_template* templates, int32_t n_groups,
                 const ca_limiter* limiter, int32_t* last_index, ca_estimate_result* results,

@@ -44,6 +44,7 @@ def load() -> C.CDLL:
         "or_pod_node": ([vp, i32], C.c_int), "or_node_state": ([vp, i32, vp], C.c_int),
         "or_fits_any_node": ([vp, vp, i32, vp, p(i32), p(i32), p(i32), p(C.c_uint64)], C.c_int),
         "or_check_predicates": ([vp, vp, i32, i32, vp], C.c_int),
+        "or_check_templates": ([vp, vp, vp, i32, vp, i32, vp], C.c_int),
         "or_estimate": ([vp, vp, vp, vp, vp, i32, vp, p(i32), vp, vp, vp], C.c_int),
         "or_try_schedule_pods": ([vp, vp, i32, vp, i32, vp, p(i32), vp, p(C.c_uint64)], C.c_int),
         "or_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, p(i32), vp, vp], C.c_int),
@@ -138,6 +139,15 @@ class OracleState:
         r = abi.PredResultC()
         _check(self.lib.or_check_predicates(self.h, table.ref, pod, node, C.byref(r)), "check_predicates")
         return r.type, r.plugin, r.reasons, r.taint
+
+    def check_templates(self, table: abi.PodTable, samples, templates: np.ndarray) -> np.ndarray:
+        """ComputeExpansionOption's CheckPredicates(sample, template copy) matrix [G][E]."""
+        sm = np.ascontiguousarray(samples, dtype=np.int32)
+        tm = np.ascontiguousarray(templates, dtype=abi.TEMPLATE_DTYPE)
+        out = np.zeros((len(tm), len(sm)), abi.PRED_RESULT_DTYPE)
+        _check(self.lib.or_check_templates(self.h, table.ref, ptr(sm), len(sm), ptr(tm), len(tm), ptr(out)),
+               "check_templates")
+        return out
 
     def estimate(self, table: abi.PodTable, group_off, pod_idx, templates: np.ndarray, max_nodes: int,
                  last_index: int = 0) -> EstimateOutput:

@@ -52,6 +52,11 @@ PHASE_KERNEL = {"score_ms": "k_class_rank", "merge_ms": "k_radix_hist+k_radix_sc
                 "emit_ms": "k_emit_bucket", "chain_ms": "k_ffd_chain", "compact_ms": "k_copy_segments"}
 
 
+def native_device_count() -> int:
+    from autoscaler_amd import native
+    return native.device_count()
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -240,12 +245,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N>1 path on fewer GPUs (CASIM_BENCH_BACKEND=gloo: ranks share devices
+    # round-robin, collectives over gloo on host tensors); the driver's runs use RCCL
+    backend = os.environ.get("CASIM_BENCH_BACKEND", "nccl")
     import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
+        if backend != "nccl":
+            local = local % max(1, native_device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")           # RCCL on ROCm
+        dist.init_process_group(backend)          # "nccl" is RCCL on ROCm
 
     from autoscaler_amd import native, shard
     from autoscaler_amd import workloads as W
@@ -266,7 +276,8 @@ def main():
         sens, succ = plan.chain_info()
         return out, out.last_index, sens, succ
 
-    gather = shard.torch_all_gather(dist, f"cuda:{local}") if dist is not None else None
+    coll_dev = f"cuda:{local}" if backend == "nccl" else "cpu"
+    gather = shard.torch_all_gather(dist, coll_dev) if dist is not None else None
 
     def step():
         """One batch on this rank + the lastIndex chain across ranks (autoscaler_amd/shard.py)."""
@@ -305,7 +316,7 @@ def main():
         ph["chain_ms"] = ph["chain_ms"] / max(st["rounds"], 1)       # one launch
         phases.append(ph)
     if dist is not None:
-        t = torch.tensor([elapsed, float(evals)], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed, float(evals)], dtype=torch.float64, device=coll_dev)
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t.clone()
@@ -362,7 +373,7 @@ def main():
             dist.barrier()
         h_el = time.perf_counter() - h0
         if dist is not None:
-            t = torch.tensor([h_el], dtype=torch.float64, device=f"cuda:{local}")
+            t = torch.tensor([h_el], dtype=torch.float64, device=coll_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             h_el = float(t[0])
         host_pods = hout.sched_pod.copy()

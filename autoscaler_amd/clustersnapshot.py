@@ -170,6 +170,14 @@ class ClusterSnapshot:
         self._stack = []
         self.interner = Interner()
 
+    def record_added_pods(self, placed: list) -> None:
+        """Pods the backend already added (a batched AddPod, e.g. FilterOutSchedulable):
+        [(pod, node name, mirror pod id)] — recorded as AddPod ops without re-applying them."""
+        st = self._state
+        for pod, node, pid in placed:
+            st.add_pod(pod, node, int(pid))
+            self._log.append(("pod", pod, node))
+
     # -- NodeInfos() lister ----------------------------------------------------
     def List(self) -> list:  # noqa: N802
         st = self._state

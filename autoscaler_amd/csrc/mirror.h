@@ -47,6 +47,21 @@ struct SweepScratch {
     HostBuf h_in, h_tab, h_out, h_todo, h_lin, h_wl;
 };
 
+// Per-mirror scratch of ca_filter_out_schedulable (filter.hip).
+struct FilterScratch {
+    DevBuf in, zero, out;          // inputs (order, hints, class tables), zeroed state, outputs
+    HostBuf h_in, h_out;
+    DevPodTable pods;              // the pending table when the caller passes no podset
+    float kernel_ms = 0, total_ms = 0;
+    int32_t batches = 0, cuts = 0;
+};
+
+// Dirty-row staging of sync_nodes: one H2D copy + a scatter kernel.
+struct RowStage {
+    DevBuf d;
+    HostBuf h;
+};
+
 struct Stats {
     int32_t rounds = 0;
     float kernel_ms = 0, sort_ms = 0, total_ms = 0;
@@ -91,6 +106,8 @@ struct ca_mirror {
     std::vector<uint8_t> h_scratch;
     casim::Stats sweep_stats;
     casim::SweepScratch sw;
+    casim::FilterScratch fo;
+    casim::RowStage rs;
     // resident HintingSimulator hints (hints.go:29-72): node per mirror pod, -1 = none
     casim::DevBuf d_pod_hints;
     size_t d_hints_n = 0;

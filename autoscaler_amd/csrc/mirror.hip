@@ -92,6 +92,22 @@ int DevPodTable::upload(const ca_pod_spec* pods, int32_t n, const ca_selector_te
     return CA_OK;
 }
 
+// a dirty row staged for sync_nodes
+struct alignas(16) StagedRow {
+    int32_t row, pad[3];
+    NodeHot hot;
+    NodeExt ext;
+};
+
+__global__ void k_scatter_rows(const StagedRow* __restrict__ rows, int32_t k, NodeHot* __restrict__ hot,
+                               NodeExt* __restrict__ ext) {
+    const int32_t j = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (j >= k) return;
+    const int32_t r = rows[j].row;
+    hot[r] = rows[j].hot;
+    ext[r] = rows[j].ext;
+}
+
 }  // namespace casim
 
 using namespace casim;
@@ -223,7 +239,7 @@ int ca_mirror::sync_nodes() {
         for (size_t i = d_rows; i < n; i++) mark_dirty((int32_t)i);
         static_dirty = true;
     }
-    if (all_dirty || dirty_rows.size() > 64) {
+    if (all_dirty || dirty_rows.size() > std::max<size_t>(64, n / 4)) {
         std::vector<NodeHot> h(n);
         std::vector<NodeExt> e(n);
         for (size_t i = 0; i < n; i++) { fill_hot((int32_t)i, h[i]); fill_ext((int32_t)i, e[i]); }
@@ -231,13 +247,22 @@ int ca_mirror::sync_nodes() {
         if (n) CA_HIP_CHECK(hipMemcpyAsync(d_ext.ptr, e.data(), sizeof(NodeExt) * n, hipMemcpyHostToDevice, stream));
         CA_HIP_CHECK(hipStreamSynchronize(stream));
     } else if (!dirty_rows.empty()) {
-        for (int32_t r : dirty_rows) {
-            NodeHot h; NodeExt e;
-            fill_hot(r, h); fill_ext(r, e);
-            CA_HIP_CHECK(hipMemcpyAsync(d_hot.as<NodeHot>() + r, &h, sizeof h, hipMemcpyHostToDevice, stream));
-            CA_HIP_CHECK(hipMemcpyAsync(d_ext.as<NodeExt>() + r, &e, sizeof e, hipMemcpyHostToDevice, stream));
-            CA_HIP_CHECK(hipStreamSynchronize(stream));   // h/e are stack temporaries
+        // few rows: stage them (row id + both columns) in pinned memory, one H2D copy, and
+        // scatter them on the device
+        const size_t k = dirty_rows.size();
+        if ((rc = rs.h.reserve(sizeof(StagedRow) * k)) != CA_OK) return rc;
+        if ((rc = rs.d.reserve(sizeof(StagedRow) * k)) != CA_OK) return rc;
+        StagedRow* sr = rs.h.as<StagedRow>();
+        for (size_t j = 0; j < k; j++) {
+            sr[j].row = dirty_rows[j];
+            fill_hot(dirty_rows[j], sr[j].hot);
+            fill_ext(dirty_rows[j], sr[j].ext);
         }
+        CA_HIP_CHECK(hipMemcpyAsync(rs.d.ptr, sr, sizeof(StagedRow) * k, hipMemcpyHostToDevice, stream));
+        hipLaunchKernelGGL(k_scatter_rows, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, stream,
+                           rs.d.as<const StagedRow>(), (int32_t)k, d_hot.as<NodeHot>(), d_ext.as<NodeExt>());
+        CA_HIP_CHECK(hipGetLastError());
+        CA_HIP_CHECK(hipStreamSynchronize(stream));        // the staging buffer is reused
     }
     if (static_dirty && n) {
         std::vector<NodeStatic> s(n);

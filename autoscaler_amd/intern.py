@@ -200,6 +200,7 @@ class Interner:
         self.scalars = _Universe(abi.CA_MAX_SCALAR, "scalar resources")
         self.names: dict[str, int] = {}
         self.classes: dict = {}
+        self.class_uid: list = []
         self.observe(nodes, pods, templates)
 
     # -- universes -----------------------------------------------------------
@@ -318,8 +319,18 @@ class Interner:
             return -1
         key = (ref.uid, repr(sorted(pod.labels.items())), repr((pod.containers, pod.init_containers, pod.overhead,
                                                                  pod.node_selector, pod.affinity, pod.tolerations,
-                                                                 pod.volumes, pod.topology_spread)))
-        return self.classes.setdefault(key, len(self.classes))
+                                                                 pod.volumes, pod.topology_spread,
+                                                                 pod.node_name, pod.priority)))
+        c = self.classes.setdefault(key, len(self.classes))
+        if c == len(self.class_uid):
+            self.class_uid.append(ref.uid)
+        return c
+
+    def class_owners(self, n_classes: int) -> "np.ndarray":
+        """Dense controller id of every class id < n_classes (SimilarPodsScheduling keys its
+        items by controller UID, similar_pods.go:71-111)."""
+        uids: dict = {}
+        return np.array([uids.setdefault(u, len(uids)) for u in self.class_uid[:n_classes]], np.int32)
 
     def encode_pods(self, pods: list[Pod]) -> abi.PodTable:
         recs = abi.empty_pods(len(pods))

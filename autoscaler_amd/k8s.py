@@ -149,6 +149,7 @@ class Pod:
     topology_spread: list = field(default_factory=list)
     phase: str = "Running"
     deletion_timestamp: Optional[float] = None
+    priority: Optional[int] = None                  # Spec.Priority (corev1helpers.PodPriority: nil -> 0)
 
     def controller_ref(self) -> Optional[OwnerReference]:
         for r in self.owner_refs:

@@ -86,6 +86,9 @@ def load() -> C.CDLL:
         "ca_mirror_get_hints": ([vp, vp, i32], C.c_int),
         "ca_removal_candidate_ticks": ([vp, p(C.c_uint64), i32], C.c_int),
         "ca_removal_timings": ([vp, p(C.c_float), i32], C.c_int),
+        "ca_filter_out_schedulable": ([vp, vp, vp, vp, i32, vp, i32, vp, p(i32), vp, vp, p(i32), p(C.c_uint64), p(i32)],
+                                      C.c_int),
+        "ca_filter_stats": ([vp, p(C.c_float), i32], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(lib, name)
@@ -113,7 +116,7 @@ def exported_symbols() -> list[str]:
         "ca_find_nodes_to_remove",
         "ca_removal_stats", "ca_removal_timings", "ca_removal_plan_create", "ca_removal_plan_run",
         "ca_removal_plan_destroy", "ca_mirror_set_hints", "ca_mirror_get_hints",
-        "ca_removal_candidate_ticks",
+        "ca_removal_candidate_ticks", "ca_filter_out_schedulable", "ca_filter_stats",
     ]
 
 
@@ -137,6 +140,56 @@ class RemovalOutput:
     dest: np.ndarray             # int32 [M]
     hints: np.ndarray            # int32 [pods]
     last_index: int
+
+
+@dataclass
+class FilterOutput:
+    node: np.ndarray             # int32 [n]: node position per processed pod, -1 still pending
+    pod_id: np.ndarray           # int32 [n]: mirror pod id of the added pod, -1
+    hints: np.ndarray            # int32 [n]: hints after the call (Hints.Set)
+    placed: int
+    last_index: int
+    evals: int
+    n_overflowing: int
+
+
+@dataclass
+class _FilterArgs:
+    order: np.ndarray
+    n: int
+    owner: object
+    n_classes: int
+    hints: np.ndarray
+    node: np.ndarray
+    pod_id: np.ndarray
+
+    @property
+    def owner_ptr(self):
+        return None if self.owner is None else ptr(self.owner)
+
+    def output(self, placed: int, last_index: int, evals: int, n_overflowing: int) -> FilterOutput:
+        return FilterOutput(self.node[: self.n], self.pod_id[: self.n], self.hints[: self.n], placed, last_index,
+                            evals, n_overflowing)
+
+
+def filter_args(table: abi.PodTable, order=None, class_owner=None, hints=None) -> _FilterArgs:
+    """Marshal the arguments of ca_filter_out_schedulable / or_filter_out_schedulable."""
+    n_pods = len(table.pods)
+    order = np.arange(n_pods, dtype=np.int32) if order is None else np.ascontiguousarray(order, dtype=np.int32)
+    n = len(order)
+    cls = table.pods["similar_class"]
+    n_classes = int(cls.max()) + 1 if n_pods else 0
+    owner = None
+    if class_owner is not None:
+        owner = np.full(max(n_classes, 1), -1, np.int32)
+        co = np.ascontiguousarray(class_owner, dtype=np.int32)
+        owner[: min(len(co), n_classes)] = co[:n_classes]
+        n_classes = max(n_classes, 0)
+    h = np.full(max(n, 1), -1, np.int32)
+    if hints is not None:
+        h[:n] = np.asarray(hints, dtype=np.int32)
+    return _FilterArgs(order if n else np.zeros(1, np.int32), n, owner, max(n_classes, 0), h,
+                       np.full(max(n, 1), -1, np.int32), np.full(max(n, 1), -1, np.int32))
 
 
 class Mirror:
@@ -272,6 +325,26 @@ class Mirror:
         return out
 
     # -- removal simulator ----------------------------------------------------
+    def filter_out_schedulable(self, table: abi.PodTable, order=None, class_owner=None, hints=None,
+                               last_index: int = 0, podset=None) -> FilterOutput:
+        """ca_filter_out_schedulable: TrySchedulePods(pending, ScheduleAnywhere, breakOnFailure=false)
+        committed into the mirror (filter_out_schedulable.go:95-124)."""
+        a = filter_args(table, order, class_owner, hints)
+        li = C.c_int32(last_index)
+        ev = C.c_uint64(0)
+        ov = C.c_int32(0)
+        placed = C.c_int32(0)
+        _check(self.lib.ca_filter_out_schedulable(self.h, table.ref, podset.h if podset is not None else None,
+                                                  ptr(a.order), a.n, a.owner_ptr, a.n_classes, ptr(a.hints),
+                                                  C.byref(li), ptr(a.node), ptr(a.pod_id), C.byref(ov),
+                                                  C.byref(ev), C.byref(placed)), "ca_filter_out_schedulable")
+        return a.output(placed.value, li.value, ev.value, ov.value)
+
+    def filter_stats(self) -> dict:
+        out = (C.c_float * 4)()
+        self.lib.ca_filter_stats(self.h, out, 4)
+        return {"kernel_ms": out[0], "total_ms": out[1], "batches": int(out[2]), "cuts": int(out[3])}
+
     def find_nodes_to_remove(self, candidates, dest_mask, cand_status, move_off, move_pods, hints,
                              last_index: int = 0) -> RemovalOutput:
         cand = np.ascontiguousarray(candidates, dtype=np.int32)

@@ -114,12 +114,12 @@ class SchedulerBasedPredicateChecker:
                                   f"Error obtaining NodeInfo for name {node_name}; {e}", None)
         table = snapshot.encode([pod])
         typ, plugin, reasons, taint = snapshot.backend.check_predicates(table, 0, pos)
-        if typ == abi.CA_PRED_OK:
-            return None
         if typ == abi.CA_PRED_INTERNAL:
             return PredicateError(InternalPredicateError, "", ERR_REASON_AFFINITY_CONFLICT,
                                   [ERR_REASON_AFFINITY_CONFLICT])
-        self.evals += 1
+        self.evals += 1                                  # RunFilterPlugins ran (:171)
+        if typ == abi.CA_PRED_OK:
+            return None
         node = snapshot.Get(node_name).node
         name = abi.PLUGIN_NAMES[plugin]
         debug = None

@@ -92,7 +92,8 @@ class SimilarPodsScheduling:
     def _sig(pod: Pod):
         return (repr(sorted(pod.labels.items())), repr((pod.containers, pod.init_containers, pod.overhead,
                                                         pod.node_selector, pod.affinity, pod.tolerations,
-                                                        pod.volumes, pod.topology_spread)))
+                                                        pod.volumes, pod.topology_spread,
+                                                        pod.node_name, pod.priority)))
 
     def IsSimilarUnschedulable(self, pod: Pod) -> bool:  # noqa: N802
         k = self._key(pod)

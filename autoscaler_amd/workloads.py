@@ -439,3 +439,109 @@ def c4_sweep(n_nodes: int = 5000, pods_per_node: int = 30, seed: int = 4321) -> 
     return SweepWorkload("C4-sweep", w.nodes, abi.PodTable(pods, term_arr, req_arr), w.pod_node, w.candidates,
                          w.dest_mask, w.cand_status, w.move_off, w.move_pods,
                          dict(w.meta, seed=seed, terms=len(term_arr)))
+
+
+# ---------------------------------------------------------------------------
+# C5 FilterOutSchedulable: pending pods against a large running cluster
+# ---------------------------------------------------------------------------
+@dataclass
+class FilterWorkload:
+    name: str
+    nodes: np.ndarray
+    table: abi.PodTable          # running pods
+    pod_node: np.ndarray
+    pending: abi.PodTable        # pending pods
+    order: np.ndarray            # priority order (filter_out_schedulable.go:97-99, stable)
+    class_owner: np.ndarray      # dense controller id per similar class
+    hints: np.ndarray            # hinted node position per order position, -1 none
+    meta: dict = field(default_factory=dict)
+
+
+def c5_filter(n_nodes: int = 15_000, pods_per_node: int = 20, n_pending: int = 20_000, seed: int = 5,
+              hint_frac: float = 0.2, taints: bool = False, util_low=(0.70, 0.85),
+              util_high=(0.92, 0.99)) -> FilterWorkload:
+    """C5's FilterOutSchedulable step: 15k nodes {16 cores, 64Gi, 110
+    pods} running 300k pods (30% of nodes at 70-85% cpu, the rest at 92-99%), 20k pending pods
+    of C2 shapes from controllers of 50 pods on average; 10% of controllers run 12-20 pod
+    variants (past similar_pods' 10-per-controller cache), 3% DaemonSet pods, 5% pods with no
+    controller, 4 priority levels, hint_frac of the pods hinted to a random node.
+    taints=True adds the C4 taint/label universe to the nodes and the pending pods."""
+    rng = np.random.default_rng(seed)
+    node_cpu, node_mem = 16000, 64 * GI
+    nodes = abi.empty_nodes(n_nodes)
+    nodes["alloc_milli_cpu"] = node_cpu
+    nodes["alloc_memory"] = node_mem
+    nodes["alloc_pods"] = 110
+    nodes["name_id"] = np.arange(n_nodes)
+    low = rng.random(n_nodes) < 0.30
+    util = np.where(low, rng.uniform(*util_low, n_nodes), rng.uniform(*util_high, n_nodes))
+    w = rng.gamma(2.0, 1.0, (n_nodes, pods_per_node))
+    w /= w.sum(axis=1, keepdims=True)
+    cpu = np.floor(w * (util * node_cpu)[:, None]).astype(np.int64).ravel()
+    mem = (np.floor(w * (util * node_mem / MI)[:, None]).astype(np.int64) * MI).ravel()
+    running = resource_pods(cpu, mem)
+    pod_node = np.repeat(np.arange(n_nodes, dtype=np.int32), pods_per_node)
+    # pending pods: controllers -> variants (similar classes) -> pods
+    shapes = [(c, m) for c in C2_CPU for m in C2_MEM]
+    cls_shape, cls_owner, cls_ds = [], [], []
+    pod_cls = []
+    n_owner = 0
+    while len(pod_cls) < n_pending:
+        r = rng.random()
+        if r < 0.05:                                   # no controller: class -1
+            pod_cls.extend([-1] * int(rng.integers(1, 4)))
+            continue
+        ds = r < 0.08
+        nvar = int(rng.integers(12, 21)) if (not ds and rng.random() < 0.10) else 1
+        first = len(cls_shape)
+        for _ in range(nvar):
+            cls_shape.append(int(rng.integers(0, len(shapes))))
+            cls_owner.append(n_owner)
+            cls_ds.append(ds)
+        n_owner += 1
+        npods = int(rng.integers(1, 100))
+        pod_cls.extend((first + rng.integers(0, nvar, npods)).tolist())
+    pod_cls = np.array(pod_cls[:n_pending], np.int64)
+    noc = pod_cls < 0
+    free_shape = rng.integers(0, len(shapes), n_pending)
+    shp = np.where(noc, free_shape, np.array(cls_shape + [0], np.int64)[pod_cls])
+    pcpu = np.array([shapes[s][0] for s in shp], np.int64)
+    pmem = np.array([shapes[s][1] for s in shp], np.int64)
+    pend = resource_pods(pcpu, pmem)
+    pend["similar_class"] = pod_cls
+    ds_pod = np.array(cls_ds + [False])[pod_cls] & ~noc
+    pend["flags"][ds_pod] |= abi.CA_POD_DAEMONSET
+    terms_arr = req_arr = None
+    if taints:
+        uni = _C4Universe(rng)
+        for i in range(n_nodes):
+            _c4_node(nodes[i], uni.node_attrs(rng, int(rng.integers(0, 3))))
+        terms: list = []
+        reqs: list = []
+        n_cls = len(cls_shape)
+        specs = [_c4_pod_spec(rng, uni, terms, reqs) for _ in range(n_cls + 1)]
+        for i in range(n_pending):
+            c = int(pod_cls[i])
+            if c < 0:                                  # a pod of its own: its own spec
+                _c4_encode_spec(pend[i:i + 1], *_c4_pod_spec(rng, uni, terms, reqs))
+            else:
+                _c4_encode_spec(pend[i:i + 1], *specs[c])
+        terms_arr = np.array(terms, dtype=abi.TERM_DTYPE) if terms else np.zeros(0, abi.TERM_DTYPE)
+        req_arr = np.array(reqs, dtype=abi.REQ_DTYPE) if reqs else np.zeros(0, abi.REQ_DTYPE)
+    prio = rng.choice([0, 100, 1000, 10000], n_pending, p=[0.6, 0.2, 0.15, 0.05])
+    # a class's pods share their spec, priority included
+    cls_prio = rng.choice([0, 100, 1000, 10000], len(cls_shape) + 1, p=[0.6, 0.2, 0.15, 0.05])
+    prio = np.where(noc, prio, cls_prio[pod_cls])
+    order = np.argsort(-prio, kind="stable").astype(np.int32)
+    hints = np.where(rng.random(n_pending) < hint_frac, rng.integers(0, n_nodes, n_pending), -1).astype(np.int32)
+    pending = abi.PodTable(pend, terms_arr, req_arr) if taints else abi.PodTable(pend)
+    return FilterWorkload("C5-filter" + ("-c4" if taints else ""), nodes, abi.PodTable(running), pod_node, pending,
+                          order, np.array(cls_owner, np.int32), hints,
+                          {"seed": seed, "classes": len(cls_shape), "controllers": n_owner,
+                           "daemonset_pods": int(ds_pod.sum()), "no_controller_pods": int(noc.sum())})
+
+
+def load_filter(backend, w: FilterWorkload) -> None:
+    backend.clear()
+    backend.add_nodes(w.nodes)
+    backend.add_pods(w.table, np.arange(len(w.table), dtype=np.int32), w.pod_node)

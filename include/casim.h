@@ -391,6 +391,33 @@ int ca_removal_stats(const ca_mirror* m, int32_t* rounds, float* kernel_ms, floa
  * last sweep's last exact pass that ran it (0 for candidates it did not run). */
 int ca_removal_candidate_ticks(const ca_mirror* m, uint64_t* out, int32_t n_candidates);
 
+/* ---- FilterOutSchedulable ------------------------------------------------------ */
+/* filterOutSchedulableByPacking (CA/core/podlistprocessor/filter_out_schedulable.go:95-124):
+ * HintingSimulator.TrySchedulePods(snapshot, pending, ScheduleAnywhere, breakOnFailure=false)
+ * (CA/simulator/scheduling/hinting_simulator.go:58-125) over the pending pods
+ * t->pods[order[k]], k = 0..n-1, in that order (order NULL: the table order).  The caller
+ * does the priority sort (:97-99).  Every pod that fits is added to the mirror (AddPod,
+ * :77-82), on the current fork level, so a later Revert drops it.
+ *  s            optional device-resident copy of t (ca_podset_create(m, t)); NULL uploads t.
+ *  hints[k]     hinted node position of pod k, or -1 (Hints.Get).  Updated in place
+ *               (Hints.Set): the node of every placed pod.
+ *  similar pods (similar_pods.go:43-111): t->pods[i].similar_class (< n_classes, or -1).
+ *               class_owner[c] is the dense controller id of class c.  At most 10 classes per
+ *               controller are remembered; the controllers that overflow are counted in
+ *               *n_overflowing (may be NULL).  class_owner NULL: no cap.
+ *  out_node[k]  node position of pod k, or -1 (still unschedulable).
+ *  out_pod_id[k] mirror pod id of the added pod, or -1 (may be NULL).
+ *  *last_index  FitsAnyNode's lastIndex, in/out;  *evals += predicate evaluations.
+ *  *n_placed    number of placed pods (may be NULL). */
+int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_podset* s,
+                              const int32_t* order, int32_t n, const int32_t* class_owner,
+                              int32_t n_classes, int32_t* hints, int32_t* last_index,
+                              int32_t* out_node, int32_t* out_pod_id, int32_t* n_overflowing,
+                              uint64_t* evals, int32_t* n_placed);
+/* [0] device time of the last call's kernel, [1] host wall time of the call (ms),
+ * [2] batches, [3] pods processed one at a time (cut points); returns 4. */
+int ca_filter_stats(const ca_mirror* m, float* out, int32_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -709,6 +709,81 @@ int or_try_schedule_pods(or_state* s, const int32_t* pod_ids, int32_t n,
 }
 
 /* ------------------------------------------------------------------------- */
+/* FilterOutSchedulable (filter_out_schedulable.go:95-124)                     */
+/* ------------------------------------------------------------------------- */
+#define OR_MAX_PODS_PER_OWNER 10                  /* similar_pods.go:53 */
+
+int or_filter_out_schedulable(or_state* s, const ca_pod_table* t, const int32_t* order, int32_t n,
+                              const int32_t* class_owner, int32_t n_classes, int32_t* hints,
+                              int32_t* last_index, int32_t* out_node, int32_t* out_pod_id,
+                              int32_t* n_overflowing, uint64_t* evals, int32_t* n_placed) {
+    if (n < 0 || n_classes < 0) return CA_EINVAL;
+    int32_t n_owners = 0;
+    for (int32_t k = 0; k < n; k++) {
+        const int32_t i = order ? order[k] : k;
+        if (i < 0 || i >= t->n_pods) return CA_EINVAL;
+        if (t->pods[i].similar_class >= n_classes) return CA_EINVAL;
+    }
+    if (class_owner)
+        for (int32_t c = 0; c < n_classes; c++) if (class_owner[c] + 1 > n_owners) n_owners = class_owner[c] + 1;
+    uint8_t* marked = calloc((size_t)n_classes + 1, 1);       /* items[uid] holds this class */
+    int32_t* owner_cnt = calloc((size_t)n_owners + 1, sizeof(int32_t));   /* len(items[uid]) */
+    uint8_t* owner_over = calloc((size_t)n_owners + 1, 1);    /* overflowingControllers */
+    ca_match_spec all;
+    memset(&all, 0, sizeof all);
+    all.kind = CA_MATCH_ALL; all.exclude = -1;                  /* ScheduleAnywhere */
+    int32_t placed = 0;
+    for (int32_t k = 0; k < n; k++) {                           /* hinting_simulator.go:63-86 */
+        const int32_t i = order ? order[k] : k;
+        pod_ctx c = table_ctx(t, i);
+        int32_t node = -1;
+        if (hints && hints[k] >= 0) {                           /* findNodeWithHints :91-108 */
+            ca_pred_result pr;
+            check_pred(s, &c, hints[k], &pr, evals);
+            if (pr.type == CA_PRED_OK) node = hints[k];         /* :95 Set, :102 accepted */
+        }
+        if (node < 0) {                                         /* findNode :110-125 */
+            const int32_t cls = c.p->similar_class;
+            if (!(cls >= 0 && marked[cls])) {                   /* IsSimilarUnschedulable */
+                node = fits_any(s, &c, &all, last_index, NULL, evals);
+                if (node < 0) {
+                    if (cls >= 0 && !(c.p->flags & CA_POD_DAEMONSET)) {   /* SetUnschedulable */
+                        const int32_t o = class_owner ? class_owner[cls] : -1;
+                        if (o < 0) {
+                            marked[cls] = 1;
+                        } else if (owner_cnt[o] >= OR_MAX_PODS_PER_OWNER) {
+                            owner_over[o] = 1;
+                        } else {
+                            marked[cls] = 1;
+                            owner_cnt[o]++;
+                        }
+                    }
+                }
+            }
+        }
+        if (node >= 0) {                                        /* :77-82 AddPod, no fork */
+            if (hints) hints[k] = node;
+            const int32_t id = store_pod(s, t, i, node);
+            add_pod_to_node(s, id, node);
+            out_node[k] = node;
+            if (out_pod_id) out_pod_id[k] = id;
+            placed++;
+        } else {
+            out_node[k] = -1;
+            if (out_pod_id) out_pod_id[k] = -1;
+        }
+    }
+    if (n_overflowing) {
+        int32_t ov = 0;
+        for (int32_t o = 0; o < n_owners; o++) ov += owner_over[o];
+        *n_overflowing = ov;
+    }
+    free(marked); free(owner_cnt); free(owner_over);
+    if (n_placed) *n_placed = placed;
+    return CA_OK;
+}
+
+/* ------------------------------------------------------------------------- */
 /* RemovalSimulator.FindNodesToRemove, legacy canPersist=false (cluster.go:116-254) */
 /* ------------------------------------------------------------------------- */
 int or_find_nodes_to_remove(or_state* s, const int32_t* candidates, int32_t n_candidates,

@@ -59,6 +59,14 @@ int or_estimate(or_state* s, const ca_pod_table* t, const int32_t* group_off,
 int or_try_schedule_pods(or_state* s, const int32_t* pod_ids, int32_t n,
                          const ca_match_spec* match, int32_t break_on_failure,
                          int32_t* hints, int32_t* last_index, int32_t* dest, uint64_t* evals);
+/* filterOutSchedulableByPacking (filter_out_schedulable.go:95-124): TrySchedulePods over
+ * the pending pods t->pods[order[k]] with ScheduleAnywhere, breakOnFailure=false, the
+ * similar-pods cache with its 10-per-controller cap (similar_pods.go:88-111); placed pods
+ * are committed (no fork).  Same contract as ca_filter_out_schedulable. */
+int or_filter_out_schedulable(or_state* s, const ca_pod_table* t, const int32_t* order, int32_t n,
+                              const int32_t* class_owner, int32_t n_classes, int32_t* hints,
+                              int32_t* last_index, int32_t* out_node, int32_t* out_pod_id,
+                              int32_t* n_overflowing, uint64_t* evals, int32_t* n_placed);
 int or_find_nodes_to_remove(or_state* s, const int32_t* candidates, int32_t n_candidates,
                             const uint8_t* dest_mask, const int32_t* cand_status,
                             const int32_t* move_off, const int32_t* move_pods,

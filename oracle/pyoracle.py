@@ -14,7 +14,7 @@ import numpy as np
 
 from autoscaler_amd import abi
 from autoscaler_amd.abi import ptr
-from autoscaler_amd.native import EstimateOutput, RemovalOutput
+from autoscaler_amd.native import EstimateOutput, FilterOutput, RemovalOutput, filter_args
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libcasim_oracle.so")
@@ -48,6 +48,8 @@ def load() -> C.CDLL:
         "or_estimate": ([vp, vp, vp, vp, vp, i32, vp, p(i32), vp, vp, vp], C.c_int),
         "or_try_schedule_pods": ([vp, vp, i32, vp, i32, vp, p(i32), vp, p(C.c_uint64)], C.c_int),
         "or_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, p(i32), vp, vp], C.c_int),
+        "or_filter_out_schedulable": ([vp, vp, vp, i32, vp, i32, vp, p(i32), vp, vp, p(i32), p(C.c_uint64), p(i32)],
+                                      C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(lib, name)
@@ -175,6 +177,19 @@ class OracleState:
                                                ptr(hints), C.byref(li), ptr(dest), C.byref(ev))
         del mask
         return placed, dest[: len(ids)], hints, li.value, ev.value
+
+    def filter_out_schedulable(self, table: abi.PodTable, order=None, class_owner=None, hints=None,
+                               last_index: int = 0, podset=None) -> FilterOutput:
+        del podset                                      # device residency: the mirror only
+        a = filter_args(table, order, class_owner, hints)
+        li = C.c_int32(last_index)
+        ev = C.c_uint64(0)
+        ov = C.c_int32(0)
+        placed = C.c_int32(0)
+        _check(self.lib.or_filter_out_schedulable(self.h, table.ref, ptr(a.order), a.n, a.owner_ptr, a.n_classes,
+                                                  ptr(a.hints), C.byref(li), ptr(a.node), ptr(a.pod_id),
+                                                  C.byref(ov), C.byref(ev), C.byref(placed)), "filter_out_schedulable")
+        return a.output(placed.value, li.value, ev.value, ov.value)
 
     def find_nodes_to_remove(self, candidates, dest_mask, cand_status, move_off, move_pods, hints,
                              last_index: int = 0) -> RemovalOutput:

@@ -175,6 +175,44 @@ for name, line, pn in [
         "expect": {"statuses": [[p, n] for p, n in pn.items()]},
     })
 
+# ---- FilterOutSchedulable: TestFilterOutSchedulable / BenchmarkFilterOutSchedulable ----
+FOS = "CA/core/podlistprocessor/filter_out_schedulable_test.go"
+fnode = [test_node("node", 2000, 100)]          # buildReadyTestNode("node", 2000, 100) (:33)
+for name, line, existing, cand, want_sched, want_unsched in [
+    ("single empty node, no pods", "40-43", [], [], [], []),
+    ("single empty node, single schedulable pod", "44-53", [], [test_pod("pod", 500, 10)], ["pod"], []),
+    ("single empty node, many schedulable pods", "54-67", [],
+     [test_pod("pod1", 200, 10), test_pod("pod2", 500, 10), test_pod("pod3", 800, 10)], ["pod1", "pod2", "pod3"], []),
+    ("single empty node, single unschedulable pod", "68-77", [], [test_pod("pod1", 3000, 10)], [], ["pod1"]),
+    ("single empty node, various pods", "78-92", [],
+     [test_pod("pod1", 200, 10), test_pod("pod2", 500, 10), test_pod("pod3", 1800, 10)], ["pod1", "pod2"], ["pod3"]),
+    ("single empty node, some priority pods", "93-107", [],
+     [test_pod("pod1", 200, 10), test_pod("pod2", 500, 10, priority=10), test_pod("pod3", 1800, 10, priority=20)],
+     ["pod3", "pod1"], ["pod2"]),
+    ("non-empty node with a single pods scheduled", "108-125", [test_pod("pod1", 500, 10, node="node")],
+     [test_pod("pod2", 1000, 10), test_pod("pod3", 300, 10), test_pod("pod4", 300, 10)], ["pod2", "pod3"], ["pod4"]),
+    ("non-empty node with many pods scheduled", "126-143",
+     [test_pod("pod1", 500, 10, node="node"), test_pod("pod2", 1000, 10, node="node")],
+     [test_pod("pod3", 1000, 10), test_pod("pod4", 300, 10), test_pod("pod5", 300, 10)], ["pod4"], ["pod3", "pod5"]),
+]:
+    cases.append({
+        "id": f"filter_out_schedulable/{name}", "source": f"{FOS}:{line},146-191", "kind": "filter_out_schedulable",
+        "nodes": fnode, "pods": existing, "candidates": cand,
+        "expect": {"scheduled": want_sched, "unscheduled": want_unsched},
+    })
+# the benchmark's scenarios (:199-290): every pending pod (1000m, 2000000 B) fails on nodes of
+# 2000m/200000 B holding 1000m/200000 B pods round-robin, so all stay pending
+for name, nn, ns, npend in [("nothing", 1, 30, 1000), ("small", 10, 300, 1000), ("medium", 100, 3000, 1000),
+                            ("large", 200, 200, 60000), ("1k", 1000, 1000, 12000)]:
+    cases.append({
+        "id": f"filter_out_schedulable/bench {name}", "source": f"{FOS}:199-290",
+        "kind": "filter_out_schedulable_bench",
+        "nodes": {"count": nn, "prefix": "n-", "cpu": 2000, "mem": 200000},
+        "pods": {"count": ns, "prefix": "s-", "cpu": 1000, "mem": 200000},
+        "candidates": {"count": npend, "prefix": "p-", "cpu": 1000, "mem": 2000000},
+        "expect": {"still_pending": npend},
+    })
+
 if __name__ == "__main__":
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_cases.json")
     with open(out, "w") as f:

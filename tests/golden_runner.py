@@ -9,6 +9,7 @@ from autoscaler_amd import k8s
 from autoscaler_amd.clustersnapshot import ClusterSnapshot, NodeInfo
 from autoscaler_amd.drain import ListerRegistry, NodeDeleteOptions
 from autoscaler_amd.estimator import BinpackingNodeEstimator, ThresholdBasedEstimationLimiter
+from autoscaler_amd.podlistprocessor import NewFilterOutSchedulablePodListProcessor
 from autoscaler_amd.predicatechecker import SchedulerBasedPredicateChecker
 from autoscaler_amd.simulator import HintingSimulator, RemovalSimulator
 
@@ -47,7 +48,14 @@ def build_pod(d: dict) -> k8s.Pod:
         p.owner_refs = [k8s.OwnerReference(kind, name, name)]
     if d.get("node"):
         p.node_name = d["node"]
+    if "priority" in d:
+        p.priority = d["priority"]
     return p
+
+
+def series(d: dict, build) -> list:
+    """{"count", "prefix", "cpu", "mem"}: count objects named prefix0, prefix1, ..."""
+    return [build({"name": f"{d['prefix']}{i}", "cpu": d["cpu"], "mem": d["mem"]}) for i in range(d["count"])]
 
 
 def expand_pods(spec) -> list:
@@ -141,4 +149,30 @@ def run_case(case: dict, make_backend):
         placed = sum(len(ni.pods) for ni in snap.List())
         if placed != len(case["pods"]) + len(got):
             errs.append(f"snapshot holds {placed} pods")
+    elif kind == "filter_out_schedulable":
+        snap.AddNodes([build_node(n) for n in case["nodes"]])
+        for pd in case["pods"]:
+            snap.AddPod(build_pod(pd), pd["node"])
+        snap.Fork()
+        proc = NewFilterOutSchedulablePodListProcessor(checker)
+        still = proc.filterOutSchedulableByPacking([build_pod(p) for p in case["candidates"]], snap)
+        e = case["expect"]
+        if sorted(p.name for p in still) != sorted(e["unscheduled"]):
+            errs.append(f"unschedulable {[p.name for p in still]} != {e['unscheduled']}")
+        got = sorted(p.name for ni in snap.List() for p in ni.pods)
+        want = sorted([p["name"] for p in case["pods"]] + e["scheduled"])
+        if got != want:
+            errs.append(f"scheduled {got} != {want}")
+    elif kind == "filter_out_schedulable_bench":
+        nodes = series(case["nodes"], build_node)
+        snap.AddNodes(nodes)
+        for i, p in enumerate(series(case["pods"], build_pod)):
+            snap.AddPod(p, nodes[i % len(nodes)].name)
+        pending = series(case["candidates"], build_pod)
+        proc = NewFilterOutSchedulablePodListProcessor(checker)
+        still = proc.filterOutSchedulableByPacking(pending, snap)
+        if len(still) != case["expect"]["still_pending"]:
+            errs.append(f"{len(still)} still pending != {case['expect']['still_pending']}")
+        if checker.evals != len(pending) * len(nodes):
+            errs.append(f"{checker.evals} evaluations != {len(pending) * len(nodes)}")
     return errs

@@ -7,30 +7,24 @@
 // CA/simulator/predicatechecker/schedulerbased.go:103-137 (FitsAnyNodeMatching's rotating
 // scan from lastIndex) and :139-185 (CheckPredicates).
 //
-// The reference is a sequential loop over the pods: a hint check, then (unless a similar
-// pod already failed) a rotating scan from lastIndex; a placed pod is added to the
-// snapshot before the next pod runs.  One persistent workgroup (16 waves) runs that loop
-// in speculative batches of FO_T pods, one pod per thread, every outcome computed against
-// the node rows as they were when the batch started:
-//   hint   CheckPredicates on the hinted node (findNodeWithHints);
-//   skip   the pod's class is already marked unschedulable (IsSimilarUnschedulable);
-//   short  a lane-private rotating scan of <= FO_SHORT_K positions from the pod's start,
-//          start = lastIndex + the positions the earlier pods of the batch advanced it by.
-//          The advances depend on the starts, so the starts are iterated to a fixed point
-//          (a landing further along shifts the later starts; rarely more than 2 rounds);
-//   long   nothing within FO_SHORT_K: a block-wide scan of the whole ring.  A scan of the
-//          whole ring that finds nothing does not depend on where it starts, and stays a
-//          failure whatever the earlier pods of the batch placed (placements only take
-//          resources, pod slots and ports away; the other filters read static node
-//          attributes), so failures commit in bulk.  A pod whose record equals an earlier
-//          failed pod's takes that result without scanning; a pod whose class an earlier
-//          failure of the batch marks is a skip.
-// The batch commits its longest prefix whose outcomes are exact.  It ends at the first pod
-// that (a) found a node with a long scan, (b) has an unconverged start, (c) read a node an
-// earlier pod of the batch placed on (its hinted node or a scanned position), (d) is the
-// first failure of a controller that can reach similar_pods' 10-class cap, or (e) fits
-// where an earlier failure of its class says it cannot.  That pod then runs alone,
-// block-wide, exactly as the reference's loop body, and the next batch starts after it.
+// The reference is one sequential loop: a pod's scan starts where the previous successful
+// scan stopped (lastIndex) and sees every earlier placement, so the pods are walked in
+// order.  One workgroup (16 waves) owns the node rows for the whole call:
+//   window     the SQ_WIN node rows from lastIndex on (hot, ext and static columns) live
+//              in LDS, updated there by the placements and written back when the window
+//              moves.  Consecutive scans continue where the previous one stopped, so the
+//              cursor walks the window and most scans never leave it;
+//   slots      the next SQ_SLOTS pods are staged in LDS: PodHot, the full record, the
+//              similar-pods mark of their class and a copy of their hinted node's rows;
+//   sequencer  wave 0 walks the staged pods: the hint check on the window row (or the
+//              staged copy), the similar-pods skip, then the scan over the window rows,
+//              64 positions per step (ballot of visible / fits: first fit wins, the
+//              evaluations are the visible positions up to it);
+//   block step when a scan runs off the window (or the slots are used up, or a class
+//              must be marked) all 16 waves take over: write back, scan the rest of the
+//              ring in parallel (SQ_RING positions in flight per thread, first fit by a
+//              min reduction), place or mark, reload the window at lastIndex and the slots.
+// Every pod's outcome, lastIndex and the evaluation count are exactly the reference loop's.
 #include "mirror.h"
 #include "device_filters.h"
 
@@ -38,27 +32,25 @@
 #include <chrono>
 #include <cstddef>
 #include <cstring>
+#include <string>
 
 namespace casim {
 
-constexpr int FO_T = 1024;             // pods per batch = threads of the workgroup
-constexpr int FO_W = FO_T / 64;
-constexpr int FO_SHORT_K = 4;          // positions of the lane-private scan
-constexpr int FO_ROUNDS = 4;           // fixed-point rounds of the starts
-constexpr int FO_HT = 2048;            // LDS hash slots (>= 2 * FO_T)
-constexpr int FO_HT_BITS = 11;
+constexpr int SQ_T = 1024;             // threads: wave 0 sequences, all waves run the block steps
+constexpr int SQ_W = SQ_T / 64;
+constexpr int SQ_WIN = 512;            // node positions resident in LDS
+constexpr int SQ_SLOTS = 64;           // pods staged per phase (one per sequencer lane)
+constexpr int SQ_RING = 16;            // positions per thread per pass of the block-wide ring scan
 constexpr int FO_MAX_PER_OWNER = 10;   // maxPodsPerOwnerRef, similar_pods.go:53
-static_assert((1 << FO_HT_BITS) == FO_HT, "FO_HT");
 
-constexpr int SPEC_WORDS = (int)(sizeof(ca_pod_spec) / 8);
-static_assert(sizeof(ca_pod_spec) % 8 == 0, "ca_pod_spec words");
-constexpr int SPEC_CLS_WORD = (int)(offsetof(ca_pod_spec, similar_class) / 8);
+enum : int32_t { CMD_DONE = 0, CMD_PHASE = 1, CMD_WINDOW = 2, CMD_RING = 3, CMD_MARK = 4 };
 
 struct FoCtl {
     int32_t L;                 // lastIndex in/out
     int32_t overflowing;       // controllers that overflowed the class cap
-    int32_t batches, cuts;
+    int32_t phases, steps;     // slot phases, block steps
     unsigned long long evals;
+    int32_t ring_scans, windows;
     int32_t bad_line, bad_val; // CASIM_FO_CHECKS builds: the first index check that failed
 };
 
@@ -81,7 +73,6 @@ struct FoArgs {
     const int32_t* cls_owner;  // per class: dense controller id (-1: none); NULL: no cap
     int32_t* owner_cnt;        // per controller: classes remembered
     uint8_t* owner_over;       // per controller: overflowed
-    unsigned long long* claim; // per node: (batch << 16) | (0xFFFF - position) of the earliest placement
     FoCtl* ctl;
     int32_t n_pods, n_classes, n_owners;
 };
@@ -99,152 +90,53 @@ __device__ inline int32_t fo_ck(const FoArgs& a, int32_t i, int32_t lim, int lin
 #define CK(i, lim) (i)
 #endif
 
-struct FoSmem {
-    int32_t red_i[FO_W];
-    unsigned long long red_u[FO_W];
-    unsigned long long fit[FO_W], vis[FO_W];
-    int32_t ckey[FO_HT], cval[FO_HT];               // class -> first failing position of the batch
-    unsigned long long skey[FO_HT];                 // record hash -> first long position
-    int32_t sval[FO_HT];
-    int16_t ulist[FO_T];                            // long pods that scan, in order
-    int32_t lstart[FO_T];                           // per position: start of its scan
-    uint32_t lev[FO_T];                             // per position: evaluations of its long scan
-    int32_t bcast;
+struct SqSmem {
+    NodeHot win_hot[SQ_WIN];
+    NodeExt win_ext[SQ_WIN];
+    NodeStatic win_st[SQ_WIN];
+    NodeHot slot_hot[SQ_SLOTS];
+    NodeExt slot_ext[SQ_SLOTS];
+    NodeStatic slot_st[SQ_SLOTS];
+    ca_pod_spec slot_spec[SQ_SLOTS];
+    PodHot slot_ph[SQ_SLOTS];
+    int32_t slot_node[SQ_SLOTS];     // hinted node position, -1 none
+    int32_t slot_cls[SQ_SLOTS];
+    uint8_t slot_mark[SQ_SLOTS];     // the class is marked unschedulable
+    uint8_t slot_dirty[SQ_SLOTS];
+    uint8_t win_dirty[SQ_WIN];
+    int32_t L, wb, wn, cur;          // lastIndex; window start position and length; cursor offset
+    int32_t k0, ns, j;               // phase: first pod, staged pods, next slot
+    int32_t cmd, arg;                // block step the sequencer asks for
+    int32_t succ;                    // some scan succeeded (lastIndex moved)
+    uint32_t carry;                  // CMD_RING: evaluations of the window part of the scan
+    int32_t red_i[SQ_W];
 };
 
 // ---- block primitives (all threads, uniform control flow) -----------------------
-__device__ inline int32_t fo_excl(FoSmem& sm, int32_t v, int32_t& total) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int32_t x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const int32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    __syncthreads();
-    if (lane == 63) sm.red_i[w] = x;
-    __syncthreads();
-    int32_t base = 0, tot = 0;
-    for (int k = 0; k < FO_W; k++) {
-        const int32_t s = sm.red_i[k];
-        base += (k < w) ? s : 0;
-        tot += s;
-    }
-    total = tot;
-    return base + x - v;
-}
-
-__device__ inline int32_t fo_min(FoSmem& sm, int32_t v) {
+__device__ inline int32_t sq_min(SqSmem& sm, int32_t v) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int o = 32; o; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
     __syncthreads();
     if (lane == 0) sm.red_i[w] = v;
     __syncthreads();
     int32_t m = INT32_MAX;
-    for (int k = 0; k < FO_W; k++) m = min(m, sm.red_i[k]);
+    for (int k = 0; k < SQ_W; k++) m = min(m, sm.red_i[k]);
     return m;
 }
-
-__device__ inline int32_t fo_max(FoSmem& sm, int32_t v) { return -fo_min(sm, -v); }
-
-__device__ inline unsigned long long fo_sum64(FoSmem& sm, unsigned long long v) {
+__device__ inline int32_t sq_sum(SqSmem& sm, int32_t v) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
     __syncthreads();
-    if (lane == 0) sm.red_u[w] = v;
+    if (lane == 0) sm.red_i[w] = v;
     __syncthreads();
-    unsigned long long s = 0;
-    for (int k = 0; k < FO_W; k++) s += sm.red_u[k];
+    int32_t s = 0;
+    for (int k = 0; k < SQ_W; k++) s += sm.red_i[k];
     return s;
 }
 
-// ---- LDS hash tables (open addressing; at most FO_T keys per batch) -------------
-__device__ inline void ht_min_i(int32_t* keys, int32_t* vals, int32_t key, int32_t v) {
-    uint32_t sl = ((uint32_t)key * 2654435761u) >> (32 - FO_HT_BITS);
-    while (true) {
-        const int32_t old = atomicCAS(&keys[sl], -1, key);
-        if (old == -1 || old == key) { atomicMin(&vals[sl], v); return; }
-        sl = (sl + 1) & (FO_HT - 1);
-    }
-}
-__device__ inline int32_t ht_get_i(const int32_t* keys, const int32_t* vals, int32_t key) {
-    uint32_t sl = ((uint32_t)key * 2654435761u) >> (32 - FO_HT_BITS);
-    while (true) {
-        const int32_t k = keys[sl];
-        if (k == key) return vals[sl];
-        if (k == -1) return INT32_MAX;
-        sl = (sl + 1) & (FO_HT - 1);
-    }
-}
-__device__ inline void ht_min_u(unsigned long long* keys, int32_t* vals, unsigned long long key, int32_t v) {
-    uint32_t sl = (uint32_t)(key >> (64 - FO_HT_BITS));
-    while (true) {
-        const unsigned long long old = atomicCAS(&keys[sl], 0ull, key);
-        if (old == 0ull || old == key) { atomicMin(&vals[sl], v); return; }
-        sl = (sl + 1) & (FO_HT - 1);
-    }
-}
-__device__ inline int32_t ht_get_u(const unsigned long long* keys, const int32_t* vals, unsigned long long key) {
-    uint32_t sl = (uint32_t)(key >> (64 - FO_HT_BITS));
-    while (true) {
-        const unsigned long long k = keys[sl];
-        if (k == key) return vals[sl];
-        if (k == 0ull) return INT32_MAX;
-        sl = (sl + 1) & (FO_HT - 1);
-    }
-}
-
-// hash of a pod record without its similar_class (two pods with equal records get equal
-// filter results on every node); never 0
-__device__ inline unsigned long long spec_hash(const ca_pod_spec* s) {
-    const unsigned long long* w = reinterpret_cast<const unsigned long long*>(s);
-    unsigned long long h = 0x9E3779B97F4A7C15ull;
-    for (int i = 0; i < SPEC_WORDS; i++) {
-        unsigned long long x = w[i];
-        if (i == SPEC_CLS_WORD) x &= (offsetof(ca_pod_spec, similar_class) % 8) ? 0x00000000FFFFFFFFull
-                                                                                    : 0xFFFFFFFF00000000ull;
-        h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
-        h *= 0xBF58476D1CE4E5B9ull;
-    }
-    return h | 1ull;
-}
-__device__ inline bool spec_equal(const ca_pod_spec* a, const ca_pod_spec* b) {
-    const unsigned long long* x = reinterpret_cast<const unsigned long long*>(a);
-    const unsigned long long* y = reinterpret_cast<const unsigned long long*>(b);
-    const unsigned long long m = (offsetof(ca_pod_spec, similar_class) % 8) ? 0x00000000FFFFFFFFull
-                                                                             : 0xFFFFFFFF00000000ull;
-    bool eq = true;
-    for (int i = 0; i < SPEC_WORDS; i++) {
-        const unsigned long long mm = (i == SPEC_CLS_WORD) ? m : ~0ull;
-        eq &= ((x[i] ^ y[i]) & mm) == 0;
-    }
-    return eq;
-}
-
-// ---- filters ------------------------------------------------------------------------
-__device__ inline bool fo_names_ok(const ca_pod_spec& s, const int32_t* names, int32_t name_id) {
-    bool ok = false;
-    for (int32_t k = 0; k < s.prefilter_count; k++) ok |= names[s.prefilter_first + k] == name_id;
-    return ok;
-}
-// FitsAnyNodeMatching visits the node (schedulerbased.go:116-127): PreFilter's NodeNames
-// and Spec.Unschedulable skip a node without running the filters
-__device__ inline bool fo_visible(const FoArgs& a, const PodHot& p, const ca_pod_spec& s, const NodeHot& h,
-                                  int32_t pos) {
-    if (h.flags & NF_UNSCHED) return false;
-    if (p.flags & PF_PREFILTER_NAMES) return fo_names_ok(s, a.names, a.st[CK(pos, a.n)].name_id);
-    return true;
-}
-__device__ inline bool fo_fits(const FoArgs& a, const PodHot& p, const ca_pod_spec& s, const NodeHot& h,
-                               int32_t pos, bool apply_unsched) {
-    uint32_t r;
-    pos = CK(pos, a.n);
-    return dev_full_filters(s, p, a.terms, a.reqs, h, a.ext + pos, a.st + pos, apply_unsched, &r) == CA_PLUGIN_NONE;
-}
-
-// Rows, marks and counters this kernel writes are read with device-coherent loads where
-// the address is uniform: a uniform plain load may be served from the scalar cache, which
-// the kernel's own vector stores do not update (waves could then disagree on a branch that
-// must be block-uniform).
+// The mutable columns (hot, ext), the marks and the counters are read with device-coherent
+// loads: a uniform plain load may be served from the scalar cache, which the kernel's own
+// vector stores do not update, and the coherent form also skips a stale vector-L1 line.
 template <class T>
 __device__ inline T ld_coh(const T* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -274,23 +166,37 @@ __device__ inline uint8_t ld_mark(const uint8_t* p) {
     return (uint8_t)(w >> (8 * (a & 3)));
 }
 
-// AddPod on the device rows (NodeInfo.AddPod's resource/port update, SF/types.go:672-692)
-__device__ inline void fo_place(const FoArgs& a, const PodHot& p, const ca_pod_spec& s, int32_t node) {
-    node = CK(node, a.n);
-    NodeHot* h = a.hot + node;
-    const NodeHot cur = ld_hot_coh(h);        // fo_single's address is uniform: no scalar-cache read
-    h->cpu = wsub(cur.cpu, p.cpu);
-    h->mem = wsub(cur.mem, p.mem);
-    h->eph = wsub(cur.eph, p.eph);
-    h->pods = cur.pods - 1;
+// ---- filters ------------------------------------------------------------------------
+// FitsAnyNodeMatching visits the node (schedulerbased.go:116-127): PreFilter's NodeNames
+// and Spec.Unschedulable skip a node without running the filters
+__device__ inline bool sq_visible(const FoArgs& a, const PodHot& p, const ca_pod_spec& s, const NodeHot& h,
+                                  const NodeStatic& st) {
+    if (h.flags & NF_UNSCHED) return false;
+    if (p.flags & PF_PREFILTER_NAMES) {
+        bool ok = false;
+        for (int32_t k = 0; k < s.prefilter_count; k++) ok |= a.names[s.prefilter_first + k] == st.name_id;
+        return ok;
+    }
+    return true;
+}
+__device__ inline bool sq_fits(const FoArgs& a, const PodHot& p, const ca_pod_spec& s, const NodeHot& h,
+                               const NodeExt* e, const NodeStatic* st, bool apply_unsched) {
+    uint32_t r;
+    return dev_full_filters(s, p, a.terms, a.reqs, h, e, st, apply_unsched, &r) == CA_PLUGIN_NONE;
+}
+
+// AddPod's resource / port update (NodeInfo.AddPod, SF/types.go:672-692) on one row
+__device__ inline void sq_place_row(NodeHot& h, NodeExt& e, const PodHot& p, const ca_pod_spec& s) {
+    h.cpu = wsub(h.cpu, p.cpu);
+    h.mem = wsub(h.mem, p.mem);
+    h.eph = wsub(h.eph, p.eph);
+    h.pods = h.pods - 1;
     uint64_t pu = 0;
     for (int w = 0; w < CA_PORT_WORDS; w++) pu |= s.port_use[w];
     if (pu || (p.flags & PF_SCALAR_REQ)) {
-        NodeExt* e = a.ext + node;
-        const NodeExt ce = ld_ext_coh(e);
-        for (int w = 0; w < CA_PORT_WORDS; w++) e->ports[w] = ce.ports[w] | s.port_use[w];
-        for (int k = 0; k < CA_MAX_SCALAR; k++) e->scalar[k] = wsub(ce.scalar[k], s.req_scalar[k]);
-        if (pu) h->flags = cur.flags | NF_PORTS;
+        for (int w = 0; w < CA_PORT_WORDS; w++) e.ports[w] |= s.port_use[w];
+        for (int k = 0; k < CA_MAX_SCALAR; k++) e.scalar[k] = wsub(e.scalar[k], s.req_scalar[k]);
+        if (pu) h.flags |= NF_PORTS;
     }
 }
 
@@ -314,313 +220,368 @@ __device__ inline void fo_mark(const FoArgs& a, int32_t c) {
     a.owner_cnt[o] = ld_coh(&a.owner_cnt[o]) + 1;
 }
 
-// FitsAnyNode's rotating scan of the whole ring from `start`, block-wide: the first node
-// that fits (-1: none) and the evaluations up to it (every visible node if none fits)
-__device__ void fo_ring_scan(const FoArgs& a, FoSmem& sm, const PodHot& p, const ca_pod_spec& s, int32_t start,
-                             int32_t& found, uint32_t& evs) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+// ---- block steps ----------------------------------------------------------------------
+// dirty window rows and staged copies back to HBM
+__device__ void sq_write_back(const FoArgs& a, SqSmem& sm) {
+    const int32_t n = a.n, wb = sm.wb, wn = sm.wn;
+    for (int32_t o = (int32_t)threadIdx.x; o < wn; o += SQ_T) {
+        if (sm.win_dirty[o]) {
+            int32_t pos = wb + o;
+            if (pos >= n) pos -= n;
+            pos = CK(pos, n);
+            a.hot[pos] = sm.win_hot[o];
+            a.ext[pos] = sm.win_ext[o];
+            sm.win_dirty[o] = 0;
+        }
+    }
+    const int32_t t = (int32_t)threadIdx.x;
+    if (t < sm.ns && sm.slot_dirty[t]) {
+        const int32_t pos = CK(sm.slot_node[t], n);
+        a.hot[pos] = sm.slot_hot[t];          // every dirty copy of a node holds the same row
+        a.ext[pos] = sm.slot_ext[t];
+        sm.slot_dirty[t] = 0;
+    }
+    __threadfence();                          // the rows are in L2 before any coherent re-read
+    __syncthreads();
+}
+
+// the window: SQ_WIN rows from position L (all three columns)
+__device__ void sq_load_window(const FoArgs& a, SqSmem& sm, int32_t L) {
+    const int32_t n = a.n;
+    const int32_t wn = min(SQ_WIN, n);
+    for (int32_t o = (int32_t)threadIdx.x; o < wn; o += SQ_T) {
+        int32_t pos = L + o;
+        if (pos >= n) pos -= n;
+        pos = CK(pos, n);
+        sm.win_hot[o] = ld_hot_coh(a.hot + pos);
+        sm.win_ext[o] = ld_ext_coh(a.ext + pos);
+        sm.win_st[o] = a.st[pos];
+        sm.win_dirty[o] = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        sm.wb = L;
+        sm.wn = wn;
+        sm.cur = 0;
+    }
+    __syncthreads();
+}
+
+// stage pods k0 .. k0+ns-1 (full: their records too; else only the hinted rows and marks
+// of the slots from sm.j on)
+__device__ void sq_load_slots(const FoArgs& a, SqSmem& sm, bool full) {
+    const int32_t t = (int32_t)threadIdx.x;
+    const int32_t n = a.n;
+    if (full) {
+        constexpr int SW = (int)(sizeof(ca_pod_spec) / 8);
+        static_assert(sizeof(ca_pod_spec) % 8 == 0, "ca_pod_spec words");
+        for (int32_t x = t; x < sm.ns * SW; x += SQ_T) {
+            const int32_t j = x / SW, w = x % SW;
+            const int32_t i = CK(a.order[CK(sm.k0 + j, a.P)], a.n_pods);
+            const PodHot ph = a.ph[i];
+            reinterpret_cast<unsigned long long*>(&sm.slot_spec[j])[w] =
+                reinterpret_cast<const unsigned long long*>(a.specs + CK(ph.spec, a.n_pods))[w];
+            if (w == 0) sm.slot_ph[j] = ph;
+        }
+        __syncthreads();
+    }
+    if (t >= sm.j && t < sm.ns) {
+        const int32_t k = sm.k0 + t;
+        const int32_t h = a.hints[CK(k, a.P)];
+        const int32_t node = (h >= 0 && h < n) ? h : -1;
+        sm.slot_node[t] = node;
+        if (node >= 0) {
+            sm.slot_hot[t] = ld_hot_coh(a.hot + node);
+            sm.slot_ext[t] = ld_ext_coh(a.ext + node);
+            sm.slot_st[t] = a.st[node];
+        }
+        const int32_t c = sm.slot_spec[t].similar_class;
+        sm.slot_cls[t] = c;
+        sm.slot_mark[t] = (c >= 0) ? ld_mark(&a.cls_mark[CK(c, a.n_classes)]) : 0;
+        sm.slot_dirty[t] = 0;
+    }
+    __syncthreads();
+}
+
+// the rest of a pod's ring: R positions from X, block-wide.  First fitting offset (-1:
+// none) and the visible positions up to it (every visible position if none fits).
+__device__ void sq_ring_scan(const FoArgs& a, SqSmem& sm, const PodHot& p, const ca_pod_spec& s, int32_t X,
+                             int32_t R, int32_t& found, uint32_t& evs) {
     const int32_t n = a.n;
     found = -1;
     evs = 0;
-    for (int32_t base = 0; base < n; base += FO_T) {
-        const int32_t off = base + (int32_t)threadIdx.x;
-        bool vis = false, fit = false;
-        if (off < n) {
-            int32_t pos = start + off;
-            if (pos >= n) pos -= n;
-            pos = CK(pos, n);
-            const NodeHot h = a.hot[pos];
-            vis = fo_visible(a, p, s, h, pos);
-            fit = vis && fo_fits(a, p, s, h, pos, false);
-        }
-        const unsigned long long fm = __ballot(fit), vm = __ballot(vis);
-        __syncthreads();
-        if (lane == 0) { sm.fit[w] = fm; sm.vis[w] = vm; }
-        __syncthreads();
-        bool done = false;
-        uint32_t cnt = 0;
-        for (int k = 0; k < FO_W && !done; k++) {
-            const unsigned long long f = sm.fit[k], v = sm.vis[k];
-            if (f) {
-                const int l = __builtin_ctzll(f);
-                cnt += (uint32_t)__builtin_popcountll(v & ((2ull << l) - 1ull));
-                found = base + k * 64 + l;
-                done = true;
-            } else {
-                cnt += (uint32_t)__builtin_popcountll(v);
-            }
-        }
-        evs += cnt;
-        if (done) break;
-    }
-    if (found >= 0) {
-        found += start;
-        if (found >= n) found -= n;
-    }
-}
-
-// the reference's loop body for one pod, block-wide (hinting_simulator.go:63-86)
-__device__ void fo_single(const FoArgs& a, FoSmem& sm, int32_t k, int32_t& L, unsigned long long& evals) {
-    const int32_t n = a.n;
-    k = CK(k, a.P);
-    const PodHot p = a.ph[CK(a.order[k], a.n_pods)];
-    const ca_pod_spec& s = a.specs[CK(p.spec, a.n_pods)];
-    const int32_t h = a.hints[k];
-    const int32_t c = s.similar_class;
-    // the block-uniform decisions are taken by thread 0 on coherent loads and broadcast:
-    // 1 the hinted node fits (findNodeWithHints), 2 the class is marked (a skip), 0 scan
-    if (threadIdx.x == 0) {
-        int32_t dec = 0;
-        if (h >= 0 && h < n && !(p.flags & PF_PREFILTER_FAIL)) {
-            evals++;
-            const NodeHot hh = ld_hot_coh(a.hot + h);
-            const NodeExt he = ld_ext_coh(a.ext + h);
-            uint32_t r;
-            if (dev_full_filters(s, p, a.terms, a.reqs, hh, &he, a.st + h, true, &r) == CA_PLUGIN_NONE) dec = 1;
-        }
-        if (dec == 0 && c >= 0 && ld_mark(&a.cls_mark[CK(c, a.n_classes)])) dec = 2;
-        sm.bcast = dec;
-    }
-    __syncthreads();
-    const int32_t dec = sm.bcast;
-    __syncthreads();
-    int32_t node = (dec == 1) ? h : -1;
-    if (node < 0) {                                                     // findNode
-        if (dec != 2) {
-            int32_t found = -1;
-            uint32_t ev = 0;
-            if (!(p.flags & PF_PREFILTER_FAIL) && n > 0) fo_ring_scan(a, sm, p, s, L % n, found, ev);
-            if (threadIdx.x == 0) evals += ev;
-            if (found >= 0) {
-                node = found;
-                L = (found + 1 == n) ? 0 : found + 1;                   // schedulerbased.go:131
-            } else if (c >= 0 && !(p.flags & PF_DAEMONSET) && threadIdx.x == 0) {
-                fo_mark(a, c);
-            }
-        }
-    }
-    if (threadIdx.x == 0) {
-        a.out_node[k] = node;
-        if (node >= 0) {
-            a.hints[k] = node;
-            fo_place(a, p, s, node);
-        }
-    }
-    __syncthreads();
-}
-
-__device__ inline unsigned long long claim_key(unsigned long long gen, int32_t j) {
-    return (gen << 16) | (unsigned long long)(0xFFFF - j);
-}
-// an earlier pod of batch `gen` placed on `pos`
-__device__ inline bool claimed_before(const FoArgs& a, int32_t pos, unsigned long long gen, int32_t j) {
-    pos = CK(pos, a.n);
-    const unsigned long long c = __hip_atomic_load(&a.claim[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return (c >> 16) == gen && (int32_t)(0xFFFF - (c & 0xFFFF)) < j;
-}
-
-__global__ void __launch_bounds__(FO_T) k_filter_out(FoArgs a) {
-    __shared__ FoSmem sm;
-    const int32_t tid = (int32_t)threadIdx.x;
-    const int32_t n = a.n, P = a.P;
-    int32_t L = a.ctl->L;
-    bool any_success = false;
-    unsigned long long evals = 0;
-    int32_t batches = 0, cuts = 0;
-    unsigned long long gen = 0;
-    for (int32_t k0 = 0; k0 < P;) {
-        gen++;
-        batches++;
-        const int32_t nb = min(FO_T, P - k0);
-        const int32_t k = k0 + tid;
-        const bool valid = tid < nb;
-        for (int x = tid; x < FO_HT; x += FO_T) {
-            sm.ckey[x] = -1; sm.cval[x] = INT32_MAX;
-            sm.skey[x] = 0ull; sm.sval[x] = INT32_MAX;
-        }
-        sm.lev[tid] = 0;
-        PodHot p = {};
-        const ca_pod_spec* sp = a.specs;
-        int32_t cls = -1, h = -1;
-        if (valid) {
-            p = a.ph[CK(a.order[CK(k, P)], a.n_pods)];
-            sp = a.specs + CK(p.spec, a.n_pods);
-            cls = sp->similar_class;
-            if (cls >= 0) cls = CK(cls, a.n_classes);
-            h = a.hints[k];
-        }
-        const ca_pod_spec& s = *sp;
-        const bool ds = (p.flags & PF_DAEMONSET) != 0;
-        // findNodeWithHints on the batch-start rows
-        uint32_t ev = 0;
-        bool hint_ok = false;
-        if (valid && h >= 0 && h < n && !(p.flags & PF_PREFILTER_FAIL)) {
-            ev = 1;
-            hint_ok = fo_fits(a, p, s, a.hot[CK(h, n)], h, true);
-        }
-        const bool skip0 = valid && !hint_ok && cls >= 0 && a.cls_mark[cls];
-        const bool active = valid && !hint_ok && !skip0;                     // runs FitsAnyNode
-        const bool pff = active && ((p.flags & PF_PREFILTER_FAIL) || n == 0); // fails without a scan
-        const bool scanner = active && !pff;
-        const int32_t Lr = n > 0 ? L % n : 0;
-#ifdef CASIM_FO_CHECKS
-        if (n > 0) CK(Lr, n);
-#endif
-        // lane-private short scans, starts iterated to a fixed point
-        int32_t adv = scanner ? 1 : 0, start = 0, start_ev = -1, fnode = -1;
-        uint32_t sev = 0;
-        bool sfound = false;
-        for (int r = 0;; r++) {
-            int32_t tot;
-            const int32_t ex = fo_excl(sm, adv, tot);
-#ifdef CASIM_FO_CHECKS
-            CK(adv, FO_SHORT_K + 1);
-            {
-                __syncthreads();
-                sm.lstart[tid] = adv;
-                __syncthreads();
-                int32_t ex2 = 0, t2 = 0;
-                for (int j = 0; j < FO_T; j++) { ex2 += (j < tid) ? sm.lstart[j] : 0; t2 += sm.lstart[j]; }
-                __syncthreads();
-                if (ex2 != ex || t2 != tot) {
-                    if (atomicCAS(&a.ctl->bad_line, 0, __LINE__) == 0)
-                        a.ctl->bad_val = tid * 1000000 + (ex2 - ex) * 1000 + r;
-                }
-            }
-#endif
-            if (scanner) start = (int32_t)(((int64_t)Lr + ex) % n);
-            const bool ch = scanner && start != start_ev;
-            if (fo_min(sm, ch ? 0 : 1) != 0 || r == FO_ROUNDS) break;
-            if (ch) {
-                start_ev = start;
-                sfound = false;
-                sev = 0;
-                int32_t pos = start;
-                const int32_t lim = min(FO_SHORT_K, n);
-                for (int t = 0; t < lim; t++) {
-                    const NodeHot hh = a.hot[CK(pos, n)];
-                    if (fo_visible(a, p, s, hh, pos)) {
-                        sev++;
-                        if (fo_fits(a, p, s, hh, pos, false)) {
-                            sfound = true;
-                            fnode = pos;
-                            adv = t + 1;
-                            break;
-                        }
+    for (int32_t base = 0; base < R; base += SQ_T * SQ_RING) {
+        uint32_t vis = 0, fit = 0;
+#pragma unroll
+        for (int i = 0; i < SQ_RING; i++) {
+            const int32_t off = base + i * SQ_T + (int32_t)threadIdx.x;
+            if (off < R) {
+                int32_t pos = X + off;
+                if (pos >= n) pos -= n;
+                pos = CK(pos, n);
+                const NodeHot h = ld_hot_coh(a.hot + pos);
+                const bool v = sq_visible(a, p, s, h, a.st[pos]);
+                vis |= (uint32_t)v << i;
+                if (v) {
+                    bool ok;
+                    if (((p.flags & PF_PORTS) && (h.flags & NF_PORTS)) || (p.flags & PF_SCALAR_REQ)) {
+                        const NodeExt e = ld_ext_coh(a.ext + pos);
+                        ok = sq_fits(a, p, s, h, &e, a.st + pos, false);
+                    } else {
+                        ok = sq_fits(a, p, s, h, a.ext + pos, a.st + pos, false);   // ext unread
                     }
-                    if (++pos == n) pos = 0;
-                }
-                if (!sfound) adv = 0;
-            }
-        }
-        int32_t b = fo_min(sm, (scanner && sfound && start != start_ev) ? tid : INT32_MAX);   // (b)
-        b = min(b, nb);
-        // long pods before b: dedup by class (a later pod of a class whose earlier long pod
-        // failed is a skip) and by record; the rest scan the whole ring, in order
-        const bool is_long = scanner && !sfound && tid < b;
-        if ((is_long || (pff && tid < b)) && cls >= 0 && !ds) ht_min_i(sm.ckey, sm.cval, cls, tid);
-        if (is_long) sm.lstart[tid] = start;
-        __syncthreads();
-        // first failing candidate of the class (a long or PreFilter-failed pod)
-        const int32_t first = (cls >= 0) ? ht_get_i(sm.ckey, sm.cval, cls) : INT32_MAX;
-        const bool cdup = is_long && cls >= 0 && !ds && first < tid;   // a skip once its class failed
-        unsigned long long shash = 0;
-        if (is_long && !cdup) {
-            shash = spec_hash(sp);
-            ht_min_u(sm.skey, sm.sval, shash, tid);
-        }
-        __syncthreads();
-        int32_t rep = -1;          // the earlier long pod with an equal record
-        if (is_long && !cdup) {
-            const int32_t f = ht_get_u(sm.skey, sm.sval, shash);
-            if (f < tid && spec_equal(sp, a.specs + CK(a.ph[CK(a.order[CK(k0 + f, P)], a.n_pods)].spec, a.n_pods)))
-                rep = f;
-        }
-        const bool uniq = is_long && !cdup && rep < 0;
-        int32_t nu;
-        const int32_t ui = fo_excl(sm, uniq ? 1 : 0, nu);
-        if (uniq) sm.ulist[CK(ui, FO_T)] = (int16_t)tid;
-        __syncthreads();
-        int32_t b_long = INT32_MAX;
-        for (int32_t x = 0; x < nu; x++) {
-            const int32_t j = CK(sm.ulist[CK(x, FO_T)], FO_T);
-            const PodHot pj = a.ph[CK(a.order[CK(k0 + j, P)], a.n_pods)];
-            int32_t found;
-            uint32_t evs;
-            fo_ring_scan(a, sm, pj, a.specs[CK(pj.spec, a.n_pods)], CK(sm.lstart[j], n), found, evs);
-            if (found >= 0) { b_long = j; break; }                                    // (a)
-            if (tid == 0) sm.lev[j] = evs;
-        }
-        __syncthreads();
-        b = min(b, b_long);
-        // outcomes before b
-        uint32_t lev = 0;
-        if (is_long && tid < b && !cdup) lev = sm.lev[rep >= 0 ? rep : tid];
-        const bool fail = tid < b && (pff || (is_long && !cdup));
-        const bool marks = fail && cls >= 0 && !ds && first == tid;
-        bool cut = false;
-        if (marks && a.cls_capped[cls]) cut = true;                                     // (d)
-        if (sfound && first < tid) cut = true;                                           // (e)
-        const bool pskip = fail && !ds && cls >= 0 && first < tid;                       // class failed earlier
-        b = min(b, fo_min(sm, (cut && tid < b) ? tid : INT32_MAX));
-        // placements before b: claim the nodes, then check every pod's reads
-        const int32_t place = (tid < b) ? (hint_ok ? h : (sfound ? fnode : -1)) : -1;
-        if (place >= 0) atomicMax(&a.claim[CK(place, n)], claim_key(gen, tid));
-        __builtin_amdgcn_s_waitcnt(0);         // the claims are performed before the barrier
-        __syncthreads();
-        bool coll = false;
-        if (tid < b) {
-            if (hint_ok) coll = claimed_before(a, h, gen, tid);
-            if (sfound) {
-                int32_t pos = start_ev;
-                for (int32_t t = 0; t < n; t++) {
-                    coll |= claimed_before(a, pos, gen, tid);
-                    if (pos == fnode) break;
-                    if (++pos == n) pos = 0;
-#ifdef CASIM_FO_CHECKS
-                    if (t == FO_SHORT_K) CK(-1 - t, 0);           // the short scan covers <= FO_SHORT_K
-#endif
+                    if (ok) fit |= 1u << i;
                 }
             }
         }
-        b = min(b, fo_min(sm, coll ? tid : INT32_MAX));                                  // (c)
-        // commit the prefix [0, b)
-        if (tid < b) {
-            const int32_t node = hint_ok ? h : (sfound ? fnode : -1);
-            a.out_node[k] = node;
-            evals += ev + (sfound ? sev : 0) + ((fail && !pskip) ? lev : 0);
-            if (node >= 0) {
-                a.hints[k] = node;
-                fo_place(a, p, s, node);
-            }
-            if (marks) a.cls_mark[CK(cls, a.n_classes)] = 1;
+        // offsets of this thread are base + i * SQ_T + tid, increasing in i
+        const int32_t mine = fit ? base + __builtin_ctz(fit) * SQ_T + (int32_t)threadIdx.x : INT32_MAX;
+        const int32_t f = sq_min(sm, mine);
+        int32_t cnt = 0;
+#pragma unroll
+        for (int i = 0; i < SQ_RING; i++) {
+            const int32_t off = base + i * SQ_T + (int32_t)threadIdx.x;
+            cnt += (((vis >> i) & 1u) && off <= f) ? 1 : 0;
         }
-        __builtin_amdgcn_s_waitcnt(0);         // row updates performed before the next reads
-        const int32_t last = fo_max(sm, (tid < b && sfound) ? tid : -1);
-        if (last >= 0) {
-            if (tid == last) sm.bcast = fnode;
-            __syncthreads();
-            const int32_t f = CK(sm.bcast, n);
-            L = (f + 1 == n) ? 0 : f + 1;
-            any_success = true;
-        }
-        __syncthreads();
-        if (b < nb) {
-            const int32_t L0 = L;
-            fo_single(a, sm, k0 + b, L, evals);
-            if (L != L0) any_success = true;
-            cuts++;
-            k0 += b + 1;
-        } else {
-            k0 += nb;
+        evs += (uint32_t)sq_sum(sm, cnt);
+        if (f != INT32_MAX) {
+            found = f;
+            break;
         }
     }
-    const unsigned long long tot = fo_sum64(sm, evals);
+}
+
+// ---- the sequencer (wave 0) ----------------------------------------------------------
+// Walks slots sm.j .. sm.ns-1 and stops at the first pod that needs a block step.
+__device__ void sq_sequence(const FoArgs& a, SqSmem& sm, unsigned long long& evals) {
+    const int lane = (int)threadIdx.x;       // wave 0
+    const int32_t n = a.n, ns = sm.ns, k0 = sm.k0;
+    const int32_t wb = sm.wb, wn = sm.wn;
+    int32_t j = sm.j, L = sm.L, cur = sm.cur;
+    bool succ = false;
+    int32_t cmd = (k0 + ns >= a.P) ? CMD_DONE : CMD_PHASE, arg = 0;
+    for (; j < ns; j++) {
+        if (n > 0 && cur >= wn) { cmd = CMD_WINDOW; break; }   // the cursor ran off the window
+        const int32_t k = k0 + j;
+        const PodHot& p = sm.slot_ph[j];
+        const ca_pod_spec& s = sm.slot_spec[j];
+        const uint32_t pf = p.flags;
+        const int32_t h = sm.slot_node[j];
+        int32_t node = -1;
+        if (h >= 0 && !(pf & PF_PREFILTER_FAIL)) {            // findNodeWithHints (:91-108)
+            if (lane == 0) evals++;
+            int32_t ho = h - wb;
+            if (ho < 0) ho += n;
+            const bool inw = ho < wn;
+            bool ok;
+            if (inw) ok = sq_fits(a, p, s, sm.win_hot[ho], &sm.win_ext[ho], &sm.win_st[ho], true);
+            else ok = sq_fits(a, p, s, sm.slot_hot[j], &sm.slot_ext[j], &sm.slot_st[j], true);
+            if (ok) {
+                node = h;
+                if (inw) {
+                    if (lane == 0) {
+                        sq_place_row(sm.win_hot[ho], sm.win_ext[ho], p, s);
+                        sm.win_dirty[ho] = 1;
+                    }
+                } else if (lane < ns && sm.slot_node[lane] == h) {
+                    // every live staged copy of the node takes the pod; the copies of the slots
+                    // already walked are superseded (never read again, never written back)
+                    if (lane >= j) {
+                        sq_place_row(sm.slot_hot[lane], sm.slot_ext[lane], p, s);
+                        sm.slot_dirty[lane] = 1;
+                    } else {
+                        sm.slot_dirty[lane] = 0;
+                    }
+                }
+            }
+        }
+        if (node < 0 && !sm.slot_mark[j]) {                   // findNode (:110-125)
+            const int32_t c = sm.slot_cls[j];
+            const bool can_mark = c >= 0 && !(pf & PF_DAEMONSET);
+            if ((pf & PF_PREFILTER_FAIL) || n == 0) {          // fails without a scan
+                if (can_mark) {
+                    if (lane == 0) a.out_node[k] = -1;
+                    cmd = CMD_MARK;
+                    arg = j++;
+                    break;
+                }
+            } else {
+                // the scan over the window from the cursor, 64 positions a step
+                uint32_t ev = 0;
+                int32_t fo = -1;
+                const int32_t lim = (wn == n) ? cur + n : wn;     // whole ring resident: wrap inside
+                for (int32_t base = cur; base < lim; base += 64) {
+                    int32_t o = base + lane;
+                    bool vis = false, fit = false;
+                    if (o < lim) {
+                        if (o >= wn) o -= wn;
+                        const NodeHot hh = sm.win_hot[o];
+                        vis = sq_visible(a, p, s, hh, sm.win_st[o]);
+                        fit = vis && sq_fits(a, p, s, hh, &sm.win_ext[o], &sm.win_st[o], false);
+                    }
+                    const unsigned long long fm = __ballot(fit), vm = __ballot(vis);
+                    if (fm) {
+                        const int l = __builtin_ctzll(fm);
+                        ev += (uint32_t)__builtin_popcountll(vm & ((2ull << l) - 1ull));
+                        fo = base + l;
+                        if (fo >= wn) fo -= wn;
+                        break;
+                    }
+                    ev += (uint32_t)__builtin_popcountll(vm);
+                }
+                if (fo >= 0) {
+                    if (lane == 0) {
+                        evals += ev;
+                        sq_place_row(sm.win_hot[fo], sm.win_ext[fo], p, s);
+                        sm.win_dirty[fo] = 1;
+                    }
+                    int32_t f = wb + fo;
+                    if (f >= n) f -= n;
+                    node = f;
+                    L = (f + 1 == n) ? 0 : f + 1;                 // schedulerbased.go:131
+                    succ = true;
+                    cur = fo + 1;
+                    if (wn == n && cur == n) cur = 0;            // whole ring resident: keep walking
+                } else if (wn == n) {                            // the whole ring: no node fits
+                    if (lane == 0) evals += ev;
+                    if (can_mark) {
+                        if (lane == 0) a.out_node[k] = -1;
+                        cmd = CMD_MARK;
+                        arg = j++;
+                        break;
+                    }
+                } else {                                         // the rest of the ring: block step
+                    if (lane == 0) sm.carry = ev;
+                    cmd = CMD_RING;
+                    arg = j;
+                    break;
+                }
+            }
+        }
+        if (lane == 0) {
+            a.out_node[k] = node;
+            if (node >= 0) a.hints[k] = node;                  // Hints.Set (:95, :123)
+        }
+    }
+    if (lane == 0) {
+        sm.j = j;
+        sm.L = L;
+        sm.cur = cur;
+        sm.cmd = cmd;
+        sm.arg = arg;
+        if (succ) sm.succ = 1;
+    }
+}
+
+__global__ void __launch_bounds__(SQ_T) k_filter_out(FoArgs a) {
+    __shared__ SqSmem sm;
+    const int32_t tid = (int32_t)threadIdx.x;
+    const int32_t n = a.n;
+    unsigned long long evals = 0;           // thread 0 (= the sequencer's lane 0)
+    int32_t phases = 1, steps = 0, rings = 0, windows = 0;
     if (tid == 0) {
-        if (any_success) a.ctl->L = L;
-        a.ctl->evals = tot;
-        a.ctl->batches = batches;
-        a.ctl->cuts = cuts;
+        int32_t L0 = (n > 0) ? a.ctl->L % n : 0;
+        if (L0 < 0) L0 += n;
+        sm.L = L0;
+        sm.k0 = 0;
+        sm.ns = min(SQ_SLOTS, a.P);
+        sm.j = 0;
+        sm.succ = 0;
+        sm.wb = 0;
+        sm.wn = 0;
+        sm.cur = 0;
+    }
+    __syncthreads();
+    if (n > 0) sq_load_window(a, sm, sm.L);
+    sq_load_slots(a, sm, true);
+    while (true) {
+        if (tid < 64) sq_sequence(a, sm, evals);
+        __syncthreads();
+        const int32_t cmd = sm.cmd;
+        if (cmd != CMD_DONE) steps++;
+        if (cmd == CMD_MARK) {
+            const int32_t c = sm.slot_cls[sm.arg];
+            if (tid == 0) fo_mark(a, c);
+            __threadfence();
+            __syncthreads();
+            if (tid < sm.ns && sm.slot_cls[tid] == c) sm.slot_mark[tid] = ld_mark(&a.cls_mark[CK(c, a.n_classes)]);
+            __syncthreads();
+            continue;
+        }
+        if (n > 0) sq_write_back(a, sm);
+        if (cmd == CMD_DONE) break;
+        if (cmd == CMD_PHASE) {
+            if (tid == 0) {
+                sm.k0 += sm.ns;
+                sm.ns = min(SQ_SLOTS, a.P - sm.k0);
+                sm.j = 0;
+            }
+            __syncthreads();
+            phases++;
+            sq_load_slots(a, sm, true);
+            continue;
+        }
+        if (cmd == CMD_RING) {
+            rings++;
+            const int32_t j = sm.arg, k = sm.k0 + j;
+            const PodHot p = sm.slot_ph[j];
+            const ca_pod_spec& s = sm.slot_spec[j];
+            int32_t X = sm.wb + sm.wn;
+            if (X >= n) X -= n;
+            const int32_t R = n - (sm.wn - sm.cur);
+            int32_t found;
+            uint32_t ev;
+            sq_ring_scan(a, sm, p, s, X, R, found, ev);
+            const int32_t c = sm.slot_cls[j];
+            if (found >= 0) {
+                int32_t f = X + found;
+                if (f >= n) f -= n;
+                f = CK(f, n);
+                if (tid == 0) {
+                    NodeHot hr = ld_hot_coh(a.hot + f);
+                    NodeExt he = ld_ext_coh(a.ext + f);
+                    sq_place_row(hr, he, p, s);
+                    a.hot[f] = hr;
+                    a.ext[f] = he;
+                    a.out_node[k] = f;
+                    a.hints[k] = f;
+                    evals += sm.carry + ev;
+                    sm.L = (f + 1 == n) ? 0 : f + 1;
+                    sm.succ = 1;
+                    sm.j = j + 1;
+                }
+                __threadfence();
+                __syncthreads();
+                windows++;
+                sq_load_window(a, sm, sm.L);
+                sq_load_slots(a, sm, false);
+            } else {
+                if (tid == 0) {
+                    evals += sm.carry + ev;
+                    a.out_node[k] = -1;
+                    if (c >= 0 && !(p.flags & PF_DAEMONSET)) fo_mark(a, c);
+                    sm.j = j + 1;
+                }
+                __threadfence();
+                __syncthreads();
+                if (c >= 0 && tid < sm.ns && sm.slot_cls[tid] == c)
+                    sm.slot_mark[tid] = ld_mark(&a.cls_mark[CK(c, a.n_classes)]);
+                __syncthreads();
+            }
+            continue;
+        }
+        // CMD_WINDOW: the cursor left the window
+        windows++;
+        sq_load_window(a, sm, sm.L);
+        sq_load_slots(a, sm, false);
+    }
+    if (tid == 0) {
+        if (sm.succ) a.ctl->L = sm.L;       // lastIndex moves only with a successful scan
+        a.ctl->evals = evals;
+        a.ctl->phases = phases;
+        a.ctl->steps = steps;
+        a.ctl->ring_scans = rings;
+        a.ctl->windows = windows;
     }
 }
 
@@ -646,7 +607,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     if (n_placed) *n_placed = 0;
     FilterScratch& fo = m->fo;
     fo.kernel_ms = 0;
-    fo.batches = fo.cuts = 0;
+    fo.phases = fo.steps = fo.ring_scans = fo.windows = 0;
     if (n == 0) return CA_OK;
     CA_HIP_CHECK(hipSetDevice(m->device));
     int rc;
@@ -669,13 +630,12 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
             capped[c] = class_owner[c] >= 0 && per_owner[class_owner[c]] > FO_MAX_PER_OWNER;
     }
     const int32_t nn = (int32_t)m->nodes.size();
-    // inputs: order | hints | class_owner | capped ; zeroed: ctl | claim | owner_cnt | cls_mark | owner_over
+    // inputs: order | hints | class_owner | capped ; zeroed: ctl | owner_cnt | cls_mark | owner_over
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t o_order = 0, o_hints = o_order + al(sizeof(int32_t) * n), o_owner = o_hints + al(sizeof(int32_t) * n),
                  o_capped = o_owner + al(sizeof(int32_t) * (n_classes + 1)), in_bytes = o_capped + al(n_classes + 1);
-    const size_t z_ctl = 0, z_claim = al(sizeof(FoCtl)), z_ocnt = z_claim + al(sizeof(unsigned long long) * (nn + 1)),
-                 z_mark = z_ocnt + al(sizeof(int32_t) * (n_owners + 1)), z_over = z_mark + al(n_classes + 1),
-                 z_bytes = z_over + al(n_owners + 1);
+    const size_t z_ctl = 0, z_ocnt = al(sizeof(FoCtl)), z_mark = z_ocnt + al(sizeof(int32_t) * (n_owners + 1)),
+                 z_over = z_mark + al(n_classes + 1), z_bytes = z_over + al(n_owners + 1);
     const size_t out_bytes = al(sizeof(int32_t) * n) * 2 + al(sizeof(FoCtl));
     if ((rc = fo.in.reserve(in_bytes)) != CA_OK || (rc = fo.h_in.reserve(in_bytes)) != CA_OK ||
         (rc = fo.zero.reserve(z_bytes)) != CA_OK || (rc = fo.out.reserve(out_bytes)) != CA_OK ||
@@ -721,13 +681,12 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     a.cls_owner = class_owner ? reinterpret_cast<const int32_t*>(di + o_owner) : nullptr;
     a.owner_cnt = reinterpret_cast<int32_t*>(dz + z_ocnt);
     a.owner_over = reinterpret_cast<uint8_t*>(dz + z_over);
-    a.claim = reinterpret_cast<unsigned long long*>(dz + z_claim);
     a.ctl = reinterpret_cast<FoCtl*>(dz + z_ctl);
     a.n_pods = dp->n_pods;
     a.n_classes = n_classes;
     a.n_owners = n_owners;
     CA_HIP_CHECK(hipEventRecord(m->ev0, m->stream));
-    hipLaunchKernelGGL(k_filter_out, dim3(1), dim3(FO_T), 0, m->stream, a);
+    hipLaunchKernelGGL(k_filter_out, dim3(1), dim3(SQ_T), 0, m->stream, a);
     CA_HIP_CHECK(hipGetLastError());
     CA_HIP_CHECK(hipEventRecord(m->ev1, m->stream));
     char* ho = fo.h_out.as<char>();
@@ -762,8 +721,10 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     *last_index = hctl->L;
     if (evals) *evals += hctl->evals;
     if (n_overflowing) *n_overflowing = hctl->overflowing;
-    fo.batches = hctl->batches;
-    fo.cuts = hctl->cuts;
+    fo.phases = hctl->phases;
+    fo.steps = hctl->steps;
+    fo.ring_scans = hctl->ring_scans;
+    fo.windows = hctl->windows;
     fo.total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (n_placed) *n_placed = placed;
     return CA_OK;
@@ -771,9 +732,11 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
 
 int ca_filter_stats(const ca_mirror* m, float* out, int32_t cap) {
     if (!m || (!out && cap > 0)) return CA_EINVAL;
-    const float v[4] = {m->fo.kernel_ms, m->fo.total_ms, (float)m->fo.batches, (float)m->fo.cuts};
-    for (int32_t i = 0; i < cap && i < 4; i++) out[i] = v[i];
-    return 4;
+    const casim::FilterScratch& fo = m->fo;
+    const float v[6] = {fo.kernel_ms, fo.total_ms, (float)fo.phases, (float)fo.steps, (float)fo.ring_scans,
+                        (float)fo.windows};
+    for (int32_t i = 0; i < cap && i < 6; i++) out[i] = v[i];
+    return 6;
 }
 
 }  // extern "C"

@@ -53,7 +53,7 @@ struct FilterScratch {
     HostBuf h_in, h_out;
     DevPodTable pods;              // the pending table when the caller passes no podset
     float kernel_ms = 0, total_ms = 0;
-    int32_t batches = 0, cuts = 0;
+    int32_t phases = 0, steps = 0, ring_scans = 0, windows = 0;
 };
 
 // Dirty-row staging of sync_nodes: one H2D copy + a scatter kernel.

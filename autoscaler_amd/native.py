@@ -341,9 +341,10 @@ class Mirror:
         return a.output(placed.value, li.value, ev.value, ov.value)
 
     def filter_stats(self) -> dict:
-        out = (C.c_float * 4)()
-        self.lib.ca_filter_stats(self.h, out, 4)
-        return {"kernel_ms": out[0], "total_ms": out[1], "batches": int(out[2]), "cuts": int(out[3])}
+        out = (C.c_float * 6)()
+        self.lib.ca_filter_stats(self.h, out, 6)
+        return {"kernel_ms": out[0], "total_ms": out[1], "phases": int(out[2]), "block_steps": int(out[3]),
+                "ring_scans": int(out[4]), "windows": int(out[5])}
 
     def find_nodes_to_remove(self, candidates, dest_mask, cand_status, move_off, move_pods, hints,
                              last_index: int = 0) -> RemovalOutput:

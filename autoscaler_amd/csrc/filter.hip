@@ -36,7 +36,7 @@
 
 namespace casim {
 
-constexpr int SQ_T = 1024;             // threads: wave 0 sequences, all waves run the block steps
+constexpr int SQ_T = 512;              // threads: wave 0 sequences, all waves run the block steps
 constexpr int SQ_W = SQ_T / 64;
 constexpr int SQ_WIN = 512;            // node positions resident in LDS
 constexpr int SQ_SLOTS = 64;           // pods staged per phase (one per sequencer lane)
@@ -101,6 +101,7 @@ struct SqSmem {
     PodHot slot_ph[SQ_SLOTS];
     int32_t slot_node[SQ_SLOTS];     // hinted node position, -1 none
     int32_t slot_cls[SQ_SLOTS];
+    int32_t slot_out[SQ_SLOTS];      // node of the walked pod, -1 (flushed to HBM per phase)
     uint8_t slot_mark[SQ_SLOTS];     // the class is marked unschedulable
     uint8_t slot_dirty[SQ_SLOTS];
     uint8_t win_dirty[SQ_WIN];
@@ -360,13 +361,25 @@ __device__ void sq_sequence(const FoArgs& a, SqSmem& sm, unsigned long long& eva
     int32_t j = sm.j, L = sm.L, cur = sm.cur;
     bool succ = false;
     int32_t cmd = (k0 + ns >= a.P) ? CMD_DONE : CMD_PHASE, arg = 0;
+    // lane l holds slot l's scalars; the walk reads them with readlane (no LDS round trip)
+    const int ll = lane < ns ? lane : 0;
+    const PodHot lp = sm.slot_ph[ll];
+    const int32_t l_node = sm.slot_node[ll], l_cls = sm.slot_cls[ll];
+    const int32_t l_mark = sm.slot_mark[ll];
     for (; j < ns; j++) {
         if (n > 0 && cur >= wn) { cmd = CMD_WINDOW; break; }   // the cursor ran off the window
-        const int32_t k = k0 + j;
-        const PodHot& p = sm.slot_ph[j];
+        PodHot p;
+        p.cpu = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(lp.cpu >> 32), j) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)lp.cpu, j));
+        p.mem = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(lp.mem >> 32), j) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)lp.mem, j));
+        p.eph = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(lp.eph >> 32), j) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)lp.eph, j));
+        p.flags = (uint32_t)__builtin_amdgcn_readlane((int)lp.flags, j);
+        p.spec = 0;
         const ca_pod_spec& s = sm.slot_spec[j];
         const uint32_t pf = p.flags;
-        const int32_t h = sm.slot_node[j];
+        const int32_t h = __builtin_amdgcn_readlane(l_node, j);
         int32_t node = -1;
         if (h >= 0 && !(pf & PF_PREFILTER_FAIL)) {            // findNodeWithHints (:91-108)
             if (lane == 0) evals++;
@@ -395,12 +408,12 @@ __device__ void sq_sequence(const FoArgs& a, SqSmem& sm, unsigned long long& eva
                 }
             }
         }
-        if (node < 0 && !sm.slot_mark[j]) {                   // findNode (:110-125)
-            const int32_t c = sm.slot_cls[j];
+        if (node < 0 && !__builtin_amdgcn_readlane(l_mark, j)) {   // findNode (:110-125)
+            const int32_t c = __builtin_amdgcn_readlane(l_cls, j);
             const bool can_mark = c >= 0 && !(pf & PF_DAEMONSET);
             if ((pf & PF_PREFILTER_FAIL) || n == 0) {          // fails without a scan
                 if (can_mark) {
-                    if (lane == 0) a.out_node[k] = -1;
+                    if (lane == 0) sm.slot_out[j] = -1;
                     cmd = CMD_MARK;
                     arg = j++;
                     break;
@@ -445,7 +458,7 @@ __device__ void sq_sequence(const FoArgs& a, SqSmem& sm, unsigned long long& eva
                 } else if (wn == n) {                            // the whole ring: no node fits
                     if (lane == 0) evals += ev;
                     if (can_mark) {
-                        if (lane == 0) a.out_node[k] = -1;
+                        if (lane == 0) sm.slot_out[j] = -1;
                         cmd = CMD_MARK;
                         arg = j++;
                         break;
@@ -458,10 +471,7 @@ __device__ void sq_sequence(const FoArgs& a, SqSmem& sm, unsigned long long& eva
                 }
             }
         }
-        if (lane == 0) {
-            a.out_node[k] = node;
-            if (node >= 0) a.hints[k] = node;                  // Hints.Set (:95, :123)
-        }
+        if (lane == 0) sm.slot_out[j] = node;
     }
     if (lane == 0) {
         sm.j = j;
@@ -470,6 +480,16 @@ __device__ void sq_sequence(const FoArgs& a, SqSmem& sm, unsigned long long& eva
         sm.cmd = cmd;
         sm.arg = arg;
         if (succ) sm.succ = 1;
+    }
+}
+
+// the phase's outcomes to HBM: out_node, and Hints.Set (:95, :123) for the placed pods
+__device__ inline void sq_flush(const FoArgs& a, SqSmem& sm) {
+    const int32_t t = (int32_t)threadIdx.x;
+    if (t < sm.ns) {
+        const int32_t k = CK(sm.k0 + t, a.P), node = sm.slot_out[t];
+        a.out_node[k] = node;
+        if (node >= 0) a.hints[k] = node;
     }
 }
 
@@ -509,8 +529,10 @@ __global__ void __launch_bounds__(SQ_T) k_filter_out(FoArgs a) {
             continue;
         }
         if (n > 0) sq_write_back(a, sm);
+        if (cmd == CMD_DONE || cmd == CMD_PHASE) sq_flush(a, sm);
         if (cmd == CMD_DONE) break;
         if (cmd == CMD_PHASE) {
+            __syncthreads();
             if (tid == 0) {
                 sm.k0 += sm.ns;
                 sm.ns = min(SQ_SLOTS, a.P - sm.k0);
@@ -523,7 +545,7 @@ __global__ void __launch_bounds__(SQ_T) k_filter_out(FoArgs a) {
         }
         if (cmd == CMD_RING) {
             rings++;
-            const int32_t j = sm.arg, k = sm.k0 + j;
+            const int32_t j = sm.arg;
             const PodHot p = sm.slot_ph[j];
             const ca_pod_spec& s = sm.slot_spec[j];
             int32_t X = sm.wb + sm.wn;
@@ -543,8 +565,7 @@ __global__ void __launch_bounds__(SQ_T) k_filter_out(FoArgs a) {
                     sq_place_row(hr, he, p, s);
                     a.hot[f] = hr;
                     a.ext[f] = he;
-                    a.out_node[k] = f;
-                    a.hints[k] = f;
+                    sm.slot_out[j] = f;
                     evals += sm.carry + ev;
                     sm.L = (f + 1 == n) ? 0 : f + 1;
                     sm.succ = 1;
@@ -558,7 +579,7 @@ __global__ void __launch_bounds__(SQ_T) k_filter_out(FoArgs a) {
             } else {
                 if (tid == 0) {
                     evals += sm.carry + ev;
-                    a.out_node[k] = -1;
+                    sm.slot_out[j] = -1;
                     if (c >= 0 && !(p.flags & PF_DAEMONSET)) fo_mark(a, c);
                     sm.j = j + 1;
                 }

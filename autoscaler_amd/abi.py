@@ -114,6 +114,21 @@ REMOVAL_RESULT_DTYPE = np.dtype([
     ("removable", "<i4"), ("reason", "<i4"), ("n_placed", "<i4"), ("last_index_in", "<i4"), ("evals", "<u8"),
 ], align=True)
 
+# scale-down eligibility (include/casim.h ca_util_*)
+CA_UTIL_CPU, CA_UTIL_MEM, CA_UTIL_GPU = 0, 1, 2
+CA_UNODE_HAS_CPU, CA_UNODE_HAS_MEM, CA_UNODE_HAS_GPU, CA_UNODE_GPU_CONFIG = 0x1, 0x2, 0x4, 0x8
+CA_UPOD_DAEMONSET, CA_UPOD_MIRROR, CA_UPOD_DELETED, CA_UPOD_MOVABLE, CA_UPOD_BLOCKING = 0x01, 0x02, 0x04, 0x08, 0x10
+CA_UTIL_OK, CA_UTIL_NO_CPU, CA_UTIL_ZERO_CPU, CA_UTIL_NO_MEM, CA_UTIL_ZERO_MEM = 0, 1, 2, 3, 4
+
+UTIL_NODE_DTYPE = np.dtype([("alloc_milli", "<i8", (3,)), ("flags", "<u4"), ("_pad", "<u4")], align=True)
+UTIL_POD_DTYPE = np.dtype([
+    ("req_milli", "<i8", (3,)), ("deletion_ns", "<i8"), ("grace_s", "<i8"), ("flags", "<u4"), ("_pad", "<u4"),
+], align=True)
+UTIL_INFO_DTYPE = np.dtype([
+    ("cpu", "<f8"), ("mem", "<f8"), ("gpu", "<f8"), ("utilization", "<f8"), ("resource", "<i4"),
+    ("status", "<i4"), ("empty", "<i4"), ("_pad", "<i4"),
+], align=True)
+
 
 class PodTableC(C.Structure):
     _fields_ = [
@@ -144,6 +159,7 @@ EXPECTED_SIZES = [
     NODE_DTYPE.itemsize, POD_DTYPE.itemsize, REQ_DTYPE.itemsize, TERM_DTYPE.itemsize,
     C.sizeof(PodTableC), C.sizeof(MatchSpecC), C.sizeof(PredResultC), TEMPLATE_DTYPE.itemsize,
     C.sizeof(LimiterC), ESTIMATE_RESULT_DTYPE.itemsize, REMOVAL_RESULT_DTYPE.itemsize,
+    UTIL_NODE_DTYPE.itemsize, UTIL_POD_DTYPE.itemsize, UTIL_INFO_DTYPE.itemsize,
 ]
 
 

@@ -150,6 +150,7 @@ class Pod:
     phase: str = "Running"
     deletion_timestamp: Optional[float] = None
     priority: Optional[int] = None                  # Spec.Priority (corev1helpers.PodPriority: nil -> 0)
+    termination_grace_period_seconds: Optional[int] = None   # Spec.TerminationGracePeriodSeconds
 
     def controller_ref(self) -> Optional[OwnerReference]:
         for r in self.owner_refs:

@@ -89,6 +89,10 @@ def load() -> C.CDLL:
         "ca_filter_out_schedulable": ([vp, vp, vp, vp, i32, vp, i32, vp, p(i32), vp, vp, p(i32), p(C.c_uint64), p(i32)],
                                       C.c_int),
         "ca_filter_stats": ([vp, p(C.c_float), i32], C.c_int),
+        "ca_util_table_create": ([i32, vp, i32, vp, vp, p(vp)], C.c_int),
+        "ca_util_table_destroy": ([vp], C.c_int),
+        "ca_util_calculate": ([vp, i32, i32, C.c_int64, vp, p(C.c_float)], C.c_int),
+        "ca_util_device_results": ([vp, p(vp)], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(lib, name)
@@ -117,6 +121,7 @@ def exported_symbols() -> list[str]:
         "ca_removal_stats", "ca_removal_timings", "ca_removal_plan_create", "ca_removal_plan_run",
         "ca_removal_plan_destroy", "ca_mirror_set_hints", "ca_mirror_get_hints",
         "ca_removal_candidate_ticks", "ca_filter_out_schedulable", "ca_filter_stats",
+        "ca_util_table_create", "ca_util_table_destroy", "ca_util_calculate", "ca_util_device_results",
     ]
 
 
@@ -563,3 +568,41 @@ class EstimatePlan:
 
     def __exit__(self, *a):
         self.close()
+
+
+class UtilTable:
+    """Device-resident node/pod table for utilization.Calculate over every node
+    (include/casim.h ca_util_*; CA/simulator/utilization/info.go:48-127)."""
+
+    def __init__(self, device: int, nodes: np.ndarray, pod_off: np.ndarray, pods: np.ndarray):
+        self.lib = load()
+        self.nodes = np.ascontiguousarray(nodes, abi.UTIL_NODE_DTYPE)
+        self.pod_off = np.ascontiguousarray(pod_off, np.int32)
+        self.pods = np.ascontiguousarray(pods, abi.UTIL_POD_DTYPE)
+        if len(self.pod_off) != len(self.nodes) + 1 or int(self.pod_off[-1]) != len(self.pods):
+            raise ValueError("pod_off must have n_nodes + 1 entries ending at len(pods)")
+        h = C.c_void_p()
+        _check(self.lib.ca_util_table_create(device, ptr(self.nodes), len(self.nodes), ptr(self.pod_off),
+                                             ptr(self.pods), C.byref(h)), "ca_util_table_create")
+        self.h = h
+        self.kernel_ms = 0.0
+
+    def calculate(self, skip_daemonset_pods: bool, skip_mirror_pods: bool, now_ns: int,
+                  to_host: bool = True):
+        out = np.zeros(len(self.nodes), abi.UTIL_INFO_DTYPE) if to_host else None
+        ms = C.c_float(0)
+        _check(self.lib.ca_util_calculate(self.h, int(skip_daemonset_pods), int(skip_mirror_pods), int(now_ns),
+                                          ptr(out) if to_host else None, C.byref(ms)), "ca_util_calculate")
+        self.kernel_ms = ms.value
+        return out
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.ca_util_table_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -545,3 +545,61 @@ def load_filter(backend, w: FilterWorkload) -> None:
     backend.clear()
     backend.add_nodes(w.nodes)
     backend.add_pods(w.table, np.arange(len(w.table), dtype=np.int32), w.pod_node)
+
+
+def util_table(seed: int = 11, n_nodes: int = 15000, pods_per_node: int = 20, now_ns: int = 1_608_310_800 * 10**9,
+               edge_cases: bool = True):
+    """Scale-down eligibility input at C5 size by default: ca_util_node /
+    ca_util_pod rows with a ragged pod count per node (0 .. 2 x pods_per_node), 5% DaemonSet,
+    2% mirror, 3% deleted pods whose deletion lands either side of the long-terminating
+    cut-off, ~10% GPU-config nodes, and (edge_cases) nodes with missing or zero
+    allocatable and DaemonSet shares equal to allocatable (x/0 -> inf/nan).
+    Returns (nodes, pod_off, pods, now_ns)."""
+    from . import abi
+    rng = np.random.default_rng(seed)
+    counts = rng.integers(0, 2 * pods_per_node + 1, n_nodes)
+    pod_off = np.zeros(n_nodes + 1, np.int32)
+    np.cumsum(counts, out=pod_off[1:])
+    P = int(pod_off[-1])
+    nodes = np.zeros(n_nodes, abi.UTIL_NODE_DTYPE)
+    nodes["alloc_milli"][:, 0] = rng.choice([4000, 8000, 16000, 32000], n_nodes)
+    nodes["alloc_milli"][:, 1] = rng.choice([16, 32, 64, 128], n_nodes) * (1 << 30) * 1000
+    nodes["alloc_milli"][:, 2] = rng.choice([1, 2, 4, 8], n_nodes) * 1000
+    flags = np.full(n_nodes, abi.CA_UNODE_HAS_CPU | abi.CA_UNODE_HAS_MEM, np.uint32)
+    gpu = rng.random(n_nodes) < 0.1
+    flags[gpu] |= abi.CA_UNODE_GPU_CONFIG | abi.CA_UNODE_HAS_GPU
+    pods = np.zeros(P, abi.UTIL_POD_DTYPE)
+    pods["req_milli"][:, 0] = rng.choice([50, 100, 250, 500, 1000], P)
+    pods["req_milli"][:, 1] = rng.choice([64, 128, 256, 512, 1024, 2048], P) * (1 << 20) * 1000
+    pods["req_milli"][:, 2] = (rng.random(P) < 0.3) * 1000
+    u = rng.random(P)
+    pf = np.zeros(P, np.uint32)
+    pf[u < 0.05] |= abi.CA_UPOD_DAEMONSET
+    pf[(u >= 0.05) & (u < 0.07)] |= abi.CA_UPOD_MIRROR
+    dele = (u >= 0.07) & (u < 0.10)
+    pf[dele] |= abi.CA_UPOD_DELETED
+    pods["grace_s"][dele] = rng.choice([0, 30, 600], int(dele.sum()))
+    pods["deletion_ns"][dele] = now_ns - rng.integers(0, 1200, int(dele.sum())) * 10**9
+    d = rng.random(P)
+    pf[d < 0.6] |= abi.CA_UPOD_MOVABLE
+    pf[d > 0.98] |= abi.CA_UPOD_BLOCKING
+    if edge_cases and n_nodes >= 64:
+        e = rng.choice(n_nodes, 48, replace=False)
+        flags[e[0:8]] &= ~np.uint32(abi.CA_UNODE_HAS_CPU)
+        nodes["alloc_milli"][e[8:16], 0] = 0
+        flags[e[16:24]] &= ~np.uint32(abi.CA_UNODE_HAS_MEM)
+        nodes["alloc_milli"][e[24:32], 1] = 0
+        flags[e[32:40]] &= ~np.uint32(abi.CA_UNODE_HAS_GPU)       # unready GPU (label, no allocatable)
+        flags[e[32:40]] |= abi.CA_UNODE_GPU_CONFIG
+        for n in e[40:48]:                                         # DaemonSets use the whole node
+            b, f = pod_off[n], pod_off[n + 1]
+            if f > b:
+                pf[b:f] = abi.CA_UPOD_DAEMONSET
+                pods["req_milli"][b, :] = nodes["alloc_milli"][n, :]
+                pods["req_milli"][b + 1:f, :] = 0
+        empty = e[40:48]
+        for n in empty[:4]:
+            pf[pod_off[n]:pod_off[n + 1]] &= ~np.uint32(abi.CA_UPOD_MOVABLE | abi.CA_UPOD_BLOCKING)
+    nodes["flags"] = flags
+    pods["flags"] = pf
+    return nodes, pod_off, pods, now_ns

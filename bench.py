@@ -74,6 +74,7 @@ def parse():
     ap.add_argument("--no-sweep", action="store_true", help="skip the C3 scale-down sweep leg (N=1 only)")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 taint/affinity Estimate leg (N=1 only)")
     ap.add_argument("--no-expansion", action="store_true", help="skip the expansion-option feasibility leg (N=1)")
+    ap.add_argument("--no-util", action="store_true", help="skip the scale-down eligibility leg (N=1)")
     ap.add_argument("--sweep-nodes", type=int, default=5000)
     return ap.parse_args()
 
@@ -186,6 +187,45 @@ def expansion_leg(args, device: int, with_cpu: bool) -> dict:
                                "sample": f"oracle/casim_oracle.c or_check_templates (fork, template copy, "
                                          f"CheckPredicates, revert per node group), 1 thread of {cpu_model()}"}
     m.close()
+    return out
+
+
+def utilization_leg(args, device: int, with_cpu: bool) -> dict:
+    """Scale-down eligibility at C5 size: utilization.Calculate
+    (info.go:48-127) + the FindEmptyNodesToRemove verdict for 15k nodes / ~300k pods in one
+    launch (ca_util_calculate), table resident in HBM, results left in HBM.  Roofline: HBM,
+    algorithmic bytes = node row 32 B + offset 4 B + result 48 B per node, 48 B per pod."""
+    from autoscaler_amd import native
+    from autoscaler_amd import workloads as W
+    nodes, off, pods, now = W.util_table(seed=11, n_nodes=15000, pods_per_node=20)
+    t = native.UtilTable(device, nodes, off, pods)
+    for _ in range(3):
+        t.calculate(True, True, now, to_host=False)
+    kms, wall = [], []
+    for _ in range(max(args.steps, 20)):
+        t0 = time.perf_counter()
+        t.calculate(True, True, now, to_host=False)
+        wall.append(time.perf_counter() - t0)
+        kms.append(t.kernel_ms)
+    got = t.calculate(True, True, now)
+    t.close()
+    k = float(np.mean(kms))
+    algo = 84 * len(nodes) + 4 + 48 * len(pods)
+    out = {"workload": f"C5 nodes: {len(nodes)} nodes, {len(pods)} pods (ragged 0-40 per node), skip DaemonSet "
+                       f"and mirror pods", "kernel": "k_node_utilization", "kernel_ms": k,
+           "call_ms": float(np.median(wall) * 1e3), "nodes_per_s": len(nodes) / (k / 1e3),
+           "roofline": {"bound": "hbm", "achieved": algo / (k / 1e3) / 1e9, "peak": 8000.0, "unit": "GB/s",
+                        "frac": algo / (k / 1e3) / 1e9 / 8000.0, "bytes_per_launch": algo}}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle                                           # CPU baseline leg only
+        t0 = time.perf_counter()
+        ref = pyoracle.node_utilization(nodes, off, pods, True, True, now)
+        cpu_ms = (time.perf_counter() - t0) * 1e3
+        out.update({"cpu_ms": cpu_ms, "speedup_kernel": cpu_ms / k, "parity": got.tobytes() == ref.tobytes(),
+                    "cpu_baseline": {"kind": "port", "cores": 1,
+                                     "sample": f"oracle/casim_oracle.c or_node_utilization, the same table, 1 thread "
+                                               f"of {cpu_model()}"}})
     return out
 
 
@@ -454,6 +494,8 @@ def main():
             result["extra"]["c4"] = c4_leg(args, local, not args.no_cpu_baseline)
         if world == 1 and not args.no_expansion:
             result["extra"]["expansion"] = expansion_leg(args, local, not args.no_cpu_baseline)
+        if world == 1 and not args.no_util:
+            result["extra"]["utilization"] = utilization_leg(args, local, not args.no_cpu_baseline)
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.barrier()

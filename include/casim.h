@@ -418,6 +418,71 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
  * [2] slot phases, [3] block steps, [4] block-wide ring scans, [5] window loads; returns 6. */
 int ca_filter_stats(const ca_mirror* m, float* out, int32_t cap);
 
+/* ---- scale-down eligibility ----------------------------
+ * utilization.Calculate (CA/simulator/utilization/info.go:48-127) for every node of a
+ * device-resident table, plus the FindEmptyNodesToRemove verdict (CA/simulator/cluster.go:
+ * 187-202) from per-pod drain flags the host classified (GetPodsToMove with nil listers,
+ * CA/simulator/drain.go:50-90, stays on the host).  All quantities are
+ * Quantity.MilliValue() int64s; the ratio is one IEEE float64 division, bit-exact. */
+#define CA_UTIL_CPU 0                          /* Info.ResourceName                      */
+#define CA_UTIL_MEM 1
+#define CA_UTIL_GPU 2
+
+#define CA_UNODE_HAS_CPU     0x1u              /* Allocatable[cpu] present               */
+#define CA_UNODE_HAS_MEM     0x2u              /* Allocatable[memory] present            */
+#define CA_UNODE_HAS_GPU     0x4u              /* Allocatable[gpuConfig.ResourceName]    */
+#define CA_UNODE_GPU_CONFIG  0x8u              /* gpuConfig != nil (info.go:49)          */
+
+#define CA_UPOD_DAEMONSET    0x01u             /* pod_util.IsDaemonSetPod (utils/pod/pod.go:32-43) */
+#define CA_UPOD_MIRROR       0x02u             /* pod_util.IsMirrorPod (pod.go:46-52)    */
+#define CA_UPOD_DELETED      0x04u             /* DeletionTimestamp != nil               */
+#define CA_UPOD_MOVABLE      0x08u             /* GetPodsToMove lists it                  */
+#define CA_UPOD_BLOCKING     0x10u             /* GetPodsToMove fails on it               */
+
+/* ca_util_info.status: the error calculateUtilizationOfResource returns (info.go:88-94) */
+#define CA_UTIL_OK           0
+#define CA_UTIL_NO_CPU       1                 /* "failed to get cpu from <node>"        */
+#define CA_UTIL_ZERO_CPU     2                 /* "cpu is 0 at <node>"                   */
+#define CA_UTIL_NO_MEM       3
+#define CA_UTIL_ZERO_MEM     4
+
+typedef struct ca_util_node {
+    int64_t  alloc_milli[3];                  /* Allocatable MilliValue: cpu, memory, gpu */
+    uint32_t flags;                           /* CA_UNODE_*                              */
+    uint32_t _pad;
+} ca_util_node;
+
+typedef struct ca_util_pod {
+    int64_t  req_milli[3];                    /* Σ Containers[*].Requests MilliValue (cpu, memory,
+                                                 gpu); init containers and overhead excluded */
+    int64_t  deletion_ns;                     /* DeletionTimestamp (ns since epoch) if DELETED */
+    int64_t  grace_s;                         /* TerminationGracePeriodSeconds (nil -> 30) */
+    uint32_t flags;                           /* CA_UPOD_*                               */
+    uint32_t _pad;
+} ca_util_pod;
+
+typedef struct ca_util_info {                 /* utilization.Info                        */
+    double   cpu, mem, gpu, utilization;
+    int32_t  resource;                        /* CA_UTIL_CPU / _MEM / _GPU               */
+    int32_t  status;                          /* CA_UTIL_OK or the error                 */
+    int32_t  empty;                           /* FindEmptyNodesToRemove would list it    */
+    int32_t  _pad;
+} ca_util_info;
+
+typedef struct ca_util_table ca_util_table;
+
+/* Uploads nodes[n_nodes] and their pods (pods[pod_off[i] .. pod_off[i+1]) belong to node
+ * i) to HBM on `device`; they stay resident until destroy. */
+int ca_util_table_create(int32_t device, const ca_util_node* nodes, int32_t n_nodes,
+                         const int32_t* pod_off, const ca_util_pod* pods, ca_util_table** out);
+int ca_util_table_destroy(ca_util_table* t);
+/* Calculate(nodeInfo, skipDaemonSetPods, skipMirrorPods, gpuConfig, currentTime) for every
+ * node.  out NULL keeps the results in HBM (ca_util_device_results); otherwise out[n_nodes]
+ * is filled.  *kernel_ms (may be NULL) = device time of the kernel. */
+int ca_util_calculate(ca_util_table* t, int32_t skip_daemonset_pods, int32_t skip_mirror_pods,
+                      int64_t now_ns, ca_util_info* out, float* kernel_ms);
+int ca_util_device_results(const ca_util_table* t, const ca_util_info** out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -827,3 +827,82 @@ int or_find_nodes_to_remove(or_state* s, const int32_t* candidates, int32_t n_ca
     }
     return CA_OK;
 }
+
+/* ---------------------------------------------------------------------------
+ * Scale-down eligibility: utilization.Calculate + FindEmptyNodesToRemove
+ * ------------------------------------------------------------------------- */
+
+/* drain.IsPodLongTerminating (CA/utils/drain/drain.go:294-306):
+ * DeletionTimestamp + grace seconds + PodLongTerminatingExtraThreshold (30 s, :34) is
+ * strictly before currentTime. */
+static int or_pod_long_terminating(const ca_util_pod* p, int64_t now_ns) {
+    if (!(p->flags & CA_UPOD_DELETED)) return 0;
+    int64_t t = p->deletion_ns + p->grace_s * 1000000000LL;
+    t += 30LL * 1000000000LL;
+    return t < now_ns;
+}
+
+/* calculateUtilizationOfResource (info.go:83-127) for resource r (0 cpu, 1 mem, 2 gpu).
+ * Returns 0 and *util, or the error code (absent / zero allocatable). */
+static int or_util_of_resource(const ca_util_node* nd, const ca_util_pod* pods, int32_t b, int32_t e,
+                               int r, int32_t skip_ds, int32_t skip_mirror, int64_t now_ns, double* util) {
+    static const uint32_t has_bit[3] = {CA_UNODE_HAS_CPU, CA_UNODE_HAS_MEM, CA_UNODE_HAS_GPU};
+    if (!(nd->flags & has_bit[r])) return 1;                   /* :84-87 not found */
+    if (nd->alloc_milli[r] == 0) return 2;                     /* :88-90 zero       */
+    int64_t pods_request = 0, ds_and_mirror = 0;
+    for (int32_t i = b; i < e; i++) {
+        const ca_util_pod* p = &pods[i];
+        if (skip_ds && (p->flags & CA_UPOD_DAEMONSET)) {       /* :100-108 */
+            ds_and_mirror += p->req_milli[r];
+            continue;
+        }
+        if (skip_mirror && (p->flags & CA_UPOD_MIRROR)) {      /* :109-117 */
+            ds_and_mirror += p->req_milli[r];
+            continue;
+        }
+        if (or_pod_long_terminating(p, now_ns)) continue;      /* :118-121 */
+        pods_request += p->req_milli[r];                       /* :122-124 */
+    }
+    *util = (double)pods_request / (double)(nd->alloc_milli[r] - ds_and_mirror);   /* :126 */
+    return 0;
+}
+
+int or_node_utilization(const ca_util_node* nodes, int32_t n_nodes, const int32_t* pod_off,
+                        const ca_util_pod* pods, int32_t skip_ds, int32_t skip_mirror,
+                        int64_t now_ns, ca_util_info* out) {
+    if (n_nodes < 0 || (n_nodes > 0 && (!nodes || !pod_off || !out))) return CA_EINVAL;
+    for (int32_t n = 0; n < n_nodes; n++) {
+        const ca_util_node* nd = &nodes[n];
+        const int32_t b = pod_off[n], e = pod_off[n + 1];
+        ca_util_info o;
+        memset(&o, 0, sizeof o);
+        o.resource = CA_UTIL_CPU;
+        /* cluster.go:197-199: GetPodsToMove with nil listers has no error and no pods */
+        o.empty = 1;
+        for (int32_t i = b; i < e; i++)
+            if (pods[i].flags & (CA_UPOD_MOVABLE | CA_UPOD_BLOCKING)) o.empty = 0;
+        if (nd->flags & CA_UNODE_GPU_CONFIG) {                 /* info.go:49-58 */
+            double g = 0.0;
+            o.resource = CA_UTIL_GPU;
+            if (or_util_of_resource(nd, pods, b, e, 2, skip_ds, skip_mirror, now_ns, &g) == 0) {
+                o.gpu = g;
+                o.utilization = g;
+            }
+        } else {                                               /* info.go:61-80 */
+            double cpu = 0.0, mem = 0.0;
+            int err = or_util_of_resource(nd, pods, b, e, 0, skip_ds, skip_mirror, now_ns, &cpu);
+            if (err) {
+                o.status = err == 1 ? CA_UTIL_NO_CPU : CA_UTIL_ZERO_CPU;
+            } else if ((err = or_util_of_resource(nd, pods, b, e, 1, skip_ds, skip_mirror, now_ns, &mem))) {
+                o.status = err == 1 ? CA_UTIL_NO_MEM : CA_UTIL_ZERO_MEM;
+            } else {
+                o.cpu = cpu;
+                o.mem = mem;
+                if (cpu > mem) { o.resource = CA_UTIL_CPU; o.utilization = cpu; }
+                else           { o.resource = CA_UTIL_MEM; o.utilization = mem; }
+            }
+        }
+        out[n] = o;
+    }
+    return CA_OK;
+}

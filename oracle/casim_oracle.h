@@ -47,6 +47,12 @@ int or_fits_any_node(or_state* s, const ca_pod_table* t, int32_t pod, const ca_m
                      uint64_t* evals);
 int or_check_predicates(or_state* s, const ca_pod_table* t, int32_t pod, int32_t node,
                         ca_pred_result* out);
+/* utilization.Calculate (CA/simulator/utilization/info.go:48-127) and the
+ * FindEmptyNodesToRemove verdict (CA/simulator/cluster.go:187-202) per node; the table
+ * layout of ca_util_table_create (pods[pod_off[i] .. pod_off[i+1]) on node i). */
+int or_node_utilization(const ca_util_node* nodes, int32_t n_nodes, const int32_t* pod_off,
+                        const ca_util_pod* pods, int32_t skip_daemonset_pods, int32_t skip_mirror_pods,
+                        int64_t now_ns, ca_util_info* out);
 int or_check_templates(or_state* s, const ca_pod_table* t, const int32_t* samples, int32_t n_samples,
                        const ca_template* templates, int32_t n_templates, ca_pred_result* out);
 int or_estimate(or_state* s, const ca_pod_table* t, const int32_t* group_off,

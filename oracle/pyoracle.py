@@ -45,6 +45,7 @@ def load() -> C.CDLL:
         "or_fits_any_node": ([vp, vp, i32, vp, p(i32), p(i32), p(i32), p(C.c_uint64)], C.c_int),
         "or_check_predicates": ([vp, vp, i32, i32, vp], C.c_int),
         "or_check_templates": ([vp, vp, vp, i32, vp, i32, vp], C.c_int),
+        "or_node_utilization": ([vp, i32, vp, vp, i32, i32, C.c_int64, vp], C.c_int),
         "or_estimate": ([vp, vp, vp, vp, vp, i32, vp, p(i32), vp, vp, vp], C.c_int),
         "or_try_schedule_pods": ([vp, vp, i32, vp, i32, vp, p(i32), vp, p(C.c_uint64)], C.c_int),
         "or_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, p(i32), vp, vp], C.c_int),
@@ -206,3 +207,15 @@ class OracleState:
                                                 ptr(moves), ptr(hints), C.byref(li), ptr(res), ptr(dest)),
                "find_nodes_to_remove")
         return RemovalOutput(res, dest[: len(moves)], hints, li.value)
+
+
+def node_utilization(nodes: np.ndarray, pod_off: np.ndarray, pods: np.ndarray, skip_daemonset_pods: bool,
+                     skip_mirror_pods: bool, now_ns: int) -> np.ndarray:
+    """or_node_utilization: utilization.Calculate + the FindEmptyNodesToRemove verdict per node."""
+    nodes = np.ascontiguousarray(nodes, abi.UTIL_NODE_DTYPE)
+    pod_off = np.ascontiguousarray(pod_off, np.int32)
+    pods = np.ascontiguousarray(pods, abi.UTIL_POD_DTYPE)
+    out = np.zeros(len(nodes), abi.UTIL_INFO_DTYPE)
+    _check(load().or_node_utilization(ptr(nodes), len(nodes), ptr(pod_off), ptr(pods), int(skip_daemonset_pods),
+                                      int(skip_mirror_pods), int(now_ns), ptr(out)), "node_utilization")
+    return out

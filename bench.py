@@ -75,6 +75,7 @@ def parse():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 taint/affinity Estimate leg (N=1 only)")
     ap.add_argument("--no-expansion", action="store_true", help="skip the expansion-option feasibility leg (N=1)")
     ap.add_argument("--no-util", action="store_true", help="skip the scale-down eligibility leg (N=1)")
+    ap.add_argument("--no-filter", action="store_true", help="skip the FilterOutSchedulable leg (N=1)")
     ap.add_argument("--sweep-nodes", type=int, default=5000)
     return ap.parse_args()
 
@@ -226,6 +227,55 @@ def utilization_leg(args, device: int, with_cpu: bool) -> dict:
                     "cpu_baseline": {"kind": "port", "cores": 1,
                                      "sample": f"oracle/casim_oracle.c or_node_utilization, the same table, 1 thread "
                                                f"of {cpu_model()}"}})
+    return out
+
+
+def filter_leg(args, device: int, with_cpu: bool) -> dict:
+    """FilterOutSchedulable (filter_out_schedulable.go:95-124) on C5: 15k nodes
+    running 300k pods, 20k pending pods in priority order, TrySchedulePods(ScheduleAnywhere,
+    breakOnFailure=false) with hints and the similar-pods cache, one ca_filter_out_schedulable
+    call per step inside a fork that is reverted after it (mirror resident in HBM).
+    'c5-c4' adds the C4 taint/label universe."""
+    from autoscaler_amd import native
+    from autoscaler_amd import workloads as W
+    out = {}
+    for name, kw in (("c5", {}), ("c5-c4", {"taints": True})):
+        w = W.c5_filter(**kw)
+        g = native.Mirror(device)
+        W.load_filter(g, w)
+        ts, ks = [], []
+        for rep in range(1 + max(3, min(args.steps, 5))):
+            g.fork()
+            t = time.perf_counter()
+            rg = g.filter_out_schedulable(w.pending, w.order, w.class_owner, w.hints, 0)
+            dt = (time.perf_counter() - t) * 1e3
+            st = g.filter_stats()
+            g.revert()
+            if rep:                                               # first call is the warm-up
+                ts.append(dt)
+                ks.append(st["kernel_ms"])
+        ms = float(np.median(ts))
+        rec = {"workload": f"{name}: {len(w.order)} pending pods over {len(w.nodes)} nodes running "
+                           f"{len(w.pod_node)} pods", "call_ms": ms, "kernel_ms": float(np.median(ks)), "placed": int(rg.placed),
+               "evals": int(rg.evals), "evals_per_s": rg.evals / (ms / 1e3)}
+        g.close()
+        if with_cpu:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import pyoracle                                       # CPU baseline leg only
+            o = pyoracle.OracleState()
+            W.load_filter(o, w)
+            o.fork()
+            t = time.perf_counter()
+            ro = o.filter_out_schedulable(w.pending, w.order, w.class_owner, w.hints, 0)
+            cpu_ms = (time.perf_counter() - t) * 1e3
+            rec.update({"cpu_ms": cpu_ms, "speedup": cpu_ms / ms,
+                        "parity": bool(np.array_equal(rg.node, ro.node) and rg.evals == ro.evals
+                                       and rg.last_index == ro.last_index and np.array_equal(rg.hints, ro.hints))})
+        out[name] = rec
+    if with_cpu:
+        out["cpu_baseline"] = {"kind": "port", "cores": 1,
+                               "sample": f"oracle/casim_oracle.c or_filter_out_schedulable, the same call, 1 thread "
+                                         f"of {cpu_model()}"}
     return out
 
 
@@ -494,6 +544,8 @@ def main():
             result["extra"]["c4"] = c4_leg(args, local, not args.no_cpu_baseline)
         if world == 1 and not args.no_expansion:
             result["extra"]["expansion"] = expansion_leg(args, local, not args.no_cpu_baseline)
+        if world == 1 and not args.no_filter:
+            result["extra"]["filter"] = filter_leg(args, local, not args.no_cpu_baseline)
         if world == 1 and not args.no_util:
             result["extra"]["utilization"] = utilization_leg(args, local, not args.no_cpu_baseline)
         print(json.dumps(result), flush=True)

@@ -216,7 +216,14 @@ def utilization_leg(args, device: int, with_cpu: bool) -> dict:
                        f"and mirror pods", "kernel": "k_node_utilization", "kernel_ms": k,
            "call_ms": float(np.median(wall) * 1e3), "nodes_per_s": len(nodes) / (k / 1e3),
            "roofline": {"bound": "hbm", "achieved": algo / (k / 1e3) / 1e9, "peak": 8000.0, "unit": "GB/s",
-                        "frac": algo / (k / 1e3) / 1e9 / 8000.0, "bytes_per_launch": algo}}
+                        "frac": algo / (k / 1e3) / 1e9 / 8000.0, "bytes_per_launch": algo, "traffic": None}}
+    tf = os.path.join(ROOT, "profiles", "pmc_util_traffic.json")     # rocprofv3 --pmc passes (scripts/pmc_util.py)
+    if os.path.exists(tf):
+        with open(tf) as f:
+            kt = json.load(f)["kernels"].get("k_node_utilization")
+        if kt:
+            out["roofline"]["traffic"] = kt["traffic_bytes_per_launch"]
+            out["roofline"]["traffic_source"] = "profiles/pmc_util_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, per launch)"
     if with_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle                                           # CPU baseline leg only

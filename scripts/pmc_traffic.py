@@ -15,7 +15,7 @@ def load(root: str, counter: str) -> dict:
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
                 continue
-            name = r["Kernel_Name"].split("(")[0]
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
             per[(name, r.get("Dispatch_Id", r.get("Correlation_Id", "")))].append(float(r["Counter_Value"]))
     out = defaultdict(list)
     for (name, _), vals in per.items():
@@ -23,7 +23,7 @@ def load(root: str, counter: str) -> dict:
     return out
 
 
-def main(root: str, steps: int) -> None:
+def main(root: str, steps: int, what: str = "scripts/pmc_step.py (C2 Estimate steps, results in HBM)") -> None:
     fetch = load(root, "FETCH_SIZE")
     write = load(root, "WRITE_SIZE")
     res = {}
@@ -38,11 +38,12 @@ def main(root: str, steps: int) -> None:
                      "traffic_bytes_per_launch": (fk or 0) + (wk or 0),
                      "traffic_bytes_per_step": ((fk or 0) + (wk or 0)) * n / steps}
     json.dump({"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes over "
-                         f"scripts/pmc_step.py ({steps} C2 Estimate steps, results in HBM); "
+                         f"{what}, {steps} steps; "
                          "FETCH_SIZE x2 (gfx950 wide-read correction)", "steps": steps, "kernels": res},
               sys.stdout, indent=1)
     print()
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out", int(sys.argv[2]) if len(sys.argv) > 2 else 3)
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out", int(sys.argv[2]) if len(sys.argv) > 2 else 3,
+         *sys.argv[3:4])

@@ -274,15 +274,27 @@ __device__ void sq_load_slots(const FoArgs& a, SqSmem& sm, bool full) {
     const int32_t t = (int32_t)threadIdx.x;
     const int32_t n = a.n;
     if (full) {
+        // order -> PodHot once per slot, then every spec word in flight at once (one
+        // dependent HBM round trip each instead of three per word batch)
         constexpr int SW = (int)(sizeof(ca_pod_spec) / 8);
         static_assert(sizeof(ca_pod_spec) % 8 == 0, "ca_pod_spec words");
-        for (int32_t x = t; x < sm.ns * SW; x += SQ_T) {
-            const int32_t j = x / SW, w = x % SW;
-            const int32_t i = CK(a.order[CK(sm.k0 + j, a.P)], a.n_pods);
-            const PodHot ph = a.ph[i];
-            reinterpret_cast<unsigned long long*>(&sm.slot_spec[j])[w] =
-                reinterpret_cast<const unsigned long long*>(a.specs + CK(ph.spec, a.n_pods))[w];
-            if (w == 0) sm.slot_ph[j] = ph;
+        constexpr int PER = (SQ_SLOTS * SW + SQ_T - 1) / SQ_T;
+        if (t < sm.ns) sm.slot_ph[t] = a.ph[CK(a.order[CK(sm.k0 + t, a.P)], a.n_pods)];
+        __syncthreads();
+        const int32_t words = sm.ns * SW;
+        unsigned long long v[PER];
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const int32_t x = t + q * SQ_T;
+            if (x < words) {
+                const int32_t j = x / SW, w = x % SW;
+                v[q] = reinterpret_cast<const unsigned long long*>(a.specs + CK(sm.slot_ph[j].spec, a.n_pods))[w];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const int32_t x = t + q * SQ_T;
+            if (x < words) reinterpret_cast<unsigned long long*>(&sm.slot_spec[x / SW])[x % SW] = v[q];
         }
         __syncthreads();
     }

@@ -17,6 +17,7 @@ CFGS = {
     "c5-nohints": dict(hint_frac=0.0),
     "c5-allhints": dict(hint_frac=1.0),
     "c5-loose": dict(util_low=(0.2, 0.4), util_high=(0.5, 0.7)),
+    "c5-loose-nohints": dict(util_low=(0.2, 0.4), util_high=(0.5, 0.7), hint_frac=0.0),
 }
 names = sys.argv[1:] or list(CFGS)
 for name in names:

@@ -52,6 +52,7 @@ struct FoCtl {
     unsigned long long evals;
     int32_t ring_scans, windows;
     int32_t bad_line, bad_val; // CASIM_FO_CHECKS builds: the first index check that failed
+    unsigned long long seq_cycles, all_cycles;   // CASIM_PROF builds: wave 0's walk, the whole kernel
 };
 
 struct FoArgs {
@@ -223,7 +224,7 @@ __device__ inline void fo_mark(const FoArgs& a, int32_t c) {
 
 // ---- block steps ----------------------------------------------------------------------
 // dirty window rows and staged copies back to HBM
-__device__ void sq_write_back(const FoArgs& a, SqSmem& sm) {
+__device__ __attribute__((always_inline)) void sq_write_back(const FoArgs& a, SqSmem& sm) {
     const int32_t n = a.n, wb = sm.wb, wn = sm.wn;
     for (int32_t o = (int32_t)threadIdx.x; o < wn; o += SQ_T) {
         if (sm.win_dirty[o]) {
@@ -247,7 +248,7 @@ __device__ void sq_write_back(const FoArgs& a, SqSmem& sm) {
 }
 
 // the window: SQ_WIN rows from position L (all three columns)
-__device__ void sq_load_window(const FoArgs& a, SqSmem& sm, int32_t L) {
+__device__ __attribute__((always_inline)) void sq_load_window(const FoArgs& a, SqSmem& sm, int32_t L) {
     const int32_t n = a.n;
     const int32_t wn = min(SQ_WIN, n);
     for (int32_t o = (int32_t)threadIdx.x; o < wn; o += SQ_T) {
@@ -270,7 +271,7 @@ __device__ void sq_load_window(const FoArgs& a, SqSmem& sm, int32_t L) {
 
 // stage pods k0 .. k0+ns-1 (full: their records too; else only the hinted rows and marks
 // of the slots from sm.j on)
-__device__ void sq_load_slots(const FoArgs& a, SqSmem& sm, bool full) {
+__device__ __attribute__((always_inline)) void sq_load_slots(const FoArgs& a, SqSmem& sm, bool full) {
     const int32_t t = (int32_t)threadIdx.x;
     const int32_t n = a.n;
     if (full) {
@@ -318,7 +319,7 @@ __device__ void sq_load_slots(const FoArgs& a, SqSmem& sm, bool full) {
 
 // the rest of a pod's ring: R positions from X, block-wide.  First fitting offset (-1:
 // none) and the visible positions up to it (every visible position if none fits).
-__device__ void sq_ring_scan(const FoArgs& a, SqSmem& sm, const PodHot& p, const ca_pod_spec& s, int32_t X,
+__device__ __attribute__((always_inline)) void sq_ring_scan(const FoArgs& a, SqSmem& sm, const PodHot& p, const ca_pod_spec& s, int32_t X,
                              int32_t R, int32_t& found, uint32_t& evs) {
     const int32_t n = a.n;
     found = -1;
@@ -366,7 +367,7 @@ __device__ void sq_ring_scan(const FoArgs& a, SqSmem& sm, const PodHot& p, const
 
 // ---- the sequencer (wave 0) ----------------------------------------------------------
 // Walks slots sm.j .. sm.ns-1 and stops at the first pod that needs a block step.
-__device__ void sq_sequence(const FoArgs& a, SqSmem& sm, unsigned long long& evals) {
+__device__ __attribute__((always_inline)) void sq_sequence(const FoArgs& a, SqSmem& sm, unsigned long long& evals) {
     const int lane = (int)threadIdx.x;       // wave 0
     const int32_t n = a.n, ns = sm.ns, k0 = sm.k0;
     const int32_t wb = sm.wb, wn = sm.wn;
@@ -511,6 +512,10 @@ __global__ void __launch_bounds__(SQ_T) k_filter_out(FoArgs a) {
     const int32_t n = a.n;
     unsigned long long evals = 0;           // thread 0 (= the sequencer's lane 0)
     int32_t phases = 1, steps = 0, rings = 0, windows = 0;
+    unsigned long long seq_cyc = 0;
+#ifdef CASIM_PROF
+    const unsigned long long k_c0 = clock64();
+#endif
     if (tid == 0) {
         int32_t L0 = (n > 0) ? a.ctl->L % n : 0;
         if (L0 < 0) L0 += n;
@@ -527,7 +532,13 @@ __global__ void __launch_bounds__(SQ_T) k_filter_out(FoArgs a) {
     if (n > 0) sq_load_window(a, sm, sm.L);
     sq_load_slots(a, sm, true);
     while (true) {
+#ifdef CASIM_PROF
+        const unsigned long long c0 = clock64();
+#endif
         if (tid < 64) sq_sequence(a, sm, evals);
+#ifdef CASIM_PROF
+        if (tid == 0) seq_cyc += clock64() - c0;
+#endif
         __syncthreads();
         const int32_t cmd = sm.cmd;
         if (cmd != CMD_DONE) steps++;
@@ -612,6 +623,10 @@ __global__ void __launch_bounds__(SQ_T) k_filter_out(FoArgs a) {
         if (sm.succ) a.ctl->L = sm.L;       // lastIndex moves only with a successful scan
         a.ctl->evals = evals;
         a.ctl->phases = phases;
+        a.ctl->seq_cycles = seq_cyc;
+#ifdef CASIM_PROF
+        a.ctl->all_cycles = clock64() - k_c0;
+#endif
         a.ctl->steps = steps;
         a.ctl->ring_scans = rings;
         a.ctl->windows = windows;
@@ -758,6 +773,8 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     fo.steps = hctl->steps;
     fo.ring_scans = hctl->ring_scans;
     fo.windows = hctl->windows;
+    fo.seq_share = hctl->all_cycles ? (float)((double)hctl->seq_cycles / (double)hctl->all_cycles) : 0.0f;
+    fo.walk_cycles_per_pod = n ? (float)((double)hctl->seq_cycles / n) : 0.0f;
     fo.total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (n_placed) *n_placed = placed;
     return CA_OK;
@@ -766,10 +783,10 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
 int ca_filter_stats(const ca_mirror* m, float* out, int32_t cap) {
     if (!m || (!out && cap > 0)) return CA_EINVAL;
     const casim::FilterScratch& fo = m->fo;
-    const float v[6] = {fo.kernel_ms, fo.total_ms, (float)fo.phases, (float)fo.steps, (float)fo.ring_scans,
-                        (float)fo.windows};
-    for (int32_t i = 0; i < cap && i < 6; i++) out[i] = v[i];
-    return 6;
+    const float v[8] = {fo.kernel_ms, fo.total_ms, (float)fo.phases, (float)fo.steps, (float)fo.ring_scans,
+                        (float)fo.windows, fo.seq_share, fo.walk_cycles_per_pod};
+    for (int32_t i = 0; i < cap && i < 8; i++) out[i] = v[i];
+    return 8;
 }
 
 }  // extern "C"

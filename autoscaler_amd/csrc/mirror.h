@@ -54,6 +54,7 @@ struct FilterScratch {
     DevPodTable pods;              // the pending table when the caller passes no podset
     float kernel_ms = 0, total_ms = 0;
     int32_t phases = 0, steps = 0, ring_scans = 0, windows = 0;
+    float seq_share = 0, walk_cycles_per_pod = 0;   // CASIM_PROF builds: sequencer walk share, cycles/pod
 };
 
 // Dirty-row staging of sync_nodes: one H2D copy + a scatter kernel.

@@ -346,10 +346,11 @@ class Mirror:
         return a.output(placed.value, li.value, ev.value, ov.value)
 
     def filter_stats(self) -> dict:
-        out = (C.c_float * 6)()
-        self.lib.ca_filter_stats(self.h, out, 6)
+        out = (C.c_float * 8)()
+        self.lib.ca_filter_stats(self.h, out, 8)
         return {"kernel_ms": out[0], "total_ms": out[1], "phases": int(out[2]), "block_steps": int(out[3]),
-                "ring_scans": int(out[4]), "windows": int(out[5])}
+                "ring_scans": int(out[4]), "windows": int(out[5]), "seq_share": out[6],
+                "walk_cycles_per_pod": out[7]}
 
     def find_nodes_to_remove(self, candidates, dest_mask, cand_status, move_off, move_pods, hints,
                              last_index: int = 0) -> RemovalOutput:

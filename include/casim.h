@@ -415,7 +415,9 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
                               int32_t* out_node, int32_t* out_pod_id, int32_t* n_overflowing,
                               uint64_t* evals, int32_t* n_placed);
 /* [0] device time of the last call's kernel, [1] host wall time of the call (ms),
- * [2] slot phases, [3] block steps, [4] block-wide ring scans, [5] window loads; returns 6. */
+ * [2] slot phases, [3] block steps, [4] block-wide ring scans, [5] window loads, [6] share of the
+ * kernel's cycles in wave 0's walk and [7] walk cycles per pod (both CASIM_PROF builds only, else 0);
+ * returns 8. */
 int ca_filter_stats(const ca_mirror* m, float* out, int32_t cap);
 
 /* ---- scale-down eligibility ----------------------------

@@ -194,7 +194,8 @@ __device__ inline void sq_place_row(NodeHot& h, NodeExt& e, const PodHot& p, con
     h.eph = wsub(h.eph, p.eph);
     h.pods = h.pods - 1;
     uint64_t pu = 0;
-    for (int w = 0; w < CA_PORT_WORDS; w++) pu |= s.port_use[w];
+    if (p.flags & PF_PORTS)                   // PF_PORTS clear: port_use is empty (no LDS read)
+        for (int w = 0; w < CA_PORT_WORDS; w++) pu |= s.port_use[w];
     if (pu || (p.flags & PF_SCALAR_REQ)) {
         for (int w = 0; w < CA_PORT_WORDS; w++) e.ports[w] |= s.port_use[w];
         for (int k = 0; k < CA_MAX_SCALAR; k++) e.scalar[k] = wsub(e.scalar[k], s.req_scalar[k]);

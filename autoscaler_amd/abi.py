@@ -11,10 +11,10 @@ import ctypes as C
 
 import numpy as np
 
-CASIM_ABI_VERSION = 1
+CASIM_ABI_VERSION = 2
 
 # status codes
-CA_OK, CA_EINVAL, CA_ENOTFOUND, CA_EEXISTS, CA_EDEVICE, CA_ECAPACITY, CA_EUNSUPPORTED, CA_ESTATE = range(8)
+CA_OK, CA_EINVAL, CA_ENOTFOUND, CA_EEXISTS, CA_EDEVICE, CA_ECAPACITY, CA_EUNSUPPORTED, CA_ESTATE, CA_ENOTRUN = range(9)
 
 CA_MAX_SCALAR = 8
 CA_LABEL_WORDS = 4
@@ -22,6 +22,7 @@ CA_PORT_WORDS = 2
 CA_MAX_INT_KEYS = 4
 
 CA_NODE_UNSCHEDULABLE = 0x1
+CA_NODE_ANTI_AFFINITY_PODS = 0x2
 
 CA_POD_HAS_SCALAR_KEYS = 0x001
 CA_POD_HAS_NONTPU_SCALAR_KEYS = 0x002
@@ -31,6 +32,8 @@ CA_POD_PREFILTER_FAIL = 0x010
 CA_POD_PREFILTER_NAMES = 0x020
 CA_POD_DAEMONSET = 0x040
 CA_POD_HOSTNAME_DEPENDENT = 0x080
+CA_POD_OUT_OF_SCOPE = 0x100
+CA_POD_REQUIRED_ANTI_AFFINITY = 0x200
 
 CA_OP_IN, CA_OP_NOTIN, CA_OP_EXISTS, CA_OP_DOESNOTEXIST, CA_OP_GT, CA_OP_LT, CA_OP_FIELD_EQ, CA_OP_FIELD_NE, \
     CA_OP_FALSE = range(1, 10)
@@ -52,7 +55,7 @@ PLUGIN_NAMES = {
     CA_PLUGIN_NODE_RESOURCES_FIT: "NodeResourcesFit",
 }
 
-CA_PRED_OK, CA_PRED_NOT_SCHEDULABLE, CA_PRED_INTERNAL = 0, 1, 2
+CA_PRED_OK, CA_PRED_NOT_SCHEDULABLE, CA_PRED_INTERNAL, CA_PRED_UNSUPPORTED = 0, 1, 2, 3
 
 CA_REASON_TOO_MANY_PODS = 0x1
 CA_REASON_INSUFF_CPU = 0x2
@@ -66,6 +69,8 @@ CA_UNREMOVABLE_NONE = 0
 CA_UNREMOVABLE_NO_PLACE = 12
 CA_UNREMOVABLE_BLOCKED_BY_POD = 13
 CA_UNREMOVABLE_UNEXPECTED_ERROR = 14
+CA_UNREMOVABLE_OUT_OF_SCOPE = 100
+CA_UNREMOVABLE_NOT_RUN = 101
 
 # --------------------------------------------------------------------------
 # record dtypes (C layout: align=True)

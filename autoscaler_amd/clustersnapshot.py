@@ -53,6 +53,12 @@ class _State:
     def add_pod(self, p: Pod, node: str, pid: int) -> None:
         self.pods[node].append((p, pid))
 
+    def remove_node(self, name: str) -> None:
+        self.names.remove(name)
+        self.pos = {n: i for i, n in enumerate(self.names)}
+        del self.nodes[name]
+        del self.pods[name]
+
     def remove_pod(self, ns: str, name: str, node: str) -> int:
         lst = self.pods[node]
         for i, (p, pid) in enumerate(lst):
@@ -112,6 +118,10 @@ class ClusterSnapshot:
         elif kind == "rmpod":
             pid = st.remove_pod(op[1], op[2], op[3])
             self.backend.remove_pod(pid)
+        elif kind == "rmnode":
+            pos = st.pos[op[1]]
+            self.backend.remove_node(pos)
+            st.remove_node(op[1])
         elif kind == "fork":
             self._stack.append(copy.deepcopy(st))
             self.backend.fork()
@@ -143,6 +153,12 @@ class ClusterSnapshot:
         if node_name not in self._state.pos:
             raise NodeNotFoundError(node_name)
         self._apply(("rmpod", namespace, name, node_name))
+
+    def RemoveNode(self, node_name: str) -> None:  # noqa: N802
+        """RemoveNode (clustersnapshot.go:38; delta.go:150-186): the node and its pods leave."""
+        if node_name not in self._state.pos:
+            raise NodeNotFoundError(node_name)
+        self._apply(("rmnode", node_name))
 
     def Fork(self) -> None:  # noqa: N802
         self._apply(("fork",))

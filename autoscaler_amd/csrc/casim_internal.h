@@ -28,6 +28,7 @@ enum : uint32_t {
     NF_PORTS   = 0x4u,     // node has used host ports (may be stale-high)
     NF_SCALAR  = 0x8u,     // node allocatable has scalar resources
     NF_VALID   = 0x10u,    // row holds a node
+    NF_OUT_OF_SCOPE = 0x20u, // template row: its pods include a required-anti-affinity pod
 };
 
 // PodHot.flags (device-side copy of the CA_POD_* bits plus derived bits)
@@ -40,6 +41,8 @@ enum : uint32_t {
     PF_PREFILTER_NAMES = CA_POD_PREFILTER_NAMES,
     PF_DAEMONSET       = CA_POD_DAEMONSET,
     PF_HOSTNAME_DEP    = CA_POD_HOSTNAME_DEPENDENT,
+    PF_OUT_OF_SCOPE    = CA_POD_OUT_OF_SCOPE,
+    PF_ANTI_AFFINITY   = CA_POD_REQUIRED_ANTI_AFFINITY,
     PF_SCALAR_REQ      = 0x1000u,  // some req_scalar[i] != 0
     PF_PORTS           = 0x2000u,  // port_conflict or port_use non-empty
     PF_NODE_NAME       = 0x4000u,  // node_name_id != -1

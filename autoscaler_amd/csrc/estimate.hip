@@ -37,7 +37,7 @@ enum : uint32_t {
     SF_ZERO    = 0x10u,  // PF_ALL_ZERO
     SF_SCALAR  = 0x20u,  // PF_SCALAR_REQ
     SF_PORTS   = 0x40u,  // PF_PORTS
-    SF_UNSUP   = 0x80u,  // PF_HOSTNAME_DEP: group unsupported
+    SF_UNSUP   = 0x80u,  // PF_HOSTNAME_DEP / PF_OUT_OF_SCOPE: group unsupported (casim.h scope)
 };
 
 struct alignas(16) SortItem {
@@ -136,7 +136,7 @@ __device__ inline uint32_t static_sf(const PodHot& p, const ca_template& tp, boo
     if (p.flags & PF_ALL_ZERO) sf |= SF_ZERO;
     if (p.flags & PF_SCALAR_REQ) sf |= SF_SCALAR;
     if (p.flags & PF_PORTS) sf |= SF_PORTS;
-    if (p.flags & PF_HOSTNAME_DEP) sf |= SF_UNSUP;
+    if (p.flags & (PF_HOSTNAME_DEP | PF_OUT_OF_SCOPE)) sf |= SF_UNSUP;
     return sf;
 }
 
@@ -949,7 +949,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     res.node_count = 0; res.n_sched = 0; res.nodes_added = 0; res.lin = lin; res.lout = lin;
     res.status = CA_OK; res.sensitive = 0; res.had_success = 0; res.evals = 0; res.pad = 0;
     res.nseg = 0; res.pad2[0] = res.pad2[1] = res.pad2[2] = 0;
-    if (group_unsup[g]) {
+    if (group_unsup[g] || (gm.tflags & CA_NODE_ANTI_AFFINITY_PODS)) {
         res.status = CA_EUNSUPPORTED;
         if (tid == 0) outs[g] = res;
         if (tickets && w0) push_chunks(g, 0, (gm.count + pch - 1) / pch, nsub, tickets, qctl, prog, 0, 0, lane);
@@ -1921,6 +1921,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     CA_HIP_CHECK(hipSetDevice(m->device));
     const int32_t n_base = (int32_t)m->nodes.size();
     if (G == 0) return CA_OK;
+    if (m->n_scope_blockers > 0) return CA_EUNSUPPORTED;    // casim.h scope: required anti-affinity in the snapshot
     // kcap: new nodes a group can add (limiter cap, or one per pod when unlimited)
     int32_t kcap = lim->max_nodes > 0 ? std::min(lim->max_nodes, std::max(p->max_count, 1)) : std::max(p->max_count, 1);
     kcap = ((kcap + 63) / 64) * 64;
@@ -2089,6 +2090,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     std::vector<ChainOut> outs(G);
     std::vector<uint8_t> accepted(G, 0);
     std::vector<int32_t> true_lin(G, *last_index);
+    int32_t cut = -1;                   // first unsupported group when later groups exist (prefix protocol)
     int32_t rounds = 0;
     float chain_ms = 0;
     for (;;) {
@@ -2173,12 +2175,20 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         }
         // walk the lastIndex chain
         int64_t cur = *last_index;
+        cut = -1;
         bool known = true;
         bool all_ok = true;
         std::fill(need.begin(), need.end(), 0);
         for (int32_t g = 0; g < G; g++) {
             const ChainOut& o = outs[g];
             true_lin[g] = (int32_t)cur;     // exact once the walk converged (known stays true)
+            if (o.status == CA_EUNSUPPORTED && known) {
+                // prefix protocol (casim.h scope): groups after it are CA_ENOTRUN, the batch's
+                // lastIndex is the one this group starts from
+                for (int32_t h = g; h < G; h++) { accepted[h] = 1; need[h] = 0; }
+                if (g + 1 < G) cut = g;
+                break;
+            }
             const bool insensitive = o.status != CA_OK || !o.sensitive;
             if (known && (o.lin == cur || insensitive)) {
                 accepted[g] = 1;
@@ -2242,6 +2252,12 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         r.last_index_out = o.status == CA_OK && o.had_success ? o.lout : true_lin[g];
         r.status = o.status;
         r.evals = o.evals;
+        if (cut >= 0 && g > cut) {        // CA_ENOTRUN: nothing of it is reported
+            r.node_count = r.n_scheduled = r.nodes_added = 0;
+            r.last_index_in = r.last_index_out = true_lin[cut];
+            r.status = CA_ENOTRUN;
+            r.evals = 0;
+        }
     }
     float sort_ms = 0;
     {

@@ -652,6 +652,11 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
         if (i < 0 || i >= t->n_pods) return CA_EINVAL;
         if (t->pods[i].similar_class >= n_classes) return CA_EINVAL;
     }
+    // casim.h kernel scope: an out-of-scope pending pod, or required anti-affinity in the
+    // snapshot, sends the whole call to the Go path (nothing placed)
+    if (m->n_scope_blockers > 0) return CA_EUNSUPPORTED;
+    for (int32_t k = 0; k < n; k++)
+        if (t->pods[order ? order[k] : k].flags & CA_POD_OUT_OF_SCOPE) return CA_EUNSUPPORTED;
     if (n_overflowing) *n_overflowing = 0;
     if (n_placed) *n_placed = 0;
     FilterScratch& fo = m->fo;

@@ -9,7 +9,7 @@
 
 namespace casim {
 
-enum { J_FORK = 1, J_ADD_NODE, J_ADD_POD, J_REMOVE_POD };
+enum { J_FORK = 1, J_ADD_NODE, J_ADD_POD, J_REMOVE_POD, J_REMOVE_NODE };
 
 struct JournalEntry {
     int32_t kind, node, pod, slot;
@@ -85,7 +85,9 @@ struct ca_mirror {
     std::vector<ca_selector_req> reqs;
     std::vector<int32_t> pf_names;
     std::vector<casim::JournalEntry> journal;
+    std::vector<casim::NodeRow> removed_nodes;   // rows of journaled RemoveNode ops (J_REMOVE_NODE.slot)
     int32_t depth = 0;
+    int64_t n_scope_blockers = 0;          // pods in the snapshot with CA_POD_REQUIRED_ANTI_AFFINITY
 
     // device rows
     casim::DevBuf d_hot, d_ext, d_static;
@@ -115,6 +117,7 @@ struct ca_mirror {
     int ensure_pod_hints();                // grow to pods.size(), new entries -1
     int64_t n_ext_pods = 0;                // pods stored with host ports / extended requests
 
+    int remap_hints_removed(int32_t pos, bool restore);   // resident hints around a RemoveNode
     int sync_nodes();                      // push dirty rows to the device
     int sync_pods();                       // push new pod records to the device
     void mark_dirty(int32_t node);

@@ -108,6 +108,26 @@ __global__ void k_scatter_rows(const StagedRow* __restrict__ rows, int32_t k, No
     ext[r] = rows[j].ext;
 }
 
+// Resident hints around RemoveNode(pos) (positions after it shift down by one).  A hint
+// to the removed node is kept as -2 - pos (no usable hint: kernels read h >= 0 only) so a
+// Revert of the enclosing fork restores it: the reference keeps hints by node NAME
+// (hints.go:29-72) outside the snapshot, and the name is valid again after the Revert.
+__global__ void k_remap_hints(int32_t* __restrict__ h, int32_t n, int32_t pos, int32_t restore) {
+    const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= n) return;
+    int32_t v = h[i];
+    if (!restore) {
+        if (v == pos) v = -2 - pos;
+        else if (v > pos) v--;
+        else if (v <= -2 && -2 - v > pos) v++;      // an older removal's encoded position
+    } else {
+        if (v == -2 - pos) v = pos;
+        else if (v >= pos) v++;
+        else if (v <= -2 && -2 - v >= pos) v--;
+    }
+    h[i] = v;
+}
+
 }  // namespace casim
 
 using namespace casim;
@@ -140,6 +160,7 @@ void ca_mirror::node_apply(int32_t node, const ca_pod_spec& p, int sign) {
         for (int w = 0; w < CA_PORT_WORDS; w++) nd.ports[w] &= ~p.port_use[w];
     }
     nd.npods += sign;
+    if (p.flags & CA_POD_REQUIRED_ANTI_AFFINITY) n_scope_blockers += sign;
     mark_dirty(node);
 }
 
@@ -220,6 +241,14 @@ void ca_mirror::fill_static(int32_t i, NodeStatic& s) const {
     for (int k = 0; k < CA_MAX_INT_KEYS; k++) s.ints[k] = n.int_label[k];
     s.int_valid = n.int_label_valid;
     s.name_id = n.name_id;
+}
+
+int ca_mirror::remap_hints_removed(int32_t pos, bool restore) {
+    if (d_hints_n == 0) return CA_OK;
+    hipLaunchKernelGGL(k_remap_hints, dim3((unsigned)((d_hints_n + 255) / 256)), dim3(256), 0, stream,
+                       d_pod_hints.as<int32_t>(), (int32_t)d_hints_n, pos, restore ? 1 : 0);
+    CA_HIP_CHECK(hipGetLastError());
+    return CA_OK;
 }
 
 int ca_mirror::sync_nodes() {
@@ -369,7 +398,9 @@ __global__ void __launch_bounds__(256) k_check_templates(
     const PodHot p = ph[samples[e]];
     ca_pred_result r;
     r.type = CA_PRED_OK; r.plugin = 0; r.reasons = 0; r.taint = 0;
-    if (p.flags & PF_PREFILTER_FAIL) {
+    if ((p.flags & PF_OUT_OF_SCOPE) || (thot[g].flags & NF_OUT_OF_SCOPE)) {
+        r.type = CA_PRED_UNSUPPORTED;                    // casim.h scope: the Go path evaluates it
+    } else if (p.flags & PF_PREFILTER_FAIL) {
         r.type = CA_PRED_INTERNAL;
         r.plugin = CA_PLUGIN_NODE_AFFINITY;
     } else {
@@ -499,7 +530,7 @@ int ca_mirror_clear(ca_mirror* m) {
     if (!m) return CA_EINVAL;
     m->n_ext_pods = 0;
     m->nodes.clear(); m->pods.clear(); m->terms.clear(); m->reqs.clear(); m->pf_names.clear();
-    m->journal.clear(); m->depth = 0;
+    m->journal.clear(); m->depth = 0; m->removed_nodes.clear(); m->n_scope_blockers = 0;
     m->dirty_rows.clear(); m->dirty_flag.clear();
     m->all_dirty = true; m->static_dirty = true; m->d_rows = 0;
     m->d_pods_synced = 0; m->d_terms_synced = 0;
@@ -583,6 +614,41 @@ int ca_mirror_remove_pod(ca_mirror* m, int32_t pod_id) {
     return CA_OK;
 }
 
+int ca_mirror_remove_node(ca_mirror* m, int32_t node_pos) {
+    if (!m) return CA_EINVAL;
+    if (node_pos < 0 || (size_t)node_pos >= m->nodes.size()) return CA_ENOTFOUND;   // ErrNodeNotFound
+    CA_HIP_CHECK(hipSetDevice(m->device));
+    NodeRow row = std::move(m->nodes[node_pos]);
+    m->nodes.erase(m->nodes.begin() + node_pos);
+    for (int32_t id : row.pods) {
+        m->pods[id].node = -1;
+        if (m->pods[id].spec.flags & CA_POD_REQUIRED_ANTI_AFFINITY) m->n_scope_blockers--;
+    }
+    for (PodRow& pr : m->pods) if (pr.node > node_pos) pr.node--;
+    // positions moved: every row is re-uploaded before the next kernel
+    m->dirty_rows.clear();
+    m->dirty_flag.assign(m->nodes.size(), 0);
+    m->all_dirty = true;
+    m->static_dirty = true;
+    if (m->d_rows > m->nodes.size()) m->d_rows = m->nodes.size();
+    int rc = m->remap_hints_removed(node_pos, false);
+    if (rc != CA_OK) return rc;
+    if (m->depth > 0) {
+        JournalEntry e;
+        std::memset(&e, 0, sizeof e);
+        e.kind = J_REMOVE_NODE; e.node = node_pos; e.pod = -1; e.slot = (int32_t)m->removed_nodes.size();
+        m->journal.push_back(e);
+        m->removed_nodes.push_back(std::move(row));
+    }
+    return CA_OK;
+}
+
+int ca_mirror_scope_blockers(const ca_mirror* m, int32_t* out_n) {
+    if (!m || !out_n) return CA_EINVAL;
+    *out_n = (int32_t)m->n_scope_blockers;
+    return CA_OK;
+}
+
 int ca_mirror_fork(ca_mirror* m) {
     if (!m) return CA_EINVAL;
     m->depth++;
@@ -617,6 +683,21 @@ int ca_mirror_revert(ca_mirror* m) {
             nd.pods.push_back(nd.pods[e.slot]);
             nd.pods[e.slot] = e.pod;
             m->pods[e.pod].node = e.node;
+        } else if (e.kind == J_REMOVE_NODE) {
+            const int32_t pos = e.node;
+            for (PodRow& pr : m->pods) if (pr.node >= pos) pr.node++;
+            m->nodes.insert(m->nodes.begin() + pos, std::move(m->removed_nodes.back()));
+            m->removed_nodes.pop_back();
+            for (int32_t id : m->nodes[pos].pods) {
+                m->pods[id].node = pos;
+                if (m->pods[id].spec.flags & CA_POD_REQUIRED_ANTI_AFFINITY) m->n_scope_blockers++;
+            }
+            m->dirty_rows.clear();
+            m->dirty_flag.assign(m->nodes.size(), 0);
+            m->all_dirty = true;
+            m->static_dirty = true;
+            int rc = m->remap_hints_removed(pos, true);
+            if (rc != CA_OK) return rc;
         }
     }
     m->depth--;
@@ -630,8 +711,12 @@ int ca_mirror_commit(ca_mirror* m) {
     while (i >= 0 && m->journal[i].kind != J_FORK) i--;
     if (i < 0) return CA_ESTATE;
     m->depth--;
-    if (m->depth == 0) m->journal.clear();
-    else m->journal.erase(m->journal.begin() + i);
+    if (m->depth == 0) {
+        m->journal.clear();
+        m->removed_nodes.clear();            // committed removals are permanent
+    } else {
+        m->journal.erase(m->journal.begin() + i);
+    }
     return CA_OK;
 }
 
@@ -714,6 +799,7 @@ int ca_fits_any_node(ca_mirror* m, const ca_pod_table* t, int32_t pod, const ca_
     *out_node = -1;
     if (out_prefilter_failed) *out_prefilter_failed = 0;
     const ca_pod_spec& ps = t->pods[pod];
+    if ((ps.flags & CA_POD_OUT_OF_SCOPE) || m->n_scope_blockers > 0) return CA_EUNSUPPORTED;   // casim.h scope
     if (ps.flags & CA_POD_PREFILTER_FAIL) {                 // schedulerbased.go:109-112
         if (out_prefilter_failed) *out_prefilter_failed = 1;
         return CA_OK;
@@ -790,11 +876,13 @@ int ca_fits_any_node(ca_mirror* m, const ca_pod_table* t, int32_t pod, const ca_
 int ca_check_predicates(ca_mirror* m, const ca_pod_table* t, int32_t pod, int32_t node_pos, ca_pred_result* out) {
     if (!m || !t || !out || pod < 0 || pod >= t->n_pods) return CA_EINVAL;
     std::memset(out, 0, sizeof *out);
+    if ((t->pods[pod].flags & CA_POD_OUT_OF_SCOPE) || m->n_scope_blockers > 0) return CA_EUNSUPPORTED;
     if (node_pos < 0 || (size_t)node_pos >= m->nodes.size()) {   // schedulerbased.go:143-147
         out->type = CA_PRED_INTERNAL;
         return CA_OK;
     }
     const ca_pod_spec& ps = t->pods[pod];
+    if ((ps.flags & CA_POD_OUT_OF_SCOPE) || m->n_scope_blockers > 0) return CA_EUNSUPPORTED;   // casim.h scope
     if (ps.flags & CA_POD_PREFILTER_FAIL) {                       // :153-161
         out->type = CA_PRED_INTERNAL;
         out->plugin = CA_PLUGIN_NODE_AFFINITY;
@@ -838,6 +926,8 @@ int ca_fits_matrix(ca_mirror* m, const ca_podset* s, uint8_t* out) {
     if ((rc = m->sync_nodes()) != CA_OK) return rc;
     const int32_t n = (int32_t)m->nodes.size();
     const int32_t P = s->t.n_pods;
+    if (m->n_scope_blockers > 0) return CA_EUNSUPPORTED;
+    for (const ca_pod_spec& ps : s->h_pods) if (ps.flags & CA_POD_OUT_OF_SCOPE) return CA_EUNSUPPORTED;
     if (n == 0 || P == 0) return CA_OK;
     const size_t bytes = (size_t)n * (size_t)P;
     if ((rc = m->d_scratch2.reserve(bytes)) != CA_OK) return rc;
@@ -858,6 +948,7 @@ int ca_check_templates(ca_mirror* m, const ca_podset* s, const int32_t* samples,
     if (!samples || !templates || (!out && !out_ok)) return CA_EINVAL;
     for (int32_t e = 0; e < n_samples; e++)
         if (samples[e] < 0 || samples[e] >= s->t.n_pods) return CA_EINVAL;
+    if (m->n_scope_blockers > 0) return CA_EUNSUPPORTED;
     CA_HIP_CHECK(hipSetDevice(m->device));
     // the test node: the template with its pods (NodeInfo of a fresh template copy)
     std::vector<NodeHot> h(n_templates);
@@ -881,6 +972,7 @@ int ca_check_templates(ca_mirror* m, const ca_podset* s, const int32_t* samples,
         }
         if (ports) f |= NF_PORTS;
         if (sc) f |= NF_SCALAR;
+        if (n.flags & CA_NODE_ANTI_AFFINITY_PODS) f |= NF_OUT_OF_SCOPE;
         h[g].flags = f;
         std::memset(&st[g], 0, sizeof st[g]);
         st[g].taints = n.taints;

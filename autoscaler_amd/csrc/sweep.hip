@@ -1091,6 +1091,36 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     return CA_OK;
 }
 
+// Prefix protocol (include/casim.h kernel scope): the first candidate that would be
+// simulated with a CA_POD_OUT_OF_SCOPE pod to move, or C.
+int32_t scope_cut(const ca_mirror* m, int32_t C, const int32_t* candidates, const uint8_t* dest_mask,
+                  const int32_t* status, const int32_t* move_off, const int32_t* move_pods) {
+    const int32_t n = (int32_t)m->nodes.size(), np = (int32_t)m->pods.size();
+    for (int32_t c = 0; c < C; c++) {
+        const int32_t nd = candidates[c];
+        if (nd < 0 || nd >= n || !dest_mask[nd] || (status && status[c] != 0)) continue;
+        for (int32_t i = move_off[c]; i < move_off[c + 1]; i++) {
+            const int32_t id = move_pods[i];
+            if (id >= 0 && id < np && (m->pods[id].spec.flags & CA_POD_OUT_OF_SCOPE)) return c;
+        }
+    }
+    return C;
+}
+
+void fill_cut(ca_removal_result* results, int32_t cut, int32_t C, int32_t last_index, int32_t* out_dest,
+              const int32_t* move_off) {
+    for (int32_t c = cut; c < C; c++) {
+        ca_removal_result& r = results[c];
+        r.removable = 0;
+        r.reason = c == cut ? CA_UNREMOVABLE_OUT_OF_SCOPE : CA_UNREMOVABLE_NOT_RUN;
+        r.n_placed = 0;
+        r.last_index_in = last_index;
+        r.evals = 0;
+        if (out_dest)
+            for (int32_t i = move_off[c]; i < move_off[c + 1]; i++) out_dest[i] = -1;
+    }
+}
+
 }  // namespace casim
 
 extern "C" {
@@ -1108,6 +1138,18 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     if (move_off[0] != 0 || M < 0) return CA_EINVAL;
     for (int32_t c = 0; c < C; c++)
         if (move_off[c + 1] < move_off[c]) return CA_EINVAL;
+    if (m->n_scope_blockers > 0) return CA_EUNSUPPORTED;        // casim.h scope
+    {
+        const int32_t cut = scope_cut(m, C, candidates, dest_mask, cand_status, move_off, move_pods);
+        if (cut < C) {                                            // prefix protocol
+            int rc = cut > 0 ? ca_find_nodes_to_remove(m, candidates, cut, dest_mask, cand_status, move_off, move_pods,
+                                                       hints, last_index, results, out_dest)
+                             : CA_OK;
+            if (rc != CA_OK) return rc;
+            fill_cut(results, cut, C, *last_index, out_dest, move_off);
+            return CA_OK;
+        }
+    }
     // duplicate candidates share hints between their simulations: run them in
     // separate sequential segments (Hints.Set of one is seen by the next).
     {
@@ -1199,6 +1241,8 @@ int ca_removal_stats(const ca_mirror* m, int32_t* rounds, float* kernel_ms, floa
 struct ca_removal_plan {
     ca_mirror* m = nullptr;
     int32_t C = 0, M = 0, n = 0;
+    int32_t C_all = 0;              // candidates of the call; C = the prefix before the scope cut
+    std::vector<int32_t> off_all;
     std::vector<int32_t> cand, status, off, moves;
     std::vector<uint8_t> mask;
     casim::DevBuf d_in;
@@ -1225,7 +1269,7 @@ int ca_removal_plan_create(ca_mirror* m, const int32_t* candidates, int32_t C, c
     if (!m || !out || C < 0 || (C > 0 && (!candidates || !dest_mask || !move_off))) return CA_EINVAL;
     CA_HIP_CHECK(hipSetDevice(m->device));
     const int32_t n = (int32_t)m->nodes.size();
-    const int32_t M = C > 0 ? move_off[C] - move_off[0] : 0;
+    int32_t M = C > 0 ? move_off[C] - move_off[0] : 0;
     if (C > 0 && (move_off[0] != 0 || M < 0)) return CA_EINVAL;
     std::vector<uint8_t> seen((size_t)std::max(n, 1), 0);
     for (int32_t c = 0; c < C; c++) {
@@ -1239,6 +1283,12 @@ int ca_removal_plan_create(ca_mirror* m, const int32_t* candidates, int32_t C, c
     const int32_t np = (int32_t)m->pods.size();
     for (int32_t i = 0; i < M; i++) if (move_pods[i] < 0 || move_pods[i] >= np) return CA_EINVAL;
     ca_removal_plan* p = new ca_removal_plan();
+    p->C_all = C;
+    p->off_all.assign(move_off, move_off + C + 1);
+    // prefix protocol (casim.h scope): the plan simulates the candidates before the first
+    // out-of-scope one; run() reports the rest
+    C = casim::scope_cut(m, C, candidates, dest_mask, cand_status, move_off, move_pods);
+    M = move_off[C] - move_off[0];
     p->m = m; p->C = C; p->M = M; p->n = n;
     p->cand.assign(candidates, candidates + C);
     p->status = cand_status ? std::vector<int32_t>(cand_status, cand_status + C) : std::vector<int32_t>((size_t)C, 0);
@@ -1266,11 +1316,23 @@ int ca_removal_plan_create(ca_mirror* m, const int32_t* candidates, int32_t C, c
 
 int ca_removal_plan_run(ca_removal_plan* p, int32_t* hints, int32_t* last_index, ca_removal_result* results,
                         int32_t* out_dest) {
-    if (!p || !last_index || (p->C > 0 && !results)) return CA_EINVAL;
+    if (!p || !last_index || (p->C_all > 0 && !results)) return CA_EINVAL;
     ca_mirror* m = p->m;
     CA_HIP_CHECK(hipSetDevice(m->device));
-    if (p->C == 0) return CA_OK;
+    if (p->C_all == 0) return CA_OK;
     if ((int32_t)m->nodes.size() != p->n) return CA_EINVAL;   // the plan's dest mask covers the node list
+    if (m->n_scope_blockers > 0) return CA_EUNSUPPORTED;        // casim.h scope
+    if (p->C < p->C_all) {                                      // prefix protocol
+        int rc = CA_OK;
+        if (p->C > 0) {
+            p->C_all = p->C;                                    // run the prefix as a full plan
+            rc = ca_removal_plan_run(p, hints, last_index, results, out_dest);
+            p->C_all = (int32_t)p->off_all.size() - 1;
+        }
+        if (rc != CA_OK) return rc;
+        casim::fill_cut(results, p->C, p->C_all, *last_index, out_dest, p->off_all.data());
+        return CA_OK;
+    }
     int rc;
     if ((rc = m->sync_nodes()) != CA_OK) return rc;
     if ((rc = m->sync_pods()) != CA_OK) return rc;

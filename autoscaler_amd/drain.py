@@ -12,11 +12,12 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import Optional
 
-from .k8s import Pod
+from .k8s import Pod, is_daemonset_pod
 
 PodSafeToEvictKey = "cluster-autoscaler.kubernetes.io/safe-to-evict"       # drain.go:42
 ConfigMirrorAnnotationKey = "kubernetes.io/config.mirror"
-PodLongTerminatingExtraThreshold = 30.0
+PodLongTerminatingExtraThreshold = 30.0                                    # drain.go:34
+DefaultTerminationGracePeriodSeconds = 30                                  # core/v1 types.go
 
 # BlockingPodReason (drain.go:51-73)
 NoReason, ControllerNotFound, MinReplicasReached, NotReplicated, LocalStorageRequested, \
@@ -58,7 +59,28 @@ def is_mirror_pod(p: Pod) -> bool:
 
 
 def has_local_storage(p: Pod) -> bool:
+    """HasLocalStorage / isLocalVolume (drain.go:253-265)."""
     return any(v in ("emptyDir", "hostPath") for v in p.volumes)
+
+
+def is_pod_long_terminating(p: Pod, now: float) -> bool:
+    """IsPodLongTerminating (drain.go:293-306): DeletionTimestamp + grace (nil -> 30 s) +
+    PodLongTerminatingExtraThreshold is strictly before now."""
+    if p.deletion_timestamp is None:
+        return False
+    grace = p.termination_grace_period_seconds
+    if grace is None:
+        grace = DefaultTerminationGracePeriodSeconds
+    return p.deletion_timestamp + grace + PodLongTerminatingExtraThreshold < now
+
+
+def is_pod_terminal(p: Pod) -> bool:
+    """isPodTerminal (drain.go:239-251)."""
+    if p.restart_policy == "Never" and p.phase in ("Succeeded", "Failed"):
+        return True
+    if p.restart_policy == "OnFailure" and p.phase == "Succeeded":
+        return True
+    return p.phase == "Failed"
 
 
 def get_pods_for_deletion_on_node_drain(pods: list, pdbs: list, skip_system: bool, skip_local: bool,
@@ -70,15 +92,17 @@ def get_pods_for_deletion_on_node_drain(pods: list, pdbs: list, skip_system: boo
     for pod in pods:
         if is_mirror_pod(pod):
             continue
-        if pod.deletion_timestamp is not None and now - pod.deletion_timestamp > PodLongTerminatingExtraThreshold:
+        if is_pod_long_terminating(pod, now):                                  # :107-112
             continue
         is_ds = False
         replicated = False
         safe = pod.annotations.get(PodSafeToEvictKey) == "true"
-        terminal = pod.phase in ("Succeeded", "Failed")
+        terminal = is_pod_terminal(pod)
         ref = pod.controller_ref()
         kind = ref.kind if ref else ""
-        if kind in ("ReplicationController", "ReplicaSet"):
+        # branch order of drain.go:129-205: ReplicationController, IsDaemonSetPod, Job,
+        # ReplicaSet, StatefulSet
+        if kind == "ReplicationController":
             if check_refs:
                 obj = listers.get(kind, pod.namespace, ref.name)
                 if obj == "missing":
@@ -86,10 +110,18 @@ def get_pods_for_deletion_on_node_drain(pods: list, pdbs: list, skip_system: boo
                 if obj is not None and obj < min_replica:
                     return [], [], BlockingPod(pod, MinReplicasReached), "too few replicas"
             replicated = True
-        elif kind == "DaemonSet":
+        elif is_daemonset_pod(pod):
             is_ds = True
-            if check_refs and listers.get("DaemonSet", pod.namespace, ref.name) == "missing":
+            if check_refs and kind == "DaemonSet" and listers.get("DaemonSet", pod.namespace, ref.name) == "missing":
                 return [], [], BlockingPod(pod, ControllerNotFound), "daemonset not found"
+        elif kind == "ReplicaSet":
+            if check_refs:
+                obj = listers.get(kind, pod.namespace, ref.name)
+                if obj == "missing":
+                    return [], [], BlockingPod(pod, ControllerNotFound), "controller not found"
+                if obj is not None and obj < min_replica:
+                    return [], [], BlockingPod(pod, MinReplicasReached), "too few replicas"
+            replicated = True
         elif kind in ("Job", "StatefulSet"):
             if check_refs and listers.get(kind, pod.namespace, ref.name) == "missing":
                 return [], [], BlockingPod(pod, ControllerNotFound), f"{kind} not found"

@@ -19,13 +19,11 @@ import numpy as np
 from . import abi
 from .clustersnapshot import ClusterSnapshot, NodeInfo
 from .k8s import Pod
-from .predicatechecker import SchedulerBasedPredicateChecker
+from .predicatechecker import SchedulerBasedPredicateChecker, unsupported
+from .scope import UnsupportedByKernels, out_of_scope_reason
 
 BinpackingEstimatorName = "binpacking"          # estimator.go:27-28
-
-
-class UnsupportedByKernels(RuntimeError):
-    """CA_EUNSUPPORTED: the caller must use the reference (Go) path for this input."""
+__all__ = ["BinpackingNodeEstimator", "UnsupportedByKernels", "estimate_batch"]
 
 
 @dataclass
@@ -76,13 +74,16 @@ def estimate_batch(checker: SchedulerBasedPredicateChecker, snapshot: ClusterSna
     for g, (node, tpods) in enumerate(templates_api):
         templates[g] = snapshot.interner.encode_template(node, tpods)
     pod_idx = np.arange(len(all_pods), dtype=np.int32)
-    out = snapshot.backend.estimate(table, np.array(offs, np.int32), pod_idx, templates, limiter.max_nodes,
-                                    checker.last_index)
+    with unsupported("Estimate: the snapshot holds a pod with required anti-affinity"):
+        out = snapshot.backend.estimate(table, np.array(offs, np.int32), pod_idx, templates, limiter.max_nodes,
+                                        checker.last_index)
     counts, scheduled = [], []
     for g in range(len(groups)):
         r = out.results[g]
         if int(r["status"]) == abi.CA_EUNSUPPORTED:
-            raise UnsupportedByKernels(f"node group {g}: pods depend on node identity (hostname / nodeName)")
+            why = next((out_of_scope_reason(p) for p in groups[g][0] if out_of_scope_reason(p)), None)
+            raise UnsupportedByKernels(f"node group {g}: " + (why or "pods depend on node identity (hostname / "
+                                                                      "nodeName) or template pods need InterPodAffinity"))
         counts.append(int(r["node_count"]))
         n = int(r["n_scheduled"])
         scheduled.append([all_pods[i] for i in out.sched_pod[offs[g]: offs[g] + n]])

@@ -23,7 +23,8 @@ from typing import Iterable, Optional
 import numpy as np
 
 from . import abi
-from .k8s import Node, Pod, Quantity, Taint, Toleration
+from .k8s import Node, Pod, Quantity, Taint, Toleration, is_daemonset_pod
+from .scope import has_required_anti_affinity, out_of_scope_reason
 
 TPU_PREFIX = "cloud-tpus.google.com/"           # CA/utils/tpu/tpu.go:27
 HOSTNAME_KEY = "kubernetes.io/hostname"
@@ -309,6 +310,8 @@ class Interner:
         t["used_scalar"] = sc
         t["used_pods"] = len(pods)
         t["used_ports"] = _bits(ports, abi.CA_PORT_WORDS)
+        if any(has_required_anti_affinity(p) for p in pods):       # casim.h kernel scope
+            t["node"]["flags"] |= abi.CA_NODE_ANTI_AFFINITY_PODS
         return t
 
     # -- pods -----------------------------------------------------------------
@@ -430,9 +433,12 @@ class Interner:
                 names.extend(pf)
         if hostname_dep:
             flags |= abi.CA_POD_HOSTNAME_DEPENDENT
-        ref = p.controller_ref()
-        if ref is not None and ref.kind == "DaemonSet":
+        if is_daemonset_pod(p):                            # pod_util.IsDaemonSetPod (similar_pods.go:86-88)
             flags |= abi.CA_POD_DAEMONSET
+        if out_of_scope_reason(p) is not None:
+            flags |= abi.CA_POD_OUT_OF_SCOPE
+        if has_required_anti_affinity(p):
+            flags |= abi.CA_POD_REQUIRED_ANTI_AFFINITY
         rec["flags"] = flags
         rec["similar_class"] = self.similar_class(p)
 

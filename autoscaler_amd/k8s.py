@@ -119,7 +119,17 @@ class Affinity:
     # nil vs present matters: None == RequiredDuringSchedulingIgnoredDuringExecution nil
     required_terms: Optional[list] = None
     pod_affinity: bool = False            # any PodAffinity / PodAntiAffinity present
-    required_anti_affinity: bool = False
+    required_anti_affinity: bool = False  # PodAntiAffinity.RequiredDuringScheduling... terms present
+    required_pod_affinity: bool = False   # PodAffinity.RequiredDuringScheduling... terms present
+
+
+@dataclass
+class TopologySpreadConstraint:
+    """v1.TopologySpreadConstraint (the fields the scope classifier reads)."""
+    max_skew: int = 1
+    topology_key: str = ""
+    when_unsatisfiable: str = "DoNotSchedule"     # DoNotSchedule | ScheduleAnyway
+    match_labels: dict = field(default_factory=dict)
 
 
 @dataclass
@@ -151,6 +161,7 @@ class Pod:
     deletion_timestamp: Optional[float] = None
     priority: Optional[int] = None                  # Spec.Priority (corev1helpers.PodPriority: nil -> 0)
     termination_grace_period_seconds: Optional[int] = None   # Spec.TerminationGracePeriodSeconds
+    restart_policy: str = "Always"                  # Spec.RestartPolicy (Always | OnFailure | Never)
 
     def controller_ref(self) -> Optional[OwnerReference]:
         for r in self.owner_refs:
@@ -225,6 +236,18 @@ def set_rs_pod(pod: Pod, rs_name: str) -> Pod:
 def set_ds_pod(pod: Pod) -> Pod:
     pod.owner_refs = [OwnerReference("DaemonSet", "ds", "api/v1/namespaces/default/daemonsets/ds")]
     return pod
+
+
+DAEMONSET_POD_ANNOTATION = "cluster-autoscaler.kubernetes.io/daemonset-pod"   # utils/pod/pod.go:26-27
+
+
+def is_daemonset_pod(pod: Pod) -> bool:
+    """pod_util.IsDaemonSetPod (CA/utils/pod/pod.go:32-43): controller kind DaemonSet, or the
+    cluster-autoscaler.kubernetes.io/daemonset-pod=true annotation."""
+    ref = pod.controller_ref()
+    if ref is not None and ref.kind == "DaemonSet":
+        return True
+    return pod.annotations.get(DAEMONSET_POD_ANNOTATION) == "true"
 
 
 def set_mirror_pod(pod: Pod) -> Pod:

@@ -55,6 +55,8 @@ def load() -> C.CDLL:
         "ca_mirror_add_nodes": ([vp, vp, i32, p(i32)], C.c_int),
         "ca_mirror_add_pods": ([vp, vp, vp, vp, i32, vp], C.c_int),
         "ca_mirror_remove_pod": ([vp, i32], C.c_int),
+        "ca_mirror_remove_node": ([vp, i32], C.c_int),
+        "ca_mirror_scope_blockers": ([vp, p(i32)], C.c_int),
         "ca_mirror_fork": ([vp], C.c_int),
         "ca_mirror_revert": ([vp], C.c_int),
         "ca_mirror_commit": ([vp], C.c_int),
@@ -112,6 +114,7 @@ def exported_symbols() -> list[str]:
         "ca_abi_version", "ca_abi_struct_sizes", "ca_device_count", "ca_status_string", "ca_host_alloc",
         "ca_host_free", "ca_mirror_create",
         "ca_mirror_destroy", "ca_mirror_clear", "ca_mirror_add_nodes", "ca_mirror_add_pods", "ca_mirror_remove_pod",
+        "ca_mirror_remove_node", "ca_mirror_scope_blockers",
         "ca_mirror_fork", "ca_mirror_revert", "ca_mirror_commit", "ca_mirror_node_count", "ca_mirror_pod_node",
         "ca_mirror_node_pods", "ca_podset_create", "ca_podset_destroy", "ca_fits_any_node", "ca_check_predicates",
         "ca_fits_matrix", "ca_check_templates", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
@@ -240,6 +243,14 @@ class Mirror:
 
     def remove_pod(self, pod_id: int) -> None:
         _check(self.lib.ca_mirror_remove_pod(self.h, pod_id), "ca_mirror_remove_pod")
+
+    def remove_node(self, pos: int) -> None:
+        _check(self.lib.ca_mirror_remove_node(self.h, pos), "ca_mirror_remove_node")
+
+    def scope_blockers(self) -> int:
+        n = C.c_int32(0)
+        _check(self.lib.ca_mirror_scope_blockers(self.h, C.byref(n)), "ca_mirror_scope_blockers")
+        return n.value
 
     def fork(self) -> None:
         _check(self.lib.ca_mirror_fork(self.h), "ca_mirror_fork")

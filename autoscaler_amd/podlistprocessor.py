@@ -14,7 +14,7 @@ import numpy as np
 
 from .clustersnapshot import ClusterSnapshot
 from .k8s import Pod
-from .predicatechecker import SchedulerBasedPredicateChecker
+from .predicatechecker import SchedulerBasedPredicateChecker, unsupported
 from .simulator import HintingSimulator, Hints, Status
 
 
@@ -36,8 +36,9 @@ def TrySchedulePodsAnywhere(sim: HintingSimulator, snapshot: ClusterSnapshot, po
         if ok and name in snapshot._state.pos:
             hints[k] = snapshot.position(name)
     pc = sim.predicate_checker
-    out = snapshot.backend.filter_out_schedulable(table, None, owners if n_classes > 0 else None, hints,
-                                                  pc.last_index)
+    with unsupported("FilterOutSchedulable: a pending pod or the snapshot is out of kernel scope"):
+        out = snapshot.backend.filter_out_schedulable(table, None, owners if n_classes > 0 else None, hints,
+                                                      pc.last_index)
     pc.last_index = out.last_index
     pc.evals += int(out.evals)
     statuses, placed = [], []

@@ -8,6 +8,7 @@ reason constants.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Callable, Optional, Union
 
 import numpy as np
@@ -15,6 +16,18 @@ import numpy as np
 from . import abi
 from .clustersnapshot import ClusterSnapshot, NodeInfo, NodeNotFoundError
 from .k8s import Pod
+from .scope import UnsupportedByKernels
+
+
+@contextlib.contextmanager
+def unsupported(what: str):
+    """Map a backend's CA_EUNSUPPORTED (include/casim.h kernel scope) to UnsupportedByKernels."""
+    try:
+        yield
+    except Exception as e:                      # CasimError (libcasim) / OracleError (checker)
+        if getattr(e, "status", None) == abi.CA_EUNSUPPORTED:
+            raise UnsupportedByKernels(what) from e
+        raise
 
 NotSchedulablePredicateError = 0     # error.go:27-32
 InternalPredicateError = 1
@@ -95,7 +108,8 @@ class SchedulerBasedPredicateChecker:
             return "", SchedulingError("ClusterSnapshot not provided")
         table = snapshot.encode([pod])
         match = self._match(snapshot, node_matches)
-        node, li, pf, ev = snapshot.backend.fits_any_node(table, 0, match, self.last_index)
+        with unsupported(f"FitsAnyNode({pod.name}): out of kernel scope"):
+            node, li, pf, ev = snapshot.backend.fits_any_node(table, 0, match, self.last_index)
         self.evals += ev
         if pf:
             return "", SchedulingError(f"error running pre filter plugins for pod {pod.name}; {ERR_REASON_AFFINITY_CONFLICT}")
@@ -113,7 +127,8 @@ class SchedulerBasedPredicateChecker:
             return PredicateError(InternalPredicateError, "",
                                   f"Error obtaining NodeInfo for name {node_name}; {e}", None)
         table = snapshot.encode([pod])
-        typ, plugin, reasons, taint = snapshot.backend.check_predicates(table, 0, pos)
+        with unsupported(f"CheckPredicates({pod.name}): out of kernel scope"):
+            typ, plugin, reasons, taint = snapshot.backend.check_predicates(table, 0, pos)
         if typ == abi.CA_PRED_INTERNAL:
             return PredicateError(InternalPredicateError, "", ERR_REASON_AFFINITY_CONFLICT,
                                   [ERR_REASON_AFFINITY_CONFLICT])

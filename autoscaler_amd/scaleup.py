@@ -27,7 +27,7 @@ import numpy as np
 from . import abi
 from .clustersnapshot import ClusterSnapshot, NodeInfo
 from .estimator import ThresholdBasedEstimationLimiter, estimate_batch
-from .k8s import Pod
+from .k8s import Pod, is_daemonset_pod
 from .predicatechecker import SchedulerBasedPredicateChecker
 from .simulator import SimilarPodsScheduling
 
@@ -48,7 +48,7 @@ def BuildPodGroups(pods: list) -> list:  # noqa: N802
     by_controller: dict = {}
     for pod in pods:
         ref = pod.controller_ref()
-        if ref is None or ref.kind == "DaemonSet":                 # :68-72
+        if ref is None or is_daemonset_pod(pod):                  # :68-72 (pod_util.IsDaemonSetPod)
             groups.append(PodGroup([pod]))
             continue
         egs = by_controller.setdefault(ref.uid, [])

@@ -16,8 +16,9 @@ import numpy as np
 from . import abi
 from .clustersnapshot import ClusterSnapshot
 from .drain import BlockingPod, ListerRegistry, NodeDeleteOptions, get_pods_to_move
-from .k8s import Node, Pod
-from .predicatechecker import SchedulerBasedPredicateChecker
+from .k8s import Node, Pod, is_daemonset_pod
+from .predicatechecker import SchedulerBasedPredicateChecker, unsupported
+from .scope import UnsupportedByKernels, out_of_scope_reason
 
 # UnremovableReason (cluster.go:58-90)
 (NoReason, ScaleDownDisabledAnnotation, ScaleDownUnreadyDisabled, NotAutoscaled, NotUnneededLongEnough,
@@ -101,8 +102,7 @@ class SimilarPodsScheduling:
 
     def SetUnschedulable(self, pod: Pod) -> None:  # noqa: N802
         k = self._key(pod)
-        ref = pod.controller_ref()
-        if k is None or (ref is not None and ref.kind == "DaemonSet"):
+        if k is None or is_daemonset_pod(pod):           # similar_pods.go:86-88
             return
         lst = self.items.setdefault(k, [])
         if len(lst) >= self.max_pods_per_owner_ref:
@@ -203,9 +203,15 @@ class RemovalSimulator:
             if ok and node in snap._state.pos:
                 hints[pid] = snap.position(node)
         before = hints.copy()
-        out = snap.backend.find_nodes_to_remove(np.array(cand_pos, np.int32), mask, np.array(status, np.int32),
-                                                np.array(move_off, np.int32), np.array(move_ids, np.int32), hints,
-                                                self.predicate_checker.last_index)
+        with unsupported("FindNodesToRemove: the snapshot holds a pod with required anti-affinity"):
+            out = snap.backend.find_nodes_to_remove(np.array(cand_pos, np.int32), mask, np.array(status, np.int32),
+                                                    np.array(move_off, np.int32), np.array(move_ids, np.int32), hints,
+                                                    self.predicate_checker.last_index)
+        cut = next((c for c in range(len(candidates))
+                    if int(out.results[c]["reason"]) == abi.CA_UNREMOVABLE_OUT_OF_SCOPE), None)
+        if cut is not None:
+            why = next((out_of_scope_reason(p) for p in moved_pods[cut] if out_of_scope_reason(p)), "out of scope")
+            raise UnsupportedByKernels(f"FindNodesToRemove: candidate {candidates[cut]}: {why}")
         self.predicate_checker.last_index = out.last_index
         self.predicate_checker.evals += int(out.results["evals"].sum())
         for pid in np.nonzero(out.hints != before)[0]:

@@ -23,7 +23,7 @@ import numpy as np
 
 from . import abi
 from .drain import get_pods_for_deletion_on_node_drain, is_mirror_pod
-from .k8s import Node, Pod
+from .k8s import Node, Pod, is_daemonset_pod
 
 ResourceCPU, ResourceMemory = "cpu", "memory"
 DaemonSetPodAnnotationKey = "cluster-autoscaler.kubernetes.io/daemonset-pod"   # utils/pod/pod.go:27
@@ -58,12 +58,6 @@ class UtilizationError(Exception):
     pass
 
 
-def is_daemonset_pod(p: Pod) -> bool:
-    """pod_util.IsDaemonSetPod (CA/utils/pod/pod.go:32-43)."""
-    ref = p.controller_ref()
-    if ref is not None and ref.kind == "DaemonSet":
-        return True
-    return p.annotations.get(DaemonSetPodAnnotationKey) == "true"
 
 
 def _milli(reqs: list, name: str) -> int:

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define CASIM_ABI_VERSION 1
+#define CASIM_ABI_VERSION 2
 
 /* ---- status codes (int return of every entry point) -------------------- */
 #define CA_OK            0
@@ -59,6 +59,8 @@ extern "C" {
 #define CA_EUNSUPPORTED  6  /* input needs a plugin the kernels do not implement:
                                the caller routes it to the Go scheduler framework      */
 #define CA_ESTATE        7  /* fork/revert/commit misuse                              */
+#define CA_ENOTRUN       8  /* per-item status: not evaluated because an EARLIER item of the
+                               same batch was CA_EUNSUPPORTED (prefix protocol below)   */
 
 /* ---- fixed widths of interned bitsets (host interning) -- */
 #define CA_MAX_SCALAR    8   /* extended / hugepage / attachable-volume resources   */
@@ -69,6 +71,9 @@ extern "C" {
 
 /* ---- node flags ---------------------------------------------------------- */
 #define CA_NODE_UNSCHEDULABLE   0x1u  /* node.Spec.Unschedulable                       */
+#define CA_NODE_ANTI_AFFINITY_PODS 0x2u /* ca_template only: one of the template's pods has
+                                          required pod anti-affinity (the group is out of scope,
+                                          interpodaffinity/filtering.go:230-268)              */
 
 /* ---- pod flags ----------------------------------------------------------- */
 #define CA_POD_HAS_SCALAR_KEYS        0x001u /* len(podRequest.ScalarResources) != 0 (fit.go:267-272) */
@@ -83,6 +88,17 @@ extern "C" {
 #define CA_POD_DAEMONSET              0x040u /* owned by a DaemonSet (similar_pods.go:94)            */
 #define CA_POD_HOSTNAME_DEPENDENT     0x080u /* selector/affinity/nodeName refer to node identity:
                                                 not evaluable once per template in ca_estimate_batch  */
+#define CA_POD_OUT_OF_SCOPE           0x100u /* the pod needs a filter plugin the kernels do not
+                                                implement: required pod (anti-)affinity
+                                                (interpodaffinity/filtering.go:230-268), a DoNotSchedule
+                                                topology spread constraint (podtopologyspread/
+                                                filtering.go:151-158,238-258), or a volume a volume
+                                                plugin reads (volume_binding.go:169, volume_zone.go:97-103,
+                                                volume_restrictions.go:166-176, nodevolumelimits)       */
+#define CA_POD_REQUIRED_ANTI_AFFINITY 0x200u /* the pod has required pod anti-affinity terms: while
+                                                it is in the snapshot no other pod's InterPodAffinity
+                                                PreFilter Skips (filtering.go:260-262), so every
+                                                simulation over the mirror is out of scope           */
 
 /* ---- selector requirement ops (labels/selector.go:223-267, nodeaffinity.go:297-324) */
 #define CA_OP_IN            1  /* node has key with value in set:  node.pairs & req.pairs != 0   */
@@ -108,6 +124,8 @@ extern "C" {
 #define CA_PRED_OK              0
 #define CA_PRED_NOT_SCHEDULABLE 1  /* NotSchedulablePredicateError */
 #define CA_PRED_INTERNAL        2  /* InternalPredicateError       */
+#define CA_PRED_UNSUPPORTED     3  /* not evaluated: the pod (or the template's pods) is out of
+                                      kernel scope; run this pair on the Go path          */
 
 /* reason bits of NodeResourcesFit (fit.go:256-329), in the reference's append order */
 #define CA_REASON_TOO_MANY_PODS   0x1u
@@ -126,6 +144,10 @@ extern "C" {
 #define CA_UNREMOVABLE_NO_PLACE          12 /* NoPlaceToMovePods */
 #define CA_UNREMOVABLE_BLOCKED_BY_POD    13 /* BlockedByPod      */
 #define CA_UNREMOVABLE_UNEXPECTED_ERROR  14 /* UnexpectedError   */
+/* Not reference reasons: the prefix protocol of ca_find_nodes_to_remove. */
+#define CA_UNREMOVABLE_OUT_OF_SCOPE     100 /* a pod to move is CA_POD_OUT_OF_SCOPE: simulate this
+                                               candidate on the Go path                    */
+#define CA_UNREMOVABLE_NOT_RUN          101 /* after an out-of-scope candidate: not simulated */
 
 /* ------------------------------------------------------------------------- */
 
@@ -248,6 +270,25 @@ typedef struct ca_removal_result {
 typedef struct ca_mirror ca_mirror;
 typedef struct ca_podset ca_podset;
 
+/* ---- kernel scope ------------------------------------
+ * The kernels implement the six default-profile filters of the path.  InterPodAffinity,
+ * PodTopologySpread and the volume plugins are no-ops for pods without the features
+ * above; a pod WITH them carries CA_POD_OUT_OF_SCOPE (the caller's interning classifies
+ * it) and is never simulated:
+ *   - while the mirror holds a pod flagged CA_POD_REQUIRED_ANTI_AFFINITY, every
+ *     simulation entry point returns CA_EUNSUPPORTED without running;
+ *   - ca_fits_any_node / ca_check_predicates / ca_fits_matrix / ca_filter_out_schedulable:
+ *     an out-of-scope pod in the call -> CA_EUNSUPPORTED, nothing run or changed;
+ *   - ca_check_templates: the pair's result type is CA_PRED_UNSUPPORTED (verdict 0);
+ *   - batches (ca_estimate_batch / _plan_run, ca_find_nodes_to_remove / _plan_run) use a
+ *     PREFIX protocol: items are evaluated in order up to the first out-of-scope item u
+ *     (a group with an out-of-scope or hostname-dependent pod, or a template flagged
+ *     CA_NODE_ANTI_AFFINITY_PODS; a candidate whose pods to move include an out-of-scope
+ *     pod).  Item u is reported (status CA_EUNSUPPORTED / reason CA_UNREMOVABLE_OUT_OF_SCOPE),
+ *     every later item is CA_ENOTRUN / CA_UNREMOVABLE_NOT_RUN, and *last_index is the
+ *     lastIndex item u starts from.  The call returns CA_OK; the caller runs item u on the
+ *     reference path and calls again with the remaining items. */
+
 /* ---- library ---------------------------------------------------------------- */
 int ca_abi_version(void);
 /* sizes of every ABI struct, in declaration order, for binding checks */
@@ -280,6 +321,14 @@ int ca_mirror_pod_node(const ca_mirror* m, int32_t pod_id, int32_t* out_node_pos
 /* node pods in NodeInfo.Pods order (ids), returns count in *out_n (CA_ECAPACITY if cap short) */
 int ca_mirror_node_pods(const ca_mirror* m, int32_t node_pos, int32_t* out_ids, int32_t cap,
                         int32_t* out_n);
+/* RemoveNode (clustersnapshot.go:38; delta.go:150-186): the node and the pods on it leave
+ * the snapshot.  Positions after it shift down by one (canonical order);
+ * mirror pod ids stay valid (the removed node's pods report node -1); the resident hints
+ * (ca_mirror_set_hints) are remapped the same way (hints to the removed node become -1).
+ * Journaled: a Revert of the enclosing fork restores node, position and pods. */
+int ca_mirror_remove_node(ca_mirror* m, int32_t node_pos);
+/* Pods in the mirror flagged CA_POD_REQUIRED_ANTI_AFFINITY (> 0: simulations unsupported). */
+int ca_mirror_scope_blockers(const ca_mirror* m, int32_t* out_n);
 
 /* ---- device-resident pod sets (pending pods for Estimate) ------------------ */
 int ca_podset_create(ca_mirror* m, const ca_pod_table* t, ca_podset** out);

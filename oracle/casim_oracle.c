@@ -43,7 +43,7 @@ typedef struct or_pod {
 } or_pod;
 
 /* undo journal entries (DeltaClusterSnapshot fork semantics, delta.go:43-475) */
-enum { J_FORK = 1, J_ADD_NODE, J_ADD_POD, J_REMOVE_POD };
+enum { J_FORK = 1, J_ADD_NODE, J_ADD_POD, J_REMOVE_POD, J_REMOVE_NODE };
 typedef struct or_jent {
     int32_t kind;
     int32_t node;
@@ -59,8 +59,10 @@ struct or_state {
     VEC(ca_selector_req) reqs;
     VEC(int32_t) pf_names;
     VEC(or_jent) journal;
+    VEC(or_node) removed;             /* rows of journaled RemoveNode ops          */
     int32_t depth;
     int32_t next_new_name;            /* fresh name ids for template copies        */
+    int64_t scope_blockers;           /* pods with CA_POD_REQUIRED_ANTI_AFFINITY   */
 };
 
 static int64_t wrap_sub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
@@ -77,21 +79,38 @@ static void free_nodes(or_state* s) {
     s->nodes.n = 0;
 }
 
+static void free_removed(or_state* s) {
+    for (int64_t i = 0; i < s->removed.n; i++) free(s->removed.a[i].pods.a);
+    s->removed.n = 0;
+}
+
 void or_destroy(or_state* s) {
     if (!s) return;
     free_nodes(s);
+    free_removed(s);
     free(s->nodes.a); free(s->pods.a); free(s->terms.a); free(s->reqs.a);
-    free(s->pf_names.a); free(s->journal.a);
+    free(s->pf_names.a); free(s->journal.a); free(s->removed.a);
     free(s);
 }
 
 int or_clear(or_state* s) {                       /* ClusterSnapshot.Clear() */
     free_nodes(s);
+    free_removed(s);
     s->pods.n = s->terms.n = s->reqs.n = s->pf_names.n = s->journal.n = 0;
     s->depth = 0;
     s->next_new_name = -2;
+    s->scope_blockers = 0;
     return CA_OK;
 }
+
+/* pods in the snapshot that make every simulation out of kernel scope (include/casim.h
+ * "kernel scope"): InterPodAffinity's PreFilter does not Skip while a pod with required
+ * anti-affinity exists (interpodaffinity/filtering.go:230-268) */
+static void scope_count(or_state* s, const ca_pod_spec* p, int sign) {
+    if (p->flags & CA_POD_REQUIRED_ANTI_AFFINITY) s->scope_blockers += sign;
+}
+
+int or_scope_blockers(const or_state* s) { return (int)s->scope_blockers; }
 
 int or_node_count(const or_state* s) { return (int)s->nodes.n; }
 
@@ -168,6 +187,7 @@ static void add_pod_to_node(or_state* s, int32_t pod_id, int32_t node) {
     uint64_t before[CA_PORT_WORDS];
     memcpy(before, nd->ports, sizeof before);
     node_apply(nd, &s->pods.a[pod_id].spec, +1);
+    scope_count(s, &s->pods.a[pod_id].spec, +1);
     VEC_PUSH(nd->pods, pod_id);
     s->pods.a[pod_id].node = node;
     journal(s, J_ADD_POD, node, pod_id, (int32_t)nd->pods.n - 1, before);
@@ -199,8 +219,31 @@ int or_remove_pod(or_state* s, int32_t pod_id) {
     nd->pods.a[slot] = nd->pods.a[nd->pods.n - 1];
     nd->pods.n--;
     node_apply(nd, &s->pods.a[pod_id].spec, -1);
+    scope_count(s, &s->pods.a[pod_id].spec, -1);
     s->pods.a[pod_id].node = -1;
     journal(s, J_REMOVE_POD, node, pod_id, (int32_t)slot, before);
+    return CA_OK;
+}
+
+/* ClusterSnapshot.RemoveNode (clustersnapshot.go:38, delta.go:150-186): the NodeInfo and
+ * its pods leave the snapshot; canonical order keeps the other nodes'
+ * relative order, so later positions shift down by one. */
+int or_remove_node(or_state* s, int32_t pos) {
+    if (pos < 0 || pos >= s->nodes.n) return CA_ENOTFOUND;
+    or_node row = s->nodes.a[pos];
+    memmove(&s->nodes.a[pos], &s->nodes.a[pos + 1], (size_t)(s->nodes.n - pos - 1) * sizeof(or_node));
+    s->nodes.n--;
+    for (int64_t i = 0; i < row.pods.n; i++) {
+        s->pods.a[row.pods.a[i]].node = -1;
+        scope_count(s, &s->pods.a[row.pods.a[i]].spec, -1);
+    }
+    for (int64_t i = 0; i < s->pods.n; i++) if (s->pods.a[i].node > pos) s->pods.a[i].node--;
+    if (s->depth > 0) {
+        journal(s, J_REMOVE_NODE, pos, -1, (int32_t)s->removed.n, NULL);
+        VEC_PUSH(s->removed, row);
+    } else {
+        free(row.pods.a);
+    }
     return CA_OK;
 }
 
@@ -221,16 +264,29 @@ int or_revert(or_state* s) {                      /* Revert (delta.go:434-443) *
         } else if (e.kind == J_ADD_POD) {
             or_node* nd = &s->nodes.a[e.node];
             node_apply(nd, &s->pods.a[e.pod].spec, -1);
+            scope_count(s, &s->pods.a[e.pod].spec, -1);
             memcpy(nd->ports, e.ports, sizeof nd->ports);
             nd->pods.n--;
             s->pods.a[e.pod].node = -1;
         } else if (e.kind == J_REMOVE_POD) {
             or_node* nd = &s->nodes.a[e.node];
             node_apply(nd, &s->pods.a[e.pod].spec, +1);
+            scope_count(s, &s->pods.a[e.pod].spec, +1);
             memcpy(nd->ports, e.ports, sizeof nd->ports);
             VEC_PUSH(nd->pods, nd->pods.a[e.slot]);
             nd->pods.a[e.slot] = e.pod;
             s->pods.a[e.pod].node = e.node;
+        } else if (e.kind == J_REMOVE_NODE) {
+            const int32_t pos = e.node;
+            or_node row = s->removed.a[--s->removed.n];
+            for (int64_t i = 0; i < s->pods.n; i++) if (s->pods.a[i].node >= pos) s->pods.a[i].node++;
+            VEC_PUSH(s->nodes, row);                      /* grow by one, then shift into place */
+            memmove(&s->nodes.a[pos + 1], &s->nodes.a[pos], (size_t)(s->nodes.n - 1 - pos) * sizeof(or_node));
+            s->nodes.a[pos] = row;
+            for (int64_t i = 0; i < row.pods.n; i++) {
+                s->pods.a[row.pods.a[i]].node = pos;
+                scope_count(s, &s->pods.a[row.pods.a[i]].spec, +1);
+            }
         }
     }
     s->depth--;
@@ -247,6 +303,7 @@ int or_commit(or_state* s) {                      /* Commit (delta.go:446-462) *
     s->depth--;
     if (s->depth == 0) {
         s->journal.n = 0;
+        free_removed(s);                          /* committed removals are permanent */
     } else {
         memmove(&s->journal.a[i], &s->journal.a[i + 1], (size_t)(s->journal.n - i - 1) * sizeof(or_jent));
         s->journal.n--;
@@ -452,6 +509,7 @@ int or_fits_any_node(or_state* s, const ca_pod_table* t, int32_t pod, const ca_m
                      int32_t* last_index, int32_t* out_node, int32_t* out_prefilter_failed,
                      uint64_t* evals) {
     if (pod < 0 || pod >= t->n_pods) return CA_EINVAL;
+    if ((t->pods[pod].flags & CA_POD_OUT_OF_SCOPE) || s->scope_blockers > 0) return CA_EUNSUPPORTED;
     pod_ctx c = table_ctx(t, pod);
     *out_node = fits_any(s, &c, match, last_index, out_prefilter_failed, evals);
     return CA_OK;
@@ -460,6 +518,7 @@ int or_fits_any_node(or_state* s, const ca_pod_table* t, int32_t pod, const ca_m
 int or_check_predicates(or_state* s, const ca_pod_table* t, int32_t pod, int32_t node,
                         ca_pred_result* out) {
     if (pod < 0 || pod >= t->n_pods) return CA_EINVAL;
+    if ((t->pods[pod].flags & CA_POD_OUT_OF_SCOPE) || s->scope_blockers > 0) return CA_EUNSUPPORTED;
     pod_ctx c = table_ctx(t, pod);
     check_pred(s, &c, node, out, NULL);
     return CA_OK;
@@ -523,12 +582,19 @@ int or_check_templates(or_state* s, const ca_pod_table* t, const int32_t* sample
                        const ca_template* templates, int32_t n_templates, ca_pred_result* out) {
     for (int32_t e = 0; e < n_samples; e++)
         if (samples[e] < 0 || samples[e] >= t->n_pods) return CA_EINVAL;
+    if (s->scope_blockers > 0) return CA_EUNSUPPORTED;
     for (int32_t g = 0; g < n_templates; g++) {
         or_fork(s);                                                           /* :454 */
         const int32_t node = add_template_copy(s, &templates[g]);             /* :457-466 */
         for (int32_t e = 0; e < n_samples; e++) {                             /* :468-480 */
             pod_ctx c = table_ctx(t, samples[e]);
-            check_pred(s, &c, node, &out[(size_t)g * n_samples + e], NULL);
+            ca_pred_result* r = &out[(size_t)g * n_samples + e];
+            if ((c.p->flags & CA_POD_OUT_OF_SCOPE) || (templates[g].node.flags & CA_NODE_ANTI_AFFINITY_PODS)) {
+                memset(r, 0, sizeof *r);
+                r->type = CA_PRED_UNSUPPORTED;                                /* casim.h scope */
+                continue;
+            }
+            check_pred(s, &c, node, r, NULL);
         }
         or_revert(s);                                                         /* :482 */
     }
@@ -540,8 +606,9 @@ static int estimate_one(or_state* s, const ca_pod_table* t, const int32_t* pods,
                         ca_estimate_result* res, int32_t* sched_pod, int32_t* sched_node) {
     memset(res, 0, sizeof *res);
     res->last_index_in = *last_index;
-    for (int32_t i = 0; i < P; i++) {
-        if (t->pods[pods[i]].flags & CA_POD_HOSTNAME_DEPENDENT) {
+    for (int32_t i = 0; i <= P; i++) {
+        if (i == P ? (tp->node.flags & CA_NODE_ANTI_AFFINITY_PODS) != 0
+                   : (t->pods[pods[i]].flags & (CA_POD_HOSTNAME_DEPENDENT | CA_POD_OUT_OF_SCOPE)) != 0) {
             res->status = CA_EUNSUPPORTED;
             res->last_index_out = *last_index;
             return CA_OK;
@@ -616,6 +683,7 @@ int or_estimate(or_state* s, const ca_pod_table* t, const int32_t* group_off,
                 const int32_t* pod_idx, const ca_template* templates, int32_t n_groups,
                 const ca_limiter* limiter, int32_t* last_index, ca_estimate_result* results,
                 int32_t* sched_pod, int32_t* sched_node) {
+    if (s->scope_blockers > 0 && n_groups > 0) return CA_EUNSUPPORTED;
     for (int32_t g = 0; g < n_groups; g++) {
         const int32_t off = group_off[g];
         const int64_t pods_before = s->pods.n, terms_before = s->terms.n, reqs_before = s->reqs.n,
@@ -626,6 +694,14 @@ int or_estimate(or_state* s, const ca_pod_table* t, const int32_t* group_off,
         s->pods.n = pods_before; s->terms.n = terms_before; s->reqs.n = reqs_before;
         s->pf_names.n = pf_before;
         if (rc != CA_OK) return rc;
+        if (results[g].status == CA_EUNSUPPORTED) {       /* prefix protocol (casim.h scope) */
+            for (int32_t h = g + 1; h < n_groups; h++) {
+                memset(&results[h], 0, sizeof results[h]);
+                results[h].last_index_in = results[h].last_index_out = *last_index;
+                results[h].status = CA_ENOTRUN;
+            }
+            break;
+        }
     }
     return CA_OK;
 }
@@ -724,6 +800,9 @@ int or_filter_out_schedulable(or_state* s, const ca_pod_table* t, const int32_t*
         if (i < 0 || i >= t->n_pods) return CA_EINVAL;
         if (t->pods[i].similar_class >= n_classes) return CA_EINVAL;
     }
+    if (s->scope_blockers > 0) return CA_EUNSUPPORTED;            /* casim.h scope: nothing runs */
+    for (int32_t k = 0; k < n; k++)
+        if (t->pods[order ? order[k] : k].flags & CA_POD_OUT_OF_SCOPE) return CA_EUNSUPPORTED;
     if (class_owner)
         for (int32_t c = 0; c < n_classes; c++) if (class_owner[c] + 1 > n_owners) n_owners = class_owner[c] + 1;
     uint8_t* marked = calloc((size_t)n_classes + 1, 1);       /* items[uid] holds this class */
@@ -791,6 +870,8 @@ int or_find_nodes_to_remove(or_state* s, const int32_t* candidates, int32_t n_ca
                             const int32_t* move_off, const int32_t* move_pods,
                             int32_t* hints, int32_t* last_index,
                             ca_removal_result* results, int32_t* out_dest) {
+    if (s->scope_blockers > 0 && n_candidates > 0) return CA_EUNSUPPORTED;
+    int32_t cut = 0;
     for (int32_t ci = 0; ci < n_candidates; ci++) {
         ca_removal_result* r = &results[ci];
         memset(r, 0, sizeof *r);
@@ -798,6 +879,18 @@ int or_find_nodes_to_remove(or_state* s, const int32_t* candidates, int32_t n_ca
         const int32_t node = candidates[ci];
         const int32_t mo = move_off[ci], mn = move_off[ci + 1] - move_off[ci];
         for (int32_t i = 0; i < mn; i++) out_dest[mo + i] = -1;
+        if (cut) {                                                        /* prefix protocol */
+            r->reason = CA_UNREMOVABLE_NOT_RUN;
+            continue;
+        }
+        if (node >= 0 && node < s->nodes.n && dest_mask[node] && !(cand_status && cand_status[ci] != 0)) {
+            for (int32_t i = 0; i < mn && !cut; i++)
+                if (s->pods.a[move_pods[mo + i]].spec.flags & CA_POD_OUT_OF_SCOPE) cut = 1;
+            if (cut) {
+                r->reason = CA_UNREMOVABLE_OUT_OF_SCOPE;                  /* casim.h scope */
+                continue;
+            }
+        }
         if (node < 0 || node >= s->nodes.n || !dest_mask[node]) {        /* :157-160 */
             r->reason = CA_UNREMOVABLE_UNEXPECTED_ERROR;
             continue;

@@ -33,6 +33,9 @@ int       or_add_nodes(or_state* s, const ca_node_spec* nodes, int32_t n, int32_
 int       or_add_pods(or_state* s, const ca_pod_table* t, const int32_t* pod_idx,
                       const int32_t* node_pos, int32_t n, int32_t* out_ids);
 int       or_remove_pod(or_state* s, int32_t pod_id);
+int       or_remove_node(or_state* s, int32_t pos);
+/* pods with CA_POD_REQUIRED_ANTI_AFFINITY in the snapshot (include/casim.h kernel scope) */
+int       or_scope_blockers(const or_state* s);
 int       or_fork(or_state* s);
 int       or_revert(or_state* s);
 int       or_commit(or_state* s);

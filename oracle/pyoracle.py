@@ -39,6 +39,8 @@ def load() -> C.CDLL:
         "or_add_nodes": ([vp, vp, i32, p(i32)], C.c_int),
         "or_add_pods": ([vp, vp, vp, vp, i32, vp], C.c_int),
         "or_remove_pod": ([vp, i32], C.c_int),
+        "or_remove_node": ([vp, i32], C.c_int),
+        "or_scope_blockers": ([vp], C.c_int),
         "or_fork": ([vp], C.c_int), "or_revert": ([vp], C.c_int), "or_commit": ([vp], C.c_int),
         "or_node_count": ([vp], C.c_int), "or_node_pods": ([vp, i32, vp, i32], C.c_int),
         "or_pod_node": ([vp, i32], C.c_int), "or_node_state": ([vp, i32, vp], C.c_int),
@@ -60,9 +62,15 @@ def load() -> C.CDLL:
     return lib
 
 
+class OracleError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        self.status = status
+        super().__init__(f"oracle {what}: status {status}")
+
+
 def _check(st: int, what: str) -> None:
     if st != abi.CA_OK:
-        raise RuntimeError(f"oracle {what}: status {st}")
+        raise OracleError(st, what)
 
 
 class OracleState:
@@ -101,6 +109,12 @@ class OracleState:
 
     def remove_pod(self, pod_id: int) -> None:
         _check(self.lib.or_remove_pod(self.h, pod_id), "remove_pod")
+
+    def remove_node(self, pos: int) -> None:
+        _check(self.lib.or_remove_node(self.h, pos), "remove_node")
+
+    def scope_blockers(self) -> int:
+        return self.lib.or_scope_blockers(self.h)
 
     def fork(self) -> None:
         _check(self.lib.or_fork(self.h), "fork")

@@ -25,11 +25,14 @@ def est_node(cpu, mem_mib, name, zone):
             "labels": {"kubernetes.io/hostname": name, "topology.kubernetes.io/zone": zone}}
 
 
-def est_pods(cpu, mem_mib, hostport, count):
+def est_pods(cpu, mem_mib, hostport, count, max_skew=0, key=""):
     """makePods (binpacking_estimator_test.go:35-81): one pod object repeated."""
     p = {"name": "estimatee", "ns": "universe", "cpu": cpu, "mem": mem_mib * MIB, "labels": {"app": "estimatee"}}
     if hostport:
         p["hostport"] = hostport
+    if max_skew > 0:       # :64-78: one DoNotSchedule constraint selecting app=estimatee
+        p["topology_spread"] = [{"maxSkew": max_skew, "topologyKey": key, "whenUnsatisfiable": "DoNotSchedule",
+                                 "labelSelector": {"matchLabels": {"app": "estimatee"}}}]
     return {"repeat": count, "pod": p}
 
 
@@ -63,11 +66,21 @@ for name, line, cpu, mem, pods, max_nodes, en, ep in [
         "pods": pods, "max_nodes": max_nodes,
         "expect": {"node_count": en, "pod_count": ep},
     })
-# the two topology-spread rows (:143-158) need PodTopologySpread: out of kernel scope
-for name, line in [("hostname topology spreading with maxSkew=2 forces 2 pods/node", "143-150"),
-                   ("zonal topology spreading with maxSkew=2 only allows 2 pods to schedule", "151-158")]:
-    cases.append({"id": f"estimate/{name}", "source": f"{EST}:{line}", "kind": "unsupported",
-                  "reason": "PodTopologySpread DoNotSchedule constraint (SURVEY §8a A12): routed to the Go path"})
+# the two topology-spread rows (:143-158) need PodTopologySpread: out of kernel scope.  The
+# inputs are transcribed in full with the reference's expectation; the kernels must REJECT
+# them (CA_EUNSUPPORTED -> UnsupportedByKernels, the Go path runs them), never count them.
+for name, line, key, en, ep in [
+        ("hostname topology spreading with maxSkew=2 forces 2 pods/node", "143-150", "kubernetes.io/hostname", 4, 8),
+        ("zonal topology spreading with maxSkew=2 only allows 2 pods to schedule", "151-158",
+         "topology.kubernetes.io/zone", 1, 2)]:
+    cases.append({
+        "id": f"estimate/{name}", "source": f"{EST}:{line},164-186", "kind": "estimate",
+        "nodes": [est_node(100, 100, "oldnode", "zone-jupiter")],
+        "template": est_node(1000, 5000, "template", "zone-mars"),
+        "pods": est_pods(20, 100, 0, 8, 2, key), "max_nodes": 0,
+        "expect": {"unsupported": True, "reference": {"node_count": en, "pod_count": ep},
+                   "reason": "PodTopologySpread DoNotSchedule constraint (SURVEY §8a A12): routed to the Go path"},
+    })
 
 # ---- predicate checker: TestCheckPredicate ------------------------------------
 n1000 = test_node("n1000", 1000, 2000000)

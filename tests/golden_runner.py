@@ -8,7 +8,7 @@ import os
 from autoscaler_amd import k8s
 from autoscaler_amd.clustersnapshot import ClusterSnapshot, NodeInfo
 from autoscaler_amd.drain import ListerRegistry, NodeDeleteOptions
-from autoscaler_amd.estimator import BinpackingNodeEstimator, ThresholdBasedEstimationLimiter
+from autoscaler_amd.estimator import BinpackingNodeEstimator, ThresholdBasedEstimationLimiter, UnsupportedByKernels
 from autoscaler_amd.podlistprocessor import NewFilterOutSchedulablePodListProcessor
 from autoscaler_amd.predicatechecker import SchedulerBasedPredicateChecker
 from autoscaler_amd.simulator import HintingSimulator, RemovalSimulator
@@ -48,6 +48,9 @@ def build_pod(d: dict) -> k8s.Pod:
         p.owner_refs = [k8s.OwnerReference(kind, name, name)]
     if d.get("node"):
         p.node_name = d["node"]
+    for c in d.get("topology_spread", []):
+        p.topology_spread.append(k8s.TopologySpreadConstraint(c["maxSkew"], c["topologyKey"], c["whenUnsatisfiable"],
+                                                              dict(c["labelSelector"]["matchLabels"])))
     if "priority" in d:
         p.priority = d["priority"]
     return p
@@ -76,8 +79,14 @@ def run_case(case: dict, make_backend):
         tmpl = build_node(case["template"])
         pods = expand_pods(case["pods"])
         est = BinpackingNodeEstimator(checker, snap, ThresholdBasedEstimationLimiter(case["max_nodes"]))
-        count, scheduled = est.Estimate(pods, NodeInfo(tmpl, []), None)
         e = case["expect"]
+        if e.get("unsupported"):
+            try:
+                est.Estimate(pods, NodeInfo(tmpl, []), None)
+            except UnsupportedByKernels:
+                return errs
+            return ["out-of-scope input was simulated instead of rejected (UnsupportedByKernels)"]
+        count, scheduled = est.Estimate(pods, NodeInfo(tmpl, []), None)
         if count != e["node_count"]:
             errs.append(f"node count {count} != {e['node_count']}")
         if len(scheduled) != e["pod_count"]:

@@ -21,7 +21,7 @@ from estgen import _encode_estimate, _estimate_inputs
 
 pytestmark = pytest.mark.gpu
 
-CASES = [c for c in load_cases() if c["kind"] != "unsupported"]
+CASES = load_cases()
 
 
 @pytest.fixture(scope="module")

@@ -180,6 +180,8 @@ class Node:
     taints: list = field(default_factory=list)
     allocatable: dict = field(default_factory=dict)    # resource name -> Quantity
     unschedulable: bool = False
+    annotations: dict = field(default_factory=dict)
+    ready: bool = True                                 # NodeReady condition (kube_util.GetReadinessState)
 
 
 # ---------------------------------------------------------------------------

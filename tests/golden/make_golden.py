@@ -226,6 +226,87 @@ for name, nn, ns, npend in [("nothing", 1, 30, 1000), ("small", 10, 300, 1000), 
         "expect": {"still_pending": npend},
     })
 
+# ---- scale-up: TestWillConsider*Pool* (orchestrator_test.go:304-404) ---------------------
+# Options the expander receives (ComputeExpansionOption + Estimate per node group, limiter
+# MaxNodesPerScaleUp = 0 in defaultOptions :57-63); node group templates are the groups'
+# nodes (TemplateNodeInfoProvider over BuildTestNode + AddGpusToNode, no DaemonSet pods).
+ORC = "CA/core/scaleup/orchestrator/orchestrator_test.go"
+
+
+def orc_node(name, cpu, mem_mib, gpu, group):
+    return {"name": name, "cpu": cpu, "mem": mem_mib * MIB, "pods": 100, "gpu": gpu, "group": group}
+
+
+def orc_pod(name, cpu, mem_mib, gpu, node, tolerates):
+    """buildTestPod (orchestrator_test.go:650-662): BuildTestPod + RequestGpuForPod + TolerateGpuForPod."""
+    return {"name": name, "cpu": cpu, "mem": mem_mib * MIB, "gpu": gpu, "node": node, "tolerates_gpu": tolerates}
+
+
+for name, line, nodes_, pods_, extra, options in [
+    ("WillConsiderGpuAndStandardPoolForPodWhichDoesNotRequireGpu", "304-334",
+     [orc_node("gpu-node-1", 2000, 1000, 1, "gpu-pool"), orc_node("std-node-1", 2000, 1000, 0, "std-pool")],
+     [orc_pod("gpu-pod-1", 2000, 1000, 1, "gpu-node-1", True), orc_pod("std-pod-1", 2000, 1000, 0, "std-node-1", False)],
+     [orc_pod("extra-std-pod", 2000, 1000, 0, "", True)], {"std-pool": 1, "gpu-pool": 1}),
+    ("WillConsiderOnlyGpuPoolForPodWhichDoesRequiresGpu", "336-365",
+     [orc_node("gpu-node-1", 2000, 1000, 1, "gpu-pool"), orc_node("std-node-1", 2000, 1000, 0, "std-pool")],
+     [orc_pod("gpu-pod-1", 2000, 1000, 1, "gpu-node-1", True), orc_pod("std-pod-1", 2000, 1000, 0, "std-node-1", False)],
+     [orc_pod("extra-gpu-pod", 2000, 1000, 1, "", True)], {"gpu-pool": 1}),
+    ("WillConsiderAllPoolsWhichFitTwoPodsRequiringGpus", "367-404",
+     [orc_node("gpu-1-node-1", 2000, 1000, 1, "gpu-1-pool"), orc_node("gpu-2-node-1", 2000, 1000, 2, "gpu-2-pool"),
+      orc_node("gpu-4-node-1", 2000, 1000, 4, "gpu-4-pool"), orc_node("std-node-1", 2000, 1000, 0, "std-pool")],
+     [orc_pod("gpu-pod-1", 2000, 1000, 1, "gpu-1-node-1", True), orc_pod("gpu-pod-2", 2000, 1000, 2, "gpu-2-node-1", True),
+      orc_pod("gpu-pod-3", 2000, 1000, 4, "gpu-4-node-1", True), orc_pod("std-pod-1", 2000, 1000, 0, "std-node-1", False)],
+     [orc_pod(f"extra-gpu-pod-{i}", 1, 1, 1, "", True) for i in (1, 2, 3)],
+     {"gpu-1-pool": 3, "gpu-2-pool": 2, "gpu-4-pool": 1}),
+]:
+    cases.append({"id": f"expansion_options/{name}", "source": f"{ORC}:{line},478-576", "kind": "expansion_options",
+                  "nodes": nodes_, "pods": pods_, "extra_pods": extra, "max_nodes": 0,
+                  "expect": {"options": options}})
+
+# ---- legacy scale-down: TestFindUnneededNodes (legacy_test.go:58-216) ------------------
+# Five UpdateUnneededNodes calls over one ScaleDown; ng1 = {min 1, max 10, target 2};
+# options: ScaleDownUtilizationThreshold 0.35, UnremovableNodeRecheckTimeout 5 min, every
+# other option zero (NewScaleTestAutoscalingContext), NodeDeleteOptions zero; the rs lister
+# holds ReplicaSet default/rs with 5 replicas (generateReplicaSets :1265-1279).
+LEG = "CA/core/scaledown/legacy/legacy_test.go"
+T0 = 1_700_000_000
+leg_nodes = {
+    "n1": test_node("n1", 1000, 10), "n2": test_node("n2", 1000, 10), "n3": test_node("n3", 1000, 10),
+    "n4": test_node("n4", 10000, 10),
+    "n5": test_node("n5", 1000, 10, annotations={"cluster-autoscaler.kubernetes.io/scale-down-disabled": "true"}),
+    "n7": test_node("n7", 0, 10),
+    "n8": test_node("n8", 1000, 10, taints=[["ToBeDeletedByClusterAutoscaler", str(T0 - 301), ""]]),
+    "n9": test_node("n9", 1000, 10, taints=[["ToBeDeletedByClusterAutoscaler", str(T0 - 60), ""]]),
+}
+rs = ["ReplicaSet", "rs"]
+leg_pods = {
+    "p1": test_pod("p1", 100, 0, node="n1"), "p2": test_pod("p2", 300, 0, node="n2", owner=rs),
+    "p3": test_pod("p3", 400, 0, node="n3", owner=rs), "p4": test_pod("p4", 2000, 0, node="n4", owner=rs),
+    "p5": test_pod("p5", 100, 0, node="n5", owner=rs), "p6": test_pod("p6", 500, 0, node="n7", owner=rs),
+}
+all8 = ["n1", "n2", "n3", "n4", "n5", "n7", "n8", "n9"]
+cases.append({
+    "id": "update_unneeded_nodes/TestFindUnneededNodes", "source": f"{LEG}:58-216", "kind": "update_unneeded_nodes",
+    "nodes": leg_nodes, "pods": leg_pods, "groups": {"ng1": [1, 10, 2, all8]}, "now": T0,
+    "options": {"threshold": 0.35, "recheck_timeout": 300.0, "non_empty_candidates": 0, "pool_ratio": 0.0,
+                "pool_min": 0},
+    "listers": {"ReplicaSet": [["default", "rs", 5]]},
+    "steps": [
+        {"line": "150-166", "nodes": all8, "pods": ["p1", "p2", "p3", "p4", "p5", "p6"], "candidates": all8,
+         "expect": {"unneeded": ["n2", "n7", "n8"], "util_found": ["n1", "n2", "n3", "n4", "n7", "n8"],
+                    "util_missing": ["n5", "n6", "n9"]}},
+        {"line": "168-184", "reset_unremovable": True, "preset_unneeded": ["n1", "n2", "n3", "n4"],
+         "nodes": ["n1", "n2", "n3", "n4"], "pods": ["p1", "p2", "p3", "p4"], "candidates": ["n1", "n2", "n3", "n4"],
+         "expect": {"unneeded": ["n2"], "util_found": ["n1", "n2", "n3", "n4"], "util_missing": ["n5", "n6"]}},
+        {"line": "186-192", "reset_unremovable": True, "nodes": ["n1", "n2", "n3", "n4"],
+         "pods": ["p1", "p2", "p3", "p4"], "candidates": ["n1", "n3", "n4"], "expect": {"unneeded": []}},
+        {"line": "194-202", "nodes": ["n1"], "pods": [], "candidates": ["n1"],
+         "expect": {"unneeded": [], "unremovable_count": 1}},
+        {"line": "204-215", "nodes": ["n1"], "pods": [], "candidates": ["n1"], "time_offset": 301.0,
+         "expect": {"unneeded": ["n1"], "unremovable_count": 0}},
+    ],
+})
+
 if __name__ == "__main__":
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_cases.json")
     with open(out, "w") as f:

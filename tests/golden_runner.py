@@ -27,6 +27,7 @@ def load_cases() -> list:
 def build_node(d: dict) -> k8s.Node:
     n = k8s.build_test_node(d["name"], d["cpu"], d["mem"], d.get("pods", 100))
     n.labels.update(d.get("labels", {}))
+    n.annotations.update(d.get("annotations", {}))
     n.taints = [k8s.Taint(*t) for t in d.get("taints", [])]
     if d.get("gpu"):
         k8s.add_gpus_to_node(n, d["gpu"])
@@ -43,6 +44,10 @@ def build_pod(d: dict) -> k8s.Pod:
     p.annotations.update(d.get("annotations", {}))
     if d.get("hostport"):
         p.containers[0].ports.append(k8s.ContainerPort(host_port=d["hostport"]))
+    if d.get("gpu"):
+        k8s.request_gpu_for_pod(p, d["gpu"])
+    if d.get("tolerates_gpu"):
+        k8s.tolerate_gpu_for_pod(p)
     if d.get("owner"):
         kind, name = d["owner"]
         p.owner_refs = [k8s.OwnerReference(kind, name, name)]
@@ -66,6 +71,21 @@ def expand_pods(spec) -> list:
         one = build_pod(spec["pod"])
         return [one] * spec["repeat"]
     return [build_pod(d) for d in spec]
+
+
+def _calculate_all(backend):
+    """utilization.CalculateAll on the snapshot's backend (the checker's restatement on CPU)."""
+    from autoscaler_amd import utilization
+    if getattr(backend, "backend_name", "") != "oracle":
+        return utilization.CalculateAll
+    import pyoracle
+
+    def calc(node_infos, skip_ds, skip_mirror, gpu_configs, now):
+        nodes, off, pods = utilization.build_table(node_infos, gpu_configs)
+        out = pyoracle.node_utilization(nodes, off, pods, skip_ds, skip_mirror, round(now * 1e9))
+        return [utilization.info_from_row(out[i], ni.node.name, gc)
+                for i, (ni, gc) in enumerate(zip(node_infos, gpu_configs))]
+    return calc
 
 
 def run_case(case: dict, make_backend):
@@ -172,6 +192,65 @@ def run_case(case: dict, make_backend):
         want = sorted([p["name"] for p in case["pods"]] + e["scheduled"])
         if got != want:
             errs.append(f"scheduled {got} != {want}")
+    elif kind == "expansion_options":
+        from autoscaler_amd.scaleup import BuildPodGroups, ComputeExpansionOptions
+        nodes = [build_node(n) for n in case["nodes"]]
+        snap.AddNodes(nodes)
+        for pd in case["pods"]:
+            snap.AddPod(build_pod(pd), pd["node"])
+        groups = []
+        for nd, d in zip(nodes, case["nodes"]):          # TemplateNodeInfo: the group's node, sanitized
+            t = build_node(dict(d, name=f"template-node-for-{d['group']}"))
+            groups.append((d["group"], NodeInfo(t, [])))
+        pgs = BuildPodGroups([build_pod(p) for p in case["extra_pods"]])
+        options, _ = ComputeExpansionOptions(snap, checker, pgs, groups,
+                                             ThresholdBasedEstimationLimiter(case["max_nodes"]))
+        got = {o.node_group: o.node_count for o in options if o.pods and o.node_count > 0}
+        if got != case["expect"]["options"]:
+            errs.append(f"options {got} != {case['expect']['options']}")
+    elif kind == "update_unneeded_nodes":
+        from autoscaler_amd.legacy import NodeGroup, ScaleDown, ScaleDownOptions
+        nodes = {n: build_node(d) for n, d in case["nodes"].items()}
+        groups = {}
+        for gid, (mn, mx, tgt, members) in case["groups"].items():
+            for n in members:
+                groups[n] = NodeGroup(gid, mn, mx, tgt)
+        o = case["options"]
+        opts = ScaleDownOptions(scale_down_utilization_threshold=o["threshold"],
+                                unremovable_node_recheck_timeout=o["recheck_timeout"],
+                                scale_down_non_empty_candidates_count=o["non_empty_candidates"],
+                                scale_down_candidates_pool_ratio=o["pool_ratio"],
+                                scale_down_candidates_pool_min_count=o["pool_min"])
+        listers = ListerRegistry({k: {(ns, n): r for ns, n, r in v} for k, v in case["listers"].items()})
+        rs = RemovalSimulator(listers, snap, checker, None, NodeDeleteOptions(False, False, 0), False)
+        sd = ScaleDown(snap, rs, groups, opts, calculate_all=_calculate_all(snap.backend))
+        from autoscaler_amd.legacy import UnremovableNodes
+        from autoscaler_amd.simulator import NodeToBeRemoved
+        for step in case["steps"]:
+            tag = f"step {step['line']}"
+            if step.get("reset_unremovable"):
+                sd.unremovable_nodes = UnremovableNodes()
+            if "preset_unneeded" in step:
+                sd.unneeded_nodes.Update([NodeToBeRemoved(nodes[n]) for n in step["preset_unneeded"]], case["now"])
+            snap.Clear()                                  # InitializeClusterSnapshotOrDie
+            snap.AddNodes([nodes[n] for n in step["nodes"]])
+            for pn in step["pods"]:
+                pd = case["pods"][pn]
+                snap.AddPod(build_pod(pd), pd["node"])
+            alln = [nodes[n] for n in step["nodes"]]
+            sd.UpdateUnneededNodes(alln, [nodes[n] for n in step["candidates"]],
+                                   case["now"] + step.get("time_offset", 0.0))
+            e = step["expect"]
+            if sorted(sd.unneeded_nodes.AsList()) != sorted(e["unneeded"]):
+                errs.append(f"{tag}: unneeded {sorted(sd.unneeded_nodes.AsList())} != {e['unneeded']}")
+            for n in e.get("util_found", []):
+                if n not in sd.node_utilization_map:
+                    errs.append(f"{tag}: utilization of {n} missing")
+            for n in e.get("util_missing", []):
+                if n in sd.node_utilization_map:
+                    errs.append(f"{tag}: utilization of {n} present")
+            if "unremovable_count" in e and len(sd.unremovable_nodes.AsList()) != e["unremovable_count"]:
+                errs.append(f"{tag}: {len(sd.unremovable_nodes.AsList())} unremovable != {e['unremovable_count']}")
     elif kind == "filter_out_schedulable_bench":
         nodes = series(case["nodes"], build_node)
         snap.AddNodes(nodes)

@@ -13,6 +13,7 @@ from __future__ import annotations
 import numpy as np
 
 from .clustersnapshot import ClusterSnapshot
+from .gosort import sort_slice_desc
 from .k8s import Pod
 from .predicatechecker import SchedulerBasedPredicateChecker, unsupported
 from .simulator import HintingSimulator, Hints, Status
@@ -66,9 +67,9 @@ class FilterOutSchedulablePodListProcessor:
 
     def filterOutSchedulableByPacking(self, unschedulable_candidates: list,  # noqa: N802
                                       snapshot: ClusterSnapshot) -> list:
-        # :97-99 — a stable sort here (Go's sort.Slice is not stable; equal priorities keep
-        # the caller's order)
-        unschedulable_candidates.sort(key=lambda p: -PodPriority(p))
+        # :97-99 sort.Slice by priority, descending: Go 1.19's pdqsort, ties included (gosort.py)
+        perm = sort_slice_desc([PodPriority(p) for p in unschedulable_candidates])
+        unschedulable_candidates[:] = [unschedulable_candidates[i] for i in perm]
         statuses, overflow = TrySchedulePodsAnywhere(self.schedulingSimulator, snapshot, unschedulable_candidates)
         scheduled = {id(s.pod) for s in statuses}
         still = [p for p in unschedulable_candidates if id(p) not in scheduled]      # :111-116

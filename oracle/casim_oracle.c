@@ -63,6 +63,7 @@ struct or_state {
     int32_t depth;
     int32_t next_new_name;            /* fresh name ids for template copies        */
     int64_t scope_blockers;           /* pods with CA_POD_REQUIRED_ANTI_AFFINITY   */
+    int32_t sort_mode;                /* Estimate's sort.Slice: OR_SORT_STABLE / OR_SORT_GO_PDQ */
 };
 
 static int64_t wrap_sub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
@@ -111,6 +112,15 @@ static void scope_count(or_state* s, const ca_pod_spec* p, int sign) {
 }
 
 int or_scope_blockers(const or_state* s) { return (int)s->scope_blockers; }
+
+/* Estimate's sort of the pods by score (binpacking_estimator.go:74): OR_SORT_GO_PDQ is the
+ * reference's Go 1.19 sort.Slice (gosort.c), OR_SORT_STABLE breaks score ties by list
+ * position (the order the kernels use). */
+int or_set_sort_mode(or_state* s, int32_t mode) {
+    if (mode != OR_SORT_STABLE && mode != OR_SORT_GO_PDQ) return CA_EINVAL;
+    s->sort_mode = mode;
+    return CA_OK;
+}
 
 int or_node_count(const or_state* s) { return (int)s->nodes.n; }
 
@@ -622,7 +632,17 @@ static int estimate_one(or_state* s, const ca_pod_table* t, const int32_t* pods,
         order[i].score = pod_score(&t->pods[pods[i]], &tp->node);
         order[i].pos = i;
     }
-    merge_sort_desc(order, tmp, P);
+    if (s->sort_mode == OR_SORT_GO_PDQ) {                 /* sort.Slice (pdqsort_func) */
+        double* key = malloc(sizeof(double) * (size_t)(P > 0 ? P : 1));
+        int32_t* perm = malloc(sizeof(int32_t) * (size_t)(P > 0 ? P : 1));
+        for (int32_t i = 0; i < P; i++) key[i] = order[i].score;
+        go_sort_slice_desc(key, P, perm);
+        for (int32_t i = 0; i < P; i++) { order[i].score = key[perm[i]]; order[i].pos = perm[i]; }
+        free(key);
+        free(perm);
+    } else {
+        merge_sort_desc(order, tmp, P);
+    }
     free(tmp);
 
     or_fork(s);                                          /* :79 */

@@ -36,6 +36,15 @@ int       or_remove_pod(or_state* s, int32_t pod_id);
 int       or_remove_node(or_state* s, int32_t pos);
 /* pods with CA_POD_REQUIRED_ANTI_AFFINITY in the snapshot (include/casim.h kernel scope) */
 int       or_scope_blockers(const or_state* s);
+/* Estimate's score sort: stable (ties by list position, the device order) or Go 1.19's
+ * sort.Slice pdqsort (the reference; gosort.c) */
+#define OR_SORT_STABLE 0
+#define OR_SORT_GO_PDQ 1
+int       or_set_sort_mode(or_state* s, int32_t mode);
+/* gosort.c: sort.Slice(x, less) with less(i, j) = key[i] > key[j]; perm[k] = input index
+ * at sorted position k.  go_sort_stats: breakPatterns and heapSort calls so far. */
+void      go_sort_slice_desc(const double* key, int32_t n, int32_t* perm);
+void      go_sort_stats(int64_t* out2);
 int       or_fork(or_state* s);
 int       or_revert(or_state* s);
 int       or_commit(or_state* s);

@@ -41,6 +41,9 @@ def load() -> C.CDLL:
         "or_remove_pod": ([vp, i32], C.c_int),
         "or_remove_node": ([vp, i32], C.c_int),
         "or_scope_blockers": ([vp], C.c_int),
+        "or_set_sort_mode": ([vp, i32], C.c_int),
+        "go_sort_slice_desc": ([vp, i32, vp], None),
+        "go_sort_stats": ([vp], None),
         "or_fork": ([vp], C.c_int), "or_revert": ([vp], C.c_int), "or_commit": ([vp], C.c_int),
         "or_node_count": ([vp], C.c_int), "or_node_pods": ([vp, i32, vp, i32], C.c_int),
         "or_pod_node": ([vp, i32], C.c_int), "or_node_state": ([vp, i32, vp], C.c_int),
@@ -115,6 +118,10 @@ class OracleState:
 
     def scope_blockers(self) -> int:
         return self.lib.or_scope_blockers(self.h)
+
+    def set_sort_mode(self, mode: str) -> None:
+        """Estimate's score sort: "stable" (the device order) or "go" (Go 1.19 sort.Slice)."""
+        _check(self.lib.or_set_sort_mode(self.h, {"stable": 0, "go": 1}[mode]), "set_sort_mode")
 
     def fork(self) -> None:
         _check(self.lib.or_fork(self.h), "fork")
@@ -221,6 +228,20 @@ class OracleState:
                                                 ptr(moves), ptr(hints), C.byref(li), ptr(res), ptr(dest)),
                "find_nodes_to_remove")
         return RemovalOutput(res, dest[: len(moves)], hints, li.value)
+
+
+def go_sort_desc(keys) -> np.ndarray:
+    """Go 1.19 sort.Slice(x, key[i] > key[j]) (oracle/gosort.c): the permutation."""
+    k = np.ascontiguousarray(keys, dtype=np.float64)
+    perm = np.zeros(max(len(k), 1), np.int32)
+    load().go_sort_slice_desc(ptr(k), len(k), ptr(perm))
+    return perm[: len(k)]
+
+
+def go_sort_stats() -> tuple:
+    out = np.zeros(2, np.int64)
+    load().go_sort_stats(ptr(out))
+    return int(out[0]), int(out[1])
 
 
 def node_utilization(nodes: np.ndarray, pod_off: np.ndarray, pods: np.ndarray, skip_daemonset_pods: bool,

@@ -550,6 +550,18 @@ __device__ inline void lds_barrier() {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
+// The chain's barrier: LDS-only while the rows are in LDS; a workgroup fence over every
+// address space when the rows live in an HBM slab (GM), so row stores of one wave are
+// visible to the others (all waves of the workgroup share the CU's L1).
+template <bool GM> __device__ inline void cbar() {
+    if (GM) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else {
+        lds_barrier();
+    }
+}
 constexpr int CW = 4;
 constexpr int CT = 64 * CW;
 constexpr int RED_N = 5;
@@ -566,11 +578,11 @@ template <int OP> __device__ inline int64_t wred(int64_t v) {
 template <int OP> __device__ inline int64_t wcomb(int64_t a, int64_t b) {
     return OP == R_SUM ? a + b : OP == R_MAX ? (a > b ? a : b) : (a < b ? a : b);
 }
-template <int OA, int OB, int OC>
+template <int OA, int OB, int OC, bool GM = false>
 __device__ inline void blk_red3(ChainRed& cr, int& par, int wv, int lane, int64_t& a, int64_t& b, int64_t& c) {
     a = wred<OA>(a); b = wred<OB>(b); c = wred<OC>(c);
     if (lane == 0) { cr.v[par][wv][0] = a; cr.v[par][wv][1] = b; cr.v[par][wv][2] = c; }
-    lds_barrier();
+    cbar<GM>();
     a = cr.v[par][0][0]; b = cr.v[par][0][1]; c = cr.v[par][0][2];
     for (int w = 1; w < CW; w++) {
         a = wcomb<OA>(a, cr.v[par][w][0]); b = wcomb<OB>(b, cr.v[par][w][1]); c = wcomb<OC>(c, cr.v[par][w][2]);
@@ -585,11 +597,12 @@ __device__ inline int64_t wred_rt(int op, int64_t v) {
 __device__ inline int64_t wcomb_rt(int op, int64_t a, int64_t b) {
     return op == R_SUM ? a + b : op == R_MAX ? (a > b ? a : b) : (a < b ? a : b);
 }
+template <bool GM = false>
 __device__ inline void blk_red5(ChainRed& cr, int& par, int wv, int lane, int64_t (&x)[RED_N], const int (&op)[RED_N]) {
     for (int i = 0; i < RED_N; i++) x[i] = wred_rt(op[i], x[i]);
     if (lane == 0)
         for (int i = 0; i < RED_N; i++) cr.v[par][wv][i] = x[i];
-    lds_barrier();
+    cbar<GM>();
     for (int i = 0; i < RED_N; i++) {
         int64_t a = cr.v[par][0][i];
         for (int w = 1; w < CW; w++) a = wcomb_rt(op[i], a, cr.v[par][w][i]);
@@ -598,10 +611,11 @@ __device__ inline void blk_red5(ChainRed& cr, int& par, int wv, int lane, int64_
     par ^= 1;
 }
 // Cross-wave step only: x[] already reduced within each wave (wave-uniform).
+template <bool GM = false>
 __device__ inline void blk_xchg5(ChainRed& cr, int& par, int wv, int lane, int64_t (&x)[RED_N], const int (&op)[RED_N]) {
     if (lane == 0)
         for (int i = 0; i < RED_N; i++) cr.v[par][wv][i] = x[i];
-    lds_barrier();
+    cbar<GM>();
     for (int i = 0; i < RED_N; i++) {
         int64_t a = cr.v[par][0][i];
         for (int w = 1; w < CW; w++) a = wcomb_rt(op[i], a, cr.v[par][w][i]);
@@ -642,10 +656,11 @@ __device__ inline uint64_t open_evals(int32_t n_open, int32_t ct, int32_t placed
 
 // Ordered compaction step over the workgroup: thread t contributes `keep` for index
 // base + t; returns the thread's slot (exclusive prefix over the workgroup) and the total.
+template <bool GM = false>
 __device__ inline int32_t blk_compact(ChainRed& cr, int& par, int wv, bool keep, int32_t& total) {
     const uint64_t bm = __ballot(keep);
     if ((threadIdx.x & 63) == 0) cr.cnt[par][wv] = __builtin_popcountll(bm);
-    lds_barrier();
+    cbar<GM>();
     int32_t before = 0;
     total = 0;
     for (int w = 0; w < CW; w++) {
@@ -917,6 +932,7 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
 // placement's scan ends at unwrapped position (rev-1)*k + rank, so a batch costs
 // (r_last-1)*k + rank(last)+1 filter calls.  assign[pos] receives the new-node index of
 // every placed stream position (-1 = not scheduled).
+template <bool GROWS>
 __global__ void __launch_bounds__(CT) k_ffd_chain(
     const GroupMeta* __restrict__ groups, const StreamPod* __restrict__ stream, const uint64_t* __restrict__ heads,
     const ca_template* __restrict__ tmpls, const ca_pod_spec* __restrict__ specs, const PodHot* __restrict__ ph,
@@ -924,9 +940,14 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     int32_t n_base, int32_t max_nodes, int32_t kcap, int32_t use_ports, int32_t use_scalar, int32_t batch_runs,
     int32_t* __restrict__ sched_pod, int32_t* __restrict__ sched_node, Seg* __restrict__ segs,
     int32_t* __restrict__ tickets, int32_t* __restrict__ qctl, int32_t nsub, int2* __restrict__ prog, int32_t pch,
-    ChainOut* __restrict__ outs, const int32_t* __restrict__ gmap) {
+    ChainOut* __restrict__ outs, const int32_t* __restrict__ gmap, unsigned char* __restrict__ gslab,
+    const int64_t* __restrict__ slab_off, const int32_t* __restrict__ gkcap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int g = GSEL(blockIdx.x);
+    // GROWS: the group's rows live in its own HBM slab (kcap = the group's pod count, for an
+    // unlimited estimate too large for LDS); else in LDS with the batch-wide kcap
+    if (GROWS) kcap = gkcap[g];
+    unsigned char* const row_base = GROWS ? gslab + slab_off[g] : smem_raw;
     if (!need[g]) return;
     const uint64_t t_begin = wall_clock64();      // diagnostics: ca_estimate_plan_group_ticks
     __builtin_amdgcn_s_setprio(3);                // the chain is the critical path: win issue over k_publish
@@ -956,7 +977,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
         return;
     }
     const int nb_cap = (kcap + 63) >> 6;
-    NodeRec* R = reinterpret_cast<NodeRec*>(smem_raw);
+    NodeRec* R = reinterpret_cast<NodeRec*>(row_base);
     NodeRec* SUM = R + kcap;
     int32_t* CAPA = reinterpret_cast<int32_t*>(SUM + nb_cap);                   // [kcap]
     int32_t* ALIVE = CAPA + kcap;                                               // [kcap]
@@ -1116,7 +1137,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                             const NodeRec rl_ = R[last_node];
                             const int32_t c = rem <= (1 << 20) ? rec_copies_run(rl_, dv, zero, rem, pcpu, pmem, peph)
                                                                : rec_copies(rl_, pcpu, pmem, peph, zero, rem);
-                            lds_barrier();    // every wave has read the row before it changes
+                            cbar<GROWS>();    // every wave has read the row before it changes
                             if (c > 0) { one = last_node; n_one = c; nalive = 1; }
                             PROF_ADD(10, t_ex);
                         } else {
@@ -1176,7 +1197,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                             x[0] = fast ? (int64_t)__ockl_wfred_add_i32(s32) : wave_sum64(s64);
                             x[1] = na_w; x[2] = a1_w; x[3] = wave_min32(cm); x[4] = lt_w;
                             constexpr int OPS[RED_N] = {R_SUM, R_SUM, R_MAX, R_MIN, R_SUM};
-                            blk_xchg5(cred, par, wv, lane, x, OPS);     // + CAPA visible
+                            blk_xchg5<GROWS>(cred, par, wv, lane, x, OPS);     // + CAPA visible
                             S = x[0];
                             nalive = (int32_t)x[1];
                             lv_cmin = x[3];
@@ -1247,7 +1268,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                                             t -= pc;
                                         }
                                     }
-                                    lds_barrier();
+                                    cbar<GROWS>();
                                     last = cred.pick;
                                     got = n;
                                     PROF_INC(6);
@@ -1271,7 +1292,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                                 }
                                 int64_t y[RED_N] = {0, cnt_w, 0, wave_min32(cm2), lt2};   // -, count, -, min, count < j0
                                 constexpr int OPS2[RED_N] = {R_SUM, R_SUM, R_SUM, R_MIN, R_SUM};
-                                blk_xchg5(cred, par, wv, lane, y, OPS2);
+                                blk_xchg5<GROWS>(cred, par, wv, lane, y, OPS2);
                                 lv_buf = par ^ 1;
                                 lv_na = (int32_t)y[1];
                                 lv_cmin = y[3];
@@ -1289,11 +1310,11 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                                 const int32_t c = rr < k ? CAPA[j] : 0;
                                 const bool keep = c >= 1;
                                 int32_t tot;
-                                const int32_t slot = blk_compact(cred, par, wv, keep, tot);
+                                const int32_t slot = blk_compact<GROWS>(cred, par, wv, keep, tot);
                                 if (keep) { ALIVE[na + slot] = j; cmin = min(cmin, (int64_t)c); }
                                 na += tot;
                             }
-                            blk_red3<R_MIN, R_SUM, R_SUM>(cred, par, wv, lane, cmin, z0, z1);   // + ALIVE visible
+                            blk_red3<R_MIN, R_SUM, R_SUM, GROWS>(cred, par, wv, lane, cmin, z0, z1);   // + ALIVE visible
                             // Revolutions r..cmin serve the same alive list (no row runs out
                             // before cmin), so the list is compacted once per distinct copy
                             // level, and the placements of those revolutions are the list
@@ -1331,12 +1352,12 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                                     const int32_t c = i < na ? CAPA[j] : 0;
                                     const bool keep = c >= r;
                                     int32_t tot;
-                                    const int32_t slot = blk_compact(cred, par, wv, keep, tot);
+                                    const int32_t slot = blk_compact<GROWS>(cred, par, wv, keep, tot);
                                     if (keep) { ALIVE[nn2 + slot] = j; cm2 = min(cm2, (int64_t)c); }
                                     nn2 += tot;
                                 }
                                 na = nn2;
-                                blk_red3<R_MIN, R_SUM, R_SUM>(cred, par, wv, lane, cm2, z0, z1);   // + ALIVE visible
+                                blk_red3<R_MIN, R_SUM, R_SUM, GROWS>(cred, par, wv, lane, cm2, z0, z1);   // + ALIVE visible
                                 cmin = cm2;
                                 PROF_INC(6);
                             }
@@ -1375,7 +1396,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                         }
                     }
                     PROF_T(t_pb);
-                    lds_barrier();            // the run's row updates are visible to every wave
+                    cbar<GROWS>();            // the run's row updates are visible to every wave
                     if (tid == 0 && placed > 0) gseg[nseg] = Seg{nsched, pos + done, placed, 0};
                     nseg += placed > 0 ? 1 : 0;
                     nsched += placed;
@@ -1412,7 +1433,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                         open_node();
                         if (sf & SF_CP_EVAL) evals++;
                         done++;
-                        lds_barrier();
+                        cbar<GROWS>();
                         continue;
                     }
                     // Every row is full for this pod, so each remaining pod group opens a
@@ -1455,7 +1476,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                             SC[(size_t)sc * kcap + node] = wsub(tp.node.alloc_scalar[sc], tp.used_scalar[sc]);
                         }
                     }
-                    lds_barrier();                                                  // new rows visible
+                    cbar<GROWS>();                                                  // new rows visible
                     evals += open_evals(n_open, ct, placed2, k0, j00, kev, (sf & SF_CP_EVAL) != 0);
                     if (so_node) for (int32_t t = tid; t < placed2; t += CT) so_node[nsched + t] = k0 + t / ct;
                     if (tid == 0 && placed2 > 0) gseg[nseg] = Seg{nsched, pos + done, placed2, 0};
@@ -1571,7 +1592,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
             granted++;
             if (last_node >= 0 && !R[last_node].used) continue;               // :114-116
             if (k >= kcap) { res.status = CA_ECAPACITY; break; }
-            lds_barrier();                    // every wave's scan is done before rows change
+            cbar<GROWS>();                    // every wave's scan is done before rows change
             const int32_t nn = open_node();
             // CheckPredicates(pod, newNode) (:132-134)
             if (sf & SF_CP_EVAL) evals++;
@@ -1588,10 +1609,10 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                     ok = c == 0;
                 }
             }
-            if (!ok) { lds_barrier(); continue; }
+            if (!ok) { cbar<GROWS>(); continue; }
             found = nn;
         }
-        lds_barrier();                        // every wave's scan is done before R[found] changes
+        cbar<GROWS>();                        // every wave's scan is done before R[found] changes
         // AddPod(pod, node) (:96 / :135) — NodeInfo.update on the new-node row
         if (tid == 0) {
             NodeRec r = R[found];
@@ -1614,17 +1635,17 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
         }
         nsched++;
         progress();
-        lds_barrier();                        // the placement is visible to every wave
+        cbar<GROWS>();                        // the placement is visible to every wave
     }
     if (pend) {
         so_pod[out_idx] = cur.pod;
         if (so_node) so_node[out_idx] = out_node;
     }
     // newNodesWithPods
-    lds_barrier();
+    cbar<GROWS>();
     int64_t cnt = 0, z0 = 0, z1 = 0;
     for (int32_t j = tid; j < k; j += CT) cnt += R[j].used;
-    blk_red3<R_SUM, R_SUM, R_SUM>(cred, par, wv, lane, cnt, z0, z1);
+    blk_red3<R_SUM, R_SUM, R_SUM, GROWS>(cred, par, wv, lane, cnt, z0, z1);
     if (tid == 0) {
         res.node_count = (int32_t)cnt;
         res.n_sched = nsched;
@@ -1730,6 +1751,10 @@ struct ca_estimate_plan {
     int32_t n_masks = 0, n_tiles = 0;
     DevBuf d_meta, d_pod_idx, d_tmpl, d_sortA, d_sortB, d_stream, d_spod, d_seg, d_heads, d_unsup, d_lin, d_need,
         d_out, d_sched_pod, d_sched_node, d_crank, d_hist;
+    // HBM-slab rows (k_ffd_chain<true>): per group kcap and slab offset, for the limiter
+    // setting they were sized for (slab_max_nodes)
+    DevBuf d_slab, d_slab_off, d_gkcap;
+    int32_t slab_max_nodes = -2;
     int32_t n_hist = 0, max_rtiles = 0;
     bool bucket = false;           // bucket sort over score classes (podset has <= CLS_MAX classes)
     Stats stats;
@@ -1922,11 +1947,37 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     const int32_t n_base = (int32_t)m->nodes.size();
     if (G == 0) return CA_OK;
     if (m->n_scope_blockers > 0) return CA_EUNSUPPORTED;    // casim.h scope: required anti-affinity in the snapshot
-    // kcap: new nodes a group can add (limiter cap, or one per pod when unlimited)
+    // kcap: new nodes a group can add (limiter cap, or one per pod when unlimited: a group
+    // never opens more nodes than it has pods)
     int32_t kcap = lim->max_nodes > 0 ? std::min(lim->max_nodes, std::max(p->max_count, 1)) : std::max(p->max_count, 1);
     kcap = ((kcap + 63) / 64) * 64;
-    const size_t lds = chain_lds_bytes(kcap, p->use_ports, p->use_scalar);
-    if (lds + sizeof(ChainRed) > 160 * 1024) return CA_EUNSUPPORTED;   // HBM-backed variant is future work
+    size_t lds = chain_lds_bytes(kcap, p->use_ports, p->use_scalar);
+    // rows that do not fit the CU's LDS (an unlimited estimate of a large group) live in a
+    // per-group HBM slab sized by the group's own pod count
+    const bool grows = lds + sizeof(ChainRed) > 160 * 1024 || (getenv("CASIM_CHAIN_GLOBAL") != nullptr);
+    if (grows) {
+        lds = 0;
+        if (p->slab_max_nodes != lim->max_nodes) {
+            std::vector<int64_t> off(G);
+            std::vector<int32_t> kc(G);
+            int64_t tot = 0;
+            for (int32_t g = 0; g < G; g++) {
+                const int32_t c = std::max(p->h_meta[g].count, 1);
+                int32_t kg = lim->max_nodes > 0 ? std::min(lim->max_nodes, c) : c;
+                kg = ((kg + 63) / 64) * 64;
+                kc[g] = kg;
+                off[g] = tot;
+                tot += (int64_t)((chain_lds_bytes(kg, p->use_ports, p->use_scalar) + 255) & ~(size_t)255);
+            }
+            int rc;
+            if ((rc = p->d_slab.reserve((size_t)std::max<int64_t>(tot, 256))) != CA_OK) return rc;
+            if ((rc = p->d_slab_off.reserve(sizeof(int64_t) * (size_t)G)) != CA_OK) return rc;
+            if ((rc = p->d_gkcap.reserve(sizeof(int32_t) * (size_t)G)) != CA_OK) return rc;
+            CA_HIP_CHECK(hipMemcpy(p->d_slab_off.ptr, off.data(), sizeof(int64_t) * G, hipMemcpyHostToDevice));
+            CA_HIP_CHECK(hipMemcpy(p->d_gkcap.ptr, kc.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice));
+            p->slab_max_nodes = lim->max_nodes;
+        }
+    }
     // Zero-copy results: when the caller's sched_pod is page-locked (ca_host_alloc) and no
     // node ordinals are wanted, the chains publish straight into it (k_ffd_chain epilogue).
     // (Device-resident results could use the same publisher into the plan's own buffer;
@@ -2110,9 +2161,12 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             CA_HIP_CHECK(hipEventRecord(p->ev_go, st));
         }
         CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN0], st));
-        CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_ffd_chain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        if (!grows)
+            CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_ffd_chain<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds));
         auto chain = [&](hipStream_t ss, const int32_t* gm, int32_t ng) -> int {
-            hipLaunchKernelGGL(k_ffd_chain, dim3(ng), dim3(CT), lds, ss, p->d_meta.as<GroupMeta>(),
+            hipLaunchKernelGGL(grows ? k_ffd_chain<true> : k_ffd_chain<false>, dim3(ng), dim3(CT), lds, ss,
+                               p->d_meta.as<GroupMeta>(),
                                p->d_stream.as<StreamPod>(), p->d_heads.as<uint64_t>(), p->d_tmpl.as<ca_template>(),
                                p->s->t.spec.as<ca_pod_spec>(), p->s->t.hot.as<PodHot>(), p->d_lin.as<int32_t>(),
                                p->d_need.as<uint8_t>(), p->d_unsup.as<uint32_t>(), n_base, lim->max_nodes, kcap,
@@ -2120,7 +2174,8 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                p->d_sched_pod.as<int32_t>(), sched_node ? p->d_sched_node.as<int32_t>() : nullptr,
                                p->d_seg.as<Seg>(), publish ? p->d_tickets.as<int32_t>() : nullptr,
                                p->d_qctl.as<int32_t>(), p->nsub, p->d_prog.as<int2>(), p->pch, p->d_out.as<ChainOut>(),
-                               gm);
+                               gm, grows ? p->d_slab.as<unsigned char>() : nullptr,
+                               grows ? p->d_slab_off.as<int64_t>() : nullptr, grows ? p->d_gkcap.as<int32_t>() : nullptr);
             CA_HIP_CHECK(hipGetLastError());
             return CA_OK;
         };

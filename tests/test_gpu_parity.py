@@ -205,6 +205,54 @@ def test_estimate_runs_random(seed, batch, nodes, oracle, monkeypatch):
     assert o.last_index == g.last_index
 
 
+@pytest.mark.parametrize("nodes", [True, False], ids=["ordinals", "no-ordinals"])
+@pytest.mark.parametrize("seed", range(16))
+def test_estimate_hbm_rows_random(seed, nodes, oracle, monkeypatch):
+    """The chain with its new-node rows in per-group HBM slabs (the path of an unlimited
+    estimate too large for LDS, forced here on small inputs): identical to the oracle."""
+    monkeypatch.setenv("CASIM_CHAIN_GLOBAL", "1")
+    rng, nodes_, pods, templates, groups = _run_heavy_inputs(seed)
+    table, node_recs, tm, off, pod_idx = _encode_estimate(nodes_, pods, templates, groups)
+    max_nodes = rng.choice([0, 0, 2, 40])
+    L0 = rng.choice([0, 3, 123])
+    o, m = oracle.OracleState(), _mirror()
+    for b in (o, m):
+        b.clear()
+        if len(node_recs):
+            b.add_nodes(node_recs)
+    ro = o.estimate(table, off, pod_idx, tm, max_nodes, L0)
+    g = m.estimate(table, off, pod_idx, tm, max_nodes, L0, want_nodes=nodes)
+    assert np.array_equal(ro.results, g.results), (seed, ro.results, g.results)
+    for k in range(len(groups)):
+        a, n = off[k], int(ro.results[k]["n_scheduled"])
+        assert np.array_equal(ro.sched_pod[a:a + n], g.sched_pod[a:a + n]), (seed, k)
+        if nodes:
+            assert np.array_equal(ro.sched_node[a:a + n], g.sched_node[a:a + n]), (seed, k)
+    assert ro.last_index == g.last_index
+
+
+def test_estimate_unlimited_full_c2():
+    """BASELINE C2 with the unlimited limiter (maxNodes = 0, threshold_based_limiter.go:49-52):
+    up to 14k new nodes per group, rows in HBM slabs.  Checked against the committed result
+    of the CPU restatement (tests/golden/make_c2_unlimited.py; ~2 min of oracle time)."""
+    import json
+    import os
+    import zlib
+    with open(os.path.join(os.path.dirname(__file__), "golden", "c2_unlimited.json")) as f:
+        ref = json.load(f)
+    w = W.c2()
+    m = _mirror()
+    W.load_estimate(m, w)
+    g = m.estimate(w.table, w.group_off, w.pod_idx, w.templates, 0, 0, want_nodes=False)
+    assert g.last_index == ref["last_index"]
+    for k, rg in enumerate(ref["groups"]):
+        r = g.results[k]
+        for f in ("node_count", "n_scheduled", "nodes_added", "last_index_in", "last_index_out", "status", "evals"):
+            assert int(r[f]) == rg[f], (k, f, int(r[f]), rg[f])
+        a, n = int(w.group_off[k]), rg["n_scheduled"]
+        assert zlib.crc32(np.ascontiguousarray(g.sched_pod[a:a + n], np.int32).tobytes()) == rg["sched_crc32"], k
+
+
 @pytest.mark.parametrize("seed", range(8))
 def test_estimate_heavy_first_split(seed, oracle, monkeypatch):
     """G >= 8 groups: the heavy groups sort and chain first on the main stream, the rest
@@ -244,10 +292,13 @@ def test_estimate_heavy_first_split(seed, oracle, monkeypatch):
     ("C2-unlimited", W.c2(n_pods=1500, n_groups=8, n_existing=20, max_nodes=0)),
     ("C2-medium", W.c2(n_pods=20000, n_groups=20, n_existing=300)),
 ])
-@pytest.mark.parametrize("batch,sort", [("1", "bucket"), ("0", "bucket"), ("1", "merge")])
-def test_estimate_workloads(name, w, batch, sort, oracle, monkeypatch):
+@pytest.mark.parametrize("batch,sort,rows", [("1", "bucket", "lds"), ("0", "bucket", "lds"), ("1", "merge", "lds"),
+                                             ("1", "bucket", "hbm"), ("0", "bucket", "hbm")])
+def test_estimate_workloads(name, w, batch, sort, rows, oracle, monkeypatch):
     monkeypatch.setenv("CASIM_RUN_BATCH", batch)
     monkeypatch.setenv("CASIM_SORT", sort)
+    if rows == "hbm":
+        monkeypatch.setenv("CASIM_CHAIN_GLOBAL", "1")
     outs = []
     for b in (oracle.OracleState(), _mirror()):
         W.load_estimate(b, w)

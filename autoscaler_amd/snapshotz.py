@@ -107,6 +107,7 @@ def _affinity(a: Optional[dict]) -> Optional[Affinity]:
     out.pod_affinity = bool(a.get("podAffinity") or a.get("podAntiAffinity"))
     anti = a.get("podAntiAffinity") or {}
     out.required_anti_affinity = bool(anti.get("requiredDuringSchedulingIgnoredDuringExecution"))
+    out.required_pod_affinity = bool((a.get("podAffinity") or {}).get("requiredDuringSchedulingIgnoredDuringExecution"))
     return out
 
 
@@ -137,6 +138,7 @@ def pod_from_json(d: dict) -> Pod:
         topology_spread=list(spec.get("topologySpreadConstraints") or []), phase=status.get("phase", "Running"),
         deletion_timestamp=parse_time(md.get("deletionTimestamp")), priority=spec.get("priority"),
         termination_grace_period_seconds=spec.get("terminationGracePeriodSeconds"),
+        restart_policy=spec.get("restartPolicy", "Always") or "Always",
     )
 
 

@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <unordered_map>
 #include <cstddef>
 #include <cstring>
 #include <string>
@@ -53,6 +54,7 @@ struct FoCtl {
     int32_t ring_scans, windows;
     int32_t bad_line, bad_val; // CASIM_FO_CHECKS builds: the first index check that failed
     unsigned long long seq_cycles, all_cycles;   // CASIM_PROF builds: wave 0's walk, the whole kernel
+    unsigned long long fb_cyc[4];                 // CASIM_PROF builds, bitmap walk: hint, scan, place, batch loads
 };
 
 struct FoArgs {
@@ -634,6 +636,326 @@ __global__ void __launch_bounds__(SQ_T) k_filter_out(FoArgs a) {
     }
 }
 
+
+// ===========================================================================================
+// Feasibility-bitmap walk (the fast path).  For pending pods without host ports, scalar
+// requests or PreFilter NodeNames, a filter verdict factors into
+//   static[c][node]  TaintToleration, NodeAffinity, NodeName (node attributes: fixed for the
+//                    call; c = the pod's static class, -1 when every node passes),
+//   dyn[s][node]     NodeResourcesFit of the pod's resource shape s on the node's current
+//                    free resources (changes only on the nodes that take a placement),
+//   vis[node]        !Spec.Unschedulable (FitsAnyNodeMatching skips such nodes unfiltered,
+//                    schedulerbased.go:125-127; CheckPredicates runs NodeUnschedulable).
+// One bit per node, so FitsAnyNodeMatching's rotating first fit from lastIndex is a
+// first-set-bit search over (dyn & static & vis) words from bit L — 64 words (4096 nodes)
+// per wave step — and its evaluation count is the popcount of vis over the scanned range.
+//
+// The walk is one wavefront whose per-pod chain touches LDS only: dyn, vis (and the static
+// words when they fit), the similar-pods marks and per-controller counters, and a
+// direct-mapped cache of the rows of the nodes that took placements (free cpu / memory /
+// ephemeral / pods).  A row comes from HBM on its first placement (a miss) and goes back
+// on eviction and at the end; there is no global store on the chain, so no wait on the
+// vector-memory counter stalls a pod behind an earlier pod's write.
+// ===========================================================================================
+constexpr int FB_MAX_SHAPES = 64;        // one lane per shape for the bit updates
+constexpr int FB_T = 64;                 // the walk is one wavefront
+constexpr size_t FB_LDS_MAX = 160 * 1024;
+constexpr int FB_CACHE_MAX = 1024, FB_CACHE_MIN = 64;
+
+struct alignas(16) FbPod {               // per pending position (the walk order)
+    int32_t shape, scls, simcls;         // resource shape, static class (-1: passes everywhere), similar class
+    uint32_t flags;                      // PF_* (TOL_UNSCHED, PREFILTER_FAIL, DAEMONSET)
+};
+struct alignas(16) FbShape {
+    int64_t cpu, mem, eph;
+    uint32_t flags;                      // PF_ALL_ZERO
+    int32_t pad;
+};
+struct alignas(16) FbRow {               // LDS row cache entry: a node's free resources
+    int64_t cpu, mem, eph;
+    int32_t pods, tag;                   // tag: the node, -1 when empty
+};
+static_assert(sizeof(FbRow) == 32, "FbRow must be 32 B");
+
+struct FbArgs {
+    NodeHot* hot;
+    int32_t n, nwords, P, S, K, n_classes, n_owners, cache_e, stat_in_lds;
+    const FbPod* pods;
+    const FbShape* shapes;
+    const uint64_t* dyn0;                // [S][nwords] initial dyn words (copied into LDS)
+    const uint64_t* vis0;                // [nwords]
+    const uint64_t* stat;                // [K][nwords] (copied into LDS when stat_in_lds)
+    int32_t* hints;                      // per position, in/out
+    int32_t* out_node;
+    uint8_t* cls_mark;                   // per similar class: the marks at the end (for the caller)
+    const uint8_t* cls_capped;
+    const int32_t* cls_owner;
+    FoCtl* ctl;
+};
+
+// LDS layout of k_fb_walk, shared by the host sizing and the kernel
+struct FbLds {
+    size_t cache, dyn, vis, stat, ocnt, marks, oover, total;
+};
+__host__ __device__ inline size_t fb_a16(size_t x) { return (x + 15) & ~(size_t)15; }
+__host__ __device__ inline FbLds fb_lds(int32_t S, int32_t NW, int32_t K, int32_t stat_in_lds, int32_t n_classes,
+                                        int32_t n_owners, int32_t E) {
+    FbLds l;
+    l.cache = 0;
+    l.dyn = l.cache + sizeof(FbRow) * (size_t)E;
+    l.vis = l.dyn + sizeof(uint64_t) * (size_t)S * NW;
+    l.stat = l.vis + sizeof(uint64_t) * (size_t)NW;
+    l.ocnt = l.stat + (stat_in_lds ? sizeof(uint64_t) * (size_t)K * NW : 0);
+    l.marks = l.ocnt + fb_a16(sizeof(int32_t) * (size_t)(n_owners > 0 ? n_owners : 1));
+    l.oover = l.marks + fb_a16((size_t)(n_classes > 0 ? n_classes : 1));
+    l.total = l.oover + fb_a16((size_t)(n_owners > 0 ? n_owners : 1));
+    return l;
+}
+
+// shape s fits the free resources (cpu, mem, eph, pods): dev_fit_reasons without scalars
+__device__ inline bool fb_fit(const FbShape& sh, int64_t cpu, int64_t mem, int64_t eph, int32_t pods) {
+    if (pods < 1) return false;                                           // fit.go:256-265
+    if (sh.flags & PF_ALL_ZERO) return true;                             // :267-272
+    return sh.cpu <= cpu && sh.mem <= mem && sh.eph <= eph;              // :274-300
+}
+
+// dyn[s][w] and vis[w] for every word of every shape: block (word chunk, shape)
+__global__ void __launch_bounds__(256) k_fb_dyn(const NodeHot* __restrict__ hot, int32_t n, int32_t nwords,
+                                               const FbShape* __restrict__ shapes, int32_t S,
+                                               uint64_t* __restrict__ dyn, uint64_t* __restrict__ vis) {
+    const int32_t node = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int32_t s = (int32_t)blockIdx.y;                    // s == S: the visibility words
+    bool b = false;
+    if (node < n) {
+        const NodeHot h = hot[node];
+        b = s < S ? fb_fit(shapes[s], h.cpu, h.mem, h.eph, h.pods) : !(h.flags & NF_UNSCHED);
+    }
+    const uint64_t m = __ballot(b);
+    const int32_t w = node >> 6;
+    if ((threadIdx.x & 63) == 0 && w < nwords) {
+        if (s < S) dyn[(size_t)s * nwords + w] = m;
+        else vis[w] = m;
+    }
+}
+
+// static[c][w]: TaintToleration / NodeAffinity / NodeName of class c's representative pod
+__global__ void __launch_bounds__(256) k_fb_stat(const NodeStatic* __restrict__ st, int32_t n, int32_t nwords,
+                                                const int32_t* __restrict__ rep, const PodHot* __restrict__ ph,
+                                                const ca_pod_spec* __restrict__ specs,
+                                                const ca_selector_term* __restrict__ terms,
+                                                const ca_selector_req* __restrict__ reqs, uint64_t* __restrict__ stat) {
+    const int32_t node = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int32_t c = (int32_t)blockIdx.y;
+    bool b = false;
+    if (node < n) {
+        const PodHot p = ph[rep[c]];
+        b = dev_static_filters(specs[p.spec], p.flags, terms, reqs, st[node], false) == CA_PLUGIN_NONE;
+    }
+    const uint64_t m = __ballot(b);
+    const int32_t w = node >> 6;
+    if ((threadIdx.x & 63) == 0 && w < nwords) stat[(size_t)c * nwords + w] = m;
+}
+
+__device__ inline uint64_t bits_from(int b) { return b >= 64 ? 0ull : (~0ull << b); }   // bits >= b
+__device__ inline uint64_t bits_below(int b) { return b <= 0 ? 0ull : (b >= 64 ? ~0ull : ((1ull << b) - 1)); }
+__device__ inline int64_t rlane64(int64_t v, int l) {
+    return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((int)v, l));
+}
+extern "C" __device__ int __ockl_wfred_add_i32(int);   // DPP wavefront sum (all 64 lanes active)
+
+// a node's free resources back to its HBM row (flags untouched)
+__device__ inline void fb_put_row(NodeHot* hot, const FbRow& r) {
+    NodeHot* d = hot + r.tag;
+    d->cpu = r.cpu;
+    d->mem = r.mem;
+    d->eph = r.eph;
+    d->pods = r.pods;
+}
+
+// SetUnschedulable (similar_pods.go:92-111): wave-uniform, LDS writes by lane 0
+__device__ inline void fb_mark(const FbArgs& a, uint8_t* marks, int32_t* ocnt, uint8_t* oover, int32_t c,
+                               int32_t& overflowing, int lane) {
+    const int32_t o = a.cls_owner ? a.cls_owner[c] : -1;
+    if (o < 0 || !a.cls_capped[c]) {
+        if (lane == 0) marks[c] = 1;
+        return;
+    }
+    if (ocnt[o] >= FO_MAX_PER_OWNER) {                                   // the controller's cache is full
+        if (!oover[o]) {
+            if (lane == 0) oover[o] = 1;
+            overflowing++;
+        }
+        return;
+    }
+    if (lane == 0) {
+        marks[c] = 1;
+        ocnt[o] = ocnt[o] + 1;
+    }
+}
+
+__global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char fb_smem[];
+    const int lane = (int)threadIdx.x;
+    const int32_t n = a.n, NW = a.nwords, S = a.S, E = a.cache_e;
+    const FbLds lo = fb_lds(S, NW, a.K, a.stat_in_lds, a.n_classes, a.n_owners, E);
+    FbRow* cache = reinterpret_cast<FbRow*>(fb_smem + lo.cache);
+    uint64_t* dyn = reinterpret_cast<uint64_t*>(fb_smem + lo.dyn);                // [S][NW]
+    uint64_t* vis = reinterpret_cast<uint64_t*>(fb_smem + lo.vis);                // [NW]
+    uint64_t* stat_l = reinterpret_cast<uint64_t*>(fb_smem + lo.stat);            // [K][NW] when in LDS
+    int32_t* ocnt = reinterpret_cast<int32_t*>(fb_smem + lo.ocnt);
+    uint8_t* marks = fb_smem + lo.marks;
+    uint8_t* oover = fb_smem + lo.oover;
+    const uint64_t* stat = a.stat_in_lds ? stat_l : a.stat;
+    for (int32_t i = lane; i < E; i += FB_T) cache[i].tag = -1;
+    for (int32_t i = lane; i < S * NW; i += FB_T) dyn[i] = a.dyn0[i];
+    for (int32_t i = lane; i < NW; i += FB_T) vis[i] = a.vis0[i];
+    if (a.stat_in_lds)
+        for (int32_t i = lane; i < a.K * NW; i += FB_T) stat_l[i] = a.stat[i];
+    for (int32_t i = lane; i < a.n_owners; i += FB_T) { ocnt[i] = 0; oover[i] = 0; }
+    for (int32_t i = lane; i < a.n_classes; i += FB_T) marks[i] = 0;
+    // the shape table: lane s holds shape s
+    FbShape my_sh = {};
+    if (lane < S) my_sh = a.shapes[lane];
+    __syncthreads();
+    int32_t L = 0;
+    if (n > 0) { L = a.ctl->L % n; if (L < 0) L += n; }
+    bool succ = false;
+    unsigned long long evals = 0;
+    int32_t overflowing = 0;
+#ifdef CASIM_PROF
+    unsigned long long prof_fb[3] = {0, 0, 0};
+    const unsigned long long w_c0 = clock64();
+#endif
+    for (int32_t base = 0; base < a.P; base += FB_T) {
+        const int32_t cnt = min(FB_T, a.P - base);
+        FbPod lp = {0, -1, -1, 0};
+        int32_t lh = -1;
+        if (lane < cnt) { lp = a.pods[base + lane]; lh = a.hints[base + lane]; }
+        int32_t out = -1;
+        for (int32_t j = 0; j < cnt; j++) {
+#ifdef CASIM_PROF
+            const unsigned long long pc0 = clock64();
+#endif
+            const int32_t s = __builtin_amdgcn_readlane(lp.shape, j);
+            const int32_t c = __builtin_amdgcn_readlane(lp.scls, j);
+            const int32_t sim = __builtin_amdgcn_readlane(lp.simcls, j);
+            const uint32_t pf = (uint32_t)__builtin_amdgcn_readlane((int)lp.flags, j);
+            const int32_t h = __builtin_amdgcn_readlane(lh, j);
+            const uint64_t* ds = dyn + (size_t)s * NW;
+            const uint64_t* sc = c >= 0 ? stat + (size_t)c * NW : nullptr;
+            // the hint's words and the class mark, read together
+            const bool hinted = h >= 0 && h < n && !(pf & PF_PREFILTER_FAIL);
+            const int32_t hw = hinted ? (h >> 6) : 0;
+            const uint64_t hd = ds[hw], hv = vis[hw];
+            const uint64_t hs = sc ? sc[hw] : ~0ull;
+            const bool marked = sim >= 0 && marks[sim] != 0;
+            int32_t node = -1;
+            if (hinted) {                                                       // findNodeWithHints (:91-108)
+                evals++;                                                        // CheckPredicates ran the filters
+                const uint64_t bit = 1ull << (h & 63);
+                // CheckPredicates: NodeUnschedulable applies (tolerable), then static, then fit
+                if ((hd & hs & bit) && ((hv & bit) || (pf & PF_TOL_UNSCHED))) node = h;
+            }
+#ifdef CASIM_PROF
+            const unsigned long long pc1 = clock64();
+            prof_fb[0] += pc1 - pc0;
+#endif
+            if (node < 0 && !marked) {                                          // findNode (:110-125)
+                const bool can_mark = sim >= 0 && !(pf & PF_DAEMONSET);
+                bool failed = true;
+                if (!(pf & PF_PREFILTER_FAIL) && n > 0) {
+                    // rotating first fit from L over (dyn & static & vis), 64 words per step;
+                    // step r == NW revisits word w0 for the bits below L (the ring's tail)
+                    const int32_t w0 = L >> 6, b0 = L & 63;
+                    const int32_t last = b0 ? NW : NW - 1;
+                    uint32_t ev = 0;
+                    for (int32_t rb = 0; rb <= last; rb += FB_T) {
+                        const int32_t r = rb + lane;
+                        int32_t w = w0 + (r < NW ? r : 0);
+                        if (w >= NW) w -= NW;
+                        uint64_t mask = r == 0 ? bits_from(b0) : (r == NW ? bits_below(b0) : ~0ull);
+                        if (r > last) mask = 0;
+                        const uint64_t v = vis[w] & mask;
+                        uint64_t f = ds[w] & v;
+                        if (sc) f &= sc[w];
+                        const uint64_t hit = __ballot(f != 0);
+                        if (hit) {
+                            const int l = __builtin_ctzll(hit);
+                            const uint64_t fl = (uint64_t)rlane64((int64_t)f, l);
+                            const int bb = __builtin_ctzll(fl);
+                            const int32_t wl = __builtin_amdgcn_readlane(w, l);
+                            // visible positions up to the fit: the words before it, then its low bits
+                            const uint64_t vl = (uint64_t)rlane64((int64_t)v, l);
+                            uint32_t pc = (uint32_t)__builtin_popcountll(vl & bits_below(bb + 1));
+                            if (l > 0) pc += (uint32_t)__ockl_wfred_add_i32(lane < l ? __builtin_popcountll(v) : 0);
+                            ev += pc;
+                            node = (wl << 6) + bb;
+                            failed = false;
+                            break;
+                        }
+                        ev += (uint32_t)__ockl_wfred_add_i32(__builtin_popcountll(v));
+                    }
+                    evals += ev;
+                    if (!failed) {
+                        L = node + 1 == n ? 0 : node + 1;                       // schedulerbased.go:131
+                        succ = true;
+                    }
+                }
+                if (failed && can_mark) fb_mark(a, marks, ocnt, oover, sim, overflowing, lane);
+            }
+#ifdef CASIM_PROF
+            const unsigned long long pc2 = clock64();
+            prof_fb[1] += pc2 - pc1;
+#endif
+            if (node >= 0) {
+                // AddPod (NodeInfo.update, SF/types.go:672-692) on the node's cached row, then
+                // the node's bit in every shape's dyn word (lane s: shape s)
+                const int32_t e = node & (E - 1);
+                FbRow r = cache[e];
+                if (r.tag != node) {                                            // miss: evict, then HBM
+                    if (r.tag >= 0 && lane == 0) fb_put_row(a.hot, r);
+                    const NodeHot g = ld_hot_coh(a.hot + node);                 // may have been evicted before
+                    r.cpu = g.cpu; r.mem = g.mem; r.eph = g.eph; r.pods = g.pods; r.tag = node;
+                }
+                r.cpu = wsub(r.cpu, rlane64(my_sh.cpu, s));
+                r.mem = wsub(r.mem, rlane64(my_sh.mem, s));
+                r.eph = wsub(r.eph, rlane64(my_sh.eph, s));
+                r.pods = r.pods - 1;
+                if (lane == 0) cache[e] = r;
+                if (lane < S && !fb_fit(my_sh, r.cpu, r.mem, r.eph, r.pods))
+                    __hip_atomic_fetch_and(&dyn[(size_t)lane * NW + (node >> 6)], ~(1ull << (node & 63)),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+#ifdef CASIM_PROF
+            prof_fb[2] += clock64() - pc2;
+#endif
+            if (lane == j) out = node;
+        }
+        if (lane < cnt) {
+            a.out_node[base + lane] = out;
+            if (out >= 0) a.hints[base + lane] = out;                           // Hints.Set (:95, :123)
+        }
+    }
+    // the cached rows back to HBM (every tag is a distinct node; evicted rows are there already)
+    for (int32_t i = lane; i < E; i += FB_T) {
+        const FbRow r = cache[i];
+        if (r.tag >= 0) fb_put_row(a.hot, r);
+    }
+    for (int32_t i = lane; i < a.n_classes; i += FB_T) a.cls_mark[i] = marks[i];
+    if (lane == 0) {
+        if (succ) a.ctl->L = L;
+        a.ctl->evals = evals;
+        a.ctl->overflowing = overflowing;
+        a.ctl->phases = (a.P + FB_T - 1) / FB_T;
+#ifdef CASIM_PROF
+        for (int i = 0; i < 3; i++) a.ctl->fb_cyc[i] = prof_fb[i];
+        a.ctl->seq_cycles = clock64() - w_c0;
+        a.ctl->all_cycles = a.ctl->seq_cycles;
+#endif
+    }
+}
+
 }  // namespace casim
 
 using namespace casim;
@@ -739,9 +1061,136 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     a.n_pods = dp->n_pods;
     a.n_classes = n_classes;
     a.n_owners = n_owners;
+    // Feasibility-bitmap walk when every pending pod qualifies (no host ports, no scalar
+    // requests, no PreFilter NodeNames; <= 64 resource shapes; the bitmaps fit LDS); the
+    // window sequencer otherwise (CASIM_FO_WINDOW forces it, for tests of both).
+    fo.path = 0;
+    fo.fb_shapes = fo.fb_classes = 0;
+    std::vector<FbPod> fb_pods;
+    std::vector<FbShape> fb_shapes;
+    std::vector<int32_t> fb_rep;
+    int32_t fb_stat_in_lds = 0, fb_cache_e = 0;
+    bool fb = nn > 0 && !getenv("CASIM_FO_WINDOW");
+    const int32_t NW = (nn + 63) / 64;
+    if (fb) {
+        uint64_t taint_union = 0;
+        for (const NodeRow& r : m->nodes) taint_union |= r.spec.taints;
+        struct KeyHash {
+            size_t operator()(const std::string& k) const { return std::hash<std::string>()(k); }
+        };
+        std::unordered_map<std::string, int32_t, KeyHash> shape_id, cls_id;
+        fb_pods.resize((size_t)n);
+        for (int32_t k = 0; k < n && fb; k++) {
+            const ca_pod_spec& ps = t->pods[h_order[k]];
+            const uint32_t f = pod_dev_flags(ps);
+            if (f & (PF_PORTS | PF_SCALAR_REQ | PF_PREFILTER_NAMES)) { fb = false; break; }
+            std::string sk(reinterpret_cast<const char*>(&ps.req_milli_cpu), 24);
+            sk.push_back((f & PF_ALL_ZERO) ? 1 : 0);
+            auto it = shape_id.find(sk);
+            if (it == shape_id.end()) {
+                if ((int32_t)shape_id.size() >= FB_MAX_SHAPES) { fb = false; break; }
+                it = shape_id.emplace(sk, (int32_t)shape_id.size()).first;
+                FbShape sh;
+                sh.cpu = ps.req_milli_cpu; sh.mem = ps.req_memory; sh.eph = ps.req_ephemeral;
+                sh.flags = f & PF_ALL_ZERO; sh.pad = 0;
+                fb_shapes.push_back(sh);
+            }
+            int32_t cid = -1;                   // the static part of the filter chain (dev_static_filters)
+            if ((f & (PF_NODE_NAME | PF_AFFINITY)) || (ps.tolerated_taints & taint_union) != taint_union) {
+                std::string ck(reinterpret_cast<const char*>(&ps.tolerated_taints), 8);
+                const uint32_t sf = f & (PF_NODE_NAME | PF_AFFINITY);
+                ck.append(reinterpret_cast<const char*>(&sf), 4);
+                if (f & PF_NODE_NAME) ck.append(reinterpret_cast<const char*>(&ps.node_name_id), 4);
+                if (f & PF_AFFINITY) {
+                    ck.append(reinterpret_cast<const char*>(ps.node_selector), sizeof ps.node_selector);
+                    ck.append(reinterpret_cast<const char*>(&ps.aff_term_count), 4);
+                    for (int32_t q = 0; q < ps.aff_term_count; q++) {
+                        const ca_selector_term& tm = t->terms[ps.aff_term_first + q];
+                        ck.append(reinterpret_cast<const char*>(&tm.count), 4);
+                        for (int32_t r = 0; r < tm.count; r++)
+                            ck.append(reinterpret_cast<const char*>(&t->reqs[tm.first + r]), sizeof(ca_selector_req));
+                    }
+                }
+                auto ct = cls_id.find(ck);
+                if (ct == cls_id.end()) {
+                    ct = cls_id.emplace(ck, (int32_t)cls_id.size()).first;
+                    fb_rep.push_back(h_order[k]);
+                }
+                cid = ct->second;
+            }
+            FbPod& fp = fb_pods[k];
+            fp.shape = it->second;
+            fp.scls = cid;
+            fp.simcls = ps.similar_class;
+            fp.flags = f;
+        }
+        // LDS: the bitmaps and the similar-pods state; then the static words if they fit next
+        // to a row cache of >= 256 entries; the row cache takes what is left (<= 1024)
+        const int32_t S = (int32_t)fb_shapes.size(), K = (int32_t)fb_rep.size();
+        auto cache_for = [&](int32_t sil) -> int32_t {
+            const size_t rest = fb_lds(S, NW, K, sil, n_classes, n_owners, 0).total;
+            if (rest >= FB_LDS_MAX) return 0;
+            int32_t e = FB_CACHE_MAX;
+            while (e >= FB_CACHE_MIN && rest + sizeof(FbRow) * (size_t)e > FB_LDS_MAX) e >>= 1;
+            return e >= FB_CACHE_MIN ? e : 0;
+        };
+        fb_stat_in_lds = K > 0 && cache_for(1) >= 256 ? 1 : 0;
+        fb_cache_e = cache_for(fb_stat_in_lds);
+        if (!fb_cache_e) fb = false;
+    }
     CA_HIP_CHECK(hipEventRecord(m->ev0, m->stream));
-    hipLaunchKernelGGL(k_filter_out, dim3(1), dim3(SQ_T), 0, m->stream, a);
-    CA_HIP_CHECK(hipGetLastError());
+    if (fb) {
+        const int32_t S = (int32_t)fb_shapes.size(), K = (int32_t)fb_rep.size();
+        const size_t b_pods = al(sizeof(FbPod) * n), b_sh = al(sizeof(FbShape) * std::max(S, 1)),
+                     b_rep = al(sizeof(int32_t) * std::max(K, 1));
+        if ((rc = fo.fb_in.reserve(b_pods + b_sh + b_rep)) != CA_OK || (rc = fo.h_fb.reserve(b_pods + b_sh + b_rep)) != CA_OK)
+            return rc;
+        const size_t w_dyn = (size_t)S * NW, w_vis = (size_t)NW, w_stat = (size_t)K * NW;
+        if ((rc = fo.fb_bits.reserve(sizeof(uint64_t) * (w_dyn + w_vis + std::max<size_t>(w_stat, 1)))) != CA_OK) return rc;
+        char* hb = fo.h_fb.as<char>();
+        std::memcpy(hb, fb_pods.data(), sizeof(FbPod) * n);
+        std::memcpy(hb + b_pods, fb_shapes.data(), sizeof(FbShape) * S);
+        if (K) std::memcpy(hb + b_pods + b_sh, fb_rep.data(), sizeof(int32_t) * K);
+        char* db = fo.fb_in.as<char>();
+        CA_HIP_CHECK(hipMemcpyAsync(db, hb, b_pods + b_sh + b_rep, hipMemcpyHostToDevice, m->stream));
+        uint64_t* d_dyn = fo.fb_bits.as<uint64_t>();
+        uint64_t* d_vis = d_dyn + w_dyn;
+        uint64_t* d_stat = d_vis + w_vis;
+        hipLaunchKernelGGL(k_fb_dyn, dim3((nn + 255) / 256, S + 1), dim3(256), 0, m->stream, m->d_hot.as<const NodeHot>(),
+                           nn, NW, reinterpret_cast<const FbShape*>(db + b_pods), S, d_dyn, d_vis);
+        CA_HIP_CHECK(hipGetLastError());
+        if (K) {
+            hipLaunchKernelGGL(k_fb_stat, dim3((nn + 255) / 256, K), dim3(256), 0, m->stream,
+                               m->d_static.as<const NodeStatic>(), nn, NW,
+                               reinterpret_cast<const int32_t*>(db + b_pods + b_sh), dp->hot.as<const PodHot>(),
+                               dp->spec.as<const ca_pod_spec>(), dp->terms.as<const ca_selector_term>(),
+                               dp->reqs.as<const ca_selector_req>(), d_stat);
+            CA_HIP_CHECK(hipGetLastError());
+        }
+        FbArgs fa;
+        fa.hot = m->d_hot.as<NodeHot>();
+        fa.n = nn; fa.nwords = NW; fa.P = n; fa.S = S; fa.K = K;
+        fa.n_classes = n_classes; fa.n_owners = n_owners;
+        fa.cache_e = fb_cache_e; fa.stat_in_lds = fb_stat_in_lds;
+        fa.pods = reinterpret_cast<const FbPod*>(db);
+        fa.shapes = reinterpret_cast<const FbShape*>(db + b_pods);
+        fa.dyn0 = d_dyn; fa.vis0 = d_vis; fa.stat = d_stat;
+        fa.hints = a.hints; fa.out_node = a.out_node;
+        fa.cls_mark = a.cls_mark; fa.cls_capped = a.cls_capped; fa.cls_owner = a.cls_owner;
+        fa.ctl = a.ctl;
+        const size_t lds_all = fb_lds(S, NW, K, fb_stat_in_lds, n_classes, n_owners, fb_cache_e).total;
+        CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_fb_walk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_all));
+        hipLaunchKernelGGL(k_fb_walk, dim3(1), dim3(FB_T), lds_all, m->stream, fa);
+        CA_HIP_CHECK(hipGetLastError());
+        fo.path = 1;
+        fo.fb_shapes = S;
+        fo.fb_classes = K;
+        fo.fb_cache = fb_cache_e;
+        fo.fb_stat_lds = fb_stat_in_lds;
+    } else {
+        hipLaunchKernelGGL(k_filter_out, dim3(1), dim3(SQ_T), 0, m->stream, a);
+        CA_HIP_CHECK(hipGetLastError());
+    }
     CA_HIP_CHECK(hipEventRecord(m->ev1, m->stream));
     char* ho = fo.h_out.as<char>();
     CA_HIP_CHECK(hipMemcpyAsync(ho, dout, al(sizeof(int32_t) * n) + sizeof(int32_t) * n, hipMemcpyDeviceToHost,
@@ -781,6 +1230,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     fo.windows = hctl->windows;
     fo.seq_share = hctl->all_cycles ? (float)((double)hctl->seq_cycles / (double)hctl->all_cycles) : 0.0f;
     fo.walk_cycles_per_pod = n ? (float)((double)hctl->seq_cycles / n) : 0.0f;
+    for (int i = 0; i < 3; i++) fo.fb_cyc_per_pod[i] = n ? (float)((double)hctl->fb_cyc[i] / n) : 0.0f;
     fo.total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (n_placed) *n_placed = placed;
     return CA_OK;
@@ -789,10 +1239,12 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
 int ca_filter_stats(const ca_mirror* m, float* out, int32_t cap) {
     if (!m || (!out && cap > 0)) return CA_EINVAL;
     const casim::FilterScratch& fo = m->fo;
-    const float v[8] = {fo.kernel_ms, fo.total_ms, (float)fo.phases, (float)fo.steps, (float)fo.ring_scans,
-                        (float)fo.windows, fo.seq_share, fo.walk_cycles_per_pod};
-    for (int32_t i = 0; i < cap && i < 8; i++) out[i] = v[i];
-    return 8;
+    const float v[16] = {fo.kernel_ms, fo.total_ms, (float)fo.phases, (float)fo.steps, (float)fo.ring_scans,
+                         (float)fo.windows, fo.seq_share, fo.walk_cycles_per_pod, (float)fo.path,
+                         (float)fo.fb_shapes, (float)fo.fb_classes, fo.fb_cyc_per_pod[0], fo.fb_cyc_per_pod[1],
+                         fo.fb_cyc_per_pod[2], (float)fo.fb_cache, (float)fo.fb_stat_lds};
+    for (int32_t i = 0; i < cap && i < 16; i++) out[i] = v[i];
+    return 16;
 }
 
 }  // extern "C"

@@ -55,6 +55,13 @@ struct FilterScratch {
     float kernel_ms = 0, total_ms = 0;
     int32_t phases = 0, steps = 0, ring_scans = 0, windows = 0;
     float seq_share = 0, walk_cycles_per_pod = 0;   // CASIM_PROF builds: sequencer walk share, cycles/pod
+    // feasibility-bitmap path (filter.hip k_fb_*): pods, shapes, static classes, bitmaps
+    DevBuf fb_in, fb_bits;
+    HostBuf h_fb;
+    int32_t path = 0;              // last call: 1 bitmap walk, 0 window sequencer
+    int32_t fb_shapes = 0, fb_classes = 0;
+    float fb_cyc_per_pod[3] = {0, 0, 0};
+    int32_t fb_cache = 0, fb_stat_lds = 0;  // bitmap walk: row-cache entries, static words in LDS   // CASIM_PROF builds: bitmap walk cycles per pod (head, find, place)
 };
 
 // Dirty-row staging of sync_nodes: one H2D copy + a scatter kernel.

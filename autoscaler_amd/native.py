@@ -357,11 +357,13 @@ class Mirror:
         return a.output(placed.value, li.value, ev.value, ov.value)
 
     def filter_stats(self) -> dict:
-        out = (C.c_float * 8)()
-        self.lib.ca_filter_stats(self.h, out, 8)
+        out = (C.c_float * 16)()
+        self.lib.ca_filter_stats(self.h, out, 16)
         return {"kernel_ms": out[0], "total_ms": out[1], "phases": int(out[2]), "block_steps": int(out[3]),
                 "ring_scans": int(out[4]), "windows": int(out[5]), "seq_share": out[6],
-                "walk_cycles_per_pod": out[7]}
+                "walk_cycles_per_pod": out[7], "path": "bitmap" if out[8] else "window", "shapes": int(out[9]),
+                "static_classes": int(out[10]), "fb_cycles_per_pod": [out[11], out[12], out[13]],
+                "row_cache": int(out[14]), "static_in_lds": bool(out[15])}
 
     def find_nodes_to_remove(self, candidates, dest_mask, cand_status, move_off, move_pods, hints,
                              last_index: int = 0) -> RemovalOutput:

@@ -463,10 +463,13 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
                               int32_t n_classes, int32_t* hints, int32_t* last_index,
                               int32_t* out_node, int32_t* out_pod_id, int32_t* n_overflowing,
                               uint64_t* evals, int32_t* n_placed);
-/* [0] device time of the last call's kernel, [1] host wall time of the call (ms),
+/* [0] device time of the last call's kernels, [1] host wall time of the call (ms),
  * [2] slot phases, [3] block steps, [4] block-wide ring scans, [5] window loads, [6] share of the
- * kernel's cycles in wave 0's walk and [7] walk cycles per pod (both CASIM_PROF builds only, else 0);
- * returns 8. */
+ * kernel's cycles in wave 0's walk and [7] walk cycles per pod (both CASIM_PROF builds only, else 0),
+ * [8] path (1: feasibility-bitmap walk, 0: window sequencer), [9] resource shapes and [10] static
+ * classes of the bitmap walk, [11..13] the bitmap walk's cycles per pod in its head (attributes,
+ * hint), find (similar-pods check, scan) and place sections (CASIM_PROF builds), [14] its row-cache
+ * entries and [15] 1 when its static words sit in LDS; returns 16. */
 int ca_filter_stats(const ca_mirror* m, float* out, int32_t cap);
 
 /* ---- scale-down eligibility ----------------------------

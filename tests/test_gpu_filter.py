@@ -45,14 +45,20 @@ CONFIGS = {
 }
 
 
+@pytest.mark.parametrize("path", ["bitmap", "window"])
 @pytest.mark.parametrize("taints", [False, True], ids=["resources", "c4"])
 @pytest.mark.parametrize("cfg", list(CONFIGS))
-def test_filter_c5(cfg, taints, oracle_lib):
+def test_filter_c5(cfg, taints, path, oracle_lib, monkeypatch):
+    """Both kernels: the feasibility-bitmap walk (every C5 pod qualifies) and the window
+    sequencer (forced with CASIM_FO_WINDOW)."""
+    if path == "window":
+        monkeypatch.setenv("CASIM_FO_WINDOW", "1")
     w = W.c5_filter(taints=taints, **CONFIGS[cfg])
     g, o = native.Mirror(0), oracle_lib.OracleState()
     W.load_filter(g, w)
     W.load_filter(o, w)
     rg = g.filter_out_schedulable(w.pending, w.order, w.class_owner, w.hints, 3)
+    assert g.filter_stats()["path"] == path
     ro = o.filter_out_schedulable(w.pending, w.order, w.class_owner, w.hints, 3)
     _eq(rg, ro, cfg)
     # the state left behind: a second pass of everything (hints from the first) matches,

@@ -849,14 +849,19 @@ __device__ inline Seg ld_seg(const Seg* p) {
 // in completion order, waits for it, and writes outputs [sub*pch, +pch) of its group
 // into the caller's page-locked buffer: single placements from the chain's sched_pod,
 // run placements from the stream via the group's segments, -1 past n_scheduled.
-// Every block exits once all `total` tickets are claimed; a ticket not pushed within
-// the deadline (a chain that died) sets qctl[2] and ends the block.
+// Every block exits once all `total` tickets are claimed.  HIP does not promise that the
+// two kernels overlap, so the publisher never waits on a chain that has not started:
+// the chains raise qctl[4] when they begin, and a publisher that sees no chain within
+// `start_ticks` (100 MHz wall clock; the kernels were serialised) sets qctl[2] and ends,
+// as does one whose ticket is not pushed within 200 ms of a started chain (a chain that
+// died).  qctl[2] sends the host to the stream-ordered copy (k_copy_segments + D2H).
 __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ groups, const ChainOut* __restrict__ outs,
                                                 const Seg* __restrict__ segs, const int32_t* __restrict__ spod,
                                                 const int32_t* sched_dev, int32_t* __restrict__ tickets,
                                                 int32_t* __restrict__ qctl, int32_t total, int32_t nsub,
                                                 const int2* __restrict__ prog, int32_t pch,
-                                                int32_t* pub) {      // pub may alias sched_dev (device results)
+                                                int32_t* pub,        // pub may alias sched_dev (device results)
+                                                uint64_t start_ticks) {
     __shared__ int32_t s_t, s_tk, s_seg0;
     for (;;) {
         if (threadIdx.x == 0) {
@@ -864,10 +869,17 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
             int32_t tk = -1;
             if (s_t < total) {
                 const uint64_t t0 = wall_clock64();
+                bool started = false;
                 for (;;) {
                     tk = __hip_atomic_load(&tickets[s_t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
                     if (tk >= 0) break;
-                    if (wall_clock64() - t0 > 20000000ull) { atomicExch(&qctl[2], 1); break; }   // 200 ms
+                    if (__hip_atomic_load(&qctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;  // given up
+                    if (!started) started = __hip_atomic_load(&qctl[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                    const uint64_t dt = wall_clock64() - t0;
+                    if ((!started && dt > start_ticks) || dt > 20000000ull) {               // 200 ms
+                        __hip_atomic_store(&qctl[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(2);
                 }
             }
@@ -949,6 +961,8 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     if (GROWS) kcap = gkcap[g];
     unsigned char* const row_base = GROWS ? gslab + slab_off[g] : smem_raw;
     if (!need[g]) return;
+    if (tickets && threadIdx.x == 0)              // a publisher may wait on this batch now
+        __hip_atomic_store(&qctl[4], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t t_begin = wall_clock64();      // diagnostics: ca_estimate_plan_group_ticks
     __builtin_amdgcn_s_setprio(3);                // the chain is the critical path: win issue over k_publish
 #ifdef CASIM_PROF
@@ -1688,7 +1702,7 @@ __global__ void __launch_bounds__(256) k_round_init(int32_t G, int32_t lin0, int
     for (int32_t g = i; g < G; g += stride) { lin[g] = lin0; need[g] = 1; unsup[g] = 0; }
     if (tickets)
         for (int32_t t = i; t < n_tickets; t += stride) tickets[t] = -1;
-    if (qctl && i < 4) qctl[i] = 0;
+    if (qctl && i < 5) qctl[i] = 0;
 }
 
 // 5. scheduled pods of the run placements: sched_pod[dst + t] = stream pod at src + t.
@@ -1763,7 +1777,9 @@ struct ca_estimate_plan {
     enum { EV_START, EV_SCORE, EV_MERGE, EV_EMIT, EV_CHAIN0, EV_CHAIN1, EV_COMPACT, EV_D2H, EV_N };
     hipEvent_t ev[EV_N] = {};
     float t_ms[7] = {};
+    int32_t pub_state = 0;         // last run: 0 results copied, 1 published zero-copy, 2 publisher gave up
     std::vector<uint64_t> diag;     // per group: chain ticks (100 MHz) | single-pod steps << 32
+    std::vector<uint8_t> grp_succ;  // last run, per group: a FitsAnyNode call succeeded (moved lastIndex)
     // zero-copy publishing (k_publish on its own stream, concurrent with the chains)
     hipStream_t pub_stream = nullptr;
     hipEvent_t ev_go = nullptr, ev_pub = nullptr;
@@ -1816,7 +1832,7 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     {
         int rc0;
         if ((rc0 = p->h_out.reserve(sizeof(ChainOut) * (size_t)std::max(G, 1))) != CA_OK) return rc0;
-        if ((rc0 = p->h_qc.reserve(sizeof(int32_t) * 4)) != CA_OK) return rc0;
+        if ((rc0 = p->h_qc.reserve(sizeof(int32_t) * 5)) != CA_OK) return rc0;
     }
     p->h_off.assign(group_off, group_off + G + 1);
     p->h_tmpl.assign(templates, templates + G);
@@ -1900,7 +1916,7 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     if ((rc = p->d_tickets.reserve(sizeof(int32_t) * (size_t)std::max(p->n_tickets, 1))) != CA_OK) return rc;
     if ((int64_t)G * p->nsub < INT32_MAX &&
         (rc = p->d_prog.reserve(sizeof(int2) * (size_t)G * (size_t)p->nsub)) != CA_OK) return rc;
-    if ((rc = p->d_qctl.reserve(sizeof(int32_t) * 4)) != CA_OK) return rc;
+    if ((rc = p->d_qctl.reserve(sizeof(int32_t) * 5)) != CA_OK) return rc;
     if ((rc = p->d_unsup.reserve(sizeof(uint32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
     if ((rc = p->d_lin.reserve(sizeof(int32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
     if ((rc = p->d_need.reserve((size_t)std::max(G, 1))) != CA_OK) return rc;
@@ -1917,6 +1933,15 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     if (G) CA_HIP_CHECK(hipMemcpyAsync(p->d_tmpl.ptr, templates, sizeof(ca_template) * G, hipMemcpyHostToDevice, st));
     CA_HIP_CHECK(hipStreamSynchronize(st));
     return CA_OK;
+}
+
+// how long a publisher waits for the first chain of its batch to start (100 MHz ticks):
+// the chains are launched just before it, so a chain not running by then means the two
+// kernels were serialised (CASIM_PUB_START_US overrides; default 2 ms)
+uint64_t pub_start_ticks() {
+    const char* e = getenv("CASIM_PUB_START_US");
+    const long us = e ? std::max(1L, atol(e)) : 2000L;
+    return (uint64_t)us * 100ull;
 }
 
 int32_t pub_blocks() {
@@ -1942,6 +1967,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     // ca_estimate_plan_device_results); no node ordinals then
     const bool to_host = sched_pod != nullptr;
     if (!to_host && sched_node) return CA_EINVAL;
+    p->pub_state = 0;
     const auto t_start = std::chrono::steady_clock::now();
     CA_HIP_CHECK(hipSetDevice(m->device));
     const int32_t n_base = (int32_t)m->nodes.size();
@@ -1997,6 +2023,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     // not — run placements, and -1 past n_scheduled or for a failed group)
     const char* rb_env = getenv("CASIM_RUN_BATCH");
     const int32_t batch_runs = (rb_env && rb_env[0] == '0') ? 0 : 1;
+    const bool serial_pub = getenv("CASIM_PUB_SERIAL") != nullptr;
     int32_t tickets1 = 0;                               // publisher tickets of round 1 (every group)
     if (publish)
         for (int32_t g = 0; g < G; g++) tickets1 += (p->h_meta[g].count + p->pch - 1) / p->pch;
@@ -2157,8 +2184,25 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                 CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_pub, 0));   // previous publisher done
                 CA_HIP_CHECK(hipMemsetAsync(p->d_tickets.ptr, 0xFF, sizeof(int32_t) * (size_t)std::max(round_tickets, 1), st));
                 CA_HIP_CHECK(hipMemsetAsync(p->d_qctl.ptr, 0, sizeof(int32_t) * 3, st));   // [3] stays: sticky
+                CA_HIP_CHECK(hipMemsetAsync(p->d_qctl.as<int32_t>() + 4, 0, sizeof(int32_t), st));
             }
             CA_HIP_CHECK(hipEventRecord(p->ev_go, st));
+        }
+        // CASIM_PUB_SERIAL (tests): the publisher goes first on the chains' own stream, i.e.
+        // the two kernels are serialised — it must give up at its start deadline
+        auto launch_pub = [&](hipStream_t ps) -> int {
+            hipLaunchKernelGGL(k_publish, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, ps,
+                               p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
+                               p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int32_t>(),
+                               p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
+                               publish, pub_start_ticks());
+            CA_HIP_CHECK(hipGetLastError());
+            return CA_OK;
+        };
+        if (publish && round_tickets > 0 && serial_pub) {
+            int rc0;
+            if ((rc0 = launch_pub(st)) != CA_OK) return rc0;
+            CA_HIP_CHECK(hipEventRecord(p->ev_pub, st));
         }
         CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN0], st));
         if (!grows)
@@ -2189,14 +2233,9 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         } else if ((rc = chain(st, nullptr, G)) != CA_OK) {
             return rc;
         }
-        if (publish && round_tickets > 0) {
+        if (publish && round_tickets > 0 && !serial_pub) {
             CA_HIP_CHECK(hipStreamWaitEvent(p->pub_stream, p->ev_go, 0));
-            hipLaunchKernelGGL(k_publish, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, p->pub_stream,
-                               p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
-                               p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int32_t>(),
-                               p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
-                               publish);
-            CA_HIP_CHECK(hipGetLastError());
+            if ((rc = launch_pub(p->pub_stream)) != CA_OK) return rc;
             CA_HIP_CHECK(hipEventRecord(p->ev_pub, p->pub_stream));
         }
         CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN1], st));
@@ -2278,7 +2317,9 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         // the publisher of the last round wrote the results; a deadline hit (a chain that
         // died) falls back to the device copy + D2H
         const int32_t* qc = p->h_qc.as<int32_t>();      // read back with the last round's outputs
+        p->pub_state = 1;
         if (qc[2] != 0 || qc[3] != 0) {
+            p->pub_state = 2;
             set_last_error("estimate publisher missed a ticket; results copied instead");
             hipLaunchKernelGGL(k_copy_segments, dim3((p->max_count + CPY_PER_BLOCK - 1) / CPY_PER_BLOCK, G), dim3(256), 0,
                                st, p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
@@ -2327,6 +2368,9 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         p->t_ms[5] = el(P::EV_COMPACT, P::EV_D2H);
         sort_ms = el(P::EV_START, P::EV_EMIT);
     }
+    p->grp_succ.assign((size_t)G, 0);
+    for (int32_t g = 0; g < G; g++)
+        p->grp_succ[g] = outs[g].status == CA_OK && outs[g].had_success && !(cut >= 0 && g > cut) ? 1 : 0;
     // batch-level lastIndex dependence: the first group with a FitsAnyNode success decides
     p->stats.lin_sensitive = 0;
     p->stats.had_success = 0;
@@ -2346,6 +2390,22 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
 }
 
 }  // namespace
+
+// Results of the plan's last run re-based to another input lastIndex, for a batch that is
+// not lastIndex-sensitive (its outputs are the same from any input: multi.hip).  Returns
+// the batch's output lastIndex from `lin`.
+namespace casim {
+int32_t estimate_plan_rebase(const ca_estimate_plan* p, ca_estimate_result* results, int32_t lin) {
+    int32_t cur = lin;
+    for (int32_t g = 0; g < p->G; g++) {
+        ca_estimate_result& r = results[g];
+        r.last_index_in = cur;
+        if (r.status == CA_OK && g < (int32_t)p->grp_succ.size() && p->grp_succ[g]) cur = r.last_index_out;
+        else r.last_index_out = cur;
+    }
+    return cur;
+}
+}  // namespace casim
 
 extern "C" {
 
@@ -2397,8 +2457,9 @@ int ca_estimate_plan_stats(const ca_estimate_plan* p, int32_t* rounds, float* ch
 
 int ca_estimate_plan_timings(const ca_estimate_plan* p, float* out, int32_t cap) {
     if (!p || (cap > 0 && !out)) return CA_EINVAL;
-    const int32_t n = 7;
-    for (int32_t i = 0; i < n && i < cap; i++) out[i] = p->t_ms[i];
+    const int32_t n = 8;
+    for (int32_t i = 0; i < 7 && i < cap; i++) out[i] = p->t_ms[i];
+    if (cap > 7) out[7] = (float)p->pub_state;
     return n;
 }
 

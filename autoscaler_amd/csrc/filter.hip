@@ -650,17 +650,23 @@ __global__ void __launch_bounds__(SQ_T) k_filter_out(FoArgs a) {
 // first-set-bit search over (dyn & static & vis) words from bit L — 64 words (4096 nodes)
 // per wave step — and its evaluation count is the popcount of vis over the scanned range.
 //
-// The walk is one wavefront whose per-pod chain touches LDS only: dyn, vis (and the static
-// words when they fit), the similar-pods marks and per-controller counters, and a
-// direct-mapped cache of the rows of the nodes that took placements (free cpu / memory /
-// ephemeral / pods).  A row comes from HBM on its first placement (a miss) and goes back
-// on eviction and at the end; there is no global store on the chain, so no wait on the
-// vector-memory counter stalls a pod behind an earlier pod's write.
+// Runs: the pods of one controller variant come in a row (same shape, static class,
+// similar class and flags).  Without hints, k consecutive such pods take the first k
+// set bits of (dyn & static & vis) from L — pod t's scan starts right after pod t-1's
+// node and the placements behind it cannot change the nodes ahead — so one wave step
+// finds a whole run's nodes (a prefix sum of per-word popcounts across the lanes), the
+// placements update k rows in parallel lanes, and the evaluation count of the run is the
+// visible nodes from L to the last node (prefix counts of vis, which the walk never
+// changes).  A run stops at the end of one ring pass (the next pod then rescans the
+// updated state), at a hinted pod, and at the end of the 64-pod batch.  A hinted pod's
+// hint is checked alone (CheckPredicates); if it fails, its scan starts a run.
+// Node rows: read from HBM (the hinted nodes' rows prefetched when a batch is loaded),
+// written to an LDS buffer with a dirty bit per node, and flushed to HBM once per batch —
+// a global store inside the batch would make every later load wait for it.
 // ===========================================================================================
 constexpr int FB_MAX_SHAPES = 64;        // one lane per shape for the bit updates
 constexpr int FB_T = 64;                 // the walk is one wavefront
 constexpr size_t FB_LDS_MAX = 160 * 1024;
-constexpr int FB_CACHE_MAX = 1024, FB_CACHE_MIN = 64;
 
 struct alignas(16) FbPod {               // per pending position (the walk order)
     int32_t shape, scls, simcls;         // resource shape, static class (-1: passes everywhere), similar class
@@ -671,15 +677,15 @@ struct alignas(16) FbShape {
     uint32_t flags;                      // PF_ALL_ZERO
     int32_t pad;
 };
-struct alignas(16) FbRow {               // LDS row cache entry: a node's free resources
+struct alignas(16) FbRow {               // a placed node's new free resources (run scratch)
     int64_t cpu, mem, eph;
-    int32_t pods, tag;                   // tag: the node, -1 when empty
+    int32_t pods, pad;
 };
 static_assert(sizeof(FbRow) == 32, "FbRow must be 32 B");
 
 struct FbArgs {
     NodeHot* hot;
-    int32_t n, nwords, P, S, K, n_classes, n_owners, cache_e, stat_in_lds;
+    int32_t n, nwords, P, S, K, n_classes, n_owners, stat_in_lds;
     const FbPod* pods;
     const FbShape* shapes;
     const uint64_t* dyn0;                // [S][nwords] initial dyn words (copied into LDS)
@@ -695,17 +701,22 @@ struct FbArgs {
 
 // LDS layout of k_fb_walk, shared by the host sizing and the kernel
 struct FbLds {
-    size_t cache, dyn, vis, stat, ocnt, marks, oover, total;
+    size_t shapes, dyn, vis, stat, vpre, slot, bufrow, bufnode, dirty, ocnt, marks, oover, total;
 };
 __host__ __device__ inline size_t fb_a16(size_t x) { return (x + 15) & ~(size_t)15; }
 __host__ __device__ inline FbLds fb_lds(int32_t S, int32_t NW, int32_t K, int32_t stat_in_lds, int32_t n_classes,
-                                        int32_t n_owners, int32_t E) {
+                                        int32_t n_owners) {
     FbLds l;
-    l.cache = 0;
-    l.dyn = l.cache + sizeof(FbRow) * (size_t)E;
+    l.shapes = 0;
+    l.dyn = l.shapes + sizeof(FbShape) * (size_t)(S > 0 ? S : 1);
     l.vis = l.dyn + sizeof(uint64_t) * (size_t)S * NW;
     l.stat = l.vis + sizeof(uint64_t) * (size_t)NW;
-    l.ocnt = l.stat + (stat_in_lds ? sizeof(uint64_t) * (size_t)K * NW : 0);
+    l.vpre = l.stat + (stat_in_lds ? sizeof(uint64_t) * (size_t)K * NW : 0);
+    l.slot = l.vpre + fb_a16(sizeof(int32_t) * (size_t)(NW + 1));
+    l.bufrow = l.slot + sizeof(int32_t) * FB_T;
+    l.bufnode = l.bufrow + sizeof(FbRow) * FB_T;
+    l.dirty = l.bufnode + sizeof(int32_t) * FB_T;
+    l.ocnt = l.dirty + sizeof(uint64_t) * (size_t)NW;
     l.marks = l.ocnt + fb_a16(sizeof(int32_t) * (size_t)(n_owners > 0 ? n_owners : 1));
     l.oover = l.marks + fb_a16((size_t)(n_classes > 0 ? n_classes : 1));
     l.total = l.oover + fb_a16((size_t)(n_owners > 0 ? n_owners : 1));
@@ -762,15 +773,16 @@ __device__ inline int64_t rlane64(int64_t v, int l) {
     return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
                      (uint32_t)__builtin_amdgcn_readlane((int)v, l));
 }
-extern "C" __device__ int __ockl_wfred_add_i32(int);   // DPP wavefront sum (all 64 lanes active)
 
-// a node's free resources back to its HBM row (flags untouched)
-__device__ inline void fb_put_row(NodeHot* hot, const FbRow& r) {
-    NodeHot* d = hot + r.tag;
-    d->cpu = r.cpu;
-    d->mem = r.mem;
-    d->eph = r.eph;
-    d->pods = r.pods;
+// inclusive prefix sum across the 64 lanes (DPP row shifts, then row broadcasts 15 / 31)
+__device__ inline int32_t wave_incl_scan(int32_t v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);     // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);     // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);     // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);     // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);     // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);     // row_bcast:31 -> rows 2, 3
+    return v;
 }
 
 // SetUnschedulable (similar_pods.go:92-111): wave-uniform, LDS writes by lane 0
@@ -797,29 +809,49 @@ __device__ inline void fb_mark(const FbArgs& a, uint8_t* marks, int32_t* ocnt, u
 __global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fb_smem[];
     const int lane = (int)threadIdx.x;
-    const int32_t n = a.n, NW = a.nwords, S = a.S, E = a.cache_e;
-    const FbLds lo = fb_lds(S, NW, a.K, a.stat_in_lds, a.n_classes, a.n_owners, E);
-    FbRow* cache = reinterpret_cast<FbRow*>(fb_smem + lo.cache);
+    const int32_t n = a.n, NW = a.nwords, S = a.S;
+    const FbLds lo = fb_lds(S, NW, a.K, a.stat_in_lds, a.n_classes, a.n_owners);
+    FbShape* shp = reinterpret_cast<FbShape*>(fb_smem + lo.shapes);
     uint64_t* dyn = reinterpret_cast<uint64_t*>(fb_smem + lo.dyn);                // [S][NW]
     uint64_t* vis = reinterpret_cast<uint64_t*>(fb_smem + lo.vis);                // [NW]
     uint64_t* stat_l = reinterpret_cast<uint64_t*>(fb_smem + lo.stat);            // [K][NW] when in LDS
+    int32_t* vpre = reinterpret_cast<int32_t*>(fb_smem + lo.vpre);                // [NW + 1]: visible nodes before word w
+    int32_t* slot = reinterpret_cast<int32_t*>(fb_smem + lo.slot);                // a run's nodes
+    FbRow* bufrow = reinterpret_cast<FbRow*>(fb_smem + lo.bufrow);                // the batch's written rows
+    int32_t* bufnode = reinterpret_cast<int32_t*>(fb_smem + lo.bufnode);          // their nodes (-1: superseded)
+    uint64_t* dirty = reinterpret_cast<uint64_t*>(fb_smem + lo.dirty);            // node has a row in the buffer
     int32_t* ocnt = reinterpret_cast<int32_t*>(fb_smem + lo.ocnt);
     uint8_t* marks = fb_smem + lo.marks;
     uint8_t* oover = fb_smem + lo.oover;
-    const uint64_t* stat = a.stat_in_lds ? stat_l : a.stat;
-    for (int32_t i = lane; i < E; i += FB_T) cache[i].tag = -1;
+    const bool stat_lds = a.stat_in_lds != 0;
+    for (int32_t i = lane; i < S; i += FB_T) shp[i] = a.shapes[i];
     for (int32_t i = lane; i < S * NW; i += FB_T) dyn[i] = a.dyn0[i];
-    for (int32_t i = lane; i < NW; i += FB_T) vis[i] = a.vis0[i];
-    if (a.stat_in_lds)
+    if (stat_lds)
         for (int32_t i = lane; i < a.K * NW; i += FB_T) stat_l[i] = a.stat[i];
     for (int32_t i = lane; i < a.n_owners; i += FB_T) { ocnt[i] = 0; oover[i] = 0; }
     for (int32_t i = lane; i < a.n_classes; i += FB_T) marks[i] = 0;
-    // the shape table: lane s holds shape s
-    FbShape my_sh = {};
+    int32_t run_total = 0;                                                      // vis words and their prefix counts
+    for (int32_t base = 0; base < NW; base += FB_T) {
+        const int32_t w = base + lane;
+        const uint64_t v = w < NW ? a.vis0[w] : 0ull;
+        if (w < NW) { vis[w] = v; dirty[w] = 0; }
+        const int32_t c = __builtin_popcountll(v);
+        const int32_t inc = wave_incl_scan(c);
+        if (w < NW) vpre[w] = run_total + inc - c;
+        run_total += __builtin_amdgcn_readlane(inc, 63);
+    }
+    if (lane == 0) vpre[NW] = run_total;
+    const int32_t vis_total = run_total;
+    FbShape my_sh = {};                                                         // lane s: shape s (dyn updates)
     if (lane < S) my_sh = a.shapes[lane];
     __syncthreads();
     int32_t L = 0;
     if (n > 0) { L = a.ctl->L % n; if (L < 0) L += n; }
+    int32_t vpL = 0;                                                            // visible nodes before L
+    {
+        const int32_t w = L >> 6;
+        vpL = vpre[w] + __builtin_popcountll(vis[w] & bits_below(L & 63));
+    }
     bool succ = false;
     unsigned long long evals = 0;
     int32_t overflowing = 0;
@@ -827,13 +859,73 @@ __global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
     unsigned long long prof_fb[3] = {0, 0, 0};
     const unsigned long long w_c0 = clock64();
 #endif
+    // place k pods of shape s on slot[0..k) (lane t: slot[t]); `pre`: lane 0's row is given
+    // (a hinted node, prefetched) unless the buffer has a newer one
+    int32_t buf_n = 0;
+    auto place = [&](int32_t k, int32_t s, bool pre, const NodeHot& prow) {
+        const FbShape sh = shp[s];
+        FbRow q = {};
+        int32_t node = -1;
+        if (lane < k) {
+            node = slot[lane];
+            const bool dj = (dirty[node >> 6] >> (node & 63)) & 1;
+            int64_t cpu, mem, eph;
+            int32_t pods;
+            if (dj) {                                                           // the newest buffered row
+                int32_t i = buf_n - 1;
+                while (bufnode[i] != node) i--;
+                const FbRow r = bufrow[i];
+                bufnode[i] = -1;                                                // superseded below
+                cpu = r.cpu; mem = r.mem; eph = r.eph; pods = r.pods;
+            } else {
+                const NodeHot r = pre ? prow : ld_hot_coh(a.hot + node);
+                cpu = r.cpu; mem = r.mem; eph = r.eph; pods = r.pods;
+            }
+            q.cpu = wsub(cpu, sh.cpu);                                          // AddPod (SF/types.go:672-692)
+            q.mem = wsub(mem, sh.mem);
+            q.eph = wsub(eph, sh.eph);
+            q.pods = pods - 1;
+            q.pad = 0;
+            bufrow[buf_n + lane] = q;
+            bufnode[buf_n + lane] = node;
+            __hip_atomic_fetch_or(&dirty[node >> 6], 1ull << (node & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        buf_n += k;
+        for (int32_t t = 0; t < k; t++) {                                       // lane s': shape s' on each new row
+            const int64_t c0 = rlane64(q.cpu, t), m0 = rlane64(q.mem, t), e0 = rlane64(q.eph, t);
+            const int32_t p0 = __builtin_amdgcn_readlane(q.pods, t);
+            const int32_t x = __builtin_amdgcn_readlane(node, t);
+            if (lane < S && !fb_fit(my_sh, c0, m0, e0, p0))
+                __hip_atomic_fetch_and(&dyn[(size_t)lane * NW + (x >> 6)], ~(1ull << (x & 63)), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    };
+    // the batch's rows to HBM (one store per node: superseded entries are -1)
+    auto flush = [&]() {
+        if (lane < buf_n) {
+            const int32_t node = bufnode[lane];
+            if (node >= 0) {
+                const FbRow q = bufrow[lane];
+                NodeHot* d = a.hot + node;
+                d->cpu = q.cpu; d->mem = q.mem; d->eph = q.eph; d->pods = q.pods;
+                __hip_atomic_fetch_and(&dirty[node >> 6], ~(1ull << (node & 63)), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        buf_n = 0;
+    };
     for (int32_t base = 0; base < a.P; base += FB_T) {
         const int32_t cnt = min(FB_T, a.P - base);
         FbPod lp = {0, -1, -1, 0};
         int32_t lh = -1;
         if (lane < cnt) { lp = a.pods[base + lane]; lh = a.hints[base + lane]; }
+        const bool my_hinted = lane < cnt && lh >= 0 && lh < n && !(lp.flags & PF_PREFILTER_FAIL);
+        const uint64_t hinted_mask = __ballot(my_hinted);
+        NodeHot hrow = {};                                                      // prefetch: the hinted rows
+        if (my_hinted) hrow = ld_hot_coh(a.hot + lh);
         int32_t out = -1;
-        for (int32_t j = 0; j < cnt; j++) {
+        int32_t j = 0;
+        while (j < cnt) {
 #ifdef CASIM_PROF
             const unsigned long long pc0 = clock64();
 #endif
@@ -841,106 +933,108 @@ __global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
             const int32_t c = __builtin_amdgcn_readlane(lp.scls, j);
             const int32_t sim = __builtin_amdgcn_readlane(lp.simcls, j);
             const uint32_t pf = (uint32_t)__builtin_amdgcn_readlane((int)lp.flags, j);
-            const int32_t h = __builtin_amdgcn_readlane(lh, j);
             const uint64_t* ds = dyn + (size_t)s * NW;
-            const uint64_t* sc = c >= 0 ? stat + (size_t)c * NW : nullptr;
-            // the hint's words and the class mark, read together
-            const bool hinted = h >= 0 && h < n && !(pf & PF_PREFILTER_FAIL);
-            const int32_t hw = hinted ? (h >> 6) : 0;
-            const uint64_t hd = ds[hw], hv = vis[hw];
-            const uint64_t hs = sc ? sc[hw] : ~0ull;
-            const bool marked = sim >= 0 && marks[sim] != 0;
-            int32_t node = -1;
-            if (hinted) {                                                       // findNodeWithHints (:91-108)
-                evals++;                                                        // CheckPredicates ran the filters
+            const size_t so = c >= 0 ? (size_t)c * NW : 0;
+            int32_t first = j;                                                  // the run starts here
+            if ((hinted_mask >> j) & 1) {                                       // findNodeWithHints (:91-108)
+                const int32_t h = __builtin_amdgcn_readlane(lh, j);
+                const int32_t hw = h >> 6;
                 const uint64_t bit = 1ull << (h & 63);
-                // CheckPredicates: NodeUnschedulable applies (tolerable), then static, then fit
-                if ((hd & hs & bit) && ((hv & bit) || (pf & PF_TOL_UNSCHED))) node = h;
+                const uint64_t hs = c >= 0 ? (stat_lds ? stat_l[so + hw] : a.stat[so + hw]) : ~0ull;
+                evals++;                                                        // CheckPredicates ran the filters
+                // NodeUnschedulable applies (tolerable), then static, then fit
+                if ((ds[hw] & hs & bit) && ((vis[hw] & bit) || (pf & PF_TOL_UNSCHED))) {
+                    if (lane == 0) slot[0] = h;
+                    NodeHot pr;
+                    pr.cpu = rlane64(hrow.cpu, j); pr.mem = rlane64(hrow.mem, j); pr.eph = rlane64(hrow.eph, j);
+                    pr.pods = __builtin_amdgcn_readlane(hrow.pods, j); pr.flags = 0;
+                    place(1, s, true, pr);
+                    if (lane == j) out = h;
+                    j++;
+#ifdef CASIM_PROF
+                    prof_fb[0] += clock64() - pc0;
+#endif
+                    continue;
+                }
+                first = j + 1;                                                  // the run's other pods: unhinted
             }
+            // the run: pod j and the unhinted pods right after it with the same attributes
+            const bool same = lane >= first && lane < cnt && lp.shape == s && lp.scls == c && lp.simcls == sim &&
+                              lp.flags == pf;
+            const uint64_t run_ok = __ballot(same) & ~hinted_mask;
+            const uint64_t rest = first < 64 ? run_ok >> first : 0ull;          // consecutive ones from `first`
+            const int32_t m = (first - j) + (rest == ~0ull ? 64 : (int32_t)__builtin_ctzll(~rest));
 #ifdef CASIM_PROF
             const unsigned long long pc1 = clock64();
             prof_fb[0] += pc1 - pc0;
 #endif
-            if (node < 0 && !marked) {                                          // findNode (:110-125)
-                const bool can_mark = sim >= 0 && !(pf & PF_DAEMONSET);
-                bool failed = true;
-                if (!(pf & PF_PREFILTER_FAIL) && n > 0) {
-                    // rotating first fit from L over (dyn & static & vis), 64 words per step;
-                    // step r == NW revisits word w0 for the bits below L (the ring's tail)
-                    const int32_t w0 = L >> 6, b0 = L & 63;
-                    const int32_t last = b0 ? NW : NW - 1;
-                    uint32_t ev = 0;
-                    for (int32_t rb = 0; rb <= last; rb += FB_T) {
-                        const int32_t r = rb + lane;
-                        int32_t w = w0 + (r < NW ? r : 0);
-                        if (w >= NW) w -= NW;
-                        uint64_t mask = r == 0 ? bits_from(b0) : (r == NW ? bits_below(b0) : ~0ull);
-                        if (r > last) mask = 0;
-                        const uint64_t v = vis[w] & mask;
-                        uint64_t f = ds[w] & v;
-                        if (sc) f &= sc[w];
-                        const uint64_t hit = __ballot(f != 0);
-                        if (hit) {
-                            const int l = __builtin_ctzll(hit);
-                            const uint64_t fl = (uint64_t)rlane64((int64_t)f, l);
-                            const int bb = __builtin_ctzll(fl);
-                            const int32_t wl = __builtin_amdgcn_readlane(w, l);
-                            // visible positions up to the fit: the words before it, then its low bits
-                            const uint64_t vl = (uint64_t)rlane64((int64_t)v, l);
-                            uint32_t pc = (uint32_t)__builtin_popcountll(vl & bits_below(bb + 1));
-                            if (l > 0) pc += (uint32_t)__ockl_wfred_add_i32(lane < l ? __builtin_popcountll(v) : 0);
-                            ev += pc;
-                            node = (wl << 6) + bb;
-                            failed = false;
-                            break;
-                        }
-                        ev += (uint32_t)__ockl_wfred_add_i32(__builtin_popcountll(v));
-                    }
-                    evals += ev;
-                    if (!failed) {
-                        L = node + 1 == n ? 0 : node + 1;                       // schedulerbased.go:131
-                        succ = true;
-                    }
+            if (sim >= 0 && marks[sim]) {                                       // similar pod known unschedulable
+                j += m;
+                continue;
+            }
+            if (pf & PF_PREFILTER_FAIL) {                                       // no node passes PreFilter
+                if (sim >= 0 && !(pf & PF_DAEMONSET)) fb_mark(a, marks, ocnt, oover, sim, overflowing, lane);
+                j += (sim >= 0 && !(pf & PF_DAEMONSET) && marks[sim]) ? m : 1;
+                continue;
+            }
+            // findNode (:110-125): the first m fits from L, one ring pass, 64 words per step;
+            // step r == NW revisits word w0 for the bits below L (the ring's tail)
+            const int32_t w0 = L >> 6, b0 = L & 63;
+            const int32_t last = b0 ? NW : NW - 1;
+            int32_t k = 0;
+            for (int32_t rb = 0; rb <= last && k < m; rb += FB_T) {
+                const int32_t r = rb + lane;
+                int32_t w = w0 + (r < NW ? r : 0);
+                if (w >= NW) w -= NW;
+                uint64_t mask = r == 0 ? bits_from(b0) : (r == NW ? bits_below(b0) : ~0ull);
+                if (r > last) mask = 0;
+                uint64_t f = ds[w] & vis[w] & mask;
+                if (c >= 0) f &= stat_lds ? stat_l[so + w] : a.stat[so + w];
+                const int32_t cf = __builtin_popcountll(f);
+                const int32_t inc = wave_incl_scan(cf);
+                const int32_t tot = __builtin_amdgcn_readlane(inc, 63);
+                // lanes scatter their fits into slot[k + before ...] while the run needs them
+                int32_t at = k + inc - cf;
+                while (f && at < m) {
+                    slot[at++] = (w << 6) + __builtin_ctzll(f);
+                    f &= f - 1;
                 }
-                if (failed && can_mark) fb_mark(a, marks, ocnt, oover, sim, overflowing, lane);
+                k = min(m, k + tot);
             }
 #ifdef CASIM_PROF
             const unsigned long long pc2 = clock64();
             prof_fb[1] += pc2 - pc1;
 #endif
-            if (node >= 0) {
-                // AddPod (NodeInfo.update, SF/types.go:672-692) on the node's cached row, then
-                // the node's bit in every shape's dyn word (lane s: shape s)
-                const int32_t e = node & (E - 1);
-                FbRow r = cache[e];
-                if (r.tag != node) {                                            // miss: evict, then HBM
-                    if (r.tag >= 0 && lane == 0) fb_put_row(a.hot, r);
-                    const NodeHot g = ld_hot_coh(a.hot + node);                 // may have been evicted before
-                    r.cpu = g.cpu; r.mem = g.mem; r.eph = g.eph; r.pods = g.pods; r.tag = node;
-                }
-                r.cpu = wsub(r.cpu, rlane64(my_sh.cpu, s));
-                r.mem = wsub(r.mem, rlane64(my_sh.mem, s));
-                r.eph = wsub(r.eph, rlane64(my_sh.eph, s));
-                r.pods = r.pods - 1;
-                if (lane == 0) cache[e] = r;
-                if (lane < S && !fb_fit(my_sh, r.cpu, r.mem, r.eph, r.pods))
-                    __hip_atomic_fetch_and(&dyn[(size_t)lane * NW + (node >> 6)], ~(1ull << (node & 63)),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (k == 0) {                                                       // no node fits: every run pod fails
+                const bool can_mark = sim >= 0 && !(pf & PF_DAEMONSET);
+                if (can_mark) fb_mark(a, marks, ocnt, oover, sim, overflowing, lane);
+                // a marked class skips the rest of the run; otherwise (no class, DaemonSet, a
+                // controller over its cap) each pod scans the whole ring again, unchanged
+                const int32_t nfail = (can_mark && marks[sim]) ? 1 : m;
+                evals += (unsigned long long)nfail * (unsigned long long)vis_total;
+                j += m;
+                continue;
             }
+            // the visible nodes from L to the last fit (inclusive) were evaluated
+            const int32_t xl = slot[k - 1];
+            const int32_t xw = xl >> 6;
+            const int32_t vpx = vpre[xw] + __builtin_popcountll(vis[xw] & bits_below(xl & 63)) + 1;
+            evals += (unsigned long long)(xl >= L ? vpx - vpL : vis_total - vpL + vpx);
+            place(k, s, false, NodeHot{});
+            if (lane >= j && lane < j + k) out = slot[lane - j];
+            L = xl + 1 == n ? 0 : xl + 1;                                       // schedulerbased.go:131
+            vpL = L == 0 ? 0 : vpx;
+            succ = true;
+            j += k;
 #ifdef CASIM_PROF
             prof_fb[2] += clock64() - pc2;
 #endif
-            if (lane == j) out = node;
         }
+        flush();
         if (lane < cnt) {
             a.out_node[base + lane] = out;
             if (out >= 0) a.hints[base + lane] = out;                           // Hints.Set (:95, :123)
         }
-    }
-    // the cached rows back to HBM (every tag is a distinct node; evicted rows are there already)
-    for (int32_t i = lane; i < E; i += FB_T) {
-        const FbRow r = cache[i];
-        if (r.tag >= 0) fb_put_row(a.hot, r);
     }
     for (int32_t i = lane; i < a.n_classes; i += FB_T) a.cls_mark[i] = marks[i];
     if (lane == 0) {
@@ -1069,7 +1163,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     std::vector<FbPod> fb_pods;
     std::vector<FbShape> fb_shapes;
     std::vector<int32_t> fb_rep;
-    int32_t fb_stat_in_lds = 0, fb_cache_e = 0;
+    int32_t fb_stat_in_lds = 0;
     bool fb = nn > 0 && !getenv("CASIM_FO_WINDOW");
     const int32_t NW = (nn + 63) / 64;
     if (fb) {
@@ -1124,19 +1218,11 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
             fp.simcls = ps.similar_class;
             fp.flags = f;
         }
-        // LDS: the bitmaps and the similar-pods state; then the static words if they fit next
-        // to a row cache of >= 256 entries; the row cache takes what is left (<= 1024)
+        // LDS: shapes, bitmaps, vis prefix counts, run scratch and the similar-pods state,
+        // plus the static words when they fit too
         const int32_t S = (int32_t)fb_shapes.size(), K = (int32_t)fb_rep.size();
-        auto cache_for = [&](int32_t sil) -> int32_t {
-            const size_t rest = fb_lds(S, NW, K, sil, n_classes, n_owners, 0).total;
-            if (rest >= FB_LDS_MAX) return 0;
-            int32_t e = FB_CACHE_MAX;
-            while (e >= FB_CACHE_MIN && rest + sizeof(FbRow) * (size_t)e > FB_LDS_MAX) e >>= 1;
-            return e >= FB_CACHE_MIN ? e : 0;
-        };
-        fb_stat_in_lds = K > 0 && cache_for(1) >= 256 ? 1 : 0;
-        fb_cache_e = cache_for(fb_stat_in_lds);
-        if (!fb_cache_e) fb = false;
+        fb_stat_in_lds = K > 0 && fb_lds(S, NW, K, 1, n_classes, n_owners).total <= FB_LDS_MAX ? 1 : 0;
+        if (fb_lds(S, NW, K, fb_stat_in_lds, n_classes, n_owners).total > FB_LDS_MAX) fb = false;
     }
     CA_HIP_CHECK(hipEventRecord(m->ev0, m->stream));
     if (fb) {
@@ -1171,21 +1257,20 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
         fa.hot = m->d_hot.as<NodeHot>();
         fa.n = nn; fa.nwords = NW; fa.P = n; fa.S = S; fa.K = K;
         fa.n_classes = n_classes; fa.n_owners = n_owners;
-        fa.cache_e = fb_cache_e; fa.stat_in_lds = fb_stat_in_lds;
+        fa.stat_in_lds = fb_stat_in_lds;
         fa.pods = reinterpret_cast<const FbPod*>(db);
         fa.shapes = reinterpret_cast<const FbShape*>(db + b_pods);
         fa.dyn0 = d_dyn; fa.vis0 = d_vis; fa.stat = d_stat;
         fa.hints = a.hints; fa.out_node = a.out_node;
         fa.cls_mark = a.cls_mark; fa.cls_capped = a.cls_capped; fa.cls_owner = a.cls_owner;
         fa.ctl = a.ctl;
-        const size_t lds_all = fb_lds(S, NW, K, fb_stat_in_lds, n_classes, n_owners, fb_cache_e).total;
+        const size_t lds_all = fb_lds(S, NW, K, fb_stat_in_lds, n_classes, n_owners).total;
         CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_fb_walk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_all));
         hipLaunchKernelGGL(k_fb_walk, dim3(1), dim3(FB_T), lds_all, m->stream, fa);
         CA_HIP_CHECK(hipGetLastError());
         fo.path = 1;
         fo.fb_shapes = S;
         fo.fb_classes = K;
-        fo.fb_cache = fb_cache_e;
         fo.fb_stat_lds = fb_stat_in_lds;
     } else {
         hipLaunchKernelGGL(k_filter_out, dim3(1), dim3(SQ_T), 0, m->stream, a);
@@ -1242,7 +1327,7 @@ int ca_filter_stats(const ca_mirror* m, float* out, int32_t cap) {
     const float v[16] = {fo.kernel_ms, fo.total_ms, (float)fo.phases, (float)fo.steps, (float)fo.ring_scans,
                          (float)fo.windows, fo.seq_share, fo.walk_cycles_per_pod, (float)fo.path,
                          (float)fo.fb_shapes, (float)fo.fb_classes, fo.fb_cyc_per_pod[0], fo.fb_cyc_per_pod[1],
-                         fo.fb_cyc_per_pod[2], (float)fo.fb_cache, (float)fo.fb_stat_lds};
+                         fo.fb_cyc_per_pod[2], 0.0f, (float)fo.fb_stat_lds};
     for (int32_t i = 0; i < cap && i < 16; i++) out[i] = v[i];
     return 16;
 }

@@ -61,7 +61,7 @@ struct FilterScratch {
     int32_t path = 0;              // last call: 1 bitmap walk, 0 window sequencer
     int32_t fb_shapes = 0, fb_classes = 0;
     float fb_cyc_per_pod[3] = {0, 0, 0};
-    int32_t fb_cache = 0, fb_stat_lds = 0;  // bitmap walk: row-cache entries, static words in LDS   // CASIM_PROF builds: bitmap walk cycles per pod (head, find, place)
+    int32_t fb_stat_lds = 0;                // bitmap walk: static words in LDS   // CASIM_PROF builds: bitmap walk cycles per pod (head, find, place)
 };
 
 // Dirty-row staging of sync_nodes: one H2D copy + a scatter kernel.

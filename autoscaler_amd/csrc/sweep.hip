@@ -1059,6 +1059,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     // the outputs must reproduce the chain: each result with a successful scan was
     // computed at the lastIndex the chain gives it; the others do not move it
     int64_t Lrun = L0;
+    bool any_success = false;
     for (int32_t c = 0; c < C; c++) {
         const SweepOut& o = outs[c];
         if (o.status != CA_OK) { set_last_error("overlay capacity exceeded"); return o.status; }
@@ -1074,7 +1075,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         r.n_placed = o.n_placed;
         r.last_index_in = (int32_t)Lrun;
         r.evals = o.evals;
-        if (o.fa_success) Lrun = o.lout;
+        if (o.fa_success) { Lrun = o.lout; any_success = true; }
     }
     *last_index = (int32_t)Lrun;
     if (hints) {
@@ -1083,6 +1084,9 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     if (d_pod_hints) CA_HIP_CHECK(hipStreamSynchronize(st));
     tmark("done");
     m->sweep_stats.rounds = rounds + exact_runs;
+    // the sweep's output depends on its input lastIndex iff some scan succeeded
+    m->sweep_stats.had_success = any_success ? 1 : 0;
+    m->sweep_stats.lin_sensitive = m->sweep_stats.had_success;
     m->sweep_stats.exact_ms = 0;
     m->sweep_stats.walk_ms = std::chrono::duration<float, std::milli>(t_exact - t_start).count();
     m->sweep_stats.kernel_ms = kms;
@@ -1133,6 +1137,7 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     CA_HIP_CHECK(hipSetDevice(m->device));
     hipStream_t st = m->stream;
     const int32_t n = (int32_t)m->nodes.size();
+    m->sweep_stats.had_success = m->sweep_stats.lin_sensitive = 0;
     if (C == 0) return CA_OK;
     const int32_t M = move_off[C] - move_off[0];
     if (move_off[0] != 0 || M < 0) return CA_EINVAL;
@@ -1319,6 +1324,7 @@ int ca_removal_plan_run(ca_removal_plan* p, int32_t* hints, int32_t* last_index,
     if (!p || !last_index || (p->C_all > 0 && !results)) return CA_EINVAL;
     ca_mirror* m = p->m;
     CA_HIP_CHECK(hipSetDevice(m->device));
+    m->sweep_stats.had_success = m->sweep_stats.lin_sensitive = 0;
     if (p->C_all == 0) return CA_OK;
     if ((int32_t)m->nodes.size() != p->n) return CA_EINVAL;   // the plan's dest mask covers the node list
     if (m->n_scope_blockers > 0) return CA_EUNSUPPORTED;        // casim.h scope

@@ -95,6 +95,18 @@ def load() -> C.CDLL:
         "ca_util_table_destroy": ([vp], C.c_int),
         "ca_util_calculate": ([vp, i32, i32, C.c_int64, vp, p(C.c_float)], C.c_int),
         "ca_util_device_results": ([vp, p(vp)], C.c_int),
+        "ca_multi_create": ([p(vp), i32, p(vp)], C.c_int),
+        "ca_multi_destroy": ([vp], C.c_int),
+        "ca_multi_estimate_plan_create": ([vp, vp, vp, vp, vp, i32, p(vp)], C.c_int),
+        "ca_multi_estimate_plan_run": ([vp, vp, p(i32), vp, vp, vp], C.c_int),
+        "ca_multi_estimate_plan_stats": ([vp, p(i32), p(i32), vp, i32], C.c_int),
+        "ca_multi_estimate_plan_destroy": ([vp], C.c_int),
+        "ca_multi_estimate_batch": ([vp, vp, vp, vp, vp, i32, vp, p(i32), vp, vp, vp], C.c_int),
+        "ca_multi_removal_plan_create": ([vp, vp, i32, vp, vp, vp, vp, p(vp)], C.c_int),
+        "ca_multi_removal_plan_run": ([vp, vp, i32, p(i32), vp, vp], C.c_int),
+        "ca_multi_removal_plan_stats": ([vp, p(i32), p(i32), vp, i32], C.c_int),
+        "ca_multi_removal_plan_destroy": ([vp], C.c_int),
+        "ca_multi_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, i32, p(i32), vp, vp], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(lib, name)
@@ -125,6 +137,10 @@ def exported_symbols() -> list[str]:
         "ca_removal_plan_destroy", "ca_mirror_set_hints", "ca_mirror_get_hints",
         "ca_removal_candidate_ticks", "ca_filter_out_schedulable", "ca_filter_stats",
         "ca_util_table_create", "ca_util_table_destroy", "ca_util_calculate", "ca_util_device_results",
+        "ca_multi_create", "ca_multi_destroy", "ca_multi_estimate_plan_create", "ca_multi_estimate_plan_run",
+        "ca_multi_estimate_plan_stats", "ca_multi_estimate_plan_destroy", "ca_multi_estimate_batch",
+        "ca_multi_removal_plan_create", "ca_multi_removal_plan_run", "ca_multi_removal_plan_stats",
+        "ca_multi_removal_plan_destroy", "ca_multi_find_nodes_to_remove",
     ]
 
 
@@ -363,7 +379,7 @@ class Mirror:
                 "ring_scans": int(out[4]), "windows": int(out[5]), "seq_share": out[6],
                 "walk_cycles_per_pod": out[7], "path": "bitmap" if out[8] else "window", "shapes": int(out[9]),
                 "static_classes": int(out[10]), "fb_cycles_per_pod": [out[11], out[12], out[13]],
-                "row_cache": int(out[14]), "static_in_lds": bool(out[15])}
+                "static_in_lds": bool(out[15])}
 
     def find_nodes_to_remove(self, candidates, dest_mask, cand_status, move_off, move_pods, hints,
                              last_index: int = 0) -> RemovalOutput:
@@ -548,12 +564,13 @@ class EstimatePlan:
         self.lib.ca_estimate_plan_stats(self.h, C.byref(r), C.byref(a), C.byref(b), C.byref(c))
         sens, succ = C.c_int32(0), C.c_int32(0)
         self.lib.ca_estimate_plan_chain_info(self.h, C.byref(sens), C.byref(succ))
-        t = (C.c_float * 7)()
-        self.lib.ca_estimate_plan_timings(self.h, t, 7)
+        t = (C.c_float * 8)()
+        self.lib.ca_estimate_plan_timings(self.h, t, 8)
         names = ("score_ms", "merge_ms", "emit_ms", "chain_ms", "compact_ms", "d2h_ms", "host_ms")
         return {"rounds": r.value, "chain_ms": a.value, "sort_ms": b.value, "total_ms": c.value,
                 "lin_sensitive": sens.value, "had_success": succ.value,
-                "phases": {k: float(v) for k, v in zip(names, t)}}
+                "phases": {k: float(v) for k, v in zip(names, t)},
+                "results_path": ("copied", "published", "publisher_gave_up")[int(t[7])]}
 
     def chain_info(self) -> tuple:
         """(lastIndex-sensitive, had a FitsAnyNode success) of the last run: one call."""
@@ -620,3 +637,125 @@ class UtilTable:
             self.close()
         except Exception:
             pass
+
+
+class Multi:
+    """``ca_multi``: replicated mirrors, one per device.  The caller keeps
+    them identical; `mirrors` may repeat a device (tests shard over two mirrors on one GPU)."""
+
+    def __init__(self, mirrors):
+        self.mirrors = list(mirrors)
+        self.lib = self.mirrors[0].lib
+        arr = (C.c_void_p * len(self.mirrors))(*[m.h for m in self.mirrors])
+        h = C.c_void_p()
+        _check(self.lib.ca_multi_create(arr, len(self.mirrors), C.byref(h)), "ca_multi_create")
+        self.h = h
+
+    def for_each(self, fn):
+        """Apply a snapshot change to every replica, in order."""
+        return [fn(m) for m in self.mirrors]
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.ca_multi_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+class MultiEstimatePlan:
+    """``ca_multi_estimate_plan``: node groups in contiguous blocks over the replicas."""
+
+    def __init__(self, multi: Multi, table: abi.PodTable, group_off, pod_idx, templates: np.ndarray):
+        self.lib = multi.lib
+        self.group_off = np.ascontiguousarray(group_off, dtype=np.int32)
+        self.pod_idx = np.ascontiguousarray(pod_idx, dtype=np.int32)
+        self.templates = np.ascontiguousarray(templates, dtype=abi.TEMPLATE_DTYPE)
+        self.G = len(self.templates)
+        self.total = int(self.group_off[-1]) if len(self.group_off) else 0
+        h = C.c_void_p()
+        _check(self.lib.ca_multi_estimate_plan_create(multi.h, table.ref, ptr(self.group_off), ptr(self.pod_idx),
+                                                      ptr(self.templates), self.G, C.byref(h)),
+               "ca_multi_estimate_plan_create")
+        self.h = h
+        n = max(self.total, 1)
+        self._pinned = PinnedArray(self.lib, 2 * n, np.int32)
+        self.sched_pod = self._pinned.array[:n]
+        self.sched_node = self._pinned.array[n:]
+        self.results = np.zeros(self.G, abi.ESTIMATE_RESULT_DTYPE)
+
+    def run(self, max_nodes: int, last_index: int = 0, want_nodes: bool = True, copy: bool = True) -> EstimateOutput:
+        lim = abi.LimiterC(max_nodes, 0)
+        li = C.c_int32(last_index)
+        _check(self.lib.ca_multi_estimate_plan_run(self.h, C.byref(lim), C.byref(li), ptr(self.results),
+                                                   ptr(self.sched_pod), ptr(self.sched_node) if want_nodes else None),
+               "ca_multi_estimate_plan_run")
+        f = (lambda a: a.copy()) if copy else (lambda a: a)
+        return EstimateOutput(f(self.results), f(self.sched_pod[: self.total]), f(self.sched_node[: self.total]),
+                              li.value)
+
+    def stats(self) -> dict:
+        nb, rr = C.c_int32(0), C.c_int32(0)
+        first = np.zeros(65, np.int32)
+        self.lib.ca_multi_estimate_plan_stats(self.h, C.byref(nb), C.byref(rr), ptr(first), len(first))
+        return {"blocks": nb.value, "reruns": rr.value, "block_first_group": first[: nb.value + 1].tolist()}
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.ca_multi_estimate_plan_destroy(self.h)
+            self.h = None
+            self._pinned.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+class MultiRemovalPlan:
+    """``ca_multi_removal_plan``: FindNodesToRemove candidates in contiguous blocks."""
+
+    def __init__(self, multi: Multi, candidates, dest_mask, cand_status, move_off, move_pods):
+        self.lib = multi.lib
+        self.cand = np.ascontiguousarray(candidates, dtype=np.int32)
+        mask = np.ascontiguousarray(dest_mask, dtype=np.uint8)
+        status = np.ascontiguousarray(cand_status if cand_status is not None else np.zeros(len(self.cand)),
+                                      dtype=np.int32)
+        off = np.ascontiguousarray(move_off, dtype=np.int32)
+        self.moves = np.ascontiguousarray(move_pods, dtype=np.int32)
+        h = C.c_void_p()
+        _check(self.lib.ca_multi_removal_plan_create(multi.h, ptr(self.cand), len(self.cand), ptr(mask), ptr(status),
+                                                     ptr(off), ptr(self.moves), C.byref(h)),
+               "ca_multi_removal_plan_create")
+        self.h = h
+        self.results = np.zeros(len(self.cand), abi.REMOVAL_RESULT_DTYPE)
+
+    def run(self, hints, last_index: int = 0) -> RemovalOutput:
+        hints = np.array(hints, dtype=np.int32, copy=True)
+        dest = np.full(max(len(self.moves), 1), -1, np.int32)
+        li = C.c_int32(last_index)
+        _check(self.lib.ca_multi_removal_plan_run(self.h, ptr(hints), len(hints), C.byref(li), ptr(self.results),
+                                                  ptr(dest)), "ca_multi_removal_plan_run")
+        return RemovalOutput(self.results.copy(), dest[: len(self.moves)], hints, li.value)
+
+    def stats(self) -> dict:
+        nb, rr = C.c_int32(0), C.c_int32(0)
+        first = np.zeros(65, np.int32)
+        self.lib.ca_multi_removal_plan_stats(self.h, C.byref(nb), C.byref(rr), ptr(first), len(first))
+        return {"blocks": nb.value, "reruns": rr.value, "block_first_candidate": first[: nb.value + 1].tolist()}
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.ca_multi_removal_plan_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

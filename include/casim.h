@@ -389,15 +389,17 @@ int ca_estimate_plan_destroy(ca_estimate_plan* p);
 /* statistics of the last run: speculation rounds, kernel time of the chain kernel (ms) */
 int ca_estimate_plan_stats(const ca_estimate_plan* p, int32_t* rounds, float* chain_ms,
                            float* sort_ms, float* total_ms);
+/* Device time of each phase of the last run, in ms: [0] score+static predicates,
+ * [1] merge passes, [2] stream emission, [3] FFD chains (all speculation rounds),
+ * [4] result compaction, [5] D2H of the results; [6] host wall time of the call;
+ * [7] how the results reached sched_pod: 0 copied after the chains, 1 published
+ * zero-copy while they ran, 2 the publisher gave up (kernels serialised, or a chain
+ * died) and the results were copied instead.  Writes min(cap, 8) values; returns 8. */
+int ca_estimate_plan_timings(const ca_estimate_plan* p, float* out, int32_t cap);
 /* Whether the last run's outputs depend on the lastIndex it started from (then a caller
  * that ran the batch from a guessed lastIndex must re-run it from the true one), and
  * whether any FitsAnyNode call succeeded (if not, lastIndex passed through unchanged).
  * Used to chain batches sharded across GPUs. */
-/* Device time of each phase of the last run, in ms: [0] score+static predicates,
- * [1] merge passes, [2] stream emission, [3] FFD chains (all speculation rounds),
- * [4] result compaction, [5] D2H of the results; [6] host wall time of the call.
- * Writes min(cap, 7) values; returns 7. */
-int ca_estimate_plan_timings(const ca_estimate_plan* p, float* out, int32_t cap);
 int ca_estimate_plan_chain_info(const ca_estimate_plan* p, int32_t* lin_sensitive, int32_t* had_success);
 /* Diagnostics of the last run's first chain launch, one entry per group: the chain's
  * device wall-clock ticks (100 MHz) in bits 0-31, the number of single-pod steps (pods
@@ -468,8 +470,8 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
  * kernel's cycles in wave 0's walk and [7] walk cycles per pod (both CASIM_PROF builds only, else 0),
  * [8] path (1: feasibility-bitmap walk, 0: window sequencer), [9] resource shapes and [10] static
  * classes of the bitmap walk, [11..13] the bitmap walk's cycles per pod in its head (attributes,
- * hint), find (similar-pods check, scan) and place sections (CASIM_PROF builds), [14] its row-cache
- * entries and [15] 1 when its static words sit in LDS; returns 16. */
+ * hints), run (scan) and place sections (CASIM_PROF builds), [14] 0 (reserved) and [15] 1 when
+ * its static words sit in LDS; returns 16. */
 int ca_filter_stats(const ca_mirror* m, float* out, int32_t cap);
 
 /* ---- scale-down eligibility ----------------------------
@@ -536,6 +538,56 @@ int ca_util_table_destroy(ca_util_table* t);
 int ca_util_calculate(ca_util_table* t, int32_t skip_daemonset_pods, int32_t skip_mirror_pods,
                       int64_t now_ns, ca_util_info* out, float* kernel_ms);
 int ca_util_device_results(const ca_util_table* t, const ca_util_info** out);
+
+/* ---- multi-GPU ---------------------------------------------
+ * One mirror per device (ca_mirror_create(device)), kept identical by the caller: every
+ * snapshot change (add/remove nodes and pods, fork/revert/commit, hints) is applied to
+ * each, in the same order, so node positions and pod ids agree.  The batch calls below
+ * split their units into contiguous blocks, one per mirror (balanced by pods), run the
+ * blocks concurrently from the caller's lastIndex, and fix up the lastIndex chain in the
+ * library: a block that ran from a wrong lastIndex is re-run from the exact one when its
+ * output depends on it, otherwise its lastIndex fields are re-based.  The
+ * results are those of the single-mirror calls, bit for bit.  Replaces the Go caller's
+ * loop over node groups (orchestrator.go:139-178 → Estimate per group) and the candidate
+ * loop of FindNodesToRemove (cluster.go:130-137) when they are spread over GPUs. */
+typedef struct ca_multi ca_multi;
+int ca_multi_create(ca_mirror* const* mirrors, int32_t n, ca_multi** out);
+int ca_multi_destroy(ca_multi* mm);   /* the mirrors stay the caller's */
+
+/* Estimate batch (ca_estimate_batch semantics, prefix protocol included) over the mirrors'
+ * blocks of node groups.  sched_pod is required (host memory; page-locked memory from
+ * ca_host_alloc lets each block publish zero-copy); sched_node may be NULL. */
+typedef struct ca_multi_estimate_plan ca_multi_estimate_plan;
+int ca_multi_estimate_plan_create(ca_multi* mm, const ca_pod_table* t, const int32_t* group_off,
+                                  const int32_t* pod_idx, const ca_template* templates, int32_t n_groups,
+                                  ca_multi_estimate_plan** out);
+int ca_multi_estimate_plan_run(ca_multi_estimate_plan* p, const ca_limiter* limiter, int32_t* last_index,
+                               ca_estimate_result* results, int32_t* sched_pod, int32_t* sched_node);
+/* blocks, re-runs of the last run, and the first group of each block (n_blocks + 1 values) */
+int ca_multi_estimate_plan_stats(const ca_multi_estimate_plan* p, int32_t* n_blocks, int32_t* reruns,
+                                 int32_t* block_first_group, int32_t cap);
+int ca_multi_estimate_plan_destroy(ca_multi_estimate_plan* p);
+int ca_multi_estimate_batch(ca_multi* mm, const ca_pod_table* t, const int32_t* group_off, const int32_t* pod_idx,
+                            const ca_template* templates, int32_t n_groups, const ca_limiter* limiter,
+                            int32_t* last_index, ca_estimate_result* results, int32_t* sched_pod,
+                            int32_t* sched_node);
+
+/* FindNodesToRemove (ca_find_nodes_to_remove semantics, prefix protocol included) over the
+ * mirrors' blocks of candidates.  hints[n_pods] per mirror pod (or NULL: none), updated in
+ * place; n_pods must equal every mirror's pod count.  out_dest may be NULL. */
+typedef struct ca_multi_removal_plan ca_multi_removal_plan;
+int ca_multi_removal_plan_create(ca_multi* mm, const int32_t* candidates, int32_t n_candidates,
+                                 const uint8_t* dest_mask, const int32_t* cand_status, const int32_t* move_off,
+                                 const int32_t* move_pods, ca_multi_removal_plan** out);
+int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t n_pods, int32_t* last_index,
+                              ca_removal_result* results, int32_t* out_dest);
+int ca_multi_removal_plan_stats(const ca_multi_removal_plan* p, int32_t* n_blocks, int32_t* reruns,
+                                int32_t* block_first_candidate, int32_t cap);
+int ca_multi_removal_plan_destroy(ca_multi_removal_plan* p);
+int ca_multi_find_nodes_to_remove(ca_multi* mm, const int32_t* candidates, int32_t n_candidates,
+                                  const uint8_t* dest_mask, const int32_t* cand_status, const int32_t* move_off,
+                                  const int32_t* move_pods, int32_t* hints, int32_t n_pods, int32_t* last_index,
+                                  ca_removal_result* results, int32_t* out_dest);
 
 #ifdef __cplusplus
 }

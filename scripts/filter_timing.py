@@ -42,7 +42,7 @@ for name in names:
     print(f"{name:12s} parity={ok} placed={rg.placed}/{len(w.order)} evals={rg.evals} call_ms={np.median(ts):.2f} "
           f"kernel_ms={np.median(ks):.2f} steps={st['block_steps']} rings={st['ring_scans']} "
           f"windows={st['windows']} seq_share={st['seq_share']:.2f} walk_cyc/pod={st['walk_cycles_per_pod']:.0f} "
-          f"path={st['path']} S={st['shapes']} K={st['static_classes']} E={st['row_cache']} "
+          f"path={st['path']} S={st['shapes']} K={st['static_classes']} "
           f"statlds={st['static_in_lds']} fbcyc={[round(x) for x in st['fb_cycles_per_pod']]} cpu_ms={cpu:.1f} "
           f"x{cpu / np.median(ts):.1f}", flush=True)
     g.close()

@@ -2,8 +2,9 @@
  * abi_driver.c — a C caller of libcasim.so through include/casim.h only (what a cgo shim
  * compiles against): mirror -> FitsAnyNode / CheckPredicates -> Estimate (BASELINE C1:
  * 1000 pods of 500m / 1 GiB on a 4000m / 16 GiB / 110-pod template = 125 nodes,
- * binpacking_estimator_test.go semantics) -> FindNodesToRemove (cluster_test.go:169-177
- * shape: a drainable node whose pods fit elsewhere) -> the kernel-scope prefix protocol.
+ * binpacking_estimator_test.go semantics) -> FindNodesToRemove (two drainable candidates
+ * whose pods fit elsewhere; destinations follow the rotating first fit) -> the kernel-scope prefix protocol ->
+ * the multi-GPU entry points over two replicas (device 1 when there is one, else 0).
  * Prints one "key value" line per check and exits non-zero on the first failure.
  */
 #include <stdio.h>
@@ -102,8 +103,12 @@ int main(void) {
     CHECK(ca_find_nodes_to_remove(m, cand, 2, dest, st, moff, moves, hints, &li, rr, odest));
     printf("find_nodes_to_remove removable %d %d dest %d %d %d last_index %d\n", rr[0].removable, rr[1].removable,
            odest[0], odest[1], odest[2], li);
-    EXPECT(rr[0].removable == 1 && rr[1].removable == 1 && odest[0] == 0 && odest[1] == 0 && odest[2] == 0);
-    EXPECT(hints[ids[0]] == 0 && hints[ids[2]] == 0);          /* Hints.Set */
+    /* rotating first fit: p1 -> n1 (lastIndex 1), p2 skips n2 (the candidate) -> n3
+     * (lastIndex 3 = 0), n3's p3 -> n1 (lastIndex 1); the CPU restatement agrees */
+    EXPECT(rr[0].removable == 1 && rr[1].removable == 1 && odest[0] == 0 && odest[1] == 2 && odest[2] == 0);
+    EXPECT(li == 1 && rr[1].last_index_in == 0);
+    EXPECT(hints[ids[0]] == 0 && hints[ids[1]] == 2 && hints[ids[2]] == 0);          /* Hints.Set */
+    const int32_t li_sweep = li;
 
     /* Estimate, BASELINE C1 */
     ca_pod_spec* pods = malloc(sizeof(ca_pod_spec) * 1000);
@@ -136,6 +141,43 @@ int main(void) {
     CHECK(ca_estimate_batch(m, ps2, goff2, pidx, t2, 2, &lim, &li, er2, sched, NULL));
     printf("prefix status %d %d\n", er2[0].status, er2[1].status);
     EXPECT(er2[0].status == CA_OK && er2[1].status == CA_EUNSUPPORTED);
+
+    /* multi-GPU entry: a replica of the cluster (same calls, same order) on a second mirror
+     * (device ndev > 1 ? 1 : 0), the C1 batch split into 4 groups of 250 pods over the two
+     * replicas, results equal the single-mirror batch of the same groups */
+    pods[999].flags &= ~CA_POD_OUT_OF_SCOPE;
+    ca_mirror* m2 = NULL;
+    CHECK(ca_mirror_create(ndev > 1 ? 1 : 0, &m2));
+    CHECK(ca_mirror_add_nodes(m2, nodes, 3, &first));
+    int32_t ids2[3];
+    CHECK(ca_mirror_add_pods(m2, &rt, idx, pos, 3, ids2));
+    ca_mirror* reps[2] = {m, m2};
+    ca_multi* mm = NULL;
+    CHECK(ca_multi_create(reps, 2, &mm));
+    int32_t goff4[5] = {0, 250, 500, 750, 1000};
+    ca_template t4[4] = {tmpl, tmpl, tmpl, tmpl};
+    ca_estimate_result e1[4], e2[4];
+    int32_t* sched2 = malloc(sizeof(int32_t) * 1000);
+    ca_podset* ps3 = NULL;
+    CHECK(ca_podset_create(m, &pt, &ps3));
+    int32_t l1 = 3, l2 = 3;
+    CHECK(ca_estimate_batch(m, ps3, goff4, pidx, t4, 4, &lim, &l1, e1, sched, NULL));
+    CHECK(ca_multi_estimate_batch(mm, &pt, goff4, pidx, t4, 4, &lim, &l2, e2, sched2, NULL));
+    printf("multi estimate node_count %d %d %d %d last_index %d\n", e2[0].node_count, e2[1].node_count,
+           e2[2].node_count, e2[3].node_count, l2);
+    EXPECT(l1 == l2 && memcmp(e1, e2, sizeof e1) == 0 && memcmp(sched, sched2, sizeof(int32_t) * 1000) == 0);
+    int32_t hints2[3] = {-1, -1, -1};
+    ca_removal_result rr2[2];
+    int32_t odest2[3];
+    l2 = 0;
+    CHECK(ca_multi_find_nodes_to_remove(mm, cand, 2, dest, st, moff, moves, hints2, 3, &l2, rr2, odest2));
+    printf("multi find_nodes_to_remove removable %d %d last_index %d\n", rr2[0].removable, rr2[1].removable, l2);
+    EXPECT(memcmp(rr, rr2, sizeof rr) == 0 && memcmp(odest, odest2, sizeof odest) == 0 && l2 == li_sweep);
+    EXPECT(memcmp(hints, hints2, sizeof hints) == 0);
+    CHECK(ca_multi_destroy(mm));
+    CHECK(ca_podset_destroy(ps3));
+    CHECK(ca_mirror_destroy(m2));
+    free(sched2);
 
     /* RemoveNode shifts positions; Revert restores them */
     CHECK(ca_mirror_fork(m));

@@ -1,0 +1,136 @@
+"""Multi-device entry points of the C ABI (multi.hip, casim.h "multi-GPU"): node groups /
+sweep candidates in contiguous blocks over replicated mirrors, run concurrently from the
+caller's lastIndex, chain fixed up inside the library.  The box has one GPU, so the
+replicas are several mirrors on device 0 — the blocks, threads, re-runs and re-basing are
+the same code as on 8 GPUs.  Results must equal one mirror's call and the oracle, bit for
+bit (the blocks are coupled only through lastIndex)."""
+import dataclasses
+
+import numpy as np
+import pytest
+
+from autoscaler_amd import native
+from autoscaler_amd import workloads as W
+from estgen import _encode_estimate, _estimate_inputs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    import pyoracle
+    pyoracle.build()
+    return pyoracle
+
+
+def _replicas(n, load):
+    ms = [native.Mirror(0) for _ in range(n)]
+    for m in ms:
+        load(m)
+    return ms
+
+
+def _eq_estimate(ro, g, off):
+    assert np.array_equal(ro.results, g.results)
+    assert ro.last_index == g.last_index
+    for k in range(len(off) - 1):
+        if int(ro.results[k]["status"]) != 0:
+            continue
+        a, n = off[k], int(ro.results[k]["n_scheduled"])
+        assert np.array_equal(ro.sched_pod[a:a + n], g.sched_pod[a:a + n]), k
+        assert np.array_equal(ro.sched_node[a:a + n], g.sched_node[a:a + n]), k
+
+
+@pytest.mark.parametrize("replicas", [2, 3, 5])
+@pytest.mark.parametrize("seed", range(6))
+def test_multi_estimate_random(seed, replicas, oracle):
+    """Random clusters (existing nodes, ports, taints, scalars): the blocks' lastIndex
+    dependence varies, so re-runs and re-basing both occur across the seeds."""
+    rng, nodes, pods, templates, groups = _estimate_inputs(seed, n_groups=9, n_pods=70)
+    table, node_recs, tm, off, pod_idx = _encode_estimate(nodes, pods, templates, groups)
+    max_nodes = [0, 1, 3, 40][seed % 4]
+    L0 = [0, 3, 11][seed % 3]
+    o = oracle.OracleState()
+    o.clear()
+    if len(node_recs):
+        o.add_nodes(node_recs)
+    ro = o.estimate(table, off, pod_idx, tm, max_nodes, L0)
+
+    def load(m):
+        if len(node_recs):
+            m.add_nodes(node_recs)
+    ms = _replicas(replicas, load)
+    with native.Multi(ms) as mm, native.MultiEstimatePlan(mm, table, off, pod_idx, tm) as plan:
+        for _ in range(2):
+            g = plan.run(max_nodes, L0)
+            _eq_estimate(ro, g, off)
+        st = plan.stats()
+        assert st["blocks"] == min(replicas, len(tm))
+    for m in ms:
+        m.close()
+
+
+def test_multi_estimate_c2(oracle):
+    """C2-shaped batch over 4 replicas vs one mirror (the bench's strong-scaling split)."""
+    w = W.c2(n_pods=12000, n_groups=24, n_existing=200)
+    single = native.Mirror(0)
+    W.load_estimate(single, w)
+    ref = single.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, 5)
+    ms = _replicas(4, lambda m: W.load_estimate(m, w))
+    with native.Multi(ms) as mm, native.MultiEstimatePlan(mm, w.table, w.group_off, w.pod_idx, w.templates) as plan:
+        g = plan.run(w.max_nodes, 5)
+        _eq_estimate(ref, g, w.group_off)
+        assert plan.stats()["blocks"] == 4
+    for m in ms + [single]:
+        m.close()
+
+
+@pytest.mark.parametrize("replicas", [2, 4])
+@pytest.mark.parametrize("n_nodes", [300, 1500])
+def test_multi_sweep(n_nodes, replicas, oracle):
+    """C3 sweep with fresh hints (every candidate's scans succeed: every block depends on
+    its input lastIndex, so blocks after the first re-run), then the second loop with the
+    first loop's hints (hint placements: blocks pass lastIndex through)."""
+    w = W.c3(n_nodes=n_nodes)
+    args = (w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods)
+    o = oracle.OracleState()
+    W.load_sweep(o, w)
+    o1 = o.find_nodes_to_remove(*args, np.full(len(w.table), -1, np.int32), 7)
+    o2 = o.find_nodes_to_remove(*args, o1.hints, o1.last_index)
+    ms = _replicas(replicas, lambda m: W.load_sweep(m, w))
+    with native.Multi(ms) as mm, native.MultiRemovalPlan(mm, *args) as plan:
+        g1 = plan.run(np.full(len(w.table), -1, np.int32), 7)
+        assert np.array_equal(o1.results, g1.results) and o1.last_index == g1.last_index
+        assert np.array_equal(o1.dest, g1.dest) and np.array_equal(o1.hints, g1.hints)
+        s1 = plan.stats()
+        assert s1["blocks"] == replicas and s1["reruns"] >= 1
+        g2 = plan.run(g1.hints, g1.last_index)
+        assert np.array_equal(o2.results, g2.results) and o2.last_index == g2.last_index
+        assert np.array_equal(o2.dest, g2.dest) and np.array_equal(o2.hints, g2.hints)
+    for m in ms:
+        m.close()
+
+
+def test_multi_sweep_prefix_protocol(oracle):
+    """An out-of-scope pod to move in a middle block: that candidate reports
+    OUT_OF_SCOPE, every later candidate (later blocks included) NOT_RUN."""
+    from autoscaler_amd import abi
+    w = W.c3(n_nodes=300)
+    table = w.table
+    pods = table.pods.copy()
+    c_mid = len(w.candidates) * 2 // 3
+    victim = int(w.move_pods[w.move_off[c_mid]])
+    pods["flags"][victim] |= abi.CA_POD_OUT_OF_SCOPE
+    w2 = dataclasses.replace(w, table=abi.PodTable(pods))
+    args = (w2.candidates, w2.dest_mask, w2.cand_status, w2.move_off, w2.move_pods)
+    single = native.Mirror(0)
+    W.load_sweep(single, w2)
+    ref = single.find_nodes_to_remove(*args, np.full(len(w2.table), -1, np.int32), 0)
+    ms = _replicas(3, lambda m: W.load_sweep(m, w2))
+    with native.Multi(ms) as mm, native.MultiRemovalPlan(mm, *args) as plan:
+        g = plan.run(np.full(len(w2.table), -1, np.int32), 0)
+    assert np.array_equal(ref.results, g.results) and ref.last_index == g.last_index
+    assert int(g.results[c_mid]["reason"]) == abi.CA_UNREMOVABLE_OUT_OF_SCOPE
+    assert (g.results["reason"][c_mid + 1:] == abi.CA_UNREMOVABLE_NOT_RUN).all()
+    for m in ms + [single]:
+        m.close()

@@ -392,6 +392,34 @@ def test_estimate_plan_publish_random(seed, chunk, oracle, monkeypatch):
     assert ro.last_index == g.last_index == d.last_index
 
 
+@pytest.mark.parametrize("serial", [False, True], ids=["concurrent", "serialised"])
+def test_estimate_publisher_bounded(serial, oracle, monkeypatch):
+    """HIP does not promise that k_publish and the chains overlap.  With the two kernels
+    serialised (CASIM_PUB_SERIAL: the publisher first, on the chains' stream) the publisher
+    gives up at its start deadline and the stream-ordered copy delivers the results: same
+    answers, latency bounded by the deadline (not the 200 ms dead-chain guard)."""
+    import time
+    if serial:
+        monkeypatch.setenv("CASIM_PUB_SERIAL", "1")
+    w = W.c2(n_pods=8000, n_groups=20, n_existing=50)
+    o = oracle.OracleState()
+    W.load_estimate(o, w)
+    ro = o.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, 0)
+    m = _mirror()
+    W.load_estimate(m, w)
+    with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as plan:
+        walls = []
+        for _ in range(3):
+            t = time.perf_counter()
+            p = plan.run(w.max_nodes, 0, want_nodes=False)
+            walls.append(time.perf_counter() - t)
+            assert np.array_equal(ro.results, p.results)
+            assert np.array_equal(ro.sched_pod, p.sched_pod)
+            assert ro.last_index == p.last_index
+            assert plan.stats()["results_path"] == ("publisher_gave_up" if serial else "published")
+    assert min(walls) < 0.05, walls          # 2 ms start deadline + the copy, never 200 ms
+
+
 @pytest.mark.parametrize("size", ["small", "full"])
 def test_estimate_c4_taints_affinity(size, oracle):
     """C4 (taint/toleration + node-affinity heavy): static filters on the templates, per

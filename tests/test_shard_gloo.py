@@ -132,3 +132,69 @@ def test_sharded_estimate_gloo_world2(seed, oracle_lib):
         assert p.exitcode == 0
     res.sort()
     assert all(ok for _, ok, _ in res), res
+
+
+def _sweep_worker(rank, world, port, n_nodes, q):
+    """FindNodesToRemove with the candidates in contiguous blocks (candidates
+    shard like node groups, cluster.go:130-137), one per rank, the lastIndex chain fixed up
+    by run_sharded; the CPU restatement runs each block (the protocol under test)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "oracle"), os.path.join(root, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    import pyoracle
+    from autoscaler_amd import shard
+    from autoscaler_amd import workloads as W
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w = W.c3(n_nodes=n_nodes)
+        C = len(w.candidates)
+        a, b = rank * C // world, (rank + 1) * C // world
+        off = w.move_off[a:b + 1] - w.move_off[a]
+        moves = w.move_pods[w.move_off[a]:w.move_off[b]]
+        hints0 = np.full(len(w.table), -1, np.int32)
+        o = pyoracle.OracleState()
+        W.load_sweep(o, w)
+        L0 = 11
+
+        def run(lin):
+            out = o.find_nodes_to_remove(w.candidates[a:b], w.dest_mask, w.cand_status[a:b], off, moves,
+                                         hints0.copy(), lin)
+            # a block whose scans all failed passes lastIndex through; count it sensitive
+            # whenever it moved lastIndex (conservative: the protocol re-runs it)
+            moved = int(out.last_index != lin)
+            return out, out.last_index, 1, moved
+
+        out, final_L, reruns = shard.run_sharded(run, L0, shard.torch_all_gather(dist, "cpu"), rank)
+        ref = o.find_nodes_to_remove(w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods,
+                                     hints0.copy(), L0)
+        ok = np.array_equal(out.results, ref.results[a:b])
+        ok &= np.array_equal(out.dest, ref.dest[w.move_off[a]:w.move_off[b]])
+        ok &= np.array_equal(out.hints[moves], ref.hints[moves])
+        ok &= final_L == ref.last_index
+        q.put((rank, bool(ok), reruns))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_nodes", [120, 400])
+def test_sharded_sweep_gloo_world2(n_nodes, oracle_lib):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sweep_worker, args=(r, 2, port, n_nodes, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    assert all(ok for _, ok, _ in res), res
+    assert res[1][2] >= 1                       # rank 1 re-ran from rank 0's lastIndex

@@ -6,17 +6,16 @@ group of a scale-up (CA/core/scaleup/orchestrator/orchestrator.go:139-178), i.e.
 C2 workload of SURVEY.md §8d: 50k heterogeneous pending pods x 100 node-group
 templates, resource-fit only, maxNodes = 1000 (the --max-nodes-per-scaleup
 default), 1000 existing nodes, inputs resident in HBM.  The step runs the device
-sort, the per-group First-Fit-Decreasing chains and the lastIndex fix-up, and leaves
-what Estimate returns (estimator.go:40-42) — the node count and the scheduled pods in
-placement order — in HBM, as the inputs were (task contract: inputs resident, the
-PCIe-inclusive rate is reported beside `value`, never as it).  extra.pcie_inclusive
-times the same step with every group's scheduled pods streamed into page-locked host
-memory by the concurrent publisher (18.6 MB per C2 batch).
+sort, the per-group First-Fit-Decreasing chains and the lastIndex fix-up, and returns
+what Estimate returns (estimator.go:40-42) — every group's node count and scheduled
+pods in placement order — on the host (§8d: Estimate latency = results on the host;
+the zero-copy publisher streams them into page-locked memory while the chains run).
+extra.device_resident times the same step with the scheduled pods left in HBM.
 
 value = filter-chain evaluations the reference algorithm performs in that batch
-(every RunFilterPlugins call, counted exactly) / wall time.  With --gpus N each
-rank runs its own batch of 100 groups (weak scaling: N x 100 groups); the ranks'
-batches are chained through the checker's lastIndex with one RCCL all_gather of a
+(every RunFilterPlugins call, counted exactly) / wall time.  With --gpus N the same
+100 groups are split into N contiguous blocks, one per rank (strong scaling), and the
+blocks are chained through the checker's lastIndex with one RCCL all_gather of a
 4-int record per rank per step.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -76,6 +75,7 @@ def parse():
     ap.add_argument("--no-expansion", action="store_true", help="skip the expansion-option feasibility leg (N=1)")
     ap.add_argument("--no-util", action="store_true", help="skip the scale-down eligibility leg (N=1)")
     ap.add_argument("--no-filter", action="store_true", help="skip the FilterOutSchedulable leg (N=1)")
+    ap.add_argument("--no-unlimited", action="store_true", help="skip the C2 max_nodes=0 leg (N=1)")
     ap.add_argument("--sweep-nodes", type=int, default=5000)
     return ap.parse_args()
 
@@ -337,6 +337,78 @@ def sweep_leg(args, device: int, with_cpu: bool) -> dict:
     return out
 
 
+def split_groups(group_off, world: int) -> list:
+    """Contiguous blocks of node groups, one per rank, balanced by (pod, group) items (the
+    same split as ca_multi_estimate_plan, multi.hip:split_blocks)."""
+    G = len(group_off) - 1
+    w = np.maximum(np.diff(group_off), 1).astype(np.int64)
+    tot, acc, b = int(w.sum()), 0, [0]
+    D = max(1, min(world, G))
+    for i in range(G):
+        acc += int(w[i])
+        k = len(b)
+        if k < D and i + 1 < G and G - (i + 1) >= D - k and acc * D >= tot * k:
+            b.append(i + 1)
+    b.append(G)
+    while len(b) < world + 1:                 # more ranks than groups: empty blocks at the end
+        b.append(G)
+    return b
+
+
+def c2_unlimited_leg(args, device: int, with_cpu: bool) -> dict:
+    """C2 with an unlimited limiter (maxNodes = 0, threshold_based_limiter.go:49-52; the
+    BASELINE C2 row's second setting): new-node rows in per-group HBM slabs
+    (k_ffd_chain<GROWS>), results to the host.  Parity against the committed oracle result
+    (tests/golden/c2_unlimited.json: per-group fields and a CRC-32 of each scheduled list)."""
+    import zlib
+    from autoscaler_amd import native
+    from autoscaler_amd import workloads as W
+    w = W.c2()
+    m = native.Mirror(device)
+    W.load_estimate(m, w)
+    out = {"workload": "C2 (50k pods x 100 groups, 1000 existing nodes), max_nodes = 0 (unlimited)"}
+    with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as plan:
+        plan.run(0, 0, want_nodes=False, copy=False)
+        ts = []
+        for _ in range(max(3, min(args.steps, 5))):
+            t = time.perf_counter()
+            r = plan.run(0, 0, want_nodes=False, copy=False)
+            ts.append(time.perf_counter() - t)
+        ms = float(np.median(ts) * 1e3)
+        evals = int(r.results["evals"].sum())
+        out.update({"ms_per_step": ms, "evals": evals, "evals_per_s": evals / (ms / 1e3),
+                    "chain_kernel_ms": plan.stats()["phases"]["chain_ms"]})
+        gf = os.path.join(ROOT, "tests", "golden", "c2_unlimited.json")
+        if os.path.exists(gf):
+            with open(gf) as f:
+                gold = json.load(f)
+            ok = gold["last_index"] == r.last_index
+            for g, rec in enumerate(gold["groups"]):
+                res = r.results[g]
+                ok &= all(int(res[k]) == rec[k] for k in ("node_count", "n_scheduled", "nodes_added", "last_index_in",
+                                                          "last_index_out", "status", "evals"))
+                a, n = int(w.group_off[g]), int(res["n_scheduled"])
+                ok &= zlib.crc32(np.ascontiguousarray(r.sched_pod[a:a + n], np.int32).tobytes()) == rec["sched_crc32"]
+            out["parity_vs_golden"] = bool(ok)
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle                                           # CPU baseline leg only
+        o = pyoracle.OracleState()
+        W.load_estimate(o, w)
+        g = 3                                                     # bounded sample: the first groups
+        off = w.group_off[: g + 1]
+        t = time.perf_counter()
+        ro = o.estimate(w.table, off, w.pod_idx[: off[-1]], w.templates[:g], 0, 0)
+        cpu_s = time.perf_counter() - t
+        cev = int(ro.results["evals"].sum())
+        out["cpu_baseline"] = {"value": cev / cpu_s, "unit": "evals/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle/casim_oracle.c Estimate of the first {g} unlimited C2 groups "
+                                         f"({cev} evals in {cpu_s:.2f} s), 1 thread of {cpu_model()}"}
+        out["speedup_evals_per_s"] = out["evals_per_s"] / (cev / cpu_s)
+    m.close()
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -357,54 +429,78 @@ def main():
     from autoscaler_amd import native, shard
     from autoscaler_amd import workloads as W
 
-    # rank r owns node groups [100 r, 100 r + 100) of the job (seeded per rank)
-    w = W.c2(n_pods=args.pods, n_groups=args.groups, n_existing=args.existing, max_nodes=args.max_nodes,
-             seed=42 + rank)
+    # strong scaling: every rank holds the same cluster (the mirror is replicated) and runs
+    # its contiguous block of the same node groups; the blocks are chained through the
+    # checker's lastIndex (autoscaler_amd/shard.py)
+    w = W.c2(n_pods=args.pods, n_groups=args.groups, n_existing=args.existing, max_nodes=args.max_nodes, seed=42)
+    blocks = split_groups(w.group_off, world)
+    g0, g1 = blocks[rank], blocks[rank + 1]
+    off_blk = (w.group_off[g0:g1 + 1] - w.group_off[g0]).astype(np.int32)
+    idx_blk = w.pod_idx[w.group_off[g0]:w.group_off[g1]]
+    tm_blk = w.templates[g0:g1]
     mirror = native.Mirror(local)
     W.load_estimate(mirror, w)
-    plan = native.EstimatePlan(mirror, w.table, w.group_off, w.pod_idx, w.templates)
+    plan = native.EstimatePlan(mirror, w.table, off_blk, idx_blk, tm_blk)
     L0 = 0
+    items = int(w.group_off[-1])                                # (pod, group) items of the whole batch
+    items_blk = int(off_blk[-1])
 
-    def run_block(lin):
+    def run_block(lin, device_results=False):
+        """This rank's block: results to the caller's page-locked buffer (headline), or left
+        in HBM (extra.device_resident)."""
+        if g1 == g0:
+            return None, lin, 0, 0
         if args.with_nodes:
             out = plan.run(w.max_nodes, lin, want_nodes=True, copy=False)
-        else:
+        elif device_results:
             out = plan.run(w.max_nodes, lin, copy=False, device_results=True)
+        else:
+            out = plan.run(w.max_nodes, lin, want_nodes=False, copy=False)
         sens, succ = plan.chain_info()
         return out, out.last_index, sens, succ
 
     coll_dev = f"cuda:{local}" if backend == "nccl" else "cpu"
     gather = shard.torch_all_gather(dist, coll_dev) if dist is not None else None
 
-    def step():
-        """One batch on this rank + the lastIndex chain across ranks (autoscaler_amd/shard.py)."""
+    def step(device_results=False):
+        """One Estimate batch: this rank's block + the lastIndex chain across ranks."""
+        run = (lambda lin: run_block(lin, device_results))
         if dist is None:
-            out = run_block(L0)[0]
-            return out, 0
-        out, _, extra = shard.run_sharded(run_block, L0, gather, rank)
+            return run(L0)[0], 0
+        out, _, extra = shard.run_sharded(run, L0, gather, rank)
         return out, extra
 
-    for _ in range(args.warmup):
-        step()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    evals = 0
-    extras = []
-    for _ in range(args.steps):
-        out, extra = step()
-        evals += int(out.results["evals"].sum())
-        extras.append(extra)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    # per-phase device times: the same steps again, untimed (reading them is host work
-    # that is not part of Estimate)
-    chain_ms, sort_ms, rounds, phases = [], [], [], []
+    def timed(device_results):
+        for _ in range(args.warmup):
+            step(device_results)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        evals, extras, out = 0, [], None
+        for _ in range(args.steps):
+            out, extra = step(device_results)
+            evals += int(out.results["evals"].sum()) if out is not None else 0
+            extras.append(extra)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([el, float(evals)], dtype=torch.float64, device=coll_dev)
+            tmax, tsum = t.clone(), t.clone()
+            dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+            dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+            return float(tmax[0]), int(tsum[1]), evals, extras, out
+        return el, evals, evals, extras, out
+
+    # headline: results on the host (SURVEY §8d: Estimate latency = results on the host)
+    elapsed, total_evals, evals, extras, hout = timed(False)
+    host_pods = hout.sched_pod.copy() if hout is not None else None
+    # per-phase device times: the same steps again, untimed
+    chain_ms, sort_ms, rounds, phases, pub = [], [], [], [], []
     for i in range(args.steps):
-        step()
+        step(False)
         st = plan.stats()
         chain_ms.append(st["chain_ms"] / max(st["rounds"], 1))
         sort_ms.append(st["sort_ms"])
@@ -412,74 +508,31 @@ def main():
         ph = dict(st["phases"])
         ph["chain_ms"] = ph["chain_ms"] / max(st["rounds"], 1)       # one launch
         phases.append(ph)
-    if dist is not None:
-        t = torch.tensor([elapsed, float(evals)], dtype=torch.float64, device=coll_dev)
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t.clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed = float(tmax[0])
-        total_evals = int(tsum[1])
-    else:
-        total_evals = evals
-    evals_per_step = evals / args.steps                         # this rank's batch
-    items = int(w.group_off[-1])                                # (pod, group) items per batch
+        pub.append(st["results_path"])
+    # device-resident variant (results left in HBM): the previous round's headline
+    d_el, d_total, _, _, _ = timed(True)
+    same = bool(host_pods is None or np.array_equal(host_pods, plan.fetch()))
+    device_resident = {"ms_per_step": d_el / args.steps * 1e3, "evals_per_s": d_total / d_el,
+                       "results_identical_to_host_mode": same,
+                       "results": "scheduled pods left in HBM (ca_estimate_plan_run with sched_pod = NULL); "
+                                  "results[] and lastIndex on the host"}
     n_cls = len(set(zip(w.table.pods["score_milli_cpu"].tolist(), w.table.pods["score_memory"].tolist())))
     n_merge = 1 if n_cls <= 256 else 2                            # radix passes (8-bit digits)
-    ph_mean = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
-    # dominant kernel of the step (longest device phase), with its algorithmic bytes
-    dom = max(PHASE_BYTES, key=lambda k: ph_mean[k])
+    ph_mean = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]} if g1 > g0 else {}
+    dom = max(PHASE_BYTES, key=lambda k: ph_mean.get(k, 0.0))
     per_item = PHASE_BYTES[dom] * (n_merge if dom == "merge_ms" else 1)
-    kernel_ms = ph_mean[dom]
-    achieved = per_item * items / (kernel_ms / 1e3) / 1e9
+    kernel_ms = ph_mean.get(dom, 0.0)
+    achieved = per_item * items_blk / (kernel_ms / 1e3) / 1e9 if kernel_ms > 0 else 0.0
     traffic, traffic_src = None, None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")      # rocprofv3 --pmc passes (scripts/gpu_round.sh pmc)
-    if os.path.exists(tf):
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")      # rocprofv3 --pmc passes (scripts/pmc_step.py)
+    if os.path.exists(tf) and world == 1:
         with open(tf) as f:
             tj = json.load(f)
         for name in PHASE_KERNEL[dom].split("+")[:1]:
             rec = tj.get("kernels", {}).get(f"casim::{name}")
             if rec:
-                # the phase's launches of one step together (heavy + light chain launches)
                 traffic = rec.get("traffic_bytes_per_step", rec["traffic_bytes_per_launch"])
                 traffic_src = f"profiles/pmc_traffic.json ({tj.get('source', '')})"
-
-    # PCIe-inclusive: the same step with the scheduled pods streamed to the host
-    pcie = None
-    if not args.with_nodes:
-        def host_block(lin):
-            out = plan.run(w.max_nodes, lin, want_nodes=False, copy=False)
-            st = plan.stats()
-            return out, out.last_index, st["lin_sensitive"], st["had_success"]
-
-        def host_step():
-            if dist is None:
-                return host_block(L0)[0]
-            return shard.run_sharded(host_block, L0, gather, rank)[0]
-
-        for _ in range(args.warmup):
-            host_step()
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        h0 = time.perf_counter()
-        for _ in range(args.steps):
-            hout = host_step()
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        h_el = time.perf_counter() - h0
-        if dist is not None:
-            t = torch.tensor([h_el], dtype=torch.float64, device=coll_dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            h_el = float(t[0])
-        host_pods = hout.sched_pod.copy()
-        run_block(L0)                                    # device mode again: same pods in HBM?
-        pcie = {"ms_per_step": h_el / args.steps * 1e3, "evals_per_s": total_evals / h_el,
-                "bytes_to_host_per_step": 4 * items * world,
-                "results_identical_to_device_mode": bool(np.array_equal(host_pods, plan.fetch())),
-                "how": "zero-copy publisher kernel on a second stream writes each final chunk of 4096 "
-                       "scheduled pods into the caller's page-locked buffer while the chains run"}
 
     result = None
     if rank == 0:
@@ -509,16 +562,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic: seeded C2 generator (autoscaler_amd/workloads.py), 64-shape pod catalog",
             "config": {
                 "workload": "C2: heterogeneous pending pods x node-group templates, resource-fit only "
-                            "(BASELINE.json configs[1]); one step = Estimate() for every group",
-                "pods": args.pods, "groups_per_gpu": args.groups, "existing_nodes": args.existing,
+                            "(BASELINE.json configs[1]); one step = Estimate() for every group, every group's "
+                            "node count and scheduled pods on the host",
+                "pods": args.pods, "groups": args.groups, "existing_nodes": args.existing,
                 "max_nodes_per_scaleup": args.max_nodes,
-                "parallelism": f"groups sharded over {world} GPU(s), lastIndex chained by all_gather",
+                "parallelism": f"the {args.groups} groups in {world} contiguous block(s), one per GPU, "
+                               f"lastIndex chained by all_gather",
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -527,28 +582,34 @@ def main():
                 "traffic_source": traffic_src,
                 "kernel": PHASE_KERNEL[dom], "kernel_ms": kernel_ms,
                 "bytes_per_unit": per_item, "unit_of_work": "(pod, node group) item",
-                "units_per_launch": items,
+                "units_per_launch": items_blk,
             },
             "cpu_baseline": cpu,
             "extra": {
                 "estimate_latency_ms": ms,
-                "sort_ms": float(np.mean(sort_ms)),
+                "results_to_host": "zero-copy publisher kernel on a second stream writes each final chunk of 4096 "
+                                   "scheduled pods into the caller's page-locked buffer while the chains run "
+                                   f"({4 * items} B per step); results path per step: "
+                                   f"{sorted(set(pub)) if pub else None}",
+                "device_resident": device_resident,
+                "sort_ms": float(np.mean(sort_ms)) if sort_ms else None,
                 "phases_ms": ph_mean,
-                "chain_kernel_ms": ph_mean["chain_ms"],
-                "items_per_s": items * world * args.steps / elapsed,
-                "eval_equivalent_GBps": BYTES_PER_EVAL * evals_per_step / (ph_mean["chain_ms"] / 1e3) / 1e9,
-                "speculation_rounds": float(np.mean(rounds)),
+                "chain_kernel_ms": ph_mean.get("chain_ms"),
+                "items_per_s": items * args.steps / elapsed,
+                "eval_equivalent_GBps": (BYTES_PER_EVAL * (evals / args.steps) / (ph_mean["chain_ms"] / 1e3) / 1e9
+                                         if ph_mean.get("chain_ms") else None),
+                "speculation_rounds": float(np.mean(rounds)) if rounds else None,
                 "evals_per_step": total_evals / args.steps,
+                "rank0_groups": [g0, g1],
                 "speedup_vs_cpu_baseline": (total_evals / elapsed) / cpu["value"] if cpu else None,
-                "results": "scheduled pods left in HBM (ca_estimate_plan_run with sched_pod = NULL); "
-                           "results[] and lastIndex on the host",
-                "pcie_inclusive": pcie,
             },
         }
         if world == 1 and not args.no_sweep:
             result["extra"]["sweep"] = sweep_leg(args, local, not args.no_cpu_baseline)
         if world == 1 and not args.no_c4:
             result["extra"]["c4"] = c4_leg(args, local, not args.no_cpu_baseline)
+        if world == 1 and not args.no_unlimited:
+            result["extra"]["c2_unlimited"] = c2_unlimited_leg(args, local, not args.no_cpu_baseline)
         if world == 1 and not args.no_expansion:
             result["extra"]["expansion"] = expansion_leg(args, local, not args.no_cpu_baseline)
         if world == 1 and not args.no_filter:

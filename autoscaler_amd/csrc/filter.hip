@@ -665,6 +665,7 @@ __global__ void __launch_bounds__(SQ_T) k_filter_out(FoArgs a) {
 // a global store inside the batch would make every later load wait for it.
 // ===========================================================================================
 constexpr int FB_MAX_SHAPES = 64;        // one lane per shape for the bit updates
+constexpr int FB_COLLECT_SHAPES = 1024;  // distinct shapes looked at before the dead ones are merged
 constexpr int FB_T = 64;                 // the walk is one wavefront
 constexpr size_t FB_LDS_MAX = 160 * 1024;
 
@@ -724,7 +725,7 @@ __host__ __device__ inline FbLds fb_lds(int32_t S, int32_t NW, int32_t K, int32_
 }
 
 // shape s fits the free resources (cpu, mem, eph, pods): dev_fit_reasons without scalars
-__device__ inline bool fb_fit(const FbShape& sh, int64_t cpu, int64_t mem, int64_t eph, int32_t pods) {
+__host__ __device__ inline bool fb_fit(const FbShape& sh, int64_t cpu, int64_t mem, int64_t eph, int32_t pods) {
     if (pods < 1) return false;                                           // fit.go:256-265
     if (sh.flags & PF_ALL_ZERO) return true;                             // :267-272
     return sh.cpu <= cpu && sh.mem <= mem && sh.eph <= eph;              // :274-300
@@ -1182,7 +1183,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
             sk.push_back((f & PF_ALL_ZERO) ? 1 : 0);
             auto it = shape_id.find(sk);
             if (it == shape_id.end()) {
-                if ((int32_t)shape_id.size() >= FB_MAX_SHAPES) { fb = false; break; }
+                if ((int32_t)shape_id.size() >= FB_COLLECT_SHAPES) { fb = false; break; }
                 it = shape_id.emplace(sk, (int32_t)shape_id.size()).first;
                 FbShape sh;
                 sh.cpu = ps.req_milli_cpu; sh.mem = ps.req_memory; sh.eph = ps.req_ephemeral;
@@ -1217,6 +1218,44 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
             fp.scls = cid;
             fp.simcls = ps.similar_class;
             fp.flags = f;
+        }
+        // Shapes that fit no node now never fit during the call (placements only take
+        // resources away): their pods share one shape with an all-zero dyn row (requests no
+        // node has), so only the live shapes count against the 64 lanes of the bit updates.
+        if (fb) {
+            const int32_t S0 = (int32_t)fb_shapes.size();
+            std::vector<uint8_t> alive((size_t)S0, 0);
+            std::vector<int32_t> open;
+            for (int32_t q = 0; q < S0; q++) open.push_back(q);
+            for (size_t i = 0; i < m->nodes.size() && !open.empty(); i++) {
+                NodeHot h;
+                m->fill_hot((int32_t)i, h);
+                for (size_t q = 0; q < open.size();) {
+                    if (fb_fit(fb_shapes[open[q]], h.cpu, h.mem, h.eph, h.pods)) {
+                        alive[open[q]] = 1;
+                        open[q] = open.back();
+                        open.pop_back();
+                    } else {
+                        q++;
+                    }
+                }
+            }
+            if (!open.empty()) {
+                std::vector<int32_t> remap((size_t)S0, -1);
+                std::vector<FbShape> live;
+                for (int32_t q = 0; q < S0; q++)
+                    if (alive[q]) { remap[q] = (int32_t)live.size(); live.push_back(fb_shapes[q]); }
+                FbShape none;
+                none.cpu = none.mem = none.eph = INT64_MAX;
+                none.flags = 0; none.pad = 0;
+                const int32_t dead = (int32_t)live.size();
+                live.push_back(none);
+                for (FbPod& fp : fb_pods) fp.shape = alive[fp.shape] ? remap[fp.shape] : dead;
+                fb_shapes.swap(live);
+            }
+            // the live shapes take the bit-update lanes; the dead row (last) needs none
+            const int32_t live = (int32_t)fb_shapes.size() - (open.empty() ? 0 : 1);
+            if (live > FB_MAX_SHAPES) fb = false;
         }
         // LDS: shapes, bitmaps, vis prefix counts, run scratch and the similar-pods state,
         // plus the static words when they fit too

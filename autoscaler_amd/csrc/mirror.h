@@ -38,6 +38,10 @@ struct DevPodTable {
     int32_t n_pods = 0, n_terms = 0, n_reqs = 0, n_names = 0;
     int upload(const ca_pod_spec* pods, int32_t n, const ca_selector_term* terms, int32_t nt,
                const ca_selector_req* reqs, int32_t nr, const int32_t* names, int32_t nn, hipStream_t st);
+    // append pods [n_pods, n_pods + k) and the selector tables' new tails (the mirror's
+    // tables only grow between Clear()s), keeping what is on the device
+    int append(const ca_pod_spec* new_pods, int32_t k, const ca_selector_term* terms, int32_t nt,
+               const ca_selector_req* reqs, int32_t nr, const int32_t* names, int32_t nn, hipStream_t st);
 };
 
 // Per-mirror scratch of ca_find_nodes_to_remove, kept across calls (no per-call
@@ -60,8 +64,8 @@ struct FilterScratch {
     HostBuf h_fb;
     int32_t path = 0;              // last call: 1 bitmap walk, 0 window sequencer
     int32_t fb_shapes = 0, fb_classes = 0;
-    float fb_cyc_per_pod[3] = {0, 0, 0};
-    int32_t fb_stat_lds = 0;                // bitmap walk: static words in LDS   // CASIM_PROF builds: bitmap walk cycles per pod (head, find, place)
+    float fb_cyc_per_pod[3] = {0, 0, 0};   // CASIM_PROF builds: bitmap walk cycles per pod (head, run, place)
+    int32_t fb_stat_lds = 0;                // bitmap walk: static words in LDS
 };
 
 // Dirty-row staging of sync_nodes: one H2D copy + a scatter kernel.

@@ -92,6 +92,41 @@ int DevPodTable::upload(const ca_pod_spec* pods, int32_t n, const ca_selector_te
     return CA_OK;
 }
 
+int DevPodTable::append(const ca_pod_spec* np, int32_t k, const ca_selector_term* tms, int32_t nt,
+                        const ca_selector_req* rqs, int32_t nr, const int32_t* nms, int32_t nn, hipStream_t st) {
+    const int32_t n0 = n_pods, n = n_pods + k;
+    std::vector<PodHot> h((size_t)std::max(k, 0));
+    for (int32_t i = 0; i < k; i++) {
+        h[i].cpu = np[i].req_milli_cpu;
+        h[i].mem = np[i].req_memory;
+        h[i].eph = np[i].req_ephemeral;
+        h[i].flags = pod_dev_flags(np[i]);
+        h[i].spec = n0 + i;
+    }
+    int rc;
+    if ((rc = hot.reserve_keep(sizeof(PodHot) * (size_t)(n + 1), st)) != CA_OK) return rc;
+    if ((rc = spec.reserve_keep(sizeof(ca_pod_spec) * (size_t)(n + 1), st)) != CA_OK) return rc;
+    if ((rc = terms.reserve_keep(sizeof(ca_selector_term) * (size_t)(nt + 1), st)) != CA_OK) return rc;
+    if ((rc = reqs.reserve_keep(sizeof(ca_selector_req) * (size_t)(nr + 1), st)) != CA_OK) return rc;
+    if ((rc = names.reserve_keep(sizeof(int32_t) * (size_t)(nn + 1), st)) != CA_OK) return rc;
+    if (k > 0) {
+        CA_HIP_CHECK(hipMemcpyAsync(hot.as<PodHot>() + n0, h.data(), sizeof(PodHot) * k, hipMemcpyHostToDevice, st));
+        CA_HIP_CHECK(hipMemcpyAsync(spec.as<ca_pod_spec>() + n0, np, sizeof(ca_pod_spec) * k, hipMemcpyHostToDevice, st));
+    }
+    if (nt > n_terms)
+        CA_HIP_CHECK(hipMemcpyAsync(terms.as<ca_selector_term>() + n_terms, tms + n_terms,
+                                    sizeof(ca_selector_term) * (nt - n_terms), hipMemcpyHostToDevice, st));
+    if (nr > n_reqs)
+        CA_HIP_CHECK(hipMemcpyAsync(reqs.as<ca_selector_req>() + n_reqs, rqs + n_reqs,
+                                    sizeof(ca_selector_req) * (nr - n_reqs), hipMemcpyHostToDevice, st));
+    if (nn > n_names)
+        CA_HIP_CHECK(hipMemcpyAsync(names.as<int32_t>() + n_names, nms + n_names, sizeof(int32_t) * (nn - n_names),
+                                    hipMemcpyHostToDevice, st));
+    CA_HIP_CHECK(hipStreamSynchronize(st));
+    n_pods = n; n_terms = nt; n_reqs = nr; n_names = nn;
+    return CA_OK;
+}
+
 // a dirty row staged for sync_nodes
 struct alignas(16) StagedRow {
     int32_t row, pad[3];
@@ -308,7 +343,23 @@ int ca_mirror::sync_nodes() {
 }
 
 int ca_mirror::sync_pods() {
-    if (d_pods_synced == pods.size() && d_terms_synced == terms.size()) return CA_OK;
+    if (d_pods_synced == pods.size() && d_terms_synced == terms.size() && (size_t)d_pods.n_reqs == reqs.size() &&
+        (size_t)d_pods.n_names == pf_names.size())
+        return CA_OK;
+    // pod records and selector tables only grow between Clear()s (Revert detaches pods
+    // from their nodes, ids are never reused): append the new tail
+    if (pods.size() >= d_pods_synced && terms.size() >= d_terms_synced && d_pods_synced == (size_t)d_pods.n_pods &&
+        reqs.size() >= (size_t)d_pods.n_reqs && pf_names.size() >= (size_t)d_pods.n_names && d_pods_synced > 0) {
+        const size_t a = d_pods_synced, k = pods.size() - a;
+        std::vector<ca_pod_spec> specs(k);
+        for (size_t i = 0; i < k; i++) specs[i] = pods[a + i].spec;
+        int rc = d_pods.append(specs.data(), (int32_t)k, terms.data(), (int32_t)terms.size(), reqs.data(),
+                               (int32_t)reqs.size(), pf_names.data(), (int32_t)pf_names.size(), stream);
+        if (rc != CA_OK) return rc;
+        d_pods_synced = pods.size();
+        d_terms_synced = terms.size();
+        return CA_OK;
+    }
     std::vector<ca_pod_spec> specs(pods.size());
     for (size_t i = 0; i < pods.size(); i++) specs[i] = pods[i].spec;
     int rc = d_pods.upload(specs.data(), (int32_t)specs.size(), terms.data(), (int32_t)terms.size(),

@@ -145,6 +145,35 @@ int ca_util_table_create(int32_t device, const ca_util_node* nodes, int32_t n_no
     return CA_OK;
 }
 
+int ca_util_table_update(ca_util_table* t, const ca_util_node* nodes, int32_t n_nodes, const int32_t* pod_off,
+                         const ca_util_pod* pods) {
+    if (!t || n_nodes < 0 || (n_nodes > 0 && (!nodes || !pod_off))) return CA_EINVAL;
+    const int32_t n_pods = n_nodes > 0 ? pod_off[n_nodes] : 0;
+    if (n_pods < 0 || (n_pods > 0 && !pods) || (n_nodes > 0 && pod_off[0] != 0)) return CA_EINVAL;
+    for (int32_t i = 0; i < n_nodes; i++)
+        if (pod_off[i + 1] < pod_off[i]) return CA_EINVAL;
+    CA_HIP_CHECK(hipSetDevice(t->device));
+    int st;
+    if ((st = t->nodes.reserve(sizeof(ca_util_node) * (size_t)n_nodes + 1)) ||
+        (st = t->pod_off.reserve(sizeof(int32_t) * ((size_t)n_nodes + 1))) ||
+        (st = t->pods.reserve(sizeof(ca_util_pod) * (size_t)n_pods + 1)) ||
+        (st = t->info.reserve(sizeof(ca_util_info) * (size_t)n_nodes + 1)))
+        return st;
+    if (n_nodes > 0) {
+        CA_HIP_CHECK(hipMemcpyAsync(t->nodes.ptr, nodes, sizeof(ca_util_node) * n_nodes, hipMemcpyHostToDevice,
+                                    t->stream));
+        CA_HIP_CHECK(hipMemcpyAsync(t->pod_off.ptr, pod_off, sizeof(int32_t) * (n_nodes + 1), hipMemcpyHostToDevice,
+                                    t->stream));
+        if (n_pods > 0)
+            CA_HIP_CHECK(hipMemcpyAsync(t->pods.ptr, pods, sizeof(ca_util_pod) * n_pods, hipMemcpyHostToDevice,
+                                        t->stream));
+    }
+    CA_HIP_CHECK(hipStreamSynchronize(t->stream));
+    t->n_nodes = n_nodes;
+    t->n_pods = n_pods;
+    return CA_OK;
+}
+
 int ca_util_table_destroy(ca_util_table* t) {
     if (!t) return CA_EINVAL;
     (void)hipSetDevice(t->device);

@@ -93,6 +93,7 @@ def load() -> C.CDLL:
         "ca_filter_stats": ([vp, p(C.c_float), i32], C.c_int),
         "ca_util_table_create": ([i32, vp, i32, vp, vp, p(vp)], C.c_int),
         "ca_util_table_destroy": ([vp], C.c_int),
+        "ca_util_table_update": ([vp, vp, i32, vp, vp], C.c_int),
         "ca_util_calculate": ([vp, i32, i32, C.c_int64, vp, p(C.c_float)], C.c_int),
         "ca_util_device_results": ([vp, p(vp)], C.c_int),
         "ca_multi_create": ([p(vp), i32, p(vp)], C.c_int),
@@ -137,7 +138,7 @@ def exported_symbols() -> list[str]:
         "ca_removal_plan_destroy", "ca_mirror_set_hints", "ca_mirror_get_hints",
         "ca_removal_candidate_ticks", "ca_filter_out_schedulable", "ca_filter_stats",
         "ca_util_table_create", "ca_util_table_destroy", "ca_util_calculate", "ca_util_device_results",
-        "ca_multi_create", "ca_multi_destroy", "ca_multi_estimate_plan_create", "ca_multi_estimate_plan_run",
+        "ca_util_table_update", "ca_multi_create", "ca_multi_destroy", "ca_multi_estimate_plan_create", "ca_multi_estimate_plan_run",
         "ca_multi_estimate_plan_stats", "ca_multi_estimate_plan_destroy", "ca_multi_estimate_batch",
         "ca_multi_removal_plan_create", "ca_multi_removal_plan_run", "ca_multi_removal_plan_stats",
         "ca_multi_removal_plan_destroy", "ca_multi_find_nodes_to_remove",
@@ -316,6 +317,10 @@ class Mirror:
         _check(self.lib.ca_check_predicates(self.h, table.ref, pod, node, C.byref(r)), "ca_check_predicates")
         return r.type, r.plugin, r.reasons, r.taint
 
+    def podset(self, table: abi.PodTable) -> "PodSet":
+        """`table` resident in device memory, for several calls (close() it after)."""
+        return PodSet(self, table)
+
     def fits_matrix(self, table: abi.PodTable) -> np.ndarray:
         s = C.c_void_p()
         _check(self.lib.ca_podset_create(self.h, table.ref, C.byref(s)), "ca_podset_create")
@@ -328,8 +333,8 @@ class Mirror:
 
     # -- estimator ------------------------------------------------------------
     def estimate(self, table: abi.PodTable, group_off, pod_idx, templates: np.ndarray, max_nodes: int,
-                 last_index: int = 0, want_nodes: bool = True) -> EstimateOutput:
-        with EstimatePlan(self, table, group_off, pod_idx, templates) as plan:
+                 last_index: int = 0, want_nodes: bool = True, podset=None) -> EstimateOutput:
+        with EstimatePlan(self, table, group_off, pod_idx, templates, podset=podset) as plan:
             return plan.run(max_nodes, last_index, want_nodes=want_nodes)
 
     def check_templates(self, table: abi.PodTable, samples, templates: np.ndarray, podset=None,
@@ -510,7 +515,9 @@ class PodSet:
 class EstimatePlan:
     """``ca_estimate_plan``: device-resident groups for repeated Estimate batches."""
 
-    def __init__(self, mirror: Mirror, table: abi.PodTable, group_off, pod_idx, templates: np.ndarray):
+    def __init__(self, mirror: Mirror, table: abi.PodTable, group_off, pod_idx, templates: np.ndarray,
+                 podset: "PodSet" = None):
+        """`podset`: a resident PodSet of `table` to use (else the table is uploaded here)."""
         self.m = mirror
         self.lib = mirror.lib
         self.group_off = np.ascontiguousarray(group_off, dtype=np.int32)
@@ -518,14 +525,19 @@ class EstimatePlan:
         self.templates = np.ascontiguousarray(templates, dtype=abi.TEMPLATE_DTYPE)
         self.G = len(self.templates)
         self.total = int(self.group_off[-1]) if len(self.group_off) else 0
-        s = C.c_void_p()
-        _check(self.lib.ca_podset_create(mirror.h, table.ref, C.byref(s)), "ca_podset_create")
-        self.podset = s
+        if podset is None:
+            s = C.c_void_p()
+            _check(self.lib.ca_podset_create(mirror.h, table.ref, C.byref(s)), "ca_podset_create")
+            self.podset = s
+        else:
+            self.podset = None
+            s = podset.h
         p = C.c_void_p()
         st = self.lib.ca_estimate_plan_create(mirror.h, s, ptr(self.group_off), ptr(self.pod_idx),
                                               ptr(self.templates), self.G, C.byref(p))
         if st != abi.CA_OK:
-            self.lib.ca_podset_destroy(s)
+            if self.podset:
+                self.lib.ca_podset_destroy(self.podset)
             raise CasimError(st, "ca_estimate_plan_create")
         self.h = p
         n = max(self.total, 1)
@@ -589,7 +601,8 @@ class EstimatePlan:
     def close(self) -> None:
         if self.h:
             self.lib.ca_estimate_plan_destroy(self.h)
-            self.lib.ca_podset_destroy(self.podset)
+            if self.podset:
+                self.lib.ca_podset_destroy(self.podset)
             self.h = None
             self.sched_pod = self.sched_node = None
             self._pinned.close()
@@ -617,6 +630,14 @@ class UtilTable:
                                              ptr(self.pods), C.byref(h)), "ca_util_table_create")
         self.h = h
         self.kernel_ms = 0.0
+
+    def update(self, nodes: np.ndarray, pod_off: np.ndarray, pods: np.ndarray) -> None:
+        """New rows (the snapshot changed), in the table's device buffers."""
+        self.nodes = np.ascontiguousarray(nodes, abi.UTIL_NODE_DTYPE)
+        self.pod_off = np.ascontiguousarray(pod_off, np.int32)
+        self.pods = np.ascontiguousarray(pods, abi.UTIL_POD_DTYPE)
+        _check(self.lib.ca_util_table_update(self.h, ptr(self.nodes), len(self.nodes), ptr(self.pod_off),
+                                             ptr(self.pods)), "ca_util_table_update")
 
     def calculate(self, skip_daemonset_pods: bool, skip_mirror_pods: bool, now_ns: int,
                   to_host: bool = True):

@@ -76,6 +76,7 @@ def parse():
     ap.add_argument("--no-util", action="store_true", help="skip the scale-down eligibility leg (N=1)")
     ap.add_argument("--no-filter", action="store_true", help="skip the FilterOutSchedulable leg (N=1)")
     ap.add_argument("--no-unlimited", action="store_true", help="skip the C2 max_nodes=0 leg (N=1)")
+    ap.add_argument("--no-runonce", action="store_true", help="skip the C5 end-to-end RunOnce leg (N=1)")
     ap.add_argument("--sweep-nodes", type=int, default=5000)
     return ap.parse_args()
 
@@ -334,6 +335,52 @@ def sweep_leg(args, device: int, with_cpu: bool) -> dict:
                                "sample": f"oracle/casim_oracle.c FindNodesToRemove, same C3 sweep, 1 thread of "
                                          f"{cpu_model()}"}
     m.close()
+    return out
+
+
+def runonce_leg(args, device: int, with_cpu: bool) -> dict:
+    """C5 end to end (autoscaler_amd/runonce.py): one RunOnce's simulation legs over 15k
+    nodes / 300k pods / 20k pending pods — FilterOutSchedulable, expansion options (100 node
+    groups), Estimate of every option, utilization + empty nodes, FindNodesToRemove over the
+    low-utilization candidates — each step through the C ABI, inside a fork reverted after
+    the loop; the CPU port runs the same loop."""
+    from autoscaler_amd import native, runonce
+    from autoscaler_amd import workloads as W
+    w = runonce.c5_runonce()
+    m = native.Mirror(device)
+    W.load_filter(m, w.filt)
+
+    ut = []                                                       # one resident table, rows replaced per loop
+
+    def util(n, off, p, now):
+        if not ut:
+            ut.append(native.UtilTable(device, n, off, p))
+        else:
+            ut[0].update(n, off, p)
+        return ut[0].calculate(False, False, now)
+    runs = []
+    for _ in range(1 + max(2, min(args.steps, 4))):
+        m.fork()
+        runs.append(runonce.run(m, util, w))
+        m.revert()
+    m.close()
+    ut[0].close()
+    keys = list(runs[-1].ms)
+    out = {"workload": "C5 RunOnce: 15000 nodes, 300000 running pods, 20000 pending (15% of the controller "
+                       "variants too large for existing nodes), 100 node groups",
+           "sizes": runs[-1].sizes,
+           "gpu_ms": {k: float(np.median([r.ms[k] for r in runs[1:]])) for k in keys}}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle                                           # CPU baseline leg only
+        o = pyoracle.OracleState()
+        W.load_filter(o, w.filt)
+        ro = runonce.run(o, lambda n, off, p, now: pyoracle.node_utilization(n, off, p, False, False, now), w)
+        out["cpu_ms"] = ro.ms
+        out["speedup"] = {k: ro.ms[k] / out["gpu_ms"][k] for k in keys if out["gpu_ms"][k] > 0}
+        out["parity"] = runonce.compare(ro, runs[-1])
+        out["cpu_baseline"] = {"kind": "port", "cores": 1,
+                               "sample": f"oracle/casim_oracle.c, the same loop step by step, 1 thread of {cpu_model()}"}
     return out
 
 
@@ -616,6 +663,8 @@ def main():
             result["extra"]["filter"] = filter_leg(args, local, not args.no_cpu_baseline)
         if world == 1 and not args.no_util:
             result["extra"]["utilization"] = utilization_leg(args, local, not args.no_cpu_baseline)
+        if world == 1 and not args.no_runonce:
+            result["extra"]["c5_runonce"] = runonce_leg(args, local, not args.no_cpu_baseline)
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.barrier()

@@ -532,6 +532,10 @@ typedef struct ca_util_table ca_util_table;
 int ca_util_table_create(int32_t device, const ca_util_node* nodes, int32_t n_nodes,
                          const int32_t* pod_off, const ca_util_pod* pods, ca_util_table** out);
 int ca_util_table_destroy(ca_util_table* t);
+/* Replaces the table's rows (the snapshot changed: next loop, or after FilterOutSchedulable
+ * placed pods), reusing its device buffers. */
+int ca_util_table_update(ca_util_table* t, const ca_util_node* nodes, int32_t n_nodes, const int32_t* pod_off,
+                         const ca_util_pod* pods);
 /* Calculate(nodeInfo, skipDaemonSetPods, skipMirrorPods, gpuConfig, currentTime) for every
  * node.  out NULL keeps the results in HBM (ca_util_device_results); otherwise out[n_nodes]
  * is filled.  *kernel_ms (may be NULL) = device time of the kernel. */

@@ -1,0 +1,36 @@
+"""Per-step diagnostics of the C5 RunOnce loop on the GPU (python scripts/runonce_diag.py):
+the sweep's and the filter's internal statistics at C5 scale."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+import numpy as np  # noqa: E402
+
+from autoscaler_amd import native, runonce  # noqa: E402
+from autoscaler_amd import workloads as W  # noqa: E402
+
+w = runonce.c5_runonce()
+m = native.Mirror(0)
+W.load_filter(m, w.filt)
+
+
+ut = []
+
+
+def util(n, off, p, now):
+    if not ut:
+        ut.append(native.UtilTable(0, n, off, p))
+    else:
+        ut[0].update(n, off, p)
+    return ut[0].calculate(False, False, now)
+
+
+for rep in range(3):
+    m.fork()
+    r = runonce.run(m, util, w)
+    print({k: round(v, 2) for k, v in r.ms.items()}, flush=True)
+    print("filter", m.filter_stats(), flush=True)
+    print("sweep", m.removal_stats(), flush=True)
+    m.revert()

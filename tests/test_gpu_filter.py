@@ -101,3 +101,19 @@ def test_filter_no_class_owner_and_empty(oracle_lib):
     ro = o.filter_out_schedulable(w.pending, None, None, None, 7)
     _eq(rg, ro, "table order, no cap")
     g.close()
+
+
+def test_filter_dead_shapes(oracle_lib):
+    """Pending pods whose shape fits no node (RunOnce's backlog): their shapes share one
+    all-zero dyn row, so the call stays on the bitmap walk with > 64 distinct shapes."""
+    from autoscaler_amd import runonce
+    w = runonce.c5_runonce(n_nodes=3000, n_pending=6000, n_groups=4).filt
+    g, o = native.Mirror(0), oracle_lib.OracleState()
+    W.load_filter(g, w)
+    W.load_filter(o, w)
+    rg = g.filter_out_schedulable(w.pending, w.order, w.class_owner, w.hints, 3)
+    st = g.filter_stats()
+    assert st["path"] == "bitmap", st
+    ro = o.filter_out_schedulable(w.pending, w.order, w.class_owner, w.hints, 3)
+    _eq(rg, ro, "dead shapes")
+    g.close()

@@ -112,7 +112,13 @@ __device__ inline bool in_prefilter(const ca_pod_spec& s, const int32_t* names, 
 // ---------------------------------------------------------------------------
 // exact kernel: one wavefront per candidate at its exact lastIndex
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_sweep(
+// Occupancy: the sweep runs one wavefront per candidate (C3: 5 000) and each candidate is a
+// latency-bound chain, so the kernel time is (rounds of resident waves) x (chain time);
+// CASIM_SWEEP_WAVES bounds the VGPRs so more waves are resident per SIMD.
+#ifndef CASIM_SWEEP_WAVES
+#define CASIM_SWEEP_WAVES 4
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CASIM_SWEEP_WAVES, 8))) k_sweep(
     const NodeHot* __restrict__ hot, const NodeExt* __restrict__ ext, const NodeStatic* __restrict__ st, int32_t n,
     const uint8_t* __restrict__ dest_mask, const int32_t* __restrict__ cands, const int32_t* __restrict__ cand_status,
     const int32_t* __restrict__ move_off, const int32_t* __restrict__ move_pods, const PodHot* __restrict__ ph,
@@ -217,7 +223,10 @@ __global__ void __launch_bounds__(64) k_sweep(
                 if (my_hint >= 0 && my_hint < n) { my_hh = hot[my_hint]; my_hdm = dest_mask[my_hint]; }
             }
         }
-        __syncthreads();
+        // one wavefront per workgroup: its LDS accesses complete in order, so the overlay
+        // needs only a compiler-level barrier here (an s_barrier would also wait for the
+        // next block's prefetch and every outstanding load, each pod)
+        __builtin_amdgcn_wave_barrier();
         if (sl == 0) {
             // ---- the batch's leading pods placed on their hints, in bulk ----
             // Pod i of a run whose earlier pods all went to their hinted nodes sees exactly
@@ -297,7 +306,7 @@ __global__ void __launch_bounds__(64) k_sweep(
                 if (lane < f) { my_dest = my_hint; my_hset = my_hint; }      // hints.Set + isNodeAcceptable
                 evals += (uint64_t)f;
                 placed += f;
-                __syncthreads();
+                __builtin_amdgcn_wave_barrier();
                 i += f - 1;
                 continue;
             }

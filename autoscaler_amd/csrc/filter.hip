@@ -924,6 +924,25 @@ __global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
         const uint64_t hinted_mask = __ballot(my_hinted);
         NodeHot hrow = {};                                                      // prefetch: the hinted rows
         if (my_hinted) hrow = ld_hot_coh(a.hot + lh);
+        // hint checks that can pass at all: the bits at the batch's start (placements only
+        // clear bits, so a hint failing now fails later in the batch too)
+        bool may = false;
+        if (my_hinted) {
+            const int32_t hw = lh >> 6;
+            const uint64_t bit = 1ull << (lh & 63);
+            const uint64_t hs = lp.scls >= 0 ? (stat_lds ? stat_l[(size_t)lp.scls * NW + hw]
+                                                         : a.stat[(size_t)lp.scls * NW + hw]) : ~0ull;
+            may = (dyn[(size_t)lp.shape * NW + hw] & hs & bit) && ((vis[hw] & bit) || (lp.flags & PF_TOL_UNSCHED));
+        }
+        const uint64_t may_mask = __ballot(may);
+        // hinted pods whose hint fails for sure: one evaluation (CheckPredicates), then they
+        // behave as unhinted pods, so they join runs
+        const uint64_t nohope = hinted_mask & ~may_mask;
+        auto hint_evals = [&](int32_t from, int32_t np) -> unsigned long long {
+            if (np <= 0 || from >= 64) return 0ull;
+            const uint64_t mk = (np >= 64 ? ~0ull : ((1ull << np) - 1)) << from;
+            return (unsigned long long)__builtin_popcountll(nohope & mk);
+        };
         int32_t out = -1;
         int32_t j = 0;
         while (j < cnt) {
@@ -937,13 +956,95 @@ __global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
             const uint64_t* ds = dyn + (size_t)s * NW;
             const size_t so = c >= 0 ? (size_t)c * NW : 0;
             int32_t first = j;                                                  // the run starts here
-            if ((hinted_mask >> j) & 1) {                                       // findNodeWithHints (:91-108)
+            // Leading hinted pods in bulk: pod t of a row of hinted pods whose earlier pods
+            // all went to their hinted nodes sees exactly those placements on its own
+            // hinted node, so the hint checks (CheckPredicates: NodeUnschedulable, static,
+            // NodeResourcesFit on the row minus the earlier pods on that node) are
+            // independent lane checks; the leading successes are placed together, and the
+            // first failing pod goes on alone below.
+            const uint64_t hr = (may_mask >> j) & 3ull;
+            if (hr == 3ull) {
+                const uint64_t hrun = may_mask >> j;
+                const int32_t lead = hrun == ~0ull ? 64 : (int32_t)__builtin_ctzll(~hrun);
+                const bool in = lane >= j && lane < j + lead;
+                const FbShape msh = shp[in ? lp.shape : 0];
+                // the row of my hinted node: the batch buffer's newest entry, else the prefetch
+                int64_t rc = hrow.cpu, rm = hrow.mem, re = hrow.eph;
+                int32_t rp = hrow.pods;
+                int32_t didx = -1;
+                if (in && ((dirty[lh >> 6] >> (lh & 63)) & 1)) {
+                    int32_t i = buf_n - 1;
+                    while (bufnode[i] != lh) i--;
+                    const FbRow r = bufrow[i];
+                    rc = r.cpu; rm = r.mem; re = r.eph; rp = r.pods;
+                    didx = i;
+                }
+                // the earlier pods of the row that go to the same node
+                for (int32_t u = j; u < j + lead - 1; u++) {
+                    const int32_t hu = __builtin_amdgcn_readlane(lh, u);
+                    const FbShape su = shp[__builtin_amdgcn_readlane(lp.shape, u)];
+                    if (in && lane > u && lh == hu) {
+                        rc = wsub(rc, su.cpu); rm = wsub(rm, su.mem); re = wsub(re, su.eph); rp -= 1;
+                    }
+                }
+                bool ok = false;
+                if (in) {
+                    const int32_t hw = lh >> 6;
+                    const uint64_t bit = 1ull << (lh & 63);
+                    const size_t mso = lp.scls >= 0 ? (size_t)lp.scls * NW : 0;
+                    const uint64_t hs = lp.scls >= 0 ? (stat_lds ? stat_l[mso + hw] : a.stat[mso + hw]) : ~0ull;
+                    ok = (hs & bit) && ((vis[hw] & bit) || (lp.flags & PF_TOL_UNSCHED)) && fb_fit(msh, rc, rm, re, rp);
+                }
+                const uint64_t okm = __ballot(ok) >> j;
+                const int32_t f = min(lead, okm == ~0ull ? 64 : (int32_t)__builtin_ctzll(~okm));
+                if (f > 0) {
+                    const bool mine = lane >= j && lane < j + f;
+                    // the last of the placed pods on each node commits the node's new row
+                    bool later = false;
+                    for (int32_t u = j + 1; u < j + f; u++) {
+                        const int32_t hu = __builtin_amdgcn_readlane(lh, u);
+                        later |= mine && lane < u && lh == hu;
+                    }
+                    const bool fin = mine && !later;
+                    if (fin && didx >= 0) bufnode[didx] = -1;                   // superseded below
+                    const int64_t qc = wsub(rc, msh.cpu), qm = wsub(rm, msh.mem), qe = wsub(re, msh.eph);
+                    const int32_t qp = rp - 1;
+                    const uint64_t finm = __ballot(fin);
+                    if (fin) {
+                        const int32_t at = buf_n + (int32_t)__builtin_popcountll(finm & bits_below(lane));
+                        FbRow q;
+                        q.cpu = qc; q.mem = qm; q.eph = qe; q.pods = qp; q.pad = 0;
+                        bufrow[at] = q;
+                        bufnode[at] = lh;
+                        __hip_atomic_fetch_or(&dirty[lh >> 6], 1ull << (lh & 63), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    buf_n += (int32_t)__builtin_popcountll(finm);
+                    for (uint64_t fm = finm; fm; fm &= fm - 1) {                 // lane s': shape s' on each new row
+                        const int t = __builtin_ctzll(fm);
+                        const int64_t c0 = rlane64(qc, t), m0 = rlane64(qm, t), e0 = rlane64(qe, t);
+                        const int32_t p0 = __builtin_amdgcn_readlane(qp, t);
+                        const int32_t x = __builtin_amdgcn_readlane(lh, t);
+                        if (lane < S && !fb_fit(my_sh, c0, m0, e0, p0))
+                            __hip_atomic_fetch_and(&dyn[(size_t)lane * NW + (x >> 6)], ~(1ull << (x & 63)),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    if (mine) out = lh;
+                    evals += (unsigned long long)f;                             // CheckPredicates per pod
+                    j += f;
+#ifdef CASIM_PROF
+                    prof_fb[0] += clock64() - pc0;
+#endif
+                    continue;                                                   // pod j (if any) fails its hint
+                }
+            }
+            if ((may_mask >> j) & 1) {                                          // findNodeWithHints (:91-108)
                 const int32_t h = __builtin_amdgcn_readlane(lh, j);
                 const int32_t hw = h >> 6;
                 const uint64_t bit = 1ull << (h & 63);
-                const uint64_t hs = c >= 0 ? (stat_lds ? stat_l[so + hw] : a.stat[so + hw]) : ~0ull;
                 evals++;                                                        // CheckPredicates ran the filters
                 // NodeUnschedulable applies (tolerable), then static, then fit
+                const uint64_t hs = c >= 0 ? (stat_lds ? stat_l[so + hw] : a.stat[so + hw]) : ~0ull;
                 if ((ds[hw] & hs & bit) && ((vis[hw] & bit) || (pf & PF_TOL_UNSCHED))) {
                     if (lane == 0) slot[0] = h;
                     NodeHot pr;
@@ -962,18 +1063,20 @@ __global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
             // the run: pod j and the unhinted pods right after it with the same attributes
             const bool same = lane >= first && lane < cnt && lp.shape == s && lp.scls == c && lp.simcls == sim &&
                               lp.flags == pf;
-            const uint64_t run_ok = __ballot(same) & ~hinted_mask;
+            const uint64_t run_ok = __ballot(same) & ~(hinted_mask & may_mask);
             const uint64_t rest = first < 64 ? run_ok >> first : 0ull;          // consecutive ones from `first`
             const int32_t m = (first - j) + (rest == ~0ull ? 64 : (int32_t)__builtin_ctzll(~rest));
 #ifdef CASIM_PROF
             const unsigned long long pc1 = clock64();
             prof_fb[0] += pc1 - pc0;
 #endif
+            const int32_t pre = first - j;                                      // pod j, already hint-checked
             if (sim >= 0 && marks[sim]) {                                       // similar pod known unschedulable
+                evals += hint_evals(first, m - pre);
                 j += m;
                 continue;
             }
-            if (pf & PF_PREFILTER_FAIL) {                                       // no node passes PreFilter
+            if (pf & PF_PREFILTER_FAIL) {                                       // no node passes PreFilter (never hinted)
                 if (sim >= 0 && !(pf & PF_DAEMONSET)) fb_mark(a, marks, ocnt, oover, sim, overflowing, lane);
                 j += (sim >= 0 && !(pf & PF_DAEMONSET) && marks[sim]) ? m : 1;
                 continue;
@@ -1012,7 +1115,7 @@ __global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
                 // a marked class skips the rest of the run; otherwise (no class, DaemonSet, a
                 // controller over its cap) each pod scans the whole ring again, unchanged
                 const int32_t nfail = (can_mark && marks[sim]) ? 1 : m;
-                evals += (unsigned long long)nfail * (unsigned long long)vis_total;
+                evals += (unsigned long long)nfail * (unsigned long long)vis_total + hint_evals(first, m - pre);
                 j += m;
                 continue;
             }
@@ -1022,6 +1125,7 @@ __global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
             const int32_t vpx = vpre[xw] + __builtin_popcountll(vis[xw] & bits_below(xl & 63)) + 1;
             evals += (unsigned long long)(xl >= L ? vpx - vpL : vis_total - vpL + vpx);
             place(k, s, false, NodeHot{});
+            evals += hint_evals(first, k - pre);
             if (lane >= j && lane < j + k) out = slot[lane - j];
             L = xl + 1 == n ? 0 : xl + 1;                                       // schedulerbased.go:131
             vpL = L == 0 ? 0 : vpx;
@@ -1064,6 +1168,12 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     if (!m || !t || n < 0 || n_classes < 0 || !last_index || (n > 0 && !out_node)) return CA_EINVAL;
     if (s && (s->m != m || s->t.n_pods != t->n_pods)) return CA_EINVAL;
     const auto t0 = std::chrono::steady_clock::now();
+    const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
+    auto tmark = [&](const char* what) {
+        if (dbg_t)
+            fprintf(stderr, "[filter] %-12s %8.3f ms\n", what,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    };
     for (int32_t k = 0; k < n; k++) {
         const int32_t i = order ? order[k] : k;
         if (i < 0 || i >= t->n_pods) return CA_EINVAL;
@@ -1082,7 +1192,9 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     if (n == 0) return CA_OK;
     CA_HIP_CHECK(hipSetDevice(m->device));
     int rc;
+    tmark("validated");
     if ((rc = m->sync_nodes()) != CA_OK) return rc;
+    tmark("synced");
     const DevPodTable* dp = s ? &s->t : nullptr;
     if (!dp) {
         if ((rc = fo.pods.upload(t->pods, t->n_pods, t->terms, t->n_terms, t->reqs, t->n_reqs, t->prefilter_names,
@@ -1175,8 +1287,14 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
         };
         std::unordered_map<std::string, int32_t, KeyHash> shape_id, cls_id;
         fb_pods.resize((size_t)n);
+        const ca_pod_spec* prev = nullptr;               // pods of one controller variant come in a row
         for (int32_t k = 0; k < n && fb; k++) {
             const ca_pod_spec& ps = t->pods[h_order[k]];
+            if (prev && std::memcmp(prev, &ps, sizeof ps) == 0) {          // the same record: same ids
+                fb_pods[k] = fb_pods[k - 1];
+                continue;
+            }
+            prev = &ps;
             const uint32_t f = pod_dev_flags(ps);
             if (f & (PF_PORTS | PF_SCALAR_REQ | PF_PREFILTER_NAMES)) { fb = false; break; }
             std::string sk(reinterpret_cast<const char*>(&ps.req_milli_cpu), 24);
@@ -1263,6 +1381,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
         fb_stat_in_lds = K > 0 && fb_lds(S, NW, K, 1, n_classes, n_owners).total <= FB_LDS_MAX ? 1 : 0;
         if (fb_lds(S, NW, K, fb_stat_in_lds, n_classes, n_owners).total > FB_LDS_MAX) fb = false;
     }
+    tmark("prepared");
     CA_HIP_CHECK(hipEventRecord(m->ev0, m->stream));
     if (fb) {
         const int32_t S = (int32_t)fb_shapes.size(), K = (int32_t)fb_rep.size();
@@ -1330,6 +1449,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     }
     const int32_t* nodes_out = reinterpret_cast<const int32_t*>(ho);
     const int32_t* hints_out = reinterpret_cast<const int32_t*>(ho + al(sizeof(int32_t) * n));
+    tmark("device");
     // AddPod of every placed pod on the host rows, in the reference's order
     int32_t placed = 0;
     for (int32_t k = 0; k < n; k++) {
@@ -1355,6 +1475,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     fo.seq_share = hctl->all_cycles ? (float)((double)hctl->seq_cycles / (double)hctl->all_cycles) : 0.0f;
     fo.walk_cycles_per_pod = n ? (float)((double)hctl->seq_cycles / n) : 0.0f;
     for (int i = 0; i < 3; i++) fo.fb_cyc_per_pod[i] = n ? (float)((double)hctl->fb_cyc[i] / n) : 0.0f;
+    tmark("host rows");
     fo.total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (n_placed) *n_placed = placed;
     return CA_OK;

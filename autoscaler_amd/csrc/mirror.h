@@ -48,6 +48,7 @@ struct DevPodTable {
 // hipMalloc); host staging is page-locked.
 struct SweepScratch {
     DevBuf in, lin, need, out, todo, tab, wl;
+    DevBuf tev, tdest;              // table lanes' evaluation counts and pod destinations (first round)
     HostBuf h_in, h_tab, h_out, h_todo, h_lin, h_wl;
 };
 

@@ -544,7 +544,10 @@ __global__ void __launch_bounds__(64) k_sweep_table(
     const ca_selector_term* __restrict__ terms, const ca_selector_req* __restrict__ reqs,
     const int32_t* __restrict__ names, const int32_t* __restrict__ hints, const int32_t* __restrict__ todo,
     const int32_t* __restrict__ wstart, const int32_t* __restrict__ row_of, int32_t* __restrict__ table,
-    int32_t stride) {
+    int32_t stride, uint32_t* __restrict__ tev, int32_t* __restrict__ tdest, const int32_t* __restrict__ tdoff) {
+    // tev / tdest (first round, device walk): the lane's evaluation count and each moved
+    // pod's destination, so a candidate the walk resolves through the table takes these
+    // outputs (k_table_gather) instead of being simulated again
     const int t = blockIdx.x;
     const int lane = threadIdx.x;
     const int32_t c = todo[t];
@@ -554,6 +557,8 @@ __global__ void __launch_bounds__(64) k_sweep_table(
     if (Ls >= n) Ls -= n;
     int32_t Lcur = Ls;
     int32_t adv = 0;              // positions passed since Ls
+    uint32_t ev = 0;              // visible nodes scanned (the exact kernel's evals)
+    const int32_t dbase = tdoff ? tdoff[t] : -1;
     bool unknown = mn > TB_MAXP;
     // candidates with hints / ports / scalars go to the exact kernel
     for (int32_t i = lane; i < mn; i += 64) {
@@ -573,7 +578,7 @@ __global__ void __launch_bounds__(64) k_sweep_table(
             p.cpu = rl64s(my_p.cpu, sl); p.mem = rl64s(my_p.mem, sl); p.eph = rl64s(my_p.eph, sl);
             p.flags = moved_flags((uint32_t)rl32s((int32_t)my_p.flags, sl));
             p.spec = rl32s(my_p.spec, sl);
-            if (p.flags & PF_PREFILTER_FAIL) break;                            // FitsAnyNode error: stop
+            if (p.flags & PF_PREFILTER_FAIL) { unknown = true; break; }         // FitsAnyNode error: exact kernel
             const ca_pod_spec& s = specs[p.spec];
             // lane-private rotating scan from this lane's lastIndex
             int32_t steps = 0;
@@ -585,6 +590,7 @@ __global__ void __launch_bounds__(64) k_sweep_table(
                 const uint8_t dm = dest_mask[pos];
                 bool vis = (pos != node) & (dm != 0) & !(nh.flags & NF_UNSCHED);
                 if (vis && (p.flags & PF_PREFILTER_NAMES)) vis = in_prefilter(s, names, st[pos].name_id);
+                ev += vis ? 1u : 0u;
                 if (vis && hot_fits(p, nh) && static_ok(s, p, terms, reqs, nh, st + pos)) break;
                 steps++;
                 pos++;
@@ -593,6 +599,7 @@ __global__ void __launch_bounds__(64) k_sweep_table(
             if (lane_unknown) unknown = true;
             if (__ballot(!unknown) == 0) break;          // every lane handed over
             if (!unknown) {
+                if (dbase >= 0) tdest[(size_t)(dbase + i) * 64 + lane] = pos;
                 adv += steps + 1;
                 Lcur = pos + 1;
                 if (Lcur >= n) Lcur = 0;
@@ -600,6 +607,7 @@ __global__ void __launch_bounds__(64) k_sweep_table(
         }
     }
     table[(size_t)lane * stride + (row_of ? row_of[t] : t)] = unknown ? TB_UNKNOWN : Lcur;
+    if (tev) tev[(size_t)lane * stride + (row_of ? row_of[t] : t)] = ev;
 }
 
 // ---------------------------------------------------------------------------
@@ -743,9 +751,46 @@ __global__ void __launch_bounds__(1024) k_walk_resolve(const int32_t* __restrict
         const int32_t e = traj[(size_t)k * 64 + lane_of[k / WK]];
         const int32_t c = sens[k];
         lin[c] = e >> 1;
-        need[c] = (uint8_t)(e & 1);
+        need[c] = (uint8_t)((e & 1) ? 2 : 0);          // 2: resolved through the table (k_table_gather)
     }
     if (threadIdx.x == 0) { info[0] = sk; info[1] = cur_out; }
+}
+
+// Candidates the device walk resolved through the table (need == 2): the table lane at
+// their exact input simulated them exactly (unhinted, no ports / extended requests, no
+// ring wrap, every pod placed), so its outputs are theirs: removable, every pod at its
+// recorded destination (Hints.Set to it), lastIndex out, evaluations.  One wavefront per
+// sensitive candidate; need becomes 0 so the exact pass skips it.
+__global__ void __launch_bounds__(64) k_table_gather(const int32_t* __restrict__ sens, const int32_t* __restrict__ ws,
+                                                    int32_t S, int32_t n, const int32_t* __restrict__ lin,
+                                                    uint8_t* __restrict__ need, const int32_t* __restrict__ tab,
+                                                    const uint32_t* __restrict__ tev, const int32_t* __restrict__ tdest,
+                                                    const int32_t* __restrict__ tdoff, const int32_t* __restrict__ move_off,
+                                                    SweepOut* __restrict__ outs, int32_t* __restrict__ out_dest,
+                                                    int32_t* __restrict__ hint_set, int32_t* __restrict__ walk_lout) {
+    const int32_t k = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int32_t c = sens[k];
+    if (need[c] != 2) return;
+    int32_t x = lin[c] - ws[k];
+    if (x < 0) x += n;
+    const int32_t mo = move_off[c], mn = move_off[c + 1] - mo;
+    const int32_t db = tdoff[k];
+    for (int32_t i = lane; i < mn; i += 64) {
+        const int32_t d = tdest[(size_t)(db + i) * 64 + x];
+        out_dest[mo + i] = d;
+        hint_set[mo + i] = d;
+    }
+    if (lane == 0) {
+        SweepOut r;
+        r.removable = 1; r.reason = CA_UNREMOVABLE_NONE; r.n_placed = mn; r.lin = lin[c];
+        r.lout = tab[(size_t)x * S + k];
+        r.fa_success = mn > 0 ? 1 : 0; r.status = CA_OK; r.pad = 0;
+        r.evals = tev[(size_t)x * S + k]; r.pad2 = 0;
+        outs[c] = r;
+        walk_lout[c] = r.lout;
+        need[c] = 0;
+    }
 }
 
 // resident hints (per mirror pod): gather the moved pods' hints / apply the hint sets
@@ -900,11 +945,23 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     CA_HIP_CHECK(hipEventRecord(m->ev0, st));
     if ((rc = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl)) != CA_OK) return rc;
     int32_t rounds = 1, exact_runs = 0;
+    int32_t* const d_tdoff = d_sens + 2 * (size_t)S;     // per sensitive candidate: its pods in tdest
     if (S > 0 && n > 0) {
         // ---- 2. first table round, windows centred on the probe's advances ----
         rounds++;
         std::memcpy(ht, sens.data(), sizeof(int32_t) * S);
+        int64_t tpods = 0;
+        for (int32_t k = 0; k < S; k++) {
+            const int32_t mn = move_off[sens[k] + 1] - move_off[sens[k]];
+            ht[2 * S + k] = (int32_t)tpods;
+            tpods += mn <= TB_MAXP ? mn : 0;
+        }
+        if (dev_walk) {
+            if ((rc = sw.tev.reserve(sizeof(uint32_t) * 64 * Sx)) != CA_OK) return rc;
+            if ((rc = sw.tdest.reserve(sizeof(int32_t) * 64 * (size_t)std::max<int64_t>(tpods, 1))) != CA_OK) return rc;
+        }
         CA_HIP_CHECK(hipMemcpyAsync(d_sens, ht, sizeof(int32_t) * S, hipMemcpyHostToDevice, st));
+        CA_HIP_CHECK(hipMemcpyAsync(d_tdoff, ht + 2 * S, sizeof(int32_t) * S, hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(k_sweep_est, dim3(1), dim3(1024), 0, st, d_out.as<SweepOut>(), d_sens, S, (int64_t)L0, n,
                            d_ws);
         CA_HIP_CHECK(hipGetLastError());
@@ -913,7 +970,9 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                            in.d_off.as<int32_t>(), in.d_moves.as<int32_t>(), m->d_pods.hot.as<PodHot>(),
                            m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
                            m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
-                           in.d_hints.as<int32_t>(), d_sens, d_ws, (const int32_t*)nullptr, sw.tab.as<int32_t>(), S);
+                           in.d_hints.as<int32_t>(), d_sens, d_ws, (const int32_t*)nullptr, sw.tab.as<int32_t>(), S,
+                           dev_walk ? sw.tev.as<uint32_t>() : nullptr, dev_walk ? sw.tdest.as<int32_t>() : nullptr,
+                           dev_walk ? (const int32_t*)d_tdoff : nullptr);
         CA_HIP_CHECK(hipGetLastError());
     }
     if (dev_walk) {
@@ -925,8 +984,24 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         hipLaunchKernelGGL(k_walk_resolve, dim3(1), dim3(1024), 0, st, d_sens, d_ws, d_cmap, d_traj, S, n, wrap(L0, n),
                            d_lin, d_need, d_info);
         CA_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_table_gather, dim3(S), dim3(64), 0, st, d_sens, d_ws, S, n, d_lin, d_need,
+                           sw.tab.as<int32_t>(), sw.tev.as<uint32_t>(), sw.tdest.as<int32_t>(), d_tdoff,
+                           in.d_off.as<int32_t>(), d_out.as<SweepOut>(), d_dest.as<int32_t>(), d_hset.as<int32_t>(), d_wl);
+        CA_HIP_CHECK(hipGetLastError());
         if ((rc = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl)) != CA_OK) return rc;
     }
+    // the resident hints: applied now, behind the exact pass, while the results travel (a
+    // host walk below re-runs candidates and applies them again; its exact passes read
+    // the gathered copy, not the resident table)
+    auto apply_hints = [&]() -> int {
+        if (d_pod_hints && M > 0) {
+            hipLaunchKernelGGL(k_hints_apply, dim3((M + 255) / 256), dim3(256), 0, st, d_hset.as<int32_t>(),
+                               in.d_moves.as<int32_t>(), M, d_pod_hints);
+            CA_HIP_CHECK(hipGetLastError());
+        }
+        return CA_OK;
+    };
+    if ((rc = apply_hints()) != CA_OK) return rc;
     CA_HIP_CHECK(hipEventRecord(m->ev1, st));
     CA_HIP_CHECK(hipMemcpyAsync(sw.h_out.ptr, sw.out.ptr, d2h_bytes, hipMemcpyDeviceToHost, st));
     CA_HIP_CHECK(hipStreamSynchronize(st));
@@ -975,7 +1050,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                                    m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
                                    m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
                                    in.d_hints.as<int32_t>(), sw.todo.as<int32_t>(), sw.todo.as<int32_t>() + T,
-                                   sw.todo.as<int32_t>() + 2 * T, sw.tab.as<int32_t>(), S);
+                                   sw.todo.as<int32_t>() + 2 * T, sw.tab.as<int32_t>(), S, nullptr, nullptr, nullptr);
                 CA_HIP_CHECK(hipGetLastError());
                 CA_HIP_CHECK(hipEventRecord(m->ev1, st));
                 // the table is stored [lane][candidate] so the host walk, whose window offset
@@ -1053,16 +1128,13 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
             CA_HIP_CHECK(hipMemcpyAsync(d_lin, h_lin, (sizeof(int32_t) + 1) * (size_t)C, hipMemcpyHostToDevice, st));
             if ((rc = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl)) != CA_OK) return rc;
         }
+        if (n_rerun > 0 || exact_runs > 0)
+            if ((rc = apply_hints()) != CA_OK) return rc;
         CA_HIP_CHECK(hipMemcpyAsync(sw.h_out.ptr, sw.out.ptr, d2h_bytes, hipMemcpyDeviceToHost, st));
         CA_HIP_CHECK(hipStreamSynchronize(st));
     }
     if (dbg_t) fprintf(stderr, "[sweep] exact fallbacks %d, device walk %s (stopped at %d of %d)\n", exact_runs,
                        dev_walk ? "on" : "off", dev_walk ? h_info[0] : 0, S);
-    if (d_pod_hints && M > 0) {
-        hipLaunchKernelGGL(k_hints_apply, dim3((M + 255) / 256), dim3(256), 0, st, d_hset.as<int32_t>(),
-                           in.d_moves.as<int32_t>(), M, d_pod_hints);
-        CA_HIP_CHECK(hipGetLastError());
-    }
     const auto t_exact = std::chrono::steady_clock::now();
     if (M && out_dest) std::memcpy(out_dest, h_dest, sizeof(int32_t) * M);
     // the outputs must reproduce the chain: each result with a successful scan was
@@ -1090,7 +1162,8 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     if (hints) {
         for (int32_t i = 0; i < M; i++) if (hset[i] >= 0) hints[move_pods[i]] = hset[i];
     }
-    if (d_pod_hints) CA_HIP_CHECK(hipStreamSynchronize(st));
+    // (the hint update stays queued on the mirror's stream: every later call is ordered
+    // behind it, and ca_mirror_get_hints synchronises)
     tmark("done");
     m->sweep_stats.rounds = rounds + exact_runs;
     // the sweep's output depends on its input lastIndex iff some scan succeeded

@@ -117,6 +117,14 @@ def load() -> C.CDLL:
     return lib
 
 
+def _fast_copy(a: np.ndarray) -> np.ndarray:
+    """Copy of a C-contiguous array through a byte view: numpy copies structured (record)
+    arrays field by field (~100 us for 5 000 sweep results), bytes in one memcpy."""
+    if a is None:
+        return None
+    return a.view(np.uint8).copy().view(a.dtype) if a.dtype.fields else a.copy()
+
+
 def _check(status: int, what: str) -> None:
     if status != abi.CA_OK:
         raise CasimError(status, what)
@@ -455,7 +463,7 @@ class RemovalPlan:
         dest = self._dest.array if want_dest else None
         _check(self.lib.ca_removal_plan_run(self.h, ptr(h) if h is not None else None, C.byref(li), ptr(self.results),
                                             ptr(dest) if dest is not None else None), "ca_removal_plan_run")
-        return RemovalOutput(self.results.copy(), dest[: len(self.moves)].copy() if dest is not None else None, h,
+        return RemovalOutput(_fast_copy(self.results), dest[: len(self.moves)].copy() if dest is not None else None, h,
                              li.value)
 
     def close(self) -> None:
@@ -557,11 +565,11 @@ class EstimatePlan:
         if device_results:
             _check(self.lib.ca_estimate_plan_run(self.h, C.byref(lim), C.byref(li), ptr(self.results), None, None),
                    "ca_estimate_plan_run")
-            return EstimateOutput(self.results.copy() if copy else self.results, None, None, li.value)
+            return EstimateOutput(_fast_copy(self.results) if copy else self.results, None, None, li.value)
         _check(self.lib.ca_estimate_plan_run(self.h, C.byref(lim), C.byref(li), ptr(self.results),
                                              ptr(self.sched_pod), ptr(self.sched_node) if want_nodes else None),
                "ca_estimate_plan_run")
-        f = (lambda a: a.copy()) if copy else (lambda a: a)
+        f = _fast_copy if copy else (lambda a: a)
         return EstimateOutput(f(self.results), f(self.sched_pod[: self.total]), f(self.sched_node[: self.total]),
                               li.value)
 
@@ -715,7 +723,7 @@ class MultiEstimatePlan:
         _check(self.lib.ca_multi_estimate_plan_run(self.h, C.byref(lim), C.byref(li), ptr(self.results),
                                                    ptr(self.sched_pod), ptr(self.sched_node) if want_nodes else None),
                "ca_multi_estimate_plan_run")
-        f = (lambda a: a.copy()) if copy else (lambda a: a)
+        f = _fast_copy if copy else (lambda a: a)
         return EstimateOutput(f(self.results), f(self.sched_pod[: self.total]), f(self.sched_node[: self.total]),
                               li.value)
 
@@ -762,7 +770,7 @@ class MultiRemovalPlan:
         li = C.c_int32(last_index)
         _check(self.lib.ca_multi_removal_plan_run(self.h, ptr(hints), len(hints), C.byref(li), ptr(self.results),
                                                   ptr(dest)), "ca_multi_removal_plan_run")
-        return RemovalOutput(self.results.copy(), dest[: len(self.moves)], hints, li.value)
+        return RemovalOutput(_fast_copy(self.results), dest[: len(self.moves)], hints, li.value)
 
     def stats(self) -> dict:
         nb, rr = C.c_int32(0), C.c_int32(0)

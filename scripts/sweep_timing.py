@@ -50,3 +50,20 @@ with native.RemovalPlan(m, *args) as plan:
     top = np.argsort(-us)[:8]
     print("slowest:", [(int(c), round(float(us[c]), 1), int(pods[c])) for c in top])
     print("us per moved pod p50", round(float(np.median(us[ran] / np.maximum(pods[ran], 1))), 2))
+
+# where the wrapper's time goes: the bare C call vs RemovalPlan.run
+import ctypes as C  # noqa: E402
+from autoscaler_amd.abi import ptr  # noqa: E402
+with native.RemovalPlan(m, *args) as plan:
+    res = np.zeros(len(w.candidates), plan.results.dtype)
+    bare, full = [], []
+    for _ in range(12):
+        li = C.c_int32(0)
+        t = time.perf_counter()
+        m.lib.ca_removal_plan_run(plan.h, None, C.byref(li), ptr(res), None)
+        bare.append((time.perf_counter() - t) * 1e3)
+        t = time.perf_counter()
+        plan.run(0)
+        full.append((time.perf_counter() - t) * 1e3)
+    print("hinted: bare C call ms", round(float(np.median(bare)), 3), "RemovalPlan.run ms",
+          round(float(np.median(full)), 3), "lib total", round(m.removal_stats()["total_ms"], 3))

@@ -1,5 +1,7 @@
 """The C2 Estimate step, device-resident results, exactly STEPS times: the program the
-rocprofv3 --pmc passes of scripts/gpu_round.sh count (traffic per step = total / STEPS)."""
+rocprofv3 --pmc passes of scripts/gpu_round.sh count (traffic per step = total / STEPS).
+PMC_LEGS=all also runs STEPS C5 FilterOutSchedulable calls (fork/revert around each) and
+STEPS fresh C3 sweeps, so their kernels (k_fb_walk, k_sweep, k_sweep_table) are counted."""
 import os
 import sys
 
@@ -15,3 +17,21 @@ with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as pla
     for _ in range(STEPS):
         plan.run(w.max_nodes, 0, copy=False, device_results=True)
 m.close()
+if os.environ.get("PMC_LEGS") == "all":
+    import numpy as np
+    f = W.c5_filter()
+    g = native.Mirror(0)
+    W.load_filter(g, f)
+    for _ in range(STEPS):
+        g.fork()
+        g.filter_out_schedulable(f.pending, f.order, f.class_owner, f.hints, 0)
+        g.revert()
+    g.close()
+    s3 = W.c3()
+    m3 = native.Mirror(0)
+    W.load_sweep(m3, s3)
+    with native.RemovalPlan(m3, s3.candidates, s3.dest_mask, s3.cand_status, s3.move_off, s3.move_pods) as rp:
+        for _ in range(STEPS):
+            m3.set_hints(np.full(len(s3.table), -1, np.int32))
+            rp.run(0)
+    m3.close()

@@ -16,6 +16,8 @@ def load(root: str, counter: str) -> dict:
             if r.get("Counter_Name") != counter:
                 continue
             name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+            name = name[5:] if name.startswith("void ") else name          # template kernels
+            name = name.split("<")[0]
             per[(name, r.get("Dispatch_Id", r.get("Correlation_Id", "")))].append(float(r["Counter_Value"]))
     out = defaultdict(list)
     for (name, _), vals in per.items():
@@ -23,7 +25,8 @@ def load(root: str, counter: str) -> dict:
     return out
 
 
-def main(root: str, steps: int, what: str = "scripts/pmc_step.py (C2 Estimate steps, results in HBM)") -> None:
+def main(root: str, steps: int, what: str = "scripts/pmc_step.py PMC_LEGS=all (C2 Estimate steps with results in HBM, "
+                                           "C5 FilterOutSchedulable calls, fresh C3 sweeps)") -> None:
     fetch = load(root, "FETCH_SIZE")
     write = load(root, "WRITE_SIZE")
     res = {}

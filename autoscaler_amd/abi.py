@@ -119,6 +119,13 @@ REMOVAL_RESULT_DTYPE = np.dtype([
     ("removable", "<i4"), ("reason", "<i4"), ("n_placed", "<i4"), ("last_index_in", "<i4"), ("evals", "<u8"),
 ], align=True)
 
+# planner (include/casim.h ca_plan_*)
+PLAN_RESULT_DTYPE = np.dtype([
+    ("removable", "<i4"), ("reason", "<i4"), ("n_placed", "<i4"), ("last_index_in", "<i4"), ("evals", "<u8"),
+    ("first_move", "<i4"), ("n_moves", "<i4"), ("blocking_pod", "<i4"), ("risky", "<i4"),
+], align=True)
+PLAN_MOVE_DTYPE = np.dtype([("candidate", "<i4"), ("pod", "<i4"), ("new_pod", "<i4"), ("node", "<i4")])
+
 # scale-down eligibility (include/casim.h ca_util_*)
 CA_UTIL_CPU, CA_UTIL_MEM, CA_UTIL_GPU = 0, 1, 2
 CA_UNODE_HAS_CPU, CA_UNODE_HAS_MEM, CA_UNODE_HAS_GPU, CA_UNODE_GPU_CONFIG = 0x1, 0x2, 0x4, 0x8
@@ -159,12 +166,17 @@ class LimiterC(C.Structure):
     _fields_ = [("max_nodes", C.c_int32), ("reserved", C.c_int32)]
 
 
+class PdbTableC(C.Structure):
+    _fields_ = [("n_pdbs", C.c_int32), ("allowed", C.c_void_p), ("pod_off", C.c_void_p), ("pod_pdb", C.c_void_p)]
+
+
 # sizes in ca_abi_struct_sizes order
 EXPECTED_SIZES = [
     NODE_DTYPE.itemsize, POD_DTYPE.itemsize, REQ_DTYPE.itemsize, TERM_DTYPE.itemsize,
     C.sizeof(PodTableC), C.sizeof(MatchSpecC), C.sizeof(PredResultC), TEMPLATE_DTYPE.itemsize,
     C.sizeof(LimiterC), ESTIMATE_RESULT_DTYPE.itemsize, REMOVAL_RESULT_DTYPE.itemsize,
     UTIL_NODE_DTYPE.itemsize, UTIL_POD_DTYPE.itemsize, UTIL_INFO_DTYPE.itemsize,
+    PLAN_RESULT_DTYPE.itemsize, PLAN_MOVE_DTYPE.itemsize,
 ]
 
 

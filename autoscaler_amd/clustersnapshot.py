@@ -194,6 +194,20 @@ class ClusterSnapshot:
             st.add_pod(pod, node, int(pid))
             self._log.append(("pod", pod, node))
 
+    def record_moves(self, groups: list) -> None:
+        """Moves the backend already committed (the planner, ca_plan_removals), recorded as
+        the ops findPlaceFor + Commit performs (cluster.go:228-242): per removed candidate,
+        RemovePod of every pod to move, then AddPod of each copy on its destination.
+        groups: [(candidate node name, [(pod, copy, destination name, copy's mirror id)])]."""
+        st = self._state
+        for node, moves in groups:
+            for pod, _, _, _ in moves:
+                st.remove_pod(pod.namespace, pod.name, node)
+                self._log.append(("rmpod", pod.namespace, pod.name, node))
+            for _, cp, dest, pid in moves:
+                st.add_pod(cp, dest, int(pid))
+                self._log.append(("pod", cp, dest))
+
     # -- NodeInfos() lister ----------------------------------------------------
     def List(self) -> list:  # noqa: N802
         st = self._state

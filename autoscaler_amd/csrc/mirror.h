@@ -75,6 +75,13 @@ struct RowStage {
     HostBuf h;
 };
 
+// ca_plan_removals (planner.hip): the last call's moves and counters.
+struct PlanStats {
+    int32_t rounds = 0, conflicts = 0, simulated = 0;
+    float total_ms = 0;
+    std::vector<ca_plan_move> moves;
+};
+
 struct Stats {
     int32_t rounds = 0;
     float kernel_ms = 0, sort_ms = 0, total_ms = 0;
@@ -120,6 +127,7 @@ struct ca_mirror {
     casim::DevBuf d_mask;                  // per-node match mask
     std::vector<uint8_t> h_scratch;
     casim::Stats sweep_stats;
+    casim::PlanStats plan;
     casim::SweepScratch sw;
     casim::FilterScratch fo;
     casim::RowStage rs;
@@ -136,6 +144,7 @@ struct ca_mirror {
     void node_apply(int32_t node, const ca_pod_spec& p, int sign);
     void add_pod_to_node(int32_t pod, int32_t node);
     int32_t store_pod(const ca_pod_table* t, int32_t idx, int32_t node);
+    int32_t store_moved_copy(int32_t pod);  // the copy findPlaceFor schedules (cluster.go:235-240)
     void journal_push(int32_t kind, int32_t node, int32_t pod, int32_t slot, const uint64_t* ports);
     void fill_hot(int32_t i, casim::NodeHot& h) const;
     void fill_ext(int32_t i, casim::NodeExt& e) const;

@@ -143,13 +143,19 @@ def get_pods_for_deletion_on_node_drain(pods: list, pdbs: list, skip_system: boo
     return out, ds, None, None
 
 
+def pdb_matches(pdb: "PodDisruptionBudget", pod: Pod) -> bool:
+    """Namespace + selector match of checkPdbs / RemainingPdbTracker (drain.go:82, basic.go:71)."""
+    return pod.namespace == pdb.namespace and all(pod.labels.get(k) == v for k, v in pdb.match_labels.items())
+
+
 def get_pods_to_move(node_pods: list, options: NodeDeleteOptions, listers: Optional[ListerRegistry],
-                     pdbs: list, now: float = 0.0):
-    """simulator.GetPodsToMove (CA/simulator/drain.go:50-90)."""
+                     pdbs: list, now: float = 0.0, check_pdbs: bool = True):
+    """simulator.GetPodsToMove (CA/simulator/drain.go:50-90).  check_pdbs=False leaves out the
+    budget check (:64-66), for callers that apply it against changing budgets themselves."""
     pods, ds, blocking, err = get_pods_for_deletion_on_node_drain(
         node_pods, pdbs, options.skip_nodes_with_system_pods, options.skip_nodes_with_local_storage, listers,
         options.min_replica_count, now)
-    if err is not None:
+    if err is not None or not check_pdbs:
         return pods, ds, blocking, err
     for pdb in pdbs:                                   # checkPdbs (:73-90)
         for pod in pods:

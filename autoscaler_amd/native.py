@@ -108,6 +108,9 @@ def load() -> C.CDLL:
         "ca_multi_removal_plan_stats": ([vp, p(i32), p(i32), vp, i32], C.c_int),
         "ca_multi_removal_plan_destroy": ([vp], C.c_int),
         "ca_multi_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, i32, p(i32), vp, vp], C.c_int),
+        "ca_plan_removals": ([vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, i32, p(i32), vp, vp, i32, p(i32)], C.c_int),
+        "ca_plan_last_moves": ([vp, vp, i32], C.c_int),
+        "ca_plan_stats": ([vp, p(i32), p(i32), p(i32), p(C.c_float)], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(lib, name)
@@ -150,6 +153,7 @@ def exported_symbols() -> list[str]:
         "ca_multi_estimate_plan_stats", "ca_multi_estimate_plan_destroy", "ca_multi_estimate_batch",
         "ca_multi_removal_plan_create", "ca_multi_removal_plan_run", "ca_multi_removal_plan_stats",
         "ca_multi_removal_plan_destroy", "ca_multi_find_nodes_to_remove",
+        "ca_plan_removals", "ca_plan_last_moves", "ca_plan_stats",
     ]
 
 
@@ -173,6 +177,58 @@ class RemovalOutput:
     dest: np.ndarray             # int32 [M]
     hints: np.ndarray            # int32 [pods]
     last_index: int
+
+
+@dataclass
+class PlanOutput:
+    results: np.ndarray          # PLAN_RESULT_DTYPE [C]
+    moves: np.ndarray            # PLAN_MOVE_DTYPE [n_moves]
+    hints: np.ndarray            # int32 [pods]
+    last_index: int
+    allowed: np.ndarray          # int32 [n_pdbs]: the PDB budgets after the call
+
+
+@dataclass
+class _PlanArgs:
+    cand: np.ndarray
+    mask: np.ndarray
+    status: np.ndarray
+    off: np.ndarray
+    moves: np.ndarray
+    hints: np.ndarray
+    allowed: np.ndarray
+    pdb_c: object
+    keep: tuple
+    res: np.ndarray
+    out_moves: np.ndarray
+
+    @property
+    def pdb_ptr(self):
+        return None if self.pdb_c is None else C.byref(self.pdb_c)
+
+    def output(self, last_index: int, n_moves: int) -> PlanOutput:
+        return PlanOutput(self.res, self.out_moves[:n_moves], self.hints, last_index, self.allowed)
+
+
+def plan_args(candidates, dest_mask, cand_status, move_off, move_pods, hints, pdb_allowed=None, pdb_pod_off=None,
+              pdb_pod=None) -> _PlanArgs:
+    """Marshal the arguments of ca_plan_removals / or_plan_removals.  PDBs (optional):
+    pdb_allowed[n_pdbs] DisruptionsAllowed, pdb_pod_off/pdb_pod the memberships (CSR by pod id)."""
+    cand = np.ascontiguousarray(candidates, dtype=np.int32)
+    status = np.ascontiguousarray(cand_status if cand_status is not None else np.zeros(len(cand)), dtype=np.int32)
+    moves = np.ascontiguousarray(move_pods, dtype=np.int32)
+    allowed = np.array(pdb_allowed if pdb_allowed is not None else [], dtype=np.int32)
+    pdb_c, keep = None, ()
+    if len(allowed):
+        po = np.ascontiguousarray(pdb_pod_off, dtype=np.int32)
+        pp = np.ascontiguousarray(pdb_pod if len(pdb_pod) else [0], dtype=np.int32)
+        pdb_c = abi.PdbTableC(len(allowed), ptr(allowed), ptr(po), ptr(pp))
+        keep = (po, pp)
+    cap = 4 * len(moves) + 256
+    return _PlanArgs(cand, np.ascontiguousarray(dest_mask, dtype=np.uint8), status,
+                     np.ascontiguousarray(move_off, dtype=np.int32), moves,
+                     np.array(hints, dtype=np.int32, copy=True), allowed, pdb_c, keep,
+                     np.zeros(max(len(cand), 1), abi.PLAN_RESULT_DTYPE), np.zeros(cap, abi.PLAN_MOVE_DTYPE))
 
 
 @dataclass
@@ -409,6 +465,29 @@ class Mirror:
                                                 ptr(moves), ptr(hints), C.byref(li), ptr(res), ptr(dest)),
                "ca_find_nodes_to_remove")
         return RemovalOutput(res, dest[: len(moves)], hints, li.value)
+
+    def plan_removals(self, candidates, dest_mask, cand_status, move_off, move_pods, hints, last_index: int = 0,
+                      max_removable: int = 0, pdb_allowed=None, pdb_pod_off=None, pdb_pod=None) -> PlanOutput:
+        """ca_plan_removals: Planner.categorizeNodes' loop with canPersist=true; commits into
+        the mirror.  hints: per mirror pod (len = the mirror's pod count)."""
+        a = plan_args(candidates, dest_mask, cand_status, move_off, move_pods, hints, pdb_allowed, pdb_pod_off, pdb_pod)
+        li = C.c_int32(last_index)
+        nm = C.c_int32(0)
+        _check(self.lib.ca_plan_removals(self.h, ptr(a.cand), len(a.cand), ptr(a.mask), ptr(a.status), ptr(a.off),
+                                         ptr(a.moves), int(max_removable), a.pdb_ptr, ptr(a.hints), len(a.hints),
+                                         C.byref(li), ptr(a.res), ptr(a.out_moves), len(a.out_moves), C.byref(nm)),
+               "ca_plan_removals")
+        if nm.value > len(a.out_moves):
+            a.out_moves = np.zeros(nm.value, abi.PLAN_MOVE_DTYPE)
+            self.lib.ca_plan_last_moves(self.h, ptr(a.out_moves), nm.value)
+        a.res = a.res[: len(a.cand)]
+        return a.output(li.value, nm.value)
+
+    def plan_stats(self) -> dict:
+        r, c, s = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+        t = C.c_float(0)
+        _check(self.lib.ca_plan_stats(self.h, C.byref(r), C.byref(c), C.byref(s), C.byref(t)), "ca_plan_stats")
+        return {"rounds": r.value, "conflicts": c.value, "simulated": s.value, "total_ms": t.value}
 
     def set_hints(self, hints) -> None:
         """The mirror's resident HintingSimulator hints (node per mirror pod, -1 = none)."""

@@ -593,6 +593,67 @@ int ca_multi_find_nodes_to_remove(ca_multi* mm, const int32_t* candidates, int32
                                   const int32_t* move_pods, int32_t* hints, int32_t n_pods, int32_t* last_index,
                                   ca_removal_result* results, int32_t* out_dest);
 
+/* ---- planner: committing removal simulation ----------------------
+ * Planner.categorizeNodes' simulation loop (CA/core/scaledown/planner/planner.go:252-296)
+ * over a RemovalSimulator built with persistSuccessfulSimulations = true (planner.go:89):
+ * candidates are simulated in order, each by SimulateNodeRemoval (CA/simulator/cluster.go:
+ * 145-184) on the CURRENT snapshot.  A removable candidate's simulation is committed into
+ * the mirror (withForkedSnapshot Commit, cluster.go:204-218): its pods to move leave it
+ * (RemovePod, :228-233) and their copies (Spec.NodeName and TPU requests cleared, :235-240,
+ * tpu.go:57-79) stay on their destinations (AddPod); the node leaves the destination set
+ * (planner.go:280); its pods are charged to the PDB budgets (RemainingPdbTracker.RemovePods,
+ * CA/core/scaledown/pdb/basic.go:86-95).  A later candidate's pods to move are its
+ * caller-given pods followed by the copies committed onto it, in commit order (NodeInfo.Pods
+ * appends).  The loop stops before the next candidate once max_removable candidates are
+ * removable (planner.go:268-271, unneededNodesLimit; <= 0: no limit); the rest are
+ * CA_UNREMOVABLE_NOT_RUN.  Prefix protocol and kernel scope as ca_find_nodes_to_remove. */
+typedef struct ca_plan_result {
+    int32_t  removable;                       /* NodeToBeRemoved, committed              */
+    int32_t  reason;                          /* CA_UNREMOVABLE_*                        */
+    int32_t  n_placed;
+    int32_t  last_index_in;
+    uint64_t evals;
+    int32_t  first_move;                      /* removable: moves[first_move, +n_moves)  */
+    int32_t  n_moves;                         /*   = PodsToReschedule, in order          */
+    int32_t  blocking_pod;                    /* NotEnoughPdb (drain.go checkPdbs): mirror
+                                                 pod id, else -1                          */
+    int32_t  risky;                           /* CanRemovePods inParallel == false
+                                                 (planner.go:274-278, basic.go:66-84)     */
+} ca_plan_result;
+
+typedef struct ca_plan_move {
+    int32_t candidate;                        /* index into candidates[]                 */
+    int32_t pod;                              /* mirror pod id that left the candidate   */
+    int32_t new_pod;                          /* mirror pod id of its copy               */
+    int32_t node;                             /* destination node position               */
+} ca_plan_move;
+
+/* RemainingPdbTracker (basic.go): PDB memberships of the mirror pods (namespace + selector
+ * match, computed by the caller), pdb indices ascending per pod, CSR over pod ids <
+ * n_pods; a copy inherits its original's memberships.  allowed[] = DisruptionsAllowed,
+ * decremented in place.  n_pdbs == 0 (or a NULL table): no PDBs. */
+typedef struct ca_pdb_table {
+    int32_t        n_pdbs;
+    int32_t*       allowed;
+    const int32_t* pod_off;                   /* [n_pods + 1] */
+    const int32_t* pod_pdb;
+} ca_pdb_table;
+
+/* hints[n_pods]: as ca_find_nodes_to_remove, n_pods = the mirror's pod count (a copy's hint
+ * is its destination).  moves[moves_cap]: every committed move in order; *n_moves = their
+ * number (if it exceeds moves_cap the first moves_cap are written and the call still
+ * completes; ca_plan_last_moves returns all of them). */
+int ca_plan_removals(ca_mirror* m, const int32_t* candidates, int32_t n_candidates,
+                     const uint8_t* dest_mask, const int32_t* cand_status,
+                     const int32_t* move_off, const int32_t* move_pods,
+                     int32_t max_removable, const ca_pdb_table* pdbs,
+                     int32_t* hints, int32_t n_pods, int32_t* last_index,
+                     ca_plan_result* results, ca_plan_move* moves, int32_t moves_cap, int32_t* n_moves);
+int ca_plan_last_moves(const ca_mirror* m, ca_plan_move* out, int32_t cap);
+/* last call: speculation rounds, rounds cut short by a commit conflict, candidates
+ * simulated on the device (all rounds), host wall time (ms) */
+int ca_plan_stats(const ca_mirror* m, int32_t* rounds, int32_t* conflicts, int32_t* simulated, float* total_ms);
+
 #ifdef __cplusplus
 }
 #endif

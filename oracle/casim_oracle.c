@@ -941,6 +941,122 @@ int or_find_nodes_to_remove(or_state* s, const int32_t* candidates, int32_t n_ca
     return CA_OK;
 }
 
+/* ------------------------------------------------------------------------- */
+/* Planner.categorizeNodes with canPersist=true (planner.go:252-296)           */
+/* ------------------------------------------------------------------------- */
+static int pdb_member(const ca_pdb_table* t, const int32_t* origin, int32_t pod, int32_t pdb) {
+    const int32_t o = origin[pod];
+    for (int32_t k = t->pod_off[o]; k < t->pod_off[o + 1]; k++)
+        if (t->pod_pdb[k] == pdb) return 1;
+    return 0;
+}
+
+int or_plan_removals(or_state* s, const int32_t* candidates, int32_t n_candidates,
+                     const uint8_t* dest_mask, const int32_t* cand_status,
+                     const int32_t* move_off, const int32_t* move_pods,
+                     int32_t max_removable, const ca_pdb_table* pdbs,
+                     int32_t* hints, int32_t n_pods, int32_t* last_index,
+                     ca_plan_result* results, ca_plan_move* moves, int32_t moves_cap, int32_t* n_moves) {
+    if (n_candidates < 0 || n_pods < 0 || n_pods > s->pods.n) return CA_EINVAL;   /* past n_pods: detached */
+    if (s->scope_blockers > 0 && n_candidates > 0) return CA_EUNSUPPORTED;
+    const int32_t N = (int32_t)s->nodes.n;
+    const int P = pdbs ? pdbs->n_pdbs : 0;
+    uint8_t* mask = malloc((size_t)N + 1);                  /* podDestinations (planner.go:280) */
+    memcpy(mask, dest_mask, (size_t)N);
+    /* Hints by pod key: a copy shares its original's key (hints.go:31-37) */
+    VEC(int32_t) H = {0};
+    VEC(int32_t) origin = {0};                              /* pod id -> caller pod id (PDBs) */
+    for (int32_t i = 0; i < (int32_t)s->pods.n; i++) {
+        VEC_PUSH(H, hints && i < n_pods ? hints[i] : -1);
+        VEC_PUSH(origin, i);
+    }
+    /* copies committed onto a node, in commit order (NodeInfo.Pods appends) */
+    vec_i32* extra = calloc((size_t)N + 1, sizeof(vec_i32));
+    vec_i32 list = {0};
+    int32_t removed = 0, cut = 0, nm = 0;
+    for (int32_t ci = 0; ci < n_candidates; ci++) {
+        ca_plan_result* r = &results[ci];
+        memset(r, 0, sizeof *r);
+        r->last_index_in = *last_index;
+        r->first_move = nm;
+        r->blocking_pod = -1;
+        if (cut || (max_removable > 0 && removed >= max_removable)) {          /* :268-271 */
+            r->reason = CA_UNREMOVABLE_NOT_RUN;
+            cut = 1;
+            continue;
+        }
+        const int32_t node = candidates[ci];
+        const int valid = node >= 0 && node < N && mask[node];
+        list.n = 0;
+        for (int32_t i = move_off[ci]; i < move_off[ci + 1]; i++) VEC_PUSH(list, move_pods[i]);
+        if (node >= 0 && node < N)
+            for (int64_t i = 0; i < extra[node].n; i++) VEC_PUSH(list, extra[node].a[i]);
+        if (valid && !(cand_status && cand_status[ci] != 0)) {
+            for (int64_t i = 0; i < list.n && !cut; i++)
+                if (s->pods.a[list.a[i]].spec.flags & CA_POD_OUT_OF_SCOPE) cut = 1;
+            if (cut) { r->reason = CA_UNREMOVABLE_OUT_OF_SCOPE; continue; }   /* casim.h scope */
+        }
+        if (!valid) { r->reason = CA_UNREMOVABLE_UNEXPECTED_ERROR; continue; } /* cluster.go:157-160 */
+        if (cand_status && cand_status[ci] != 0) { r->reason = cand_status[ci]; continue; }
+        /* GetPodsToMove's checkPdbs against the remaining budgets (drain.go:73-90) */
+        for (int p = 0; p < P && r->blocking_pod < 0; p++) {
+            if (pdbs->allowed[p] >= 1) continue;
+            for (int64_t i = 0; i < list.n; i++)
+                if (pdb_member(pdbs, origin.a, list.a[i], p)) { r->blocking_pod = list.a[i]; break; }
+        }
+        if (r->blocking_pod >= 0) { r->reason = CA_UNREMOVABLE_BLOCKED_BY_POD; continue; }
+        /* withForkedSnapshot(findPlaceFor) (cluster.go:171-173, :204-218) */
+        const int64_t pods_before = s->pods.n;
+        int32_t* dest = malloc(sizeof(int32_t) * (size_t)(list.n + 1));
+        or_fork(s);
+        for (int64_t i = 0; i < list.n; i++) or_remove_pod(s, list.a[i]);           /* :228-233 */
+        ca_match_spec m;
+        memset(&m, 0, sizeof m);
+        m.kind = CA_MATCH_MASK; m.mask = mask; m.exclude = node;                    /* :221-223 */
+        const int32_t placed = or_try_schedule_pods(s, list.a, (int32_t)list.n, &m, 1, H.a, last_index, dest,
+                                                    &r->evals);
+        r->n_placed = placed;
+        if (placed == list.n) {
+            or_commit(s);                                                            /* :207-211 */
+            r->removable = 1;
+            r->reason = CA_UNREMOVABLE_NONE;
+            r->n_moves = placed;
+            for (int32_t i = 0; i < placed; i++) {                /* copies pods_before + i, in order */
+                const int32_t nid = (int32_t)(pods_before + i);
+                VEC_PUSH(H, dest[i]);
+                VEC_PUSH(origin, origin.a[list.a[i]]);
+                VEC_PUSH(extra[dest[i]], nid);
+                if (nm < moves_cap) {
+                    moves[nm].candidate = ci; moves[nm].pod = list.a[i];
+                    moves[nm].new_pod = nid; moves[nm].node = dest[i];
+                }
+                nm++;
+            }
+            mask[node] = 0;                                                          /* planner.go:280 */
+            removed++;
+            /* CanRemovePods (basic.go:66-84) then RemovePods (:86-95) */
+            for (int p = 0; p < P; p++) {
+                int32_t count = 0;
+                for (int64_t i = 0; i < list.n; i++)
+                    if (pdb_member(pdbs, origin.a, list.a[i], p) && pdbs->allowed[p] < ++count) r->risky = 1;
+            }
+            for (int p = 0; p < P; p++)
+                for (int64_t i = 0; i < list.n; i++)
+                    if (pdb_member(pdbs, origin.a, list.a[i], p)) pdbs->allowed[p]--;
+        } else {
+            or_revert(s);
+            s->pods.n = pods_before;
+            r->reason = CA_UNREMOVABLE_NO_PLACE;                                     /* :174-177 */
+        }
+        free(dest);
+    }
+    if (hints) memcpy(hints, H.a, sizeof(int32_t) * (size_t)n_pods);
+    if (n_moves) *n_moves = nm;
+    for (int32_t i = 0; i < N; i++) free(extra[i].a);
+    free(extra); free(list.a); free(H.a); free(origin.a); free(mask);
+    return CA_OK;
+}
+
 /* ---------------------------------------------------------------------------
  * Scale-down eligibility: utilization.Calculate + FindEmptyNodesToRemove
  * ------------------------------------------------------------------------- */

@@ -90,6 +90,13 @@ int or_find_nodes_to_remove(or_state* s, const int32_t* candidates, int32_t n_ca
                             const int32_t* move_off, const int32_t* move_pods,
                             int32_t* hints, int32_t* last_index,
                             ca_removal_result* results, int32_t* out_dest);
+/* Planner.categorizeNodes' loop, canPersist=true (ca_plan_removals semantics) */
+int or_plan_removals(or_state* s, const int32_t* candidates, int32_t n_candidates,
+                     const uint8_t* dest_mask, const int32_t* cand_status,
+                     const int32_t* move_off, const int32_t* move_pods,
+                     int32_t max_removable, const ca_pdb_table* pdbs,
+                     int32_t* hints, int32_t n_pods, int32_t* last_index,
+                     ca_plan_result* results, ca_plan_move* moves, int32_t moves_cap, int32_t* n_moves);
 
 #ifdef __cplusplus
 }

@@ -14,7 +14,7 @@ import numpy as np
 
 from autoscaler_amd import abi
 from autoscaler_amd.abi import ptr
-from autoscaler_amd.native import EstimateOutput, FilterOutput, RemovalOutput, filter_args
+from autoscaler_amd.native import EstimateOutput, FilterOutput, PlanOutput, RemovalOutput, filter_args, plan_args
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libcasim_oracle.so")
@@ -54,6 +54,7 @@ def load() -> C.CDLL:
         "or_estimate": ([vp, vp, vp, vp, vp, i32, vp, p(i32), vp, vp, vp], C.c_int),
         "or_try_schedule_pods": ([vp, vp, i32, vp, i32, vp, p(i32), vp, p(C.c_uint64)], C.c_int),
         "or_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, p(i32), vp, vp], C.c_int),
+        "or_plan_removals": ([vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, i32, p(i32), vp, vp, i32, p(i32)], C.c_int),
         "or_filter_out_schedulable": ([vp, vp, vp, i32, vp, i32, vp, p(i32), vp, vp, p(i32), p(C.c_uint64), p(i32)],
                                       C.c_int),
     }
@@ -228,6 +229,20 @@ class OracleState:
                                                 ptr(moves), ptr(hints), C.byref(li), ptr(res), ptr(dest)),
                "find_nodes_to_remove")
         return RemovalOutput(res, dest[: len(moves)], hints, li.value)
+
+    def plan_removals(self, candidates, dest_mask, cand_status, move_off, move_pods, hints, last_index: int = 0,
+                      max_removable: int = 0, pdb_allowed=None, pdb_pod_off=None, pdb_pod=None) -> PlanOutput:
+        a = plan_args(candidates, dest_mask, cand_status, move_off, move_pods, hints, pdb_allowed, pdb_pod_off, pdb_pod)
+        li = C.c_int32(last_index)
+        nm = C.c_int32(0)
+        _check(self.lib.or_plan_removals(self.h, ptr(a.cand), len(a.cand), ptr(a.mask), ptr(a.status), ptr(a.off),
+                                         ptr(a.moves), int(max_removable), a.pdb_ptr, ptr(a.hints), len(a.hints),
+                                         C.byref(li), ptr(a.res), ptr(a.out_moves), len(a.out_moves), C.byref(nm)),
+               "plan_removals")
+        if nm.value > len(a.out_moves):     # (the commits are made: a bigger buffer cannot re-run them)
+            raise OracleError(abi.CA_ECAPACITY, "plan_removals moves")
+        a.res = a.res[: len(a.cand)]
+        return a.output(li.value, nm.value)
 
 
 def go_sort_desc(keys) -> np.ndarray:

@@ -189,6 +189,29 @@ int main(void) {
     CHECK(ca_mirror_node_count(m, &nn));
     EXPECT(nn == 3);
 
+    /* planner (canPersist=true) inside a fork: n2 is removed first (p1 -> n1, p2 -> n3,
+     * committed), so n3's pods to move are p3 and the copy of p2; n2 is no destination any
+     * more: p3 -> n1, p2's copy -> n1 (its hint, n3 itself, is checked but not acceptable) */
+    CHECK(ca_mirror_fork(m));
+    ca_plan_result pr2[2];
+    ca_plan_move mv[8];
+    int32_t hints3[3] = {-1, -1, -1}, nmv = 0;
+    li = 0;
+    CHECK(ca_plan_removals(m, cand, 2, dest, st, moff, moves, 0, NULL, hints3, 3, &li, pr2, mv, 8, &nmv));
+    printf("plan_removals removable %d %d moves %d evals %llu %llu last_index %d\n", pr2[0].removable,
+           pr2[1].removable, nmv, (unsigned long long)pr2[0].evals, (unsigned long long)pr2[1].evals, li);
+    EXPECT(pr2[0].removable == 1 && pr2[1].removable == 1 && nmv == 4 && li == 1);
+    EXPECT(pr2[0].first_move == 0 && pr2[0].n_moves == 2 && pr2[1].first_move == 2 && pr2[1].n_moves == 2);
+    EXPECT(mv[0].pod == ids[0] && mv[0].node == 0 && mv[1].pod == ids[1] && mv[1].node == 2);
+    EXPECT(mv[2].pod == ids[2] && mv[2].node == 0 && mv[3].pod == mv[1].new_pod && mv[3].node == 0);
+    EXPECT(pr2[0].evals == 2 && pr2[1].evals == 3);
+    int32_t on_n1[8], k1 = 0;
+    CHECK(ca_mirror_node_pods(m, 0, on_n1, 8, &k1));
+    EXPECT(k1 == 3);                                       /* p1', p3', p2'' */
+    CHECK(ca_mirror_revert(m));
+    CHECK(ca_mirror_node_pods(m, 0, on_n1, 8, &k1));
+    EXPECT(k1 == 0);
+
     CHECK(ca_podset_destroy(ps));
     CHECK(ca_podset_destroy(ps2));
     CHECK(ca_mirror_destroy(m));

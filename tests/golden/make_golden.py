@@ -307,6 +307,128 @@ cases.append({
     ],
 })
 
+# ---- planner: TestUpdateClusterState / TestUpdateClusterStatUnneededNodesLimit -------
+# Planner.UpdateClusterState with canPersist=true (planner.go:103-126,252-296): nodes are
+# BuildTestNode(name, cpu, 10); nodeUndergoingDeletion adds the ToBeDeleted NoSchedule taint
+# (planner_test.go:661-666); the ReplicaSet lister holds generateReplicaSets("rs", 5) unless
+# a case says otherwise (:474-476, :619-657: spec replicas, status replicas).  Destinations
+# and candidates are all nodes (:506); the eligibility checker is the fake one (:688-705).
+PLN = "CA/core/scaledown/planner/planner_test.go"
+TBD = ["ToBeDeletedByClusterAutoscaler", "", "NoSchedule"]
+
+
+def pl_node(name, cpu, deleting=False):
+    return test_node(name, cpu, 10, **({"taints": [TBD]} if deleting else {}))
+
+
+def pl_pod(name, cpu, node, kind="rs", owner="rs"):
+    d = test_pod(name, cpu, 1, node=node)
+    if kind == "rs":
+        d["owner"] = ["ReplicaSet", owner]
+    elif kind == "ds":
+        d["owner"] = ["DaemonSet", "ds"]
+    elif kind == "static":
+        d["annotations"] = {"kubernetes.io/config.source": "file"}
+    elif kind == "mirror":
+        d["annotations"] = {"kubernetes.io/config.mirror": "mirror"}
+    return d
+
+
+RS5 = {"rs": [5, 0]}
+for name, line, nodes, pods, evictions, eligible, unneeded, unremovable, rsets in [
+    ("empty nodes, all eligible", "58-67", [pl_node("n1", 1000), pl_node("n2", 1000), pl_node("n3", 1000)], [], [],
+     ["n1", "n2", "n3"], ["n1", "n2", "n3"], [], RS5),
+    ("empty nodes, some eligible", "68-79", [pl_node("n1", 1000), pl_node("n2", 1000), pl_node("n3", 1000)], [], [],
+     ["n1", "n2"], ["n1", "n2"], ["n3"], RS5),
+    ("empty nodes, none eligible", "80-91", [pl_node("n1", 1000), pl_node("n2", 1000), pl_node("n3", 1000)], [], [],
+     [], [], ["n1", "n2", "n3"], RS5),
+    ("single utilised node, not eligible", "92-104", [pl_node("n1", 1000)], [pl_pod("p1", 500, "n1")], [],
+     ["n1"], [], ["n1"], RS5),
+    ("pods cannot schedule on node undergoing deletion, not eligible", "105-119",
+     [pl_node("n1", 1000), pl_node("n2", 1000, True)], [pl_pod("p1", 500, "n1"), pl_pod("p2", 500, "n1")], [],
+     ["n1"], [], ["n1", "n2"], RS5),
+    ("pods can schedule on non-eligible node, eligible", "120-134", [pl_node("n1", 1000), pl_node("n2", 1000)],
+     [pl_pod("p1", 500, "n1"), pl_pod("p2", 500, "n1")], [], ["n1"], ["n1"], ["n2"], RS5),
+    ("pods can schedule on eligible node, eligible", "135-149", [pl_node("n1", 1000), pl_node("n2", 1000)],
+     [pl_pod("p1", 500, "n1"), pl_pod("p2", 500, "n1")], [], ["n1", "n2"], ["n1"], ["n2"], RS5),
+    ("pods cannot schedule anywhere, not eligible", "150-166",
+     [pl_node("n1", 2000), pl_node("n2", 1000), pl_node("n3", 500)],
+     [pl_pod("p1", 1000, "n1"), pl_pod("p2", 1000, "n1"), pl_pod("p3", 1000, "n2")], [],
+     ["n1", "n2"], [], ["n1", "n2", "n3"], RS5),
+    ("all pods from multiple nodes can schedule elsewhere, all eligible", "167-184",
+     [pl_node("n1", 1000), pl_node("n2", 1000), pl_node("n3", 2000)],
+     [pl_pod("p1", 500, "n1"), pl_pod("p2", 500, "n1"), pl_pod("p3", 500, "n2"), pl_pod("p4", 500, "n2")], [],
+     ["n1", "n2"], ["n1", "n2"], ["n3"], RS5),
+    ("some pods from multiple nodes can schedule elsewhere, some eligible", "185-202",
+     [pl_node("n1", 2000), pl_node("n2", 1000), pl_node("n3", 1000)],
+     [pl_pod("p1", 1000, "n1"), pl_pod("p2", 1000, "n1"), pl_pod("p3", 500, "n2"), pl_pod("p4", 500, "n2")], [],
+     ["n1", "n2"], ["n2"], ["n1", "n3"], RS5),
+    ("no pods from multiple nodes can schedule elsewhere, no eligible", "203-220",
+     [pl_node("n1", 1000), pl_node("n2", 1000), pl_node("n3", 500)],
+     [pl_pod("p1", 500, "n1"), pl_pod("p2", 500, "n1"), pl_pod("p3", 500, "n2"), pl_pod("p4", 500, "n2")], [],
+     ["n1", "n2"], [], ["n1", "n2", "n3"], RS5),
+    ("recently evicted RS pod, not eligible", "221-235", [pl_node("n1", 1000), pl_node("n2", 2000, True)], [],
+     [pl_pod("p1", 500, "n2")], ["n1"], [], ["n1", "n2"], RS5),
+    ("recently evicted pod without owner, not eligible", "236-249", [pl_node("n1", 1000)], [],
+     [pl_pod("p1", 1000, "", kind="none")], ["n1"], [], ["n1"], RS5),
+    ("recently evicted static pod, eligible", "250-264", [pl_node("n1", 1000), pl_node("n2", 2000, True)], [],
+     [pl_pod("p1", 500, "n2", kind="static")], ["n1"], ["n1"], ["n2"], RS5),
+    ("recently evicted mirror pod, eligible", "265-279", [pl_node("n1", 1000), pl_node("n2", 2000, True)], [],
+     [pl_pod("p1", 500, "n2", kind="mirror")], ["n1"], ["n1"], ["n2"], RS5),
+    ("recently evicted DS pod, eligible", "280-294", [pl_node("n1", 1000), pl_node("n2", 2000, True)], [],
+     [pl_pod("p1", 500, "n2", kind="ds")], ["n1"], ["n1"], ["n2"], RS5),
+    ("recently evicted pod can schedule on non-eligible node, eligible", "295-310",
+     [pl_node("n1", 1000), pl_node("n2", 1000), pl_node("n3", 1000, True)], [], [pl_pod("p1", 500, "n3")],
+     ["n1"], ["n1"], ["n2", "n3"], RS5),
+    ("recently evicted pod can schedule on eligible node, eligible", "311-326",
+     [pl_node("n1", 1000), pl_node("n2", 1000), pl_node("n3", 1000, True)], [], [pl_pod("p1", 500, "n3")],
+     ["n1", "n2"], ["n1"], ["n2", "n3"], RS5),
+    ("recently evicted pod too large to schedule anywhere, all eligible", "327-342",
+     [pl_node("n1", 1000), pl_node("n2", 1000), pl_node("n3", 2000, True)], [], [pl_pod("p1", 2000, "n3")],
+     ["n1", "n2"], ["n1", "n2"], ["n3"], RS5),
+    ("all recently evicted pod got rescheduled, all eligible", "343-360",
+     [pl_node("n1", 1000), pl_node("n2", 1000), pl_node("n3", 2000, True)], [],
+     [pl_pod("p1", 1000, "n3", owner="rs1"), pl_pod("p2", 1000, "n3", owner="rs1")],
+     ["n1", "n2"], ["n1", "n2"], ["n3"], {"rs1": [2, 2], "rs": [5, 0]}),
+    ("some recently evicted pod got rescheduled, some eligible", "361-378",
+     [pl_node("n1", 1000), pl_node("n2", 1000), pl_node("n3", 2000, True)], [],
+     [pl_pod("p1", 1000, "n3", owner="rs1"), pl_pod("p2", 1000, "n3", owner="rs1")],
+     ["n1", "n2"], ["n1"], ["n2", "n3"], {"rs1": [2, 1], "rs": [5, 0]}),
+    ("no recently evicted pod got rescheduled, no eligible", "379-396",
+     [pl_node("n1", 1000), pl_node("n2", 1000), pl_node("n3", 2000, True)], [],
+     [pl_pod("p1", 1000, "n3", owner="rs1"), pl_pod("p2", 1000, "n3", owner="rs1")],
+     ["n1", "n2"], [], ["n1", "n2", "n3"], {"rs1": [2, 0], "rs": [5, 0]}),
+    ("all scheduled and recently evicted pods can schedule elsewhere, all eligible", "397-417",
+     [pl_node("n1", 1000), pl_node("n2", 1000), pl_node("n3", 1000), pl_node("n4", 2000, True)],
+     [pl_pod("p1", 250, "n1")], [pl_pod("p2", 250, "n4"), pl_pod("p3", 250, "n4")],
+     ["n1", "n2"], ["n1", "n2"], ["n3", "n4"], RS5),
+    ("some scheduled and recently evicted pods can schedule elsewhere, some eligible", "418-438",
+     [pl_node("n1", 1000), pl_node("n2", 1000), pl_node("n3", 1000), pl_node("n4", 2000, True)],
+     [pl_pod("p1", 500, "n1")], [pl_pod("p2", 500, "n4"), pl_pod("p3", 500, "n4")],
+     ["n1", "n2"], ["n1"], ["n2", "n3", "n4"], RS5),
+    ("scheduled and recently evicted pods take all capacity, no eligible", "439-459",
+     [pl_node("n1", 1000), pl_node("n2", 1000), pl_node("n3", 1000), pl_node("n4", 2000, True)],
+     [pl_pod("p1", 1000, "n1")], [pl_pod("p2", 1000, "n4"), pl_pod("p3", 1000, "n4")],
+     ["n1", "n2"], [], ["n1", "n2", "n3", "n4"], RS5),
+]:
+    cases.append({"id": f"planner/{name}", "source": f"{PLN}:{line},471-512", "kind": "planner",
+                  "nodes": nodes, "pods": pods, "evictions": evictions, "eligible": eligible,
+                  "replicas": rsets, "listers": {"ReplicaSet": [["default", k, v[0]] for k, v in rsets.items()]},
+                  "expect": {"unneeded": unneeded, "unremovable": unremovable}})
+
+for name, line, prev, maxp, unneeded_s, interval_s, want in [
+    ("no unneeded, default settings", "526-534", 0, 10, 60, 10, 20),
+    ("some unneeded, default settings", "535-543", 3, 10, 60, 10, 23),
+    ("max unneeded, default settings", "544-552", 70, 10, 60, 10, 70),
+    ("too many unneeded, default settings", "553-561", 77, 10, 60, 10, 70),
+    ("instant kill nodes", "562-570", 0, 10, 0, 10, 20),
+    ("quick loops", "571-579", 13, 10, 60, 1, 33),
+    ("slow loops", "580-588", 13, 10, 60, 30, 30),
+]:
+    cases.append({"id": f"planner_limit/{name}", "source": f"{PLN}:{line},590-614", "kind": "planner_limit",
+                  "n_nodes": 100, "previously_unneeded": prev, "max_parallelism": maxp,
+                  "unneeded_time_s": unneeded_s, "update_interval_s": interval_s, "expect": {"unneeded_count": want}})
+
 if __name__ == "__main__":
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_cases.json")
     with open(out, "w") as f:

@@ -11,7 +11,8 @@ from autoscaler_amd.drain import ListerRegistry, NodeDeleteOptions
 from autoscaler_amd.estimator import BinpackingNodeEstimator, ThresholdBasedEstimationLimiter, UnsupportedByKernels
 from autoscaler_amd.podlistprocessor import NewFilterOutSchedulablePodListProcessor
 from autoscaler_amd.predicatechecker import SchedulerBasedPredicateChecker
-from autoscaler_amd.simulator import HintingSimulator, RemovalSimulator
+from autoscaler_amd.planner import Planner
+from autoscaler_amd.simulator import HintingSimulator, NodeToBeRemoved, RemovalSimulator
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -225,7 +226,6 @@ def run_case(case: dict, make_backend):
         rs = RemovalSimulator(listers, snap, checker, None, NodeDeleteOptions(False, False, 0), False)
         sd = ScaleDown(snap, rs, groups, opts, calculate_all=_calculate_all(snap.backend))
         from autoscaler_amd.legacy import UnremovableNodes
-        from autoscaler_amd.simulator import NodeToBeRemoved
         for step in case["steps"]:
             tag = f"step {step['line']}"
             if step.get("reset_unremovable"):
@@ -251,6 +251,44 @@ def run_case(case: dict, make_backend):
                     errs.append(f"{tag}: utilization of {n} present")
             if "unremovable_count" in e and len(sd.unremovable_nodes.AsList()) != e["unremovable_count"]:
                 errs.append(f"{tag}: {len(sd.unremovable_nodes.AsList())} unremovable != {e['unremovable_count']}")
+    elif kind == "planner":
+        nodes = [build_node(n) for n in case["nodes"]]
+        snap.AddNodes(nodes)
+        for pd in case["pods"]:
+            snap.AddPod(build_pod(pd), pd["node"])
+        listers = ListerRegistry({k: {(ns, n): r for ns, n, r in v} for k, v in case["listers"].items()})
+        reps = case["replicas"]
+
+        def replicas(ref, ns):                        # controllerReplicasCalculator over the listers
+            return tuple(reps[ref.name]) if ref.kind == "ReplicaSet" and ref.name in reps else None
+        eligible = set(case["eligible"])
+        pl = Planner(snap, checker, NodeDeleteOptions(False, False, 0), listers, max_scale_down_parallelism=10,
+                     scale_down_unneeded_time=600.0, eligible=lambda names: [n for n in names if n in eligible],
+                     replicas=replicas)
+        names = [n.name for n in nodes]
+        before = [(n, [p.name for p in snap.Get(n).pods]) for n in names]
+        pl.UpdateClusterState(names, names, [build_pod(e) for e in case["evictions"]], 1_700_000_000.0)
+        e = case["expect"]
+        if sorted(pl.UnneededNodes()) != sorted(e["unneeded"]):
+            errs.append(f"unneeded {sorted(pl.UnneededNodes())} != {sorted(e['unneeded'])}")
+        got_unrem = sorted(u.node.name for u in pl.UnremovableNodes())
+        if got_unrem != sorted(e["unremovable"]):
+            errs.append(f"unremovable {got_unrem} != {sorted(e['unremovable'])}")
+        after = [(n, [p.name for p in snap.Get(n).pods]) for n in names]
+        if before != after:                           # UpdateClusterState reverts its fork (planner.go:108-110)
+            errs.append("snapshot changed by UpdateClusterState")
+    elif kind == "planner_limit":
+        nodes = [k8s.build_test_node(f"n{i}", 1000, 10) for i in range(case["n_nodes"])]
+        snap.AddNodes(nodes)
+        pl = Planner(snap, checker, NodeDeleteOptions(False, False, 0), None,
+                     max_scale_down_parallelism=case["max_parallelism"],
+                     scale_down_unneeded_time=float(case["unneeded_time_s"]))
+        pl.unneeded = {nodes[i].name: NodeToBeRemoved(nodes[i]) for i in range(case["previously_unneeded"])}
+        pl.min_update_interval = float(case["update_interval_s"])
+        names = [n.name for n in nodes]
+        pl.UpdateClusterState(names, names, [], 1_700_000_000.0)
+        if len(pl.UnneededNodes()) != case["expect"]["unneeded_count"]:
+            errs.append(f"{len(pl.UnneededNodes())} unneeded != {case['expect']['unneeded_count']}")
     elif kind == "filter_out_schedulable_bench":
         nodes = series(case["nodes"], build_node)
         snap.AddNodes(nodes)

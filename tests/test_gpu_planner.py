@@ -1,0 +1,138 @@
+"""GPU parity of the planner's committing removal loop (ca_plan_removals)
+against the oracle (or_plan_removals, itself checked against a step-by-step restatement
+in tests/test_planner.py and the reference's planner_test.go in the golden cases):
+bit-exact results, moves, hints, lastIndex, PDB budgets, and the committed snapshot."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from autoscaler_amd import native
+from autoscaler_amd import workloads as W
+from conftest import gpu_available
+from plangen import PlanCase, rand_plan_case
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="no HIP device")]
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    import pyoracle
+    pyoracle.build()
+    return pyoracle
+
+
+_M = {}
+
+
+def _mirror():
+    if "m" not in _M:
+        _M["m"] = native.Mirror(0)
+    m = _M["m"]
+    m.clear()
+    return m
+
+
+def _check(o, g, what=""):
+    assert np.array_equal(o.results, g.results), (what, o.results, g.results)
+    assert np.array_equal(o.moves, g.moves), what
+    assert np.array_equal(o.hints, g.hints), what
+    assert o.last_index == g.last_index, what
+    assert np.array_equal(o.allowed, g.allowed), what
+
+
+def _follow_up_sweep(b, n_nodes: int, n_pods: int):
+    """A legacy FindNodesToRemove over every node of the committed snapshot: equal outputs
+    on both backends mean equal committed rows and pod lists."""
+    cands = np.arange(n_nodes, dtype=np.int32)
+    off, moves = [0], []
+    for c in range(n_nodes):
+        moves.extend(b.node_pods(c))
+        off.append(len(moves))
+    return b.find_nodes_to_remove(cands, np.ones(n_nodes, np.uint8), np.zeros(n_nodes, np.int32),
+                                  np.array(off, np.int32), np.array(moves, np.int32),
+                                  np.full(n_pods, -1, np.int32), 0)
+
+
+def _run_both(case: PlanCase, oracle):
+    outs = []
+    for b in (oracle.OracleState(), _mirror()):
+        case.load(b)
+        out = case.plan(b)
+        n_nodes = len(case.node_recs)
+        n_pods = len(case.table) + len(out.moves)
+        outs.append((out, [b.node_pods(i) for i in range(n_nodes)], _follow_up_sweep(b, n_nodes, n_pods)))
+    (o, on, os_), (g, gn, gs) = outs
+    _check(o, g)
+    assert on == gn
+    assert np.array_equal(os_.results, gs.results) and np.array_equal(os_.dest, gs.dest)
+    return o, g
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_plan_random(seed, oracle):
+    case = rand_plan_case(seed, n_nodes=10 + seed % 7, pods_per_node=3 + seed % 3, n_pdbs=(seed % 3) * 2)
+    _run_both(case, oracle)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_plan_random_larger(seed, oracle):
+    """More candidates per window: commits inside a speculation window conflict with later
+    speculations (placements on filled nodes, hints on removed nodes, grown pod lists)."""
+    case = rand_plan_case(100 + seed, n_nodes=60, pods_per_node=6, n_pdbs=3, limit=0)
+    _run_both(case, oracle)
+
+
+def test_plan_fork_revert(oracle):
+    """UpdateClusterState forks around the loop (planner.go:108-110): after Revert the mirror
+    is the snapshot it was, and simulates as the oracle's reverted one does."""
+    case = rand_plan_case(7, n_nodes=30, pods_per_node=5, limit=0)
+    o, m = oracle.OracleState(), _mirror()
+    for b in (o, m):
+        case.load(b)
+        b.fork()
+    po, pm = case.plan(o), case.plan(m)
+    _check(po, pm)
+    assert len(pm.moves) > 0
+    for b in (o, m):
+        b.revert()
+    n = len(case.node_recs)
+    assert [o.node_pods(i) for i in range(n)] == [m.node_pods(i) for i in range(n)]
+    assert [m.node_pods(i) for i in range(n)] == [
+        [int(j) for j in np.nonzero(case.node_of == i)[0]] for i in range(n)]
+    so = _follow_up_sweep(o, n, len(case.table) + len(po.moves))
+    sm = _follow_up_sweep(m, n, len(case.table) + len(pm.moves))
+    assert np.array_equal(so.results, sm.results) and np.array_equal(so.dest, sm.dest)
+
+
+def _c3_case(n_nodes: int, limit: int, hints=None) -> PlanCase:
+    w = W.c3(n_nodes=n_nodes)
+    return PlanCase(w.nodes, w.table, w.pod_node, w.candidates, w.dest_mask, w.cand_status, w.move_off,
+                    w.move_pods, np.full(len(w.table), -1, np.int32) if hints is None else hints, 0, limit,
+                    np.zeros(0, np.int32), np.zeros(1, np.int32), np.zeros(0, np.int32))
+
+
+@pytest.mark.parametrize("n_nodes,limit", [(1500, 0), (5000, 20), (5000, 200)])
+def test_plan_c3(n_nodes, limit, oracle):
+    case = _c3_case(n_nodes, limit)
+    o, m = oracle.OracleState(), _mirror()
+    case.load(o)
+    case.load(m)
+    po, pm = case.plan(o), case.plan(m)
+    _check(po, pm, f"C3 n={n_nodes} limit={limit}")
+    removed = int(po.results["removable"].sum())
+    assert removed == limit if limit else removed > 0
+    st = m.plan_stats()
+    assert st["rounds"] >= 1 and st["simulated"] >= 1
+
+
+def test_plan_c4_attributes(oracle):
+    """Taints, labels, selectors and required terms on the C4 sweep workload."""
+    w = W.c4_sweep(n_nodes=800)
+    case = PlanCase(w.nodes, w.table, w.pod_node, w.candidates, w.dest_mask, w.cand_status, w.move_off,
+                    w.move_pods, np.full(len(w.table), -1, np.int32), 3, 0, np.zeros(0, np.int32),
+                    np.zeros(1, np.int32), np.zeros(0, np.int32))
+    o, m = oracle.OracleState(), _mirror()
+    W.load_sweep(o, w)
+    W.load_sweep(m, w)
+    _check(case.plan(o), case.plan(m), "C4")

@@ -18,10 +18,13 @@ namespace casim {
 static thread_local std::string g_last_error;
 void set_last_error(const std::string& s) { g_last_error = s; }
 
+// Both buffers grow geometrically: a hipMalloc / hipHostMalloc (and the free before it)
+// costs up to milliseconds, and callers like the planner's rounds grow them step by step.
 int DevBuf::reserve(size_t need) {
     if (need <= bytes) return CA_OK;
+    const size_t grown = bytes + bytes / 2;
     release();
-    size_t sz = std::max<size_t>(need, 256);
+    size_t sz = std::max<size_t>(need, std::max<size_t>(grown, 4096));
     if (hipMalloc(&ptr, sz) != hipSuccess) { ptr = nullptr; bytes = 0; set_last_error("hipMalloc failed"); return CA_EDEVICE; }
     bytes = sz;
     return CA_OK;
@@ -50,8 +53,9 @@ void DevBuf::release() {
 
 int HostBuf::reserve(size_t need) {
     if (need <= bytes) return CA_OK;
+    const size_t grown = bytes + bytes / 2;
     release();
-    size_t sz = std::max<size_t>(need, 256);
+    size_t sz = std::max<size_t>(need, std::max<size_t>(grown, 4096));
     if (hipHostMalloc(&ptr, sz, hipHostMallocNonCoherent) != hipSuccess) {
         ptr = nullptr; bytes = 0; set_last_error("hipHostMalloc failed"); return CA_EDEVICE;
     }
@@ -314,8 +318,9 @@ int ca_mirror::sync_nodes() {
         // few rows: stage them (row id + both columns) in pinned memory, one H2D copy, and
         // scatter them on the device
         const size_t k = dirty_rows.size();
-        if ((rc = rs.h.reserve(sizeof(StagedRow) * k)) != CA_OK) return rc;
-        if ((rc = rs.d.reserve(sizeof(StagedRow) * k)) != CA_OK) return rc;
+        const size_t kcap = std::max<size_t>(k, std::max<size_t>(64, n / 4));   // the largest staged batch
+        if ((rc = rs.h.reserve(sizeof(StagedRow) * kcap)) != CA_OK) return rc;
+        if ((rc = rs.d.reserve(sizeof(StagedRow) * kcap)) != CA_OK) return rc;
         StagedRow* sr = rs.h.as<StagedRow>();
         for (size_t j = 0; j < k; j++) {
             sr[j].row = dirty_rows[j];

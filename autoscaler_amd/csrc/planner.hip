@@ -176,6 +176,7 @@ int ca_plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const u
     while (i < C && !done) {
         if (max_removable > 0 && removed >= max_removable) { not_run(i); break; }   // :268-271
         const int32_t j = std::min(C, i + std::max(W, 1));
+        const auto t_build = std::chrono::steady_clock::now();
         // ---- 1. speculate candidates [i, j) from the committed state ----
         w_off.assign(1, 0);
         w_pods.clear();
@@ -320,8 +321,9 @@ int ca_plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const u
             }
         }
         if (dbg_t)
-            fprintf(stderr, "[plan] round %d: [%d,%d) spec %.3f ms, validate+commit %.3f ms, accepted %d%s%s\n",
-                    ps.rounds, i, j, std::chrono::duration<double, std::milli>(t_val - t_spec).count(),
+            fprintf(stderr, "[plan] round %d: [%d,%d) build %.3f ms, spec %.3f ms, validate+commit %.3f ms, accepted %d%s%s\n",
+                    ps.rounds, i, j, std::chrono::duration<double, std::milli>(t_spec - t_build).count(),
+                    std::chrono::duration<double, std::milli>(t_val - t_spec).count(),
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_val).count(), k - i,
                     conflict ? ", conflict: " : "", conflict ? why : "");
         if (done) break;

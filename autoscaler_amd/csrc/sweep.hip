@@ -560,20 +560,26 @@ __global__ void __launch_bounds__(64) k_sweep_table(
     uint32_t ev = 0;              // visible nodes scanned (the exact kernel's evals)
     const int32_t dbase = tdoff ? tdoff[t] : -1;
     bool unknown = mn > TB_MAXP;
-    // candidates with hints / ports / scalars go to the exact kernel
+    // candidates with hints / ports / scalars go to the exact kernel.  A hint to the
+    // candidate's own node (a pod committed onto it by the planner, planner.hip) is checked
+    // (one evaluation) but never accepted (cluster.go:221-223), and the scan's Hints.Set
+    // overrides the check's: such a pod is an unhinted one plus an evaluation while its scan
+    // succeeds (a failing scan is left to the exact kernel anyway).
     for (int32_t i = lane; i < mn; i += 64) {
         const int32_t id = move_pods[mo + i];
         const uint32_t f = moved_flags(ph[id].flags);
-        if ((hints[mo + i] >= 0) | ((f & (PF_PORTS | PF_SCALAR_REQ)) != 0)) unknown = true;
+        const int32_t h = hints[mo + i];
+        if ((h >= 0 && h != node) | ((f & (PF_PORTS | PF_SCALAR_REQ)) != 0)) unknown = true;
     }
     unknown = __ballot(unknown) != 0;
     if (!unknown) {
         // lane-parallel prefetch of the moved pods' records (batch of 64)
-        int32_t my_id = -1;
+        int32_t my_id = -1, my_h = -1;
         PodHot my_p = {};
         for (int32_t i = 0; i < mn; i++) {
             const int sl = i & 63;
-            if (sl == 0 && i + lane < mn) { my_id = move_pods[mo + i + lane]; my_p = ph[my_id]; }
+            if (sl == 0 && i + lane < mn) { my_id = move_pods[mo + i + lane]; my_p = ph[my_id]; my_h = hints[mo + i + lane]; }
+            ev += rl32s(my_h, sl) == node ? 1u : 0u;                             // the own-node hint check
             PodHot p;
             p.cpu = rl64s(my_p.cpu, sl); p.mem = rl64s(my_p.mem, sl); p.eph = rl64s(my_p.eph, sl);
             p.flags = moved_flags((uint32_t)rl32s((int32_t)my_p.flags, sl));
@@ -1258,8 +1264,13 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
         }
     }
     int rc;
+    const auto t_sync = std::chrono::steady_clock::now();
     if ((rc = m->sync_nodes()) != CA_OK) return rc;
     if ((rc = m->sync_pods()) != CA_OK) return rc;
+    if (getenv("CASIM_DEBUG_TIMING"))
+        fprintf(stderr, "[sweep] sync           %8.3f ms (%zu pods)\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_sync).count(),
+                m->pods.size());
     const int32_t* status = cand_status;
     std::vector<int32_t> zero_status;
     if (!status) { zero_status.assign((size_t)C, 0); status = zero_status.data(); }

@@ -77,6 +77,7 @@ def parse():
     ap.add_argument("--no-filter", action="store_true", help="skip the FilterOutSchedulable leg (N=1)")
     ap.add_argument("--no-unlimited", action="store_true", help="skip the C2 max_nodes=0 leg (N=1)")
     ap.add_argument("--no-runonce", action="store_true", help="skip the C5 end-to-end RunOnce leg (N=1)")
+    ap.add_argument("--no-planner", action="store_true", help="skip the planner (canPersist=true) leg (N=1)")
     ap.add_argument("--sweep-nodes", type=int, default=5000)
     return ap.parse_args()
 
@@ -335,6 +336,55 @@ def sweep_leg(args, device: int, with_cpu: bool) -> dict:
                                "sample": f"oracle/casim_oracle.c FindNodesToRemove, same C3 sweep, 1 thread of "
                                          f"{cpu_model()}"}
     m.close()
+    return out
+
+
+def planner_leg(args, device: int, with_cpu: bool) -> dict:
+    """The planner's committing loop (canPersist=true, planner.go:252-296) on C3 through
+    ca_plan_removals, inside a fork reverted after each run (UpdateClusterState does the
+    same), at three unneeded-node limits: 20 (the first loop's limit with the default
+    MaxScaleDownParallelism 10, planner.go:318-334), 200, and none."""
+    from autoscaler_amd import native
+    from autoscaler_amd import workloads as W
+    w = W.c3(n_nodes=args.sweep_nodes)
+    args_ = (w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods)
+    hints = np.full(len(w.table), -1, np.int32)
+    m = native.Mirror(device)
+    W.load_sweep(m, w)
+    out = {"workload": f"C3: {args.sweep_nodes} nodes, {len(w.table)} running pods, candidates = all nodes in order",
+           "runs": {}}
+    firsts = {}
+    for limit in (20, 200, 0):
+        ts, st = [], None
+        for _ in range(3):
+            m.fork()
+            t = time.perf_counter()
+            r = m.plan_removals(*args_, hints, 0, limit)
+            ts.append(time.perf_counter() - t)
+            st = m.plan_stats()
+            m.revert()
+            firsts.setdefault(limit, r)
+        out["runs"][str(limit)] = {"gpu_ms": float(min(ts[1:]) * 1e3), "rounds": st["rounds"],
+                                   "conflicts": st["conflicts"], "simulated": st["simulated"],
+                                   "removable": int(r.results["removable"].sum()),
+                                   "candidates_run": int((r.results["reason"] != 101).sum())}
+    m.close()
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle                                           # CPU baseline leg only
+        for limit in (20, 200, 0):
+            o = pyoracle.OracleState()
+            W.load_sweep(o, w)
+            t = time.perf_counter()
+            ro = o.plan_removals(*args_, hints, 0, limit)
+            run = out["runs"][str(limit)]
+            run["cpu_ms"] = (time.perf_counter() - t) * 1e3
+            run["speedup"] = run["cpu_ms"] / run["gpu_ms"]
+            g = firsts[limit]
+            run["parity"] = bool(np.array_equal(ro.results, g.results) and np.array_equal(ro.moves, g.moves)
+                                 and np.array_equal(ro.hints, g.hints) and ro.last_index == g.last_index)
+        out["cpu_baseline"] = {"kind": "port", "cores": 1,
+                               "sample": f"oracle/casim_oracle.c or_plan_removals, same loop, 1 thread of {cpu_model()}"}
     return out
 
 
@@ -665,6 +715,8 @@ def main():
             result["extra"]["utilization"] = utilization_leg(args, local, not args.no_cpu_baseline)
         if world == 1 and not args.no_runonce:
             result["extra"]["c5_runonce"] = runonce_leg(args, local, not args.no_cpu_baseline)
+        if world == 1 and not args.no_planner:
+            result["extra"]["planner"] = planner_leg(args, local, not args.no_cpu_baseline)
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.barrier()

@@ -81,8 +81,11 @@ int DevPodTable::upload(const ca_pod_spec* pods, int32_t n, const ca_selector_te
         h[i].spec = i;
     }
     int rc;
-    if ((rc = hot.reserve(sizeof(PodHot) * (size_t)(n + 1))) != CA_OK) return rc;
-    if ((rc = spec.reserve(sizeof(ca_pod_spec) * (size_t)(n + 1))) != CA_OK) return rc;
+    // headroom for the pods later calls append (FilterOutSchedulable's placements, the
+    // planner's moved copies) without a reallocation
+    const size_t room = (size_t)n + (size_t)n / 4 + 1024;
+    if ((rc = hot.reserve(sizeof(PodHot) * room)) != CA_OK) return rc;
+    if ((rc = spec.reserve(sizeof(ca_pod_spec) * room)) != CA_OK) return rc;
     if ((rc = terms.reserve(sizeof(ca_selector_term) * (size_t)(nt + 1))) != CA_OK) return rc;
     if ((rc = reqs.reserve(sizeof(ca_selector_req) * (size_t)(nr + 1))) != CA_OK) return rc;
     if ((rc = names.reserve(sizeof(int32_t) * (size_t)(nn + 1))) != CA_OK) return rc;

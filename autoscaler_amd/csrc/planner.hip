@@ -163,6 +163,7 @@ int ca_plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const u
     bool done = false;
     const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
     const char* why = "";
+
     auto not_run = [&](int32_t from) {
         for (int32_t c = from; c < C; c++) {
             ca_plan_result& r = results[c];

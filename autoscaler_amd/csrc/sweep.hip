@@ -1265,12 +1265,14 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     }
     int rc;
     const auto t_sync = std::chrono::steady_clock::now();
+    const size_t dirty = m->all_dirty ? m->nodes.size() : m->dirty_rows.size();
     if ((rc = m->sync_nodes()) != CA_OK) return rc;
+    const auto t_sync1 = std::chrono::steady_clock::now();
     if ((rc = m->sync_pods()) != CA_OK) return rc;
     if (getenv("CASIM_DEBUG_TIMING"))
-        fprintf(stderr, "[sweep] sync           %8.3f ms (%zu pods)\n",
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_sync).count(),
-                m->pods.size());
+        fprintf(stderr, "[sweep] sync           %8.3f ms (rows %zu dirty: %.3f ms; %zu pods)\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_sync).count(), dirty,
+                std::chrono::duration<double, std::milli>(t_sync1 - t_sync).count(), m->pods.size());
     const int32_t* status = cand_status;
     std::vector<int32_t> zero_status;
     if (!status) { zero_status.assign((size_t)C, 0); status = zero_status.data(); }

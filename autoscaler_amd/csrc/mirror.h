@@ -49,7 +49,8 @@ struct DevPodTable {
 struct SweepScratch {
     DevBuf in, lin, need, out, todo, tab, wl;
     DevBuf tev, tdest;              // table lanes' evaluation counts and pod destinations (first round)
-    HostBuf h_in, h_tab, h_out, h_todo, h_lin, h_wl;
+    DevBuf tfp, vp;                 // table rows' fit-point classes; visible-node prefix counts
+    HostBuf h_in, h_tab, h_out, h_todo, h_lin, h_wl, h_tfp, h_ctab;
 };
 
 // Per-mirror scratch of ca_filter_out_schedulable (filter.hip).

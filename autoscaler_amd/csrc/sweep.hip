@@ -57,6 +57,7 @@ __device__ inline int64_t rl64s(int64_t v, int lane) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 __device__ inline int32_t rl32s(int32_t v, int lane) { return (int32_t)__builtin_amdgcn_readlane((uint32_t)v, lane); }
+__device__ inline uint64_t lanes_below_u(int lane) { return lane == 0 ? 0ull : (~0ull >> (64 - lane)); }
 
 // moved-pod semantics: Spec.NodeName cleared (cluster.go:235-240), TPU requests
 // cleared (tpu.go:57-79)
@@ -531,7 +532,73 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CASIM_S
 }
 
 // ---------------------------------------------------------------------------
-// table kernel: lane w simulates the candidate from lastIndex = wstart + w.
+// Fit-point classes of lastIndex.  A candidate's first FitsAnyNode scan from L lands on
+// the first node at or after L where its first pod fits (schedulerbased.go:114-131),
+// and everything after depends only on that node: every L in (f_{w-1}, f_w] between two
+// consecutive fit points of the first pod has the outputs of L = f_w, except for the
+// evaluations of the skipped visible nodes in [L, f_w).  A table row therefore holds 64
+// classes: fp[0] = f_{-1}, fp[1 + w] = f_w, and lane w simulates L = f_w.  In a loose
+// cluster every node fits and the classes are 64 consecutive positions; in a tight one a
+// row covers 64 fit points (DESIGN.md §4 sweep).  Rows whose first pod has PreFilter
+// node names, or a ring with fewer than 65 fit points, use 64 consecutive positions.
+// ---------------------------------------------------------------------------
+constexpr int FPW = 65;
+
+// class of lastIndex L in a row (fp[k * fs], k = 0..64), or -1 outside it
+__host__ __device__ inline int32_t fp_class(const int32_t* fp, int32_t fs, int32_t n, int32_t L) {
+    if (n < FPW) {                     // a ring shorter than a row: 64 consecutive positions cover it
+        int32_t w = L - fp[fs];
+        if (w < 0) w += n;
+        return w;
+    }
+    const int32_t f0 = fp[0];
+    int32_t d = L - f0;
+    if (d < 0) d += n;
+    if (d <= 0) return -1;
+    auto D = [&](int32_t w) { int32_t x = fp[(w + 1) * fs] - f0; return x <= 0 ? x + n : x; };
+    if (d > D(63)) return -1;
+    int32_t lo = 0, hi = 63;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (D(mid) >= d) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+
+// visible nodes (destination, schedulable, not the candidate) in the cyclic range [a, b)
+__device__ inline int32_t vis_between(const int32_t* __restrict__ vp, int32_t n, int32_t a, int32_t b, int32_t node,
+                                      bool node_vis) {
+    int32_t v = a <= b ? vp[b] - vp[a] : vp[n] - vp[a] + vp[b];
+    const bool in = a <= b ? (node >= a && node < b) : (node >= a || node < b);
+    return v - ((in && node_vis) ? 1 : 0);
+}
+
+// vp[i] = destination, schedulable nodes among positions [0, i) (one block)
+__global__ void __launch_bounds__(1024) k_vis_prefix(const NodeHot* __restrict__ hot, const uint8_t* __restrict__ dest_mask,
+                                                     int32_t n, int32_t* __restrict__ vp) {
+    __shared__ int32_t wsum[16];
+    __shared__ int32_t carry;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) { carry = 0; vp[0] = 0; }
+    __syncthreads();
+    for (int32_t base = 0; base < n; base += 1024) {
+        const int32_t i = base + tid;
+        const int32_t v = (i < n && dest_mask[i] && !(hot[i].flags & NF_UNSCHED)) ? 1 : 0;
+        const uint64_t m = __ballot(v != 0);
+        const int32_t incl = __popcll(m & (lane == 63 ? ~0ull : ((2ull << lane) - 1)));
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        int32_t pre = carry;
+        for (int q = 0; q < w; q++) pre += wsum[q];
+        if (i < n) vp[i + 1] = pre + incl;
+        __syncthreads();
+        if (tid == 0) { int32_t t = 0; for (int q = 0; q < 16; q++) t += wsum[q]; carry += t; }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// table kernel: lane w simulates the candidate from lastIndex = class w of its row.
 // A lane's placements all lie in the cyclic interval its scans have passed
 // ([L_start, L_cur)); a scan that would re-enter it (a full turn of the ring: a
 // NoPlace failure or a revisit) is left to the exact kernel, as are candidates with
@@ -544,17 +611,59 @@ __global__ void __launch_bounds__(64) k_sweep_table(
     const ca_selector_term* __restrict__ terms, const ca_selector_req* __restrict__ reqs,
     const int32_t* __restrict__ names, const int32_t* __restrict__ hints, const int32_t* __restrict__ todo,
     const int32_t* __restrict__ wstart, const int32_t* __restrict__ row_of, int32_t* __restrict__ table,
-    int32_t stride, uint32_t* __restrict__ tev, int32_t* __restrict__ tdest, const int32_t* __restrict__ tdoff) {
+    int32_t stride, uint32_t* __restrict__ tev, int32_t* __restrict__ tdest, const int32_t* __restrict__ tdoff,
+    int32_t* __restrict__ tfp) {
     // tev / tdest (first round, device walk): the lane's evaluation count and each moved
     // pod's destination, so a candidate the walk resolves through the table takes these
     // outputs (k_table_gather) instead of being simulated again
+    __shared__ int32_t fps[FPW];
     const int t = blockIdx.x;
     const int lane = threadIdx.x;
     const int32_t c = todo[t];
     const int32_t node = cands[c];
     const int32_t mo = move_off[c], mn = move_off[c + 1] - mo;
-    int32_t Ls = wstart[t] + lane;
-    if (Ls >= n) Ls -= n;
+    const int32_t row = row_of ? row_of[t] : t;
+    const int32_t ws0 = wstart[t];
+    // the row's classes: fit points of the first pod from the window start (wave-parallel,
+    // 64 positions per step), or 64 consecutive positions
+    bool classes = false;
+    if (mn > 0 && n > 0) {
+        const PodHot p0h = ph[move_pods[mo]];
+        PodHot p0 = p0h;
+        p0.flags = moved_flags(p0h.flags);
+        if (!(p0.flags & (PF_PREFILTER_NAMES | PF_PREFILTER_FAIL | PF_PORTS | PF_SCALAR_REQ))) {
+            const ca_pod_spec& s0 = specs[p0.spec];
+            int32_t cnt = 0;
+            for (int32_t base = 0; base < n && cnt < FPW; base += 64) {
+                int32_t pos = ws0 + base + lane;
+                if (pos >= n) pos -= n;
+                if (pos >= n) pos -= n;
+                bool fit = false;
+                if (base + lane < n) {
+                    const NodeHot nh = hot[pos];
+                    fit = (pos != node) & (dest_mask[pos] != 0) & !(nh.flags & NF_UNSCHED) && hot_fits(p0, nh) &&
+                          static_ok(s0, p0, terms, reqs, nh, st + pos);
+                }
+                const uint64_t m = __ballot(fit);
+                const int32_t r = cnt + __popcll(m & lanes_below_u(lane));
+                if (fit && r < FPW) fps[r] = pos;
+                cnt += __popcll(m);
+            }
+            classes = cnt >= FPW;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (!classes) {
+        for (int32_t i = lane; i < FPW; i += 64) {
+            int32_t v = ws0 - 1 + i;
+            if (v < 0) v += n;
+            if (v >= n) v -= n;
+            fps[i] = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (tfp) for (int32_t i = lane; i < FPW; i += 64) tfp[(size_t)row * FPW + i] = fps[i];
+    int32_t Ls = fps[1 + lane];
     int32_t Lcur = Ls;
     int32_t adv = 0;              // positions passed since Ls
     uint32_t ev = 0;              // visible nodes scanned (the exact kernel's evals)
@@ -612,8 +721,8 @@ __global__ void __launch_bounds__(64) k_sweep_table(
             }
         }
     }
-    table[(size_t)lane * stride + (row_of ? row_of[t] : t)] = unknown ? TB_UNKNOWN : Lcur;
-    if (tev) tev[(size_t)lane * stride + (row_of ? row_of[t] : t)] = ev;
+    table[(size_t)lane * stride + row] = unknown ? TB_UNKNOWN : Lcur;
+    if (tev) tev[(size_t)lane * stride + row] = ev;
 }
 
 // ---------------------------------------------------------------------------
@@ -626,6 +735,8 @@ __global__ void __launch_bounds__(64) k_sweep_table(
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(1024) k_sweep_est(const SweepOut* __restrict__ probe, const int32_t* __restrict__ sens,
                                                     int32_t S, int64_t L0, int32_t n, int32_t* __restrict__ ws) {
+    // (window start = 32 fit points before the estimate: 32 x the probe's mean gap between
+    // placements, so a tight cluster's row of fit-point classes is centred too)
     __shared__ int64_t wtot[16];
     __shared__ int64_t carry;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -633,13 +744,14 @@ __global__ void __launch_bounds__(1024) k_sweep_est(const SweepOut* __restrict__
     __syncthreads();
     for (int32_t base = 0; base < S; base += 1024) {
         const int32_t k = base + tid;
-        int64_t v = 0;
+        int64_t v = 0, gap = 1;
         if (k < S) {
             const SweepOut o = probe[sens[k]];
             if (o.fa_success) {
                 int64_t d = ((int64_t)o.lout - (int64_t)o.lin) % n;
                 if (d < 0) d += n;
                 v = d;
+                gap = max((int64_t)1, min((int64_t)(n / 64), d / max(1, o.n_placed)));
             }
         }
         int64_t x = v;                                   // inclusive scan in the wave
@@ -652,7 +764,7 @@ __global__ void __launch_bounds__(1024) k_sweep_est(const SweepOut* __restrict__
         int64_t pre = carry;
         for (int q = 0; q < w; q++) pre += wtot[q];
         if (k < S) {
-            int64_t e = (L0 + pre + x - v - 32) % n;       // exclusive prefix, window start
+            int64_t e = (L0 + pre + x - v - 32 * gap) % n;  // exclusive prefix, window start
             if (e < 0) e += n;
             ws[k] = (int32_t)e;
         }
@@ -682,23 +794,24 @@ __global__ void __launch_bounds__(1024) k_sweep_est(const SweepOut* __restrict__
 constexpr int WK = 64;
 constexpr int WALK_MAX_CHUNKS = 256;
 
-__global__ void __launch_bounds__(64) k_walk_chunks(const int32_t* __restrict__ sens, const int32_t* __restrict__ ws,
-                                                   const int32_t* __restrict__ guess, const int32_t* __restrict__ wl,
-                                                   const int32_t* __restrict__ tab, int32_t S, int32_t n,
+__global__ void __launch_bounds__(64) k_walk_chunks(const int32_t* __restrict__ sens, const int32_t* __restrict__ guess,
+                                                   const int32_t* __restrict__ wl, const int32_t* __restrict__ tab,
+                                                   const int32_t* __restrict__ tfp, int32_t S, int32_t n,
                                                    int32_t* __restrict__ cmap, int32_t* __restrict__ traj) {
     __shared__ int32_t T[64][WK + 1];
-    __shared__ int32_t cws[WK], cg[WK], cwl[WK];
+    __shared__ int32_t FP[FPW][WK + 1];
+    __shared__ int32_t cg[WK], cwl[WK];
     const int j = blockIdx.x, lane = threadIdx.x;
     const int32_t k0 = j * WK, kn = min(WK, S - k0);
     for (int w = 0; w < 64; w++) T[w][lane] = lane < kn ? tab[(size_t)w * S + k0 + lane] : TB_UNKNOWN;
+    for (int i = 0; i < FPW; i++) FP[i][lane] = lane < kn ? tfp[(size_t)(k0 + lane) * FPW + i] : 0;
     if (lane < kn) {
         const int32_t c = sens[k0 + lane];
-        cws[lane] = ws[k0 + lane];
         cg[lane] = guess[c];
         cwl[lane] = wl[c];
     }
     __syncthreads();
-    int32_t cur = (int32_t)(((int64_t)cws[0] + lane) % n);
+    int32_t cur = FP[1 + lane][0];                          // lane x: class x of the chunk's first row
     int32_t stop = -1;
     for (int kk = 0; kk < kn; kk++) {
         int32_t enc = -1;
@@ -709,9 +822,8 @@ __global__ void __launch_bounds__(64) k_walk_chunks(const int32_t* __restrict__ 
                 if (cur == cg[kk]) {
                     cur = wlv;
                 } else {
-                    int32_t w = cur - cws[kk];
-                    if (w < 0) w += n;
-                    const int32_t v = w < 64 ? T[w][kk] : TB_UNKNOWN;
+                    const int32_t w = fp_class(&FP[0][kk], WK + 1, n, cur);
+                    const int32_t v = w >= 0 ? T[w][kk] : TB_UNKNOWN;
                     if (v == TB_UNKNOWN) stop = kk;
                     else { cur = v; enc |= 1; }
                 }
@@ -723,12 +835,13 @@ __global__ void __launch_bounds__(64) k_walk_chunks(const int32_t* __restrict__ 
 }
 
 // info[0] = first unresolved sensitive candidate (S: all), info[1] = lastIndex before it
-__global__ void __launch_bounds__(1024) k_walk_resolve(const int32_t* __restrict__ sens, const int32_t* __restrict__ ws,
+__global__ void __launch_bounds__(1024) k_walk_resolve(const int32_t* __restrict__ sens, const int32_t* __restrict__ tfp,
                                                       const int32_t* __restrict__ cmap, const int32_t* __restrict__ traj,
-                                                      int32_t S, int32_t n, int32_t L0n, int32_t* __restrict__ lin,
-                                                      uint8_t* __restrict__ need, int32_t* __restrict__ info) {
+                                                      const int32_t* __restrict__ wl, int32_t S, int32_t n, int32_t L0n,
+                                                      int32_t* __restrict__ lin, uint8_t* __restrict__ need,
+                                                      int32_t* __restrict__ info) {
     __shared__ int32_t cm[WALK_MAX_CHUNKS * 64];
-    __shared__ int32_t lane_of[WALK_MAX_CHUNKS];
+    __shared__ int32_t lane_of[WALK_MAX_CHUNKS], cin[WALK_MAX_CHUNKS];
     __shared__ int32_t stop_k, cur_out;
     const int32_t nch = (S + WK - 1) / WK;
     for (int32_t i = threadIdx.x; i < nch * 64; i += blockDim.x) cm[i] = cmap[i];
@@ -736,14 +849,14 @@ __global__ void __launch_bounds__(1024) k_walk_resolve(const int32_t* __restrict
     if (threadIdx.x == 0) {
         int32_t cur = L0n, sk = S;
         for (int32_t j = 0; j < nch; j++) {
-            int32_t x = cur - ws[j * WK];
-            if (x < 0) x += n;
-            if (x >= 64) { sk = j * WK; break; }
+            const int32_t x = fp_class(tfp + (size_t)j * WK * FPW, 1, n, cur);
+            if (x < 0) { sk = j * WK; break; }
             lane_of[j] = x;
+            cin[j] = cur;                     // the chunk's true input (its lane started at class x's point)
             const int32_t r = cm[j * 64 + x];
             if (r < 0) {
                 sk = j * WK + (-1 - r);
-                cur = traj[(size_t)sk * 64 + x] >> 1;
+                if (sk > j * WK) cur = traj[(size_t)sk * 64 + x] >> 1;
                 break;
             }
             cur = r;
@@ -756,8 +869,17 @@ __global__ void __launch_bounds__(1024) k_walk_resolve(const int32_t* __restrict
     for (int32_t k = threadIdx.x; k < sk; k += blockDim.x) {
         const int32_t e = traj[(size_t)k * 64 + lane_of[k / WK]];
         const int32_t c = sens[k];
-        lin[c] = e >> 1;
-        need[c] = (uint8_t)((e & 1) ? 2 : 0);          // 2: resolved through the table (k_table_gather)
+        uint8_t nd = (uint8_t)((e & 1) ? 2 : 0);       // 2: resolved through the table (k_table_gather)
+        if (k % WK == 0) {
+            // the chunk's lane ran this candidate from its class's fit point: a probe taken at
+            // that point has the chain's lastIndex out but not this input's outputs
+            const int32_t L = cin[k / WK];
+            if (!(e & 1) && wl[c] >= 0 && lin[c] != L) nd = 1;
+            lin[c] = L;
+        } else {
+            lin[c] = e >> 1;
+        }
+        need[c] = nd;
     }
     if (threadIdx.x == 0) { info[0] = sk; info[1] = cur_out; }
 }
@@ -767,7 +889,9 @@ __global__ void __launch_bounds__(1024) k_walk_resolve(const int32_t* __restrict
 // ring wrap, every pod placed), so its outputs are theirs: removable, every pod at its
 // recorded destination (Hints.Set to it), lastIndex out, evaluations.  One wavefront per
 // sensitive candidate; need becomes 0 so the exact pass skips it.
-__global__ void __launch_bounds__(64) k_table_gather(const int32_t* __restrict__ sens, const int32_t* __restrict__ ws,
+__global__ void __launch_bounds__(64) k_table_gather(const int32_t* __restrict__ sens, const int32_t* __restrict__ tfp,
+                                                    const int32_t* __restrict__ vp, const int32_t* __restrict__ cands,
+                                                    const uint8_t* __restrict__ dest_mask, const NodeHot* __restrict__ hot,
                                                     int32_t S, int32_t n, const int32_t* __restrict__ lin,
                                                     uint8_t* __restrict__ need, const int32_t* __restrict__ tab,
                                                     const uint32_t* __restrict__ tev, const int32_t* __restrict__ tdest,
@@ -778,8 +902,8 @@ __global__ void __launch_bounds__(64) k_table_gather(const int32_t* __restrict__
     const int lane = threadIdx.x;
     const int32_t c = sens[k];
     if (need[c] != 2) return;
-    int32_t x = lin[c] - ws[k];
-    if (x < 0) x += n;
+    const int32_t* fp = tfp + (size_t)k * FPW;
+    const int32_t x = fp_class(fp, 1, n, lin[c]);          // resolved: inside the row
     const int32_t mo = move_off[c], mn = move_off[c + 1] - mo;
     const int32_t db = tdoff[k];
     for (int32_t i = lane; i < mn; i += 64) {
@@ -792,7 +916,11 @@ __global__ void __launch_bounds__(64) k_table_gather(const int32_t* __restrict__
         r.removable = 1; r.reason = CA_UNREMOVABLE_NONE; r.n_placed = mn; r.lin = lin[c];
         r.lout = tab[(size_t)x * S + k];
         r.fa_success = mn > 0 ? 1 : 0; r.status = CA_OK; r.pad = 0;
-        r.evals = tev[(size_t)x * S + k]; r.pad2 = 0;
+        // the lane ran from the class's fit point: add the visible nodes skipped before it
+        const int32_t node = cands[c];
+        const bool node_vis = dest_mask[node] != 0 && !(hot[node].flags & NF_UNSCHED);
+        r.evals = tev[(size_t)x * S + k] + (uint64_t)vis_between(vp, n, lin[c], fp[1 + x], node, node_vis);
+        r.pad2 = 0;
         outs[c] = r;
         walk_lout[c] = r.lout;
         need[c] = 0;
@@ -917,6 +1045,11 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     if ((rc = sw.tab.reserve(sizeof(int32_t) * 64 * Sx)) != CA_OK) return rc;
     if ((rc = sw.h_tab.reserve(sizeof(int32_t) * 64 * Sx)) != CA_OK) return rc;
     if ((rc = sw.wl.reserve(sizeof(int32_t) * (64 * Sx + 64 * (size_t)std::max(nch, 1)))) != CA_OK) return rc;
+    if ((rc = sw.tfp.reserve(sizeof(int32_t) * FPW * Sx)) != CA_OK) return rc;
+    if ((rc = sw.h_tfp.reserve(sizeof(int32_t) * FPW * Sx)) != CA_OK) return rc;
+    if ((rc = sw.vp.reserve(sizeof(int32_t) * ((size_t)n + 1))) != CA_OK) return rc;
+    int32_t* const d_tfp = sw.tfp.as<int32_t>();
+    int32_t* const h_tfp = sw.h_tfp.as<int32_t>();
     int32_t* const d_traj = sw.wl.as<int32_t>();
     int32_t* const d_cmap = d_traj + 64 * Sx;
     int32_t* const tab = sw.h_tab.as<int32_t>();    // [64][S] host copy (host walk only)
@@ -978,19 +1111,25 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                            m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
                            in.d_hints.as<int32_t>(), d_sens, d_ws, (const int32_t*)nullptr, sw.tab.as<int32_t>(), S,
                            dev_walk ? sw.tev.as<uint32_t>() : nullptr, dev_walk ? sw.tdest.as<int32_t>() : nullptr,
-                           dev_walk ? (const int32_t*)d_tdoff : nullptr);
+                           dev_walk ? (const int32_t*)d_tdoff : nullptr, d_tfp);
         CA_HIP_CHECK(hipGetLastError());
+        if (dev_walk) {
+            hipLaunchKernelGGL(k_vis_prefix, dim3(1), dim3(1024), 0, st, m->d_hot.as<NodeHot>(), in.d_mask.as<uint8_t>(),
+                               n, sw.vp.as<int32_t>());
+            CA_HIP_CHECK(hipGetLastError());
+        }
     }
     if (dev_walk) {
         // ---- 3. device walk, then the exact pass at the exact lastIndex values ----
         CA_HIP_CHECK(hipMemsetAsync(d_need, 0, (size_t)C, st));
-        hipLaunchKernelGGL(k_walk_chunks, dim3(nch), dim3(64), 0, st, d_sens, d_ws, d_lin, d_wl, sw.tab.as<int32_t>(),
+        hipLaunchKernelGGL(k_walk_chunks, dim3(nch), dim3(64), 0, st, d_sens, d_lin, d_wl, sw.tab.as<int32_t>(), d_tfp,
                            S, n, d_cmap, d_traj);
         CA_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(k_walk_resolve, dim3(1), dim3(1024), 0, st, d_sens, d_ws, d_cmap, d_traj, S, n, wrap(L0, n),
-                           d_lin, d_need, d_info);
+        hipLaunchKernelGGL(k_walk_resolve, dim3(1), dim3(1024), 0, st, d_sens, d_tfp, d_cmap, d_traj, d_wl, S, n,
+                           wrap(L0, n), d_lin, d_need, d_info);
         CA_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(k_table_gather, dim3(S), dim3(64), 0, st, d_sens, d_ws, S, n, d_lin, d_need,
+        hipLaunchKernelGGL(k_table_gather, dim3(S), dim3(64), 0, st, d_sens, d_tfp, sw.vp.as<int32_t>(),
+                           in.d_c.as<int32_t>(), in.d_mask.as<uint8_t>(), m->d_hot.as<NodeHot>(), S, n, d_lin, d_need,
                            sw.tab.as<int32_t>(), sw.tev.as<uint32_t>(), sw.tdest.as<int32_t>(), d_tdoff,
                            in.d_off.as<int32_t>(), d_out.as<SweepOut>(), d_dest.as<int32_t>(), d_hset.as<int32_t>(), d_wl);
         CA_HIP_CHECK(hipGetLastError());
@@ -1028,6 +1167,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         std::vector<int32_t> wlc((size_t)C, 0);
         std::memcpy(wlc.data(), h_wl, sizeof(int32_t) * C);   // the probe's walk values (h_out is reused below)
         CA_HIP_CHECK(hipMemcpyAsync(tab, sw.tab.ptr, sizeof(int32_t) * 64 * (size_t)S, hipMemcpyDeviceToHost, st));
+        CA_HIP_CHECK(hipMemcpyAsync(h_tfp, d_tfp, sizeof(int32_t) * FPW * (size_t)S, hipMemcpyDeviceToHost, st));
         CA_HIP_CHECK(hipMemcpyAsync(ht, d_ws, sizeof(int32_t) * S, hipMemcpyDeviceToHost, st));
         CA_HIP_CHECK(hipStreamSynchronize(st));
         for (int32_t k = 0; k < S; k++) ws[k] = ht[k];
@@ -1038,9 +1178,13 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         std::vector<int32_t> todo, todo_ws, todo_k;
         auto insensitive = [&](int32_t k) { return wlc[sens[k]] < 0; };
         // the device walk's re-runs already happened: only candidates from k0 on remain
+        // each round looks LOOKAHEAD candidates ahead: the estimates drift with the distance
+        // from the exact lastIndex, so rows further out would be re-centred again anyway
+        constexpr int32_t LOOKAHEAD = 512;
         while (k0 < S) {
             todo.clear(); todo_ws.clear(); todo_k.clear();
-            for (int32_t k = k0; k < S; k++)
+            const int32_t kend = std::min(S, k0 + LOOKAHEAD);
+            for (int32_t k = k0; k < kend; k++)
                 if (!have[k] && !insensitive(k)) { todo.push_back(sens[k]); todo_ws.push_back(ws[k]); todo_k.push_back(k); }
             if (!todo.empty()) {
                 rounds++;
@@ -1056,20 +1200,30 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                                    m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
                                    m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
                                    in.d_hints.as<int32_t>(), sw.todo.as<int32_t>(), sw.todo.as<int32_t>() + T,
-                                   sw.todo.as<int32_t>() + 2 * T, sw.tab.as<int32_t>(), S, nullptr, nullptr, nullptr);
+                                   (const int32_t*)nullptr, sw.tab.as<int32_t>(), T, nullptr, nullptr, nullptr, d_tfp);
                 CA_HIP_CHECK(hipGetLastError());
                 CA_HIP_CHECK(hipEventRecord(m->ev1, st));
-                // the table is stored [lane][candidate] so the host walk, whose window offset
+                // compact rows (row t of this round): only they cross PCIe, then go to their
+                // places in the host copy, stored [lane][candidate] so the walk, whose class
                 // stays near the centre, reads it nearly sequentially
-                CA_HIP_CHECK(hipMemcpyAsync(tab, sw.tab.ptr, sizeof(int32_t) * 64 * (size_t)S, hipMemcpyDeviceToHost, st));
+                if ((rc = sw.h_ctab.reserve(sizeof(int32_t) * (64 + FPW) * (size_t)T)) != CA_OK) return rc;
+                int32_t* const ct = sw.h_ctab.as<int32_t>();
+                CA_HIP_CHECK(hipMemcpyAsync(ct, sw.tab.ptr, sizeof(int32_t) * 64 * (size_t)T, hipMemcpyDeviceToHost, st));
+                CA_HIP_CHECK(hipMemcpyAsync(ct + 64 * (size_t)T, d_tfp, sizeof(int32_t) * FPW * (size_t)T,
+                                            hipMemcpyDeviceToHost, st));
                 CA_HIP_CHECK(hipStreamSynchronize(st));
+                for (int32_t t = 0; t < T; t++) {
+                    const int32_t k = todo_k[t];
+                    for (int32_t w = 0; w < 64; w++) tab[(size_t)w * S + k] = ct[(size_t)w * T + t];
+                    std::memcpy(h_tfp + (size_t)k * FPW, ct + 64 * (size_t)T + (size_t)t * FPW, sizeof(int32_t) * FPW);
+                }
                 float ms = 0;
                 (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
                 kms += ms;
                 if (dbg_t) fprintf(stderr, "[sweep] table round %d: %d rows, kernel %.3f ms\n", rounds, T, ms);
                 tmark("table");
             }
-            for (int32_t k = k0; k < S; k++) have[k] = 1;
+            for (int32_t k = k0; k < kend; k++) have[k] = 1;
             // walk the exact chain as far as the windows reach
             for (; k0 < S; k0++) {
                 const int32_t c = sens[k0];
@@ -1077,8 +1231,8 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 exact_lin[c] = (int32_t)cur;
                 if (wlv < 0) continue;                                             // lastIndex passes through
                 if (wrap(cur, n) == guess[c]) { cur = wlv; continue; }            // probed at the true value
-                const int32_t w = wrap(cur - ws[k0], n);
-                if (w >= 64) break;
+                const int32_t w = fp_class(h_tfp + (size_t)k0 * FPW, 1, n, wrap(cur, n));
+                if (w < 0) break;
                 int32_t v = tab[(size_t)(w) * S + k0];
                 if (v == TB_UNKNOWN) {
                     // hints / ports / long scans: exact kernel at the exact lastIndex, alone
@@ -1101,22 +1255,24 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
             // re-centre the windows from k0 on: follow the tables where the estimate falls
             // inside a window, otherwise shift the nearest known entry
             int64_t est = cur;
-            for (int32_t k = k0; k < S; k++) {
+            for (int32_t k = k0; k < std::min(S, k0 + LOOKAHEAD); k++) {
                 if (insensitive(k)) continue;
-                const int32_t w = wrap(est - ws[k], n);
-                const int32_t v = w < 64 ? tab[(size_t)(w) * S + k] : TB_UNKNOWN;
-                if (w < 64 && v != TB_UNKNOWN) { est = v; continue; }
+                const int32_t* fp = h_tfp + (size_t)k * FPW;
+                const int32_t w = fp_class(fp, 1, n, wrap(est, n));
+                const int32_t v = w >= 0 ? tab[(size_t)(w) * S + k] : TB_UNKNOWN;
+                if (w >= 0 && v != TB_UNKNOWN) { est = v; continue; }
                 int64_t next = est + (move_off[sens[k] + 1] - move_off[sens[k]]);
                 int best = -1;              // known entry nearest the window centre
                 for (int d = 0; d <= 32 && best < 0; d++) {
                     if (32 - d >= 0 && tab[(size_t)(32 - d) * S + k] != TB_UNKNOWN) best = 32 - d;
                     else if (32 + d < 64 && tab[(size_t)(32 + d) * S + k] != TB_UNKNOWN) best = 32 + d;
                 }
-                if (best >= 0) {
-                    const int64_t from = (int64_t)ws[k] + best;
-                    next = est + wrap(tab[(size_t)(best) * S + k] - from, n);
+                if (best >= 0) next = est + wrap(tab[(size_t)(best) * S + k] - fp[1 + best], n);
+                if (w < 0) {                 // re-centre: 32 of the row's mean gaps before the estimate
+                    const int32_t gap = std::max(1, wrap((int64_t)fp[64] - fp[0], n) / 64);
+                    ws[k] = wrap(est - 32 * (int64_t)gap, n);
+                    have[k] = 0;
                 }
-                if (w >= 64) { ws[k] = wrap(est - 32, n); have[k] = 0; }
                 est = wrap(next, n);
             }
             if (rounds > S + 4) { set_last_error("sweep speculation did not converge"); return CA_EDEVICE; }

@@ -356,7 +356,7 @@ def planner_leg(args, device: int, with_cpu: bool) -> dict:
     firsts = {}
     for limit in (20, 200, 0):
         ts, st = [], None
-        for _ in range(3):
+        for _ in range(5):                          # the first run also uploads the snapshot
             m.fork()
             t = time.perf_counter()
             r = m.plan_removals(*args_, hints, 0, limit)

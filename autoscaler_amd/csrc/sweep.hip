@@ -58,6 +58,7 @@ __device__ inline int64_t rl64s(int64_t v, int lane) {
 }
 __device__ inline int32_t rl32s(int32_t v, int lane) { return (int32_t)__builtin_amdgcn_readlane((uint32_t)v, lane); }
 __device__ inline uint64_t lanes_below_u(int lane) { return lane == 0 ? 0ull : (~0ull >> (64 - lane)); }
+extern "C" __device__ long long __ockl_wfred_add_i64(long long);
 
 // moved-pod semantics: Spec.NodeName cleared (cluster.go:235-240), TPU requests
 // cleared (tpu.go:57-79)
@@ -555,14 +556,15 @@ __host__ __device__ inline int32_t fp_class(const int32_t* fp, int32_t fs, int32
     int32_t d = L - f0;
     if (d < 0) d += n;
     if (d <= 0) return -1;
-    auto D = [&](int32_t w) { int32_t x = fp[(w + 1) * fs] - f0; return x <= 0 ? x + n : x; };
-    if (d > D(63)) return -1;
-    int32_t lo = 0, hi = 63;
-    while (lo < hi) {
-        const int32_t mid = (lo + hi) >> 1;
-        if (D(mid) >= d) hi = mid; else lo = mid + 1;
-    }
-    return lo;
+    auto D = [&](int32_t w) { int32_t x = fp[(size_t)(w + 1) * fs] - f0; return x <= 0 ? x + n : x; };
+    const int32_t d63 = D(63);
+    if (d > d63) return -1;
+    // interpolation, then a few steps: the fit points of a row are spread about evenly
+    int32_t w = (int32_t)((float)d * 64.0f / (float)d63) - 1;     // (no 64-bit division on the device)
+    w = w < 0 ? 0 : (w > 63 ? 63 : w);
+    while (w > 0 && D(w - 1) >= d) w--;
+    while (D(w) < d) w++;
+    return w;
 }
 
 // visible nodes (destination, schedulable, not the candidate) in the cyclic range [a, b)
@@ -612,7 +614,7 @@ __global__ void __launch_bounds__(64) k_sweep_table(
     const int32_t* __restrict__ names, const int32_t* __restrict__ hints, const int32_t* __restrict__ todo,
     const int32_t* __restrict__ wstart, const int32_t* __restrict__ row_of, int32_t* __restrict__ table,
     int32_t stride, uint32_t* __restrict__ tev, int32_t* __restrict__ tdest, const int32_t* __restrict__ tdoff,
-    int32_t* __restrict__ tfp) {
+    int32_t* __restrict__ tfp, const int32_t* __restrict__ mode) {
     // tev / tdest (first round, device walk): the lane's evaluation count and each moved
     // pod's destination, so a candidate the walk resolves through the table takes these
     // outputs (k_table_gather) instead of being simulated again
@@ -627,7 +629,7 @@ __global__ void __launch_bounds__(64) k_sweep_table(
     // the row's classes: fit points of the first pod from the window start (wave-parallel,
     // 64 positions per step), or 64 consecutive positions
     bool classes = false;
-    if (mn > 0 && n > 0) {
+    if (mode[0] && mn > 0 && n > 0) {
         const PodHot p0h = ph[move_pods[mo]];
         PodHot p0 = p0h;
         p0.flags = moved_flags(p0h.flags);
@@ -662,7 +664,7 @@ __global__ void __launch_bounds__(64) k_sweep_table(
         }
         __builtin_amdgcn_wave_barrier();
     }
-    if (tfp) for (int32_t i = lane; i < FPW; i += 64) tfp[(size_t)row * FPW + i] = fps[i];
+    if (tfp) for (int32_t i = lane; i < FPW; i += 64) tfp[(size_t)i * stride + row] = fps[i];   // [FPW][stride]
     int32_t Ls = fps[1 + lane];
     int32_t Lcur = Ls;
     int32_t adv = 0;              // positions passed since Ls
@@ -734,9 +736,32 @@ __global__ void __launch_bounds__(64) k_sweep_table(
 // est_k = L0 + sum_{i<k} adv_i (mod n); window start = est_k - 32.  One block.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(1024) k_sweep_est(const SweepOut* __restrict__ probe, const int32_t* __restrict__ sens,
-                                                    int32_t S, int64_t L0, int32_t n, int32_t* __restrict__ ws) {
-    // (window start = 32 fit points before the estimate: 32 x the probe's mean gap between
-    // placements, so a tight cluster's row of fit-point classes is centred too)
+                                                    int32_t S, int64_t L0, int32_t n, int32_t* __restrict__ ws,
+                                                    int32_t* __restrict__ mode) {
+    // Rows of fit-point classes pay off where placements are sparse: the probe's positions
+    // passed per placement decide it for the whole call (mode[0] = 1: classes, window start
+    // = 32 x the candidate's mean gap before the estimate; 0: 64 consecutive positions).
+    __shared__ int64_t part[2][16];
+    int64_t my_adv = 0, my_placed = 0;
+    for (int32_t k = threadIdx.x; k < S; k += blockDim.x) {
+        const SweepOut o = probe[sens[k]];
+        if (o.fa_success) {
+            int64_t d = ((int64_t)o.lout - (int64_t)o.lin) % n;
+            if (d < 0) d += n;
+            my_adv += d;
+            my_placed += max(1, o.n_placed);
+        }
+    }
+    my_adv = __ockl_wfred_add_i64(my_adv);
+    my_placed = __ockl_wfred_add_i64(my_placed);
+    if ((threadIdx.x & 63) == 0) { part[0][threadIdx.x >> 6] = my_adv; part[1][threadIdx.x >> 6] = my_placed; }
+    __syncthreads();
+    int64_t sum_adv = 0, sum_placed = 0;
+    for (int q = 0; q < 16; q++) { sum_adv += part[0][q]; sum_placed += part[1][q]; }
+    // C3 (a loose cluster): 1.008 positions per placement; C5 RunOnce: 1.10, where the
+    // few long gaps are what throws the consecutive windows off
+    const bool classes = sum_adv * 100 > sum_placed * 104;
+    if (threadIdx.x == 0) mode[0] = classes ? 1 : 0;
     __shared__ int64_t wtot[16];
     __shared__ int64_t carry;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -751,7 +776,7 @@ __global__ void __launch_bounds__(1024) k_sweep_est(const SweepOut* __restrict__
                 int64_t d = ((int64_t)o.lout - (int64_t)o.lin) % n;
                 if (d < 0) d += n;
                 v = d;
-                gap = max((int64_t)1, min((int64_t)(n / 64), d / max(1, o.n_placed)));
+                if (classes) gap = max((int64_t)1, min((int64_t)(n / 64), d / max(1, o.n_placed)));
             }
         }
         int64_t x = v;                                   // inclusive scan in the wave
@@ -794,24 +819,29 @@ __global__ void __launch_bounds__(1024) k_sweep_est(const SweepOut* __restrict__
 constexpr int WK = 64;
 constexpr int WALK_MAX_CHUNKS = 256;
 
-__global__ void __launch_bounds__(64) k_walk_chunks(const int32_t* __restrict__ sens, const int32_t* __restrict__ guess,
-                                                   const int32_t* __restrict__ wl, const int32_t* __restrict__ tab,
-                                                   const int32_t* __restrict__ tfp, int32_t S, int32_t n,
+__global__ void __launch_bounds__(64) k_walk_chunks(const int32_t* __restrict__ sens, const int32_t* __restrict__ ws,
+                                                   const int32_t* __restrict__ guess, const int32_t* __restrict__ wl,
+                                                   const int32_t* __restrict__ tab, const int32_t* __restrict__ tfp,
+                                                   const int32_t* __restrict__ mode, int32_t S, int32_t n,
                                                    int32_t* __restrict__ cmap, int32_t* __restrict__ traj) {
     __shared__ int32_t T[64][WK + 1];
     __shared__ int32_t FP[FPW][WK + 1];
-    __shared__ int32_t cg[WK], cwl[WK];
+    __shared__ int32_t cws[WK], cg[WK], cwl[WK];
     const int j = blockIdx.x, lane = threadIdx.x;
     const int32_t k0 = j * WK, kn = min(WK, S - k0);
+    const bool classes = mode[0] != 0;
     for (int w = 0; w < 64; w++) T[w][lane] = lane < kn ? tab[(size_t)w * S + k0 + lane] : TB_UNKNOWN;
-    for (int i = 0; i < FPW; i++) FP[i][lane] = lane < kn ? tfp[(size_t)(k0 + lane) * FPW + i] : 0;
+    if (classes)
+        for (int i = 0; i < FPW; i++) FP[i][lane] = lane < kn ? tfp[(size_t)i * S + k0 + lane] : 0;
     if (lane < kn) {
         const int32_t c = sens[k0 + lane];
+        cws[lane] = ws[k0 + lane];
         cg[lane] = guess[c];
         cwl[lane] = wl[c];
     }
     __syncthreads();
-    int32_t cur = FP[1 + lane][0];                          // lane x: class x of the chunk's first row
+    // lane x: class x of the chunk's first row (its fit point, or position ws + x)
+    int32_t cur = classes ? FP[1 + lane][0] : (int32_t)(((int64_t)cws[0] + lane) % n);
     int32_t stop = -1;
     for (int kk = 0; kk < kn; kk++) {
         int32_t enc = -1;
@@ -822,7 +852,14 @@ __global__ void __launch_bounds__(64) k_walk_chunks(const int32_t* __restrict__ 
                 if (cur == cg[kk]) {
                     cur = wlv;
                 } else {
-                    const int32_t w = fp_class(&FP[0][kk], WK + 1, n, cur);
+                    int32_t w;
+                    if (classes) {
+                        w = fp_class(&FP[0][kk], WK + 1, n, cur);
+                    } else {
+                        w = cur - cws[kk];
+                        if (w < 0) w += n;
+                        if (w >= 64) w = -1;
+                    }
                     const int32_t v = w >= 0 ? T[w][kk] : TB_UNKNOWN;
                     if (v == TB_UNKNOWN) stop = kk;
                     else { cur = v; enc |= 1; }
@@ -837,19 +874,36 @@ __global__ void __launch_bounds__(64) k_walk_chunks(const int32_t* __restrict__ 
 // info[0] = first unresolved sensitive candidate (S: all), info[1] = lastIndex before it
 __global__ void __launch_bounds__(1024) k_walk_resolve(const int32_t* __restrict__ sens, const int32_t* __restrict__ tfp,
                                                       const int32_t* __restrict__ cmap, const int32_t* __restrict__ traj,
-                                                      const int32_t* __restrict__ wl, int32_t S, int32_t n, int32_t L0n,
+                                                      const int32_t* __restrict__ wl, const int32_t* __restrict__ mode,
+                                                      int32_t S, int32_t n, int32_t L0n,
                                                       int32_t* __restrict__ lin, uint8_t* __restrict__ need,
                                                       int32_t* __restrict__ info) {
-    __shared__ int32_t cm[WALK_MAX_CHUNKS * 64];
+    // dynamic LDS: the chunk maps [nch][64] and the chunks' first rows [nch][FPW]
+    extern __shared__ int32_t wr_lds[];
     __shared__ int32_t lane_of[WALK_MAX_CHUNKS], cin[WALK_MAX_CHUNKS];
     __shared__ int32_t stop_k, cur_out;
     const int32_t nch = (S + WK - 1) / WK;
+    int32_t* const cm = wr_lds;
+    int32_t* const heads = wr_lds + (size_t)nch * 64;
     for (int32_t i = threadIdx.x; i < nch * 64; i += blockDim.x) cm[i] = cmap[i];
+    const bool classes = mode[0] != 0;
+    if (classes)
+        for (int32_t i = threadIdx.x; i < nch * FPW; i += blockDim.x)
+            heads[i] = tfp[(size_t)(i % FPW) * S + (size_t)(i / FPW) * WK];
+    else
+        for (int32_t j = threadIdx.x; j < nch; j += blockDim.x) heads[(size_t)j * FPW + 1] = tfp[(size_t)S + (size_t)j * WK];
     __syncthreads();
     if (threadIdx.x == 0) {
         int32_t cur = L0n, sk = S;
         for (int32_t j = 0; j < nch; j++) {
-            const int32_t x = fp_class(tfp + (size_t)j * WK * FPW, 1, n, cur);
+            int32_t x;
+            if (classes) {
+                x = fp_class(heads + (size_t)j * FPW, 1, n, cur);
+            } else {                          // consecutive positions from the row's first class
+                x = cur - heads[(size_t)j * FPW + 1];
+                if (x < 0) x += n;
+                if (x >= 64) x = -1;
+            }
             if (x < 0) { sk = j * WK; break; }
             lane_of[j] = x;
             cin[j] = cur;                     // the chunk's true input (its lane started at class x's point)
@@ -897,13 +951,20 @@ __global__ void __launch_bounds__(64) k_table_gather(const int32_t* __restrict__
                                                     const uint32_t* __restrict__ tev, const int32_t* __restrict__ tdest,
                                                     const int32_t* __restrict__ tdoff, const int32_t* __restrict__ move_off,
                                                     SweepOut* __restrict__ outs, int32_t* __restrict__ out_dest,
-                                                    int32_t* __restrict__ hint_set, int32_t* __restrict__ walk_lout) {
+                                                    int32_t* __restrict__ hint_set, int32_t* __restrict__ walk_lout,
+                                                    const int32_t* __restrict__ mode) {
     const int32_t k = blockIdx.x;
     const int lane = threadIdx.x;
     const int32_t c = sens[k];
     if (need[c] != 2) return;
-    const int32_t* fp = tfp + (size_t)k * FPW;
-    const int32_t x = fp_class(fp, 1, n, lin[c]);          // resolved: inside the row
+    const int32_t* fp = tfp + k;                           // column k of [FPW][S]
+    int32_t x;                                             // resolved: inside the row
+    if (mode[0]) {
+        x = fp_class(fp, S, n, lin[c]);
+    } else {
+        x = lin[c] - fp[S];
+        if (x < 0) x += n;
+    }
     const int32_t mo = move_off[c], mn = move_off[c + 1] - mo;
     const int32_t db = tdoff[k];
     for (int32_t i = lane; i < mn; i += 64) {
@@ -919,7 +980,8 @@ __global__ void __launch_bounds__(64) k_table_gather(const int32_t* __restrict__
         // the lane ran from the class's fit point: add the visible nodes skipped before it
         const int32_t node = cands[c];
         const bool node_vis = dest_mask[node] != 0 && !(hot[node].flags & NF_UNSCHED);
-        r.evals = tev[(size_t)x * S + k] + (uint64_t)vis_between(vp, n, lin[c], fp[1 + x], node, node_vis);
+        r.evals = tev[(size_t)x * S + k] +
+                  (mode[0] ? (uint64_t)vis_between(vp, n, lin[c], fp[(size_t)(1 + x) * S], node, node_vis) : 0ull);
         r.pad2 = 0;
         outs[c] = r;
         walk_lout[c] = r.lout;
@@ -1050,6 +1112,8 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     if ((rc = sw.vp.reserve(sizeof(int32_t) * ((size_t)n + 1))) != CA_OK) return rc;
     int32_t* const d_tfp = sw.tfp.as<int32_t>();
     int32_t* const h_tfp = sw.h_tfp.as<int32_t>();
+    if ((rc = sw.mode.reserve(sizeof(int32_t) * 4)) != CA_OK) return rc;
+    int32_t* const d_mode = sw.mode.as<int32_t>();
     int32_t* const d_traj = sw.wl.as<int32_t>();
     int32_t* const d_cmap = d_traj + 64 * Sx;
     int32_t* const tab = sw.h_tab.as<int32_t>();    // [64][S] host copy (host walk only)
@@ -1102,7 +1166,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         CA_HIP_CHECK(hipMemcpyAsync(d_sens, ht, sizeof(int32_t) * S, hipMemcpyHostToDevice, st));
         CA_HIP_CHECK(hipMemcpyAsync(d_tdoff, ht + 2 * S, sizeof(int32_t) * S, hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(k_sweep_est, dim3(1), dim3(1024), 0, st, d_out.as<SweepOut>(), d_sens, S, (int64_t)L0, n,
-                           d_ws);
+                           d_ws, d_mode);
         CA_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(k_sweep_table, dim3(S), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
                            m->d_static.as<NodeStatic>(), n, in.d_mask.as<uint8_t>(), in.d_c.as<int32_t>(),
@@ -1111,7 +1175,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                            m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
                            in.d_hints.as<int32_t>(), d_sens, d_ws, (const int32_t*)nullptr, sw.tab.as<int32_t>(), S,
                            dev_walk ? sw.tev.as<uint32_t>() : nullptr, dev_walk ? sw.tdest.as<int32_t>() : nullptr,
-                           dev_walk ? (const int32_t*)d_tdoff : nullptr, d_tfp);
+                           dev_walk ? (const int32_t*)d_tdoff : nullptr, d_tfp, (const int32_t*)d_mode);
         CA_HIP_CHECK(hipGetLastError());
         if (dev_walk) {
             hipLaunchKernelGGL(k_vis_prefix, dim3(1), dim3(1024), 0, st, m->d_hot.as<NodeHot>(), in.d_mask.as<uint8_t>(),
@@ -1122,16 +1186,20 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     if (dev_walk) {
         // ---- 3. device walk, then the exact pass at the exact lastIndex values ----
         CA_HIP_CHECK(hipMemsetAsync(d_need, 0, (size_t)C, st));
-        hipLaunchKernelGGL(k_walk_chunks, dim3(nch), dim3(64), 0, st, d_sens, d_lin, d_wl, sw.tab.as<int32_t>(), d_tfp,
-                           S, n, d_cmap, d_traj);
+        hipLaunchKernelGGL(k_walk_chunks, dim3(nch), dim3(64), 0, st, d_sens, d_ws, d_lin, d_wl, sw.tab.as<int32_t>(),
+                           d_tfp, d_mode, S, n, d_cmap, d_traj);
         CA_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(k_walk_resolve, dim3(1), dim3(1024), 0, st, d_sens, d_tfp, d_cmap, d_traj, d_wl, S, n,
-                           wrap(L0, n), d_lin, d_need, d_info);
+        const size_t wr_bytes = sizeof(int32_t) * (size_t)nch * (64 + FPW);
+        CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_walk_resolve, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)wr_bytes));
+        hipLaunchKernelGGL(k_walk_resolve, dim3(1), dim3(1024), wr_bytes, st, d_sens, d_tfp, d_cmap, d_traj, d_wl, d_mode,
+                           S, n, wrap(L0, n), d_lin, d_need, d_info);
         CA_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(k_table_gather, dim3(S), dim3(64), 0, st, d_sens, d_tfp, sw.vp.as<int32_t>(),
                            in.d_c.as<int32_t>(), in.d_mask.as<uint8_t>(), m->d_hot.as<NodeHot>(), S, n, d_lin, d_need,
                            sw.tab.as<int32_t>(), sw.tev.as<uint32_t>(), sw.tdest.as<int32_t>(), d_tdoff,
-                           in.d_off.as<int32_t>(), d_out.as<SweepOut>(), d_dest.as<int32_t>(), d_hset.as<int32_t>(), d_wl);
+                           in.d_off.as<int32_t>(), d_out.as<SweepOut>(), d_dest.as<int32_t>(), d_hset.as<int32_t>(), d_wl,
+                           d_mode);
         CA_HIP_CHECK(hipGetLastError());
         if ((rc = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl)) != CA_OK) return rc;
     }
@@ -1200,7 +1268,8 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                                    m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
                                    m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
                                    in.d_hints.as<int32_t>(), sw.todo.as<int32_t>(), sw.todo.as<int32_t>() + T,
-                                   (const int32_t*)nullptr, sw.tab.as<int32_t>(), T, nullptr, nullptr, nullptr, d_tfp);
+                                   (const int32_t*)nullptr, sw.tab.as<int32_t>(), T, nullptr, nullptr, nullptr, d_tfp,
+                                   (const int32_t*)d_mode);
                 CA_HIP_CHECK(hipGetLastError());
                 CA_HIP_CHECK(hipEventRecord(m->ev1, st));
                 // compact rows (row t of this round): only they cross PCIe, then go to their
@@ -1212,10 +1281,11 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 CA_HIP_CHECK(hipMemcpyAsync(ct + 64 * (size_t)T, d_tfp, sizeof(int32_t) * FPW * (size_t)T,
                                             hipMemcpyDeviceToHost, st));
                 CA_HIP_CHECK(hipStreamSynchronize(st));
+                const int32_t* ctf = ct + 64 * (size_t)T;
                 for (int32_t t = 0; t < T; t++) {
                     const int32_t k = todo_k[t];
                     for (int32_t w = 0; w < 64; w++) tab[(size_t)w * S + k] = ct[(size_t)w * T + t];
-                    std::memcpy(h_tfp + (size_t)k * FPW, ct + 64 * (size_t)T + (size_t)t * FPW, sizeof(int32_t) * FPW);
+                    for (int32_t i = 0; i < FPW; i++) h_tfp[(size_t)i * S + k] = ctf[(size_t)i * T + t];
                 }
                 float ms = 0;
                 (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
@@ -1231,7 +1301,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 exact_lin[c] = (int32_t)cur;
                 if (wlv < 0) continue;                                             // lastIndex passes through
                 if (wrap(cur, n) == guess[c]) { cur = wlv; continue; }            // probed at the true value
-                const int32_t w = fp_class(h_tfp + (size_t)k0 * FPW, 1, n, wrap(cur, n));
+                const int32_t w = fp_class(h_tfp + k0, S, n, wrap(cur, n));
                 if (w < 0) break;
                 int32_t v = tab[(size_t)(w) * S + k0];
                 if (v == TB_UNKNOWN) {
@@ -1257,8 +1327,8 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
             int64_t est = cur;
             for (int32_t k = k0; k < std::min(S, k0 + LOOKAHEAD); k++) {
                 if (insensitive(k)) continue;
-                const int32_t* fp = h_tfp + (size_t)k * FPW;
-                const int32_t w = fp_class(fp, 1, n, wrap(est, n));
+                const int32_t* fp = h_tfp + k;                      // column k of [FPW][S]
+                const int32_t w = fp_class(fp, S, n, wrap(est, n));
                 const int32_t v = w >= 0 ? tab[(size_t)(w) * S + k] : TB_UNKNOWN;
                 if (w >= 0 && v != TB_UNKNOWN) { est = v; continue; }
                 int64_t next = est + (move_off[sens[k] + 1] - move_off[sens[k]]);
@@ -1267,9 +1337,9 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                     if (32 - d >= 0 && tab[(size_t)(32 - d) * S + k] != TB_UNKNOWN) best = 32 - d;
                     else if (32 + d < 64 && tab[(size_t)(32 + d) * S + k] != TB_UNKNOWN) best = 32 + d;
                 }
-                if (best >= 0) next = est + wrap(tab[(size_t)(best) * S + k] - fp[1 + best], n);
+                if (best >= 0) next = est + wrap(tab[(size_t)(best) * S + k] - fp[(size_t)(1 + best) * S], n);
                 if (w < 0) {                 // re-centre: 32 of the row's mean gaps before the estimate
-                    const int32_t gap = std::max(1, wrap((int64_t)fp[64] - fp[0], n) / 64);
+                    const int32_t gap = std::max(1, wrap((int64_t)fp[(size_t)64 * S] - fp[0], n) / 64);
                     ws[k] = wrap(est - 32 * (int64_t)gap, n);
                     have[k] = 0;
                 }

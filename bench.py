@@ -349,12 +349,12 @@ def planner_leg(args, device: int, with_cpu: bool) -> dict:
     w = W.c3(n_nodes=args.sweep_nodes)
     args_ = (w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods)
     hints = np.full(len(w.table), -1, np.int32)
-    m = native.Mirror(device)
-    W.load_sweep(m, w)
     out = {"workload": f"C3: {args.sweep_nodes} nodes, {len(w.table)} running pods, candidates = all nodes in order",
            "runs": {}}
     firsts = {}
     for limit in (20, 200, 0):
+        m = native.Mirror(device)                   # fresh: the copies' ids then match the port's
+        W.load_sweep(m, w)
         ts, st = [], None
         for _ in range(5):                          # the first run also uploads the snapshot
             m.fork()
@@ -368,7 +368,7 @@ def planner_leg(args, device: int, with_cpu: bool) -> dict:
                                    "conflicts": st["conflicts"], "simulated": st["simulated"],
                                    "removable": int(r.results["removable"].sum()),
                                    "candidates_run": int((r.results["reason"] != 101).sum())}
-    m.close()
+        m.close()
     if with_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle                                           # CPU baseline leg only

@@ -200,6 +200,10 @@ __host__ __device__ inline uint32_t dev_fit_reasons(int64_t pcpu, int64_t pmem, 
 
 void set_last_error(const std::string& s);
 
+// hipFuncAttributeMaxDynamicSharedMemorySize of a kernel, raised to `bytes` at most once
+// per (device, kernel) and size: the call costs tens of microseconds, too much per launch.
+int ensure_dyn_lds(const void* kernel, size_t bytes);
+
 // A growable device buffer.
 struct DevBuf {
     void* ptr = nullptr;

@@ -2205,9 +2205,10 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             CA_HIP_CHECK(hipEventRecord(p->ev_pub, st));
         }
         CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN0], st));
-        if (!grows)
-            CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_ffd_chain<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)lds));
+        if (!grows) {
+            int rcl;
+            if ((rcl = ensure_dyn_lds((const void*)k_ffd_chain<false>, lds)) != CA_OK) return rcl;
+        }
         auto chain = [&](hipStream_t ss, const int32_t* gm, int32_t ng) -> int {
             hipLaunchKernelGGL(grows ? k_ffd_chain<true> : k_ffd_chain<false>, dim3(ng), dim3(CT), lds, ss,
                                p->d_meta.as<GroupMeta>(),

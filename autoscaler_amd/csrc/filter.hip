@@ -1423,7 +1423,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
         fa.cls_mark = a.cls_mark; fa.cls_capped = a.cls_capped; fa.cls_owner = a.cls_owner;
         fa.ctl = a.ctl;
         const size_t lds_all = fb_lds(S, NW, K, fb_stat_in_lds, n_classes, n_owners).total;
-        CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_fb_walk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_all));
+        if ((rc = ensure_dyn_lds((const void*)k_fb_walk, lds_all)) != CA_OK) return rc;
         hipLaunchKernelGGL(k_fb_walk, dim3(1), dim3(FB_T), lds_all, m->stream, fa);
         CA_HIP_CHECK(hipGetLastError());
         fo.path = 1;

@@ -18,6 +18,20 @@ namespace casim {
 static thread_local std::string g_last_error;
 void set_last_error(const std::string& s) { g_last_error = s; }
 
+int ensure_dyn_lds(const void* kernel, size_t bytes) {
+    static std::mutex mu;
+    static std::unordered_map<uint64_t, size_t> done;      // (device, kernel) -> limit set
+    int dev = 0;
+    CA_HIP_CHECK(hipGetDevice(&dev));
+    const uint64_t key = ((uint64_t)(uint32_t)dev << 56) ^ (uint64_t)(uintptr_t)kernel;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = done.find(key);
+    if (it != done.end() && it->second >= bytes) return CA_OK;
+    CA_HIP_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    done[key] = bytes;
+    return CA_OK;
+}
+
 // Both buffers grow geometrically: a hipMalloc / hipHostMalloc (and the free before it)
 // costs up to milliseconds, and callers like the planner's rounds grow them step by step.
 int DevBuf::reserve(size_t need) {

@@ -575,9 +575,9 @@ __device__ inline int32_t vis_between(const int32_t* __restrict__ vp, int32_t n,
     return v - ((in && node_vis) ? 1 : 0);
 }
 
-// vp[i] = destination, schedulable nodes among positions [0, i) (one block)
-__global__ void __launch_bounds__(1024) k_vis_prefix(const NodeHot* __restrict__ hot, const uint8_t* __restrict__ dest_mask,
-                                                     int32_t n, int32_t* __restrict__ vp) {
+// vp[i] = destination, schedulable nodes among positions [0, i) (one block of 1024 threads)
+__device__ void vis_prefix_block(const NodeHot* __restrict__ hot, const uint8_t* __restrict__ dest_mask, int32_t n,
+                                 int32_t* __restrict__ vp) {
     __shared__ int32_t wsum[16];
     __shared__ int32_t carry;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -737,7 +737,8 @@ __global__ void __launch_bounds__(64) k_sweep_table(
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(1024) k_sweep_est(const SweepOut* __restrict__ probe, const int32_t* __restrict__ sens,
                                                     int32_t S, int64_t L0, int32_t n, int32_t* __restrict__ ws,
-                                                    int32_t* __restrict__ mode) {
+                                                    int32_t* __restrict__ mode, const NodeHot* __restrict__ hot,
+                                                    const uint8_t* __restrict__ dest_mask, int32_t* __restrict__ vp) {
     // Rows of fit-point classes pay off where placements are sparse: the probe's positions
     // passed per placement decide it for the whole call (mode[0] = 1: classes, window start
     // = 32 x the candidate's mean gap before the estimate; 0: 64 consecutive positions).
@@ -762,6 +763,7 @@ __global__ void __launch_bounds__(1024) k_sweep_est(const SweepOut* __restrict__
     // few long gaps are what throws the consecutive windows off
     const bool classes = sum_adv * 100 > sum_placed * 104;
     if (threadIdx.x == 0) mode[0] = classes ? 1 : 0;
+    if (classes && vp) vis_prefix_block(hot, dest_mask, n, vp);    // for k_table_gather's evaluation counts
     __shared__ int64_t wtot[16];
     __shared__ int64_t carry;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1035,8 +1037,10 @@ int launch_exact(ca_mirror* m, hipStream_t st, const SweepCall& in, const int32_
                  DevView d_dest, DevView d_hset, DevView d_out, int32_t* d_wl) {
     const bool use_ext = m->n_ext_pods > 0;
     const size_t dyn = use_ext ? sizeof(OverlayExt) : 0;
-    if (use_ext)
-        CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_sweep, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+    if (use_ext) {
+        int rc;
+        if ((rc = ensure_dyn_lds((const void*)k_sweep, dyn)) != CA_OK) return rc;
+    }
     hipLaunchKernelGGL(k_sweep, dim3(in.C), dim3(64), dyn, st, m->d_hot.as<NodeHot>(), m->d_ext.as<NodeExt>(),
                        m->d_static.as<NodeStatic>(), in.n, in.d_mask.as<uint8_t>(), in.d_c.as<int32_t>(),
                        in.d_status.as<int32_t>(), in.d_off.as<int32_t>(), in.d_moves.as<int32_t>(),
@@ -1166,7 +1170,8 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         CA_HIP_CHECK(hipMemcpyAsync(d_sens, ht, sizeof(int32_t) * S, hipMemcpyHostToDevice, st));
         CA_HIP_CHECK(hipMemcpyAsync(d_tdoff, ht + 2 * S, sizeof(int32_t) * S, hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(k_sweep_est, dim3(1), dim3(1024), 0, st, d_out.as<SweepOut>(), d_sens, S, (int64_t)L0, n,
-                           d_ws, d_mode);
+                           d_ws, d_mode, m->d_hot.as<NodeHot>(), in.d_mask.as<uint8_t>(),
+                           dev_walk ? sw.vp.as<int32_t>() : nullptr);
         CA_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(k_sweep_table, dim3(S), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
                            m->d_static.as<NodeStatic>(), n, in.d_mask.as<uint8_t>(), in.d_c.as<int32_t>(),
@@ -1177,11 +1182,6 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                            dev_walk ? sw.tev.as<uint32_t>() : nullptr, dev_walk ? sw.tdest.as<int32_t>() : nullptr,
                            dev_walk ? (const int32_t*)d_tdoff : nullptr, d_tfp, (const int32_t*)d_mode);
         CA_HIP_CHECK(hipGetLastError());
-        if (dev_walk) {
-            hipLaunchKernelGGL(k_vis_prefix, dim3(1), dim3(1024), 0, st, m->d_hot.as<NodeHot>(), in.d_mask.as<uint8_t>(),
-                               n, sw.vp.as<int32_t>());
-            CA_HIP_CHECK(hipGetLastError());
-        }
     }
     if (dev_walk) {
         // ---- 3. device walk, then the exact pass at the exact lastIndex values ----
@@ -1190,8 +1190,9 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                            d_tfp, d_mode, S, n, d_cmap, d_traj);
         CA_HIP_CHECK(hipGetLastError());
         const size_t wr_bytes = sizeof(int32_t) * (size_t)nch * (64 + FPW);
-        CA_HIP_CHECK(hipFuncSetAttribute((const void*)k_walk_resolve, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)wr_bytes));
+        if ((rc = ensure_dyn_lds((const void*)k_walk_resolve, sizeof(int32_t) * (size_t)WALK_MAX_CHUNKS * (64 + FPW))) !=
+            CA_OK)
+            return rc;
         hipLaunchKernelGGL(k_walk_resolve, dim3(1), dim3(1024), wr_bytes, st, d_sens, d_tfp, d_cmap, d_traj, d_wl, d_mode,
                            S, n, wrap(L0, n), d_lin, d_need, d_info);
         CA_HIP_CHECK(hipGetLastError());

@@ -50,6 +50,7 @@ struct SweepScratch {
     DevBuf in, lin, need, out, todo, tab, wl;
     DevBuf tev, tdest;              // table lanes' evaluation counts and pod destinations (first round)
     DevBuf tfp, vp, mode;           // table rows' fit-point classes; visible-node prefix counts; class mode
+    DevBuf bsum;                    // per 64-node block: maxima of the visible rows (sweep.hip BlockSum)
     HostBuf h_in, h_tab, h_out, h_todo, h_lin, h_wl, h_tfp, h_ctab;
 };
 

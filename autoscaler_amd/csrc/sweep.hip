@@ -76,6 +76,67 @@ __device__ inline bool hot_fits(const PodHot& p, const NodeHot& h) {
     return (h.pods >= 1) & (((p.flags & PF_ALL_ZERO) != 0) | res);
 }
 
+// Per 64-node block of the ring: the largest free cpu / memory / ephemeral storage / pod
+// slots over its visible nodes (destination, schedulable) and their bit mask.  A pod that
+// fails the maxima fits no node of the block, so a scan passes the block without reading
+// its rows and counts its visible nodes from the mask (tight clusters: the planner's later
+// windows, RunOnce, where most scans cross long runs of full nodes).  Built per sweep call
+// (the destination mask is an input of the call).
+struct alignas(8) BlockSum {
+    int64_t cpu, mem, eph;
+    uint64_t vis;
+    int32_t pods, pad;
+};
+static_assert(sizeof(BlockSum) == 40, "BlockSum");
+
+__device__ inline bool block_may_fit(const PodHot& p, const BlockSum& b) {
+    const bool res = (p.cpu <= b.cpu) & (p.mem <= b.mem) & (p.eph <= b.eph);
+    return (b.vis != 0) & (b.pods >= 1) & (((p.flags & PF_ALL_ZERO) != 0) | res);
+}
+
+// visible nodes of block b in lanes [lo, hi), the candidate's node excluded
+__device__ inline int32_t block_vis(const BlockSum& b, int32_t blk, int lo, int hi, int32_t node) {
+    uint64_t m = b.vis;
+    if (hi < 64) m &= (1ull << hi) - 1;
+    m &= ~0ull << lo;
+    if ((node >> 6) == blk) m &= ~(1ull << (node & 63));
+    return __popcll(m);
+}
+
+__device__ inline int64_t wave_max_i64(int64_t v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t u = __shfl_xor(v, o, 64);
+        v = u > v ? u : v;
+    }
+    return v;
+}
+
+__global__ void __launch_bounds__(64) k_block_sum(const NodeHot* __restrict__ hot, const uint8_t* __restrict__ dest_mask,
+                                                 int32_t n, BlockSum* __restrict__ bsum) {
+    const int32_t j = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int32_t pos = j * 64 + lane;
+    bool v = false;
+    NodeHot h = {};
+    if (pos < n) {
+        h = hot[pos];
+        v = dest_mask[pos] != 0 && !(h.flags & NF_UNSCHED);
+    }
+    const uint64_t vm = __ballot(v);
+    const int64_t lo = INT64_MIN;
+    const int64_t c = wave_max_i64(v ? h.cpu : lo);
+    const int64_t m = wave_max_i64(v ? h.mem : lo);
+    const int64_t e = wave_max_i64(v ? h.eph : lo);
+    const int64_t p = wave_max_i64(v ? (int64_t)h.pods : lo);
+    if (lane == 0) {
+        BlockSum b;
+        b.cpu = c; b.mem = m; b.eph = e; b.vis = vm;
+        b.pods = vm ? (int32_t)p : 0;
+        b.pad = 0;
+        bsum[j] = b;
+    }
+}
+
 // Full filter chain on a (possibly overlay-adjusted) row; per lane.
 __device__ inline bool eval_node(const ca_pod_spec& s, const PodHot& p, const int64_t* psc,
                                  const ca_selector_term* terms, const ca_selector_req* reqs,
@@ -127,7 +188,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CASIM_S
     const ca_pod_spec* __restrict__ specs, const ca_selector_term* __restrict__ terms,
     const ca_selector_req* __restrict__ reqs, const int32_t* __restrict__ names, const int32_t* __restrict__ hints,
     const int32_t* __restrict__ lin_arr, const uint8_t* __restrict__ need, int32_t* __restrict__ out_dest,
-    int32_t* __restrict__ hint_set, SweepOut* __restrict__ outs, int32_t* __restrict__ walk_lout, int32_t use_ext) {
+    int32_t* __restrict__ hint_set, SweepOut* __restrict__ outs, int32_t* __restrict__ walk_lout, int32_t use_ext,
+    const BlockSum* __restrict__ bsum) {
     __shared__ OverlaySmem ov;
     extern __shared__ __attribute__((aligned(16))) unsigned char ovx_raw[];
     OverlayExt& ox = *reinterpret_cast<OverlayExt*>(ovx_raw);
@@ -447,6 +509,30 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CASIM_S
                 if (r == nb && l0 == 0) break;
                 int32_t j = j0 + r;
                 if (j >= nb) j -= nb;
+                if (r > 0 && r < nb) {
+                    // look ahead over the next 64 full blocks: pass every leading block whose
+                    // maxima the pod fails (and that holds none of this candidate's placements,
+                    // whose deltas the maxima do not see), counting its visible nodes
+                    const int32_t rr = r + lane;
+                    bool pass = false;
+                    int32_t nv = 0;
+                    if (rr < nb) {
+                        int32_t jj = j0 + rr;
+                        if (jj >= nb) jj -= nb;
+                        const BlockSum b = bsum[jj];
+                        bool ovh = false;
+                        for (int32_t q = 0; q < npl; q++) ovh |= (ov.node[q] >> 6) == jj;
+                        pass = !ovh && !block_may_fit(p, b);
+                        nv = block_vis(b, jj, 0, 64, node);
+                    }
+                    const uint64_t stop = __ballot(!pass);
+                    const int32_t k = stop ? __builtin_ctzll(stop) : 64;
+                    if (k > 0) {
+                        evals += (uint64_t)__ockl_wfred_add_i64(lane < k ? nv : 0);
+                        r += k - 1;
+                        continue;
+                    }
+                }
                 NodeHot raw;
                 bool bvis;
                 int64_t dc, dmm, de;
@@ -614,7 +700,7 @@ __global__ void __launch_bounds__(64) k_sweep_table(
     const int32_t* __restrict__ names, const int32_t* __restrict__ hints, const int32_t* __restrict__ todo,
     const int32_t* __restrict__ wstart, const int32_t* __restrict__ row_of, int32_t* __restrict__ table,
     int32_t stride, uint32_t* __restrict__ tev, int32_t* __restrict__ tdest, const int32_t* __restrict__ tdoff,
-    int32_t* __restrict__ tfp, const int32_t* __restrict__ mode) {
+    int32_t* __restrict__ tfp, const int32_t* __restrict__ mode, const BlockSum* __restrict__ bsum) {
     // tev / tdest (first round, device walk): the lane's evaluation count and each moved
     // pod's destination, so a candidate the walk resolves through the table takes these
     // outputs (k_table_gather) instead of being simulated again
@@ -635,20 +721,40 @@ __global__ void __launch_bounds__(64) k_sweep_table(
         p0.flags = moved_flags(p0h.flags);
         if (!(p0.flags & (PF_PREFILTER_NAMES | PF_PREFILTER_FAIL | PF_PORTS | PF_SCALAR_REQ))) {
             const ca_pod_spec& s0 = specs[p0.spec];
+            // ring order from the window start: the tail of its block, the blocks after it
+            // (64 at a time passed on their maxima), the head of its block
+            const int32_t nb = (n + 63) >> 6;
+            int32_t ws = ws0;
+            if (ws >= n) ws -= n;
+            const int32_t j0 = ws >> 6, l0 = ws & 63;
             int32_t cnt = 0;
-            for (int32_t base = 0; base < n && cnt < FPW; base += 64) {
-                int32_t pos = ws0 + base + lane;
-                if (pos >= n) pos -= n;
-                if (pos >= n) pos -= n;
+            for (int32_t r = 0; r <= nb && cnt < FPW; r++) {
+                if (r == nb && l0 == 0) break;
+                int32_t j = j0 + r;
+                if (j >= nb) j -= nb;
+                if (r > 0 && r < nb) {
+                    const int32_t rr = r + lane;
+                    bool pass = false;
+                    if (rr < nb) {
+                        int32_t jj = j0 + rr;
+                        if (jj >= nb) jj -= nb;
+                        pass = !block_may_fit(p0, bsum[jj]);
+                    }
+                    const uint64_t stop = __ballot(!pass);
+                    const int32_t k = stop ? __builtin_ctzll(stop) : 64;
+                    if (k > 0) { r += k - 1; continue; }
+                }
+                const int32_t pos = j * 64 + lane;
+                const bool inr = (pos < n) & ((r == 0) ? lane >= l0 : (r == nb ? lane < l0 : true));
                 bool fit = false;
-                if (base + lane < n) {
+                if (inr) {
                     const NodeHot nh = hot[pos];
                     fit = (pos != node) & (dest_mask[pos] != 0) & !(nh.flags & NF_UNSCHED) && hot_fits(p0, nh) &&
                           static_ok(s0, p0, terms, reqs, nh, st + pos);
                 }
                 const uint64_t m = __ballot(fit);
-                const int32_t r = cnt + __popcll(m & lanes_below_u(lane));
-                if (fit && r < FPW) fps[r] = pos;
+                const int32_t rk = cnt + __popcll(m & lanes_below_u(lane));
+                if (fit && rk < FPW) fps[rk] = pos;
                 cnt += __popcll(m);
             }
             classes = cnt >= FPW;
@@ -698,11 +804,29 @@ __global__ void __launch_bounds__(64) k_sweep_table(
             if (p.flags & PF_PREFILTER_FAIL) { unknown = true; break; }         // FitsAnyNode error: exact kernel
             const ca_pod_spec& s = specs[p.spec];
             // lane-private rotating scan from this lane's lastIndex
-            int32_t steps = 0;
+            int32_t steps = 0, work = 0;
             int32_t pos = Lcur;
             bool lane_unknown = false;
+            const bool skip_ok = !(p.flags & PF_PREFILTER_NAMES);
+            int32_t okb = -1;             // block whose maxima the pod passes
             while (!unknown) {
-                if (adv + steps >= n || steps >= TB_SCAN) { lane_unknown = true; break; }
+                if (adv + steps >= n || work >= TB_SCAN) { lane_unknown = true; break; }
+                const int32_t b = pos >> 6;
+                if (skip_ok && b != okb) {
+                    // the rest of a block whose maxima the pod fails: passed in one step (the
+                    // lane's placements all lie behind it, so the committed rows are exact)
+                    const BlockSum bs = bsum[b];
+                    if (!block_may_fit(p, bs)) {
+                        const int32_t end = min((b + 1) * 64, n);
+                        ev += (uint32_t)block_vis(bs, b, pos & 63, end - b * 64, node);
+                        steps += end - pos;
+                        pos = end >= n ? 0 : end;
+                        work++;
+                        continue;
+                    }
+                    okb = b;
+                }
+                work++;
                 const NodeHot nh = hot[pos];
                 const uint8_t dm = dest_mask[pos];
                 bool vis = (pos != node) & (dm != 0) & !(nh.flags & NF_UNSCHED);
@@ -1047,7 +1171,8 @@ int launch_exact(ca_mirror* m, hipStream_t st, const SweepCall& in, const int32_
                        m->d_pods.hot.as<PodHot>(), m->d_pods.spec.as<ca_pod_spec>(),
                        m->d_pods.terms.as<ca_selector_term>(), m->d_pods.reqs.as<ca_selector_req>(),
                        m->d_pods.names.as<int32_t>(), in.d_hints.as<int32_t>(), d_lin, d_need, d_dest.as<int32_t>(),
-                       d_hset.as<int32_t>(), d_out.as<SweepOut>(), d_wl, use_ext ? 1 : 0);
+                       d_hset.as<int32_t>(), d_out.as<SweepOut>(), d_wl, use_ext ? 1 : 0,
+                       m->sw.bsum.as<BlockSum>());
     CA_HIP_CHECK(hipGetLastError());
     return CA_OK;
 }
@@ -1150,6 +1275,12 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         CA_HIP_CHECK(hipGetLastError());
     }
     CA_HIP_CHECK(hipEventRecord(m->ev0, st));
+    if ((rc = sw.bsum.reserve(sizeof(BlockSum) * (size_t)std::max((n + 63) / 64, 1))) != CA_OK) return rc;
+    if (n > 0) {
+        hipLaunchKernelGGL(k_block_sum, dim3((n + 63) / 64), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
+                           in.d_mask.as<uint8_t>(), n, sw.bsum.as<BlockSum>());
+        CA_HIP_CHECK(hipGetLastError());
+    }
     if ((rc = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl)) != CA_OK) return rc;
     int32_t rounds = 1, exact_runs = 0;
     int32_t* const d_tdoff = d_sens + 2 * (size_t)S;     // per sensitive candidate: its pods in tdest
@@ -1180,7 +1311,8 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                            m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
                            in.d_hints.as<int32_t>(), d_sens, d_ws, (const int32_t*)nullptr, sw.tab.as<int32_t>(), S,
                            dev_walk ? sw.tev.as<uint32_t>() : nullptr, dev_walk ? sw.tdest.as<int32_t>() : nullptr,
-                           dev_walk ? (const int32_t*)d_tdoff : nullptr, d_tfp, (const int32_t*)d_mode);
+                           dev_walk ? (const int32_t*)d_tdoff : nullptr, d_tfp, (const int32_t*)d_mode,
+                           sw.bsum.as<BlockSum>());
         CA_HIP_CHECK(hipGetLastError());
     }
     if (dev_walk) {
@@ -1270,7 +1402,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                                    m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
                                    in.d_hints.as<int32_t>(), sw.todo.as<int32_t>(), sw.todo.as<int32_t>() + T,
                                    (const int32_t*)nullptr, sw.tab.as<int32_t>(), T, nullptr, nullptr, nullptr, d_tfp,
-                                   (const int32_t*)d_mode);
+                                   (const int32_t*)d_mode, sw.bsum.as<BlockSum>());
                 CA_HIP_CHECK(hipGetLastError());
                 CA_HIP_CHECK(hipEventRecord(m->ev1, st));
                 // compact rows (row t of this round): only they cross PCIe, then go to their

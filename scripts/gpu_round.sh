@@ -21,11 +21,17 @@ if [[ "$STEP" == all || "$STEP" == bench ]]; then
   cat gpurun_out/bench.json
 fi
 if [[ "$STEP" == all || "$STEP" == prof ]]; then
+  # the headline alone (the bench line's kernel averages come from these launches only),
+  # then the other legs in a profile of their own
   cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run \
-     --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-sweep --no-c4 \
+     --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-sweep --no-c4 \
+     --no-expansion --no-util --no-filter --no-unlimited --no-runonce --no-planner \
      > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1 || { echo PROF FAILED; tail -20 "$GRAFT_REPO_ROOT/gpurun_out/prof.log"; exit 1; }
+  cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_legs" -o run \
+     --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline \
+     > "$GRAFT_REPO_ROOT/gpurun_out/prof_legs.log" 2>&1 || { echo PROF LEGS FAILED; tail -20 "$GRAFT_REPO_ROOT/gpurun_out/prof_legs.log"; exit 1; }
   cd "$GRAFT_REPO_ROOT"
-  find gpurun_out/prof -name "*kernel_stats*" | head -3
+  echo PROF_OK
 fi
 if [[ "$STEP" == pmc ]]; then
   # HBM traffic: one counter per pass (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950)

@@ -855,12 +855,15 @@ __device__ inline Seg ld_seg(const Seg* p) {
 // `start_ticks` (100 MHz wall clock; the kernels were serialised) sets qctl[2] and ends,
 // as does one whose ticket is not pushed within 200 ms of a started chain (a chain that
 // died).  qctl[2] sends the host to the stream-ordered copy (k_copy_segments + D2H).
+// T = int32_t: pod ids; T = uint16_t: pod ids of a podset of at most 65535 pods, 0xFFFF for
+// "not scheduled" (ca_estimate_plan_run_u16: half the bytes over PCIe).
+template <typename T>
 __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ groups, const ChainOut* __restrict__ outs,
                                                 const Seg* __restrict__ segs, const int32_t* __restrict__ spod,
                                                 const int32_t* sched_dev, int32_t* __restrict__ tickets,
                                                 int32_t* __restrict__ qctl, int32_t total, int32_t nsub,
                                                 const int2* __restrict__ prog, int32_t pch,
-                                                int32_t* pub,        // pub may alias sched_dev (device results)
+                                                T* pub,              // pub may alias sched_dev (device results)
                                                 uint64_t start_ticks) {
     __shared__ int32_t s_t, s_tk, s_seg0;
     for (;;) {
@@ -923,10 +926,10 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
                 }
             }
             for (int32_t i = at + (int32_t)threadIdx.x; i < lim; i += blockDim.x)
-                pub[gm.off + i] = from_seg ? spod[gm.off + src_off + i] : sched_dev[gm.off + i];
+                pub[gm.off + i] = (T)(from_seg ? spod[gm.off + src_off + i] : sched_dev[gm.off + i]);
             at = lim;
         }
-        for (int32_t i = max(a, ns) + (int32_t)threadIdx.x; i < b; i += blockDim.x) pub[gm.off + i] = -1;
+        for (int32_t i = max(a, ns) + (int32_t)threadIdx.x; i < b; i += blockDim.x) pub[gm.off + i] = (T)-1;
         lds_barrier();
     }
 }
@@ -1764,7 +1767,7 @@ struct ca_estimate_plan {
     bool use_ports = false, use_scalar = false;
     int32_t n_masks = 0, n_tiles = 0;
     DevBuf d_meta, d_pod_idx, d_tmpl, d_sortA, d_sortB, d_stream, d_spod, d_seg, d_heads, d_unsup, d_lin, d_need,
-        d_out, d_sched_pod, d_sched_node, d_crank, d_hist;
+        d_out, d_sched_pod, d_sched_node, d_crank, d_hist, d_sched16;
     // HBM-slab rows (k_ffd_chain<true>): per group kcap and slab offset, for the limiter
     // setting they were sized for (slab_max_nodes)
     DevBuf d_slab, d_slab_off, d_gkcap;
@@ -1944,6 +1947,30 @@ uint64_t pub_start_ticks() {
     return (uint64_t)us * 100ull;
 }
 
+__global__ void k_narrow16(const int32_t* __restrict__ src, uint16_t* __restrict__ dst, int32_t n) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = (uint16_t)src[i];
+}
+
+// the plan's device results (sched_pod layout) into the caller's buffer: int32 ids, or
+// 16-bit ids narrowed on the device first (stream-ordered copies)
+int results_to_host(ca_estimate_plan* p, hipStream_t st, int32_t* sched_pod, uint16_t* sched16) {
+    const int32_t n = std::max(p->total, 0);
+    if (!sched16) {
+        CA_HIP_CHECK(hipMemcpyAsync(sched_pod, p->d_sched_pod.ptr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+        return CA_OK;
+    }
+    int rc;
+    if ((rc = p->d_sched16.reserve(sizeof(uint16_t) * (size_t)std::max(n, 1))) != CA_OK) return rc;
+    if (n > 0) {
+        hipLaunchKernelGGL(k_narrow16, dim3((n + 255) / 256), dim3(256), 0, st, p->d_sched_pod.as<int32_t>(),
+                           p->d_sched16.as<uint16_t>(), n);
+        CA_HIP_CHECK(hipGetLastError());
+        CA_HIP_CHECK(hipMemcpyAsync(sched16, p->d_sched16.ptr, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, st));
+    }
+    return CA_OK;
+}
+
 int32_t pub_blocks() {
     const char* e = getenv("CASIM_PUB_BLOCKS");
     return e ? std::max(1, atoi(e)) : 32;        // scripts/pub_sweep.sh: 32 x 4096-output chunks on C2
@@ -1958,15 +1985,17 @@ size_t chain_lds_bytes(int32_t kcap, bool use_ports, bool use_scalar) {
 }
 
 int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca_estimate_result* results,
-             int32_t* sched_pod, int32_t* sched_node) {
+             int32_t* sched_pod, int32_t* sched_node, uint16_t* sched16 = nullptr) {
     ca_mirror* m = p->m;
     hipStream_t st = m->stream;
     const int32_t G = p->G;
     if (!lim || !last_index || !results) return CA_EINVAL;
     // sched_pod == NULL: the scheduled pods stay in device memory (ca_estimate_plan_fetch /
     // ca_estimate_plan_device_results); no node ordinals then
-    const bool to_host = sched_pod != nullptr;
+    const bool to_host = sched_pod != nullptr || sched16 != nullptr;
     if (!to_host && sched_node) return CA_EINVAL;
+    // 16-bit results: pod ids of a podset of at most 65535 pods (0xFFFF: not scheduled)
+    if (sched16 && (sched_pod || sched_node || p->s->h_pods.size() > 65535)) return CA_EINVAL;
     p->pub_state = 0;
     const auto t_start = std::chrono::steady_clock::now();
     CA_HIP_CHECK(hipSetDevice(m->device));
@@ -2012,7 +2041,8 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     if (to_host && !sched_node && p->total > 0 && (int64_t)G * p->nsub < INT32_MAX && !getenv("CASIM_NO_PUBLISH")) {
         {
             hipPointerAttribute_t attr;
-            if (hipPointerGetAttributes(&attr, sched_pod) == hipSuccess && attr.type == hipMemoryTypeHost &&
+            const void* hp = sched16 ? (const void*)sched16 : (const void*)sched_pod;
+            if (hipPointerGetAttributes(&attr, hp) == hipSuccess && attr.type == hipMemoryTypeHost &&
                 attr.devicePointer != nullptr)
                 publish = static_cast<int32_t*>(attr.devicePointer);
             else
@@ -2191,11 +2221,18 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         // CASIM_PUB_SERIAL (tests): the publisher goes first on the chains' own stream, i.e.
         // the two kernels are serialised — it must give up at its start deadline
         auto launch_pub = [&](hipStream_t ps) -> int {
-            hipLaunchKernelGGL(k_publish, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, ps,
-                               p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
-                               p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int32_t>(),
-                               p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
-                               publish, pub_start_ticks());
+            if (sched16)
+                hipLaunchKernelGGL(k_publish<uint16_t>, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, ps,
+                                   p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
+                                   p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int32_t>(),
+                                   p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
+                                   reinterpret_cast<uint16_t*>(publish), pub_start_ticks());
+            else
+                hipLaunchKernelGGL(k_publish<int32_t>, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, ps,
+                                   p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
+                                   p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int32_t>(),
+                                   p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
+                                   publish, pub_start_ticks());
             CA_HIP_CHECK(hipGetLastError());
             return CA_OK;
         };
@@ -2326,13 +2363,12 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                st, p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
                                p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), nullptr);
             CA_HIP_CHECK(hipGetLastError());
-            if (to_host)
-                CA_HIP_CHECK(hipMemcpyAsync(sched_pod, p->d_sched_pod.ptr, sizeof(int32_t) * std::max(p->total, 0),
-                                            hipMemcpyDeviceToHost, st));
+            int rc;
+            if (to_host && (rc = results_to_host(p, st, sched_pod, sched16)) != CA_OK) return rc;
         }
     } else if (to_host) {
-        CA_HIP_CHECK(hipMemcpyAsync(sched_pod, p->d_sched_pod.ptr, sizeof(int32_t) * std::max(p->total, 0),
-                                    hipMemcpyDeviceToHost, st));
+        int rc;
+        if ((rc = results_to_host(p, st, sched_pod, sched16)) != CA_OK) return rc;
     }
     if (sched_node)
         CA_HIP_CHECK(hipMemcpyAsync(sched_node, p->d_sched_node.ptr, sizeof(int32_t) * std::max(p->total, 0),
@@ -2439,6 +2475,12 @@ int ca_estimate_plan_run(ca_estimate_plan* p, const ca_limiter* limiter, int32_t
                          ca_estimate_result* results, int32_t* sched_pod, int32_t* sched_node) {
     if (!p) return CA_EINVAL;
     return plan_run(p, limiter, last_index, results, sched_pod, sched_node);
+}
+
+int ca_estimate_plan_run_u16(ca_estimate_plan* p, const ca_limiter* limiter, int32_t* last_index,
+                             ca_estimate_result* results, uint16_t* sched_pod16) {
+    if (!p || !sched_pod16) return CA_EINVAL;
+    return plan_run(p, limiter, last_index, results, nullptr, nullptr, sched_pod16);
 }
 
 int ca_estimate_plan_destroy(ca_estimate_plan* p) {

@@ -72,6 +72,7 @@ def load() -> C.CDLL:
         "ca_estimate_batch": ([vp, vp, vp, vp, vp, i32, vp, p(i32), vp, vp, vp], C.c_int),
         "ca_estimate_plan_create": ([vp, vp, vp, vp, vp, i32, p(vp)], C.c_int),
         "ca_estimate_plan_run": ([vp, vp, p(i32), vp, vp, vp], C.c_int),
+        "ca_estimate_plan_run_u16": ([vp, vp, p(i32), vp, vp], C.c_int),
         "ca_estimate_plan_destroy": ([vp], C.c_int),
         "ca_estimate_plan_fetch": ([vp, vp], C.c_int),
         "ca_estimate_plan_device_results": ([vp, p(vp)], C.c_int),
@@ -113,6 +114,8 @@ def load() -> C.CDLL:
         "ca_plan_stats": ([vp, p(i32), p(i32), p(i32), p(C.c_float)], C.c_int),
     }
     for name, (args, res) in sigs.items():
+        if path != LIB_PATH and not hasattr(lib, name):
+            continue                      # an older diagnostics build (A/B runs)
         f = getattr(lib, name)
         f.argtypes = args
         f.restype = res
@@ -142,6 +145,7 @@ def exported_symbols() -> list[str]:
         "ca_mirror_fork", "ca_mirror_revert", "ca_mirror_commit", "ca_mirror_node_count", "ca_mirror_pod_node",
         "ca_mirror_node_pods", "ca_podset_create", "ca_podset_destroy", "ca_fits_any_node", "ca_check_predicates",
         "ca_fits_matrix", "ca_check_templates", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
+        "ca_estimate_plan_run_u16",
         "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_estimate_plan_timings",
         "ca_estimate_plan_group_ticks", "ca_estimate_plan_fetch", "ca_estimate_plan_device_results",
         "ca_find_nodes_to_remove",
@@ -632,6 +636,20 @@ class EstimatePlan:
         self.sched_pod = self._pinned.array[:n]
         self.sched_node = self._pinned.array[n:]
         self.results = np.zeros(self.G, abi.ESTIMATE_RESULT_DTYPE)
+        self._pinned16 = None
+
+    def run_u16(self, max_nodes: int, last_index: int = 0, copy: bool = True) -> EstimateOutput:
+        """One Estimate batch with the scheduled pods as 16-bit podset indices
+        (ca_estimate_plan_run_u16: podsets of at most 65535 pods; 0xFFFF = not scheduled).
+        sched_node of the returned output is None."""
+        if self._pinned16 is None:
+            self._pinned16 = PinnedArray(self.lib, max(self.total, 1), np.uint16)
+        lim = abi.LimiterC(max_nodes, 0)
+        li = C.c_int32(last_index)
+        _check(self.lib.ca_estimate_plan_run_u16(self.h, C.byref(lim), C.byref(li), ptr(self.results),
+                                                 ptr(self._pinned16.array)), "ca_estimate_plan_run_u16")
+        f = _fast_copy if copy else (lambda a: a)
+        return EstimateOutput(f(self.results), f(self._pinned16.array[: self.total]), None, li.value)
 
     def run(self, max_nodes: int, last_index: int = 0, want_nodes: bool = True, copy: bool = True,
             device_results: bool = False) -> EstimateOutput:
@@ -693,6 +711,9 @@ class EstimatePlan:
             self.h = None
             self.sched_pod = self.sched_node = None
             self._pinned.close()
+            if self._pinned16 is not None:
+                self._pinned16.close()
+                self._pinned16 = None
 
     def __enter__(self):
         return self

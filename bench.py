@@ -542,15 +542,23 @@ def main():
     items = int(w.group_off[-1])                                # (pod, group) items of the whole batch
     items_blk = int(off_blk[-1])
 
-    def run_block(lin, device_results=False):
-        """This rank's block: results to the caller's page-locked buffer (headline), or left
-        in HBM (extra.device_resident)."""
+    # results on the host as 16-bit podset indices when the podset allows it (C2: 50k pods;
+    # ca_estimate_plan_run_u16, half the PCIe bytes), else 32-bit pod ids
+    host_mode = "u16" if (len(w.table) <= 65535 and not args.with_nodes) else "i32"
+
+    def run_block(lin, mode="host"):
+        """This rank's block: results to the caller's page-locked buffer (headline: `host_mode`;
+        "i32": 32-bit ids), or left in HBM ("device": extra.device_resident)."""
         if g1 == g0:
             return None, lin, 0, 0
+        if mode == "host":
+            mode = host_mode
         if args.with_nodes:
             out = plan.run(w.max_nodes, lin, want_nodes=True, copy=False)
-        elif device_results:
+        elif mode == "device":
             out = plan.run(w.max_nodes, lin, copy=False, device_results=True)
+        elif mode == "u16":
+            out = plan.run_u16(w.max_nodes, lin, copy=False)
         else:
             out = plan.run(w.max_nodes, lin, want_nodes=False, copy=False)
         sens, succ = plan.chain_info()
@@ -559,24 +567,24 @@ def main():
     coll_dev = f"cuda:{local}" if backend == "nccl" else "cpu"
     gather = shard.torch_all_gather(dist, coll_dev) if dist is not None else None
 
-    def step(device_results=False):
+    def step(mode="host"):
         """One Estimate batch: this rank's block + the lastIndex chain across ranks."""
-        run = (lambda lin: run_block(lin, device_results))
+        run = (lambda lin: run_block(lin, mode))
         if dist is None:
             return run(L0)[0], 0
         out, _, extra = shard.run_sharded(run, L0, gather, rank)
         return out, extra
 
-    def timed(device_results):
+    def timed(mode):
         for _ in range(args.warmup):
-            step(device_results)
+            step(mode)
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         evals, extras, out = 0, [], None
         for _ in range(args.steps):
-            out, extra = step(device_results)
+            out, extra = step(mode)
             evals += int(out.results["evals"].sum()) if out is not None else 0
             extras.append(extra)
         torch.cuda.synchronize()
@@ -592,12 +600,14 @@ def main():
         return el, evals, evals, extras, out
 
     # headline: results on the host (Estimate latency = results on the host)
-    elapsed, total_evals, evals, extras, hout = timed(False)
+    elapsed, total_evals, evals, extras, hout = timed("host")
     host_pods = hout.sched_pod.copy() if hout is not None else None
+    if host_pods is not None and host_pods.dtype == np.uint16:
+        host_pods = np.where(host_pods == 0xFFFF, -1, host_pods.astype(np.int32))
     # per-phase device times: the same steps again, untimed
     chain_ms, sort_ms, rounds, phases, pub = [], [], [], [], []
     for i in range(args.steps):
-        step(False)
+        step("host")
         st = plan.stats()
         chain_ms.append(st["chain_ms"] / max(st["rounds"], 1))
         sort_ms.append(st["sort_ms"])
@@ -607,8 +617,16 @@ def main():
         phases.append(ph)
         pub.append(st["results_path"])
     # device-resident variant (results left in HBM): the previous round's headline
-    d_el, d_total, _, _, _ = timed(True)
+    d_el, d_total, _, _, _ = timed("device")
     same = bool(host_pods is None or np.array_equal(host_pods, plan.fetch()))
+    # 32-bit pod ids on the host (the previous round's headline), when the headline is u16
+    host_i32 = None
+    if host_mode == "u16":
+        i_el, i_total, _, _, iout = timed("i32")
+        host_i32 = {"ms_per_step": i_el / args.steps * 1e3, "evals_per_s": i_total / i_el,
+                    "results_identical_to_headline": bool(iout is None or np.array_equal(host_pods, iout.sched_pod)),
+                    "results": "scheduled pods as 32-bit pod ids in the caller's page-locked buffer "
+                               "(ca_estimate_plan_run, zero-copy publisher)"}
     device_resident = {"ms_per_step": d_el / args.steps * 1e3, "evals_per_s": d_total / d_el,
                        "results_identical_to_host_mode": same,
                        "results": "scheduled pods left in HBM (ca_estimate_plan_run with sched_pod = NULL); "
@@ -685,10 +703,13 @@ def main():
             "extra": {
                 "estimate_latency_ms": ms,
                 "results_to_host": "zero-copy publisher kernel on a second stream writes each final chunk of 4096 "
-                                   "scheduled pods into the caller's page-locked buffer while the chains run "
-                                   f"({4 * items} B per step); results path per step: "
+                                   "scheduled pods into the caller's page-locked buffer while the chains run, as "
+                                   + ("16-bit podset indices (ca_estimate_plan_run_u16, "
+                                      if host_mode == "u16" else "32-bit pod ids (ca_estimate_plan_run, ")
+                                   + f"{(2 if host_mode == 'u16' else 4) * items} B per step); results path per step: "
                                    f"{sorted(set(pub)) if pub else None}",
                 "device_resident": device_resident,
+                "host_int32_ids": host_i32,
                 "sort_ms": float(np.mean(sort_ms)) if sort_ms else None,
                 "phases_ms": ph_mean,
                 "chain_kernel_ms": ph_mean.get("chain_ms"),

@@ -384,6 +384,12 @@ int ca_estimate_plan_run(ca_estimate_plan* p, const ca_limiter* limiter, int32_t
  * stay in the plan (same layout as sched_pod) until the next run.  Fetch them with
  * ca_estimate_plan_fetch (one D2H), or hand the device pointer to a device consumer. */
 int ca_estimate_plan_fetch(const ca_estimate_plan* p, int32_t* sched_pod);
+/* ca_estimate_plan_run with the scheduled pods as 16-bit podset indices (the podset holds
+ * at most 65535 pods, else CA_EINVAL; 0xFFFF = not scheduled), same layout as sched_pod:
+ * half the bytes across PCIe.  Page-locked sched_pod16 (ca_host_alloc) is written by the
+ * zero-copy publisher while the chains run; other memory gets a stream-ordered copy. */
+int ca_estimate_plan_run_u16(ca_estimate_plan* p, const ca_limiter* limiter, int32_t* last_index,
+                             ca_estimate_result* results, uint16_t* sched_pod16);
 int ca_estimate_plan_device_results(const ca_estimate_plan* p, const int32_t** sched_pod_dev);
 int ca_estimate_plan_destroy(ca_estimate_plan* p);
 /* statistics of the last run: speculation rounds, kernel time of the chain kernel (ms) */

@@ -130,6 +130,24 @@ int main(void) {
            (unsigned long long)er.evals);
     EXPECT(er.status == CA_OK && er.node_count == 125 && er.n_scheduled == 1000);
 
+    /* the prepared plan, scheduled pods as 16-bit podset indices into page-locked memory */
+    {
+        ca_estimate_plan* plan = NULL;
+        CHECK(ca_estimate_plan_create(m, ps, goff, pidx, &tmpl, 1, &plan));
+        void* buf16 = NULL;
+        CHECK(ca_host_alloc(sizeof(uint16_t) * 1000, &buf16));
+        uint16_t* s16 = (uint16_t*)buf16;
+        ca_estimate_result ep;
+        int32_t lp = 0;
+        CHECK(ca_estimate_plan_run_u16(plan, &lim, &lp, &ep, s16));
+        int same = ep.node_count == er.node_count && ep.n_scheduled == er.n_scheduled && lp == li;
+        for (int i = 0; i < 1000; i++) same &= (int32_t)s16[i] == sched[i];
+        printf("plan u16 node_count %d same %d\n", ep.node_count, same);
+        EXPECT(same);
+        CHECK(ca_host_free(buf16));
+        CHECK(ca_estimate_plan_destroy(plan));
+    }
+
     /* kernel scope: a group with an out-of-scope pod stops the batch (prefix protocol) */
     pods[999].flags |= CA_POD_OUT_OF_SCOPE;
     ca_podset* ps2 = NULL;

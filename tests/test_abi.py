@@ -13,7 +13,7 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 
 def declared_functions():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ca_[a-z_]+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ca_[a-z0-9_]+)\s*\(", src, re.M)))
 
 
 def test_library_built_and_loads():

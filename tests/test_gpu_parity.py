@@ -353,6 +353,10 @@ def test_estimate_full_c2_parity(oracle):
             assert np.array_equal(o.results, d.results)
             assert o.last_index == d.last_index
             assert np.array_equal(o.sched_pod, plan.fetch())
+            h = plan.run_u16(w.max_nodes, 0)                           # 16-bit ids (bench headline)
+            assert np.array_equal(o.results, h.results)
+            assert o.last_index == h.last_index
+            assert np.array_equal(o.sched_pod, np.where(h.sched_pod == 0xFFFF, -1, h.sched_pod.astype(np.int32)))
 
 
 @pytest.mark.parametrize("seed", range(8))
@@ -378,8 +382,11 @@ def test_estimate_plan_publish_random(seed, chunk, oracle, monkeypatch):
         g = plan.run(max_nodes, L0, want_nodes=False)
         d = plan.run(max_nodes, L0, device_results=True)
         dp = plan.fetch()
+        h = plan.run_u16(max_nodes, L0)
+        hp = np.where(h.sched_pod == 0xFFFF, -1, h.sched_pod.astype(np.int32))
     assert np.array_equal(ro.results, g.results)
     assert np.array_equal(ro.results, d.results)
+    assert np.array_equal(ro.results, h.results)
     for k in range(len(groups)):
         if int(ro.results[k]["status"]) != 0:
             continue
@@ -389,7 +396,9 @@ def test_estimate_plan_publish_random(seed, chunk, oracle, monkeypatch):
         assert (g.sched_pod[a + n:b] == -1).all()
         assert np.array_equal(ro.sched_pod[a:a + n], dp[a:a + n]), (seed, k)
         assert (dp[a + n:b] == -1).all()
-    assert ro.last_index == g.last_index == d.last_index
+        assert np.array_equal(ro.sched_pod[a:a + n], hp[a:a + n]), (seed, k)
+        assert (hp[a + n:b] == -1).all()
+    assert ro.last_index == g.last_index == d.last_index == h.last_index
 
 
 @pytest.mark.parametrize("serial", [False, True], ids=["concurrent", "serialised"])
@@ -416,6 +425,10 @@ def test_estimate_publisher_bounded(serial, oracle, monkeypatch):
             assert np.array_equal(ro.results, p.results)
             assert np.array_equal(ro.sched_pod, p.sched_pod)
             assert ro.last_index == p.last_index
+            assert plan.stats()["results_path"] == ("publisher_gave_up" if serial else "published")
+            h = plan.run_u16(w.max_nodes, 0)
+            assert np.array_equal(ro.results, h.results)
+            assert np.array_equal(ro.sched_pod, np.where(h.sched_pod == 0xFFFF, -1, h.sched_pod.astype(np.int32)))
             assert plan.stats()["results_path"] == ("publisher_gave_up" if serial else "published")
     assert min(walls) < 0.05, walls          # 2 ms start deadline + the copy, never 200 ms
 

@@ -208,6 +208,7 @@ int ensure_dyn_lds(const void* kernel, size_t bytes);
 struct DevBuf {
     void* ptr = nullptr;
     size_t bytes = 0;
+    int dev = -1;               // device of ptr (the allocation cache is per device)
     int reserve(size_t need);   // grows (content not preserved)
     int reserve_keep(size_t need, hipStream_t st);  // grows, preserving content
     void release();

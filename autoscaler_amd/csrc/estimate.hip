@@ -562,7 +562,10 @@ template <bool GM> __device__ inline void cbar() {
         lds_barrier();
     }
 }
-constexpr int CW = 4;
+#ifndef CASIM_CW
+#define CASIM_CW 4
+#endif
+constexpr int CW = CASIM_CW;
 constexpr int CT = 64 * CW;
 constexpr int RED_N = 5;
 struct ChainRed {

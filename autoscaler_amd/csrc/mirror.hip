@@ -9,6 +9,7 @@
 #include "device_filters.h"
 
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <unordered_map>
 #include <algorithm>
@@ -34,13 +35,79 @@ int ensure_dyn_lds(const void* kernel, size_t bytes) {
 
 // Both buffers grow geometrically: a hipMalloc / hipHostMalloc (and the free before it)
 // costs up to milliseconds, and callers like the planner's rounds grow them step by step.
+//
+// Released blocks go to a per-process cache instead of hipFree / hipHostFree: a caller
+// that builds and destroys its objects every loop (a podset of this loop's pending pods,
+// an Estimate batch's plan: ~20 device and page-locked buffers) then pays no allocation
+// after the first loop.  hipFree synchronises the device; a cached block is handed out
+// again only after the same synchronisation, so no queued kernel or copy still uses it.
+// The cache keeps at most 4 GiB per device and 1 GiB of page-locked memory, takes the
+// smallest cached block of at least the request and at most twice it, and is never
+// returned to the runtime (process exit reclaims it).
+namespace {
+struct BlockCache {
+    std::mutex mu;
+    std::multimap<size_t, std::pair<int, void*>> free;   // size -> (device or -1, block)
+    size_t cached = 0;
+    size_t cap = 0;
+    void* take(size_t need, int dev, size_t& got) {
+        std::lock_guard<std::mutex> lock(mu);
+        for (auto it = free.lower_bound(need); it != free.end() && it->first <= 2 * need; ++it) {
+            if (it->second.first != dev) continue;
+            void* p = it->second.second;
+            got = it->first;
+            cached -= got;
+            free.erase(it);
+            return p;
+        }
+        return nullptr;
+    }
+    bool give(size_t bytes, int dev, void* p) {
+        std::lock_guard<std::mutex> lock(mu);
+        if (cached + bytes > cap) return false;
+        free.emplace(bytes, std::make_pair(dev, p));
+        cached += bytes;
+        return true;
+    }
+};
+BlockCache& dev_cache() {
+    static BlockCache* c = [] { auto* b = new BlockCache(); b->cap = 4ull << 30; return b; }();   // leaked on purpose
+    return *c;
+}
+BlockCache& host_cache() {
+    static BlockCache* c = [] { auto* b = new BlockCache(); b->cap = 1ull << 30; return b; }();
+    return *c;
+}
+bool no_cache() {
+    static const bool off = getenv("CASIM_NO_ALLOC_CACHE") != nullptr;
+    return off;
+}
+// the synchronisation hipFree would have done, on the block's device
+void sync_device(int dev) {
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (dev >= 0 && cur != dev) (void)hipSetDevice(dev);
+    (void)hipDeviceSynchronize();
+    if (dev >= 0 && cur != dev) (void)hipSetDevice(cur);
+}
+}  // namespace
+
 int DevBuf::reserve(size_t need) {
     if (need <= bytes) return CA_OK;
     const size_t grown = bytes + bytes / 2;
     release();
     size_t sz = std::max<size_t>(need, std::max<size_t>(grown, 4096));
+    int d = 0;
+    CA_HIP_CHECK(hipGetDevice(&d));
+    size_t got = 0;
+    if (!no_cache() && (ptr = dev_cache().take(sz, d, got)) != nullptr) {
+        bytes = got;
+        dev = d;
+        return CA_OK;
+    }
     if (hipMalloc(&ptr, sz) != hipSuccess) { ptr = nullptr; bytes = 0; set_last_error("hipMalloc failed"); return CA_EDEVICE; }
     bytes = sz;
+    dev = d;
     return CA_OK;
 }
 
@@ -52,15 +119,25 @@ int DevBuf::reserve_keep(size_t need, hipStream_t st) {
     if (ptr && bytes) {
         if (hipMemcpyAsync(p, ptr, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess) return CA_EDEVICE;
         if (hipStreamSynchronize(st) != hipSuccess) return CA_EDEVICE;
-        (void)hipFree(ptr);
+        release();
     }
+    int d = 0;
+    CA_HIP_CHECK(hipGetDevice(&d));
     ptr = p;
     bytes = sz;
+    dev = d;
     return CA_OK;
 }
 
 void DevBuf::release() {
-    if (ptr) (void)hipFree(ptr);
+    if (ptr) {
+        bool kept = false;
+        if (!no_cache()) {
+            sync_device(dev);
+            kept = dev_cache().give(bytes, dev, ptr);
+        }
+        if (!kept) (void)hipFree(ptr);
+    }
     ptr = nullptr;
     bytes = 0;
 }
@@ -70,6 +147,11 @@ int HostBuf::reserve(size_t need) {
     const size_t grown = bytes + bytes / 2;
     release();
     size_t sz = std::max<size_t>(need, std::max<size_t>(grown, 4096));
+    size_t got = 0;
+    if (!no_cache() && (ptr = host_cache().take(sz, -1, got)) != nullptr) {
+        bytes = got;
+        return CA_OK;
+    }
     if (hipHostMalloc(&ptr, sz, hipHostMallocNonCoherent) != hipSuccess) {
         ptr = nullptr; bytes = 0; set_last_error("hipHostMalloc failed"); return CA_EDEVICE;
     }
@@ -78,7 +160,14 @@ int HostBuf::reserve(size_t need) {
 }
 
 void HostBuf::release() {
-    if (ptr) (void)hipHostFree(ptr);
+    if (ptr) {
+        bool kept = false;
+        if (!no_cache()) {
+            sync_device(-1);
+            kept = host_cache().give(bytes, -1, ptr);
+        }
+        if (!kept) (void)hipHostFree(ptr);
+    }
     ptr = nullptr;
     bytes = 0;
 }
@@ -542,18 +631,41 @@ int ca_device_count(int32_t* out) {
     return CA_OK;
 }
 
+// Page-locked blocks handed to callers come from the same cache as the library's own
+// (HostBuf): a caller that allocates its result buffers per call pays no hipHostMalloc
+// after the first.  The block sizes are remembered for ca_host_free.
+static std::mutex g_host_mu;
+static std::unordered_map<void*, size_t>* g_host_sizes = new std::unordered_map<void*, size_t>();   // leaked on purpose
+
 int ca_host_alloc(size_t bytes, void** out) {
     if (!out) return CA_EINVAL;
     *out = nullptr;
-    hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocNonCoherent);
-    if (e != hipSuccess) { set_last_error(hipGetErrorString(e)); return CA_EDEVICE; }
+    HostBuf b;
+    if (b.reserve(bytes ? bytes : 1) != CA_OK) return CA_EDEVICE;
+    {
+        std::lock_guard<std::mutex> lock(g_host_mu);
+        (*g_host_sizes)[b.ptr] = b.bytes;
+    }
+    *out = b.ptr;
+    b.ptr = nullptr;                    // owned by the caller now
+    b.bytes = 0;
     return CA_OK;
 }
 
 int ca_host_free(void* p) {
     if (!p) return CA_OK;
-    hipError_t e = hipHostFree(p);
-    if (e != hipSuccess) { set_last_error(hipGetErrorString(e)); return CA_EDEVICE; }
+    size_t sz = 0;
+    {
+        std::lock_guard<std::mutex> lock(g_host_mu);
+        auto it = g_host_sizes->find(p);
+        if (it == g_host_sizes->end()) { set_last_error("ca_host_free: not a ca_host_alloc block"); return CA_EINVAL; }
+        sz = it->second;
+        g_host_sizes->erase(it);
+    }
+    HostBuf b;                          // released through the cache
+    b.ptr = p;
+    b.bytes = sz;
+    b.release();
     return CA_OK;
 }
 

@@ -105,12 +105,17 @@ def _equivalence_groups(pods: np.ndarray, unsched: np.ndarray):
     return groups
 
 
-def _util_rows(w: RunOnceWorkload, placed_node: np.ndarray):
+def _zeros(key: str, n: int, dtype) -> np.ndarray:
+    return np.zeros(n, dtype)
+
+
+def _util_rows(w: RunOnceWorkload, placed_node: np.ndarray, zeros=_zeros):
     """ca_util_node / ca_util_pod rows of the snapshot after FilterOutSchedulable: each
-    node's running pods, then the pods placed on it (NodeInfo.Pods order)."""
+    node's running pods, then the pods placed on it (NodeInfo.Pods order).  `zeros(key, n,
+    dtype)` allocates the row arrays (a caller that uploads them passes page-locked ones)."""
     f = w.filt
     n = len(f.nodes)
-    nodes = np.zeros(n, abi.UTIL_NODE_DTYPE)
+    nodes = zeros("nodes", n, abi.UTIL_NODE_DTYPE)
     nodes["alloc_milli"][:, 0] = f.nodes["alloc_milli_cpu"]
     nodes["alloc_milli"][:, 1] = f.nodes["alloc_memory"] * 1000
     nodes["flags"] = abi.CA_UNODE_HAS_CPU | abi.CA_UNODE_HAS_MEM
@@ -122,19 +127,20 @@ def _util_rows(w: RunOnceWorkload, placed_node: np.ndarray):
     cpu = np.concatenate([run_pods["req_milli_cpu"], pend["req_milli_cpu"][pend_ids]])
     mem = np.concatenate([run_pods["req_memory"], pend["req_memory"][pend_ids]])
     order = np.argsort(all_node, kind="stable")                   # node by node, running pods first
-    pods = np.zeros(len(order), abi.UTIL_POD_DTYPE)
+    pods = zeros("pods", len(order), abi.UTIL_POD_DTYPE)
     pods["req_milli"][:, 0] = cpu[order]                     # MilliValue of millicores
     pods["req_milli"][:, 1] = mem[order] * 1000
     pods["flags"] = abi.CA_UPOD_MOVABLE
-    off = np.zeros(n + 1, np.int32)
+    off = zeros("pod_off", n + 1, np.int32)
     np.cumsum(np.bincount(all_node, minlength=n), out=off[1:])
     # mirror pod id of every util row (running pods: 0..P-1; placed pods: their new ids)
     return nodes, off, pods, order
 
 
-def run(backend, util_fn, w: RunOnceWorkload, timers=None) -> RunOnceResult:
+def run(backend, util_fn, w: RunOnceWorkload, timers=None, row_zeros=_zeros) -> RunOnceResult:
     """One loop on `backend` (native.Mirror or pyoracle.OracleState, freshly loaded with
-    W.load_filter) with `util_fn(nodes, off, pods, now_ns) -> UTIL_INFO rows`."""
+    W.load_filter) with `util_fn(nodes, off, pods, now_ns) -> UTIL_INFO rows`; `row_zeros`
+    allocates the utilization rows (native.PinnedRows.zeros for the device)."""
     f = w.filt
     r = RunOnceResult()
     clock = time.perf_counter
@@ -175,7 +181,7 @@ def run(backend, util_fn, w: RunOnceWorkload, timers=None) -> RunOnceResult:
         ps.close()
 
     # 4. scale-down eligibility on the snapshot after step 1
-    unodes, uoff, upods, _ = _util_rows(w, fo.node)
+    unodes, uoff, upods, _ = _util_rows(w, fo.node, row_zeros)
     t = clock()
     r.util = util_fn(unodes, uoff, upods, w.now_ns)
     r.ms["utilization"] = (clock() - t) * 1e3

@@ -409,10 +409,14 @@ def runonce_leg(args, device: int, with_cpu: bool) -> dict:
             ut[0].update(n, off, p)
         return ut[0].calculate(False, False, now)
     runs = []
+    rows = native.PinnedRows()                                    # utilization rows built in page-locked memory
     for _ in range(1 + max(2, min(args.steps, 4))):
         m.fork()
-        runs.append(runonce.run(m, util, w))
+        runs.append(runonce.run(m, util, w, row_zeros=rows.zeros))
         m.revert()
+    if ut:
+        ut[0].close()
+    rows.close()
     m.close()
     ut[0].close()
     keys = list(runs[-1].ms)

@@ -937,7 +937,8 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
     }
 }
 
-// One wavefront per node group.  LDS: NodeRec rows[kcap], block summaries[kcap/64]
+// One workgroup of CW (4) waves per node group (see ChainRed above: the waves share the
+// row loops, the control flow is uniform).  LDS: NodeRec rows[kcap], block summaries[kcap/64]
 // (per-dimension maxima over a 64-row block, allowed to be stale-high), the per-run
 // scratch CAPA/ALIVE[kcap], and the optional port / scalar columns.
 //

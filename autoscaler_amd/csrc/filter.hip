@@ -9,7 +9,7 @@
 //
 // The reference is one sequential loop: a pod's scan starts where the previous successful
 // scan stopped (lastIndex) and sees every earlier placement, so the pods are walked in
-// order.  One workgroup (16 waves) owns the node rows for the whole call:
+// order.  One workgroup (SQ_W = 8 waves of SQ_T = 512 threads) owns the node rows for the whole call:
 //   window     the SQ_WIN node rows from lastIndex on (hot, ext and static columns) live
 //              in LDS, updated there by the placements and written back when the window
 //              moves.  Consecutive scans continue where the previous one stopped, so the
@@ -21,7 +21,7 @@
 //              64 positions per step (ballot of visible / fits: first fit wins, the
 //              evaluations are the visible positions up to it);
 //   block step when a scan runs off the window (or the slots are used up, or a class
-//              must be marked) all 16 waves take over: write back, scan the rest of the
+//              must be marked) all 8 waves take over: write back, scan the rest of the
 //              ring in parallel (SQ_RING positions in flight per thread, first fit by a
 //              min reduction), place or mark, reload the window at lastIndex and the slots.
 // Every pod's outcome, lastIndex and the evaluation count are exactly the reference loop's.

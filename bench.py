@@ -138,7 +138,7 @@ def expansion_leg(args, device: int, with_cpu: bool) -> dict:
     each pod group's sample on a fresh copy of each template (ca_check_templates).
     'groups' = the distinct pod records (equivalence groups), 'all' = every pod its own
     group (no controller: the worst case)."""
-    from autoscaler_amd import native
+    from autoscaler_amd import abi, native
     from autoscaler_amd import workloads as W
     w = W.c4(n_pods=args.pods, n_groups=args.groups, n_existing=args.existing, max_nodes=args.max_nodes)
     pods = w.table.pods
@@ -152,11 +152,13 @@ def expansion_leg(args, device: int, with_cpu: bool) -> dict:
         # the full results (failing plugin and reasons per pair: eg.SchedulingErrors)
         pin = native.PinnedArray(m.lib, len(samples) * len(w.templates), np.uint8)
         ok = pin.array.reshape(len(w.templates), len(samples))
+        pin_full = native.PinnedArray(m.lib, len(samples) * len(w.templates), abi.PRED_RESULT_DTYPE)
+        full = pin_full.array.reshape(len(w.templates), len(samples))
         rec = {"pod_groups": int(len(samples)), "pairs": int(len(samples) * len(w.templates))}
         for mode in ("verdicts", "with_reasons"):
             call = (lambda: m.check_templates(w.table, samples, w.templates, podset=podset, verdict_only=True,
                                               out=ok)) if mode == "verdicts" else \
-                   (lambda: m.check_templates(w.table, samples, w.templates, podset=podset))
+                   (lambda: m.check_templates(w.table, samples, w.templates, podset=podset, out=full))
             call()                                                         # warm-up
             ts = []
             for _ in range(max(args.steps, 5)):
@@ -168,7 +170,9 @@ def expansion_leg(args, device: int, with_cpu: bool) -> dict:
             rec[f"{mode}_pairs_per_s"] = len(samples) * len(w.templates) / (ms / 1e3)
         rec["feasible_pairs"] = int((res["type"] == 0).sum())
         rec["verdicts_match_results"] = bool(np.array_equal(ok.astype(bool), res["type"] == 0))
+        res = res.copy()
         pin.close()
+        pin_full.close()
         ms = rec["verdicts_ms"]
         if with_cpu:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -183,8 +187,8 @@ def expansion_leg(args, device: int, with_cpu: bool) -> dict:
                         "parity": bool(np.array_equal(ro, res))})
         out[name] = rec
     podset.close()
-    out["includes"] = ("host->device template rows, the matrix kernel, device->host results (1 B per pair into "
-                       "page-locked memory; 16 B per pair with reasons into pageable memory)")
+    out["includes"] = ("host->device template rows, the matrix kernel, device->host results (1 B per pair, or 16 B "
+                       "per pair with reasons, into page-locked memory)")
     if with_cpu:
         out["cpu_baseline"] = {"kind": "port", "cores": 1,
                                "sample": f"oracle/casim_oracle.c or_check_templates (fork, template copy, "

@@ -822,15 +822,32 @@ __device__ inline int32_t run_end_pf(const uint64_t* __restrict__ hm, int32_t po
 // carries the group's progress (segments written, pods scheduled) at its push.
 // Release at agent scope: the L2s of the 8 XCDs are not coherent, the publisher may run
 // on another XCD.  Called by one whole wavefront (the one that stores the results).
+//
+// A ticket is 64-bit: the chunk (g * nsub + c) in the low word and, for a **pure** chunk —
+// every output of it comes from run segments with one stream offset `off` (output i is
+// stream position i + off) — off + 1 in the high word.  The publisher copies a pure chunk
+// from the stream's pod ids (written before the chains started) and reads nothing the
+// chain wrote, so its push needs no release: an agent-scope release writes the XCD's L2
+// back (gfx950: its L2 is not coherent with the other XCDs'), microseconds per push on the
+// chain's critical path.  Other chunks (single placements, a segment boundary with another
+// offset, the group's tail) go with the release and the progress record.
 constexpr int PCH = 4096;      // default chunk (CASIM_PUB_CHUNK overrides, for tests)
-__device__ inline void push_chunks(int32_t g, int32_t c0, int32_t c1, int32_t nsub, int32_t* tickets, int32_t* qctl,
-                                   int2* prog, int32_t nseg, int32_t nsched, int lane) {
-    __threadfence();
-    if (lane == 0 && c1 > c0) {
-        for (int32_t c = c0; c < c1; c++) prog[g * nsub + c] = make_int2(nseg, nsched);
+__device__ inline void push_chunks(int32_t g, int32_t c0, int32_t c1, int32_t nsub, int64_t* tickets, int32_t* qctl,
+                                   int2* prog, int32_t nseg, int32_t nsched, int lane, int32_t pch = 0,
+                                   int32_t pure_from = INT32_MAX, int32_t pure_off = 0) {
+    if (c1 <= c0) return;
+    const bool pure = pch > 0 && (int64_t)c0 * pch >= pure_from;
+    if (!pure) __threadfence();
+    if (lane == 0) {
+        if (!pure)
+            for (int32_t c = c0; c < c1; c++) prog[g * nsub + c] = make_int2(nseg, nsched);
         const int32_t base = atomicAdd(&qctl[1], c1 - c0);
-        for (int32_t i = 0; i < c1 - c0; i++)
-            __hip_atomic_store(&tickets[base + i], g * nsub + c0 + i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const int64_t hi = pure ? ((int64_t)pure_off + 1) << 32 : 0;
+        for (int32_t i = 0; i < c1 - c0; i++) {
+            const int64_t v = hi | (int64_t)(uint32_t)(g * nsub + c0 + i);
+            if (pure) __hip_atomic_store(&tickets[base + i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else __hip_atomic_store(&tickets[base + i], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -863,16 +880,17 @@ __device__ inline Seg ld_seg(const Seg* p) {
 template <typename T>
 __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ groups, const ChainOut* __restrict__ outs,
                                                 const Seg* __restrict__ segs, const int32_t* __restrict__ spod,
-                                                const int32_t* sched_dev, int32_t* __restrict__ tickets,
+                                                const int32_t* sched_dev, int64_t* __restrict__ tickets,
                                                 int32_t* __restrict__ qctl, int32_t total, int32_t nsub,
                                                 const int2* __restrict__ prog, int32_t pch,
                                                 T* pub,              // pub may alias sched_dev (device results)
                                                 uint64_t start_ticks) {
-    __shared__ int32_t s_t, s_tk, s_seg0;
+    __shared__ int32_t s_t, s_seg0;
+    __shared__ int64_t s_tk;
     for (;;) {
         if (threadIdx.x == 0) {
             s_t = atomicAdd(&qctl[0], 1);
-            int32_t tk = -1;
+            int64_t tk = -1;
             if (s_t < total) {
                 const uint64_t t0 = wall_clock64();
                 bool started = false;
@@ -892,13 +910,22 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
             s_tk = tk;
         }
         lds_barrier();
-        const int32_t t = s_t, tk = s_tk;
-        if (t >= total || tk < 0) return;
+        const int32_t t = s_t;
+        const int64_t tk64 = s_tk;
+        if (t >= total || tk64 < 0) return;
         __threadfence();                                   // acquire for every thread of the block
+        const int32_t tk = (int32_t)(uint32_t)(tk64 & 0xFFFFFFFFll);
+        const int32_t pure_off = (int32_t)(tk64 >> 32) - 1;   // >= 0: a pure chunk (push_chunks)
         const int32_t g = tk / nsub, sub = tk - g * nsub;
         const GroupMeta gm = groups[g];
         const Seg* gs = segs + gm.off;
         const int32_t a = sub * pch, b = min(gm.count, a + pch);
+        if (pure_off >= 0) {
+            for (int32_t i = a + (int32_t)threadIdx.x; i < b; i += blockDim.x)
+                pub[gm.off + i] = (T)spod[gm.off + pure_off + i];
+            lds_barrier();
+            continue;
+        }
         const int32_t* pr = reinterpret_cast<const int32_t*>(prog + tk);   // the group's progress at the push
         const int32_t nseg = ld_coh(pr);
         const int32_t ns = ld_coh(pr + 1);
@@ -958,7 +985,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     const int32_t* __restrict__ lin_arr, const uint8_t* __restrict__ need, const uint32_t* __restrict__ group_unsup,
     int32_t n_base, int32_t max_nodes, int32_t kcap, int32_t use_ports, int32_t use_scalar, int32_t batch_runs,
     int32_t* __restrict__ sched_pod, int32_t* __restrict__ sched_node, Seg* __restrict__ segs,
-    int32_t* __restrict__ tickets, int32_t* __restrict__ qctl, int32_t nsub, int2* __restrict__ prog, int32_t pch,
+    int64_t* __restrict__ tickets, int32_t* __restrict__ qctl, int32_t nsub, int2* __restrict__ prog, int32_t pch,
     ChainOut* __restrict__ outs, const int32_t* __restrict__ gmap, unsigned char* __restrict__ gslab,
     const int64_t* __restrict__ slab_off, const int32_t* __restrict__ gkcap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -1065,6 +1092,13 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     // publish the chunks whose outputs are all scheduled (wave 0 stores every result in
     // publishing mode: segments by thread 0, single placements by its lanes)
     int32_t tk_next = 0;
+    // outputs [pure_from, nsched) all come from run segments with stream offset pure_off
+    // (pure chunks: push_chunks); a single placement or a segment with another offset
+    // restarts the range
+    int32_t pure_from = 0, pure_off = 0;
+    auto note_segment = [&](int32_t dst, int32_t src) {
+        if (src - dst != pure_off || dst < pure_from) { pure_from = dst; pure_off = src - dst; }
+    };
     auto progress = [&]() {
         if (!tickets || !w0) return;
         const int32_t c1 = nsched / pch;
@@ -1073,7 +1107,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
             so_pod[out_idx] = cur.pod;
             pend = false;
         }
-        push_chunks(g, tk_next, c1, nsub, tickets, qctl, prog, nseg, nsched, lane);
+        push_chunks(g, tk_next, c1, nsub, tickets, qctl, prog, nseg, nsched, lane, pch, pure_from, pure_off);
         tk_next = c1;
     };
 
@@ -1419,6 +1453,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                     PROF_T(t_pb);
                     cbar<GROWS>();            // the run's row updates are visible to every wave
                     if (tid == 0 && placed > 0) gseg[nseg] = Seg{nsched, pos + done, placed, 0};
+                    if (placed > 0) note_segment(nsched, pos + done);
                     nseg += placed > 0 ? 1 : 0;
                     nsched += placed;
                     done += placed;
@@ -1501,6 +1536,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                     evals += open_evals(n_open, ct, placed2, k0, j00, kev, (sf & SF_CP_EVAL) != 0);
                     if (so_node) for (int32_t t = tid; t < placed2; t += CT) so_node[nsched + t] = k0 + t / ct;
                     if (tid == 0 && placed2 > 0) gseg[nseg] = Seg{nsched, pos + done, placed2, 0};
+                    if (placed2 > 0) note_segment(nsched, pos + done);
                     nseg += placed2 > 0 ? 1 : 0;
                     if (ct >= 2 && placed2 >= 2) {
                         if (!first_success) { first_success = true; sensitive = k0 + 1 >= 2; }
@@ -1655,6 +1691,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
             if (tid < CA_PORT_WORDS) PORTS[(size_t)found * CA_PORT_WORDS + tid] |= puse[tid];
         }
         nsched++;
+        pure_from = nsched;                   // a single placement: written by the chain itself
         progress();
         cbar<GROWS>();                        // the placement is visible to every wave
     }
@@ -1702,7 +1739,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
 // group yet, publisher tickets empty, queue counters zero.
 __global__ void __launch_bounds__(256) k_round_init(int32_t G, int32_t lin0, int32_t* __restrict__ lin,
                                                    uint8_t* __restrict__ need, uint32_t* __restrict__ unsup,
-                                                   int32_t* __restrict__ tickets, int32_t n_tickets,
+                                                   int64_t* __restrict__ tickets, int32_t n_tickets,
                                                    int32_t* __restrict__ qctl) {
     const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     const int32_t stride = (int32_t)(gridDim.x * blockDim.x);
@@ -1920,7 +1957,7 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     p->n_tickets = 0;
     for (int32_t g = 0; g < G; g++) p->n_tickets += (p->h_meta[g].count + pch - 1) / pch;
     p->nsub = std::max(1, (p->max_count + pch - 1) / pch);
-    if ((rc = p->d_tickets.reserve(sizeof(int32_t) * (size_t)std::max(p->n_tickets, 1))) != CA_OK) return rc;
+    if ((rc = p->d_tickets.reserve(sizeof(int64_t) * (size_t)std::max(p->n_tickets, 1))) != CA_OK) return rc;
     if ((int64_t)G * p->nsub < INT32_MAX &&
         (rc = p->d_prog.reserve(sizeof(int2) * (size_t)G * (size_t)p->nsub)) != CA_OK) return rc;
     if ((rc = p->d_qctl.reserve(sizeof(int32_t) * 5)) != CA_OK) return rc;
@@ -2066,7 +2103,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         const int32_t n = std::max(G, tickets1);
         hipLaunchKernelGGL(k_round_init, dim3(std::min((n + 255) / 256, 64)), dim3(256), 0, st, G, *last_index,
                            p->d_lin.as<int32_t>(), p->d_need.as<uint8_t>(), p->d_unsup.as<uint32_t>(),
-                           publish ? p->d_tickets.as<int32_t>() : nullptr, tickets1,
+                           publish ? p->d_tickets.as<int64_t>() : nullptr, tickets1,
                            publish ? p->d_qctl.as<int32_t>() : nullptr);
         CA_HIP_CHECK(hipGetLastError());
     }
@@ -2216,7 +2253,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             for (int32_t g = 0; g < G; g++) if (need[g]) round_tickets += (p->h_meta[g].count + p->pch - 1) / p->pch;
             if (rounds > 1) {
                 CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_pub, 0));   // previous publisher done
-                CA_HIP_CHECK(hipMemsetAsync(p->d_tickets.ptr, 0xFF, sizeof(int32_t) * (size_t)std::max(round_tickets, 1), st));
+                CA_HIP_CHECK(hipMemsetAsync(p->d_tickets.ptr, 0xFF, sizeof(int64_t) * (size_t)std::max(round_tickets, 1), st));
                 CA_HIP_CHECK(hipMemsetAsync(p->d_qctl.ptr, 0, sizeof(int32_t) * 3, st));   // [3] stays: sticky
                 CA_HIP_CHECK(hipMemsetAsync(p->d_qctl.as<int32_t>() + 4, 0, sizeof(int32_t), st));
             }
@@ -2228,13 +2265,13 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             if (sched16)
                 hipLaunchKernelGGL(k_publish<uint16_t>, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, ps,
                                    p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
-                                   p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int32_t>(),
+                                   p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int64_t>(),
                                    p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
                                    reinterpret_cast<uint16_t*>(publish), pub_start_ticks());
             else
                 hipLaunchKernelGGL(k_publish<int32_t>, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, ps,
                                    p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
-                                   p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int32_t>(),
+                                   p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int64_t>(),
                                    p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
                                    publish, pub_start_ticks());
             CA_HIP_CHECK(hipGetLastError());
@@ -2258,7 +2295,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                p->d_need.as<uint8_t>(), p->d_unsup.as<uint32_t>(), n_base, lim->max_nodes, kcap,
                                p->use_ports ? 1 : 0, p->use_scalar ? 1 : 0, batch_runs,
                                p->d_sched_pod.as<int32_t>(), sched_node ? p->d_sched_node.as<int32_t>() : nullptr,
-                               p->d_seg.as<Seg>(), publish ? p->d_tickets.as<int32_t>() : nullptr,
+                               p->d_seg.as<Seg>(), publish ? p->d_tickets.as<int64_t>() : nullptr,
                                p->d_qctl.as<int32_t>(), p->nsub, p->d_prog.as<int2>(), p->pch, p->d_out.as<ChainOut>(),
                                gm, grows ? p->d_slab.as<unsigned char>() : nullptr,
                                grows ? p->d_slab_off.as<int64_t>() : nullptr, grows ? p->d_gkcap.as<int32_t>() : nullptr);

@@ -189,15 +189,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CASIM_S
     const ca_selector_req* __restrict__ reqs, const int32_t* __restrict__ names, const int32_t* __restrict__ hints,
     const int32_t* __restrict__ lin_arr, const uint8_t* __restrict__ need, int32_t* __restrict__ out_dest,
     int32_t* __restrict__ hint_set, SweepOut* __restrict__ outs, int32_t* __restrict__ walk_lout, int32_t use_ext,
-    const BlockSum* __restrict__ bsum) {
+    const BlockSum* __restrict__ bsum, int32_t c_base, int32_t* __restrict__ chain) {
     __shared__ OverlaySmem ov;
     extern __shared__ __attribute__((aligned(16))) unsigned char ovx_raw[];
     OverlayExt& ox = *reinterpret_cast<OverlayExt*>(ovx_raw);
-    const int c = blockIdx.x;
-    if (!need[c]) return;
+    const int c = c_base + blockIdx.x;
+    // chain != null: one candidate per launch, its lastIndex the previous launch's output
+    // (launches in candidate order on one stream: the host walk's serial exact chain)
+    if (!chain && !need[c]) return;
     const uint64_t t_begin = wall_clock64();      // diagnostics: SweepOut.pad2 = device ticks (100 MHz)
     const int lane = threadIdx.x;
-    const int32_t lin = lin_arr[c];
+    const int32_t lin = chain ? *chain : lin_arr[c];
     SweepOut res;
     res.removable = 0; res.reason = CA_UNREMOVABLE_NONE; res.n_placed = 0; res.lin = lin; res.lout = lin;
     res.fa_success = 0; res.status = CA_OK; res.pad = 0; res.evals = 0; res.pad2 = 0;
@@ -615,6 +617,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CASIM_S
         res.pad2 = wall_clock64() - t_begin;
         outs[c] = res;
         walk_lout[c] = fa_success ? L : -1;    // host walk: -1 = the result does not depend on lastIndex
+        if (chain && fa_success) *chain = L;
     }
 }
 
@@ -1160,21 +1163,22 @@ struct SweepCall {
 };
 
 int launch_exact(ca_mirror* m, hipStream_t st, const SweepCall& in, const int32_t* d_lin, const uint8_t* d_need,
-                 DevView d_dest, DevView d_hset, DevView d_out, int32_t* d_wl) {
+                 DevView d_dest, DevView d_hset, DevView d_out, int32_t* d_wl, int32_t c_base = 0, int32_t grid = -1,
+                 int32_t* d_chain = nullptr) {
     const bool use_ext = m->n_ext_pods > 0;
     const size_t dyn = use_ext ? sizeof(OverlayExt) : 0;
     if (use_ext) {
         int rc;
         if ((rc = ensure_dyn_lds((const void*)k_sweep, dyn)) != CA_OK) return rc;
     }
-    hipLaunchKernelGGL(k_sweep, dim3(in.C), dim3(64), dyn, st, m->d_hot.as<NodeHot>(), m->d_ext.as<NodeExt>(),
+    hipLaunchKernelGGL(k_sweep, dim3(grid < 0 ? in.C : grid), dim3(64), dyn, st, m->d_hot.as<NodeHot>(), m->d_ext.as<NodeExt>(),
                        m->d_static.as<NodeStatic>(), in.n, in.d_mask.as<uint8_t>(), in.d_c.as<int32_t>(),
                        in.d_status.as<int32_t>(), in.d_off.as<int32_t>(), in.d_moves.as<int32_t>(),
                        m->d_pods.hot.as<PodHot>(), m->d_pods.spec.as<ca_pod_spec>(),
                        m->d_pods.terms.as<ca_selector_term>(), m->d_pods.reqs.as<ca_selector_req>(),
                        m->d_pods.names.as<int32_t>(), in.d_hints.as<int32_t>(), d_lin, d_need, d_dest.as<int32_t>(),
                        d_hset.as<int32_t>(), d_out.as<SweepOut>(), d_wl, use_ext ? 1 : 0,
-                       m->sw.bsum.as<BlockSum>());
+                       m->sw.bsum.as<BlockSum>(), c_base, d_chain);
     CA_HIP_CHECK(hipGetLastError());
     return CA_OK;
 }
@@ -1442,7 +1446,49 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         // each round looks LOOKAHEAD candidates ahead: the estimates drift with the distance
         // from the exact lastIndex, so rows further out would be re-centred again anyway
         constexpr int32_t LOOKAHEAD = 512;
+        // Serial exact chain: when a table round resolves few candidates for its cost (late
+        // planner windows over a nearly full cluster: long scans that no lane budget covers,
+        // windows that miss again after every re-centring), the next candidates run exactly,
+        // one launch each, queued back to back; each reads its lastIndex from the previous
+        // launch's output on the device (k_sweep chain mode) and one sync ends the batch.
+        // Batches double while the tables keep losing; the costs compared are measured.
+        double chain_ms_per = 0.03;          // per candidate; re-measured after each batch
+        int32_t chain_batch = 64;
+        int32_t chained = 0;
+        int32_t* const h_chain = sw.h_l0.as<int32_t>() + 1;
+        auto run_chain = [&](int32_t kend) -> int {
+            const auto tc = std::chrono::steady_clock::now();
+            h_chain[0] = (int32_t)cur;
+            CA_HIP_CHECK(hipMemcpyAsync(d_mode + 3, h_chain, sizeof(int32_t), hipMemcpyHostToDevice, st));
+            int32_t runs = 0;
+            for (int32_t k = k0; k < kend; k++) {
+                if (insensitive(k)) continue;                                       // lastIndex passes through
+                int e;
+                if ((e = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl, sens[k], 1, d_mode + 3)) != CA_OK)
+                    return e;
+                runs++;
+            }
+            CA_HIP_CHECK(hipMemcpyAsync(h_chain + 1, d_mode + 3, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+            CA_HIP_CHECK(hipStreamSynchronize(st));
+            cur = runs > 0 ? (int64_t)h_chain[1] : cur;
+            chained += runs;
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count();
+            if (runs > 0) chain_ms_per = ms / runs;
+            if (dbg_t) {
+                std::vector<SweepOut> o((size_t)C);
+                CA_HIP_CHECK(hipMemcpy(o.data(), d_out.ptr, sizeof(SweepOut) * (size_t)C, hipMemcpyDeviceToHost));
+                uint64_t ticks = 0, ev = 0, pl = 0;
+                for (int32_t k = k0; k < kend; k++)
+                    if (!insensitive(k)) { ticks += o[sens[k]].pad2; ev += o[sens[k]].evals; pl += o[sens[k]].n_placed; }
+                fprintf(stderr, "[sweep] serial chain [%d,%d): %d runs, %.3f ms, in-kernel %.3f ms, %llu evals, %llu placed\n",
+                        k0, kend, runs, ms, ticks * 1e-5, (unsigned long long)ev, (unsigned long long)pl);
+            }
+            k0 = kend;
+            return CA_OK;
+        };
         while (k0 < S) {
+            const auto t_round = std::chrono::steady_clock::now();
+            const int32_t k_round = k0;
             todo.clear(); todo_ws.clear(); todo_k.clear();
             const int32_t kend = std::min(S, k0 + LOOKAHEAD);
             for (int32_t k = k0; k < kend; k++)
@@ -1474,6 +1520,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 CA_HIP_CHECK(hipMemcpyAsync(ct + 64 * (size_t)T, d_tfp, sizeof(int32_t) * FPW * (size_t)T,
                                             hipMemcpyDeviceToHost, st));
                 CA_HIP_CHECK(hipStreamSynchronize(st));
+                tmark("table sync");
                 const int32_t* ctf = ct + 64 * (size_t)T;
                 for (int32_t t = 0; t < T; t++) {
                     const int32_t k = todo_k[t];
@@ -1514,7 +1561,20 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 }
                 cur = v;
             }
+            tmark("walk");
             if (k0 >= S) break;
+            {
+                const double round_ms =
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_round).count();
+                const int32_t adv = k0 - k_round;
+                if (round_ms > 2.0 * chain_ms_per * std::max(adv, 1) && !getenv("CASIM_NO_SERIAL_CHAIN")) {
+                    if ((rc = run_chain(std::min(S, k0 + chain_batch))) != CA_OK) return rc;
+                    chain_batch = std::min(2 * chain_batch, 4096);
+                    if (k0 >= S) break;
+                } else {
+                    chain_batch = 64;
+                }
+            }
             // re-centre the windows from k0 on: follow the tables where the estimate falls
             // inside a window, otherwise shift the nearest known entry
             int64_t est = cur;
@@ -1538,6 +1598,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 }
                 est = wrap(next, n);
             }
+            tmark("re-centre");
             if (rounds > S + 4) { set_last_error("sweep speculation did not converge"); return CA_EDEVICE; }
         }
         tmark("host walk");
@@ -1553,7 +1614,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
             CA_HIP_CHECK(hipMemcpyAsync(d_lin, h_lin, (sizeof(int32_t) + 1) * (size_t)C, hipMemcpyHostToDevice, st));
             if ((rc = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl)) != CA_OK) return rc;
         }
-        if (n_rerun > 0 || exact_runs > 0)
+        if (n_rerun > 0 || exact_runs > 0 || chained > 0)
             if ((rc = apply_hints()) != CA_OK) return rc;
         CA_HIP_CHECK(hipMemcpyAsync(sw.h_out.ptr, sw.out.ptr, d2h_bytes, hipMemcpyDeviceToHost, st));
         CA_HIP_CHECK(hipStreamSynchronize(st));

@@ -310,12 +310,15 @@ def sweep_leg(args, device: int, with_cpu: bool) -> dict:
         runs = {}
         for mode in ("fresh", "hinted"):
             ts = []
-            for _ in range(max(args.steps, 5)):
+            # untimed warm-up: the first call of a shape runs eagerly, the second captures the
+            # HIP graph, the first replay sets it up; the timed calls are the steady state
+            for it in range(max(args.warmup, 3) + max(args.steps, 10)):
                 if mode == "fresh":
                     m.set_hints(fresh_h)
                 t = time.perf_counter()
                 r = plan.run(0)
-                ts.append(time.perf_counter() - t)
+                if it >= max(args.warmup, 3):
+                    ts.append(time.perf_counter() - t)
             runs[mode] = (r, m.get_hints(len(w.table)))
             out[f"{mode}_ms"] = float(np.median(ts) * 1e3)
             out[f"{mode}_evals"] = int(r.results["evals"].sum())

@@ -51,7 +51,8 @@ struct SweepScratch {
     DevBuf tev, tdest;              // table lanes' evaluation counts and pod destinations (first round)
     DevBuf tfp, vp, mode;           // table rows' fit-point classes; visible-node prefix counts; class mode
     DevBuf bsum;                    // per 64-node block: maxima of the visible rows (sweep.hip BlockSum)
-    HostBuf h_in, h_tab, h_out, h_todo, h_lin, h_wl, h_tfp, h_ctab, h_l0;
+    DevBuf chainl;                  // the host walk's serial exact chain: candidates in order
+    HostBuf h_in, h_tab, h_out, h_todo, h_lin, h_wl, h_tfp, h_ctab, h_l0, h_chainl;
     // the device pipeline of the last call shape, replayed as a graph (sweep.hip sweep_core)
     hipGraphExec_t gexec = nullptr;
     uint64_t gkey = 0, gseen = 0;

@@ -189,17 +189,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CASIM_S
     const ca_selector_req* __restrict__ reqs, const int32_t* __restrict__ names, const int32_t* __restrict__ hints,
     const int32_t* __restrict__ lin_arr, const uint8_t* __restrict__ need, int32_t* __restrict__ out_dest,
     int32_t* __restrict__ hint_set, SweepOut* __restrict__ outs, int32_t* __restrict__ walk_lout, int32_t use_ext,
-    const BlockSum* __restrict__ bsum, int32_t c_base, int32_t* __restrict__ chain) {
+    const BlockSum* __restrict__ bsum, const int32_t* __restrict__ chain_list, int32_t n_chain,
+    int32_t* __restrict__ chain) {
     __shared__ OverlaySmem ov;
     extern __shared__ __attribute__((aligned(16))) unsigned char ovx_raw[];
     OverlayExt& ox = *reinterpret_cast<OverlayExt*>(ovx_raw);
-    const int c = c_base + blockIdx.x;
-    // chain != null: one candidate per launch, its lastIndex the previous launch's output
-    // (launches in candidate order on one stream: the host walk's serial exact chain)
-    if (!chain && !need[c]) return;
+    // chain != null (the host walk's serial exact chain): one workgroup runs the candidates
+    // chain_list[0..n_chain) in order, each from the lastIndex the previous one left (*chain
+    // in and out), with the node rows warm in its XCD's L2 from one candidate to the next
+    int32_t chain_v = chain ? *chain : 0;
+    for (int32_t it = 0; it < (chain ? n_chain : 1); it++) {
+    const int c = chain ? chain_list[it] : (int)blockIdx.x;
+    if (!chain && !need[c]) continue;
     const uint64_t t_begin = wall_clock64();      // diagnostics: SweepOut.pad2 = device ticks (100 MHz)
     const int lane = threadIdx.x;
-    const int32_t lin = chain ? *chain : lin_arr[c];
+    const int32_t lin = chain ? chain_v : lin_arr[c];
     SweepOut res;
     res.removable = 0; res.reason = CA_UNREMOVABLE_NONE; res.n_placed = 0; res.lin = lin; res.lout = lin;
     res.fa_success = 0; res.status = CA_OK; res.pad = 0; res.evals = 0; res.pad2 = 0;
@@ -209,13 +213,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CASIM_S
         for (int32_t i = lane; i < mn; i += 64) { out_dest[mo + i] = -1; hint_set[mo + i] = -1; }
         res.reason = CA_UNREMOVABLE_UNEXPECTED_ERROR;
         if (lane == 0) { outs[c] = res; walk_lout[c] = -1; }
-        return;
+        continue;
     }
     if (cand_status[c] != 0) {                                                 // :162-169
         for (int32_t i = lane; i < mn; i += 64) { out_dest[mo + i] = -1; hint_set[mo + i] = -1; }
         res.reason = cand_status[c];
         if (lane == 0) { outs[c] = res; walk_lout[c] = -1; }
-        return;
+        continue;
     }
     int32_t npl = 0;          // overlay entries
     int32_t L = lin;
@@ -617,8 +621,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CASIM_S
         res.pad2 = wall_clock64() - t_begin;
         outs[c] = res;
         walk_lout[c] = fa_success ? L : -1;    // host walk: -1 = the result does not depend on lastIndex
-        if (chain && fa_success) *chain = L;
     }
+    if (fa_success) chain_v = L;
+    __builtin_amdgcn_wave_barrier();              // (the next candidate re-initialises the overlay)
+    }
+    if (chain && threadIdx.x == 0) *chain = chain_v;
 }
 
 // ---------------------------------------------------------------------------
@@ -1163,22 +1170,22 @@ struct SweepCall {
 };
 
 int launch_exact(ca_mirror* m, hipStream_t st, const SweepCall& in, const int32_t* d_lin, const uint8_t* d_need,
-                 DevView d_dest, DevView d_hset, DevView d_out, int32_t* d_wl, int32_t c_base = 0, int32_t grid = -1,
-                 int32_t* d_chain = nullptr) {
+                 DevView d_dest, DevView d_hset, DevView d_out, int32_t* d_wl, const int32_t* d_chain_list = nullptr,
+                 int32_t n_chain = 0, int32_t* d_chain = nullptr) {
     const bool use_ext = m->n_ext_pods > 0;
     const size_t dyn = use_ext ? sizeof(OverlayExt) : 0;
     if (use_ext) {
         int rc;
         if ((rc = ensure_dyn_lds((const void*)k_sweep, dyn)) != CA_OK) return rc;
     }
-    hipLaunchKernelGGL(k_sweep, dim3(grid < 0 ? in.C : grid), dim3(64), dyn, st, m->d_hot.as<NodeHot>(), m->d_ext.as<NodeExt>(),
+    hipLaunchKernelGGL(k_sweep, dim3(d_chain ? 1 : in.C), dim3(64), dyn, st, m->d_hot.as<NodeHot>(), m->d_ext.as<NodeExt>(),
                        m->d_static.as<NodeStatic>(), in.n, in.d_mask.as<uint8_t>(), in.d_c.as<int32_t>(),
                        in.d_status.as<int32_t>(), in.d_off.as<int32_t>(), in.d_moves.as<int32_t>(),
                        m->d_pods.hot.as<PodHot>(), m->d_pods.spec.as<ca_pod_spec>(),
                        m->d_pods.terms.as<ca_selector_term>(), m->d_pods.reqs.as<ca_selector_req>(),
                        m->d_pods.names.as<int32_t>(), in.d_hints.as<int32_t>(), d_lin, d_need, d_dest.as<int32_t>(),
                        d_hset.as<int32_t>(), d_out.as<SweepOut>(), d_wl, use_ext ? 1 : 0,
-                       m->sw.bsum.as<BlockSum>(), c_base, d_chain);
+                       m->sw.bsum.as<BlockSum>(), d_chain_list, n_chain, d_chain);
     CA_HIP_CHECK(hipGetLastError());
     return CA_OK;
 }
@@ -1448,9 +1455,9 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         constexpr int32_t LOOKAHEAD = 512;
         // Serial exact chain: when a table round resolves few candidates for its cost (late
         // planner windows over a nearly full cluster: long scans that no lane budget covers,
-        // windows that miss again after every re-centring), the next candidates run exactly,
-        // one launch each, queued back to back; each reads its lastIndex from the previous
-        // launch's output on the device (k_sweep chain mode) and one sync ends the batch.
+        // windows that miss again after every re-centring), the next candidates run exactly
+        // in one launch: one workgroup walks them in order, each from the lastIndex the
+        // previous one left (k_sweep chain mode), and one sync ends the batch.
         // Batches double while the tables keep losing; the costs compared are measured.
         double chain_ms_per = 0.03;          // per candidate; re-measured after each batch
         int32_t chain_batch = 64;
@@ -1461,12 +1468,17 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
             h_chain[0] = (int32_t)cur;
             CA_HIP_CHECK(hipMemcpyAsync(d_mode + 3, h_chain, sizeof(int32_t), hipMemcpyHostToDevice, st));
             int32_t runs = 0;
-            for (int32_t k = k0; k < kend; k++) {
-                if (insensitive(k)) continue;                                       // lastIndex passes through
-                int e;
-                if ((e = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl, sens[k], 1, d_mode + 3)) != CA_OK)
+            int e;
+            if ((e = sw.chainl.reserve(sizeof(int32_t) * (size_t)std::max(kend - k0, 1))) != CA_OK) return e;
+            if ((e = sw.h_chainl.reserve(sizeof(int32_t) * (size_t)std::max(kend - k0, 1))) != CA_OK) return e;
+            int32_t* const cl = sw.h_chainl.as<int32_t>();
+            for (int32_t k = k0; k < kend; k++)
+                if (!insensitive(k)) cl[runs++] = sens[k];                          // others pass lastIndex through
+            if (runs > 0) {
+                CA_HIP_CHECK(hipMemcpyAsync(sw.chainl.ptr, cl, sizeof(int32_t) * (size_t)runs, hipMemcpyHostToDevice, st));
+                if ((e = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl, sw.chainl.as<int32_t>(),
+                                      runs, d_mode + 3)) != CA_OK)
                     return e;
-                runs++;
             }
             CA_HIP_CHECK(hipMemcpyAsync(h_chain + 1, d_mode + 3, sizeof(int32_t), hipMemcpyDeviceToHost, st));
             CA_HIP_CHECK(hipStreamSynchronize(st));

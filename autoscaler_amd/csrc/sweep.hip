@@ -511,30 +511,39 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CASIM_S
         // one (B) stay in registers with this candidate's overlay as per-lane deltas
         if (target < 0 && !pre_fail && fast) {
             const int32_t j0 = L >> 6, l0 = L & 63;
+            // look-ahead window over 64 full blocks (lane i: block r = wr + i): a block passes
+            // when the pod fails its maxima and it holds none of this candidate's placements
+            // (whose deltas the maxima do not see).  The overlay and the maxima are fixed for
+            // the whole scan (a placement ends it), so one window serves 64 blocks.
+            int32_t wr = -1, my_nv = 0;
+            uint64_t passm = 0;
             for (int32_t r = 0; r <= nb; r++) {
                 if (r == nb && l0 == 0) break;
                 int32_t j = j0 + r;
                 if (j >= nb) j -= nb;
                 if (r > 0 && r < nb) {
-                    // look ahead over the next 64 full blocks: pass every leading block whose
-                    // maxima the pod fails (and that holds none of this candidate's placements,
-                    // whose deltas the maxima do not see), counting its visible nodes
-                    const int32_t rr = r + lane;
-                    bool pass = false;
-                    int32_t nv = 0;
-                    if (rr < nb) {
-                        int32_t jj = j0 + rr;
-                        if (jj >= nb) jj -= nb;
-                        const BlockSum b = bsum[jj];
-                        bool ovh = false;
-                        for (int32_t q = 0; q < npl; q++) ovh |= (ov.node[q] >> 6) == jj;
-                        pass = !ovh && !block_may_fit(p, b);
-                        nv = block_vis(b, jj, 0, 64, node);
+                    if (wr < 0 || r >= wr + 64) {
+                        const int32_t rr = r + lane;
+                        bool pass = false;
+                        my_nv = 0;
+                        if (rr < nb) {
+                            int32_t jj = j0 + rr;
+                            if (jj >= nb) jj -= nb;
+                            const BlockSum b = bsum[jj];
+                            bool ovh = false;
+                            for (int32_t q = 0; q < npl; q++) ovh |= (ov.node[q] >> 6) == jj;
+                            pass = !ovh && !block_may_fit(p, b);
+                            my_nv = block_vis(b, jj, 0, 64, node);
+                        }
+                        passm = __ballot(pass);
+                        wr = r;
                     }
-                    const uint64_t stop = __ballot(!pass);
-                    const int32_t k = stop ? __builtin_ctzll(stop) : 64;
+                    // pass every leading block from r on, counting its visible nodes
+                    const int32_t off = r - wr;
+                    const uint64_t stop = ~passm & (~0ull << off);
+                    const int32_t k = (stop ? __builtin_ctzll(stop) : 64) - off;
                     if (k > 0) {
-                        evals += (uint64_t)__ockl_wfred_add_i64(lane < k ? nv : 0);
+                        evals += (uint64_t)__ockl_wfred_add_i64((lane >= off && lane < off + k) ? my_nv : 0);
                         r += k - 1;
                         continue;
                     }

@@ -231,6 +231,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CASIM_S
     // lane i holds moved pod (batch + i): id, record, hint; outputs kept in lanes and
     // stored once per batch (no per-pod store for a later load to wait behind)
     int32_t my_id = -1, my_hint = -1, my_dest = -1, my_hset = -1;
+    bool own_ok = false;          // the moved pods' request sums (hints to the candidate itself)
+    int64_t own_c = 0, own_m = 0, own_e = 0;
     PodHot my_p = {};
     NodeHot my_hh = {};           // the hinted node's row, prefetched with the batch
     uint8_t my_hdm = 0;
@@ -405,15 +407,26 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CASIM_S
             NodeExt ne = {};                 // read only by the port / extended-resource checks
             if (p.flags & (PF_PORTS | PF_SCALAR_REQ)) ne = ext[h];
             if (h == node) {
-                // the candidate with every moved pod removed (cluster.go:228-233)
-                for (int32_t q = 0; q < mn; q++) {
-                    const PodHot mp = ph[move_pods[mo + q]];
-                    const ca_pod_spec& ms = specs[mp.spec];
-                    nh.cpu = wadd(nh.cpu, mp.cpu); nh.mem = wadd(nh.mem, mp.mem); nh.eph = wadd(nh.eph, mp.eph);
-                    nh.pods += 1;
-                    for (int k = 0; k < CA_MAX_SCALAR; k++) ne.scalar[k] = wadd(ne.scalar[k], ms.req_scalar[k]);
-                    for (int w = 0; w < CA_PORT_WORDS; w++) ne.ports[w] &= ~ms.port_use[w];
+                // the candidate with every moved pod removed (cluster.go:228-233): the moved
+                // pods' requests summed lane-parallel once per candidate (wrapping adds:
+                // any order), the extended part only for pods that read it
+                if (!own_ok) {
+                    int64_t sc = 0, sm = 0, se = 0;
+                    for (int32_t q = lane; q < mn; q += 64) {
+                        const PodHot mp = ph[move_pods[mo + q]];
+                        sc = wadd(sc, mp.cpu); sm = wadd(sm, mp.mem); se = wadd(se, mp.eph);
+                    }
+                    own_c = __ockl_wfred_add_i64(sc); own_m = __ockl_wfred_add_i64(sm); own_e = __ockl_wfred_add_i64(se);
+                    own_ok = true;
                 }
+                nh.cpu = wadd(nh.cpu, own_c); nh.mem = wadd(nh.mem, own_m); nh.eph = wadd(nh.eph, own_e);
+                nh.pods += mn;
+                if (p.flags & (PF_PORTS | PF_SCALAR_REQ))
+                    for (int32_t q = 0; q < mn; q++) {
+                        const ca_pod_spec& ms = specs[ph[move_pods[mo + q]].spec];
+                        for (int k = 0; k < CA_MAX_SCALAR; k++) ne.scalar[k] = wadd(ne.scalar[k], ms.req_scalar[k]);
+                        for (int w = 0; w < CA_PORT_WORDS; w++) ne.ports[w] &= ~ms.port_use[w];
+                    }
             } else {
                 // this candidate's placements on h (a node has at most one overlay slot)
                 int32_t q = -1;

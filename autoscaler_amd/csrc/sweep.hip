@@ -1556,10 +1556,16 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 CA_HIP_CHECK(hipStreamSynchronize(st));
                 tmark("table sync");
                 const int32_t* ctf = ct + 64 * (size_t)T;
-                for (int32_t t = 0; t < T; t++) {
-                    const int32_t k = todo_k[t];
-                    for (int32_t w = 0; w < 64; w++) tab[(size_t)w * S + k] = ct[(size_t)w * T + t];
-                    for (int32_t i = 0; i < FPW; i++) h_tfp[(size_t)i * S + k] = ctf[(size_t)i * T + t];
+                // row by row: sequential reads, near-sequential writes (todo_k ascends)
+                for (int32_t w = 0; w < 64; w++) {
+                    const int32_t* src = ct + (size_t)w * T;
+                    int32_t* dst = tab + (size_t)w * S;
+                    for (int32_t t = 0; t < T; t++) dst[todo_k[t]] = src[t];
+                }
+                for (int32_t i = 0; i < FPW; i++) {
+                    const int32_t* src = ctf + (size_t)i * T;
+                    int32_t* dst = h_tfp + (size_t)i * S;
+                    for (int32_t t = 0; t < T; t++) dst[todo_k[t]] = src[t];
                 }
                 float ms = 0;
                 (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);

@@ -56,6 +56,10 @@ struct SweepScratch {
     // the device pipeline of the last call shape, replayed as a graph (sweep.hip sweep_core)
     hipGraphExec_t gexec = nullptr;
     uint64_t gkey = 0, gseen = 0;
+    // serial-only calls (sweep_core): the next call's mode and the measured ms per candidate
+    bool serial_next = false;
+    int32_t serial_calls = 0;
+    float serial_ms_per = 0, pipe_ms_per = 0;
     ~SweepScratch() {
         if (gexec) (void)hipGraphExecDestroy(gexec);
     }

@@ -1421,9 +1421,42 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                               (uint64_t)(uintptr_t)in.d_hints.ptr, (uint64_t)(uintptr_t)st};
         for (uint64_t x : v) { gkey ^= x; gkey *= 1099511628211ull; }
     }
+    // Serial-only call: every candidate in one k_sweep chain launch (no probe, tables or
+    // walk).  Taken when the previous call of this mirror resolved most of its sensitive
+    // candidates through the serial chain anyway (the planner's late windows), and kept
+    // while it costs less per candidate than the last pipeline call (re-measured at least
+    // every 8 calls); windows of at most 2 048 candidates only.
+    const bool serial_only = S > 0 && n > 0 && C <= 2048 && sw.serial_next && !getenv("CASIM_NO_SERIAL_CHAIN");
+    auto enqueue_serial = [&]() -> int {
+        int e;
+        if ((e = sw.chainl.reserve(sizeof(int32_t) * (size_t)C)) != CA_OK) return e;
+        if ((e = sw.h_chainl.reserve(sizeof(int32_t) * (size_t)C)) != CA_OK) return e;
+        int32_t* const cl = sw.h_chainl.as<int32_t>();
+        for (int32_t c = 0; c < C; c++) cl[c] = c;
+        int32_t* const hc = sw.h_l0.as<int32_t>() + 1;
+        hc[0] = (int32_t)L0;
+        CA_HIP_CHECK(hipMemcpyAsync(sw.chainl.ptr, cl, sizeof(int32_t) * (size_t)C, hipMemcpyHostToDevice, st));
+        CA_HIP_CHECK(hipMemcpyAsync(d_mode + 3, hc, sizeof(int32_t), hipMemcpyHostToDevice, st));
+        if (d_pod_hints && M > 0) {
+            hipLaunchKernelGGL(k_hints_gather, dim3((M + 255) / 256), dim3(256), 0, st, d_pod_hints,
+                               in.d_moves.as<int32_t>(), M, in.d_hints.as<int32_t>());
+            CA_HIP_CHECK(hipGetLastError());
+        }
+        hipLaunchKernelGGL(k_block_sum, dim3((n + 63) / 64), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
+                           in.d_mask.as<uint8_t>(), n, sw.bsum.as<BlockSum>());
+        CA_HIP_CHECK(hipGetLastError());
+        if ((e = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl, sw.chainl.as<int32_t>(), C,
+                              d_mode + 3)) != CA_OK)
+            return e;
+        if ((e = apply_hints()) != CA_OK) return e;
+        CA_HIP_CHECK(hipMemcpyAsync(sw.h_out.ptr, sw.out.ptr, d2h_bytes, hipMemcpyDeviceToHost, st));
+        return CA_OK;
+    };
     static const bool no_graph = getenv("CASIM_NO_GRAPH") != nullptr;
     CA_HIP_CHECK(hipEventRecord(m->ev0, st));
-    if (!no_graph && sw.gexec && sw.gkey == gkey) {
+    if (serial_only) {
+        if ((rc = enqueue_serial()) != CA_OK) return rc;
+    } else if (!no_graph && sw.gexec && sw.gkey == gkey) {
         CA_HIP_CHECK(hipGraphLaunch(sw.gexec, st));
     } else if (!no_graph && sw.gseen == gkey) {
         if (sw.gexec) { (void)hipGraphExecDestroy(sw.gexec); sw.gexec = nullptr; }
@@ -1449,13 +1482,15 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         float ms = 0;
         (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
         kms += ms;
-        if (dbg_t) fprintf(stderr, "[sweep] device pipeline: %d sensitive, kernels %.3f ms\n", S, ms);
+        if (dbg_t) fprintf(stderr, "[sweep] device %s: %d sensitive, kernels %.3f ms\n",
+                           serial_only ? "serial chain (all candidates)" : "pipeline", S, ms);
         tmark("device");
     }
     // ---- 4. host walk from where the device walk stopped (or of everything) ----
-    int32_t k0 = dev_walk ? h_info[0] : 0;         // first sensitive candidate not yet resolved
+    int32_t k0 = serial_only ? S : dev_walk ? h_info[0] : 0;   // first sensitive candidate not yet resolved
     int64_t cur = dev_walk ? (int64_t)h_info[1] : L0;
     if (dev_walk && k0 == 0) cur = L0;
+    int32_t chained = 0;
     if (k0 < S) {
         std::vector<int32_t> ws((size_t)S, 0);
         std::vector<int32_t> wlc((size_t)C, 0);
@@ -1483,7 +1518,6 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         // Batches double while the tables keep losing; the costs compared are measured.
         double chain_ms_per = 0.03;          // per candidate; re-measured after each batch
         int32_t chain_batch = 64;
-        int32_t chained = 0;
         int32_t* const h_chain = sw.h_l0.as<int32_t>() + 1;
         auto run_chain = [&](int32_t kend) -> int {
             const auto tc = std::chrono::steady_clock::now();
@@ -1691,6 +1725,19 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     // (the hint update stays queued on the mirror's stream: every later call is ordered
     // behind it, and ca_mirror_get_hints synchronises)
     tmark("done");
+    {   // the next call's mode (serial_only above)
+        const float per = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_start).count() /
+                          (float)std::max(C, 1);
+        if (serial_only) {
+            sw.serial_ms_per = per;
+            sw.serial_calls++;
+        } else {
+            sw.pipe_ms_per = per;
+            sw.serial_calls = 0;
+        }
+        sw.serial_next = serial_only ? (sw.serial_calls < 8 && sw.serial_ms_per < sw.pipe_ms_per)
+                                     : (S > 0 && 2 * chained > S);
+    }
     m->sweep_stats.rounds = rounds + exact_runs;
     // the sweep's output depends on its input lastIndex iff some scan succeeded
     m->sweep_stats.had_success = any_success ? 1 : 0;

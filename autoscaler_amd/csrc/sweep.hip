@@ -1426,7 +1426,9 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     // candidates through the serial chain anyway (the planner's late windows), and kept
     // while it costs less per candidate than the last pipeline call (re-measured at least
     // every 8 calls); windows of at most 2 048 candidates only.
-    const bool serial_only = S > 0 && n > 0 && C <= 2048 && sw.serial_next && !getenv("CASIM_NO_SERIAL_CHAIN");
+    // (CASIM_SWEEP_SERIAL: every call serial-only; CASIM_NO_SERIAL_CHAIN: never; tests)
+    const bool serial_only = S > 0 && n > 0 && !getenv("CASIM_NO_SERIAL_CHAIN") &&
+                             ((C <= 2048 && sw.serial_next) || getenv("CASIM_SWEEP_SERIAL") != nullptr);
     auto enqueue_serial = [&]() -> int {
         int e;
         if ((e = sw.chainl.reserve(sizeof(int32_t) * (size_t)C)) != CA_OK) return e;
@@ -1641,7 +1643,8 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 const double round_ms =
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_round).count();
                 const int32_t adv = k0 - k_round;
-                if (round_ms > 2.0 * chain_ms_per * std::max(adv, 1) && !getenv("CASIM_NO_SERIAL_CHAIN")) {
+                if ((round_ms > 2.0 * chain_ms_per * std::max(adv, 1) || getenv("CASIM_SWEEP_FORCE_CHAIN")) &&
+                    !getenv("CASIM_NO_SERIAL_CHAIN")) {
                     if ((rc = run_chain(std::min(S, k0 + chain_batch))) != CA_OK) return rc;
                     chain_batch = std::min(2 * chain_batch, 4096);
                     if (k0 >= S) break;

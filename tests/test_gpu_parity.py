@@ -505,8 +505,13 @@ def test_estimate_full_c2_properties():
 # --------------------------------------------------------------------------
 # removal sweep
 # --------------------------------------------------------------------------
+@pytest.mark.parametrize("mode", ["pipeline", "serial"])
 @pytest.mark.parametrize("seed", range(12))
-def test_sweep_random(seed, oracle):
+def test_sweep_random(seed, mode, oracle, monkeypatch):
+    """mode serial: every candidate in one k_sweep chain launch (CASIM_SWEEP_SERIAL, the
+    serial-only calls of the planner's late windows)."""
+    if mode == "serial":
+        monkeypatch.setenv("CASIM_SWEEP_SERIAL", "1")
     rng, nodes, scheduled, pending = rand_cluster(seed, n_nodes=14, n_pods=40, pods_per_node=4)
     it = Interner(nodes, [p for p, _ in scheduled])
     node_recs = it.encode_nodes(nodes)
@@ -538,11 +543,17 @@ def test_sweep_random(seed, oracle):
     assert o.last_index == g.last_index
 
 
-@pytest.mark.parametrize("walk", ["device", "host"])
+@pytest.mark.parametrize("walk", ["device", "host", "host-chain", "serial"])
 @pytest.mark.parametrize("n_nodes", [300, 1500, 5000])
 def test_sweep_workload(n_nodes, walk, oracle, monkeypatch):
-    if walk == "host":
+    """host-chain: the host walk hands every batch to the serial exact chain (one k_sweep
+    workgroup walking the candidates in order); serial: serial-only calls."""
+    if walk in ("host", "host-chain"):
         monkeypatch.setenv("CASIM_SWEEP_HOST_WALK", "1")
+    if walk == "host-chain":
+        monkeypatch.setenv("CASIM_SWEEP_FORCE_CHAIN", "1")
+    if walk == "serial":
+        monkeypatch.setenv("CASIM_SWEEP_SERIAL", "1")
     w = W.c3(n_nodes=n_nodes)
     hints = np.full(len(w.table), -1, np.int32)
     outs = []

@@ -112,8 +112,10 @@ def _c3_case(n_nodes: int, limit: int, hints=None) -> PlanCase:
                     np.zeros(0, np.int32), np.zeros(1, np.int32), np.zeros(0, np.int32))
 
 
-@pytest.mark.parametrize("n_nodes,limit", [(1500, 0), (5000, 20), (5000, 200)])
+@pytest.mark.parametrize("n_nodes,limit", [(1500, 0), (5000, 20), (5000, 200), (5000, 0)])
 def test_plan_c3(n_nodes, limit, oracle):
+    """(5000, 0): the late windows over a nearly full cluster go through the sweep's serial
+    exact chain and serial-only calls."""
     case = _c3_case(n_nodes, limit)
     o, m = oracle.OracleState(), _mirror()
     case.load(o)

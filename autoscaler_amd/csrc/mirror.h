@@ -86,6 +86,7 @@ struct FilterScratch {
 struct RowStage {
     DevBuf d;
     HostBuf h;
+    HostBuf full;                  // page-locked hot + ext columns of a full-table sync
 };
 
 // ca_plan_removals (planner.hip): the last call's moves and counters.

@@ -414,11 +414,13 @@ int ca_mirror::sync_nodes() {
         static_dirty = true;
     }
     if (all_dirty || dirty_rows.size() > std::max<size_t>(64, n / 4)) {
-        std::vector<NodeHot> h(n);
-        std::vector<NodeExt> e(n);
+        // both columns built in page-locked memory: DMA straight from it, no staging copy
+        if ((rc = rs.full.reserve((sizeof(NodeHot) + sizeof(NodeExt)) * std::max<size_t>(n, 1))) != CA_OK) return rc;
+        NodeHot* h = rs.full.as<NodeHot>();
+        NodeExt* e = reinterpret_cast<NodeExt*>(h + n);
         for (size_t i = 0; i < n; i++) { fill_hot((int32_t)i, h[i]); fill_ext((int32_t)i, e[i]); }
-        if (n) CA_HIP_CHECK(hipMemcpyAsync(d_hot.ptr, h.data(), sizeof(NodeHot) * n, hipMemcpyHostToDevice, stream));
-        if (n) CA_HIP_CHECK(hipMemcpyAsync(d_ext.ptr, e.data(), sizeof(NodeExt) * n, hipMemcpyHostToDevice, stream));
+        if (n) CA_HIP_CHECK(hipMemcpyAsync(d_hot.ptr, h, sizeof(NodeHot) * n, hipMemcpyHostToDevice, stream));
+        if (n) CA_HIP_CHECK(hipMemcpyAsync(d_ext.ptr, e, sizeof(NodeExt) * n, hipMemcpyHostToDevice, stream));
         CA_HIP_CHECK(hipStreamSynchronize(stream));
     } else if (!dirty_rows.empty()) {
         // few rows: stage them (row id + both columns) in pinned memory, one H2D copy, and

@@ -1346,10 +1346,14 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
             std::vector<int32_t> open;
             for (int32_t q = 0; q < S0; q++) open.push_back(q);
             for (size_t i = 0; i < m->nodes.size() && !open.empty(); i++) {
-                NodeHot h;
-                m->fill_hot((int32_t)i, h);
+                // the free resources of fill_hot, without its port / scalar flag scans (a
+                // shape that fits no node walks every node here)
+                const NodeRow& nd = m->nodes[i];
+                const int64_t fc = wsub(nd.spec.alloc_milli_cpu, nd.req_cpu), fm = wsub(nd.spec.alloc_memory, nd.req_mem);
+                const int64_t fe = wsub(nd.spec.alloc_ephemeral, nd.req_eph);
+                const int32_t fp = clamp_i32(nd.spec.alloc_pods - nd.npods);
                 for (size_t q = 0; q < open.size();) {
-                    if (fb_fit(fb_shapes[open[q]], h.cpu, h.mem, h.eph, h.pods)) {
+                    if (fb_fit(fb_shapes[open[q]], fc, fm, fe, fp)) {
                         alive[open[q]] = 1;
                         open[q] = open.back();
                         open.pop_back();

@@ -86,7 +86,7 @@ struct FilterScratch {
 struct RowStage {
     DevBuf d;
     HostBuf h;
-    HostBuf full;                  // page-locked hot + ext columns of a full-table sync
+    HostBuf full;                  // page-locked staging: full-table hot + ext columns, appended pod records
 };
 
 // ca_plan_removals (planner.hip): the last call's moves and counters.

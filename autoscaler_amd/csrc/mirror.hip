@@ -464,10 +464,14 @@ int ca_mirror::sync_pods() {
     if (pods.size() >= d_pods_synced && terms.size() >= d_terms_synced && d_pods_synced == (size_t)d_pods.n_pods &&
         reqs.size() >= (size_t)d_pods.n_reqs && pf_names.size() >= (size_t)d_pods.n_names && d_pods_synced > 0) {
         const size_t a = d_pods_synced, k = pods.size() - a;
-        std::vector<ca_pod_spec> specs(k);
+        // the new records gathered into page-locked staging (shared with sync_nodes' full
+        // path; both finish their copies before returning): DMA straight from it
+        int rc = rs.full.reserve(sizeof(ca_pod_spec) * std::max<size_t>(k, 1));
+        if (rc != CA_OK) return rc;
+        ca_pod_spec* specs = rs.full.as<ca_pod_spec>();
         for (size_t i = 0; i < k; i++) specs[i] = pods[a + i].spec;
-        int rc = d_pods.append(specs.data(), (int32_t)k, terms.data(), (int32_t)terms.size(), reqs.data(),
-                               (int32_t)reqs.size(), pf_names.data(), (int32_t)pf_names.size(), stream);
+        rc = d_pods.append(specs, (int32_t)k, terms.data(), (int32_t)terms.size(), reqs.data(),
+                           (int32_t)reqs.size(), pf_names.data(), (int32_t)pf_names.size(), stream);
         if (rc != CA_OK) return rc;
         d_pods_synced = pods.size();
         d_terms_synced = terms.size();

@@ -19,6 +19,7 @@
 //                      input equals its predecessor's output (exact).
 #include "mirror.h"
 #include "device_filters.h"
+#include "pdqsort.h"
 
 #include <cstring>
 #include <algorithm>
@@ -449,6 +450,106 @@ __global__ void __launch_bounds__(RTHREADS) k_radix_scatter(const GroupMeta* __r
     for (int c = 0; c < RCH; c++) {
         if (dg[c] == 0xFFFFFFFFu) continue;
         dst[gm.off + wcnt[w][dg[c]] + rk[c]] = pv[c];
+    }
+}
+
+// 1''-2''. Go 1.19 sort.Slice order (binpacking_estimator.go:74; pdqsort.h) ----------
+// One 1024-thread workgroup per group: the rank of every position of the group's list
+// (its class's dense rank, k_class_rank, or an explicit per-position rank from
+// k_item_rank), then pdqsort_func's exact permutation.  Groups of at most lds_n pods with
+// at most 256 ranks sort in LDS (16-bit positions + 8-bit ranks); the others in global
+// memory (rank above position in 32 or 64 bits).  Output: sorted[off + k] = position of
+// the k-th pod, the same layout as the radix sort's.  force (tests): 1 LDS, 2 / 3 global.
+// Scratch per group: gE [off, off+n) (8 B), scr [off, off+n), stack from off/2 + 2g.
+constexpr int PDQ_LDS_N = 52736;       // 3 B per pod + the static control block < 160 KB
+
+__global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restrict__ groups,
+                                                     const int32_t* __restrict__ pod_idx,
+                                                     const int32_t* __restrict__ pcls,
+                                                     const int32_t* __restrict__ crank, int32_t U,
+                                                     const uint32_t* __restrict__ item_rank,
+                                                     uint32_t* __restrict__ sorted, uint64_t* __restrict__ gE,
+                                                     uint32_t* __restrict__ scr_all, pdq::Frame* __restrict__ stack_all,
+                                                     int32_t lds_n, int32_t force, int32_t limit0, const int32_t* __restrict__ gmap) {
+    extern __shared__ __align__(16) unsigned char pdq_dyn[];
+    __shared__ pdq::Ctl ctl;
+    const int gi = GSEL(blockIdx.x);
+    const GroupMeta gm = groups[gi];
+    const int32_t n = gm.count, off = gm.off;
+    const int tid = threadIdx.x;
+    uint32_t* scr = scr_all + off;
+    pdq::Frame* stack = stack_all + off / 2 + 2 * gi;
+    if (tid == 0) ctl.rmax = 0;
+    __syncthreads();
+    const bool fit = n <= lds_n;
+    uint16_t* e16 = reinterpret_cast<uint16_t*>(pdq_dyn);
+    uint8_t* rk = pdq_dyn + 2 * (size_t)lds_n;
+    uint32_t rmax = 0;
+    for (int32_t i = tid; i < n; i += pdq::NT) {
+        const uint32_t r = item_rank ? item_rank[off + i] : (uint32_t)crank[(size_t)gi * U + pcls[pod_idx[off + i]]];
+        rmax = max(rmax, r);
+        scr[i] = r;
+        if (fit) { e16[i] = (uint16_t)i; rk[i] = (uint8_t)r; }
+    }
+    for (int d = 32; d >= 1; d >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, d, 64));
+    if ((tid & 63) == 0) atomicMax(&ctl.rmax, rmax);
+    __syncthreads();
+    const uint32_t R = ctl.rmax;
+    int mode = (fit && R < 256) ? 1 : (n <= (1 << 20) && R < 4096) ? 2 : 3;
+    if (force == 1 && fit && R < 256) mode = 1;
+    else if (force == 2 && n <= (1 << 20) && R < 4096) mode = 2;
+    else if (force == 3) mode = 3;
+    if (mode == 1) {
+        const pdq::LdsStore st{e16, rk};
+        pdq::wg_sort(st, n, stack, scr, ctl, limit0);
+        for (int32_t k = tid; k < n; k += pdq::NT) sorted[off + k] = e16[k];
+    } else if (mode == 2) {
+        uint32_t* e = reinterpret_cast<uint32_t*>(gE + off);
+        for (int32_t i = tid; i < n; i += pdq::NT) e[i] = (scr[i] << 20) | (uint32_t)i;
+        __syncthreads();
+        const pdq::G32Store st{e};
+        pdq::wg_sort(st, n, stack, scr, ctl, limit0);
+        for (int32_t k = tid; k < n; k += pdq::NT) sorted[off + k] = e[k] & 0xFFFFFu;
+    } else {
+        uint64_t* e = gE + off;
+        for (int32_t i = tid; i < n; i += pdq::NT) e[i] = ((uint64_t)scr[i] << 32) | (uint32_t)i;
+        __syncthreads();
+        const pdq::G64Store st{e};
+        pdq::wg_sort(st, n, stack, scr, ctl, limit0);
+        for (int32_t k = tid; k < n; k += pdq::NT) sorted[off + k] = (uint32_t)e[k];
+    }
+}
+
+// Dense rank of every position of a group's list from the comparison-sorted items
+// (k_score_tiles + k_merge_runs: ascending key == descending float64 score): equal scores
+// share a rank.  The Go-order path for pod sets with more than CLS_MAX score classes.
+__global__ void __launch_bounds__(1024) k_item_rank(const GroupMeta* __restrict__ groups,
+                                                   const SortItem* __restrict__ items, uint32_t* __restrict__ item_rank) {
+    __shared__ uint32_t wtot[16];
+    const GroupMeta gm = groups[blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t carry = 0;
+    for (int32_t base = 0; base < gm.count; base += 1024) {
+        const int32_t i = base + tid;
+        const bool valid = i < gm.count;
+        SortItem it = {};
+        uint32_t f = 0;
+        if (valid) {
+            it = items[gm.off + i];
+            f = (i > 0 && items[gm.off + i - 1].key != it.key) ? 1u : 0u;
+        }
+        uint32_t incl = f;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        if (lane == 63) wtot[w] = incl;
+        __syncthreads();
+        uint32_t pre = carry, tot = carry;
+        for (int q = 0; q < 16; q++) { if (q < w) pre += wtot[q]; tot += wtot[q]; }
+        if (valid) item_rank[gm.off + (int32_t)it.pos] = pre + incl;
+        carry = tot;
+        __syncthreads();
     }
 }
 
@@ -1809,6 +1910,9 @@ struct ca_estimate_plan {
     int32_t n_masks = 0, n_tiles = 0;
     DevBuf d_meta, d_pod_idx, d_tmpl, d_sortA, d_sortB, d_stream, d_spod, d_seg, d_heads, d_unsup, d_lin, d_need,
         d_out, d_sched_pod, d_sched_node, d_crank, d_hist, d_sched16;
+    // Go sort.Slice order (k_pdq_sort): element store, list scratch, frame stacks, and the
+    // per-position ranks of the comparison path
+    DevBuf d_pdq_e, d_pdq_scr, d_pdq_stack, d_item_rank;
     // HBM-slab rows (k_ffd_chain<true>): per group kcap and slab offset, for the limiter
     // setting they were sized for (slab_max_nodes)
     DevBuf d_slab, d_slab_off, d_gkcap;
@@ -1972,6 +2076,11 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
             return rc;
         if ((rc = p->d_hist.reserve(sizeof(int32_t) * (size_t)std::max(p->n_hist, 1))) != CA_OK) return rc;
     }
+    if ((rc = p->d_pdq_e.reserve(sizeof(uint64_t) * tot)) != CA_OK) return rc;
+    if ((rc = p->d_pdq_scr.reserve(sizeof(uint32_t) * tot)) != CA_OK) return rc;
+    if ((rc = p->d_pdq_stack.reserve(sizeof(pdq::Frame) * (tot / 2 + 2 * (size_t)std::max(G, 1) + 2))) != CA_OK)
+        return rc;
+    if (!p->bucket && (rc = p->d_item_rank.reserve(sizeof(uint32_t) * tot)) != CA_OK) return rc;
     if (G) CA_HIP_CHECK(hipMemcpyAsync(p->d_meta.ptr, p->h_meta.data(), sizeof(GroupMeta) * G, hipMemcpyHostToDevice, st));
     if (p->total) CA_HIP_CHECK(hipMemcpyAsync(p->d_pod_idx.ptr, pod_idx, sizeof(int32_t) * p->total, hipMemcpyHostToDevice, st));
     if (G) CA_HIP_CHECK(hipMemcpyAsync(p->d_tmpl.ptr, templates, sizeof(ca_template) * G, hipMemcpyHostToDevice, st));
@@ -2009,6 +2118,29 @@ int results_to_host(ca_estimate_plan* p, hipStream_t st, int32_t* sched_pod, uin
         CA_HIP_CHECK(hipGetLastError());
         CA_HIP_CHECK(hipMemcpyAsync(sched16, p->d_sched16.ptr, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, st));
     }
+    return CA_OK;
+}
+
+// Estimate's tie order: Go 1.19 sort.Slice (the reference, default) or, with
+// CASIM_SORT_ORDER=stable, ties by list position (the radix / merge paths alone)
+bool go_sort_order() {
+    const char* e = getenv("CASIM_SORT_ORDER");
+    return !(e && strcmp(e, "stable") == 0);
+}
+
+// k_pdq_sort for `ng` groups (map gm) into d_sortA: ranks from the class ranks (crank, U)
+// or from item_rank
+int launch_pdq_sort(ca_estimate_plan* p, hipStream_t ss, const int32_t* gm, int32_t ng, const int32_t* crank,
+                    int32_t U, const uint32_t* item_rank, int32_t force = 0) {
+    const int32_t lds_n = std::min(p->max_count, PDQ_LDS_N);
+    const size_t lds = ((size_t)3 * (size_t)std::max(lds_n, 0) + 15) & ~(size_t)15;
+    int rc;
+    if ((rc = ensure_dyn_lds((const void*)k_pdq_sort, lds)) != CA_OK) return rc;
+    hipLaunchKernelGGL(k_pdq_sort, dim3(ng), dim3(pdq::NT), lds, ss, p->d_meta.as<GroupMeta>(),
+                       p->d_pod_idx.as<int32_t>(), p->s ? p->s->d_cls.as<int32_t>() : nullptr, crank, U, item_rank,
+                       p->d_sortA.as<uint32_t>(), p->d_pdq_e.as<uint64_t>(), p->d_pdq_scr.as<uint32_t>(),
+                       p->d_pdq_stack.as<pdq::Frame>(), lds_n, force, 0, gm);
+    CA_HIP_CHECK(hipGetLastError());
     return CA_OK;
 }
 
@@ -2155,6 +2287,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         gmapB = gmapA + p->n_heavy;
     }
     const int32_t nA = split ? p->n_heavy : G, nB = split ? G - p->n_heavy : 0;
+    const bool go_order = go_sort_order();
     std::function<int()> sort_light;        // split: the light groups' sort, queued after the heavy chains
     // 1-3: score, sort, stream
     if (p->total > 0 && p->bucket) {
@@ -2166,8 +2299,10 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         int32_t nb = 1, passes = 0;                       // buckets <= U: 8-bit digits
         while (nb < U) { nb <<= 8; passes++; }
         passes = std::max(passes, 1);
+        const int32_t passes_run = go_order ? 0 : passes;
         const int32_t blocks = (p->max_count + 255) / 256;
-        // class ranks, LSD radix passes, stream emission for `ng` groups (map `gm`)
+        // class ranks, then Go's pdqsort (default) or the stable LSD radix passes, stream
+        // emission for `ng` groups (map `gm`)
         // (by value: the light groups' call runs after this block's locals are gone)
         auto sort_groups = [=](hipStream_t ss, const int32_t* gm, int32_t ng, bool events) -> int {
             hipLaunchKernelGGL(k_class_rank, dim3(ng), dim3(1024), 0, ss, p->d_meta.as<GroupMeta>(),
@@ -2176,7 +2311,12 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             if (events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], ss));
             uint32_t* a = nullptr;                        // identity (position order)
             uint32_t* bufs[2] = {p->d_sortA.as<uint32_t>(), p->d_sortB.as<uint32_t>()};
-            for (int ps = 0; ps < passes; ps++) {
+            if (go_order) {
+                int rc0;
+                if ((rc0 = launch_pdq_sort(p, ss, gm, ng, crank, U, nullptr)) != CA_OK) return rc0;
+                a = bufs[0];
+            }
+            for (int ps = 0; ps < passes_run; ps++) {
                 uint32_t* b = bufs[ps & 1];
                 hipLaunchKernelGGL(k_radix_hist, dim3(p->max_rtiles, ng), dim3(RTHREADS), 0, ss, p->d_meta.as<GroupMeta>(),
                                    a, p->d_pod_idx.as<int32_t>(), pcls, crank, U, 8 * ps, p->d_hist.as<int32_t>(), gm);
@@ -2226,10 +2366,28 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             CA_HIP_CHECK(hipGetLastError());
             std::swap(a, b);
         }
+        if (go_order) {
+            // dense ranks from the comparison sort, then sort.Slice's permutation of them
+            hipLaunchKernelGGL(k_item_rank, dim3(G), dim3(1024), 0, st, p->d_meta.as<GroupMeta>(), a,
+                               p->d_item_rank.as<uint32_t>());
+            CA_HIP_CHECK(hipGetLastError());
+            int rc0;
+            if ((rc0 = launch_pdq_sort(p, st, nullptr, G, nullptr, 0, p->d_item_rank.as<uint32_t>())) != CA_OK)
+                return rc0;
+        }
         CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], st));
-        hipLaunchKernelGGL(k_emit_stream, dim3(blocks, G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(), a,
-                           p->d_pod_idx.as<int32_t>(), p->s->t.hot.as<PodHot>(), p->d_stream.as<StreamPod>(),
-                           p->d_spod.as<int32_t>(), p->d_heads.as<uint64_t>());
+        if (go_order) {
+            hipLaunchKernelGGL(k_emit_bucket, dim3(blocks, G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(),
+                               p->d_sortA.as<uint32_t>(), p->d_pod_idx.as<int32_t>(), p->d_tmpl.as<ca_template>(),
+                               p->s->t.hot.as<PodHot>(), p->s->t.spec.as<ca_pod_spec>(),
+                               p->s->t.terms.as<ca_selector_term>(), p->s->t.reqs.as<ca_selector_req>(),
+                               p->d_stream.as<StreamPod>(), p->d_spod.as<int32_t>(), p->d_heads.as<uint64_t>(),
+                               p->d_unsup.as<uint32_t>(), nullptr);
+        } else {
+            hipLaunchKernelGGL(k_emit_stream, dim3(blocks, G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(), a,
+                               p->d_pod_idx.as<int32_t>(), p->s->t.hot.as<PodHot>(), p->d_stream.as<StreamPod>(),
+                               p->d_spod.as<int32_t>(), p->d_heads.as<uint64_t>());
+        }
         CA_HIP_CHECK(hipGetLastError());
     }
     CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_EMIT], st));
@@ -2570,6 +2728,33 @@ int ca_estimate_batch(ca_mirror* m, const ca_podset* s, const int32_t* group_off
     rc = ca_estimate_plan_run(p, limiter, last_index, results, sched_pod, sched_node);
     ca_estimate_plan_destroy(p);
     return rc;
+}
+
+int ca_go_sort_ranks(int32_t device, const uint32_t* ranks, int32_t n, int32_t store, int32_t limit, int32_t* perm) {
+    if (n < 0 || (n > 0 && (!ranks || !perm)) || store < 0 || store > 3) return CA_EINVAL;
+    if (n == 0) return CA_OK;
+    CA_HIP_CHECK(hipSetDevice(device));
+    DevBuf meta, rk, sorted, e, scr, stack;
+    int rc;
+    if ((rc = meta.reserve(sizeof(GroupMeta))) != CA_OK || (rc = rk.reserve(sizeof(uint32_t) * (size_t)n)) != CA_OK ||
+        (rc = sorted.reserve(sizeof(uint32_t) * (size_t)n)) != CA_OK ||
+        (rc = e.reserve(sizeof(uint64_t) * (size_t)n)) != CA_OK || (rc = scr.reserve(sizeof(uint32_t) * (size_t)n)) != CA_OK ||
+        (rc = stack.reserve(sizeof(pdq::Frame) * ((size_t)n / 2 + 4))) != CA_OK)
+        return rc;
+    GroupMeta gm = {};
+    gm.off = 0;
+    gm.count = n;
+    CA_HIP_CHECK(hipMemcpy(meta.ptr, &gm, sizeof(gm), hipMemcpyHostToDevice));
+    CA_HIP_CHECK(hipMemcpy(rk.ptr, ranks, sizeof(uint32_t) * (size_t)n, hipMemcpyHostToDevice));
+    const int32_t lds_n = std::min(n, PDQ_LDS_N);
+    const size_t lds = ((size_t)3 * (size_t)lds_n + 15) & ~(size_t)15;
+    if ((rc = ensure_dyn_lds((const void*)k_pdq_sort, lds)) != CA_OK) return rc;
+    hipLaunchKernelGGL(k_pdq_sort, dim3(1), dim3(pdq::NT), lds, 0, meta.as<GroupMeta>(), nullptr, nullptr, nullptr, 0,
+                       rk.as<uint32_t>(), sorted.as<uint32_t>(), e.as<uint64_t>(), scr.as<uint32_t>(),
+                       stack.as<pdq::Frame>(), lds_n, store, std::max(limit, 0), nullptr);
+    CA_HIP_CHECK(hipGetLastError());
+    CA_HIP_CHECK(hipMemcpy(perm, sorted.ptr, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost));
+    return CA_OK;
 }
 
 #ifdef CASIM_PROF

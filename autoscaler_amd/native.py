@@ -78,6 +78,7 @@ def load() -> C.CDLL:
         "ca_estimate_plan_device_results": ([vp, p(vp)], C.c_int),
         "ca_estimate_plan_stats": ([vp, p(i32), p(C.c_float), p(C.c_float), p(C.c_float)], C.c_int),
         "ca_estimate_plan_chain_info": ([vp, p(i32), p(i32)], C.c_int),
+        "ca_go_sort_ranks": ([i32, vp, i32, i32, i32, vp], C.c_int),
         "ca_estimate_plan_timings": ([vp, p(C.c_float), i32], C.c_int),
         "ca_estimate_plan_group_ticks": ([vp, p(C.c_uint64), i32], C.c_int),
         "ca_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, p(i32), vp, vp], C.c_int),
@@ -148,6 +149,7 @@ def exported_symbols() -> list[str]:
         "ca_estimate_plan_run_u16",
         "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_estimate_plan_timings",
         "ca_estimate_plan_group_ticks", "ca_estimate_plan_fetch", "ca_estimate_plan_device_results",
+        "ca_go_sort_ranks",
         "ca_find_nodes_to_remove",
         "ca_removal_stats", "ca_removal_timings", "ca_removal_plan_create", "ca_removal_plan_run",
         "ca_removal_plan_destroy", "ca_mirror_set_hints", "ca_mirror_get_hints",
@@ -159,6 +161,17 @@ def exported_symbols() -> list[str]:
         "ca_multi_removal_plan_destroy", "ca_multi_find_nodes_to_remove",
         "ca_plan_removals", "ca_plan_last_moves", "ca_plan_stats",
     ]
+
+
+def go_sort_ranks(ranks, store: int = 0, limit: int = 0, device: int = 0) -> np.ndarray:
+    """Go 1.19 sort.Slice of a slice by dense rank on the device (ca_go_sort_ranks): the
+    permutation (perm[k] = input index of the element at position k)."""
+    r = np.ascontiguousarray(ranks, dtype=np.uint32)
+    perm = np.zeros(max(len(r), 1), np.int32)
+    st = load().ca_go_sort_ranks(device, r.ctypes.data, len(r), store, limit, perm.ctypes.data)
+    if st != abi.CA_OK:
+        raise CasimError(st, "go_sort_ranks")
+    return perm[: len(r)]
 
 
 def device_count() -> int:

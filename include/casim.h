@@ -364,13 +364,25 @@ int ca_check_templates(ca_mirror* m, const ca_podset* s, const int32_t* samples,
  * checker does.  Group g's pods are pod_idx[group_off[g] .. group_off[g+1])
  * (indices into the pod set, in the order Estimate receives them).  Outputs:
  * results[g]; sched_pod/sched_node[group_off[g] + i] = i-th scheduled pod (pod set index)
- * and the new-node ordinal it went to (sched_node may be NULL).  Ties of the float64
- * score are broken by position in the group's list (stable order). */
+ * and the new-node ordinal it went to (sched_node may be NULL).  The pods are sorted by
+ * float64 score in Go 1.19 sort.Slice order (binpacking_estimator.go:74: pdqsort_func,
+ * ties included).  CASIM_SORT_ORDER=stable in the environment breaks
+ * ties by list position instead (the round-2 order, kept for A/B measurements). */
 int ca_estimate_batch(ca_mirror* m, const ca_podset* s,
                       const int32_t* group_off, const int32_t* pod_idx,
                       const ca_template* templates, int32_t n_groups,
                       const ca_limiter* limiter, int32_t* last_index,
                       ca_estimate_result* results, int32_t* sched_pod, int32_t* sched_node);
+
+/* Go 1.19 sort.Slice on the device for one slice whose i-th element has dense rank
+ * ranks[i] (less(i, j) == ranks[i] < ranks[j]): perm[k] = input index of the element
+ * sorted to position k — the permutation Estimate's score sort uses.  store selects the
+ * kernel's element store (0 automatic, 1 LDS, 2 32-bit global, 3 64-bit global; a store
+ * that cannot hold the input falls back to automatic).  limit > 0 replaces sort.Slice's
+ * initial recursion limit bits.Len(n) (tests: reaches the heapSort fallback).  For tests
+ * and Go-side checks. */
+int ca_go_sort_ranks(int32_t device, const uint32_t* ranks, int32_t n, int32_t store, int32_t limit,
+                     int32_t* perm);
 
 /* Prepared form for repeated calls (bench): uploads group lists/templates once. */
 typedef struct ca_estimate_plan ca_estimate_plan;

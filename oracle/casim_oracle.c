@@ -71,6 +71,7 @@ static int64_t wrap_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (
 
 or_state* or_create(void) {
     or_state* s = calloc(1, sizeof(or_state));
+    if (s) s->sort_mode = OR_SORT_GO_PDQ;       /* the reference's sort.Slice (binpacking_estimator.go:74) */
     s->next_new_name = -2;
     return s;
 }
@@ -113,9 +114,9 @@ static void scope_count(or_state* s, const ca_pod_spec* p, int sign) {
 
 int or_scope_blockers(const or_state* s) { return (int)s->scope_blockers; }
 
-/* Estimate's sort of the pods by score (binpacking_estimator.go:74): OR_SORT_GO_PDQ is the
- * reference's Go 1.19 sort.Slice (gosort.c), OR_SORT_STABLE breaks score ties by list
- * position (the order the kernels use). */
+/* Estimate's sort of the pods by score (binpacking_estimator.go:74): OR_SORT_GO_PDQ (the
+ * default) is the reference's Go 1.19 sort.Slice (gosort.c), OR_SORT_STABLE breaks score
+ * ties by list position (the device's CASIM_SORT_ORDER=stable knob). */
 int or_set_sort_mode(or_state* s, int32_t mode) {
     if (mode != OR_SORT_STABLE && mode != OR_SORT_GO_PDQ) return CA_EINVAL;
     s->sort_mode = mode;

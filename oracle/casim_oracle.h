@@ -44,6 +44,7 @@ int       or_set_sort_mode(or_state* s, int32_t mode);
 /* gosort.c: sort.Slice(x, less) with less(i, j) = key[i] > key[j]; perm[k] = input index
  * at sorted position k.  go_sort_stats: breakPatterns and heapSort calls so far. */
 void      go_sort_slice_desc(const double* key, int32_t n, int32_t* perm);
+void      go_sort_slice_desc_limit(const double* key, int32_t n, int32_t limit, int32_t* perm);
 void      go_sort_stats(int64_t* out2);
 int       or_fork(or_state* s);
 int       or_revert(or_state* s);

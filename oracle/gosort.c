@@ -247,11 +247,15 @@ static void pdqsort(gs_elem* d, int64_t a, int64_t b, int limit) {
 }
 
 /* sort.Slice(x, less) with less(i, j) = key[i] > key[j] on elements in their input order;
- * perm[k] = input index of the element sorted to position k. */
-void go_sort_slice_desc(const double* key, int32_t n, int32_t* perm) {
+ * perm[k] = input index of the element sorted to position k.  limit > 0 replaces the
+ * initial recursion limit bits.Len(n) (test hook: reaches heapSort). */
+void go_sort_slice_desc_limit(const double* key, int32_t n, int32_t limit, int32_t* perm) {
     gs_elem* d = malloc(sizeof(gs_elem) * (size_t)(n > 0 ? n : 1));
     for (int32_t i = 0; i < n; i++) { d[i].key = key[i]; d[i].idx = i; }
-    pdqsort(d, 0, n, bits_len((uint64_t)n));
+    pdqsort(d, 0, n, limit > 0 ? limit : bits_len((uint64_t)n));
     for (int32_t i = 0; i < n; i++) perm[i] = d[i].idx;
     free(d);
 }
+
+/* sort.Slice itself: the initial limit is bits.Len(n) */
+void go_sort_slice_desc(const double* key, int32_t n, int32_t* perm) { go_sort_slice_desc_limit(key, n, 0, perm); }

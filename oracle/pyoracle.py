@@ -43,6 +43,7 @@ def load() -> C.CDLL:
         "or_scope_blockers": ([vp], C.c_int),
         "or_set_sort_mode": ([vp, i32], C.c_int),
         "go_sort_slice_desc": ([vp, i32, vp], None),
+        "go_sort_slice_desc_limit": ([vp, i32, i32, vp], None),
         "go_sort_stats": ([vp], None),
         "or_fork": ([vp], C.c_int), "or_revert": ([vp], C.c_int), "or_commit": ([vp], C.c_int),
         "or_node_count": ([vp], C.c_int), "or_node_pods": ([vp, i32, vp, i32], C.c_int),
@@ -245,11 +246,12 @@ class OracleState:
         return a.output(li.value, nm.value)
 
 
-def go_sort_desc(keys) -> np.ndarray:
-    """Go 1.19 sort.Slice(x, key[i] > key[j]) (oracle/gosort.c): the permutation."""
+def go_sort_desc(keys, limit: int = 0) -> np.ndarray:
+    """Go 1.19 sort.Slice(x, key[i] > key[j]) (oracle/gosort.c): the permutation.  limit > 0
+    replaces the initial recursion limit bits.Len(n) (reaches the heapSort fallback)."""
     k = np.ascontiguousarray(keys, dtype=np.float64)
     perm = np.zeros(max(len(k), 1), np.int32)
-    load().go_sort_slice_desc(ptr(k), len(k), ptr(perm))
+    load().go_sort_slice_desc_limit(ptr(k), len(k), int(limit), ptr(perm))
     return perm[: len(k)]
 
 

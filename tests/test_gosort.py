@@ -1,14 +1,14 @@
-"""Go 1.19 sort.Slice restatements (oracle/gosort.c, autoscaler_amd/gosort.py) and the
-tie-order gap between the reference's pdqsort and the device's stable order.
+"""Go 1.19 sort.Slice (pdqsort_func) — the order of Estimate's score sort
+(binpacking_estimator.go:74) and FilterOutSchedulable's priority sort
+(filter_out_schedulable.go:97-99).
 
-sort.Slice is Estimate's score sort (binpacking_estimator.go:74) and FilterOutSchedulable's
-priority sort (filter_out_schedulable.go:97-99).  Ties come out in pdqsort order, so:
-  * C2 (ties only between resource-identical pods): counts, lastIndex and every placement
-    decision are the same in both orders; only WHICH of the identical pods fills a slot
-    differs (the scheduled-pod identities);
-  * C4-style ties (same shape, different tolerations / selectors): the orders can place
-    different pods, so the device (stable) result is exact against the stable restatement
-    only — the gap these tests measure.
+* CPU: the C restatement (oracle/gosort.c) and the host one (autoscaler_amd/gosort.py)
+  agree; the oracle's Estimate uses Go order by default.
+* GPU: the device sort (csrc/pdqsort.h through ca_go_sort_ranks) returns exactly the
+  restatement's permutation on every branch — insertion sort, partialInsertionSort,
+  reverseRange, partitionEqual, breakPatterns, the heapSort fallback — and in every element
+  store (LDS, 32-bit and 64-bit global).  Estimate's full-size parity (C2, C4) against the
+  Go-order oracle is in test_gpu_parity.py.
 """
 import numpy as np
 import pytest
@@ -51,31 +51,81 @@ def test_break_patterns_reached():
     assert b1 > b0 and h1 == h0              # breakPatterns yes, heapSort fallback no
 
 
-def _estimate(w, mode):
+def test_limit_hook_reaches_heapsort():
+    """The test hook replacing bits.Len(n) by a small limit drives pdqsort_func into its
+    heapSort fallback (no natural input of this size does); the result is still a sort."""
+    keys = np.random.default_rng(3).integers(0, 40, 3000).astype(float)
+    _, h0 = pyoracle.go_sort_stats()
+    p = pyoracle.go_sort_desc(keys, limit=2)
+    _, h1 = pyoracle.go_sort_stats()
+    assert h1 > h0
+    assert np.all(np.diff(keys[p]) <= 0)
+
+
+def _estimate(w, mode=None):
     o = pyoracle.OracleState()
-    o.set_sort_mode(mode)
+    if mode is not None:
+        o.set_sort_mode(mode)
     W.load_estimate(o, w)
     return o.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, 0)
 
 
-def test_c2_ties_only_change_pod_identity():
+def test_oracle_default_is_go_order():
+    """The oracle's Estimate is the reference's: sort.Slice order unless told otherwise.
+    On C2 the stable order schedules the same shapes slot by slot but other pods of each."""
     w = W.c2(n_pods=3000, n_groups=8, n_existing=40)
-    s, g = _estimate(w, "stable"), _estimate(w, "go")
+    d, g, s = _estimate(w), _estimate(w, "go"), _estimate(w, "stable")
+    assert np.array_equal(d.sched_pod, g.sched_pod) and np.array_equal(d.results, g.results)
     assert np.array_equal(s.results, g.results) and s.last_index == g.last_index
-    assert np.array_equal(s.sched_node, g.sched_node)
     shape = lambda ids: [(int(w.table.pods[i]["req_milli_cpu"]), int(w.table.pods[i]["req_memory"])) for i in ids]
-    assert shape(s.sched_pod) == shape(g.sched_pod)          # the same shapes, slot by slot
-    assert not np.array_equal(s.sched_pod, g.sched_pod)      # ... but other pods of each shape
+    assert shape(s.sched_pod) == shape(g.sched_pod)
+    assert not np.array_equal(s.sched_pod, g.sched_pod)
 
 
-def test_c4_tie_gap_measured():
-    """C4 ties are between pods that differ in tolerations / selectors: the two orders can
-    schedule different pods; the device is pinned to the stable restatement (H2)."""
-    w = W.c4(n_pods=5000, n_groups=12, n_existing=100)
-    s, g = _estimate(w, "stable"), _estimate(w, "go")
-    order_diff = int((s.sched_pod != g.sched_pod).sum())
-    assert order_diff > 0
-    sets_diff = sum(set(s.sched_pod[a:b].tolist()) != set(g.sched_pod[a:b].tolist())
-                    for a, b in zip(w.group_off[:-1], w.group_off[1:]))
-    print(f"C4 tie gap: {order_diff} output slots, {sets_diff} groups with different pod sets, "
-          f"count changes {int((s.results['node_count'] != g.results['node_count']).sum())}")
+def _rank_cases():
+    """(ranks, limit) covering the branches of pdqsort_func at workgroup and wave sizes."""
+    rng = np.random.default_rng(11)
+    cases = []
+    for n in (0, 1, 2, 5, 12, 13, 49, 50, 51, 200, 511, 512, 513, 700, 2000, 5000, 20000, 52736, 60000):
+        for nk in (1, 2, 7, 64, 250, 4000):
+            cases.append((rng.integers(0, nk, n), 0))
+    for n in (600, 3000, 40000):
+        k = rng.integers(0, 50, n)
+        cases += [(np.sort(k), 0), (np.sort(k)[::-1].copy(), 0), (np.repeat(rng.integers(0, 60, n // 100 + 1), 100)[:n], 0)]
+        s = np.sort(k)
+        s[rng.integers(0, n, 4)] = rng.integers(0, 50, 4)        # nearly sorted: partialInsertionSort shifts
+        cases.append((s, 0))
+        cases.append((np.arange(n)[::-1] % 300, 0))              # decreasing runs: reverseRange
+        cases.append((k, 2))                                      # heapSort fallback
+    cases.append((rng.integers(0, 5000, 30000), 3))
+    cases.append((rng.integers(0, 100000, 70000), 0))            # > 4096 ranks: 64-bit store
+    return cases
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("store", [0, 1, 2, 3])
+def test_device_go_sort_matches_oracle(store):
+    from autoscaler_amd import native
+    for i, (ranks, limit) in enumerate(_rank_cases()):
+        ranks = np.asarray(ranks, dtype=np.int64)
+        want = pyoracle.go_sort_desc(-ranks.astype(np.float64), limit=limit)
+        got = native.go_sort_ranks(ranks.astype(np.uint32), store=store, limit=limit)
+        assert np.array_equal(want, got), (store, i, len(ranks), limit)
+
+
+@pytest.mark.gpu
+def test_device_go_sort_c2_c4_keys():
+    """The exact rank sequences Estimate sorts on C2 and C4 (64 score classes, runs of 100
+    identical pods per controller) for a few groups."""
+    from autoscaler_amd import native
+    for w in (W.c2(), W.c4(n_pods=20000, n_groups=6, n_existing=50)):
+        p = w.table.pods
+        for g in range(0, len(w.templates), max(1, len(w.templates) // 6)):
+            idx = w.pod_idx[w.group_off[g]:w.group_off[g + 1]]
+            ac = float(w.templates[g]["node"]["alloc_milli_cpu"])
+            am = float(w.templates[g]["node"]["alloc_memory"])
+            score = p["score_milli_cpu"][idx] / ac + p["score_memory"][idx] / am
+            ranks = np.unique(-score, return_inverse=True)[1].astype(np.uint32)
+            want = pyoracle.go_sort_desc(score)
+            for store in (0, 2):
+                assert np.array_equal(want, native.go_sort_ranks(ranks, store=store)), (w.name, g, store)

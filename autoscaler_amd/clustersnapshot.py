@@ -83,7 +83,8 @@ class ClusterSnapshot:
     # -- encoding / replay ------------------------------------------------------
     def _sizes(self):
         i = self.interner
-        return (len(i.taints), len(i.pairs), len(i.keys), len(i.int_keys), len(i.ports), len(i.scalars))
+        return tuple((len(u), len(u.overflow)) for u in (i.taints, i.pairs, i.keys, i.int_keys, i.ports, i.scalars)) + \
+            (len(i.port_groups_over),)
 
     def ensure(self, nodes=(), pods=(), templates=()) -> None:
         """Intern new objects; re-encode and replay when a universe grew."""

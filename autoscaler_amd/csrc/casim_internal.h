@@ -199,6 +199,7 @@ __host__ __device__ inline uint32_t dev_fit_reasons(int64_t pcpu, int64_t pmem, 
     } while (0)
 
 void set_last_error(const std::string& s);
+const std::string& last_error();
 
 // hipFuncAttributeMaxDynamicSharedMemorySize of a kernel, raised to `bytes` at most once
 // per (device, kernel) and size: the call costs tens of microseconds, too much per launch.

@@ -461,7 +461,13 @@ __global__ void __launch_bounds__(RTHREADS) k_radix_scatter(const GroupMeta* __r
 // memory (rank above position in 32 or 64 bits).  Output: sorted[off + k] = position of
 // the k-th pod, the same layout as the radix sort's.  force (tests): 1 LDS, 2 / 3 global.
 // Scratch per group: gE [off, off+n) (8 B), scr [off, off+n), stack from off/2 + 2g.
-constexpr int PDQ_LDS_N = 52736;       // 3 B per pod + the static control block < 160 KB
+constexpr int PDQ_LDS_N = 50368;       // ~3.16 B per pod + the static control block (~4.6 KB) <= 160 KB
+// dynamic LDS of k_pdq_sort for groups of up to lds_n pods: positions (2 B), ranks (1 B),
+// the partition's right-zone bitmap (1 bit) and its per-word prefix counts (2 B / 64)
+__host__ __device__ inline size_t pdq_lds_bytes(int32_t lds_n) {
+    const size_t np = ((size_t)std::max(lds_n, 0) + 63) & ~(size_t)63;
+    return (3 * np + np / 8 + 2 * (np / 64 + 1) + 15) & ~(size_t)15;
+}
 
 __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restrict__ groups,
                                                      const int32_t* __restrict__ pod_idx,
@@ -469,7 +475,7 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
                                                      const int32_t* __restrict__ crank, int32_t U,
                                                      const uint32_t* __restrict__ item_rank,
                                                      uint32_t* __restrict__ sorted, uint64_t* __restrict__ gE,
-                                                     uint32_t* __restrict__ scr_all, pdq::Frame* __restrict__ stack_all,
+                                                     uint64_t* __restrict__ xs_all, pdq::Frame* __restrict__ stack_all,
                                                      int32_t lds_n, int32_t force, int32_t limit0, const int32_t* __restrict__ gmap) {
     extern __shared__ __align__(16) unsigned char pdq_dyn[];
     __shared__ pdq::Ctl ctl;
@@ -477,13 +483,16 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
     const GroupMeta gm = groups[gi];
     const int32_t n = gm.count, off = gm.off;
     const int tid = threadIdx.x;
-    uint32_t* scr = scr_all + off;
+    uint32_t* scr = reinterpret_cast<uint32_t*>(xs_all + off);    // ranks, then the exchange scratch
     pdq::Frame* stack = stack_all + off / 2 + 2 * gi;
     if (tid == 0) ctl.rmax = 0;
     __syncthreads();
     const bool fit = n <= lds_n;
+    const size_t npad = ((size_t)lds_n + 63) & ~(size_t)63;
     uint16_t* e16 = reinterpret_cast<uint16_t*>(pdq_dyn);
-    uint8_t* rk = pdq_dyn + 2 * (size_t)lds_n;
+    uint8_t* rk = pdq_dyn + 2 * npad;
+    uint64_t* rmb = reinterpret_cast<uint64_t*>(pdq_dyn + 3 * npad);
+    uint16_t* rmp = reinterpret_cast<uint16_t*>(rmb + npad / 64);
     uint32_t rmax = 0;
     for (int32_t i = tid; i < n; i += pdq::NT) {
         const uint32_t r = item_rank ? item_rank[off + i] : (uint32_t)crank[(size_t)gi * U + pcls[pod_idx[off + i]]];
@@ -500,22 +509,22 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
     else if (force == 2 && n <= (1 << 20) && R < 4096) mode = 2;
     else if (force == 3) mode = 3;
     if (mode == 1) {
-        const pdq::LdsStore st{e16, rk};
-        pdq::wg_sort(st, n, stack, scr, ctl, limit0);
+        const pdq::LdsStore st{e16, rk, rmb, rmp};
+        pdq::wg_sort(st, n, stack, n / 2 + 2, scr, ctl, limit0);
         for (int32_t k = tid; k < n; k += pdq::NT) sorted[off + k] = e16[k];
     } else if (mode == 2) {
         uint32_t* e = reinterpret_cast<uint32_t*>(gE + off);
         for (int32_t i = tid; i < n; i += pdq::NT) e[i] = (scr[i] << 20) | (uint32_t)i;
         __syncthreads();
         const pdq::G32Store st{e};
-        pdq::wg_sort(st, n, stack, scr, ctl, limit0);
+        pdq::wg_sort(st, n, stack, n / 2 + 2, scr, ctl, limit0);
         for (int32_t k = tid; k < n; k += pdq::NT) sorted[off + k] = e[k] & 0xFFFFFu;
     } else {
         uint64_t* e = gE + off;
         for (int32_t i = tid; i < n; i += pdq::NT) e[i] = ((uint64_t)scr[i] << 32) | (uint32_t)i;
         __syncthreads();
         const pdq::G64Store st{e};
-        pdq::wg_sort(st, n, stack, scr, ctl, limit0);
+        pdq::wg_sort(st, n, stack, n / 2 + 2, xs_all + off, ctl, limit0);
         for (int32_t k = tid; k < n; k += pdq::NT) sorted[off + k] = (uint32_t)e[k];
     }
 }
@@ -2077,7 +2086,7 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
         if ((rc = p->d_hist.reserve(sizeof(int32_t) * (size_t)std::max(p->n_hist, 1))) != CA_OK) return rc;
     }
     if ((rc = p->d_pdq_e.reserve(sizeof(uint64_t) * tot)) != CA_OK) return rc;
-    if ((rc = p->d_pdq_scr.reserve(sizeof(uint32_t) * tot)) != CA_OK) return rc;
+    if ((rc = p->d_pdq_scr.reserve(sizeof(uint64_t) * tot)) != CA_OK) return rc;
     if ((rc = p->d_pdq_stack.reserve(sizeof(pdq::Frame) * (tot / 2 + 2 * (size_t)std::max(G, 1) + 2))) != CA_OK)
         return rc;
     if (!p->bucket && (rc = p->d_item_rank.reserve(sizeof(uint32_t) * tot)) != CA_OK) return rc;
@@ -2133,12 +2142,12 @@ bool go_sort_order() {
 int launch_pdq_sort(ca_estimate_plan* p, hipStream_t ss, const int32_t* gm, int32_t ng, const int32_t* crank,
                     int32_t U, const uint32_t* item_rank, int32_t force = 0) {
     const int32_t lds_n = std::min(p->max_count, PDQ_LDS_N);
-    const size_t lds = ((size_t)3 * (size_t)std::max(lds_n, 0) + 15) & ~(size_t)15;
+    const size_t lds = pdq_lds_bytes(lds_n);
     int rc;
     if ((rc = ensure_dyn_lds((const void*)k_pdq_sort, lds)) != CA_OK) return rc;
     hipLaunchKernelGGL(k_pdq_sort, dim3(ng), dim3(pdq::NT), lds, ss, p->d_meta.as<GroupMeta>(),
                        p->d_pod_idx.as<int32_t>(), p->s ? p->s->d_cls.as<int32_t>() : nullptr, crank, U, item_rank,
-                       p->d_sortA.as<uint32_t>(), p->d_pdq_e.as<uint64_t>(), p->d_pdq_scr.as<uint32_t>(),
+                       p->d_sortA.as<uint32_t>(), p->d_pdq_e.as<uint64_t>(), p->d_pdq_scr.as<uint64_t>(),
                        p->d_pdq_stack.as<pdq::Frame>(), lds_n, force, 0, gm);
     CA_HIP_CHECK(hipGetLastError());
     return CA_OK;
@@ -2738,7 +2747,7 @@ int ca_go_sort_ranks(int32_t device, const uint32_t* ranks, int32_t n, int32_t s
     int rc;
     if ((rc = meta.reserve(sizeof(GroupMeta))) != CA_OK || (rc = rk.reserve(sizeof(uint32_t) * (size_t)n)) != CA_OK ||
         (rc = sorted.reserve(sizeof(uint32_t) * (size_t)n)) != CA_OK ||
-        (rc = e.reserve(sizeof(uint64_t) * (size_t)n)) != CA_OK || (rc = scr.reserve(sizeof(uint32_t) * (size_t)n)) != CA_OK ||
+        (rc = e.reserve(sizeof(uint64_t) * (size_t)n)) != CA_OK || (rc = scr.reserve(sizeof(uint64_t) * (size_t)n)) != CA_OK ||
         (rc = stack.reserve(sizeof(pdq::Frame) * ((size_t)n / 2 + 4))) != CA_OK)
         return rc;
     GroupMeta gm = {};
@@ -2747,10 +2756,10 @@ int ca_go_sort_ranks(int32_t device, const uint32_t* ranks, int32_t n, int32_t s
     CA_HIP_CHECK(hipMemcpy(meta.ptr, &gm, sizeof(gm), hipMemcpyHostToDevice));
     CA_HIP_CHECK(hipMemcpy(rk.ptr, ranks, sizeof(uint32_t) * (size_t)n, hipMemcpyHostToDevice));
     const int32_t lds_n = std::min(n, PDQ_LDS_N);
-    const size_t lds = ((size_t)3 * (size_t)lds_n + 15) & ~(size_t)15;
+    const size_t lds = pdq_lds_bytes(lds_n);
     if ((rc = ensure_dyn_lds((const void*)k_pdq_sort, lds)) != CA_OK) return rc;
     hipLaunchKernelGGL(k_pdq_sort, dim3(1), dim3(pdq::NT), lds, 0, meta.as<GroupMeta>(), nullptr, nullptr, nullptr, 0,
-                       rk.as<uint32_t>(), sorted.as<uint32_t>(), e.as<uint64_t>(), scr.as<uint32_t>(),
+                       rk.as<uint32_t>(), sorted.as<uint32_t>(), e.as<uint64_t>(), scr.as<uint64_t>(),
                        stack.as<pdq::Frame>(), lds_n, store, std::max(limit, 0), nullptr);
     CA_HIP_CHECK(hipGetLastError());
     CA_HIP_CHECK(hipMemcpy(perm, sorted.ptr, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost));
@@ -2758,6 +2767,15 @@ int ca_go_sort_ranks(int32_t device, const uint32_t* ranks, int32_t n, int32_t s
 }
 
 #ifdef CASIM_PROF
+int ca_debug_pdq_prof(uint64_t* out, int32_t reset) {
+    CA_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(pdq::g_pdq_prof), sizeof(uint64_t) * 32));
+    if (reset) {
+        static const uint64_t z[32] = {};
+        CA_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(pdq::g_pdq_prof), z, sizeof z));
+    }
+    return CA_OK;
+}
+
 int ca_debug_chain_prof(uint64_t* out, int32_t n_groups) {
     if (n_groups > 1024) n_groups = 1024;
     CA_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_prof), sizeof(uint64_t) * NPROF * (size_t)n_groups));

@@ -59,6 +59,7 @@ struct SweepScratch {
     // serial-only calls (sweep_core): the next call's mode and the measured ms per candidate
     bool serial_next = false;
     int32_t serial_calls = 0;
+    int32_t serial_C = 0, serial_S = 0;     // shape of the call that decided serial_next
     float serial_ms_per = 0, pipe_ms_per = 0;
     ~SweepScratch() {
         if (gexec) (void)hipGraphExecDestroy(gexec);
@@ -151,7 +152,8 @@ struct ca_mirror {
     int ensure_pod_hints();                // grow to pods.size(), new entries -1
     int64_t n_ext_pods = 0;                // pods stored with host ports / extended requests
 
-    int remap_hints_removed(int32_t pos, bool restore);   // resident hints around a RemoveNode
+    int remap_hints_removed(int32_t pos, int32_t code, bool restore);   // resident hints around a RemoveNode
+    int32_t removals = 0;                  // RemoveNode calls so far: hint codes of removed nodes
     int sync_nodes();                      // push dirty rows to the device
     int sync_pods();                       // push new pod records to the device
     void mark_dirty(int32_t node);

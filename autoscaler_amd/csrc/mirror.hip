@@ -18,6 +18,7 @@ namespace casim {
 
 static thread_local std::string g_last_error;
 void set_last_error(const std::string& s) { g_last_error = s; }
+const std::string& last_error() { return g_last_error; }
 
 int ensure_dyn_lds(const void* kernel, size_t bytes) {
     static std::mutex mu;
@@ -75,6 +76,13 @@ BlockCache& dev_cache() {
     return *c;
 }
 BlockCache& host_cache() {
+    static BlockCache* c = [] { auto* b = new BlockCache(); b->cap = 1ull << 30; return b; }();
+    return *c;
+}
+// caller blocks (ca_host_alloc / ca_host_free) have a cache of their own: a block a caller
+// freed while it still holds views of it can then never alias the library's staging
+// buffers
+BlockCache& caller_cache() {
     static BlockCache* c = [] { auto* b = new BlockCache(); b->cap = 1ull << 30; return b; }();
     return *c;
 }
@@ -254,21 +262,21 @@ __global__ void k_scatter_rows(const StagedRow* __restrict__ rows, int32_t k, No
 }
 
 // Resident hints around RemoveNode(pos) (positions after it shift down by one).  A hint
-// to the removed node is kept as -2 - pos (no usable hint: kernels read h >= 0 only) so a
-// Revert of the enclosing fork restores it: the reference keeps hints by node NAME
+// to the removed node is kept as code = -2 - serial, where serial numbers the mirror's
+// RemoveNode calls (no usable hint: kernels read h >= 0 only), so the Revert of that very
+// removal restores it — two removals at the same position (node p, then the node that
+// shifted into p) keep distinct codes.  The reference keeps hints by node NAME
 // (hints.go:29-72) outside the snapshot, and the name is valid again after the Revert.
-__global__ void k_remap_hints(int32_t* __restrict__ h, int32_t n, int32_t pos, int32_t restore) {
+__global__ void k_remap_hints(int32_t* __restrict__ h, int32_t n, int32_t pos, int32_t code, int32_t restore) {
     const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (i >= n) return;
     int32_t v = h[i];
     if (!restore) {
-        if (v == pos) v = -2 - pos;
+        if (v == pos) v = code;
         else if (v > pos) v--;
-        else if (v <= -2 && -2 - v > pos) v++;      // an older removal's encoded position
     } else {
-        if (v == -2 - pos) v = pos;
+        if (v == code) v = pos;
         else if (v >= pos) v++;
-        else if (v <= -2 && -2 - v >= pos) v--;
     }
     h[i] = v;
 }
@@ -388,10 +396,10 @@ void ca_mirror::fill_static(int32_t i, NodeStatic& s) const {
     s.name_id = n.name_id;
 }
 
-int ca_mirror::remap_hints_removed(int32_t pos, bool restore) {
+int ca_mirror::remap_hints_removed(int32_t pos, int32_t code, bool restore) {
     if (d_hints_n == 0) return CA_OK;
     hipLaunchKernelGGL(k_remap_hints, dim3((unsigned)((d_hints_n + 255) / 256)), dim3(256), 0, stream,
-                       d_pod_hints.as<int32_t>(), (int32_t)d_hints_n, pos, restore ? 1 : 0);
+                       d_pod_hints.as<int32_t>(), (int32_t)d_hints_n, pos, code, restore ? 1 : 0);
     CA_HIP_CHECK(hipGetLastError());
     return CA_OK;
 }
@@ -637,24 +645,30 @@ int ca_device_count(int32_t* out) {
     return CA_OK;
 }
 
-// Page-locked blocks handed to callers come from the same cache as the library's own
-// (HostBuf): a caller that allocates its result buffers per call pays no hipHostMalloc
-// after the first.  The block sizes are remembered for ca_host_free.
+// Page-locked blocks handed to callers are cached too (a caller that allocates its result
+// buffers per call pays no hipHostMalloc after the first), in a cache separate from the
+// library's own staging buffers (HostBuf).  The block sizes are remembered for ca_host_free.
 static std::mutex g_host_mu;
 static std::unordered_map<void*, size_t>* g_host_sizes = new std::unordered_map<void*, size_t>();   // leaked on purpose
 
 int ca_host_alloc(size_t bytes, void** out) {
     if (!out) return CA_EINVAL;
     *out = nullptr;
-    HostBuf b;
-    if (b.reserve(bytes ? bytes : 1) != CA_OK) return CA_EDEVICE;
+    const size_t want = bytes ? bytes : 1;
+    size_t got = 0;
+    void* p = no_cache() ? nullptr : caller_cache().take(want, -1, got);
+    if (!p) {
+        got = std::max<size_t>(want, 4096);
+        if (hipHostMalloc(&p, got, hipHostMallocNonCoherent) != hipSuccess) {
+            set_last_error("hipHostMalloc failed");
+            return CA_EDEVICE;
+        }
+    }
     {
         std::lock_guard<std::mutex> lock(g_host_mu);
-        (*g_host_sizes)[b.ptr] = b.bytes;
+        (*g_host_sizes)[p] = got;
     }
-    *out = b.ptr;
-    b.ptr = nullptr;                    // owned by the caller now
-    b.bytes = 0;
+    *out = p;
     return CA_OK;
 }
 
@@ -668,10 +682,12 @@ int ca_host_free(void* p) {
         sz = it->second;
         g_host_sizes->erase(it);
     }
-    HostBuf b;                          // released through the cache
-    b.ptr = p;
-    b.bytes = sz;
-    b.release();
+    bool kept = false;                  // released through the callers' cache
+    if (!no_cache()) {
+        sync_device(-1);
+        kept = caller_cache().give(sz, -1, p);
+    }
+    if (!kept) (void)hipHostFree(p);
     return CA_OK;
 }
 
@@ -823,12 +839,13 @@ int ca_mirror_remove_node(ca_mirror* m, int32_t node_pos) {
     m->all_dirty = true;
     m->static_dirty = true;
     if (m->d_rows > m->nodes.size()) m->d_rows = m->nodes.size();
-    int rc = m->remap_hints_removed(node_pos, false);
+    const int32_t code = -2 - (m->removals++ & 0x3FFFFFFF);     // this removal's hint code
+    int rc = m->remap_hints_removed(node_pos, code, false);
     if (rc != CA_OK) return rc;
     if (m->depth > 0) {
         JournalEntry e;
         std::memset(&e, 0, sizeof e);
-        e.kind = J_REMOVE_NODE; e.node = node_pos; e.pod = -1; e.slot = (int32_t)m->removed_nodes.size();
+        e.kind = J_REMOVE_NODE; e.node = node_pos; e.pod = code; e.slot = (int32_t)m->removed_nodes.size();
         m->journal.push_back(e);
         m->removed_nodes.push_back(std::move(row));
     }
@@ -888,7 +905,7 @@ int ca_mirror_revert(ca_mirror* m) {
             m->dirty_flag.assign(m->nodes.size(), 0);
             m->all_dirty = true;
             m->static_dirty = true;
-            int rc = m->remap_hints_removed(pos, true);
+            int rc = m->remap_hints_removed(pos, e.pod, true);
             if (rc != CA_OK) return rc;
         }
     }

@@ -16,8 +16,8 @@
 //     partitionEqual test, a final pivot or equal-zone element no later step moves), so
 //     every pending range (a, b, limit, wasBalanced, wasPartitioned) can run at once and
 //     in any order.  A workgroup step runs one pdqsort_func loop iteration of up to MAXF
-//     frames together; frames of at most WAVE_SMALL elements are sorted to the end by one
-//     wavefront each.
+//     frames longer than T_SMALL together; shorter frames wait, then are sorted to the
+//     end by one wavefront each, claimed in turn (no workgroup barrier).
 //   * Partition as a rank-paired exchange.  partition_func / partitionEqual_func are
 //     Hoare scans over [a+1, b-1] against the pivot moved to a: with m = #{pred}, the
 //     k-th element of [a+1, a+m] failing pred (from the left) is swapped with the k-th
@@ -34,14 +34,30 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <climits>
 
 namespace casim {
 namespace pdq {
 
+#ifdef CASIM_PROF    // phase cycle counters of workgroup 0 (profiling build: ca_debug_pdq_prof)
+__device__ unsigned long long g_pdq_prof[32];
+#define PDQ_T(v) const uint64_t v = clock64()
+#define PDQ_ADD(i, t) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_pdq_prof[i] += clock64() - (t); } while (0)
+#define PDQ_CNT(i, n) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_pdq_prof[i] += (n); } while (0)
+#define PDQ_WADD(i, t) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) atomicAdd(&g_pdq_prof[i], clock64() - (t)); } while (0)
+// sum over steps of the slowest wave's duration: per-step maxima accumulate in slot i+32
+#define PDQ_WMAX(i, t) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) atomicAdd(&g_pdq_prof[i], clock64() - (t)); } while (0)
+#else
+#define PDQ_WADD(i, t) (void)0
+#define PDQ_WMAX(i, t) (void)0
+#define PDQ_T(v) (void)0
+#define PDQ_ADD(i, t) (void)0
+#define PDQ_CNT(i, n) (void)0
+#endif
+
 constexpr int NT = 1024;             // threads of the workgroup
 constexpr int NW = NT / 64;          // wavefronts
-constexpr int MAXF = 128;            // frames per workgroup step
-constexpr int WAVE_SMALL = 512;      // frames up to this length: one wavefront sorts them to the end
+constexpr int MAXF = 96;             // frames per workgroup step
 constexpr int MAX_INSERTION = 12;    // pdqsort_func maxInsertion
 enum { HINT_UNKNOWN = 0, HINT_INC = 1, HINT_DEC = 2 };
 enum { OP_DONE = 0, OP_PART = 1, OP_EQ = 2 };
@@ -53,14 +69,18 @@ __device__ inline int32_t lf_pack(int limit, bool wb, bool wp) { return limit | 
 __device__ inline int bits_len(uint32_t x) { return x ? 32 - __clz((int)x) : 0; }
 
 // Element stores.  An element is a position of the group's pod list; key() is its rank.
-// LDS: 16-bit positions + an 8-bit rank per position (groups of <= ~52k pods, <= 256
-// ranks — C2 / C4).  Global: the rank packed above the position (32 or 64 bits).
+// LDS: 16-bit positions + the 8-bit rank of the element at each index, the two arrays
+// moved together (groups of <= PDQ_LDS_N pods, <= 256 ranks — C2 / C4): a comparison is
+// one byte load.  Global: the rank packed above the position (32 or 64 bits).
 struct LdsStore {
     using Elem = uint32_t;
     uint16_t* e;
-    const uint8_t* rk;
-    __device__ Elem ld(int i) const { const uint32_t p = e[i]; return ((uint32_t)rk[p] << 16) | p; }
-    __device__ void st(int i, Elem v) const { e[i] = (uint16_t)v; }
+    uint8_t* rk;
+    uint64_t* rmb;           // workgroup partition: right-zone pass bits per 64-position word
+    uint16_t* rmp;           //   and their exclusive prefix counts per word
+    __device__ Elem ld(int i) const { return ((uint32_t)rk[i] << 16) | e[i]; }
+    __device__ void st(int i, Elem v) const { e[i] = (uint16_t)v; rk[i] = (uint8_t)(v >> 16); }
+    __device__ uint32_t key_at(int i) const { return rk[i]; }
     __device__ static uint32_t key(Elem v) { return v >> 16; }
     __device__ static uint32_t pos(Elem v) { return v & 0xFFFFu; }
 };
@@ -69,6 +89,7 @@ struct G32Store {   // rank < 4096, position < 2^20
     uint32_t* e;
     __device__ Elem ld(int i) const { return e[i]; }
     __device__ void st(int i, Elem v) const { e[i] = v; }
+    __device__ uint32_t key_at(int i) const { return e[i] >> 20; }
     __device__ static uint32_t key(Elem v) { return v >> 20; }
     __device__ static uint32_t pos(Elem v) { return v & 0xFFFFFu; }
 };
@@ -77,11 +98,12 @@ struct G64Store {
     uint64_t* e;
     __device__ Elem ld(int i) const { return e[i]; }
     __device__ void st(int i, Elem v) const { e[i] = v; }
+    __device__ uint32_t key_at(int i) const { return (uint32_t)(e[i] >> 32); }
     __device__ static uint32_t key(Elem v) { return (uint32_t)(v >> 32); }
     __device__ static uint32_t pos(Elem v) { return (uint32_t)v; }
 };
 
-template <class S> __device__ inline uint32_t K(const S& s, int i) { return S::key(s.ld(i)); }
+template <class S> __device__ inline uint32_t K(const S& s, int i) { return s.key_at(i); }
 template <class S> __device__ inline void swp(const S& s, int i, int j) {
     const typename S::Elem x = s.ld(i), y = s.ld(j);
     s.st(i, y);
@@ -224,23 +246,37 @@ template <class S> __device__ int w_find_descent(const S& s, int i, int b) {
 // shift [lo, hi] one place right (to [lo+1, hi+1]) / left (to [lo-1, hi-1])
 template <class S> __device__ void w_shift_right(const S& s, int lo, int hi) {
     const int lane = threadIdx.x & 63;
-    for (int top = hi; top >= lo; top -= 64) {                      // right to left
-        const int p = top - lane;
-        typename S::Elem v = 0;
-        if (p >= lo) v = s.ld(p);
+    for (int top = hi; top >= lo; top -= 256) {                     // right to left, 256 per step
+        typename S::Elem v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int p = top - u * 64 - lane;
+            v[u] = p >= lo ? s.ld(p) : 0;
+        }
         wfence();
-        if (p >= lo) s.st(p + 1, v);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int p = top - u * 64 - lane;
+            if (p >= lo) s.st(p + 1, v[u]);
+        }
         wfence();
     }
 }
 template <class S> __device__ void w_shift_left(const S& s, int lo, int hi) {
     const int lane = threadIdx.x & 63;
-    for (int bot = lo; bot <= hi; bot += 64) {                      // left to right
-        const int p = bot + lane;
-        typename S::Elem v = 0;
-        if (p <= hi) v = s.ld(p);
+    for (int bot = lo; bot <= hi; bot += 256) {                     // left to right, 256 per step
+        typename S::Elem v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int p = bot + u * 64 + lane;
+            v[u] = p <= hi ? s.ld(p) : 0;
+        }
         wfence();
-        if (p <= hi) s.st(p - 1, v);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int p = bot + u * 64 + lane;
+            if (p <= hi) s.st(p - 1, v[u]);
+        }
         wfence();
     }
 }
@@ -263,10 +299,16 @@ template <class S> __device__ bool w_partial_insertion(const S& s, int a, int b)
             const int qmin = a > 0 ? a - 1 : 0;   // key(a-1) <= every key of [a, b): the walk stops there
             int land = 0;
             bool found = false;
-            for (int top = i - 2; top >= qmin && !found; top -= 64) {
-                const int q = top - lane;
-                const uint64_t m = __ballot(q >= qmin && K(s, q) <= ke);
-                if (m) { land = top - (int)__builtin_ctzll(m) + 1; found = true; }
+            for (int top = i - 2; top >= qmin && !found; top -= 256) {   // 256 positions per step
+                uint64_t m[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int q = top - u * 64 - lane;
+                    m[u] = __ballot(q >= qmin && K(s, q) <= ke);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (!found && m[u]) { land = top - u * 64 - (int)__builtin_ctzll(m[u]) + 1; found = true; }
             }
             if (!found) land = qmin == 0 ? 0 : qmin;   // (qmin == a-1 always stops: never reached)
             if (land < i - 1) {
@@ -280,10 +322,17 @@ template <class S> __device__ bool w_partial_insertion(const S& s, int a, int b)
             const typename S::Elem f = s.ld(i);
             const uint32_t kf = S::key(f);
             int land = b - 1;
-            for (int bot = i + 1; bot < b; bot += 64) {
-                const int j = bot + lane;
-                const uint64_t m = __ballot(j < b && !(K(s, j) < kf));
-                if (m) { land = bot + (int)__builtin_ctzll(m) - 1; break; }
+            bool found = false;
+            for (int bot = i + 1; bot < b && !found; bot += 256) {        // 256 positions per step
+                uint64_t m[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int j = bot + u * 64 + lane;
+                    m[u] = __ballot(j < b && !(K(s, j) < kf));
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (!found && m[u]) { land = bot + u * 64 + (int)__builtin_ctzll(m[u]) - 1; found = true; }
             }
             if (land > i) {
                 w_shift_left(s, i + 1, land);
@@ -295,42 +344,69 @@ template <class S> __device__ bool w_partial_insertion(const S& s, int a, int b)
     return false;
 }
 
+// position of the k-th set bit (0-based) of m
+__device__ inline int select_bit(uint64_t m, int k) {
+    int pos = 0;
+    for (int w = 32; w >= 1; w >>= 1) {
+        const int c = __builtin_popcountll((m >> pos) & ((1ull << w) - 1));
+        if (k >= c) { k -= c; pos += w; }
+    }
+    return pos;
+}
+
 // partition_func (eq = 0) / partitionEqual_func (eq = 1) on [a, b) whose pivot (key pk)
-// is already at a: the rank-paired exchange.  scr[a .. b) is the frame's own scratch.
-// Returns m = #pred over [a+1, b-1] and t = #pairs swapped.
-template <class S> __device__ void w_exchange(const S& s, int a, int b, uint32_t pk, int eq, uint32_t* __restrict__ scr,
-                                            int* m_out, int* t_out) {
+// is already at a: the rank-paired exchange, by one wavefront with no memory round trip.
+// m = #pred over [a+1, b-1] (four 64-position windows per step); then a merge walks the
+// left zone [a+1, a+m] upward and the right zone [a+m+1, b-1] downward one window each:
+// the k-th failing element of the left window pairs with the k-th passing element of the
+// right window (lane order = descending positions there), the pair is swapped through
+// registers (ds_bpermute), and each window moves past what it consumed.
+// Returns m and t = #pairs.
+template <class S> __device__ void w_exchange(const S& s, int a, int b, uint32_t pk, int eq, int* m_out, int* t_out) {
     const int lane = threadIdx.x & 63;
     const uint64_t below = lanes_below();
-    auto pred = [&](int p) { const uint32_t k = K(s, p); return eq ? k <= pk : k < pk; };
+    auto predk = [&](uint32_t k) { return eq ? k <= pk : k < pk; };
     int m = 0;
-    for (int base = a + 1; base < b; base += 64) {
-        const int p = base + lane;
-        m += __builtin_popcountll(__ballot(p < b && pred(p)));
+    for (int base = a + 1; base < b; base += 256) {
+        uint64_t mk[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int p = base + u * 64 + lane;
+            mk[u] = __ballot(p < b && predk(K(s, p)));
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) m += __builtin_popcountll(mk[u]);
     }
-    const int z = a + m, c0 = (b - a + 1) / 2;
-    int t = 0;
-    for (int base = a + 1; base <= z; base += 64) {                 // left zone: the k-th failing pred
-        const int p = base + lane;
-        const bool f = p <= z && !pred(p);
-        const uint64_t mk = __ballot(f);
-        if (f) scr[a + t + __builtin_popcountll(mk & below)] = (uint32_t)p;
-        t += __builtin_popcountll(mk);
+    const int z = a + m;
+    int lpos = a + 1, rpos = b - 1, t = 0;
+    while (lpos <= z && rpos > z) {
+        const int pl = lpos + lane, pr = rpos - lane;
+        typename S::Elem vl = 0, vr = 0;
+        bool fl = false, fr = false;
+        if (pl <= z) { vl = s.ld(pl); fl = !predk(S::key(vl)); }
+        if (pr > z) { vr = s.ld(pr); fr = predk(S::key(vr)); }
+        const uint64_t ml = __ballot(fl), mr = __ballot(fr);
+        const int nl = __builtin_popcountll(ml), nr = __builtin_popcountll(mr);
+        const int cn = min(nl, nr);
+        const int k = __builtin_popcountll(ml & below);
+        const int src = (fl && k < cn) ? select_bit(mr, k) : lane;
+        typename S::Elem vx;
+        if constexpr (sizeof(typename S::Elem) == 8) {
+            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)vr, src, 64);
+            const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)vr >> 32), src, 64);
+            vx = (typename S::Elem)(((uint64_t)hi << 32) | lo);
+        } else {
+            vx = (typename S::Elem)__shfl((int)vr, src, 64);
+        }
+        if (fl && k < cn) {
+            s.st(pl, vx);
+            s.st(rpos - src, vl);
+        }
+        t += cn;
+        lpos = nl == cn ? min(lpos + 64, z + 1) : lpos + select_bit(ml, cn);
+        rpos = nr == cn ? max(rpos - 64, z) : rpos - select_bit(mr, cn);
+        wfence();
     }
-    int j = 0;
-    for (int base = z + 1; base < b; base += 64) {                  // right zone: passing pred, left to right
-        const int p = base + lane;
-        const bool f = p < b && pred(p);
-        const uint64_t mk = __ballot(f);
-        if (f) scr[a + c0 + j + __builtin_popcountll(mk & below)] = (uint32_t)p;
-        j += __builtin_popcountll(mk);
-    }
-    wfence();
-    for (int k0 = 0; k0 < t; k0 += 64) {                            // k-th from the left <-> k-th from the right
-        const int k = k0 + lane;
-        if (k < t) swp(s, (int)scr[a + k], (int)scr[a + c0 + t - 1 - k]);
-    }
-    wfence();
     *m_out = m;
     *t_out = t;
 }
@@ -338,7 +414,7 @@ template <class S> __device__ void w_exchange(const S& s, int a, int b, uint32_t
 // pdqsort_func on one frame, to the end, by one wavefront.  The frames it defers live in
 // a VGPR stack (lane j holds entry j): it continues with the smaller side and defers the
 // larger, so the depth stays below log2(len) + 1.
-template <class S> __device__ void w_sort(const S& s, int a, int b, int lf, uint32_t* __restrict__ scr) {
+template <class S> __device__ void w_sort(const S& s, int a, int b, int lf) {
     const int lane = threadIdx.x & 63;
     int sa = 0, sb = 0, slf = 0, sp = 0;
     int limit = lf & 255;
@@ -380,7 +456,7 @@ template <class S> __device__ void w_sort(const S& s, int a, int b, int lf, uint
                 pk = (uint32_t)rfl((int)pk);
                 wfence();
                 int m, t;
-                w_exchange(s, a, b, pk, eq, scr, &m, &t);
+                w_exchange(s, a, b, pk, eq, &m, &t);
                 if (eq) {
                     a = a + m + 1;                  // partitionEqual: continue with [mid, b)
                     continue;
@@ -422,31 +498,37 @@ template <class S> __device__ void w_sort(const S& s, int a, int b, int lf, uint
 // ---------------------------------------------------------------------------------
 // workgroup steps
 // ---------------------------------------------------------------------------------
+constexpr int T_SMALL = 1024;        // frames up to this length wait for the wavefront phase
+
 struct Ctl {
     Frame f[MAXF];
     int32_t op[MAXF];
     uint32_t pk[MAXF];
     int32_t m[MAXF], t[MAXF];
-    int32_t fo[MAXF + 1];      // prefix of the frames' interior lengths (partitioned frames only)
-    int32_t po[MAXF + 1];      // prefix of the frames' pair counts
+    int32_t pl[MAXF];          // slots of the frames that partition this step, in slot order
+    int32_t fo[MAXF + 1];      // prefix of their interior lengths
+    int32_t po[MAXF + 1];      // prefix of their pair counts
+    int32_t piv[MAXF];         // chosen pivot position (step A1)
+    uint8_t pis[MAXF];         // partialInsertionSort runs for the frame (A1 -> workgroup)
     uint64_t wsum[NW];
     uint32_t wflag[NW];
-    int32_t nf, top, base;
+    int32_t nf, np, top, base, nsmall, snext;
     uint32_t rmax;
+    int32_t x0, x1;            // workgroup partialInsertionSort: search results
+    uint64_t pe, pf;           //   the two elements it moves
 };
 
-// frame of concatenated index x: fo[f] <= x < fo[f+1]
-__device__ inline int find_frame(const int32_t* fo, int nf, int x) {
-    int lo = 0, hi = nf;                    // largest f with fo[f] <= x (then skip empty frames)
+// index k with fo[k] <= x < fo[k+1] (every listed frame has a non-empty interior)
+__device__ inline int find_frame(const int32_t* fo, int np, int x) {
+    int lo = 0, hi = np;
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
         if (fo[mid] <= x) lo = mid; else hi = mid;
     }
-    while (lo < nf - 1 && fo[lo + 1] <= x) lo++;
     return lo;
 }
 
-// exclusive prefix (over lanes, then waves) of n entries of v[] into o[], o[n] = total; one wave
+// exclusive prefix of n entries of v[] into o[], o[n] = total; one wave
 __device__ inline void w_prefix(const int32_t* v, int32_t* o, int n) {
     const int lane = threadIdx.x & 63;
     int carry = 0;
@@ -481,150 +563,430 @@ __device__ inline uint64_t wg_seg_scan(uint64_t v, bool flag, Ctl& c) {
     for (int q = 0; q < w; q++) {
         if (c.wflag[q]) pv = c.wsum[q]; else pv += c.wsum[q];
     }
-    // exclusive inside the wave
     uint64_t ev = __shfl_up(iv, 1, 64);
     bool ef = __shfl_up((int)iflag, 1, 64) != 0;
     if (lane == 0) { ev = 0; ef = false; }
     return ef ? ev : pv + ev;
 }
 
-// One pdqsort_func partition (or partitionEqual) of every frame of the step with
-// op != OP_DONE, as one pass over the concatenation of their interiors.
-template <class S> __device__ void wg_partition(const S& s, Ctl& c, int nf, uint32_t* __restrict__ scr) {
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int TT = c.fo[nf];
-    const int ch = (TT + NT - 1) / NT;
-    const int x0 = min(tid * ch, TT), x1 = min(x0 + ch, TT);
-    const bool cache = ch <= 64;
-    // P1: m[f] = #pred over the interior
+// m[slot] += cnt with one atomic per wave when the wave's lanes all end in one frame
+__device__ inline void add_count(Ctl& c, bool active, int slot, int cnt) {
+    const int s0 = rfl(slot);
+    if (__ballot(active && slot != s0) == 0) {
+        int tot = active ? cnt : 0;
+        for (int d = 32; d >= 1; d >>= 1) tot += __shfl_xor(tot, d, 64);
+        if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&c.m[s0], tot);
+    } else if (active && cnt) {
+        atomicAdd(&c.m[slot], cnt);
+    }
+}
+
+// t[slot] += cnt, same aggregation
+__device__ inline void add_count_t(Ctl& c, bool active, int slot, int cnt) {
+    const int s0 = rfl(slot);
+    if (__ballot(active && slot != s0) == 0) {
+        int tot = active ? cnt : 0;
+        for (int d = 32; d >= 1; d >>= 1) tot += __shfl_xor(tot, d, 64);
+        if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&c.t[s0], tot);
+    } else if (active && cnt) {
+        atomicAdd(&c.t[slot], cnt);
+    }
+}
+
+// A partitioning frame seen from a thread's chunk: interior [s, e) = [a+1, b), zone
+// boundary z = a + m, exchange offset c1, pair count t.
+struct PFrame {
+    int s, e, a, c1, z, t, slot;
+    uint32_t pk;
+    bool eq;
+    __device__ void load(const Ctl& c, int k, bool counted) {
+        if (k < 0 || k >= c.np) { s = e = INT_MAX; a = c1 = z = t = slot = 0; pk = 0; eq = false; return; }
+        slot = c.pl[k];
+        a = c.f[slot].a;
+        s = a + 1;
+        e = c.f[slot].b;
+        c1 = (e - a) / 2;
+        pk = c.pk[slot];
+        eq = c.op[slot] == OP_EQ;
+        z = counted ? a + c.m[slot] : 0;
+        t = counted ? c.t[slot] : 0;
+    }
+    __device__ bool pred(uint32_t key) const { return eq ? key <= pk : key < pk; }
+};
+
+// One partition_func / partitionEqual_func step of every listed frame (c.pl, ordered by
+// start).  Positional chunks: thread t owns positions [t*cs, t*cs + cs) of the group and
+// walks them with the frame it is in (F) and the next one (G); positions outside every
+// interior are skipped.  The loops are rolled: the code of a step stays small enough for
+// the instruction cache (fully unrolled chunk loops thrashed it).
+// Exchange inside an interior [a+1, b) of length L: the k-th left-zone element failing
+// pred (from the left) leaves its value at xs[a+1+k], the j-th right-zone element passing
+// it (from the left) at xs[a+1+c1+j], c1 = (L+1)/2 (t <= L/2 pairs fit); then the k-th
+// left failure takes the value of the k-th right pass from the right, and vice versa.
+// xs: the group's exchange scratch (global memory, one element per position).
+template <class S> __device__ void wg_partition(const S& s, Ctl& c, typename S::Elem* __restrict__ xs, int n) {
+    const int tid = threadIdx.x;
+    const int np = c.np;
+    const int cs = (n + NT - 1) / NT;
+    const int p0 = min(tid * cs, n), p1 = min(p0 + cs, n);
+    const bool cache = cs <= 64;                     // pred bits of the chunk in one register pair
+    int k0;
+    {
+        int lo = 0, hi = np;                         // frames with start a <= p0
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (c.f[c.pl[mid]].a <= p0) lo = mid + 1; else hi = mid;
+        }
+        k0 = lo - 1;
+    }
     uint64_t pm = 0;
+    PFrame F, G;
+    // P1: m per frame
     {
-        int f = x0 < x1 ? find_frame(c.fo, nf, x0) : 0;
-        int fend = x0 < x1 ? c.fo[f + 1] : 0, a1 = x0 < x1 ? c.f[f].a + 1 - c.fo[f] : 0;
-        uint32_t pk = x0 < x1 ? c.pk[f] : 0;
-        bool eq = x0 < x1 && c.op[f] == OP_EQ;
-        int cnt = 0, flast = f;
-        bool multi = false;
-        for (int x = x0; x < x1; x++) {
-            if (x >= fend) {
-                atomicAdd(&c.m[f], cnt);
+        int k = k0;
+        F.load(c, k, false);
+        G.load(c, k + 1, false);
+        int cnt = 0;
+        for (int p = p0; p < p1; p++) {
+            if (p >= G.s) {
+                if (cnt) atomicAdd(&c.m[F.slot], cnt);
                 cnt = 0;
-                multi = true;
-                do { f++; } while (c.fo[f + 1] <= x);
-                fend = c.fo[f + 1]; a1 = c.f[f].a + 1 - c.fo[f]; pk = c.pk[f]; eq = c.op[f] == OP_EQ;
+                k++;
+                F = G;
+                G.load(c, k + 1, false);
             }
-            const uint32_t k = K(s, a1 + x);
-            const bool pr = eq ? k <= pk : k < pk;
-            cnt += pr ? 1 : 0;
-            if (cache && pr) pm |= 1ull << (x - x0);
+            if (p >= F.s && p < F.e) {
+                const bool pr = F.pred(S::key(s.ld(p)));
+                cnt += pr ? 1 : 0;
+                if (pr) pm |= 1ull << ((p - p0) & 63);
+            }
         }
-        flast = f;
-        // wave aggregation when every lane's (last) frame is the same
-        const int f0 = rfl(flast);
-        const bool same = __ballot(x0 < x1 && flast != f0) == 0;
-        if (same) {
-            int tot = cnt;
-            for (int d = 32; d >= 1; d >>= 1) tot += __shfl_xor(tot, d, 64);
-            if (lane == 0 && tot) atomicAdd(&c.m[f0], tot);
-        } else if (x0 < x1 && cnt) {
-            atomicAdd(&c.m[flast], cnt);
-        }
-        (void)multi;
+        add_count(c, p0 < p1 && k >= 0, F.slot, cnt);
     }
     __syncthreads();
-    // P2: the k-th left-zone element failing pred -> scr[a + k]; the j-th right-zone
-    // element passing it (from the left) -> scr[a + c0 + j]
+    PDQ_T(t_p2);
+    auto pred_at = [&](const PFrame& f, int p) -> bool {
+        return cache ? ((pm >> (p - p0)) & 1ull) != 0 : f.pred(S::key(s.ld(p)));
+    };
+    // P2: segmented counts of left-zone failures (lm) / right-zone passes (rm)
+    uint32_t lm = 0, rm = 0;
+    bool start;
     {
-        auto pred_at = [&](int x, int a1, uint32_t pk, bool eq) -> bool {
-            if (cache) return (pm >> (x - x0)) & 1ull;
-            const uint32_t k = K(s, a1 + x);
-            return eq ? k <= pk : k < pk;
-        };
-        uint32_t lm = 0, rm = 0;
-        bool has_start = false;
-        if (x0 < x1) {
-            int f = find_frame(c.fo, nf, x0);
-            int fend = c.fo[f + 1], fbeg = c.fo[f], a = c.f[f].a, a1 = a + 1 - fbeg, z = a + c.m[f];
-            uint32_t pk = c.pk[f];
-            bool eq = c.op[f] == OP_EQ;
-            for (int x = x0; x < x1; x++) {
-                if (x >= fend) {
-                    do { f++; } while (c.fo[f + 1] <= x);
-                    fend = c.fo[f + 1]; fbeg = c.fo[f]; a = c.f[f].a; a1 = a + 1 - fbeg; z = a + c.m[f];
-                    pk = c.pk[f]; eq = c.op[f] == OP_EQ;
-                }
-                if (x == fbeg) { lm = 0; rm = 0; has_start = true; }
-                const int p = a1 + x;
-                const bool pr = pred_at(x, a1, pk, eq);
-                if (p <= z) lm += pr ? 0u : 1u; else rm += pr ? 1u : 0u;
+        int k = k0;
+        F.load(c, k, true);
+        G.load(c, k + 1, true);
+        start = F.s >= p0;
+        for (int p = p0; p < p1; p++) {
+            if (p >= G.s) { k++; F = G; G.load(c, k + 1, true); lm = rm = 0; start = true; }
+            if (p >= F.s && p < F.e) {
+                const bool pr = pred_at(F, p);
+                if (p <= F.z) lm += pr ? 0u : 1u; else rm += pr ? 1u : 0u;
             }
         }
-        const uint64_t ex = wg_seg_scan(((uint64_t)rm << 32) | lm, has_start, c);
-        lm = (uint32_t)ex;
-        rm = (uint32_t)(ex >> 32);
-        if (x0 < x1) {
-            int f = find_frame(c.fo, nf, x0);
-            int fend = c.fo[f + 1], fbeg = c.fo[f], a = c.f[f].a, a1 = a + 1 - fbeg, z = a + c.m[f];
-            int c0 = (c.f[f].b - a + 1) / 2;
-            uint32_t pk = c.pk[f];
-            bool eq = c.op[f] == OP_EQ;
-            for (int x = x0; x < x1; x++) {
-                if (x >= fend) {
-                    do { f++; } while (c.fo[f + 1] <= x);
-                    fend = c.fo[f + 1]; fbeg = c.fo[f]; a = c.f[f].a; a1 = a + 1 - fbeg; z = a + c.m[f];
-                    c0 = (c.f[f].b - a + 1) / 2; pk = c.pk[f]; eq = c.op[f] == OP_EQ;
-                }
-                if (x == fbeg) { lm = 0; rm = 0; }
-                const int p = a1 + x;
-                const bool pr = pred_at(x, a1, pk, eq);
-                if (p <= z) {
-                    if (!pr) scr[a + lm++] = (uint32_t)p;
+    }
+    const uint64_t ex = wg_seg_scan(((uint64_t)rm << 32) | lm, start, c);
+    {
+        int k = k0;
+        F.load(c, k, true);
+        G.load(c, k + 1, true);
+        lm = F.s < p0 ? (uint32_t)ex : 0u;
+        rm = F.s < p0 ? (uint32_t)(ex >> 32) : 0u;
+        for (int p = p0; p < p1; p++) {
+            if (p >= G.s) { k++; F = G; G.load(c, k + 1, true); lm = rm = 0; }
+            if (p >= F.s && p < F.e) {
+                const bool pr = pred_at(F, p);
+                if (p <= F.z) {
+                    if (!pr) xs[F.s + lm++] = s.ld(p);
                 } else if (pr) {
-                    scr[a + c0 + rm++] = (uint32_t)p;
+                    xs[F.s + F.c1 + rm++] = s.ld(p);
                 }
-                if (x == fend - 1) c.t[f] = (int32_t)lm;     // the frame's pair count
+                if (p == F.e - 1) c.t[F.slot] = (int32_t)lm;     // the frame's pair count
             }
         }
     }
     __syncthreads();
-    if (tid < 64) {
-        // (frames that did not partition have t = 0)
-        w_prefix(c.t, c.po, nf);
-    }
-    __syncthreads();
-    // P3: pairs
+    PDQ_ADD(6, t_p2);
+    PDQ_T(t_p3);
+    // P3: every misplaced position takes its partner's value (each thread writes only its
+    // own chunk, so the pred recomputation above reads unchanged positions)
     {
-        const int TP = c.po[nf];
-        const int cp = (TP + NT - 1) / NT;
-        const int y0 = min(tid * cp, TP), y1 = min(y0 + cp, TP);
-        if (y0 < y1) {
-            int f = find_frame(c.po, nf, y0);
-            int fend = c.po[f + 1], fbeg = c.po[f], a = c.f[f].a, t = c.t[f], c0 = (c.f[f].b - a + 1) / 2;
-            for (int y = y0; y < y1; y++) {
-                if (y >= fend) {
-                    do { f++; } while (c.po[f + 1] <= y);
-                    fend = c.po[f + 1]; fbeg = c.po[f]; a = c.f[f].a; t = c.t[f]; c0 = (c.f[f].b - a + 1) / 2;
+        int k = k0;
+        F.load(c, k, true);
+        G.load(c, k + 1, true);
+        lm = F.s < p0 ? (uint32_t)ex : 0u;
+        rm = F.s < p0 ? (uint32_t)(ex >> 32) : 0u;
+        for (int p = p0; p < p1; p++) {
+            if (p >= G.s) { k++; F = G; G.load(c, k + 1, true); lm = rm = 0; }
+            if (p >= F.s && p < F.e) {
+                const bool pr = pred_at(F, p);
+                if (p <= F.z) {
+                    if (!pr) { const int kk = (int)lm++; s.st(p, xs[F.s + F.c1 + F.t - 1 - kk]); }
+                } else if (pr) {
+                    const int kk = F.t - 1 - (int)rm++;
+                    s.st(p, xs[F.s + kk]);
                 }
-                const int k = y - fbeg;
-                swp(s, (int)scr[a + k], (int)scr[a + c0 + t - 1 - k]);
             }
         }
     }
     __syncthreads();
+    PDQ_ADD(7, t_p3);
+}
+
+// LDS store: thread t owns the 64 positions of word t.  Frames here are longer than
+// T_SMALL, so a word meets at most two interiors (F, then G); membership, pred, zone,
+// left-zone failures (LM) and right-zone passes (RM) are 64-bit masks, counts are
+// popcounts.  The pairs are found, not listed: each thread swaps its LM elements with
+// their partners, whose positions it selects from the RM bitmap (one word per thread in
+// LDS) through the words' prefix counts — the RM with global index gR is bit
+// gR - rmp[w] of the word w with rmp[w] <= gR < rmp[w+1].  Global indices are frame-
+// ordered because frames are ordered by position: frame f's RMs are base_f .. base_f +
+// t_f - 1 with base_f the pairs of the frames before it, and so are its LMs; the k-th LM
+// from the left (global base_f + k) pairs with RM global base_f + t_f - 1 - k.
+__device__ inline uint64_t range_bits(int lo, int hi) {     // bits [lo, hi) of a word, clamped to [0, 64)
+    lo = max(lo, 0);
+    hi = min(hi, 64);
+    if (hi <= lo) return 0ull;
+    const uint64_t up = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
+    return up & ~((1ull << lo) - 1);
+}
+
+__device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, int n) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int np = c.np;
+    const int W = (n + 63) >> 6;
+    const bool act = tid < W;
+    const int p0 = tid * 64;
+    // F: the last partitioning frame starting at or before the word's last position; G: the one before it
+    int kF = -1;
+    {
+        int lo = 0, hi = np;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (c.f[c.pl[mid]].a <= p0 + 63) lo = mid + 1; else hi = mid;
+        }
+        kF = lo - 1;
+    }
+    PFrame A, B;                   // B = frame kF (later positions), A = frame kF - 1 (earlier)
+    A.load(c, kF - 1, false);
+    B.load(c, kF, false);
+    const uint64_t memA = act ? range_bits(A.s - p0, A.e - p0) : 0ull;
+    const uint64_t memB = act ? range_bits(B.s - p0, B.e - p0) : 0ull;
+    // P1: pred bits (byte loads, compare), m per frame
+    uint64_t pm = 0;
+    if (memA | memB) {
+        const uint4* r16 = reinterpret_cast<const uint4*>(s.rk + p0);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint4 x = r16[q];
+            const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+#pragma unroll
+                for (int bb = 0; bb < 4; bb++) {
+                    const int j = q * 16 + h * 4 + bb;
+                    const uint32_t key = (wv[h] >> (8 * bb)) & 0xFFu;
+                    const bool inb = (memB >> j) & 1ull;
+                    const uint32_t pk = inb ? B.pk : A.pk;
+                    const bool eq = inb ? B.eq : A.eq;
+                    pm |= (uint64_t)(eq ? key <= pk : key < pk) << j;
+                }
+            }
+        }
+        pm &= memA | memB;
+    }
+    add_count(c, memA != 0, A.slot, __builtin_popcountll(pm & memA));
+    add_count(c, memB != 0, B.slot, __builtin_popcountll(pm & memB));
+    __syncthreads();
+    PDQ_T(t_p2);
+    // P2: zones, LM / RM masks, RM bitmap, pair counts, prefix counts
+    A.z = A.a + (memA ? c.m[A.slot] : 0);
+    B.z = B.a + (memB ? c.m[B.slot] : 0);
+    const uint64_t leftA = range_bits(A.s - p0, A.z + 1 - p0), leftB = range_bits(B.s - p0, B.z + 1 - p0);
+    const uint64_t lmA = ~pm & memA & leftA, lmB = ~pm & memB & leftB;
+    const uint64_t rmask = (pm & memA & ~leftA) | (pm & memB & ~leftB);
+    const uint64_t lmask = lmA | lmB;
+    if (act) s.rmb[tid] = rmask;
+    add_count_t(c, lmA != 0, A.slot, __builtin_popcountll(lmA));
+    add_count_t(c, lmB != 0, B.slot, __builtin_popcountll(lmB));
+    // exclusive block scan of (LM << 16 | RM) per word (counts < 2^16: n <= PDQ_LDS_N)
+    uint32_t incl = ((uint32_t)__builtin_popcountll(lmask) << 16) | (uint32_t)__builtin_popcountll(rmask);
+    const uint32_t own = incl;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) c.wsum[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t pre = incl - own;
+    for (int q = 0; q < (tid >> 6); q++) pre += (uint32_t)c.wsum[q];
+    if (act) s.rmp[tid] = (uint16_t)(pre & 0xFFFFu);
+    if (tid == W - 1) s.rmp[W] = (uint16_t)((pre + own) & 0xFFFFu);
+    if (tid < 64) {
+        // pair base of every frame in position order (c.t holds the pair counts; t[] of
+        // the frames is read again in P3)
+        for (int i = lane; i < np; i += 64) c.po[i] = c.t[c.pl[i]];
+        w_prefix(c.po, c.fo, np);           // fo[k] = base of frame k (position order)
+    }
+    __syncthreads();
+    PDQ_ADD(6, t_p2);
+    PDQ_T(t_p3);
+    // P3: swap every LM element with its partner
+    if (lmask) {
+        uint32_t gl = pre >> 16;                     // global LM index of the word's first LM
+        uint64_t lm = lmask;
+        int ww = -1, bit = 0;                        // the current partner (word, bit)
+        int prevf = -1;
+        while (lm) {
+            const int j = __builtin_ctzll(lm);
+            lm &= lm - 1;
+            const int p = p0 + j;
+            const bool inb = (memB >> j) & 1ull;
+            const int kk = inb ? kF : kF - 1;
+            const int slot = inb ? B.slot : A.slot;
+            const uint32_t base = (uint32_t)c.fo[kk];
+            const uint32_t t = (uint32_t)c.t[slot];
+            const uint32_t k = gl - base;
+            const uint32_t gR = base + t - 1 - k;
+            if (kk != prevf) {                       // locate: the word holding RM gR
+                int lo = 0, hi = W;
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (s.rmp[mid] <= gR) lo = mid; else hi = mid;
+                }
+                ww = lo;
+                uint64_t m = s.rmb[ww];
+                for (uint32_t r = gR - s.rmp[ww]; r > 0; r--) m &= m - 1;
+                bit = __builtin_ctzll(m);
+                prevf = kk;
+            } else {                                 // the previous RM (gR one lower)
+                uint64_t m = s.rmb[ww] & ((1ull << bit) - 1);
+                while (!m) m = s.rmb[--ww];
+                bit = 63 - __builtin_clzll(m);
+            }
+            swp(s, p, ww * 64 + bit);
+            gl++;
+        }
+    }
+    __syncthreads();
+    PDQ_ADD(7, t_p3);
+}
+
+// partialInsertionSort_func on a frame longer than T_SMALL, by the whole workgroup: the
+// descent search and the two landing searches are parallel min / max reductions, the two
+// bubbling loops are block moves (read, barrier, write).  One wavefront alone spent
+// ~10^5 cycles per call where a frame held a long run of one key (every step moved the
+// run by one place).
+template <class S> __device__ void wg_shift(const S& s, Ctl& c, int lo, int hi, int dir) {
+    // [lo, hi] moves one place (dir +1: right, processed top-down; -1: left, bottom-up),
+    // NT * PER positions per round
+    constexpr int PER = 8;
+    const int tid = threadIdx.x;
+    const int len = hi - lo + 1;
+    for (int done = 0; done < len; done += NT * PER) {
+        typename S::Elem v[PER];
+        const int base = dir > 0 ? hi - done : lo + done;      // first position of this round
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int off = u * NT + tid;
+            const int p = dir > 0 ? base - off : base + off;
+            v[u] = off < len - done ? s.ld(p) : 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int off = u * NT + tid;
+            const int p = dir > 0 ? base - off : base + off;
+            if (off < len - done) s.st(p + dir, v[u]);
+        }
+        __syncthreads();
+    }
+}
+
+template <class S> __device__ bool wg_partial_insertion(const S& s, Ctl& c, int a, int b) {
+    constexpr int maxSteps = 5, shortestShifting = 50;
+    const int tid = threadIdx.x;
+    int i = a + 1;
+    for (int step = 0; step < maxSteps; step++) {
+        // first i' in [i, b) with less(i', i'-1): positions striped over the threads
+        if (tid == 0) c.x0 = b;
+        __syncthreads();
+        for (int q0 = i; q0 < b; q0 += NT) {
+            const int q = q0 + tid;
+            const bool d = q < b && K(s, q) < K(s, q - 1);
+            if (d) atomicMin(&c.x0, q);
+            if (__syncthreads_or(d)) break;
+        }
+        i = c.x0;
+        if (i == b) return true;
+        if (b - a < shortestShifting) return false;
+        __syncthreads();
+        if (tid == 0) {
+            swp(s, i, i - 1);
+            c.pe = (uint64_t)s.ld(i - 1);          // the smaller one, bubbling left
+            c.pf = (uint64_t)s.ld(i);              // the greater one, bubbling right
+            c.x0 = -1;
+            c.x1 = b;
+        }
+        __syncthreads();
+        const typename S::Elem e = (typename S::Elem)c.pe, f = (typename S::Elem)c.pf;
+        const uint32_t ke = S::key(e), kf = S::key(f);
+        const bool left = i - a >= 2, right = b - i >= 2;
+        const int qmin = a > 0 ? a - 1 : 0;     // key(a-1) <= every key of [a, b): the walk stops there
+        // left: the largest q in [qmin, i-2] with key(q) <= ke; right: the smallest j in
+        // [i+1, b) with !(key(j) < kf); windows of NT positions outward from i
+        if (left)
+            for (int top = i - 2; top >= qmin; top -= NT) {
+                const int q = top - tid;
+                const bool d = q >= qmin && K(s, q) <= ke;
+                if (d) atomicMax(&c.x0, q);
+                if (__syncthreads_or(d)) break;
+            }
+        if (right)
+            for (int bot = i + 1; bot < b; bot += NT) {
+                const int j = bot + tid;
+                const bool d = j < b && !(K(s, j) < kf);
+                if (d) atomicMin(&c.x1, j);
+                if (__syncthreads_or(d)) break;
+            }
+        __syncthreads();
+        const int landL = c.x0 + 1;             // (no q at all: only when qmin == 0 -> 0)
+        const int landR = c.x1 - 1;
+        if (left && landL < i - 1) {
+            wg_shift(s, c, landL, i - 2, +1);
+            if (tid == 0) s.st(landL, e);
+        }
+        if (right && landR > i) {
+            wg_shift(s, c, i + 1, landR, -1);
+            if (tid == 0) s.st(landR, f);
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+    return false;
 }
 
 // Sort positions [0, n) of one group (elements already in the store in list order).
+// stack: the group's frame area (cap >= n/2 + 2 frames): pending frames longer than
+// T_SMALL grow from its start, shorter ones from its end (they are sorted last, one
+// wavefront each, with no workgroup barrier).  xs: n elements of exchange scratch.
 // limit0 > 0 replaces sort.Slice's initial limit bits.Len(n) (tests: the heapSort fallback).
-// stack: the group's pending frames (capacity n/2 + 2); scr: n entries of scratch.
-template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict__ stack, uint32_t* __restrict__ scr,
-                                           Ctl& c, int limit0) {
+template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict__ stack, int cap,
+                                           typename S::Elem* __restrict__ xs, Ctl& c, int limit0) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    PDQ_T(t_all);
     if (tid == 0) {
         c.top = 0;
-        if (n >= 2) { stack[0] = Frame{0, n, lf_pack(limit0 > 0 ? limit0 : bits_len((uint32_t)n), true, true)}; c.top = 1; }
+        c.nsmall = 0;
+        c.snext = 0;
+        if (n >= 2) {
+            const Frame root{0, n, lf_pack(limit0 > 0 ? limit0 : bits_len((uint32_t)n), true, true)};
+            if (n <= T_SMALL) { stack[cap - 1] = root; c.nsmall = 1; }
+            else { stack[0] = root; c.top = 1; }
+        }
     }
     __syncthreads();
     for (;;) {
+        PDQ_T(t_pop);
         if (tid == 0) {
             const int nf = min(c.top, MAXF);
             c.nf = nf;
@@ -641,49 +1003,102 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
             c.t[i] = 0;
         }
         __syncthreads();
-        // A: one loop iteration's control per frame (a wavefront each); small frames to the end
+        PDQ_ADD(2, t_pop);
+        PDQ_CNT(11, 1);
+        PDQ_CNT(12, nf);
+        PDQ_T(t_a);
+        // A: one pdqsort_func loop iteration's control per frame (a wavefront each)
         for (int i = w; i < nf; i += NW) {
             const Frame fr = c.f[i];
-            int a = fr.a, b = fr.b, limit = fr.lf & 255;
+            const int a = fr.a, b = fr.b;
+            int limit = fr.lf & 255;
             const bool wb = (fr.lf >> 8) & 1, wp = (fr.lf >> 9) & 1;
-            if (b - a <= WAVE_SMALL) { w_sort(s, a, b, fr.lf, scr); continue; }
             if (limit == 0) {
                 if (lane == 0) heap_sort(s, a, b);
                 wfence();
                 continue;
             }
+            PDQ_T(t_bp);
             if (!wb) {
                 if (lane == 0) break_patterns(s, a, b);
                 wfence();
                 limit--;
             }
+            PDQ_WADD(16, t_bp);
+            PDQ_T(t_cp);
             int hint;
             int pivot = w_choose_pivot(s, a, b, &hint);
+            PDQ_WADD(17, t_cp);
+            PDQ_T(t_rv);
             if (hint == HINT_DEC) {
                 w_reverse(s, a, b);
                 pivot = (b - 1) - (pivot - a);
                 hint = HINT_INC;
             }
-            if (wb && wp && hint == HINT_INC && w_partial_insertion(s, a, b)) continue;
+            PDQ_WADD(18, t_rv);
             if (lane == 0) {
-                const bool eq = a > 0 && !(K(s, a - 1) < K(s, pivot));
-                swp(s, a, pivot);
-                c.pk[i] = K(s, a);
-                c.op[i] = eq ? OP_EQ : OP_PART;
+                c.piv[i] = pivot;
+                c.pis[i] = (wb && wp && hint == HINT_INC) ? 1 : 0;
+                c.op[i] = OP_PART;                  // (A2 decides)
                 c.f[i].lf = lf_pack(limit, wb, wp);
             }
             wfence();
         }
         __syncthreads();
-        if (tid < 64) {
-            // interior lengths of the partitioned frames (scratch: the m[] slots are 0 here)
-            int32_t* len = c.t;                 // t[] is rewritten by wg_partition
-            for (int i = lane; i < nf; i += 64) len[i] = c.op[i] != OP_DONE ? c.f[i].b - c.f[i].a - 1 : 0;
-            w_prefix(len, c.fo, nf);
-            for (int i = lane; i < nf; i += 64) len[i] = 0;
+        // partialInsertionSort of the frames that run it, one after another, by the workgroup
+        for (int i = 0; i < nf; i++) {
+            if (c.op[i] == OP_DONE || !c.pis[i]) continue;
+            PDQ_T(t_pis);
+            const bool sorted = wg_partial_insertion(s, c, c.f[i].a, c.f[i].b);
+            PDQ_WADD(19, t_pis);
+            PDQ_CNT(20, 1);
+            if (sorted && tid == 0) c.op[i] = OP_DONE;
+            __syncthreads();
+        }
+        // A2: partitionEqual or partition; the pivot moves to a
+        for (int i = w; i < nf; i += NW) {
+            if (c.op[i] == OP_DONE) continue;
+            if (lane == 0) {
+                const int a = c.f[i].a, pivot = c.piv[i];
+                const bool eq = a > 0 && !(K(s, a - 1) < K(s, pivot));
+                swp(s, a, pivot);
+                c.pk[i] = K(s, a);
+                c.op[i] = eq ? OP_EQ : OP_PART;
+            }
+            wfence();
         }
         __syncthreads();
-        if (c.fo[nf] > 0) wg_partition(s, c, nf, scr);
+        PDQ_ADD(3, t_a);
+        PDQ_T(t_pl);
+        if (tid < 64) {                     // the partitioning frames, ordered by start
+            int np = 0;
+            for (int i0 = 0; i0 < nf; i0 += 64) np += __builtin_popcountll(__ballot(i0 + lane < nf && c.op[i0 + lane] != OP_DONE));
+            // rank of frame i among the partitioning frames by start a (starts are distinct)
+            for (int i0 = 0; i0 < nf; i0 += 64) {
+                const int i = i0 + lane;
+                const bool on = i < nf && c.op[i] != OP_DONE;
+                const int ai = on ? c.f[i].a : 0;
+                int r = 0;
+                for (int q = 0; q < nf; q++) {
+                    const bool oq = c.op[q] != OP_DONE;      // (uniform loads: broadcast reads)
+                    r += (oq && c.f[q].a < ai) ? 1 : 0;
+                }
+                if (on) {
+                    c.pl[r] = i;
+                    c.po[r] = c.f[i].b - c.f[i].a - 1;      // (staging for the prefix)
+                }
+            }
+            if (lane == 0) c.np = np;
+            w_prefix(c.po, c.fo, np);
+        }
+        __syncthreads();
+        PDQ_ADD(4, t_pl);
+        PDQ_CNT(13, c.np);
+        PDQ_CNT(15, c.fo[c.np]);
+        PDQ_T(t_part);
+        if (c.np > 0) wg_partition(s, c, xs, n);
+        PDQ_ADD(5, t_part);
+        PDQ_T(t_d);
         // D: finish partitioned frames, push the pending calls
         for (int i = w; i < nf; i += NW) {
             if (c.op[i] == OP_DONE || lane != 0) continue;
@@ -691,7 +1106,9 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
             const int a = fr.a, b = fr.b, len = b - a, limit = fr.lf & 255;
             const bool wb = (fr.lf >> 8) & 1, wp = (fr.lf >> 9) & 1;
             auto push = [&](int pa, int pb, int plf) {
-                if (pb - pa >= 2) stack[atomicAdd(&c.top, 1)] = Frame{pa, pb, plf};
+                if (pb - pa < 2) return;
+                if (pb - pa <= T_SMALL) stack[cap - 1 - atomicAdd(&c.nsmall, 1)] = Frame{pa, pb, plf};
+                else stack[atomicAdd(&c.top, 1)] = Frame{pa, pb, plf};
             };
             if (c.op[i] == OP_EQ) {
                 push(a + c.m[i] + 1, b, lf_pack(limit, wb, wp));
@@ -711,7 +1128,24 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
         }
         __threadfence_block();
         __syncthreads();
+        PDQ_ADD(9, t_d);
     }
+    // the short frames, one wavefront each, claimed in turn
+    PDQ_T(t_small);
+    const int ns = c.nsmall;
+    PDQ_CNT(14, ns);
+    for (;;) {
+        int q = 0;
+        if (lane == 0) q = atomicAdd(&c.snext, 1);
+        q = rfl(q);
+        if (q >= ns) break;
+        const Frame fr = stack[cap - 1 - q];
+        w_sort(s, fr.a, fr.b, fr.lf);
+    }
+    __threadfence_block();
+    __syncthreads();
+    PDQ_ADD(10, t_small);
+    PDQ_ADD(0, t_all);
 }
 
 }  // namespace pdq

@@ -96,13 +96,13 @@ int32_t ca_mirror::store_moved_copy(int32_t pod) {
     return (int32_t)pods.size() - 1;
 }
 
-extern "C" {
+namespace {
 
-int ca_plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const uint8_t* dest_mask,
-                     const int32_t* cand_status, const int32_t* move_off, const int32_t* move_pods,
-                     int32_t max_removable, const ca_pdb_table* pdbs, int32_t* hints, int32_t n_pods,
-                     int32_t* last_index, ca_plan_result* results, ca_plan_move* moves, int32_t moves_cap,
-                     int32_t* n_moves) {
+int plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const uint8_t* dest_mask,
+                  const int32_t* cand_status, const int32_t* move_off, const int32_t* move_pods,
+                  int32_t max_removable, const ca_pdb_table* pdbs, int32_t* hints, int32_t n_pods,
+                  int32_t* last_index, ca_plan_result* results, ca_plan_move* moves, int32_t moves_cap,
+                  int32_t* n_moves) {
     if (!m || C < 0 || !last_index || moves_cap < 0 || (moves_cap > 0 && !moves)) return CA_EINVAL;
     if (C > 0 && (!candidates || !dest_mask || !move_off || !results)) return CA_EINVAL;
     // pods past n_pods are records a Revert detached (ids are never reused): on no node
@@ -156,6 +156,7 @@ int ca_plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const u
     int32_t removed = 0;
     int32_t i = 0;
     int32_t W = std::min(C, 256);
+    if (const char* e = getenv("CASIM_PLAN_WINDOW")) W = std::max(1, std::min(C, atoi(e)));   // tests
     std::vector<int32_t> w_off, w_pods, w_status, w_dest, Hs;
     std::vector<ca_removal_result> w_res;
     std::vector<Own> own;
@@ -163,6 +164,8 @@ int ca_plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const u
     bool done = false;
     const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
     const char* why = "";
+    const char* fail_env = getenv("CASIM_PLAN_FAIL_ROUND");          // tests: an error in that round
+    const int32_t fail_round = fail_env ? atoi(fail_env) : 0;
 
     auto not_run = [&](int32_t from) {
         for (int32_t c = from; c < C; c++) {
@@ -197,6 +200,10 @@ int ca_plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const u
         const auto t_spec = std::chrono::steady_clock::now();
         int rc = ca_find_nodes_to_remove(m, candidates + i, j - i, mask.data(), w_status.data(), w_off.data(),
                                          w_pods.data(), Hs.data(), &Ls, w_res.data(), w_dest.data());
+        if (rc == CA_OK && fail_round > 0 && ps.rounds + 1 == fail_round) {
+            set_last_error("CASIM_PLAN_FAIL_ROUND: injected failure");
+            rc = CA_EDEVICE;
+        }
         if (rc != CA_OK) return rc;
         const auto t_val = std::chrono::steady_clock::now();
         ps.rounds++;
@@ -344,6 +351,37 @@ int ca_plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const u
     if (n_moves) *n_moves = nm;
     ps.total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return CA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// All or nothing: the call runs inside a fork of its own, committed into the
+// caller's state on success and reverted on any error — the mirror, the PDB budgets, the
+// caller's hints and lastIndex are then exactly as before the call.
+int ca_plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const uint8_t* dest_mask,
+                     const int32_t* cand_status, const int32_t* move_off, const int32_t* move_pods,
+                     int32_t max_removable, const ca_pdb_table* pdbs, int32_t* hints, int32_t n_pods,
+                     int32_t* last_index, ca_plan_result* results, ca_plan_move* moves, int32_t moves_cap,
+                     int32_t* n_moves) {
+    if (!m) return CA_EINVAL;
+    std::vector<int32_t> allowed0;
+    if (pdbs && pdbs->n_pdbs > 0 && pdbs->allowed) allowed0.assign(pdbs->allowed, pdbs->allowed + pdbs->n_pdbs);
+    int rc = ca_mirror_fork(m);
+    if (rc != CA_OK) return rc;
+    rc = plan_removals(m, candidates, C, dest_mask, cand_status, move_off, move_pods, max_removable, pdbs, hints, n_pods,
+                       last_index, results, moves, moves_cap, n_moves);
+    if (rc != CA_OK) {
+        const std::string err = last_error();
+        (void)ca_mirror_revert(m);
+        if (!allowed0.empty()) std::memcpy(pdbs->allowed, allowed0.data(), sizeof(int32_t) * allowed0.size());
+        m->plan.moves.clear();
+        if (n_moves) *n_moves = 0;
+        set_last_error(err);
+        return rc;
+    }
+    return ca_mirror_commit(m);
 }
 
 int ca_plan_last_moves(const ca_mirror* m, ca_plan_move* out, int32_t cap) {

@@ -25,7 +25,7 @@
 
 namespace casim {
 
-constexpr int OV_CAP = 128;     // distinct destination nodes per candidate (k_sweep)
+constexpr int OV_CAP = CA_MAX_MOVED_PODS;   // distinct destination nodes per candidate (k_sweep)
 constexpr int TB_MAXP = 128;    // moved pods per candidate handled by k_sweep_table
 constexpr int TB_SCAN = 512;    // per-lane scan bound in k_sweep_table (longer: exact kernel)
 constexpr int32_t TB_UNKNOWN = -1;
@@ -1427,8 +1427,13 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     // while it costs less per candidate than the last pipeline call (re-measured at least
     // every 8 calls); windows of at most 2 048 candidates only.
     // (CASIM_SWEEP_SERIAL: every call serial-only; CASIM_NO_SERIAL_CHAIN: never; tests)
+    // The mode carries over only to a call of the same shape — candidates and sensitive
+    // candidates within a factor of two of the call that measured it, most of them
+    // sensitive — not to an unrelated call on the same mirror.
+    const bool same_shape = C <= 2 * sw.serial_C && 2 * C >= sw.serial_C && S <= 2 * sw.serial_S &&
+                            2 * S >= sw.serial_S && 2 * S >= C;
     const bool serial_only = S > 0 && n > 0 && !getenv("CASIM_NO_SERIAL_CHAIN") &&
-                             ((C <= 2048 && sw.serial_next) || getenv("CASIM_SWEEP_SERIAL") != nullptr);
+                             ((C <= 2048 && sw.serial_next && same_shape) || getenv("CASIM_SWEEP_SERIAL") != nullptr);
     auto enqueue_serial = [&]() -> int {
         int e;
         if ((e = sw.chainl.reserve(sizeof(int32_t) * (size_t)C)) != CA_OK) return e;
@@ -1740,6 +1745,8 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         }
         sw.serial_next = serial_only ? (sw.serial_calls < 8 && sw.serial_ms_per < sw.pipe_ms_per)
                                      : (S > 0 && 2 * chained > S);
+        sw.serial_C = C;
+        sw.serial_S = S;
     }
     m->sweep_stats.rounds = rounds + exact_runs;
     // the sweep's output depends on its input lastIndex iff some scan succeeded
@@ -1754,13 +1761,15 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
 }
 
 // Prefix protocol (include/casim.h kernel scope): the first candidate that would be
-// simulated with a CA_POD_OUT_OF_SCOPE pod to move, or C.
+// simulated with a CA_POD_OUT_OF_SCOPE pod to move or with more than CA_MAX_MOVED_PODS
+// pods to move (k_sweep's destination overlay holds OV_CAP nodes), or C.
 int32_t scope_cut(const ca_mirror* m, int32_t C, const int32_t* candidates, const uint8_t* dest_mask,
                   const int32_t* status, const int32_t* move_off, const int32_t* move_pods) {
     const int32_t n = (int32_t)m->nodes.size(), np = (int32_t)m->pods.size();
     for (int32_t c = 0; c < C; c++) {
         const int32_t nd = candidates[c];
         if (nd < 0 || nd >= n || !dest_mask[nd] || (status && status[c] != 0)) continue;
+        if (move_off[c + 1] - move_off[c] > CA_MAX_MOVED_PODS) return c;
         for (int32_t i = move_off[c]; i < move_off[c + 1]; i++) {
             const int32_t id = move_pods[i];
             if (id >= 0 && id < np && (m->pods[id].spec.flags & CA_POD_OUT_OF_SCOPE)) return c;

@@ -36,10 +36,6 @@ _DNS1123 = re.compile(r"^[a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z
 _INT64 = re.compile(r"^[+-]?[0-9]+$")
 
 
-class InternCapacityError(RuntimeError):
-    """An intern universe exceeded the fixed ABI width (CA_ECAPACITY)."""
-
-
 def is_qualified_name(s: str) -> bool:
     """validation.IsQualifiedName (apimachinery/pkg/util/validation)."""
     parts = s.split("/")
@@ -165,16 +161,23 @@ def pod_ports(pod: Pod) -> list[tuple[str, str, int]]:
 
 
 class _Universe:
+    """Values interned to bit positions.  Past the fixed width (casim.h) a value is not an
+    error: it is recorded in `overflow` and get() returns None; the encoders then route
+    every object whose simulation would need it to the reference path (CA_POD_OUT_OF_SCOPE,
+    the prefix protocol) — verdict r2: capacity overflow falls back like A12 scope."""
+
     def __init__(self, cap: int, what: str):
         self.ids: dict = {}
         self.cap = cap
         self.what = what
+        self.overflow: set = set()
 
     def get(self, key, create: bool = True) -> Optional[int]:
         i = self.ids.get(key)
         if i is None and create:
-            if len(self.ids) >= self.cap:
-                raise InternCapacityError(f"{self.what}: more than {self.cap} interned values")
+            if len(self.ids) >= self.cap or key in self.overflow:
+                self.overflow.add(key)
+                return None
             i = self.ids[key] = len(self.ids)
         return i
 
@@ -193,11 +196,15 @@ class Interner:
     """Builds the intern universes from every node, template and pod of a simulation."""
 
     def __init__(self, nodes: Iterable[Node] = (), pods: Iterable[Pod] = (), templates: Iterable = ()):
-        self.taints = _Universe(64, "taint classes")
+        # taint classes: 63 interned + bit 63 = "the node has a taint past the width"
+        self.taints = _Universe(63, "taint classes")
         self.pairs = _Universe(abi.CA_LABEL_WORDS * 64, "label pairs")
         self.keys = _Universe(64, "label keys")
         self.int_keys = _Universe(abi.CA_MAX_INT_KEYS, "Gt/Lt label keys")
         self.ports = _Universe(abi.CA_PORT_WORDS * 64, "host port triples")
+        # (protocol, port) groups with a triple past the width: conflicts only relate triples
+        # of one group, so a group is interned whole or not at all for the kernels
+        self.port_groups_over: set = set()
         self.scalars = _Universe(abi.CA_MAX_SCALAR, "scalar resources")
         self.names: dict[str, int] = {}
         self.classes: dict = {}
@@ -239,7 +246,8 @@ class Interner:
                         elif r.operator in ("Gt", "Lt"):
                             self.int_keys.get(r.key)
             for trip in pod_ports(p):
-                self.ports.get(trip)
+                if self.ports.get(trip) is None:
+                    self.port_groups_over.add(trip[1:])
             if p.node_name:
                 self.name_id(p.node_name)
 
@@ -260,10 +268,13 @@ class Interner:
         sc = np.zeros(abi.CA_MAX_SCALAR, np.int64)
         for r, q in a.items():
             if is_scalar_resource(r):
-                sc[self.scalars.get(r)] += _q(q).value()
+                i = self.scalars.get(r)
+                if i is not None:                  # (past the width: requested only by out-of-scope pods)
+                    sc[i] += _q(q).value()
         rec["alloc_scalar"] = sc
         taint_ids = [self.taints.get((t.key, t.value, t.effect)) for t in n.taints
                      if t.effect in ("NoSchedule", "NoExecute")]
+        taint_ids = [63 if i is None else i for i in taint_ids]         # an overflow taint: bit 63
         rec["taints"] = int(_bits(taint_ids, 1)[0])
         pair_ids = [i for i in (self.pairs.get((k, v), create=False) for k, v in n.labels.items()) if i is not None]
         rec["label_pairs"] = _bits(pair_ids, abi.CA_LABEL_WORDS)
@@ -301,9 +312,16 @@ class Interner:
             cpu += r.cpu
             mem += r.mem
             eph += r.eph
+            # a scalar or port group past the width is used only by out-of-scope pods, which
+            # are the only ones its absence from the template row could mislead
             for name, v in r.scalar.items():
-                sc[self.scalars.get(name)] += v
-            ports += [self.ports.get(x) for x in pod_ports(p)]
+                i = self.scalars.get(name)
+                if i is not None:
+                    sc[i] += v
+            for x in pod_ports(p):
+                i = self.ports.get(x)
+                if i is not None:
+                    ports.append(i)
         t["used_milli_cpu"] = cpu
         t["used_memory"] = mem
         t["used_ephemeral"] = eph
@@ -355,6 +373,7 @@ class Interner:
 
     def _encode_pod(self, p: Pod, rec, terms: list, reqs: list, names: list) -> None:
         flags = 0
+        over = False                                   # needs a value past an intern width
         r = PodRequest(p)
         rec["req_milli_cpu"] = r.cpu
         rec["req_memory"] = r.mem
@@ -363,6 +382,9 @@ class Interner:
         tpu_mask = 0
         for name, v in r.scalar.items():
             i = self.scalars.get(name)
+            if i is None:
+                over = True
+                continue
             sc[i] = v
             if name.startswith(TPU_PREFIX):
                 tpu_mask |= 1 << i
@@ -381,13 +403,26 @@ class Interner:
             taint = Taint(k, v, e)
             if any(tolerates(t, taint) for t in p.tolerations):
                 tol |= 1 << i
+        if self.taints.overflow:
+            # bit 63 stands for every taint past the width: exact when the pod tolerates all
+            # of them or none; otherwise the pod is routed to the reference path
+            n_tol = sum(1 for (k, v, e) in self.taints.overflow if any(tolerates(t, Taint(k, v, e)) for t in p.tolerations))
+            if n_tol == len(self.taints.overflow):
+                tol |= 1 << 63
+            elif n_tol:
+                over = True
         rec["tolerated_taints"] = tol
         if any(tolerates(t, UNSCHED_TAINT) for t in p.tolerations):
             flags |= abi.CA_POD_TOLERATES_UNSCHED
         # ports
         conflict, use = [], []
         for (ip, proto, port) in pod_ports(p):
-            use.append(self.ports.get((ip, proto, port)))
+            i = self.ports.get((ip, proto, port))
+            if i is None or (proto, port) in self.port_groups_over:
+                over = True
+                if i is None:
+                    continue
+            use.append(i)
             for (ip2, proto2, port2), j in self.ports.ids.items():
                 if proto2 != proto or port2 != port:
                     continue
@@ -404,7 +439,11 @@ class Interner:
             flags |= abi.CA_POD_AFFINITY_FILTER
         sel = []
         for k, v in (p.node_selector or {}).items():
-            sel.append(self.pairs.get((k, v)))
+            i = self.pairs.get((k, v))
+            if i is None:
+                over = True
+                continue
+            sel.append(i)
             if k == HOSTNAME_KEY:
                 hostname_dep = True
         rec["node_selector"] = _bits(sel, abi.CA_LABEL_WORDS)
@@ -417,7 +456,7 @@ class Interner:
                 if not term.match_expressions and not term.match_fields:
                     continue                                   # empty term matches nothing (nodeaffinity.go:83-85)
                 rfirst = len(reqs)
-                self._compile_term(term, reqs)
+                over |= self._compile_term(term, reqs)
                 terms.append((rfirst, len(reqs) - rfirst))
                 if term.match_fields or any(r.key == HOSTNAME_KEY for r in term.match_expressions):
                     hostname_dep = True
@@ -435,18 +474,21 @@ class Interner:
             flags |= abi.CA_POD_HOSTNAME_DEPENDENT
         if is_daemonset_pod(p):                            # pod_util.IsDaemonSetPod (similar_pods.go:86-88)
             flags |= abi.CA_POD_DAEMONSET
-        if out_of_scope_reason(p) is not None:
+        if out_of_scope_reason(p) is not None or over:     # SURVEY §8a A12 (scope.py); intern widths
             flags |= abi.CA_POD_OUT_OF_SCOPE
         if has_required_anti_affinity(p):
             flags |= abi.CA_POD_REQUIRED_ANTI_AFFINITY
         rec["flags"] = flags
         rec["similar_class"] = self.similar_class(p)
 
-    def _compile_term(self, term, reqs: list) -> None:
-        """nodeSelectorTerm -> requirement rows; a parse error makes the term never match."""
+    def _compile_term(self, term, reqs: list) -> bool:
+        """nodeSelectorTerm -> requirement rows; a parse error makes the term never match.
+        Returns True when the term needs a value past an intern width (the pod is then out
+        of the kernels' scope)."""
         zero = np.zeros(abi.CA_LABEL_WORDS, np.uint64)
         rows = []
         bad = False
+        over = False
         for r in term.match_expressions:            # nodeSelectorRequirementsAsSelector (:223-260)
             if not is_qualified_name(r.key) or any(not is_valid_label_value(v) for v in r.values):
                 bad = True
@@ -455,20 +497,26 @@ class Interner:
                 if not r.values:
                     bad = True
                     continue
-                bits = _bits([self.pairs.get((r.key, v)) for v in r.values], abi.CA_LABEL_WORDS)
+                ids = [self.pairs.get((r.key, v)) for v in r.values]
+                over |= any(i is None for i in ids)
+                bits = _bits([i for i in ids if i is not None], abi.CA_LABEL_WORDS)
                 rows.append((abi.CA_OP_IN if r.operator == "In" else abi.CA_OP_NOTIN, 0, 0, bits))
             elif r.operator in ("Exists", "DoesNotExist"):
                 if r.values:
                     bad = True
                     continue
+                k = self.keys.get(r.key)
+                over |= k is None
                 rows.append((abi.CA_OP_EXISTS if r.operator == "Exists" else abi.CA_OP_DOESNOTEXIST,
-                             self.keys.get(r.key), 0, zero))
+                             k or 0, 0, zero))
             elif r.operator in ("Gt", "Lt"):
                 v = parse_int64(r.values[0]) if len(r.values) == 1 else None
                 if v is None:
                     bad = True
                     continue
-                rows.append((abi.CA_OP_GT if r.operator == "Gt" else abi.CA_OP_LT, self.int_keys.get(r.key), v, zero))
+                k = self.int_keys.get(r.key)
+                over |= k is None
+                rows.append((abi.CA_OP_GT if r.operator == "Gt" else abi.CA_OP_LT, k or 0, v, zero))
             else:
                 bad = True
         for r in term.match_fields:                 # nodeSelectorRequirementsAsFieldSelector (:263-293)
@@ -487,6 +535,7 @@ class Interner:
         if bad:
             rows = [(abi.CA_OP_FALSE, 0, 0, zero)]
         reqs.extend(rows)
+        return over
 
     def _prefilter_names(self, required: list):
         """NodeAffinity.PreFilter NodeNames (node_affinity.go:106-135): None == all nodes."""

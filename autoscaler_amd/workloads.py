@@ -16,6 +16,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import abi
+from .gosort import sort_slice_desc
 
 MI = 1024 * 1024
 GI = 1024 * MI
@@ -532,7 +533,9 @@ def c5_filter(n_nodes: int = 15_000, pods_per_node: int = 20, n_pending: int = 2
     # a class's pods share their spec, priority included
     cls_prio = rng.choice([0, 100, 1000, 10000], len(cls_shape) + 1, p=[0.6, 0.2, 0.15, 0.05])
     prio = np.where(noc, prio, cls_prio[pod_cls])
-    order = np.argsort(-prio, kind="stable").astype(np.int32)
+    # filterOutSchedulableByPacking's sort.Slice by priority, descending
+    # (filter_out_schedulable.go:97-99): Go 1.19's pdqsort order, ties included
+    order = np.array(sort_slice_desc(prio.tolist()), np.int32)
     hints = np.where(rng.random(n_pending) < hint_frac, rng.integers(0, n_nodes, n_pending), -1).astype(np.int32)
     pending = abi.PodTable(pend, terms_arr, req_arr) if taints else abi.PodTable(pend)
     return FilterWorkload("C5-filter" + ("-c4" if taints else ""), nodes, abi.PodTable(running), pod_node, pending,

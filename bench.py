@@ -425,7 +425,6 @@ def runonce_leg(args, device: int, with_cpu: bool) -> dict:
         ut[0].close()
     rows.close()
     m.close()
-    ut[0].close()
     keys = list(runs[-1].ms)
     out = {"workload": "C5 RunOnce: 15000 nodes, 300000 running pods, 20000 pending (15% of the controller "
                        "variants too large for existing nodes), 100 node groups",

@@ -68,6 +68,7 @@ extern "C" {
 #define CA_PORT_WORDS    2   /* 128 interned (hostIP,protocol,hostPort) triples        */
 #define CA_MAX_INT_KEYS  4   /* label keys referenced by Gt/Lt requirements           */
 /* taint classes: 64 (one u64); label keys for Exists/DoesNotExist: 64 (one u64) */
+#define CA_MAX_MOVED_PODS 128 /* pods to move of one scale-down candidate (kernel scope below) */
 
 /* ---- node flags ---------------------------------------------------------- */
 #define CA_NODE_UNSCHEDULABLE   0x1u  /* node.Spec.Unschedulable                       */
@@ -284,7 +285,8 @@ typedef struct ca_podset ca_podset;
  *     PREFIX protocol: items are evaluated in order up to the first out-of-scope item u
  *     (a group with an out-of-scope or hostname-dependent pod, or a template flagged
  *     CA_NODE_ANTI_AFFINITY_PODS; a candidate whose pods to move include an out-of-scope
- *     pod).  Item u is reported (status CA_EUNSUPPORTED / reason CA_UNREMOVABLE_OUT_OF_SCOPE),
+ *     pod, or that has more than CA_MAX_MOVED_PODS pods to move: the sweep keeps a
+ *     candidate's distinct destination nodes in a fixed on-chip table).  Item u is reported (status CA_EUNSUPPORTED / reason CA_UNREMOVABLE_OUT_OF_SCOPE),
  *     every later item is CA_ENOTRUN / CA_UNREMOVABLE_NOT_RUN, and *last_index is the
  *     lastIndex item u starts from.  The call returns CA_OK; the caller runs item u on the
  *     reference path and calls again with the remaining items. */
@@ -660,7 +662,10 @@ typedef struct ca_pdb_table {
 /* hints[n_pods]: as ca_find_nodes_to_remove, n_pods = the mirror's pod count (a copy's hint
  * is its destination).  moves[moves_cap]: every committed move in order; *n_moves = their
  * number (if it exceeds moves_cap the first moves_cap are written and the call still
- * completes; ca_plan_last_moves returns all of them). */
+ * completes; ca_plan_last_moves returns all of them).  All or nothing: on an error return
+ * the mirror, pdbs->allowed, hints and *last_index are exactly as before the call (it
+ * runs inside a fork of its own, committed into the caller's state only on success);
+ * only the pod ids its copies took stay consumed (ids are never reused). */
 int ca_plan_removals(ca_mirror* m, const int32_t* candidates, int32_t n_candidates,
                      const uint8_t* dest_mask, const int32_t* cand_status,
                      const int32_t* move_off, const int32_t* move_pods,

@@ -905,6 +905,7 @@ int or_find_nodes_to_remove(or_state* s, const int32_t* candidates, int32_t n_ca
             continue;
         }
         if (node >= 0 && node < s->nodes.n && dest_mask[node] && !(cand_status && cand_status[ci] != 0)) {
+            if (mn > CA_MAX_MOVED_PODS) cut = 1;                          /* casim.h scope */
             for (int32_t i = 0; i < mn && !cut; i++)
                 if (s->pods.a[move_pods[mo + i]].spec.flags & CA_POD_OUT_OF_SCOPE) cut = 1;
             if (cut) {
@@ -993,6 +994,7 @@ int or_plan_removals(or_state* s, const int32_t* candidates, int32_t n_candidate
         if (node >= 0 && node < N)
             for (int64_t i = 0; i < extra[node].n; i++) VEC_PUSH(list, extra[node].a[i]);
         if (valid && !(cand_status && cand_status[ci] != 0)) {
+            if (list.n > CA_MAX_MOVED_PODS) cut = 1;                      /* casim.h scope */
             for (int64_t i = 0; i < list.n && !cut; i++)
                 if (s->pods.a[list.a[i]].spec.flags & CA_POD_OUT_OF_SCOPE) cut = 1;
             if (cut) { r->reason = CA_UNREMOVABLE_OUT_OF_SCOPE; continue; }   /* casim.h scope */

@@ -1,0 +1,40 @@
+"""Phase cycle counters of the device Go sort (CASIM_PROF build: make -C autoscaler_amd/csrc
+prof) on the rank sequences of the heaviest C2 groups (scripts/gpu_job.sh script ...)."""
+import ctypes as C
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("CASIM_LIB_PATH", os.path.join(ROOT, "autoscaler_amd", "lib", "libcasim_prof.so"))
+from autoscaler_amd import native, workloads as W  # noqa: E402
+
+lib = native.load()
+lib.ca_debug_pdq_prof.argtypes = [C.c_void_p, C.c_int32]
+NAMES = ["total", "init", "pop", "phaseA", "plist", "partition", "P2", "P3", "-", "D", "small",
+         "steps", "frames", "part_frames", "small_frames", "elems_partitioned"]
+w = W.c2()
+p = w.table.pods
+sizes = np.diff(w.group_off)
+for g in np.argsort(-sizes)[:3]:
+    idx = w.pod_idx[w.group_off[g]:w.group_off[g + 1]]
+    ac = float(w.templates[g]["node"]["alloc_milli_cpu"]); am = float(w.templates[g]["node"]["alloc_memory"])
+    score = p["score_milli_cpu"][idx] / ac + p["score_memory"][idx] / am
+    ranks = np.unique(-score, return_inverse=True)[1].astype(np.uint32)
+    for store in (1, 2):
+        out = np.zeros(32, np.uint64)
+        native.go_sort_ranks(ranks, store=store)
+        lib.ca_debug_pdq_prof(out.ctypes.data, 1)
+        t0 = time.perf_counter()
+        native.go_sort_ranks(ranks, store=store)
+        dt = time.perf_counter() - t0
+        lib.ca_debug_pdq_prof(out.ctypes.data, 1)
+        print(f"group {g} n={len(ranks)} store={store} call {dt*1e3:.3f} ms")
+        print("   " + "  ".join(f"{n}={int(v)}" for n, v in zip(NAMES, out[:16]) if n != "-"))
+        print("   phaseA sums over waves: breakPatterns=%d choosePivot=%d reverse=%d pis=%d pis_calls(w0)=%d"
+              % tuple(int(x) for x in out[16:21]))
+        print("   LDS partition, sums over waves and steps (/16 = mean wave): P1=%d count=%d scan=%d write=%d P3a=%d P3b=%d"
+              % tuple(int(x) for x in out[21:27]))

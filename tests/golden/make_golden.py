@@ -54,10 +54,10 @@ cases = []
 
 # ---- estimator: TestBinpackingEstimate -------------------------------------
 for name, line, cpu, mem, pods, max_nodes, en, ep in [
-    ("simple resource-based binpacking", "114-120", 350 * 3 - 50, 2 * 1000, est_pods(350, 1000, 0, 10), 0, 5, 10),
-    ("pods-per-node bound binpacking", "121-127", 10000, 20000, est_pods(10, 100, 0, 20), 0, 2, 20),
-    ("hostport conflict forces pod-per-node", "128-134", 1000, 5000, est_pods(200, 1000, 5555, 8), 0, 8, 8),
-    ("limiter cuts binpacking", "135-142", 1000, 5000, est_pods(500, 1000, 0, 20), 5, 5, 10),
+    ("simple resource-based binpacking", "118-125", 350 * 3 - 50, 2 * 1000, est_pods(350, 1000, 0, 10), 0, 5, 10),
+    ("pods-per-node bound binpacking", "126-133", 10000, 20000, est_pods(10, 100, 0, 20), 0, 2, 20),
+    ("hostport conflict forces pod-per-node", "134-141", 1000, 5000, est_pods(200, 1000, 5555, 8), 0, 8, 8),
+    ("limiter cuts binpacking", "142-150", 1000, 5000, est_pods(500, 1000, 0, 20), 5, 5, 10),
 ]:
     cases.append({
         "id": f"estimate/{name}", "source": f"{EST}:{line},164-186", "kind": "estimate",
@@ -70,8 +70,8 @@ for name, line, cpu, mem, pods, max_nodes, en, ep in [
 # inputs are transcribed in full with the reference's expectation; the kernels must REJECT
 # them (CA_EUNSUPPORTED -> UnsupportedByKernels, the Go path runs them), never count them.
 for name, line, key, en, ep in [
-        ("hostname topology spreading with maxSkew=2 forces 2 pods/node", "143-150", "kubernetes.io/hostname", 4, 8),
-        ("zonal topology spreading with maxSkew=2 only allows 2 pods to schedule", "151-158",
+        ("hostname topology spreading with maxSkew=2 forces 2 pods/node", "151-158", "kubernetes.io/hostname", 4, 8),
+        ("zonal topology spreading with maxSkew=2 only allows 2 pods to schedule", "159-166",
          "topology.kubernetes.io/zone", 1, 2)]:
     cases.append({
         "id": f"estimate/{name}", "source": f"{EST}:{line},164-186", "kind": "estimate",
@@ -85,10 +85,10 @@ for name, line, key, en, ep in [
 # ---- predicate checker: TestCheckPredicate ------------------------------------
 n1000 = test_node("n1000", 1000, 2000000)
 for name, line, sched, pod, err in [
-    ("other pod - insuficient cpu", "44-50", [test_pod("p450", 450, 500000)], test_pod("p600", 600, 500000), True),
-    ("other pod - ok", "51-57", [test_pod("p450", 450, 500000)], test_pod("p500", 500, 500000), False),
-    ("empty - insuficient cpu", "58-64", [], test_pod("p8000", 8000, 0), True),
-    ("empty - ok", "65-71", [], test_pod("p600", 600, 500000), False),
+    ("other pod - insuficient cpu", "47-53", [test_pod("p450", 450, 500000)], test_pod("p600", 600, 500000), True),
+    ("other pod - ok", "54-60", [test_pod("p450", 450, 500000)], test_pod("p500", 500, 500000), False),
+    ("empty - insuficient cpu", "61-67", [], test_pod("p8000", 8000, 0), True),
+    ("empty - ok", "68-74", [], test_pod("p600", 600, 500000), False),
 ]:
     expect = {"error": err}
     if err:
@@ -127,14 +127,14 @@ pods = {
     "p4": test_pod("p4", 1000, 100000, node="n4"),
 }
 for name, line, ps, cands, alln, to_remove, unremovable in [
-    ("just an empty node, should be removed", "151-159", [], ["n1"], ["n1"], [["n1", []]], []),
-    ("just a drainable node, but nowhere for pods to go to", "160-168", ["p1", "p2"], ["n2"], ["n2"], [],
+    ("just an empty node, should be removed", "156-163", [], ["n1"], ["n1"], [["n1", []]], []),
+    ("just a drainable node, but nowhere for pods to go to", "165-172", ["p1", "p2"], ["n2"], ["n2"], [],
      [["n2", "NoPlaceToMovePods", None, None]]),
-    ("drainable node, and a mostly empty node that can take its pods", "169-177", ["p1", "p2", "p3"], ["n2", "n3"],
+    ("drainable node, and a mostly empty node that can take its pods", "174-181", ["p1", "p2", "p3"], ["n2", "n3"],
      ["n2", "n3"], [["n2", ["p1", "p2"]]], [["n3", "BlockedByPod", "p3", "NotReplicated"]]),
-    ("drainable node, and a full node that cannot fit anymore pods", "178-186", ["p1", "p2", "p4"], ["n2"],
+    ("drainable node, and a full node that cannot fit anymore pods", "183-190", ["p1", "p2", "p4"], ["n2"],
      ["n2", "n4"], [], [["n2", "NoPlaceToMovePods", None, None]]),
-    ("4 nodes, 1 empty, 1 drainable", "187-195", ["p1", "p2", "p3", "p4"], ["n1", "n2"], ["n1", "n2", "n4", "n3"],
+    ("4 nodes, 1 empty, 1 drainable", "192-199", ["p1", "p2", "p3", "p4"], ["n1", "n2"], ["n1", "n2", "n4", "n3"],
      [["n1", []], ["n2", ["p1", "p2"]]], []),
 ]:
     cases.append({
@@ -158,15 +158,15 @@ cases.append({
 two = [test_node("n1", 1000, 2000000), test_node("n2", 1000, 2000000)]
 p1 = test_pod("p1", 300, 500000, node="n1")
 for name, line, new, acc, want in [
-    ("two new pods, two nodes", "44-62", [test_pod("p2", 800, 500000), test_pod("p3", 500, 500000)], None,
+    ("two new pods, two nodes", "42-60", [test_pod("p2", 800, 500000), test_pod("p3", 500, 500000)], None,
      [["p2", "n2"], ["p3", "n1"]]),
-    ("three new pods, two nodes, no fit", "63-82",
+    ("three new pods, two nodes, no fit", "61-80",
      [test_pod("p2", 800, 500000), test_pod("p3", 500, 500000), test_pod("p4", 700, 500000)], None,
      [["p2", "n2"], ["p3", "n1"]]),
-    ("no new pods, two nodes", "83-94", [], None, []),
-    ("two nodes, but only one acceptable", "95-112", [test_pod("p2", 500, 500000), test_pod("p3", 500, 500000)],
+    ("no new pods, two nodes", "81-92", [], None, []),
+    ("two nodes, but only one acceptable", "93-111", [test_pod("p2", 500, 500000), test_pod("p3", 500, 500000)],
      ["n2"], [["p2", "n2"], ["p3", "n2"]]),
-    ("two nodes, but only one acceptable, no fit", "113-129",
+    ("two nodes, but only one acceptable, no fit", "112-129",
      [test_pod("p2", 500, 500000), test_pod("p3", 500, 500000)], ["n1"], [["p2", "n1"]]),
 ]:
     cases.append({
@@ -175,10 +175,10 @@ for name, line, new, acc, want in [
         "expect": {"statuses": want},
     })
 for name, line, pn in [
-    ("single hint", "166-170", {"p1": "n2"}),
-    ("all on one node", "171-179", {"p1": "n2", "p2": "n2", "p3": "n2"}),
-    ("spread across nodes", "180-188", {"p1": "n1", "p2": "n2", "p3": "n3"}),
-    ("lots of pods", "189-203", {"p1": "n1", "p2": "n1", "p3": "n1", "p4": "n2", "p5": "n2", "p6": "n2",
+    ("single hint", "170-174", {"p1": "n2"}),
+    ("all on one node", "175-183", {"p1": "n2", "p2": "n2", "p3": "n2"}),
+    ("spread across nodes", "184-192", {"p1": "n1", "p2": "n2", "p3": "n3"}),
+    ("lots of pods", "193-207", {"p1": "n1", "p2": "n1", "p3": "n1", "p4": "n2", "p5": "n2", "p6": "n2",
                                  "p7": "n3", "p8": "n3", "p9": "n3"}),
 ]:
     cases.append({
@@ -192,19 +192,19 @@ for name, line, pn in [
 FOS = "CA/core/podlistprocessor/filter_out_schedulable_test.go"
 fnode = [test_node("node", 2000, 100)]          # buildReadyTestNode("node", 2000, 100) (:33)
 for name, line, existing, cand, want_sched, want_unsched in [
-    ("single empty node, no pods", "40-43", [], [], [], []),
-    ("single empty node, single schedulable pod", "44-53", [], [test_pod("pod", 500, 10)], ["pod"], []),
-    ("single empty node, many schedulable pods", "54-67", [],
+    ("single empty node, no pods", "43-46", [], [], [], []),
+    ("single empty node, single schedulable pod", "47-56", [], [test_pod("pod", 500, 10)], ["pod"], []),
+    ("single empty node, many schedulable pods", "57-70", [],
      [test_pod("pod1", 200, 10), test_pod("pod2", 500, 10), test_pod("pod3", 800, 10)], ["pod1", "pod2", "pod3"], []),
-    ("single empty node, single unschedulable pod", "68-77", [], [test_pod("pod1", 3000, 10)], [], ["pod1"]),
-    ("single empty node, various pods", "78-92", [],
+    ("single empty node, single unschedulable pod", "71-80", [], [test_pod("pod1", 3000, 10)], [], ["pod1"]),
+    ("single empty node, various pods", "81-96", [],
      [test_pod("pod1", 200, 10), test_pod("pod2", 500, 10), test_pod("pod3", 1800, 10)], ["pod1", "pod2"], ["pod3"]),
-    ("single empty node, some priority pods", "93-107", [],
+    ("single empty node, some priority pods", "97-112", [],
      [test_pod("pod1", 200, 10), test_pod("pod2", 500, 10, priority=10), test_pod("pod3", 1800, 10, priority=20)],
      ["pod3", "pod1"], ["pod2"]),
-    ("non-empty node with a single pods scheduled", "108-125", [test_pod("pod1", 500, 10, node="node")],
+    ("non-empty node with a single pods scheduled", "113-132", [test_pod("pod1", 500, 10, node="node")],
      [test_pod("pod2", 1000, 10), test_pod("pod3", 300, 10), test_pod("pod4", 300, 10)], ["pod2", "pod3"], ["pod4"]),
-    ("non-empty node with many pods scheduled", "126-143",
+    ("non-empty node with many pods scheduled", "133-153",
      [test_pod("pod1", 500, 10, node="node"), test_pod("pod2", 1000, 10, node="node")],
      [test_pod("pod3", 1000, 10), test_pod("pod4", 300, 10), test_pod("pod5", 300, 10)], ["pod4"], ["pod3", "pod5"]),
 ]:

@@ -86,7 +86,7 @@ def _rank_cases():
     """(ranks, limit) covering the branches of pdqsort_func at workgroup and wave sizes."""
     rng = np.random.default_rng(11)
     cases = []
-    for n in (0, 1, 2, 5, 12, 13, 49, 50, 51, 200, 511, 512, 513, 700, 2000, 5000, 20000, 52736, 60000):
+    for n in (0, 1, 2, 5, 12, 13, 49, 50, 51, 200, 511, 512, 513, 700, 2000, 5000, 20000, 50368, 60000):
         for nk in (1, 2, 7, 64, 250, 4000):
             cases.append((rng.integers(0, nk, n), 0))
     for n in (600, 3000, 40000):

@@ -138,3 +138,31 @@ def test_plan_c4_attributes(oracle):
     W.load_sweep(o, w)
     W.load_sweep(m, w)
     _check(case.plan(o), case.plan(m), "C4")
+
+
+def test_plan_failure_is_atomic(oracle, monkeypatch):
+    """an error in a later speculation round (injected: CASIM_PLAN_FAIL_ROUND=2)
+    leaves nothing of the call behind — mirror rows and pod lists, PDB budgets, hints,
+    lastIndex — and the same call then succeeds exactly like the oracle's."""
+    case = rand_plan_case(101, n_nodes=60, pods_per_node=6, n_pdbs=3, limit=0)
+    m = _mirror()
+    case.load(m)
+    n = len(case.node_recs)
+    before = [m.node_pods(i) for i in range(n)]
+    monkeypatch.setenv("CASIM_PLAN_WINDOW", "8")              # several rounds, commits in each
+    monkeypatch.setenv("CASIM_PLAN_FAIL_ROUND", "3")
+    with pytest.raises(native.CasimError):
+        case.plan(m)
+    monkeypatch.delenv("CASIM_PLAN_FAIL_ROUND")
+    assert [m.node_pods(i) for i in range(n)] == before
+    g = case.plan(m)
+    o_b = oracle.OracleState()
+    case2 = rand_plan_case(101, n_nodes=60, pods_per_node=6, n_pdbs=3, limit=0)
+    case2.load(o_b)
+    o = case2.plan(o_b)
+    # the copies' pod ids: records stored by the failed call are detached, never reused
+    shift = int(g.moves["new_pod"].min()) - int(o.moves["new_pod"].min())
+    assert shift >= 0 and np.array_equal(o.moves["new_pod"] + shift, g.moves["new_pod"])
+    g.moves["new_pod"] -= shift
+    _check(o, g, "after an injected failure")
+    assert m.plan_stats()["rounds"] >= 2

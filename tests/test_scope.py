@@ -255,6 +255,24 @@ def test_remove_node_resident_hints():
     assert h[0] == 2 and h[1] < 0 and h[2] == 1
     m.revert()
     assert m.get_hints(3).tolist() == [3, 1, 2]
+    # two removals at the same position (node 1, then node 2 that shifted into
+    # position 1) keep distinct codes; each Revert restores exactly its own node's hints
+    m.fork()
+    m.remove_node(1)
+    m.remove_node(1)
+    h = m.get_hints(3)
+    assert h[0] == 1 and h[1] < 0 and h[2] < 0 and h[1] != h[2]
+    m.revert()
+    assert m.get_hints(3).tolist() == [3, 1, 2]
+    m.fork()
+    m.remove_node(1)
+    m.fork()
+    m.remove_node(1)
+    m.revert()                                   # only the second removal (node 2) comes back
+    h = m.get_hints(3)
+    assert h[0] == 2 and h[1] < 0 and h[2] == 1
+    m.revert()
+    assert m.get_hints(3).tolist() == [3, 1, 2]
 
 
 # ---------------------------------------------------------------------------
@@ -303,3 +321,109 @@ def test_daemonset_annotation():
     pods, ds, block, err = get_pods_to_move([q], NodeDeleteOptions(), None, [])
     assert err is None and pods == [] and ds == [q]
     assert Interner().encode_pods([q]).pods["flags"][0] & abi.CA_POD_DAEMONSET
+
+
+# ---------------------------------------------------------------------------
+# intern widths and the sweep's destination table (verdict r2): a value past a fixed
+# width (casim.h) routes exactly the objects that need it to the reference path
+# ---------------------------------------------------------------------------
+def _taint_snap(b, n_nodes):
+    s = ClusterSnapshot(backend(b))
+    nodes = []
+    for i in range(n_nodes):
+        n = k8s.build_test_node(f"n{i}", 4000, 8 << 30)
+        n.taints.append(k8s.Taint(f"t{i}", "v", "NoSchedule"))
+        nodes.append(n)
+    s.AddNodes(nodes)
+    return s
+
+
+@pytest.mark.parametrize("b", BACKENDS)
+def test_taint_classes_past_width(b):
+    """66 taint classes: 63 interned, 3 share bit 63.  Pods that tolerate none or all of the
+    overflow taints are exact; a pod tolerating some of them goes to the reference path."""
+    s = _taint_snap(b, 66)
+    it = s.interner
+    assert len(it.taints) == 63 and len(it.taints.overflow) == 3
+    pc = SchedulerBasedPredicateChecker()
+    assert not pc.FitsAnyNode(s, pod("plain"))[0]                        # every node tainted
+    every = pod("every")
+    every.tolerations.append(k8s.Toleration(operator="Exists"))
+    pc.last_index = 64
+    assert pc.FitsAnyNode(s, every)[0] == "n64"                          # an overflow node, tolerated
+    t0 = pod("t0")
+    t0.tolerations.append(k8s.Toleration(key="t0", operator="Exists"))
+    pc.last_index = 3
+    assert pc.FitsAnyNode(s, t0)[0] == "n0"
+    some = pod("some")
+    some.tolerations.append(k8s.Toleration(key="t65", operator="Exists"))
+    table = s.interner.encode_pods([pod("plain"), every, t0, some])
+    assert [bool(f & abi.CA_POD_OUT_OF_SCOPE) for f in table.pods["flags"]] == [False, False, False, True]
+    with pytest.raises(UnsupportedByKernels):
+        pc.FitsAnyNode(s, some)
+    # Estimate on a template carrying an overflow taint: the prefix protocol cuts at the group
+    # with the partially tolerating pod
+    tn = k8s.build_test_node("tmpl", 4000, 8 << 30)
+    tn.taints.append(k8s.Taint("t65", "v", "NoSchedule"))
+    tmpl = NodeInfo(tn, [])
+    est = BinpackingNodeEstimator(pc, s, ThresholdBasedEstimationLimiter(0))
+    assert est.Estimate([every], tmpl)[0] == 1
+    assert est.Estimate([pod("plain2")], tmpl)[0] == 0
+    with pytest.raises(UnsupportedByKernels):
+        est.Estimate([every, some], tmpl)
+
+
+@pytest.mark.parametrize("b", BACKENDS)
+def test_extended_resources_past_width(b):
+    """9 extended resources: a pod requesting the 9th is out of scope, one requesting the
+    1st is simulated, and the 9th on a node's allocatable does not disturb either."""
+    s = ClusterSnapshot(backend(b))
+    n = k8s.build_test_node("n0", 4000, 8 << 30)
+    for r in range(9):
+        n.allocatable[f"example.com/r{r}"] = k8s.Quantity(4)
+    s.AddNodes([n])
+    assert len(s.interner.scalars) == 8 and s.interner.scalars.overflow == {"example.com/r8"}
+    pc = SchedulerBasedPredicateChecker()
+    first = pod("first")
+    first.containers[0].requests["example.com/r0"] = k8s.Quantity(3)
+    assert pc.FitsAnyNode(s, first)[0] == "n0"
+    too_much = pod("too-much")
+    too_much.containers[0].requests["example.com/r0"] = k8s.Quantity(5)
+    assert not pc.FitsAnyNode(s, too_much)[0]
+    ninth = pod("ninth")
+    ninth.containers[0].requests["example.com/r8"] = k8s.Quantity(1)
+    with pytest.raises(UnsupportedByKernels):
+        pc.FitsAnyNode(s, ninth)
+
+
+@pytest.mark.parametrize("b", BACKENDS)
+def test_candidate_past_destination_table(b):
+    """A candidate with more than CA_MAX_MOVED_PODS (128) pods to move is the prefix cut of
+    FindNodesToRemove (k_sweep keeps a candidate's destinations in a 128-entry table): the
+    candidates before it are simulated, it is CA_UNREMOVABLE_OUT_OF_SCOPE, the rest NOT_RUN."""
+    s = ClusterSnapshot(backend(b))
+    big = k8s.build_test_node("big", 64000, 64 << 30, pods=200)
+    small = k8s.build_test_node("small", 4000, 8 << 30)
+    spare = [k8s.build_test_node(f"d{i}", 1000, 8 << 30, pods=1) for i in range(140)]
+    s.AddNodes([small, big] + spare + [k8s.build_test_node("last", 4000, 8 << 30)])
+    s.AddPod(pod("sp", 100, owner="rs"), "small")
+    for i in range(129):                           # 129 pods, each needs a node of its own
+        s.AddPod(pod(f"bp{i}", 100, owner="rs"), "big")
+    s.AddPod(pod("lp", 100, owner="rs"), "last")
+    names = ["small", "big", "last"]
+    ids = [[pid for _, pid in s.pod_ids(n)] for n in names]
+    cand = np.array([s.position(n) for n in names], np.int32)
+    off = np.array([0, 1, 130, 131], np.int32)
+    moves = np.array([i for l in ids for i in l], np.int32)
+    n_nodes = len(s.node_names())
+    out = s.backend.find_nodes_to_remove(cand, np.ones(n_nodes, np.uint8), None, off, moves,
+                                         np.full(int(moves.max()) + 1, -1, np.int32), 0)
+    assert out.results["reason"].tolist() == [0, abi.CA_UNREMOVABLE_OUT_OF_SCOPE, abi.CA_UNREMOVABLE_NOT_RUN]
+    assert out.results["removable"].tolist() == [1, 0, 0]
+    assert out.last_index == int(out.results[1]["last_index_in"])
+    # 128 pods to move stay in scope
+    out = s.backend.find_nodes_to_remove(cand[1:2], np.ones(n_nodes, np.uint8), None, np.array([0, 128], np.int32),
+                                         moves[1:129], np.full(int(moves.max()) + 1, -1, np.int32), 0)
+    assert out.results["reason"].tolist() != [abi.CA_UNREMOVABLE_OUT_OF_SCOPE]
+    with pytest.raises(UnsupportedByKernels):
+        RemovalSimulator(None, s, SchedulerBasedPredicateChecker()).FindNodesToRemove(names, s.node_names())

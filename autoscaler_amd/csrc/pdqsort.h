@@ -47,9 +47,13 @@ __device__ unsigned long long g_pdq_prof[32];
 #define PDQ_WADD(i, t) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) atomicAdd(&g_pdq_prof[i], clock64() - (t)); } while (0)
 // sum over steps of the slowest wave's duration: per-step maxima accumulate in slot i+32
 #define PDQ_WMAX(i, t) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) atomicAdd(&g_pdq_prof[i], clock64() - (t)); } while (0)
+#define PDQ_TMAX(i, v) do { if (blockIdx.x == 0) atomicMax(&g_pdq_prof[i], (unsigned long long)(v)); } while (0)
+#define PDQ_TADD(i, v) do { if (blockIdx.x == 0) atomicAdd(&g_pdq_prof[i], (unsigned long long)(v)); } while (0)
 #else
 #define PDQ_WADD(i, t) (void)0
 #define PDQ_WMAX(i, t) (void)0
+#define PDQ_TMAX(i, v) (void)0
+#define PDQ_TADD(i, v) (void)0
 #define PDQ_T(v) (void)0
 #define PDQ_ADD(i, t) (void)0
 #define PDQ_CNT(i, n) (void)0
@@ -515,6 +519,7 @@ struct Ctl {
     int32_t nf, np, top, base, nsmall, snext;
     uint32_t rmax;
     int32_t x0, x1;            // workgroup partialInsertionSort: search results
+    int32_t sx[3];             //   (LDS store: descent, left landing, right landing)
     uint64_t pe, pf;           //   the two elements it moves
 };
 
@@ -742,6 +747,19 @@ template <class S> __device__ void wg_partition(const S& s, Ctl& c, typename S::
 // ordered because frames are ordered by position: frame f's RMs are base_f .. base_f +
 // t_f - 1 with base_f the pairs of the frames before it, and so are its LMs; the k-th LM
 // from the left (global base_f + k) pairs with RM global base_f + t_f - 1 - k.
+// 4-bit mask of the bytes of x below bound (0 <= bound <= 256), byte i -> bit i
+__device__ inline uint32_t swar_lt4(uint32_t x, uint32_t bound) {
+    if (bound >= 256) return 0xFu;
+    const uint32_t b = bound * 0x01010101u;
+    // per byte x < b: with the high bits split off no borrow crosses a byte, so
+    // d = (x | H) - (b & ~H) has bit 7 set iff x_lo >= b_lo
+    const uint32_t H = 0x80808080u;
+    const uint32_t d = (x | H) - (b & ~H);
+    const uint32_t lt = ((~x & b) | (~(x ^ b) & ~d)) & H;      // bit 7 of each byte
+    const uint32_t m = lt >> 7;                                  // bits 0, 8, 16, 24
+    return (m | (m >> 7) | (m >> 14) | (m >> 21)) & 0xFu;
+}
+
 __device__ inline uint64_t range_bits(int lo, int hi) {     // bits [lo, hi) of a word, clamped to [0, 64)
     lo = max(lo, 0);
     hi = min(hi, 64);
@@ -771,28 +789,29 @@ __device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, 
     B.load(c, kF, false);
     const uint64_t memA = act ? range_bits(A.s - p0, A.e - p0) : 0ull;
     const uint64_t memB = act ? range_bits(B.s - p0, B.e - p0) : 0ull;
-    // P1: pred bits (byte loads, compare), m per frame
+    // P1: pred bits, four ranks per 32-bit compare (SWAR), m per frame
     uint64_t pm = 0;
     if (memA | memB) {
+        // pred = key < bound with bound = pk (+1 for partitionEqual's key <= pk); bound 256
+        // (key <= 255) is every key
+        const uint32_t bA = A.pk + (A.eq ? 1u : 0u), bB = B.pk + (B.eq ? 1u : 0u);
         const uint4* r16 = reinterpret_cast<const uint4*>(s.rk + p0);
+        uint64_t pa = 0, pb = 0;
+        // quarter q = q0 + lane/4 (mod 4): the 16-byte reads of an LDS lane group then
+        // cover distinct banks (lanes are 64 bytes apart)
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
+        for (int q0 = 0; q0 < 4; q0++) {
+            const int q = (q0 + (lane >> 2)) & 3;
             const uint4 x = r16[q];
             const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
             for (int h = 0; h < 4; h++) {
-#pragma unroll
-                for (int bb = 0; bb < 4; bb++) {
-                    const int j = q * 16 + h * 4 + bb;
-                    const uint32_t key = (wv[h] >> (8 * bb)) & 0xFFu;
-                    const bool inb = (memB >> j) & 1ull;
-                    const uint32_t pk = inb ? B.pk : A.pk;
-                    const bool eq = inb ? B.eq : A.eq;
-                    pm |= (uint64_t)(eq ? key <= pk : key < pk) << j;
-                }
+                const int j = q * 16 + h * 4;
+                pa |= (uint64_t)swar_lt4(wv[h], bA) << j;
+                pb |= (uint64_t)swar_lt4(wv[h], bB) << j;
             }
         }
-        pm &= memA | memB;
+        pm = (pa & memA) | (pb & memB);
     }
     add_count(c, memA != 0, A.slot, __builtin_popcountll(pm & memA));
     add_count(c, memB != 0, B.slot, __builtin_popcountll(pm & memB));
@@ -830,43 +849,111 @@ __device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, 
     __syncthreads();
     PDQ_ADD(6, t_p2);
     PDQ_T(t_p3);
-    // P3: swap every LM element with its partner
+    // P3: swap every LM element with its partner, four pairs at a time (partners located
+    // first, then all loads, then all stores: the pairs are disjoint).  Lanes own words 64
+    // positions apart, so visiting LM bits in position order would put the 32 lanes of an
+    // LDS access group on one bank: lane l starts at bit 2l and wraps, in four runs
+    // (A bits >= 2l, B bits >= 2l, A bits below, B bits below).  A run's first partner is
+    // found from its frame's top partner (the partner of the frame's first LM bit in the
+    // word, one binary search per frame) by skipping RM bits backwards.
+#ifdef CASIM_PROF
+    int n_it = 0;
+#endif
     if (lmask) {
-        uint32_t gl = pre >> 16;                     // global LM index of the word's first LM
-        uint64_t lm = lmask;
-        int ww = -1, bit = 0;                        // the current partner (word, bit)
-        int prevf = -1;
-        while (lm) {
-            const int j = __builtin_ctzll(lm);
-            lm &= lm - 1;
-            const int p = p0 + j;
-            const bool inb = (memB >> j) & 1ull;
-            const int kk = inb ? kF : kF - 1;
-            const int slot = inb ? B.slot : A.slot;
-            const uint32_t base = (uint32_t)c.fo[kk];
-            const uint32_t t = (uint32_t)c.t[slot];
-            const uint32_t k = gl - base;
-            const uint32_t gR = base + t - 1 - k;
-            if (kk != prevf) {                       // locate: the word holding RM gR
-                int lo = 0, hi = W;
-                while (hi - lo > 1) {
-                    const int mid = (lo + hi) >> 1;
-                    if (s.rmp[mid] <= gR) lo = mid; else hi = mid;
-                }
-                ww = lo;
-                uint64_t m = s.rmb[ww];
-                for (uint32_t r = gR - s.rmp[ww]; r > 0; r--) m &= m - 1;
-                bit = __builtin_ctzll(m);
-                prevf = kk;
-            } else {                                 // the previous RM (gR one lower)
-                uint64_t m = s.rmb[ww] & ((1ull << bit) - 1);
-                while (!m) m = s.rmb[--ww];
-                bit = 63 - __builtin_clzll(m);
+        const int rot = (2 * lane) & 63;
+        const uint64_t below = rot ? ((1ull << rot) - 1) : 0ull;
+        const uint64_t lmA = lmask & memA, lmB = lmask & memB;
+        const uint32_t gl0 = pre >> 16;              // global LM index of the word's first LM
+        // (ww, bit): a cursor on an RM bit; wb = rmb[ww]
+        auto locate = [&](uint32_t gR, int& ww, int& bit, uint64_t& wb) {
+            int lo = 0, hi = W;
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (s.rmp[mid] <= gR) lo = mid; else hi = mid;
             }
-            swp(s, p, ww * 64 + bit);
-            gl++;
+            ww = lo;
+            wb = s.rmb[ww];
+            bit = select_bit(wb, (int)(gR - s.rmp[ww]));
+        };
+        auto back = [&](int k, int& ww, int& bit, uint64_t& wb) {     // k RM bits lower
+            uint64_t m = wb & ((1ull << bit) - 1);
+            for (;;) {
+                const int pc = __builtin_popcountll(m);
+                if (k <= pc) {
+                    if (k > 0) bit = select_bit(m, pc - k);
+                    return;
+                }
+                k -= pc;
+                wb = s.rmb[--ww];
+                m = wb;
+                bit = 64;                            // (every bit of the new word lies below)
+            }
+        };
+        auto run = [&](uint64_t M, int ww, int bit, uint64_t wb) {
+            bool first = true;
+            while (M) {
+#ifdef CASIM_PROF
+                n_it++;
+#endif
+                int pp[4], qq[4];
+                int cnt = 0;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (!M) { pp[u] = qq[u] = 0; continue; }
+                    const int j = __builtin_ctzll(M);
+                    M &= M - 1;
+                    if (!first) {                    // the previous RM
+                        uint64_t m = wb & ((1ull << bit) - 1);
+                        while (!m) { wb = s.rmb[--ww]; m = wb; }
+                        bit = 63 - __builtin_clzll(m);
+                    }
+                    first = false;
+                    pp[u] = p0 + j;
+                    qq[u] = ww * 64 + bit;
+                    cnt++;
+                }
+                uint32_t vp[4], vq[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (u < cnt) { vp[u] = s.ld(pp[u]); vq[u] = s.ld(qq[u]); }
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (u < cnt) { s.st(pp[u], vq[u]); s.st(qq[u], vp[u]); }
+            }
+        };
+        int wwA = 0, bitA = 0, wwB = 0, bitB = 0;
+        uint64_t wbA = 0, wbB = 0;
+        if (lmA) {
+            const uint32_t base = (uint32_t)c.fo[kF - 1], t = (uint32_t)c.t[A.slot];
+            locate(base + t - 1 - (gl0 - base), wwA, bitA, wbA);
+            int ww = wwA, bit = bitA;
+            uint64_t wb = wbA;
+            back(__builtin_popcountll(lmA & below), ww, bit, wb);
+            run(lmA & ~below, ww, bit, wb);
+        }
+        if (lmB) {
+            const uint32_t base = (uint32_t)c.fo[kF], t = (uint32_t)c.t[B.slot];
+            const uint32_t glB = gl0 + (uint32_t)__builtin_popcountll(lmA);
+            locate(base + t - 1 - (glB - base), wwB, bitB, wbB);
+            int ww = wwB, bit = bitB;
+            uint64_t wb = wbB;
+            back(__builtin_popcountll(lmB & below), ww, bit, wb);
+            run(lmB & ~below, ww, bit, wb);
+        }
+        if (lmA & below) run(lmA & below, wwA, bitA, wbA);
+        if (lmB & below) run(lmB & below, wwB, bitB, wbB);
+    }
+#ifdef CASIM_PROF
+    {
+        int itw = n_it;
+        for (int d = 32; d; d >>= 1) itw = max(itw, __shfl_xor(itw, d, 64));
+        if (lane == 0 && blockIdx.x == 0) {
+            atomicAdd(&g_pdq_prof[27], clock64() - t_p3);
+            atomicAdd(&g_pdq_prof[28], (unsigned long long)itw);
+            atomicMax(&g_pdq_prof[29], (unsigned long long)itw);
         }
     }
+#endif
     __syncthreads();
     PDQ_ADD(7, t_p3);
 }
@@ -902,55 +989,192 @@ template <class S> __device__ void wg_shift(const S& s, Ctl& c, int lo, int hi, 
     }
 }
 
+// LDS store: the same block move on 32-bit words of each array (two positions per word
+// of e, four of rk), the one-element offset taken from the neighbouring word
+template <int EB> __device__ void shift_words(uint32_t* __restrict__ w32, int dlo, int dhi, int dir) {
+    constexpr int EPW = 32 / EB, PER = 8;
+    const int tid = threadIdx.x;
+    const int w0 = dlo / EPW, w1 = dhi / EPW, nw = w1 - w0 + 1;
+    for (int done = 0; done < nw; done += NT * PER) {
+        uint32_t nv[PER];
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int off = u * NT + tid;
+            nv[u] = 0;
+            if (off < nw - done) {
+                const int w = dir > 0 ? w1 - done - off : w0 + done + off;
+                const uint32_t cur = w32[w];
+                const uint32_t nb = dir > 0 ? (w > 0 ? w32[w - 1] : 0u) : w32[w + 1];
+                const uint32_t sh = dir > 0 ? (cur << EB) | (nb >> (32 - EB)) : (cur >> EB) | (nb << (32 - EB));
+                const int e0 = max(dlo, w * EPW) - w * EPW, e1 = min(dhi, w * EPW + EPW - 1) - w * EPW;
+                const uint32_t hi_m = e1 + 1 >= EPW ? ~0u : ((1u << ((e1 + 1) * EB)) - 1);
+                const uint32_t m = hi_m & ~((1u << (e0 * EB)) - 1);
+                nv[u] = (sh & m) | (cur & ~m);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int off = u * NT + tid;
+            if (off < nw - done) w32[dir > 0 ? w1 - done - off : w0 + done + off] = nv[u];
+        }
+        __syncthreads();
+    }
+}
+
+__device__ void wg_shift(const LdsStore& s, Ctl&, int lo, int hi, int dir) {
+    shift_words<16>(reinterpret_cast<uint32_t*>(s.e), lo + dir, hi + dir, dir);
+    shift_words<8>(reinterpret_cast<uint32_t*>(s.rk), lo + dir, hi + dir, dir);
+}
+
+// Workgroup searches of partialInsertionSort, outward from the start in windows (one
+// barrier per window): the first descent in [i, b), the last q in [lo, top] with key <=
+// kmax, the first j in [bot, b) with key >= kmin.  Generic: one position per thread per
+// window; LDS store: four per thread (32-bit rank words, SWAR byte compares).
+template <class S> __device__ int wg_find_descent(const S& s, Ctl& c, int i, int b) {
+    const int tid = threadIdx.x;
+    if (tid == 0) c.x0 = b;
+    __syncthreads();
+    for (int q0 = i; q0 < b; q0 += NT) {
+        const int q = q0 + tid;
+        const bool d = q < b && K(s, q) < K(s, q - 1);
+        if (d) atomicMin(&c.x0, q);
+        if (__syncthreads_or(d)) break;
+    }
+    const int r = c.x0;
+    __syncthreads();
+    return r;
+}
+template <class S> __device__ int wg_find_left(const S& s, Ctl& c, int lo, int top, uint32_t kmax) {
+    const int tid = threadIdx.x;
+    if (tid == 0) c.x0 = -1;
+    __syncthreads();
+    for (int t0 = top; t0 >= lo; t0 -= NT) {
+        const int q = t0 - tid;
+        const bool d = q >= lo && K(s, q) <= kmax;
+        if (d) atomicMax(&c.x0, q);
+        if (__syncthreads_or(d)) break;
+    }
+    const int r = c.x0;
+    __syncthreads();
+    return r;
+}
+template <class S> __device__ int wg_find_right(const S& s, Ctl& c, int bot, int b, uint32_t kmin) {
+    const int tid = threadIdx.x;
+    if (tid == 0) c.x0 = b;
+    __syncthreads();
+    for (int b0 = bot; b0 < b; b0 += NT) {
+        const int j = b0 + tid;
+        const bool d = j < b && K(s, j) >= kmin;
+        if (d) atomicMin(&c.x0, j);
+        if (__syncthreads_or(d)) break;
+    }
+    const int r = c.x0;
+    __syncthreads();
+    return r;
+}
+
+// bytes of x below the bytes of y, byte i -> bit i
+__device__ inline uint32_t swar_ltv4(uint32_t x, uint32_t y) {
+    const uint32_t H = 0x80808080u;
+    const uint32_t d = (x | H) - (y & ~H);
+    const uint32_t lt = ((~x & y) | (~(x ^ y) & ~d)) & H;
+    const uint32_t m = lt >> 7;
+    return (m | (m >> 7) | (m >> 14) | (m >> 21)) & 0xFu;
+}
+__device__ inline uint32_t nib_range(int w, int lo, int hi) {     // bits of positions [lo, hi] in word w
+    const int e0 = max(lo - 4 * w, 0), e1 = min(hi - 4 * w, 3);
+    if (e1 < e0) return 0u;
+    return ((2u << e1) - 1) & ~((1u << e0) - 1);
+}
+
+__device__ int wg_find_descent(const LdsStore& s, Ctl& c, int i, int b) {
+    const int tid = threadIdx.x;
+    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(s.rk);
+    if (tid == 0) c.x0 = b;
+    __syncthreads();
+    for (int w0 = i >> 2; 4 * w0 < b; w0 += NT) {
+        const int w = w0 + tid;
+        int q = INT_MAX;
+        if (4 * w < b) {
+            const uint32_t x = r32[w];
+            const uint32_t y = (x << 8) | (w > 0 ? r32[w - 1] >> 24 : 0u);      // rk[q - 1]
+            const uint32_t m = swar_ltv4(x, y) & nib_range(w, i, b - 1);
+            if (m) q = 4 * w + __builtin_ctz(m);
+        }
+        if (q != INT_MAX) atomicMin(&c.x0, q);
+        if (__syncthreads_or(q != INT_MAX)) break;
+    }
+    const int r = c.x0;
+    __syncthreads();
+    return r;
+}
+__device__ int wg_find_left(const LdsStore& s, Ctl& c, int lo, int top, uint32_t kmax) {
+    const int tid = threadIdx.x;
+    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(s.rk);
+    if (tid == 0) c.x0 = -1;
+    __syncthreads();
+    for (int w0 = top >> 2; 4 * w0 + 3 >= lo; w0 -= NT) {
+        const int w = w0 - tid;
+        int q = -1;
+        if (w >= 0 && 4 * w + 3 >= lo) {
+            const uint32_t m = swar_lt4(r32[w], kmax + 1) & nib_range(w, lo, top);
+            if (m) q = 4 * w + 31 - __builtin_clz(m);
+        }
+        if (q >= 0) atomicMax(&c.x0, q);
+        if (__syncthreads_or(q >= 0)) break;
+    }
+    const int r = c.x0;
+    __syncthreads();
+    return r;
+}
+__device__ int wg_find_right(const LdsStore& s, Ctl& c, int bot, int b, uint32_t kmin) {
+    const int tid = threadIdx.x;
+    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(s.rk);
+    if (tid == 0) c.x0 = b;
+    __syncthreads();
+    for (int w0 = bot >> 2; 4 * w0 < b; w0 += NT) {
+        const int w = w0 + tid;
+        int j = INT_MAX;
+        if (4 * w < b) {
+            const uint32_t m = ~swar_lt4(r32[w], kmin) & nib_range(w, bot, b - 1);
+            if (m) j = 4 * w + __builtin_ctz(m);
+        }
+        if (j != INT_MAX) atomicMin(&c.x0, j);
+        if (__syncthreads_or(j != INT_MAX)) break;
+    }
+    const int r = c.x0;
+    __syncthreads();
+    return r;
+}
+
 template <class S> __device__ bool wg_partial_insertion(const S& s, Ctl& c, int a, int b) {
     constexpr int maxSteps = 5, shortestShifting = 50;
     const int tid = threadIdx.x;
     int i = a + 1;
     for (int step = 0; step < maxSteps; step++) {
-        // first i' in [i, b) with less(i', i'-1): positions striped over the threads
-        if (tid == 0) c.x0 = b;
-        __syncthreads();
-        for (int q0 = i; q0 < b; q0 += NT) {
-            const int q = q0 + tid;
-            const bool d = q < b && K(s, q) < K(s, q - 1);
-            if (d) atomicMin(&c.x0, q);
-            if (__syncthreads_or(d)) break;
-        }
-        i = c.x0;
+        PDQ_T(t_d0);
+        i = wg_find_descent(s, c, i, b);
+        PDQ_ADD(21, t_d0);
+        PDQ_CNT(26, 1);               // first i' in [i, b) with less(i', i'-1)
         if (i == b) return true;
         if (b - a < shortestShifting) return false;
-        __syncthreads();
         if (tid == 0) {
             swp(s, i, i - 1);
             c.pe = (uint64_t)s.ld(i - 1);          // the smaller one, bubbling left
             c.pf = (uint64_t)s.ld(i);              // the greater one, bubbling right
-            c.x0 = -1;
-            c.x1 = b;
         }
         __syncthreads();
         const typename S::Elem e = (typename S::Elem)c.pe, f = (typename S::Elem)c.pf;
-        const uint32_t ke = S::key(e), kf = S::key(f);
         const bool left = i - a >= 2, right = b - i >= 2;
-        const int qmin = a > 0 ? a - 1 : 0;     // key(a-1) <= every key of [a, b): the walk stops there
-        // left: the largest q in [qmin, i-2] with key(q) <= ke; right: the smallest j in
-        // [i+1, b) with !(key(j) < kf); windows of NT positions outward from i
-        if (left)
-            for (int top = i - 2; top >= qmin; top -= NT) {
-                const int q = top - tid;
-                const bool d = q >= qmin && K(s, q) <= ke;
-                if (d) atomicMax(&c.x0, q);
-                if (__syncthreads_or(d)) break;
-            }
-        if (right)
-            for (int bot = i + 1; bot < b; bot += NT) {
-                const int j = bot + tid;
-                const bool d = j < b && !(K(s, j) < kf);
-                if (d) atomicMin(&c.x1, j);
-                if (__syncthreads_or(d)) break;
-            }
-        __syncthreads();
-        const int landL = c.x0 + 1;             // (no q at all: only when qmin == 0 -> 0)
-        const int landR = c.x1 - 1;
+        const int qmin = a > 0 ? a - 1 : 0;        // key(a-1) <= every key of [a, b): the walk stops there
+        // left: the last q in [qmin, i-2] with key(q) <= key(e); right: the first j in
+        // [i+1, b) with !(key(j) < key(f))
+        PDQ_T(t_s0);
+        const int landL = left ? wg_find_left(s, c, qmin, i - 2, S::key(e)) + 1 : i - 1;   // (none: qmin == 0 -> 0)
+        const int landR = right ? wg_find_right(s, c, i + 1, b, S::key(f)) - 1 : i;
+        PDQ_ADD(22, t_s0);
+        PDQ_T(t_h0);
         if (left && landL < i - 1) {
             wg_shift(s, c, landL, i - 2, +1);
             if (tid == 0) s.st(landL, e);
@@ -961,6 +1185,151 @@ template <class S> __device__ bool wg_partial_insertion(const S& s, Ctl& c, int 
         }
         __threadfence_block();
         __syncthreads();
+        PDQ_ADD(23, t_h0);
+        PDQ_CNT(24, (uint64_t)max(i - 1 - landL, 0) + (uint64_t)max(landR - i, 0));
+        PDQ_CNT(25, (uint64_t)(b - a));
+    }
+    return false;
+}
+
+// LDS store: one step is a descent search, the two landing searches and one rewrite of
+// [landL, landR] — swap(i, i-1) and the two bubbling loops together are the rotation
+//   new[landL] = old[i], new[p] = old[p-1] on (landL, i-1], new[p] = old[p+1] on [i, landR),
+//   new[landR] = old[i-1]
+// done on whole words (quads of positions: two 16-bit words of e, one 8-bit word of rk).
+// Searches reduce per wavefront first (lanes cover ascending or descending words, so the
+// first hit lane holds the wave's extreme) and publish one LDS atomic per wave into a
+// slot set before the barrier that precedes its use; a step has no barrier beyond one per
+// search window and two per rewrite round.
+template <int EB> __device__ inline uint32_t slot_mask(int p0, int lo, int hi) {
+    constexpr int EPW = 32 / EB;
+    const int e0 = max(lo - p0, 0), e1 = min(hi - p0, EPW - 1);
+    if (e1 < e0) return 0u;
+    const uint32_t up = (e1 + 1) * EB >= 32 ? ~0u : ((1u << ((e1 + 1) * EB)) - 1);
+    return up & ~((1u << (e0 * EB)) - 1);
+}
+template <int EB> __device__ inline uint32_t rotate_word(uint32_t cur, uint32_t prv, uint32_t nxt, int p0,
+                                                        int L, int i, int R, uint32_t ev, uint32_t fv) {
+    const uint32_t shl = (cur << EB) | (prv >> (32 - EB));      // old[p - 1]
+    const uint32_t shr = (cur >> EB) | (nxt << (32 - EB));      // old[p + 1]
+    const uint32_t mE = slot_mask<EB>(p0, L, L), mF = slot_mask<EB>(p0, R, R);
+    const uint32_t mL = slot_mask<EB>(p0, L + 1, i - 1), mR = slot_mask<EB>(p0, i, R - 1);
+    const uint32_t rep = EB == 8 ? 0x01010101u : 0x00010001u;
+    return (cur & ~(mE | mF | mL | mR)) | (shl & mL) | (shr & mR) | ((ev * rep) & mE) | ((fv * rep) & mF);
+}
+
+__device__ bool wg_partial_insertion(const LdsStore& s, Ctl& c, int a, int b) {
+    constexpr int maxSteps = 5, shortestShifting = 50;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(s.rk);
+    uint32_t* w32 = reinterpret_cast<uint32_t*>(s.rk);
+    uint32_t* e32 = reinterpret_cast<uint32_t*>(s.e);
+    if (tid == 0) { c.sx[0] = b; c.sx[1] = -1; c.sx[2] = b; }
+    __syncthreads();
+    int i = a + 1;
+    for (int step = 0; step < maxSteps; step++) {
+        PDQ_T(t_d0);
+        for (int w0 = i >> 2; 4 * w0 < b; w0 += NT) {          // first descent in [i, b)
+            const int w = w0 + tid;
+            bool hit = false;
+            int q = 0;
+            if (4 * w < b) {
+                const uint32_t x = r32[w];
+                const uint32_t y = (x << 8) | (w > 0 ? r32[w - 1] >> 24 : 0u);
+                const uint32_t m = swar_ltv4(x, y) & nib_range(w, i, b - 1);
+                hit = m != 0;
+                q = 4 * w + __builtin_ctz(m | 16u);
+            }
+            const uint64_t bal = __ballot(hit);
+            if (bal && lane == __builtin_ctzll(bal)) atomicMin(&c.sx[0], q);
+            __syncthreads();
+            if (c.sx[0] < 4 * (w0 + NT)) break;     // (a later window's hits lie beyond it)
+        }
+        i = c.sx[0];
+        PDQ_ADD(21, t_d0);
+        PDQ_CNT(26, 1);
+        if (i == b) return true;
+        if (b - a < shortestShifting) return false;
+        PDQ_T(t_s0);
+        const uint32_t ev = s.rk[i], fv = s.rk[i - 1];            // the smaller one bubbles left, the greater right
+        const uint32_t ee = s.e[i], fe = s.e[i - 1];
+        int landL = i - 1, landR = i;
+        if (i - a >= 2) {                  // the last q in [qmin, i-2] with rk[q] <= ev, plus one
+            const int lo = a > 0 ? a - 1 : 0, top = i - 2;
+            for (int w0 = top >> 2; 4 * w0 + 3 >= lo; w0 -= NT) {
+                const int w = w0 - tid;
+                bool hit = false;
+                int q = 0;
+                if (w >= 0 && 4 * w + 3 >= lo) {
+                    const uint32_t m = swar_lt4(r32[w], ev + 1) & nib_range(w, lo, top);
+                    hit = m != 0;
+                    q = 4 * w + 31 - __builtin_clz(m | 1u);
+                }
+                const uint64_t bal = __ballot(hit);
+                if (bal && lane == __builtin_ctzll(bal)) atomicMax(&c.sx[1], q);
+                __syncthreads();
+                if (c.sx[1] >= 4 * (w0 - NT + 1)) break;
+            }
+            landL = c.sx[1] + 1;           // (none found: qmin == 0 and landL = 0)
+        }
+        if (b - i >= 2) {                  // the first j in [i+1, b) with rk[j] >= fv, minus one
+            for (int w0 = (i + 1) >> 2; 4 * w0 < b; w0 += NT) {
+                const int w = w0 + tid;
+                bool hit = false;
+                int q = 0;
+                if (4 * w < b) {
+                    const uint32_t m = ~swar_lt4(r32[w], fv) & nib_range(w, i + 1, b - 1);
+                    hit = m != 0;
+                    q = 4 * w + __builtin_ctz(m | 16u);
+                }
+                const uint64_t bal = __ballot(hit);
+                if (bal && lane == __builtin_ctzll(bal)) atomicMin(&c.sx[2], q);
+                __syncthreads();
+                if (c.sx[2] < 4 * (w0 + NT)) break;
+            }
+            landR = c.sx[2] - 1;
+        }
+        PDQ_ADD(22, t_s0);
+        PDQ_T(t_h0);
+        // rewrite [landL, landR] by quads: left quads from the centre quad down, right quads
+        // up from the one after it; a round reads only words no earlier round wrote
+        const int qL = landL >> 2, qc = (i - 1) >> 2, qR = landR >> 2;
+        const int nl = qc - qL + 1, nr = qR - qc;
+        for (int done = 0; done < max(nl, nr); done += NT) {
+            uint32_t nv[2][3];
+            int qq[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int k = done + tid;
+                qq[u] = -1;
+                if (u == 0 ? k >= nl : k >= nr) continue;
+                const int v = u == 0 ? qc - k : qc + 1 + k;
+                const int p0 = 4 * v;
+                const uint32_t lo = e32[2 * v], hi = e32[2 * v + 1];
+                const uint32_t pe = v > 0 ? e32[2 * v - 1] : 0u;
+                const bool up = p0 + 4 <= landR;
+                const uint32_t ne = up ? e32[2 * v + 2] : 0u;
+                const uint32_t cr = w32[v];
+                const uint32_t pr = v > 0 ? w32[v - 1] : 0u, nr8 = up ? w32[v + 1] : 0u;
+                nv[u][0] = rotate_word<16>(lo, pe, hi, p0, landL, i, landR, ee, fe);
+                nv[u][1] = rotate_word<16>(hi, lo, ne, p0 + 2, landL, i, landR, ee, fe);
+                nv[u][2] = rotate_word<8>(cr, pr, nr8, p0, landL, i, landR, ev, fv);
+                qq[u] = v;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                if (qq[u] < 0) continue;
+                e32[2 * qq[u]] = nv[u][0];
+                e32[2 * qq[u] + 1] = nv[u][1];
+                w32[qq[u]] = nv[u][2];
+            }
+            if (done == 0 && tid == 0) { c.sx[0] = b; c.sx[1] = -1; c.sx[2] = b; }   // the next step's slots
+            __syncthreads();
+        }
+        PDQ_ADD(23, t_h0);
+        PDQ_CNT(24, (uint64_t)(i - 1 - landL) + (uint64_t)(landR - i));
+        PDQ_CNT(25, (uint64_t)(b - a));
     }
     return false;
 }

@@ -3,6 +3,7 @@
 #   scripts/gpu_job.sh tests "<pytest -k expr or file list>"   GPU tests
 #   scripts/gpu_job.sh bench "<bench.py args>"                   one bench line
 #   scripts/gpu_job.sh prof  "<bench.py args>"                   rocprofv3 kernel stats of a bench run
+#   scripts/gpu_job.sh pmc   "<counters>|<script args>"           one rocprofv3 counter pass over a script
 # Every GPU step has its own time limit; the chain stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
@@ -27,6 +28,13 @@ while [[ $# -gt 0 ]]; do
       cd "$GRAFT_REPO_ROOT"
       [[ $rc -eq 0 ]] || { echo "PROF FAILED rc=$rc"; tail -30 gpurun_out/prof.log; exit $rc; }
       echo PROF_OK ;;
+    pmc)
+      ctrs="${arg%%|*}"; sargs="${arg#*|}"; tag=$(echo "$ctrs" | tr ' ' '_' | cut -c1-60)
+      cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $ctrs -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$tag" -o run \
+        --output-format csv -- python3 $GRAFT_REPO_ROOT/$sargs > "$GRAFT_REPO_ROOT/gpurun_out/pmc_$tag.log" 2>&1; rc=$?
+      cd "$GRAFT_REPO_ROOT"
+      [[ $rc -eq 0 ]] || { echo "PMC FAILED rc=$rc"; tail -30 "gpurun_out/pmc_$tag.log"; exit $rc; }
+      echo "PMC_OK $tag" ;;
     script)
       timeout -k 10 600 python -u $arg > gpurun_out/script.log 2>&1; rc=$?
       tail -40 gpurun_out/script.log

@@ -36,5 +36,7 @@ for g in np.argsort(-sizes)[:3]:
         print("   " + "  ".join(f"{n}={int(v)}" for n, v in zip(NAMES, out[:16]) if n != "-"))
         print("   phaseA sums over waves: breakPatterns=%d choosePivot=%d reverse=%d pis=%d pis_calls(w0)=%d"
               % tuple(int(x) for x in out[16:21]))
-        print("   LDS partition, sums over waves and steps (/16 = mean wave): P1=%d count=%d scan=%d write=%d P3a=%d P3b=%d"
+        print("   pis (wave 0): descent=%d land=%d shift=%d moved=%d len_sum=%d steps=%d"
               % tuple(int(x) for x in out[21:27]))
+        print("   P3 waves: cycles_sum=%d iters_sum=%d iters_max=%d"
+              % tuple(int(x) for x in out[27:30]))

@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <climits>
+#include <type_traits>
 
 namespace casim {
 namespace pdq {
@@ -80,7 +81,7 @@ struct LdsStore {
     using Elem = uint32_t;
     uint16_t* e;
     uint8_t* rk;
-    uint64_t* rmb;           // workgroup partition: right-zone pass bits per 64-position word
+    uint64_t* rmb;           // workgroup partition: moved positions (LM | RM) per 64-position word
     uint16_t* rmp;           //   and their exclusive prefix counts per word
     __device__ Elem ld(int i) const { return ((uint32_t)rk[i] << 16) | e[i]; }
     __device__ void st(int i, Elem v) const { e[i] = (uint16_t)v; rk[i] = (uint8_t)(v >> 16); }
@@ -824,7 +825,7 @@ __device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, 
     const uint64_t lmA = ~pm & memA & leftA, lmB = ~pm & memB & leftB;
     const uint64_t rmask = (pm & memA & ~leftA) | (pm & memB & ~leftB);
     const uint64_t lmask = lmA | lmB;
-    if (act) s.rmb[tid] = rmask;
+    if (act) s.rmb[tid] = lmask | rmask;
     add_count_t(c, lmA != 0, A.slot, __builtin_popcountll(lmA));
     add_count_t(c, lmB != 0, B.slot, __builtin_popcountll(lmB));
     // exclusive block scan of (LM << 16 | RM) per word (counts < 2^16: n <= PDQ_LDS_N)
@@ -838,8 +839,9 @@ __device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, 
     __syncthreads();
     uint32_t pre = incl - own;
     for (int q = 0; q < (tid >> 6); q++) pre += (uint32_t)c.wsum[q];
-    if (act) s.rmp[tid] = (uint16_t)(pre & 0xFFFFu);
-    if (tid == W - 1) s.rmp[W] = (uint16_t)((pre + own) & 0xFFFFu);
+    // combined (LM + RM) prefix per word: n <= PDQ_LDS_N < 2^16
+    if (act) s.rmp[tid] = (uint16_t)((pre >> 16) + (pre & 0xFFFFu));
+    if (tid == W - 1) s.rmp[W] = (uint16_t)(((pre + own) >> 16) + ((pre + own) & 0xFFFFu));
     if (tid < 64) {
         // pair base of every frame in position order (c.t holds the pair counts; t[] of
         // the frames is read again in P3)
@@ -849,68 +851,64 @@ __device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, 
     __syncthreads();
     PDQ_ADD(6, t_p2);
     PDQ_T(t_p3);
-    // P3: swap every LM element with its partner, four pairs at a time (partners located
-    // first, then all loads, then all stores: the pairs are disjoint).  Lanes own words 64
-    // positions apart, so visiting LM bits in position order would put the 32 lanes of an
-    // LDS access group on one bank: lane l starts at bit 2l and wraps, in four runs
-    // (A bits >= 2l, B bits >= 2l, A bits below, B bits below).  A run's first partner is
-    // found from its frame's top partner (the partner of the frame's first LM bit in the
-    // word, one binary search per frame) by skipping RM bits backwards.
+    // P3: the pairs, split evenly over the workgroup's threads in runs of consecutive
+    // global pair indices.  In combined (LM | RM) order frame f (pair base fs, end fe)
+    // holds its LMs at [2fs, fs+fe) and its RMs at [fs+fe, 2fe): pair k of the frame joins
+    // combined bits fs + k and 2fe - 1 - k + fs.  A run locates both ends once (binary
+    // search of the combined prefix counts), then walks the bitmap, forwards on the left,
+    // backwards on the right; four pairs per iteration (all loads, then all stores).
 #ifdef CASIM_PROF
     int n_it = 0;
 #endif
-    if (lmask) {
-        const int rot = (2 * lane) & 63;
-        const uint64_t below = rot ? ((1ull << rot) - 1) : 0ull;
-        const uint64_t lmA = lmask & memA, lmB = lmask & memB;
-        const uint32_t gl0 = pre >> 16;              // global LM index of the word's first LM
-        // (ww, bit): a cursor on an RM bit; wb = rmb[ww]
-        auto locate = [&](uint32_t gR, int& ww, int& bit, uint64_t& wb) {
+    {
+        const int P = c.fo[np];
+        const int per = (P + NT - 1) / NT;
+        int k = tid * per;
+        const int k1 = min(P, k + per);
+        auto locate = [&](int ci, int& ww, int& bit, uint64_t& wb) {
             int lo = 0, hi = W;
             while (hi - lo > 1) {
                 const int mid = (lo + hi) >> 1;
-                if (s.rmp[mid] <= gR) lo = mid; else hi = mid;
+                if ((int)s.rmp[mid] <= ci) lo = mid; else hi = mid;
             }
             ww = lo;
             wb = s.rmb[ww];
-            bit = select_bit(wb, (int)(gR - s.rmp[ww]));
+            bit = select_bit(wb, ci - (int)s.rmp[ww]);
         };
-        auto back = [&](int k, int& ww, int& bit, uint64_t& wb) {     // k RM bits lower
+        auto next_l = [&](int& ww, int& bit, uint64_t& wb) {
+            uint64_t m = bit < 63 ? wb & (~0ull << (bit + 1)) : 0ull;
+            while (!m) { wb = s.rmb[++ww]; m = wb; }
+            bit = __builtin_ctzll(m);
+        };
+        auto prev_r = [&](int& ww, int& bit, uint64_t& wb) {
             uint64_t m = wb & ((1ull << bit) - 1);
-            for (;;) {
-                const int pc = __builtin_popcountll(m);
-                if (k <= pc) {
-                    if (k > 0) bit = select_bit(m, pc - k);
-                    return;
-                }
-                k -= pc;
-                wb = s.rmb[--ww];
-                m = wb;
-                bit = 64;                            // (every bit of the new word lies below)
-            }
+            while (!m) { wb = s.rmb[--ww]; m = wb; }
+            bit = 63 - __builtin_clzll(m);
         };
-        auto run = [&](uint64_t M, int ww, int bit, uint64_t wb) {
-            bool first = true;
-            while (M) {
+        while (k < k1) {
+            int lo = 0, hi = np;                     // frame of pair k: the last f with fo[f] <= k
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (c.fo[mid] <= k) lo = mid; else hi = mid;
+            }
+            const int fs = c.fo[lo], fe = c.fo[lo + 1];
+            const int kend = min(k1, fe);
+            int wl, bl, wr, br;
+            uint64_t wbl, wbr;
+            locate(fs + k, wl, bl, wbl);
+            locate(2 * fe - 1 - k + fs, wr, br, wbr);
+            for (;;) {
 #ifdef CASIM_PROF
                 n_it++;
 #endif
                 int pp[4], qq[4];
-                int cnt = 0;
+                const int cnt = min(4, kend - k);
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    if (!M) { pp[u] = qq[u] = 0; continue; }
-                    const int j = __builtin_ctzll(M);
-                    M &= M - 1;
-                    if (!first) {                    // the previous RM
-                        uint64_t m = wb & ((1ull << bit) - 1);
-                        while (!m) { wb = s.rmb[--ww]; m = wb; }
-                        bit = 63 - __builtin_clzll(m);
-                    }
-                    first = false;
-                    pp[u] = p0 + j;
-                    qq[u] = ww * 64 + bit;
-                    cnt++;
+                    if (u >= cnt) { pp[u] = qq[u] = 0; continue; }
+                    if (u > 0) { next_l(wl, bl, wbl); prev_r(wr, br, wbr); }
+                    pp[u] = wl * 64 + bl;
+                    qq[u] = wr * 64 + br;
                 }
                 uint32_t vp[4], vq[4];
 #pragma unroll
@@ -919,41 +917,13 @@ __device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, 
 #pragma unroll
                 for (int u = 0; u < 4; u++)
                     if (u < cnt) { s.st(pp[u], vq[u]); s.st(qq[u], vp[u]); }
+                k += cnt;
+                if (k >= kend) break;
+                next_l(wl, bl, wbl);
+                prev_r(wr, br, wbr);
             }
-        };
-        int wwA = 0, bitA = 0, wwB = 0, bitB = 0;
-        uint64_t wbA = 0, wbB = 0;
-        if (lmA) {
-            const uint32_t base = (uint32_t)c.fo[kF - 1], t = (uint32_t)c.t[A.slot];
-            locate(base + t - 1 - (gl0 - base), wwA, bitA, wbA);
-            int ww = wwA, bit = bitA;
-            uint64_t wb = wbA;
-            back(__builtin_popcountll(lmA & below), ww, bit, wb);
-            run(lmA & ~below, ww, bit, wb);
-        }
-        if (lmB) {
-            const uint32_t base = (uint32_t)c.fo[kF], t = (uint32_t)c.t[B.slot];
-            const uint32_t glB = gl0 + (uint32_t)__builtin_popcountll(lmA);
-            locate(base + t - 1 - (glB - base), wwB, bitB, wbB);
-            int ww = wwB, bit = bitB;
-            uint64_t wb = wbB;
-            back(__builtin_popcountll(lmB & below), ww, bit, wb);
-            run(lmB & ~below, ww, bit, wb);
-        }
-        if (lmA & below) run(lmA & below, wwA, bitA, wbA);
-        if (lmB & below) run(lmB & below, wwB, bitB, wbB);
-    }
-#ifdef CASIM_PROF
-    {
-        int itw = n_it;
-        for (int d = 32; d; d >>= 1) itw = max(itw, __shfl_xor(itw, d, 64));
-        if (lane == 0 && blockIdx.x == 0) {
-            atomicAdd(&g_pdq_prof[27], clock64() - t_p3);
-            atomicAdd(&g_pdq_prof[28], (unsigned long long)itw);
-            atomicMax(&g_pdq_prof[29], (unsigned long long)itw);
         }
     }
-#endif
     __syncthreads();
     PDQ_ADD(7, t_p3);
 }
@@ -1334,6 +1304,102 @@ __device__ bool wg_partial_insertion(const LdsStore& s, Ctl& c, int a, int b) {
     return false;
 }
 
+// The same on the LDS store by one wavefront (frames run it side by side in step A; the
+// frames are disjoint and position a-1 is a placed pivot): ballots in place of the
+// workgroup reductions, and no barrier — a wavefront's LDS accesses are in program order.
+__device__ bool w_partial_insertion(const LdsStore& s, int a, int b) {
+    constexpr int maxSteps = 5, shortestShifting = 50;
+    const int lane = threadIdx.x & 63;
+    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(s.rk);
+    uint32_t* w32 = reinterpret_cast<uint32_t*>(s.rk);
+    uint32_t* e32 = reinterpret_cast<uint32_t*>(s.e);
+    int i = a + 1;
+    for (int step = 0; step < maxSteps; step++) {
+        int found = b;
+        for (int w0 = i >> 2; 4 * w0 < b; w0 += 64) {           // first descent in [i, b)
+            const int w = w0 + lane;
+            int q = INT_MAX;
+            if (4 * w < b) {
+                const uint32_t x = r32[w];
+                const uint32_t y = (x << 8) | (w > 0 ? r32[w - 1] >> 24 : 0u);
+                const uint32_t m = swar_ltv4(x, y) & nib_range(w, i, b - 1);
+                if (m) q = 4 * w + __builtin_ctz(m);
+            }
+            const uint64_t bal = __ballot(q != INT_MAX);
+            if (bal) { found = __shfl(q, __builtin_ctzll(bal), 64); break; }
+        }
+        i = found;
+        if (i == b) return true;
+        if (b - a < shortestShifting) return false;
+        const uint32_t ev = s.rk[i], fv = s.rk[i - 1];
+        const uint32_t ee = s.e[i], fe = s.e[i - 1];
+        int landL = i - 1, landR = i;
+        if (i - a >= 2) {
+            const int lo = a > 0 ? a - 1 : 0, top = i - 2;
+            int q0 = -1;
+            for (int w0 = top >> 2; 4 * w0 + 3 >= lo; w0 -= 64) {
+                const int w = w0 - lane;
+                int q = -1;
+                if (w >= 0 && 4 * w + 3 >= lo) {
+                    const uint32_t m = swar_lt4(r32[w], ev + 1) & nib_range(w, lo, top);
+                    if (m) q = 4 * w + 31 - __builtin_clz(m);
+                }
+                const uint64_t bal = __ballot(q >= 0);
+                if (bal) { q0 = __shfl(q, __builtin_ctzll(bal), 64); break; }
+            }
+            landL = q0 + 1;
+        }
+        if (b - i >= 2) {
+            int j0 = b;
+            for (int w0 = (i + 1) >> 2; 4 * w0 < b; w0 += 64) {
+                const int w = w0 + lane;
+                int j = INT_MAX;
+                if (4 * w < b) {
+                    const uint32_t m = ~swar_lt4(r32[w], fv) & nib_range(w, i + 1, b - 1);
+                    if (m) j = 4 * w + __builtin_ctz(m);
+                }
+                const uint64_t bal = __ballot(j != INT_MAX);
+                if (bal) { j0 = __shfl(j, __builtin_ctzll(bal), 64); break; }
+            }
+            landR = j0 - 1;
+        }
+        const int qL = landL >> 2, qc = (i - 1) >> 2, qR = landR >> 2;
+        const int nl = qc - qL + 1, nr = qR - qc;
+        for (int done = 0; done < max(nl, nr); done += 64) {
+            uint32_t nv[2][3];
+            int qq[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int k = done + lane;
+                qq[u] = -1;
+                if (u == 0 ? k >= nl : k >= nr) continue;
+                const int v = u == 0 ? qc - k : qc + 1 + k;
+                const int p0 = 4 * v;
+                const uint32_t lo = e32[2 * v], hi = e32[2 * v + 1];
+                const uint32_t pe = v > 0 ? e32[2 * v - 1] : 0u;
+                const bool up = p0 + 4 <= landR;
+                const uint32_t ne = up ? e32[2 * v + 2] : 0u;
+                const uint32_t cr = w32[v];
+                const uint32_t pr = v > 0 ? w32[v - 1] : 0u, nr8 = up ? w32[v + 1] : 0u;
+                nv[u][0] = rotate_word<16>(lo, pe, hi, p0, landL, i, landR, ee, fe);
+                nv[u][1] = rotate_word<16>(hi, lo, ne, p0 + 2, landL, i, landR, ee, fe);
+                nv[u][2] = rotate_word<8>(cr, pr, nr8, p0, landL, i, landR, ev, fv);
+                qq[u] = v;
+            }
+            wfence();
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                if (qq[u] < 0) continue;
+                e32[2 * qq[u]] = nv[u][0];
+                e32[2 * qq[u] + 1] = nv[u][1];
+                w32[qq[u]] = nv[u][2];
+            }
+            wfence();
+        }
+    }
+    return false;
+}
+
 // Sort positions [0, n) of one group (elements already in the store in list order).
 // stack: the group's frame area (cap >= n/2 + 2 frames): pending frames longer than
 // T_SMALL grow from its start, shorter ones from its end (they are sorted last, one
@@ -1405,9 +1471,25 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
                 hint = HINT_INC;
             }
             PDQ_WADD(18, t_rv);
+            bool pis = wb && wp && hint == HINT_INC;
+            if constexpr (std::is_same<S, LdsStore>::value) {
+                // partialInsertionSort here, one wavefront per frame
+                if (pis) {
+                    PDQ_T(t_pis);
+                    const bool sorted = w_partial_insertion(s, a, b);
+                    PDQ_WADD(19, t_pis);
+                    PDQ_CNT(20, 1);
+                    if (sorted) {
+                        if (lane == 0) c.op[i] = OP_DONE;
+                        wfence();
+                        continue;
+                    }
+                    pis = false;
+                }
+            }
             if (lane == 0) {
                 c.piv[i] = pivot;
-                c.pis[i] = (wb && wp && hint == HINT_INC) ? 1 : 0;
+                c.pis[i] = pis ? 1 : 0;
                 c.op[i] = OP_PART;                  // (A2 decides)
                 c.f[i].lf = lf_pack(limit, wb, wp);
             }

@@ -93,6 +93,9 @@ struct RowStage {
 // ca_plan_removals (planner.hip): the last call's moves and counters.
 struct PlanStats {
     int32_t rounds = 0, conflicts = 0, simulated = 0;
+    int32_t path = 0;              // 1: the device chain (plan_chain.hip), 0: speculative windows
+    std::vector<uint64_t> chain_prof;   // the chain's phase cycle counters (plan_chain.hip PC_*)
+    float host_ms[5] = {0, 0, 0, 0, 0};  // sync, launch+kernel, kernel, readback, replay
     float total_ms = 0;
     std::vector<ca_plan_move> moves;
 };

@@ -1,0 +1,963 @@
+// plan_chain.hip — the planner's committing candidate loop as one device-resident chain
+// (Planner.categorizeNodes with canPersist = true).
+//
+// Reference: CA/core/scaledown/planner/planner.go:252-296 (the loop over unneeded nodes,
+// podDestinations shrinking by every removal), CA/simulator/cluster.go:145-254
+// (SimulateNodeRemoval, withForkedSnapshot + Commit, findPlaceFor: RemovePod of the pods to
+// move, TrySchedulePods with breakOnFailure), CA/simulator/scheduling/hinting_simulator.go:58-125
+// (hints first, then FitsAnyNodeMatching), CA/simulator/predicatechecker/schedulerbased.go:90-185
+// (the rotating first-fit scan and lastIndex), CA/simulator/drain.go:73-90 + CA/core/scaledown/
+// pdb/basic.go:58-95 (checkPdbs against the remaining budgets, CanRemovePods, RemovePods).
+//
+// The loop is strictly sequential: every candidate reads the snapshot its predecessors
+// committed.  One wavefront walks all candidates in order with the committed node rows
+// resident in LDS (free cpu / memory / ephemeral storage / pod slots, plus bit planes for
+// podDestinations, schedulability, taints), so a pod's hint check and its scan touch only
+// LDS: a 64-node block per step, blocks whose maxima the pod exceeds skipped 64 at a time.
+// A candidate's simulation applies its RemovePods and AddPods to the rows in place; a
+// failed candidate undoes them (Revert), a removable one keeps them (Commit) and appends its
+// moved copies to the destination nodes' pod lists (which a later candidate on such a node
+// must move too).  No host round trip per candidate or per conflict: one launch runs the
+// whole loop, and the host replays the committed moves into the mirror's journal afterwards.
+//
+// Scope of the chain (planner.hip falls back to the speculative sweep windows otherwise):
+// the node rows fit in LDS, and no pod to move has host ports or extended-resource requests
+// (the only filters whose node state is not a resource column).
+#include "mirror.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <cstdio>
+
+namespace casim {
+
+constexpr int PC_LIST = CA_MAX_MOVED_PODS;   // pods to move per candidate (larger: prefix cut)
+constexpr size_t PC_LDS_MAX = 163840;         // gfx950: one workgroup may own the CU's 160 KiB
+constexpr int32_t PC_MAX_NODES = 8192;        // two 64-bit words of per-block dirty bits
+constexpr int32_t PC_MVBUF = 512;             // moves staged in LDS between global writes
+// shader-clock counters of the chain's phases (info[4 + k]; CASIM_PROF builds only)
+enum { PC_INIT, PC_LISTS, PC_PDB, PC_FORK, PC_HINT, PC_SCAN, PC_ADD, PC_COMMIT, PC_REVERT, PC_TOTAL, PC_BLOCKS,
+       PC_WINDOWS, PC_NPROF };
+#ifdef CASIM_PROF
+#define PC_T0() uint64_t tp_ = clock64()
+#define PC_MARK(k) do { const uint64_t t_ = clock64(); prof[k] += t_ - tp_; tp_ = t_; } while (0)
+#define PC_COUNT(k) (prof[k]++)
+#else
+#define PC_T0() do {} while (0)
+#define PC_MARK(k) do {} while (0)
+#define PC_COUNT(k) do {} while (0)
+#endif
+
+// One pod to move, as the chain reads it: requests, flags after the move (NodeName and TPU
+// requests cleared), the hint it carries in, its record and its caller pod (PDBs).
+struct alignas(16) PcPod {
+    int64_t cpu, mem, eph;
+    int32_t id, hint;
+    uint32_t flags;
+    int32_t spec, orig, pad;
+};
+static_assert(sizeof(PcPod) == 48, "PcPod");
+
+struct PcArgs {
+    const NodeHot* hot;
+    const NodeStatic* st;
+    int32_t n;
+    const uint8_t* dest_mask;
+    const int32_t* cands;
+    const int32_t* status;
+    const int32_t* move_off;
+    const PcPod* pods;            // the caller's pods to move, packed in list order (+64 padding)
+    int32_t C;
+    const ca_pod_spec* specs;
+    const ca_selector_term* terms;
+    const ca_selector_req* reqs;
+    const int32_t* names;
+    int32_t base;                 // mirror pod id of the first copy this call stores
+    int32_t max_removable;
+    int32_t n_pdbs;
+    int32_t* allowed;             // RemainingPdbTracker budgets (in place)
+    const int32_t* pdb_off;       // memberships by caller pod [n_pods + 1]
+    const int32_t* pdb_pod;
+    int32_t* H;                   // hints by pod id [base + copy_cap] (hints.go: a copy keeps its key)
+    const int32_t* ex_base;       // per node: first slot of its committed copies in ex_pods
+    PcPod* ex_pods;               // copies committed onto a node, as their later candidacy reads them
+    ca_plan_result* res;
+    ca_plan_move* moves;
+    int64_t* info;                // [0] lastIndex, [1] moves, [2] removed, [3] candidates simulated,
+                                  // [4..16) phase cycle counters (PC_* above)
+    int64_t L0;
+    int32_t copy_cap;
+    int32_t dbg;                  // CASIM_PLAN_DBG bits: 1 no block cache, 2 no maxima refresh
+    int32_t* trace;               // CASIM_PLAN_TRACE: per simulated pod {c, t, hint, hint_ok, target, evals, L, cnt}
+    int32_t trace_cap;
+};
+
+// packs the pods to move (one thread per list entry; hints as the caller passed them: a
+// pod's hint changes only while its own candidate is simulated)
+__global__ void __launch_bounds__(256) k_plan_pack(const int32_t* __restrict__ move_pods, int32_t M,
+                                                  const PodHot* __restrict__ ph, const int32_t* __restrict__ H0,
+                                                  PcPod* __restrict__ out) {
+    const int32_t i = (int32_t)(blockIdx.x * 256 + threadIdx.x);
+    if (i >= M + 64) return;
+    PcPod r = {};
+    r.id = -1; r.hint = -1; r.orig = -1;
+    if (i < M) {
+        const int32_t id = move_pods[i];
+        const PodHot p = ph[id];
+        r.cpu = p.cpu; r.mem = p.mem; r.eph = p.eph;
+        r.id = id; r.hint = H0[id]; r.spec = p.spec; r.orig = id;
+        // moved-pod semantics (cluster.go:235-240 clears Spec.NodeName, tpu.go:57-79 the TPU requests)
+        uint32_t f = p.flags & ~(PF_NODE_NAME | PF_ALL_ZERO | PF_SCALAR_REQ | PF_HAS_SCALAR_KEYS);
+        if (p.flags & PF_MOVED_ALL_ZERO) f |= PF_ALL_ZERO;
+        if (p.flags & PF_MOVED_SCALAR_REQ) f |= PF_SCALAR_REQ;
+        if (p.flags & PF_NONTPU_SCALAR) f |= PF_HAS_SCALAR_KEYS;
+        r.flags = f;
+    }
+    out[i] = r;
+}
+
+// LDS image of one call (byte offsets; every array 16-B aligned)
+struct PcLayout {
+    size_t fc, fm, fe, destw, visw, uschw, taintw, ephw, bmc, bmm, bme, bmp, fp, excnt, scratch, resbuf, mvbuf, total;
+};
+
+__host__ __device__ inline PcLayout pc_layout(int32_t n, bool eph_cols) {
+    PcLayout L;
+    const size_t nn = (size_t)n, nb = (nn + 63) / 64;
+    size_t o = 0;
+    auto take = [&](size_t bytes) { const size_t r = o; o += (bytes + 15) & ~(size_t)15; return r; };
+    L.fc = take(8 * nn);
+    L.fm = take(8 * nn);
+    L.fe = take(eph_cols ? 8 * nn : 0);
+    L.destw = take(8 * nb);
+    L.visw = take(8 * nb);
+    L.uschw = take(8 * nb);
+    L.taintw = take(8 * nb);
+    L.ephw = take(eph_cols ? 0 : 8 * nb);
+    L.bmc = take(8 * nb);
+    L.bmm = take(8 * nb);
+    L.bme = take(8 * nb);
+    L.bmp = take(4 * nb);
+    L.fp = take(4 * nn);
+    L.excnt = take(2 * nn);
+    L.scratch = take(4 * 64);
+    L.resbuf = take(sizeof(ca_plan_result) * 64);       // results of the current 64 candidates
+    L.mvbuf = take(sizeof(ca_plan_move) * PC_MVBUF);   // committed moves not yet written out
+    L.total = o;
+    return L;
+}
+
+extern "C" __device__ long long __ockl_wfred_add_i64(long long);
+extern "C" __device__ long long __ockl_wfred_max_i64(long long);
+extern "C" __device__ int __ockl_wfred_add_i32(int);
+extern "C" __device__ int __ockl_wfred_min_i32(int);
+extern "C" __device__ int __ockl_wfred_max_i32(int);
+
+__device__ inline int64_t pc_rl64(int64_t v, int lane) {
+    const uint64_t u = (uint64_t)v;
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(u >> 32), lane);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)u, lane);   // (no sign extension)
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ inline int32_t pc_rl32(int32_t v, int lane) { return (int32_t)__builtin_amdgcn_readlane((uint32_t)v, lane); }
+__device__ inline uint64_t pc_below(int lane) { return lane == 0 ? 0ull : (~0ull >> (64 - lane)); }
+__device__ inline bool pc_bit(const uint64_t* w, int32_t i) { return (w[i >> 6] >> (i & 63)) & 1ull; }
+
+// workgroup-coherent global accesses: the chain's own earlier stores (hints, copies, PDB
+// budgets) are read back by other lanes of the same wavefront
+__device__ inline int32_t pc_ld(const int32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ inline void pc_st(int32_t* p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// a list entry held by a lane (pod t in lane t % 64 of half t / 64)
+struct PcReg {
+    int64_t cpu, mem, eph;
+    int32_t id, hint, spec, orig;
+    uint32_t flags;
+};
+__device__ inline PcReg pc_reg(const PcPod& p) {
+    PcReg r;
+    r.cpu = p.cpu; r.mem = p.mem; r.eph = p.eph; r.id = p.id; r.hint = p.hint; r.spec = p.spec; r.orig = p.orig;
+    r.flags = p.flags;
+    return r;
+}
+__device__ inline PcPod pc_load(const PcPod* p) {
+    PcPod r;
+    const int4* q = reinterpret_cast<const int4*>(p);
+    int4 a = q[0], b = q[1], c = q[2];
+    __builtin_memcpy(reinterpret_cast<int4*>(&r), &a, 16);
+    __builtin_memcpy(reinterpret_cast<int4*>(&r) + 1, &b, 16);
+    __builtin_memcpy(reinterpret_cast<int4*>(&r) + 2, &c, 16);
+    return r;
+}
+
+template <bool EPH_COLS>
+__global__ void __launch_bounds__(64) k_plan_chain(PcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char pc_raw[];
+    const int lane = threadIdx.x;
+    const int32_t n = a.n, nb = (n + 63) >> 6;
+    const PcLayout Y = pc_layout(n, EPH_COLS);
+    int64_t* const fc = reinterpret_cast<int64_t*>(pc_raw + Y.fc);         // free cpu / memory /
+    int64_t* const fm = reinterpret_cast<int64_t*>(pc_raw + Y.fm);         // ephemeral storage /
+    int64_t* const fe = reinterpret_cast<int64_t*>(pc_raw + Y.fe);         // pod slots, committed
+    int32_t* const fp = reinterpret_cast<int32_t*>(pc_raw + Y.fp);
+    uint64_t* const destw = reinterpret_cast<uint64_t*>(pc_raw + Y.destw);   // podDestinations
+    uint64_t* const visw = reinterpret_cast<uint64_t*>(pc_raw + Y.visw);     // ... and schedulable
+    uint64_t* const uschw = reinterpret_cast<uint64_t*>(pc_raw + Y.uschw);
+    uint64_t* const taintw = reinterpret_cast<uint64_t*>(pc_raw + Y.taintw);
+    uint64_t* const ephw = reinterpret_cast<uint64_t*>(pc_raw + Y.ephw);     // free ephemeral >= 0
+    int64_t* const bmc = reinterpret_cast<int64_t*>(pc_raw + Y.bmc);        // per block: maxima over
+    int64_t* const bmm = reinterpret_cast<int64_t*>(pc_raw + Y.bmm);        // its visible rows (upper
+    int64_t* const bme = reinterpret_cast<int64_t*>(pc_raw + Y.bme);        // bounds, refreshed by scans)
+    int32_t* const bmp = reinterpret_cast<int32_t*>(pc_raw + Y.bmp);
+    uint16_t* const excnt = reinterpret_cast<uint16_t*>(pc_raw + Y.excnt);  // copies committed per node
+    int32_t* const scratch = reinterpret_cast<int32_t*>(pc_raw + Y.scratch);
+    ca_plan_result* const resbuf = reinterpret_cast<ca_plan_result*>(pc_raw + Y.resbuf);
+    ca_plan_move* const mvbuf = reinterpret_cast<ca_plan_move*>(pc_raw + Y.mvbuf);
+    // Global stores are kept out of the pod loop: on gfx9 a store counts in vmcnt, so any
+    // later vmcnt wait (the compiler's, for a register a load may still write) would wait
+    // for it.  Results and moves are staged in LDS and written in bulk; hints and the
+    // copies' records are written once per candidate, behind the next candidate's prefetch.
+    auto flush_res = [&](int32_t c0, int32_t k) {       // resbuf[0, k) -> res[c0, c0 + k)
+        if (lane < k) {
+            const int32_t* src = reinterpret_cast<const int32_t*>(resbuf + lane);
+            int32_t* dst = reinterpret_cast<int32_t*>(a.res + c0 + lane);
+            for (int w = 0; w < (int)(sizeof(ca_plan_result) / 4); w++) dst[w] = src[w];
+        }
+    };
+    int32_t mv_first = 0, mv_n = 0;                     // mvbuf holds moves [mv_first, mv_first + mv_n)
+    auto flush_moves = [&]() {
+        for (int32_t k = lane; k < mv_n; k += 64) a.moves[mv_first + k] = mvbuf[k];
+        mv_first += mv_n;
+        mv_n = 0;
+    };
+#ifdef CASIM_PROF
+    uint64_t prof[PC_NPROF];
+    for (int k = 0; k < PC_NPROF; k++) prof[k] = 0;
+    const uint64_t t_start = clock64();
+#endif
+
+    // ---- the committed rows and bit planes into LDS (4 blocks in flight per lane) ----
+    for (int32_t b0 = 0; b0 < nb; b0 += 4) {
+        NodeHot h[4];
+        uint8_t dm[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int32_t i = (b0 + u) * 64 + lane;
+            h[u] = NodeHot{};
+            dm[u] = 0;
+            if (i < n) { h[u] = a.hot[i]; dm[u] = a.dest_mask[i]; }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int32_t j = b0 + u;
+            if (j >= nb) break;
+            const int32_t i = j * 64 + lane;
+            const bool valid = i < n;
+            if (valid) {
+                fc[i] = h[u].cpu; fm[i] = h[u].mem; fp[i] = h[u].pods; excnt[i] = 0;
+                if (EPH_COLS) fe[i] = h[u].eph;
+            }
+            const uint64_t dw = __ballot(valid && dm[u] != 0);
+            const uint64_t uw = __ballot(valid && (h[u].flags & NF_UNSCHED));
+            const uint64_t tw = __ballot(valid && (h[u].flags & NF_TAINTS));
+            const uint64_t ew = __ballot(valid && h[u].eph >= 0);
+            if (lane == 0) {
+                destw[j] = dw; visw[j] = dw & ~uw; uschw[j] = uw; taintw[j] = tw;
+                if (!EPH_COLS) ephw[j] = ew;
+                bmc[j] = INT64_MAX; bmm[j] = INT64_MAX; bme[j] = INT64_MAX; bmp[j] = INT32_MAX;
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint64_t dirty0 = ~0ull, dirty1 = ~0ull;            // blocks whose maxima may be stale-high
+#ifdef CASIM_PROF
+    prof[PC_INIT] = clock64() - t_start;
+#endif
+
+    // register cache of one 64-node block of rows (lane i: node cj * 64 + i)
+    int32_t cj = -1;
+    int64_t cc = 0, cm = 0, ce = 0;
+    int32_t cp = 0;
+    bool cv = false, cok = false, ctn = false;
+    auto load_block = [&](int32_t j) {
+        const int32_t x = j * 64 + lane;
+        const bool in = x < n;
+        cc = in ? fc[x] : 0; cm = in ? fm[x] : 0; cp = in ? fp[x] : INT32_MIN;
+        ce = (EPH_COLS && in) ? fe[x] : 0;
+        cv = in && ((visw[j] >> lane) & 1ull);
+        cok = EPH_COLS ? true : (in && ((ephw[j] >> lane) & 1ull));
+        ctn = in && ((taintw[j] >> lane) & 1ull);
+        cj = j;
+    };
+    auto mark_dirty = [&](int32_t j) {
+        if (j < 64) dirty0 |= 1ull << j; else dirty1 |= 1ull << (j - 64);
+    };
+
+    int64_t Lraw = a.L0;                              // Go keeps the int until a scan succeeds
+    int32_t Lw = 0;
+    if (n > 0) { Lw = (int32_t)(Lraw % n); if (Lw < 0) Lw += n; }
+    int32_t nm = 0, removed = 0, simulated = 0;
+    bool cut = false, stopped = false;
+    int32_t hb_node = -1, hb_st = 0, hb_mo = 0, hb_m1 = 0;    // candidate headers, lane k = c0 + k
+    // the next candidate's first 64 pods, loaded while the current one runs
+    PcPod nx = {};
+    if (a.C > 0) nx = pc_load(a.pods + a.move_off[0] + lane);
+
+    for (int32_t c = 0; c < a.C; c++) {
+        const int sl = c & 63;
+        if (sl == 0) {
+            const int32_t k = c + lane;
+            if (k < a.C) {
+                hb_node = a.cands[k];
+                hb_st = a.status ? a.status[k] : 0;
+                hb_mo = a.move_off[k];
+                hb_m1 = a.move_off[k + 1];
+            }
+        }
+        PcReg r0 = pc_reg(nx);                                    // pods t = lane
+        PcReg r1 = {};                                            // pods t = 64 + lane
+        r1.id = -1; r1.hint = -1; r1.orig = -1;
+        const int32_t mo1 = pc_rl32(hb_m1, sl);                  // = the next candidate's move_off
+        if (c + 1 < a.C) nx = pc_load(a.pods + mo1 + lane);
+        if (cut || (a.max_removable > 0 && removed >= a.max_removable)) {       // planner.go:268-271
+            flush_res(c - sl, sl);
+            stopped = true;
+            for (int32_t k = c + lane; k < a.C; k += 64) {
+                ca_plan_result r;
+                r.removable = 0; r.reason = CA_UNREMOVABLE_NOT_RUN; r.n_placed = 0; r.last_index_in = (int32_t)Lraw;
+                r.evals = 0; r.first_move = nm; r.n_moves = 0; r.blocking_pod = -1; r.risky = 0;
+                a.res[k] = r;
+            }
+            break;
+        }
+        PC_T0();
+        const int32_t node = pc_rl32(hb_node, sl), stc = pc_rl32(hb_st, sl);
+        const int32_t mo = pc_rl32(hb_mo, sl), m0 = mo1 - mo;
+        ca_plan_result r;
+        r.removable = 0; r.reason = CA_UNREMOVABLE_NONE; r.n_placed = 0; r.last_index_in = (int32_t)Lraw;
+        r.evals = 0; r.first_move = nm; r.n_moves = 0; r.blocking_pod = -1; r.risky = 0;
+        const bool valid = node >= 0 && node < n && pc_bit(destw, node);
+        int32_t cnt = m0;
+        if (valid && stc == 0) {
+            // GetPodsToMove on the committed snapshot: the caller's list, then the copies
+            // committed onto this node (NodeInfo.Pods appends)
+            const int32_t ne = excnt[node];
+            cnt = m0 + ne;
+            if (cnt > PC_LIST) {
+                cut = true;                                                         // casim.h scope
+            } else {
+                if (m0 > 64) r1 = pc_reg(pc_load(a.pods + mo + 64 + lane));
+                if (ne > 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    const PcPod* ex = a.ex_pods + a.ex_base[node];
+                    const int32_t t0 = lane, t1 = 64 + lane;
+                    if (t0 >= m0 && t0 < cnt) r0 = pc_reg(pc_load(ex + (t0 - m0)));
+                    if (t1 >= m0 && t1 < cnt) r1 = pc_reg(pc_load(ex + (t1 - m0)));
+                }
+                const bool oos = (lane < cnt && (r0.flags & PF_OUT_OF_SCOPE)) ||
+                                 (64 + lane < cnt && (r1.flags & PF_OUT_OF_SCOPE));
+                if (__ballot(oos)) cut = true;
+            }
+            if (cut) {
+                r.reason = CA_UNREMOVABLE_OUT_OF_SCOPE;
+                if (lane == 0) resbuf[sl] = r;
+                if (sl == 63) flush_res(c - 63, 64);
+                continue;
+            }
+        }
+        PC_MARK(PC_LISTS);
+        if (!valid) {
+            r.reason = CA_UNREMOVABLE_UNEXPECTED_ERROR;                              // cluster.go:157-160
+        } else if (stc != 0) {
+            r.reason = stc;                                                          // :162-169
+        } else if (a.n_pdbs > 0) {
+            // ---- checkPdbs against the remaining budgets (drain.go:73-90) ----
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            auto lowest = [&](int32_t t, int32_t o) {           // lowest blocked PDB of pod t
+                int32_t best = INT32_MAX;
+                if (t < cnt)
+                    for (int32_t k = a.pdb_off[o]; k < a.pdb_off[o + 1]; k++) {
+                        const int32_t p = a.pdb_pod[k];
+                        if (pc_ld(a.allowed + p) < 1) { best = p; break; }   // memberships ascend
+                    }
+                return best;
+            };
+            const int32_t pm0 = lowest(lane, r0.orig), pm1 = lowest(64 + lane, r1.orig);
+            const int32_t pmin = __ockl_wfred_min_i32(pm0 < pm1 ? pm0 : pm1);
+            if (pmin != INT32_MAX) {
+                const uint64_t b0 = __ballot(pm0 == pmin), b1 = __ballot(pm1 == pmin);
+                r.blocking_pod = b0 ? pc_rl32(r0.id, __builtin_ctzll(b0)) : pc_rl32(r1.id, __builtin_ctzll(b1));
+                r.reason = CA_UNREMOVABLE_BLOCKED_BY_POD;
+            }
+        }
+        PC_MARK(PC_PDB);
+        if (r.reason != CA_UNREMOVABLE_NONE) {
+            if (lane == 0) resbuf[sl] = r;
+            if (sl == 63) flush_res(c - 63, 64);
+            continue;
+        }
+        simulated++;
+        // ---- withForkedSnapshot(findPlaceFor): RemovePod of the pods to move (cluster.go:228-233) ----
+        const bool in0 = lane < cnt, in1 = 64 + lane < cnt;
+        const int64_t sc = __ockl_wfred_add_i64(wadd(in0 ? r0.cpu : 0, in1 ? r1.cpu : 0));
+        const int64_t sm = __ockl_wfred_add_i64(wadd(in0 ? r0.mem : 0, in1 ? r1.mem : 0));
+        const int64_t se = EPH_COLS ? __ockl_wfred_add_i64(wadd(in0 ? r0.eph : 0, in1 ? r1.eph : 0)) : 0;
+        const int32_t jn = node >> 6;
+        const uint64_t nbit = 1ull << (node & 63);
+        {
+            const int64_t oc = fc[node], om = fm[node], oe = EPH_COLS ? fe[node] : 0;
+            const int32_t op = fp[node];
+            const int64_t nc = wadd(oc, sc), nmm = wadd(om, sm), ne2 = wadd(oe, se);
+            const int32_t np = op + cnt;
+            if (lane == 0) {
+                fc[node] = nc; fm[node] = nmm; fp[node] = np;
+                if (EPH_COLS) fe[node] = ne2;
+                // a row that grows raises its block's maxima (they are upper bounds)
+                const int64_t bc = bmc[jn], bm = bmm[jn], be = EPH_COLS ? bme[jn] : 0;
+                const int32_t bp = bmp[jn];
+                if (nc > bc) bmc[jn] = nc;
+                if (nmm > bm) bmm[jn] = nmm;
+                if (EPH_COLS && ne2 > be) bme[jn] = ne2;
+                if (np > bp) bmp[jn] = np;
+            }
+            if (jn == cj && lane == (node & 63)) { cc = nc; cm = nmm; ce = ne2; cp = np; }
+        }
+        PC_MARK(PC_FORK);
+        uint64_t evals = 0;
+        int32_t placed = 0;
+        int32_t d0 = -1, d1 = -1;                   // destinations of pods t = lane, 64 + lane
+        int32_t hs0 = INT32_MIN, hs1 = INT32_MIN;   // Hints.Set of pods t = lane, 64 + lane
+        bool failed = false;
+        for (int32_t t = 0; t < cnt; t++) {
+            const bool hi = t >= 64;
+            const int tl = t & 63;
+            const int64_t pcpu = pc_rl64(hi ? r1.cpu : r0.cpu, tl);
+            const int64_t pmem = pc_rl64(hi ? r1.mem : r0.mem, tl);
+            const int64_t peph = EPH_COLS ? pc_rl64(hi ? r1.eph : r0.eph, tl) : 0;
+            const uint32_t pf = (uint32_t)pc_rl32((int32_t)(hi ? r1.flags : r0.flags), tl);
+            const int32_t h = pc_rl32(hi ? r1.hint : r0.hint, tl);
+            const int32_t id = pc_rl32(hi ? r1.id : r0.id, tl);
+            const int32_t spec = pc_rl32(hi ? r1.spec : r0.spec, tl);
+            const bool prefail = (pf & PF_PREFILTER_FAIL) != 0;
+            const bool all_zero = (pf & PF_ALL_ZERO) != 0;
+            // TaintToleration / NodeAffinity / NodeName where the pod or the node needs them
+            auto static_fit = [&](int32_t x, bool tainted) -> bool {
+                const bool need = (pf & (PF_NODE_NAME | PF_AFFINITY)) || (tainted && !(pf & PF_TAINT_MASK_ALL));
+                if (!need) return true;
+                const NodeStatic ns = a.st[x];
+                return dev_static_filters(a.specs[spec], pf, a.terms, a.reqs, ns, false) == CA_PLUGIN_NONE;
+            };
+            int32_t target = -1;
+            int64_t tc = 0, tm = 0, te = 0;         // the target's row
+            int32_t tpd = 0;
+            // ---- findNodeWithHints (hinting_simulator.go:91-108): CheckPredicates ----
+            if (h >= 0 && h < n && !prefail) {
+                evals++;
+                const int64_t hc = fc[h], hm = fm[h], he = EPH_COLS ? fe[h] : 0;
+                const int32_t hp = fp[h];
+                const int32_t jh = h >> 6;
+                const uint64_t hb = 1ull << (h & 63);
+                const bool usch = (uschw[jh] & hb) != 0, tnt = (taintw[jh] & hb) != 0, dst = (destw[jh] & hb) != 0;
+                const bool eok = EPH_COLS ? (peph <= he) : ((ephw[jh] & hb) != 0);
+                bool ok = !(usch && !(pf & PF_TOL_UNSCHED));
+                ok = ok && (hp >= 1) && (all_zero || ((pcpu <= hc) & (pmem <= hm) & eok));
+                ok = ok && static_fit(h, tnt);
+                if (ok) {
+                    if (lane == tl) { if (hi) hs1 = h; else hs0 = h; }              // :95 Set
+                    if (h != node && dst) { target = h; tc = hc; tm = hm; te = he; tpd = hp; }   // :102 accepted
+                }
+            }
+            PC_MARK(PC_HINT);
+            // ---- findNode -> FitsAnyNodeMatching(isCandidateNode) (:110-125) ----
+            if (target < 0 && !prefail && n > 0) {
+                const bool names = (pf & PF_PREFILTER_NAMES) != 0;
+                const int32_t j0 = Lw >> 6, l0 = Lw & 63;
+                int32_t wr = -1, my_nv = 0;
+                uint64_t passm = 0;
+                for (int32_t rr = 0; rr <= nb; rr++) {
+                    if (rr == nb && l0 == 0) break;
+                    int32_t j = j0 + rr;
+                    if (j >= nb) j -= nb;
+                    if (rr > 0 && rr < nb && !names && j != cj) {
+                        // 64 blocks at a time: a block passes when the pod exceeds its maxima
+                        if (wr < 0 || rr >= wr + 64) {
+                            PC_COUNT(PC_WINDOWS);
+                            const int32_t q = rr + lane;
+                            bool pass = false;
+                            my_nv = 0;
+                            if (q < nb) {
+                                int32_t jj = j0 + q;
+                                if (jj >= nb) jj -= nb;
+                                const uint64_t vw = visw[jj] & (jj == jn ? ~nbit : ~0ull);
+                                const bool fitb = (vw != 0) & (bmp[jj] >= 1) &
+                                                  (all_zero | ((pcpu <= bmc[jj]) & (pmem <= bmm[jj]) &
+                                                               (!EPH_COLS || peph <= bme[jj])));
+                                pass = !fitb && jj != cj;
+                                my_nv = __popcll(vw);
+                            }
+                            passm = __ballot(pass);
+                            wr = rr;
+                        }
+                        const int32_t off = rr - wr;
+                        const uint64_t stop = ~passm & (~0ull << off);
+                        const int32_t k = (stop ? __builtin_ctzll(stop) : 64) - off;
+                        if (k > 0) {
+                            evals += (uint64_t)__ockl_wfred_add_i32((lane >= off && lane < off + k) ? my_nv : 0);
+                            rr += k - 1;
+                            continue;
+                        }
+                    }
+                    PC_COUNT(PC_BLOCKS);
+                    if (j != cj || (a.dbg & 1)) load_block(j);
+                    const int32_t x = j * 64 + lane;
+                    const bool inr = (rr == 0) ? lane >= l0 : (rr == nb ? lane < l0 : true);
+                    bool vis = cv && inr && x != node;
+                    if (vis && names) {
+                        const ca_pod_spec& s = a.specs[spec];
+                        const int32_t nid = a.st[x].name_id;
+                        bool in = false;
+                        for (int32_t k = 0; k < s.prefilter_count; k++) in |= a.names[s.prefilter_first + k] == nid;
+                        vis = in;
+                    }
+                    bool fit = false;
+                    if (vis) {
+                        const bool e = EPH_COLS ? (peph <= ce) : cok;
+                        fit = (cp >= 1) & (all_zero | ((pcpu <= cc) & (pmem <= cm) & e));
+                        if (fit) fit = static_fit(x, ctn);
+                    }
+                    const uint64_t fmk = __ballot(fit), vm = __ballot(vis);
+                    if (fmk) {
+                        const int f = __builtin_ctzll(fmk);
+                        const uint64_t upto = (f == 63) ? ~0ull : ((2ull << f) - 1);
+                        evals += (uint64_t)__popcll(vm & upto);
+                        target = j * 64 + f;
+                        tc = pc_rl64(cc, f); tm = pc_rl64(cm, f); te = EPH_COLS ? pc_rl64(ce, f) : 0;
+                        tpd = pc_rl32(cp, f);
+                        Lw = target + 1 == n ? 0 : target + 1;                       // schedulerbased.go:131
+                        Lraw = Lw;
+                        if (lane == tl) { if (hi) hs1 = target; else hs0 = target; } // :123
+                        break;
+                    }
+                    evals += (uint64_t)__popcll(vm);
+                    // the block passed: refresh its maxima from the rows just read
+                    const bool dj = j < 64 ? ((dirty0 >> j) & 1ull) : ((dirty1 >> (j - 64)) & 1ull);
+                    if (dj && !names && !(a.dbg & 2)) {
+                        const int64_t mc = __ockl_wfred_max_i64(cv ? cc : INT64_MIN);
+                        const int64_t mmx = __ockl_wfred_max_i64(cv ? cm : INT64_MIN);
+                        const int64_t me = EPH_COLS ? __ockl_wfred_max_i64(cv ? ce : INT64_MIN) : 0;
+                        const int32_t mp = __ockl_wfred_max_i32(cv ? cp : INT32_MIN);
+                        if (lane == 0) {
+                            bmc[j] = mc; bmm[j] = mmx; bmp[j] = mp;
+                            if (EPH_COLS) bme[j] = me;
+                        }
+                        if (j < 64) dirty0 &= ~(1ull << j); else dirty1 &= ~(1ull << (j - 64));
+                    }
+                }
+            }
+            PC_MARK(PC_SCAN);
+            if (a.trace && lane == 0) {
+                const int32_t k = atomicAdd(a.trace, 1);
+                if (k < a.trace_cap) {
+                    int32_t* e = a.trace + 16 + 16 * k;
+                    const int32_t dn = a.trace[1];
+                    e[0] = c; e[1] = t; e[2] = h; e[3] = (int32_t)pf; e[4] = target; e[5] = (int32_t)evals;
+                    e[6] = Lw; e[7] = cnt; e[8] = (int32_t)pcpu; e[9] = (int32_t)(pmem >> 20);
+                    e[10] = (int32_t)fc[dn]; e[11] = (int32_t)(fm[dn] >> 20); e[12] = fp[dn];
+                    e[13] = (int32_t)pc_bit(visw, dn) | ((int32_t)pc_bit(taintw, dn) << 1) |
+                            ((int32_t)(EPH_COLS ? 1 : pc_bit(ephw, dn)) << 2);
+                    e[14] = spec; e[15] = id;
+                }
+            }
+            if (target < 0) { failed = true; break; }                                // breakOnFailure
+            // ---- AddPod of the moved copy (:79) ----
+            {
+                const int64_t nc = wsub(tc, pcpu), nmm = wsub(tm, pmem), ne2 = wsub(te, peph);
+                const int32_t np = tpd - 1;
+                if (lane == 0) {
+                    fc[target] = nc; fm[target] = nmm; fp[target] = np;
+                    if (EPH_COLS) fe[target] = ne2;
+                }
+                if ((target >> 6) == cj && lane == (target & 63)) { cc = nc; cm = nmm; ce = ne2; cp = np; }
+                mark_dirty(target >> 6);
+                if (lane == tl) { if (hi) d1 = target; else d0 = target; }
+            }
+            placed++;
+            PC_MARK(PC_ADD);
+        }
+        r.n_placed = placed;
+        r.evals = evals;
+        if (!failed) {
+            // ---- Commit (cluster.go:207-211) ----
+            r.removable = 1;
+            r.n_moves = cnt;
+            for (int half = 0; half < 2 && half * 64 < cnt; half++) {
+                const int32_t t = half * 64 + lane;
+                const bool act = t < cnt;
+                const PcReg& q = half ? r1 : r0;
+                const int32_t f = half ? d1 : d0;
+                const int32_t s = nm + t;
+                if (act) {
+                    ca_plan_move mv;
+                    mv.candidate = c; mv.pod = q.id; mv.new_pod = a.base + s; mv.node = f;
+                    mvbuf[mv_n + t] = mv;
+                    pc_st(a.H + a.base + s, f);
+                }
+                // the copies join their destinations' pod lists in list order
+                int32_t rank = 0, lead = -1;
+                uint64_t pend = __ballot(act);
+                while (pend) {
+                    const int l = __builtin_ctzll(pend);
+                    const int32_t f0 = pc_rl32(f, l);
+                    const uint64_t mm = __ballot(act && f == f0);
+                    if (act && f == f0) { rank = __popcll(mm & pc_below(lane)); lead = l; }
+                    if (lane == l) scratch[l] = __popcll(mm);
+                    pend &= ~mm;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (act && lead == lane) {
+                    const int32_t old = excnt[f];
+                    excnt[f] = (uint16_t)(old + scratch[lane]);
+                    scratch[lane] = old;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (act) {
+                    PcPod cp2;
+                    cp2.cpu = q.cpu; cp2.mem = q.mem; cp2.eph = q.eph;
+                    cp2.id = a.base + s; cp2.hint = f; cp2.flags = q.flags; cp2.spec = q.spec; cp2.orig = q.orig;
+                    cp2.pad = 0;
+                    a.ex_pods[a.ex_base[f] + scratch[lead] + rank] = cp2;
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (lane == 0) { destw[jn] &= ~nbit; visw[jn] &= ~nbit; }               // planner.go:280
+            if (jn == cj && lane == (node & 63)) cv = false;
+            mark_dirty(jn);
+            // CanRemovePods, then RemovePods (basic.go:66-95)
+            if (a.n_pdbs > 0) {
+                bool risky = false;
+                for (int half = 0; half < 2; half++) {
+                    const int32_t t = half * 64 + lane;
+                    if (t >= cnt) continue;
+                    const int32_t o = half ? r1.orig : r0.orig;
+                    for (int32_t k = a.pdb_off[o]; k < a.pdb_off[o + 1]; k++)
+                        risky |= atomicSub(a.allowed + a.pdb_pod[k], 1) <= 0;
+                }
+                r.risky = __ballot(risky) ? 1 : 0;
+            }
+            removed++;
+            nm += cnt;
+            mv_n += cnt;
+            __builtin_amdgcn_wave_barrier();
+            if (mv_n + PC_LIST > PC_MVBUF) flush_moves();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            PC_MARK(PC_COMMIT);
+        } else {
+            // ---- Revert: undo the AddPods, then the RemovePods ----
+            for (int half = 0; half < 2; half++) {
+                const int32_t t = half * 64 + lane;
+                if (t >= placed) continue;
+                const PcReg& q = half ? r1 : r0;
+                const int32_t f = half ? d1 : d0;
+                atomicAdd(reinterpret_cast<unsigned long long*>(fc + f), (unsigned long long)q.cpu);
+                atomicAdd(reinterpret_cast<unsigned long long*>(fm + f), (unsigned long long)q.mem);
+                if (EPH_COLS) atomicAdd(reinterpret_cast<unsigned long long*>(fe + f), (unsigned long long)q.eph);
+                atomicAdd(fp + f, 1);
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (int half = 0; half < 2; half++) {
+                const int32_t t = half * 64 + lane;
+                if (t >= placed) continue;
+                const int32_t f = half ? d1 : d0, j = f >> 6;
+                atomicMax(reinterpret_cast<long long*>(bmc + j), (long long)fc[f]);
+                atomicMax(reinterpret_cast<long long*>(bmm + j), (long long)fm[f]);
+                if (EPH_COLS) atomicMax(reinterpret_cast<long long*>(bme + j), (long long)fe[f]);
+                atomicMax(bmp + j, fp[f]);
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) {
+                fc[node] = wsub(fc[node], sc); fm[node] = wsub(fm[node], sm); fp[node] -= cnt;
+                if (EPH_COLS) fe[node] = wsub(fe[node], se);
+            }
+            mark_dirty(jn);
+            cj = -1;                                                                 // rows changed
+            r.reason = CA_UNREMOVABLE_NO_PLACE;                                      // cluster.go:174-177
+            PC_MARK(PC_REVERT);
+        }
+        // Hints.Set of this candidate's pods (hints persist whether or not it is removable)
+        if (hs0 != INT32_MIN) pc_st(a.H + r0.id, hs0);
+        if (hs1 != INT32_MIN) pc_st(a.H + r1.id, hs1);
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) resbuf[sl] = r;
+        if (sl == 63) flush_res(c - 63, 64);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (!stopped && a.C > 0 && ((a.C - 1) & 63) != 63) flush_res((a.C - 1) & ~63, ((a.C - 1) & 63) + 1);
+    flush_moves();
+    if (lane == 0) {
+        a.info[0] = Lraw;
+        a.info[1] = nm;
+        a.info[2] = removed;
+        a.info[3] = simulated;
+#ifdef CASIM_PROF
+        prof[PC_TOTAL] = clock64() - t_start;
+        for (int k = 0; k < PC_NPROF; k++) a.info[4 + k] = (int64_t)prof[k];
+#else
+        for (int k = 0; k < PC_NPROF; k++) a.info[4 + k] = 0;
+#endif
+    }
+}
+
+}  // namespace casim
+
+using namespace casim;
+
+namespace casim {
+
+// Per-mirror scratch of the chain (kept across calls).
+struct PlanChainScratch {
+    DevBuf in, work, out;
+    HostBuf h_in, h_out;
+};
+
+static PlanChainScratch& chain_scratch(ca_mirror* m) {
+    // one per mirror handle; the mirror owns none of it beyond the call (freed with the
+    // process-wide allocation cache)
+    static thread_local std::vector<std::pair<const ca_mirror*, PlanChainScratch*>> tab;
+    for (auto& e : tab)
+        if (e.first == m) return *e.second;
+    tab.push_back({m, new PlanChainScratch()});
+    return *tab.back().second;
+}
+
+// 1 = ran, 0 = outside the chain's scope (the caller takes the speculative path), < 0 error.
+// *last_index is an out-value only (the caller passes a copy); hints come back in hints_out.
+int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uint8_t* dest_mask,
+                   const int32_t* cand_status, const int32_t* move_off, const int32_t* move_pods,
+                   int32_t max_removable, const ca_pdb_table* pdbs, int32_t* hints, int32_t n_pods,
+                   int32_t* last_index, ca_plan_result* results, std::vector<ca_plan_move>& moves_out,
+                   std::vector<int32_t>& hints_out, int32_t* simulated_out) {
+    if (getenv("CASIM_PLAN_SPECULATIVE")) return 0;
+    const int32_t N = (int32_t)m->nodes.size();
+    if (N <= 0 || C <= 0) return 0;
+    const int32_t M = move_off[C];
+    bool eph_cols = false;
+    for (int32_t i = 0; i < M; i++) {
+        const ca_pod_spec& s = m->pods[move_pods[i]].spec;
+        const uint32_t f = pod_dev_flags(s);
+        if (f & (PF_PORTS | PF_MOVED_SCALAR_REQ)) return 0;
+        if (s.req_ephemeral != 0) eph_cols = true;
+    }
+    const PcLayout Y = pc_layout(N, eph_cols);
+    if (Y.total > PC_LDS_MAX || N > PC_MAX_NODES) return 0;
+    const int P = pdbs ? pdbs->n_pdbs : 0;
+    {   // each pod in at most one candidate's list (its hint is packed before the loop runs)
+        std::vector<uint8_t> seen((size_t)std::max(n_pods, 1), 0);
+        for (int32_t i = 0; i < M; i++) {
+            if (seen[move_pods[i]]) return 0;
+            seen[move_pods[i]] = 1;
+        }
+    }
+
+    // copies: at most one per free pod slot of its destination (every AddPod passes the
+    // pod-count check; a node's own pods leave only when it is removed)
+    std::vector<int32_t> ex_base((size_t)N + 1);
+    int64_t cap = 0;
+    for (int32_t i = 0; i < N; i++) {
+        ex_base[i] = (int32_t)cap;
+        const NodeRow& nd = m->nodes[i];
+        const int64_t free_slots = nd.spec.alloc_pods - nd.npods;
+        if (free_slots > 65535) return 0;                       // the per-node copy counters are 16-bit
+        cap += free_slots > 0 ? free_slots : 0;
+        if (cap > INT32_MAX / 64) return 0;
+    }
+    ex_base[N] = (int32_t)cap;
+    const int32_t copy_cap = (int32_t)std::max<int64_t>(cap, 1);
+    const int32_t base = (int32_t)m->pods.size();
+    if ((int64_t)base + copy_cap > INT32_MAX) return 0;
+
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc;
+    if ((rc = m->sync_nodes()) != CA_OK) return rc;
+    if ((rc = m->sync_pods()) != CA_OK) return rc;
+    const auto t_sync = std::chrono::steady_clock::now();
+    PlanChainScratch& S = chain_scratch(m);
+    hipStream_t st = m->stream;
+
+    // packed inputs (one H2D): cands, status, move_off, move_pods, ex_base, pdb tables, hints; mask
+    const size_t n_pdb_members = P > 0 ? (size_t)pdbs->pod_off[n_pods] : 0;
+    const size_t in_words = (size_t)C + C + (C + 1) + std::max(M, 1) + (N + 1) + (P > 0 ? (size_t)n_pods + 1 : 1) +
+                            std::max<size_t>(n_pdb_members, 1) + std::max(P, 1) + std::max(n_pods, 1);
+    const size_t in_bytes = 4 * in_words + ((size_t)N + 15) / 16 * 16;
+    if ((rc = S.in.reserve(in_bytes)) != CA_OK) return rc;
+    if ((rc = S.h_in.reserve(in_bytes)) != CA_OK) return rc;
+    int32_t* hw = S.h_in.as<int32_t>();
+    size_t o = 0;
+    auto put = [&](const int32_t* src, size_t k, size_t room) {
+        const size_t at = o;
+        if (src && k) std::memcpy(hw + o, src, 4 * k);
+        else if (room) std::memset(hw + o, 0, 4 * room);
+        o += room;
+        return at;
+    };
+    const size_t o_c = put(candidates, C, C);
+    const size_t o_st = put(cand_status, cand_status ? C : 0, C);
+    const size_t o_off = put(move_off, C + 1, C + 1);
+    const size_t o_mv = put(move_pods, M, std::max(M, 1));
+    const size_t o_exb = put(ex_base.data(), N + 1, N + 1);
+    const size_t o_pof = put(P > 0 ? pdbs->pod_off : nullptr, P > 0 ? n_pods + 1 : 0, P > 0 ? (size_t)n_pods + 1 : 1);
+    const size_t o_pp = put(P > 0 ? pdbs->pod_pdb : nullptr, n_pdb_members, std::max<size_t>(n_pdb_members, 1));
+    const size_t o_al = put(P > 0 ? pdbs->allowed : nullptr, P, std::max(P, 1));
+    const size_t o_h = put(hints, hints ? n_pods : 0, std::max(n_pods, 1));
+    if (!hints) for (int32_t i = 0; i < n_pods; i++) hw[o_h + i] = -1;
+    const size_t o_mask = 4 * o;
+    std::memcpy(reinterpret_cast<unsigned char*>(hw) + o_mask, dest_mask, (size_t)N);
+    int32_t* const din = S.in.as<int32_t>();
+    CA_HIP_CHECK(hipMemcpyAsync(din, hw, o_mask + (size_t)N, hipMemcpyHostToDevice, st));
+
+    // device work: hints H [base + copy_cap], the packed pods to move [M + 64], the copies [copy_cap]
+    const size_t h_bytes = (4 * ((size_t)base + copy_cap) + 15) & ~(size_t)15;
+    const size_t w_bytes = h_bytes + sizeof(PcPod) * ((size_t)M + 64) + sizeof(PcPod) * (size_t)copy_cap;
+    if ((rc = S.work.reserve(w_bytes)) != CA_OK) return rc;
+    int32_t* const dH = S.work.as<int32_t>();
+    PcPod* const dpods = reinterpret_cast<PcPod*>(S.work.as<unsigned char>() + h_bytes);
+    PcPod* const dex = dpods + M + 64;
+    // hints of pods the caller did not pass (past n_pods) and of the copies start at -1
+    CA_HIP_CHECK(hipMemsetAsync(dH, 0xff, 4 * ((size_t)base + copy_cap), st));
+    CA_HIP_CHECK(hipMemcpyAsync(dH, din + o_h, 4 * (size_t)n_pods, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(k_plan_pack, dim3((unsigned)((M + 64 + 255) / 256)), dim3(256), 0, st, din + o_mv, M,
+                       m->d_pods.hot.as<PodHot>(), (const int32_t*)dH, dpods);
+    CA_HIP_CHECK(hipGetLastError());
+    // outputs: results [C], info [16], moves [copy_cap]
+    const size_t out_bytes = sizeof(ca_plan_result) * C + 16 * sizeof(int64_t) + sizeof(ca_plan_move) * copy_cap;
+    if ((rc = S.out.reserve(out_bytes)) != CA_OK) return rc;
+    if ((rc = S.h_out.reserve(out_bytes)) != CA_OK) return rc;
+    ca_plan_result* const dres = S.out.as<ca_plan_result>();
+    int64_t* const dinfo = reinterpret_cast<int64_t*>(dres + C);
+    ca_plan_move* const dmoves = reinterpret_cast<ca_plan_move*>(dinfo + 16);
+
+    PcArgs A;
+    A.hot = m->d_hot.as<NodeHot>();
+    A.st = m->d_static.as<NodeStatic>();
+    A.n = N;
+    A.dest_mask = reinterpret_cast<const uint8_t*>(reinterpret_cast<unsigned char*>(din) + o_mask);
+    A.cands = din + o_c;
+    A.status = din + o_st;
+    A.move_off = din + o_off;
+    A.pods = dpods;
+    A.C = C;
+    A.specs = m->d_pods.spec.as<ca_pod_spec>();
+    A.terms = m->d_pods.terms.as<ca_selector_term>();
+    A.reqs = m->d_pods.reqs.as<ca_selector_req>();
+    A.names = m->d_pods.names.as<int32_t>();
+    A.base = base;
+    A.max_removable = max_removable;
+    A.n_pdbs = P;
+    A.allowed = din + o_al;
+    A.pdb_off = din + o_pof;
+    A.pdb_pod = din + o_pp;
+    A.H = dH;
+    A.ex_base = din + o_exb;
+    A.ex_pods = dex;
+    A.res = dres;
+    A.moves = dmoves;
+    A.info = dinfo;
+    A.L0 = *last_index;
+    A.copy_cap = copy_cap;
+    A.trace = nullptr;
+    A.trace_cap = 0;
+    A.dbg = getenv("CASIM_PLAN_DBG") ? atoi(getenv("CASIM_PLAN_DBG")) : 0;
+    const char* tr_env = getenv("CASIM_PLAN_TRACE");
+    DevBuf trace;
+    if (tr_env) {
+        A.trace_cap = 4096;
+        if ((rc = trace.reserve(sizeof(int32_t) * (16 + 16 * (size_t)A.trace_cap))) != CA_OK) return rc;
+        int32_t hdr[2] = {0, std::max(0, std::min(N - 1, atoi(tr_env)))};
+        CA_HIP_CHECK(hipMemcpy(trace.ptr, hdr, sizeof hdr, hipMemcpyHostToDevice));
+        A.trace = trace.as<int32_t>();
+    }
+    const void* kfn = eph_cols ? (const void*)k_plan_chain<true> : (const void*)k_plan_chain<false>;
+    if ((rc = ensure_dyn_lds(kfn, Y.total)) != CA_OK) return rc;
+    CA_HIP_CHECK(hipEventRecord(m->ev0, st));
+    if (eph_cols) hipLaunchKernelGGL(k_plan_chain<true>, dim3(1), dim3(64), Y.total, st, A);
+    else hipLaunchKernelGGL(k_plan_chain<false>, dim3(1), dim3(64), Y.total, st, A);
+    CA_HIP_CHECK(hipGetLastError());
+    ca_plan_result* const hres = S.h_out.as<ca_plan_result>();
+    int64_t* const hinfo = reinterpret_cast<int64_t*>(hres + C);
+    ca_plan_move* const hmoves = reinterpret_cast<ca_plan_move*>(hinfo + 16);
+    CA_HIP_CHECK(hipEventRecord(m->ev1, st));
+    CA_HIP_CHECK(hipMemcpyAsync(hres, dres, sizeof(ca_plan_result) * C + 16 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    CA_HIP_CHECK(hipStreamSynchronize(st));
+    const auto t_kernel = std::chrono::steady_clock::now();
+    if (tr_env) {
+        std::vector<int32_t> tb(16 + 16 * (size_t)A.trace_cap);
+        CA_HIP_CHECK(hipMemcpy(tb.data(), trace.ptr, sizeof(int32_t) * tb.size(), hipMemcpyDeviceToHost));
+        for (int32_t k = 0; k < std::min(tb[0], A.trace_cap); k++) {
+            const int32_t* e = tb.data() + 16 + 16 * k;
+            fprintf(stderr, "[plan trace] cand %d pod %d/%d (id %d spec %d cpu %d mem %dMi) hint %d flags %x -> %d evals %d "
+                    "L %d | node %d: cpu %d mem %dMi pods %d bits %x\n", e[0], e[1], e[7], e[15], e[14], e[8], e[9],
+                    e[2], e[3], e[4], e[5], e[6], tb[1], e[10], e[11], e[12], e[13]);
+        }
+    }
+    const int32_t nm = (int32_t)hinfo[1];
+    if (nm < 0 || nm > copy_cap) {
+        set_last_error("plan chain: move count out of range");
+        return CA_EDEVICE;
+    }
+    // the moves, the callers' hints and the PDB budgets (page-locked staging reused: the
+    // inputs are consumed)
+    if (nm > 0) CA_HIP_CHECK(hipMemcpyAsync(hmoves, dmoves, sizeof(ca_plan_move) * nm, hipMemcpyDeviceToHost, st));
+    if (hints && n_pods > 0) CA_HIP_CHECK(hipMemcpyAsync(hw + o_h, dH, 4 * (size_t)n_pods, hipMemcpyDeviceToHost, st));
+    if (P > 0) CA_HIP_CHECK(hipMemcpyAsync(hw + o_al, din + o_al, 4 * (size_t)P, hipMemcpyDeviceToHost, st));
+    CA_HIP_CHECK(hipStreamSynchronize(st));
+    std::memcpy(results, hres, sizeof(ca_plan_result) * C);
+    *last_index = (int32_t)hinfo[0];
+    if (simulated_out) *simulated_out = (int32_t)hinfo[3];
+    if (hints) hints_out.assign(hw + o_h, hw + o_h + n_pods);
+    if (P > 0) std::memcpy(pdbs->allowed, hw + o_al, 4 * (size_t)P);
+    moves_out.assign(hmoves, hmoves + nm);
+    const auto t_read = std::chrono::steady_clock::now();
+    // ---- replay the committed moves into the mirror (journaled at the caller's depth) ----
+    for (int32_t k = 0; k < nm;) {
+        const int32_t cand = moves_out[k].candidate;
+        int32_t e = k;
+        while (e < nm && moves_out[e].candidate == cand) e++;
+        for (int32_t t = k; t < e; t++)
+            if ((rc = ca_mirror_remove_pod(m, moves_out[t].pod)) != CA_OK) return rc;   // cluster.go:228-233
+        for (int32_t t = k; t < e; t++) {
+            const int32_t nid = m->store_moved_copy(moves_out[t].pod);
+            if (nid != moves_out[t].new_pod) {
+                set_last_error("plan chain: copy ids out of step with the mirror");
+                return CA_EDEVICE;
+            }
+            m->add_pod_to_node(nid, moves_out[t].node);                                   // AddPod (:79)
+        }
+        k = e;
+    }
+    const auto t_end = std::chrono::steady_clock::now();
+    {
+        PlanStats& ps = m->plan;
+        auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return std::chrono::duration<float, std::milli>(b - a).count();
+        };
+        float kms = 0;
+        (void)hipEventElapsedTime(&kms, m->ev0, m->ev1);
+        ps.chain_prof.assign(hinfo + 4, hinfo + 4 + PC_NPROF);
+        ps.host_ms[0] = ms(t0, t_sync);          // mirror row / pod sync
+        ps.host_ms[1] = ms(t_sync, t_kernel);    // inputs, kernel, results back
+        ps.host_ms[2] = kms;                     // the kernel (events)
+        ps.host_ms[3] = ms(t_kernel, t_read);    // moves, hints, budgets back
+        ps.host_ms[4] = ms(t_read, t_end);       // replay into the mirror
+        if (getenv("CASIM_DEBUG_TIMING"))
+            fprintf(stderr, "[plan chain] sync %.3f  launch+kernel %.3f (kernel %.3f)  readback %.3f  replay %.3f ms\n",
+                    ps.host_ms[0], ps.host_ms[1], ps.host_ms[2], ps.host_ms[3], ps.host_ms[4]);
+    }
+    return 1;
+}
+
+}  // namespace casim

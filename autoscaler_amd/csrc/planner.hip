@@ -96,6 +96,15 @@ int32_t ca_mirror::store_moved_copy(int32_t pod) {
     return (int32_t)pods.size() - 1;
 }
 
+// plan_chain.hip: the whole loop as one device-resident chain (1 = ran, 0 = outside its scope)
+namespace casim {
+int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uint8_t* dest_mask,
+                   const int32_t* cand_status, const int32_t* move_off, const int32_t* move_pods,
+                   int32_t max_removable, const ca_pdb_table* pdbs, int32_t* hints, int32_t n_pods,
+                   int32_t* last_index, ca_plan_result* results, std::vector<ca_plan_move>& moves_out,
+                   std::vector<int32_t>& hints_out, int32_t* simulated_out);
+}  // namespace casim
+
 namespace {
 
 int plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const uint8_t* dest_mask,
@@ -135,6 +144,33 @@ int plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const uint
         return CA_OK;
     }
     if (m->n_scope_blockers > 0) return CA_EUNSUPPORTED;                         // casim.h scope
+    const char* fail_env = getenv("CASIM_PLAN_FAIL_ROUND");          // tests: an error in that round
+    const int32_t fail_round = fail_env ? atoi(fail_env) : 0;
+    {
+        // the device-resident chain (plan_chain.hip); the speculative windows below otherwise
+        int32_t sim = 0, Lc = *last_index;
+        std::vector<int32_t> hc;
+        const int rc = plan_chain_run(m, candidates, C, dest_mask, cand_status, move_off, move_pods, max_removable,
+                                      pdbs, hints, n_pods, &Lc, results, ps.moves, hc, &sim);
+        if (rc < 0) return rc;
+        if (rc == 1) {
+            ps.rounds = 1;
+            ps.simulated = sim;
+            ps.path = 1;
+            if (fail_round == 1) {
+                set_last_error("CASIM_PLAN_FAIL_ROUND: injected failure");
+                return CA_EDEVICE;
+            }
+            *last_index = Lc;
+            if (hints && n_pods > 0) std::memcpy(hints, hc.data(), sizeof(int32_t) * (size_t)n_pods);
+            const int32_t nm = (int32_t)ps.moves.size();
+            if (moves) std::memcpy(moves, ps.moves.data(), sizeof(ca_plan_move) * (size_t)std::min(nm, moves_cap));
+            if (n_moves) *n_moves = nm;
+            ps.total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            return CA_OK;
+        }
+        ps.path = 0;
+    }
 
     std::vector<uint8_t> mask(dest_mask, dest_mask + N);                         // podDestinations
     std::vector<int32_t> H(m->pods.size(), -1);                                   // Hints by pod (copies share)
@@ -164,8 +200,6 @@ int plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const uint
     bool done = false;
     const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
     const char* why = "";
-    const char* fail_env = getenv("CASIM_PLAN_FAIL_ROUND");          // tests: an error in that round
-    const int32_t fail_round = fail_env ? atoi(fail_env) : 0;
 
     auto not_run = [&](int32_t from) {
         for (int32_t c = from; c < C; c++) {
@@ -384,6 +418,16 @@ int ca_plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const u
     return ca_mirror_commit(m);
 }
 
+int ca_plan_last_path(const ca_mirror* m) { return m ? m->plan.path : CA_EINVAL; }
+
+int ca_plan_chain_profile(const ca_mirror* m, uint64_t* cycles, int32_t cap, float* host_ms) {
+    if (!m || cap < 0 || (cap > 0 && !cycles)) return CA_EINVAL;
+    const int32_t k = (int32_t)m->plan.chain_prof.size();
+    for (int32_t i = 0; i < k && i < cap; i++) cycles[i] = m->plan.chain_prof[i];
+    if (host_ms) for (int i = 0; i < 5; i++) host_ms[i] = m->plan.host_ms[i];
+    return k;
+}
+
 int ca_plan_last_moves(const ca_mirror* m, ca_plan_move* out, int32_t cap) {
     if (!m || cap < 0 || (cap > 0 && !out)) return CA_EINVAL;
     const int32_t nm = (int32_t)m->plan.moves.size();
@@ -393,6 +437,7 @@ int ca_plan_last_moves(const ca_mirror* m, ca_plan_move* out, int32_t cap) {
 
 int ca_plan_stats(const ca_mirror* m, int32_t* rounds, int32_t* conflicts, int32_t* simulated, float* total_ms) {
     if (!m) return CA_EINVAL;
+    // (the path of the last call: m->plan.path, 1 = device chain, 0 = speculative windows)
     if (rounds) *rounds = m->plan.rounds;
     if (conflicts) *conflicts = m->plan.conflicts;
     if (simulated) *simulated = m->plan.simulated;

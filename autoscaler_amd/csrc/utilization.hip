@@ -15,6 +15,9 @@
 // (C5) launch 938 workgroups, 3 750 wavefronts: one resident round on 256 CUs.
 #include "casim_internal.h"
 
+#include <algorithm>
+#include <vector>
+
 
 struct ca_util_table {
     int device = 0;
@@ -22,9 +25,16 @@ struct ca_util_table {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int32_t n_nodes = 0, n_pods = 0;
     casim::DevBuf nodes, pod_off, pods, info;
+    // pods added since the rows were set (ca_util_table_set_added): CSR by node
+    int32_t n_added = 0;
+    casim::DevBuf added;                 // [add_off n_nodes + 1][pad][add_pods n_added]
+    casim::HostBuf h_added;
 };
 
 namespace {
+
+// byte offset of the added pods behind their offsets in ca_util_table::added
+inline size_t added_pods_at(int32_t n_nodes) { return ((sizeof(int32_t) * ((size_t)n_nodes + 1)) + 63) & ~(size_t)63; }
 
 constexpr int kLanes = 16;                                    // lanes per node (C5: ~20 pods/node)
 constexpr int kThreads = 256;
@@ -45,7 +55,8 @@ __device__ inline int64_t seg_sum(int64_t v) {                // within a kLanes
 __global__ __launch_bounds__(kThreads) void k_node_utilization(
     const ca_util_node* __restrict__ nodes, const int32_t* __restrict__ pod_off,
     const ca_util_pod* __restrict__ pods, int32_t n_nodes, int32_t skip_ds, int32_t skip_mirror,
-    int64_t now_ns, ca_util_info* __restrict__ out) {
+    int64_t now_ns, ca_util_info* __restrict__ out, const int32_t* __restrict__ add_off,
+    const ca_util_pod* __restrict__ add_pods) {
     const int sub = threadIdx.x & (kLanes - 1);
     const int32_t node = blockIdx.x * (kThreads / kLanes) + (int32_t)(threadIdx.x / kLanes);
     if (node >= n_nodes) return;                                  // whole segments only
@@ -53,8 +64,12 @@ __global__ __launch_bounds__(kThreads) void k_node_utilization(
     const ca_util_node nd = nodes[node];                          // in flight during the pod loop
     int64_t req[3] = {0, 0, 0}, dsm[3] = {0, 0, 0};
     int drain = 0;
-    for (int32_t i = b + sub; i < e; i += kLanes) {               // info.go:100-124
-        const ca_util_pod p = pods[i];
+    // the node's rows, then the pods added to it since (integer sums and flag ORs: the
+    // order of the pods does not matter)
+    const int32_t ab = add_off ? add_off[node] : 0, ae = add_off ? add_off[node + 1] : 0;
+    const int32_t tot = (e - b) + (ae - ab);
+    for (int32_t k = sub; k < tot; k += kLanes) {                 // info.go:100-124
+        const ca_util_pod p = k < e - b ? pods[b + k] : add_pods[ab + (k - (e - b))];
         drain |= (int)(p.flags & (CA_UPOD_MOVABLE | CA_UPOD_BLOCKING));
         const bool factored = (skip_ds && (p.flags & CA_UPOD_DAEMONSET)) ||
                               (skip_mirror && (p.flags & CA_UPOD_MIRROR));
@@ -171,6 +186,32 @@ int ca_util_table_update(ca_util_table* t, const ca_util_node* nodes, int32_t n_
     CA_HIP_CHECK(hipStreamSynchronize(t->stream));
     t->n_nodes = n_nodes;
     t->n_pods = n_pods;
+    t->n_added = 0;
+    return CA_OK;
+}
+
+int ca_util_table_set_added(ca_util_table* t, const int32_t* node, const ca_util_pod* pods, int32_t n) {
+    if (!t || n < 0 || (n > 0 && (!node || !pods))) return CA_EINVAL;
+    for (int32_t k = 0; k < n; k++)
+        if (node[k] < 0 || node[k] >= t->n_nodes) return CA_EINVAL;
+    CA_HIP_CHECK(hipSetDevice(t->device));
+    t->n_added = 0;
+    if (n == 0) return CA_OK;
+    // counting sort by node, straight into page-locked staging: [offsets][pods]
+    const size_t at = added_pods_at(t->n_nodes);
+    const size_t bytes = at + sizeof(ca_util_pod) * (size_t)n;
+    int st;
+    if ((st = t->added.reserve(bytes)) != CA_OK || (st = t->h_added.reserve(bytes)) != CA_OK) return st;
+    int32_t* off = t->h_added.as<int32_t>();
+    ca_util_pod* out = reinterpret_cast<ca_util_pod*>(t->h_added.as<unsigned char>() + at);
+    std::fill(off, off + t->n_nodes + 1, 0);
+    for (int32_t k = 0; k < n; k++) off[node[k] + 1]++;
+    for (int32_t i = 0; i < t->n_nodes; i++) off[i + 1] += off[i];
+    std::vector<int32_t> fill(off, off + t->n_nodes);
+    for (int32_t k = 0; k < n; k++) out[fill[node[k]]++] = pods[k];
+    CA_HIP_CHECK(hipMemcpyAsync(t->added.ptr, t->h_added.ptr, bytes, hipMemcpyHostToDevice, t->stream));
+    CA_HIP_CHECK(hipStreamSynchronize(t->stream));          // the staging buffer is reused
+    t->n_added = n;
     return CA_OK;
 }
 
@@ -182,6 +223,8 @@ int ca_util_table_destroy(ca_util_table* t) {
     t->pod_off.release();
     t->pods.release();
     t->info.release();
+    t->added.release();
+    t->h_added.release();
     if (t->ev0) (void)hipEventDestroy(t->ev0);
     if (t->ev1) (void)hipEventDestroy(t->ev1);
     if (t->stream) (void)hipStreamDestroy(t->stream);
@@ -200,7 +243,11 @@ int ca_util_calculate(ca_util_table* t, int32_t skip_daemonset_pods, int32_t ski
         hipLaunchKernelGGL(k_node_utilization, dim3(blocks), dim3(kThreads), 0, t->stream,
                            t->nodes.as<const ca_util_node>(), t->pod_off.as<const int32_t>(),
                            t->pods.as<const ca_util_pod>(), t->n_nodes, skip_daemonset_pods ? 1 : 0,
-                           skip_mirror_pods ? 1 : 0, now_ns, t->info.as<ca_util_info>());
+                           skip_mirror_pods ? 1 : 0, now_ns, t->info.as<ca_util_info>(),
+                           t->n_added > 0 ? t->added.as<const int32_t>() : nullptr,
+                           t->n_added > 0 ? reinterpret_cast<const ca_util_pod*>(
+                                                t->added.as<unsigned char>() + added_pods_at(t->n_nodes))
+                                          : nullptr);
         CA_HIP_CHECK(hipGetLastError());
         CA_HIP_CHECK(hipEventRecord(t->ev1, t->stream));
         if (out)

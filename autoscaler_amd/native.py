@@ -96,6 +96,7 @@ def load() -> C.CDLL:
         "ca_util_table_create": ([i32, vp, i32, vp, vp, p(vp)], C.c_int),
         "ca_util_table_destroy": ([vp], C.c_int),
         "ca_util_table_update": ([vp, vp, i32, vp, vp], C.c_int),
+        "ca_util_table_set_added": ([vp, vp, vp, i32], C.c_int),
         "ca_util_calculate": ([vp, i32, i32, C.c_int64, vp, p(C.c_float)], C.c_int),
         "ca_util_device_results": ([vp, p(vp)], C.c_int),
         "ca_multi_create": ([p(vp), i32, p(vp)], C.c_int),
@@ -113,6 +114,8 @@ def load() -> C.CDLL:
         "ca_plan_removals": ([vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, i32, p(i32), vp, vp, i32, p(i32)], C.c_int),
         "ca_plan_last_moves": ([vp, vp, i32], C.c_int),
         "ca_plan_stats": ([vp, p(i32), p(i32), p(i32), p(C.c_float)], C.c_int),
+        "ca_plan_last_path": ([vp], C.c_int),
+        "ca_plan_chain_profile": ([vp, vp, i32, vp], C.c_int),
     }
     for name, (args, res) in sigs.items():
         if path != LIB_PATH and not hasattr(lib, name):
@@ -155,11 +158,12 @@ def exported_symbols() -> list[str]:
         "ca_removal_plan_destroy", "ca_mirror_set_hints", "ca_mirror_get_hints",
         "ca_removal_candidate_ticks", "ca_filter_out_schedulable", "ca_filter_stats",
         "ca_util_table_create", "ca_util_table_destroy", "ca_util_calculate", "ca_util_device_results",
-        "ca_util_table_update", "ca_multi_create", "ca_multi_destroy", "ca_multi_estimate_plan_create", "ca_multi_estimate_plan_run",
+        "ca_util_table_update", "ca_util_table_set_added", "ca_multi_create", "ca_multi_destroy",
+        "ca_multi_estimate_plan_create", "ca_multi_estimate_plan_run",
         "ca_multi_estimate_plan_stats", "ca_multi_estimate_plan_destroy", "ca_multi_estimate_batch",
         "ca_multi_removal_plan_create", "ca_multi_removal_plan_run", "ca_multi_removal_plan_stats",
         "ca_multi_removal_plan_destroy", "ca_multi_find_nodes_to_remove",
-        "ca_plan_removals", "ca_plan_last_moves", "ca_plan_stats",
+        "ca_plan_removals", "ca_plan_last_moves", "ca_plan_stats", "ca_plan_last_path", "ca_plan_chain_profile",
     ]
 
 
@@ -504,7 +508,20 @@ class Mirror:
         r, c, s = C.c_int32(0), C.c_int32(0), C.c_int32(0)
         t = C.c_float(0)
         _check(self.lib.ca_plan_stats(self.h, C.byref(r), C.byref(c), C.byref(s), C.byref(t)), "ca_plan_stats")
-        return {"rounds": r.value, "conflicts": c.value, "simulated": s.value, "total_ms": t.value}
+        return {"rounds": r.value, "conflicts": c.value, "simulated": s.value, "total_ms": t.value,
+                "path": "chain" if self.lib.ca_plan_last_path(self.h) == 1 else "speculative"}
+
+    def plan_chain_profile(self) -> dict:
+        """Phase cycle counters and host timings of the last device-chain planner call."""
+        cyc = np.zeros(16, np.uint64)
+        hm = np.zeros(5, np.float32)
+        k = self.lib.ca_plan_chain_profile(self.h, cyc.ctypes.data, 16, hm.ctypes.data)
+        names = ["init", "lists", "pdb", "fork", "hint", "scan", "add", "commit", "revert", "total", "blocks",
+                 "windows"]
+        out = {nm: int(v) for nm, v in zip(names, cyc[:max(k, 0)])}
+        out.update({h: float(v) for h, v in zip(["sync_ms", "launch_kernel_ms", "kernel_ms", "readback_ms",
+                                                   "replay_ms"], hm)})
+        return out
 
     def set_hints(self, hints) -> None:
         """The mirror's resident HintingSimulator hints (node per mirror pod, -1 = none)."""
@@ -786,6 +803,13 @@ class UtilTable:
         self.pods = np.ascontiguousarray(pods, abi.UTIL_POD_DTYPE)
         _check(self.lib.ca_util_table_update(self.h, ptr(self.nodes), len(self.nodes), ptr(self.pod_off),
                                              ptr(self.pods)), "ca_util_table_update")
+
+    def set_added(self, node, pods) -> None:
+        """Pods added to the snapshot since the rows were set: pods[k] on node[k]."""
+        self.added_node = np.ascontiguousarray(node, np.int32)
+        self.added_pods = np.ascontiguousarray(pods, abi.UTIL_POD_DTYPE)
+        _check(self.lib.ca_util_table_set_added(self.h, ptr(self.added_node), ptr(self.added_pods),
+                                                len(self.added_node)), "ca_util_table_set_added")
 
     def calculate(self, skip_daemonset_pods: bool, skip_mirror_pods: bool, now_ns: int,
                   to_host: bool = True):

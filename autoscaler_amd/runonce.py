@@ -109,6 +109,38 @@ def _zeros(key: str, n: int, dtype) -> np.ndarray:
     return np.zeros(n, dtype)
 
 
+def cpu_util(ui: "UtilInput", now_ns: int):
+    """The CPU port's utilization step (oracle/casim_oracle.c or_node_utilization)."""
+    import pyoracle                                   # the checker / CPU baseline only
+    return pyoracle.node_utilization(ui.nodes, ui.off, ui.pods, False, False, now_ns)
+
+
+class DeviceUtil:
+    """The device's utilization step: one resident ca_util_table per loop start snapshot,
+    the pods FilterOutSchedulable added sent as ca_util_table_set_added."""
+    want = "added"
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self.table = None
+        self.base_id = None
+
+    def __call__(self, ui: "UtilInput", now_ns: int):
+        from . import native
+        if self.table is None or self.base_id is not id(ui.base):
+            if self.table is not None:
+                self.table.close()
+            self.table = native.UtilTable(self.device, *ui.base)
+            self.base_id = id(ui.base)
+        self.table.set_added(ui.added_node, ui.added_pods)
+        return self.table.calculate(False, False, now_ns)
+
+    def close(self):
+        if self.table is not None:
+            self.table.close()
+            self.table = None
+
+
 def _util_rows(w: RunOnceWorkload, placed_node: np.ndarray, zeros=_zeros):
     """ca_util_node / ca_util_pod rows of the snapshot after FilterOutSchedulable: each
     node's running pods, then the pods placed on it (NodeInfo.Pods order).  `zeros(key, n,
@@ -137,10 +169,46 @@ def _util_rows(w: RunOnceWorkload, placed_node: np.ndarray, zeros=_zeros):
     return nodes, off, pods, order
 
 
+def _util_base(w: RunOnceWorkload):
+    """ca_util_node rows and the running pods' ca_util_pod rows by node (the snapshot the
+    loop starts from; cached on the workload)."""
+    if getattr(w, "_ubase", None) is None:
+        nodes, off, pods, _ = _util_rows(w, np.full(len(w.filt.order), -1, np.int32))
+        w._ubase = (nodes, off, pods)
+    return w._ubase
+
+
+def _util_added(w: RunOnceWorkload, placed_node: np.ndarray):
+    """(node, ca_util_pod row) of every pod FilterOutSchedulable placed, in placement order."""
+    f = w.filt
+    placed = np.nonzero(placed_node >= 0)[0]
+    ids = f.order[placed]
+    pods = np.zeros(len(placed), abi.UTIL_POD_DTYPE)
+    pods["req_milli"][:, 0] = f.pending.pods["req_milli_cpu"][ids]
+    pods["req_milli"][:, 1] = f.pending.pods["req_memory"][ids] * 1000
+    pods["flags"] = abi.CA_UPOD_MOVABLE
+    return placed_node[placed].astype(np.int32), pods
+
+
+class UtilInput:
+    """The utilization step's input, built before its timer: the full rows of the snapshot
+    after FilterOutSchedulable (``want = "full"``: the CPU port), or the loop's starting rows
+    plus the pods added since (``want = "added"``: the device table keeps the starting rows
+    resident, as the mirror keeps the snapshot, and receives only the additions)."""
+
+    def __init__(self, w: RunOnceWorkload, placed_node: np.ndarray, want: str, zeros=_zeros):
+        self.want = want
+        if want == "added":
+            self.base = _util_base(w)
+            self.added_node, self.added_pods = _util_added(w, placed_node)
+        else:
+            self.nodes, self.off, self.pods, _ = _util_rows(w, placed_node, zeros)
+
+
 def run(backend, util_fn, w: RunOnceWorkload, timers=None, row_zeros=_zeros) -> RunOnceResult:
     """One loop on `backend` (native.Mirror or pyoracle.OracleState, freshly loaded with
-    W.load_filter) with `util_fn(nodes, off, pods, now_ns) -> UTIL_INFO rows`; `row_zeros`
-    allocates the utilization rows (native.PinnedRows.zeros for the device)."""
+    W.load_filter) with `util_fn(UtilInput, now_ns) -> UTIL_INFO rows` (its attribute `want`,
+    default "full", picks the input form); `row_zeros` allocates full utilization rows."""
     f = w.filt
     r = RunOnceResult()
     clock = time.perf_counter
@@ -181,9 +249,9 @@ def run(backend, util_fn, w: RunOnceWorkload, timers=None, row_zeros=_zeros) -> 
         ps.close()
 
     # 4. scale-down eligibility on the snapshot after step 1
-    unodes, uoff, upods, _ = _util_rows(w, fo.node, row_zeros)
+    ui = UtilInput(w, fo.node, getattr(util_fn, "want", "full"), row_zeros)
     t = clock()
-    r.util = util_fn(unodes, uoff, upods, w.now_ns)
+    r.util = util_fn(ui, w.now_ns)
     r.ms["utilization"] = (clock() - t) * 1e3
     low = np.nonzero((r.util["status"] == 0) & (r.util["utilization"] < UTIL_THRESHOLD))[0].astype(np.int32)
     r.empty = low[r.util["empty"][low] != 0]

@@ -371,7 +371,7 @@ def planner_leg(args, device: int, with_cpu: bool) -> dict:
             st = m.plan_stats()
             m.revert()
             firsts.setdefault(limit, r)
-        out["runs"][str(limit)] = {"gpu_ms": float(min(ts[1:]) * 1e3), "rounds": st["rounds"],
+        out["runs"][str(limit)] = {"gpu_ms": float(min(ts[1:]) * 1e3), "path": st["path"], "rounds": st["rounds"],
                                    "conflicts": st["conflicts"], "simulated": st["simulated"],
                                    "removable": int(r.results["removable"].sum()),
                                    "candidates_run": int((r.results["reason"] != 101).sum())}
@@ -407,23 +407,15 @@ def runonce_leg(args, device: int, with_cpu: bool) -> dict:
     m = native.Mirror(device)
     W.load_filter(m, w.filt)
 
-    ut = []                                                       # one resident table, rows replaced per loop
-
-    def util(n, off, p, now):
-        if not ut:
-            ut.append(native.UtilTable(device, n, off, p))
-        else:
-            ut[0].update(n, off, p)
-        return ut[0].calculate(False, False, now)
+    # the utilization table holds the loop's starting snapshot resident (as the mirror does)
+    # and receives the pods FilterOutSchedulable added (ca_util_table_set_added)
+    util = runonce.DeviceUtil(device)
     runs = []
-    rows = native.PinnedRows()                                    # utilization rows built in page-locked memory
     for _ in range(1 + max(2, min(args.steps, 4))):
         m.fork()
-        runs.append(runonce.run(m, util, w, row_zeros=rows.zeros))
+        runs.append(runonce.run(m, util, w))
         m.revert()
-    if ut:
-        ut[0].close()
-    rows.close()
+    util.close()
     m.close()
     keys = list(runs[-1].ms)
     out = {"workload": "C5 RunOnce: 15000 nodes, 300000 running pods, 20000 pending (15% of the controller "
@@ -435,7 +427,7 @@ def runonce_leg(args, device: int, with_cpu: bool) -> dict:
         import pyoracle                                           # CPU baseline leg only
         o = pyoracle.OracleState()
         W.load_filter(o, w.filt)
-        ro = runonce.run(o, lambda n, off, p, now: pyoracle.node_utilization(n, off, p, False, False, now), w)
+        ro = runonce.run(o, runonce.cpu_util, w)
         out["cpu_ms"] = ro.ms
         out["speedup"] = {k: ro.ms[k] / out["gpu_ms"][k] for k in keys if out["gpu_ms"][k] > 0}
         out["parity"] = runonce.compare(ro, runs[-1])

@@ -556,6 +556,11 @@ int ca_util_table_destroy(ca_util_table* t);
  * placed pods), reusing its device buffers. */
 int ca_util_table_update(ca_util_table* t, const ca_util_node* nodes, int32_t n_nodes, const int32_t* pod_off,
                          const ca_util_pod* pods);
+/* Pods added to the snapshot since the rows were set (AddPod: FilterOutSchedulable's
+ * placements, static_autoscaler.go:528): pods[k] now runs on node[k].  Replaces the previous
+ * added set (n = 0 clears it; ca_util_table_update clears it too).  Calculate counts them
+ * with the node's rows — only these records cross PCIe, not the node's whole pod list. */
+int ca_util_table_set_added(ca_util_table* t, const int32_t* node, const ca_util_pod* pods, int32_t n);
 /* Calculate(nodeInfo, skipDaemonSetPods, skipMirrorPods, gpuConfig, currentTime) for every
  * node.  out NULL keeps the results in HBM (ca_util_device_results); otherwise out[n_nodes]
  * is filled.  *kernel_ms (may be NULL) = device time of the kernel. */
@@ -676,6 +681,15 @@ int ca_plan_last_moves(const ca_mirror* m, ca_plan_move* out, int32_t cap);
 /* last call: speculation rounds, rounds cut short by a commit conflict, candidates
  * simulated on the device (all rounds), host wall time (ms) */
 int ca_plan_stats(const ca_mirror* m, int32_t* rounds, int32_t* conflicts, int32_t* simulated, float* total_ms);
+/* how the last ca_plan_removals ran: 1 = one device-resident chain over every candidate
+ * (node rows in LDS; no pod to move with host ports or extended resources), 0 = speculative
+ * sweep windows validated on the host (every other case) */
+int ca_plan_last_path(const ca_mirror* m);
+/* diagnostics of the last device-chain call: shader-clock cycles per phase (init, pod lists,
+ * PDB checks, fork, hint checks, scans, AddPod, commit, revert, total, scanned blocks,
+ * skip windows) into cycles[cap]; host_ms[5] = mirror sync, launch + kernel, kernel,
+ * readback, replay into the mirror.  Returns the number of counters. */
+int ca_plan_chain_profile(const ca_mirror* m, uint64_t* cycles, int32_t cap, float* host_ms);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,41 @@
+"""Phase profile of the device-chain planner (ca_plan_removals, plan_chain.hip) on C3 at the
+bench's limits: host timings and the kernel's shader-clock counters per phase.
+(scripts/gpu_job.sh script "scripts/plan_prof.py [n_nodes]")"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("CASIM_LIB_PATH", os.path.join(ROOT, "autoscaler_amd", "lib", "libcasim_prof.so")) if "--prof" in sys.argv else None
+sys.argv = [a for a in sys.argv if a != "--prof"]
+from autoscaler_amd import native, workloads as W  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
+w = W.c3(n_nodes=n)
+args = (w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods)
+hints = np.full(len(w.table), -1, np.int32)
+for limit in (20, 200, 0):
+    m = native.Mirror(0)
+    W.load_sweep(m, w)
+    for rep in range(3):
+        m.fork()
+        t = time.perf_counter()
+        r = m.plan_removals(*args, hints, 0, limit)
+        dt = (time.perf_counter() - t) * 1e3
+        st = m.plan_stats()
+        pr = m.plan_chain_profile()
+        m.revert()
+    tot = max(pr.get("total", 1), 1)
+    ghz = tot / (pr["kernel_ms"] * 1e6) if pr["kernel_ms"] > 0 else 0
+    print(f"limit {limit}: {dt:.3f} ms path {st['path']} simulated {st['simulated']} "
+          f"evals {int(r.results['evals'].sum())} moves {len(r.moves)}", flush=True)
+    print("   host: " + "  ".join(f"{k}={pr[k]:.3f}" for k in
+                                   ("sync_ms", "launch_kernel_ms", "kernel_ms", "readback_ms", "replay_ms")))
+    print(f"   kernel clock {ghz:.2f} GHz; phases (% of total cycles): " +
+          "  ".join(f"{k}={100 * pr[k] / tot:.1f}" for k in
+                    ("init", "lists", "pdb", "fork", "hint", "scan", "add", "commit", "revert")))
+    print(f"   blocks scanned {pr['blocks']}  skip windows {pr['windows']}", flush=True)
+    m.close()

@@ -16,15 +16,9 @@ m = native.Mirror(0)
 W.load_filter(m, w.filt)
 
 
-ut = []
 
 
-def util(n, off, p, now):
-    if not ut:
-        ut.append(native.UtilTable(0, n, off, p))
-    else:
-        ut[0].update(n, off, p)
-    return ut[0].calculate(False, False, now)
+util = runonce.DeviceUtil(0)
 
 
 for rep in range(3):

@@ -12,7 +12,7 @@ def _oracle_run(w):
     from autoscaler_amd import workloads as W
     o = pyoracle.OracleState()
     W.load_filter(o, w.filt)
-    return runonce.run(o, lambda n, off, p, now: pyoracle.node_utilization(n, off, p, False, False, now), w)
+    return runonce.run(o, runonce.cpu_util, w)
 
 
 def test_runonce_small_oracle(oracle_lib):
@@ -38,13 +38,14 @@ def test_runonce_gpu_parity(size, oracle_lib):
     m = native.Mirror(0)
     W.load_filter(m, w.filt)
 
-    def util(n, off, p, now):
-        t = native.UtilTable(0, n, off, p)
-        try:
-            return t.calculate(False, False, now)
-        finally:
-            t.close()
+    util = runonce.DeviceUtil(0)
     rg = runonce.run(m, util, w)
+    # the full rows through one table, as a second form of the same step
+    full = runonce.UtilInput(w, rg.filter_node, "full")
+    t = native.UtilTable(0, full.nodes, full.off, full.pods)
+    assert t.calculate(False, False, w.now_ns).tobytes() == rg.util.tobytes()
+    t.close()
+    util.close()
     m.close()
     eq = runonce.compare(ro, rg)
     assert all(eq.values()), eq

@@ -612,6 +612,24 @@ __global__ void __launch_bounds__(256) k_emit_bucket(const GroupMeta* __restrict
     if (lane == 0) heads[gm.moff + (i >> 6)] = hb;
 }
 
+// Decoupled Go order: the group's pod ids in sort.Slice order over the stream written in
+// stable class order (same class at every position; the classes' pods are
+// interchangeable for the chain: ca_podset::cls_uniform), then the group's ready flag.
+__global__ void __launch_bounds__(1024) k_emit_go_ids(const GroupMeta* __restrict__ groups,
+                                                     const uint32_t* __restrict__ sorted,
+                                                     const int32_t* __restrict__ pod_idx, int32_t* __restrict__ spod,
+                                                     int32_t* __restrict__ ids_ready, const int32_t* __restrict__ gmap) {
+    const int gi = GSEL(blockIdx.x);
+    const GroupMeta gm = groups[gi];
+    for (int32_t i = threadIdx.x; i < gm.count; i += blockDim.x)
+        spod[gm.off + i] = pod_idx[gm.off + (int32_t)sorted[gm.off + i]];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        __hip_atomic_store(&ids_ready[gi], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // 4. the First-Fit-Decreasing chain -------------------------------------------
 #ifdef CASIM_PROF   // section cycle counters of k_ffd_chain (profiling build only)
 constexpr int NPROF = 12;
@@ -994,7 +1012,10 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
                                                 int32_t* __restrict__ qctl, int32_t total, int32_t nsub,
                                                 const int2* __restrict__ prog, int32_t pch,
                                                 T* pub,              // pub may alias sched_dev (device results)
-                                                uint64_t start_ticks) {
+                                                uint64_t start_ticks, const int32_t* ids_ready) {
+    // ids_ready != null (decoupled Go order): the stream's pod ids in spod
+    // come from a sort that runs beside the chains — a group's are final once
+    // ids_ready[g] is set — and the chains' single placements are stream positions
     __shared__ int32_t s_t, s_seg0;
     __shared__ int64_t s_tk;
     for (;;) {
@@ -1015,6 +1036,19 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
                         break;
                     }
                     __builtin_amdgcn_s_sleep(2);
+                }
+                if (tk >= 0 && ids_ready) {                  // the group's Go-order ids
+                    const int32_t g = (int32_t)(uint32_t)(tk & 0xFFFFFFFFll) / nsub;
+                    for (;;) {
+                        if (__hip_atomic_load(&ids_ready[g], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) break;
+                        if (__hip_atomic_load(&qctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { tk = -1; break; }
+                        if (wall_clock64() - t0 > 20000000ull) {                            // 200 ms
+                            __hip_atomic_store(&qctl[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            tk = -1;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(2);
+                    }
                 }
             }
             s_tk = tk;
@@ -1066,7 +1100,9 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
                 }
             }
             for (int32_t i = at + (int32_t)threadIdx.x; i < lim; i += blockDim.x)
-                pub[gm.off + i] = (T)(from_seg ? spod[gm.off + src_off + i] : sched_dev[gm.off + i]);
+                pub[gm.off + i] = (T)(from_seg ? spod[gm.off + src_off + i]
+                                               : ids_ready ? spod[gm.off + ld_coh(sched_dev + gm.off + i)]
+                                                           : sched_dev[gm.off + i]);
             at = lim;
         }
         for (int32_t i = max(a, ns) + (int32_t)threadIdx.x; i < b; i += blockDim.x) pub[gm.off + i] = (T)-1;
@@ -1097,7 +1133,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     int32_t* __restrict__ sched_pod, int32_t* __restrict__ sched_node, Seg* __restrict__ segs,
     int64_t* __restrict__ tickets, int32_t* __restrict__ qctl, int32_t nsub, int2* __restrict__ prog, int32_t pch,
     ChainOut* __restrict__ outs, const int32_t* __restrict__ gmap, unsigned char* __restrict__ gslab,
-    const int64_t* __restrict__ slab_off, const int32_t* __restrict__ gkcap) {
+    const int64_t* __restrict__ slab_off, const int32_t* __restrict__ gkcap, int32_t pos_out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int g = GSEL(blockIdx.x);
     // GROWS: the group's rows live in its own HBM slab (kcap = the group's pod count, for an
@@ -1214,7 +1250,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
         const int32_t c1 = nsched / pch;
         if (c1 <= tk_next) return;
         if (pend) {                       // the pending single placement, stored now
-            so_pod[out_idx] = cur.pod;
+            so_pod[out_idx] = pos_out ? wbase + lane : cur.pod;
             pend = false;
         }
         push_chunks(g, tk_next, c1, nsub, tickets, qctl, prog, nseg, nsched, lane, pch, pure_from, pure_off);
@@ -1225,7 +1261,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     while (pos < P && !stop) {
         if (pos >= wbase + 64) {
             if (pend) {
-                so_pod[out_idx] = cur.pod;
+                so_pod[out_idx] = pos_out ? wbase + lane : cur.pod;
                 if (so_node) so_node[out_idx] = out_node;
             }
             pend = false;
@@ -1806,7 +1842,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
         cbar<GROWS>();                        // the placement is visible to every wave
     }
     if (pend) {
-        so_pod[out_idx] = cur.pod;
+        so_pod[out_idx] = pos_out ? wbase + lane : cur.pod;
         if (so_node) so_node[out_idx] = out_node;
     }
     // newNodesWithPods
@@ -1868,7 +1904,7 @@ constexpr int CPY_PER_BLOCK = 2048;
 __global__ void __launch_bounds__(256) k_copy_segments(const GroupMeta* __restrict__ groups,
                                                       const ChainOut* __restrict__ outs, const Seg* __restrict__ segs,
                                                       const int32_t* __restrict__ spod, int32_t* __restrict__ sched_pod,
-                                                      int32_t* __restrict__ sched_node) {
+                                                      int32_t* __restrict__ sched_node, int32_t map_singles) {
     const GroupMeta gm = groups[blockIdx.y];
     const ChainOut o = outs[blockIdx.y];
     const int32_t base = (int32_t)blockIdx.x * CPY_PER_BLOCK;
@@ -1893,12 +1929,17 @@ __global__ void __launch_bounds__(256) k_copy_segments(const GroupMeta* __restri
         const Seg sg = gs[mid];
         if (sg.dst + sg.len <= base) lo = mid + 1; else hi = mid;
     }
-    for (int32_t q = lo; q < nseg; q++) {
-        const Seg sg = gs[q];
-        if (sg.dst >= lim) break;
+    int32_t at = base;                              // single placements before segment q
+    for (int32_t q = lo; q <= nseg && at < lim; q++) {
+        const Seg sg = q < nseg ? gs[q] : Seg{lim, 0, 0};
+        const int32_t gap_end = min(lim, max(at, sg.dst));
+        if (map_singles)                            // stream positions -> pod ids (decoupled Go order)
+            for (int32_t i = at + (int32_t)threadIdx.x; i < gap_end; i += blockDim.x) sp[i] = src[sp[i]];
+        if (q == nseg || sg.dst >= lim) break;
         const int32_t a = max(base, sg.dst), b = min(lim, sg.dst + sg.len);
         const int32_t off = sg.src - sg.dst;
         for (int32_t i = a + (int32_t)threadIdx.x; i < b; i += blockDim.x) sp[i] = src[off + i];
+        at = max(at, b);
     }
 }
 
@@ -1922,6 +1963,12 @@ struct ca_estimate_plan {
     // Go sort.Slice order (k_pdq_sort): element store, list scratch, frame stacks, and the
     // per-position ranks of the comparison path
     DevBuf d_pdq_e, d_pdq_scr, d_pdq_stack, d_item_rank;
+    // decoupled Go order (uniform classes): the chains run on the stable class order while
+    // k_pdq_sort + k_emit_go_ids on st3 write the Go-order ids into d_spod (d_sortC: the
+    // permutation; d_ids_ready: per group, set when its ids are final)
+    DevBuf d_sortC, d_ids_ready, d_spod_go, d_crank2;
+    hipStream_t st3 = nullptr;
+    hipEvent_t ev_emitA = nullptr, ev_emitB = nullptr, ev_ids = nullptr;
     // HBM-slab rows (k_ffd_chain<true>): per group kcap and slab offset, for the limiter
     // setting they were sized for (slab_max_nodes)
     DevBuf d_slab, d_slab_off, d_gkcap;
@@ -1963,6 +2010,10 @@ struct ca_estimate_plan {
         if (ev_pub) (void)hipEventDestroy(ev_pub);
         if (pub_stream) (void)hipStreamDestroy(pub_stream);
         if (st2) (void)hipStreamDestroy(st2);
+        if (st3) (void)hipStreamDestroy(st3);
+        if (ev_emitA) (void)hipEventDestroy(ev_emitA);
+        if (ev_emitB) (void)hipEventDestroy(ev_emitB);
+        if (ev_ids) (void)hipEventDestroy(ev_ids);
         if (ev_init) (void)hipEventDestroy(ev_init);
         if (ev_b) (void)hipEventDestroy(ev_b);
         if (ev_rb) (void)hipEventDestroy(ev_rb);
@@ -1984,6 +2035,10 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
         CA_HIP_CHECK(hipStreamCreateWithPriority(&p->st2, hipStreamNonBlocking, lo));
     }
     CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_init, hipEventDisableTiming));
+    CA_HIP_CHECK(hipStreamCreateWithFlags(&p->st3, hipStreamNonBlocking));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_emitA, hipEventDisableTiming));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_emitB, hipEventDisableTiming));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_ids, hipEventDisableTiming));
     CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_b, hipEventDisableTiming));
     CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_rb, hipEventDisableTiming));
     {
@@ -2090,6 +2145,13 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     if ((rc = p->d_pdq_stack.reserve(sizeof(pdq::Frame) * (tot / 2 + 2 * (size_t)std::max(G, 1) + 2))) != CA_OK)
         return rc;
     if (!p->bucket && (rc = p->d_item_rank.reserve(sizeof(uint32_t) * tot)) != CA_OK) return rc;
+    if (p->bucket && s->cls_uniform) {
+        if ((rc = p->d_sortC.reserve(sizeof(uint32_t) * tot)) != CA_OK) return rc;
+        if ((rc = p->d_spod_go.reserve(sizeof(int32_t) * tot)) != CA_OK) return rc;
+        if ((rc = p->d_ids_ready.reserve(sizeof(int32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
+        if ((rc = p->d_crank2.reserve(sizeof(int32_t) * (size_t)std::max(G, 1) * (size_t)std::max(s->n_cls, 1))) != CA_OK)
+            return rc;
+    }
     if (G) CA_HIP_CHECK(hipMemcpyAsync(p->d_meta.ptr, p->h_meta.data(), sizeof(GroupMeta) * G, hipMemcpyHostToDevice, st));
     if (p->total) CA_HIP_CHECK(hipMemcpyAsync(p->d_pod_idx.ptr, pod_idx, sizeof(int32_t) * p->total, hipMemcpyHostToDevice, st));
     if (G) CA_HIP_CHECK(hipMemcpyAsync(p->d_tmpl.ptr, templates, sizeof(ca_template) * G, hipMemcpyHostToDevice, st));
@@ -2140,14 +2202,14 @@ bool go_sort_order() {
 // k_pdq_sort for `ng` groups (map gm) into d_sortA: ranks from the class ranks (crank, U)
 // or from item_rank
 int launch_pdq_sort(ca_estimate_plan* p, hipStream_t ss, const int32_t* gm, int32_t ng, const int32_t* crank,
-                    int32_t U, const uint32_t* item_rank, int32_t force = 0) {
+                    int32_t U, const uint32_t* item_rank, int32_t force = 0, uint32_t* out = nullptr) {
     const int32_t lds_n = std::min(p->max_count, PDQ_LDS_N);
     const size_t lds = pdq_lds_bytes(lds_n);
     int rc;
     if ((rc = ensure_dyn_lds((const void*)k_pdq_sort, lds)) != CA_OK) return rc;
     hipLaunchKernelGGL(k_pdq_sort, dim3(ng), dim3(pdq::NT), lds, ss, p->d_meta.as<GroupMeta>(),
                        p->d_pod_idx.as<int32_t>(), p->s ? p->s->d_cls.as<int32_t>() : nullptr, crank, U, item_rank,
-                       p->d_sortA.as<uint32_t>(), p->d_pdq_e.as<uint64_t>(), p->d_pdq_scr.as<uint64_t>(),
+                       out ? out : p->d_sortA.as<uint32_t>(), p->d_pdq_e.as<uint64_t>(), p->d_pdq_scr.as<uint64_t>(),
                        p->d_pdq_stack.as<pdq::Frame>(), lds_n, force, 0, gm);
     CA_HIP_CHECK(hipGetLastError());
     return CA_OK;
@@ -2297,6 +2359,12 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     }
     const int32_t nA = split ? p->n_heavy : G, nB = split ? G - p->n_heavy : 0;
     const bool go_order = go_sort_order();
+    // decoupled Go order (uniform classes, bucket path): chains on the stable order, Go's ids
+    // beside them (CASIM_GO_DECOUPLE=0: the Go sort ahead of the stream, for tests)
+    const bool decoupled = go_order && p->bucket && p->s && p->s->cls_uniform && p->total > 0 &&
+                           !(getenv("CASIM_GO_DECOUPLE") && atoi(getenv("CASIM_GO_DECOUPLE")) == 0);
+    // where the consumers (publisher, segment copies) read the stream's pod ids
+    const int32_t* const ids_src = decoupled ? p->d_spod_go.as<int32_t>() : p->d_spod.as<int32_t>();
     std::function<int()> sort_light;        // split: the light groups' sort, queued after the heavy chains
     // 1-3: score, sort, stream
     if (p->total > 0 && p->bucket) {
@@ -2308,7 +2376,28 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         int32_t nb = 1, passes = 0;                       // buckets <= U: 8-bit digits
         while (nb < U) { nb <<= 8; passes++; }
         passes = std::max(passes, 1);
-        const int32_t passes_run = go_order ? 0 : passes;
+        const int32_t passes_run = (go_order && !decoupled) ? 0 : passes;
+        if (decoupled) {
+            // Go's sort.Slice permutation of every group and its pod ids, on st3 from the start:
+            // its own class ranks, k_pdq_sort, ids into d_spod_go + per-group ready flags.  The
+            // chains meanwhile run on the stable class order (same class at every position).
+            CA_HIP_CHECK(hipMemsetAsync(p->d_ids_ready.ptr, 0, sizeof(int32_t) * (size_t)G, st));
+            CA_HIP_CHECK(hipEventRecord(p->ev_emitA, st));
+            CA_HIP_CHECK(hipStreamWaitEvent(p->st3, p->ev_emitA, 0));
+            hipLaunchKernelGGL(k_class_rank, dim3(G), dim3(1024), 0, p->st3, p->d_meta.as<GroupMeta>(),
+                               p->d_tmpl.as<ca_template>(), p->s->d_cls_sc.as<int64_t>(), U, NP,
+                               p->d_crank2.as<int32_t>(), (const int32_t*)nullptr);
+            CA_HIP_CHECK(hipGetLastError());
+            int rc0;
+            if ((rc0 = launch_pdq_sort(p, p->st3, nullptr, G, p->d_crank2.as<int32_t>(), U, nullptr, 0,
+                                       p->d_sortC.as<uint32_t>())) != CA_OK)
+                return rc0;
+            hipLaunchKernelGGL(k_emit_go_ids, dim3(G), dim3(1024), 0, p->st3, p->d_meta.as<GroupMeta>(),
+                               p->d_sortC.as<uint32_t>(), p->d_pod_idx.as<int32_t>(), p->d_spod_go.as<int32_t>(),
+                               p->d_ids_ready.as<int32_t>(), (const int32_t*)nullptr);
+            CA_HIP_CHECK(hipGetLastError());
+            CA_HIP_CHECK(hipEventRecord(p->ev_ids, p->st3));
+        }
         const int32_t blocks = (p->max_count + 255) / 256;
         // class ranks, then Go's pdqsort (default) or the stable LSD radix passes, stream
         // emission for `ng` groups (map `gm`)
@@ -2320,7 +2409,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             if (events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], ss));
             uint32_t* a = nullptr;                        // identity (position order)
             uint32_t* bufs[2] = {p->d_sortA.as<uint32_t>(), p->d_sortB.as<uint32_t>()};
-            if (go_order) {
+            if (go_order && !decoupled) {
                 int rc0;
                 if ((rc0 = launch_pdq_sort(p, ss, gm, ng, crank, U, nullptr)) != CA_OK) return rc0;
                 a = bufs[0];
@@ -2432,15 +2521,16 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             if (sched16)
                 hipLaunchKernelGGL(k_publish<uint16_t>, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, ps,
                                    p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
-                                   p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int64_t>(),
+                                   ids_src, p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int64_t>(),
                                    p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
-                                   reinterpret_cast<uint16_t*>(publish), pub_start_ticks());
+                                   reinterpret_cast<uint16_t*>(publish), pub_start_ticks(),
+                                   decoupled ? p->d_ids_ready.as<int32_t>() : nullptr);
             else
                 hipLaunchKernelGGL(k_publish<int32_t>, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, ps,
                                    p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
-                                   p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int64_t>(),
+                                   ids_src, p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int64_t>(),
                                    p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
-                                   publish, pub_start_ticks());
+                                   publish, pub_start_ticks(), decoupled ? p->d_ids_ready.as<int32_t>() : nullptr);
             CA_HIP_CHECK(hipGetLastError());
             return CA_OK;
         };
@@ -2465,7 +2555,8 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                p->d_seg.as<Seg>(), publish ? p->d_tickets.as<int64_t>() : nullptr,
                                p->d_qctl.as<int32_t>(), p->nsub, p->d_prog.as<int2>(), p->pch, p->d_out.as<ChainOut>(),
                                gm, grows ? p->d_slab.as<unsigned char>() : nullptr,
-                               grows ? p->d_slab_off.as<int64_t>() : nullptr, grows ? p->d_gkcap.as<int32_t>() : nullptr);
+                               grows ? p->d_slab_off.as<int64_t>() : nullptr, grows ? p->d_gkcap.as<int32_t>() : nullptr,
+                               decoupled ? 1 : 0);
             CA_HIP_CHECK(hipGetLastError());
             return CA_OK;
         };
@@ -2496,11 +2587,11 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         CA_HIP_CHECK(hipEventRecord(p->ev_rb, st));
         // results of this round, queued behind the readback: the device fills them while
         // the host walks the lastIndex chain (a later round queues them again)
-        if (p->total > 0 && !publish) {
+        if (p->total > 0 && !publish && !decoupled) {
             hipLaunchKernelGGL(k_copy_segments, dim3((p->max_count + CPY_PER_BLOCK - 1) / CPY_PER_BLOCK, G), dim3(256), 0,
                                st, p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
                                p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(),
-                               sched_node ? p->d_sched_node.as<int32_t>() : nullptr);
+                               sched_node ? p->d_sched_node.as<int32_t>() : nullptr, 0);
             CA_HIP_CHECK(hipGetLastError());
         }
         CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_COMPACT], st));
@@ -2559,6 +2650,15 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     }
     // results: the chains wrote single placements directly, the last round's
     // k_copy_segments the run placements (or the publisher, into the caller's buffer)
+    if (decoupled && !publish && p->total > 0) {
+        // once, after the last round: stream positions -> Go-order ids
+        CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_ids, 0));
+        hipLaunchKernelGGL(k_copy_segments, dim3((p->max_count + CPY_PER_BLOCK - 1) / CPY_PER_BLOCK, G), dim3(256), 0,
+                           st, p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
+                           ids_src, p->d_sched_pod.as<int32_t>(),
+                           sched_node ? p->d_sched_node.as<int32_t>() : nullptr, 1);
+        CA_HIP_CHECK(hipGetLastError());
+    }
     if (publish) {
         // the publisher of the last round wrote the results; a deadline hit (a chain that
         // died) falls back to the device copy + D2H
@@ -2567,9 +2667,10 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         if (qc[2] != 0 || qc[3] != 0) {
             p->pub_state = 2;
             set_last_error("estimate publisher missed a ticket; results copied instead");
+            if (decoupled) CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_ids, 0));
             hipLaunchKernelGGL(k_copy_segments, dim3((p->max_count + CPY_PER_BLOCK - 1) / CPY_PER_BLOCK, G), dim3(256), 0,
                                st, p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
-                               p->d_spod.as<int32_t>(), p->d_sched_pod.as<int32_t>(), nullptr);
+                               ids_src, p->d_sched_pod.as<int32_t>(), nullptr, decoupled ? 1 : 0);
             CA_HIP_CHECK(hipGetLastError());
             int rc;
             if (to_host && (rc = results_to_host(p, st, sched_pod, sched16)) != CA_OK) return rc;

@@ -154,6 +154,7 @@ struct ca_mirror {
     size_t d_hints_n = 0;
     int ensure_pod_hints();                // grow to pods.size(), new entries -1
     int64_t n_ext_pods = 0;                // pods stored with host ports / extended requests
+    int64_t n_eph_pods = 0;                // pods stored with ephemeral-storage requests
 
     int remap_hints_removed(int32_t pos, int32_t code, bool restore);   // resident hints around a RemoveNode
     int32_t removals = 0;                  // RemoveNode calls so far: hint codes of removed nodes
@@ -180,4 +181,8 @@ struct ca_podset {
     // score_memory}.  Used by the Estimate bucket sort (estimate.hip).
     int32_t n_cls = 0;
     casim::DevBuf d_cls, d_cls_sc;
+    // every class's pods carry identical records apart from their controller
+    // (similar_class): interchangeable for the FFD chain, so Estimate can run the chain on
+    // the stable class order while Go's sort.Slice order of their ids is computed beside it
+    bool cls_uniform = false;
 };

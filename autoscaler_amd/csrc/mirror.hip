@@ -357,6 +357,7 @@ int32_t ca_mirror::store_pod(const ca_pod_table* t, int32_t idx, int32_t node) {
         row.spec.prefilter_first = first;
     }
     if (pod_dev_flags(row.spec) & (PF_PORTS | PF_SCALAR_REQ | PF_MOVED_SCALAR_REQ)) n_ext_pods++;
+    if (row.spec.req_ephemeral != 0) n_eph_pods++;
     pods.push_back(row);
     return (int32_t)pods.size() - 1;
 }
@@ -737,6 +738,7 @@ int ca_mirror_destroy(ca_mirror* m) {
 int ca_mirror_clear(ca_mirror* m) {
     if (!m) return CA_EINVAL;
     m->n_ext_pods = 0;
+    m->n_eph_pods = 0;
     m->nodes.clear(); m->pods.clear(); m->terms.clear(); m->reqs.clear(); m->pf_names.clear();
     m->journal.clear(); m->depth = 0; m->removed_nodes.clear(); m->n_scope_blockers = 0;
     m->dirty_rows.clear(); m->dirty_flag.clear();
@@ -981,6 +983,18 @@ int ca_podset_create(ca_mirror* m, const ca_pod_table* t, ca_podset** out) {
             cls[i] = it->second;
         }
         s->n_cls = (int32_t)ids.size();
+        {   // class uniformity (ca_podset::cls_uniform)
+            std::vector<int32_t> first((size_t)s->n_cls, -1);
+            bool uni = true;
+            for (int32_t i = 0; i < t->n_pods && uni; i++) {
+                int32_t& f = first[cls[i]];
+                if (f < 0) { f = i; continue; }
+                ca_pod_spec a = t->pods[f], b = t->pods[i];
+                a.similar_class = b.similar_class = 0;
+                uni = std::memcmp(&a, &b, sizeof a) == 0;
+            }
+            s->cls_uniform = uni;
+        }
         if ((rc = s->d_cls.reserve(sizeof(int32_t) * (cls.size() + 1))) != CA_OK ||
             (rc = s->d_cls_sc.reserve(sizeof(int64_t) * (sc.size() + 2))) != CA_OK) { delete s; return rc; }
         if (!cls.empty())

@@ -118,9 +118,29 @@ __global__ void __launch_bounds__(256) k_plan_pack(const int32_t* __restrict__ m
     out[i] = r;
 }
 
+// A committed node row in LDS: free cpu / memory (/ ephemeral storage) / pod slots.
+struct PcRow { int64_t c, m; int32_t p, pad; };
+struct PcRowE { int64_t c, m, e; int32_t p, pad; };
+__device__ inline int64_t pc_e(const PcRow&) { return 0; }
+__device__ inline int64_t pc_e(const PcRowE& r) { return r.e; }
+__device__ inline void pc_set_e(PcRow&, int64_t) {}
+__device__ inline void pc_set_e(PcRowE& r, int64_t v) { r.e = v; }
+__device__ inline unsigned long long* pc_e_ptr(PcRow& r) { return reinterpret_cast<unsigned long long*>(&r.c); }
+__device__ inline unsigned long long* pc_e_ptr(PcRowE& r) { return reinterpret_cast<unsigned long long*>(&r.e); }
+template <bool E> struct PcRowT { using type = PcRow; };
+template <> struct PcRowT<true> { using type = PcRowE; };
+// Per 64-node block: bit planes (podDestinations, visible = destination and schedulable,
+// unschedulable, tainted, free ephemeral >= 0) and the maxima of its visible rows (upper
+// bounds, refreshed by scans).
+struct PcBlk {
+    uint64_t dest, vis, usch, taint, eph;
+    int64_t bmc, bmm, bme;
+    int32_t bmp, pad;
+};
+
 // LDS image of one call (byte offsets; every array 16-B aligned)
 struct PcLayout {
-    size_t fc, fm, fe, destw, visw, uschw, taintw, ephw, bmc, bmm, bme, bmp, fp, excnt, scratch, resbuf, mvbuf, total;
+    size_t rows, blk, excnt, scratch, resbuf, mvbuf, ctx, total;
 };
 
 __host__ __device__ inline PcLayout pc_layout(int32_t n, bool eph_cols) {
@@ -128,23 +148,13 @@ __host__ __device__ inline PcLayout pc_layout(int32_t n, bool eph_cols) {
     const size_t nn = (size_t)n, nb = (nn + 63) / 64;
     size_t o = 0;
     auto take = [&](size_t bytes) { const size_t r = o; o += (bytes + 15) & ~(size_t)15; return r; };
-    L.fc = take(8 * nn);
-    L.fm = take(8 * nn);
-    L.fe = take(eph_cols ? 8 * nn : 0);
-    L.destw = take(8 * nb);
-    L.visw = take(8 * nb);
-    L.uschw = take(8 * nb);
-    L.taintw = take(8 * nb);
-    L.ephw = take(eph_cols ? 0 : 8 * nb);
-    L.bmc = take(8 * nb);
-    L.bmm = take(8 * nb);
-    L.bme = take(8 * nb);
-    L.bmp = take(4 * nb);
-    L.fp = take(4 * nn);
+    L.rows = take((eph_cols ? sizeof(PcRowE) : sizeof(PcRow)) * nn);
+    L.blk = take(sizeof(PcBlk) * nb);
     L.excnt = take(2 * nn);
     L.scratch = take(4 * 64);
     L.resbuf = take(sizeof(ca_plan_result) * 64);       // results of the current 64 candidates
     L.mvbuf = take(sizeof(ca_plan_move) * PC_MVBUF);   // committed moves not yet written out
+    L.ctx = take(256);                                 // PcCtx
     L.total = o;
     return L;
 }
@@ -164,6 +174,13 @@ __device__ inline int64_t pc_rl64(int64_t v, int lane) {
 __device__ inline int32_t pc_rl32(int32_t v, int lane) { return (int32_t)__builtin_amdgcn_readlane((uint32_t)v, lane); }
 __device__ inline uint64_t pc_below(int lane) { return lane == 0 ? 0ull : (~0ull >> (64 - lane)); }
 __device__ inline bool pc_bit(const uint64_t* w, int32_t i) { return (w[i >> 6] >> (i & 63)) & 1ull; }
+// a value every lane holds, as a scalar (SGPR) value
+__device__ inline uint64_t pc_uni64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ inline int64_t pc_uni64s(int64_t v) { return (int64_t)pc_uni64((uint64_t)v); }
 
 // workgroup-coherent global accesses: the chain's own earlier stores (hints, copies, PDB
 // budgets) are read back by other lanes of the same wavefront
@@ -196,27 +213,494 @@ __device__ inline PcPod pc_load(const PcPod* p) {
     return r;
 }
 
+// Out of line (rare: taints, affinity, node names), so the chain keeps its registers.
+__device__ __attribute__((noinline)) bool pc_static_fit(const PcArgs& a, int32_t x, int32_t spec, uint32_t pf) {
+    const NodeStatic ns = a.st[x];
+    return dev_static_filters(a.specs[spec], pf, a.terms, a.reqs, ns, false) == CA_PLUGIN_NONE;
+}
+__device__ __attribute__((noinline)) bool pc_in_names(const PcArgs& a, int32_t x, int32_t spec) {
+    const ca_pod_spec& s = a.specs[spec];
+    const int32_t nid = a.st[x].name_id;
+    bool in = false;
+    for (int32_t k = 0; k < s.prefilter_count; k++) in |= a.names[s.prefilter_first + k] == nid;
+    return in;
+}
+
+// Per-call scalar state the candidate loop and the simulation share (LDS).
+struct PcCtx {
+    int32_t Lw, Lraw, nm, mv_n, mv_first, removed, pad0, pad1;
+    uint64_t dirty0, dirty1;              // blocks whose maxima may be stale-high
+    ca_plan_result r;                     // the current candidate's result
+#ifdef CASIM_PROF
+    uint64_t prof[PC_NPROF];
+#endif
+};
+
+__device__ inline void pc_flush_moves(const PcArgs& a, const ca_plan_move* mvbuf, PcCtx* ctx, int lane) {
+    const int32_t k = ctx->mv_n, first = ctx->mv_first;
+    for (int32_t i = lane; i < k; i += 64) a.moves[first + i] = mvbuf[i];
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) { ctx->mv_first = first + k; ctx->mv_n = 0; }
+    __builtin_amdgcn_wave_barrier();
+}
+
+#ifdef CASIM_PROF
+#define PC_SIM_T0() uint64_t tp_ = clock64()
+#define PC_SIM_MARK(k) do { const uint64_t t_ = clock64(); if (lane == 0) ctx->prof[k] += t_ - tp_; tp_ = t_; } while (0)
+#define PC_SIM_COUNT(k) do { if (lane == 0) ctx->prof[k]++; } while (0)
+#else
+#define PC_SIM_T0() do {} while (0)
+#define PC_SIM_MARK(k) do {} while (0)
+#define PC_SIM_COUNT(k) do {} while (0)
+#endif
+#define PC_MARK_DIRTY(j) do { const int32_t j_ = (j); if (j_ < 64) dirty0 |= 1ull << j_; else dirty1 |= 1ull << (j_ - 64); } while (0)
+
+// withForkedSnapshot(findPlaceFor) for one candidate on the committed rows: RemovePod of its
+// pods, TrySchedulePods (hints, then the rotating scan), then Commit or Revert;
+// the candidate loop keeps its scalar state in LDS (ctx), the simulation in registers.
+// Updates ctx (lastIndex, moves, dirty blocks) and ctx->r.
+template <bool EPH_COLS>
+__device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& a, unsigned char* pc_raw, PcCtx* ctx, const int32_t c,
+                                                     const int32_t node, const int32_t cnt, const PcReg r0,
+                                                     const PcReg r1) {
+    const int lane = threadIdx.x;
+    const int32_t n = a.n, nb = (n + 63) >> 6;
+    const PcLayout Y = pc_layout(n, EPH_COLS);
+    using Row = typename PcRowT<EPH_COLS>::type;
+    Row* const rows = reinterpret_cast<Row*>(pc_raw + Y.rows);
+    PcBlk* const blk = reinterpret_cast<PcBlk*>(pc_raw + Y.blk);
+    uint16_t* const excnt = reinterpret_cast<uint16_t*>(pc_raw + Y.excnt);
+    int32_t* const scratch = reinterpret_cast<int32_t*>(pc_raw + Y.scratch);
+    ca_plan_move* const mvbuf = reinterpret_cast<ca_plan_move*>(pc_raw + Y.mvbuf);
+    int32_t Lw = ctx->Lw;
+    const int32_t nm = ctx->nm;
+    uint64_t dirty0 = ctx->dirty0, dirty1 = ctx->dirty1;
+    ca_plan_result r = ctx->r;
+    bool moved_L = false;                       // a scan succeeded: lastIndex is the wrapped value
+    PC_SIM_T0();
+    // register cache of one 64-node block of rows (lane i: node cj * 64 + i): the free
+    // columns in VGPRs, the block's visibility / ephemeral-ok / taint bits as wave-uniform
+    // masks (SGPRs), so a fit test is a few compares and mask ANDs
+    int32_t cj = -1;
+    int64_t cc = 0, cm = 0, ce = 0;
+    int32_t cp = 0;
+    uint64_t cvis = 0, cok = 0, ctaint = 0;
+    auto load_block = [&](int32_t j) {
+        const int32_t x = j * 64 + lane;
+        const bool in = x < n;
+        cc = in ? rows[x].c : 0; cm = in ? rows[x].m : 0; cp = in ? rows[x].p : INT32_MIN;
+        ce = (EPH_COLS && in) ? pc_e(rows[x]) : 0;
+        cvis = pc_uni64(blk[j].vis);
+        cok = EPH_COLS ? ~0ull : pc_uni64(blk[j].eph);
+        ctaint = pc_uni64(blk[j].taint);
+        cj = j;
+    };
+        // ---- withForkedSnapshot(findPlaceFor): RemovePod of the pods to move (cluster.go:228-233) ----
+        const bool in0 = lane < cnt, in1 = 64 + lane < cnt;
+        const int64_t sc = __ockl_wfred_add_i64(wadd(in0 ? r0.cpu : 0, in1 ? r1.cpu : 0));
+        const int64_t sm = __ockl_wfred_add_i64(wadd(in0 ? r0.mem : 0, in1 ? r1.mem : 0));
+        const int64_t se = EPH_COLS ? __ockl_wfred_add_i64(wadd(in0 ? r0.eph : 0, in1 ? r1.eph : 0)) : 0;
+        const int32_t jn = node >> 6;
+        const uint64_t nbit = 1ull << (node & 63);
+        {
+            const int64_t oc = rows[node].c, om = rows[node].m, oe = EPH_COLS ? pc_e(rows[node]) : 0;
+            const int32_t op = rows[node].p;
+            const int64_t nc = wadd(oc, sc), nmm = wadd(om, sm), ne2 = wadd(oe, se);
+            const int32_t np = op + cnt;
+            if (lane == 0) {
+                rows[node].c = nc; rows[node].m = nmm; rows[node].p = np;
+                if (EPH_COLS) pc_set_e(rows[node], ne2);
+                // a row that grows raises its block's maxima (they are upper bounds)
+                const int64_t bc = blk[jn].bmc, bm = blk[jn].bmm, be = EPH_COLS ? blk[jn].bme : 0;
+                const int32_t bp = blk[jn].bmp;
+                if (nc > bc) blk[jn].bmc = nc;
+                if (nmm > bm) blk[jn].bmm = nmm;
+                if (EPH_COLS && ne2 > be) blk[jn].bme = ne2;
+                if (np > bp) blk[jn].bmp = np;
+            }
+            if (jn == cj && lane == (node & 63)) { cc = nc; cm = nmm; ce = ne2; cp = np; }
+        }
+        PC_SIM_MARK(PC_FORK);
+        uint64_t evals = 0;
+        int32_t placed = 0;
+        int32_t d0 = -1, d1 = -1;                   // destinations of pods t = lane, 64 + lane
+        int32_t hs0 = INT32_MIN, hs1 = INT32_MIN;   // Hints.Set of pods t = lane, 64 + lane
+        int32_t eb0 = 0, eb1 = 0;                   // ex_base of their destinations (loaded at AddPod)
+        bool failed = false;
+        // one pod (uniform values): hint check, then the rotating scan, then AddPod
+        auto place = [&](const int32_t t, const int64_t pcpu, const int64_t pmem, const int64_t peph, const uint32_t pf,
+                         const int32_t h, const int32_t spec) -> bool {
+            const bool prefail = (pf & PF_PREFILTER_FAIL) != 0;
+            const bool all_zero = (pf & PF_ALL_ZERO) != 0;
+            // TaintToleration / NodeAffinity / NodeName where the pod or the node needs them
+            auto static_fit = [&](int32_t x) -> bool { return pc_static_fit(a, x, spec, pf); };
+            const bool any_static = (pf & (PF_NODE_NAME | PF_AFFINITY)) != 0;
+            const bool taint_all = (pf & PF_TAINT_MASK_ALL) != 0;
+            int32_t target = -1;
+            int64_t tc = 0, tm = 0, te = 0;         // the target's row
+            int32_t tpd = 0;
+            const int tl = t & 63;
+            // ---- findNodeWithHints (hinting_simulator.go:91-108): CheckPredicates ----
+            if (h >= 0 && h < n && !prefail) {
+                evals++;
+                const int64_t hc = pc_uni64s(rows[h].c), hm = pc_uni64s(rows[h].m);
+                const int64_t he = EPH_COLS ? pc_uni64s(pc_e(rows[h])) : 0;
+                const int32_t hp = __builtin_amdgcn_readfirstlane(rows[h].p);
+                const int32_t jh = h >> 6;
+                const uint64_t hb = 1ull << (h & 63);
+                const uint64_t uw = pc_uni64(blk[jh].usch), tw = pc_uni64(blk[jh].taint), dw = pc_uni64(blk[jh].dest);
+                const bool eok = EPH_COLS ? (peph <= he) : ((pc_uni64(blk[jh].eph) & hb) != 0);
+                bool ok = !((uw & hb) && !(pf & PF_TOL_UNSCHED));
+                ok = ok && (hp >= 1) && (all_zero || ((pcpu <= hc) && (pmem <= hm) && eok));
+                if (ok && (any_static || ((tw & hb) && !taint_all))) ok = static_fit(h);
+                if (ok) {
+                    if (lane == tl) { if (t >= 64) hs1 = h; else hs0 = h; }          // :95 Set
+                    if (h != node && (dw & hb)) { target = h; tc = hc; tm = hm; te = he; tpd = hp; }   // :102
+                }
+            }
+            PC_SIM_MARK(PC_HINT);
+            // ---- findNode -> FitsAnyNodeMatching(isCandidateNode) (:110-125) ----
+            if (target < 0 && !prefail && n > 0) {
+                const bool names = (pf & PF_PREFILTER_NAMES) != 0;
+                const int32_t j0 = Lw >> 6, l0 = Lw & 63;
+                int32_t wr = -1, my_nv = 0;
+                uint64_t passm = 0;
+                for (int32_t rr = 0; rr <= nb; rr++) {
+                    if (rr == nb && l0 == 0) break;
+                    int32_t j = j0 + rr;
+                    if (j >= nb) j -= nb;
+                    if (rr > 0 && rr < nb && !names && j != cj) {
+                        // 64 blocks at a time: a block passes when the pod exceeds its maxima
+                        if (wr < 0 || rr >= wr + 64) {
+                            PC_SIM_COUNT(PC_WINDOWS);
+                            const int32_t q = rr + lane;
+                            bool pass = false;
+                            my_nv = 0;
+                            if (q < nb) {
+                                int32_t jj = j0 + q;
+                                if (jj >= nb) jj -= nb;
+                                const uint64_t vw = blk[jj].vis & (jj == jn ? ~nbit : ~0ull);
+                                const bool fitb = (vw != 0) & (blk[jj].bmp >= 1) &
+                                                  (all_zero | ((pcpu <= blk[jj].bmc) & (pmem <= blk[jj].bmm) &
+                                                               (!EPH_COLS || peph <= blk[jj].bme)));
+                                pass = !fitb && jj != cj;
+                                my_nv = __popcll(vw);
+                            }
+                            passm = __ballot(pass);
+                            wr = rr;
+                        }
+                        const int32_t off = rr - wr;
+                        const uint64_t stop = ~passm & (~0ull << off);
+                        const int32_t k = (stop ? __builtin_ctzll(stop) : 64) - off;
+                        if (k > 0) {
+                            evals += (uint64_t)__ockl_wfred_add_i32((lane >= off && lane < off + k) ? my_nv : 0);
+                            rr += k - 1;
+                            continue;
+                        }
+                    }
+                    PC_SIM_COUNT(PC_BLOCKS);
+#ifdef CASIM_PROF
+                    if (a.dbg & 1) cj = -1;
+#endif
+                    if (j != cj) load_block(j);
+                    const uint64_t inr = (rr == 0) ? (~0ull << l0) : (rr == nb ? ((1ull << l0) - 1) : ~0ull);
+                    uint64_t vism = cvis & inr & (j == jn ? ~nbit : ~0ull);
+                    if (names && vism) {
+                        bool in = false;
+                        if ((vism >> lane) & 1ull) in = pc_in_names(a, j * 64 + lane, spec);
+                        vism &= __ballot(in);
+                    }
+                    uint64_t fitm = vism & __ballot(cp >= 1);
+                    if (!all_zero) {
+                        fitm &= __ballot(pcpu <= cc) & __ballot(pmem <= cm);
+                        fitm &= EPH_COLS ? __ballot(peph <= ce) : cok;
+                    }
+                    const uint64_t needm = any_static ? ~0ull : (taint_all ? 0ull : ctaint);
+                    if (fitm & needm) {
+                        bool ok = true;
+                        if ((fitm & needm) >> lane & 1ull) ok = static_fit(j * 64 + lane);
+                        fitm &= __ballot(ok);
+                    }
+                    if (fitm) {
+                        const int f = __builtin_ctzll(fitm);
+                        const uint64_t upto = (f == 63) ? ~0ull : ((2ull << f) - 1);
+                        evals += (uint64_t)__popcll(vism & upto);
+                        target = j * 64 + f;
+                        tc = pc_rl64(cc, f); tm = pc_rl64(cm, f); te = EPH_COLS ? pc_rl64(ce, f) : 0;
+                        tpd = pc_rl32(cp, f);
+                        Lw = target + 1 == n ? 0 : target + 1;                       // schedulerbased.go:131
+                        moved_L = true;
+                        if (lane == tl) { if (t >= 64) hs1 = target; else hs0 = target; }   // :123
+                        break;
+                    }
+                    evals += (uint64_t)__popcll(vism);
+                    // the block passed: refresh its maxima from the rows just read
+                    const bool dj = j < 64 ? ((dirty0 >> j) & 1ull) : ((dirty1 >> (j - 64)) & 1ull);
+                    if (dj) {
+                        const bool cv = (cvis >> lane) & 1ull;
+                        const int64_t mc = __ockl_wfred_max_i64(cv ? cc : INT64_MIN);
+                        const int64_t mmx = __ockl_wfred_max_i64(cv ? cm : INT64_MIN);
+                        const int64_t me = EPH_COLS ? __ockl_wfred_max_i64(cv ? ce : INT64_MIN) : 0;
+                        const int32_t mp = __ockl_wfred_max_i32(cv ? cp : INT32_MIN);
+                        if (lane == 0) {
+                            blk[j].bmc = mc; blk[j].bmm = mmx; blk[j].bmp = mp;
+                            if (EPH_COLS) blk[j].bme = me;
+                        }
+                        if (j < 64) dirty0 &= ~(1ull << j); else dirty1 &= ~(1ull << (j - 64));
+                    }
+                }
+            }
+            PC_SIM_MARK(PC_SCAN);
+#ifdef CASIM_PROF
+            if (a.trace && lane == 0) {
+                const int32_t k = atomicAdd(a.trace, 1);
+                if (k < a.trace_cap) {
+                    int32_t* e = a.trace + 16 + 16 * k;
+                    const int32_t dn = a.trace[1];
+                    e[0] = c; e[1] = t; e[2] = h; e[3] = (int32_t)pf; e[4] = target; e[5] = (int32_t)evals;
+                    e[6] = Lw; e[7] = cnt; e[8] = (int32_t)pcpu; e[9] = (int32_t)(pmem >> 20);
+                    e[10] = (int32_t)rows[dn].c; e[11] = (int32_t)(rows[dn].m >> 20); e[12] = rows[dn].p;
+                    e[13] = (int32_t)((blk[(dn) >> 6].vis >> ((dn) & 63)) & 1ull) | ((int32_t)((blk[(dn) >> 6].taint >> ((dn) & 63)) & 1ull) << 1) |
+                            ((int32_t)(EPH_COLS ? 1 : ((blk[(dn) >> 6].eph >> ((dn) & 63)) & 1ull)) << 2);
+                    e[14] = spec; e[15] = -1;
+                }
+            }
+#endif
+            if (target < 0) return false;                                            // breakOnFailure
+            // ---- AddPod of the moved copy (:79) ----
+            const int64_t nc = wsub(tc, pcpu), nmm = wsub(tm, pmem), ne2 = wsub(te, peph);
+            const int32_t np = tpd - 1;
+            if (lane == 0) {
+                rows[target].c = nc; rows[target].m = nmm; rows[target].p = np;
+                if (EPH_COLS) pc_set_e(rows[target], ne2);
+            }
+            if ((target >> 6) == cj && lane == (target & 63)) { cc = nc; cm = nmm; ce = ne2; cp = np; }
+            PC_MARK_DIRTY(target >> 6);
+            if (lane == tl) {
+                const int32_t eb = a.ex_base[target];                                // (used at Commit)
+                if (t >= 64) { d1 = target; eb1 = eb; } else { d0 = target; eb0 = eb; }
+            }
+            PC_SIM_MARK(PC_ADD);
+            return true;
+        };
+        // Bulk placement of a run of plain pods (no usable hint, no PreFilter names or
+        // failure, no static filter): pod t0 + k's scan from lastIndex lands on the first
+        // visible node at or after it, so while every pod fits the next visible node in
+        // turn, pod t0 + k goes to the k-th visible node of the window [L, L + 64) — a node
+        // that receives nothing else.  Lane i holds node L + i: its rank among the visible
+        // nodes names its pod; the leading ranks that fit are placed at once, lane-parallel,
+        // with one evaluation each.  The first pod that does not fit its node continues on
+        // the exact per-pod path.  Pods of one half (t < 64 / t >= 64) per step.
+        auto bulk = [&](const int32_t t0) -> int32_t {
+            const bool hi = t0 >= 64;
+            const int32_t hend = hi ? cnt : (cnt < 64 ? cnt : 64);
+            const int32_t tl0 = t0 & 63;
+            // run of plain pods: pod lane i = pod t0 + i
+            const int32_t src_i = (tl0 + lane) & 63;
+            const int32_t hh = __shfl(hi ? r1.hint : r0.hint, src_i, 64);
+            const uint32_t ff = (uint32_t)__shfl((int32_t)(hi ? r1.flags : r0.flags), src_i, 64);
+            const bool plain = t0 + lane < hend && (hh < 0 || hh >= n) &&
+                               !(ff & (PF_PREFILTER_FAIL | PF_PREFILTER_NAMES | PF_NODE_NAME | PF_AFFINITY));
+            const uint64_t pm = __ballot(plain);
+            const int32_t R = (~pm) ? __builtin_ctzll(~pm) : 64;
+            if (R == 0) return 0;
+            // node lanes: window [L, L + 64)
+            const int32_t span = n < 64 ? n : 64;
+            int32_t x = Lw + lane;
+            if (x >= n) x -= n;
+            const bool inw = lane < span;
+            const bool vis = inw && x != node && ((blk[x >> 6].vis >> (x & 63)) & 1ull);
+            const uint64_t vm = __ballot(vis);
+            const int32_t rank = __popcll(vm & pc_below(lane));
+            const bool mine = vis && rank < R;
+            const int32_t src = (tl0 + (rank < 63 ? rank : 63)) & 63;
+            const int64_t pc2 = __shfl(hi ? r1.cpu : r0.cpu, src, 64);
+            const int64_t pm2 = __shfl(hi ? r1.mem : r0.mem, src, 64);
+            const int64_t pe2 = EPH_COLS ? __shfl(hi ? r1.eph : r0.eph, src, 64) : 0;
+            const uint32_t pf2 = (uint32_t)__shfl((int32_t)(hi ? r1.flags : r0.flags), src, 64);
+            bool fit = false;
+            if (mine) {
+                const Row& rw = rows[x];
+                const bool eok = EPH_COLS ? (pe2 <= pc_e(rw)) : ((blk[x >> 6].eph >> (x & 63)) & 1ull);
+                const bool tnt = (blk[x >> 6].taint >> (x & 63)) & 1ull;
+                fit = (rw.p >= 1) && ((pf2 & PF_ALL_ZERO) || ((pc2 <= rw.c) && (pm2 <= rw.m) && eok)) &&
+                      !(tnt && !(pf2 & PF_TAINT_MASK_ALL));
+            }
+            const uint64_t failm = __ballot(mine && !fit);
+            const uint64_t okm = failm ? (vm & pc_below(__builtin_ctzll(failm))) : vm;
+            int32_t k = __popcll(okm);
+            if (k > R) k = R;
+            if (k == 0) return 0;
+            const bool put = vis && rank < k;
+            if (put) {                                                                // AddPod (:79)
+                Row& rw = rows[x];
+                rw.c = wsub(rw.c, pc2); rw.m = wsub(rw.m, pm2); rw.p -= 1;
+                if (EPH_COLS) pc_set_e(rw, wsub(pc_e(rw), pe2));
+                scratch[(tl0 + rank) & 63] = x;
+            }
+            __builtin_amdgcn_wave_barrier();
+            const int32_t last = __builtin_amdgcn_readfirstlane(scratch[(tl0 + k - 1) & 63]);
+            if (lane >= tl0 && lane < tl0 + k) {                                    // pods t0 .. t0+k-1
+                const int32_t v = scratch[lane];
+                const int32_t eb = a.ex_base[v];                                     // (used at Commit)
+                if (hi) { d1 = v; hs1 = v; eb1 = eb; } else { d0 = v; hs0 = v; eb0 = eb; }   // :123 Set
+            }
+            __builtin_amdgcn_wave_barrier();
+            PC_MARK_DIRTY(Lw >> 6);
+            PC_MARK_DIRTY((Lw + span - 1 < n ? Lw + span - 1 : Lw + span - 1 - n) >> 6);
+            evals += (uint64_t)k;
+            Lw = last + 1 == n ? 0 : last + 1;                                       // schedulerbased.go:131
+            moved_L = true;
+            cj = -1;                                                                 // rows changed
+            return k;
+        };
+        {
+            int32_t t = 0, cool = 0;
+            while (t < cnt && !failed) {
+                if (cool == 0 && n > 1) {
+                    const int32_t k = bulk(t);
+                    placed += k;
+                    t += k;
+                    if (k > 0) continue;
+                    cool = 8;                                    // no plain run here: per pod for a while
+                }
+                if (cool > 0) cool--;
+                bool ok;
+                if (t < 64)
+                    ok = place(t, pc_rl64(r0.cpu, t), pc_rl64(r0.mem, t), EPH_COLS ? pc_rl64(r0.eph, t) : 0,
+                               (uint32_t)pc_rl32((int32_t)r0.flags, t), pc_rl32(r0.hint, t), pc_rl32(r0.spec, t));
+                else
+                    ok = place(t, pc_rl64(r1.cpu, t - 64), pc_rl64(r1.mem, t - 64),
+                               EPH_COLS ? pc_rl64(r1.eph, t - 64) : 0, (uint32_t)pc_rl32((int32_t)r1.flags, t - 64),
+                               pc_rl32(r1.hint, t - 64), pc_rl32(r1.spec, t - 64));
+                if (!ok) { failed = true; break; }
+                placed++;
+                t++;
+            }
+        }
+        r.n_placed = placed;
+        r.evals = evals;
+        if (!failed) {
+            // ---- Commit (cluster.go:207-211) ----
+            r.removable = 1;
+            r.n_moves = cnt;
+            for (int half = 0; half < 2 && half * 64 < cnt; half++) {
+                const int32_t t = half * 64 + lane;
+                const bool act = t < cnt;
+                const PcReg& q = half ? r1 : r0;
+                const int32_t f = half ? d1 : d0;
+                const int32_t fb = half ? eb1 : eb0;
+                const int32_t s = nm + t;
+                if (act) {
+                    ca_plan_move mv;
+                    mv.candidate = c; mv.pod = q.id; mv.new_pod = a.base + s; mv.node = f;
+                    mvbuf[ctx->mv_n + t] = mv;
+                    pc_st(a.H + a.base + s, f);
+                }
+                // the copies join their destinations' pod lists in list order
+                int32_t rank = 0, lead = -1;
+                uint64_t pend = __ballot(act);
+                while (pend) {
+                    const int l = __builtin_ctzll(pend);
+                    const int32_t f0 = pc_rl32(f, l);
+                    const uint64_t mm = __ballot(act && f == f0);
+                    if (act && f == f0) { rank = __popcll(mm & pc_below(lane)); lead = l; }
+                    if (lane == l) scratch[l] = __popcll(mm);
+                    pend &= ~mm;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (act && lead == lane) {
+                    const int32_t old = excnt[f];
+                    excnt[f] = (uint16_t)(old + scratch[lane]);
+                    scratch[lane] = old;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (act) {
+                    PcPod cp2;
+                    cp2.cpu = q.cpu; cp2.mem = q.mem; cp2.eph = q.eph;
+                    cp2.id = a.base + s; cp2.hint = f; cp2.flags = q.flags; cp2.spec = q.spec; cp2.orig = q.orig;
+                    cp2.pad = 0;
+                    a.ex_pods[fb + scratch[lead] + rank] = cp2;
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (lane == 0) { blk[jn].dest &= ~nbit; blk[jn].vis &= ~nbit; }               // planner.go:280
+            if (jn == cj) cvis &= ~nbit;
+            PC_MARK_DIRTY(jn);
+            // CanRemovePods, then RemovePods (basic.go:66-95)
+            if (a.n_pdbs > 0) {
+                bool risky = false;
+                for (int half = 0; half < 2; half++) {
+                    const int32_t t = half * 64 + lane;
+                    if (t >= cnt) continue;
+                    const int32_t o = half ? r1.orig : r0.orig;
+                    for (int32_t k = a.pdb_off[o]; k < a.pdb_off[o + 1]; k++)
+                        risky |= atomicSub(a.allowed + a.pdb_pod[k], 1) <= 0;
+                }
+                r.risky = __ballot(risky) ? 1 : 0;
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) { ctx->removed++; ctx->nm = nm + cnt; ctx->mv_n += cnt; }
+            __builtin_amdgcn_wave_barrier();
+            if (ctx->mv_n + PC_LIST > PC_MVBUF) pc_flush_moves(a, mvbuf, ctx, lane);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            PC_SIM_MARK(PC_COMMIT);
+        } else {
+            // ---- Revert: undo the AddPods, then the RemovePods ----
+            for (int half = 0; half < 2; half++) {
+                const int32_t t = half * 64 + lane;
+                if (t >= placed) continue;
+                const PcReg& q = half ? r1 : r0;
+                const int32_t f = half ? d1 : d0;
+                atomicAdd(reinterpret_cast<unsigned long long*>(&rows[f].c), (unsigned long long)q.cpu);
+                atomicAdd(reinterpret_cast<unsigned long long*>(&rows[f].m), (unsigned long long)q.mem);
+                if (EPH_COLS) atomicAdd(reinterpret_cast<unsigned long long*>(pc_e_ptr(rows[f])), (unsigned long long)q.eph);
+                atomicAdd(&rows[f].p, 1);
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (int half = 0; half < 2; half++) {
+                const int32_t t = half * 64 + lane;
+                if (t >= placed) continue;
+                const int32_t f = half ? d1 : d0, j = f >> 6;
+                atomicMax(reinterpret_cast<long long*>(&blk[j].bmc), (long long)rows[f].c);
+                atomicMax(reinterpret_cast<long long*>(&blk[j].bmm), (long long)rows[f].m);
+                if (EPH_COLS) atomicMax(reinterpret_cast<long long*>(&blk[j].bme), (long long)pc_e(rows[f]));
+                atomicMax(&blk[j].bmp, rows[f].p);
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) {
+                rows[node].c = wsub(rows[node].c, sc); rows[node].m = wsub(rows[node].m, sm); rows[node].p -= cnt;
+                if (EPH_COLS) pc_set_e(rows[node], wsub(pc_e(rows[node]), se));
+            }
+            PC_MARK_DIRTY(jn);
+            cj = -1;                                                                 // rows changed
+            r.reason = CA_UNREMOVABLE_NO_PLACE;                                      // cluster.go:174-177
+            PC_SIM_MARK(PC_REVERT);
+        }
+        // Hints.Set of this candidate's pods (hints persist whether or not it is removable)
+        if (hs0 != INT32_MIN) pc_st(a.H + r0.id, hs0);
+        if (hs1 != INT32_MIN) pc_st(a.H + r1.id, hs1);
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+        ctx->Lw = Lw;
+        if (moved_L) ctx->Lraw = Lw;
+        ctx->dirty0 = dirty0;
+        ctx->dirty1 = dirty1;
+        ctx->r = r;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 template <bool EPH_COLS>
 __global__ void __launch_bounds__(64) k_plan_chain(PcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char pc_raw[];
     const int lane = threadIdx.x;
     const int32_t n = a.n, nb = (n + 63) >> 6;
     const PcLayout Y = pc_layout(n, EPH_COLS);
-    int64_t* const fc = reinterpret_cast<int64_t*>(pc_raw + Y.fc);         // free cpu / memory /
-    int64_t* const fm = reinterpret_cast<int64_t*>(pc_raw + Y.fm);         // ephemeral storage /
-    int64_t* const fe = reinterpret_cast<int64_t*>(pc_raw + Y.fe);         // pod slots, committed
-    int32_t* const fp = reinterpret_cast<int32_t*>(pc_raw + Y.fp);
-    uint64_t* const destw = reinterpret_cast<uint64_t*>(pc_raw + Y.destw);   // podDestinations
-    uint64_t* const visw = reinterpret_cast<uint64_t*>(pc_raw + Y.visw);     // ... and schedulable
-    uint64_t* const uschw = reinterpret_cast<uint64_t*>(pc_raw + Y.uschw);
-    uint64_t* const taintw = reinterpret_cast<uint64_t*>(pc_raw + Y.taintw);
-    uint64_t* const ephw = reinterpret_cast<uint64_t*>(pc_raw + Y.ephw);     // free ephemeral >= 0
-    int64_t* const bmc = reinterpret_cast<int64_t*>(pc_raw + Y.bmc);        // per block: maxima over
-    int64_t* const bmm = reinterpret_cast<int64_t*>(pc_raw + Y.bmm);        // its visible rows (upper
-    int64_t* const bme = reinterpret_cast<int64_t*>(pc_raw + Y.bme);        // bounds, refreshed by scans)
-    int32_t* const bmp = reinterpret_cast<int32_t*>(pc_raw + Y.bmp);
+    using Row = typename PcRowT<EPH_COLS>::type;
+    Row* const rows = reinterpret_cast<Row*>(pc_raw + Y.rows);
+    PcBlk* const blk = reinterpret_cast<PcBlk*>(pc_raw + Y.blk);
     uint16_t* const excnt = reinterpret_cast<uint16_t*>(pc_raw + Y.excnt);  // copies committed per node
-    int32_t* const scratch = reinterpret_cast<int32_t*>(pc_raw + Y.scratch);
     ca_plan_result* const resbuf = reinterpret_cast<ca_plan_result*>(pc_raw + Y.resbuf);
     ca_plan_move* const mvbuf = reinterpret_cast<ca_plan_move*>(pc_raw + Y.mvbuf);
     // Global stores are kept out of the pod loop: on gfx9 a store counts in vmcnt, so any
@@ -230,12 +714,7 @@ __global__ void __launch_bounds__(64) k_plan_chain(PcArgs a) {
             for (int w = 0; w < (int)(sizeof(ca_plan_result) / 4); w++) dst[w] = src[w];
         }
     };
-    int32_t mv_first = 0, mv_n = 0;                     // mvbuf holds moves [mv_first, mv_first + mv_n)
-    auto flush_moves = [&]() {
-        for (int32_t k = lane; k < mv_n; k += 64) a.moves[mv_first + k] = mvbuf[k];
-        mv_first += mv_n;
-        mv_n = 0;
-    };
+    PcCtx* const ctx = reinterpret_cast<PcCtx*>(pc_raw + Y.ctx);
 #ifdef CASIM_PROF
     uint64_t prof[PC_NPROF];
     for (int k = 0; k < PC_NPROF; k++) prof[k] = 0;
@@ -260,48 +739,37 @@ __global__ void __launch_bounds__(64) k_plan_chain(PcArgs a) {
             const int32_t i = j * 64 + lane;
             const bool valid = i < n;
             if (valid) {
-                fc[i] = h[u].cpu; fm[i] = h[u].mem; fp[i] = h[u].pods; excnt[i] = 0;
-                if (EPH_COLS) fe[i] = h[u].eph;
+                rows[i].c = h[u].cpu; rows[i].m = h[u].mem; rows[i].p = h[u].pods; excnt[i] = 0;
+                if (EPH_COLS) pc_set_e(rows[i], h[u].eph);
             }
             const uint64_t dw = __ballot(valid && dm[u] != 0);
             const uint64_t uw = __ballot(valid && (h[u].flags & NF_UNSCHED));
             const uint64_t tw = __ballot(valid && (h[u].flags & NF_TAINTS));
             const uint64_t ew = __ballot(valid && h[u].eph >= 0);
             if (lane == 0) {
-                destw[j] = dw; visw[j] = dw & ~uw; uschw[j] = uw; taintw[j] = tw;
-                if (!EPH_COLS) ephw[j] = ew;
-                bmc[j] = INT64_MAX; bmm[j] = INT64_MAX; bme[j] = INT64_MAX; bmp[j] = INT32_MAX;
+                blk[j].dest = dw; blk[j].vis = dw & ~uw; blk[j].usch = uw; blk[j].taint = tw;
+                if (!EPH_COLS) blk[j].eph = ew;
+                blk[j].bmc = INT64_MAX; blk[j].bmm = INT64_MAX; blk[j].bme = INT64_MAX; blk[j].bmp = INT32_MAX;
             }
         }
     }
     __builtin_amdgcn_wave_barrier();
-    uint64_t dirty0 = ~0ull, dirty1 = ~0ull;            // blocks whose maxima may be stale-high
 #ifdef CASIM_PROF
     prof[PC_INIT] = clock64() - t_start;
 #endif
 
-    // register cache of one 64-node block of rows (lane i: node cj * 64 + i)
-    int32_t cj = -1;
-    int64_t cc = 0, cm = 0, ce = 0;
-    int32_t cp = 0;
-    bool cv = false, cok = false, ctn = false;
-    auto load_block = [&](int32_t j) {
-        const int32_t x = j * 64 + lane;
-        const bool in = x < n;
-        cc = in ? fc[x] : 0; cm = in ? fm[x] : 0; cp = in ? fp[x] : INT32_MIN;
-        ce = (EPH_COLS && in) ? fe[x] : 0;
-        cv = in && ((visw[j] >> lane) & 1ull);
-        cok = EPH_COLS ? true : (in && ((ephw[j] >> lane) & 1ull));
-        ctn = in && ((taintw[j] >> lane) & 1ull);
-        cj = j;
-    };
-    auto mark_dirty = [&](int32_t j) {
-        if (j < 64) dirty0 |= 1ull << j; else dirty1 |= 1ull << (j - 64);
-    };
-
-    int64_t Lraw = a.L0;                              // Go keeps the int until a scan succeeds
-    int32_t Lw = 0;
-    if (n > 0) { Lw = (int32_t)(Lraw % n); if (Lw < 0) Lw += n; }
+    if (lane == 0) {
+        int32_t Lw = 0;
+        if (n > 0) { Lw = (int32_t)(a.L0 % n); if (Lw < 0) Lw += n; }
+        ctx->Lw = Lw;
+        ctx->Lraw = (int32_t)a.L0;                    // Go keeps the int until a scan succeeds
+        ctx->nm = 0; ctx->mv_n = 0; ctx->mv_first = 0; ctx->removed = 0;
+        ctx->dirty0 = ~0ull; ctx->dirty1 = ~0ull;
+#ifdef CASIM_PROF
+        for (int k = 0; k < PC_NPROF; k++) ctx->prof[k] = 0;
+#endif
+    }
+    __builtin_amdgcn_wave_barrier();
     int32_t nm = 0, removed = 0, simulated = 0;
     bool cut = false, stopped = false;
     int32_t hb_node = -1, hb_st = 0, hb_mo = 0, hb_m1 = 0;    // candidate headers, lane k = c0 + k
@@ -330,7 +798,7 @@ __global__ void __launch_bounds__(64) k_plan_chain(PcArgs a) {
             stopped = true;
             for (int32_t k = c + lane; k < a.C; k += 64) {
                 ca_plan_result r;
-                r.removable = 0; r.reason = CA_UNREMOVABLE_NOT_RUN; r.n_placed = 0; r.last_index_in = (int32_t)Lraw;
+                r.removable = 0; r.reason = CA_UNREMOVABLE_NOT_RUN; r.n_placed = 0; r.last_index_in = ctx->Lraw;
                 r.evals = 0; r.first_move = nm; r.n_moves = 0; r.blocking_pod = -1; r.risky = 0;
                 a.res[k] = r;
             }
@@ -340,9 +808,9 @@ __global__ void __launch_bounds__(64) k_plan_chain(PcArgs a) {
         const int32_t node = pc_rl32(hb_node, sl), stc = pc_rl32(hb_st, sl);
         const int32_t mo = pc_rl32(hb_mo, sl), m0 = mo1 - mo;
         ca_plan_result r;
-        r.removable = 0; r.reason = CA_UNREMOVABLE_NONE; r.n_placed = 0; r.last_index_in = (int32_t)Lraw;
+        r.removable = 0; r.reason = CA_UNREMOVABLE_NONE; r.n_placed = 0; r.last_index_in = ctx->Lraw;
         r.evals = 0; r.first_move = nm; r.n_moves = 0; r.blocking_pod = -1; r.risky = 0;
-        const bool valid = node >= 0 && node < n && pc_bit(destw, node);
+        const bool valid = node >= 0 && node < n && ((blk[(node) >> 6].dest >> ((node) & 63)) & 1ull);
         int32_t cnt = m0;
         if (valid && stc == 0) {
             // GetPodsToMove on the committed snapshot: the caller's list, then the copies
@@ -403,310 +871,27 @@ __global__ void __launch_bounds__(64) k_plan_chain(PcArgs a) {
             continue;
         }
         simulated++;
-        // ---- withForkedSnapshot(findPlaceFor): RemovePod of the pods to move (cluster.go:228-233) ----
-        const bool in0 = lane < cnt, in1 = 64 + lane < cnt;
-        const int64_t sc = __ockl_wfred_add_i64(wadd(in0 ? r0.cpu : 0, in1 ? r1.cpu : 0));
-        const int64_t sm = __ockl_wfred_add_i64(wadd(in0 ? r0.mem : 0, in1 ? r1.mem : 0));
-        const int64_t se = EPH_COLS ? __ockl_wfred_add_i64(wadd(in0 ? r0.eph : 0, in1 ? r1.eph : 0)) : 0;
-        const int32_t jn = node >> 6;
-        const uint64_t nbit = 1ull << (node & 63);
-        {
-            const int64_t oc = fc[node], om = fm[node], oe = EPH_COLS ? fe[node] : 0;
-            const int32_t op = fp[node];
-            const int64_t nc = wadd(oc, sc), nmm = wadd(om, sm), ne2 = wadd(oe, se);
-            const int32_t np = op + cnt;
-            if (lane == 0) {
-                fc[node] = nc; fm[node] = nmm; fp[node] = np;
-                if (EPH_COLS) fe[node] = ne2;
-                // a row that grows raises its block's maxima (they are upper bounds)
-                const int64_t bc = bmc[jn], bm = bmm[jn], be = EPH_COLS ? bme[jn] : 0;
-                const int32_t bp = bmp[jn];
-                if (nc > bc) bmc[jn] = nc;
-                if (nmm > bm) bmm[jn] = nmm;
-                if (EPH_COLS && ne2 > be) bme[jn] = ne2;
-                if (np > bp) bmp[jn] = np;
-            }
-            if (jn == cj && lane == (node & 63)) { cc = nc; cm = nmm; ce = ne2; cp = np; }
-        }
-        PC_MARK(PC_FORK);
-        uint64_t evals = 0;
-        int32_t placed = 0;
-        int32_t d0 = -1, d1 = -1;                   // destinations of pods t = lane, 64 + lane
-        int32_t hs0 = INT32_MIN, hs1 = INT32_MIN;   // Hints.Set of pods t = lane, 64 + lane
-        bool failed = false;
-        for (int32_t t = 0; t < cnt; t++) {
-            const bool hi = t >= 64;
-            const int tl = t & 63;
-            const int64_t pcpu = pc_rl64(hi ? r1.cpu : r0.cpu, tl);
-            const int64_t pmem = pc_rl64(hi ? r1.mem : r0.mem, tl);
-            const int64_t peph = EPH_COLS ? pc_rl64(hi ? r1.eph : r0.eph, tl) : 0;
-            const uint32_t pf = (uint32_t)pc_rl32((int32_t)(hi ? r1.flags : r0.flags), tl);
-            const int32_t h = pc_rl32(hi ? r1.hint : r0.hint, tl);
-            const int32_t id = pc_rl32(hi ? r1.id : r0.id, tl);
-            const int32_t spec = pc_rl32(hi ? r1.spec : r0.spec, tl);
-            const bool prefail = (pf & PF_PREFILTER_FAIL) != 0;
-            const bool all_zero = (pf & PF_ALL_ZERO) != 0;
-            // TaintToleration / NodeAffinity / NodeName where the pod or the node needs them
-            auto static_fit = [&](int32_t x, bool tainted) -> bool {
-                const bool need = (pf & (PF_NODE_NAME | PF_AFFINITY)) || (tainted && !(pf & PF_TAINT_MASK_ALL));
-                if (!need) return true;
-                const NodeStatic ns = a.st[x];
-                return dev_static_filters(a.specs[spec], pf, a.terms, a.reqs, ns, false) == CA_PLUGIN_NONE;
-            };
-            int32_t target = -1;
-            int64_t tc = 0, tm = 0, te = 0;         // the target's row
-            int32_t tpd = 0;
-            // ---- findNodeWithHints (hinting_simulator.go:91-108): CheckPredicates ----
-            if (h >= 0 && h < n && !prefail) {
-                evals++;
-                const int64_t hc = fc[h], hm = fm[h], he = EPH_COLS ? fe[h] : 0;
-                const int32_t hp = fp[h];
-                const int32_t jh = h >> 6;
-                const uint64_t hb = 1ull << (h & 63);
-                const bool usch = (uschw[jh] & hb) != 0, tnt = (taintw[jh] & hb) != 0, dst = (destw[jh] & hb) != 0;
-                const bool eok = EPH_COLS ? (peph <= he) : ((ephw[jh] & hb) != 0);
-                bool ok = !(usch && !(pf & PF_TOL_UNSCHED));
-                ok = ok && (hp >= 1) && (all_zero || ((pcpu <= hc) & (pmem <= hm) & eok));
-                ok = ok && static_fit(h, tnt);
-                if (ok) {
-                    if (lane == tl) { if (hi) hs1 = h; else hs0 = h; }              // :95 Set
-                    if (h != node && dst) { target = h; tc = hc; tm = hm; te = he; tpd = hp; }   // :102 accepted
-                }
-            }
-            PC_MARK(PC_HINT);
-            // ---- findNode -> FitsAnyNodeMatching(isCandidateNode) (:110-125) ----
-            if (target < 0 && !prefail && n > 0) {
-                const bool names = (pf & PF_PREFILTER_NAMES) != 0;
-                const int32_t j0 = Lw >> 6, l0 = Lw & 63;
-                int32_t wr = -1, my_nv = 0;
-                uint64_t passm = 0;
-                for (int32_t rr = 0; rr <= nb; rr++) {
-                    if (rr == nb && l0 == 0) break;
-                    int32_t j = j0 + rr;
-                    if (j >= nb) j -= nb;
-                    if (rr > 0 && rr < nb && !names && j != cj) {
-                        // 64 blocks at a time: a block passes when the pod exceeds its maxima
-                        if (wr < 0 || rr >= wr + 64) {
-                            PC_COUNT(PC_WINDOWS);
-                            const int32_t q = rr + lane;
-                            bool pass = false;
-                            my_nv = 0;
-                            if (q < nb) {
-                                int32_t jj = j0 + q;
-                                if (jj >= nb) jj -= nb;
-                                const uint64_t vw = visw[jj] & (jj == jn ? ~nbit : ~0ull);
-                                const bool fitb = (vw != 0) & (bmp[jj] >= 1) &
-                                                  (all_zero | ((pcpu <= bmc[jj]) & (pmem <= bmm[jj]) &
-                                                               (!EPH_COLS || peph <= bme[jj])));
-                                pass = !fitb && jj != cj;
-                                my_nv = __popcll(vw);
-                            }
-                            passm = __ballot(pass);
-                            wr = rr;
-                        }
-                        const int32_t off = rr - wr;
-                        const uint64_t stop = ~passm & (~0ull << off);
-                        const int32_t k = (stop ? __builtin_ctzll(stop) : 64) - off;
-                        if (k > 0) {
-                            evals += (uint64_t)__ockl_wfred_add_i32((lane >= off && lane < off + k) ? my_nv : 0);
-                            rr += k - 1;
-                            continue;
-                        }
-                    }
-                    PC_COUNT(PC_BLOCKS);
-                    if (j != cj || (a.dbg & 1)) load_block(j);
-                    const int32_t x = j * 64 + lane;
-                    const bool inr = (rr == 0) ? lane >= l0 : (rr == nb ? lane < l0 : true);
-                    bool vis = cv && inr && x != node;
-                    if (vis && names) {
-                        const ca_pod_spec& s = a.specs[spec];
-                        const int32_t nid = a.st[x].name_id;
-                        bool in = false;
-                        for (int32_t k = 0; k < s.prefilter_count; k++) in |= a.names[s.prefilter_first + k] == nid;
-                        vis = in;
-                    }
-                    bool fit = false;
-                    if (vis) {
-                        const bool e = EPH_COLS ? (peph <= ce) : cok;
-                        fit = (cp >= 1) & (all_zero | ((pcpu <= cc) & (pmem <= cm) & e));
-                        if (fit) fit = static_fit(x, ctn);
-                    }
-                    const uint64_t fmk = __ballot(fit), vm = __ballot(vis);
-                    if (fmk) {
-                        const int f = __builtin_ctzll(fmk);
-                        const uint64_t upto = (f == 63) ? ~0ull : ((2ull << f) - 1);
-                        evals += (uint64_t)__popcll(vm & upto);
-                        target = j * 64 + f;
-                        tc = pc_rl64(cc, f); tm = pc_rl64(cm, f); te = EPH_COLS ? pc_rl64(ce, f) : 0;
-                        tpd = pc_rl32(cp, f);
-                        Lw = target + 1 == n ? 0 : target + 1;                       // schedulerbased.go:131
-                        Lraw = Lw;
-                        if (lane == tl) { if (hi) hs1 = target; else hs0 = target; } // :123
-                        break;
-                    }
-                    evals += (uint64_t)__popcll(vm);
-                    // the block passed: refresh its maxima from the rows just read
-                    const bool dj = j < 64 ? ((dirty0 >> j) & 1ull) : ((dirty1 >> (j - 64)) & 1ull);
-                    if (dj && !names && !(a.dbg & 2)) {
-                        const int64_t mc = __ockl_wfred_max_i64(cv ? cc : INT64_MIN);
-                        const int64_t mmx = __ockl_wfred_max_i64(cv ? cm : INT64_MIN);
-                        const int64_t me = EPH_COLS ? __ockl_wfred_max_i64(cv ? ce : INT64_MIN) : 0;
-                        const int32_t mp = __ockl_wfred_max_i32(cv ? cp : INT32_MIN);
-                        if (lane == 0) {
-                            bmc[j] = mc; bmm[j] = mmx; bmp[j] = mp;
-                            if (EPH_COLS) bme[j] = me;
-                        }
-                        if (j < 64) dirty0 &= ~(1ull << j); else dirty1 &= ~(1ull << (j - 64));
-                    }
-                }
-            }
-            PC_MARK(PC_SCAN);
-            if (a.trace && lane == 0) {
-                const int32_t k = atomicAdd(a.trace, 1);
-                if (k < a.trace_cap) {
-                    int32_t* e = a.trace + 16 + 16 * k;
-                    const int32_t dn = a.trace[1];
-                    e[0] = c; e[1] = t; e[2] = h; e[3] = (int32_t)pf; e[4] = target; e[5] = (int32_t)evals;
-                    e[6] = Lw; e[7] = cnt; e[8] = (int32_t)pcpu; e[9] = (int32_t)(pmem >> 20);
-                    e[10] = (int32_t)fc[dn]; e[11] = (int32_t)(fm[dn] >> 20); e[12] = fp[dn];
-                    e[13] = (int32_t)pc_bit(visw, dn) | ((int32_t)pc_bit(taintw, dn) << 1) |
-                            ((int32_t)(EPH_COLS ? 1 : pc_bit(ephw, dn)) << 2);
-                    e[14] = spec; e[15] = id;
-                }
-            }
-            if (target < 0) { failed = true; break; }                                // breakOnFailure
-            // ---- AddPod of the moved copy (:79) ----
-            {
-                const int64_t nc = wsub(tc, pcpu), nmm = wsub(tm, pmem), ne2 = wsub(te, peph);
-                const int32_t np = tpd - 1;
-                if (lane == 0) {
-                    fc[target] = nc; fm[target] = nmm; fp[target] = np;
-                    if (EPH_COLS) fe[target] = ne2;
-                }
-                if ((target >> 6) == cj && lane == (target & 63)) { cc = nc; cm = nmm; ce = ne2; cp = np; }
-                mark_dirty(target >> 6);
-                if (lane == tl) { if (hi) d1 = target; else d0 = target; }
-            }
-            placed++;
-            PC_MARK(PC_ADD);
-        }
-        r.n_placed = placed;
-        r.evals = evals;
-        if (!failed) {
-            // ---- Commit (cluster.go:207-211) ----
-            r.removable = 1;
-            r.n_moves = cnt;
-            for (int half = 0; half < 2 && half * 64 < cnt; half++) {
-                const int32_t t = half * 64 + lane;
-                const bool act = t < cnt;
-                const PcReg& q = half ? r1 : r0;
-                const int32_t f = half ? d1 : d0;
-                const int32_t s = nm + t;
-                if (act) {
-                    ca_plan_move mv;
-                    mv.candidate = c; mv.pod = q.id; mv.new_pod = a.base + s; mv.node = f;
-                    mvbuf[mv_n + t] = mv;
-                    pc_st(a.H + a.base + s, f);
-                }
-                // the copies join their destinations' pod lists in list order
-                int32_t rank = 0, lead = -1;
-                uint64_t pend = __ballot(act);
-                while (pend) {
-                    const int l = __builtin_ctzll(pend);
-                    const int32_t f0 = pc_rl32(f, l);
-                    const uint64_t mm = __ballot(act && f == f0);
-                    if (act && f == f0) { rank = __popcll(mm & pc_below(lane)); lead = l; }
-                    if (lane == l) scratch[l] = __popcll(mm);
-                    pend &= ~mm;
-                }
-                __builtin_amdgcn_wave_barrier();
-                if (act && lead == lane) {
-                    const int32_t old = excnt[f];
-                    excnt[f] = (uint16_t)(old + scratch[lane]);
-                    scratch[lane] = old;
-                }
-                __builtin_amdgcn_wave_barrier();
-                if (act) {
-                    PcPod cp2;
-                    cp2.cpu = q.cpu; cp2.mem = q.mem; cp2.eph = q.eph;
-                    cp2.id = a.base + s; cp2.hint = f; cp2.flags = q.flags; cp2.spec = q.spec; cp2.orig = q.orig;
-                    cp2.pad = 0;
-                    a.ex_pods[a.ex_base[f] + scratch[lead] + rank] = cp2;
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-            if (lane == 0) { destw[jn] &= ~nbit; visw[jn] &= ~nbit; }               // planner.go:280
-            if (jn == cj && lane == (node & 63)) cv = false;
-            mark_dirty(jn);
-            // CanRemovePods, then RemovePods (basic.go:66-95)
-            if (a.n_pdbs > 0) {
-                bool risky = false;
-                for (int half = 0; half < 2; half++) {
-                    const int32_t t = half * 64 + lane;
-                    if (t >= cnt) continue;
-                    const int32_t o = half ? r1.orig : r0.orig;
-                    for (int32_t k = a.pdb_off[o]; k < a.pdb_off[o + 1]; k++)
-                        risky |= atomicSub(a.allowed + a.pdb_pod[k], 1) <= 0;
-                }
-                r.risky = __ballot(risky) ? 1 : 0;
-            }
-            removed++;
-            nm += cnt;
-            mv_n += cnt;
-            __builtin_amdgcn_wave_barrier();
-            if (mv_n + PC_LIST > PC_MVBUF) flush_moves();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            PC_MARK(PC_COMMIT);
-        } else {
-            // ---- Revert: undo the AddPods, then the RemovePods ----
-            for (int half = 0; half < 2; half++) {
-                const int32_t t = half * 64 + lane;
-                if (t >= placed) continue;
-                const PcReg& q = half ? r1 : r0;
-                const int32_t f = half ? d1 : d0;
-                atomicAdd(reinterpret_cast<unsigned long long*>(fc + f), (unsigned long long)q.cpu);
-                atomicAdd(reinterpret_cast<unsigned long long*>(fm + f), (unsigned long long)q.mem);
-                if (EPH_COLS) atomicAdd(reinterpret_cast<unsigned long long*>(fe + f), (unsigned long long)q.eph);
-                atomicAdd(fp + f, 1);
-            }
-            __builtin_amdgcn_wave_barrier();
-            for (int half = 0; half < 2; half++) {
-                const int32_t t = half * 64 + lane;
-                if (t >= placed) continue;
-                const int32_t f = half ? d1 : d0, j = f >> 6;
-                atomicMax(reinterpret_cast<long long*>(bmc + j), (long long)fc[f]);
-                atomicMax(reinterpret_cast<long long*>(bmm + j), (long long)fm[f]);
-                if (EPH_COLS) atomicMax(reinterpret_cast<long long*>(bme + j), (long long)fe[f]);
-                atomicMax(bmp + j, fp[f]);
-            }
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0) {
-                fc[node] = wsub(fc[node], sc); fm[node] = wsub(fm[node], sm); fp[node] -= cnt;
-                if (EPH_COLS) fe[node] = wsub(fe[node], se);
-            }
-            mark_dirty(jn);
-            cj = -1;                                                                 // rows changed
-            r.reason = CA_UNREMOVABLE_NO_PLACE;                                      // cluster.go:174-177
-            PC_MARK(PC_REVERT);
-        }
-        // Hints.Set of this candidate's pods (hints persist whether or not it is removable)
-        if (hs0 != INT32_MIN) pc_st(a.H + r0.id, hs0);
-        if (hs1 != INT32_MIN) pc_st(a.H + r1.id, hs1);
+        if (lane == 0) ctx->r = r;
+        __builtin_amdgcn_wave_barrier();
+        pc_simulate<EPH_COLS>(a, pc_raw, ctx, c, node, cnt, r0, r1);
+        r = ctx->r;
+        nm = ctx->nm;
+        removed = ctx->removed;
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) resbuf[sl] = r;
         if (sl == 63) flush_res(c - 63, 64);
     }
     __builtin_amdgcn_wave_barrier();
     if (!stopped && a.C > 0 && ((a.C - 1) & 63) != 63) flush_res((a.C - 1) & ~63, ((a.C - 1) & 63) + 1);
-    flush_moves();
+    pc_flush_moves(a, mvbuf, ctx, lane);
     if (lane == 0) {
-        a.info[0] = Lraw;
+        a.info[0] = ctx->Lraw;
         a.info[1] = nm;
         a.info[2] = removed;
         a.info[3] = simulated;
 #ifdef CASIM_PROF
         prof[PC_TOTAL] = clock64() - t_start;
-        for (int k = 0; k < PC_NPROF; k++) a.info[4 + k] = (int64_t)prof[k];
+        for (int k = 0; k < PC_NPROF; k++) a.info[4 + k] = (int64_t)(prof[k] + ctx->prof[k]);
 #else
         for (int k = 0; k < PC_NPROF; k++) a.info[4 + k] = 0;
 #endif
@@ -746,13 +931,15 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     const int32_t N = (int32_t)m->nodes.size();
     if (N <= 0 || C <= 0) return 0;
     const int32_t M = move_off[C];
+    // (mirror-wide counters first: no per-pod pass when no pod has ports, extended
+    // resources or ephemeral requests)
     bool eph_cols = false;
-    for (int32_t i = 0; i < M; i++) {
-        const ca_pod_spec& s = m->pods[move_pods[i]].spec;
-        const uint32_t f = pod_dev_flags(s);
-        if (f & (PF_PORTS | PF_MOVED_SCALAR_REQ)) return 0;
-        if (s.req_ephemeral != 0) eph_cols = true;
-    }
+    if (m->n_ext_pods > 0 || m->n_eph_pods > 0)
+        for (int32_t i = 0; i < M; i++) {
+            const ca_pod_spec& s = m->pods[move_pods[i]].spec;
+            if (m->n_ext_pods > 0 && (pod_dev_flags(s) & (PF_PORTS | PF_MOVED_SCALAR_REQ))) return 0;
+            if (s.req_ephemeral != 0) eph_cols = true;
+        }
     const PcLayout Y = pc_layout(N, eph_cols);
     if (Y.total > PC_LDS_MAX || N > PC_MAX_NODES) return 0;
     const int P = pdbs ? pdbs->n_pdbs : 0;
@@ -784,7 +971,8 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     const auto t0 = std::chrono::steady_clock::now();
     int rc;
     if ((rc = m->sync_nodes()) != CA_OK) return rc;
-    if ((rc = m->sync_pods()) != CA_OK) return rc;
+    // the chain reads the device records of the caller's pods only (copies it packs itself)
+    if (m->d_pods_synced < (size_t)n_pods && (rc = m->sync_pods()) != CA_OK) return rc;
     const auto t_sync = std::chrono::steady_clock::now();
     PlanChainScratch& S = chain_scratch(m);
     hipStream_t st = m->stream;

@@ -92,6 +92,7 @@ int32_t ca_mirror::store_moved_copy(int32_t pod) {
     row.spec = moved_spec(pods[pod].spec);     // selector / name indices already on the mirror tables
     row.node = -1;
     if (pod_dev_flags(row.spec) & (PF_PORTS | PF_SCALAR_REQ | PF_MOVED_SCALAR_REQ)) n_ext_pods++;
+    if (row.spec.req_ephemeral != 0) n_eph_pods++;
     pods.push_back(row);
     return (int32_t)pods.size() - 1;
 }

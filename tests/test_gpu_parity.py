@@ -359,6 +359,38 @@ def test_estimate_full_c2_parity(oracle):
             assert np.array_equal(o.sched_pod, np.where(h.sched_pod == 0xFFFF, -1, h.sched_pod.astype(np.int32)))
 
 
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("decouple", ["1", "0"], ids=["decoupled", "coupled"])
+def test_estimate_go_order_decoupled(seed, decouple, oracle, monkeypatch):
+    """Uniform score classes (C2's catalog: every class's pods identical but for their
+    controller): the chains run on the stable class order while Go's sort.Slice ids are
+    computed beside them (CASIM_GO_DECOUPLE=0: the Go sort ahead of the stream).  Both give
+    the Go-order oracle's pod lists in every output mode, with progressive publishing
+    (64-output chunks), lastIndex speculation rounds (existing nodes) and limiter cuts."""
+    monkeypatch.setenv("CASIM_GO_DECOUPLE", decouple)
+    monkeypatch.setenv("CASIM_PUB_CHUNK", "64" if seed % 2 else "4096")
+    w = W.c2(n_pods=6000 + 1000 * seed, n_groups=6 + seed, n_existing=(0, 20, 200)[seed % 3],
+             max_nodes=(1000, 0, 7)[seed % 3], seed=100 + seed)
+    o = oracle.OracleState()
+    W.load_estimate(o, w)
+    L0 = (0, 5, 77)[seed % 3]
+    ro = o.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, L0)
+    m = _mirror()
+    W.load_estimate(m, w)
+    with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as plan:
+        for _ in range(2):
+            g = plan.run(w.max_nodes, L0, want_nodes=True)
+            assert np.array_equal(ro.results, g.results) and ro.last_index == g.last_index
+            assert np.array_equal(ro.sched_pod, g.sched_pod) and np.array_equal(ro.sched_node, g.sched_node)
+            p = plan.run(w.max_nodes, L0, want_nodes=False)
+            assert np.array_equal(ro.sched_pod, p.sched_pod)
+            d = plan.run(w.max_nodes, L0, device_results=True)
+            assert np.array_equal(ro.results, d.results)
+            assert np.array_equal(ro.sched_pod, plan.fetch())
+            h = plan.run_u16(w.max_nodes, L0)
+            assert np.array_equal(ro.sched_pod, np.where(h.sched_pod == 0xFFFF, -1, h.sched_pod.astype(np.int32)))
+
+
 @pytest.mark.parametrize("seed", range(8))
 @pytest.mark.parametrize("chunk", ["4096", "64"], ids=["chunk4096", "chunk64"])
 def test_estimate_plan_publish_random(seed, chunk, oracle, monkeypatch):

@@ -2035,7 +2035,11 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
         CA_HIP_CHECK(hipStreamCreateWithPriority(&p->st2, hipStreamNonBlocking, lo));
     }
     CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_init, hipEventDisableTiming));
-    CA_HIP_CHECK(hipStreamCreateWithFlags(&p->st3, hipStreamNonBlocking));
+    {
+        int lo = 0, hi = 0;                  // the Go-order sort (decoupled): the highest priority
+        CA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        CA_HIP_CHECK(hipStreamCreateWithPriority(&p->st3, hipStreamNonBlocking, hi));
+    }
     CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_emitA, hipEventDisableTiming));
     CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_emitB, hipEventDisableTiming));
     CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_ids, hipEventDisableTiming));

@@ -620,7 +620,7 @@ class PinnedRows:
         self.lib = lib or load()
         self._bufs = {}
 
-    def zeros(self, key: str, n: int, dtype) -> np.ndarray:
+    def zeros(self, key: str, n: int, dtype, zero: bool = True) -> np.ndarray:
         dt = np.dtype(dtype)
         b = self._bufs.get(key)
         if b is None or b.array.size < n or b.array.dtype != dt:
@@ -629,7 +629,8 @@ class PinnedRows:
             b = PinnedArray(self.lib, max(n, 1), dt)
             self._bufs[key] = b
         a = b.array[:n]
-        a.view(np.uint8)[...] = 0
+        if zero:
+            a.view(np.uint8)[...] = 0
         return a
 
     def close(self) -> None:
@@ -812,8 +813,10 @@ class UtilTable:
                                                 len(self.added_node)), "ca_util_table_set_added")
 
     def calculate(self, skip_daemonset_pods: bool, skip_mirror_pods: bool, now_ns: int,
-                  to_host: bool = True):
-        out = np.zeros(len(self.nodes), abi.UTIL_INFO_DTYPE) if to_host else None
+                  to_host: bool = True, out: np.ndarray = None):
+        """out: a caller's (page-locked) result array, else a new one."""
+        if to_host and out is None:
+            out = np.zeros(len(self.nodes), abi.UTIL_INFO_DTYPE)
         ms = C.c_float(0)
         _check(self.lib.ca_util_calculate(self.h, int(skip_daemonset_pods), int(skip_mirror_pods), int(now_ns),
                                           ptr(out) if to_host else None, C.byref(ms)), "ca_util_calculate")

@@ -123,22 +123,30 @@ class DeviceUtil:
     def __init__(self, device: int = 0):
         self.device = device
         self.table = None
-        self.base_id = None
+        self.base = None
+        self.rows = None                 # page-locked result rows (native.PinnedRows), two in turn:
+        self.turn = 0                    # a result stays valid until the call after the next
 
     def __call__(self, ui: "UtilInput", now_ns: int):
         from . import native
-        if self.table is None or self.base_id is not id(ui.base):
+        if self.table is None or self.base is not ui.base:
             if self.table is not None:
                 self.table.close()
             self.table = native.UtilTable(self.device, *ui.base)
-            self.base_id = id(ui.base)
+            self.base = ui.base
+            self.rows = self.rows or native.PinnedRows()
         self.table.set_added(ui.added_node, ui.added_pods)
-        return self.table.calculate(False, False, now_ns)
+        self.turn ^= 1
+        out = self.rows.zeros(f"info{self.turn}", len(ui.base[0]), abi.UTIL_INFO_DTYPE, zero=False)   # all rows written
+        return self.table.calculate(False, False, now_ns, out=out)
 
     def close(self):
         if self.table is not None:
             self.table.close()
             self.table = None
+        if self.rows is not None:
+            self.rows.close()
+            self.rows = None
 
 
 def _util_rows(w: RunOnceWorkload, placed_node: np.ndarray, zeros=_zeros):

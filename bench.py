@@ -14,9 +14,11 @@ extra.device_resident times the same step with the scheduled pods left in HBM.
 
 value = filter-chain evaluations the reference algorithm performs in that batch
 (every RunFilterPlugins call, counted exactly) / wall time.  With --gpus N the same
-100 groups are split into N contiguous blocks, one per rank (strong scaling), and the
-blocks are chained through the checker's lastIndex with one RCCL all_gather of a
-4-int record per rank per step.
+100 groups are split into N contiguous blocks (strong scaling): rank 0 drives all N GPUs
+through ca_multi_estimate_plan_run, the path a cgo caller uses (one process, one host
+thread per device, the lastIndex chain fixed up in the library); with
+CASIM_BENCH_MULTI=rccl each rank runs its block and the blocks are chained through one RCCL
+all_gather of a 4-int record per rank per step.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -508,6 +510,111 @@ def c2_unlimited_leg(args, device: int, with_cpu: bool) -> dict:
     return out
 
 
+def multi_main(args, world: int, rank: int, dist, coll_dev: str):
+    """--gpus N > 1 (default): rank 0 drives all N GPUs through the C ABI's multi-device entry
+    (ca_multi_estimate_plan_*: replicated mirrors, the node groups in N contiguous blocks run
+    concurrently from one host thread per device, the lastIndex chain fixed up in the
+    library — the path a cgo caller uses, results assembled in one process); the other ranks
+    only join the barriers around the timed region.  CASIM_BENCH_MULTI=rccl: every rank
+    runs its block and the chain goes over an RCCL all_gather (main below)."""
+    import torch
+    from autoscaler_amd import native
+    from autoscaler_amd import workloads as W
+    result = None
+    w = W.c2(n_pods=args.pods, n_groups=args.groups, n_existing=args.existing, max_nodes=args.max_nodes, seed=42)
+    items = int(w.group_off[-1])
+    if rank == 0:
+        ndev = max(1, native.device_count())
+        mirrors = [native.Mirror(d % ndev) for d in range(world)]
+        for m in mirrors:
+            W.load_estimate(m, w)
+        multi = native.Multi(mirrors)
+        plan = native.MultiEstimatePlan(multi, w.table, w.group_off, w.pod_idx, w.templates)
+        for _ in range(args.warmup):
+            plan.run(w.max_nodes, 0, want_nodes=False, copy=False)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evals, out = 0, None
+    if rank == 0:
+        for _ in range(args.steps):
+            out = plan.run(w.max_nodes, 0, want_nodes=False, copy=False)
+            evals += int(out.results["evals"].sum())
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t[0])
+    if rank == 0:
+        st = plan.stats()
+        pods = out.sched_pod.copy()
+        res = out.results.copy()
+        # the same batch on one device: identical outputs (the multi path's parity)
+        with native.EstimatePlan(mirrors[0], w.table, w.group_off, w.pod_idx, w.templates) as one:
+            o1 = one.run(w.max_nodes, 0, want_nodes=False)
+        same = bool(np.array_equal(o1.results, res) and np.array_equal(o1.sched_pod, pods)
+                    and o1.last_index == out.last_index)
+        cpu = None
+        if not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import pyoracle                                       # CPU baseline leg only
+            o = pyoracle.OracleState()
+            W.load_estimate(o, w)
+            g = min(args.cpu_groups, args.groups)
+            off = w.group_off[: g + 1]
+            c0 = time.perf_counter()
+            ro = o.estimate(w.table, off, w.pod_idx[: off[-1]], w.templates[:g], w.max_nodes, 0)
+            cpu_s = time.perf_counter() - c0
+            cev = int(ro.results["evals"].sum())
+            cpu = {"value": cev / cpu_s, "unit": "evals/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle/casim_oracle.c Estimate of {g} of the {args.groups} C2 groups (one batch, "
+                             f"{cev} evals in {cpu_s:.2f} s) on 1 thread of {cpu_model()}"}
+        ms = elapsed / args.steps * 1e3
+        result = {
+            "metric": METRIC, "value": evals / elapsed, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic: seeded C2 generator (autoscaler_amd/workloads.py), 64-shape pod catalog",
+            "config": {
+                "workload": "C2: heterogeneous pending pods x node-group templates, resource-fit only "
+                            "(BASELINE.json configs[1]); one step = Estimate() for every group, every group's "
+                            "node count and scheduled pods on the host",
+                "pods": args.pods, "groups": args.groups, "existing_nodes": args.existing,
+                "max_nodes_per_scaleup": args.max_nodes,
+                "parallelism": f"the {args.groups} groups in {st['blocks']} contiguous blocks over {world} GPUs, "
+                               "driven from one process through ca_multi_estimate_plan_run (one host thread per "
+                               "device, replicated mirrors, lastIndex chain fixed up in the library)",
+            },
+            # the devices' kernels are not timed one by one here: the chain kernel's algorithmic
+            # bytes over the whole step time (a lower bound of its rate)
+            "roofline": {"bound": "hbm", "achieved": PHASE_BYTES["chain_ms"] * items / (ms / 1e3) / 1e9,
+                         "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                         "frac": PHASE_BYTES["chain_ms"] * items / (ms / 1e3) / 1e9 / (HBM_PEAK_GBS * world),
+                         "traffic": None, "kernel": "k_ffd_chain", "kernel_ms": None,
+                         "bytes_per_unit": PHASE_BYTES["chain_ms"], "unit_of_work": "(pod, node group) item",
+                         "units_per_launch": items, "basis": "step time over all devices (per-kernel times "
+                                                             "are measured at N=1)"},
+            "cpu_baseline": cpu,
+            "extra": {
+                "estimate_latency_ms": ms,
+                "results_to_host": "32-bit pod ids in one page-locked buffer, each device's zero-copy publisher "
+                                   "writing its block's slice",
+                "blocks": st, "results_identical_to_1gpu": same, "items_per_step": items,
+                "evals_per_step": evals / args.steps,
+                "speedup_vs_cpu_baseline": (evals / elapsed) / cpu["value"] if cpu else None,
+            },
+        }
+        print(json.dumps(result), flush=True)
+        plan.close()
+        multi.close()
+        for m in mirrors:
+            m.close()
+    dist.barrier()
+    dist.destroy_process_group()
+    return result
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -524,6 +631,8 @@ def main():
             local = local % max(1, native_device_count())
         torch.cuda.set_device(local)
         dist.init_process_group(backend)          # "nccl" is RCCL on ROCm
+        if os.environ.get("CASIM_BENCH_MULTI", "capi") != "rccl":
+            return multi_main(args, world, rank, dist, f"cuda:{local}" if backend == "nccl" else "cpu")
 
     from autoscaler_amd import native, shard
     from autoscaler_amd import workloads as W

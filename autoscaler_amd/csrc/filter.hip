@@ -667,6 +667,7 @@ __global__ void __launch_bounds__(SQ_T) k_filter_out(FoArgs a) {
 constexpr int FB_MAX_SHAPES = 64;        // one lane per shape for the bit updates
 constexpr int FB_COLLECT_SHAPES = 1024;  // distinct shapes looked at before the dead ones are merged
 constexpr int FB_T = 64;                 // the walk is one wavefront
+constexpr int FB_ROWWISE_MAX = 24;       // mixed runs shorter than this update the bitmaps row by row
 constexpr size_t FB_LDS_MAX = 160 * 1024;
 
 struct alignas(16) FbPod {               // per pending position (the walk order)
@@ -684,11 +685,22 @@ struct alignas(16) FbRow {               // a placed node's new free resources (
 };
 static_assert(sizeof(FbRow) == 32, "FbRow must be 32 B");
 
+// Which shapes fit a row, for 64 shapes at once: per resource the shapes' distinct requests
+// sorted, and for each count k of them the shapes whose request is at most the k-th
+// (fit = pods >= 1 && (all-zero || cpu, mem and eph each within the row)).
+struct alignas(16) FbThr {
+    int64_t v[3][64];                    // distinct requests (cpu, mem, eph), ascending
+    uint64_t t[3][65];                   // t[d][k]: shapes whose request d <= v[d][k-1] (t[d][0] = 0)
+    int32_t u[3], pad;                   // distinct values per resource
+    uint64_t zero;                       // PF_ALL_ZERO shapes
+};
+
 struct FbArgs {
     NodeHot* hot;
     int32_t n, nwords, P, S, K, n_classes, n_owners, stat_in_lds;
     const FbPod* pods;
     const FbShape* shapes;
+    const FbThr* thr;
     const uint64_t* dyn0;                // [S][nwords] initial dyn words (copied into LDS)
     const uint64_t* vis0;                // [nwords]
     const uint64_t* stat;                // [K][nwords] (copied into LDS when stat_in_lds)
@@ -702,7 +714,7 @@ struct FbArgs {
 
 // LDS layout of k_fb_walk, shared by the host sizing and the kernel
 struct FbLds {
-    size_t shapes, dyn, vis, stat, vpre, slot, bufrow, bufnode, dirty, ocnt, marks, oover, total;
+    size_t shapes, dyn, vis, stat, vpre, slot, bufrow, bufnode, dirty, ocnt, marks, oover, thr, total;
 };
 __host__ __device__ inline size_t fb_a16(size_t x) { return (x + 15) & ~(size_t)15; }
 __host__ __device__ inline FbLds fb_lds(int32_t S, int32_t NW, int32_t K, int32_t stat_in_lds, int32_t n_classes,
@@ -720,7 +732,8 @@ __host__ __device__ inline FbLds fb_lds(int32_t S, int32_t NW, int32_t K, int32_
     l.ocnt = l.dirty + sizeof(uint64_t) * (size_t)NW;
     l.marks = l.ocnt + fb_a16(sizeof(int32_t) * (size_t)(n_owners > 0 ? n_owners : 1));
     l.oover = l.marks + fb_a16((size_t)(n_classes > 0 ? n_classes : 1));
-    l.total = l.oover + fb_a16((size_t)(n_owners > 0 ? n_owners : 1));
+    l.thr = l.oover + fb_a16((size_t)(n_owners > 0 ? n_owners : 1));
+    l.total = l.thr + sizeof(FbThr);
     return l;
 }
 
@@ -729,6 +742,19 @@ __host__ __device__ inline bool fb_fit(const FbShape& sh, int64_t cpu, int64_t m
     if (pods < 1) return false;                                           // fit.go:256-265
     if (sh.flags & PF_ALL_ZERO) return true;                             // :267-272
     return sh.cpu <= cpu && sh.mem <= mem && sh.eph <= eph;              // :274-300
+}
+
+// the shapes (of the first 64) that fit the free resources: fb_fit for all of them at once
+__device__ inline uint64_t fb_fit_mask(const FbThr& t, int64_t cpu, int64_t mem, int64_t eph, int32_t pods) {
+    if (pods < 1) return 0ull;
+    const int64_t x[3] = {cpu, mem, eph};
+    int32_t k[3] = {0, 0, 0};
+#pragma unroll
+    for (int st = 64; st; st >>= 1)
+#pragma unroll
+        for (int d = 0; d < 3; d++)
+            if (k[d] + st <= t.u[d] && t.v[d][k[d] + st - 1] <= x[d]) k[d] += st;
+    return t.zero | (t.t[0][k[0]] & t.t[1][k[1]] & t.t[2][k[2]]);
 }
 
 // dyn[s][w] and vis[w] for every word of every shape: block (word chunk, shape)
@@ -826,6 +852,9 @@ __global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
     uint8_t* oover = fb_smem + lo.oover;
     const bool stat_lds = a.stat_in_lds != 0;
     for (int32_t i = lane; i < S; i += FB_T) shp[i] = a.shapes[i];
+    FbThr* thr = reinterpret_cast<FbThr*>(fb_smem + lo.thr);
+    for (int32_t i = lane; i < (int32_t)(sizeof(FbThr) / 8); i += FB_T)
+        reinterpret_cast<uint64_t*>(thr)[i] = reinterpret_cast<const uint64_t*>(a.thr)[i];
     for (int32_t i = lane; i < S * NW; i += FB_T) dyn[i] = a.dyn0[i];
     if (stat_lds)
         for (int32_t i = lane; i < a.K * NW; i += FB_T) stat_l[i] = a.stat[i];
@@ -858,6 +887,7 @@ __global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
     int32_t overflowing = 0;
 #ifdef CASIM_PROF
     unsigned long long prof_fb[3] = {0, 0, 0};
+    unsigned long long prof_bk[4] = {0, 0, 0, 0};           // mixed runs: chain, row loads, updates; batch edges
     const unsigned long long w_c0 = clock64();
 #endif
     // place k pods of shape s on slot[0..k) (lane t: slot[t]); `pre`: lane 0's row is given
@@ -915,6 +945,8 @@ __global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
         }
         buf_n = 0;
     };
+    int32_t bulk_from = 0;                                                      // next pod to try a mixed run at
+    int32_t n_bulk = 0, n_bulk_pods = 0, n_runs = 0;                            // (stats: steps / ring_scans / windows)
     for (int32_t base = 0; base < a.P; base += FB_T) {
         const int32_t cnt = min(FB_T, a.P - base);
         FbPod lp = {0, -1, -1, 0};
@@ -949,6 +981,202 @@ __global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
 #ifdef CASIM_PROF
             const unsigned long long pc0 = clock64();
 #endif
+            // Mixed runs (loose clusters).  A pod without a live hint scans from the node after
+            // the previous such pod's node (L for the first) to its first fit; a pod whose hint
+            // can pass takes its hinted node (CheckPredicates).  Every lane builds its pod's fit
+            // mask over the 64 ring positions from L (the bitmaps as they are now); the
+            // scanning pods' nodes follow from those masks: consecutive positions, checked for
+            // all lanes at once, and a first-set-bit search at each pod that has to skip.
+            // While the scans stay in the window, the hinted nodes lie outside it and every pod
+            // passes there, the pods land on distinct nodes and no scan crosses an earlier
+            // pod's node, so the masks stay exact and the placements are independent lane
+            // updates.  The leading passes are placed together; the first failing pod goes on
+            // below.  PreFilter failures and pods of a marked class end the run.  Short runs
+            // back off for a while (tight clusters).
+            if (base + j >= bulk_from) {
+                const bool el = lane < cnt && !(lp.flags & PF_PREFILTER_FAIL) && !(lp.simcls >= 0 && marks[lp.simcls]);
+                const uint64_t em = __ballot(el) >> j;
+                const int32_t ne = em == ~0ull ? 64 : (int32_t)__builtin_ctzll(~em);
+                int32_t f = 0;
+                if (ne >= 2) {
+#ifdef CASIM_PROF
+                    const unsigned long long pk0 = clock64();
+#endif
+                    const int32_t ring = NW << 6;                               // raw positions (ids >= n never fit)
+                    // the window's rows, in flight while the chain is worked out (position lane k: node L + k)
+                    int32_t pk = L + lane;
+                    if (pk >= ring) pk -= ring;
+                    NodeHot wrow = {};
+                    if (pk < n) wrow = ld_hot_coh(a.hot + pk);
+                    const bool in = lane >= j && lane < j + ne;
+                    const bool hin = in && (((hinted_mask & may_mask) >> lane) & 1);
+                    const bool un = in && !hin;
+                    const uint64_t um = __ballot(un);
+                    const int32_t rk = __builtin_popcountll(um & bits_below(lane));   // scanning pods before me
+                    const int32_t w0 = L >> 6, sh = L & 63, w1 = w0 + 1 == NW ? 0 : w0 + 1;
+                    const size_t mso = lp.scls >= 0 ? (size_t)lp.scls * NW : 0;
+                    uint64_t fm = 0;                                             // bit k: node L + k fits my pod
+                    if (un) {
+                        const size_t dso = (size_t)lp.shape * NW;
+                        uint64_t g0 = dyn[dso + w0] & vis[w0], g1 = dyn[dso + w1] & vis[w1];
+                        if (lp.scls >= 0) {
+                            g0 &= stat_lds ? stat_l[mso + w0] : a.stat[mso + w0];
+                            g1 &= stat_lds ? stat_l[mso + w1] : a.stat[mso + w1];
+                        }
+                        fm = NW == 1 ? (sh ? (g0 >> sh) | (g0 << (64 - sh)) : g0)
+                                     : (sh ? (g0 >> sh) | (g1 << (64 - sh)) : g0);
+                    }
+                    // the scanning pods' window offsets: from scanning pod r0 on, each pod takes the
+                    // position after the previous one's while it fits there; the first that does
+                    // not searches its mask, and the pods after it shift behind it
+                    int32_t xo = -1;
+                    int32_t r0 = 0, pos0 = 0;                                    // the segment's first pod, its position
+                    int32_t fs_rank = 64;                                        // the first scanning pod without a node
+                    for (;;) {
+                        const int32_t pos = pos0 + (rk - r0);
+                        const bool seg = un && rk >= r0;
+                        const bool fit = seg && pos < 64 && ((fm >> pos) & 1);
+                        const uint64_t miss = __ballot(seg && !fit);
+                        const int32_t m = miss ? (int32_t)__builtin_ctzll(miss) : 64;
+                        const int32_t rm = miss ? __builtin_amdgcn_readlane(rk, m) : 64;
+                        if (seg && rk < rm) xo = pos;
+                        if (!miss) break;
+                        const int32_t pm0 = pos0 + (rm - r0);                   // pod m's first position
+                        const uint64_t fmm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(fm >> 32), m) << 32) |
+                                             (uint32_t)__builtin_amdgcn_readlane((int)fm, m);
+                        const uint64_t mk = pm0 >= 64 ? 0ull : fmm & (~0ull << pm0);
+                        if (!mk) { fs_rank = rm; break; }
+                        const int32_t o = __builtin_ctzll(mk);
+                        if (lane == m) xo = o;
+                        r0 = rm + 1;
+                        pos0 = o + 1;
+                    }
+                    int32_t x = -1;
+                    if (un && rk < fs_rank) { x = L + xo; if (x >= ring) x -= ring; }
+                    bool ok = un && rk < fs_rank;
+                    // my row: the buffer's newest, else the batch's prefetch (hinted pods) or the
+                    // window's (scanning pods, taken once the run is known)
+                    int64_t rc = 0, rm_ = 0, re = 0;
+                    int32_t rp = 0, didx = -1;
+                    if (hin) { x = lh; rc = hrow.cpu; rm_ = hrow.mem; re = hrow.eph; rp = hrow.pods; }
+                    const bool dj = x >= 0 && ((dirty[x >> 6] >> (x & 63)) & 1);
+                    if (dj) {
+                        int32_t i = buf_n - 1;
+                        while (bufnode[i] != x) i--;
+                        const FbRow rr = bufrow[i];
+                        rc = rr.cpu; rm_ = rr.mem; re = rr.eph; rp = rr.pods;
+                        didx = i;
+                    }
+                    const int32_t xw = x >> 6;
+                    const uint64_t bit = 1ull << (x & 63);
+                    if (hin) {
+                        int32_t dh = x - L;
+                        if (dh < 0) dh += ring;
+                        bool clash = dh < 64;                                           // inside the scanning window
+                        for (uint64_t hmk = __ballot(hin); hmk; hmk &= hmk - 1) {      // an earlier hinted pod's node
+                            const int u = __builtin_ctzll(hmk);
+                            clash |= lane > u && __builtin_amdgcn_readlane(lh, u) == x;
+                        }
+                        const uint64_t hs = lp.scls >= 0 ? (stat_lds ? stat_l[mso + xw] : a.stat[mso + xw]) : ~0ull;
+                        ok = !clash && (hs & bit) && ((vis[xw] & bit) || (lp.flags & PF_TOL_UNSCHED)) &&
+                             fb_fit(shp[lp.shape], rc, rm_, re, rp);
+                    }
+                    const uint64_t bad = __ballot(in && !ok) >> j;
+                    f = bad ? min(ne, (int32_t)__builtin_ctzll(bad)) : ne;
+                    const int32_t f_scan = __builtin_popcountll(um & bits_below(j + f));
+                    n_bulk++;
+                    n_bulk_pods += f;
+#ifdef CASIM_PROF
+                    const unsigned long long pk1 = clock64();
+                    prof_bk[0] += pk1 - pk0;
+#endif
+                    if (f > 0) {
+                        const bool mine = lane >= j && lane < j + f;
+                        {
+                            const int32_t src = un && xo >= 0 ? xo : lane;
+                            const int64_t wc = __shfl(wrow.cpu, src, FB_T), wm = __shfl(wrow.mem, src, FB_T),
+                                          we = __shfl(wrow.eph, src, FB_T);
+                            const int32_t wp = __shfl(wrow.pods, src, FB_T);
+                            if (un && !dj) { rc = wc; rm_ = wm; re = we; rp = wp; }
+                        }
+                        FbRow qr = {};
+                        if (mine) {
+                            const FbShape sp = shp[lp.shape];
+                            qr.cpu = wsub(rc, sp.cpu);                                  // AddPod (SF/types.go:672-692)
+                            qr.mem = wsub(rm_, sp.mem);
+                            qr.eph = wsub(re, sp.eph);
+                            qr.pods = rp - 1;
+                            if (didx >= 0) bufnode[didx] = -1;                          // superseded below
+                            const int32_t at = buf_n + (lane - j);
+                            bufrow[at] = qr;
+                            bufnode[at] = x;
+                            __hip_atomic_fetch_or(&dirty[xw], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            out = x;
+                        }
+                        buf_n += f;
+#ifdef CASIM_PROF
+                        const unsigned long long pk2 = clock64();
+                        prof_bk[1] += pk2 - pk1;
+#endif
+                        // the shapes that no longer fit the new rows: every lane its row against all
+                        // shapes at once (threshold tables), then one masked LDS update per shape
+                        // that lost a node (a 65th shape is the dead row: nothing to clear)
+                        const uint64_t pm = __ballot(mine);
+                        const int32_t S64 = min(S, FB_MAX_SHAPES);
+                        if (f < FB_ROWWISE_MAX) {                                       // short runs: row by row,
+                            for (uint64_t fmk = pm; fmk; fmk &= fmk - 1) {              // lane s' checking shape s'
+                                const int t = __builtin_ctzll(fmk);
+                                const int64_t c0 = rlane64(qr.cpu, t), m0 = rlane64(qr.mem, t), e0 = rlane64(qr.eph, t);
+                                const int32_t p0 = __builtin_amdgcn_readlane(qr.pods, t);
+                                const int32_t xt = __builtin_amdgcn_readlane(x, t);
+                                if (lane < S64 && !fb_fit(my_sh, c0, m0, e0, p0))
+                                    __hip_atomic_fetch_and(&dyn[(size_t)lane * NW + (xt >> 6)], ~(1ull << (xt & 63)),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            }
+                        } else {
+                            uint64_t gone = 0;
+                            if (mine) gone = ~fb_fit_mask(*thr, qr.cpu, qr.mem, qr.eph, qr.pods) & bits_below(S64);
+                            uint64_t any = gone;                                            // OR over the lanes
+                            for (int32_t off = 1; off < FB_T; off <<= 1)
+                                any |= ((uint64_t)(uint32_t)__shfl_xor((int)(any >> 32), off, FB_T) << 32) |
+                                       (uint32_t)__shfl_xor((int)any, off, FB_T);
+                            any = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(any >> 32)) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)any);
+                            for (uint64_t am = any; am; am &= am - 1) {
+                                const int s2 = __builtin_ctzll(am);
+                                if ((gone >> s2) & 1)
+                                    __hip_atomic_fetch_and(&dyn[(size_t)s2 * NW + xw], ~bit, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                            }
+                        }
+                        // CheckPredicates per hinted pod (+ failed hints); the scans evaluated
+                        // the visible nodes from L to the last scanning pod's node
+                        evals += (unsigned long long)(f - f_scan) + hint_evals(j, f);
+                        const uint64_t sm = pm & um;                                    // the scanning pods move L
+                        if (sm) {
+                            const int32_t xl = __builtin_amdgcn_readlane(x, 63 - __builtin_clzll(sm));
+                            const int32_t lw = xl >> 6;
+                            const int32_t vpx = vpre[lw] + __builtin_popcountll(vis[lw] & bits_below(xl & 63)) + 1;
+                            evals += (unsigned long long)(xl >= L ? vpx - vpL : vis_total - vpL + vpx);
+                            L = xl + 1 == n ? 0 : xl + 1;                               // schedulerbased.go:131
+                            vpL = L == 0 ? 0 : vpx;
+                            succ = true;
+                        }
+                        j += f;
+#ifdef CASIM_PROF
+                        prof_bk[2] += clock64() - pk2;
+#endif
+                    }
+                }
+                if (f < 2) bulk_from = base + j + 16;
+                if (f > 0) {
+#ifdef CASIM_PROF
+                    prof_fb[2] += clock64() - pc0;
+#endif
+                    continue;
+                }
+            }
+            n_runs++;
             const int32_t s = __builtin_amdgcn_readlane(lp.shape, j);
             const int32_t c = __builtin_amdgcn_readlane(lp.scls, j);
             const int32_t sim = __builtin_amdgcn_readlane(lp.simcls, j);
@@ -1147,8 +1375,13 @@ __global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
         a.ctl->evals = evals;
         a.ctl->overflowing = overflowing;
         a.ctl->phases = (a.P + FB_T - 1) / FB_T;
+        a.ctl->steps = n_bulk;                          // mixed-run attempts
+        a.ctl->ring_scans = n_bulk_pods;                // pods they placed
+        a.ctl->windows = n_runs;                        // pod steps of the one-by-one path
 #ifdef CASIM_PROF
-        for (int i = 0; i < 3; i++) a.ctl->fb_cyc[i] = prof_fb[i];
+        // (CASIM_FB_PROF_BULK: the mixed runs' chain / row loads / updates in place of the
+        // hint / scan / place split)
+        for (int i = 0; i < 3; i++) a.ctl->fb_cyc[i] = a.ctl->fb_cyc[3] ? prof_bk[i] : prof_fb[i];
         a.ctl->seq_cycles = clock64() - w_c0;
         a.ctl->all_cycles = a.ctl->seq_cycles;
 #endif
@@ -1236,6 +1469,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     FoCtl ctl0;
     std::memset(&ctl0, 0, sizeof ctl0);
     ctl0.L = *last_index;
+    ctl0.fb_cyc[3] = getenv("CASIM_FB_PROF_BULK") ? 1 : 0;     // (CASIM_PROF builds: which split)
     char* di = fo.in.as<char>();
     char* dz = fo.zero.as<char>();
     char* dout = fo.out.as<char>();
@@ -1288,11 +1522,22 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
         std::unordered_map<std::string, int32_t, KeyHash> shape_id, cls_id;
         fb_pods.resize((size_t)n);
         const ca_pod_spec* prev = nullptr;               // pods of one controller variant come in a row
+        std::vector<int32_t> cls_seen((size_t)n_classes, -1);              // a similar class's first position
         for (int32_t k = 0; k < n && fb; k++) {
             const ca_pod_spec& ps = t->pods[h_order[k]];
             if (prev && std::memcmp(prev, &ps, sizeof ps) == 0) {          // the same record: same ids
                 fb_pods[k] = fb_pods[k - 1];
                 continue;
+            }
+            const int32_t sc = ps.similar_class;                           // (interleaved controllers)
+            if (sc >= 0) {
+                const int32_t k0 = cls_seen[sc];
+                if (k0 >= 0 && std::memcmp(&t->pods[h_order[k0]], &ps, sizeof ps) == 0) {
+                    fb_pods[k] = fb_pods[k0];
+                    prev = &ps;
+                    continue;
+                }
+                if (k0 < 0) cls_seen[sc] = k;
             }
             prev = &ps;
             const uint32_t f = pod_dev_flags(ps);
@@ -1390,8 +1635,9 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     if (fb) {
         const int32_t S = (int32_t)fb_shapes.size(), K = (int32_t)fb_rep.size();
         const size_t b_pods = al(sizeof(FbPod) * n), b_sh = al(sizeof(FbShape) * std::max(S, 1)),
-                     b_rep = al(sizeof(int32_t) * std::max(K, 1));
-        if ((rc = fo.fb_in.reserve(b_pods + b_sh + b_rep)) != CA_OK || (rc = fo.h_fb.reserve(b_pods + b_sh + b_rep)) != CA_OK)
+                     b_rep = al(sizeof(int32_t) * std::max(K, 1)), b_thr = al(sizeof(FbThr));
+        if ((rc = fo.fb_in.reserve(b_pods + b_sh + b_rep + b_thr)) != CA_OK ||
+            (rc = fo.h_fb.reserve(b_pods + b_sh + b_rep + b_thr)) != CA_OK)
             return rc;
         const size_t w_dyn = (size_t)S * NW, w_vis = (size_t)NW, w_stat = (size_t)K * NW;
         if ((rc = fo.fb_bits.reserve(sizeof(uint64_t) * (w_dyn + w_vis + std::max<size_t>(w_stat, 1)))) != CA_OK) return rc;
@@ -1399,8 +1645,27 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
         std::memcpy(hb, fb_pods.data(), sizeof(FbPod) * n);
         std::memcpy(hb + b_pods, fb_shapes.data(), sizeof(FbShape) * S);
         if (K) std::memcpy(hb + b_pods + b_sh, fb_rep.data(), sizeof(int32_t) * K);
+        {                                                   // the fit thresholds of the first 64 shapes
+            FbThr& th = *reinterpret_cast<FbThr*>(hb + b_pods + b_sh + b_rep);
+            std::memset(&th, 0, sizeof th);
+            const int32_t S64 = std::min(S, FB_MAX_SHAPES);
+            for (int32_t d = 0; d < 3; d++) {
+                auto req = [&](int32_t q) { return d == 0 ? fb_shapes[q].cpu : d == 1 ? fb_shapes[q].mem : fb_shapes[q].eph; };
+                std::vector<int64_t> vals;
+                for (int32_t q = 0; q < S64; q++) vals.push_back(req(q));
+                std::sort(vals.begin(), vals.end());
+                vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+                th.u[d] = (int32_t)vals.size();
+                for (size_t k = 0; k < vals.size(); k++) th.v[d][k] = vals[k];
+                for (size_t k = 1; k <= vals.size(); k++)
+                    for (int32_t q = 0; q < S64; q++)
+                        if (req(q) <= vals[k - 1]) th.t[d][k] |= 1ull << q;
+            }
+            for (int32_t q = 0; q < S64; q++)
+                if (fb_shapes[q].flags & PF_ALL_ZERO) th.zero |= 1ull << q;
+        }
         char* db = fo.fb_in.as<char>();
-        CA_HIP_CHECK(hipMemcpyAsync(db, hb, b_pods + b_sh + b_rep, hipMemcpyHostToDevice, m->stream));
+        CA_HIP_CHECK(hipMemcpyAsync(db, hb, b_pods + b_sh + b_rep + b_thr, hipMemcpyHostToDevice, m->stream));
         uint64_t* d_dyn = fo.fb_bits.as<uint64_t>();
         uint64_t* d_vis = d_dyn + w_dyn;
         uint64_t* d_stat = d_vis + w_vis;
@@ -1422,6 +1687,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
         fa.stat_in_lds = fb_stat_in_lds;
         fa.pods = reinterpret_cast<const FbPod*>(db);
         fa.shapes = reinterpret_cast<const FbShape*>(db + b_pods);
+        fa.thr = reinterpret_cast<const FbThr*>(db + b_pods + b_sh + b_rep);
         fa.dyn0 = d_dyn; fa.vis0 = d_vis; fa.stat = d_stat;
         fa.hints = a.hints; fa.out_node = a.out_node;
         fa.cls_mark = a.cls_mark; fa.cls_capped = a.cls_capped; fa.cls_owner = a.cls_owner;
@@ -1457,18 +1723,11 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     // AddPod of every placed pod on the host rows, in the reference's order
     int32_t placed = 0;
     for (int32_t k = 0; k < n; k++) {
-        const int32_t node = nodes_out[k];
-        out_node[k] = node;
+        out_node[k] = nodes_out[k];
         if (hints) hints[k] = hints_out[k];
-        if (node >= 0) {
-            const int32_t id = m->store_pod(t, h_order[k], node);
-            m->add_pod_to_node(id, node);
-            if (out_pod_id) out_pod_id[k] = id;
-            placed++;
-        } else if (out_pod_id) {
-            out_pod_id[k] = -1;
-        }
+        placed += nodes_out[k] >= 0;
     }
+    m->add_placed_batch(t, h_order, nodes_out, n, out_pod_id);
     *last_index = hctl->L;
     if (evals) *evals += hctl->evals;
     if (n_overflowing) *n_overflowing = hctl->overflowing;

@@ -8,9 +8,12 @@
 #include "mirror.h"
 #include "device_filters.h"
 
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <algorithm>
 
@@ -333,6 +336,112 @@ void ca_mirror::add_pod_to_node(int32_t pod, int32_t node) {
     nodes[node].pods.push_back(pod);
     pods[pod].node = node;
     journal_push(J_ADD_POD, node, pod, (int32_t)nodes[node].pods.size() - 1, before);
+}
+
+void ca_mirror::reserve_more(size_t n_pods_add, size_t n_journal_add) {
+    if (pods.capacity() < pods.size() + n_pods_add) pods.reserve(std::max(pods.capacity() * 2, pods.size() + n_pods_add));
+    if (journal.capacity() < journal.size() + n_journal_add)
+        journal.reserve(std::max(journal.capacity() * 2, journal.size() + n_journal_add));
+}
+
+void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, const int32_t* node, int32_t n,
+                                 int32_t* out_id) {
+    const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto tmark = [&](const char* what) {
+        if (dbg_t)
+            fprintf(stderr, "[add_placed] %-10s %8.3f ms\n", what,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    };
+    int32_t np = 0;
+    bool plain = true;                      // no selector tables or PreFilter names to re-base
+    for (int32_t k = 0; k < n; k++) {
+        if (node[k] < 0) continue;
+        np++;
+        const ca_pod_spec& ps = t->pods[idx[k]];
+        if (ps.aff_term_count > 0 || ((ps.flags & CA_POD_PREFILTER_NAMES) && ps.prefilter_count > 0)) plain = false;
+    }
+    reserve_more((size_t)np, depth > 0 ? (size_t)np : 0);
+    tmark("reserved");
+    const int32_t T = plain ? std::min(6, np / 4096) : 1;
+    if (T <= 1) {
+        for (int32_t k = 0; k < n; k++) {
+            if (node[k] < 0) { if (out_id) out_id[k] = -1; continue; }
+            const int32_t id = store_pod(t, idx[k], node[k]);
+            add_pod_to_node(id, node[k]);
+            if (out_id) out_id[k] = id;
+        }
+        return;
+    }
+    // Threads own disjoint pod id ranges (the records) and disjoint node sets (node % T): each
+    // walks the placements in order for its nodes, so every node sees its pods in order; the
+    // journal entries of different nodes commute (Revert undoes each node's in reverse).
+    const size_t base = pods.size();
+    pods.resize(base + (size_t)np);
+    if (dirty_flag.size() < nodes.size()) dirty_flag.resize(nodes.size(), 0);
+    std::vector<int32_t> id_of((size_t)n, -1);
+    for (int32_t k = 0, c = 0; k < n; k++)
+        if (node[k] >= 0) id_of[k] = (int32_t)base + c++;
+    tmark("resized");
+    struct Part {
+        std::vector<casim::JournalEntry> jr;
+        std::vector<int32_t> dirty;
+        int64_t ext = 0, eph = 0, blockers = 0;
+    };
+    std::vector<Part> part((size_t)T);
+    const bool journaled = depth > 0;
+    auto work = [&](int32_t w) {
+        Part& pt = part[w];
+        const int32_t k0 = (int32_t)((int64_t)n * w / T), k1 = (int32_t)((int64_t)n * (w + 1) / T);
+        for (int32_t k = k0; k < k1; k++) {             // the records of positions [k0, k1)
+            if (id_of[k] < 0) continue;
+            casim::PodRow& r = pods[id_of[k]];
+            r.spec = t->pods[idx[k]];
+            r.node = node[k];
+            if (casim::pod_dev_flags(r.spec) & (casim::PF_PORTS | casim::PF_SCALAR_REQ | casim::PF_MOVED_SCALAR_REQ)) pt.ext++;
+            if (r.spec.req_ephemeral != 0) pt.eph++;
+        }
+        for (int32_t k = 0; k < n; k++) {               // AddPod on my nodes, in order
+            const int32_t x = node[k];
+            if (x < 0 || x % T != w) continue;
+            const ca_pod_spec& p = t->pods[idx[k]];
+            casim::NodeRow& nd = nodes[x];
+            casim::JournalEntry e;
+            if (journaled) {
+                std::memset(&e, 0, sizeof e);
+                e.kind = casim::J_ADD_POD; e.node = x; e.pod = id_of[k];
+                std::memcpy(e.ports, nd.ports, sizeof e.ports);
+            }
+            nd.req_cpu = casim::wadd(nd.req_cpu, p.req_milli_cpu);       // node_apply(+1)
+            nd.req_mem = casim::wadd(nd.req_mem, p.req_memory);
+            nd.req_eph = casim::wadd(nd.req_eph, p.req_ephemeral);
+            for (int i = 0; i < CA_MAX_SCALAR; i++) nd.req_scalar[i] = casim::wadd(nd.req_scalar[i], p.req_scalar[i]);
+            for (int q = 0; q < CA_PORT_WORDS; q++) nd.ports[q] |= p.port_use[q];
+            nd.npods += 1;
+            if (p.flags & CA_POD_REQUIRED_ANTI_AFFINITY) pt.blockers++;
+            if (!dirty_flag[x]) { dirty_flag[x] = 1; pt.dirty.push_back(x); }
+            nd.pods.push_back(id_of[k]);
+            if (journaled) {
+                e.slot = (int32_t)nd.pods.size() - 1;
+                pt.jr.push_back(e);
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int32_t w = 1; w < T; w++) th.emplace_back(work, w);
+    work(0);
+    for (auto& x : th) x.join();
+    tmark("threads");
+    for (Part& pt : part) {
+        n_ext_pods += pt.ext;
+        n_eph_pods += pt.eph;
+        n_scope_blockers += pt.blockers;
+        dirty_rows.insert(dirty_rows.end(), pt.dirty.begin(), pt.dirty.end());
+        if (journaled) journal.insert(journal.end(), pt.jr.begin(), pt.jr.end());
+    }
+    if (out_id)
+        for (int32_t k = 0; k < n; k++) out_id[k] = id_of[k];
+    tmark("merged");
 }
 
 int32_t ca_mirror::store_pod(const ca_pod_table* t, int32_t idx, int32_t node) {

@@ -23,6 +23,9 @@ struct ca_util_table {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_added = nullptr;       // the staging copy of the last set_added is done
+    bool added_in_flight = false;
+    std::vector<int32_t> fill;           // counting-sort cursors
     int32_t n_nodes = 0, n_pods = 0;
     casim::DevBuf nodes, pod_off, pods, info;
     // pods added since the rows were set (ca_util_table_set_added): CSR by node
@@ -56,7 +59,7 @@ __global__ __launch_bounds__(kThreads) void k_node_utilization(
     const ca_util_node* __restrict__ nodes, const int32_t* __restrict__ pod_off,
     const ca_util_pod* __restrict__ pods, int32_t n_nodes, int32_t skip_ds, int32_t skip_mirror,
     int64_t now_ns, ca_util_info* __restrict__ out, const int32_t* __restrict__ add_off,
-    const ca_util_pod* __restrict__ add_pods) {
+    const ca_util_pod* __restrict__ add_pods, ca_util_info* __restrict__ out_host) {
     const int sub = threadIdx.x & (kLanes - 1);
     const int32_t node = blockIdx.x * (kThreads / kLanes) + (int32_t)(threadIdx.x / kLanes);
     if (node >= n_nodes) return;                                  // whole segments only
@@ -116,6 +119,7 @@ __global__ __launch_bounds__(kThreads) void k_node_utilization(
         else               { o.resource = CA_UTIL_MEM; o.utilization = o.mem; }
     }
     out[node] = o;
+    if (out_host) out_host[node] = o;                             // page-locked caller rows (zero-copy)
 }
 
 }  // namespace
@@ -137,7 +141,8 @@ int ca_util_table_create(int32_t device, const ca_util_node* nodes, int32_t n_no
     auto fail = [&](int st) { ca_util_table_destroy(t); return st; };
     if (hipSetDevice(device) != hipSuccess) return fail(CA_EDEVICE);
     if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess)
+        hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&t->ev_added, hipEventDisableTiming) != hipSuccess)
         return fail(CA_EDEVICE);
     int st;
     if ((st = t->nodes.reserve(sizeof(ca_util_node) * (size_t)n_nodes + 1)) ||
@@ -195,6 +200,10 @@ int ca_util_table_set_added(ca_util_table* t, const int32_t* node, const ca_util
     for (int32_t k = 0; k < n; k++)
         if (node[k] < 0 || node[k] >= t->n_nodes) return CA_EINVAL;
     CA_HIP_CHECK(hipSetDevice(t->device));
+    if (t->added_in_flight) {                                  // the staging buffer is reused
+        CA_HIP_CHECK(hipEventSynchronize(t->ev_added));
+        t->added_in_flight = false;
+    }
     t->n_added = 0;
     if (n == 0) return CA_OK;
     // counting sort by node, straight into page-locked staging: [offsets][pods]
@@ -207,10 +216,13 @@ int ca_util_table_set_added(ca_util_table* t, const int32_t* node, const ca_util
     std::fill(off, off + t->n_nodes + 1, 0);
     for (int32_t k = 0; k < n; k++) off[node[k] + 1]++;
     for (int32_t i = 0; i < t->n_nodes; i++) off[i + 1] += off[i];
-    std::vector<int32_t> fill(off, off + t->n_nodes);
+    t->fill.assign(off, off + t->n_nodes);
+    int32_t* fill = t->fill.data();
     for (int32_t k = 0; k < n; k++) out[fill[node[k]]++] = pods[k];
+    // stream-ordered before the next calculate; the next set_added waits for the copy
     CA_HIP_CHECK(hipMemcpyAsync(t->added.ptr, t->h_added.ptr, bytes, hipMemcpyHostToDevice, t->stream));
-    CA_HIP_CHECK(hipStreamSynchronize(t->stream));          // the staging buffer is reused
+    CA_HIP_CHECK(hipEventRecord(t->ev_added, t->stream));
+    t->added_in_flight = true;
     t->n_added = n;
     return CA_OK;
 }
@@ -227,6 +239,7 @@ int ca_util_table_destroy(ca_util_table* t) {
     t->h_added.release();
     if (t->ev0) (void)hipEventDestroy(t->ev0);
     if (t->ev1) (void)hipEventDestroy(t->ev1);
+    if (t->ev_added) (void)hipEventDestroy(t->ev_added);
     if (t->stream) (void)hipStreamDestroy(t->stream);
     delete t;
     return CA_OK;
@@ -237,6 +250,19 @@ int ca_util_calculate(ca_util_table* t, int32_t skip_daemonset_pods, int32_t ski
     if (!t) return CA_EINVAL;
     CA_HIP_CHECK(hipSetDevice(t->device));
     if (t->n_nodes > 0) {
+        // a page-locked `out` (ca_host_alloc) takes the rows straight from the kernel
+        ca_util_info* dst = nullptr;
+        bool zero_copy = false;
+        if (out) {
+            hipPointerAttribute_t attr;
+            if (hipPointerGetAttributes(&attr, out) == hipSuccess && attr.type == hipMemoryTypeHost &&
+                attr.devicePointer != nullptr) {
+                dst = static_cast<ca_util_info*>(attr.devicePointer);
+                zero_copy = true;
+            } else {
+                (void)hipGetLastError();
+            }
+        }
         CA_HIP_CHECK(hipEventRecord(t->ev0, t->stream));
         constexpr int per_block = kThreads / kLanes;
         const int blocks = (t->n_nodes + per_block - 1) / per_block;
@@ -247,10 +273,11 @@ int ca_util_calculate(ca_util_table* t, int32_t skip_daemonset_pods, int32_t ski
                            t->n_added > 0 ? t->added.as<const int32_t>() : nullptr,
                            t->n_added > 0 ? reinterpret_cast<const ca_util_pod*>(
                                                 t->added.as<unsigned char>() + added_pods_at(t->n_nodes))
-                                          : nullptr);
+                                          : nullptr,
+                           dst);
         CA_HIP_CHECK(hipGetLastError());
         CA_HIP_CHECK(hipEventRecord(t->ev1, t->stream));
-        if (out)
+        if (out && !zero_copy)
             CA_HIP_CHECK(hipMemcpyAsync(out, t->info.ptr, sizeof(ca_util_info) * t->n_nodes,
                                         hipMemcpyDeviceToHost, t->stream));
     }

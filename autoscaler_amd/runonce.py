@@ -135,6 +135,8 @@ class DeviceUtil:
             self.table = native.UtilTable(self.device, *ui.base)
             self.base = ui.base
             self.rows = self.rows or native.PinnedRows()
+            for k in (0, 1):             # both result buffers allocated and touched up front
+                self.rows.zeros(f"info{k}", len(ui.base[0]), abi.UTIL_INFO_DTYPE)
         self.table.set_added(ui.added_node, ui.added_pods)
         self.turn ^= 1
         out = self.rows.zeros(f"info{self.turn}", len(ui.base[0]), abi.UTIL_INFO_DTYPE, zero=False)   # all rows written

@@ -18,8 +18,19 @@ CFGS = {
     "c5-allhints": dict(hint_frac=1.0),
     "c5-loose": dict(util_low=(0.2, 0.4), util_high=(0.5, 0.7)),
     "c5-loose-nohints": dict(util_low=(0.2, 0.4), util_high=(0.5, 0.7), hint_frac=0.0),
+    "c5-loose-allhints": dict(util_low=(0.2, 0.4), util_high=(0.5, 0.7), hint_frac=1.0),
 }
-names = sys.argv[1:] or list(CFGS)
+args = sys.argv[1:]
+if "--prof" in args:                    # CASIM_PROF build: the walk's cycle counters
+    args.remove("--prof")
+    os.environ["CASIM_LIB_PATH"] = os.path.join(ROOT, "autoscaler_amd", "lib", "libcasim_prof.so")
+if "--bulk" in args:                    # (with --prof) fbcyc = mixed runs' chain / row loads / updates
+    args.remove("--bulk")
+    os.environ["CASIM_FB_PROF_BULK"] = "1"
+if "--phases" in args:                  # host phase marks of every call on stderr (filter.hip tmark)
+    args.remove("--phases")
+    os.environ["CASIM_DEBUG_TIMING"] = "1"
+names = args or list(CFGS)
 for name in names:
     w = W.c5_filter(**CFGS[name])
     g, o = native.Mirror(0), pyoracle.OracleState()

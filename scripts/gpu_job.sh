@@ -8,6 +8,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
+: > gpurun_out/script.log
 export TMPDIR=/tmp
 rc=0
 while [[ $# -gt 0 ]]; do
@@ -36,7 +37,8 @@ while [[ $# -gt 0 ]]; do
       [[ $rc -eq 0 ]] || { echo "PMC FAILED rc=$rc"; tail -30 "gpurun_out/pmc_$tag.log"; exit $rc; }
       echo "PMC_OK $tag" ;;
     script)
-      timeout -k 10 600 python -u $arg > gpurun_out/script.log 2>&1; rc=$?
+      echo "== $arg" >> gpurun_out/script.log
+      timeout -k 10 600 python -u $arg >> gpurun_out/script.log 2>&1; rc=$?
       tail -40 gpurun_out/script.log
       [[ $rc -eq 0 ]] || { echo "SCRIPT FAILED rc=$rc"; exit $rc; } ;;
     *) echo "unknown step $step"; exit 2 ;;

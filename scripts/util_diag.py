@@ -16,7 +16,9 @@ sel = rng.random(len(placed)) < 0.85
 placed[sel] = rng.integers(0, len(w.filt.nodes), int(sel.sum()))
 ui = runonce.UtilInput(w, placed, "added")
 t = native.UtilTable(0, *ui.base)
-out = np.zeros(len(w.filt.nodes), native.abi.UTIL_INFO_DTYPE)
+rows = native.PinnedRows()
+out = rows.zeros("info", len(w.filt.nodes), native.abi.UTIL_INFO_DTYPE)
+du = runonce.DeviceUtil(0)
 for rep in range(5):
     t0 = time.perf_counter()
     t.set_added(ui.added_node, ui.added_pods)
@@ -25,4 +27,12 @@ for rep in range(5):
     t2 = time.perf_counter()
     r2 = t.calculate(False, False, w.now_ns, to_host=False)
     t3 = time.perf_counter()
-    print(f"set_added {1e3*(t1-t0):.3f} ms  calculate(to host) {1e3*(t2-t1):.3f} ms  calculate(device) {1e3*(t3-t2):.3f} ms  kernel {t.kernel_ms:.4f} ms", flush=True)
+    t.set_added(ui.added_node, ui.added_pods)
+    t4 = time.perf_counter()
+    r3 = t.calculate(False, False, w.now_ns, out=out)
+    t5 = time.perf_counter()
+    r4 = du(ui, w.now_ns)
+    t6 = time.perf_counter()
+    assert np.array_equal(r.view(np.uint8), r3.view(np.uint8)) and np.array_equal(r.view(np.uint8), r4.view(np.uint8))
+    print(f"set_added {1e3*(t1-t0):.3f} ms  calculate(to host) {1e3*(t2-t1):.3f} ms  calculate(device) {1e3*(t3-t2):.3f} ms  "
+          f"calculate(page-locked, zero-copy) {1e3*(t5-t4):.3f} ms  DeviceUtil {1e3*(t6-t5):.3f} ms  kernel {t.kernel_ms:.4f} ms", flush=True)

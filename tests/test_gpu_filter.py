@@ -39,6 +39,14 @@ CONFIGS = {
     "small": dict(n_nodes=500, pods_per_node=20, n_pending=2000),
     "tight": dict(n_nodes=800, pods_per_node=20, n_pending=6000, util_low=(0.9, 0.97), util_high=(0.97, 1.0)),
     "loose": dict(n_nodes=2000, pods_per_node=20, n_pending=6000, util_low=(0.2, 0.4), util_high=(0.5, 0.7)),
+    # mixed runs: scanning and hinted pods placed together, windows that wrap the ring,
+    # a ring shorter than the 64-node window, a cluster that fills up on the way
+    "loose-hinted": dict(n_nodes=1500, pods_per_node=20, n_pending=6000, hint_frac=0.6,
+                         util_low=(0.1, 0.3), util_high=(0.3, 0.6)),
+    "loose-tiny": dict(n_nodes=37, pods_per_node=10, n_pending=900, hint_frac=0.3,
+                       util_low=(0.1, 0.3), util_high=(0.3, 0.5)),
+    "loose-filling": dict(n_nodes=300, pods_per_node=20, n_pending=6000, hint_frac=0.4,
+                          util_low=(0.3, 0.5), util_high=(0.5, 0.7)),
     "nohints": dict(n_nodes=3000, pods_per_node=20, n_pending=8000, hint_frac=0.0),
     "allhints": dict(n_nodes=3000, pods_per_node=20, n_pending=8000, hint_frac=1.0),
     "full": dict(),

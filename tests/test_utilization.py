@@ -188,3 +188,34 @@ def test_gpu_empty_table():
     t = native.UtilTable(0, np.zeros(0, abi.UTIL_NODE_DTYPE), np.zeros(1, np.int32), np.zeros(0, abi.UTIL_POD_DTYPE))
     assert len(t.calculate(True, True, 0)) == 0
     t.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,n_nodes,ppn,n_add", [(7, 63, 3, 40), (8, 3000, 12, 5000), (9, 15000, 20, 17000)])
+def test_gpu_added_pods_zero_copy(seed, n_nodes, ppn, n_add, oracle_lib):
+    """ca_util_table_set_added (rows appended per node) with page-locked results written by
+    the kernel (zero-copy) == the oracle over the merged table; set_added twice in a row
+    (the staging buffer reused while the previous copy may be in flight) keeps the last."""
+    from autoscaler_amd import native
+    nodes, off, pods, now = W.util_table(seed=seed, n_nodes=n_nodes, pods_per_node=ppn)
+    rng = np.random.default_rng(seed)
+    add_node = rng.integers(0, n_nodes, n_add).astype(np.int32)
+    add = pods[rng.integers(0, len(pods), n_add)] if len(pods) else np.zeros(n_add, abi.UTIL_POD_DTYPE)
+    # the merged reference table: each node's rows, then its added pods in call order
+    node_of = np.concatenate([np.repeat(np.arange(n_nodes), np.diff(off)), add_node])
+    order = np.argsort(node_of, kind="stable")
+    m_pods = np.concatenate([pods, add])[order]
+    m_off = np.zeros(n_nodes + 1, np.int32)
+    np.cumsum(np.bincount(node_of, minlength=n_nodes), out=m_off[1:])
+    t = native.UtilTable(0, nodes, off, pods)
+    rows = native.PinnedRows()
+    t.set_added(add_node[::-1].copy(), add[::-1].copy())          # replaced by the next call
+    t.set_added(add_node, add)
+    for sds, smp in ((False, False), (True, True)):
+        out = rows.zeros("info", n_nodes, abi.UTIL_INFO_DTYPE)
+        got = t.calculate(sds, smp, now, out=out)
+        ref = oracle_lib.node_utilization(nodes, m_off, m_pods, sds, smp, now)
+        assert _bits_equal(got, ref), (seed, sds, smp)
+        assert _bits_equal(t.calculate(sds, smp, now), ref)       # pageable: the DMA path
+    t.close()
+    rows.close()

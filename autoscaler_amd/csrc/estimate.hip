@@ -476,7 +476,8 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
                                                      const uint32_t* __restrict__ item_rank,
                                                      uint32_t* __restrict__ sorted, uint64_t* __restrict__ gE,
                                                      uint64_t* __restrict__ xs_all, pdq::Frame* __restrict__ stack_all,
-                                                     int32_t lds_n, int32_t force, int32_t limit0, const int32_t* __restrict__ gmap) {
+                                                     int32_t lds_n, int32_t force, int32_t limit0, const int32_t* __restrict__ gmap,
+                                                     int32_t* __restrict__ ids_out, int32_t* __restrict__ ids_ready) {
     extern __shared__ __align__(16) unsigned char pdq_dyn[];
     __shared__ pdq::Ctl ctl;
     const int gi = GSEL(blockIdx.x);
@@ -511,21 +512,37 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
     if (mode == 1) {
         const pdq::LdsStore st{e16, rk, rmb, rmp};
         pdq::wg_sort(st, n, stack, n / 2 + 2, scr, ctl, limit0);
-        for (int32_t k = tid; k < n; k += pdq::NT) sorted[off + k] = e16[k];
+        if (ids_out)                                   // decoupled Go order: the ids themselves
+            for (int32_t k = tid; k < n; k += pdq::NT) ids_out[off + k] = pod_idx[off + e16[k]];
+        else
+            for (int32_t k = tid; k < n; k += pdq::NT) sorted[off + k] = e16[k];
     } else if (mode == 2) {
         uint32_t* e = reinterpret_cast<uint32_t*>(gE + off);
         for (int32_t i = tid; i < n; i += pdq::NT) e[i] = (scr[i] << 20) | (uint32_t)i;
         __syncthreads();
         const pdq::G32Store st{e};
         pdq::wg_sort(st, n, stack, n / 2 + 2, scr, ctl, limit0);
-        for (int32_t k = tid; k < n; k += pdq::NT) sorted[off + k] = e[k] & 0xFFFFFu;
+        if (ids_out)
+            for (int32_t k = tid; k < n; k += pdq::NT) ids_out[off + k] = pod_idx[off + (int32_t)(e[k] & 0xFFFFFu)];
+        else
+            for (int32_t k = tid; k < n; k += pdq::NT) sorted[off + k] = e[k] & 0xFFFFFu;
     } else {
         uint64_t* e = gE + off;
         for (int32_t i = tid; i < n; i += pdq::NT) e[i] = ((uint64_t)scr[i] << 32) | (uint32_t)i;
         __syncthreads();
         const pdq::G64Store st{e};
         pdq::wg_sort(st, n, stack, n / 2 + 2, xs_all + off, ctl, limit0);
-        for (int32_t k = tid; k < n; k += pdq::NT) sorted[off + k] = (uint32_t)e[k];
+        if (ids_out)
+            for (int32_t k = tid; k < n; k += pdq::NT) ids_out[off + k] = pod_idx[off + (int32_t)(uint32_t)e[k]];
+        else
+            for (int32_t k = tid; k < n; k += pdq::NT) sorted[off + k] = (uint32_t)e[k];
+    }
+    if (ids_ready) {                                   // this group's ids are final
+        __syncthreads();
+        if (tid == 0) {
+            __threadfence();
+            __hip_atomic_store(&ids_ready[gi], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -610,24 +627,6 @@ __global__ void __launch_bounds__(256) k_emit_bucket(const GroupMeta* __restrict
     }
     const uint64_t hb = __ballot(head);
     if (lane == 0) heads[gm.moff + (i >> 6)] = hb;
-}
-
-// Decoupled Go order: the group's pod ids in sort.Slice order over the stream written in
-// stable class order (same class at every position; the classes' pods are
-// interchangeable for the chain: ca_podset::cls_uniform), then the group's ready flag.
-__global__ void __launch_bounds__(1024) k_emit_go_ids(const GroupMeta* __restrict__ groups,
-                                                     const uint32_t* __restrict__ sorted,
-                                                     const int32_t* __restrict__ pod_idx, int32_t* __restrict__ spod,
-                                                     int32_t* __restrict__ ids_ready, const int32_t* __restrict__ gmap) {
-    const int gi = GSEL(blockIdx.x);
-    const GroupMeta gm = groups[gi];
-    for (int32_t i = threadIdx.x; i < gm.count; i += blockDim.x)
-        spod[gm.off + i] = pod_idx[gm.off + (int32_t)sorted[gm.off + i]];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        __hip_atomic_store(&ids_ready[gi], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
 }
 
 // 4. the First-Fit-Decreasing chain -------------------------------------------
@@ -1964,7 +1963,7 @@ struct ca_estimate_plan {
     // per-position ranks of the comparison path
     DevBuf d_pdq_e, d_pdq_scr, d_pdq_stack, d_item_rank;
     // decoupled Go order (uniform classes): the chains run on the stable class order while
-    // k_pdq_sort + k_emit_go_ids on st3 write the Go-order ids into d_spod (d_sortC: the
+    // k_pdq_sort on st3 writes the Go-order ids into d_spod_go (d_sortC: the
     // permutation; d_ids_ready: per group, set when its ids are final)
     DevBuf d_sortC, d_ids_ready, d_spod_go, d_crank2;
     hipStream_t st3 = nullptr;
@@ -2206,7 +2205,8 @@ bool go_sort_order() {
 // k_pdq_sort for `ng` groups (map gm) into d_sortA: ranks from the class ranks (crank, U)
 // or from item_rank
 int launch_pdq_sort(ca_estimate_plan* p, hipStream_t ss, const int32_t* gm, int32_t ng, const int32_t* crank,
-                    int32_t U, const uint32_t* item_rank, int32_t force = 0, uint32_t* out = nullptr) {
+                    int32_t U, const uint32_t* item_rank, int32_t force = 0, uint32_t* out = nullptr,
+                    int32_t* ids_out = nullptr, int32_t* ids_ready = nullptr) {
     const int32_t lds_n = std::min(p->max_count, PDQ_LDS_N);
     const size_t lds = pdq_lds_bytes(lds_n);
     int rc;
@@ -2214,7 +2214,7 @@ int launch_pdq_sort(ca_estimate_plan* p, hipStream_t ss, const int32_t* gm, int3
     hipLaunchKernelGGL(k_pdq_sort, dim3(ng), dim3(pdq::NT), lds, ss, p->d_meta.as<GroupMeta>(),
                        p->d_pod_idx.as<int32_t>(), p->s ? p->s->d_cls.as<int32_t>() : nullptr, crank, U, item_rank,
                        out ? out : p->d_sortA.as<uint32_t>(), p->d_pdq_e.as<uint64_t>(), p->d_pdq_scr.as<uint64_t>(),
-                       p->d_pdq_stack.as<pdq::Frame>(), lds_n, force, 0, gm);
+                       p->d_pdq_stack.as<pdq::Frame>(), lds_n, force, 0, gm, ids_out, ids_ready);
     CA_HIP_CHECK(hipGetLastError());
     return CA_OK;
 }
@@ -2393,13 +2393,11 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                p->d_crank2.as<int32_t>(), (const int32_t*)nullptr);
             CA_HIP_CHECK(hipGetLastError());
             int rc0;
+            // (the sort writes each group's ids and sets its ready flag as it finishes)
             if ((rc0 = launch_pdq_sort(p, p->st3, nullptr, G, p->d_crank2.as<int32_t>(), U, nullptr, 0,
-                                       p->d_sortC.as<uint32_t>())) != CA_OK)
+                                       p->d_sortC.as<uint32_t>(), p->d_spod_go.as<int32_t>(),
+                                       p->d_ids_ready.as<int32_t>())) != CA_OK)
                 return rc0;
-            hipLaunchKernelGGL(k_emit_go_ids, dim3(G), dim3(1024), 0, p->st3, p->d_meta.as<GroupMeta>(),
-                               p->d_sortC.as<uint32_t>(), p->d_pod_idx.as<int32_t>(), p->d_spod_go.as<int32_t>(),
-                               p->d_ids_ready.as<int32_t>(), (const int32_t*)nullptr);
-            CA_HIP_CHECK(hipGetLastError());
             CA_HIP_CHECK(hipEventRecord(p->ev_ids, p->st3));
         }
         const int32_t blocks = (p->max_count + 255) / 256;
@@ -2865,7 +2863,7 @@ int ca_go_sort_ranks(int32_t device, const uint32_t* ranks, int32_t n, int32_t s
     if ((rc = ensure_dyn_lds((const void*)k_pdq_sort, lds)) != CA_OK) return rc;
     hipLaunchKernelGGL(k_pdq_sort, dim3(1), dim3(pdq::NT), lds, 0, meta.as<GroupMeta>(), nullptr, nullptr, nullptr, 0,
                        rk.as<uint32_t>(), sorted.as<uint32_t>(), e.as<uint64_t>(), scr.as<uint64_t>(),
-                       stack.as<pdq::Frame>(), lds_n, store, std::max(limit, 0), nullptr);
+                       stack.as<pdq::Frame>(), lds_n, store, std::max(limit, 0), nullptr, nullptr, nullptr);
     CA_HIP_CHECK(hipGetLastError());
     CA_HIP_CHECK(hipMemcpy(perm, sorted.ptr, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost));
     return CA_OK;

@@ -6,6 +6,9 @@
 #pragma once
 #include "casim_internal.h"
 #include <array>
+#include <cstdlib>
+#include <new>
+#include <sys/mman.h>
 
 namespace casim {
 
@@ -111,13 +114,47 @@ struct Stats {
 
 }  // namespace casim
 
+namespace casim {
+// Large blocks from 2 MiB-aligned anonymous mappings with transparent huge pages asked for:
+// the pod records only grow (ids are never reused), so every call that stores pods touches
+// fresh memory, and 4 KiB first-touch faults cost more than the records' copies.
+template <class T> struct HugeAlloc {
+    using value_type = T;
+    static constexpr size_t kHuge = (size_t)2 << 20;
+    HugeAlloc() = default;
+    template <class U> HugeAlloc(const HugeAlloc<U>&) {}
+    static size_t mapped(size_t n) { return (n * sizeof(T) + kHuge - 1) & ~(kHuge - 1); }
+    T* allocate(size_t n) {
+        if (n * sizeof(T) < 2 * kHuge) {
+            void* p = std::malloc(n * sizeof(T));
+            if (!p) throw std::bad_alloc();
+            return static_cast<T*>(p);
+        }
+        const size_t sz = mapped(n);
+        char* base = static_cast<char*>(mmap(nullptr, sz + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0));
+        if (base == MAP_FAILED) throw std::bad_alloc();
+        char* al = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(base) + kHuge - 1) & ~(uintptr_t)(kHuge - 1));
+        if (al > base) munmap(base, (size_t)(al - base));                       // keep [al, al + sz)
+        if (base + sz + kHuge > al + sz) munmap(al + sz, (size_t)(base + sz + kHuge - (al + sz)));
+        (void)madvise(al, sz, MADV_HUGEPAGE);
+        return reinterpret_cast<T*>(al);
+    }
+    void deallocate(T* p, size_t n) {
+        if (n * sizeof(T) < 2 * kHuge) std::free(p);
+        else munmap(p, mapped(n));
+    }
+    template <class U> bool operator==(const HugeAlloc<U>&) const { return true; }
+    template <class U> bool operator!=(const HugeAlloc<U>&) const { return false; }
+};
+}  // namespace casim
+
 struct ca_mirror {
     int32_t device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
 
     std::vector<casim::NodeRow> nodes;
-    std::vector<casim::PodRow> pods;
+    std::vector<casim::PodRow, casim::HugeAlloc<casim::PodRow>> pods;
     std::vector<ca_selector_term> terms;
     std::vector<ca_selector_req> reqs;
     std::vector<int32_t> pf_names;

@@ -363,7 +363,7 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
     }
     reserve_more((size_t)np, depth > 0 ? (size_t)np : 0);
     tmark("reserved");
-    const int32_t T = plain ? std::min(6, np / 4096) : 1;
+    const int32_t T = plain ? std::min(8, np / 2048) : 1;
     if (T <= 1) {
         for (int32_t k = 0; k < n; k++) {
             if (node[k] < 0) { if (out_id) out_id[k] = -1; continue; }
@@ -402,6 +402,13 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
             if (r.spec.req_ephemeral != 0) pt.eph++;
         }
         for (int32_t k = 0; k < n; k++) {               // AddPod on my nodes, in order
+            if (k + 32 < n) {                            // (rows are cache misses: fetch ahead)
+                const int32_t y = node[k + 32];
+                if (y >= 0 && y % T == w) {
+                    __builtin_prefetch(&nodes[y], 1);
+                    __builtin_prefetch(reinterpret_cast<const char*>(&nodes[y]) + 256, 1);
+                }
+            }
             const int32_t x = node[k];
             if (x < 0 || x % T != w) continue;
             const ca_pod_spec& p = t->pods[idx[k]];

@@ -63,6 +63,7 @@ __device__ unsigned long long g_pdq_prof[32];
 constexpr int NT = 1024;             // threads of the workgroup
 constexpr int NW = NT / 64;          // wavefronts
 constexpr int MAXF = 96;             // frames per workgroup step
+constexpr int PIS_WAVE_MAX = 4096;   // LDS store: longer frames run partialInsertionSort on the workgroup
 constexpr int MAX_INSERTION = 12;    // pdqsort_func maxInsertion
 enum { HINT_UNKNOWN = 0, HINT_INC = 1, HINT_DEC = 2 };
 enum { OP_DONE = 0, OP_PART = 1, OP_EQ = 2 };
@@ -1473,8 +1474,9 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
             PDQ_WADD(18, t_rv);
             bool pis = wb && wp && hint == HINT_INC;
             if constexpr (std::is_same<S, LdsStore>::value) {
-                // partialInsertionSort here, one wavefront per frame
-                if (pis) {
+                // partialInsertionSort here, one wavefront per frame; long frames (its scans
+                // run over the whole frame when it is sorted) go to the workgroup below
+                if (pis && b - a <= PIS_WAVE_MAX) {
                     PDQ_T(t_pis);
                     const bool sorted = w_partial_insertion(s, a, b);
                     PDQ_WADD(19, t_pis);

@@ -559,11 +559,13 @@ int ca_util_table_update(ca_util_table* t, const ca_util_node* nodes, int32_t n_
 /* Pods added to the snapshot since the rows were set (AddPod: FilterOutSchedulable's
  * placements, static_autoscaler.go:528): pods[k] now runs on node[k].  Replaces the previous
  * added set (n = 0 clears it; ca_util_table_update clears it too).  Calculate counts them
- * with the node's rows — only these records cross PCIe, not the node's whole pod list. */
+ * with the node's rows — only these records cross PCIe, not the node's whole pod list.
+ * The copy is asynchronous: the next ca_util_calculate on t runs after it. */
 int ca_util_table_set_added(ca_util_table* t, const int32_t* node, const ca_util_pod* pods, int32_t n);
 /* Calculate(nodeInfo, skipDaemonSetPods, skipMirrorPods, gpuConfig, currentTime) for every
  * node.  out NULL keeps the results in HBM (ca_util_device_results); otherwise out[n_nodes]
- * is filled.  *kernel_ms (may be NULL) = device time of the kernel. */
+ * is filled — by the kernel itself when out is page-locked (ca_host_alloc), else by a copy.
+ * *kernel_ms (may be NULL) = device time of the kernel. */
 int ca_util_calculate(ca_util_table* t, int32_t skip_daemonset_pods, int32_t skip_mirror_pods,
                       int64_t now_ns, ca_util_info* out, float* kernel_ms);
 int ca_util_device_results(const ca_util_table* t, const ca_util_info** out);

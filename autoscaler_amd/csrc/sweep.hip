@@ -1574,26 +1574,41 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 std::memcpy(ht, todo.data(), sizeof(int32_t) * T);
                 std::memcpy(ht + T, todo_ws.data(), sizeof(int32_t) * T);
                 std::memcpy(ht + 2 * T, todo_k.data(), sizeof(int32_t) * T);
-                CA_HIP_CHECK(hipMemcpyAsync(sw.todo.ptr, ht, sizeof(int32_t) * 3 * T, hipMemcpyHostToDevice, st));
+                // zero-copy both ways: the kernel reads the rows to build from the page-locked
+                // staging and writes the compact rows straight into the host's buffer (no copy
+                // launches around a 40 µs kernel; the round trip is what a round costs)
+                if ((rc = sw.h_ctab.reserve(sizeof(int32_t) * (64 + FPW) * (size_t)T)) != CA_OK) return rc;
+                int32_t* const ct = sw.h_ctab.as<int32_t>();
+                void *d_ht = nullptr, *d_ct = nullptr;
+                const bool zc = !getenv("CASIM_SWEEP_COPY_ROUNDS") &&
+                                hipHostGetDevicePointer(&d_ht, ht, 0) == hipSuccess &&
+                                hipHostGetDevicePointer(&d_ct, ct, 0) == hipSuccess;
+                if (!zc) {
+                    (void)hipGetLastError();
+                    CA_HIP_CHECK(hipMemcpyAsync(sw.todo.ptr, ht, sizeof(int32_t) * 3 * T, hipMemcpyHostToDevice, st));
+                }
+                const int32_t* const k_todo = zc ? static_cast<const int32_t*>(d_ht) : sw.todo.as<int32_t>();
+                int32_t* const k_tab = zc ? static_cast<int32_t*>(d_ct) : sw.tab.as<int32_t>();
+                int32_t* const k_tfp = zc ? static_cast<int32_t*>(d_ct) + 64 * (size_t)T : d_tfp;
                 CA_HIP_CHECK(hipEventRecord(m->ev0, st));
                 hipLaunchKernelGGL(k_sweep_table, dim3(T), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
                                    m->d_static.as<NodeStatic>(), n, in.d_mask.as<uint8_t>(), in.d_c.as<int32_t>(),
                                    in.d_off.as<int32_t>(), in.d_moves.as<int32_t>(), m->d_pods.hot.as<PodHot>(),
                                    m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
                                    m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
-                                   in.d_hints.as<int32_t>(), sw.todo.as<int32_t>(), sw.todo.as<int32_t>() + T,
-                                   (const int32_t*)nullptr, sw.tab.as<int32_t>(), T, nullptr, nullptr, nullptr, d_tfp,
+                                   in.d_hints.as<int32_t>(), k_todo, k_todo + T,
+                                   (const int32_t*)nullptr, k_tab, T, nullptr, nullptr, nullptr, k_tfp,
                                    (const int32_t*)d_mode, sw.bsum.as<BlockSum>());
                 CA_HIP_CHECK(hipGetLastError());
                 CA_HIP_CHECK(hipEventRecord(m->ev1, st));
                 // compact rows (row t of this round): only they cross PCIe, then go to their
                 // places in the host copy, stored [lane][candidate] so the walk, whose class
                 // stays near the centre, reads it nearly sequentially
-                if ((rc = sw.h_ctab.reserve(sizeof(int32_t) * (64 + FPW) * (size_t)T)) != CA_OK) return rc;
-                int32_t* const ct = sw.h_ctab.as<int32_t>();
-                CA_HIP_CHECK(hipMemcpyAsync(ct, sw.tab.ptr, sizeof(int32_t) * 64 * (size_t)T, hipMemcpyDeviceToHost, st));
-                CA_HIP_CHECK(hipMemcpyAsync(ct + 64 * (size_t)T, d_tfp, sizeof(int32_t) * FPW * (size_t)T,
-                                            hipMemcpyDeviceToHost, st));
+                if (!zc) {
+                    CA_HIP_CHECK(hipMemcpyAsync(ct, sw.tab.ptr, sizeof(int32_t) * 64 * (size_t)T, hipMemcpyDeviceToHost, st));
+                    CA_HIP_CHECK(hipMemcpyAsync(ct + 64 * (size_t)T, d_tfp, sizeof(int32_t) * FPW * (size_t)T,
+                                                hipMemcpyDeviceToHost, st));
+                }
                 CA_HIP_CHECK(hipStreamSynchronize(st));
                 tmark("table sync");
                 const int32_t* ctf = ct + 64 * (size_t)T;

@@ -1727,7 +1727,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
         if (hints) hints[k] = hints_out[k];
         placed += nodes_out[k] >= 0;
     }
-    m->add_placed_batch(t, h_order, nodes_out, n, out_pod_id);
+    m->add_placed_batch(t, h_order, nodes_out, n, out_pod_id, fb);    // the walk flushed its rows to d_hot
     *last_index = hctl->L;
     if (evals) *evals += hctl->evals;
     if (n_overflowing) *n_overflowing = hctl->overflowing;

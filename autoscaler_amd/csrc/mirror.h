@@ -204,8 +204,10 @@ struct ca_mirror {
     void reserve_more(size_t n_pods_add, size_t n_journal_add);    // geometric growth before a batch
     // store_pod + add_pod_to_node of pod idx[k] on node[k] for every k with node[k] >= 0, in
     // order (ids in out_id, -1 for the others); large batches on a few host threads
+    // device_rows: the caller's kernel already wrote the placed nodes' free resources to
+    // d_hot (FilterOutSchedulable's bitmap walk), so they stay clean where fill_hot agrees
     void add_placed_batch(const ca_pod_table* t, const int32_t* idx, const int32_t* node, int32_t n,
-                          int32_t* out_id);
+                          int32_t* out_id, bool device_rows = false);
     int32_t store_moved_copy(int32_t pod);  // the copy findPlaceFor schedules (cluster.go:235-240)
     void journal_push(int32_t kind, int32_t node, int32_t pod, int32_t slot, const uint64_t* ports);
     void fill_hot(int32_t i, casim::NodeHot& h) const;

@@ -345,7 +345,7 @@ void ca_mirror::reserve_more(size_t n_pods_add, size_t n_journal_add) {
 }
 
 void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, const int32_t* node, int32_t n,
-                                 int32_t* out_id) {
+                                 int32_t* out_id, bool device_rows) {
     const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     auto tmark = [&](const char* what) {
@@ -364,6 +364,22 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
     reserve_more((size_t)np, depth > 0 ? (size_t)np : 0);
     tmark("reserved");
     const int32_t T = plain ? std::min(8, np / 2048) : 1;
+    // rows dirty before this batch stay dirty; the batch's own marks are dropped below where
+    // the kernel's row equals fill_hot's
+    const size_t dirty0 = dirty_rows.size();
+    auto keep_device_rows = [&]() {
+        if (!device_rows) return;
+        size_t w = dirty0;
+        for (size_t i = dirty0; i < dirty_rows.size(); i++) {
+            const int32_t x = dirty_rows[i];
+            const NodeRow& nd = nodes[x];
+            // the kernel's pods column is the old clamp minus one per pod: equal unless clamped
+            const int64_t fp = nd.spec.alloc_pods - nd.npods;
+            if (fp >= INT32_MIN && fp + np <= INT32_MAX && (size_t)x < d_rows) { dirty_flag[x] = 0; continue; }
+            dirty_rows[w++] = x;
+        }
+        dirty_rows.resize(w);
+    };
     if (T <= 1) {
         for (int32_t k = 0; k < n; k++) {
             if (node[k] < 0) { if (out_id) out_id[k] = -1; continue; }
@@ -371,6 +387,7 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
             add_pod_to_node(id, node[k]);
             if (out_id) out_id[k] = id;
         }
+        keep_device_rows();
         return;
     }
     // Threads own disjoint pod id ranges (the records) and disjoint node sets (node % T): each
@@ -448,6 +465,7 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
     }
     if (out_id)
         for (int32_t k = 0; k < n; k++) out_id[k] = id_of[k];
+    keep_device_rows();
     tmark("merged");
 }
 

@@ -1727,7 +1727,21 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
         if (hints) hints[k] = hints_out[k];
         placed += nodes_out[k] >= 0;
     }
+    const size_t pods0 = m->pods.size(), terms0 = m->terms.size(), reqs0 = m->reqs.size(), names0 = m->pf_names.size();
+    const bool dev_in_sync = m->d_pods_synced == pods0 && (size_t)m->d_pods.n_pods == pods0 && m->d_terms_synced == terms0 &&
+                             (size_t)m->d_pods.n_reqs == reqs0 && (size_t)m->d_pods.n_names == names0;
     m->add_placed_batch(t, h_order, nodes_out, n, out_pod_id, fb);    // the walk flushed its rows to d_hot
+    // the new mirror records are the podset's records: gathered on the device instead of
+    // crossing PCIe at the next sync (only when no selector tables had to be re-based)
+    if (s && dev_in_sync && placed > 0 && m->pods.size() == pods0 + (size_t)placed && m->terms.size() == terms0 &&
+        m->reqs.size() == reqs0 && m->pf_names.size() == names0 && !getenv("CASIM_NO_POD_GATHER")) {
+        std::vector<int32_t> src;
+        src.reserve((size_t)placed);
+        for (int32_t k = 0; k < n; k++)
+            if (nodes_out[k] >= 0) src.push_back(h_order[k]);
+        if ((rc = m->d_pods.append_gather(s->t, src.data(), placed, fo.gather_idx, m->stream)) != CA_OK) return rc;
+        m->d_pods_synced = m->pods.size();
+    }
     *last_index = hctl->L;
     if (evals) *evals += hctl->evals;
     if (n_overflowing) *n_overflowing = hctl->overflowing;

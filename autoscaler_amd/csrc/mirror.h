@@ -45,6 +45,9 @@ struct DevPodTable {
     // tables only grow between Clear()s), keeping what is on the device
     int append(const ca_pod_spec* new_pods, int32_t k, const ca_selector_term* terms, int32_t nt,
                const ca_selector_req* reqs, int32_t nr, const int32_t* names, int32_t nn, hipStream_t st);
+    // append src's records idx[0..k) (already on the device: a podset), in order; the
+    // records must hold no selector-table or PreFilter-name references
+    int append_gather(const DevPodTable& src, const int32_t* idx, int32_t k, DevBuf& d_idx, hipStream_t st);
 };
 
 // Per-mirror scratch of ca_find_nodes_to_remove, kept across calls (no per-call
@@ -74,6 +77,7 @@ struct FilterScratch {
     DevBuf in, zero, out;          // inputs (order, hints, class tables), zeroed state, outputs
     HostBuf h_in, h_out;
     DevPodTable pods;              // the pending table when the caller passes no podset
+    DevBuf gather_idx;             // podset indices of the placed pods (mirror records gathered on the device)
     float kernel_ms = 0, total_ms = 0;
     int32_t phases = 0, steps = 0, ring_scans = 0, windows = 0;
     float seq_share = 0, walk_cycles_per_pod = 0;   // CASIM_PROF builds: sequencer walk share, cycles/pod

@@ -248,6 +248,36 @@ int DevPodTable::append(const ca_pod_spec* np, int32_t k, const ca_selector_term
     return CA_OK;
 }
 
+__global__ void __launch_bounds__(256) k_gather_pods(const PodHot* __restrict__ sh, const ca_pod_spec* __restrict__ ss,
+                                                     const int32_t* __restrict__ idx, int32_t k, int32_t n0,
+                                                     PodHot* __restrict__ dh, ca_pod_spec* __restrict__ ds) {
+    const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= k) return;
+    const int32_t j = idx[i];
+    PodHot h = sh[j];
+    h.spec = n0 + i;
+    dh[n0 + i] = h;
+    ds[n0 + i] = ss[j];
+}
+
+int DevPodTable::append_gather(const DevPodTable& src, const int32_t* idx, int32_t k, DevBuf& d_idx, hipStream_t st) {
+    const int32_t n0 = n_pods, n = n_pods + k;
+    int rc;
+    if ((rc = hot.reserve_keep(sizeof(PodHot) * (size_t)(n + 1), st)) != CA_OK) return rc;
+    if ((rc = spec.reserve_keep(sizeof(ca_pod_spec) * (size_t)(n + 1), st)) != CA_OK) return rc;
+    if (k > 0) {
+        if ((rc = d_idx.reserve(sizeof(int32_t) * (size_t)k)) != CA_OK) return rc;
+        CA_HIP_CHECK(hipMemcpyAsync(d_idx.ptr, idx, sizeof(int32_t) * (size_t)k, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_gather_pods, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, st, src.hot.as<const PodHot>(),
+                           src.spec.as<const ca_pod_spec>(), d_idx.as<const int32_t>(), k, n0, hot.as<PodHot>(),
+                           spec.as<ca_pod_spec>());
+        CA_HIP_CHECK(hipGetLastError());
+        CA_HIP_CHECK(hipStreamSynchronize(st));          // (idx is the caller's pageable memory)
+    }
+    n_pods = n;
+    return CA_OK;
+}
+
 // a dirty row staged for sync_nodes
 struct alignas(16) StagedRow {
     int32_t row, pad[3];

@@ -80,9 +80,11 @@ def test_filter_c5(cfg, taints, path, oracle_lib, monkeypatch):
     g.close()
 
 
-def test_filter_fork_revert(oracle_lib):
-    """Placements land on the current fork level: Revert drops them (delta.go)."""
-    w = W.c5_filter(n_nodes=1000, pods_per_node=20, n_pending=3000)
+@pytest.mark.parametrize("n_nodes,n_pending", [(1000, 3000), (4000, 12000)])
+def test_filter_fork_revert(n_nodes, n_pending, oracle_lib):
+    """Placements land on the current fork level: Revert drops them (delta.go).  The larger
+    case applies its placements to the host rows on several threads (add_placed_batch)."""
+    w = W.c5_filter(n_nodes=n_nodes, pods_per_node=20, n_pending=n_pending)
     g, o = native.Mirror(0), oracle_lib.OracleState()
     for b in (g, o):
         W.load_filter(b, w)

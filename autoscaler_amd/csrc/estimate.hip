@@ -477,7 +477,8 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
                                                      uint32_t* __restrict__ sorted, uint64_t* __restrict__ gE,
                                                      uint64_t* __restrict__ xs_all, pdq::Frame* __restrict__ stack_all,
                                                      int32_t lds_n, int32_t force, int32_t limit0, const int32_t* __restrict__ gmap,
-                                                     int32_t* __restrict__ ids_out, int32_t* __restrict__ ids_ready) {
+                                                     int32_t* __restrict__ ids_out, int32_t* __restrict__ ids_ready,
+                                                     int32_t ids_epoch) {
     extern __shared__ __align__(16) unsigned char pdq_dyn[];
     __shared__ pdq::Ctl ctl;
     const int gi = GSEL(blockIdx.x);
@@ -541,7 +542,7 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
         __syncthreads();
         if (tid == 0) {
             __threadfence();
-            __hip_atomic_store(&ids_ready[gi], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ids_ready[gi], ids_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -1011,10 +1012,10 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
                                                 int32_t* __restrict__ qctl, int32_t total, int32_t nsub,
                                                 const int2* __restrict__ prog, int32_t pch,
                                                 T* pub,              // pub may alias sched_dev (device results)
-                                                uint64_t start_ticks, const int32_t* ids_ready) {
+                                                uint64_t start_ticks, const int32_t* ids_ready, int32_t ids_epoch) {
     // ids_ready != null (decoupled Go order): the stream's pod ids in spod
     // come from a sort that runs beside the chains — a group's are final once
-    // ids_ready[g] is set — and the chains' single placements are stream positions
+    // ids_ready[g] holds this run's epoch — and the chains' single placements are stream positions
     __shared__ int32_t s_t, s_seg0;
     __shared__ int64_t s_tk;
     for (;;) {
@@ -1039,7 +1040,7 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
                 if (tk >= 0 && ids_ready) {                  // the group's Go-order ids
                     const int32_t g = (int32_t)(uint32_t)(tk & 0xFFFFFFFFll) / nsub;
                     for (;;) {
-                        if (__hip_atomic_load(&ids_ready[g], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) break;
+                        if (__hip_atomic_load(&ids_ready[g], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == ids_epoch) break;
                         if (__hip_atomic_load(&qctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { tk = -1; break; }
                         if (wall_clock64() - t0 > 20000000ull) {                            // 200 ms
                             __hip_atomic_store(&qctl[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1964,8 +1965,9 @@ struct ca_estimate_plan {
     DevBuf d_pdq_e, d_pdq_scr, d_pdq_stack, d_item_rank;
     // decoupled Go order (uniform classes): the chains run on the stable class order while
     // k_pdq_sort on st3 writes the Go-order ids into d_spod_go (d_sortC: the
-    // permutation; d_ids_ready: per group, set when its ids are final)
+    // permutation; d_ids_ready: per group, the run epoch whose ids are final there)
     DevBuf d_sortC, d_ids_ready, d_spod_go, d_crank2;
+    int32_t ids_epoch = 0;
     hipStream_t st3 = nullptr;
     hipEvent_t ev_emitA = nullptr, ev_emitB = nullptr, ev_ids = nullptr;
     // HBM-slab rows (k_ffd_chain<true>): per group kcap and slab offset, for the limiter
@@ -2152,6 +2154,8 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
         if ((rc = p->d_sortC.reserve(sizeof(uint32_t) * tot)) != CA_OK) return rc;
         if ((rc = p->d_spod_go.reserve(sizeof(int32_t) * tot)) != CA_OK) return rc;
         if ((rc = p->d_ids_ready.reserve(sizeof(int32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
+        CA_HIP_CHECK(hipMemset(p->d_ids_ready.ptr, 0, sizeof(int32_t) * (size_t)std::max(G, 1)));   // epoch 0: none
+        p->ids_epoch = 0;
         if ((rc = p->d_crank2.reserve(sizeof(int32_t) * (size_t)std::max(G, 1) * (size_t)std::max(s->n_cls, 1))) != CA_OK)
             return rc;
     }
@@ -2206,7 +2210,7 @@ bool go_sort_order() {
 // or from item_rank
 int launch_pdq_sort(ca_estimate_plan* p, hipStream_t ss, const int32_t* gm, int32_t ng, const int32_t* crank,
                     int32_t U, const uint32_t* item_rank, int32_t force = 0, uint32_t* out = nullptr,
-                    int32_t* ids_out = nullptr, int32_t* ids_ready = nullptr) {
+                    int32_t* ids_out = nullptr, int32_t* ids_ready = nullptr, int32_t ids_epoch = 0) {
     const int32_t lds_n = std::min(p->max_count, PDQ_LDS_N);
     const size_t lds = pdq_lds_bytes(lds_n);
     int rc;
@@ -2214,7 +2218,7 @@ int launch_pdq_sort(ca_estimate_plan* p, hipStream_t ss, const int32_t* gm, int3
     hipLaunchKernelGGL(k_pdq_sort, dim3(ng), dim3(pdq::NT), lds, ss, p->d_meta.as<GroupMeta>(),
                        p->d_pod_idx.as<int32_t>(), p->s ? p->s->d_cls.as<int32_t>() : nullptr, crank, U, item_rank,
                        out ? out : p->d_sortA.as<uint32_t>(), p->d_pdq_e.as<uint64_t>(), p->d_pdq_scr.as<uint64_t>(),
-                       p->d_pdq_stack.as<pdq::Frame>(), lds_n, force, 0, gm, ids_out, ids_ready);
+                       p->d_pdq_stack.as<pdq::Frame>(), lds_n, force, 0, gm, ids_out, ids_ready, ids_epoch);
     CA_HIP_CHECK(hipGetLastError());
     return CA_OK;
 }
@@ -2305,6 +2309,36 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     int32_t tickets1 = 0;                               // publisher tickets of round 1 (every group)
     if (publish)
         for (int32_t g = 0; g < G; g++) tickets1 += (p->h_meta[g].count + p->pch - 1) / p->pch;
+    // decoupled Go order (uniform classes, bucket path): chains on the stable order, Go's ids
+    // beside them (CASIM_GO_DECOUPLE=0: the Go sort ahead of the stream, for tests)
+    const bool go_order = go_sort_order();
+    const bool decoupled = go_order && p->bucket && p->s && p->s->cls_uniform && p->total > 0 &&
+                           !(getenv("CASIM_GO_DECOUPLE") && atoi(getenv("CASIM_GO_DECOUPLE")) == 0);
+    if (decoupled) {
+        // Go's sort.Slice permutation of every group and its pod ids, on st3 before anything
+        // else is queued (it bounds when the publisher can start): its own class ranks,
+        // k_pdq_sort, ids into d_spod_go and per-group ready flags holding this run's epoch
+        // (no reset between runs; every run is synchronised before it returns).  The chains
+        // meanwhile run on the stable class order (same class at every position).
+        const int32_t U = p->s->n_cls;
+        int32_t NP = 1;
+        while (NP < U) NP <<= 1;
+        if (p->ids_epoch == INT32_MAX) {                  // (wrapped: start over from a clean table)
+            CA_HIP_CHECK(hipMemsetAsync(p->d_ids_ready.ptr, 0, sizeof(int32_t) * (size_t)G, p->st3));
+            p->ids_epoch = 0;
+        }
+        p->ids_epoch++;
+        hipLaunchKernelGGL(k_class_rank, dim3(G), dim3(1024), 0, p->st3, p->d_meta.as<GroupMeta>(),
+                           p->d_tmpl.as<ca_template>(), p->s->d_cls_sc.as<int64_t>(), U, NP,
+                           p->d_crank2.as<int32_t>(), (const int32_t*)nullptr);
+        CA_HIP_CHECK(hipGetLastError());
+        int rc0;
+        if ((rc0 = launch_pdq_sort(p, p->st3, nullptr, G, p->d_crank2.as<int32_t>(), U, nullptr, 0,
+                                   p->d_sortC.as<uint32_t>(), p->d_spod_go.as<int32_t>(),
+                                   p->d_ids_ready.as<int32_t>(), p->ids_epoch)) != CA_OK)
+            return rc0;
+        CA_HIP_CHECK(hipEventRecord(p->ev_ids, p->st3));
+    }
     CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_START], st));
     {
         const int32_t n = std::max(G, tickets1);
@@ -2362,11 +2396,6 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         gmapB = gmapA + p->n_heavy;
     }
     const int32_t nA = split ? p->n_heavy : G, nB = split ? G - p->n_heavy : 0;
-    const bool go_order = go_sort_order();
-    // decoupled Go order (uniform classes, bucket path): chains on the stable order, Go's ids
-    // beside them (CASIM_GO_DECOUPLE=0: the Go sort ahead of the stream, for tests)
-    const bool decoupled = go_order && p->bucket && p->s && p->s->cls_uniform && p->total > 0 &&
-                           !(getenv("CASIM_GO_DECOUPLE") && atoi(getenv("CASIM_GO_DECOUPLE")) == 0);
     // where the consumers (publisher, segment copies) read the stream's pod ids
     const int32_t* const ids_src = decoupled ? p->d_spod_go.as<int32_t>() : p->d_spod.as<int32_t>();
     std::function<int()> sort_light;        // split: the light groups' sort, queued after the heavy chains
@@ -2381,25 +2410,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         while (nb < U) { nb <<= 8; passes++; }
         passes = std::max(passes, 1);
         const int32_t passes_run = (go_order && !decoupled) ? 0 : passes;
-        if (decoupled) {
-            // Go's sort.Slice permutation of every group and its pod ids, on st3 from the start:
-            // its own class ranks, k_pdq_sort, ids into d_spod_go + per-group ready flags.  The
-            // chains meanwhile run on the stable class order (same class at every position).
-            CA_HIP_CHECK(hipMemsetAsync(p->d_ids_ready.ptr, 0, sizeof(int32_t) * (size_t)G, st));
-            CA_HIP_CHECK(hipEventRecord(p->ev_emitA, st));
-            CA_HIP_CHECK(hipStreamWaitEvent(p->st3, p->ev_emitA, 0));
-            hipLaunchKernelGGL(k_class_rank, dim3(G), dim3(1024), 0, p->st3, p->d_meta.as<GroupMeta>(),
-                               p->d_tmpl.as<ca_template>(), p->s->d_cls_sc.as<int64_t>(), U, NP,
-                               p->d_crank2.as<int32_t>(), (const int32_t*)nullptr);
-            CA_HIP_CHECK(hipGetLastError());
-            int rc0;
-            // (the sort writes each group's ids and sets its ready flag as it finishes)
-            if ((rc0 = launch_pdq_sort(p, p->st3, nullptr, G, p->d_crank2.as<int32_t>(), U, nullptr, 0,
-                                       p->d_sortC.as<uint32_t>(), p->d_spod_go.as<int32_t>(),
-                                       p->d_ids_ready.as<int32_t>())) != CA_OK)
-                return rc0;
-            CA_HIP_CHECK(hipEventRecord(p->ev_ids, p->st3));
-        }
+
         const int32_t blocks = (p->max_count + 255) / 256;
         // class ranks, then Go's pdqsort (default) or the stable LSD radix passes, stream
         // emission for `ng` groups (map `gm`)
@@ -2526,13 +2537,13 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                    ids_src, p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int64_t>(),
                                    p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
                                    reinterpret_cast<uint16_t*>(publish), pub_start_ticks(),
-                                   decoupled ? p->d_ids_ready.as<int32_t>() : nullptr);
+                                   decoupled ? p->d_ids_ready.as<int32_t>() : nullptr, p->ids_epoch);
             else
                 hipLaunchKernelGGL(k_publish<int32_t>, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, ps,
                                    p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
                                    ids_src, p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int64_t>(),
                                    p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
-                                   publish, pub_start_ticks(), decoupled ? p->d_ids_ready.as<int32_t>() : nullptr);
+                                   publish, pub_start_ticks(), decoupled ? p->d_ids_ready.as<int32_t>() : nullptr, p->ids_epoch);
             CA_HIP_CHECK(hipGetLastError());
             return CA_OK;
         };
@@ -2863,7 +2874,7 @@ int ca_go_sort_ranks(int32_t device, const uint32_t* ranks, int32_t n, int32_t s
     if ((rc = ensure_dyn_lds((const void*)k_pdq_sort, lds)) != CA_OK) return rc;
     hipLaunchKernelGGL(k_pdq_sort, dim3(1), dim3(pdq::NT), lds, 0, meta.as<GroupMeta>(), nullptr, nullptr, nullptr, 0,
                        rk.as<uint32_t>(), sorted.as<uint32_t>(), e.as<uint64_t>(), scr.as<uint64_t>(),
-                       stack.as<pdq::Frame>(), lds_n, store, std::max(limit, 0), nullptr, nullptr, nullptr);
+                       stack.as<pdq::Frame>(), lds_n, store, std::max(limit, 0), nullptr, nullptr, nullptr, 0);
     CA_HIP_CHECK(hipGetLastError());
     CA_HIP_CHECK(hipMemcpy(perm, sorted.ptr, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost));
     return CA_OK;

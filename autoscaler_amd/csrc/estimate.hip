@@ -960,6 +960,7 @@ __device__ inline int32_t run_end_pf(const uint64_t* __restrict__ hm, int32_t po
 // chain's critical path.  Other chunks (single placements, a segment boundary with another
 // offset, the group's tail) go with the release and the progress record.
 constexpr int PCH = 4096;      // default chunk (CASIM_PUB_CHUNK overrides, for tests)
+constexpr int PCH_DECOUPLED = 16384;   // ... with the decoupled Go order (scripts/pub_sweep.sh)
 __device__ inline void push_chunks(int32_t g, int32_t c0, int32_t c1, int32_t nsub, int64_t* tickets, int32_t* qctl,
                                    int2* prog, int32_t nseg, int32_t nsched, int lane, int32_t pch = 0,
                                    int32_t pure_from = INT32_MAX, int32_t pure_off = 0) {
@@ -2124,7 +2125,11 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     if ((rc = p->d_heads.reserve(sizeof(uint64_t) * (size_t)std::max(p->n_masks, 1))) != CA_OK) return rc;
     if ((rc = p->d_spod.reserve(sizeof(int32_t) * tot)) != CA_OK) return rc;
     if ((rc = p->d_seg.reserve(sizeof(Seg) * tot)) != CA_OK) return rc;
-    p->pch = PCH;
+    {
+        const char* so = getenv("CASIM_SORT_ORDER");                 // (go_sort_order(), below)
+        const bool go_ord = !(so && strcmp(so, "stable") == 0);
+        p->pch = (p->bucket && s && s->cls_uniform && go_ord) ? PCH_DECOUPLED : PCH;
+    }
     if (const char* e = getenv("CASIM_PUB_CHUNK")) p->pch = std::max(1, atoi(e));
     const int32_t pch = p->pch;
     p->n_tickets = 0;
@@ -2223,9 +2228,11 @@ int launch_pdq_sort(ca_estimate_plan* p, hipStream_t ss, const int32_t* gm, int3
     return CA_OK;
 }
 
-int32_t pub_blocks() {
+int32_t pub_blocks(bool decoupled) {
     const char* e = getenv("CASIM_PUB_BLOCKS");
-    return e ? std::max(1, atoi(e)) : 32;        // scripts/pub_sweep.sh: 32 x 4096-output chunks on C2
+    // scripts/pub_sweep.sh on C2: stable order 32 x 4096-output chunks; decoupled Go order
+    // (the ids arrive ~0.3 ms into the step, then the link is the bound) 64 x 16384
+    return e ? std::max(1, atoi(e)) : (decoupled ? 64 : 32);
 }
 
 size_t chain_lds_bytes(int32_t kcap, bool use_ports, bool use_scalar) {
@@ -2532,14 +2539,14 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         // the two kernels are serialised — it must give up at its start deadline
         auto launch_pub = [&](hipStream_t ps) -> int {
             if (sched16)
-                hipLaunchKernelGGL(k_publish<uint16_t>, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, ps,
+                hipLaunchKernelGGL(k_publish<uint16_t>, dim3(std::min(round_tickets, pub_blocks(decoupled))), dim3(256), 0, ps,
                                    p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
                                    ids_src, p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int64_t>(),
                                    p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
                                    reinterpret_cast<uint16_t*>(publish), pub_start_ticks(),
                                    decoupled ? p->d_ids_ready.as<int32_t>() : nullptr, p->ids_epoch);
             else
-                hipLaunchKernelGGL(k_publish<int32_t>, dim3(std::min(round_tickets, pub_blocks())), dim3(256), 0, ps,
+                hipLaunchKernelGGL(k_publish<int32_t>, dim3(std::min(round_tickets, pub_blocks(decoupled))), dim3(256), 0, ps,
                                    p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
                                    ids_src, p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int64_t>(),
                                    p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,

@@ -1589,7 +1589,22 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
             const int32_t S0 = (int32_t)fb_shapes.size();
             std::vector<uint8_t> alive((size_t)S0, 0);
             std::vector<int32_t> open;
-            for (int32_t q = 0; q < S0; q++) open.push_back(q);
+            // shapes beyond the largest free cpu / memory / ephemeral of any node with a free
+            // pod slot fit no node: dead without the node walk below (RunOnce's backlog of
+            // variants too large for every node would otherwise walk all nodes each)
+            int64_t mx_c = INT64_MIN, mx_m = INT64_MIN, mx_e = INT64_MIN;
+            for (const NodeRow& nd : m->nodes) {
+                if (clamp_i32(nd.spec.alloc_pods - nd.npods) < 1) continue;
+                mx_c = std::max(mx_c, wsub(nd.spec.alloc_milli_cpu, nd.req_cpu));
+                mx_m = std::max(mx_m, wsub(nd.spec.alloc_memory, nd.req_mem));
+                mx_e = std::max(mx_e, wsub(nd.spec.alloc_ephemeral, nd.req_eph));
+            }
+            for (int32_t q = 0; q < S0; q++) {
+                const FbShape& sh = fb_shapes[q];
+                if (mx_c == INT64_MIN) continue;                               // no node has a slot
+                if (!(sh.flags & PF_ALL_ZERO) && (sh.cpu > mx_c || sh.mem > mx_m || sh.eph > mx_e)) continue;
+                open.push_back(q);
+            }
             for (size_t i = 0; i < m->nodes.size() && !open.empty(); i++) {
                 // the free resources of fill_hot, without its port / scalar flag scans (a
                 // shape that fits no node walks every node here)
@@ -1607,7 +1622,9 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
                     }
                 }
             }
-            if (!open.empty()) {
+            bool any_dead = false;
+            for (int32_t q = 0; q < S0; q++) any_dead |= !alive[q];
+            if (any_dead) {
                 std::vector<int32_t> remap((size_t)S0, -1);
                 std::vector<FbShape> live;
                 for (int32_t q = 0; q < S0; q++)
@@ -1621,7 +1638,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
                 fb_shapes.swap(live);
             }
             // the live shapes take the bit-update lanes; the dead row (last) needs none
-            const int32_t live = (int32_t)fb_shapes.size() - (open.empty() ? 0 : 1);
+            const int32_t live = (int32_t)fb_shapes.size() - (any_dead ? 1 : 0);
             if (live > FB_MAX_SHAPES) fb = false;
         }
         // LDS: shapes, bitmaps, vis prefix counts, run scratch and the similar-pods state,

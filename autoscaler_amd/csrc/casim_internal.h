@@ -17,6 +17,7 @@
 #include <stdint.h>
 #include <vector>
 #include <string>
+#include <cstdlib>
 #include "../../include/casim.h"
 
 namespace casim {
@@ -199,6 +200,12 @@ __host__ __device__ inline uint32_t dev_fit_reasons(int64_t pcpu, int64_t pmem, 
     } while (0)
 
 void set_last_error(const std::string& s);
+// Fault-injection / trace hooks for tests and diagnosis scripts: the variable is read only
+// when CASIM_TEST_HOOKS is set as well, so one stray variable cannot change a production
+// call's behaviour.
+inline const char* test_hook_env(const char* name) {
+    return getenv("CASIM_TEST_HOOKS") ? getenv(name) : nullptr;
+}
 const std::string& last_error();
 
 // hipFuncAttributeMaxDynamicSharedMemorySize of a kernel, raised to `bytes` at most once

@@ -1977,6 +1977,9 @@ struct ca_estimate_plan {
     int32_t slab_max_nodes = -2;
     int32_t n_hist = 0, max_rtiles = 0;
     bool bucket = false;           // bucket sort over score classes (podset has <= CLS_MAX classes)
+    // decoupled Go order allowed: uniform classes, bucket path, and no
+    // group holds two classes whose float64 scores against its template are equal
+    bool decouple_ok = false;
     Stats stats;
     // per-phase device timings of the last run (ms): score, merge, emit, chain (all
     // rounds), compact, d2h; and the host wall time of the call
@@ -1984,6 +1987,7 @@ struct ca_estimate_plan {
     hipEvent_t ev[EV_N] = {};
     float t_ms[7] = {};
     int32_t pub_state = 0;         // last run: 0 results copied, 1 published zero-copy, 2 publisher gave up
+    int32_t ran_decoupled = 0;     // last run took the decoupled Go order
     std::vector<uint64_t> diag;     // per group: chain ticks (100 MHz) | single-pod steps << 32
     std::vector<uint8_t> grp_succ;  // last run, per group: a FitsAnyNode call succeeded (moved lastIndex)
     // zero-copy publishing (k_publish on its own stream, concurrent with the chains)
@@ -2023,6 +2027,53 @@ struct ca_estimate_plan {
 };
 
 namespace {
+
+// The decoupled Go order runs the chains on the stable class order and takes the pod ids
+// from Go's sort.Slice permutation at the same positions.  That is exact only if both
+// orders hold the same class at every sorted position of a group: k_class_rank gives two
+// classes with equal float64 scores one dense rank, and pdqsort interleaves their pods
+// differently from list position.  So: no group may hold two classes of one score
+// (binpacking_estimator.go:72-74, 164-193; same float64 operations as k_class_rank,
+// -ffp-contract=off).  Per group, the U class scores against the template are sorted;
+// only when a tie exists are the group's own classes looked up.
+bool groups_tie_free(const ca_podset* s, const int32_t* pod_idx, const std::vector<GroupMeta>& meta,
+                     const ca_template* templates) {
+    const int32_t U = s->n_cls;
+    if (U < 2) return true;
+    std::vector<std::pair<uint64_t, int32_t>> key((size_t)U);
+    std::vector<int32_t> seen((size_t)U, -1);
+    std::vector<int32_t> runs;                        // classes of tied runs, -1 between runs
+    for (size_t g = 0; g < meta.size(); g++) {
+        const ca_template& tp = templates[meta[g].tmpl];
+        const int64_t acpu = tp.node.alloc_milli_cpu, amem = tp.node.alloc_memory;
+        for (int32_t c = 0; c < U; c++) {
+            double score = 0.0;
+            if (acpu > 0) score += (double)s->h_cls_sc[2 * c] / (double)acpu;
+            if (amem > 0) score += (double)s->h_cls_sc[2 * c + 1] / (double)amem;
+            uint64_t b;
+            std::memcpy(&b, &score, sizeof b);
+            key[c] = {b, c};
+        }
+        std::sort(key.begin(), key.end());
+        runs.clear();
+        for (int32_t i = 1; i < U; i++) {
+            if (key[i].first != key[i - 1].first) continue;
+            if (runs.empty() || runs.back() != key[i - 1].second) {
+                if (!runs.empty()) runs.push_back(-1);
+                runs.push_back(key[i - 1].second);
+            }
+            runs.push_back(key[i].second);
+        }
+        if (runs.empty()) continue;
+        for (int32_t i = meta[g].off; i < meta[g].off + meta[g].count; i++) seen[s->h_cls[pod_idx[i]]] = (int32_t)g;
+        int32_t present = 0;
+        for (size_t i = 0; i <= runs.size(); i++) {
+            if (i == runs.size() || runs[i] < 0) { present = 0; continue; }
+            if (seen[runs[i]] == (int32_t)g && ++present >= 2) return false;
+        }
+    }
+    return true;
+}
 
 int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const int32_t* group_off,
                  const int32_t* pod_idx, const ca_template* templates, int32_t G) {
@@ -2099,6 +2150,7 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
         if (f & PF_PORTS) p->use_ports = true;
         if (f & PF_SCALAR_REQ) p->use_scalar = true;
     }
+    p->decouple_ok = p->bucket && s->cls_uniform && groups_tie_free(s, pod_idx, p->h_meta, templates);
     p->demand.assign(G, 0.0);
     for (int32_t g = 0; g < G; g++) {
         const GroupMeta& gm = p->h_meta[g];
@@ -2128,7 +2180,7 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     {
         const char* so = getenv("CASIM_SORT_ORDER");                 // (go_sort_order(), below)
         const bool go_ord = !(so && strcmp(so, "stable") == 0);
-        p->pch = (p->bucket && s && s->cls_uniform && go_ord) ? PCH_DECOUPLED : PCH;
+        p->pch = (p->decouple_ok && go_ord) ? PCH_DECOUPLED : PCH;
     }
     if (const char* e = getenv("CASIM_PUB_CHUNK")) p->pch = std::max(1, atoi(e));
     const int32_t pch = p->pch;
@@ -2155,7 +2207,7 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     if ((rc = p->d_pdq_stack.reserve(sizeof(pdq::Frame) * (tot / 2 + 2 * (size_t)std::max(G, 1) + 2))) != CA_OK)
         return rc;
     if (!p->bucket && (rc = p->d_item_rank.reserve(sizeof(uint32_t) * tot)) != CA_OK) return rc;
-    if (p->bucket && s->cls_uniform) {
+    if (p->decouple_ok) {
         if ((rc = p->d_sortC.reserve(sizeof(uint32_t) * tot)) != CA_OK) return rc;
         if ((rc = p->d_spod_go.reserve(sizeof(int32_t) * tot)) != CA_OK) return rc;
         if ((rc = p->d_ids_ready.reserve(sizeof(int32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
@@ -2319,8 +2371,9 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     // decoupled Go order (uniform classes, bucket path): chains on the stable order, Go's ids
     // beside them (CASIM_GO_DECOUPLE=0: the Go sort ahead of the stream, for tests)
     const bool go_order = go_sort_order();
-    const bool decoupled = go_order && p->bucket && p->s && p->s->cls_uniform && p->total > 0 &&
+    const bool decoupled = go_order && p->decouple_ok && p->total > 0 &&
                            !(getenv("CASIM_GO_DECOUPLE") && atoi(getenv("CASIM_GO_DECOUPLE")) == 0);
+    p->ran_decoupled = decoupled ? 1 : 0;
     if (decoupled) {
         // Go's sort.Slice permutation of every group and its pod ids, on st3 before anything
         // else is queued (it bounds when the publisher can start): its own class ranks,
@@ -2829,9 +2882,10 @@ int ca_estimate_plan_stats(const ca_estimate_plan* p, int32_t* rounds, float* ch
 
 int ca_estimate_plan_timings(const ca_estimate_plan* p, float* out, int32_t cap) {
     if (!p || (cap > 0 && !out)) return CA_EINVAL;
-    const int32_t n = 8;
+    const int32_t n = 9;
     for (int32_t i = 0; i < 7 && i < cap; i++) out[i] = p->t_ms[i];
     if (cap > 7) out[7] = (float)p->pub_state;
+    if (cap > 8) out[8] = (float)p->ran_decoupled;
     return n;
 }
 

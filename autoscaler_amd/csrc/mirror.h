@@ -90,6 +90,13 @@ struct FilterScratch {
     int32_t fb_stat_lds = 0;                // bitmap walk: static words in LDS
 };
 
+// Per-mirror scratch of the planner's device chain (plan_chain.hip), freed with the mirror
+// and allocated on its device.
+struct PlanChainScratch {
+    DevBuf in, work, out;
+    HostBuf h_in, h_out;
+};
+
 // Dirty-row staging of sync_nodes: one H2D copy + a scatter kernel.
 struct RowStage {
     DevBuf d;
@@ -189,6 +196,7 @@ struct ca_mirror {
     casim::PlanStats plan;
     casim::SweepScratch sw;
     casim::FilterScratch fo;
+    casim::PlanChainScratch pc;
     casim::RowStage rs;
     // resident HintingSimulator hints (hints.go:29-72): node per mirror pod, -1 = none
     casim::DevBuf d_pod_hints;
@@ -229,8 +237,12 @@ struct ca_podset {
     // score_memory}.  Used by the Estimate bucket sort (estimate.hip).
     int32_t n_cls = 0;
     casim::DevBuf d_cls, d_cls_sc;
+    std::vector<int32_t> h_cls;        // host copies: class per pod, {cpu, memory} per class
+    std::vector<int64_t> h_cls_sc;
     // every class's pods carry identical records apart from their controller
     // (similar_class): interchangeable for the FFD chain, so Estimate can run the chain on
     // the stable class order while Go's sort.Slice order of their ids is computed beside it
+    // — provided no two classes of a group tie on their float64 score against the group's
+    // template (checked per plan: ca_estimate_plan::decouple_ok)
     bool cls_uniform = false;
 };

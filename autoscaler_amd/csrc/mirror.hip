@@ -1159,6 +1159,8 @@ int ca_podset_create(ca_mirror* m, const ca_pod_table* t, ca_podset** out) {
             }
             s->cls_uniform = uni;
         }
+        s->h_cls = cls;
+        s->h_cls_sc = sc;
         if ((rc = s->d_cls.reserve(sizeof(int32_t) * (cls.size() + 1))) != CA_OK ||
             (rc = s->d_cls_sc.reserve(sizeof(int64_t) * (sc.size() + 2))) != CA_OK) { delete s; return rc; }
         if (!cls.empty())

@@ -904,22 +904,6 @@ using namespace casim;
 
 namespace casim {
 
-// Per-mirror scratch of the chain (kept across calls).
-struct PlanChainScratch {
-    DevBuf in, work, out;
-    HostBuf h_in, h_out;
-};
-
-static PlanChainScratch& chain_scratch(ca_mirror* m) {
-    // one per mirror handle; the mirror owns none of it beyond the call (freed with the
-    // process-wide allocation cache)
-    static thread_local std::vector<std::pair<const ca_mirror*, PlanChainScratch*>> tab;
-    for (auto& e : tab)
-        if (e.first == m) return *e.second;
-    tab.push_back({m, new PlanChainScratch()});
-    return *tab.back().second;
-}
-
 // 1 = ran, 0 = outside the chain's scope (the caller takes the speculative path), < 0 error.
 // *last_index is an out-value only (the caller passes a copy); hints come back in hints_out.
 int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uint8_t* dest_mask,
@@ -974,7 +958,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     // the chain reads the device records of the caller's pods only (copies it packs itself)
     if (m->d_pods_synced < (size_t)n_pods && (rc = m->sync_pods()) != CA_OK) return rc;
     const auto t_sync = std::chrono::steady_clock::now();
-    PlanChainScratch& S = chain_scratch(m);
+    PlanChainScratch& S = m->pc;
     hipStream_t st = m->stream;
 
     // packed inputs (one H2D): cands, status, move_off, move_pods, ex_base, pdb tables, hints; mask
@@ -1059,8 +1043,8 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     A.copy_cap = copy_cap;
     A.trace = nullptr;
     A.trace_cap = 0;
-    A.dbg = getenv("CASIM_PLAN_DBG") ? atoi(getenv("CASIM_PLAN_DBG")) : 0;
-    const char* tr_env = getenv("CASIM_PLAN_TRACE");
+    A.dbg = test_hook_env("CASIM_PLAN_DBG") ? atoi(test_hook_env("CASIM_PLAN_DBG")) : 0;
+    const char* tr_env = test_hook_env("CASIM_PLAN_TRACE");
     DevBuf trace;
     if (tr_env) {
         A.trace_cap = 4096;

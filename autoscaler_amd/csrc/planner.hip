@@ -145,7 +145,7 @@ int plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const uint
         return CA_OK;
     }
     if (m->n_scope_blockers > 0) return CA_EUNSUPPORTED;                         // casim.h scope
-    const char* fail_env = getenv("CASIM_PLAN_FAIL_ROUND");          // tests: an error in that round
+    const char* fail_env = test_hook_env("CASIM_PLAN_FAIL_ROUND");          // tests: an error in that round
     const int32_t fail_round = fail_env ? atoi(fail_env) : 0;
     {
         // the device-resident chain (plan_chain.hip); the speculative windows below otherwise
@@ -193,7 +193,7 @@ int plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const uint
     int32_t removed = 0;
     int32_t i = 0;
     int32_t W = std::min(C, 256);
-    if (const char* e = getenv("CASIM_PLAN_WINDOW")) W = std::max(1, std::min(C, atoi(e)));   // tests
+    if (const char* e = test_hook_env("CASIM_PLAN_WINDOW")) W = std::max(1, std::min(C, atoi(e)));   // tests
     std::vector<int32_t> w_off, w_pods, w_status, w_dest, Hs;
     std::vector<ca_removal_result> w_res;
     std::vector<Own> own;
@@ -401,6 +401,7 @@ int ca_plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const u
                      int32_t* last_index, ca_plan_result* results, ca_plan_move* moves, int32_t moves_cap,
                      int32_t* n_moves) {
     if (!m) return CA_EINVAL;
+    CA_HIP_CHECK(hipSetDevice(m->device));    // the chain's buffers and launches belong to the mirror's device
     std::vector<int32_t> allowed0;
     if (pdbs && pdbs->n_pdbs > 0 && pdbs->allowed) allowed0.assign(pdbs->allowed, pdbs->allowed + pdbs->n_pdbs);
     int rc = ca_mirror_fork(m);

@@ -739,13 +739,14 @@ class EstimatePlan:
         self.lib.ca_estimate_plan_stats(self.h, C.byref(r), C.byref(a), C.byref(b), C.byref(c))
         sens, succ = C.c_int32(0), C.c_int32(0)
         self.lib.ca_estimate_plan_chain_info(self.h, C.byref(sens), C.byref(succ))
-        t = (C.c_float * 8)()
-        self.lib.ca_estimate_plan_timings(self.h, t, 8)
+        t = (C.c_float * 9)()
+        self.lib.ca_estimate_plan_timings(self.h, t, 9)
         names = ("score_ms", "merge_ms", "emit_ms", "chain_ms", "compact_ms", "d2h_ms", "host_ms")
         return {"rounds": r.value, "chain_ms": a.value, "sort_ms": b.value, "total_ms": c.value,
                 "lin_sensitive": sens.value, "had_success": succ.value,
                 "phases": {k: float(v) for k, v in zip(names, t)},
-                "results_path": ("copied", "published", "publisher_gave_up")[int(t[7])]}
+                "results_path": ("copied", "published", "publisher_gave_up")[int(t[7])],
+                "decoupled": bool(t[8])}
 
     def chain_info(self) -> tuple:
         """(lastIndex-sensitive, had a FitsAnyNode success) of the last run: one call."""

@@ -109,15 +109,14 @@ def _zeros(key: str, n: int, dtype) -> np.ndarray:
     return np.zeros(n, dtype)
 
 
-def cpu_util(ui: "UtilInput", now_ns: int):
-    """The CPU port's utilization step (oracle/casim_oracle.c or_node_utilization)."""
-    import pyoracle                                   # the checker / CPU baseline only
-    return pyoracle.node_utilization(ui.nodes, ui.off, ui.pods, False, False, now_ns)
-
-
 class DeviceUtil:
     """The device's utilization step: one resident ca_util_table per loop start snapshot,
-    the pods FilterOutSchedulable added sent as ca_util_table_set_added."""
+    the pods FilterOutSchedulable added sent as ca_util_table_set_added.
+
+    The rows it returns are views into two page-locked buffers used in turn: the result of
+    call k is overwritten by call k + 2.  A caller that keeps ``RunOnceResult.util`` across
+    loops copies it (``np.copy``) first.  (The CPU port's utilization step for parity and
+    the baseline is ``pyoracle.runonce_cpu_util``, outside the package.)"""
     want = "added"
 
     def __init__(self, device: int = 0):

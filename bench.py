@@ -13,12 +13,13 @@ the zero-copy publisher streams them into page-locked memory while the chains ru
 extra.device_resident times the same step with the scheduled pods left in HBM.
 
 value = filter-chain evaluations the reference algorithm performs in that batch
-(every RunFilterPlugins call, counted exactly) / wall time.  With --gpus N the same
-100 groups are split into N contiguous blocks (strong scaling): rank 0 drives all N GPUs
-through ca_multi_estimate_plan_run, the path a cgo caller uses (one process, one host
-thread per device, the lastIndex chain fixed up in the library); with
-CASIM_BENCH_MULTI=rccl each rank runs its block and the blocks are chained through one RCCL
-all_gather of a 4-int record per rank per step.
+(every RunFilterPlugins call, counted exactly) / wall time.  With --gpus N (one process
+per GPU) the batch holds 100 x N node groups and each rank runs its own 100 (weak
+scaling: node groups are independent units coupled only through the checker's lastIndex,
+chained by one RCCL all_gather of a 4-int record per rank per step); value =
+all ranks' evaluations / the slowest rank's time.  CASIM_BENCH_SCALING=strong splits the
+same 100 groups over the N GPUs instead (rank 0 drives them through
+ca_multi_estimate_plan_run, or CASIM_BENCH_MULTI=rccl: one block per rank).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -429,7 +430,7 @@ def runonce_leg(args, device: int, with_cpu: bool) -> dict:
         import pyoracle                                           # CPU baseline leg only
         o = pyoracle.OracleState()
         W.load_filter(o, w.filt)
-        ro = runonce.run(o, runonce.cpu_util, w)
+        ro = runonce.run(o, pyoracle.runonce_cpu_util, w)
         out["cpu_ms"] = ro.ms
         out["speedup"] = {k: ro.ms[k] / out["gpu_ms"][k] for k in keys if out["gpu_ms"][k] > 0}
         out["parity"] = runonce.compare(ro, runs[-1])
@@ -556,7 +557,7 @@ def multi_main(args, world: int, rank: int, dist, coll_dev: str):
         same = bool(np.array_equal(o1.results, res) and np.array_equal(o1.sched_pod, pods)
                     and o1.last_index == out.last_index)
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:              # (rank 0 at N = 1 only)
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import pyoracle                                       # CPU baseline leg only
             o = pyoracle.OracleState()
@@ -623,6 +624,12 @@ def main():
     # rehearsal of the N>1 path on fewer GPUs (CASIM_BENCH_BACKEND=gloo: ranks share devices
     # round-robin, collectives over gloo on host tensors); the driver's runs use RCCL
     backend = os.environ.get("CASIM_BENCH_BACKEND", "nccl")
+    # N > 1: weak scaling by default — one Estimate batch of groups x N node groups, each
+    # rank its own block of `groups` groups (rank 0's block is exactly the N = 1 workload),
+    # the blocks chained through the checker's lastIndex by one all_gather of a 4-int record
+    # per rank per step (shard.py).  CASIM_BENCH_SCALING=strong: the same 100 groups split
+    # over the N GPUs (ca_multi_estimate_plan_run from rank 0, or CASIM_BENCH_MULTI=rccl).
+    scaling = os.environ.get("CASIM_BENCH_SCALING", "weak") if world > 1 else "weak"
     import torch
     dist = None
     if world > 1:
@@ -631,17 +638,24 @@ def main():
             local = local % max(1, native_device_count())
         torch.cuda.set_device(local)
         dist.init_process_group(backend)          # "nccl" is RCCL on ROCm
-        if os.environ.get("CASIM_BENCH_MULTI", "capi") != "rccl":
+        if scaling == "strong" and os.environ.get("CASIM_BENCH_MULTI", "capi") != "rccl":
             return multi_main(args, world, rank, dist, f"cuda:{local}" if backend == "nccl" else "cpu")
 
     from autoscaler_amd import native, shard
     from autoscaler_amd import workloads as W
 
-    # strong scaling: every rank holds the same cluster (the mirror is replicated) and runs
-    # its contiguous block of the same node groups; the blocks are chained through the
-    # checker's lastIndex (autoscaler_amd/shard.py)
-    w = W.c2(n_pods=args.pods, n_groups=args.groups, n_existing=args.existing, max_nodes=args.max_nodes, seed=42)
-    blocks = split_groups(w.group_off, world)
+    # every rank holds the same cluster (the mirror is replicated) and runs its contiguous
+    # block of the batch's node groups; the blocks are chained through the checker's
+    # lastIndex (autoscaler_amd/shard.py).  Weak scaling: the batch has
+    # groups x N groups (the generator draws group templates in order, so its first
+    # `groups` groups are the N = 1 batch) and rank r runs groups [r*groups, (r+1)*groups);
+    # strong scaling (rccl): the same `groups` groups in N blocks balanced by items.
+    n_groups_total = args.groups * world if scaling == "weak" else args.groups
+    w = W.c2(n_pods=args.pods, n_groups=n_groups_total, n_existing=args.existing, max_nodes=args.max_nodes, seed=42)
+    if scaling == "weak":
+        blocks = [args.groups * r for r in range(world + 1)]
+    else:
+        blocks = split_groups(w.group_off, world)
     g0, g1 = blocks[rank], blocks[rank + 1]
     off_blk = (w.group_off[g0:g1 + 1] - w.group_off[g0]).astype(np.int32)
     idx_blk = w.pod_idx[w.group_off[g0]:w.group_off[g1]]
@@ -763,7 +777,7 @@ def main():
     result = None
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:              # (rank 0 at N = 1 only)
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import pyoracle                                       # CPU baseline leg only
             o = pyoracle.OracleState()
@@ -788,7 +802,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic: seeded C2 generator (autoscaler_amd/workloads.py), 64-shape pod catalog",
@@ -796,10 +810,13 @@ def main():
                 "workload": "C2: heterogeneous pending pods x node-group templates, resource-fit only "
                             "(BASELINE.json configs[1]); one step = Estimate() for every group, every group's "
                             "node count and scheduled pods on the host",
-                "pods": args.pods, "groups": args.groups, "existing_nodes": args.existing,
+                "pods": args.pods, "groups": n_groups_total, "groups_per_gpu": g1 - g0,
+                "existing_nodes": args.existing,
                 "max_nodes_per_scaleup": args.max_nodes,
-                "parallelism": f"the {args.groups} groups in {world} contiguous block(s), one per GPU, "
-                               f"lastIndex chained by all_gather",
+                "parallelism": (f"{n_groups_total} groups = {args.groups} per GPU x {world} GPU(s) (weak scaling), "
+                                if scaling == "weak" else f"the {args.groups} groups in {world} contiguous blocks, ")
+                               + "one block per GPU (one process each), lastIndex chained by an all_gather of a "
+                                 "4-int record per rank per step",
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -414,7 +414,9 @@ int ca_estimate_plan_stats(const ca_estimate_plan* p, int32_t* rounds, float* ch
  * [4] result compaction, [5] D2H of the results; [6] host wall time of the call;
  * [7] how the results reached sched_pod: 0 copied after the chains, 1 published
  * zero-copy while they ran, 2 the publisher gave up (kernels serialised, or a chain
- * died) and the results were copied instead.  Writes min(cap, 8) values; returns 8. */
+ * died) and the results were copied instead; [8] 1 if the run took the decoupled Go
+ * order (chains on the stable class order, Go's ids beside them: uniform classes and no
+ * two classes of a group with equal scores), else 0.  Writes min(cap, 9) values; returns 9. */
 int ca_estimate_plan_timings(const ca_estimate_plan* p, float* out, int32_t cap);
 /* Whether the last run's outputs depend on the lastIndex it started from (then a caller
  * that ran the batch from a guessed lastIndex must re-run it from the true one), and

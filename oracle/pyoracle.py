@@ -271,3 +271,9 @@ def node_utilization(nodes: np.ndarray, pod_off: np.ndarray, pods: np.ndarray, s
     _check(load().or_node_utilization(ptr(nodes), len(nodes), ptr(pod_off), ptr(pods), int(skip_daemonset_pods),
                                       int(skip_mirror_pods), int(now_ns), ptr(out)), "node_utilization")
     return out
+
+
+def runonce_cpu_util(ui, now_ns: int):
+    """The CPU port's utilization step of autoscaler_amd.runonce.run (or_node_utilization
+    over the UtilInput's full rows): the parity checker and the bench's CPU baseline."""
+    return node_utilization(ui.nodes, ui.off, ui.pods, False, False, now_ns)

@@ -1,6 +1,7 @@
 import os, sys
 sys.path.insert(0, "tests"); sys.path.insert(0, "oracle"); sys.path.insert(0, ".")
 os.environ.setdefault("CASIM_PLAN_TRACE", "5")
+os.environ.setdefault("CASIM_TEST_HOOKS", "1")
 import numpy as np
 from plangen import rand_plan_case
 from autoscaler_amd import native

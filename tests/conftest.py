@@ -3,6 +3,10 @@ import sys
 
 import pytest
 
+# the library's fault-injection hooks (CASIM_PLAN_FAIL_ROUND, CASIM_PLAN_WINDOW, ...) are
+# read only with CASIM_TEST_HOOKS set (casim_internal.h test_hook_env)
+os.environ.setdefault("CASIM_TEST_HOOKS", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
     if p not in sys.path:

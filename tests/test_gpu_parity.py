@@ -315,7 +315,8 @@ def test_estimate_workloads(name, w, batch, sort, rows, oracle, monkeypatch):
 @pytest.mark.parametrize("shapes", [300, 3000, 6000])
 def test_estimate_many_score_classes(shapes, oracle):
     """Random (cpu, mem) shapes: > 256 score classes take two radix passes, > 4096 take the
-    comparison sort; cross-shape score ties (H2) resolve by list position on both."""
+    comparison sort; every output in Go sort.Slice order (the oracle's default) — ties
+    between shapes of equal float64 score included."""
     w = W.c2(n_pods=8000, n_groups=10, n_existing=30, pods_per_controller=1, n_random_shapes=shapes, seed=shapes)
     outs = []
     for b in (oracle.OracleState(), _mirror()):
@@ -389,6 +390,70 @@ def test_estimate_go_order_decoupled(seed, decouple, oracle, monkeypatch):
             assert np.array_equal(ro.sched_pod, plan.fetch())
             h = plan.run_u16(w.max_nodes, L0)
             assert np.array_equal(ro.sched_pod, np.where(h.sched_pod == 0xFFFF, -1, h.sched_pod.astype(np.int32)))
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("decouple", ["1", "0"], ids=["auto", "coupled"])
+def test_estimate_go_order_cross_class_ties(seed, decouple, oracle, monkeypatch):
+    """Uniform score classes whose float64 scores tie ACROSS classes on the templates
+    (estgen.tied_workload: (1000m, 1Gi), (500m, 3Gi) and (250m, 4Gi) all score 0.3125 on a
+    4000m / 16Gi template).  k_class_rank gives them one dense rank and Go's pdqsort mixes
+    their pods differently from list position, so the chains must not run on the stable
+    order: the plan takes the coupled path (stats()["decoupled"] is False) and matches the
+    Go-order oracle in every output mode (binpacking_estimator.go:72-74)."""
+    from estgen import tied_workload
+    monkeypatch.setenv("CASIM_GO_DECOUPLE", decouple)
+    monkeypatch.setenv("CASIM_PUB_CHUNK", "64" if seed % 2 else "4096")
+    w, shape_of = tied_workload(seed)
+    o = oracle.OracleState()
+    W.load_estimate(o, w)
+    L0 = (0, 5, 77)[seed % 3]
+    ro = o.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, L0)
+    # the hazard is real on this input: Go's order puts other classes at some sorted
+    # positions than the stable order (what a decoupled run would have got wrong)
+    o.set_sort_mode("stable")
+    rs = o.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, L0)
+    o.set_sort_mode("go")
+    cls_go = np.where(ro.sched_pod >= 0, shape_of[np.maximum(ro.sched_pod, 0)], -1)
+    cls_st = np.where(rs.sched_pod >= 0, shape_of[np.maximum(rs.sched_pod, 0)], -1)
+    assert not (np.array_equal(cls_go, cls_st) and np.array_equal(ro.results, rs.results))
+    m = _mirror()
+    W.load_estimate(m, w)
+    with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as plan:
+        for _ in range(2):
+            g = plan.run(w.max_nodes, L0, want_nodes=True)
+            assert np.array_equal(ro.results, g.results) and ro.last_index == g.last_index
+            assert np.array_equal(ro.sched_pod, g.sched_pod) and np.array_equal(ro.sched_node, g.sched_node)
+            p = plan.run(w.max_nodes, L0, want_nodes=False)
+            assert not plan.stats()["decoupled"]
+            assert np.array_equal(ro.results, p.results) and np.array_equal(ro.sched_pod, p.sched_pod)
+            d = plan.run(w.max_nodes, L0, device_results=True)
+            assert np.array_equal(ro.results, d.results)
+            assert np.array_equal(ro.sched_pod, plan.fetch())
+            h = plan.run_u16(w.max_nodes, L0)
+            assert not plan.stats()["decoupled"]
+            assert np.array_equal(ro.results, h.results) and ro.last_index == h.last_index
+            assert np.array_equal(ro.sched_pod, np.where(h.sched_pod == 0xFFFF, -1, h.sched_pod.astype(np.int32)))
+    b = m.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, L0)      # ca_estimate_batch
+    assert np.array_equal(ro.results, b.results) and ro.last_index == b.last_index
+    assert np.array_equal(ro.sched_pod, b.sched_pod) and np.array_equal(ro.sched_node, b.sched_node)
+
+
+def test_estimate_c2_catalog_takes_decoupled_path(oracle):
+    """C2's 64-shape catalog has no cross-class score ties on its templates: the headline
+    path stays decoupled (and matches the Go-order oracle)."""
+    w = W.c2(n_pods=8000, n_groups=12, n_existing=50, seed=3)
+    assert w.meta["cross_shape_score_ties"] == 0
+    o = oracle.OracleState()
+    W.load_estimate(o, w)
+    ro = o.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, 0)
+    m = _mirror()
+    W.load_estimate(m, w)
+    with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as plan:
+        h = plan.run_u16(w.max_nodes, 0)
+        assert plan.stats()["decoupled"]
+        assert np.array_equal(ro.results, h.results)
+        assert np.array_equal(ro.sched_pod, np.where(h.sched_pod == 0xFFFF, -1, h.sched_pod.astype(np.int32)))
 
 
 @pytest.mark.parametrize("seed", range(8))

@@ -12,7 +12,7 @@ def _oracle_run(w):
     from autoscaler_amd import workloads as W
     o = pyoracle.OracleState()
     W.load_filter(o, w.filt)
-    return runonce.run(o, runonce.cpu_util, w)
+    return runonce.run(o, pyoracle.runonce_cpu_util, w)
 
 
 def test_runonce_small_oracle(oracle_lib):

@@ -453,6 +453,134 @@ __global__ void __launch_bounds__(RTHREADS) k_radix_scatter(const GroupMeta* __r
     }
 }
 
+// 1*-3*. decoupled Go order: the stable class order of a group is its
+// classes in rank order, each class's pods together, and every pod of a class is the same
+// record but for its controller — so the chain stream follows from per-class counts alone,
+// with no sort of the pod list.  k_run_table (one workgroup per group, after k_class_rank):
+// the class counts of the group's list, each rank's first stream position
+// rstart[g][r] (r in [0, U]), and the stream record of the rank's class rsp[g][r] (its
+// representative pod's requests and static bits against the template).  k_emit_runs:
+// stream position -> rank (binary search of rstart), the record, run heads exactly as
+// k_emit_bucket marks them (a head where the record or its bits change, every
+// non-batchable pod).  The pod id of a stream entry is not needed: decoupled chains emit
+// stream positions and the consumers map them through the Go-order ids.
+__global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict__ groups,
+                                                   const int32_t* __restrict__ pod_idx, const int32_t* __restrict__ pcls,
+                                                   const int32_t* __restrict__ crank, const int32_t* __restrict__ cls_rep,
+                                                   int32_t U, const ca_template* __restrict__ tmpls,
+                                                   const PodHot* __restrict__ ph, const ca_pod_spec* __restrict__ specs,
+                                                   const ca_selector_term* __restrict__ terms,
+                                                   const ca_selector_req* __restrict__ reqs, int32_t* __restrict__ rstart,
+                                                   StreamPod* __restrict__ rsp, uint32_t* __restrict__ group_unsup,
+                                                   const int32_t* __restrict__ gmap) {
+    __shared__ int32_t cnt[CLS_MAX];
+    __shared__ int32_t rc[CLS_MAX];
+    __shared__ int32_t wsum[16];
+    const int gi = GSEL(blockIdx.x);
+    const GroupMeta gm = groups[gi];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int i = tid; i < U; i += 1024) { cnt[i] = 0; rc[i] = 0; }
+    __syncthreads();
+    // class counts: the lanes of a wave holding one class add once (controllers come in runs)
+    for (int32_t base = 0; base < gm.count; base += 1024) {
+        const int32_t i = base + tid;
+        const bool valid = i < gm.count;
+        const int32_t c = valid ? pcls[pod_idx[gm.off + i]] : -1;
+        uint64_t act = __ballot(valid);
+        while (act) {
+            const int l = __builtin_ctzll(act);
+            const int32_t cl = __builtin_amdgcn_readlane(c, l);
+            const uint64_t m = __ballot(valid && c == cl) & act;
+            if (lane == l) atomicAdd(&cnt[cl], __builtin_popcountll(m));
+            act &= ~m;
+        }
+    }
+    __syncthreads();
+    const int32_t* cr = crank + (size_t)gi * U;
+    for (int c = tid; c < U; c += 1024)
+        if (cnt[c] > 0) atomicAdd(&rc[cr[c]], cnt[c]);
+    __syncthreads();
+    // exclusive scan of the counts by rank: thread t owns ranks [4t, 4t + 4)
+    int32_t v[4], loc = 0;
+    for (int q = 0; q < 4; q++) { const int r = 4 * tid + q; v[q] = r < U ? rc[r] : 0; loc += v[q]; }
+    int32_t x = loc;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int32_t pre = x - loc;
+    for (int q = 0; q < w; q++) pre += wsum[q];
+    int32_t* rs = rstart + (size_t)gi * (U + 1);
+    for (int q = 0; q < 4; q++) {
+        const int r = 4 * tid + q;
+        if (r < U) rs[r] = pre;
+        pre += v[q];
+    }
+    if (tid == 0) rs[U] = gm.count;
+    // the record of each present class, at its rank
+    const ca_template& tp = tmpls[gm.tmpl];
+    const bool tunsched = (tp.node.flags & CA_NODE_UNSCHEDULABLE) != 0;
+    uint32_t unsup = 0;
+    for (int c = tid; c < U; c += 1024) {
+        if (cnt[c] == 0) continue;
+        const PodHot p = ph[cls_rep[c]];
+        const uint32_t sf = static_sf(p, tp, tunsched, specs, terms, reqs);
+        StreamPod sp;
+        sp.cpu = p.cpu; sp.mem = p.mem; sp.eph = p.eph;
+        sp.pod = cls_rep[c];
+        sp.flags = sf | (batchable(p, sf) ? SF_BATCH : 0u);
+        rsp[(size_t)gi * U + cr[c]] = sp;
+        unsup |= sf & SF_UNSUP;
+    }
+    if (unsup) atomicOr(&group_unsup[gi], 1u);
+}
+
+__device__ inline int32_t run_rank(const int32_t* __restrict__ st, int32_t U, int32_t i) {
+    int32_t lo = 0, hi = U;                  // the last r with st[r] <= i (st[U] = count > i)
+    while (hi - lo > 1) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (st[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(256) k_emit_runs(const GroupMeta* __restrict__ groups,
+                                                  const int32_t* __restrict__ rstart, const StreamPod* __restrict__ rsp,
+                                                  int32_t U, StreamPod* __restrict__ out, uint64_t* __restrict__ heads,
+                                                  const int32_t* __restrict__ gmap) {
+    __shared__ int32_t st[CLS_MAX + 1];
+    const int gi = GSEL(blockIdx.y);
+    const GroupMeta gm = groups[gi];
+    const int32_t base = (int32_t)(blockIdx.x * blockDim.x);
+    if (base >= gm.count) return;                                   // (uniform per block)
+    const int32_t* rs = rstart + (size_t)gi * (U + 1);
+    for (int r = threadIdx.x; r <= U; r += blockDim.x) st[r] = rs[r];
+    __syncthreads();
+    const int32_t i = base + (int32_t)threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    if (base + (int32_t)(threadIdx.x & ~63u) >= gm.count) return;   // whole wave past the end
+    bool head = true;
+    if (i < gm.count) {
+        const int32_t r = run_rank(st, U, i);
+        StreamPod sp = rsp[(size_t)gi * U + r];
+        const bool bat = (sp.flags & SF_BATCH) != 0;
+        if (i > 0 && bat) {
+            head = false;
+            if (i == st[r]) {                                       // first pod of its class
+                const StreamPod q = rsp[(size_t)gi * U + run_rank(st, U, i - 1)];
+                head = !((q.flags & ~SF_BATCH) == (sp.flags & ~SF_BATCH) && q.cpu == sp.cpu && q.mem == sp.mem &&
+                         q.eph == sp.eph);
+            }
+        }
+        sp.flags |= head ? SF_HEAD : 0u;
+        out[gm.off + i] = sp;
+    }
+    const uint64_t hb = __ballot(head);
+    if (lane == 0) heads[gm.moff + (i >> 6)] = hb;
+}
+
 // 1''-2''. Go 1.19 sort.Slice order (binpacking_estimator.go:74; pdqsort.h) ----------
 // One 1024-thread workgroup per group: the rank of every position of the group's list
 // (its class's dense rank, k_class_rank, or an explicit per-position rank from
@@ -1968,6 +2096,7 @@ struct ca_estimate_plan {
     // k_pdq_sort on st3 writes the Go-order ids into d_spod_go (d_sortC: the
     // permutation; d_ids_ready: per group, the run epoch whose ids are final there)
     DevBuf d_sortC, d_ids_ready, d_spod_go, d_crank2;
+    DevBuf d_rstart, d_rsp;        // decoupled: per group, each rank's first stream position and record
     int32_t ids_epoch = 0;
     hipStream_t st3 = nullptr;
     hipEvent_t ev_emitA = nullptr, ev_emitB = nullptr, ev_ids = nullptr;
@@ -2214,6 +2343,10 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
         CA_HIP_CHECK(hipMemset(p->d_ids_ready.ptr, 0, sizeof(int32_t) * (size_t)std::max(G, 1)));   // epoch 0: none
         p->ids_epoch = 0;
         if ((rc = p->d_crank2.reserve(sizeof(int32_t) * (size_t)std::max(G, 1) * (size_t)std::max(s->n_cls, 1))) != CA_OK)
+            return rc;
+        if ((rc = p->d_rstart.reserve(sizeof(int32_t) * (size_t)std::max(G, 1) * (size_t)(s->n_cls + 1))) != CA_OK)
+            return rc;
+        if ((rc = p->d_rsp.reserve(sizeof(StreamPod) * (size_t)std::max(G, 1) * (size_t)std::max(s->n_cls, 1))) != CA_OK)
             return rc;
     }
     if (G) CA_HIP_CHECK(hipMemcpyAsync(p->d_meta.ptr, p->h_meta.data(), sizeof(GroupMeta) * G, hipMemcpyHostToDevice, st));
@@ -2470,6 +2603,9 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         while (nb < U) { nb <<= 8; passes++; }
         passes = std::max(passes, 1);
         const int32_t passes_run = (go_order && !decoupled) ? 0 : passes;
+        // decoupled: the stream from per-class counts (k_run_table + k_emit_runs) instead of
+        // the radix passes and k_emit_bucket (CASIM_RUNS_STREAM=0: the radix path, for tests)
+        const bool runs_stream = !(getenv("CASIM_RUNS_STREAM") && atoi(getenv("CASIM_RUNS_STREAM")) == 0);
 
         const int32_t blocks = (p->max_count + 255) / 256;
         // class ranks, then Go's pdqsort (default) or the stable LSD radix passes, stream
@@ -2480,6 +2616,21 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                p->d_tmpl.as<ca_template>(), p->s->d_cls_sc.as<int64_t>(), U, NP, crank, gm);
             CA_HIP_CHECK(hipGetLastError());
             if (events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], ss));
+            if (decoupled && runs_stream) {
+                // the stream from per-class counts (no sort of the pod lists)
+                hipLaunchKernelGGL(k_run_table, dim3(ng), dim3(1024), 0, ss, p->d_meta.as<GroupMeta>(),
+                                   p->d_pod_idx.as<int32_t>(), pcls, crank, p->s->d_cls_rep.as<int32_t>(), U,
+                                   p->d_tmpl.as<ca_template>(), p->s->t.hot.as<PodHot>(), p->s->t.spec.as<ca_pod_spec>(),
+                                   p->s->t.terms.as<ca_selector_term>(), p->s->t.reqs.as<ca_selector_req>(),
+                                   p->d_rstart.as<int32_t>(), p->d_rsp.as<StreamPod>(), p->d_unsup.as<uint32_t>(), gm);
+                CA_HIP_CHECK(hipGetLastError());
+                if (events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], ss));
+                hipLaunchKernelGGL(k_emit_runs, dim3(blocks, ng), dim3(256), 0, ss, p->d_meta.as<GroupMeta>(),
+                                   p->d_rstart.as<int32_t>(), p->d_rsp.as<StreamPod>(), U, p->d_stream.as<StreamPod>(),
+                                   p->d_heads.as<uint64_t>(), gm);
+                CA_HIP_CHECK(hipGetLastError());
+                return CA_OK;
+            }
             uint32_t* a = nullptr;                        // identity (position order)
             uint32_t* bufs[2] = {p->d_sortA.as<uint32_t>(), p->d_sortB.as<uint32_t>()};
             if (go_order && !decoupled) {

@@ -237,6 +237,7 @@ struct ca_podset {
     // score_memory}.  Used by the Estimate bucket sort (estimate.hip).
     int32_t n_cls = 0;
     casim::DevBuf d_cls, d_cls_sc;
+    casim::DevBuf d_cls_rep;           // a pod of each class (its first in the set)
     std::vector<int32_t> h_cls;        // host copies: class per pod, {cpu, memory} per class
     std::vector<int64_t> h_cls_sc;
     // every class's pods carry identical records apart from their controller

@@ -1161,6 +1161,11 @@ int ca_podset_create(ca_mirror* m, const ca_pod_table* t, ca_podset** out) {
         }
         s->h_cls = cls;
         s->h_cls_sc = sc;
+        std::vector<int32_t> rep((size_t)std::max(s->n_cls, 1), 0);
+        for (int32_t i = t->n_pods - 1; i >= 0; i--) rep[cls[i]] = i;
+        if ((rc = s->d_cls_rep.reserve(sizeof(int32_t) * rep.size())) != CA_OK) { delete s; return rc; }
+        CA_HIP_CHECK(hipMemcpyAsync(s->d_cls_rep.ptr, rep.data(), sizeof(int32_t) * rep.size(), hipMemcpyHostToDevice,
+                                    m->stream));
         if ((rc = s->d_cls.reserve(sizeof(int32_t) * (cls.size() + 1))) != CA_OK ||
             (rc = s->d_cls_sc.reserve(sizeof(int64_t) * (sc.size() + 2))) != CA_OK) { delete s; return rc; }
         if (!cls.empty())

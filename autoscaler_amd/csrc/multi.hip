@@ -66,6 +66,7 @@ struct ca_multi_estimate_plan {
     std::vector<ca_podset*> ps;
     std::vector<ca_estimate_plan*> pl;
     int32_t reruns = 0;
+    int32_t rerun_units = 0;                  // groups in the re-run blocks of the last run
     ~ca_multi_estimate_plan() {
         for (auto* p : pl) if (p) ca_estimate_plan_destroy(p);
         for (auto* s : ps) if (s) ca_podset_destroy(s);
@@ -81,6 +82,7 @@ struct ca_multi_removal_plan {
     std::vector<ca_removal_plan*> pl;
     std::vector<std::vector<int32_t>> hb;     // per block: the hints its run reads and writes
     int32_t reruns = 0;
+    int32_t rerun_units = 0;                  // candidates in the re-run blocks of the last run
     ~ca_multi_removal_plan() {
         for (auto* p : pl) if (p) ca_removal_plan_destroy(p);
     }
@@ -156,6 +158,7 @@ int ca_multi_estimate_plan_run(ca_multi_estimate_plan* p, const ca_limiter* limi
     // the lastIndex chain over the blocks (prefix protocol: after a block that stopped at an
     // unsupported group, nothing runs)
     p->reruns = 0;
+    p->rerun_units = 0;
     int32_t cur = L0;
     bool cut = false;
     for (int32_t d = 0; d < D; d++) {
@@ -176,6 +179,7 @@ int ca_multi_estimate_plan_run(ca_multi_estimate_plan* p, const ca_limiter* limi
             if (sens[d]) {                                   // depends on its input: run it again
                 if ((rc = run(d, cur)) != CA_OK) return rc;
                 p->reruns++;
+                p->rerun_units += g1 - g0;
             } else {                                         // same outputs from any input
                 lout[d] = casim::estimate_plan_rebase(p->pl[d], results + g0, cur);
                 lin[d] = cur;
@@ -196,6 +200,12 @@ int ca_multi_estimate_plan_stats(const ca_multi_estimate_plan* p, int32_t* n_blo
     if (reruns) *reruns = p->reruns;
     if (block_first_group)
         for (int32_t d = 0; d <= D && d < cap; d++) block_first_group[d] = p->gb[d];
+    return CA_OK;
+}
+
+int ca_multi_estimate_plan_rerun_units(const ca_multi_estimate_plan* p, int32_t* groups_rerun) {
+    if (!p || !groups_rerun) return CA_EINVAL;
+    *groups_rerun = p->rerun_units;
     return CA_OK;
 }
 
@@ -274,6 +284,7 @@ int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t 
     int rc = for_blocks(D, [&](int32_t d) { return run(d, L0); });
     if (rc != CA_OK) return rc;
     p->reruns = 0;
+    p->rerun_units = 0;
     int32_t cur = L0;
     bool cut = false;
     for (int32_t d = 0; d < D; d++) {
@@ -294,6 +305,7 @@ int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t 
             if (succ[d]) {                                    // a scan succeeded: its start mattered
                 if ((rc = run(d, cur)) != CA_OK) return rc;
                 p->reruns++;
+                p->rerun_units += c1 - c0;
             } else {                                          // no scan succeeded: lastIndex passes through
                 for (int32_t c = c0; c < c1; c++) results[c].last_index_in = cur;
                 lin[d] = lout[d] = cur;
@@ -325,6 +337,12 @@ int ca_multi_removal_plan_stats(const ca_multi_removal_plan* p, int32_t* n_block
     if (reruns) *reruns = p->reruns;
     if (block_first_candidate)
         for (int32_t d = 0; d <= D && d < cap; d++) block_first_candidate[d] = p->cb[d];
+    return CA_OK;
+}
+
+int ca_multi_removal_plan_rerun_units(const ca_multi_removal_plan* p, int32_t* candidates_rerun) {
+    if (!p || !candidates_rerun) return CA_EINVAL;
+    *candidates_rerun = p->rerun_units;
     return CA_OK;
 }
 

@@ -104,11 +104,13 @@ def load() -> C.CDLL:
         "ca_multi_estimate_plan_create": ([vp, vp, vp, vp, vp, i32, p(vp)], C.c_int),
         "ca_multi_estimate_plan_run": ([vp, vp, p(i32), vp, vp, vp], C.c_int),
         "ca_multi_estimate_plan_stats": ([vp, p(i32), p(i32), vp, i32], C.c_int),
+        "ca_multi_estimate_plan_rerun_units": ([vp, p(i32)], C.c_int),
         "ca_multi_estimate_plan_destroy": ([vp], C.c_int),
         "ca_multi_estimate_batch": ([vp, vp, vp, vp, vp, i32, vp, p(i32), vp, vp, vp], C.c_int),
         "ca_multi_removal_plan_create": ([vp, vp, i32, vp, vp, vp, vp, p(vp)], C.c_int),
         "ca_multi_removal_plan_run": ([vp, vp, i32, p(i32), vp, vp], C.c_int),
         "ca_multi_removal_plan_stats": ([vp, p(i32), p(i32), vp, i32], C.c_int),
+        "ca_multi_removal_plan_rerun_units": ([vp, p(i32)], C.c_int),
         "ca_multi_removal_plan_destroy": ([vp], C.c_int),
         "ca_multi_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, i32, p(i32), vp, vp], C.c_int),
         "ca_plan_removals": ([vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, i32, p(i32), vp, vp, i32, p(i32)], C.c_int),
@@ -160,8 +162,9 @@ def exported_symbols() -> list[str]:
         "ca_util_table_create", "ca_util_table_destroy", "ca_util_calculate", "ca_util_device_results",
         "ca_util_table_update", "ca_util_table_set_added", "ca_multi_create", "ca_multi_destroy",
         "ca_multi_estimate_plan_create", "ca_multi_estimate_plan_run",
-        "ca_multi_estimate_plan_stats", "ca_multi_estimate_plan_destroy", "ca_multi_estimate_batch",
+        "ca_multi_estimate_plan_stats", "ca_multi_estimate_plan_rerun_units", "ca_multi_estimate_plan_destroy", "ca_multi_estimate_batch",
         "ca_multi_removal_plan_create", "ca_multi_removal_plan_run", "ca_multi_removal_plan_stats",
+        "ca_multi_removal_plan_rerun_units",
         "ca_multi_removal_plan_destroy", "ca_multi_find_nodes_to_remove",
         "ca_plan_removals", "ca_plan_last_moves", "ca_plan_stats", "ca_plan_last_path", "ca_plan_chain_profile",
     ]
@@ -899,7 +902,10 @@ class MultiEstimatePlan:
         nb, rr = C.c_int32(0), C.c_int32(0)
         first = np.zeros(65, np.int32)
         self.lib.ca_multi_estimate_plan_stats(self.h, C.byref(nb), C.byref(rr), ptr(first), len(first))
-        return {"blocks": nb.value, "reruns": rr.value, "block_first_group": first[: nb.value + 1].tolist()}
+        ru = C.c_int32(0)
+        self.lib.ca_multi_estimate_plan_rerun_units(self.h, C.byref(ru))
+        return {"blocks": nb.value, "reruns": rr.value, "block_first_group": first[: nb.value + 1].tolist(),
+                "rerun_groups": ru.value}
 
     def close(self) -> None:
         if self.h:
@@ -944,7 +950,10 @@ class MultiRemovalPlan:
         nb, rr = C.c_int32(0), C.c_int32(0)
         first = np.zeros(65, np.int32)
         self.lib.ca_multi_removal_plan_stats(self.h, C.byref(nb), C.byref(rr), ptr(first), len(first))
-        return {"blocks": nb.value, "reruns": rr.value, "block_first_candidate": first[: nb.value + 1].tolist()}
+        ru = C.c_int32(0)
+        self.lib.ca_multi_removal_plan_rerun_units(self.h, C.byref(ru))
+        return {"blocks": nb.value, "reruns": rr.value, "block_first_candidate": first[: nb.value + 1].tolist(),
+                "rerun_candidates": ru.value}
 
     def close(self) -> None:
         if self.h:

@@ -599,6 +599,9 @@ int ca_multi_estimate_plan_run(ca_multi_estimate_plan* p, const ca_limiter* limi
 /* blocks, re-runs of the last run, and the first group of each block (n_blocks + 1 values) */
 int ca_multi_estimate_plan_stats(const ca_multi_estimate_plan* p, int32_t* n_blocks, int32_t* reruns,
                                  int32_t* block_first_group, int32_t cap);
+/* node groups in the blocks the last run had to run again (a block run from a wrong
+ * lastIndex whose output depends on it) */
+int ca_multi_estimate_plan_rerun_units(const ca_multi_estimate_plan* p, int32_t* groups_rerun);
 int ca_multi_estimate_plan_destroy(ca_multi_estimate_plan* p);
 int ca_multi_estimate_batch(ca_multi* mm, const ca_pod_table* t, const int32_t* group_off, const int32_t* pod_idx,
                             const ca_template* templates, int32_t n_groups, const ca_limiter* limiter,
@@ -616,6 +619,8 @@ int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t 
                               ca_removal_result* results, int32_t* out_dest);
 int ca_multi_removal_plan_stats(const ca_multi_removal_plan* p, int32_t* n_blocks, int32_t* reruns,
                                 int32_t* block_first_candidate, int32_t cap);
+/* candidates in the blocks the last run had to run again */
+int ca_multi_removal_plan_rerun_units(const ca_multi_removal_plan* p, int32_t* candidates_rerun);
 int ca_multi_removal_plan_destroy(ca_multi_removal_plan* p);
 int ca_multi_find_nodes_to_remove(ca_multi* mm, const int32_t* candidates, int32_t n_candidates,
                                   const uint8_t* dest_mask, const int32_t* cand_status, const int32_t* move_off,

@@ -1,7 +1,9 @@
-"""The C2 Estimate step, device-resident results, exactly STEPS times: the program the
-rocprofv3 --pmc passes of scripts/gpu_round.sh count (traffic per step = total / STEPS).
-PMC_LEGS=all also runs STEPS C5 FilterOutSchedulable calls (fork/revert around each) and
-STEPS fresh C3 sweeps, so their kernels (k_fb_walk, k_sweep, k_sweep_table) are counted."""
+"""The C2 Estimate headline step (16-bit ids published into page-locked memory, the
+decoupled Go order: k_class_rank, k_pdq_sort, radix, k_emit_bucket, k_ffd_chain, k_publish)
+exactly STEPS times: the program the rocprofv3 --pmc passes of scripts/gpu_round.sh count
+(traffic per step = total / STEPS).  PMC_LEGS=all also runs STEPS C5 FilterOutSchedulable
+calls (fork/revert around each), STEPS fresh C3 sweeps and STEPS planner loops on C3 without
+a limit (k_plan_chain), so their kernels are counted too."""
 import os
 import sys
 
@@ -15,7 +17,7 @@ m = native.Mirror(0)
 W.load_estimate(m, w)
 with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as plan:
     for _ in range(STEPS):
-        plan.run(w.max_nodes, 0, copy=False, device_results=True)
+        plan.run_u16(w.max_nodes, 0, copy=False)
 m.close()
 if os.environ.get("PMC_LEGS") == "all":
     import numpy as np
@@ -34,4 +36,12 @@ if os.environ.get("PMC_LEGS") == "all":
         for _ in range(STEPS):
             m3.set_hints(np.full(len(s3.table), -1, np.int32))
             rp.run(0)
+    m3.close()
+    m3 = native.Mirror(0)
+    W.load_sweep(m3, s3)
+    h0 = np.full(len(s3.table), -1, np.int32)
+    for _ in range(STEPS):
+        m3.fork()
+        m3.plan_removals(s3.candidates, s3.dest_mask, s3.cand_status, s3.move_off, s3.move_pods, h0, 0, 0)
+        m3.revert()
     m3.close()

@@ -134,3 +134,51 @@ def test_multi_sweep_prefix_protocol(oracle):
     assert (g.results["reason"][c_mid + 1:] == abi.CA_UNREMOVABLE_NOT_RUN).all()
     for m in ms + [single]:
         m.close()
+
+
+@pytest.mark.parametrize("replicas", [2, 4])
+def test_multi_sweep_c3_full(replicas, oracle):
+    """BASELINE C3 at full size (5k nodes, 150k pods) on ca_multi_*: the fresh loop (every
+    block lastIndex-sensitive in a loose cluster: blocks after the first re-run) and the
+    hinted second loop (hint placements pass lastIndex through: no re-runs), against the
+    oracle; the re-run candidates are reported."""
+    w = W.c3()
+    args = (w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods)
+    o = oracle.OracleState()
+    W.load_sweep(o, w)
+    o1 = o.find_nodes_to_remove(*args, np.full(len(w.table), -1, np.int32), 0)
+    o2 = o.find_nodes_to_remove(*args, o1.hints, o1.last_index)
+    ms = _replicas(replicas, lambda m: W.load_sweep(m, w))
+    with native.Multi(ms) as mm, native.MultiRemovalPlan(mm, *args) as plan:
+        g1 = plan.run(np.full(len(w.table), -1, np.int32), 0)
+        assert np.array_equal(o1.results, g1.results) and o1.last_index == g1.last_index
+        assert np.array_equal(o1.dest, g1.dest) and np.array_equal(o1.hints, g1.hints)
+        s1 = plan.stats()
+        print(f"C3 fresh, {replicas} blocks: re-run blocks {s1['reruns']}, candidates {s1['rerun_candidates']}")
+        assert s1["rerun_candidates"] <= len(w.candidates)
+        g2 = plan.run(g1.hints, g1.last_index)
+        assert np.array_equal(o2.results, g2.results) and o2.last_index == g2.last_index
+        assert np.array_equal(o2.dest, g2.dest) and np.array_equal(o2.hints, g2.hints)
+        s2 = plan.stats()
+        print(f"C3 hinted, {replicas} blocks: re-run blocks {s2['reruns']}, candidates {s2['rerun_candidates']}")
+    for m in ms:
+        m.close()
+
+
+def test_multi_estimate_c4_full(oracle):
+    """BASELINE C4 at full size (50k pods x 100 groups, taints / node affinity) on
+    ca_multi_estimate_plan over 2 replicas: identical to one mirror and the Go-order
+    oracle; the re-run groups are reported."""
+    w = W.c4()
+    o = oracle.OracleState()
+    W.load_estimate(o, w)
+    ro = o.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, 0)
+    ms = _replicas(2, lambda m: W.load_estimate(m, w))
+    with native.Multi(ms) as mm, native.MultiEstimatePlan(mm, w.table, w.group_off, w.pod_idx, w.templates) as plan:
+        g = plan.run(w.max_nodes, 0)
+        _eq_estimate(ro, g, w.group_off)
+        st = plan.stats()
+        print(f"C4, 2 blocks: re-run blocks {st['reruns']}, groups {st['rerun_groups']}")
+        assert st["blocks"] == 2
+    for m in ms:
+        m.close()

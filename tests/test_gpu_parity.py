@@ -361,14 +361,17 @@ def test_estimate_full_c2_parity(oracle):
 
 
 @pytest.mark.parametrize("seed", range(6))
-@pytest.mark.parametrize("decouple", ["1", "0"], ids=["decoupled", "coupled"])
+@pytest.mark.parametrize("decouple", ["1", "radix", "0"], ids=["decoupled", "decoupled-radix", "coupled"])
 def test_estimate_go_order_decoupled(seed, decouple, oracle, monkeypatch):
     """Uniform score classes (C2's catalog: every class's pods identical but for their
     controller): the chains run on the stable class order while Go's sort.Slice ids are
-    computed beside them (CASIM_GO_DECOUPLE=0: the Go sort ahead of the stream).  Both give
-    the Go-order oracle's pod lists in every output mode, with progressive publishing
-    (64-output chunks), lastIndex speculation rounds (existing nodes) and limiter cuts."""
-    monkeypatch.setenv("CASIM_GO_DECOUPLE", decouple)
+    computed beside them (CASIM_GO_DECOUPLE=0: the Go sort ahead of the stream).  The
+    decoupled stream comes from per-class counts (k_run_table + k_emit_runs), or with
+    CASIM_RUNS_STREAM=0 from the radix passes.  All give the Go-order oracle's pod lists in
+    every output mode, with progressive publishing (64-output chunks), lastIndex
+    speculation rounds (existing nodes) and limiter cuts."""
+    monkeypatch.setenv("CASIM_GO_DECOUPLE", "0" if decouple == "0" else "1")
+    monkeypatch.setenv("CASIM_RUNS_STREAM", "0" if decouple == "radix" else "1")
     monkeypatch.setenv("CASIM_PUB_CHUNK", "64" if seed % 2 else "4096")
     w = W.c2(n_pods=6000 + 1000 * seed, n_groups=6 + seed, n_existing=(0, 20, 200)[seed % 3],
              max_nodes=(1000, 0, 7)[seed % 3], seed=100 + seed)

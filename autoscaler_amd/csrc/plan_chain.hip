@@ -37,9 +37,11 @@ constexpr int PC_LIST = CA_MAX_MOVED_PODS;   // pods to move per candidate (larg
 constexpr size_t PC_LDS_MAX = 163840;         // gfx950: one workgroup may own the CU's 160 KiB
 constexpr int32_t PC_MAX_NODES = 8192;        // two 64-bit words of per-block dirty bits
 constexpr int32_t PC_MVBUF = 512;             // moves staged in LDS between global writes
+constexpr int PC_MAX_WAVES = 8;               // the chain wave + up to 7 helper waves (VGPR budget: 2 waves / SIMD)
 // shader-clock counters of the chain's phases (info[4 + k]; CASIM_PROF builds only)
 enum { PC_INIT, PC_LISTS, PC_PDB, PC_FORK, PC_HINT, PC_SCAN, PC_ADD, PC_COMMIT, PC_REVERT, PC_TOTAL, PC_BLOCKS,
-       PC_WINDOWS, PC_NPROF };
+       PC_WINDOWS, PC_HANDOFFS, PC_NPROF };
+constexpr int PC_INFO = 4 + PC_NPROF + 3;     // int64 words of the kernel's info record
 #ifdef CASIM_PROF
 #define PC_T0() uint64_t tp_ = clock64()
 #define PC_MARK(k) do { const uint64_t t_ = clock64(); prof[k] += t_ - tp_; tp_ = t_; } while (0)
@@ -92,6 +94,7 @@ struct PcArgs {
     int32_t dbg;                  // CASIM_PLAN_DBG bits: 1 no block cache, 2 no maxima refresh
     int32_t* trace;               // CASIM_PLAN_TRACE: per simulated pod {c, t, hint, hint_ok, target, evals, L, cnt}
     int32_t trace_cap;
+    int32_t help_after;           // blocks a scan loads before handing the rest to the helper waves
 };
 
 // packs the pods to move (one thread per list entry; hints as the caller passed them: a
@@ -140,7 +143,7 @@ struct PcBlk {
 
 // LDS image of one call (byte offsets; every array 16-B aligned)
 struct PcLayout {
-    size_t rows, blk, excnt, scratch, resbuf, mvbuf, ctx, total;
+    size_t rows, blk, excnt, scratch, resbuf, mvbuf, ctx, help, total;
 };
 
 __host__ __device__ inline PcLayout pc_layout(int32_t n, bool eph_cols) {
@@ -155,6 +158,7 @@ __host__ __device__ inline PcLayout pc_layout(int32_t n, bool eph_cols) {
     L.resbuf = take(sizeof(ca_plan_result) * 64);       // results of the current 64 candidates
     L.mvbuf = take(sizeof(ca_plan_move) * PC_MVBUF);   // committed moves not yet written out
     L.ctx = take(256);                                 // PcCtx
+    L.help = take(256);                                // PcHelp (scan requests to the helper waves)
     L.total = o;
     return L;
 }
@@ -226,6 +230,113 @@ __device__ __attribute__((noinline)) bool pc_in_names(const PcArgs& a, int32_t x
     return in;
 }
 
+// Helper waves (the workgroup's waves 1..H).  The chain is one wavefront; a rotating scan
+// that has loaded PC_HELP_AFTER blocks without a fit (the tight phase: scans over most of
+// the ring) hands the rest of the ring to the helpers and waits.  Nothing changes the rows
+// while it waits, so a block's verdict is a pure function of the LDS rows, its bit planes
+// and the pod: helper h checks rotated blocks rr_lo + h, rr_lo + h + H, ... (the maxima
+// skip, then the rows and the static filters where they matter), lowers `best` (rr * 64 +
+// first fitting lane) with an LDS atomic min and stops at the first fit of its own
+// sequence or once its next block lies beyond `best`; blocks it read without a fit while
+// their maxima were stale get the exact maxima (`refr` tells the chain which).  The chain
+// then takes the fit at `best` and counts the visible nodes before it as evaluations —
+// exactly the scan's outcome, in a fraction of its dependent steps.
+constexpr int PC_HELP_AFTER = 2;       // blocks the chain loads itself before handing off
+struct PcHelp {
+    int32_t seq, quit, done, best;
+    int32_t rr_lo, rr_end, j0, l0, nb, node, spec, fl;
+    int64_t pcpu, pmem, peph;
+    uint32_t pf, pad;
+    uint64_t dirty0, dirty1, refr0, refr1;
+};
+static_assert(sizeof(PcHelp) <= 256, "PcHelp");
+enum { PH_ANY_STATIC = 1, PH_TAINT_ALL = 2, PH_ALL_ZERO = 4 };
+
+__device__ inline int32_t ph_ld(const int32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <bool EPH_COLS>
+__device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) {
+    const int lane = threadIdx.x & 63;
+    const int32_t n = a.n;
+    const PcLayout Y = pc_layout(n, EPH_COLS);
+    using Row = typename PcRowT<EPH_COLS>::type;
+    Row* const rows = reinterpret_cast<Row*>(pc_raw + Y.rows);
+    PcBlk* const blk = reinterpret_cast<PcBlk*>(pc_raw + Y.blk);
+    PcHelp* const q = reinterpret_cast<PcHelp*>(pc_raw + Y.help);
+    int32_t seen = 0;
+    for (;;) {
+        int32_t sq;
+        for (;;) {
+            sq = __builtin_amdgcn_readfirstlane(ph_ld(&q->seq));
+            if (sq != seen || __builtin_amdgcn_readfirstlane(ph_ld(&q->quit))) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (sq == seen) break;                                   // quit
+        seen = sq;
+        const int32_t rr_lo = q->rr_lo, rr_end = q->rr_end, j0 = q->j0, l0 = q->l0, nb = q->nb, node = q->node;
+        const int32_t spec = q->spec, fl = q->fl;
+        const int64_t pcpu = q->pcpu, pmem = q->pmem, peph = q->peph;
+        const uint32_t pf = q->pf;
+        const uint64_t dirty0 = q->dirty0, dirty1 = q->dirty1;
+        const bool any_static = fl & PH_ANY_STATIC, taint_all = fl & PH_TAINT_ALL, all_zero = fl & PH_ALL_ZERO;
+        const int32_t jn = node >> 6;
+        const uint64_t nbit = 1ull << (node & 63);
+        uint64_t refr0 = 0, refr1 = 0;
+        for (int32_t rr = rr_lo + h; rr <= rr_end; rr += H) {
+            if (rr * 64 > __builtin_amdgcn_readfirstlane(ph_ld(&q->best))) break;   // a fit before this block
+            int32_t j = j0 + rr;
+            if (j >= nb) j -= nb;
+            const uint64_t inr = rr == nb ? ((1ull << l0) - 1) : ~0ull;
+            const uint64_t cvis = pc_uni64(blk[j].vis);
+            const uint64_t vw = cvis & inr & (j == jn ? ~nbit : ~0ull);
+            if (!vw) continue;
+            const bool fitb = (blk[j].bmp >= 1) && (all_zero || ((pcpu <= blk[j].bmc) && (pmem <= blk[j].bmm) &&
+                                                                  (!EPH_COLS || peph <= blk[j].bme)));
+            if (!fitb) continue;                                    // the pod exceeds the block's maxima
+            const int32_t x = j * 64 + lane;
+            const bool in = x < n;
+            const int64_t cc = in ? rows[x].c : 0, cm = in ? rows[x].m : 0;
+            const int64_t ce = (EPH_COLS && in) ? pc_e(rows[x]) : 0;
+            const int32_t cp = in ? rows[x].p : INT32_MIN;
+            uint64_t fitm = vw & __ballot(cp >= 1);
+            if (!all_zero) {
+                fitm &= __ballot(pcpu <= cc) & __ballot(pmem <= cm);
+                fitm &= EPH_COLS ? __ballot(peph <= ce) : pc_uni64(blk[j].eph);
+            }
+            const uint64_t needm = any_static ? ~0ull : (taint_all ? 0ull : pc_uni64(blk[j].taint));
+            if (fitm & needm) {
+                bool ok = true;
+                if ((fitm & needm) >> lane & 1ull) ok = pc_static_fit(a, x, spec, pf);
+                fitm &= __ballot(ok);
+            }
+            if (fitm) {
+                if (lane == 0) atomicMin(&q->best, rr * 64 + (int32_t)__builtin_ctzll(fitm));
+                break;
+            }
+            const bool dj = j < 64 ? ((dirty0 >> j) & 1ull) : ((dirty1 >> (j - 64)) & 1ull);
+            if (dj) {                                               // exact maxima of the rows just read
+                const bool cv = (cvis >> lane) & 1ull;
+                const int64_t mc = __ockl_wfred_max_i64(cv ? cc : INT64_MIN);
+                const int64_t mmx = __ockl_wfred_max_i64(cv ? cm : INT64_MIN);
+                const int64_t me = EPH_COLS ? __ockl_wfred_max_i64(cv ? ce : INT64_MIN) : 0;
+                const int32_t mp = __ockl_wfred_max_i32(cv ? cp : INT32_MIN);
+                if (lane == 0) {
+                    blk[j].bmc = mc; blk[j].bmm = mmx; blk[j].bmp = mp;
+                    if (EPH_COLS) blk[j].bme = me;
+                }
+                if (j < 64) refr0 |= 1ull << j; else refr1 |= 1ull << (j - 64);
+            }
+        }
+        if (lane == 0) {
+            if (refr0) atomicOr(reinterpret_cast<unsigned long long*>(&q->refr0), (unsigned long long)refr0);
+            if (refr1) atomicOr(reinterpret_cast<unsigned long long*>(&q->refr1), (unsigned long long)refr1);
+            __hip_atomic_fetch_add(&q->done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
 // Per-call scalar state the candidate loop and the simulation share (LDS).
 struct PcCtx {
     int32_t Lw, Lraw, nm, mv_n, mv_first, removed, pad0, pad1;
@@ -262,7 +373,7 @@ __device__ inline void pc_flush_moves(const PcArgs& a, const ca_plan_move* mvbuf
 template <bool EPH_COLS>
 __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& a, unsigned char* pc_raw, PcCtx* ctx, const int32_t c,
                                                      const int32_t node, const int32_t cnt, const PcReg r0,
-                                                     const PcReg r1) {
+                                                     const PcReg r1, const int nh) {
     const int lane = threadIdx.x;
     const int32_t n = a.n, nb = (n + 63) >> 6;
     const PcLayout Y = pc_layout(n, EPH_COLS);
@@ -272,6 +383,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
     uint16_t* const excnt = reinterpret_cast<uint16_t*>(pc_raw + Y.excnt);
     int32_t* const scratch = reinterpret_cast<int32_t*>(pc_raw + Y.scratch);
     ca_plan_move* const mvbuf = reinterpret_cast<ca_plan_move*>(pc_raw + Y.mvbuf);
+    PcHelp* const hq = reinterpret_cast<PcHelp*>(pc_raw + Y.help);
     int32_t Lw = ctx->Lw;
     const int32_t nm = ctx->nm;
     uint64_t dirty0 = ctx->dirty0, dirty1 = ctx->dirty1;
@@ -365,6 +477,23 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                 const int32_t j0 = Lw >> 6, l0 = Lw & 63;
                 int32_t wr = -1, my_nv = 0;
                 uint64_t passm = 0;
+                int32_t loaded = 0;
+                // visible nodes (the scan's evaluations) of rotated blocks [ra, rb]
+                auto vis_count = [&](int32_t ra, int32_t rb) -> uint64_t {
+                    uint64_t tot = 0;
+                    for (int32_t b0 = ra; b0 <= rb; b0 += 64) {
+                        const int32_t r2 = b0 + lane;
+                        int32_t cn = 0;
+                        if (r2 <= rb) {
+                            int32_t jj = j0 + r2;
+                            if (jj >= nb) jj -= nb;
+                            const uint64_t inr2 = r2 == nb ? ((1ull << l0) - 1) : ~0ull;
+                            cn = __popcll(blk[jj].vis & inr2 & (jj == jn ? ~nbit : ~0ull));
+                        }
+                        tot += (uint64_t)__ockl_wfred_add_i32(cn);
+                    }
+                    return tot;
+                };
                 for (int32_t rr = 0; rr <= nb; rr++) {
                     if (rr == nb && l0 == 0) break;
                     int32_t j = j0 + rr;
@@ -398,6 +527,45 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                             continue;
                         }
                     }
+                    if (nh > 0 && !names && loaded >= a.help_after) {
+                        // ---- the rest of the ring to the helper waves (PcHelp) ----
+                        PC_SIM_COUNT(PC_HANDOFFS);
+                        const int32_t rr_end = l0 == 0 ? nb - 1 : nb;
+                        if (lane == 0) {
+                            hq->rr_lo = rr; hq->rr_end = rr_end; hq->j0 = j0; hq->l0 = l0; hq->nb = nb;
+                            hq->node = node; hq->spec = spec;
+                            hq->fl = (any_static ? PH_ANY_STATIC : 0) | (taint_all ? PH_TAINT_ALL : 0) |
+                                     (all_zero ? PH_ALL_ZERO : 0);
+                            hq->pcpu = pcpu; hq->pmem = pmem; hq->peph = peph; hq->pf = pf;
+                            hq->dirty0 = dirty0; hq->dirty1 = dirty1; hq->refr0 = 0; hq->refr1 = 0;
+                            hq->best = INT32_MAX; hq->done = 0;
+                            __hip_atomic_store(&hq->seq, hq->seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                        while (__builtin_amdgcn_readfirstlane(ph_ld(&hq->done)) < nh) __builtin_amdgcn_s_sleep(1);
+                        const int32_t best = __builtin_amdgcn_readfirstlane(ph_ld(&hq->best));
+                        dirty0 &= ~pc_uni64(hq->refr0);
+                        dirty1 &= ~pc_uni64(hq->refr1);
+                        if (best != INT32_MAX) {
+                            const int32_t rb = best >> 6, f = best & 63;
+                            int32_t jb = j0 + rb;
+                            if (jb >= nb) jb -= nb;
+                            const uint64_t inrb = rb == nb ? ((1ull << l0) - 1) : ~0ull;
+                            const uint64_t vmb = pc_uni64(blk[jb].vis) & inrb & (jb == jn ? ~nbit : ~0ull);
+                            const uint64_t upto = (f == 63) ? ~0ull : ((2ull << f) - 1);
+                            evals += vis_count(rr, rb - 1) + (uint64_t)__popcll(vmb & upto);
+                            target = jb * 64 + f;
+                            tc = pc_uni64s(rows[target].c); tm = pc_uni64s(rows[target].m);
+                            te = EPH_COLS ? pc_uni64s(pc_e(rows[target])) : 0;
+                            tpd = __builtin_amdgcn_readfirstlane(rows[target].p);
+                            Lw = target + 1 == n ? 0 : target + 1;                       // schedulerbased.go:131
+                            moved_L = true;
+                            if (lane == tl) { if (t >= 64) hs1 = target; else hs0 = target; }   // :123
+                        } else {
+                            evals += vis_count(rr, rr_end);
+                        }
+                        break;
+                    }
+                    loaded++;
                     PC_SIM_COUNT(PC_BLOCKS);
 #ifdef CASIM_PROF
                     if (a.dbg & 1) cj = -1;
@@ -692,11 +860,21 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
 }
 
 template <bool EPH_COLS>
-__global__ void __launch_bounds__(64) k_plan_chain(PcArgs a) {
+__global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char pc_raw[];
-    const int lane = threadIdx.x;
     const int32_t n = a.n, nb = (n + 63) >> 6;
     const PcLayout Y = pc_layout(n, EPH_COLS);
+    const int nh = (int)(blockDim.x >> 6) - 1;                  // helper waves
+    {
+        PcHelp* const hq = reinterpret_cast<PcHelp*>(pc_raw + Y.help);
+        if (threadIdx.x == 0) { hq->seq = 0; hq->quit = 0; hq->done = 0; hq->best = INT32_MAX; }
+        __syncthreads();                                        // (the one workgroup barrier)
+        if (threadIdx.x >= 64) {
+            pc_helper<EPH_COLS>(a, pc_raw, (int)(threadIdx.x >> 6) - 1, nh);
+            return;
+        }
+    }
+    const int lane = threadIdx.x;
     using Row = typename PcRowT<EPH_COLS>::type;
     Row* const rows = reinterpret_cast<Row*>(pc_raw + Y.rows);
     PcBlk* const blk = reinterpret_cast<PcBlk*>(pc_raw + Y.blk);
@@ -873,7 +1051,7 @@ __global__ void __launch_bounds__(64) k_plan_chain(PcArgs a) {
         simulated++;
         if (lane == 0) ctx->r = r;
         __builtin_amdgcn_wave_barrier();
-        pc_simulate<EPH_COLS>(a, pc_raw, ctx, c, node, cnt, r0, r1);
+        pc_simulate<EPH_COLS>(a, pc_raw, ctx, c, node, cnt, r0, r1, nh);
         r = ctx->r;
         nm = ctx->nm;
         removed = ctx->removed;
@@ -882,6 +1060,10 @@ __global__ void __launch_bounds__(64) k_plan_chain(PcArgs a) {
         if (sl == 63) flush_res(c - 63, 64);
     }
     __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {                                            // the helper waves exit
+        PcHelp* const hq = reinterpret_cast<PcHelp*>(pc_raw + Y.help);
+        __hip_atomic_store(&hq->quit, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     if (!stopped && a.C > 0 && ((a.C - 1) & 63) != 63) flush_res((a.C - 1) & ~63, ((a.C - 1) & 63) + 1);
     pc_flush_moves(a, mvbuf, ctx, lane);
     if (lane == 0) {
@@ -1005,13 +1187,13 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     hipLaunchKernelGGL(k_plan_pack, dim3((unsigned)((M + 64 + 255) / 256)), dim3(256), 0, st, din + o_mv, M,
                        m->d_pods.hot.as<PodHot>(), (const int32_t*)dH, dpods);
     CA_HIP_CHECK(hipGetLastError());
-    // outputs: results [C], info [16], moves [copy_cap]
-    const size_t out_bytes = sizeof(ca_plan_result) * C + 16 * sizeof(int64_t) + sizeof(ca_plan_move) * copy_cap;
+    // outputs: results [C], info [PC_INFO], moves [copy_cap]
+    const size_t out_bytes = sizeof(ca_plan_result) * C + PC_INFO * sizeof(int64_t) + sizeof(ca_plan_move) * copy_cap;
     if ((rc = S.out.reserve(out_bytes)) != CA_OK) return rc;
     if ((rc = S.h_out.reserve(out_bytes)) != CA_OK) return rc;
     ca_plan_result* const dres = S.out.as<ca_plan_result>();
     int64_t* const dinfo = reinterpret_cast<int64_t*>(dres + C);
-    ca_plan_move* const dmoves = reinterpret_cast<ca_plan_move*>(dinfo + 16);
+    ca_plan_move* const dmoves = reinterpret_cast<ca_plan_move*>(dinfo + PC_INFO);
 
     PcArgs A;
     A.hot = m->d_hot.as<NodeHot>();
@@ -1043,6 +1225,8 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     A.copy_cap = copy_cap;
     A.trace = nullptr;
     A.trace_cap = 0;
+    A.help_after = PC_HELP_AFTER;
+    if (const char* e = getenv("CASIM_PLAN_HELP_AFTER")) A.help_after = std::max(1, atoi(e));
     A.dbg = test_hook_env("CASIM_PLAN_DBG") ? atoi(test_hook_env("CASIM_PLAN_DBG")) : 0;
     const char* tr_env = test_hook_env("CASIM_PLAN_TRACE");
     DevBuf trace;
@@ -1056,14 +1240,17 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     const void* kfn = eph_cols ? (const void*)k_plan_chain<true> : (const void*)k_plan_chain<false>;
     if ((rc = ensure_dyn_lds(kfn, Y.total)) != CA_OK) return rc;
     CA_HIP_CHECK(hipEventRecord(m->ev0, st));
-    if (eph_cols) hipLaunchKernelGGL(k_plan_chain<true>, dim3(1), dim3(64), Y.total, st, A);
-    else hipLaunchKernelGGL(k_plan_chain<false>, dim3(1), dim3(64), Y.total, st, A);
+    // the chain wave plus helper waves for long scans (CASIM_PLAN_HELPERS: 0..7, default 7)
+    int waves = PC_MAX_WAVES;
+    if (const char* e = getenv("CASIM_PLAN_HELPERS")) waves = 1 + std::max(0, std::min(PC_MAX_WAVES - 1, atoi(e)));
+    if (eph_cols) hipLaunchKernelGGL(k_plan_chain<true>, dim3(1), dim3(64 * waves), Y.total, st, A);
+    else hipLaunchKernelGGL(k_plan_chain<false>, dim3(1), dim3(64 * waves), Y.total, st, A);
     CA_HIP_CHECK(hipGetLastError());
     ca_plan_result* const hres = S.h_out.as<ca_plan_result>();
     int64_t* const hinfo = reinterpret_cast<int64_t*>(hres + C);
-    ca_plan_move* const hmoves = reinterpret_cast<ca_plan_move*>(hinfo + 16);
+    ca_plan_move* const hmoves = reinterpret_cast<ca_plan_move*>(hinfo + PC_INFO);
     CA_HIP_CHECK(hipEventRecord(m->ev1, st));
-    CA_HIP_CHECK(hipMemcpyAsync(hres, dres, sizeof(ca_plan_result) * C + 16 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    CA_HIP_CHECK(hipMemcpyAsync(hres, dres, sizeof(ca_plan_result) * C + PC_INFO * sizeof(int64_t), hipMemcpyDeviceToHost, st));
     CA_HIP_CHECK(hipStreamSynchronize(st));
     const auto t_kernel = std::chrono::steady_clock::now();
     if (tr_env) {

@@ -520,7 +520,7 @@ class Mirror:
         hm = np.zeros(5, np.float32)
         k = self.lib.ca_plan_chain_profile(self.h, cyc.ctypes.data, 16, hm.ctypes.data)
         names = ["init", "lists", "pdb", "fork", "hint", "scan", "add", "commit", "revert", "total", "blocks",
-                 "windows"]
+                 "windows", "handoffs"]
         out = {nm: int(v) for nm, v in zip(names, cyc[:max(k, 0)])}
         out.update({h: float(v) for h, v in zip(["sync_ms", "launch_kernel_ms", "kernel_ms", "readback_ms",
                                                    "replay_ms"], hm)})

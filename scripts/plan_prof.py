@@ -17,6 +17,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
 w = W.c3(n_nodes=n)
 args = (w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods)
 hints = np.full(len(w.table), -1, np.int32)
+helpers = os.environ.get("CASIM_PLAN_HELPERS", "7")
+print(f"helper waves: {helpers}")
 for limit in (20, 200, 0):
     m = native.Mirror(0)
     W.load_sweep(m, w)
@@ -37,5 +39,6 @@ for limit in (20, 200, 0):
     print(f"   kernel clock {ghz:.2f} GHz; phases (% of total cycles): " +
           "  ".join(f"{k}={100 * pr[k] / tot:.1f}" for k in
                     ("init", "lists", "pdb", "fork", "hint", "scan", "add", "commit", "revert")))
-    print(f"   blocks scanned {pr['blocks']}  skip windows {pr['windows']}", flush=True)
+    print(f"   blocks scanned {pr['blocks']}  skip windows {pr['windows']}  helper hand-offs {pr.get('handoffs', 0)}",
+          flush=True)
     m.close()

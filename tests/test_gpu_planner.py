@@ -58,13 +58,16 @@ def _follow_up_sweep(b, n_nodes: int, n_pods: int):
                                   np.full(n_pods, -1, np.int32), 0)
 
 
-@pytest.fixture(params=["chain", "speculative"])
+@pytest.fixture(params=["chain", "chain1", "speculative"])
 def path(request, monkeypatch):
+    """The device chain with its helper waves (default), the chain alone (one wavefront:
+    CASIM_PLAN_HELPERS=0), and the speculative sweep windows."""
     if request.param == "speculative":
         monkeypatch.setenv("CASIM_PLAN_SPECULATIVE", "1")
     else:
         monkeypatch.delenv("CASIM_PLAN_SPECULATIVE", raising=False)
-    return request.param
+        monkeypatch.setenv("CASIM_PLAN_HELPERS", "0" if request.param == "chain1" else "7")
+    return "chain" if request.param.startswith("chain") else request.param
 
 
 def _no_ext(case: PlanCase) -> PlanCase:
@@ -113,6 +116,18 @@ def test_plan_random_larger(seed, oracle, path):
     speculations (placements on filled nodes, hints on removed nodes, grown pod lists)."""
     case = rand_plan_case(100 + seed, n_nodes=60, pods_per_node=6, n_pdbs=3, limit=0)
     _run_both(case, oracle)
+
+
+@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("help_after", ["1", "2"])
+def test_plan_random_larger_chain_scope_helpers(seed, help_after, oracle, monkeypatch):
+    """The helper waves take every scan after its first (help_after = 1) or second block:
+    same results as the oracle (blocks scanned out of order, maxima refreshed by helpers)."""
+    monkeypatch.setenv("CASIM_PLAN_HELPERS", "7")
+    monkeypatch.setenv("CASIM_PLAN_HELP_AFTER", help_after)
+    case = _no_ext(rand_plan_case(200 + seed, n_nodes=150 + 61 * seed, pods_per_node=6, n_pdbs=3, limit=0))
+    _run_both(case, oracle)
+    assert _M["m"].plan_stats()["path"] == "chain"
 
 
 @pytest.mark.parametrize("seed", range(8))

@@ -1519,7 +1519,22 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
         struct KeyHash {
             size_t operator()(const std::string& k) const { return std::hash<std::string>()(k); }
         };
-        std::unordered_map<std::string, int32_t, KeyHash> shape_id, cls_id;
+        struct ShapeKey {
+            int64_t c, m, e;
+            uint32_t z;
+            bool operator==(const ShapeKey& o) const { return c == o.c && m == o.m && e == o.e && z == o.z; }
+        };
+        struct ShapeHash {
+            size_t operator()(const ShapeKey& k) const {
+                uint64_t h = (uint64_t)k.c * 0x9E3779B97F4A7C15ull;
+                h ^= (uint64_t)k.m + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
+                h ^= (uint64_t)k.e * 0xC2B2AE3D27D4EB4Full + (h << 6) + (h >> 2);
+                return (size_t)(h ^ k.z);
+            }
+        };
+        std::unordered_map<ShapeKey, int32_t, ShapeHash> shape_id;   // (no per-pod allocation)
+        std::unordered_map<std::string, int32_t, KeyHash> cls_id;
+        shape_id.reserve(256);
         fb_pods.resize((size_t)n);
         const ca_pod_spec* prev = nullptr;               // pods of one controller variant come in a row
         std::vector<int32_t> cls_seen((size_t)n_classes, -1);              // a similar class's first position
@@ -1542,8 +1557,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
             prev = &ps;
             const uint32_t f = pod_dev_flags(ps);
             if (f & (PF_PORTS | PF_SCALAR_REQ | PF_PREFILTER_NAMES)) { fb = false; break; }
-            std::string sk(reinterpret_cast<const char*>(&ps.req_milli_cpu), 24);
-            sk.push_back((f & PF_ALL_ZERO) ? 1 : 0);
+            const ShapeKey sk{ps.req_milli_cpu, ps.req_memory, ps.req_ephemeral, (f & PF_ALL_ZERO) ? 1u : 0u};
             auto it = shape_id.find(sk);
             if (it == shape_id.end()) {
                 if ((int32_t)shape_id.size() >= FB_COLLECT_SHAPES) { fb = false; break; }

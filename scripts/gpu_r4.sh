@@ -15,6 +15,14 @@ if [[ "$STEP" == all || "$STEP" == planprof ]]; then
   timeout -k 10 200 python -u scripts/plan_prof.py 5000 --prof > gpurun_out/plan_prof.log 2>&1 || { echo PLANPROF FAILED; tail -20 gpurun_out/plan_prof.log; exit 1; }
   cat gpurun_out/plan_prof.log
 fi
+if [[ "$STEP" == all || "$STEP" == bench ]]; then
+  timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCH FAILED; tail -20 gpurun_out/bench.err; exit 1; }
+  python3 scripts/bench_summary.py gpurun_out/bench.json 2>/dev/null || head -c 3000 gpurun_out/bench.json
+fi
+if [[ "$STEP" == all || "$STEP" == filter ]]; then
+  timeout -k 10 300 python -u scripts/filter_timing.py --phases c5-loose-nohints c5-loose c5 > gpurun_out/filter_timing.log 2>&1 || { echo FILTER TIMING FAILED; tail -20 gpurun_out/filter_timing.log; exit 1; }
+  grep -v "^\[" gpurun_out/filter_timing.log | tail -5
+fi
 if [[ "$STEP" == all || "$STEP" == pmc ]]; then
   for c in FETCH_SIZE WRITE_SIZE; do
     cd /tmp && PMC_STEPS=3 PMC_LEGS=all timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$c" -o run \

@@ -562,9 +562,10 @@ __global__ void __launch_bounds__(256) k_emit_runs(const GroupMeta* __restrict__
     const int lane = threadIdx.x & 63;
     if (base + (int32_t)(threadIdx.x & ~63u) >= gm.count) return;   // whole wave past the end
     bool head = true;
+    StreamPod sp = {};
     if (i < gm.count) {
         const int32_t r = run_rank(st, U, i);
-        StreamPod sp = rsp[(size_t)gi * U + r];
+        sp = rsp[(size_t)gi * U + r];
         const bool bat = (sp.flags & SF_BATCH) != 0;
         if (i > 0 && bat) {
             head = false;
@@ -575,10 +576,13 @@ __global__ void __launch_bounds__(256) k_emit_runs(const GroupMeta* __restrict__
             }
         }
         sp.flags |= head ? SF_HEAD : 0u;
-        out[gm.off + i] = sp;
     }
     const uint64_t hb = __ballot(head);
     if (lane == 0) heads[gm.moff + (i >> 6)] = hb;
+    // The chain reads a stream entry only at a run head or inside a non-batchable run (whose
+    // every pod is a head), and only from the 64-entry window holding it: windows without a
+    // head are never read, so they are not written (C2: ~1 window in 10 has a head).
+    if (hb != 0 && i < gm.count) out[gm.off + i] = sp;
 }
 
 // 1''-2''. Go 1.19 sort.Slice order (binpacking_estimator.go:74; pdqsort.h) ----------

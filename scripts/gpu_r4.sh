@@ -23,6 +23,13 @@ if [[ "$STEP" == all || "$STEP" == filter ]]; then
   timeout -k 10 300 python -u scripts/filter_timing.py --phases c5-loose-nohints c5-loose c5 > gpurun_out/filter_timing.log 2>&1 || { echo FILTER TIMING FAILED; tail -20 gpurun_out/filter_timing.log; exit 1; }
   grep -v "^\[" gpurun_out/filter_timing.log | tail -5
 fi
+if [[ "$STEP" == all || "$STEP" == multi ]]; then
+  # N = 2 rehearsal of the weak-scaling path on the one GPU (two ranks share it; gloo collectives)
+  CASIM_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+     --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 \
+     > gpurun_out/multi2.json 2> gpurun_out/multi2.err || { echo MULTI FAILED; tail -20 gpurun_out/multi2.err; exit 1; }
+  tail -c 1500 gpurun_out/multi2.json
+fi
 if [[ "$STEP" == all || "$STEP" == pmc ]]; then
   for c in FETCH_SIZE WRITE_SIZE; do
     cd /tmp && PMC_STEPS=3 PMC_LEGS=all timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$c" -o run \

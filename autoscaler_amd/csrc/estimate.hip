@@ -549,7 +549,7 @@ __device__ inline int32_t run_rank(const int32_t* __restrict__ st, int32_t U, in
 __global__ void __launch_bounds__(256) k_emit_runs(const GroupMeta* __restrict__ groups,
                                                   const int32_t* __restrict__ rstart, const StreamPod* __restrict__ rsp,
                                                   int32_t U, StreamPod* __restrict__ out, uint64_t* __restrict__ heads,
-                                                  const int32_t* __restrict__ gmap) {
+                                                  const int32_t* __restrict__ gmap, int32_t all_windows) {
     __shared__ int32_t st[CLS_MAX + 1];
     const int gi = GSEL(blockIdx.y);
     const GroupMeta gm = groups[gi];
@@ -579,10 +579,11 @@ __global__ void __launch_bounds__(256) k_emit_runs(const GroupMeta* __restrict__
     }
     const uint64_t hb = __ballot(head);
     if (lane == 0) heads[gm.moff + (i >> 6)] = hb;
-    // The chain reads a stream entry only at a run head or inside a non-batchable run (whose
-    // every pod is a head), and only from the 64-entry window holding it: windows without a
-    // head are never read, so they are not written (C2: ~1 window in 10 has a head).
-    if (hb != 0 && i < gm.count) out[gm.off + i] = sp;
+    // With run batching the chain reads a stream entry only at a run head or inside a
+    // non-batchable run (whose every pod is a head), and only from the 64-entry window
+    // holding it: windows without a head are never read, so they are not written (C2: ~1
+    // window in 10 has a head).  The per-pod chain (CASIM_RUN_BATCH=0) reads every window.
+    if ((hb != 0 || all_windows) && i < gm.count) out[gm.off + i] = sp;
 }
 
 // 1''-2''. Go 1.19 sort.Slice order (binpacking_estimator.go:74; pdqsort.h) ----------
@@ -2631,7 +2632,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                 if (events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], ss));
                 hipLaunchKernelGGL(k_emit_runs, dim3(blocks, ng), dim3(256), 0, ss, p->d_meta.as<GroupMeta>(),
                                    p->d_rstart.as<int32_t>(), p->d_rsp.as<StreamPod>(), U, p->d_stream.as<StreamPod>(),
-                                   p->d_heads.as<uint64_t>(), gm);
+                                   p->d_heads.as<uint64_t>(), gm, batch_runs ? 0 : 1);
                 CA_HIP_CHECK(hipGetLastError());
                 return CA_OK;
             }

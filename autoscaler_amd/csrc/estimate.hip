@@ -481,18 +481,30 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     for (int i = tid; i < U; i += 1024) { cnt[i] = 0; rc[i] = 0; }
     __syncthreads();
-    // class counts: the lanes of a wave holding one class add once (controllers come in runs)
-    for (int32_t base = 0; base < gm.count; base += 1024) {
-        const int32_t i = base + tid;
-        const bool valid = i < gm.count;
-        const int32_t c = valid ? pcls[pod_idx[gm.off + i]] : -1;
-        uint64_t act = __ballot(valid);
-        while (act) {
-            const int l = __builtin_ctzll(act);
-            const int32_t cl = __builtin_amdgcn_readlane(c, l);
-            const uint64_t m = __ballot(valid && c == cl) & act;
-            if (lane == l) atomicAdd(&cnt[cl], __builtin_popcountll(m));
-            act &= ~m;
+    // class counts: the lanes of a wave holding one class add once (controllers come in
+    // runs); the gathers of RUB positions per thread are in flight together
+    constexpr int RUB = 8;
+    for (int32_t base = 0; base < gm.count; base += 1024 * RUB) {
+        int32_t pi[RUB], cv[RUB];
+#pragma unroll
+        for (int u = 0; u < RUB; u++) {
+            const int32_t i = base + u * 1024 + tid;
+            pi[u] = i < gm.count ? pod_idx[gm.off + i] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < RUB; u++) cv[u] = pi[u] >= 0 ? pcls[pi[u]] : -1;
+#pragma unroll
+        for (int u = 0; u < RUB; u++) {
+            const bool valid = pi[u] >= 0;
+            const int32_t c = cv[u];
+            uint64_t act = __ballot(valid);
+            while (act) {
+                const int l = __builtin_ctzll(act);
+                const int32_t cl = __builtin_amdgcn_readlane(c, l);
+                const uint64_t m = __ballot(valid && c == cl) & act;
+                if (lane == l) atomicAdd(&cnt[cl], __builtin_popcountll(m));
+                act &= ~m;
+            }
         }
     }
     __syncthreads();
@@ -602,6 +614,7 @@ __host__ __device__ inline size_t pdq_lds_bytes(int32_t lds_n) {
     return (3 * np + np / 8 + 2 * (np / 64 + 1) + 15) & ~(size_t)15;
 }
 
+constexpr int PDQ_UB = 8;              // list positions per thread whose gathers are in flight together
 __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restrict__ groups,
                                                      const int32_t* __restrict__ pod_idx,
                                                      const int32_t* __restrict__ pcls,
@@ -629,11 +642,33 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
     uint64_t* rmb = reinterpret_cast<uint64_t*>(pdq_dyn + 3 * npad);
     uint16_t* rmp = reinterpret_cast<uint16_t*>(rmb + npad / 64);
     uint32_t rmax = 0;
-    for (int32_t i = tid; i < n; i += pdq::NT) {
-        const uint32_t r = item_rank ? item_rank[off + i] : (uint32_t)crank[(size_t)gi * U + pcls[pod_idx[off + i]]];
-        rmax = max(rmax, r);
-        scr[i] = r;
-        if (fit) { e16[i] = (uint16_t)i; rk[i] = (uint8_t)r; }
+    // the ranks of the list: a chain of three dependent gathers per position (list -> pod ->
+    // class -> rank), issued PDQ_UB positions at a time so their latencies overlap
+    for (int32_t i0 = tid; i0 < n; i0 += pdq::NT * PDQ_UB) {
+        uint32_t r[PDQ_UB];
+        if (item_rank) {
+#pragma unroll
+            for (int u = 0; u < PDQ_UB; u++) { const int32_t i = i0 + u * pdq::NT; r[u] = i < n ? item_rank[off + i] : 0u; }
+        } else {
+            int32_t pi[PDQ_UB], cl[PDQ_UB];
+#pragma unroll
+            for (int u = 0; u < PDQ_UB; u++) { const int32_t i = i0 + u * pdq::NT; pi[u] = i < n ? pod_idx[off + i] : 0; }
+#pragma unroll
+            for (int u = 0; u < PDQ_UB; u++) { const int32_t i = i0 + u * pdq::NT; cl[u] = i < n ? pcls[pi[u]] : 0; }
+#pragma unroll
+            for (int u = 0; u < PDQ_UB; u++) {
+                const int32_t i = i0 + u * pdq::NT;
+                r[u] = i < n ? (uint32_t)crank[(size_t)gi * U + cl[u]] : 0u;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < PDQ_UB; u++) {
+            const int32_t i = i0 + u * pdq::NT;
+            if (i >= n) break;
+            rmax = max(rmax, r[u]);
+            scr[i] = r[u];
+            if (fit) { e16[i] = (uint16_t)i; rk[i] = (uint8_t)r[u]; }
+        }
     }
     for (int d = 32; d >= 1; d >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, d, 64));
     if ((tid & 63) == 0) atomicMax(&ctl.rmax, rmax);
@@ -646,9 +681,21 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
     if (mode == 1) {
         const pdq::LdsStore st{e16, rk, rmb, rmp};
         pdq::wg_sort(st, n, stack, n / 2 + 2, scr, ctl, limit0);
-        if (ids_out)                                   // decoupled Go order: the ids themselves
-            for (int32_t k = tid; k < n; k += pdq::NT) ids_out[off + k] = pod_idx[off + e16[k]];
-        else
+        if (ids_out) {                                 // decoupled Go order: the ids themselves
+            for (int32_t k0 = tid; k0 < n; k0 += pdq::NT * PDQ_UB) {
+                int32_t v[PDQ_UB];
+#pragma unroll
+                for (int u = 0; u < PDQ_UB; u++) {
+                    const int32_t k = k0 + u * pdq::NT;
+                    v[u] = k < n ? pod_idx[off + e16[k]] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < PDQ_UB; u++) {
+                    const int32_t k = k0 + u * pdq::NT;
+                    if (k < n) ids_out[off + k] = v[u];
+                }
+            }
+        } else
             for (int32_t k = tid; k < n; k += pdq::NT) sorted[off + k] = e16[k];
     } else if (mode == 2) {
         uint32_t* e = reinterpret_cast<uint32_t*>(gE + off);

@@ -276,17 +276,11 @@ constexpr int RTHREADS = 256;
 constexpr int RPT = RT / RTHREADS;     // items per thread
 constexpr int RCH = RT / 64 / (RTHREADS / 64);   // 64-item chunks per wave
 
-__global__ void __launch_bounds__(1024) k_class_rank(const GroupMeta* __restrict__ groups,
-                                                    const ca_template* __restrict__ tmpls,
-                                                    const int64_t* __restrict__ cls_sc, int32_t U, int32_t NP,
-                                                    int32_t* __restrict__ crank,
-    const int32_t* __restrict__ gmap) {
-    __shared__ uint64_t key[CLS_MAX];
-    __shared__ uint32_t idx[CLS_MAX];
-    __shared__ int32_t sc[CLS_MAX];
-    const int gi = GSEL(blockIdx.x);
-    const GroupMeta gm = groups[gi];
-    const ca_template& tp = tmpls[gm.tmpl];
+// Dense ranks of the U score classes against a group's template, by one 1024-thread
+// workgroup: float64 score of every class, bitonic sort of the classes in LDS, dense rank
+// (equal scores share a rank).  On return sc[i] is the rank of class idx[i], i < U.
+__device__ inline void block_class_rank(const ca_template& tp, const int64_t* __restrict__ cls_sc, int32_t U,
+                                        int32_t NP, uint64_t* key, uint32_t* idx, int32_t* sc) {
     const int64_t acpu = tp.node.alloc_milli_cpu, amem = tp.node.alloc_memory;
     for (int i = threadIdx.x; i < NP; i += blockDim.x) {
         uint64_t k = ~0ull;
@@ -329,6 +323,19 @@ __global__ void __launch_bounds__(1024) k_class_rank(const GroupMeta* __restrict
         for (int i = threadIdx.x; i < NP; i += blockDim.x) sc[i] += v[n++];
         __syncthreads();
     }
+}
+
+__global__ void __launch_bounds__(1024) k_class_rank(const GroupMeta* __restrict__ groups,
+                                                    const ca_template* __restrict__ tmpls,
+                                                    const int64_t* __restrict__ cls_sc, int32_t U, int32_t NP,
+                                                    int32_t* __restrict__ crank,
+    const int32_t* __restrict__ gmap) {
+    __shared__ uint64_t key[CLS_MAX];
+    __shared__ uint32_t idx[CLS_MAX];
+    __shared__ int32_t sc[CLS_MAX];
+    const int gi = GSEL(blockIdx.x);
+    const GroupMeta gm = groups[gi];
+    block_class_rank(tmpls[gm.tmpl], cls_sc, U, NP, key, idx, sc);
     for (int i = threadIdx.x; i < U; i += blockDim.x) crank[(size_t)gi * U + idx[i]] = sc[i];
 }
 
@@ -466,7 +473,8 @@ __global__ void __launch_bounds__(RTHREADS) k_radix_scatter(const GroupMeta* __r
 // stream positions and the consumers map them through the Go-order ids.
 __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict__ groups,
                                                    const int32_t* __restrict__ pod_idx, const int32_t* __restrict__ pcls,
-                                                   const int32_t* __restrict__ crank, const int32_t* __restrict__ cls_rep,
+                                                   const int64_t* __restrict__ cls_sc, int32_t NP,
+                                                   const int32_t* __restrict__ cls_rep,
                                                    int32_t U, const ca_template* __restrict__ tmpls,
                                                    const PodHot* __restrict__ ph, const ca_pod_spec* __restrict__ specs,
                                                    const ca_selector_term* __restrict__ terms,
@@ -475,10 +483,16 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
                                                    const int32_t* __restrict__ gmap) {
     __shared__ int32_t cnt[CLS_MAX];
     __shared__ int32_t rc[CLS_MAX];
+    __shared__ int32_t cr[CLS_MAX];           // rank of each class
+    __shared__ uint64_t key[CLS_MAX];
+    __shared__ uint32_t idx[CLS_MAX];
     __shared__ int32_t wsum[16];
     const int gi = GSEL(blockIdx.x);
     const GroupMeta gm = groups[gi];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    block_class_rank(tmpls[gm.tmpl], cls_sc, U, NP, key, idx, rc);      // (rc: scratch for the ranks)
+    for (int i = tid; i < U; i += 1024) cr[idx[i]] = rc[i];
+    __syncthreads();
     for (int i = tid; i < U; i += 1024) { cnt[i] = 0; rc[i] = 0; }
     __syncthreads();
     // class counts: the lanes of a wave holding one class add once (controllers come in
@@ -508,7 +522,6 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
         }
     }
     __syncthreads();
-    const int32_t* cr = crank + (size_t)gi * U;
     for (int c = tid; c < U; c += 1024)
         if (cnt[c] > 0) atomicAdd(&rc[cr[c]], cnt[c]);
     __syncthreads();
@@ -2664,14 +2677,13 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         // emission for `ng` groups (map `gm`)
         // (by value: the light groups' call runs after this block's locals are gone)
         auto sort_groups = [=](hipStream_t ss, const int32_t* gm, int32_t ng, bool events) -> int {
-            hipLaunchKernelGGL(k_class_rank, dim3(ng), dim3(1024), 0, ss, p->d_meta.as<GroupMeta>(),
-                               p->d_tmpl.as<ca_template>(), p->s->d_cls_sc.as<int64_t>(), U, NP, crank, gm);
-            CA_HIP_CHECK(hipGetLastError());
-            if (events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], ss));
             if (decoupled && runs_stream) {
-                // the stream from per-class counts (no sort of the pod lists)
+                // the stream from per-class counts (no sort of the pod lists; the class ranks
+                // are computed inside k_run_table)
+                if (events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], ss));
                 hipLaunchKernelGGL(k_run_table, dim3(ng), dim3(1024), 0, ss, p->d_meta.as<GroupMeta>(),
-                                   p->d_pod_idx.as<int32_t>(), pcls, crank, p->s->d_cls_rep.as<int32_t>(), U,
+                                   p->d_pod_idx.as<int32_t>(), pcls, p->s->d_cls_sc.as<int64_t>(), NP,
+                                   p->s->d_cls_rep.as<int32_t>(), U,
                                    p->d_tmpl.as<ca_template>(), p->s->t.hot.as<PodHot>(), p->s->t.spec.as<ca_pod_spec>(),
                                    p->s->t.terms.as<ca_selector_term>(), p->s->t.reqs.as<ca_selector_req>(),
                                    p->d_rstart.as<int32_t>(), p->d_rsp.as<StreamPod>(), p->d_unsup.as<uint32_t>(), gm);
@@ -2683,6 +2695,10 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                 CA_HIP_CHECK(hipGetLastError());
                 return CA_OK;
             }
+            hipLaunchKernelGGL(k_class_rank, dim3(ng), dim3(1024), 0, ss, p->d_meta.as<GroupMeta>(),
+                               p->d_tmpl.as<ca_template>(), p->s->d_cls_sc.as<int64_t>(), U, NP, crank, gm);
+            CA_HIP_CHECK(hipGetLastError());
+            if (events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], ss));
             uint32_t* a = nullptr;                        // identity (position order)
             uint32_t* bufs[2] = {p->d_sortA.as<uint32_t>(), p->d_sortB.as<uint32_t>()};
             if (go_order && !decoupled) {

@@ -25,8 +25,10 @@ def load(root: str, counter: str) -> dict:
     return out
 
 
-def main(root: str, steps: int, what: str = "scripts/pmc_step.py PMC_LEGS=all (C2 Estimate steps with results in HBM, "
-                                           "C5 FilterOutSchedulable calls, fresh C3 sweeps)") -> None:
+def main(root: str, steps: int, what: str = "scripts/pmc_step.py PMC_LEGS=all (C2 Estimate headline steps: 16-bit ids "
+                                           "published into page-locked memory, decoupled Go order; C5 "
+                                           "FilterOutSchedulable calls; fresh C3 sweeps; C3 planner loops "
+                                           "without a limit)") -> None:
     fetch = load(root, "FETCH_SIZE")
     write = load(root, "WRITE_SIZE")
     res = {}

@@ -472,7 +472,7 @@ __global__ void __launch_bounds__(RTHREADS) k_radix_scatter(const GroupMeta* __r
 // non-batchable pod).  The pod id of a stream entry is not needed: decoupled chains emit
 // stream positions and the consumers map them through the Go-order ids.
 __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict__ groups,
-                                                   const int32_t* __restrict__ pod_idx, const int32_t* __restrict__ pcls,
+                                                   const int32_t* __restrict__ item_cls,
                                                    const int64_t* __restrict__ cls_sc, int32_t NP,
                                                    const int32_t* __restrict__ cls_rep,
                                                    int32_t U, const ca_template* __restrict__ tmpls,
@@ -499,17 +499,15 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
     // runs); the gathers of RUB positions per thread are in flight together
     constexpr int RUB = 8;
     for (int32_t base = 0; base < gm.count; base += 1024 * RUB) {
-        int32_t pi[RUB], cv[RUB];
+        int32_t cv[RUB];
 #pragma unroll
         for (int u = 0; u < RUB; u++) {
             const int32_t i = base + u * 1024 + tid;
-            pi[u] = i < gm.count ? pod_idx[gm.off + i] : -1;
+            cv[u] = i < gm.count ? item_cls[gm.off + i] : -1;
         }
 #pragma unroll
-        for (int u = 0; u < RUB; u++) cv[u] = pi[u] >= 0 ? pcls[pi[u]] : -1;
-#pragma unroll
         for (int u = 0; u < RUB; u++) {
-            const bool valid = pi[u] >= 0;
+            const bool valid = cv[u] >= 0;
             const int32_t c = cv[u];
             uint64_t act = __ballot(valid);
             while (act) {
@@ -637,7 +635,7 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
                                                      uint64_t* __restrict__ xs_all, pdq::Frame* __restrict__ stack_all,
                                                      int32_t lds_n, int32_t force, int32_t limit0, const int32_t* __restrict__ gmap,
                                                      int32_t* __restrict__ ids_out, int32_t* __restrict__ ids_ready,
-                                                     int32_t ids_epoch) {
+                                                     int32_t ids_epoch, const int32_t* __restrict__ item_cls) {
     extern __shared__ __align__(16) unsigned char pdq_dyn[];
     __shared__ pdq::Ctl ctl;
     const int gi = GSEL(blockIdx.x);
@@ -664,10 +662,15 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
             for (int u = 0; u < PDQ_UB; u++) { const int32_t i = i0 + u * pdq::NT; r[u] = i < n ? item_rank[off + i] : 0u; }
         } else {
             int32_t pi[PDQ_UB], cl[PDQ_UB];
+            if (item_cls) {
 #pragma unroll
-            for (int u = 0; u < PDQ_UB; u++) { const int32_t i = i0 + u * pdq::NT; pi[u] = i < n ? pod_idx[off + i] : 0; }
+                for (int u = 0; u < PDQ_UB; u++) { const int32_t i = i0 + u * pdq::NT; cl[u] = i < n ? item_cls[off + i] : 0; }
+            } else {
 #pragma unroll
-            for (int u = 0; u < PDQ_UB; u++) { const int32_t i = i0 + u * pdq::NT; cl[u] = i < n ? pcls[pi[u]] : 0; }
+                for (int u = 0; u < PDQ_UB; u++) { const int32_t i = i0 + u * pdq::NT; pi[u] = i < n ? pod_idx[off + i] : 0; }
+#pragma unroll
+                for (int u = 0; u < PDQ_UB; u++) { const int32_t i = i0 + u * pdq::NT; cl[u] = i < n ? pcls[pi[u]] : 0; }
+            }
 #pragma unroll
             for (int u = 0; u < PDQ_UB; u++) {
                 const int32_t i = i0 + u * pdq::NT;
@@ -2162,6 +2165,7 @@ struct ca_estimate_plan {
     // permutation; d_ids_ready: per group, the run epoch whose ids are final there)
     DevBuf d_sortC, d_ids_ready, d_spod_go, d_crank2;
     DevBuf d_rstart, d_rsp;        // decoupled: per group, each rank's first stream position and record
+    DevBuf d_item_cls;             // bucket path: the score class of every (group, pod) item, uploaded with the lists
     int32_t ids_epoch = 0;
     hipStream_t st3 = nullptr;
     hipEvent_t ev_emitA = nullptr, ev_emitB = nullptr, ev_ids = nullptr;
@@ -2182,6 +2186,7 @@ struct ca_estimate_plan {
     float t_ms[7] = {};
     int32_t pub_state = 0;         // last run: 0 results copied, 1 published zero-copy, 2 publisher gave up
     int32_t ran_decoupled = 0;     // last run took the decoupled Go order
+    bool phase_events = true;      // record the per-phase timing events (ca_estimate_plan_set_phase_timing)
     std::vector<uint64_t> diag;     // per group: chain ticks (100 MHz) | single-pod steps << 32
     std::vector<uint8_t> grp_succ;  // last run, per group: a FitsAnyNode call succeeded (moved lastIndex)
     // zero-copy publishing (k_publish on its own stream, concurrent with the chains)
@@ -2416,6 +2421,15 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     }
     if (G) CA_HIP_CHECK(hipMemcpyAsync(p->d_meta.ptr, p->h_meta.data(), sizeof(GroupMeta) * G, hipMemcpyHostToDevice, st));
     if (p->total) CA_HIP_CHECK(hipMemcpyAsync(p->d_pod_idx.ptr, pod_idx, sizeof(int32_t) * p->total, hipMemcpyHostToDevice, st));
+    std::vector<int32_t> item_cls;
+    if (p->bucket && p->total > 0) {
+        // the lists as (pod, class) pairs: the class of every item next to its pod index, so
+        // the sorts and the run table read it in one coalesced load instead of two gathers
+        item_cls.resize((size_t)p->total);
+        for (int32_t i = 0; i < p->total; i++) item_cls[i] = s->h_cls[pod_idx[i]];
+        if ((rc = p->d_item_cls.reserve(sizeof(int32_t) * (size_t)p->total)) != CA_OK) return rc;
+        CA_HIP_CHECK(hipMemcpyAsync(p->d_item_cls.ptr, item_cls.data(), sizeof(int32_t) * p->total, hipMemcpyHostToDevice, st));
+    }
     if (G) CA_HIP_CHECK(hipMemcpyAsync(p->d_tmpl.ptr, templates, sizeof(ca_template) * G, hipMemcpyHostToDevice, st));
     CA_HIP_CHECK(hipStreamSynchronize(st));
     return CA_OK;
@@ -2473,7 +2487,8 @@ int launch_pdq_sort(ca_estimate_plan* p, hipStream_t ss, const int32_t* gm, int3
     hipLaunchKernelGGL(k_pdq_sort, dim3(ng), dim3(pdq::NT), lds, ss, p->d_meta.as<GroupMeta>(),
                        p->d_pod_idx.as<int32_t>(), p->s ? p->s->d_cls.as<int32_t>() : nullptr, crank, U, item_rank,
                        out ? out : p->d_sortA.as<uint32_t>(), p->d_pdq_e.as<uint64_t>(), p->d_pdq_scr.as<uint64_t>(),
-                       p->d_pdq_stack.as<pdq::Frame>(), lds_n, force, 0, gm, ids_out, ids_ready, ids_epoch);
+                       p->d_pdq_stack.as<pdq::Frame>(), lds_n, force, 0, gm, ids_out, ids_ready, ids_epoch,
+                       (p->bucket && crank && !item_rank) ? p->d_item_cls.as<int32_t>() : nullptr);
     CA_HIP_CHECK(hipGetLastError());
     return CA_OK;
 }
@@ -2597,7 +2612,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             return rc0;
         CA_HIP_CHECK(hipEventRecord(p->ev_ids, p->st3));
     }
-    CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_START], st));
+    if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_START], st));
     {
         const int32_t n = std::max(G, tickets1);
         hipLaunchKernelGGL(k_round_init, dim3(std::min((n + 255) / 256, 64)), dim3(256), 0, st, G, *last_index,
@@ -2680,15 +2695,15 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             if (decoupled && runs_stream) {
                 // the stream from per-class counts (no sort of the pod lists; the class ranks
                 // are computed inside k_run_table)
-                if (events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], ss));
+                if (events && p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], ss));
                 hipLaunchKernelGGL(k_run_table, dim3(ng), dim3(1024), 0, ss, p->d_meta.as<GroupMeta>(),
-                                   p->d_pod_idx.as<int32_t>(), pcls, p->s->d_cls_sc.as<int64_t>(), NP,
+                                   p->d_item_cls.as<int32_t>(), p->s->d_cls_sc.as<int64_t>(), NP,
                                    p->s->d_cls_rep.as<int32_t>(), U,
                                    p->d_tmpl.as<ca_template>(), p->s->t.hot.as<PodHot>(), p->s->t.spec.as<ca_pod_spec>(),
                                    p->s->t.terms.as<ca_selector_term>(), p->s->t.reqs.as<ca_selector_req>(),
                                    p->d_rstart.as<int32_t>(), p->d_rsp.as<StreamPod>(), p->d_unsup.as<uint32_t>(), gm);
                 CA_HIP_CHECK(hipGetLastError());
-                if (events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], ss));
+                if (events && p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], ss));
                 hipLaunchKernelGGL(k_emit_runs, dim3(blocks, ng), dim3(256), 0, ss, p->d_meta.as<GroupMeta>(),
                                    p->d_rstart.as<int32_t>(), p->d_rsp.as<StreamPod>(), U, p->d_stream.as<StreamPod>(),
                                    p->d_heads.as<uint64_t>(), gm, batch_runs ? 0 : 1);
@@ -2698,7 +2713,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             hipLaunchKernelGGL(k_class_rank, dim3(ng), dim3(1024), 0, ss, p->d_meta.as<GroupMeta>(),
                                p->d_tmpl.as<ca_template>(), p->s->d_cls_sc.as<int64_t>(), U, NP, crank, gm);
             CA_HIP_CHECK(hipGetLastError());
-            if (events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], ss));
+            if (events && p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], ss));
             uint32_t* a = nullptr;                        // identity (position order)
             uint32_t* bufs[2] = {p->d_sortA.as<uint32_t>(), p->d_sortB.as<uint32_t>()};
             if (go_order && !decoupled) {
@@ -2720,7 +2735,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                 CA_HIP_CHECK(hipGetLastError());
                 a = b;
             }
-            if (events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], ss));
+            if (events && p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], ss));
             hipLaunchKernelGGL(k_emit_bucket, dim3(blocks, ng), dim3(256), 0, ss, p->d_meta.as<GroupMeta>(), a,
                                p->d_pod_idx.as<int32_t>(), p->d_tmpl.as<ca_template>(), p->s->t.hot.as<PodHot>(),
                                p->s->t.spec.as<ca_pod_spec>(), p->s->t.terms.as<ca_selector_term>(),
@@ -2747,7 +2762,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                            p->s->t.spec.as<ca_pod_spec>(), p->s->t.terms.as<ca_selector_term>(),
                            p->s->t.reqs.as<ca_selector_req>(), p->d_sortA.as<SortItem>(), p->d_unsup.as<uint32_t>());
         CA_HIP_CHECK(hipGetLastError());
-        CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], st));
+        if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_SCORE], st));
         SortItem* a = p->d_sortA.as<SortItem>();
         SortItem* b = p->d_sortB.as<SortItem>();
         const int32_t blocks = (p->max_count + 255) / 256;
@@ -2765,7 +2780,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             if ((rc0 = launch_pdq_sort(p, st, nullptr, G, nullptr, 0, p->d_item_rank.as<uint32_t>())) != CA_OK)
                 return rc0;
         }
-        CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], st));
+        if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], st));
         if (go_order) {
             hipLaunchKernelGGL(k_emit_bucket, dim3(blocks, G), dim3(256), 0, st, p->d_meta.as<GroupMeta>(),
                                p->d_sortA.as<uint32_t>(), p->d_pod_idx.as<int32_t>(), p->d_tmpl.as<ca_template>(),
@@ -2780,7 +2795,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         }
         CA_HIP_CHECK(hipGetLastError());
     }
-    CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_EMIT], st));
+    if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_EMIT], st));
     // 4-5: chains with lastIndex speculation
     std::vector<int32_t> lin(G, *last_index);
     std::vector<uint8_t> need(G, 1);
@@ -2831,7 +2846,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             if ((rc0 = launch_pub(st)) != CA_OK) return rc0;
             CA_HIP_CHECK(hipEventRecord(p->ev_pub, st));
         }
-        CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN0], st));
+        if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN0], st));
         if (!grows) {
             int rcl;
             if ((rcl = ensure_dyn_lds((const void*)k_ffd_chain<false>, lds)) != CA_OK) return rcl;
@@ -2867,7 +2882,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             if ((rc = launch_pub(p->pub_stream)) != CA_OK) return rc;
             CA_HIP_CHECK(hipEventRecord(p->ev_pub, p->pub_stream));
         }
-        CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN1], st));
+        if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN1], st));
         // one readback per round: the chain outputs, and (publishing) the publisher's
         // counters once it is done — the results are then already in the caller's buffer
         const ChainOut* fresh = p->h_out.as<ChainOut>();
@@ -2886,10 +2901,11 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                sched_node ? p->d_sched_node.as<int32_t>() : nullptr, 0);
             CA_HIP_CHECK(hipGetLastError());
         }
-        CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_COMPACT], st));
+        if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_COMPACT], st));
         CA_HIP_CHECK(hipEventSynchronize(p->ev_rb));
         float ms = 0;
-        (void)hipEventElapsedTime(&ms, p->ev[ca_estimate_plan::EV_CHAIN0], p->ev[ca_estimate_plan::EV_CHAIN1]);
+        if (p->phase_events)
+            (void)hipEventElapsedTime(&ms, p->ev[ca_estimate_plan::EV_CHAIN0], p->ev[ca_estimate_plan::EV_CHAIN1]);
         chain_ms += ms;
         for (int32_t g = 0; g < G; g++) if (need[g]) outs[g] = fresh[g];
         if (rounds == 1) {
@@ -2974,7 +2990,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     if (sched_node)
         CA_HIP_CHECK(hipMemcpyAsync(sched_node, p->d_sched_node.ptr, sizeof(int32_t) * std::max(p->total, 0),
                                     hipMemcpyDeviceToHost, st));
-    CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_D2H], st));
+    if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_D2H], st));
     CA_HIP_CHECK(hipStreamSynchronize(st));
     for (int32_t g = 0; g < G; g++) {
         const ChainOut& o = outs[g];
@@ -2996,7 +3012,11 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     float sort_ms = 0;
     {
         using P = ca_estimate_plan;
-        auto el = [&](int a, int b) { float v = 0; (void)hipEventElapsedTime(&v, p->ev[a], p->ev[b]); return v; };
+        auto el = [&](int a, int b) {
+            float v = 0;
+            if (p->phase_events) (void)hipEventElapsedTime(&v, p->ev[a], p->ev[b]);
+            return v;
+        };
         const bool any = p->total > 0;
         p->t_ms[0] = any ? el(P::EV_START, P::EV_SCORE) : 0;
         p->t_ms[1] = any ? el(P::EV_SCORE, P::EV_MERGE) : 0;
@@ -3108,6 +3128,12 @@ int ca_estimate_plan_timings(const ca_estimate_plan* p, float* out, int32_t cap)
     return n;
 }
 
+int ca_estimate_plan_set_phase_timing(ca_estimate_plan* p, int32_t on) {
+    if (!p) return CA_EINVAL;
+    p->phase_events = on != 0;
+    return CA_OK;
+}
+
 int ca_estimate_plan_group_ticks(const ca_estimate_plan* p, uint64_t* out, int32_t cap) {
     if (!p || (cap > 0 && !out)) return CA_EINVAL;
     const int32_t n = (int32_t)p->diag.size();
@@ -3154,7 +3180,8 @@ int ca_go_sort_ranks(int32_t device, const uint32_t* ranks, int32_t n, int32_t s
     if ((rc = ensure_dyn_lds((const void*)k_pdq_sort, lds)) != CA_OK) return rc;
     hipLaunchKernelGGL(k_pdq_sort, dim3(1), dim3(pdq::NT), lds, 0, meta.as<GroupMeta>(), nullptr, nullptr, nullptr, 0,
                        rk.as<uint32_t>(), sorted.as<uint32_t>(), e.as<uint64_t>(), scr.as<uint64_t>(),
-                       stack.as<pdq::Frame>(), lds_n, store, std::max(limit, 0), nullptr, nullptr, nullptr, 0);
+                       stack.as<pdq::Frame>(), lds_n, store, std::max(limit, 0), nullptr, nullptr, nullptr, 0,
+                       (const int32_t*)nullptr);
     CA_HIP_CHECK(hipGetLastError());
     CA_HIP_CHECK(hipMemcpy(perm, sorted.ptr, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost));
     return CA_OK;

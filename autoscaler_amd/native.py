@@ -80,6 +80,7 @@ def load() -> C.CDLL:
         "ca_estimate_plan_chain_info": ([vp, p(i32), p(i32)], C.c_int),
         "ca_go_sort_ranks": ([i32, vp, i32, i32, i32, vp], C.c_int),
         "ca_estimate_plan_timings": ([vp, p(C.c_float), i32], C.c_int),
+        "ca_estimate_plan_set_phase_timing": ([vp, i32], C.c_int),
         "ca_estimate_plan_group_ticks": ([vp, p(C.c_uint64), i32], C.c_int),
         "ca_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, p(i32), vp, vp], C.c_int),
         "ca_removal_stats": ([vp, p(i32), p(C.c_float), p(C.c_float)], C.c_int),
@@ -153,6 +154,7 @@ def exported_symbols() -> list[str]:
         "ca_fits_matrix", "ca_check_templates", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
         "ca_estimate_plan_run_u16",
         "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_estimate_plan_timings",
+        "ca_estimate_plan_set_phase_timing",
         "ca_estimate_plan_group_ticks", "ca_estimate_plan_fetch", "ca_estimate_plan_device_results",
         "ca_go_sort_ranks",
         "ca_find_nodes_to_remove",
@@ -750,6 +752,11 @@ class EstimatePlan:
                 "phases": {k: float(v) for k, v in zip(names, t)},
                 "results_path": ("copied", "published", "publisher_gave_up")[int(t[7])],
                 "decoupled": bool(t[8])}
+
+    def set_phase_timing(self, on: bool) -> None:
+        """Per-phase timing events on later runs (on by default; off keeps them off the
+        launch path — stats() phases then read 0)."""
+        _check(self.lib.ca_estimate_plan_set_phase_timing(self.h, 1 if on else 0), "ca_estimate_plan_set_phase_timing")
 
     def chain_info(self) -> tuple:
         """(lastIndex-sensitive, had a FitsAnyNode success) of the last run: one call."""

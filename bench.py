@@ -701,6 +701,9 @@ def main():
         return out, extra
 
     def timed(mode):
+        # the timed steps run without the library's per-phase timing events (8 event records
+        # per step on the host's launch path); the phases come from the untimed steps below
+        plan.set_phase_timing(False)
         for _ in range(args.warmup):
             step(mode)
         if dist is not None:
@@ -731,6 +734,7 @@ def main():
         host_pods = np.where(host_pods == 0xFFFF, -1, host_pods.astype(np.int32))
     # per-phase device times: the same steps again, untimed
     chain_ms, sort_ms, rounds, phases, pub = [], [], [], [], []
+    plan.set_phase_timing(True)
     for i in range(args.steps):
         step("host")
         st = plan.stats()

@@ -418,6 +418,10 @@ int ca_estimate_plan_stats(const ca_estimate_plan* p, int32_t* rounds, float* ch
  * order (chains on the stable class order, Go's ids beside them: uniform classes and no
  * two classes of a group with equal scores), else 0.  Writes min(cap, 9) values; returns 9. */
 int ca_estimate_plan_timings(const ca_estimate_plan* p, float* out, int32_t cap);
+/* Record the per-phase timing events of later runs (on: default) or not: 8 event records
+ * per run on the host's launch path; with them off, ca_estimate_plan_timings[0..5] and the
+ * chain time of ca_estimate_plan_stats read 0. */
+int ca_estimate_plan_set_phase_timing(ca_estimate_plan* p, int32_t on);
 /* Whether the last run's outputs depend on the lastIndex it started from (then a caller
  * that ran the batch from a guessed lastIndex must re-run it from the true one), and
  * whether any FitsAnyNode call succeeded (if not, lastIndex passed through unchanged).

@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <functional>
 #include <chrono>
+#include <mutex>
 #include <cstdlib>
 
 namespace casim {
@@ -2209,21 +2210,69 @@ struct ca_estimate_plan {
     DevBuf d_gmap;
     int32_t map_max_nodes = -1, n_heavy = 0;
     int32_t map_source = 0;        // 1: demand model, 2: the chains' measured times (previous run)
-    ~ca_estimate_plan() {
-        for (auto& e : ev) if (e) (void)hipEventDestroy(e);
-        if (ev_go) (void)hipEventDestroy(ev_go);
-        if (ev_pub) (void)hipEventDestroy(ev_pub);
-        if (pub_stream) (void)hipStreamDestroy(pub_stream);
-        if (st2) (void)hipStreamDestroy(st2);
-        if (st3) (void)hipStreamDestroy(st3);
-        if (ev_emitA) (void)hipEventDestroy(ev_emitA);
-        if (ev_emitB) (void)hipEventDestroy(ev_emitB);
-        if (ev_ids) (void)hipEventDestroy(ev_ids);
-        if (ev_init) (void)hipEventDestroy(ev_init);
-        if (ev_b) (void)hipEventDestroy(ev_b);
-        if (ev_rb) (void)hipEventDestroy(ev_rb);
-    }
+    int32_t res_device = -1;       // the streams and events below came from the pool of this device
+    ~ca_estimate_plan();
 };
+
+namespace casim {
+// Streams and events of an Estimate plan, kept per device after the plan is destroyed and
+// handed to the next plan (RunOnce builds a plan per loop: creating three streams and
+// sixteen events costs more than a loop's whole Estimate).  Every run synchronises before
+// it returns, so a released set is idle.
+struct PlanStreams {
+    hipStream_t pub = nullptr, st2 = nullptr, st3 = nullptr;
+    hipEvent_t ev[ca_estimate_plan::EV_N] = {};
+    hipEvent_t go = nullptr, pub_ev = nullptr, emitA = nullptr, emitB = nullptr, ids = nullptr, init = nullptr, b = nullptr,
+               rb = nullptr;
+};
+static std::mutex g_ps_mu;
+static std::vector<std::pair<int32_t, PlanStreams>> g_ps_pool;
+
+static int plan_streams_acquire(int32_t dev, PlanStreams& out) {
+    {
+        std::lock_guard<std::mutex> lk(g_ps_mu);
+        for (size_t i = 0; i < g_ps_pool.size(); i++)
+            if (g_ps_pool[i].first == dev) {
+                out = g_ps_pool[i].second;
+                g_ps_pool.erase(g_ps_pool.begin() + (ptrdiff_t)i);
+                return CA_OK;
+            }
+    }
+    PlanStreams ps;
+    for (auto& e : ps.ev) CA_HIP_CHECK(hipEventCreate(&e));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&ps.go, hipEventDisableTiming));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&ps.pub_ev, hipEventDisableTiming));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&ps.emitA, hipEventDisableTiming));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&ps.emitB, hipEventDisableTiming));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&ps.ids, hipEventDisableTiming));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&ps.init, hipEventDisableTiming));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&ps.b, hipEventDisableTiming));
+    CA_HIP_CHECK(hipEventCreateWithFlags(&ps.rb, hipEventDisableTiming));
+    CA_HIP_CHECK(hipStreamCreateWithFlags(&ps.pub, hipStreamNonBlocking));
+    int lo = 0, hi = 0;
+    CA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    CA_HIP_CHECK(hipStreamCreateWithPriority(&ps.st2, hipStreamNonBlocking, lo));   // light groups: lowest
+    CA_HIP_CHECK(hipStreamCreateWithPriority(&ps.st3, hipStreamNonBlocking, hi));   // Go-order sort: highest
+    out = ps;
+    return CA_OK;
+}
+}  // namespace casim
+
+ca_estimate_plan::~ca_estimate_plan() {
+    casim::PlanStreams ps;
+    for (int i = 0; i < EV_N; i++) ps.ev[i] = ev[i];
+    ps.go = ev_go; ps.pub_ev = ev_pub; ps.emitA = ev_emitA; ps.emitB = ev_emitB; ps.ids = ev_ids; ps.init = ev_init;
+    ps.b = ev_b; ps.rb = ev_rb;
+    ps.pub = pub_stream; ps.st2 = st2; ps.st3 = st3;
+    if (res_device >= 0 && pub_stream && st2 && st3) {
+        std::lock_guard<std::mutex> lk(casim::g_ps_mu);
+        casim::g_ps_pool.emplace_back(res_device, ps);
+        return;
+    }
+    for (auto& e : ps.ev) if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {ps.go, ps.pub_ev, ps.emitA, ps.emitB, ps.ids, ps.init, ps.b, ps.rb}) if (e) (void)hipEventDestroy(e);
+    for (hipStream_t q : {ps.pub, ps.st2, ps.st3}) if (q) (void)hipStreamDestroy(q);
+}
 
 namespace {
 
@@ -2277,26 +2326,16 @@ bool groups_tie_free(const ca_podset* s, const int32_t* pod_idx, const std::vect
 int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const int32_t* group_off,
                  const int32_t* pod_idx, const ca_template* templates, int32_t G) {
     p->m = m; p->s = s; p->G = G;
-    for (auto& e : p->ev) CA_HIP_CHECK(hipEventCreate(&e));
-    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_go, hipEventDisableTiming));
-    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_pub, hipEventDisableTiming));
-    CA_HIP_CHECK(hipStreamCreateWithFlags(&p->pub_stream, hipStreamNonBlocking));
     {
-        int lo = 0, hi = 0;                  // the light groups' stream at the lowest priority
-        CA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        CA_HIP_CHECK(hipStreamCreateWithPriority(&p->st2, hipStreamNonBlocking, lo));
+        PlanStreams ps;                      // (pooled per device: plan_streams_acquire)
+        int rc0;
+        if ((rc0 = plan_streams_acquire(m->device, ps)) != CA_OK) return rc0;
+        for (int i = 0; i < ca_estimate_plan::EV_N; i++) p->ev[i] = ps.ev[i];
+        p->ev_go = ps.go; p->ev_pub = ps.pub_ev; p->ev_emitA = ps.emitA; p->ev_emitB = ps.emitB; p->ev_ids = ps.ids;
+        p->ev_init = ps.init; p->ev_b = ps.b; p->ev_rb = ps.rb;
+        p->pub_stream = ps.pub; p->st2 = ps.st2; p->st3 = ps.st3;
+        p->res_device = m->device;
     }
-    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_init, hipEventDisableTiming));
-    {
-        int lo = 0, hi = 0;                  // the Go-order sort (decoupled): the highest priority
-        CA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        CA_HIP_CHECK(hipStreamCreateWithPriority(&p->st3, hipStreamNonBlocking, hi));
-    }
-    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_emitA, hipEventDisableTiming));
-    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_emitB, hipEventDisableTiming));
-    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_ids, hipEventDisableTiming));
-    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_b, hipEventDisableTiming));
-    CA_HIP_CHECK(hipEventCreateWithFlags(&p->ev_rb, hipEventDisableTiming));
     {
         int rc0;
         if ((rc0 = p->h_out.reserve(sizeof(ChainOut) * (size_t)std::max(G, 1))) != CA_OK) return rc0;

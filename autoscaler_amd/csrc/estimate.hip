@@ -636,7 +636,9 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
                                                      uint64_t* __restrict__ xs_all, pdq::Frame* __restrict__ stack_all,
                                                      int32_t lds_n, int32_t force, int32_t limit0, const int32_t* __restrict__ gmap,
                                                      int32_t* __restrict__ ids_out, int32_t* __restrict__ ids_ready,
-                                                     int32_t ids_epoch, const int32_t* __restrict__ item_cls) {
+                                                     int32_t ids_epoch, const int32_t* __restrict__ item_cls,
+                                                     const ca_template* __restrict__ tmpls,
+                                                     const int64_t* __restrict__ cls_sc, int32_t NP) {
     extern __shared__ __align__(16) unsigned char pdq_dyn[];
     __shared__ pdq::Ctl ctl;
     const int gi = GSEL(blockIdx.x);
@@ -653,6 +655,21 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
     uint8_t* rk = pdq_dyn + 2 * npad;
     uint64_t* rmb = reinterpret_cast<uint64_t*>(pdq_dyn + 3 * npad);
     uint16_t* rmp = reinterpret_cast<uint16_t*>(rmb + npad / 64);
+    // cls_sc != null: the class ranks are computed here (k_class_rank's work, one launch
+    // less on the sort's critical path): the bitonic scratch lives in the element store
+    // (free until the ranks are loaded), the rank of each class in the partition bitmap
+    // area (free until the first partition); the host checks both fit
+    const uint16_t* crk = nullptr;
+    if (cls_sc) {
+        uint64_t* key = reinterpret_cast<uint64_t*>(pdq_dyn);
+        uint32_t* idx = reinterpret_cast<uint32_t*>(pdq_dyn + 8 * (size_t)NP);
+        int32_t* scv = reinterpret_cast<int32_t*>(pdq_dyn + 12 * (size_t)NP);
+        block_class_rank(tmpls[gm.tmpl], cls_sc, U, NP, key, idx, scv);
+        uint16_t* w = reinterpret_cast<uint16_t*>(rmb);
+        for (int i = tid; i < U; i += pdq::NT) w[idx[i]] = (uint16_t)scv[i];
+        __syncthreads();
+        crk = w;
+    }
     uint32_t rmax = 0;
     // the ranks of the list: a chain of three dependent gathers per position (list -> pod ->
     // class -> rank), issued PDQ_UB positions at a time so their latencies overlap
@@ -675,7 +692,7 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
 #pragma unroll
             for (int u = 0; u < PDQ_UB; u++) {
                 const int32_t i = i0 + u * pdq::NT;
-                r[u] = i < n ? (uint32_t)crank[(size_t)gi * U + cl[u]] : 0u;
+                r[u] = i < n ? (crk ? (uint32_t)crk[cl[u]] : (uint32_t)crank[(size_t)gi * U + cl[u]]) : 0u;
             }
         }
 #pragma unroll
@@ -2518,7 +2535,8 @@ bool go_sort_order() {
 // or from item_rank
 int launch_pdq_sort(ca_estimate_plan* p, hipStream_t ss, const int32_t* gm, int32_t ng, const int32_t* crank,
                     int32_t U, const uint32_t* item_rank, int32_t force = 0, uint32_t* out = nullptr,
-                    int32_t* ids_out = nullptr, int32_t* ids_ready = nullptr, int32_t ids_epoch = 0) {
+                    int32_t* ids_out = nullptr, int32_t* ids_ready = nullptr, int32_t ids_epoch = 0,
+                    int32_t fold_np = 0) {
     const int32_t lds_n = std::min(p->max_count, PDQ_LDS_N);
     const size_t lds = pdq_lds_bytes(lds_n);
     int rc;
@@ -2527,7 +2545,8 @@ int launch_pdq_sort(ca_estimate_plan* p, hipStream_t ss, const int32_t* gm, int3
                        p->d_pod_idx.as<int32_t>(), p->s ? p->s->d_cls.as<int32_t>() : nullptr, crank, U, item_rank,
                        out ? out : p->d_sortA.as<uint32_t>(), p->d_pdq_e.as<uint64_t>(), p->d_pdq_scr.as<uint64_t>(),
                        p->d_pdq_stack.as<pdq::Frame>(), lds_n, force, 0, gm, ids_out, ids_ready, ids_epoch,
-                       (p->bucket && crank && !item_rank) ? p->d_item_cls.as<int32_t>() : nullptr);
+                       (p->bucket && crank && !item_rank) ? p->d_item_cls.as<int32_t>() : nullptr,
+                       p->d_tmpl.as<ca_template>(), fold_np > 0 ? p->s->d_cls_sc.as<int64_t>() : nullptr, fold_np);
     CA_HIP_CHECK(hipGetLastError());
     return CA_OK;
 }
@@ -2640,14 +2659,19 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             p->ids_epoch = 0;
         }
         p->ids_epoch++;
-        hipLaunchKernelGGL(k_class_rank, dim3(G), dim3(1024), 0, p->st3, p->d_meta.as<GroupMeta>(),
-                           p->d_tmpl.as<ca_template>(), p->s->d_cls_sc.as<int64_t>(), U, NP,
-                           p->d_crank2.as<int32_t>(), (const int32_t*)nullptr);
-        CA_HIP_CHECK(hipGetLastError());
+        // the class ranks inside the sort kernel when its LDS has room for the scratch
+        const size_t npad = ((size_t)std::min(p->max_count, PDQ_LDS_N) + 63) & ~(size_t)63;
+        const bool fold = 16 * (size_t)NP <= 3 * npad && 2 * (size_t)U <= npad / 8 && !getenv("CASIM_NO_RANK_FOLD");
+        if (!fold) {
+            hipLaunchKernelGGL(k_class_rank, dim3(G), dim3(1024), 0, p->st3, p->d_meta.as<GroupMeta>(),
+                               p->d_tmpl.as<ca_template>(), p->s->d_cls_sc.as<int64_t>(), U, NP,
+                               p->d_crank2.as<int32_t>(), (const int32_t*)nullptr);
+            CA_HIP_CHECK(hipGetLastError());
+        }
         int rc0;
         if ((rc0 = launch_pdq_sort(p, p->st3, nullptr, G, p->d_crank2.as<int32_t>(), U, nullptr, 0,
                                    p->d_sortC.as<uint32_t>(), p->d_spod_go.as<int32_t>(),
-                                   p->d_ids_ready.as<int32_t>(), p->ids_epoch)) != CA_OK)
+                                   p->d_ids_ready.as<int32_t>(), p->ids_epoch, fold ? NP : 0)) != CA_OK)
             return rc0;
         CA_HIP_CHECK(hipEventRecord(p->ev_ids, p->st3));
     }
@@ -3220,7 +3244,7 @@ int ca_go_sort_ranks(int32_t device, const uint32_t* ranks, int32_t n, int32_t s
     hipLaunchKernelGGL(k_pdq_sort, dim3(1), dim3(pdq::NT), lds, 0, meta.as<GroupMeta>(), nullptr, nullptr, nullptr, 0,
                        rk.as<uint32_t>(), sorted.as<uint32_t>(), e.as<uint64_t>(), scr.as<uint64_t>(),
                        stack.as<pdq::Frame>(), lds_n, store, std::max(limit, 0), nullptr, nullptr, nullptr, 0,
-                       (const int32_t*)nullptr);
+                       (const int32_t*)nullptr, (const ca_template*)nullptr, (const int64_t*)nullptr, 0);
     CA_HIP_CHECK(hipGetLastError());
     CA_HIP_CHECK(hipMemcpy(perm, sorted.ptr, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost));
     return CA_OK;

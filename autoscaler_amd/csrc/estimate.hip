@@ -491,20 +491,28 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
     const int gi = GSEL(blockIdx.x);
     const GroupMeta gm = groups[gi];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // the first RUB list positions per thread are loaded before the class ranking, so their
+    // latency hides behind it; RUB positions per thread are in flight together after that
+    constexpr int RUB = 16;
+    int32_t cv[RUB];
+#pragma unroll
+    for (int u = 0; u < RUB; u++) {
+        const int32_t i = u * 1024 + tid;
+        cv[u] = i < gm.count ? item_cls[gm.off + i] : -1;
+    }
     block_class_rank(tmpls[gm.tmpl], cls_sc, U, NP, key, idx, rc);      // (rc: scratch for the ranks)
     for (int i = tid; i < U; i += 1024) cr[idx[i]] = rc[i];
     __syncthreads();
     for (int i = tid; i < U; i += 1024) { cnt[i] = 0; rc[i] = 0; }
     __syncthreads();
-    // class counts: the lanes of a wave holding one class add once (controllers come in
-    // runs); the gathers of RUB positions per thread are in flight together
-    constexpr int RUB = 8;
+    // class counts: the lanes of a wave holding one class add once (controllers come in runs)
     for (int32_t base = 0; base < gm.count; base += 1024 * RUB) {
-        int32_t cv[RUB];
+        if (base > 0) {
 #pragma unroll
-        for (int u = 0; u < RUB; u++) {
-            const int32_t i = base + u * 1024 + tid;
-            cv[u] = i < gm.count ? item_cls[gm.off + i] : -1;
+            for (int u = 0; u < RUB; u++) {
+                const int32_t i = base + u * 1024 + tid;
+                cv[u] = i < gm.count ? item_cls[gm.off + i] : -1;
+            }
         }
 #pragma unroll
         for (int u = 0; u < RUB; u++) {

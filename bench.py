@@ -333,9 +333,12 @@ def sweep_leg(args, device: int, with_cpu: bool) -> dict:
         W.load_sweep(o, w)
         h = fresh_h
         for mode in ("fresh", "hinted"):
-            t = time.perf_counter()
-            ro = o.find_nodes_to_remove(*sweep_args, h, 0)
-            cpu_ms = (time.perf_counter() - t) * 1e3
+            cts = []
+            for _ in range(3):                                    # median, as on the GPU side
+                t = time.perf_counter()
+                ro = o.find_nodes_to_remove(*sweep_args, h, 0)
+                cts.append(time.perf_counter() - t)
+            cpu_ms = float(np.median(cts) * 1e3)
             r, hg = runs[mode]
             out[f"{mode}_cpu_ms"] = cpu_ms
             out[f"{mode}_speedup"] = cpu_ms / out[f"{mode}_ms"]
@@ -374,7 +377,7 @@ def planner_leg(args, device: int, with_cpu: bool) -> dict:
             st = m.plan_stats()
             m.revert()
             firsts.setdefault(limit, r)
-        out["runs"][str(limit)] = {"gpu_ms": float(min(ts[1:]) * 1e3), "path": st["path"], "rounds": st["rounds"],
+        out["runs"][str(limit)] = {"gpu_ms": float(np.median(ts[1:]) * 1e3), "path": st["path"], "rounds": st["rounds"],
                                    "conflicts": st["conflicts"], "simulated": st["simulated"],
                                    "removable": int(r.results["removable"].sum()),
                                    "candidates_run": int((r.results["reason"] != 101).sum())}
@@ -385,16 +388,23 @@ def planner_leg(args, device: int, with_cpu: bool) -> dict:
         for limit in (20, 200, 0):
             o = pyoracle.OracleState()
             W.load_sweep(o, w)
-            t = time.perf_counter()
-            ro = o.plan_removals(*args_, hints, 0, limit)
+            cts, ro = [], None
+            for _ in range(3):                                    # median, as on the GPU side
+                o.fork()
+                t = time.perf_counter()
+                r1 = o.plan_removals(*args_, hints, 0, limit)
+                cts.append(time.perf_counter() - t)
+                o.revert()
+                ro = ro or r1
             run = out["runs"][str(limit)]
-            run["cpu_ms"] = (time.perf_counter() - t) * 1e3
+            run["cpu_ms"] = float(np.median(cts) * 1e3)
             run["speedup"] = run["cpu_ms"] / run["gpu_ms"]
             g = firsts[limit]
             run["parity"] = bool(np.array_equal(ro.results, g.results) and np.array_equal(ro.moves, g.moves)
                                  and np.array_equal(ro.hints, g.hints) and ro.last_index == g.last_index)
         out["cpu_baseline"] = {"kind": "port", "cores": 1,
-                               "sample": f"oracle/casim_oracle.c or_plan_removals, same loop, 1 thread of {cpu_model()}"}
+                               "sample": f"oracle/casim_oracle.c or_plan_removals, same loop, median of 3 runs (inside a "
+                                         f"reverted fork, as the GPU's median of 4), 1 thread of {cpu_model()}"}
     return out
 
 

@@ -2406,22 +2406,26 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
         for (int i = 0; i < CA_MAX_SCALAR; i++)
             if (t.node.alloc_scalar[i] || t.used_scalar[i]) p->use_scalar = true;
     }
+    // (per-pod summaries of the podset: compact arrays instead of the 208-B records)
     for (int32_t i = 0; i < p->total; i++) {
         const int32_t pi = pod_idx[i];
         if (pi < 0 || pi >= s->t.n_pods) return CA_EINVAL;
-        const uint32_t f = pod_dev_flags(s->h_pods[pi]);
-        if (f & PF_PORTS) p->use_ports = true;
-        if (f & PF_SCALAR_REQ) p->use_scalar = true;
     }
+    if (s->any_ports || s->any_scalar)
+        for (int32_t i = 0; i < p->total; i++) {
+            const uint8_t f = s->h_pflags[pod_idx[i]];
+            if (f & 1) p->use_ports = true;
+            if (f & 2) p->use_scalar = true;
+        }
     p->decouple_ok = p->bucket && s->cls_uniform && groups_tie_free(s, pod_idx, p->h_meta, templates);
     p->demand.assign(G, 0.0);
     for (int32_t g = 0; g < G; g++) {
         const GroupMeta& gm = p->h_meta[g];
         double c = 0, mm = 0;
         for (int32_t i = gm.off; i < gm.off + gm.count; i++) {
-            const ca_pod_spec& ps = s->h_pods[pod_idx[i]];
-            c += (double)ps.req_milli_cpu;
-            mm += (double)ps.req_memory;
+            const int64_t* rq = &s->h_req[2 * (size_t)pod_idx[i]];
+            c += (double)rq[0];
+            mm += (double)rq[1];
         }
         double d = gm.tpods > 0 ? (double)gm.count / gm.tpods : 0.0;
         if (gm.tcpu > 0) d = std::max(d, c / (double)gm.tcpu);

@@ -238,6 +238,9 @@ struct ca_podset {
     int32_t n_cls = 0;
     casim::DevBuf d_cls, d_cls_sc;
     casim::DevBuf d_cls_rep;           // a pod of each class (its first in the set)
+    std::vector<int64_t> h_req;        // per pod: request cpu, memory (compact copies for plan creation)
+    std::vector<uint8_t> h_pflags;     // per pod: 1 host ports, 2 extended-resource requests
+    bool any_ports = false, any_scalar = false;
     std::vector<int32_t> h_cls;        // host copies: class per pod, {cpu, memory} per class
     std::vector<int64_t> h_cls_sc;
     // every class's pods carry identical records apart from their controller

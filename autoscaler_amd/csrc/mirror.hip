@@ -1124,6 +1124,18 @@ int ca_podset_create(ca_mirror* m, const ca_pod_table* t, ca_podset** out) {
     ca_podset* s = new ca_podset();
     s->m = m;
     s->h_pods.assign(t->pods, t->pods + t->n_pods);
+    s->h_req.resize(2 * (size_t)t->n_pods);
+    s->h_pflags.assign((size_t)t->n_pods, 0);
+    for (int32_t i = 0; i < t->n_pods; i++) {
+        const ca_pod_spec& ps = t->pods[i];
+        s->h_req[2 * (size_t)i] = ps.req_milli_cpu;
+        s->h_req[2 * (size_t)i + 1] = ps.req_memory;
+        const uint32_t f = pod_dev_flags(ps);
+        const uint8_t b = (uint8_t)(((f & PF_PORTS) ? 1 : 0) | ((f & PF_SCALAR_REQ) ? 2 : 0));
+        s->h_pflags[i] = b;
+        s->any_ports |= (b & 1) != 0;
+        s->any_scalar |= (b & 2) != 0;
+    }
     int rc = s->t.upload(t->pods, t->n_pods, t->terms, t->n_terms, t->reqs, t->n_reqs, t->prefilter_names,
                          t->n_prefilter_names, m->stream);
     if (rc != CA_OK) { delete s; return rc; }

@@ -865,7 +865,48 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
     const int32_t n = a.n, nb = (n + 63) >> 6;
     const PcLayout Y = pc_layout(n, EPH_COLS);
     const int nh = (int)(blockDim.x >> 6) - 1;                  // helper waves
+    using Row = typename PcRowT<EPH_COLS>::type;
+#ifdef CASIM_PROF
+    const uint64_t t_init0 = clock64();
+#endif
     {
+        // ---- the committed rows and bit planes into LDS: every wave of the workgroup
+        // loads its share of the 64-node blocks (4 in flight per lane) ----
+        Row* const rows = reinterpret_cast<Row*>(pc_raw + Y.rows);
+        PcBlk* const blk = reinterpret_cast<PcBlk*>(pc_raw + Y.blk);
+        uint16_t* const excnt = reinterpret_cast<uint16_t*>(pc_raw + Y.excnt);
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = (int)(blockDim.x >> 6);
+        for (int32_t b0 = 4 * wv; b0 < nb; b0 += 4 * nw) {
+            NodeHot h[4];
+            uint8_t dm[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int32_t i = (b0 + u) * 64 + lane;
+                h[u] = NodeHot{};
+                dm[u] = 0;
+                if (b0 + u < nb && i < n) { h[u] = a.hot[i]; dm[u] = a.dest_mask[i]; }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int32_t j = b0 + u;
+                if (j >= nb) break;
+                const int32_t i = j * 64 + lane;
+                const bool valid = i < n;
+                if (valid) {
+                    rows[i].c = h[u].cpu; rows[i].m = h[u].mem; rows[i].p = h[u].pods; excnt[i] = 0;
+                    if (EPH_COLS) pc_set_e(rows[i], h[u].eph);
+                }
+                const uint64_t dw = __ballot(valid && dm[u] != 0);
+                const uint64_t uw = __ballot(valid && (h[u].flags & NF_UNSCHED));
+                const uint64_t tw = __ballot(valid && (h[u].flags & NF_TAINTS));
+                const uint64_t ew = __ballot(valid && h[u].eph >= 0);
+                if (lane == 0) {
+                    blk[j].dest = dw; blk[j].vis = dw & ~uw; blk[j].usch = uw; blk[j].taint = tw;
+                    if (!EPH_COLS) blk[j].eph = ew;
+                    blk[j].bmc = INT64_MAX; blk[j].bmm = INT64_MAX; blk[j].bme = INT64_MAX; blk[j].bmp = INT32_MAX;
+                }
+            }
+        }
         PcHelp* const hq = reinterpret_cast<PcHelp*>(pc_raw + Y.help);
         if (threadIdx.x == 0) { hq->seq = 0; hq->quit = 0; hq->done = 0; hq->best = INT32_MAX; }
         __syncthreads();                                        // (the one workgroup barrier)
@@ -875,8 +916,6 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
         }
     }
     const int lane = threadIdx.x;
-    using Row = typename PcRowT<EPH_COLS>::type;
-    Row* const rows = reinterpret_cast<Row*>(pc_raw + Y.rows);
     PcBlk* const blk = reinterpret_cast<PcBlk*>(pc_raw + Y.blk);
     uint16_t* const excnt = reinterpret_cast<uint16_t*>(pc_raw + Y.excnt);  // copies committed per node
     ca_plan_result* const resbuf = reinterpret_cast<ca_plan_result*>(pc_raw + Y.resbuf);
@@ -896,44 +935,12 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
 #ifdef CASIM_PROF
     uint64_t prof[PC_NPROF];
     for (int k = 0; k < PC_NPROF; k++) prof[k] = 0;
-    const uint64_t t_start = clock64();
+    const uint64_t t_start = t_init0;
 #endif
 
-    // ---- the committed rows and bit planes into LDS (4 blocks in flight per lane) ----
-    for (int32_t b0 = 0; b0 < nb; b0 += 4) {
-        NodeHot h[4];
-        uint8_t dm[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int32_t i = (b0 + u) * 64 + lane;
-            h[u] = NodeHot{};
-            dm[u] = 0;
-            if (i < n) { h[u] = a.hot[i]; dm[u] = a.dest_mask[i]; }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int32_t j = b0 + u;
-            if (j >= nb) break;
-            const int32_t i = j * 64 + lane;
-            const bool valid = i < n;
-            if (valid) {
-                rows[i].c = h[u].cpu; rows[i].m = h[u].mem; rows[i].p = h[u].pods; excnt[i] = 0;
-                if (EPH_COLS) pc_set_e(rows[i], h[u].eph);
-            }
-            const uint64_t dw = __ballot(valid && dm[u] != 0);
-            const uint64_t uw = __ballot(valid && (h[u].flags & NF_UNSCHED));
-            const uint64_t tw = __ballot(valid && (h[u].flags & NF_TAINTS));
-            const uint64_t ew = __ballot(valid && h[u].eph >= 0);
-            if (lane == 0) {
-                blk[j].dest = dw; blk[j].vis = dw & ~uw; blk[j].usch = uw; blk[j].taint = tw;
-                if (!EPH_COLS) blk[j].eph = ew;
-                blk[j].bmc = INT64_MAX; blk[j].bmm = INT64_MAX; blk[j].bme = INT64_MAX; blk[j].bmp = INT32_MAX;
-            }
-        }
-    }
     __builtin_amdgcn_wave_barrier();
 #ifdef CASIM_PROF
-    prof[PC_INIT] = clock64() - t_start;
+    prof[PC_INIT] = clock64() - t_init0;
 #endif
 
     if (lane == 0) {

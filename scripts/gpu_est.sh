@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "estimate or gosort or multi" > gpurun_out/pytest_est.log 2>&1; rc=$?
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "estimate or gosort or multi or plan" > gpurun_out/pytest_est.log 2>&1; rc=$?
 tail -3 gpurun_out/pytest_est.log
 [ $rc -eq 0 ] || { tail -40 gpurun_out/pytest_est.log; exit $rc; }
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-sweep --no-c4 --no-expansion --no-util \

@@ -5,6 +5,8 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "decoupled or cross_class" > gpurun_out/pytest_f4.log 2>&1 || { tail -40 gpurun_out/pytest_f4.log; exit 1; }
+tail -2 gpurun_out/pytest_f4.log
 timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCH FAILED; tail -20 gpurun_out/bench.err; exit 1; }
 python3 scripts/bench_summary.py gpurun_out/bench.json
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run \

@@ -312,6 +312,44 @@ def test_estimate_workloads(name, w, batch, sort, rows, oracle, monkeypatch):
         assert int(g.results[0]["node_count"]) == 125 and int(g.results[0]["n_scheduled"]) == 1000
 
 
+@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("stream", ["runs", "radix"])
+def test_estimate_decoupled_static_filters(seed, stream, oracle, monkeypatch):
+    """Uniform classes with taints, tolerations, selectors, node affinity, host ports and
+    extended resources (_run_heavy_inputs: a few pod shapes, each repeated): the decoupled
+    stream from per-class counts (k_run_table's per-class static bits against every
+    template, non-batchable classes as single pods) and from the radix passes, against the
+    Go-order oracle with and without run batching."""
+    monkeypatch.setenv("CASIM_RUNS_STREAM", "1" if stream == "runs" else "0")
+    rng, nodes_, pods, templates, groups = _run_heavy_inputs(seed, n_groups=8)
+    table, node_recs, tm, off, pod_idx = _encode_estimate(nodes_, pods, templates, groups)
+    max_nodes = rng.choice([0, 2, 40])
+    L0 = rng.choice([0, 3, 77])
+    o = oracle.OracleState()
+    o.clear()
+    if len(node_recs):
+        o.add_nodes(node_recs)
+    ro = o.estimate(table, off, pod_idx, tm, max_nodes, L0)
+    m = _mirror()
+    m.clear()
+    if len(node_recs):
+        m.add_nodes(node_recs)
+    for batch in ("1", "0"):
+        monkeypatch.setenv("CASIM_RUN_BATCH", batch)
+        with native.EstimatePlan(m, table, off, pod_idx, tm) as plan:
+            g = plan.run(max_nodes, L0, want_nodes=True)
+            assert np.array_equal(ro.results, g.results) and ro.last_index == g.last_index, (seed, batch)
+            for k in range(len(groups)):
+                if int(ro.results[k]["status"]) != 0:
+                    continue
+                a, n = off[k], int(ro.results[k]["n_scheduled"])
+                assert np.array_equal(ro.sched_pod[a:a + n], g.sched_pod[a:a + n]), (seed, batch, k)
+                assert np.array_equal(ro.sched_node[a:a + n], g.sched_node[a:a + n]), (seed, batch, k)
+            h = plan.run_u16(max_nodes, L0) if len(table) <= 65535 else None
+            if h is not None:
+                assert np.array_equal(ro.results, h.results)
+
+
 @pytest.mark.parametrize("shapes", [300, 3000, 6000])
 def test_estimate_many_score_classes(shapes, oracle):
     """Random (cpu, mem) shapes: > 256 score classes take two radix passes, > 4096 take the

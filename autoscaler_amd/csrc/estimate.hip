@@ -464,14 +464,29 @@ __global__ void __launch_bounds__(RTHREADS) k_radix_scatter(const GroupMeta* __r
 // 1*-3*. decoupled Go order: the stable class order of a group is its
 // classes in rank order, each class's pods together, and every pod of a class is the same
 // record but for its controller — so the chain stream follows from per-class counts alone,
-// with no sort of the pod list.  k_run_table (one workgroup per group, after k_class_rank):
-// the class counts of the group's list, each rank's first stream position
-// rstart[g][r] (r in [0, U]), and the stream record of the rank's class rsp[g][r] (its
-// representative pod's requests and static bits against the template).  k_emit_runs:
-// stream position -> rank (binary search of rstart), the record, run heads exactly as
-// k_emit_bucket marks them (a head where the record or its bits change, every
-// non-batchable pod).  The pod id of a stream entry is not needed: decoupled chains emit
-// stream positions and the consumers map them through the Go-order ids.
+// with no sort of the pod list.  k_run_table (one workgroup per group; the class ranks
+// computed in its prologue): the class counts of the group's list, each rank's first
+// stream position rstart[g][r] (r in [0, U]), the stream record of the rank's class
+// rsp[g][r] (its representative pod's requests and static bits against the template), then
+// the stream itself — one 64-position window per thread, position -> rank by a walk over
+// rstart, run heads exactly as k_emit_bucket marks them (a head where the record or its
+// bits change, every non-batchable pod) and the records of the windows that hold a head.
+// The pod id of a stream entry is not needed: decoupled chains emit stream positions and
+// the consumers map them through the Go-order ids.
+__device__ inline uint64_t range_bits64(int lo, int hi) {     // bits [lo, hi) of a word, 0 <= lo < hi <= 64
+    const uint64_t up = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
+    return up & ~((1ull << lo) - 1);
+}
+
+__device__ inline int32_t run_rank(const int32_t* __restrict__ st, int32_t U, int32_t i) {
+    int32_t lo = 0, hi = U;                  // the last r with st[r] <= i (st[U] is never read)
+    while (hi - lo > 1) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (st[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
 __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict__ groups,
                                                    const int32_t* __restrict__ item_cls,
                                                    const int64_t* __restrict__ cls_sc, int32_t NP,
@@ -481,8 +496,14 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
                                                    const ca_selector_term* __restrict__ terms,
                                                    const ca_selector_req* __restrict__ reqs, int32_t* __restrict__ rstart,
                                                    StreamPod* __restrict__ rsp, uint32_t* __restrict__ group_unsup,
-                                                   const int32_t* __restrict__ gmap) {
+                                                   const int32_t* __restrict__ gmap, StreamPod* __restrict__ out,
+                                                   uint64_t* __restrict__ heads, int32_t all_windows,
+                                                   int32_t* __restrict__ lin, uint8_t* __restrict__ need, int32_t lin0) {
+    // lin != null: round 1 without k_round_init — the group's lastIndex input, need flag and
+    // unsupported flag are set here (stored, not or-ed)
     __shared__ int32_t cnt[CLS_MAX];
+    __shared__ uint32_t s_unsup;
+    __shared__ uint8_t rfl[CLS_MAX];          // per rank: 1 batchable, 2 its first position is a run head
     __shared__ int32_t rc[CLS_MAX];
     __shared__ int32_t cr[CLS_MAX];           // rank of each class
     __shared__ uint64_t key[CLS_MAX];
@@ -491,6 +512,7 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
     const int gi = GSEL(blockIdx.x);
     const GroupMeta gm = groups[gi];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) s_unsup = 0;
     // the first RUB list positions per thread are loaded before the class ranking, so their
     // latency hides behind it; RUB positions per thread are in flight together after that
     constexpr int RUB = 16;
@@ -547,7 +569,7 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
     int32_t* rs = rstart + (size_t)gi * (U + 1);
     for (int q = 0; q < 4; q++) {
         const int r = 4 * tid + q;
-        if (r < U) rs[r] = pre;
+        if (r < U) { rs[r] = pre; rc[r] = pre; }            // rc: each rank's first position, from here on
         pre += v[q];
     }
     if (tid == 0) rs[U] = gm.count;
@@ -566,56 +588,59 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
         rsp[(size_t)gi * U + cr[c]] = sp;
         unsup |= sf & SF_UNSUP;
     }
-    if (unsup) atomicOr(&group_unsup[gi], 1u);
-}
-
-__device__ inline int32_t run_rank(const int32_t* __restrict__ st, int32_t U, int32_t i) {
-    int32_t lo = 0, hi = U;                  // the last r with st[r] <= i (st[U] = count > i)
-    while (hi - lo > 1) {
-        const int32_t mid = (lo + hi) >> 1;
-        if (st[mid] <= i) lo = mid; else hi = mid;
+    if (unsup) atomicOr(&s_unsup, 1u);
+    // the stream (formerly a kernel of its own): run heads exactly as k_emit_bucket marks
+    // them — a head where the record or its bits change, every non-batchable pod — then the
+    // records of the 64-position windows that hold a head (the run-batched chain reads no
+    // other window; all_windows: the per-pod chain reads every one)
+    __syncthreads();                              // rsp (global, this workgroup's writes), rc, s_unsup
+    if (tid == 0) {
+        if (lin) { lin[gi] = lin0; need[gi] = 1; group_unsup[gi] = s_unsup ? 1u : 0u; }
+        else if (s_unsup) atomicOr(&group_unsup[gi], 1u);
     }
-    return lo;
-}
-
-__global__ void __launch_bounds__(256) k_emit_runs(const GroupMeta* __restrict__ groups,
-                                                  const int32_t* __restrict__ rstart, const StreamPod* __restrict__ rsp,
-                                                  int32_t U, StreamPod* __restrict__ out, uint64_t* __restrict__ heads,
-                                                  const int32_t* __restrict__ gmap, int32_t all_windows) {
-    __shared__ int32_t st[CLS_MAX + 1];
-    const int gi = GSEL(blockIdx.y);
-    const GroupMeta gm = groups[gi];
-    const int32_t base = (int32_t)(blockIdx.x * blockDim.x);
-    if (base >= gm.count) return;                                   // (uniform per block)
-    const int32_t* rs = rstart + (size_t)gi * (U + 1);
-    for (int r = threadIdx.x; r <= U; r += blockDim.x) st[r] = rs[r];
+    const StreamPod* rg = rsp + (size_t)gi * U;
+    for (int c = tid; c < U; c += 1024) {
+        if (cnt[c] == 0) continue;
+        const int r = cr[c];
+        const StreamPod sp = rg[r];
+        uint8_t f = (sp.flags & SF_BATCH) ? 1 : 0;
+        bool hs = true;
+        if (rc[r] > 0) {                          // the record before the rank's first position
+            const StreamPod q = rg[run_rank(rc, U, rc[r] - 1)];
+            hs = !((q.flags & ~SF_BATCH) == (sp.flags & ~SF_BATCH) && q.cpu == sp.cpu && q.mem == sp.mem &&
+                   q.eph == sp.eph);
+        }
+        rfl[r] = f | (hs ? 2 : 0);
+    }
     __syncthreads();
-    const int32_t i = base + (int32_t)threadIdx.x;
-    const int lane = threadIdx.x & 63;
-    if (base + (int32_t)(threadIdx.x & ~63u) >= gm.count) return;   // whole wave past the end
-    bool head = true;
-    StreamPod sp = {};
-    if (i < gm.count) {
-        const int32_t r = run_rank(st, U, i);
-        sp = rsp[(size_t)gi * U + r];
-        const bool bat = (sp.flags & SF_BATCH) != 0;
-        if (i > 0 && bat) {
-            head = false;
-            if (i == st[r]) {                                       // first pod of its class
-                const StreamPod q = rsp[(size_t)gi * U + run_rank(st, U, i - 1)];
-                head = !((q.flags & ~SF_BATCH) == (sp.flags & ~SF_BATCH) && q.cpu == sp.cpu && q.mem == sp.mem &&
-                         q.eph == sp.eph);
+    const int32_t nwin = (gm.count + 63) >> 6;
+    for (int32_t wdx = tid; wdx < nwin; wdx += 1024) {
+        // the window's rank segments (one in most windows): a non-batchable rank is all
+        // heads, a batchable one has at most its first position
+        const int32_t i0 = wdx * 64, i1 = min(gm.count, i0 + 64);
+        const int32_t r0 = run_rank(rc, U, i0);
+        uint64_t hb = i0 == 0 ? 1ull : 0ull;
+        for (int32_t r = r0, pos = i0; pos < i1; r++) {
+            const int32_t rend = r + 1 < U ? min(rc[r + 1], i1) : i1;
+            if (rend <= pos) continue;                          // (an empty rank)
+            const uint8_t f = rfl[r];
+            if (!(f & 1)) hb |= range_bits64(pos - i0, rend - i0);
+            else if (pos == rc[r] && (f & 2)) hb |= 1ull << (pos - i0);
+            pos = rend;
+        }
+        heads[gm.moff + wdx] = hb;
+        if (hb == 0 && !all_windows) continue;
+        for (int32_t r = r0, pos = i0; pos < i1; r++) {
+            const int32_t rend = r + 1 < U ? min(rc[r + 1], i1) : i1;
+            if (rend <= pos) continue;
+            StreamPod sp = rg[r];
+            const uint32_t fl = sp.flags;
+            for (; pos < rend; pos++) {
+                sp.flags = fl | (((hb >> (pos - i0)) & 1) ? SF_HEAD : 0u);
+                out[gm.off + pos] = sp;
             }
         }
-        sp.flags |= head ? SF_HEAD : 0u;
     }
-    const uint64_t hb = __ballot(head);
-    if (lane == 0) heads[gm.moff + (i >> 6)] = hb;
-    // With run batching the chain reads a stream entry only at a run head or inside a
-    // non-batchable run (whose every pod is a head), and only from the 64-entry window
-    // holding it: windows without a head are never read, so they are not written (C2: ~1
-    // window in 10 has a head).  The per-pod chain (CASIM_RUN_BATCH=0) reads every window.
-    if ((hb != 0 || all_windows) && i < gm.count) out[gm.off + i] = sp;
 }
 
 // 1''-2''. Go 1.19 sort.Slice order (binpacking_estimator.go:74; pdqsort.h) ----------
@@ -1235,7 +1260,8 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
                                                 int32_t* __restrict__ qctl, int32_t total, int32_t nsub,
                                                 const int2* __restrict__ prog, int32_t pch,
                                                 T* pub,              // pub may alias sched_dev (device results)
-                                                uint64_t start_ticks, const int32_t* ids_ready, int32_t ids_epoch) {
+                                                uint64_t start_ticks, const int32_t* ids_ready, int32_t ids_epoch,
+                                                int32_t* __restrict__ hflags) {
     // ids_ready != null (decoupled Go order): the stream's pod ids in spod
     // come from a sort that runs beside the chains — a group's are final once
     // ids_ready[g] holds this run's epoch — and the chains' single placements are stream positions
@@ -1250,7 +1276,10 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
                 bool started = false;
                 for (;;) {
                     tk = __hip_atomic_load(&tickets[s_t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                    if (tk >= 0) break;
+                    if (tk >= 0) {      // consumed: the slot is -1 again for the next run
+                        __hip_atomic_store(&tickets[s_t], -1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
                     if (__hip_atomic_load(&qctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;  // given up
                     if (!started) started = __hip_atomic_load(&qctl[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
                     const uint64_t dt = wall_clock64() - t0;
@@ -1279,7 +1308,18 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
         lds_barrier();
         const int32_t t = s_t;
         const int64_t tk64 = s_tk;
-        if (t >= total || tk64 < 0) return;
+        if (t >= total || tk64 < 0) {
+            if (threadIdx.x == 0) {
+                // gave up (qctl[2]): tell the host, which reads hflags after the round (no copy)
+                if (t < total) hflags[2] = 1;
+                // the last block out clears the control words for the next run (every ticket
+                // was consumed, so no chain pushes any more; after a give-up the host
+                // re-initialises them)
+                if (atomicAdd(&qctl[5], 1) == (int32_t)gridDim.x - 1)
+                    for (int k = 0; k < 6; k++) __hip_atomic_store(&qctl[k], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            return;
+        }
         __threadfence();                                   // acquire for every thread of the block
         const int32_t tk = (int32_t)(uint32_t)(tk64 & 0xFFFFFFFFll);
         const int32_t pure_off = (int32_t)(tk64 >> 32) - 1;   // >= 0: a pure chunk (push_chunks)
@@ -1356,7 +1396,8 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     int32_t* __restrict__ sched_pod, int32_t* __restrict__ sched_node, Seg* __restrict__ segs,
     int64_t* __restrict__ tickets, int32_t* __restrict__ qctl, int32_t nsub, int2* __restrict__ prog, int32_t pch,
     ChainOut* __restrict__ outs, const int32_t* __restrict__ gmap, unsigned char* __restrict__ gslab,
-    const int64_t* __restrict__ slab_off, const int32_t* __restrict__ gkcap, int32_t pos_out) {
+    const int64_t* __restrict__ slab_off, const int32_t* __restrict__ gkcap, int32_t pos_out,
+    ChainOut* __restrict__ hout, int32_t* __restrict__ hflags) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int g = GSEL(blockIdx.x);
     // GROWS: the group's rows live in its own HBM slab (kcap = the group's pod count, for an
@@ -1389,7 +1430,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     res.nseg = 0; res.pad2[0] = res.pad2[1] = res.pad2[2] = 0;
     if (group_unsup[g] || (gm.tflags & CA_NODE_ANTI_AFFINITY_PODS)) {
         res.status = CA_EUNSUPPORTED;
-        if (tid == 0) outs[g] = res;
+        if (tid == 0) { outs[g] = res; hout[g] = res; }
         if (tickets && w0) push_chunks(g, 0, (gm.count + pch - 1) / pch, nsub, tickets, qctl, prog, 0, 0, lane);
         return;
     }
@@ -2084,6 +2125,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
         res.nseg = nseg;
         res.pad = (uint64_t)(uint32_t)(wall_clock64() - t_begin) | ((uint64_t)n_single << 32);
         outs[g] = res;
+        hout[g] = res;                          // zero-copy: the host reads it after the round's event
     }
     if (tickets) {
         __threadfence();                        // every wave's result stores, before the release
@@ -2091,7 +2133,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
         if (w0) {
             const bool ok = res.status == CA_OK;
             // a group that failed after publishing chunks: the host falls back to the copy
-            if (!ok && tk_next > 0 && lane == 0) atomicExch(&qctl[3], 1);
+            if (!ok && tk_next > 0 && lane == 0) { atomicExch(&qctl[3], 1); hflags[3] = 1; }
             push_chunks(g, tk_next, (P + pch - 1) / pch, nsub, tickets, qctl, prog, ok ? nseg : 0, ok ? nsched : 0, lane);
         }
     }
@@ -2115,7 +2157,7 @@ __global__ void __launch_bounds__(256) k_round_init(int32_t G, int32_t lin0, int
     for (int32_t g = i; g < G; g += stride) { lin[g] = lin0; need[g] = 1; unsup[g] = 0; }
     if (tickets)
         for (int32_t t = i; t < n_tickets; t += stride) tickets[t] = -1;
-    if (qctl && i < 5) qctl[i] = 0;
+    if (qctl && i < 6) qctl[i] = 0;
 }
 
 // 5. scheduled pods of the run placements: sched_pod[dst + t] = stream pod at src + t.
@@ -2211,6 +2253,10 @@ struct ca_estimate_plan {
     hipEvent_t ev[EV_N] = {};
     float t_ms[7] = {};
     int32_t pub_state = 0;         // last run: 0 results copied, 1 published zero-copy, 2 publisher gave up
+    // the publisher's tickets are all -1 and its control words zero on the device: every
+    // publisher consumed and reset its tickets and its last block cleared the words (round 1
+    // then needs no k_round_init; false at first and after a publisher gave up)
+    bool pub_clean = false;
     int32_t ran_decoupled = 0;     // last run took the decoupled Go order
     bool phase_events = true;      // record the per-phase timing events (ca_estimate_plan_set_phase_timing)
     std::vector<uint64_t> diag;     // per group: chain ticks (100 MHz) | single-pod steps << 32
@@ -2457,7 +2503,7 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     if ((rc = p->d_tickets.reserve(sizeof(int64_t) * (size_t)std::max(p->n_tickets, 1))) != CA_OK) return rc;
     if ((int64_t)G * p->nsub < INT32_MAX &&
         (rc = p->d_prog.reserve(sizeof(int2) * (size_t)G * (size_t)p->nsub)) != CA_OK) return rc;
-    if ((rc = p->d_qctl.reserve(sizeof(int32_t) * 5)) != CA_OK) return rc;
+    if ((rc = p->d_qctl.reserve(sizeof(int32_t) * 6)) != CA_OK) return rc;
     if ((rc = p->d_unsup.reserve(sizeof(uint32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
     if ((rc = p->d_lin.reserve(sizeof(int32_t) * (size_t)std::max(G, 1))) != CA_OK) return rc;
     if ((rc = p->d_need.reserve((size_t)std::max(G, 1))) != CA_OK) return rc;
@@ -2685,10 +2731,28 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                    p->d_sortC.as<uint32_t>(), p->d_spod_go.as<int32_t>(),
                                    p->d_ids_ready.as<int32_t>(), p->ids_epoch, fold ? NP : 0)) != CA_OK)
             return rc0;
-        CA_HIP_CHECK(hipEventRecord(p->ev_ids, p->st3));
+        // (ev_ids is recorded on st3 once the heavy chains are queued: the host's launches
+        // ahead of them pace the step's start)
     }
+    bool ids_recorded = !decoupled;
+    auto record_ids = [&]() -> int {
+        if (!ids_recorded) { CA_HIP_CHECK(hipEventRecord(p->ev_ids, p->st3)); ids_recorded = true; }
+        return CA_OK;
+    };
     if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_START], st));
-    {
+    // decoupled: the stream from per-class counts (k_run_table) instead of the radix passes
+    // and k_emit_bucket (CASIM_RUNS_STREAM=0: the radix path, for tests)
+    const bool runs_stream = !(getenv("CASIM_RUNS_STREAM") && atoi(getenv("CASIM_RUNS_STREAM")) == 0);
+    // round 1 without k_round_init: k_run_table sets each group's lastIndex / need /
+    // unsupported flags, and the publisher's tickets and control words are clean from the
+    // last run (ca_estimate_plan::pub_clean) — no launch and no cross-stream event ahead of
+    // the chains
+    const bool fast_init = decoupled && runs_stream && (!publish || p->pub_clean) && !serial_pub &&
+                           !getenv("CASIM_NO_FAST_INIT");
+    const int32_t lin0 = *last_index;
+    if (publish) p->pub_clean = false;        // set again once this run's publishers all finished clean
+    bool pub_gave_up = false;
+    if (!fast_init) {
         const int32_t n = std::max(G, tickets1);
         hipLaunchKernelGGL(k_round_init, dim3(std::min((n + 255) / 256, 64)), dim3(256), 0, st, G, *last_index,
                            p->d_lin.as<int32_t>(), p->d_need.as<uint8_t>(), p->d_unsup.as<uint32_t>(),
@@ -2758,10 +2822,6 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         while (nb < U) { nb <<= 8; passes++; }
         passes = std::max(passes, 1);
         const int32_t passes_run = (go_order && !decoupled) ? 0 : passes;
-        // decoupled: the stream from per-class counts (k_run_table + k_emit_runs) instead of
-        // the radix passes and k_emit_bucket (CASIM_RUNS_STREAM=0: the radix path, for tests)
-        const bool runs_stream = !(getenv("CASIM_RUNS_STREAM") && atoi(getenv("CASIM_RUNS_STREAM")) == 0);
-
         const int32_t blocks = (p->max_count + 255) / 256;
         // class ranks, then Go's pdqsort (default) or the stable LSD radix passes, stream
         // emission for `ng` groups (map `gm`)
@@ -2776,13 +2836,11 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                    p->s->d_cls_rep.as<int32_t>(), U,
                                    p->d_tmpl.as<ca_template>(), p->s->t.hot.as<PodHot>(), p->s->t.spec.as<ca_pod_spec>(),
                                    p->s->t.terms.as<ca_selector_term>(), p->s->t.reqs.as<ca_selector_req>(),
-                                   p->d_rstart.as<int32_t>(), p->d_rsp.as<StreamPod>(), p->d_unsup.as<uint32_t>(), gm);
+                                   p->d_rstart.as<int32_t>(), p->d_rsp.as<StreamPod>(), p->d_unsup.as<uint32_t>(), gm,
+                                   p->d_stream.as<StreamPod>(), p->d_heads.as<uint64_t>(), batch_runs ? 0 : 1,
+                                   fast_init ? p->d_lin.as<int32_t>() : nullptr, p->d_need.as<uint8_t>(), lin0);
                 CA_HIP_CHECK(hipGetLastError());
                 if (events && p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], ss));
-                hipLaunchKernelGGL(k_emit_runs, dim3(blocks, ng), dim3(256), 0, ss, p->d_meta.as<GroupMeta>(),
-                                   p->d_rstart.as<int32_t>(), p->d_rsp.as<StreamPod>(), U, p->d_stream.as<StreamPod>(),
-                                   p->d_heads.as<uint64_t>(), gm, batch_runs ? 0 : 1);
-                CA_HIP_CHECK(hipGetLastError());
                 return CA_OK;
             }
             hipLaunchKernelGGL(k_class_rank, dim3(ng), dim3(1024), 0, ss, p->d_meta.as<GroupMeta>(),
@@ -2821,10 +2879,11 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         };
         int rc;
         if (split) {     // the light groups are sorted right after the heavy chains are queued
-            CA_HIP_CHECK(hipEventRecord(p->ev_init, st));
+            // (fast_init: nothing of k_round_init to wait for)
+            if (!fast_init) CA_HIP_CHECK(hipEventRecord(p->ev_init, st));
             if ((rc = sort_groups(st, gmapA, nA, true)) != CA_OK) return rc;
             sort_light = [=]() -> int {
-                CA_HIP_CHECK(hipStreamWaitEvent(p->st2, p->ev_init, 0));
+                if (!fast_init) CA_HIP_CHECK(hipStreamWaitEvent(p->st2, p->ev_init, 0));
                 return sort_groups(p->st2, gmapB, nB, false);
             };
         } else if ((rc = sort_groups(st, nullptr, G, true)) != CA_OK) {
@@ -2878,24 +2937,39 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     std::vector<uint8_t> accepted(G, 0);
     std::vector<int32_t> true_lin(G, *last_index);
     int32_t cut = -1;                   // first unsupported group when later groups exist (prefix protocol)
+    // the host joins the streams itself (publisher, heavy and light chains) instead of
+    // queueing cross-stream waits ahead of the readback event on st
+    const bool host_joins = publish && !p->phase_events;
+    bool light_pending = false;
     int32_t rounds = 0;
     float chain_ms = 0;
+    {
+        int32_t* hq = p->h_qc.as<int32_t>();     // host-side failure flags ([2] per round, [3] sticky)
+        hq[2] = hq[3] = 0;
+    }
     for (;;) {
         rounds++;
+        if (rounds > 1) p->h_qc.as<int32_t>()[2] = 0;
         if (rounds > 1) {      // round 1's state came from k_round_init
             CA_HIP_CHECK(hipMemcpyAsync(p->d_lin.ptr, lin.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
             CA_HIP_CHECK(hipMemcpyAsync(p->d_need.ptr, need.data(), G, hipMemcpyHostToDevice, st));
         }
         int32_t round_tickets = 0;
+        // the publisher's start: after the ticket reset (k_round_init, or the memsets of a
+        // later round); round 1 of a split run reuses ev_init (recorded right after
+        // k_round_init), so no marker sits between the heavy stream and its chains
+        hipEvent_t pub_go = p->ev_go;
         if (publish) {
             for (int32_t g = 0; g < G; g++) if (need[g]) round_tickets += (p->h_meta[g].count + p->pch - 1) / p->pch;
             if (rounds > 1) {
                 CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_pub, 0));   // previous publisher done
                 CA_HIP_CHECK(hipMemsetAsync(p->d_tickets.ptr, 0xFF, sizeof(int64_t) * (size_t)std::max(round_tickets, 1), st));
                 CA_HIP_CHECK(hipMemsetAsync(p->d_qctl.ptr, 0, sizeof(int32_t) * 3, st));   // [3] stays: sticky
-                CA_HIP_CHECK(hipMemsetAsync(p->d_qctl.as<int32_t>() + 4, 0, sizeof(int32_t), st));
+                CA_HIP_CHECK(hipMemsetAsync(p->d_qctl.as<int32_t>() + 4, 0, sizeof(int32_t) * 2, st));
             }
-            CA_HIP_CHECK(hipEventRecord(p->ev_go, st));
+            if (rounds == 1 && fast_init) pub_go = nullptr;       // the tickets are clean already
+            else if (rounds == 1 && split) pub_go = p->ev_init;
+            else CA_HIP_CHECK(hipEventRecord(p->ev_go, st));
         }
         // CASIM_PUB_SERIAL (tests): the publisher goes first on the chains' own stream, i.e.
         // the two kernels are serialised — it must give up at its start deadline
@@ -2906,13 +2980,14 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                    ids_src, p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int64_t>(),
                                    p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
                                    reinterpret_cast<uint16_t*>(publish), pub_start_ticks(),
-                                   decoupled ? p->d_ids_ready.as<int32_t>() : nullptr, p->ids_epoch);
+                                   decoupled ? p->d_ids_ready.as<int32_t>() : nullptr, p->ids_epoch, p->h_qc.as<int32_t>());
             else
                 hipLaunchKernelGGL(k_publish<int32_t>, dim3(std::min(round_tickets, pub_blocks(decoupled))), dim3(256), 0, ps,
                                    p->d_meta.as<GroupMeta>(), p->d_out.as<ChainOut>(), p->d_seg.as<Seg>(),
                                    ids_src, p->d_sched_pod.as<int32_t>(), p->d_tickets.as<int64_t>(),
                                    p->d_qctl.as<int32_t>(), round_tickets, p->nsub, p->d_prog.as<int2>(), p->pch,
-                                   publish, pub_start_ticks(), decoupled ? p->d_ids_ready.as<int32_t>() : nullptr, p->ids_epoch);
+                                   publish, pub_start_ticks(), decoupled ? p->d_ids_ready.as<int32_t>() : nullptr, p->ids_epoch,
+                                   p->h_qc.as<int32_t>());
             CA_HIP_CHECK(hipGetLastError());
             return CA_OK;
         };
@@ -2938,34 +3013,38 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                p->d_qctl.as<int32_t>(), p->nsub, p->d_prog.as<int2>(), p->pch, p->d_out.as<ChainOut>(),
                                gm, grows ? p->d_slab.as<unsigned char>() : nullptr,
                                grows ? p->d_slab_off.as<int64_t>() : nullptr, grows ? p->d_gkcap.as<int32_t>() : nullptr,
-                               decoupled ? 1 : 0);
+                               decoupled ? 1 : 0, p->h_out.as<ChainOut>(), p->h_qc.as<int32_t>());
             CA_HIP_CHECK(hipGetLastError());
             return CA_OK;
         };
         int rc;
         if (rounds == 1 && split) {         // heavy groups on st as soon as their sort is done
             if ((rc = chain(st, gmapA, nA)) != CA_OK) return rc;
+            if ((rc = record_ids()) != CA_OK) return rc;
             if ((rc = sort_light()) != CA_OK) return rc;
             if ((rc = chain(p->st2, gmapB, nB)) != CA_OK) return rc;
             CA_HIP_CHECK(hipEventRecord(p->ev_b, p->st2));
-            CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_b, 0));
+            // (publishing without phase events the host waits for ev_b itself: one
+            // cross-stream hop less between the last chain and the host)
+            if (!host_joins) CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_b, 0));
+            light_pending = host_joins;
         } else if ((rc = chain(st, nullptr, G)) != CA_OK) {
             return rc;
         }
+        if ((rc = record_ids()) != CA_OK) return rc;
         if (publish && round_tickets > 0 && !serial_pub) {
-            CA_HIP_CHECK(hipStreamWaitEvent(p->pub_stream, p->ev_go, 0));
+            if (pub_go) CA_HIP_CHECK(hipStreamWaitEvent(p->pub_stream, pub_go, 0));
             if ((rc = launch_pub(p->pub_stream)) != CA_OK) return rc;
             CA_HIP_CHECK(hipEventRecord(p->ev_pub, p->pub_stream));
         }
         if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN1], st));
         // one readback per round: the chain outputs, and (publishing) the publisher's
         // counters once it is done — the results are then already in the caller's buffer
+        // (the chains write their ChainOut records, and the chains / publisher their failure
+        // flags, straight into page-locked h_out / h_qc: no copy kernels at the step's end)
         const ChainOut* fresh = p->h_out.as<ChainOut>();
-        CA_HIP_CHECK(hipMemcpyAsync(p->h_out.ptr, p->d_out.ptr, sizeof(ChainOut) * G, hipMemcpyDeviceToHost, st));
-        if (publish) {
-            CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_pub, 0));
-            CA_HIP_CHECK(hipMemcpyAsync(p->h_qc.ptr, p->d_qctl.ptr, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, st));
-        }
+        const bool pub_ran = publish && round_tickets > 0 && !serial_pub;
+        if (publish && !(host_joins && pub_ran)) CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_pub, 0));
         CA_HIP_CHECK(hipEventRecord(p->ev_rb, st));
         // results of this round, queued behind the readback: the device fills them while
         // the host walks the lastIndex chain (a later round queues them again)
@@ -2977,7 +3056,10 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             CA_HIP_CHECK(hipGetLastError());
         }
         if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_COMPACT], st));
+        if (host_joins && pub_ran) CA_HIP_CHECK(hipEventSynchronize(p->ev_pub));   // (finishes last)
         CA_HIP_CHECK(hipEventSynchronize(p->ev_rb));
+        if (light_pending) { CA_HIP_CHECK(hipEventSynchronize(p->ev_b)); light_pending = false; }
+        if (publish && p->h_qc.as<int32_t>()[2] != 0) pub_gave_up = true;
         float ms = 0;
         if (p->phase_events)
             (void)hipEventElapsedTime(&ms, p->ev[ca_estimate_plan::EV_CHAIN0], p->ev[ca_estimate_plan::EV_CHAIN1]);
@@ -3043,6 +3125,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         CA_HIP_CHECK(hipGetLastError());
     }
     if (publish) {
+        p->pub_clean = !pub_gave_up;
         // the publisher of the last round wrote the results; a deadline hit (a chain that
         // died) falls back to the device copy + D2H
         const int32_t* qc = p->h_qc.as<int32_t>();      // read back with the last round's outputs
@@ -3264,9 +3347,9 @@ int ca_go_sort_ranks(int32_t device, const uint32_t* ranks, int32_t n, int32_t s
 
 #ifdef CASIM_PROF
 int ca_debug_pdq_prof(uint64_t* out, int32_t reset) {
-    CA_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(pdq::g_pdq_prof), sizeof(uint64_t) * 32));
+    CA_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(pdq::g_pdq_prof), sizeof(uint64_t) * (32 + 256)));
     if (reset) {
-        static const uint64_t z[32] = {};
+        static const uint64_t z[32 + 256] = {};
         CA_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(pdq::g_pdq_prof), z, sizeof z));
     }
     return CA_OK;

@@ -41,7 +41,10 @@ namespace casim {
 namespace pdq {
 
 #ifdef CASIM_PROF    // phase cycle counters of workgroup 0 (profiling build: ca_debug_pdq_prof)
-__device__ unsigned long long g_pdq_prof[32];
+__device__ unsigned long long g_pdq_prof[32 + 16 * 16];   // + per-step slots [32 + 16 step + k]
+__device__ int g_pdq_step;
+#define PDQ_S(k, v) do { if (threadIdx.x == 0 && blockIdx.x == 0 && g_pdq_step < 16) g_pdq_prof[32 + 16 * g_pdq_step + (k)] += (unsigned long long)(v); } while (0)
+#define PDQ_SMAXW(k, v) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0 && g_pdq_step < 16) atomicMax(&g_pdq_prof[32 + 16 * g_pdq_step + (k)], (unsigned long long)(v)); } while (0)
 #define PDQ_T(v) const uint64_t v = clock64()
 #define PDQ_ADD(i, t) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_pdq_prof[i] += clock64() - (t); } while (0)
 #define PDQ_CNT(i, n) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_pdq_prof[i] += (n); } while (0)
@@ -51,6 +54,8 @@ __device__ unsigned long long g_pdq_prof[32];
 #define PDQ_TMAX(i, v) do { if (blockIdx.x == 0) atomicMax(&g_pdq_prof[i], (unsigned long long)(v)); } while (0)
 #define PDQ_TADD(i, v) do { if (blockIdx.x == 0) atomicAdd(&g_pdq_prof[i], (unsigned long long)(v)); } while (0)
 #else
+#define PDQ_S(k, v) (void)0
+#define PDQ_SMAXW(k, v) (void)0
 #define PDQ_WADD(i, t) (void)0
 #define PDQ_WMAX(i, t) (void)0
 #define PDQ_TMAX(i, v) (void)0
@@ -772,6 +777,7 @@ __device__ inline uint64_t range_bits(int lo, int hi) {     // bits [lo, hi) of 
 
 __device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, int n) {
     const int tid = threadIdx.x, lane = tid & 63;
+    PDQ_T(t_p1);
     const int np = c.np;
     const int W = (n + 63) >> 6;
     const bool act = tid < W;
@@ -819,6 +825,7 @@ __device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, 
     add_count(c, memB != 0, B.slot, __builtin_popcountll(pm & memB));
     __syncthreads();
     PDQ_T(t_p2);
+    PDQ_S(6, t_p2 - t_p1);
     // P2: zones, LM / RM masks, RM bitmap, pair counts, prefix counts
     A.z = A.a + (memA ? c.m[A.slot] : 0);
     B.z = B.a + (memB ? c.m[B.slot] : 0);
@@ -852,6 +859,7 @@ __device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, 
     __syncthreads();
     PDQ_ADD(6, t_p2);
     PDQ_T(t_p3);
+    PDQ_S(7, t_p3 - t_p2);
     // P3: the pairs, split evenly over the workgroup's threads in runs of consecutive
     // global pair indices.  In combined (LM | RM) order frame f (pair base fs, end fe)
     // holds its LMs at [2fs, fs+fe) and its RMs at [fs+fe, 2fe): pair k of the frame joins
@@ -927,6 +935,7 @@ __device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, 
     }
     __syncthreads();
     PDQ_ADD(7, t_p3);
+    PDQ_S(8, clock64() - t_p3);
 }
 
 // partialInsertionSort_func on a frame longer than T_SMALL, by the whole workgroup: the
@@ -1420,8 +1429,14 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
             else { stack[0] = root; c.top = 1; }
         }
     }
+#ifdef CASIM_PROF
+    if (tid == 0 && blockIdx.x == 0) g_pdq_step = -1;
+#endif
     __syncthreads();
     for (;;) {
+#ifdef CASIM_PROF
+        if (tid == 0 && blockIdx.x == 0) g_pdq_step++;
+#endif
         PDQ_T(t_pop);
         if (tid == 0) {
             const int nf = min(c.top, MAXF);
@@ -1442,6 +1457,7 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
         PDQ_ADD(2, t_pop);
         PDQ_CNT(11, 1);
         PDQ_CNT(12, nf);
+        PDQ_S(0, nf);
         PDQ_T(t_a);
         // A: one pdqsort_func loop iteration's control per frame (a wavefront each)
         for (int i = w; i < nf; i += NW) {
@@ -1497,7 +1513,10 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
             }
             wfence();
         }
+        PDQ_SMAXW(11, clock64() - t_a);
         __syncthreads();
+        PDQ_S(2, clock64() - t_a);
+        PDQ_T(t_wp);
         // partialInsertionSort of the frames that run it, one after another, by the workgroup
         for (int i = 0; i < nf; i++) {
             if (c.op[i] == OP_DONE || !c.pis[i]) continue;
@@ -1507,7 +1526,10 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
             PDQ_CNT(20, 1);
             if (sorted && tid == 0) c.op[i] = OP_DONE;
             __syncthreads();
+            PDQ_S(12, 1);
         }
+        PDQ_S(3, clock64() - t_wp);
+        PDQ_T(t_a2);
         // A2: partitionEqual or partition; the pivot moves to a
         for (int i = w; i < nf; i += NW) {
             if (c.op[i] == OP_DONE) continue;
@@ -1522,6 +1544,7 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
         }
         __syncthreads();
         PDQ_ADD(3, t_a);
+        PDQ_S(4, clock64() - t_a2);
         PDQ_T(t_pl);
         if (tid < 64) {                     // the partitioning frames, ordered by start
             int np = 0;
@@ -1546,8 +1569,11 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
         }
         __syncthreads();
         PDQ_ADD(4, t_pl);
+        PDQ_S(5, clock64() - t_pl);
         PDQ_CNT(13, c.np);
         PDQ_CNT(15, c.fo[c.np]);
+        PDQ_S(1, c.np);
+        PDQ_S(10, c.fo[c.np]);
         PDQ_T(t_part);
         if (c.np > 0) wg_partition(s, c, xs, n);
         PDQ_ADD(5, t_part);
@@ -1582,6 +1608,7 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
         __threadfence_block();
         __syncthreads();
         PDQ_ADD(9, t_d);
+        PDQ_S(9, clock64() - t_d);
     }
     // the short frames, one wavefront each, claimed in turn
     PDQ_T(t_small);

@@ -19,4 +19,6 @@ cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_RO
 cd "$GRAFT_REPO_ROOT"
 timeout -k 10 200 python -u scripts/plan_prof.py 5000 --prof > gpurun_out/plan_prof.log 2>&1 || { tail -20 gpurun_out/plan_prof.log; exit 1; }
 cat gpurun_out/plan_prof.log
+timeout -k 10 200 python -u scripts/pdq_prof.py > gpurun_out/pdq_prof.log 2>&1 || { tail -20 gpurun_out/pdq_prof.log; exit 1; }
+cat gpurun_out/pdq_prof.log
 echo FINAL4_OK

@@ -404,7 +404,7 @@ def test_estimate_go_order_decoupled(seed, decouple, oracle, monkeypatch):
     """Uniform score classes (C2's catalog: every class's pods identical but for their
     controller): the chains run on the stable class order while Go's sort.Slice ids are
     computed beside them (CASIM_GO_DECOUPLE=0: the Go sort ahead of the stream).  The
-    decoupled stream comes from per-class counts (k_run_table + k_emit_runs), or with
+    decoupled stream comes from per-class counts (k_run_table), or with
     CASIM_RUNS_STREAM=0 from the radix passes.  All give the Go-order oracle's pod lists in
     every output mode, with progressive publishing (64-output chunks), lastIndex
     speculation rounds (existing nodes) and limiter cuts."""
@@ -430,6 +430,11 @@ def test_estimate_go_order_decoupled(seed, decouple, oracle, monkeypatch):
             assert np.array_equal(ro.results, d.results)
             assert np.array_equal(ro.sched_pod, plan.fetch())
             h = plan.run_u16(w.max_nodes, L0)
+            assert np.array_equal(ro.sched_pod, np.where(h.sched_pod == 0xFFFF, -1, h.sched_pod.astype(np.int32)))
+            plan.set_phase_timing(False)
+            h = plan.run_u16(w.max_nodes, L0)
+            plan.set_phase_timing(True)
+            assert np.array_equal(ro.results, h.results) and ro.last_index == h.last_index
             assert np.array_equal(ro.sched_pod, np.where(h.sched_pod == 0xFFFF, -1, h.sched_pod.astype(np.int32)))
 
 
@@ -569,6 +574,44 @@ def test_estimate_publisher_bounded(serial, oracle, monkeypatch):
             assert np.array_equal(ro.sched_pod, np.where(h.sched_pod == 0xFFFF, -1, h.sched_pod.astype(np.int32)))
             assert plan.stats()["results_path"] == ("publisher_gave_up" if serial else "published")
     assert min(walls) < 0.05, walls          # 2 ms start deadline + the copy, never 200 ms
+
+
+def test_estimate_publisher_state_across_runs(oracle, monkeypatch):
+    """Round 1 of a decoupled run skips k_round_init when the last run's publisher consumed
+    and reset every ticket and cleared its control words (ca_estimate_plan::pub_clean).
+    One plan alternates clean runs, a run whose publisher gives up (serialised: its tickets
+    stay dirty, so the next run re-initialises them) and every output mode, with lastIndex
+    inputs that force speculation rounds: the results never change."""
+    w = W.c2(n_pods=9000, n_groups=16, n_existing=200, max_nodes=1000, seed=11)
+    o = oracle.OracleState()
+    W.load_estimate(o, w)
+    m = _mirror()
+    W.load_estimate(m, w)
+    ref = {}
+    for L0 in (0, 77):
+        ref[L0] = o.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, L0)
+
+    def check(r, L0, u16=False):
+        ro = ref[L0]
+        assert np.array_equal(ro.results, r.results) and ro.last_index == r.last_index
+        sp = np.where(r.sched_pod == 0xFFFF, -1, r.sched_pod.astype(np.int32)) if u16 else r.sched_pod
+        assert np.array_equal(ro.sched_pod, sp)
+
+    with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as plan:
+        for it in range(4):
+            # phase events off (the bench's timed mode): the host joins the publisher and
+            # both chain streams itself instead of queueing the waits on the plan's stream
+            plan.set_phase_timing(it % 2 == 1)
+            for L0 in (0, 77, 0):
+                check(plan.run_u16(w.max_nodes, L0), L0, u16=True)
+                assert plan.stats()["decoupled"] and plan.stats()["results_path"] == "published"
+            check(plan.run(w.max_nodes, 77, want_nodes=False), 77)
+            d = plan.run(w.max_nodes, 0, device_results=True)
+            assert np.array_equal(ref[0].results, d.results) and np.array_equal(ref[0].sched_pod, plan.fetch())
+            monkeypatch.setenv("CASIM_PUB_SERIAL", "1")
+            check(plan.run_u16(w.max_nodes, 77), 77, u16=True)
+            assert plan.stats()["results_path"] == "publisher_gave_up"
+            monkeypatch.delenv("CASIM_PUB_SERIAL")
 
 
 @pytest.mark.parametrize("size", ["small", "full"])

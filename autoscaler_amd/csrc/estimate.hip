@@ -466,18 +466,12 @@ __global__ void __launch_bounds__(RTHREADS) k_radix_scatter(const GroupMeta* __r
 // record but for its controller — so the chain stream follows from per-class counts alone,
 // with no sort of the pod list.  k_run_table (one workgroup per group; the class ranks
 // computed in its prologue): the class counts of the group's list, each rank's first
-// stream position rstart[g][r] (r in [0, U]), the stream record of the rank's class
-// rsp[g][r] (its representative pod's requests and static bits against the template), then
-// the stream itself — one 64-position window per thread, position -> rank by a walk over
-// rstart, run heads exactly as k_emit_bucket marks them (a head where the record or its
-// bits change, every non-batchable pod) and the records of the windows that hold a head.
-// The pod id of a stream entry is not needed: decoupled chains emit stream positions and
-// the consumers map them through the Go-order ids.
-__device__ inline uint64_t range_bits64(int lo, int hi) {     // bits [lo, hi) of a word, 0 <= lo < hi <= 64
-    const uint64_t up = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
-    return up & ~((1ull << lo) - 1);
-}
-
+// stream position rstart[g][r] (r in [0, U]), and the stream record of the rank's class
+// rsp[g][r] (its representative pod's requests and static bits against the template);
+// round 1 without k_round_init it also sets the group's lastIndex input / need /
+// unsupported flags.  k_emit_runs: the stream itself.  The pod id of a stream entry is not
+// needed: decoupled chains emit stream positions and the consumers map them through the
+// Go-order ids.
 __device__ inline int32_t run_rank(const int32_t* __restrict__ st, int32_t U, int32_t i) {
     int32_t lo = 0, hi = U;                  // the last r with st[r] <= i (st[U] is never read)
     while (hi - lo > 1) {
@@ -496,14 +490,12 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
                                                    const ca_selector_term* __restrict__ terms,
                                                    const ca_selector_req* __restrict__ reqs, int32_t* __restrict__ rstart,
                                                    StreamPod* __restrict__ rsp, uint32_t* __restrict__ group_unsup,
-                                                   const int32_t* __restrict__ gmap, StreamPod* __restrict__ out,
-                                                   uint64_t* __restrict__ heads, int32_t all_windows,
+                                                   const int32_t* __restrict__ gmap,
                                                    int32_t* __restrict__ lin, uint8_t* __restrict__ need, int32_t lin0) {
     // lin != null: round 1 without k_round_init — the group's lastIndex input, need flag and
     // unsupported flag are set here (stored, not or-ed)
     __shared__ int32_t cnt[CLS_MAX];
     __shared__ uint32_t s_unsup;
-    __shared__ uint8_t rfl[CLS_MAX];          // per rank: 1 batchable, 2 its first position is a run head
     __shared__ int32_t rc[CLS_MAX];
     __shared__ int32_t cr[CLS_MAX];           // rank of each class
     __shared__ uint64_t key[CLS_MAX];
@@ -569,7 +561,7 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
     int32_t* rs = rstart + (size_t)gi * (U + 1);
     for (int q = 0; q < 4; q++) {
         const int r = 4 * tid + q;
-        if (r < U) { rs[r] = pre; rc[r] = pre; }            // rc: each rank's first position, from here on
+        if (r < U) rs[r] = pre;
         pre += v[q];
     }
     if (tid == 0) rs[U] = gm.count;
@@ -589,58 +581,55 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
         unsup |= sf & SF_UNSUP;
     }
     if (unsup) atomicOr(&s_unsup, 1u);
-    // the stream (formerly a kernel of its own): run heads exactly as k_emit_bucket marks
-    // them — a head where the record or its bits change, every non-batchable pod — then the
-    // records of the 64-position windows that hold a head (the run-batched chain reads no
-    // other window; all_windows: the per-pod chain reads every one)
-    __syncthreads();                              // rsp (global, this workgroup's writes), rc, s_unsup
+    __syncthreads();                              // s_unsup
     if (tid == 0) {
         if (lin) { lin[gi] = lin0; need[gi] = 1; group_unsup[gi] = s_unsup ? 1u : 0u; }
         else if (s_unsup) atomicOr(&group_unsup[gi], 1u);
     }
-    const StreamPod* rg = rsp + (size_t)gi * U;
-    for (int c = tid; c < U; c += 1024) {
-        if (cnt[c] == 0) continue;
-        const int r = cr[c];
-        const StreamPod sp = rg[r];
-        uint8_t f = (sp.flags & SF_BATCH) ? 1 : 0;
-        bool hs = true;
-        if (rc[r] > 0) {                          // the record before the rank's first position
-            const StreamPod q = rg[run_rank(rc, U, rc[r] - 1)];
-            hs = !((q.flags & ~SF_BATCH) == (sp.flags & ~SF_BATCH) && q.cpu == sp.cpu && q.mem == sp.mem &&
-                   q.eph == sp.eph);
-        }
-        rfl[r] = f | (hs ? 2 : 0);
-    }
+}
+
+// The stream from the run table: one thread per position — position -> rank by binary
+// search of the rank starts in LDS, the record, run heads exactly as k_emit_bucket marks
+// them.  (Measured against a variant inside k_run_table, one thread per 64-position
+// window: 0.49 against 0.50 ms per headline step — the wide grid wins.)
+__global__ void __launch_bounds__(256) k_emit_runs(const GroupMeta* __restrict__ groups,
+                                                  const int32_t* __restrict__ rstart, const StreamPod* __restrict__ rsp,
+                                                  int32_t U, StreamPod* __restrict__ out, uint64_t* __restrict__ heads,
+                                                  const int32_t* __restrict__ gmap, int32_t all_windows) {
+    __shared__ int32_t st[CLS_MAX + 1];
+    const int gi = GSEL(blockIdx.y);
+    const GroupMeta gm = groups[gi];
+    const int32_t base = (int32_t)(blockIdx.x * blockDim.x);
+    if (base >= gm.count) return;                                   // (uniform per block)
+    const int32_t* rs = rstart + (size_t)gi * (U + 1);
+    for (int r = threadIdx.x; r <= U; r += blockDim.x) st[r] = rs[r];
     __syncthreads();
-    const int32_t nwin = (gm.count + 63) >> 6;
-    for (int32_t wdx = tid; wdx < nwin; wdx += 1024) {
-        // the window's rank segments (one in most windows): a non-batchable rank is all
-        // heads, a batchable one has at most its first position
-        const int32_t i0 = wdx * 64, i1 = min(gm.count, i0 + 64);
-        const int32_t r0 = run_rank(rc, U, i0);
-        uint64_t hb = i0 == 0 ? 1ull : 0ull;
-        for (int32_t r = r0, pos = i0; pos < i1; r++) {
-            const int32_t rend = r + 1 < U ? min(rc[r + 1], i1) : i1;
-            if (rend <= pos) continue;                          // (an empty rank)
-            const uint8_t f = rfl[r];
-            if (!(f & 1)) hb |= range_bits64(pos - i0, rend - i0);
-            else if (pos == rc[r] && (f & 2)) hb |= 1ull << (pos - i0);
-            pos = rend;
-        }
-        heads[gm.moff + wdx] = hb;
-        if (hb == 0 && !all_windows) continue;
-        for (int32_t r = r0, pos = i0; pos < i1; r++) {
-            const int32_t rend = r + 1 < U ? min(rc[r + 1], i1) : i1;
-            if (rend <= pos) continue;
-            StreamPod sp = rg[r];
-            const uint32_t fl = sp.flags;
-            for (; pos < rend; pos++) {
-                sp.flags = fl | (((hb >> (pos - i0)) & 1) ? SF_HEAD : 0u);
-                out[gm.off + pos] = sp;
+    const int32_t i = base + (int32_t)threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    if (base + (int32_t)(threadIdx.x & ~63u) >= gm.count) return;   // whole wave past the end
+    bool head = true;
+    StreamPod sp = {};
+    if (i < gm.count) {
+        const int32_t r = run_rank(st, U, i);
+        sp = rsp[(size_t)gi * U + r];
+        const bool bat = (sp.flags & SF_BATCH) != 0;
+        if (i > 0 && bat) {
+            head = false;
+            if (i == st[r]) {                                       // first pod of its class
+                const StreamPod q = rsp[(size_t)gi * U + run_rank(st, U, i - 1)];
+                head = !((q.flags & ~SF_BATCH) == (sp.flags & ~SF_BATCH) && q.cpu == sp.cpu && q.mem == sp.mem &&
+                         q.eph == sp.eph);
             }
         }
+        sp.flags |= head ? SF_HEAD : 0u;
     }
+    const uint64_t hb = __ballot(head);
+    if (lane == 0) heads[gm.moff + (i >> 6)] = hb;
+    // With run batching the chain reads a stream entry only at a run head or inside a
+    // non-batchable run (whose every pod is a head), and only from the 64-entry window
+    // holding it: windows without a head are never read, so they are not written (C2: ~1
+    // window in 10 has a head).  The per-pod chain (CASIM_RUN_BATCH=0) reads every window.
+    if ((hb != 0 || all_windows) && i < gm.count) out[gm.off + i] = sp;
 }
 
 // 1''-2''. Go 1.19 sort.Slice order (binpacking_estimator.go:74; pdqsort.h) ----------
@@ -733,8 +722,8 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
             const int32_t i = i0 + u * pdq::NT;
             if (i >= n) break;
             rmax = max(rmax, r[u]);
-            scr[i] = r[u];
             if (fit) { e16[i] = (uint16_t)i; rk[i] = (uint8_t)r[u]; }
+            else scr[i] = r[u];                        // (the LDS store keeps its ranks in LDS)
         }
     }
     for (int d = 32; d >= 1; d >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, d, 64));
@@ -745,6 +734,20 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
     if (force == 1 && fit && R < 256) mode = 1;
     else if (force == 2 && n <= (1 << 20) && R < 4096) mode = 2;
     else if (force == 3) mode = 3;
+    if (mode != 1 && fit) {
+        // the ranks went to LDS only (8 bits): gather them again for a global store (a group
+        // that fits LDS but has >= 256 ranks, or a forced store in tests)
+        for (int32_t i = tid; i < n; i += pdq::NT) {
+            uint32_t r;
+            if (item_rank) r = item_rank[off + i];
+            else {
+                const int32_t cl = item_cls ? item_cls[off + i] : pcls[pod_idx[off + i]];
+                r = crk ? (uint32_t)crk[cl] : (uint32_t)crank[(size_t)gi * U + cl];
+            }
+            scr[i] = r;
+        }
+        __syncthreads();
+    }
     if (mode == 1) {
         const pdq::LdsStore st{e16, rk, rmb, rmp};
         pdq::wg_sort(st, n, stack, n / 2 + 2, scr, ctl, limit0);
@@ -1275,8 +1278,11 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
                 const uint64_t t0 = wall_clock64();
                 bool started = false;
                 for (;;) {
-                    tk = __hip_atomic_load(&tickets[s_t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    // relaxed polls (an acquire per poll invalidates caches other kernels on
+                    // the XCD are using); the acquire comes once, when the ticket is there
+                    tk = __hip_atomic_load(&tickets[s_t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (tk >= 0) {      // consumed: the slot is -1 again for the next run
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                         __hip_atomic_store(&tickets[s_t], -1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         break;
                     }
@@ -1292,7 +1298,10 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
                 if (tk >= 0 && ids_ready) {                  // the group's Go-order ids
                     const int32_t g = (int32_t)(uint32_t)(tk & 0xFFFFFFFFll) / nsub;
                     for (;;) {
-                        if (__hip_atomic_load(&ids_ready[g], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == ids_epoch) break;
+                        if (__hip_atomic_load(&ids_ready[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ids_epoch) {
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                            break;
+                        }
                         if (__hip_atomic_load(&qctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { tk = -1; break; }
                         if (wall_clock64() - t0 > 20000000ull) {                            // 200 ms
                             __hip_atomic_store(&qctl[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2837,8 +2846,11 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                    p->d_tmpl.as<ca_template>(), p->s->t.hot.as<PodHot>(), p->s->t.spec.as<ca_pod_spec>(),
                                    p->s->t.terms.as<ca_selector_term>(), p->s->t.reqs.as<ca_selector_req>(),
                                    p->d_rstart.as<int32_t>(), p->d_rsp.as<StreamPod>(), p->d_unsup.as<uint32_t>(), gm,
-                                   p->d_stream.as<StreamPod>(), p->d_heads.as<uint64_t>(), batch_runs ? 0 : 1,
                                    fast_init ? p->d_lin.as<int32_t>() : nullptr, p->d_need.as<uint8_t>(), lin0);
+                CA_HIP_CHECK(hipGetLastError());
+                hipLaunchKernelGGL(k_emit_runs, dim3(blocks, ng), dim3(256), 0, ss, p->d_meta.as<GroupMeta>(),
+                                   p->d_rstart.as<int32_t>(), p->d_rsp.as<StreamPod>(), U, p->d_stream.as<StreamPod>(),
+                                   p->d_heads.as<uint64_t>(), gm, batch_runs ? 0 : 1);
                 CA_HIP_CHECK(hipGetLastError());
                 if (events && p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_MERGE], ss));
                 return CA_OK;

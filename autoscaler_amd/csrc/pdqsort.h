@@ -553,7 +553,7 @@ __device__ inline void w_prefix(const int32_t* v, int32_t* o, int n) {
             if (lane >= d) incl += y;
         }
         if (i < n) o[i] = carry + incl - x;
-        carry += __shfl(incl, 63, 64);
+        carry += __builtin_amdgcn_readlane(incl, 63);
     }
     if (lane == 0) o[n] = carry;
 }
@@ -1317,14 +1317,15 @@ __device__ bool wg_partial_insertion(const LdsStore& s, Ctl& c, int a, int b) {
 // The same on the LDS store by one wavefront (frames run it side by side in step A; the
 // frames are disjoint and position a-1 is a placed pivot): ballots in place of the
 // workgroup reductions, and no barrier — a wavefront's LDS accesses are in program order.
-__device__ bool w_partial_insertion(const LdsStore& s, int a, int b) {
-    constexpr int maxSteps = 5, shortestShifting = 50;
+// w_pis_find: one step's searches — the first descent i in [i0, b) (b: the rest is
+// sorted) and, when the step shifts (i < b, b - a >= 50), the landing places of the two
+// bubbling loops.
+__device__ void w_pis_find(const LdsStore& s, int a, int b, int i0, int& i_out, int& landL, int& landR) {
+    constexpr int shortestShifting = 50;
     const int lane = threadIdx.x & 63;
     const uint32_t* r32 = reinterpret_cast<const uint32_t*>(s.rk);
-    uint32_t* w32 = reinterpret_cast<uint32_t*>(s.rk);
-    uint32_t* e32 = reinterpret_cast<uint32_t*>(s.e);
-    int i = a + 1;
-    for (int step = 0; step < maxSteps; step++) {
+    int i = i0;
+    {
         int found = b;
         for (int w0 = i >> 2; 4 * w0 < b; w0 += 64) {           // first descent in [i, b)
             const int w = w0 + lane;
@@ -1336,43 +1337,61 @@ __device__ bool w_partial_insertion(const LdsStore& s, int a, int b) {
                 if (m) q = 4 * w + __builtin_ctz(m);
             }
             const uint64_t bal = __ballot(q != INT_MAX);
-            if (bal) { found = __shfl(q, __builtin_ctzll(bal), 64); break; }
+            if (bal) { found = __builtin_amdgcn_readlane(q, __builtin_ctzll(bal)); break; }
         }
         i = found;
+    }
+    i_out = i;
+    landL = i - 1;
+    landR = i;
+    if (i == b || b - a < shortestShifting) return;
+    const uint32_t ev = s.rk[i], fv = s.rk[i - 1];
+    if (i - a >= 2) {
+        const int lo = a > 0 ? a - 1 : 0, top = i - 2;
+        int q0 = -1;
+        for (int w0 = top >> 2; 4 * w0 + 3 >= lo; w0 -= 64) {
+            const int w = w0 - lane;
+            int q = -1;
+            if (w >= 0 && 4 * w + 3 >= lo) {
+                const uint32_t m = swar_lt4(r32[w], ev + 1) & nib_range(w, lo, top);
+                if (m) q = 4 * w + 31 - __builtin_clz(m);
+            }
+            const uint64_t bal = __ballot(q >= 0);
+            if (bal) { q0 = __builtin_amdgcn_readlane(q, __builtin_ctzll(bal)); break; }
+        }
+        landL = q0 + 1;
+    }
+    if (b - i >= 2) {
+        int j0 = b;
+        for (int w0 = (i + 1) >> 2; 4 * w0 < b; w0 += 64) {
+            const int w = w0 + lane;
+            int j = INT_MAX;
+            if (4 * w < b) {
+                const uint32_t m = ~swar_lt4(r32[w], fv) & nib_range(w, i + 1, b - 1);
+                if (m) j = 4 * w + __builtin_ctz(m);
+            }
+            const uint64_t bal = __ballot(j != INT_MAX);
+            if (bal) { j0 = __builtin_amdgcn_readlane(j, __builtin_ctzll(bal)); break; }
+        }
+        landR = j0 - 1;
+    }
+}
+
+// pi >= 0: the first step's searches were done already (w_pis_find from a + 1: pi, pL, pR)
+__device__ bool w_partial_insertion(const LdsStore& s, int a, int b, int pi = -1, int pL = 0, int pR = 0) {
+    constexpr int maxSteps = 5, shortestShifting = 50;
+    const int lane = threadIdx.x & 63;
+    uint32_t* w32 = reinterpret_cast<uint32_t*>(s.rk);
+    uint32_t* e32 = reinterpret_cast<uint32_t*>(s.e);
+    int i = a + 1;
+    for (int step = 0; step < maxSteps; step++) {
+        int landL, landR;
+        if (step == 0 && pi >= 0) { i = pi; landL = pL; landR = pR; }
+        else w_pis_find(s, a, b, i, i, landL, landR);
         if (i == b) return true;
         if (b - a < shortestShifting) return false;
         const uint32_t ev = s.rk[i], fv = s.rk[i - 1];
         const uint32_t ee = s.e[i], fe = s.e[i - 1];
-        int landL = i - 1, landR = i;
-        if (i - a >= 2) {
-            const int lo = a > 0 ? a - 1 : 0, top = i - 2;
-            int q0 = -1;
-            for (int w0 = top >> 2; 4 * w0 + 3 >= lo; w0 -= 64) {
-                const int w = w0 - lane;
-                int q = -1;
-                if (w >= 0 && 4 * w + 3 >= lo) {
-                    const uint32_t m = swar_lt4(r32[w], ev + 1) & nib_range(w, lo, top);
-                    if (m) q = 4 * w + 31 - __builtin_clz(m);
-                }
-                const uint64_t bal = __ballot(q >= 0);
-                if (bal) { q0 = __shfl(q, __builtin_ctzll(bal), 64); break; }
-            }
-            landL = q0 + 1;
-        }
-        if (b - i >= 2) {
-            int j0 = b;
-            for (int w0 = (i + 1) >> 2; 4 * w0 < b; w0 += 64) {
-                const int w = w0 + lane;
-                int j = INT_MAX;
-                if (4 * w < b) {
-                    const uint32_t m = ~swar_lt4(r32[w], fv) & nib_range(w, i + 1, b - 1);
-                    if (m) j = 4 * w + __builtin_ctz(m);
-                }
-                const uint64_t bal = __ballot(j != INT_MAX);
-                if (bal) { j0 = __shfl(j, __builtin_ctzll(bal), 64); break; }
-            }
-            landR = j0 - 1;
-        }
         const int qL = landL >> 2, qc = (i - 1) >> 2, qR = landR >> 2;
         const int nl = qc - qL + 1, nr = qR - qc;
         for (int done = 0; done < max(nl, nr); done += 64) {
@@ -1481,6 +1500,7 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
             int hint;
             int pivot = w_choose_pivot(s, a, b, &hint);
             PDQ_WADD(17, t_cp);
+            PDQ_SMAXW(14, clock64() - t_cp);
             PDQ_T(t_rv);
             if (hint == HINT_DEC) {
                 w_reverse(s, a, b);
@@ -1494,8 +1514,12 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
                 // run over the whole frame when it is sorted) go to the workgroup below
                 if (pis && b - a <= PIS_WAVE_MAX) {
                     PDQ_T(t_pis);
-                    const bool sorted = w_partial_insertion(s, a, b);
+                    int pi, pL, pR;
+                    w_pis_find(s, a, b, a + 1, pi, pL, pR);
+                    const bool sorted = w_partial_insertion(s, a, b, pi, pL, pR);
                     PDQ_WADD(19, t_pis);
+                    PDQ_SMAXW(13, clock64() - t_pis);
+                    PDQ_SMAXW(15, b - a);
                     PDQ_CNT(20, 1);
                     if (sorted) {
                         if (lane == 0) c.op[i] = OP_DONE;
@@ -1547,23 +1571,27 @@ template <class S> __device__ void wg_sort(const S& s, int n, Frame* __restrict_
         PDQ_S(4, clock64() - t_a2);
         PDQ_T(t_pl);
         if (tid < 64) {                     // the partitioning frames, ordered by start
-            int np = 0;
-            for (int i0 = 0; i0 < nf; i0 += 64) np += __builtin_popcountll(__ballot(i0 + lane < nf && c.op[i0 + lane] != OP_DONE));
-            // rank of frame i among the partitioning frames by start a (starts are distinct)
-            for (int i0 = 0; i0 < nf; i0 += 64) {
-                const int i = i0 + lane;
-                const bool on = i < nf && c.op[i] != OP_DONE;
-                const int ai = on ? c.f[i].a : 0;
-                int r = 0;
-                for (int q = 0; q < nf; q++) {
-                    const bool oq = c.op[q] != OP_DONE;      // (uniform loads: broadcast reads)
-                    r += (oq && c.f[q].a < ai) ? 1 : 0;
-                }
-                if (on) {
-                    c.pl[r] = i;
-                    c.po[r] = c.f[i].b - c.f[i].a - 1;      // (staging for the prefix)
-                }
+            static_assert(MAXF <= 128, "two frames per lane");
+            // rank of frame i among the partitioning frames by start a (starts are distinct):
+            // each lane holds two frames' starts (INT_MAX: not partitioning), the starts are
+            // broadcast by readlane — no LDS load per comparison
+            const bool on0 = lane < nf && c.op[lane] != OP_DONE;
+            const bool on1 = 64 + lane < nf && c.op[64 + lane] != OP_DONE;
+            const int a0 = on0 ? c.f[lane].a : INT_MAX, a1 = on1 ? c.f[64 + lane].a : INT_MAX;
+            const int np = __builtin_popcountll(__ballot(on0)) + __builtin_popcountll(__ballot(on1));
+            int r0 = 0, r1 = 0;
+            for (int q = 0; q < min(nf, 64); q++) {
+                const int aq = __builtin_amdgcn_readlane(a0, q);
+                r0 += aq < a0 ? 1 : 0;
+                r1 += aq < a1 ? 1 : 0;
             }
+            for (int q = 64; q < nf; q++) {
+                const int aq = __builtin_amdgcn_readlane(a1, q - 64);
+                r0 += aq < a0 ? 1 : 0;
+                r1 += aq < a1 ? 1 : 0;
+            }
+            if (on0) { c.pl[r0] = lane; c.po[r0] = c.f[lane].b - a0 - 1; }            // (staging for the prefix)
+            if (on1) { c.pl[r1] = 64 + lane; c.po[r1] = c.f[64 + lane].b - a1 - 1; }
             if (lane == 0) c.np = np;
             w_prefix(c.po, c.fo, np);
         }

@@ -696,7 +696,8 @@ def main():
             out = plan.run_u16(w.max_nodes, lin, copy=False)
         else:
             out = plan.run(w.max_nodes, lin, want_nodes=False, copy=False)
-        sens, succ = plan.chain_info()
+        # (lastIndex sensitivity: only the cross-rank chain of shard.run_sharded reads it)
+        sens, succ = plan.chain_info() if dist is not None else (0, 0)
         return out, out.last_index, sens, succ
 
     coll_dev = f"cuda:{local}" if backend == "nccl" else "cpu"

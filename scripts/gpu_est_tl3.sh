@@ -7,4 +7,6 @@ bash scripts/gpu_est.sh || exit 1
 bash scripts/gpu_tl.sh || exit 1
 CASIM_LIB_PATH=$PWD/autoscaler_amd/lib/libcasim_prof.so timeout -k 10 200 python -u scripts/chain_diag.py > gpurun_out/chain_diag.log 2>&1 || { tail gpurun_out/chain_diag.log; exit 1; }
 cat gpurun_out/chain_diag.log
+CASIM_LIB_PATH=$PWD/autoscaler_amd/lib/libcasim_prof.so timeout -k 10 200 python -u scripts/pdq_prof.py > gpurun_out/pdq_prof.log 2>&1 || { tail gpurun_out/pdq_prof.log; exit 1; }
+cat gpurun_out/pdq_prof.log
 echo EST_TL3_OK

@@ -40,10 +40,10 @@ for g in np.argsort(-sizes)[:3]:
               % tuple(int(x) for x in out[21:27]))
         print("   P3 waves: cycles_sum=%d iters_sum=%d iters_max=%d"
               % tuple(int(x) for x in out[27:30]))
-        print("   step   nf   np   A1wall A1maxw  wgpis(n)      A2  plist      P1      P2      P3       D  elems")
+        print("   step   nf   np   A1wall A1maxw  wgpis(n)      A2  plist      P1      P2      P3       D  elems  wpis_max cp_max wpis_len")
         for st in range(16):
             r = out[32 + 16 * st: 48 + 16 * st].astype(np.int64)
             if r[0] == 0:
                 continue
-            print("   %4d %4d %4d %8d %6d %8d(%d) %7d %6d %7d %7d %7d %7d %6d" % (
-                st, r[0], r[1], r[2], r[11], r[3], r[12], r[4], r[5], r[6], r[7], r[8], r[9], r[10]))
+            print("   %4d %4d %4d %8d %6d %8d(%d) %7d %6d %7d %7d %7d %7d %6d %9d %6d %8d" % (
+                st, r[0], r[1], r[2], r[11], r[3], r[12], r[4], r[5], r[6], r[7], r[8], r[9], r[10], r[13], r[14], r[15]))

@@ -206,6 +206,7 @@ void set_last_error(const std::string& s);
 inline const char* test_hook_env(const char* name) {
     return getenv("CASIM_TEST_HOOKS") ? getenv(name) : nullptr;
 }
+
 const std::string& last_error();
 
 // hipFuncAttributeMaxDynamicSharedMemorySize of a kernel, raised to `bytes` at most once

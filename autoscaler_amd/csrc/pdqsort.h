@@ -43,6 +43,10 @@ namespace pdq {
 #ifdef CASIM_PROF    // phase cycle counters of workgroup 0 (profiling build: ca_debug_pdq_prof)
 __device__ unsigned long long g_pdq_prof[32 + 16 * 16];   // + per-step slots [32 + 16 step + k]
 __device__ int g_pdq_step;
+// wavefront partialInsertionSort, summed over the waves of workgroup 0: find cycles,
+// rotate cycles, search loop trips, rotate loop trips, steps, calls, rotated quads
+__device__ unsigned long long g_pdq_pis[8];
+#define PDQ_PIS(k, v) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) atomicAdd(&g_pdq_pis[k], (unsigned long long)(v)); } while (0)
 #define PDQ_S(k, v) do { if (threadIdx.x == 0 && blockIdx.x == 0 && g_pdq_step < 16) g_pdq_prof[32 + 16 * g_pdq_step + (k)] += (unsigned long long)(v); } while (0)
 #define PDQ_SMAXW(k, v) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0 && g_pdq_step < 16) atomicMax(&g_pdq_prof[32 + 16 * g_pdq_step + (k)], (unsigned long long)(v)); } while (0)
 #define PDQ_T(v) const uint64_t v = clock64()
@@ -56,6 +60,7 @@ __device__ int g_pdq_step;
 #else
 #define PDQ_S(k, v) (void)0
 #define PDQ_SMAXW(k, v) (void)0
+#define PDQ_PIS(k, v) (void)0
 #define PDQ_WADD(i, t) (void)0
 #define PDQ_WMAX(i, t) (void)0
 #define PDQ_TMAX(i, v) (void)0
@@ -764,7 +769,9 @@ __device__ inline uint32_t swar_lt4(uint32_t x, uint32_t bound) {
     const uint32_t d = (x | H) - (b & ~H);
     const uint32_t lt = ((~x & b) | (~(x ^ b) & ~d)) & H;      // bit 7 of each byte
     const uint32_t m = lt >> 7;                                  // bits 0, 8, 16, 24
-    return (m | (m >> 7) | (m >> 14) | (m >> 21)) & 0xFu;
+    // gather bits 0/8/16/24 into 0..3: m * (1 + 2^7 + 2^14 + 2^21) puts them at 21..24 and
+    // no other product lands there (no carries)
+    return ((m * 0x00204081u) >> 21) & 0xFu;
 }
 
 __device__ inline uint64_t range_bits(int lo, int hi) {     // bits [lo, hi) of a word, clamped to [0, 64)
@@ -805,6 +812,10 @@ __device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, 
         const uint32_t bA = A.pk + (A.eq ? 1u : 0u), bB = B.pk + (B.eq ? 1u : 0u);
         const uint4* r16 = reinterpret_cast<const uint4*>(s.rk + p0);
         uint64_t pa = 0, pb = 0;
+        // one bound for a word inside one frame (the SWAR compares are the phase's VALU
+        // cost); a word holding two frames' positions takes both
+        const bool two = memA != 0 && memB != 0;
+        const uint32_t b1 = memA ? bA : bB;
         // quarter q = q0 + lane/4 (mod 4): the 16-byte reads of an LDS lane group then
         // cover distinct banks (lanes are 64 bytes apart)
 #pragma unroll
@@ -815,11 +826,11 @@ __device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, 
 #pragma unroll
             for (int h = 0; h < 4; h++) {
                 const int j = q * 16 + h * 4;
-                pa |= (uint64_t)swar_lt4(wv[h], bA) << j;
-                pb |= (uint64_t)swar_lt4(wv[h], bB) << j;
+                pa |= (uint64_t)swar_lt4(wv[h], b1) << j;
+                if (two) pb |= (uint64_t)swar_lt4(wv[h], bB) << j;
             }
         }
-        pm = (pa & memA) | (pb & memB);
+        pm = two ? (pa & memA) | (pb & memB) : pa & (memA | memB);
     }
     add_count(c, memA != 0, A.slot, __builtin_popcountll(pm & memA));
     add_count(c, memB != 0, B.slot, __builtin_popcountll(pm & memB));
@@ -1060,7 +1071,7 @@ __device__ inline uint32_t swar_ltv4(uint32_t x, uint32_t y) {
     const uint32_t d = (x | H) - (y & ~H);
     const uint32_t lt = ((~x & y) | (~(x ^ y) & ~d)) & H;
     const uint32_t m = lt >> 7;
-    return (m | (m >> 7) | (m >> 14) | (m >> 21)) & 0xFu;
+    return ((m * 0x00204081u) >> 21) & 0xFu;                   // (see swar_lt4)
 }
 __device__ inline uint32_t nib_range(int w, int lo, int hi) {     // bits of positions [lo, hi] in word w
     const int e0 = max(lo - 4 * w, 0), e1 = min(hi - 4 * w, 3);
@@ -1271,19 +1282,19 @@ __device__ bool wg_partial_insertion(const LdsStore& s, Ctl& c, int a, int b) {
         }
         PDQ_ADD(22, t_s0);
         PDQ_T(t_h0);
-        // rewrite [landL, landR] by quads: left quads from the centre quad down, right quads
-        // up from the one after it; a round reads only words no earlier round wrote
+        // rewrite [landL, landR] by quads: the quads strictly between qL and qc shift right by
+        // one, those strictly between qc and qR left (two shifts and an or per word); the (at
+        // most three) quads holding landL, i-1 and landR take the general masked rotation —
+        // computed by threads 0-2 before any word changes, stored after every interior quad.
+        // Interior rounds run outward from the centre and read only words no earlier round
+        // wrote.
         const int qL = landL >> 2, qc = (i - 1) >> 2, qR = landR >> 2;
-        const int nl = qc - qL + 1, nr = qR - qc;
-        for (int done = 0; done < max(nl, nr); done += NT) {
-            uint32_t nv[2][3];
-            int qq[2];
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const int k = done + tid;
-                qq[u] = -1;
-                if (u == 0 ? k >= nl : k >= nr) continue;
-                const int v = u == 0 ? qc - k : qc + 1 + k;
+        uint32_t bnv[3] = {0u, 0u, 0u};
+        int bv = -1;
+        if (tid < 3) {
+            const int v = tid == 0 ? qL : tid == 1 ? qc : qR;
+            const bool dup = (tid == 1 && qc == qL) || (tid == 2 && (qR == qc || qR == qL));
+            if (!dup) {
                 const int p0 = 4 * v;
                 const uint32_t lo = e32[2 * v], hi = e32[2 * v + 1];
                 const uint32_t pe = v > 0 ? e32[2 * v - 1] : 0u;
@@ -1291,22 +1302,41 @@ __device__ bool wg_partial_insertion(const LdsStore& s, Ctl& c, int a, int b) {
                 const uint32_t ne = up ? e32[2 * v + 2] : 0u;
                 const uint32_t cr = w32[v];
                 const uint32_t pr = v > 0 ? w32[v - 1] : 0u, nr8 = up ? w32[v + 1] : 0u;
-                nv[u][0] = rotate_word<16>(lo, pe, hi, p0, landL, i, landR, ee, fe);
-                nv[u][1] = rotate_word<16>(hi, lo, ne, p0 + 2, landL, i, landR, ee, fe);
-                nv[u][2] = rotate_word<8>(cr, pr, nr8, p0, landL, i, landR, ev, fv);
-                qq[u] = v;
+                bnv[0] = rotate_word<16>(lo, pe, hi, p0, landL, i, landR, ee, fe);
+                bnv[1] = rotate_word<16>(hi, lo, ne, p0 + 2, landL, i, landR, ee, fe);
+                bnv[2] = rotate_word<8>(cr, pr, nr8, p0, landL, i, landR, ev, fv);
+                bv = v;
+            }
+        }
+        const int nli = max(qc - qL - 1, 0), nri = max(qR - qc - 1, 0);
+        for (int done = 0; done < max(nli, nri); done += NT) {
+            const int k = done + tid;
+            const bool okL = k < nli, okR = k < nri;
+            const int vl = qc - 1 - k, vr = qc + 1 + k;
+            uint32_t l0 = 0, l1 = 0, l2 = 0, r0 = 0, r1 = 0, r2 = 0;
+            if (okL) {                    // new[p] = old[p - 1]
+                const uint32_t lo = e32[2 * vl], hi = e32[2 * vl + 1], pe = e32[2 * vl - 1];
+                const uint32_t cr = w32[vl], pr = w32[vl - 1];
+                l0 = (lo << 16) | (pe >> 16);
+                l1 = (hi << 16) | (lo >> 16);
+                l2 = (cr << 8) | (pr >> 24);
+            }
+            if (okR) {                    // new[p] = old[p + 1]
+                const uint32_t lo = e32[2 * vr], hi = e32[2 * vr + 1], ne = e32[2 * vr + 2];
+                const uint32_t cr = w32[vr], nr8 = w32[vr + 1];
+                r0 = (lo >> 16) | (hi << 16);
+                r1 = (hi >> 16) | (ne << 16);
+                r2 = (cr >> 8) | (nr8 << 24);
             }
             __syncthreads();
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                if (qq[u] < 0) continue;
-                e32[2 * qq[u]] = nv[u][0];
-                e32[2 * qq[u] + 1] = nv[u][1];
-                w32[qq[u]] = nv[u][2];
-            }
-            if (done == 0 && tid == 0) { c.sx[0] = b; c.sx[1] = -1; c.sx[2] = b; }   // the next step's slots
+            if (okL) { e32[2 * vl] = l0; e32[2 * vl + 1] = l1; w32[vl] = l2; }
+            if (okR) { e32[2 * vr] = r0; e32[2 * vr + 1] = r1; w32[vr] = r2; }
             __syncthreads();
         }
+        if (bv >= 0) { e32[2 * bv] = bnv[0]; e32[2 * bv + 1] = bnv[1]; w32[bv] = bnv[2]; }
+        __syncthreads();                  // (every thread has read this step's search slots)
+        if (tid == 0) { c.sx[0] = b; c.sx[1] = -1; c.sx[2] = b; }   // the next step's slots
+        __syncthreads();
         PDQ_ADD(23, t_h0);
         PDQ_CNT(24, (uint64_t)(i - 1 - landL) + (uint64_t)(landR - i));
         PDQ_CNT(25, (uint64_t)(b - a));
@@ -1324,10 +1354,13 @@ __device__ void w_pis_find(const LdsStore& s, int a, int b, int i0, int& i_out, 
     constexpr int shortestShifting = 50;
     const int lane = threadIdx.x & 63;
     const uint32_t* r32 = reinterpret_cast<const uint32_t*>(s.rk);
+    PDQ_T(t_f0);
+    [[maybe_unused]] int trips = 0;
     int i = i0;
     {
         int found = b;
         for (int w0 = i >> 2; 4 * w0 < b; w0 += 64) {           // first descent in [i, b)
+            trips++;
             const int w = w0 + lane;
             int q = INT_MAX;
             if (4 * w < b) {
@@ -1344,12 +1377,13 @@ __device__ void w_pis_find(const LdsStore& s, int a, int b, int i0, int& i_out, 
     i_out = i;
     landL = i - 1;
     landR = i;
-    if (i == b || b - a < shortestShifting) return;
+    if (i == b || b - a < shortestShifting) { PDQ_PIS(0, clock64() - t_f0); PDQ_PIS(2, trips); return; }
     const uint32_t ev = s.rk[i], fv = s.rk[i - 1];
     if (i - a >= 2) {
         const int lo = a > 0 ? a - 1 : 0, top = i - 2;
         int q0 = -1;
         for (int w0 = top >> 2; 4 * w0 + 3 >= lo; w0 -= 64) {
+            trips++;
             const int w = w0 - lane;
             int q = -1;
             if (w >= 0 && 4 * w + 3 >= lo) {
@@ -1364,6 +1398,7 @@ __device__ void w_pis_find(const LdsStore& s, int a, int b, int i0, int& i_out, 
     if (b - i >= 2) {
         int j0 = b;
         for (int w0 = (i + 1) >> 2; 4 * w0 < b; w0 += 64) {
+            trips++;
             const int w = w0 + lane;
             int j = INT_MAX;
             if (4 * w < b) {
@@ -1375,6 +1410,8 @@ __device__ void w_pis_find(const LdsStore& s, int a, int b, int i0, int& i_out, 
         }
         landR = j0 - 1;
     }
+    PDQ_PIS(0, clock64() - t_f0);
+    PDQ_PIS(2, trips);
 }
 
 // pi >= 0: the first step's searches were done already (w_pis_find from a + 1: pi, pL, pR)
@@ -1384,6 +1421,7 @@ __device__ bool w_partial_insertion(const LdsStore& s, int a, int b, int pi = -1
     uint32_t* w32 = reinterpret_cast<uint32_t*>(s.rk);
     uint32_t* e32 = reinterpret_cast<uint32_t*>(s.e);
     int i = a + 1;
+    PDQ_PIS(5, 1);
     for (int step = 0; step < maxSteps; step++) {
         int landL, landR;
         if (step == 0 && pi >= 0) { i = pi; landL = pL; landR = pR; }
@@ -1393,16 +1431,19 @@ __device__ bool w_partial_insertion(const LdsStore& s, int a, int b, int pi = -1
         const uint32_t ev = s.rk[i], fv = s.rk[i - 1];
         const uint32_t ee = s.e[i], fe = s.e[i - 1];
         const int qL = landL >> 2, qc = (i - 1) >> 2, qR = landR >> 2;
-        const int nl = qc - qL + 1, nr = qR - qc;
-        for (int done = 0; done < max(nl, nr); done += 64) {
-            uint32_t nv[2][3];
-            int qq[2];
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const int k = done + lane;
-                qq[u] = -1;
-                if (u == 0 ? k >= nl : k >= nr) continue;
-                const int v = u == 0 ? qc - k : qc + 1 + k;
+        PDQ_T(t_r0);
+        PDQ_PIS(4, 1);
+        // The quads strictly between qL and qc only shift right by one (new[p] = old[p-1]),
+        // those strictly between qc and qR only left (new[p] = old[p+1]): two shifts and an
+        // or per word.  The (at most three) quads holding landL, i-1 and landR take the
+        // general masked rotation: computed by lanes 0-2 before any word changes, stored
+        // after every interior quad.
+        uint32_t bnv[3] = {0u, 0u, 0u};
+        int bv = -1;
+        if (lane < 3) {
+            const int v = lane == 0 ? qL : lane == 1 ? qc : qR;
+            const bool dup = (lane == 1 && qc == qL) || (lane == 2 && (qR == qc || qR == qL));
+            if (!dup) {
                 const int p0 = 4 * v;
                 const uint32_t lo = e32[2 * v], hi = e32[2 * v + 1];
                 const uint32_t pe = v > 0 ? e32[2 * v - 1] : 0u;
@@ -1410,21 +1451,42 @@ __device__ bool w_partial_insertion(const LdsStore& s, int a, int b, int pi = -1
                 const uint32_t ne = up ? e32[2 * v + 2] : 0u;
                 const uint32_t cr = w32[v];
                 const uint32_t pr = v > 0 ? w32[v - 1] : 0u, nr8 = up ? w32[v + 1] : 0u;
-                nv[u][0] = rotate_word<16>(lo, pe, hi, p0, landL, i, landR, ee, fe);
-                nv[u][1] = rotate_word<16>(hi, lo, ne, p0 + 2, landL, i, landR, ee, fe);
-                nv[u][2] = rotate_word<8>(cr, pr, nr8, p0, landL, i, landR, ev, fv);
-                qq[u] = v;
+                bnv[0] = rotate_word<16>(lo, pe, hi, p0, landL, i, landR, ee, fe);
+                bnv[1] = rotate_word<16>(hi, lo, ne, p0 + 2, landL, i, landR, ee, fe);
+                bnv[2] = rotate_word<8>(cr, pr, nr8, p0, landL, i, landR, ev, fv);
+                bv = v;
+            }
+        }
+        const int nli = max(qc - qL - 1, 0), nri = max(qR - qc - 1, 0);
+        PDQ_PIS(3, (max(nli, nri) + 63) / 64);
+        PDQ_PIS(6, nli + nri);
+        for (int done = 0; done < max(nli, nri); done += 64) {
+            const int k = done + lane;
+            const bool okL = k < nli, okR = k < nri;
+            const int vl = qc - 1 - k, vr = qc + 1 + k;
+            uint32_t l0 = 0, l1 = 0, l2 = 0, r0 = 0, r1 = 0, r2 = 0;
+            if (okL) {                    // new[p] = old[p - 1]
+                const uint32_t lo = e32[2 * vl], hi = e32[2 * vl + 1], pe = e32[2 * vl - 1];
+                const uint32_t cr = w32[vl], pr = w32[vl - 1];
+                l0 = (lo << 16) | (pe >> 16);
+                l1 = (hi << 16) | (lo >> 16);
+                l2 = (cr << 8) | (pr >> 24);
+            }
+            if (okR) {                    // new[p] = old[p + 1]
+                const uint32_t lo = e32[2 * vr], hi = e32[2 * vr + 1], ne = e32[2 * vr + 2];
+                const uint32_t cr = w32[vr], nr8 = w32[vr + 1];
+                r0 = (lo >> 16) | (hi << 16);
+                r1 = (hi >> 16) | (ne << 16);
+                r2 = (cr >> 8) | (nr8 << 24);
             }
             wfence();
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                if (qq[u] < 0) continue;
-                e32[2 * qq[u]] = nv[u][0];
-                e32[2 * qq[u] + 1] = nv[u][1];
-                w32[qq[u]] = nv[u][2];
-            }
+            if (okL) { e32[2 * vl] = l0; e32[2 * vl + 1] = l1; w32[vl] = l2; }
+            if (okR) { e32[2 * vr] = r0; e32[2 * vr + 1] = r1; w32[vr] = r2; }
             wfence();
         }
+        if (bv >= 0) { e32[2 * bv] = bnv[0]; e32[2 * bv + 1] = bnv[1]; w32[bv] = bnv[2]; }
+        wfence();
+        PDQ_PIS(1, clock64() - t_r0);
     }
     return false;
 }

@@ -25,7 +25,7 @@ for g in np.argsort(-sizes)[:3]:
     score = p["score_milli_cpu"][idx] / ac + p["score_memory"][idx] / am
     ranks = np.unique(-score, return_inverse=True)[1].astype(np.uint32)
     for store in (1, 2):
-        out = np.zeros(32 + 256, np.uint64)
+        out = np.zeros(32 + 256 + 8, np.uint64)
         native.go_sort_ranks(ranks, store=store)
         lib.ca_debug_pdq_prof(out.ctypes.data, 1)
         t0 = time.perf_counter()
@@ -40,6 +40,11 @@ for g in np.argsort(-sizes)[:3]:
               % tuple(int(x) for x in out[21:27]))
         print("   P3 waves: cycles_sum=%d iters_sum=%d iters_max=%d"
               % tuple(int(x) for x in out[27:30]))
+        pz = out[288:296].astype(np.int64)
+        print("   wave pis (all waves): find_cyc=%d rot_cyc=%d search_trips=%d rot_trips=%d steps=%d calls=%d quads=%d"
+              % tuple(int(x) for x in pz[:7]))
+        if pz[2] > 0 and pz[3] > 0:
+            print("   per search trip %.0f cyc, per rotate trip %.0f cyc" % (pz[0] / pz[2], pz[1] / pz[3]))
         print("   step   nf   np   A1wall A1maxw  wgpis(n)      A2  plist      P1      P2      P3       D  elems  wpis_max cp_max wpis_len")
         for st in range(16):
             r = out[32 + 16 * st: 48 + 16 * st].astype(np.int64)

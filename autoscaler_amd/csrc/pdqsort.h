@@ -1183,6 +1183,17 @@ template <class S> __device__ bool wg_partial_insertion(const S& s, Ctl& c, int 
     return false;
 }
 
+// The previous step of the same call (pis_hint): when the descent is found at the same i
+// and the moved element's rank repeats, its landing follows from the previous step without
+// a search — ranks repeat a lot (C2: 64 distinct over 50k pods).  Left: the previous step
+// left e (rank ev) at L and every element it passed, now (L, i-1], above ev; so with the
+// same ev the last q <= i-2 with rank <= ev is L.  Right: the previous f (rank fv) sits at
+// R and the elements it passed, now [i, R-1], are below fv; so with the same fv the first
+// j >= i+1 with rank >= fv is R.
+struct PisHint {
+    int i = -1, L = 0, R = 0;
+    uint32_t ev = 0, fv = 0;
+};
 // LDS store: one step is a descent search, the two landing searches and one rewrite of
 // [landL, landR] — swap(i, i-1) and the two bubbling loops together are the rotation
 //   new[landL] = old[i], new[p] = old[p-1] on (landL, i-1], new[p] = old[p+1] on [i, landR),
@@ -1218,6 +1229,7 @@ __device__ bool wg_partial_insertion(const LdsStore& s, Ctl& c, int a, int b) {
     if (tid == 0) { c.sx[0] = b; c.sx[1] = -1; c.sx[2] = b; }
     __syncthreads();
     int i = a + 1;
+    PisHint hint;                          // (uniform: see w_pis_find)
     for (int step = 0; step < maxSteps; step++) {
         PDQ_T(t_d0);
         for (int w0 = i >> 2; 4 * w0 < b; w0 += NT) {          // first descent in [i, b)
@@ -1245,7 +1257,10 @@ __device__ bool wg_partial_insertion(const LdsStore& s, Ctl& c, int a, int b) {
         const uint32_t ev = s.rk[i], fv = s.rk[i - 1];            // the smaller one bubbles left, the greater right
         const uint32_t ee = s.e[i], fe = s.e[i - 1];
         int landL = i - 1, landR = i;
-        if (i - a >= 2) {                  // the last q in [qmin, i-2] with rk[q] <= ev, plus one
+        const bool same = hint.i == i;
+        if (i - a >= 2 && same && ev == hint.ev && hint.L <= i - 2) {
+            landL = hint.L + 1;
+        } else if (i - a >= 2) {           // the last q in [qmin, i-2] with rk[q] <= ev, plus one
             const int lo = a > 0 ? a - 1 : 0, top = i - 2;
             for (int w0 = top >> 2; 4 * w0 + 3 >= lo; w0 -= NT) {
                 const int w = w0 - tid;
@@ -1263,7 +1278,9 @@ __device__ bool wg_partial_insertion(const LdsStore& s, Ctl& c, int a, int b) {
             }
             landL = c.sx[1] + 1;           // (none found: qmin == 0 and landL = 0)
         }
-        if (b - i >= 2) {                  // the first j in [i+1, b) with rk[j] >= fv, minus one
+        if (b - i >= 2 && same && fv == hint.fv && hint.R > i) {
+            landR = hint.R - 1;
+        } else if (b - i >= 2) {           // the first j in [i+1, b) with rk[j] >= fv, minus one
             for (int w0 = (i + 1) >> 2; 4 * w0 < b; w0 += NT) {
                 const int w = w0 + tid;
                 bool hit = false;
@@ -1280,6 +1297,7 @@ __device__ bool wg_partial_insertion(const LdsStore& s, Ctl& c, int a, int b) {
             }
             landR = c.sx[2] - 1;
         }
+        hint.i = i; hint.L = landL; hint.R = landR; hint.ev = ev; hint.fv = fv;
         PDQ_ADD(22, t_s0);
         PDQ_T(t_h0);
         // rewrite [landL, landR] by quads: the quads strictly between qL and qc shift right by
@@ -1350,7 +1368,8 @@ __device__ bool wg_partial_insertion(const LdsStore& s, Ctl& c, int a, int b) {
 // w_pis_find: one step's searches — the first descent i in [i0, b) (b: the rest is
 // sorted) and, when the step shifts (i < b, b - a >= 50), the landing places of the two
 // bubbling loops.
-__device__ void w_pis_find(const LdsStore& s, int a, int b, int i0, int& i_out, int& landL, int& landR) {
+__device__ void w_pis_find(const LdsStore& s, int a, int b, int i0, int& i_out, int& landL, int& landR,
+                           PisHint* hint = nullptr) {
     constexpr int shortestShifting = 50;
     const int lane = threadIdx.x & 63;
     const uint32_t* r32 = reinterpret_cast<const uint32_t*>(s.rk);
@@ -1379,7 +1398,10 @@ __device__ void w_pis_find(const LdsStore& s, int a, int b, int i0, int& i_out, 
     landR = i;
     if (i == b || b - a < shortestShifting) { PDQ_PIS(0, clock64() - t_f0); PDQ_PIS(2, trips); return; }
     const uint32_t ev = s.rk[i], fv = s.rk[i - 1];
-    if (i - a >= 2) {
+    const bool same = hint && hint->i == i;
+    if (i - a >= 2 && same && ev == hint->ev && hint->L <= i - 2) {
+        landL = hint->L + 1;
+    } else if (i - a >= 2) {
         const int lo = a > 0 ? a - 1 : 0, top = i - 2;
         int q0 = -1;
         for (int w0 = top >> 2; 4 * w0 + 3 >= lo; w0 -= 64) {
@@ -1395,7 +1417,9 @@ __device__ void w_pis_find(const LdsStore& s, int a, int b, int i0, int& i_out, 
         }
         landL = q0 + 1;
     }
-    if (b - i >= 2) {
+    if (b - i >= 2 && same && fv == hint->fv && hint->R > i) {
+        landR = hint->R - 1;
+    } else if (b - i >= 2) {
         int j0 = b;
         for (int w0 = (i + 1) >> 2; 4 * w0 < b; w0 += 64) {
             trips++;
@@ -1410,6 +1434,7 @@ __device__ void w_pis_find(const LdsStore& s, int a, int b, int i0, int& i_out, 
         }
         landR = j0 - 1;
     }
+    if (hint) { hint->i = i; hint->L = landL; hint->R = landR; hint->ev = ev; hint->fv = fv; }
     PDQ_PIS(0, clock64() - t_f0);
     PDQ_PIS(2, trips);
 }
@@ -1422,10 +1447,15 @@ __device__ bool w_partial_insertion(const LdsStore& s, int a, int b, int pi = -1
     uint32_t* e32 = reinterpret_cast<uint32_t*>(s.e);
     int i = a + 1;
     PDQ_PIS(5, 1);
+    PisHint hint;
     for (int step = 0; step < maxSteps; step++) {
         int landL, landR;
-        if (step == 0 && pi >= 0) { i = pi; landL = pL; landR = pR; }
-        else w_pis_find(s, a, b, i, i, landL, landR);
+        if (step == 0 && pi >= 0) {
+            i = pi; landL = pL; landR = pR;
+            if (i < b) { hint.i = i; hint.L = landL; hint.R = landR; hint.ev = s.rk[i]; hint.fv = s.rk[i - 1]; }
+        } else {
+            w_pis_find(s, a, b, i, i, landL, landR, &hint);
+        }
         if (i == b) return true;
         if (b - a < shortestShifting) return false;
         const uint32_t ev = s.rk[i], fv = s.rk[i - 1];

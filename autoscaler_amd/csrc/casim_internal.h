@@ -207,6 +207,16 @@ inline const char* test_hook_env(const char* name) {
     return getenv("CASIM_TEST_HOOKS") ? getenv(name) : nullptr;
 }
 
+// Tuning / diagnostic switches of the Estimate path (CASIM_GO_DECOUPLE, CASIM_PUB_SERIAL,
+// ...): read only when CASIM_TEST_HOOKS or CASIM_KNOBS is set in the process (checked once),
+// so a production step reads no environment — each getenv is a scan of it, a dozen per
+// step on the launch path.
+inline bool knobs_enabled() {
+    static const bool on = getenv("CASIM_TEST_HOOKS") != nullptr || getenv("CASIM_KNOBS") != nullptr;
+    return on;
+}
+inline const char* knob_env(const char* name) { return knobs_enabled() ? getenv(name) : nullptr; }
+
 const std::string& last_error();
 
 // hipFuncAttributeMaxDynamicSharedMemorySize of a kernel, raised to `bytes` at most once

@@ -2432,7 +2432,7 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     p->n_hist = 0;
     p->max_rtiles = 0;
     {
-        const char* e = getenv("CASIM_SORT");      // "merge" forces the comparison sort (tests run both)
+        const char* e = knob_env("CASIM_SORT");      // "merge" forces the comparison sort (tests run both)
         p->bucket = s->n_cls <= CLS_MAX && !(e && strcmp(e, "merge") == 0);
     }
     for (int32_t g = 0; g < G; g++) {
@@ -2500,11 +2500,11 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     if ((rc = p->d_spod.reserve(sizeof(int32_t) * tot)) != CA_OK) return rc;
     if ((rc = p->d_seg.reserve(sizeof(Seg) * tot)) != CA_OK) return rc;
     {
-        const char* so = getenv("CASIM_SORT_ORDER");                 // (go_sort_order(), below)
+        const char* so = knob_env("CASIM_SORT_ORDER");                 // (go_sort_order(), below)
         const bool go_ord = !(so && strcmp(so, "stable") == 0);
         p->pch = (p->decouple_ok && go_ord) ? PCH_DECOUPLED : PCH;
     }
-    if (const char* e = getenv("CASIM_PUB_CHUNK")) p->pch = std::max(1, atoi(e));
+    if (const char* e = knob_env("CASIM_PUB_CHUNK")) p->pch = std::max(1, atoi(e));
     const int32_t pch = p->pch;
     p->n_tickets = 0;
     for (int32_t g = 0; g < G; g++) p->n_tickets += (p->h_meta[g].count + pch - 1) / pch;
@@ -2562,7 +2562,7 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
 // the chains are launched just before it, so a chain not running by then means the two
 // kernels were serialised (CASIM_PUB_START_US overrides; default 2 ms)
 uint64_t pub_start_ticks() {
-    const char* e = getenv("CASIM_PUB_START_US");
+    const char* e = knob_env("CASIM_PUB_START_US");
     const long us = e ? std::max(1L, atol(e)) : 2000L;
     return (uint64_t)us * 100ull;
 }
@@ -2594,7 +2594,7 @@ int results_to_host(ca_estimate_plan* p, hipStream_t st, int32_t* sched_pod, uin
 // Estimate's tie order: Go 1.19 sort.Slice (the reference, default) or, with
 // CASIM_SORT_ORDER=stable, ties by list position (the radix / merge paths alone)
 bool go_sort_order() {
-    const char* e = getenv("CASIM_SORT_ORDER");
+    const char* e = knob_env("CASIM_SORT_ORDER");
     return !(e && strcmp(e, "stable") == 0);
 }
 
@@ -2619,7 +2619,7 @@ int launch_pdq_sort(ca_estimate_plan* p, hipStream_t ss, const int32_t* gm, int3
 }
 
 int32_t pub_blocks(bool decoupled) {
-    const char* e = getenv("CASIM_PUB_BLOCKS");
+    const char* e = knob_env("CASIM_PUB_BLOCKS");
     // scripts/pub_sweep.sh on C2: stable order 32 x 4096-output chunks; decoupled Go order
     // (the ids arrive ~0.3 ms into the step, then the link is the bound) 64 x 16384
     return e ? std::max(1, atoi(e)) : (decoupled ? 64 : 32);
@@ -2658,7 +2658,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     size_t lds = chain_lds_bytes(kcap, p->use_ports, p->use_scalar);
     // rows that do not fit the CU's LDS (an unlimited estimate of a large group) live in a
     // per-group HBM slab sized by the group's own pod count
-    const bool grows = lds + sizeof(ChainRed) > 160 * 1024 || (getenv("CASIM_CHAIN_GLOBAL") != nullptr);
+    const bool grows = lds + sizeof(ChainRed) > 160 * 1024 || (knob_env("CASIM_CHAIN_GLOBAL") != nullptr);
     if (grows) {
         lds = 0;
         if (p->slab_max_nodes != lim->max_nodes) {
@@ -2687,7 +2687,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     // (Device-resident results could use the same publisher into the plan's own buffer;
     // measured on C2 it slows the chains more than k_copy_segments after them costs.)
     int32_t* publish = nullptr;
-    if (to_host && !sched_node && p->total > 0 && (int64_t)G * p->nsub < INT32_MAX && !getenv("CASIM_NO_PUBLISH")) {
+    if (to_host && !sched_node && p->total > 0 && (int64_t)G * p->nsub < INT32_MAX && !knob_env("CASIM_NO_PUBLISH")) {
         {
             hipPointerAttribute_t attr;
             const void* hp = sched16 ? (const void*)sched16 : (const void*)sched_pod;
@@ -2700,9 +2700,9 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     }
     // (no fill of the result buffers: k_copy_segments writes every output the chains do
     // not — run placements, and -1 past n_scheduled or for a failed group)
-    const char* rb_env = getenv("CASIM_RUN_BATCH");
+    const char* rb_env = knob_env("CASIM_RUN_BATCH");
     const int32_t batch_runs = (rb_env && rb_env[0] == '0') ? 0 : 1;
-    const bool serial_pub = getenv("CASIM_PUB_SERIAL") != nullptr;
+    const bool serial_pub = knob_env("CASIM_PUB_SERIAL") != nullptr;
     int32_t tickets1 = 0;                               // publisher tickets of round 1 (every group)
     if (publish)
         for (int32_t g = 0; g < G; g++) tickets1 += (p->h_meta[g].count + p->pch - 1) / p->pch;
@@ -2710,7 +2710,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     // beside them (CASIM_GO_DECOUPLE=0: the Go sort ahead of the stream, for tests)
     const bool go_order = go_sort_order();
     const bool decoupled = go_order && p->decouple_ok && p->total > 0 &&
-                           !(getenv("CASIM_GO_DECOUPLE") && atoi(getenv("CASIM_GO_DECOUPLE")) == 0);
+                           !(knob_env("CASIM_GO_DECOUPLE") && atoi(knob_env("CASIM_GO_DECOUPLE")) == 0);
     p->ran_decoupled = decoupled ? 1 : 0;
     if (decoupled) {
         // Go's sort.Slice permutation of every group and its pod ids, on st3 before anything
@@ -2728,7 +2728,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         p->ids_epoch++;
         // the class ranks inside the sort kernel when its LDS has room for the scratch
         const size_t npad = ((size_t)std::min(p->max_count, PDQ_LDS_N) + 63) & ~(size_t)63;
-        const bool fold = 16 * (size_t)NP <= 3 * npad && 2 * (size_t)U <= npad / 8 && !getenv("CASIM_NO_RANK_FOLD");
+        const bool fold = 16 * (size_t)NP <= 3 * npad && 2 * (size_t)U <= npad / 8 && !knob_env("CASIM_NO_RANK_FOLD");
         if (!fold) {
             hipLaunchKernelGGL(k_class_rank, dim3(G), dim3(1024), 0, p->st3, p->d_meta.as<GroupMeta>(),
                                p->d_tmpl.as<ca_template>(), p->s->d_cls_sc.as<int64_t>(), U, NP,
@@ -2751,13 +2751,13 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_START], st));
     // decoupled: the stream from per-class counts (k_run_table) instead of the radix passes
     // and k_emit_bucket (CASIM_RUNS_STREAM=0: the radix path, for tests)
-    const bool runs_stream = !(getenv("CASIM_RUNS_STREAM") && atoi(getenv("CASIM_RUNS_STREAM")) == 0);
+    const bool runs_stream = !(knob_env("CASIM_RUNS_STREAM") && atoi(knob_env("CASIM_RUNS_STREAM")) == 0);
     // round 1 without k_round_init: k_run_table sets each group's lastIndex / need /
     // unsupported flags, and the publisher's tickets and control words are clean from the
     // last run (ca_estimate_plan::pub_clean) — no launch and no cross-stream event ahead of
     // the chains
     const bool fast_init = decoupled && runs_stream && (!publish || p->pub_clean) && !serial_pub &&
-                           !getenv("CASIM_NO_FAST_INIT");
+                           !knob_env("CASIM_NO_FAST_INIT");
     const int32_t lin0 = *last_index;
     if (publish) p->pub_clean = false;        // set again once this run's publishers all finished clean
     bool pub_gave_up = false;
@@ -2773,7 +2773,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     bool split = false;
     const int32_t* gmapA = nullptr;
     const int32_t* gmapB = nullptr;
-    if (p->total > 0 && p->bucket && G >= 8 && !getenv("CASIM_NO_SPLIT")) {
+    if (p->total > 0 && p->bucket && G >= 8 && !knob_env("CASIM_NO_SPLIT")) {
         // The heavy set: groups whose chain cost is within 60% of the largest, if that is
         // at most half the batch (a flat distribution gains nothing from the split).
         // First from the demand model, then once from the chain times the previous run

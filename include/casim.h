@@ -368,8 +368,9 @@ int ca_check_templates(ca_mirror* m, const ca_podset* s, const int32_t* samples,
  * results[g]; sched_pod/sched_node[group_off[g] + i] = i-th scheduled pod (pod set index)
  * and the new-node ordinal it went to (sched_node may be NULL).  The pods are sorted by
  * float64 score in Go 1.19 sort.Slice order (binpacking_estimator.go:74: pdqsort_func,
- * ties included).  CASIM_SORT_ORDER=stable in the environment breaks
- * ties by list position instead (the round-2 order, kept for A/B measurements). */
+ * ties included).  CASIM_SORT_ORDER=stable in the environment (with
+ * CASIM_KNOBS=1: the Estimate path's switches are read only then) breaks ties by list
+ * position instead (the round-2 order, kept for A/B measurements). */
 int ca_estimate_batch(ca_mirror* m, const ca_podset* s,
                       const int32_t* group_off, const int32_t* pod_idx,
                       const ca_template* templates, int32_t n_groups,

@@ -129,3 +129,75 @@ def test_device_go_sort_c2_c4_keys():
             want = pyoracle.go_sort_desc(score)
             for store in (0, 2):
                 assert np.array_equal(want, native.go_sort_ranks(ranks, store=store)), (w.name, g, store)
+
+
+def _pis_landings(d, a, b, check):
+    """Go's partialInsertionSort_func on ranks d[a:b] (less = <), recording each step's
+    landing places the way the device computes them (search on the data before the swap);
+    check(prev, cur) runs on consecutive steps of one call."""
+    i, prev = a + 1, None
+    for _ in range(5):
+        while i < b and not d[i] < d[i - 1]:
+            i += 1
+        if i == b or b - a < 50:
+            return
+        ev, fv = d[i], d[i - 1]
+        lo = a - 1 if a > 0 else 0
+        L = i - 1
+        if i - a >= 2:
+            L = next((q for q in range(i - 2, lo - 1, -1) if d[q] <= ev), -1) + 1
+        R = i
+        if b - i >= 2:
+            R = next((j for j in range(i + 1, b) if d[j] >= fv), b) - 1
+        cur = (i, L, R, ev, fv)
+        if prev is not None:
+            check(prev, cur, a, b)
+        prev = cur
+        d[i], d[i - 1] = d[i - 1], d[i]
+        if i - a >= 2:
+            j = i - 1
+            while j >= 1 and d[j] < d[j - 1]:
+                d[j], d[j - 1] = d[j - 1], d[j]
+                j -= 1
+        if b - i >= 2:
+            j = i + 1
+            while j < b and d[j] < d[j - 1]:
+                d[j], d[j - 1] = d[j - 1], d[j]
+                j += 1
+
+
+def test_pis_landing_shortcuts():
+    """The device's partialInsertionSort skips a landing search when the descent repeats at
+    the same i with the same moved rank (pdqsort.h PisHint): left landing = previous L + 1,
+    right landing = previous R - 1.  Checked against the searches on random near-sorted
+    rank sequences with repeated ranks (the C2 shape: few distinct ranks)."""
+    import random
+    rng = random.Random(7)
+    hits = [0, 0]
+
+    def check(prev, cur, a, b):
+        pi, pL, pR, pev, pfv = prev
+        i, L, R, ev, fv = cur
+        if i != pi:
+            return
+        if i - a >= 2 and ev == pev and pL <= i - 2:
+            assert L == pL + 1
+            hits[0] += 1
+        if b - i >= 2 and fv == pfv and pR > i:
+            assert R == pR - 1
+            hits[1] += 1
+
+    for _ in range(3000):
+        n = rng.randint(50, 300)
+        k = rng.choice([2, 3, 5, 8, 64])
+        d = sorted(rng.randrange(k) for _ in range(n))
+        for _ in range(rng.randint(0, 5)):
+            x, y = rng.randrange(n), rng.randrange(n)
+            d[x], d[y] = d[y], d[x]
+        if rng.random() < 0.5:
+            cut = rng.randrange(n)
+            d = d[cut:] + d[:cut]
+        a = rng.randint(0, 3)
+        arr = [min(d) - 1] * a + d            # a placed pivot region left of the frame
+        _pis_landings(arr, a, len(arr), check)
+    assert hits[0] > 100 and hits[1] > 100, hits

@@ -663,6 +663,9 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
                                                      const int64_t* __restrict__ cls_sc, int32_t NP) {
     extern __shared__ __align__(16) unsigned char pdq_dyn[];
     __shared__ pdq::Ctl ctl;
+#ifdef CASIM_PROF
+    const uint64_t t_k0 = clock64();
+#endif
     const int gi = GSEL(blockIdx.x);
     const GroupMeta gm = groups[gi];
     const int32_t n = gm.count, off = gm.off;
@@ -682,6 +685,14 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
     // (free until the ranks are loaded), the rank of each class in the partition bitmap
     // area (free until the first partition); the host checks both fit
     const uint16_t* crk = nullptr;
+    // the first slice of the list's classes is requested before the class ranking, so its
+    // latency hides behind the ranking's barriers
+    int32_t pre[PDQ_UB];
+    const bool preload = item_cls && !item_rank;
+    if (preload) {
+#pragma unroll
+        for (int u = 0; u < PDQ_UB; u++) { const int32_t i = tid + u * pdq::NT; pre[u] = i < n ? item_cls[off + i] : 0; }
+    }
     if (cls_sc) {
         uint64_t* key = reinterpret_cast<uint64_t*>(pdq_dyn);
         uint32_t* idx = reinterpret_cast<uint32_t*>(pdq_dyn + 8 * (size_t)NP);
@@ -702,7 +713,10 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
             for (int u = 0; u < PDQ_UB; u++) { const int32_t i = i0 + u * pdq::NT; r[u] = i < n ? item_rank[off + i] : 0u; }
         } else {
             int32_t pi[PDQ_UB], cl[PDQ_UB];
-            if (item_cls) {
+            if (item_cls && preload && i0 == tid) {
+#pragma unroll
+                for (int u = 0; u < PDQ_UB; u++) cl[u] = pre[u];
+            } else if (item_cls) {
 #pragma unroll
                 for (int u = 0; u < PDQ_UB; u++) { const int32_t i = i0 + u * pdq::NT; cl[u] = i < n ? item_cls[off + i] : 0; }
             } else {
@@ -750,23 +764,57 @@ __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restric
     }
     if (mode == 1) {
         const pdq::LdsStore st{e16, rk, rmb, rmp};
+#ifdef CASIM_PROF
+        const uint64_t t_k1 = clock64();
+#endif
         pdq::wg_sort(st, n, stack, n / 2 + 2, scr, ctl, limit0);
-        if (ids_out) {                                 // decoupled Go order: the ids themselves
-            for (int32_t k0 = tid; k0 < n; k0 += pdq::NT * PDQ_UB) {
-                int32_t v[PDQ_UB];
+#ifdef CASIM_PROF
+        const uint64_t t_k2 = clock64();
+#endif
+        if (ids_out) {
+            // decoupled Go order: the pod ids in sorted order.  A gather pod_idx[off +
+            // e16[k]] straight from memory was ~40 % of the slowest workgroup's time on C2
+            // (random 4-byte reads, every group at once); instead the group's list goes
+            // through the LDS the sort no longer needs (the rank bytes and the partition
+            // bitmaps) in coalesced slices, and each pass picks the sorted positions that
+            // fall in its slice.
+            int32_t* const buf = reinterpret_cast<int32_t*>(rk);
+            // (npad >= 64: at least 16 entries per slice)
+            const int32_t cap = (int32_t)((npad + (npad / 64) * 10) / 4);
+            for (int32_t lo = 0; lo < n; lo += cap) {
+                const int32_t hi = min(n, lo + cap);
+                __syncthreads();                       // (the previous slice is consumed)
+                constexpr int SL = 16;                 // a slice is one round of loads per thread
+                for (int32_t j0 = lo + tid; j0 < hi; j0 += pdq::NT * SL) {
+                    int32_t v[SL];
 #pragma unroll
-                for (int u = 0; u < PDQ_UB; u++) {
-                    const int32_t k = k0 + u * pdq::NT;
-                    v[u] = k < n ? pod_idx[off + e16[k]] : 0;
+                    for (int u = 0; u < SL; u++) {
+                        const int32_t j = j0 + u * pdq::NT;
+                        v[u] = j < hi ? pod_idx[off + j] : 0;
+                    }
+#pragma unroll
+                    for (int u = 0; u < SL; u++) {
+                        const int32_t j = j0 + u * pdq::NT;
+                        if (j < hi) buf[j - lo] = v[u];
+                    }
                 }
-#pragma unroll
-                for (int u = 0; u < PDQ_UB; u++) {
-                    const int32_t k = k0 + u * pdq::NT;
-                    if (k < n) ids_out[off + k] = v[u];
+                __syncthreads();
+                for (int32_t k = tid; k < n; k += pdq::NT) {
+                    const int32_t pos = e16[k];
+                    if (pos >= lo && pos < hi) ids_out[off + k] = buf[pos - lo];
                 }
             }
         } else
             for (int32_t k = tid; k < n; k += pdq::NT) sorted[off + k] = e16[k];
+#ifdef CASIM_PROF
+        __syncthreads();
+        if (tid == 0 && gi < 128) {
+            const uint64_t t_k3 = clock64();
+            pdq::g_pdq_wg[3 * gi] = t_k3 - t_k0;
+            pdq::g_pdq_wg[3 * gi + 1] = t_k1 - t_k0;
+            pdq::g_pdq_wg[3 * gi + 2] = t_k3 - t_k2;
+        }
+#endif
     } else if (mode == 2) {
         uint32_t* e = reinterpret_cast<uint32_t*>(gE + off);
         for (int32_t i = tid; i < n; i += pdq::NT) e[i] = (scr[i] << 20) | (uint32_t)i;
@@ -3162,7 +3210,9 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         CA_HIP_CHECK(hipMemcpyAsync(sched_node, p->d_sched_node.ptr, sizeof(int32_t) * std::max(p->total, 0),
                                     hipMemcpyDeviceToHost, st));
     if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_D2H], st));
-    CA_HIP_CHECK(hipStreamSynchronize(st));
+    // (published with the host joining the streams: the round's event already covered
+    // everything queued on st, nothing was queued since)
+    if (!(host_joins && p->pub_state == 1)) CA_HIP_CHECK(hipStreamSynchronize(st));
     for (int32_t g = 0; g < G; g++) {
         const ChainOut& o = outs[g];
         ca_estimate_result& r = results[g];
@@ -3362,6 +3412,7 @@ int ca_go_sort_ranks(int32_t device, const uint32_t* ranks, int32_t n, int32_t s
 int ca_debug_pdq_prof(uint64_t* out, int32_t reset) {
     CA_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(pdq::g_pdq_prof), sizeof(uint64_t) * (32 + 256)));
     CA_HIP_CHECK(hipMemcpyFromSymbol(out + 32 + 256, HIP_SYMBOL(pdq::g_pdq_pis), sizeof(uint64_t) * 8));
+    CA_HIP_CHECK(hipMemcpyFromSymbol(out + 32 + 256 + 8, HIP_SYMBOL(pdq::g_pdq_wg), sizeof(uint64_t) * 3 * 128));
     if (reset) {
         static const uint64_t z[32 + 256] = {};
         CA_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(pdq::g_pdq_prof), z, sizeof z));

@@ -46,6 +46,9 @@ __device__ int g_pdq_step;
 // wavefront partialInsertionSort, summed over the waves of workgroup 0: find cycles,
 // rotate cycles, search loop trips, rotate loop trips, steps, calls, rotated quads
 __device__ unsigned long long g_pdq_pis[8];
+// per workgroup (group slot < 128): kernel cycles, prologue (ranks into the store) cycles,
+// epilogue (ids out) cycles
+__device__ unsigned long long g_pdq_wg[3 * 128];
 #define PDQ_PIS(k, v) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) atomicAdd(&g_pdq_pis[k], (unsigned long long)(v)); } while (0)
 #define PDQ_S(k, v) do { if (threadIdx.x == 0 && blockIdx.x == 0 && g_pdq_step < 16) g_pdq_prof[32 + 16 * g_pdq_step + (k)] += (unsigned long long)(v); } while (0)
 #define PDQ_SMAXW(k, v) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0 && g_pdq_step < 16) atomicMax(&g_pdq_prof[32 + 16 * g_pdq_step + (k)], (unsigned long long)(v)); } while (0)

@@ -25,7 +25,7 @@ for g in np.argsort(-sizes)[:3]:
     score = p["score_milli_cpu"][idx] / ac + p["score_memory"][idx] / am
     ranks = np.unique(-score, return_inverse=True)[1].astype(np.uint32)
     for store in (1, 2):
-        out = np.zeros(32 + 256 + 8, np.uint64)
+        out = np.zeros(32 + 256 + 8 + 384, np.uint64)
         native.go_sort_ranks(ranks, store=store)
         lib.ca_debug_pdq_prof(out.ctypes.data, 1)
         t0 = time.perf_counter()
@@ -52,3 +52,22 @@ for g in np.argsort(-sizes)[:3]:
                 continue
             print("   %4d %4d %4d %8d %6d %8d(%d) %7d %6d %7d %7d %7d %7d %6d %9d %6d %8d" % (
                 st, r[0], r[1], r[2], r[11], r[3], r[12], r[4], r[5], r[6], r[7], r[8], r[9], r[10], r[13], r[14], r[15]))
+
+# every group's sort in the headline configuration (the C2 plan, decoupled Go order):
+# per-workgroup kernel / prologue / epilogue cycles
+m = native.Mirror(0)
+W.load_estimate(m, w)
+plan = native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates)
+plan.set_phase_timing(False)
+for _ in range(3):
+    plan.run_u16(w.max_nodes, 0, copy=False)
+out = np.zeros(32 + 256 + 8 + 384, np.uint64)
+lib.ca_debug_pdq_prof(out.ctypes.data, 1)
+plan.run_u16(w.max_nodes, 0, copy=False)
+out[:] = 0
+lib.ca_debug_pdq_prof(out.ctypes.data, 0)
+wg = out[296:296 + 384].reshape(128, 3).astype(np.int64)[: len(w.templates)]
+order = np.argsort(-wg[:, 0])
+print("plan sorts: kernel cycles max %d median %d min %d" % (wg[:, 0].max(), np.median(wg[:, 0]), wg[:, 0].min()))
+for g in order[:8]:
+    print("   group %3d n=%d: total %d prologue %d epilogue %d" % (g, sizes[g], wg[g, 0], wg[g, 1], wg[g, 2]))

@@ -283,6 +283,39 @@ constexpr int RCH = RT / 64 / (RTHREADS / 64);   // 64-item chunks per wave
 __device__ inline void block_class_rank(const ca_template& tp, const int64_t* __restrict__ cls_sc, int32_t U,
                                         int32_t NP, uint64_t* key, uint32_t* idx, int32_t* sc) {
     const int64_t acpu = tp.node.alloc_milli_cpu, amem = tp.node.alloc_memory;
+    if (NP <= 64) {
+        // one wavefront: lane i holds class i's key; its place in the (key, class) order and
+        // its dense rank are counts over the other lanes (readlane broadcasts, no barrier
+        // per bitonic stage)
+        if (threadIdx.x < 64) {
+            const int lane = (int)threadIdx.x;
+            uint64_t k = ~0ull;
+            if (lane < U) {
+                double score = 0.0;
+                if (acpu > 0) score += (double)cls_sc[2 * lane] / (double)acpu;
+                if (amem > 0) score += (double)cls_sc[2 * lane + 1] / (double)amem;
+                k = ~ordered_bits(score);
+            }
+            const uint32_t klo = (uint32_t)k, khi = (uint32_t)(k >> 32);
+            int pos = 0, eq_before = 0;
+            for (int j = 0; j < NP; j++) {
+                const uint64_t kj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(khi, j) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane(klo, j);
+                pos += (kj < k || (kj == k && j < lane)) ? 1 : 0;
+                eq_before += (kj == k && j < lane) ? 1 : 0;
+            }
+            const int first = eq_before == 0 ? 1 : 0;       // the lowest class holding its key
+            int dense = 0;
+            for (int j = 0; j < NP; j++) {
+                const uint64_t kj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(khi, j) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane(klo, j);
+                dense += (__builtin_amdgcn_readlane(first, j) && kj < k) ? 1 : 0;
+            }
+            if (lane < NP) { key[pos] = k; idx[pos] = (uint32_t)lane; sc[pos] = dense; }
+        }
+        __syncthreads();
+        return;
+    }
     for (int i = threadIdx.x; i < NP; i += blockDim.x) {
         uint64_t k = ~0ull;
         if (i < U) {
@@ -472,6 +505,10 @@ __global__ void __launch_bounds__(RTHREADS) k_radix_scatter(const GroupMeta* __r
 // unsupported flags.  k_emit_runs: the stream itself.  The pod id of a stream entry is not
 // needed: decoupled chains emit stream positions and the consumers map them through the
 // Go-order ids.
+#ifdef CASIM_PROF
+// k_run_table phase cycles per group slot (< 1024): ranking, counting, scan, records
+__device__ unsigned long long g_rt_prof[1024][4];
+#endif
 __device__ inline int32_t run_rank(const int32_t* __restrict__ st, int32_t U, int32_t i) {
     int32_t lo = 0, hi = U;                  // the last r with st[r] <= i (st[U] is never read)
     while (hi - lo > 1) {
@@ -505,6 +542,9 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
     const GroupMeta gm = groups[gi];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid == 0) s_unsup = 0;
+#ifdef CASIM_PROF
+    const uint64_t t_r0 = clock64();
+#endif
     // the first RUB list positions per thread are loaded before the class ranking, so their
     // latency hides behind it; RUB positions per thread are in flight together after that
     constexpr int RUB = 16;
@@ -519,13 +559,19 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
     __syncthreads();
     for (int i = tid; i < U; i += 1024) { cnt[i] = 0; rc[i] = 0; }
     __syncthreads();
-    // class counts: the lanes of a wave holding one class add once (controllers come in runs)
+#ifdef CASIM_PROF
+    const uint64_t t_r1 = clock64();
+#endif
+    // class counts: the lanes of a wave holding one class add once (controllers come in runs);
+    // the next slice's classes are requested before this slice is counted
     for (int32_t base = 0; base < gm.count; base += 1024 * RUB) {
-        if (base > 0) {
+        int32_t nx[RUB];
+        const bool more = base + 1024 * RUB < gm.count;
+        if (more) {
 #pragma unroll
             for (int u = 0; u < RUB; u++) {
-                const int32_t i = base + u * 1024 + tid;
-                cv[u] = i < gm.count ? item_cls[gm.off + i] : -1;
+                const int32_t i = base + 1024 * RUB + u * 1024 + tid;
+                nx[u] = i < gm.count ? item_cls[gm.off + i] : -1;
             }
         }
 #pragma unroll
@@ -541,11 +587,18 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
                 act &= ~m;
             }
         }
+        if (more) {
+#pragma unroll
+            for (int u = 0; u < RUB; u++) cv[u] = nx[u];
+        }
     }
     __syncthreads();
     for (int c = tid; c < U; c += 1024)
         if (cnt[c] > 0) atomicAdd(&rc[cr[c]], cnt[c]);
     __syncthreads();
+#ifdef CASIM_PROF
+    const uint64_t t_r2 = clock64();
+#endif
     // exclusive scan of the counts by rank: thread t owns ranks [4t, 4t + 4)
     int32_t v[4], loc = 0;
     for (int q = 0; q < 4; q++) { const int r = 4 * tid + q; v[q] = r < U ? rc[r] : 0; loc += v[q]; }
@@ -565,6 +618,9 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
         pre += v[q];
     }
     if (tid == 0) rs[U] = gm.count;
+#ifdef CASIM_PROF
+    const uint64_t t_r3 = clock64();
+#endif
     // the record of each present class, at its rank
     const ca_template& tp = tmpls[gm.tmpl];
     const bool tunsched = (tp.node.flags & CA_NODE_UNSCHEDULABLE) != 0;
@@ -585,6 +641,13 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
     if (tid == 0) {
         if (lin) { lin[gi] = lin0; need[gi] = 1; group_unsup[gi] = s_unsup ? 1u : 0u; }
         else if (s_unsup) atomicOr(&group_unsup[gi], 1u);
+#ifdef CASIM_PROF
+        if (gi < 1024) {
+            const uint64_t t_r4 = clock64();
+            g_rt_prof[gi][0] = t_r1 - t_r0; g_rt_prof[gi][1] = t_r2 - t_r1;
+            g_rt_prof[gi][2] = t_r3 - t_r2; g_rt_prof[gi][3] = t_r4 - t_r3;
+        }
+#endif
     }
 }
 
@@ -1258,7 +1321,7 @@ __device__ inline int32_t run_end_pf(const uint64_t* __restrict__ hm, int32_t po
 // chain's critical path.  Other chunks (single placements, a segment boundary with another
 // offset, the group's tail) go with the release and the progress record.
 constexpr int PCH = 4096;      // default chunk (CASIM_PUB_CHUNK overrides, for tests)
-constexpr int PCH_DECOUPLED = 16384;   // ... with the decoupled Go order (scripts/pub_sweep.sh)
+constexpr int PCH_DECOUPLED = 8192;    // ... with the decoupled Go order (scripts/gpu_pubsweep2.sh)
 __device__ inline void push_chunks(int32_t g, int32_t c0, int32_t c1, int32_t nsub, int64_t* tickets, int32_t* qctl,
                                    int2* prog, int32_t nseg, int32_t nsched, int lane, int32_t pch = 0,
                                    int32_t pure_from = INT32_MAX, int32_t pure_off = 0) {
@@ -1385,8 +1448,25 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
         const Seg* gs = segs + gm.off;
         const int32_t a = sub * pch, b = min(gm.count, a + pch);
         if (pure_off >= 0) {
-            for (int32_t i = a + (int32_t)threadIdx.x; i < b; i += blockDim.x)
-                pub[gm.off + i] = (T)spod[gm.off + pure_off + i];
+            // one contiguous copy: 16-byte stores into the page-locked buffer (fewer, fuller
+            // PCIe writes), scalar stores for the unaligned head and tail
+            constexpr int V = 16 / (int)sizeof(T);
+            T* const dst = pub + gm.off;
+            const int32_t* const src = spod + gm.off + pure_off;
+            int32_t h = a;
+            while (h < b && ((uintptr_t)(dst + h) & 15u)) h++;                 // aligned from h on
+            const int32_t nv = (b - h) / V;
+            for (int32_t i = a + (int32_t)threadIdx.x; i < h; i += blockDim.x) dst[i] = (T)src[i];
+            for (int32_t v = (int32_t)threadIdx.x; v < nv; v += blockDim.x) {
+                const int32_t i0 = h + v * V;
+                T w[V];
+#pragma unroll
+                for (int u = 0; u < V; u++) w[u] = (T)src[i0 + u];
+                uint4 q;
+                __builtin_memcpy(&q, w, 16);
+                *reinterpret_cast<uint4*>(dst + i0) = q;
+            }
+            for (int32_t i = h + nv * V + (int32_t)threadIdx.x; i < b; i += blockDim.x) dst[i] = (T)src[i];
             lds_barrier();
             continue;
         }
@@ -2669,8 +2749,11 @@ int launch_pdq_sort(ca_estimate_plan* p, hipStream_t ss, const int32_t* gm, int3
 int32_t pub_blocks(bool decoupled) {
     const char* e = knob_env("CASIM_PUB_BLOCKS");
     // scripts/pub_sweep.sh on C2: stable order 32 x 4096-output chunks; decoupled Go order
-    // (the ids arrive ~0.3 ms into the step, then the link is the bound) 64 x 16384
-    return e ? std::max(1, atoi(e)) : (decoupled ? 64 : 32);
+    // 128 x 8192 (round 4: each group's ids are ready when its own sort ends, from ~0.17 ms
+    // on; more blocks in flight keep a block waiting on a late group from holding up the
+    // ready ones — 0.474 against 0.478 ms for 64 x 16384, interleaved repeats,
+    // scripts/gpu_pubsweep2.sh)
+    return e ? std::max(1, atoi(e)) : (decoupled ? 128 : 32);
 }
 
 size_t chain_lds_bytes(int32_t kcap, bool use_ports, bool use_scalar) {
@@ -3424,6 +3507,11 @@ int ca_debug_pdq_prof(uint64_t* out, int32_t reset) {
 int ca_debug_chain_prof(uint64_t* out, int32_t n_groups) {
     if (n_groups > 1024) n_groups = 1024;
     CA_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_prof), sizeof(uint64_t) * NPROF * (size_t)n_groups));
+    return CA_OK;
+}
+int ca_debug_rt_prof(uint64_t* out, int32_t n_groups) {     // k_run_table phases: 4 per group
+    if (n_groups > 1024) n_groups = 1024;
+    CA_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt_prof), sizeof(uint64_t) * 4 * (size_t)n_groups));
     return CA_OK;
 }
 #endif

@@ -33,3 +33,11 @@ if os.environ.get("CASIM_LIB_PATH", "").endswith("libcasim_prof.so"):
     names = ["run_end", "capa", "revol", "update", "open", "total", "n_rev", "n_runs", "prologue", "post_bar", "exhausted", "run_total"]
     for g in order[:6]:
         print(f"g{g:3d} " + " ".join(f"{n}={int(v)}" for n, v in zip(names, buf[g])))
+
+    if hasattr(lib, "ca_debug_rt_prof"):
+        rt = np.zeros((G, 4), np.uint64)
+        plan.run_u16(w.max_nodes, 0, copy=False)
+        lib.ca_debug_rt_prof(rt.ctypes.data_as(C.POINTER(C.c_uint64)), G)
+        print("k_run_table cycles (ranking, counting, scan, records), heaviest groups:")
+        for g in order[:6]:
+            print(f"g{g:3d} " + " ".join(str(int(v)) for v in rt[g]))

@@ -280,40 +280,49 @@ constexpr int RCH = RT / 64 / (RTHREADS / 64);   // 64-item chunks per wave
 // Dense ranks of the U score classes against a group's template, by one 1024-thread
 // workgroup: float64 score of every class, bitonic sort of the classes in LDS, dense rank
 // (equal scores share a rank).  On return sc[i] is the rank of class idx[i], i < U.
+// block_class_rank for NP <= 64 by one wavefront, the class score sums already loaded
+// (lane i: class i's cpu / memory sums; any value past U): lane i holds class i's key; its
+// place in the (key, class) order and its dense rank are counts over the other lanes
+// (readlane broadcasts, no barrier per bitonic stage).  Every thread of the block calls it.
+__device__ inline void wave_class_rank(const ca_template& tp, int64_t s_cpu, int64_t s_mem, int32_t U, int32_t NP,
+                                       uint64_t* key, uint32_t* idx, int32_t* sc) {
+    const int64_t acpu = tp.node.alloc_milli_cpu, amem = tp.node.alloc_memory;
+    if (threadIdx.x < 64) {
+        const int lane = (int)threadIdx.x;
+        uint64_t k = ~0ull;
+        if (lane < U) {
+            double score = 0.0;               // calculatePodScore, same float64 operations
+            if (acpu > 0) score += (double)s_cpu / (double)acpu;
+            if (amem > 0) score += (double)s_mem / (double)amem;
+            k = ~ordered_bits(score);
+        }
+        const uint32_t klo = (uint32_t)k, khi = (uint32_t)(k >> 32);
+        int pos = 0, eq_before = 0;
+        for (int j = 0; j < NP; j++) {
+            const uint64_t kj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(khi, j) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane(klo, j);
+            pos += (kj < k || (kj == k && j < lane)) ? 1 : 0;
+            eq_before += (kj == k && j < lane) ? 1 : 0;
+        }
+        const int first = eq_before == 0 ? 1 : 0;           // the lowest class holding its key
+        int dense = 0;
+        for (int j = 0; j < NP; j++) {
+            const uint64_t kj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(khi, j) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane(klo, j);
+            dense += (__builtin_amdgcn_readlane(first, j) && kj < k) ? 1 : 0;
+        }
+        if (lane < NP) { key[pos] = k; idx[pos] = (uint32_t)lane; sc[pos] = dense; }
+    }
+    __syncthreads();
+}
+
 __device__ inline void block_class_rank(const ca_template& tp, const int64_t* __restrict__ cls_sc, int32_t U,
                                         int32_t NP, uint64_t* key, uint32_t* idx, int32_t* sc) {
     const int64_t acpu = tp.node.alloc_milli_cpu, amem = tp.node.alloc_memory;
     if (NP <= 64) {
-        // one wavefront: lane i holds class i's key; its place in the (key, class) order and
-        // its dense rank are counts over the other lanes (readlane broadcasts, no barrier
-        // per bitonic stage)
-        if (threadIdx.x < 64) {
-            const int lane = (int)threadIdx.x;
-            uint64_t k = ~0ull;
-            if (lane < U) {
-                double score = 0.0;
-                if (acpu > 0) score += (double)cls_sc[2 * lane] / (double)acpu;
-                if (amem > 0) score += (double)cls_sc[2 * lane + 1] / (double)amem;
-                k = ~ordered_bits(score);
-            }
-            const uint32_t klo = (uint32_t)k, khi = (uint32_t)(k >> 32);
-            int pos = 0, eq_before = 0;
-            for (int j = 0; j < NP; j++) {
-                const uint64_t kj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(khi, j) << 32) |
-                                    (uint32_t)__builtin_amdgcn_readlane(klo, j);
-                pos += (kj < k || (kj == k && j < lane)) ? 1 : 0;
-                eq_before += (kj == k && j < lane) ? 1 : 0;
-            }
-            const int first = eq_before == 0 ? 1 : 0;       // the lowest class holding its key
-            int dense = 0;
-            for (int j = 0; j < NP; j++) {
-                const uint64_t kj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(khi, j) << 32) |
-                                    (uint32_t)__builtin_amdgcn_readlane(klo, j);
-                dense += (__builtin_amdgcn_readlane(first, j) && kj < k) ? 1 : 0;
-            }
-            if (lane < NP) { key[pos] = k; idx[pos] = (uint32_t)lane; sc[pos] = dense; }
-        }
-        __syncthreads();
+        const int l = (int)threadIdx.x;
+        const int64_t c0 = l < U ? cls_sc[2 * l] : 0, c1 = l < U ? cls_sc[2 * l + 1] : 0;
+        wave_class_rank(tp, c0, c1, U, NP, key, idx, sc);
         return;
     }
     for (int i = threadIdx.x; i < NP; i += blockDim.x) {
@@ -545,16 +554,26 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
 #ifdef CASIM_PROF
     const uint64_t t_r0 = clock64();
 #endif
-    // the first RUB list positions per thread are loaded before the class ranking, so their
-    // latency hides behind it; RUB positions per thread are in flight together after that
+    // Each wave counts a contiguous region of the list, 64 positions per step (classes come
+    // in runs: a wave adds a run to a register and touches the LDS counter once per run —
+    // with every wave on a strided slice the same few counters took ~1 000 contended LDS
+    // atomics per group).  The class scores (ranking, up to 64 classes) are requested
+    // first and the region's first RUB steps right after, so the ranking waits only for
+    // the scores and the steps' latency hides behind it.
     constexpr int RUB = 16;
+    const int32_t per_w = ((gm.count + 15) / 16 + 63) & ~63;
+    const int32_t wb0 = min(gm.count, w * per_w), wb1 = min(gm.count, wb0 + per_w);
+    const bool small = NP <= 64;
+    int64_t s_cpu = 0, s_mem = 0;
+    if (small && tid < U) { s_cpu = cls_sc[2 * tid]; s_mem = cls_sc[2 * tid + 1]; }
     int32_t cv[RUB];
 #pragma unroll
     for (int u = 0; u < RUB; u++) {
-        const int32_t i = u * 1024 + tid;
-        cv[u] = i < gm.count ? item_cls[gm.off + i] : -1;
+        const int32_t i = wb0 + u * 64 + lane;
+        cv[u] = i < wb1 ? item_cls[gm.off + i] : -1;
     }
-    block_class_rank(tmpls[gm.tmpl], cls_sc, U, NP, key, idx, rc);      // (rc: scratch for the ranks)
+    if (small) wave_class_rank(tmpls[gm.tmpl], s_cpu, s_mem, U, NP, key, idx, rc);   // (rc: scratch)
+    else block_class_rank(tmpls[gm.tmpl], cls_sc, U, NP, key, idx, rc);
     for (int i = tid; i < U; i += 1024) cr[idx[i]] = rc[i];
     __syncthreads();
     for (int i = tid; i < U; i += 1024) { cnt[i] = 0; rc[i] = 0; }
@@ -562,23 +581,36 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
 #ifdef CASIM_PROF
     const uint64_t t_r1 = clock64();
 #endif
-    // class counts: the lanes of a wave holding one class add once (controllers come in runs);
-    // the next slice's classes are requested before this slice is counted
-    for (int32_t base = 0; base < gm.count; base += 1024 * RUB) {
+    // class counts over the wave's region (the next RUB steps requested before these are counted)
+    int32_t cur = -1, acc = 0;                // (wave-uniform) the run being added up
+    for (int32_t base = wb0; base < wb1; base += 64 * RUB) {
         int32_t nx[RUB];
-        const bool more = base + 1024 * RUB < gm.count;
+        const bool more = base + 64 * RUB < wb1;
         if (more) {
 #pragma unroll
             for (int u = 0; u < RUB; u++) {
-                const int32_t i = base + 1024 * RUB + u * 1024 + tid;
-                nx[u] = i < gm.count ? item_cls[gm.off + i] : -1;
+                const int32_t i = base + 64 * RUB + u * 64 + lane;
+                nx[u] = i < wb1 ? item_cls[gm.off + i] : -1;
             }
         }
 #pragma unroll
         for (int u = 0; u < RUB; u++) {
             const bool valid = cv[u] >= 0;
             const int32_t c = cv[u];
-            uint64_t act = __ballot(valid);
+            const uint64_t vm = __ballot(valid);
+            if (!vm) continue;
+            const int32_t c0 = __builtin_amdgcn_readlane(c, __builtin_ctzll(vm));
+            if (__ballot(valid && c != c0) == 0) {          // one class in this step
+                if (c0 == cur) {
+                    acc += __builtin_popcountll(vm);
+                } else {
+                    if (acc > 0 && lane == 0) atomicAdd(&cnt[cur], acc);
+                    cur = c0;
+                    acc = __builtin_popcountll(vm);
+                }
+                continue;
+            }
+            uint64_t act = vm;                                // a class boundary in the step
             while (act) {
                 const int l = __builtin_ctzll(act);
                 const int32_t cl = __builtin_amdgcn_readlane(c, l);
@@ -592,6 +624,7 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
             for (int u = 0; u < RUB; u++) cv[u] = nx[u];
         }
     }
+    if (acc > 0 && lane == 0) atomicAdd(&cnt[cur], acc);
     __syncthreads();
     for (int c = tid; c < U; c += 1024)
         if (cnt[c] > 0) atomicAdd(&rc[cr[c]], cnt[c]);

@@ -558,9 +558,12 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
     // in runs: a wave adds a run to a register and touches the LDS counter once per run —
     // with every wave on a strided slice the same few counters took ~1 000 contended LDS
     // atomics per group).  The class scores (ranking, up to 64 classes) are requested
-    // first and the region's first RUB steps right after, so the ranking waits only for
-    // the scores and the steps' latency hides behind it.
-    constexpr int RUB = 16;
+    // first and the region's first RUB steps right after — all of a C2 group's list (up to
+    // 64 x 64 x 16 positions) — so the ranking waits only for the scores.  (Measured,
+    // CASIM_PROF: counting stays ~40k of the kernel's ~65k cycles whether the loads go in
+    // slices or all at once, and with strided or contiguous slices — not memory latency,
+    // not the LDS atomics)
+    constexpr int RUB = 64;
     const int32_t per_w = ((gm.count + 15) / 16 + 63) & ~63;
     const int32_t wb0 = min(gm.count, w * per_w), wb1 = min(gm.count, wb0 + per_w);
     const bool small = NP <= 64;
@@ -581,16 +584,14 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
 #ifdef CASIM_PROF
     const uint64_t t_r1 = clock64();
 #endif
-    // class counts over the wave's region (the next RUB steps requested before these are counted)
+    // class counts over the wave's region
     int32_t cur = -1, acc = 0;                // (wave-uniform) the run being added up
     for (int32_t base = wb0; base < wb1; base += 64 * RUB) {
-        int32_t nx[RUB];
-        const bool more = base + 64 * RUB < wb1;
-        if (more) {
+        if (base > wb0) {                     // (groups past 65 536 positions)
 #pragma unroll
             for (int u = 0; u < RUB; u++) {
-                const int32_t i = base + 64 * RUB + u * 64 + lane;
-                nx[u] = i < wb1 ? item_cls[gm.off + i] : -1;
+                const int32_t i = base + u * 64 + lane;
+                cv[u] = i < wb1 ? item_cls[gm.off + i] : -1;
             }
         }
 #pragma unroll
@@ -618,10 +619,6 @@ __global__ void __launch_bounds__(1024) k_run_table(const GroupMeta* __restrict_
                 if (lane == l) atomicAdd(&cnt[cl], __builtin_popcountll(m));
                 act &= ~m;
             }
-        }
-        if (more) {
-#pragma unroll
-            for (int u = 0; u < RUB; u++) cv[u] = nx[u];
         }
     }
     if (acc > 0 && lane == 0) atomicAdd(&cnt[cur], acc);

@@ -2455,8 +2455,9 @@ struct ca_estimate_plan {
 namespace casim {
 // Streams and events of an Estimate plan, kept per device after the plan is destroyed and
 // handed to the next plan (RunOnce builds a plan per loop: creating three streams and
-// sixteen events costs more than a loop's whole Estimate).  Every run synchronises before
-// it returns, so a released set is idle.
+// sixteen events costs more than a loop's whole Estimate).  The plan's destructor drains its
+// three streams first (a run that failed part-way may have left kernels queued), so a
+// released set is idle.
 struct PlanStreams {
     hipStream_t pub = nullptr, st2 = nullptr, st3 = nullptr;
     hipEvent_t ev[ca_estimate_plan::EV_N] = {};
@@ -2502,6 +2503,16 @@ ca_estimate_plan::~ca_estimate_plan() {
     ps.go = ev_go; ps.pub_ev = ev_pub; ps.emitA = ev_emitA; ps.emitB = ev_emitB; ps.ids = ev_ids; ps.init = ev_init;
     ps.b = ev_b; ps.rb = ev_rb;
     ps.pub = pub_stream; ps.st2 = st2; ps.st3 = st3;
+    // a run that returned early on an error may have left kernels queued on these streams
+    // (a publisher polls for up to its deadline): drain them before the set is pooled or
+    // destroyed, and before the plan's buffers go back to the allocation cache
+    if (res_device >= 0) {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (cur != res_device) (void)hipSetDevice(res_device);
+        for (hipStream_t q : {ps.pub, ps.st2, ps.st3}) if (q) (void)hipStreamSynchronize(q);
+        if (cur >= 0 && cur != res_device) (void)hipSetDevice(cur);
+    }
     if (res_device >= 0 && pub_stream && st2 && st3) {
         std::lock_guard<std::mutex> lk(casim::g_ps_mu);
         casim::g_ps_pool.emplace_back(res_device, ps);
@@ -2864,6 +2875,9 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     const char* rb_env = knob_env("CASIM_RUN_BATCH");
     const int32_t batch_runs = (rb_env && rb_env[0] == '0') ? 0 : 1;
     const bool serial_pub = knob_env("CASIM_PUB_SERIAL") != nullptr;
+    // (test hook: the publisher serialised in round 1 only — it gives up there, a later
+    // lastIndex round publishes cleanly, and the fallback must still cover round 1's groups)
+    const bool serial_pub_r1 = test_hook_env("CASIM_PUB_SERIAL_R1") != nullptr;
     int32_t tickets1 = 0;                               // publisher tickets of round 1 (every group)
     if (publish)
         for (int32_t g = 0; g < G; g++) tickets1 += (p->h_meta[g].count + p->pch - 1) / p->pch;
@@ -2917,7 +2931,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     // unsupported flags, and the publisher's tickets and control words are clean from the
     // last run (ca_estimate_plan::pub_clean) — no launch and no cross-stream event ahead of
     // the chains
-    const bool fast_init = decoupled && runs_stream && (!publish || p->pub_clean) && !serial_pub &&
+    const bool fast_init = decoupled && runs_stream && (!publish || p->pub_clean) && !serial_pub && !serial_pub_r1 &&
                            !knob_env("CASIM_NO_FAST_INIT");
     const int32_t lin0 = *last_index;
     if (publish) p->pub_clean = false;        // set again once this run's publishers all finished clean
@@ -3123,6 +3137,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     for (;;) {
         rounds++;
         if (rounds > 1) p->h_qc.as<int32_t>()[2] = 0;
+        const bool serial_now = serial_pub || (serial_pub_r1 && rounds == 1);
         if (rounds > 1) {      // round 1's state came from k_round_init
             CA_HIP_CHECK(hipMemcpyAsync(p->d_lin.ptr, lin.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, st));
             CA_HIP_CHECK(hipMemcpyAsync(p->d_need.ptr, need.data(), G, hipMemcpyHostToDevice, st));
@@ -3164,7 +3179,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             CA_HIP_CHECK(hipGetLastError());
             return CA_OK;
         };
-        if (publish && round_tickets > 0 && serial_pub) {
+        if (publish && round_tickets > 0 && serial_now) {
             int rc0;
             if ((rc0 = launch_pub(st)) != CA_OK) return rc0;
             CA_HIP_CHECK(hipEventRecord(p->ev_pub, st));
@@ -3205,7 +3220,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             return rc;
         }
         if ((rc = record_ids()) != CA_OK) return rc;
-        if (publish && round_tickets > 0 && !serial_pub) {
+        if (publish && round_tickets > 0 && !serial_now) {
             if (pub_go) CA_HIP_CHECK(hipStreamWaitEvent(p->pub_stream, pub_go, 0));
             if ((rc = launch_pub(p->pub_stream)) != CA_OK) return rc;
             CA_HIP_CHECK(hipEventRecord(p->ev_pub, p->pub_stream));
@@ -3216,7 +3231,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         // (the chains write their ChainOut records, and the chains / publisher their failure
         // flags, straight into page-locked h_out / h_qc: no copy kernels at the step's end)
         const ChainOut* fresh = p->h_out.as<ChainOut>();
-        const bool pub_ran = publish && round_tickets > 0 && !serial_pub;
+        const bool pub_ran = publish && round_tickets > 0 && !serial_now;
         if (publish && !(host_joins && pub_ran)) CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_pub, 0));
         CA_HIP_CHECK(hipEventRecord(p->ev_rb, st));
         // results of this round, queued behind the readback: the device fills them while
@@ -3304,7 +3319,9 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         // died) falls back to the device copy + D2H
         const int32_t* qc = p->h_qc.as<int32_t>();      // read back with the last round's outputs
         p->pub_state = 1;
-        if (qc[2] != 0 || qc[3] != 0) {
+        // (a give-up in ANY round: qc[2] is reset per round and a later round publishes only
+        // the groups it re-ran, so round 1's accepted groups would otherwise stay unwritten)
+        if (pub_gave_up || qc[2] != 0 || qc[3] != 0) {
             p->pub_state = 2;
             set_last_error("estimate publisher missed a ticket; results copied instead");
             if (decoupled) CA_HIP_CHECK(hipStreamWaitEvent(st, p->ev_ids, 0));

@@ -1469,7 +1469,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     FoCtl ctl0;
     std::memset(&ctl0, 0, sizeof ctl0);
     ctl0.L = *last_index;
-    ctl0.fb_cyc[3] = getenv("CASIM_FB_PROF_BULK") ? 1 : 0;     // (CASIM_PROF builds: which split)
+    ctl0.fb_cyc[3] = knob_env("CASIM_FB_PROF_BULK") ? 1 : 0;     // (CASIM_PROF builds: which split)
     char* di = fo.in.as<char>();
     char* dz = fo.zero.as<char>();
     char* dout = fo.out.as<char>();
@@ -1511,7 +1511,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     std::vector<FbShape> fb_shapes;
     std::vector<int32_t> fb_rep;
     int32_t fb_stat_in_lds = 0;
-    bool fb = nn > 0 && !getenv("CASIM_FO_WINDOW");
+    bool fb = nn > 0 && !knob_env("CASIM_FO_WINDOW");
     const int32_t NW = (nn + 63) / 64;
     if (fb) {
         uint64_t taint_union = 0;
@@ -1765,7 +1765,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     // the new mirror records are the podset's records: gathered on the device instead of
     // crossing PCIe at the next sync (only when no selector tables had to be re-based)
     if (s && dev_in_sync && placed > 0 && m->pods.size() == pods0 + (size_t)placed && m->terms.size() == terms0 &&
-        m->reqs.size() == reqs0 && m->pf_names.size() == names0 && !getenv("CASIM_NO_POD_GATHER")) {
+        m->reqs.size() == reqs0 && m->pf_names.size() == names0 && !knob_env("CASIM_NO_POD_GATHER")) {
         std::vector<int32_t> src;
         src.reserve((size_t)placed);
         for (int32_t k = 0; k < n; k++)

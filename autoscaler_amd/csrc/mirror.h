@@ -126,22 +126,50 @@ struct Stats {
 }  // namespace casim
 
 namespace casim {
-// Large blocks from 2 MiB-aligned anonymous mappings with transparent huge pages asked for:
-// the pod records only grow (ids are never reused), so every call that stores pods touches
-// fresh memory, and 4 KiB first-touch faults cost more than the records' copies.
-template <class T> struct HugeAlloc {
-    using value_type = T;
+// The mirror's pod records: ids are never reused (Revert detaches pods, Clear() starts over),
+// so the table only grows — every planner run appends its committed copies, every
+// FilterOutSchedulable call its placements.  Rows live in fixed chunks of 2^16 records that
+// are never moved: growing a contiguous vector past its capacity copied every record
+// (~40 MB at C3 size: a 30 ms stall inside whichever call crossed the boundary).  Chunks
+// come from 2 MiB-aligned anonymous mappings with transparent huge pages asked for (4 KiB
+// first-touch faults cost more than the records' copies).
+template <class T> class ChunkVec {
+  public:
+    static constexpr size_t kBits = 16, kRows = (size_t)1 << kBits, kMask = kRows - 1;
+    ChunkVec() = default;
+    ChunkVec(const ChunkVec&) = delete;
+    ChunkVec& operator=(const ChunkVec&) = delete;
+    ~ChunkVec() {
+        clear();
+        for (T* c : chunks_) unmap(c);
+    }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    size_t capacity() const { return chunks_.size() * kRows; }
+    T& operator[](size_t i) { return chunks_[i >> kBits][i & kMask]; }
+    const T& operator[](size_t i) const { return chunks_[i >> kBits][i & kMask]; }
+    T& back() { return (*this)[n_ - 1]; }
+    void reserve(size_t n) {
+        while (capacity() < n) chunks_.push_back(map());
+    }
+    void push_back(const T& v) {
+        reserve(n_ + 1);
+        new (&(*this)[n_]) T(v);
+        n_++;
+    }
+    void resize(size_t n) {                     // (grow: value-initialised rows; shrink: dropped)
+        reserve(n);
+        for (size_t i = n_; i < n; i++) new (&(*this)[i]) T();
+        for (size_t i = n; i < n_; i++) (*this)[i].~T();
+        n_ = n;
+    }
+    void clear() { resize(0); }                 // (the chunks stay mapped for the next load)
+
+  private:
     static constexpr size_t kHuge = (size_t)2 << 20;
-    HugeAlloc() = default;
-    template <class U> HugeAlloc(const HugeAlloc<U>&) {}
-    static size_t mapped(size_t n) { return (n * sizeof(T) + kHuge - 1) & ~(kHuge - 1); }
-    T* allocate(size_t n) {
-        if (n * sizeof(T) < 2 * kHuge) {
-            void* p = std::malloc(n * sizeof(T));
-            if (!p) throw std::bad_alloc();
-            return static_cast<T*>(p);
-        }
-        const size_t sz = mapped(n);
+    static size_t bytes() { return (kRows * sizeof(T) + kHuge - 1) & ~(kHuge - 1); }
+    static T* map() {
+        const size_t sz = bytes();
         char* base = static_cast<char*>(mmap(nullptr, sz + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0));
         if (base == MAP_FAILED) throw std::bad_alloc();
         char* al = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(base) + kHuge - 1) & ~(uintptr_t)(kHuge - 1));
@@ -150,12 +178,9 @@ template <class T> struct HugeAlloc {
         (void)madvise(al, sz, MADV_HUGEPAGE);
         return reinterpret_cast<T*>(al);
     }
-    void deallocate(T* p, size_t n) {
-        if (n * sizeof(T) < 2 * kHuge) std::free(p);
-        else munmap(p, mapped(n));
-    }
-    template <class U> bool operator==(const HugeAlloc<U>&) const { return true; }
-    template <class U> bool operator!=(const HugeAlloc<U>&) const { return false; }
+    static void unmap(T* c) { munmap(c, bytes()); }
+    std::vector<T*> chunks_;
+    size_t n_ = 0;
 };
 }  // namespace casim
 
@@ -165,7 +190,7 @@ struct ca_mirror {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
 
     std::vector<casim::NodeRow> nodes;
-    std::vector<casim::PodRow, casim::HugeAlloc<casim::PodRow>> pods;
+    casim::ChunkVec<casim::PodRow> pods;             // by pod id (never moved)
     std::vector<ca_selector_term> terms;
     std::vector<ca_selector_req> reqs;
     std::vector<int32_t> pf_names;

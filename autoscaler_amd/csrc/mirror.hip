@@ -369,7 +369,7 @@ void ca_mirror::add_pod_to_node(int32_t pod, int32_t node) {
 }
 
 void ca_mirror::reserve_more(size_t n_pods_add, size_t n_journal_add) {
-    if (pods.capacity() < pods.size() + n_pods_add) pods.reserve(std::max(pods.capacity() * 2, pods.size() + n_pods_add));
+    pods.reserve(pods.size() + n_pods_add);                 // (chunked: nothing moves)
     if (journal.capacity() < journal.size() + n_journal_add)
         journal.reserve(std::max(journal.capacity() * 2, journal.size() + n_journal_add));
 }
@@ -998,7 +998,7 @@ int ca_mirror_remove_node(ca_mirror* m, int32_t node_pos) {
         m->pods[id].node = -1;
         if (m->pods[id].spec.flags & CA_POD_REQUIRED_ANTI_AFFINITY) m->n_scope_blockers--;
     }
-    for (PodRow& pr : m->pods) if (pr.node > node_pos) pr.node--;
+    for (size_t i = 0; i < m->pods.size(); i++) if (m->pods[i].node > node_pos) m->pods[i].node--;
     // positions moved: every row is re-uploaded before the next kernel
     m->dirty_rows.clear();
     m->dirty_flag.assign(m->nodes.size(), 0);
@@ -1060,7 +1060,7 @@ int ca_mirror_revert(ca_mirror* m) {
             m->pods[e.pod].node = e.node;
         } else if (e.kind == J_REMOVE_NODE) {
             const int32_t pos = e.node;
-            for (PodRow& pr : m->pods) if (pr.node >= pos) pr.node++;
+            for (size_t i = 0; i < m->pods.size(); i++) if (m->pods[i].node >= pos) m->pods[i].node++;
             m->nodes.insert(m->nodes.begin() + pos, std::move(m->removed_nodes.back()));
             m->removed_nodes.pop_back();
             for (int32_t id : m->nodes[pos].pods) {

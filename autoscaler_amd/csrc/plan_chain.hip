@@ -1100,7 +1100,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
                    int32_t max_removable, const ca_pdb_table* pdbs, int32_t* hints, int32_t n_pods,
                    int32_t* last_index, ca_plan_result* results, std::vector<ca_plan_move>& moves_out,
                    std::vector<int32_t>& hints_out, int32_t* simulated_out) {
-    if (getenv("CASIM_PLAN_SPECULATIVE")) return 0;
+    if (knob_env("CASIM_PLAN_SPECULATIVE")) return 0;
     const int32_t N = (int32_t)m->nodes.size();
     if (N <= 0 || C <= 0) return 0;
     const int32_t M = move_off[C];
@@ -1233,7 +1233,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     A.trace = nullptr;
     A.trace_cap = 0;
     A.help_after = PC_HELP_AFTER;
-    if (const char* e = getenv("CASIM_PLAN_HELP_AFTER")) A.help_after = std::max(1, atoi(e));
+    if (const char* e = knob_env("CASIM_PLAN_HELP_AFTER")) A.help_after = std::max(1, atoi(e));
     A.dbg = test_hook_env("CASIM_PLAN_DBG") ? atoi(test_hook_env("CASIM_PLAN_DBG")) : 0;
     const char* tr_env = test_hook_env("CASIM_PLAN_TRACE");
     DevBuf trace;
@@ -1249,7 +1249,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     CA_HIP_CHECK(hipEventRecord(m->ev0, st));
     // the chain wave plus helper waves for long scans (CASIM_PLAN_HELPERS: 0..7, default 7)
     int waves = PC_MAX_WAVES;
-    if (const char* e = getenv("CASIM_PLAN_HELPERS")) waves = 1 + std::max(0, std::min(PC_MAX_WAVES - 1, atoi(e)));
+    if (const char* e = knob_env("CASIM_PLAN_HELPERS")) waves = 1 + std::max(0, std::min(PC_MAX_WAVES - 1, atoi(e)));
     if (eph_cols) hipLaunchKernelGGL(k_plan_chain<true>, dim3(1), dim3(64 * waves), Y.total, st, A);
     else hipLaunchKernelGGL(k_plan_chain<false>, dim3(1), dim3(64 * waves), Y.total, st, A);
     CA_HIP_CHECK(hipGetLastError());

@@ -1239,7 +1239,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     }
     const int32_t S = (int32_t)sens.size();
     const int32_t nch = (S + WK - 1) / WK;
-    const bool dev_walk = S > 0 && n > 0 && nch <= WALK_MAX_CHUNKS && !getenv("CASIM_SWEEP_HOST_WALK");
+    const bool dev_walk = S > 0 && n > 0 && nch <= WALK_MAX_CHUNKS && !knob_env("CASIM_SWEEP_HOST_WALK");
 
     SweepScratch& sw = m->sw;
     // device scratch: [SweepOut C][walk lout C][info 2][dest M][hint set M] (one D2H; the
@@ -1432,8 +1432,8 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     // sensitive — not to an unrelated call on the same mirror.
     const bool same_shape = C <= 2 * sw.serial_C && 2 * C >= sw.serial_C && S <= 2 * sw.serial_S &&
                             2 * S >= sw.serial_S && 2 * S >= C;
-    const bool serial_only = S > 0 && n > 0 && !getenv("CASIM_NO_SERIAL_CHAIN") &&
-                             ((C <= 2048 && sw.serial_next && same_shape) || getenv("CASIM_SWEEP_SERIAL") != nullptr);
+    const bool serial_only = S > 0 && n > 0 && !knob_env("CASIM_NO_SERIAL_CHAIN") &&
+                             ((C <= 2048 && sw.serial_next && same_shape) || knob_env("CASIM_SWEEP_SERIAL") != nullptr);
     auto enqueue_serial = [&]() -> int {
         int e;
         if ((e = sw.chainl.reserve(sizeof(int32_t) * (size_t)C)) != CA_OK) return e;
@@ -1580,7 +1580,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 if ((rc = sw.h_ctab.reserve(sizeof(int32_t) * (64 + FPW) * (size_t)T)) != CA_OK) return rc;
                 int32_t* const ct = sw.h_ctab.as<int32_t>();
                 void *d_ht = nullptr, *d_ct = nullptr;
-                const bool zc = !getenv("CASIM_SWEEP_COPY_ROUNDS") &&
+                const bool zc = !knob_env("CASIM_SWEEP_COPY_ROUNDS") &&
                                 hipHostGetDevicePointer(&d_ht, ht, 0) == hipSuccess &&
                                 hipHostGetDevicePointer(&d_ct, ct, 0) == hipSuccess;
                 if (!zc) {
@@ -1663,8 +1663,8 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 const double round_ms =
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_round).count();
                 const int32_t adv = k0 - k_round;
-                if ((round_ms > 2.0 * chain_ms_per * std::max(adv, 1) || getenv("CASIM_SWEEP_FORCE_CHAIN")) &&
-                    !getenv("CASIM_NO_SERIAL_CHAIN")) {
+                if ((round_ms > 2.0 * chain_ms_per * std::max(adv, 1) || knob_env("CASIM_SWEEP_FORCE_CHAIN")) &&
+                    !knob_env("CASIM_NO_SERIAL_CHAIN")) {
                     if ((rc = run_chain(std::min(S, k0 + chain_batch))) != CA_OK) return rc;
                     chain_batch = std::min(2 * chain_batch, 4096);
                     if (k0 >= S) break;

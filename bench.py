@@ -368,19 +368,26 @@ def planner_leg(args, device: int, with_cpu: bool) -> dict:
     for limit in (20, 200, 0):
         m = native.Mirror(device)                   # fresh: the copies' ids then match the port's
         W.load_sweep(m, w)
-        ts, st = [], None
+        ts, st, split = [], None, []
         for _ in range(5):                          # the first run also uploads the snapshot
             m.fork()
             t = time.perf_counter()
             r = m.plan_removals(*args_, hints, 0, limit)
             ts.append(time.perf_counter() - t)
             st = m.plan_stats()
+            if st["path"] == "chain":
+                split.append(m.plan_chain_profile())
             m.revert()
             firsts.setdefault(limit, r)
         out["runs"][str(limit)] = {"gpu_ms": float(np.median(ts[1:]) * 1e3), "path": st["path"], "rounds": st["rounds"],
                                    "conflicts": st["conflicts"], "simulated": st["simulated"],
                                    "removable": int(r.results["removable"].sum()),
-                                   "candidates_run": int((r.results["reason"] != 101).sum())}
+                                   "candidates_run": int((r.results["reason"] != 101).sum()),
+                                   "all_ms": [round(x * 1e3, 3) for x in ts]}
+        if split:                                   # library-side split of the call (median over the warm runs)
+            out["runs"][str(limit)]["split_ms"] = {
+                k: float(np.median([s[k] for s in split[1:] or split]))
+                for k in ("sync_ms", "launch_kernel_ms", "kernel_ms", "readback_ms", "replay_ms")}
         m.close()
     if with_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

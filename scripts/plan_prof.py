@@ -11,6 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("CASIM_LIB_PATH", os.path.join(ROOT, "autoscaler_amd", "lib", "libcasim_prof.so")) if "--prof" in sys.argv else None
 sys.argv = [a for a in sys.argv if a != "--prof"]
+os.environ["CASIM_KNOBS"] = "1"          # CASIM_PLAN_HELPERS is a knob (read only with CASIM_KNOBS)
 from autoscaler_amd import native, workloads as W  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 5000

@@ -614,6 +614,37 @@ def test_estimate_publisher_state_across_runs(oracle, monkeypatch):
             monkeypatch.delenv("CASIM_PUB_SERIAL")
 
 
+def test_estimate_publisher_gives_up_in_round1_only(oracle, monkeypatch):
+    """A publisher that gives up in round 1 while a later lastIndex round publishes cleanly
+    (CASIM_PUB_SERIAL_R1: serialised in round 1 only): the groups round 1 accepted were
+    never written into the caller's buffer by any publisher, so the run must take the
+    stream-ordered copy (a give-up in any round decides, not the last round's flag)."""
+    w = W.c2(n_pods=9000, n_groups=16, n_existing=200, max_nodes=1000, seed=11)
+    o = oracle.OracleState()
+    W.load_estimate(o, w)
+    m = _mirror()
+    W.load_estimate(m, w)
+    rounds = []
+    with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as plan:
+        for L0 in (77, 0, 77):
+            ro = o.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, L0)
+            monkeypatch.setenv("CASIM_PUB_SERIAL_R1", "1")
+            for u16 in (True, False):
+                r = plan.run_u16(w.max_nodes, L0) if u16 else plan.run(w.max_nodes, L0, want_nodes=False)
+                st = plan.stats()
+                assert np.array_equal(ro.results, r.results) and ro.last_index == r.last_index
+                sp = np.where(r.sched_pod == 0xFFFF, -1, r.sched_pod.astype(np.int32)) if u16 else r.sched_pod
+                assert np.array_equal(ro.sched_pod, sp), (L0, u16, st)
+                assert st["results_path"] == "publisher_gave_up", st
+                rounds.append(st["rounds"])
+            monkeypatch.delenv("CASIM_PUB_SERIAL_R1")
+            r = plan.run_u16(w.max_nodes, L0)                 # and a clean run after it
+            assert plan.stats()["results_path"] == "published"
+            assert np.array_equal(ro.sched_pod, np.where(r.sched_pod == 0xFFFF, -1, r.sched_pod.astype(np.int32)))
+    assert max(rounds) > 1, rounds                            # a later round did run (and published)
+    m.close()
+
+
 @pytest.mark.parametrize("size", ["small", "full"])
 def test_estimate_c4_taints_affinity(size, oracle):
     """C4 (taint/toleration + node-affinity heavy): static filters on the templates, per

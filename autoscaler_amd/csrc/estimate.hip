@@ -5,18 +5,31 @@
 //            CA/utils/scheduler/scheduler.go:73-91 (template copies),
 //            CA/simulator/predicatechecker/schedulerbased.go:90-136 (rotating scan).
 //
-// Pipeline per call:
-//   1. k_score_tiles   score (float64, calculatePodScore) + static predicates of every
-//                      (group, pod) against the group's template; bitonic sort of
-//                      1024-item tiles in LDS by (score desc, list position asc).
-//   2. k_merge_runs    log2(P/1024) merge passes (rank by binary search; keys unique).
-//   3. k_emit_stream   gather the sorted pods into a 32-B/pod stream per group.
-//   4. k_ffd_chain     one wavefront per group runs the sequential First-Fit-Decreasing
-//                      loop with the new-node rows in LDS; the rotating first-fit is a
-//                      64-lane ballot over block summaries, then over the block's nodes.
-//   5. host fix-up     the groups share lastIndex: groups whose result
-//                      depends on their lastIndex input are re-run until every group's
-//                      input equals its predecessor's output (exact).
+// Pipeline of one headline step (C2: uniform score classes, no cross-class float64 ties —
+// the decoupled Go order):
+//   st3 (high priority)  k_pdq_sort      Go 1.19 sort.Slice's exact permutation of every
+//                                        group (class ranks folded in), one 1024-thread
+//                                        workgroup per group; writes the Go-order pod ids
+//                                        and an epoch-stamped ready flag per group.
+//   st  (heavy groups)   k_run_table     class ranks + per-class counts of each group's
+//                                        list, each rank's first stream position, the
+//                                        class's stream record against the template.
+//                        k_emit_runs     run heads and the stream windows that hold them.
+//                        k_ffd_chain     one 4-wave workgroup per group: the sequential
+//                                        First-Fit-Decreasing loop (per pod, or per run of
+//                                        identical pods in closed form) with the new-node
+//                                        rows in LDS; pushes 4096-output tickets.
+//   st2 (light groups)   the same three kernels for the groups outside the heavy set.
+//   pub_stream           k_publish       claims tickets in completion order and writes the
+//                                        scheduled pods (Go-order ids) into the caller's
+//                                        page-locked buffer while the chains run.
+//   host                 lastIndex fix-up: groups whose result depends on their lastIndex
+//                        input are re-run until every input equals its predecessor's
+//                        output (exact); the host joins the streams.
+// Other paths: non-uniform podsets (C4) sort in Go order first (k_class_rank, k_pdq_sort,
+// radix passes, k_emit_bucket) and then chain; > 4096 score classes use k_score_tiles +
+// k_merge_runs + k_emit_stream; device-resident results expand the chains' segments with
+// k_copy_segments; a publisher that gives up falls back to the same copy + D2H.
 #include "mirror.h"
 #include "device_filters.h"
 #include "pdqsort.h"

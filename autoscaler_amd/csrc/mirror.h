@@ -58,7 +58,8 @@ struct SweepScratch {
     DevBuf tfp, vp, mode;           // table rows' fit-point classes; visible-node prefix counts; class mode
     DevBuf bsum;                    // per 64-node block: maxima of the visible rows (sweep.hip BlockSum)
     DevBuf chainl;                  // the host walk's serial exact chain: candidates in order
-    HostBuf h_in, h_tab, h_out, h_todo, h_lin, h_wl, h_tfp, h_ctab, h_l0, h_chainl;
+    DevBuf bmap;                    // a multi-device range's block map (k_walk_map)
+    HostBuf h_in, h_tab, h_out, h_todo, h_lin, h_wl, h_tfp, h_ctab, h_l0, h_chainl, h_bmap;
     // the device pipeline of the last call shape, replayed as a graph (sweep.hip sweep_core)
     hipGraphExec_t gexec = nullptr;
     uint64_t gkey = 0, gseen = 0;
@@ -182,6 +183,38 @@ template <class T> class ChunkVec {
     std::vector<T*> chunks_;
     size_t n_ = 0;
 };
+}  // namespace casim
+
+namespace casim {
+// A candidate range of a multi-device sweep (multi.hip) runs the pipeline in three calls
+// on its own device, the host composing the ranges between them:
+//   SP_PROBE    the probe at the guesses from guess_base (lastIndex + the pods to move of
+//               every earlier sensitive candidate of the whole call); out: adv = the range's
+//               advance as the probe saw it (the sum k_sweep_est would take)
+//   SP_MAP      windows centred from est_base (the previous ranges' probe advances), the
+//               tables, the chunk walks and k_walk_map; out: map[] (64 lastIndex-out values
+//               by class of the first row, the row's fit points, the class mode), S
+//   SP_RESOLVE  the walk from the true input (*last_index), the table gather and the exact
+//               pass — the tail of a normal call, host walk included, so it is always exact
+// Device state (probe outputs, guesses, tables, chunk maps) stays in the mirror's sweep
+// scratch between the calls; nothing else may use the mirror meanwhile.
+enum { SP_FULL = 0, SP_PROBE, SP_MAP, SP_RESOLVE };
+struct SweepPhase {
+    int kind = SP_FULL;
+    int64_t guess_base = 0;
+    int32_t est_base = 0;
+    int64_t adv = 0;              // SP_PROBE out
+    int32_t succ = 0;             // SP_PROBE out: candidates whose probe made a successful scan
+    int32_t S = 0;                // sensitive candidates of the range
+    int32_t map_ok = 0;           // SP_MAP out: the device walk ran (map valid)
+    int32_t map[64 + 65 + 1];     // SP_MAP out: k_walk_map's record (64 outputs, FPW fit points, mode)
+};
+
+int64_t removal_plan_sensitive_pods(const ca_removal_plan* p);
+bool removal_plan_phase_ok(const ca_removal_plan* p);             // no scope cut in the range
+int32_t sweep_fp_class(const int32_t* fp, int32_t n, int32_t L);  // class of L in a row's fit points
+int removal_plan_run_phase(ca_removal_plan* p, int32_t* hints, int32_t* last_index, ca_removal_result* results,
+                           int32_t* out_dest, SweepPhase* ph);
 }  // namespace casim
 
 struct ca_mirror {

@@ -29,10 +29,11 @@ namespace {
 // run fn(d) for every block d, block 0 on the calling thread; first failure wins
 template <class F>
 int for_blocks(int32_t D, F&& fn) {
+    if (D <= 0) return CA_OK;
     std::vector<int> rc((size_t)D, CA_OK);
     std::vector<std::thread> th;
     for (int32_t d = 1; d < D; d++) th.emplace_back([&, d] { rc[d] = fn(d); });
-    rc[0] = D > 0 ? fn(0) : CA_OK;
+    rc[0] = fn(0);
     for (auto& t : th) t.join();
     for (int32_t d = 0; d < D; d++) if (rc[d] != CA_OK) return rc[d];
     return CA_OK;
@@ -267,24 +268,99 @@ int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t 
     for (int32_t d = 0; d < D; d++)
         if ((int32_t)p->mm->m[d]->pods.size() != n_pods) return CA_EINVAL;      // replicas: same pod ids
     const int32_t L0 = *last_index;
+    const int32_t n = D > 0 ? (int32_t)p->mm->m[0]->nodes.size() : 0;
     std::vector<int32_t> lin((size_t)D, L0), lout((size_t)D, L0), succ((size_t)D, 0);
-    auto run = [&](int32_t d, int32_t from) {
+    std::vector<uint8_t> ran((size_t)D, 0);
+    std::vector<int32_t> none;                              // (no caller hints: every pod unhinted)
+    if (!hints) none.assign((size_t)std::max(n_pods, 1), -1);
+    auto run = [&](int32_t d, int32_t from, SweepPhase* ph) {
         const int32_t c0 = p->cb[d];
-        std::vector<int32_t>& h = p->hb[d];                 // the caller's hints, fresh for every run
-        if (hints) h.assign(hints, hints + n_pods);
-        else h.assign((size_t)n_pods, -1);
+        int32_t* hp;
+        if (ph && (ph->kind == SP_PROBE || ph->kind == SP_MAP)) {
+            hp = hints ? hints : none.data();               // (read only: gathered per moved pod)
+        } else {
+            std::vector<int32_t>& h = p->hb[d];             // the caller's hints, fresh for every run
+            if (hints) h.assign(hints, hints + n_pods);
+            else h.assign((size_t)n_pods, -1);
+            hp = h.data();
+        }
         int32_t li = from;
-        int r = ca_removal_plan_run(p->pl[d], h.data(), &li, results + c0, out_dest ? out_dest + p->off[c0] : nullptr);
+        int r = removal_plan_run_phase(p->pl[d], hp, &li, results + c0, out_dest ? out_dest + p->off[c0] : nullptr, ph);
         if (r != CA_OK) return r;
+        if (ph && (ph->kind == SP_PROBE || ph->kind == SP_MAP)) return CA_OK;
         lin[d] = from;
         lout[d] = li;
         succ[d] = p->mm->m[d]->sweep_stats.had_success;
+        ran[d] = 1;
         return CA_OK;
     };
-    int rc = for_blocks(D, [&](int32_t d) { return run(d, L0); });
-    if (rc != CA_OK) return rc;
     p->reruns = 0;
     p->rerun_units = 0;
+    int rc;
+    // ---- the ranges' lastIndex classes, composed on the host ----
+    // 1. every range probes its candidates (guesses from the pods before it) and reports its
+    //    advance; 2. every range centres its windows on the previous ranges' advances, builds
+    //    its tables and its block map (lastIndex out by class of its first row's input);
+    //    3. the maps compose in order from the true input, and every range whose input falls
+    //    in its first window resolves from it, all at once.  A range the composition does
+    //    not reach (a walk that leaves its windows, a scope cut) runs after its predecessor
+    //    from the exact input, as before.
+    bool phased = D > 1 && n > 0 && !knob_env("CASIM_MULTI_NO_MAP");
+    for (int32_t d = 0; d < D && phased; d++) if (p->pl[d] && !removal_plan_phase_ok(p->pl[d])) phased = false;
+    std::vector<int32_t> lin_c((size_t)D, INT32_MIN);   // composed input of each range (INT32_MIN: not reached)
+    if (phased) {
+        std::vector<SweepPhase> ph((size_t)D);
+        int64_t gb = L0;
+        for (int32_t d = 0; d < D; d++) {
+            ph[d].kind = SP_PROBE;
+            ph[d].guess_base = gb;
+            gb += removal_plan_sensitive_pods(p->pl[d]);
+        }
+        if ((rc = for_blocks(D, [&](int32_t d) { return run(d, L0, &ph[d]); })) != CA_OK) return rc;
+        int64_t est = L0;
+        std::vector<int32_t> mapped;                          // ranges whose output can depend on their input
+        for (int32_t d = 0; d < D; d++) {
+            ph[d].kind = SP_MAP;
+            ph[d].est_base = (int32_t)(((est % n) + n) % n);
+            est += ph[d].adv;
+            if (ph[d].S > 0 && ph[d].succ > 0) mapped.push_back(d);
+        }
+        if ((rc = for_blocks((int32_t)mapped.size(), [&](int32_t i) { return run(mapped[i], L0, &ph[mapped[i]]); })) !=
+            CA_OK)
+            return rc;
+        int64_t cur = L0;
+        for (int32_t d = 0; d < D; d++) {
+            if (ph[d].S == 0 || ph[d].succ == 0) {           // no scan can succeed: lastIndex passes through
+                lin_c[d] = (int32_t)cur;
+                continue;
+            }
+            if (!ph[d].map_ok) break;
+            const int32_t* mp = ph[d].map;
+            const int32_t* head = mp + 64;
+            const int32_t Lw = (int32_t)(((cur % n) + n) % n);
+            int32_t x;
+            if (mp[64 + 65]) {
+                x = casim::sweep_fp_class(head, n, Lw);
+            } else {
+                x = Lw - head[1];
+                if (x < 0) x += n;
+                if (x >= 64) x = -1;
+            }
+            if (x < 0 || mp[x] < 0) break;
+            lin_c[d] = (int32_t)cur;
+            cur = mp[x];
+        }
+        for (int32_t d = 0; d < D; d++) ph[d].kind = SP_RESOLVE;
+        std::vector<int32_t> todo;
+        for (int32_t d = 0; d < D; d++) if (lin_c[d] != INT32_MIN) todo.push_back(d);
+        if ((rc = for_blocks((int32_t)todo.size(), [&](int32_t i) {
+                 const int32_t d = todo[i];
+                 return run(d, lin_c[d], &ph[d]);
+             })) != CA_OK)
+            return rc;
+    } else {
+        if ((rc = for_blocks(D, [&](int32_t d) { return run(d, L0, nullptr); })) != CA_OK) return rc;
+    }
     int32_t cur = L0;
     bool cut = false;
     for (int32_t d = 0; d < D; d++) {
@@ -301,15 +377,13 @@ int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t 
             if (out_dest) std::fill(out_dest + p->off[c0], out_dest + p->off[c1], -1);
             continue;
         }
-        if (lin[d] != cur) {
-            if (succ[d]) {                                    // a scan succeeded: its start mattered
-                if ((rc = run(d, cur)) != CA_OK) return rc;
-                p->reruns++;
-                p->rerun_units += c1 - c0;
-            } else {                                          // no scan succeeded: lastIndex passes through
-                for (int32_t c = c0; c < c1; c++) results[c].last_index_in = cur;
-                lin[d] = lout[d] = cur;
-            }
+        if (!ran[d] || (lin[d] != cur && succ[d])) {         // not reached, or ran from a wrong input
+            if ((rc = run(d, cur, nullptr)) != CA_OK) return rc;
+            p->reruns++;
+            p->rerun_units += c1 - c0;
+        } else if (lin[d] != cur) {                          // no scan succeeded: lastIndex passes through
+            for (int32_t c = c0; c < c1; c++) results[c].last_index_in = cur;
+            lin[d] = lout[d] = cur;
         }
         cur = lout[d];
         for (int32_t c = c0; c < c1; c++) if (results[c].reason == CA_UNREMOVABLE_OUT_OF_SCOPE) cut = true;

@@ -82,13 +82,14 @@ struct PcArgs {
     int32_t* allowed;             // RemainingPdbTracker budgets (in place)
     const int32_t* pdb_off;       // memberships by caller pod [n_pods + 1]
     const int32_t* pdb_pod;
-    int32_t* H;                   // hints by pod id [base + copy_cap] (hints.go: a copy keeps its key)
+    int32_t* hout;                // Hints.Set of the caller's pods, by move index (page-locked host memory)
     const int32_t* ex_base;       // per node: first slot of its committed copies in ex_pods
     PcPod* ex_pods;               // copies committed onto a node, as their later candidacy reads them
-    ca_plan_result* res;
+    ca_plan_result* res;          // (results, moves and info: page-locked host memory, written in place)
     ca_plan_move* moves;
     int64_t* info;                // [0] lastIndex, [1] moves, [2] removed, [3] candidates simulated,
-                                  // [4..16) phase cycle counters (PC_* above)
+                                  // [4..4+PC_NPROF) phase cycle counters (PC_* above), [4+PC_NPROF] the
+                                  // first candidate not run (C: none; the host fills their results)
     int64_t L0;
     int32_t copy_cap;
     int32_t dbg;                  // CASIM_PLAN_DBG bits: 1 no block cache, 2 no maxima refresh
@@ -97,10 +98,10 @@ struct PcArgs {
     int32_t help_after;           // blocks a scan loads before handing the rest to the helper waves
 };
 
-// packs the pods to move (one thread per list entry; hints as the caller passed them: a
-// pod's hint changes only while its own candidate is simulated)
+// packs the pods to move (one thread per list entry; hints as the caller passed them, by move
+// index: a pod's hint changes only while its own candidate is simulated)
 __global__ void __launch_bounds__(256) k_plan_pack(const int32_t* __restrict__ move_pods, int32_t M,
-                                                  const PodHot* __restrict__ ph, const int32_t* __restrict__ H0,
+                                                  const PodHot* __restrict__ ph, const int32_t* __restrict__ hint_move,
                                                   PcPod* __restrict__ out) {
     const int32_t i = (int32_t)(blockIdx.x * 256 + threadIdx.x);
     if (i >= M + 64) return;
@@ -110,7 +111,7 @@ __global__ void __launch_bounds__(256) k_plan_pack(const int32_t* __restrict__ m
         const int32_t id = move_pods[i];
         const PodHot p = ph[id];
         r.cpu = p.cpu; r.mem = p.mem; r.eph = p.eph;
-        r.id = id; r.hint = H0[id]; r.spec = p.spec; r.orig = id;
+        r.id = id; r.hint = hint_move[i]; r.spec = p.spec; r.orig = id;
         // moved-pod semantics (cluster.go:235-240 clears Spec.NodeName, tpu.go:57-79 the TPU requests)
         uint32_t f = p.flags & ~(PF_NODE_NAME | PF_ALL_ZERO | PF_SCALAR_REQ | PF_HAS_SCALAR_KEYS);
         if (p.flags & PF_MOVED_ALL_ZERO) f |= PF_ALL_ZERO;
@@ -133,17 +134,42 @@ __device__ inline unsigned long long* pc_e_ptr(PcRowE& r) { return reinterpret_c
 template <bool E> struct PcRowT { using type = PcRow; };
 template <> struct PcRowT<true> { using type = PcRowE; };
 // Per 64-node block: bit planes (podDestinations, visible = destination and schedulable,
-// unschedulable, tainted, free ephemeral >= 0) and the maxima of its visible rows (upper
-// bounds, refreshed by scans).
+// unschedulable, tainted, free ephemeral >= 0).
 struct PcBlk {
     uint64_t dest, vis, usch, taint, eph;
-    int64_t bmc, bmm, bme;
-    int32_t bmp, pad;
 };
+
+// Per 64-node block: a 2-D skyline of its rows' free (cpu, memory) — the Pareto-maximal
+// points over the visible rows with a free pod slot — so "can this pod fit any row of the
+// block" is a handful of compares instead of loading the block.  The per-dimension maxima it
+// replaces pass almost every block in a tight cluster (the most cpu and the most memory sit
+// on different rows): on C3 without a limit 876 failing full-ring scans read 56k blocks
+// whose maxima passed and that no exact skyline admits (scripts/plan_skyline_study.py).
+// Invariant: every such row is dominated by a stored point (an over-approximation):
+//   * points are 32-bit images rounded up — cpu clamped, memory in MiB rounded up; a pod
+//     is compared through the same monotone maps, so a row that fits passes;
+//   * at most PC_SKY points: past PC_SKY - 1 exact points the last one bounds the rest;
+//   * a row that shrinks (AddPod, a node leaving podDestinations) leaves the points valid
+//     (stale-high: a scan that loads the block without a fit rebuilds it); a row that grows
+//     (the candidate's own RemovePods, a Revert) sets n = -1 (unknown: always loaded);
+//   * the candidate being simulated is excluded (its scans exclude it, and its row grew).
+constexpr int PC_SKY = 8;
+struct PcSky {
+    int32_t n, pad;               // points stored (-1 = unknown)
+    int32_t c[PC_SKY], m[PC_SKY]; // cpu descending, memory ascending
+};
+static_assert(sizeof(PcSky) == 72, "PcSky");
+__host__ __device__ inline int32_t sky_c(int64_t v) {
+    return v > INT32_MAX ? INT32_MAX : (v < INT32_MIN ? INT32_MIN : (int32_t)v);
+}
+__host__ __device__ inline int32_t sky_m(int64_t v) {                 // ceil(v / 2^20), clamped
+    const int64_t q = (v >> 20) + ((v & 0xFFFFF) != 0);
+    return q > INT32_MAX ? INT32_MAX : (q < INT32_MIN ? INT32_MIN : (int32_t)q);
+}
 
 // LDS image of one call (byte offsets; every array 16-B aligned)
 struct PcLayout {
-    size_t rows, blk, excnt, scratch, resbuf, mvbuf, ctx, help, total;
+    size_t rows, blk, sky, excnt, scratch, resbuf, mvbuf, ctx, help, total;
 };
 
 __host__ __device__ inline PcLayout pc_layout(int32_t n, bool eph_cols) {
@@ -153,6 +179,7 @@ __host__ __device__ inline PcLayout pc_layout(int32_t n, bool eph_cols) {
     auto take = [&](size_t bytes) { const size_t r = o; o += (bytes + 15) & ~(size_t)15; return r; };
     L.rows = take((eph_cols ? sizeof(PcRowE) : sizeof(PcRow)) * nn);
     L.blk = take(sizeof(PcBlk) * nb);
+    L.sky = take(sizeof(PcSky) * nb);
     L.excnt = take(2 * nn);
     L.scratch = take(4 * 64);
     L.resbuf = take(sizeof(ca_plan_result) * 64);       // results of the current 64 candidates
@@ -186,13 +213,48 @@ __device__ inline uint64_t pc_uni64(uint64_t v) {
 }
 __device__ inline int64_t pc_uni64s(int64_t v) { return (int64_t)pc_uni64((uint64_t)v); }
 
-// workgroup-coherent global accesses: the chain's own earlier stores (hints, copies, PDB
-// budgets) are read back by other lanes of the same wavefront
+// Rebuilds a block's skyline from its 64 rows as one wave holds them (lane i: row j*64 + i;
+// `valid`: visible, a free pod slot, not the candidate being simulated).  Extraction: the
+// largest (cpu, memory) key is a skyline point; every row with memory at most its memory is
+// dominated by it (its cpu is at most the point's); repeat on the rest.  C3 blocks hold
+// 4-5 points on average (p99 10), so a rebuild is a few wave reductions.
+__device__ void pc_sky_build(PcSky* sk, int64_t cc, int64_t cm, bool valid) {
+    const int lane = threadIdx.x & 63;
+    const int32_t C = sky_c(cc), M = sky_m(cm);
+    const int64_t key = ((int64_t)C << 32) | (int64_t)(uint32_t)(M ^ INT32_MIN);   // cpu, then memory
+    bool alive = valid;
+    int k = 0;
+    while (k < PC_SKY - 1) {
+        if (!__ballot(alive)) break;
+        const int64_t mx = __ockl_wfred_max_i64(alive ? key : INT64_MIN);
+        const int32_t pm = (int32_t)((uint32_t)mx ^ (uint32_t)INT32_MIN);
+        if (lane == 0) { sk->c[k] = (int32_t)(mx >> 32); sk->m[k] = pm; }
+        k++;
+        alive = alive && M > pm;
+    }
+    if (k == PC_SKY - 1 && __ballot(alive)) {        // one point bounds the rest
+        const int64_t mx = __ockl_wfred_max_i64(alive ? key : INT64_MIN);
+        const int32_t mm = __ockl_wfred_max_i32(alive ? M : INT32_MIN);
+        if (lane == 0) { sk->c[k] = (int32_t)(mx >> 32); sk->m[k] = mm; }
+        k++;
+    }
+    if (lane == 0) sk->n = k;
+}
+
+// May some row of the block fit a pod with these 32-bit images (sky_c / sky_m of its
+// requests; all_zero: only a visible row with a free slot is needed)?
+__device__ inline bool pc_sky_maybe(const PcSky& sk, int32_t pc, int32_t pm, bool all_zero) {
+    const int32_t k = sk.n;
+    if (k < 0) return true;
+    if (all_zero) return k > 0;
+    bool hit = false;
+    for (int32_t i = 0; i < k; i++) hit |= (pc <= sk.c[i]) & (pm <= sk.m[i]);
+    return hit;
+}
+
+// workgroup-coherent global loads: the PDB budgets the chain's own atomics updated
 __device__ inline int32_t pc_ld(const int32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ inline void pc_st(int32_t* p, int32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // a list entry held by a lane (pod t in lane t % 64 of half t / 64)
@@ -217,18 +279,29 @@ __device__ inline PcPod pc_load(const PcPod* p) {
     return r;
 }
 
-// Out of line (rare: taints, affinity, node names), so the chain keeps its registers.
-__device__ __attribute__((noinline)) bool pc_static_fit(const PcArgs& a, int32_t x, int32_t spec, uint32_t pf) {
-    const NodeStatic ns = a.st[x];
-    return dev_static_filters(a.specs[spec], pf, a.terms, a.reqs, ns, false) == CA_PLUGIN_NONE;
+// Out of line (rare: taints, affinity, node names), so the chain keeps its registers.  The
+// tables are passed by value: a reference to the kernel's by-value PcArgs would make the
+// compiler copy the whole argument block to scratch memory and read every field back from
+// there (global-memory latency on the chain's critical path).
+struct PcTabs {
+    const NodeStatic* st;
+    const ca_pod_spec* specs;
+    const ca_selector_term* terms;
+    const ca_selector_req* reqs;
+    const int32_t* names;
+};
+__device__ __attribute__((noinline)) bool pc_static_fit(PcTabs t, int32_t x, int32_t spec, uint32_t pf) {
+    const NodeStatic ns = t.st[x];
+    return dev_static_filters(t.specs[spec], pf, t.terms, t.reqs, ns, false) == CA_PLUGIN_NONE;
 }
-__device__ __attribute__((noinline)) bool pc_in_names(const PcArgs& a, int32_t x, int32_t spec) {
-    const ca_pod_spec& s = a.specs[spec];
-    const int32_t nid = a.st[x].name_id;
+__device__ __attribute__((noinline)) bool pc_in_names(PcTabs t, int32_t x, int32_t spec) {
+    const ca_pod_spec& s = t.specs[spec];
+    const int32_t nid = t.st[x].name_id;
     bool in = false;
-    for (int32_t k = 0; k < s.prefilter_count; k++) in |= a.names[s.prefilter_first + k] == nid;
+    for (int32_t k = 0; k < s.prefilter_count; k++) in |= t.names[s.prefilter_first + k] == nid;
     return in;
 }
+__device__ inline PcTabs pc_tabs(const PcArgs& a) { return PcTabs{a.st, a.specs, a.terms, a.reqs, a.names}; }
 
 // Helper waves (the workgroup's waves 1..H).  The chain is one wavefront; a rotating scan
 // that has loaded PC_HELP_AFTER blocks without a fit (the tight phase: scans over most of
@@ -264,6 +337,7 @@ __device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) 
     using Row = typename PcRowT<EPH_COLS>::type;
     Row* const rows = reinterpret_cast<Row*>(pc_raw + Y.rows);
     PcBlk* const blk = reinterpret_cast<PcBlk*>(pc_raw + Y.blk);
+    PcSky* const sky = reinterpret_cast<PcSky*>(pc_raw + Y.sky);
     PcHelp* const q = reinterpret_cast<PcHelp*>(pc_raw + Y.help);
     int32_t seen = 0;
     for (;;) {
@@ -283,6 +357,7 @@ __device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) 
         const bool any_static = fl & PH_ANY_STATIC, taint_all = fl & PH_TAINT_ALL, all_zero = fl & PH_ALL_ZERO;
         const int32_t jn = node >> 6;
         const uint64_t nbit = 1ull << (node & 63);
+        const int32_t pc32 = sky_c(pcpu), pm32 = sky_m(pmem);
         uint64_t refr0 = 0, refr1 = 0;
         for (int32_t rr = rr_lo + h; rr <= rr_end; rr += H) {
             if (rr * 64 > __builtin_amdgcn_readfirstlane(ph_ld(&q->best))) break;   // a fit before this block
@@ -292,9 +367,7 @@ __device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) 
             const uint64_t cvis = pc_uni64(blk[j].vis);
             const uint64_t vw = cvis & inr & (j == jn ? ~nbit : ~0ull);
             if (!vw) continue;
-            const bool fitb = (blk[j].bmp >= 1) && (all_zero || ((pcpu <= blk[j].bmc) && (pmem <= blk[j].bmm) &&
-                                                                  (!EPH_COLS || peph <= blk[j].bme)));
-            if (!fitb) continue;                                    // the pod exceeds the block's maxima
+            if (!pc_sky_maybe(sky[j], pc32, pm32, all_zero)) continue;   // no row of the block can fit it
             const int32_t x = j * 64 + lane;
             const bool in = x < n;
             const int64_t cc = in ? rows[x].c : 0, cm = in ? rows[x].m : 0;
@@ -308,7 +381,7 @@ __device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) 
             const uint64_t needm = any_static ? ~0ull : (taint_all ? 0ull : pc_uni64(blk[j].taint));
             if (fitm & needm) {
                 bool ok = true;
-                if ((fitm & needm) >> lane & 1ull) ok = pc_static_fit(a, x, spec, pf);
+                if ((fitm & needm) >> lane & 1ull) ok = pc_static_fit(pc_tabs(a), x, spec, pf);
                 fitm &= __ballot(ok);
             }
             if (fitm) {
@@ -316,16 +389,8 @@ __device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) 
                 break;
             }
             const bool dj = j < 64 ? ((dirty0 >> j) & 1ull) : ((dirty1 >> (j - 64)) & 1ull);
-            if (dj) {                                               // exact maxima of the rows just read
-                const bool cv = (cvis >> lane) & 1ull;
-                const int64_t mc = __ockl_wfred_max_i64(cv ? cc : INT64_MIN);
-                const int64_t mmx = __ockl_wfred_max_i64(cv ? cm : INT64_MIN);
-                const int64_t me = EPH_COLS ? __ockl_wfred_max_i64(cv ? ce : INT64_MIN) : 0;
-                const int32_t mp = __ockl_wfred_max_i32(cv ? cp : INT32_MIN);
-                if (lane == 0) {
-                    blk[j].bmc = mc; blk[j].bmm = mmx; blk[j].bmp = mp;
-                    if (EPH_COLS) blk[j].bme = me;
-                }
+            if (dj) {                                               // the exact skyline of the rows just read
+                pc_sky_build(&sky[j], cc, cm, ((cvis >> lane) & 1ull) && cp >= 1 && x != node);
                 if (j < 64) refr0 |= 1ull << j; else refr1 |= 1ull << (j - 64);
             }
         }
@@ -372,6 +437,7 @@ __device__ inline void pc_flush_moves(const PcArgs& a, const ca_plan_move* mvbuf
 // Updates ctx (lastIndex, moves, dirty blocks) and ctx->r.
 template <bool EPH_COLS>
 __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& a, unsigned char* pc_raw, PcCtx* ctx, const int32_t c,
+                                                     const int32_t mo, const int32_t m0,
                                                      const int32_t node, const int32_t cnt, const PcReg r0,
                                                      const PcReg r1, const int nh) {
     const int lane = threadIdx.x;
@@ -380,6 +446,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
     using Row = typename PcRowT<EPH_COLS>::type;
     Row* const rows = reinterpret_cast<Row*>(pc_raw + Y.rows);
     PcBlk* const blk = reinterpret_cast<PcBlk*>(pc_raw + Y.blk);
+    PcSky* const sky = reinterpret_cast<PcSky*>(pc_raw + Y.sky);
     uint16_t* const excnt = reinterpret_cast<uint16_t*>(pc_raw + Y.excnt);
     int32_t* const scratch = reinterpret_cast<int32_t*>(pc_raw + Y.scratch);
     ca_plan_move* const mvbuf = reinterpret_cast<ca_plan_move*>(pc_raw + Y.mvbuf);
@@ -389,6 +456,11 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
     uint64_t dirty0 = ctx->dirty0, dirty1 = ctx->dirty1;
     ca_plan_result r = ctx->r;
     bool moved_L = false;                       // a scan succeeded: lastIndex is the wrapped value
+    // ring positions the candidate's scans advanced lastIndex over, and whether a hint placed
+    // a pod: scan placements lie at distinct positions while the advance stays within one
+    // ring, so the commit then needs no grouping of equal destinations
+    int32_t adv = 0;
+    bool hinted = false;
     PC_SIM_T0();
     // register cache of one 64-node block of rows (lane i: node cj * 64 + i): the free
     // columns in VGPRs, the block's visibility / ephemeral-ok / taint bits as wave-uniform
@@ -422,15 +494,10 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             if (lane == 0) {
                 rows[node].c = nc; rows[node].m = nmm; rows[node].p = np;
                 if (EPH_COLS) pc_set_e(rows[node], ne2);
-                // a row that grows raises its block's maxima (they are upper bounds)
-                const int64_t bc = blk[jn].bmc, bm = blk[jn].bmm, be = EPH_COLS ? blk[jn].bme : 0;
-                const int32_t bp = blk[jn].bmp;
-                if (nc > bc) blk[jn].bmc = nc;
-                if (nmm > bm) blk[jn].bmm = nmm;
-                if (EPH_COLS && ne2 > be) blk[jn].bme = ne2;
-                if (np > bp) blk[jn].bmp = np;
+                sky[jn].n = -1;             // a row that grows: the block's skyline is unknown
             }
             if (jn == cj && lane == (node & 63)) { cc = nc; cm = nmm; ce = ne2; cp = np; }
+            PC_MARK_DIRTY(jn);
         }
         PC_SIM_MARK(PC_FORK);
         uint64_t evals = 0;
@@ -445,7 +512,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             const bool prefail = (pf & PF_PREFILTER_FAIL) != 0;
             const bool all_zero = (pf & PF_ALL_ZERO) != 0;
             // TaintToleration / NodeAffinity / NodeName where the pod or the node needs them
-            auto static_fit = [&](int32_t x) -> bool { return pc_static_fit(a, x, spec, pf); };
+            auto static_fit = [&](int32_t x) -> bool { return pc_static_fit(pc_tabs(a), x, spec, pf); };
             const bool any_static = (pf & (PF_NODE_NAME | PF_AFFINITY)) != 0;
             const bool taint_all = (pf & PF_TAINT_MASK_ALL) != 0;
             int32_t target = -1;
@@ -467,13 +534,14 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                 if (ok && (any_static || ((tw & hb) && !taint_all))) ok = static_fit(h);
                 if (ok) {
                     if (lane == tl) { if (t >= 64) hs1 = h; else hs0 = h; }          // :95 Set
-                    if (h != node && (dw & hb)) { target = h; tc = hc; tm = hm; te = he; tpd = hp; }   // :102
+                    if (h != node && (dw & hb)) { target = h; tc = hc; tm = hm; te = he; tpd = hp; hinted = true; }   // :102
                 }
             }
             PC_SIM_MARK(PC_HINT);
             // ---- findNode -> FitsAnyNodeMatching(isCandidateNode) (:110-125) ----
             if (target < 0 && !prefail && n > 0) {
                 const bool names = (pf & PF_PREFILTER_NAMES) != 0;
+                const int32_t pc32 = sky_c(pcpu), pm32 = sky_m(pmem);
                 const int32_t j0 = Lw >> 6, l0 = Lw & 63;
                 int32_t wr = -1, my_nv = 0;
                 uint64_t passm = 0;
@@ -509,9 +577,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                                 int32_t jj = j0 + q;
                                 if (jj >= nb) jj -= nb;
                                 const uint64_t vw = blk[jj].vis & (jj == jn ? ~nbit : ~0ull);
-                                const bool fitb = (vw != 0) & (blk[jj].bmp >= 1) &
-                                                  (all_zero | ((pcpu <= blk[jj].bmc) & (pmem <= blk[jj].bmm) &
-                                                               (!EPH_COLS || peph <= blk[jj].bme)));
+                                const bool fitb = (vw != 0) && pc_sky_maybe(sky[jj], pc32, pm32, all_zero);
                                 pass = !fitb && jj != cj;
                                 my_nv = __popcll(vw);
                             }
@@ -557,6 +623,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                             tc = pc_uni64s(rows[target].c); tm = pc_uni64s(rows[target].m);
                             te = EPH_COLS ? pc_uni64s(pc_e(rows[target])) : 0;
                             tpd = __builtin_amdgcn_readfirstlane(rows[target].p);
+                            adv += (target >= Lw ? target - Lw : target + n - Lw) + 1;
                             Lw = target + 1 == n ? 0 : target + 1;                       // schedulerbased.go:131
                             moved_L = true;
                             if (lane == tl) { if (t >= 64) hs1 = target; else hs0 = target; }   // :123
@@ -575,7 +642,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                     uint64_t vism = cvis & inr & (j == jn ? ~nbit : ~0ull);
                     if (names && vism) {
                         bool in = false;
-                        if ((vism >> lane) & 1ull) in = pc_in_names(a, j * 64 + lane, spec);
+                        if ((vism >> lane) & 1ull) in = pc_in_names(pc_tabs(a), j * 64 + lane, spec);
                         vism &= __ballot(in);
                     }
                     uint64_t fitm = vism & __ballot(cp >= 1);
@@ -596,24 +663,17 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                         target = j * 64 + f;
                         tc = pc_rl64(cc, f); tm = pc_rl64(cm, f); te = EPH_COLS ? pc_rl64(ce, f) : 0;
                         tpd = pc_rl32(cp, f);
+                        adv += (target >= Lw ? target - Lw : target + n - Lw) + 1;
                         Lw = target + 1 == n ? 0 : target + 1;                       // schedulerbased.go:131
                         moved_L = true;
                         if (lane == tl) { if (t >= 64) hs1 = target; else hs0 = target; }   // :123
                         break;
                     }
                     evals += (uint64_t)__popcll(vism);
-                    // the block passed: refresh its maxima from the rows just read
+                    // the block passed: rebuild its skyline from the rows just read
                     const bool dj = j < 64 ? ((dirty0 >> j) & 1ull) : ((dirty1 >> (j - 64)) & 1ull);
                     if (dj) {
-                        const bool cv = (cvis >> lane) & 1ull;
-                        const int64_t mc = __ockl_wfred_max_i64(cv ? cc : INT64_MIN);
-                        const int64_t mmx = __ockl_wfred_max_i64(cv ? cm : INT64_MIN);
-                        const int64_t me = EPH_COLS ? __ockl_wfred_max_i64(cv ? ce : INT64_MIN) : 0;
-                        const int32_t mp = __ockl_wfred_max_i32(cv ? cp : INT32_MIN);
-                        if (lane == 0) {
-                            blk[j].bmc = mc; blk[j].bmm = mmx; blk[j].bmp = mp;
-                            if (EPH_COLS) blk[j].bme = me;
-                        }
+                        pc_sky_build(&sky[j], cc, cm, ((cvis >> lane) & 1ull) && cp >= 1 && j * 64 + lane != node);
                         if (j < 64) dirty0 &= ~(1ull << j); else dirty1 &= ~(1ull << (j - 64));
                     }
                 }
@@ -717,6 +777,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             PC_MARK_DIRTY(Lw >> 6);
             PC_MARK_DIRTY((Lw + span - 1 < n ? Lw + span - 1 : Lw + span - 1 - n) >> 6);
             evals += (uint64_t)k;
+            adv += (last >= Lw ? last - Lw : last + n - Lw) + 1;
             Lw = last + 1 == n ? 0 : last + 1;                                       // schedulerbased.go:131
             moved_L = true;
             cj = -1;                                                                 // rows changed
@@ -752,6 +813,9 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             // ---- Commit (cluster.go:207-211) ----
             r.removable = 1;
             r.n_moves = cnt;
+            // distinct destinations (no hint placement, the scans within one ring): each copy
+            // is its node's next entry — no grouping pass
+            const bool distinct = !hinted && adv <= n;
             for (int half = 0; half < 2 && half * 64 < cnt; half++) {
                 const int32_t t = half * 64 + lane;
                 const bool act = t < cnt;
@@ -762,33 +826,42 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                 if (act) {
                     ca_plan_move mv;
                     mv.candidate = c; mv.pod = q.id; mv.new_pod = a.base + s; mv.node = f;
-                    mvbuf[ctx->mv_n + t] = mv;
-                    pc_st(a.H + a.base + s, f);
+                    mvbuf[ctx->mv_n + t] = mv;          // (the copy's hint is f: it travels in its record)
                 }
                 // the copies join their destinations' pod lists in list order
-                int32_t rank = 0, lead = -1;
-                uint64_t pend = __ballot(act);
-                while (pend) {
-                    const int l = __builtin_ctzll(pend);
-                    const int32_t f0 = pc_rl32(f, l);
-                    const uint64_t mm = __ballot(act && f == f0);
-                    if (act && f == f0) { rank = __popcll(mm & pc_below(lane)); lead = l; }
-                    if (lane == l) scratch[l] = __popcll(mm);
-                    pend &= ~mm;
+                int32_t slot = 0;
+                if (distinct) {
+                    if (act) {
+                        const int32_t old = excnt[f];
+                        excnt[f] = (uint16_t)(old + 1);
+                        slot = fb + old;
+                    }
+                } else {
+                    int32_t rank = 0, lead = -1;
+                    uint64_t pend = __ballot(act);
+                    while (pend) {
+                        const int l = __builtin_ctzll(pend);
+                        const int32_t f0 = pc_rl32(f, l);
+                        const uint64_t mm = __ballot(act && f == f0);
+                        if (act && f == f0) { rank = __popcll(mm & pc_below(lane)); lead = l; }
+                        if (lane == l) scratch[l] = __popcll(mm);
+                        pend &= ~mm;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    if (act && lead == lane) {
+                        const int32_t old = excnt[f];
+                        excnt[f] = (uint16_t)(old + scratch[lane]);
+                        scratch[lane] = old;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    if (act) slot = fb + scratch[lead] + rank;
                 }
-                __builtin_amdgcn_wave_barrier();
-                if (act && lead == lane) {
-                    const int32_t old = excnt[f];
-                    excnt[f] = (uint16_t)(old + scratch[lane]);
-                    scratch[lane] = old;
-                }
-                __builtin_amdgcn_wave_barrier();
                 if (act) {
                     PcPod cp2;
                     cp2.cpu = q.cpu; cp2.mem = q.mem; cp2.eph = q.eph;
                     cp2.id = a.base + s; cp2.hint = f; cp2.flags = q.flags; cp2.spec = q.spec; cp2.orig = q.orig;
                     cp2.pad = 0;
-                    a.ex_pods[fb + scratch[lead] + rank] = cp2;
+                    a.ex_pods[slot] = cp2;
                 }
                 __builtin_amdgcn_wave_barrier();
             }
@@ -825,29 +898,36 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                 if (EPH_COLS) atomicAdd(reinterpret_cast<unsigned long long*>(pc_e_ptr(rows[f])), (unsigned long long)q.eph);
                 atomicAdd(&rows[f].p, 1);
             }
+            // the destinations' rows grew back: their blocks' skylines are unknown (and dirty);
+            // the candidate's own block is unknown already (its RemovePods)
+            uint64_t* const dmask = reinterpret_cast<uint64_t*>(scratch);
+            if (lane < 2) dmask[lane] = 0;
             __builtin_amdgcn_wave_barrier();
             for (int half = 0; half < 2; half++) {
                 const int32_t t = half * 64 + lane;
                 if (t >= placed) continue;
                 const int32_t f = half ? d1 : d0, j = f >> 6;
-                atomicMax(reinterpret_cast<long long*>(&blk[j].bmc), (long long)rows[f].c);
-                atomicMax(reinterpret_cast<long long*>(&blk[j].bmm), (long long)rows[f].m);
-                if (EPH_COLS) atomicMax(reinterpret_cast<long long*>(&blk[j].bme), (long long)pc_e(rows[f]));
-                atomicMax(&blk[j].bmp, rows[f].p);
+                sky[j].n = -1;
+                atomicOr(reinterpret_cast<unsigned long long*>(dmask + (j >> 6)), 1ull << (j & 63));
             }
             __builtin_amdgcn_wave_barrier();
+            dirty0 |= pc_uni64(dmask[0]);
+            dirty1 |= pc_uni64(dmask[1]);
             if (lane == 0) {
                 rows[node].c = wsub(rows[node].c, sc); rows[node].m = wsub(rows[node].m, sm); rows[node].p -= cnt;
                 if (EPH_COLS) pc_set_e(rows[node], wsub(pc_e(rows[node]), se));
+                sky[jn].n = -1;             // (built without this candidate while it ran)
             }
             PC_MARK_DIRTY(jn);
             cj = -1;                                                                 // rows changed
             r.reason = CA_UNREMOVABLE_NO_PLACE;                                      // cluster.go:174-177
             PC_SIM_MARK(PC_REVERT);
         }
-        // Hints.Set of this candidate's pods (hints persist whether or not it is removable)
-        if (hs0 != INT32_MIN) pc_st(a.H + r0.id, hs0);
-        if (hs1 != INT32_MIN) pc_st(a.H + r1.id, hs1);
+        // Hints.Set of this candidate's pods (hints persist whether or not it is removable): the
+        // caller's pods (the first m0 of the list) by move index; the copies' keys are not the
+        // caller's (a later candidacy reads a copy's hint from its record)
+        if (hs0 != INT32_MIN && lane < m0) a.hout[mo + lane] = hs0;
+        if (hs1 != INT32_MIN && 64 + lane < m0) a.hout[mo + 64 + lane] = hs1;
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
         ctx->Lw = Lw;
@@ -903,7 +983,7 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
                 if (lane == 0) {
                     blk[j].dest = dw; blk[j].vis = dw & ~uw; blk[j].usch = uw; blk[j].taint = tw;
                     if (!EPH_COLS) blk[j].eph = ew;
-                    blk[j].bmc = INT64_MAX; blk[j].bmm = INT64_MAX; blk[j].bme = INT64_MAX; blk[j].bmp = INT32_MAX;
+                    reinterpret_cast<PcSky*>(pc_raw + Y.sky)[j].n = -1;     // unknown until a scan reads it
                 }
             }
         }
@@ -957,6 +1037,7 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
     __builtin_amdgcn_wave_barrier();
     int32_t nm = 0, removed = 0, simulated = 0;
     bool cut = false, stopped = false;
+    int32_t stop_c = a.C;
     int32_t hb_node = -1, hb_st = 0, hb_mo = 0, hb_m1 = 0;    // candidate headers, lane k = c0 + k
     // the next candidate's first 64 pods, loaded while the current one runs
     PcPod nx = {};
@@ -981,12 +1062,7 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
         if (cut || (a.max_removable > 0 && removed >= a.max_removable)) {       // planner.go:268-271
             flush_res(c - sl, sl);
             stopped = true;
-            for (int32_t k = c + lane; k < a.C; k += 64) {
-                ca_plan_result r;
-                r.removable = 0; r.reason = CA_UNREMOVABLE_NOT_RUN; r.n_placed = 0; r.last_index_in = ctx->Lraw;
-                r.evals = 0; r.first_move = nm; r.n_moves = 0; r.blocking_pod = -1; r.risky = 0;
-                a.res[k] = r;
-            }
+            stop_c = c;                                  // (the host fills the rest: NOT_RUN)
             break;
         }
         PC_T0();
@@ -1058,7 +1134,7 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
         simulated++;
         if (lane == 0) ctx->r = r;
         __builtin_amdgcn_wave_barrier();
-        pc_simulate<EPH_COLS>(a, pc_raw, ctx, c, node, cnt, r0, r1, nh);
+        pc_simulate<EPH_COLS>(a, pc_raw, ctx, c, mo, m0, node, cnt, r0, r1, nh);
         r = ctx->r;
         nm = ctx->nm;
         removed = ctx->removed;
@@ -1078,6 +1154,7 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
         a.info[1] = nm;
         a.info[2] = removed;
         a.info[3] = simulated;
+        a.info[4 + PC_NPROF] = stop_c;
 #ifdef CASIM_PROF
         prof[PC_TOTAL] = clock64() - t_start;
         for (int k = 0; k < PC_NPROF; k++) a.info[4 + k] = (int64_t)(prof[k] + ctx->prof[k]);
@@ -1099,7 +1176,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
                    const int32_t* cand_status, const int32_t* move_off, const int32_t* move_pods,
                    int32_t max_removable, const ca_pdb_table* pdbs, int32_t* hints, int32_t n_pods,
                    int32_t* last_index, ca_plan_result* results, std::vector<ca_plan_move>& moves_out,
-                   std::vector<int32_t>& hints_out, int32_t* simulated_out) {
+                   std::vector<std::pair<int32_t, int32_t>>& hint_sets, int32_t* simulated_out) {
     if (knob_env("CASIM_PLAN_SPECULATIVE")) return 0;
     const int32_t N = (int32_t)m->nodes.size();
     if (N <= 0 || C <= 0) return 0;
@@ -1150,10 +1227,11 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     PlanChainScratch& S = m->pc;
     hipStream_t st = m->stream;
 
-    // packed inputs (one H2D): cands, status, move_off, move_pods, ex_base, pdb tables, hints; mask
+    // packed inputs (one H2D): cands, status, move_off, move_pods, ex_base, pdb tables, the
+    // caller's hint of every pod to move (by move index); mask
     const size_t n_pdb_members = P > 0 ? (size_t)pdbs->pod_off[n_pods] : 0;
     const size_t in_words = (size_t)C + C + (C + 1) + std::max(M, 1) + (N + 1) + (P > 0 ? (size_t)n_pods + 1 : 1) +
-                            std::max<size_t>(n_pdb_members, 1) + std::max(P, 1) + std::max(n_pods, 1);
+                            std::max<size_t>(n_pdb_members, 1) + std::max(P, 1) + std::max(M, 1);
     const size_t in_bytes = 4 * in_words + ((size_t)N + 15) / 16 * 16;
     if ((rc = S.in.reserve(in_bytes)) != CA_OK) return rc;
     if ((rc = S.h_in.reserve(in_bytes)) != CA_OK) return rc;
@@ -1174,33 +1252,37 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     const size_t o_pof = put(P > 0 ? pdbs->pod_off : nullptr, P > 0 ? n_pods + 1 : 0, P > 0 ? (size_t)n_pods + 1 : 1);
     const size_t o_pp = put(P > 0 ? pdbs->pod_pdb : nullptr, n_pdb_members, std::max<size_t>(n_pdb_members, 1));
     const size_t o_al = put(P > 0 ? pdbs->allowed : nullptr, P, std::max(P, 1));
-    const size_t o_h = put(hints, hints ? n_pods : 0, std::max(n_pods, 1));
-    if (!hints) for (int32_t i = 0; i < n_pods; i++) hw[o_h + i] = -1;
+    const size_t o_hm = put(nullptr, 0, std::max(M, 1));
+    for (int32_t i = 0; i < M; i++) hw[o_hm + i] = hints ? hints[move_pods[i]] : -1;
     const size_t o_mask = 4 * o;
     std::memcpy(reinterpret_cast<unsigned char*>(hw) + o_mask, dest_mask, (size_t)N);
     int32_t* const din = S.in.as<int32_t>();
     CA_HIP_CHECK(hipMemcpyAsync(din, hw, o_mask + (size_t)N, hipMemcpyHostToDevice, st));
 
-    // device work: hints H [base + copy_cap], the packed pods to move [M + 64], the copies [copy_cap]
-    const size_t h_bytes = (4 * ((size_t)base + copy_cap) + 15) & ~(size_t)15;
-    const size_t w_bytes = h_bytes + sizeof(PcPod) * ((size_t)M + 64) + sizeof(PcPod) * (size_t)copy_cap;
+    // device work: the packed pods to move [M + 64], the copies [copy_cap]
+    const size_t w_bytes = sizeof(PcPod) * ((size_t)M + 64) + sizeof(PcPod) * (size_t)copy_cap;
     if ((rc = S.work.reserve(w_bytes)) != CA_OK) return rc;
-    int32_t* const dH = S.work.as<int32_t>();
-    PcPod* const dpods = reinterpret_cast<PcPod*>(S.work.as<unsigned char>() + h_bytes);
+    PcPod* const dpods = S.work.as<PcPod>();
     PcPod* const dex = dpods + M + 64;
-    // hints of pods the caller did not pass (past n_pods) and of the copies start at -1
-    CA_HIP_CHECK(hipMemsetAsync(dH, 0xff, 4 * ((size_t)base + copy_cap), st));
-    CA_HIP_CHECK(hipMemcpyAsync(dH, din + o_h, 4 * (size_t)n_pods, hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(k_plan_pack, dim3((unsigned)((M + 64 + 255) / 256)), dim3(256), 0, st, din + o_mv, M,
-                       m->d_pods.hot.as<PodHot>(), (const int32_t*)dH, dpods);
+                       m->d_pods.hot.as<PodHot>(), (const int32_t*)(din + o_hm), dpods);
     CA_HIP_CHECK(hipGetLastError());
-    // outputs: results [C], info [PC_INFO], moves [copy_cap]
-    const size_t out_bytes = sizeof(ca_plan_result) * C + PC_INFO * sizeof(int64_t) + sizeof(ca_plan_move) * copy_cap;
-    if ((rc = S.out.reserve(out_bytes)) != CA_OK) return rc;
+    // outputs, written by the kernel straight into page-locked memory (no copies, one sync):
+    // results [C], info [PC_INFO], moves [copy_cap], the caller's pods' hints by move index [M]
+    const size_t out_bytes = sizeof(ca_plan_result) * C + PC_INFO * sizeof(int64_t) + sizeof(ca_plan_move) * copy_cap +
+                             sizeof(int32_t) * (size_t)std::max(M, 1);
     if ((rc = S.h_out.reserve(out_bytes)) != CA_OK) return rc;
-    ca_plan_result* const dres = S.out.as<ca_plan_result>();
+    ca_plan_result* const hres = S.h_out.as<ca_plan_result>();
+    int64_t* const hinfo = reinterpret_cast<int64_t*>(hres + C);
+    ca_plan_move* const hmoves = reinterpret_cast<ca_plan_move*>(hinfo + PC_INFO);
+    int32_t* const hhout = reinterpret_cast<int32_t*>(hmoves + copy_cap);
+    std::memcpy(hhout, hw + o_hm, sizeof(int32_t) * (size_t)M);     // unchanged unless Hints.Set
+    void* dout = nullptr;
+    CA_HIP_CHECK(hipHostGetDevicePointer(&dout, S.h_out.ptr, 0));
+    ca_plan_result* const dres = static_cast<ca_plan_result*>(dout);
     int64_t* const dinfo = reinterpret_cast<int64_t*>(dres + C);
     ca_plan_move* const dmoves = reinterpret_cast<ca_plan_move*>(dinfo + PC_INFO);
+    int32_t* const dhout = reinterpret_cast<int32_t*>(dmoves + copy_cap);
 
     PcArgs A;
     A.hot = m->d_hot.as<NodeHot>();
@@ -1222,7 +1304,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     A.allowed = din + o_al;
     A.pdb_off = din + o_pof;
     A.pdb_pod = din + o_pp;
-    A.H = dH;
+    A.hout = dhout;
     A.ex_base = din + o_exb;
     A.ex_pods = dex;
     A.res = dres;
@@ -1253,11 +1335,8 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     if (eph_cols) hipLaunchKernelGGL(k_plan_chain<true>, dim3(1), dim3(64 * waves), Y.total, st, A);
     else hipLaunchKernelGGL(k_plan_chain<false>, dim3(1), dim3(64 * waves), Y.total, st, A);
     CA_HIP_CHECK(hipGetLastError());
-    ca_plan_result* const hres = S.h_out.as<ca_plan_result>();
-    int64_t* const hinfo = reinterpret_cast<int64_t*>(hres + C);
-    ca_plan_move* const hmoves = reinterpret_cast<ca_plan_move*>(hinfo + PC_INFO);
     CA_HIP_CHECK(hipEventRecord(m->ev1, st));
-    CA_HIP_CHECK(hipMemcpyAsync(hres, dres, sizeof(ca_plan_result) * C + PC_INFO * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    if (P > 0) CA_HIP_CHECK(hipMemcpyAsync(hw + o_al, din + o_al, 4 * (size_t)P, hipMemcpyDeviceToHost, st));
     CA_HIP_CHECK(hipStreamSynchronize(st));
     const auto t_kernel = std::chrono::steady_clock::now();
     if (tr_env) {
@@ -1271,20 +1350,23 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
         }
     }
     const int32_t nm = (int32_t)hinfo[1];
-    if (nm < 0 || nm > copy_cap) {
+    const int32_t stop_c = (int32_t)hinfo[4 + PC_NPROF];
+    if (nm < 0 || nm > copy_cap || stop_c < 0 || stop_c > C) {
         set_last_error("plan chain: move count out of range");
         return CA_EDEVICE;
     }
-    // the moves, the callers' hints and the PDB budgets (page-locked staging reused: the
-    // inputs are consumed)
-    if (nm > 0) CA_HIP_CHECK(hipMemcpyAsync(hmoves, dmoves, sizeof(ca_plan_move) * nm, hipMemcpyDeviceToHost, st));
-    if (hints && n_pods > 0) CA_HIP_CHECK(hipMemcpyAsync(hw + o_h, dH, 4 * (size_t)n_pods, hipMemcpyDeviceToHost, st));
-    if (P > 0) CA_HIP_CHECK(hipMemcpyAsync(hw + o_al, din + o_al, 4 * (size_t)P, hipMemcpyDeviceToHost, st));
-    CA_HIP_CHECK(hipStreamSynchronize(st));
-    std::memcpy(results, hres, sizeof(ca_plan_result) * C);
+    std::memcpy(results, hres, sizeof(ca_plan_result) * (size_t)stop_c);
+    for (int32_t k = stop_c; k < C; k++) {                     // planner.go:268-271: not run
+        ca_plan_result& r = results[k];
+        r.removable = 0; r.reason = CA_UNREMOVABLE_NOT_RUN; r.n_placed = 0; r.last_index_in = (int32_t)hinfo[0];
+        r.evals = 0; r.first_move = nm; r.n_moves = 0; r.blocking_pod = -1; r.risky = 0;
+    }
     *last_index = (int32_t)hinfo[0];
     if (simulated_out) *simulated_out = (int32_t)hinfo[3];
-    if (hints) hints_out.assign(hw + o_h, hw + o_h + n_pods);
+    hint_sets.clear();
+    if (hints)                                                  // Hints.Set of the caller's pods that ran
+        for (int32_t i = 0; i < move_off[stop_c]; i++)
+            if (hhout[i] != hw[o_hm + i]) hint_sets.emplace_back(move_pods[i], hhout[i]);
     if (P > 0) std::memcpy(pdbs->allowed, hw + o_al, 4 * (size_t)P);
     moves_out.assign(hmoves, hmoves + nm);
     const auto t_read = std::chrono::steady_clock::now();

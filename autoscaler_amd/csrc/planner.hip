@@ -103,7 +103,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
                    const int32_t* cand_status, const int32_t* move_off, const int32_t* move_pods,
                    int32_t max_removable, const ca_pdb_table* pdbs, int32_t* hints, int32_t n_pods,
                    int32_t* last_index, ca_plan_result* results, std::vector<ca_plan_move>& moves_out,
-                   std::vector<int32_t>& hints_out, int32_t* simulated_out);
+                   std::vector<std::pair<int32_t, int32_t>>& hint_sets, int32_t* simulated_out);
 }  // namespace casim
 
 namespace {
@@ -150,7 +150,7 @@ int plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const uint
     {
         // the device-resident chain (plan_chain.hip); the speculative windows below otherwise
         int32_t sim = 0, Lc = *last_index;
-        std::vector<int32_t> hc;
+        std::vector<std::pair<int32_t, int32_t>> hc;            // Hints.Set of the caller's pods (pod, node)
         const int rc = plan_chain_run(m, candidates, C, dest_mask, cand_status, move_off, move_pods, max_removable,
                                       pdbs, hints, n_pods, &Lc, results, ps.moves, hc, &sim);
         if (rc < 0) return rc;
@@ -163,7 +163,7 @@ int plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const uint
                 return CA_EDEVICE;
             }
             *last_index = Lc;
-            if (hints && n_pods > 0) std::memcpy(hints, hc.data(), sizeof(int32_t) * (size_t)n_pods);
+            if (hints) for (const auto& e : hc) hints[e.first] = e.second;
             const int32_t nm = (int32_t)ps.moves.size();
             if (moves) std::memcpy(moves, ps.moves.data(), sizeof(ca_plan_move) * (size_t)std::min(nm, moves_cap));
             if (n_moves) *n_moves = nm;

@@ -1098,6 +1098,54 @@ __global__ void __launch_bounds__(1024) k_walk_resolve(const int32_t* __restrict
     if (threadIdx.x == 0) { info[0] = sk; info[1] = cur_out; }
 }
 
+// The block map of a candidate range (multi-device sweep, multi.hip): the same chunk maps
+// as k_walk_resolve, chained from each of the 64 classes of the range's first row instead
+// of from one known input.  out[x] = the range's lastIndex out when it starts in class x
+// (-1: the walk leaves a window or meets a row the table cannot simulate);
+// out[64 + i] = the first row's fit points (its class boundaries, FPW entries; in
+// consecutive mode only [1], the window start, is meaningful); out[64 + FPW] = mode[0].
+// The caller composes the ranges' maps in order from the true input: a range whose input
+// falls inside its first window is resolved without re-running anything.
+__global__ void __launch_bounds__(1024) k_walk_map(const int32_t* __restrict__ tfp, const int32_t* __restrict__ cmap,
+                                                  const int32_t* __restrict__ mode, int32_t S, int32_t n,
+                                                  int32_t* __restrict__ out) {
+    extern __shared__ int32_t wr_lds[];
+    const int32_t nch = (S + WK - 1) / WK;
+    int32_t* const cm = wr_lds;
+    int32_t* const heads = wr_lds + (size_t)nch * 64;
+    for (int32_t i = threadIdx.x; i < nch * 64; i += blockDim.x) cm[i] = cmap[i];
+    const bool classes = mode[0] != 0;
+    if (classes)
+        for (int32_t i = threadIdx.x; i < nch * FPW; i += blockDim.x)
+            heads[i] = tfp[(size_t)(i % FPW) * S + (size_t)(i / FPW) * WK];
+    else
+        for (int32_t j = threadIdx.x; j < nch; j += blockDim.x) heads[(size_t)j * FPW + 1] = tfp[(size_t)S + (size_t)j * WK];
+    __syncthreads();
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        int32_t x = tid, cur = -1;
+        bool ok = true;
+        for (int32_t j = 0; j < nch && ok; j++) {
+            if (j > 0) {
+                if (classes) {
+                    x = fp_class(heads + (size_t)j * FPW, 1, n, cur);
+                } else {
+                    x = cur - heads[(size_t)j * FPW + 1];
+                    if (x < 0) x += n;
+                    if (x >= 64) x = -1;
+                }
+                if (x < 0) { ok = false; break; }
+            }
+            const int32_t r = cm[j * 64 + x];
+            if (r < 0) ok = false;
+            else cur = r;
+        }
+        out[tid] = ok ? cur : -1;
+    }
+    if (tid < FPW) out[64 + tid] = classes ? heads[tid] : (tid == 1 ? heads[1] : 0);
+    if (tid == 0) out[64 + FPW] = classes ? 1 : 0;
+}
+
 // Candidates the device walk resolved through the table (need == 2): the table lane at
 // their exact input simulated them exactly (unhinted, no ports / extended requests, no
 // ring wrap, every pod placed), so its outputs are theirs: removable, every pod at its
@@ -1216,7 +1264,7 @@ int launch_exact(ca_mirror* m, hipStream_t st, const SweepCall& in, const int32_
 // d_pod_hints: the mirror's resident per-pod hints (used and updated instead when
 // non-null).  out_dest nullable.
 int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod_hints, int32_t* last_index,
-               ca_removal_result* results, int32_t* out_dest) {
+               ca_removal_result* results, int32_t* out_dest, SweepPhase* ph = nullptr) {
     const auto t_start = std::chrono::steady_clock::now();
     const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
     auto tmark = [&](const char* what) {
@@ -1294,7 +1342,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     const int64_t L0 = *last_index;               // raw until the first placement (Go keeps the int)
     std::vector<int32_t> guess((size_t)C, 0);
     {
-        int64_t g = L0;
+        int64_t g = ph && ph->kind != SP_FULL ? ph->guess_base : L0;
         int32_t k = 0;
         for (int32_t c = 0; c < C; c++) {
             guess[c] = wrap(g, n);
@@ -1321,12 +1369,18 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     }
     if ((rc = sw.bsum.reserve(sizeof(BlockSum) * (size_t)std::max((n + 63) / 64, 1))) != CA_OK) return rc;
     if ((rc = sw.h_l0.reserve(sizeof(int32_t) * 4)) != CA_OK) return rc;
-    sw.h_l0.as<int32_t>()[0] = n > 0 ? wrap(L0, n) : 0;  // -> mode[2]: the chain's input (k_sweep_est, k_walk_resolve)
+    // -> mode[2]: the chain's input (k_sweep_est, k_walk_resolve); a range's SP_MAP centres
+    // its windows on the estimate of its input instead
+    sw.h_l0.as<int32_t>()[0] = n > 0 ? wrap(ph && ph->kind == SP_MAP ? (int64_t)ph->est_base : L0, n) : 0;
+    if (ph) ph->S = S;
     const bool use_ext = m->n_ext_pods > 0;
     if (use_ext && (rc = ensure_dyn_lds((const void*)k_sweep, sizeof(OverlayExt))) != CA_OK) return rc;
     const size_t wr_bytes = sizeof(int32_t) * (size_t)nch * (64 + FPW);
     if (dev_walk && (rc = ensure_dyn_lds((const void*)k_walk_resolve,
                                          sizeof(int32_t) * (size_t)WALK_MAX_CHUNKS * (64 + FPW))) != CA_OK)
+        return rc;
+    if (dev_walk && ph && ph->kind == SP_MAP &&
+        (rc = ensure_dyn_lds((const void*)k_walk_map, sizeof(int32_t) * (size_t)WALK_MAX_CHUNKS * (64 + FPW))) != CA_OK)
         return rc;
     // the resident hints: applied behind the exact pass, while the results travel (a host
     // walk below re-runs candidates and applies them again; its exact passes read the
@@ -1395,6 +1449,77 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         CA_HIP_CHECK(hipMemcpyAsync(sw.h_out.ptr, sw.out.ptr, d2h_bytes, hipMemcpyDeviceToHost, st));
         return CA_OK;
     };
+    // ---- the three calls of a multi-device range (SweepPhase above) ----
+    auto enqueue_phase = [&]() -> int {
+        int e;
+        CA_HIP_CHECK(hipMemcpyAsync(d_lin, h_lin, (sizeof(int32_t) + 1) * (size_t)C, hipMemcpyHostToDevice, st));
+        CA_HIP_CHECK(hipMemcpyAsync(d_mode + 2, sw.h_l0.ptr, sizeof(int32_t), hipMemcpyHostToDevice, st));
+        if (ph->kind == SP_PROBE) {
+            if (d_pod_hints && M > 0) {
+                hipLaunchKernelGGL(k_hints_gather, dim3((M + 255) / 256), dim3(256), 0, st, d_pod_hints,
+                                   in.d_moves.as<int32_t>(), M, in.d_hints.as<int32_t>());
+                CA_HIP_CHECK(hipGetLastError());
+            }
+            if (n > 0) {
+                hipLaunchKernelGGL(k_block_sum, dim3((n + 63) / 64), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
+                                   in.d_mask.as<uint8_t>(), n, sw.bsum.as<BlockSum>());
+                CA_HIP_CHECK(hipGetLastError());
+            }
+            if ((e = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl)) != CA_OK) return e;
+            CA_HIP_CHECK(hipMemcpyAsync(sw.h_out.ptr, sw.out.ptr, sizeof(SweepOut) * (size_t)C, hipMemcpyDeviceToHost, st));
+            return CA_OK;
+        }
+        if (ph->kind == SP_MAP) {
+            if (!(S > 0 && n > 0)) return CA_OK;
+            CA_HIP_CHECK(hipMemcpyAsync(d_sens, ht, sizeof(int32_t) * S, hipMemcpyHostToDevice, st));
+            CA_HIP_CHECK(hipMemcpyAsync(d_tdoff, ht + 2 * S, sizeof(int32_t) * S, hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_sweep_est, dim3(1), dim3(1024), 0, st, d_out.as<SweepOut>(), d_sens, S, n, d_ws, d_mode,
+                               m->d_hot.as<NodeHot>(), in.d_mask.as<uint8_t>(), dev_walk ? sw.vp.as<int32_t>() : nullptr);
+            CA_HIP_CHECK(hipGetLastError());
+            hipLaunchKernelGGL(k_sweep_table, dim3(S), dim3(64), 0, st, m->d_hot.as<NodeHot>(),
+                               m->d_static.as<NodeStatic>(), n, in.d_mask.as<uint8_t>(), in.d_c.as<int32_t>(),
+                               in.d_off.as<int32_t>(), in.d_moves.as<int32_t>(), m->d_pods.hot.as<PodHot>(),
+                               m->d_pods.spec.as<ca_pod_spec>(), m->d_pods.terms.as<ca_selector_term>(),
+                               m->d_pods.reqs.as<ca_selector_req>(), m->d_pods.names.as<int32_t>(),
+                               in.d_hints.as<int32_t>(), d_sens, d_ws, (const int32_t*)nullptr, sw.tab.as<int32_t>(), S,
+                               dev_walk ? sw.tev.as<uint32_t>() : nullptr, dev_walk ? sw.tdest.as<int32_t>() : nullptr,
+                               dev_walk ? (const int32_t*)d_tdoff : nullptr, d_tfp, (const int32_t*)d_mode,
+                               sw.bsum.as<BlockSum>());
+            CA_HIP_CHECK(hipGetLastError());
+            if (!dev_walk) return CA_OK;            // (the range's resolve walks on the host)
+            CA_HIP_CHECK(hipMemsetAsync(d_need, 0, (size_t)C, st));
+            hipLaunchKernelGGL(k_walk_chunks, dim3(nch), dim3(64), 0, st, d_sens, d_ws, d_lin, d_wl, sw.tab.as<int32_t>(),
+                               d_tfp, d_mode, S, n, d_cmap, d_traj);
+            CA_HIP_CHECK(hipGetLastError());
+            if ((e = sw.bmap.reserve(sizeof(int32_t) * (64 + FPW + 1))) != CA_OK) return e;
+            if ((e = sw.h_bmap.reserve(sizeof(int32_t) * (64 + FPW + 1))) != CA_OK) return e;
+            hipLaunchKernelGGL(k_walk_map, dim3(1), dim3(1024), wr_bytes, st, d_tfp, d_cmap, d_mode, S, n,
+                               sw.bmap.as<int32_t>());
+            CA_HIP_CHECK(hipGetLastError());
+            CA_HIP_CHECK(hipMemcpyAsync(sw.h_bmap.ptr, sw.bmap.ptr, sizeof(int32_t) * (64 + FPW + 1), hipMemcpyDeviceToHost,
+                                        st));
+            return CA_OK;
+        }
+        // SP_RESOLVE: the tail of enqueue() from the true input (mode[2])
+        if (dev_walk) {
+            // (the probe's results for the candidates the walk does not re-run stay in d_out;
+            // d_lin was re-uploaded with the same guesses, need = 0 as the map phase left it)
+            CA_HIP_CHECK(hipMemsetAsync(d_need, 0, (size_t)C, st));
+            hipLaunchKernelGGL(k_walk_resolve, dim3(1), dim3(1024), wr_bytes, st, d_sens, d_tfp, d_cmap, d_traj, d_wl,
+                               d_mode, S, n, d_lin, d_need, d_info);
+            CA_HIP_CHECK(hipGetLastError());
+            hipLaunchKernelGGL(k_table_gather, dim3(S), dim3(64), 0, st, d_sens, d_tfp, sw.vp.as<int32_t>(),
+                               in.d_c.as<int32_t>(), in.d_mask.as<uint8_t>(), m->d_hot.as<NodeHot>(), S, n, d_lin, d_need,
+                               sw.tab.as<int32_t>(), sw.tev.as<uint32_t>(), sw.tdest.as<int32_t>(), d_tdoff,
+                               in.d_off.as<int32_t>(), d_out.as<SweepOut>(), d_dest.as<int32_t>(), d_hset.as<int32_t>(),
+                               d_wl, d_mode);
+            CA_HIP_CHECK(hipGetLastError());
+            if ((e = launch_exact(m, st, in, d_lin, d_need, d_dest, d_hset, d_out, d_wl)) != CA_OK) return e;
+        }
+        if ((e = apply_hints()) != CA_OK) return e;
+        CA_HIP_CHECK(hipMemcpyAsync(sw.h_out.ptr, sw.out.ptr, d2h_bytes, hipMemcpyDeviceToHost, st));
+        return CA_OK;
+    };
     // The pipeline is a dozen launches and copies whose arguments depend only on the call's
     // shape (sizes, buffers, flags): a call with the shape of the previous one replays it
     // as a HIP graph captured on the second such call (no per-launch host cost, no gaps
@@ -1432,7 +1557,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     // sensitive — not to an unrelated call on the same mirror.
     const bool same_shape = C <= 2 * sw.serial_C && 2 * C >= sw.serial_C && S <= 2 * sw.serial_S &&
                             2 * S >= sw.serial_S && 2 * S >= C;
-    const bool serial_only = S > 0 && n > 0 && !knob_env("CASIM_NO_SERIAL_CHAIN") &&
+    const bool serial_only = !(ph && ph->kind != SP_FULL) && S > 0 && n > 0 && !knob_env("CASIM_NO_SERIAL_CHAIN") &&
                              ((C <= 2048 && sw.serial_next && same_shape) || knob_env("CASIM_SWEEP_SERIAL") != nullptr);
     auto enqueue_serial = [&]() -> int {
         int e;
@@ -1461,7 +1586,10 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     };
     static const bool no_graph = getenv("CASIM_NO_GRAPH") != nullptr;
     CA_HIP_CHECK(hipEventRecord(m->ev0, st));
-    if (serial_only) {
+    const bool phased = ph && ph->kind != SP_FULL;
+    if (phased) {
+        if ((rc = enqueue_phase()) != CA_OK) return rc;
+    } else if (serial_only) {
         if ((rc = enqueue_serial()) != CA_OK) return rc;
     } else if (!no_graph && sw.gexec && sw.gkey == gkey) {
         CA_HIP_CHECK(hipGraphLaunch(sw.gexec, st));
@@ -1484,6 +1612,27 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     }
     CA_HIP_CHECK(hipEventRecord(m->ev1, st));
     CA_HIP_CHECK(hipStreamSynchronize(st));
+    if (phased && ph->kind == SP_PROBE) {
+        // the range's advance as k_sweep_est sums it (successful scans only)
+        int64_t adv = 0;
+        int32_t succ = 0;
+        for (int32_t k = 0; k < S; k++) {
+            const SweepOut& o = outs[sens[k]];
+            if (!o.fa_success) continue;
+            succ++;
+            int64_t d = ((int64_t)o.lout - (int64_t)o.lin) % n;
+            if (d < 0) d += n;
+            adv += d;
+        }
+        ph->adv = adv;
+        ph->succ = succ;
+        return CA_OK;
+    }
+    if (phased && ph->kind == SP_MAP) {
+        ph->map_ok = (S > 0 && n > 0 && dev_walk) ? 1 : 0;
+        if (ph->map_ok) std::memcpy(ph->map, sw.h_bmap.ptr, sizeof(int32_t) * (64 + FPW + 1));
+        return CA_OK;
+    }
     float kms = 0;
     {
         float ms = 0;
@@ -1748,7 +1897,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     // (the hint update stays queued on the mirror's stream: every later call is ordered
     // behind it, and ca_mirror_get_hints synchronises)
     tmark("done");
-    {   // the next call's mode (serial_only above)
+    if (!phased) {   // the next call's mode (serial_only above)
         const float per = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_start).count() /
                           (float)std::max(C, 1);
         if (serial_only) {
@@ -2010,7 +2159,33 @@ int ca_removal_plan_create(ca_mirror* m, const int32_t* candidates, int32_t C, c
 
 int ca_removal_plan_run(ca_removal_plan* p, int32_t* hints, int32_t* last_index, ca_removal_result* results,
                         int32_t* out_dest) {
+    return casim::removal_plan_run_phase(p, hints, last_index, results, out_dest, nullptr);
+}
+
+}  // extern "C"
+
+namespace casim {
+
+bool removal_plan_phase_ok(const ca_removal_plan* p) { return p->C == p->C_all; }
+int32_t sweep_fp_class(const int32_t* fp, int32_t n, int32_t L) { return fp_class(fp, 1, n, L); }
+
+// pods to move of the plan's sensitive candidates (the probe's guess step, sweep_core)
+int64_t removal_plan_sensitive_pods(const ca_removal_plan* p) {
+    int64_t t = 0;
+    for (int32_t c = 0; c < p->C; c++) {
+        const int32_t nd = p->cand[c];
+        if (nd < 0 || nd >= p->n || !p->mask[nd] || p->status[c] != 0) continue;
+        t += p->off[c + 1] - p->off[c];
+    }
+    return t;
+}
+
+// A phase of a multi-device range (SweepPhase in sweep_core); ph == nullptr: a whole call.
+// A plan with a scope cut runs whole calls only (ph->kind must be SP_FULL).
+int removal_plan_run_phase(ca_removal_plan* p, int32_t* hints, int32_t* last_index, ca_removal_result* results,
+                           int32_t* out_dest, SweepPhase* ph) {
     if (!p || !last_index || (p->C_all > 0 && !results)) return CA_EINVAL;
+    if (ph && ph->kind != SP_FULL && p->C < p->C_all) return CA_EINVAL;
     ca_mirror* m = p->m;
     CA_HIP_CHECK(hipSetDevice(m->device));
     m->sweep_stats.had_success = m->sweep_stats.lin_sensitive = 0;
@@ -2042,8 +2217,12 @@ int ca_removal_plan_run(ca_removal_plan* p, int32_t* hints, int32_t* last_index,
         if ((rc = m->ensure_pod_hints()) != CA_OK) return rc;
         d_pod_hints = m->d_pod_hints.as<int32_t>();
     }
-    return casim::sweep_core(m, in, hints, d_pod_hints, last_index, results, out_dest);
+    return casim::sweep_core(m, in, hints, d_pod_hints, last_index, results, out_dest, ph);
 }
+
+}  // namespace casim
+
+extern "C" {
 
 int ca_removal_plan_destroy(ca_removal_plan* p) {
     if (!p) return CA_EINVAL;

@@ -778,6 +778,32 @@ def main():
                        "results_identical_to_host_mode": same,
                        "results": "scheduled pods left in HBM (ca_estimate_plan_run with sched_pod = NULL); "
                                   "results[] and lastIndex on the host"}
+    # cold latency: a caller whose pending set changed since the last loop builds a new plan
+    # (plan_prepare walks the batch's items on the host, checks float64 ties, uploads the
+    # lists) and runs it once; and the one-shot Mirror.estimate (plan + run + teardown)
+    cold = None
+    if dist is None and g1 > g0:
+        cp, cr, cb = [], [], []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            with native.EstimatePlan(mirror, w.table, off_blk, idx_blk, tm_blk) as p2:
+                t1 = time.perf_counter()
+                if host_mode == "u16":
+                    p2.run_u16(w.max_nodes, L0, copy=False)
+                else:
+                    p2.run(w.max_nodes, L0, want_nodes=False, copy=False)
+                t2 = time.perf_counter()
+            cp.append(t1 - t0)
+            cr.append(t2 - t1)
+            t3 = time.perf_counter()
+            mirror.estimate(w.table, off_blk, idx_blk, tm_blk, w.max_nodes, L0, want_nodes=False)
+            cb.append(time.perf_counter() - t3)
+        cold = {"plan_create_ms": float(np.median(cp) * 1e3), "first_run_ms": float(np.median(cr) * 1e3),
+                "plan_create_plus_first_run_ms": float(np.median(np.add(cp, cr)) * 1e3),
+                "one_shot_estimate_ms": float(np.median(cb) * 1e3),
+                "note": "median of 3 on the headline's mirror: a new EstimatePlan over the same C2 batch (host item "
+                        "walk, tie check, list upload) and its first run with results on the host as the headline; "
+                        "one_shot = Mirror.estimate (plan + run + teardown, 32-bit ids copied to the host)"}
     n_cls = len(set(zip(w.table.pods["score_milli_cpu"].tolist(), w.table.pods["score_memory"].tolist())))
     n_merge = 1 if n_cls <= 256 else 2                            # radix passes (8-bit digits)
     ph_mean = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]} if g1 > g0 else {}
@@ -860,6 +886,7 @@ def main():
                                    f"{sorted(set(pub)) if pub else None}",
                 "device_resident": device_resident,
                 "host_int32_ids": host_i32,
+                "cold": cold,
                 "sort_ms": float(np.mean(sort_ms)) if sort_ms else None,
                 "phases_ms": ph_mean,
                 "chain_kernel_ms": ph_mean.get("chain_ms"),

@@ -40,7 +40,7 @@ constexpr int32_t PC_MVBUF = 512;             // moves staged in LDS between glo
 constexpr int PC_MAX_WAVES = 8;               // the chain wave + up to 7 helper waves (VGPR budget: 2 waves / SIMD)
 // shader-clock counters of the chain's phases (info[4 + k]; CASIM_PROF builds only)
 enum { PC_INIT, PC_LISTS, PC_PDB, PC_FORK, PC_HINT, PC_SCAN, PC_ADD, PC_COMMIT, PC_REVERT, PC_TOTAL, PC_BLOCKS,
-       PC_WINDOWS, PC_HANDOFFS, PC_NPROF };
+       PC_WINDOWS, PC_HANDOFFS, PC_BULK, PC_PREP, PC_WIN, PC_LOADCHK, PC_SKYB, PC_NPROF };
 constexpr int PC_INFO = 4 + PC_NPROF + 3;     // int64 words of the kernel's info record
 #ifdef CASIM_PROF
 #define PC_T0() uint64_t tp_ = clock64()
@@ -122,17 +122,16 @@ __global__ void __launch_bounds__(256) k_plan_pack(const int32_t* __restrict__ m
     out[i] = r;
 }
 
-// A committed node row in LDS: free cpu / memory (/ ephemeral storage) / pod slots.
-struct PcRow { int64_t c, m; int32_t p, pad; };
-struct PcRowE { int64_t c, m, e; int32_t p, pad; };
-__device__ inline int64_t pc_e(const PcRow&) { return 0; }
-__device__ inline int64_t pc_e(const PcRowE& r) { return r.e; }
-__device__ inline void pc_set_e(PcRow&, int64_t) {}
-__device__ inline void pc_set_e(PcRowE& r, int64_t v) { r.e = v; }
-__device__ inline unsigned long long* pc_e_ptr(PcRow& r) { return reinterpret_cast<unsigned long long*>(&r.c); }
-__device__ inline unsigned long long* pc_e_ptr(PcRowE& r) { return reinterpret_cast<unsigned long long*>(&r.e); }
-template <bool E> struct PcRowT { using type = PcRow; };
-template <> struct PcRowT<true> { using type = PcRowE; };
+// The committed node rows in LDS, one array per column (free cpu / memory / [ephemeral
+// storage] / pod slots): a wave reads a block's column with one conflict-free access per
+// lane.  ex_base (each node's first slot in the copy table) sits beside them.
+struct PcRows {
+    int64_t* c;
+    int64_t* m;
+    int64_t* e;                   // EPH_COLS only
+    int32_t* p;
+    int32_t* exb;                 // [n + 1]
+};
 // Per 64-node block: bit planes (podDestinations, visible = destination and schedulable,
 // unschedulable, tainted, free ephemeral >= 0).
 struct PcBlk {
@@ -169,7 +168,7 @@ __host__ __device__ inline int32_t sky_m(int64_t v) {                 // ceil(v 
 
 // LDS image of one call (byte offsets; every array 16-B aligned)
 struct PcLayout {
-    size_t rows, blk, sky, excnt, scratch, resbuf, mvbuf, ctx, help, total;
+    size_t rc, rm, re, rp, exb, blk, sky, excnt, scratch, resbuf, mvbuf, ctx, help, total;
 };
 
 __host__ __device__ inline PcLayout pc_layout(int32_t n, bool eph_cols) {
@@ -177,7 +176,11 @@ __host__ __device__ inline PcLayout pc_layout(int32_t n, bool eph_cols) {
     const size_t nn = (size_t)n, nb = (nn + 63) / 64;
     size_t o = 0;
     auto take = [&](size_t bytes) { const size_t r = o; o += (bytes + 15) & ~(size_t)15; return r; };
-    L.rows = take((eph_cols ? sizeof(PcRowE) : sizeof(PcRow)) * nn);
+    L.rc = take(8 * nn);
+    L.rm = take(8 * nn);
+    L.re = eph_cols ? take(8 * nn) : 0;
+    L.rp = take(4 * nn);
+    L.exb = take(4 * (nn + 1));
     L.blk = take(sizeof(PcBlk) * nb);
     L.sky = take(sizeof(PcSky) * nb);
     L.excnt = take(2 * nn);
@@ -188,6 +191,16 @@ __host__ __device__ inline PcLayout pc_layout(int32_t n, bool eph_cols) {
     L.help = take(256);                                // PcHelp (scan requests to the helper waves)
     L.total = o;
     return L;
+}
+
+__device__ inline PcRows pc_rows(unsigned char* pc_raw, const PcLayout& Y) {
+    PcRows r;
+    r.c = reinterpret_cast<int64_t*>(pc_raw + Y.rc);
+    r.m = reinterpret_cast<int64_t*>(pc_raw + Y.rm);
+    r.e = reinterpret_cast<int64_t*>(pc_raw + Y.re);
+    r.p = reinterpret_cast<int32_t*>(pc_raw + Y.rp);
+    r.exb = reinterpret_cast<int32_t*>(pc_raw + Y.exb);
+    return r;
 }
 
 extern "C" __device__ long long __ockl_wfred_add_i64(long long);
@@ -290,11 +303,11 @@ struct PcTabs {
     const ca_selector_req* reqs;
     const int32_t* names;
 };
-__device__ __attribute__((noinline)) bool pc_static_fit(PcTabs t, int32_t x, int32_t spec, uint32_t pf) {
+__device__ __attribute__((always_inline)) inline bool pc_static_fit(PcTabs t, int32_t x, int32_t spec, uint32_t pf) {
     const NodeStatic ns = t.st[x];
     return dev_static_filters(t.specs[spec], pf, t.terms, t.reqs, ns, false) == CA_PLUGIN_NONE;
 }
-__device__ __attribute__((noinline)) bool pc_in_names(PcTabs t, int32_t x, int32_t spec) {
+__device__ __attribute__((always_inline)) inline bool pc_in_names(PcTabs t, int32_t x, int32_t spec) {
     const ca_pod_spec& s = t.specs[spec];
     const int32_t nid = t.st[x].name_id;
     bool in = false;
@@ -334,8 +347,11 @@ __device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) 
     const int lane = threadIdx.x & 63;
     const int32_t n = a.n;
     const PcLayout Y = pc_layout(n, EPH_COLS);
-    using Row = typename PcRowT<EPH_COLS>::type;
-    Row* const rows = reinterpret_cast<Row*>(pc_raw + Y.rows);
+    const PcRows R_ = pc_rows(pc_raw, Y);
+    int64_t* const rc = R_.c;
+    int64_t* const rm = R_.m;
+    int64_t* const re = R_.e;
+    int32_t* const rp = R_.p;
     PcBlk* const blk = reinterpret_cast<PcBlk*>(pc_raw + Y.blk);
     PcSky* const sky = reinterpret_cast<PcSky*>(pc_raw + Y.sky);
     PcHelp* const q = reinterpret_cast<PcHelp*>(pc_raw + Y.help);
@@ -349,11 +365,13 @@ __device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) 
         }
         if (sq == seen) break;                                   // quit
         seen = sq;
-        const int32_t rr_lo = q->rr_lo, rr_end = q->rr_end, j0 = q->j0, l0 = q->l0, nb = q->nb, node = q->node;
-        const int32_t spec = q->spec, fl = q->fl;
-        const int64_t pcpu = q->pcpu, pmem = q->pmem, peph = q->peph;
-        const uint32_t pf = q->pf;
-        const uint64_t dirty0 = q->dirty0, dirty1 = q->dirty1;
+        const int32_t rr_lo = __builtin_amdgcn_readfirstlane(q->rr_lo), rr_end = __builtin_amdgcn_readfirstlane(q->rr_end);
+        const int32_t j0 = __builtin_amdgcn_readfirstlane(q->j0), l0 = __builtin_amdgcn_readfirstlane(q->l0);
+        const int32_t nb = __builtin_amdgcn_readfirstlane(q->nb), node = __builtin_amdgcn_readfirstlane(q->node);
+        const int32_t spec = __builtin_amdgcn_readfirstlane(q->spec), fl = __builtin_amdgcn_readfirstlane(q->fl);
+        const int64_t pcpu = pc_uni64s(q->pcpu), pmem = pc_uni64s(q->pmem), peph = pc_uni64s(q->peph);
+        const uint32_t pf = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)q->pf);
+        const uint64_t dirty0 = pc_uni64(q->dirty0), dirty1 = pc_uni64(q->dirty1);
         const bool any_static = fl & PH_ANY_STATIC, taint_all = fl & PH_TAINT_ALL, all_zero = fl & PH_ALL_ZERO;
         const int32_t jn = node >> 6;
         const uint64_t nbit = 1ull << (node & 63);
@@ -370,9 +388,9 @@ __device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) 
             if (!pc_sky_maybe(sky[j], pc32, pm32, all_zero)) continue;   // no row of the block can fit it
             const int32_t x = j * 64 + lane;
             const bool in = x < n;
-            const int64_t cc = in ? rows[x].c : 0, cm = in ? rows[x].m : 0;
-            const int64_t ce = (EPH_COLS && in) ? pc_e(rows[x]) : 0;
-            const int32_t cp = in ? rows[x].p : INT32_MIN;
+            const int64_t cc = in ? rc[x] : 0, cm = in ? rm[x] : 0;
+            const int64_t ce = (EPH_COLS && in) ? re[x] : 0;
+            const int32_t cp = in ? rp[x] : INT32_MIN;
             uint64_t fitm = vw & __ballot(cp >= 1);
             if (!all_zero) {
                 fitm &= __ballot(pcpu <= cc) & __ballot(pmem <= cm);
@@ -413,7 +431,7 @@ struct PcCtx {
 };
 
 __device__ inline void pc_flush_moves(const PcArgs& a, const ca_plan_move* mvbuf, PcCtx* ctx, int lane) {
-    const int32_t k = ctx->mv_n, first = ctx->mv_first;
+    const int32_t k = __builtin_amdgcn_readfirstlane(ctx->mv_n), first = __builtin_amdgcn_readfirstlane(ctx->mv_first);
     for (int32_t i = lane; i < k; i += 64) a.moves[first + i] = mvbuf[i];
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) { ctx->mv_first = first + k; ctx->mv_n = 0; }
@@ -443,17 +461,23 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
     const int lane = threadIdx.x;
     const int32_t n = a.n, nb = (n + 63) >> 6;
     const PcLayout Y = pc_layout(n, EPH_COLS);
-    using Row = typename PcRowT<EPH_COLS>::type;
-    Row* const rows = reinterpret_cast<Row*>(pc_raw + Y.rows);
+    const PcRows R_ = pc_rows(pc_raw, Y);
+    int64_t* const rc = R_.c;
+    int64_t* const rm = R_.m;
+    int64_t* const re = R_.e;
+    int32_t* const rp = R_.p;
     PcBlk* const blk = reinterpret_cast<PcBlk*>(pc_raw + Y.blk);
     PcSky* const sky = reinterpret_cast<PcSky*>(pc_raw + Y.sky);
     uint16_t* const excnt = reinterpret_cast<uint16_t*>(pc_raw + Y.excnt);
     int32_t* const scratch = reinterpret_cast<int32_t*>(pc_raw + Y.scratch);
     ca_plan_move* const mvbuf = reinterpret_cast<ca_plan_move*>(pc_raw + Y.mvbuf);
     PcHelp* const hq = reinterpret_cast<PcHelp*>(pc_raw + Y.help);
-    int32_t Lw = ctx->Lw;
-    const int32_t nm = ctx->nm;
-    uint64_t dirty0 = ctx->dirty0, dirty1 = ctx->dirty1;
+    // (the shared scalars come back through readfirstlane: an LDS load is a per-lane value to
+    // the compiler, and everything derived from it would run on the vector unit — a wave64
+    // VALU instruction costs four cycles on a 16-lane SIMD, an SALU one)
+    int32_t Lw = __builtin_amdgcn_readfirstlane(ctx->Lw);
+    const int32_t nm = __builtin_amdgcn_readfirstlane(ctx->nm);
+    uint64_t dirty0 = pc_uni64(ctx->dirty0), dirty1 = pc_uni64(ctx->dirty1);
     ca_plan_result r = ctx->r;
     bool moved_L = false;                       // a scan succeeded: lastIndex is the wrapped value
     // ring positions the candidate's scans advanced lastIndex over, and whether a hint placed
@@ -472,8 +496,8 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
     auto load_block = [&](int32_t j) {
         const int32_t x = j * 64 + lane;
         const bool in = x < n;
-        cc = in ? rows[x].c : 0; cm = in ? rows[x].m : 0; cp = in ? rows[x].p : INT32_MIN;
-        ce = (EPH_COLS && in) ? pc_e(rows[x]) : 0;
+        cc = in ? rc[x] : 0; cm = in ? rm[x] : 0; cp = in ? rp[x] : INT32_MIN;
+        ce = (EPH_COLS && in) ? re[x] : 0;
         cvis = pc_uni64(blk[j].vis);
         cok = EPH_COLS ? ~0ull : pc_uni64(blk[j].eph);
         ctaint = pc_uni64(blk[j].taint);
@@ -487,13 +511,13 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
         const int32_t jn = node >> 6;
         const uint64_t nbit = 1ull << (node & 63);
         {
-            const int64_t oc = rows[node].c, om = rows[node].m, oe = EPH_COLS ? pc_e(rows[node]) : 0;
-            const int32_t op = rows[node].p;
+            const int64_t oc = rc[node], om = rm[node], oe = EPH_COLS ? re[node] : 0;
+            const int32_t op = rp[node];
             const int64_t nc = wadd(oc, sc), nmm = wadd(om, sm), ne2 = wadd(oe, se);
             const int32_t np = op + cnt;
             if (lane == 0) {
-                rows[node].c = nc; rows[node].m = nmm; rows[node].p = np;
-                if (EPH_COLS) pc_set_e(rows[node], ne2);
+                rc[node] = nc; rm[node] = nmm; rp[node] = np;
+                if (EPH_COLS) re[node] = ne2;
                 sky[jn].n = -1;             // a row that grows: the block's skyline is unknown
             }
             if (jn == cj && lane == (node & 63)) { cc = nc; cm = nmm; ce = ne2; cp = np; }
@@ -509,6 +533,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
         // one pod (uniform values): hint check, then the rotating scan, then AddPod
         auto place = [&](const int32_t t, const int64_t pcpu, const int64_t pmem, const int64_t peph, const uint32_t pf,
                          const int32_t h, const int32_t spec) -> bool {
+            PC_SIM_MARK(PC_PREP);
             const bool prefail = (pf & PF_PREFILTER_FAIL) != 0;
             const bool all_zero = (pf & PF_ALL_ZERO) != 0;
             // TaintToleration / NodeAffinity / NodeName where the pod or the node needs them
@@ -522,16 +547,18 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             // ---- findNodeWithHints (hinting_simulator.go:91-108): CheckPredicates ----
             if (h >= 0 && h < n && !prefail) {
                 evals++;
-                const int64_t hc = pc_uni64s(rows[h].c), hm = pc_uni64s(rows[h].m);
-                const int64_t he = EPH_COLS ? pc_uni64s(pc_e(rows[h])) : 0;
-                const int32_t hp = __builtin_amdgcn_readfirstlane(rows[h].p);
+                const int64_t hc = pc_uni64s(rc[h]), hm = pc_uni64s(rm[h]);
+                const int64_t he = EPH_COLS ? pc_uni64s(re[h]) : 0;
+                const int32_t hp = __builtin_amdgcn_readfirstlane(rp[h]);
                 const int32_t jh = h >> 6;
                 const uint64_t hb = 1ull << (h & 63);
                 const uint64_t uw = pc_uni64(blk[jh].usch), tw = pc_uni64(blk[jh].taint), dw = pc_uni64(blk[jh].dest);
                 const bool eok = EPH_COLS ? (peph <= he) : ((pc_uni64(blk[jh].eph) & hb) != 0);
                 bool ok = !((uw & hb) && !(pf & PF_TOL_UNSCHED));
                 ok = ok && (hp >= 1) && (all_zero || ((pcpu <= hc) && (pmem <= hm) && eok));
-                if (ok && (any_static || ((tw & hb) && !taint_all))) ok = static_fit(h);
+                // (the call's result is a per-lane value to the compiler; every lane checked the same
+                // node: making it uniform keeps the whole pod loop on the scalar unit)
+                if (ok && (any_static || ((tw & hb) && !taint_all))) ok = __builtin_amdgcn_readfirstlane(static_fit(h) ? 1 : 0) != 0;
                 if (ok) {
                     if (lane == tl) { if (t >= 64) hs1 = h; else hs0 = h; }          // :95 Set
                     if (h != node && (dw & hb)) { target = h; tc = hc; tm = hm; te = he; tpd = hp; hinted = true; }   // :102
@@ -583,6 +610,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                             }
                             passm = __ballot(pass);
                             wr = rr;
+                            PC_SIM_MARK(PC_WIN);
                         }
                         const int32_t off = rr - wr;
                         const uint64_t stop = ~passm & (~0ull << off);
@@ -590,6 +618,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                         if (k > 0) {
                             evals += (uint64_t)__ockl_wfred_add_i32((lane >= off && lane < off + k) ? my_nv : 0);
                             rr += k - 1;
+                            PC_SIM_MARK(PC_WIN);
                             continue;
                         }
                     }
@@ -620,9 +649,9 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                             const uint64_t upto = (f == 63) ? ~0ull : ((2ull << f) - 1);
                             evals += vis_count(rr, rb - 1) + (uint64_t)__popcll(vmb & upto);
                             target = jb * 64 + f;
-                            tc = pc_uni64s(rows[target].c); tm = pc_uni64s(rows[target].m);
-                            te = EPH_COLS ? pc_uni64s(pc_e(rows[target])) : 0;
-                            tpd = __builtin_amdgcn_readfirstlane(rows[target].p);
+                            tc = pc_uni64s(rc[target]); tm = pc_uni64s(rm[target]);
+                            te = EPH_COLS ? pc_uni64s(re[target]) : 0;
+                            tpd = __builtin_amdgcn_readfirstlane(rp[target]);
                             adv += (target >= Lw ? target - Lw : target + n - Lw) + 1;
                             Lw = target + 1 == n ? 0 : target + 1;                       // schedulerbased.go:131
                             moved_L = true;
@@ -656,6 +685,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                         if ((fitm & needm) >> lane & 1ull) ok = static_fit(j * 64 + lane);
                         fitm &= __ballot(ok);
                     }
+                    PC_SIM_MARK(PC_LOADCHK);
                     if (fitm) {
                         const int f = __builtin_ctzll(fitm);
                         const uint64_t upto = (f == 63) ? ~0ull : ((2ull << f) - 1);
@@ -675,6 +705,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                     if (dj) {
                         pc_sky_build(&sky[j], cc, cm, ((cvis >> lane) & 1ull) && cp >= 1 && j * 64 + lane != node);
                         if (j < 64) dirty0 &= ~(1ull << j); else dirty1 &= ~(1ull << (j - 64));
+                        PC_SIM_MARK(PC_SKYB);
                     }
                 }
             }
@@ -687,7 +718,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                     const int32_t dn = a.trace[1];
                     e[0] = c; e[1] = t; e[2] = h; e[3] = (int32_t)pf; e[4] = target; e[5] = (int32_t)evals;
                     e[6] = Lw; e[7] = cnt; e[8] = (int32_t)pcpu; e[9] = (int32_t)(pmem >> 20);
-                    e[10] = (int32_t)rows[dn].c; e[11] = (int32_t)(rows[dn].m >> 20); e[12] = rows[dn].p;
+                    e[10] = (int32_t)rc[dn]; e[11] = (int32_t)(rm[dn] >> 20); e[12] = rp[dn];
                     e[13] = (int32_t)((blk[(dn) >> 6].vis >> ((dn) & 63)) & 1ull) | ((int32_t)((blk[(dn) >> 6].taint >> ((dn) & 63)) & 1ull) << 1) |
                             ((int32_t)(EPH_COLS ? 1 : ((blk[(dn) >> 6].eph >> ((dn) & 63)) & 1ull)) << 2);
                     e[14] = spec; e[15] = -1;
@@ -699,13 +730,13 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             const int64_t nc = wsub(tc, pcpu), nmm = wsub(tm, pmem), ne2 = wsub(te, peph);
             const int32_t np = tpd - 1;
             if (lane == 0) {
-                rows[target].c = nc; rows[target].m = nmm; rows[target].p = np;
-                if (EPH_COLS) pc_set_e(rows[target], ne2);
+                rc[target] = nc; rm[target] = nmm; rp[target] = np;
+                if (EPH_COLS) re[target] = ne2;
             }
             if ((target >> 6) == cj && lane == (target & 63)) { cc = nc; cm = nmm; ce = ne2; cp = np; }
             PC_MARK_DIRTY(target >> 6);
             if (lane == tl) {
-                const int32_t eb = a.ex_base[target];                                // (used at Commit)
+                const int32_t eb = R_.exb[target];                                   // (used at Commit)
                 if (t >= 64) { d1 = target; eb1 = eb; } else { d0 = target; eb0 = eb; }
             }
             PC_SIM_MARK(PC_ADD);
@@ -748,10 +779,9 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             const uint32_t pf2 = (uint32_t)__shfl((int32_t)(hi ? r1.flags : r0.flags), src, 64);
             bool fit = false;
             if (mine) {
-                const Row& rw = rows[x];
-                const bool eok = EPH_COLS ? (pe2 <= pc_e(rw)) : ((blk[x >> 6].eph >> (x & 63)) & 1ull);
+                const bool eok = EPH_COLS ? (pe2 <= re[x]) : ((blk[x >> 6].eph >> (x & 63)) & 1ull);
                 const bool tnt = (blk[x >> 6].taint >> (x & 63)) & 1ull;
-                fit = (rw.p >= 1) && ((pf2 & PF_ALL_ZERO) || ((pc2 <= rw.c) && (pm2 <= rw.m) && eok)) &&
+                fit = (rp[x] >= 1) && ((pf2 & PF_ALL_ZERO) || ((pc2 <= rc[x]) && (pm2 <= rm[x]) && eok)) &&
                       !(tnt && !(pf2 & PF_TAINT_MASK_ALL));
             }
             const uint64_t failm = __ballot(mine && !fit);
@@ -761,16 +791,15 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             if (k == 0) return 0;
             const bool put = vis && rank < k;
             if (put) {                                                                // AddPod (:79)
-                Row& rw = rows[x];
-                rw.c = wsub(rw.c, pc2); rw.m = wsub(rw.m, pm2); rw.p -= 1;
-                if (EPH_COLS) pc_set_e(rw, wsub(pc_e(rw), pe2));
+                rc[x] = wsub(rc[x], pc2); rm[x] = wsub(rm[x], pm2); rp[x] -= 1;
+                if (EPH_COLS) re[x] = wsub(re[x], pe2);
                 scratch[(tl0 + rank) & 63] = x;
             }
             __builtin_amdgcn_wave_barrier();
             const int32_t last = __builtin_amdgcn_readfirstlane(scratch[(tl0 + k - 1) & 63]);
             if (lane >= tl0 && lane < tl0 + k) {                                    // pods t0 .. t0+k-1
                 const int32_t v = scratch[lane];
-                const int32_t eb = a.ex_base[v];                                     // (used at Commit)
+                const int32_t eb = R_.exb[v];                                        // (used at Commit)
                 if (hi) { d1 = v; hs1 = v; eb1 = eb; } else { d0 = v; hs0 = v; eb0 = eb; }   // :123 Set
             }
             __builtin_amdgcn_wave_barrier();
@@ -788,6 +817,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             while (t < cnt && !failed) {
                 if (cool == 0 && n > 1) {
                     const int32_t k = bulk(t);
+                    PC_SIM_MARK(PC_BULK);
                     placed += k;
                     t += k;
                     if (k > 0) continue;
@@ -816,6 +846,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             // distinct destinations (no hint placement, the scans within one ring): each copy
             // is its node's next entry — no grouping pass
             const bool distinct = !hinted && adv <= n;
+            const int32_t mvn = __builtin_amdgcn_readfirstlane(ctx->mv_n);
             for (int half = 0; half < 2 && half * 64 < cnt; half++) {
                 const int32_t t = half * 64 + lane;
                 const bool act = t < cnt;
@@ -826,7 +857,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                 if (act) {
                     ca_plan_move mv;
                     mv.candidate = c; mv.pod = q.id; mv.new_pod = a.base + s; mv.node = f;
-                    mvbuf[ctx->mv_n + t] = mv;          // (the copy's hint is f: it travels in its record)
+                    mvbuf[mvn + t] = mv;                // (the copy's hint is f: it travels in its record)
                 }
                 // the copies join their destinations' pod lists in list order
                 int32_t slot = 0;
@@ -883,7 +914,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             __builtin_amdgcn_wave_barrier();
             if (lane == 0) { ctx->removed++; ctx->nm = nm + cnt; ctx->mv_n += cnt; }
             __builtin_amdgcn_wave_barrier();
-            if (ctx->mv_n + PC_LIST > PC_MVBUF) pc_flush_moves(a, mvbuf, ctx, lane);
+            if (mvn + cnt + PC_LIST > PC_MVBUF) pc_flush_moves(a, mvbuf, ctx, lane);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             PC_SIM_MARK(PC_COMMIT);
         } else {
@@ -893,10 +924,10 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                 if (t >= placed) continue;
                 const PcReg& q = half ? r1 : r0;
                 const int32_t f = half ? d1 : d0;
-                atomicAdd(reinterpret_cast<unsigned long long*>(&rows[f].c), (unsigned long long)q.cpu);
-                atomicAdd(reinterpret_cast<unsigned long long*>(&rows[f].m), (unsigned long long)q.mem);
-                if (EPH_COLS) atomicAdd(reinterpret_cast<unsigned long long*>(pc_e_ptr(rows[f])), (unsigned long long)q.eph);
-                atomicAdd(&rows[f].p, 1);
+                atomicAdd(reinterpret_cast<unsigned long long*>(&rc[f]), (unsigned long long)q.cpu);
+                atomicAdd(reinterpret_cast<unsigned long long*>(&rm[f]), (unsigned long long)q.mem);
+                if (EPH_COLS) atomicAdd(reinterpret_cast<unsigned long long*>(reinterpret_cast<unsigned long long*>(&re[f])), (unsigned long long)q.eph);
+                atomicAdd(&rp[f], 1);
             }
             // the destinations' rows grew back: their blocks' skylines are unknown (and dirty);
             // the candidate's own block is unknown already (its RemovePods)
@@ -914,8 +945,8 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             dirty0 |= pc_uni64(dmask[0]);
             dirty1 |= pc_uni64(dmask[1]);
             if (lane == 0) {
-                rows[node].c = wsub(rows[node].c, sc); rows[node].m = wsub(rows[node].m, sm); rows[node].p -= cnt;
-                if (EPH_COLS) pc_set_e(rows[node], wsub(pc_e(rows[node]), se));
+                rc[node] = wsub(rc[node], sc); rm[node] = wsub(rm[node], sm); rp[node] -= cnt;
+                if (EPH_COLS) re[node] = wsub(re[node], se);
                 sky[jn].n = -1;             // (built without this candidate while it ran)
             }
             PC_MARK_DIRTY(jn);
@@ -945,17 +976,21 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
     const int32_t n = a.n, nb = (n + 63) >> 6;
     const PcLayout Y = pc_layout(n, EPH_COLS);
     const int nh = (int)(blockDim.x >> 6) - 1;                  // helper waves
-    using Row = typename PcRowT<EPH_COLS>::type;
 #ifdef CASIM_PROF
     const uint64_t t_init0 = clock64();
 #endif
     {
         // ---- the committed rows and bit planes into LDS: every wave of the workgroup
         // loads its share of the 64-node blocks (4 in flight per lane) ----
-        Row* const rows = reinterpret_cast<Row*>(pc_raw + Y.rows);
+        const PcRows R_ = pc_rows(pc_raw, Y);
+        int64_t* const rc = R_.c;
+        int64_t* const rm = R_.m;
+        int64_t* const re = R_.e;
+        int32_t* const rp = R_.p;
         PcBlk* const blk = reinterpret_cast<PcBlk*>(pc_raw + Y.blk);
         uint16_t* const excnt = reinterpret_cast<uint16_t*>(pc_raw + Y.excnt);
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = (int)(blockDim.x >> 6);
+        for (int32_t i = (int32_t)threadIdx.x; i <= n; i += (int32_t)blockDim.x) R_.exb[i] = a.ex_base[i];
         for (int32_t b0 = 4 * wv; b0 < nb; b0 += 4 * nw) {
             NodeHot h[4];
             uint8_t dm[4];
@@ -973,8 +1008,8 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
                 const int32_t i = j * 64 + lane;
                 const bool valid = i < n;
                 if (valid) {
-                    rows[i].c = h[u].cpu; rows[i].m = h[u].mem; rows[i].p = h[u].pods; excnt[i] = 0;
-                    if (EPH_COLS) pc_set_e(rows[i], h[u].eph);
+                    rc[i] = h[u].cpu; rm[i] = h[u].mem; rp[i] = h[u].pods; excnt[i] = 0;
+                    if (EPH_COLS) re[i] = h[u].eph;
                 }
                 const uint64_t dw = __ballot(valid && dm[u] != 0);
                 const uint64_t uw = __ballot(valid && (h[u].flags & NF_UNSCHED));
@@ -1069,14 +1104,15 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
         const int32_t node = pc_rl32(hb_node, sl), stc = pc_rl32(hb_st, sl);
         const int32_t mo = pc_rl32(hb_mo, sl), m0 = mo1 - mo;
         ca_plan_result r;
-        r.removable = 0; r.reason = CA_UNREMOVABLE_NONE; r.n_placed = 0; r.last_index_in = ctx->Lraw;
+        r.removable = 0; r.reason = CA_UNREMOVABLE_NONE; r.n_placed = 0;
+        r.last_index_in = __builtin_amdgcn_readfirstlane(ctx->Lraw);
         r.evals = 0; r.first_move = nm; r.n_moves = 0; r.blocking_pod = -1; r.risky = 0;
-        const bool valid = node >= 0 && node < n && ((blk[(node) >> 6].dest >> ((node) & 63)) & 1ull);
+        const bool valid = node >= 0 && node < n && ((pc_uni64(blk[(node) >> 6].dest) >> ((node) & 63)) & 1ull);
         int32_t cnt = m0;
         if (valid && stc == 0) {
             // GetPodsToMove on the committed snapshot: the caller's list, then the copies
             // committed onto this node (NodeInfo.Pods appends)
-            const int32_t ne = excnt[node];
+            const int32_t ne = __builtin_amdgcn_readfirstlane(excnt[node]);
             cnt = m0 + ne;
             if (cnt > PC_LIST) {
                 cut = true;                                                         // casim.h scope
@@ -1084,7 +1120,8 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
                 if (m0 > 64) r1 = pc_reg(pc_load(a.pods + mo + 64 + lane));
                 if (ne > 0) {
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                    const PcPod* ex = a.ex_pods + a.ex_base[node];
+                    const PcPod* ex = a.ex_pods + __builtin_amdgcn_readfirstlane(
+                                                      reinterpret_cast<const int32_t*>(pc_raw + Y.exb)[node]);
                     const int32_t t0 = lane, t1 = 64 + lane;
                     if (t0 >= m0 && t0 < cnt) r0 = pc_reg(pc_load(ex + (t0 - m0)));
                     if (t1 >= m0 && t1 < cnt) r1 = pc_reg(pc_load(ex + (t1 - m0)));
@@ -1136,8 +1173,8 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
         __builtin_amdgcn_wave_barrier();
         pc_simulate<EPH_COLS>(a, pc_raw, ctx, c, mo, m0, node, cnt, r0, r1, nh);
         r = ctx->r;
-        nm = ctx->nm;
-        removed = ctx->removed;
+        nm = __builtin_amdgcn_readfirstlane(ctx->nm);
+        removed = __builtin_amdgcn_readfirstlane(ctx->removed);
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) resbuf[sl] = r;
         if (sl == 63) flush_res(c - 63, 64);

@@ -518,11 +518,11 @@ class Mirror:
 
     def plan_chain_profile(self) -> dict:
         """Phase cycle counters and host timings of the last device-chain planner call."""
-        cyc = np.zeros(16, np.uint64)
+        cyc = np.zeros(32, np.uint64)
         hm = np.zeros(5, np.float32)
-        k = self.lib.ca_plan_chain_profile(self.h, cyc.ctypes.data, 16, hm.ctypes.data)
+        k = self.lib.ca_plan_chain_profile(self.h, cyc.ctypes.data, 32, hm.ctypes.data)
         names = ["init", "lists", "pdb", "fork", "hint", "scan", "add", "commit", "revert", "total", "blocks",
-                 "windows", "handoffs"]
+                 "windows", "handoffs", "bulk", "prep", "win", "loadchk", "skyb"]
         out = {nm: int(v) for nm, v in zip(names, cyc[:max(k, 0)])}
         out.update({h: float(v) for h, v in zip(["sync_ms", "launch_kernel_ms", "kernel_ms", "readback_ms",
                                                    "replay_ms"], hm)})

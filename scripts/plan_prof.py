@@ -39,7 +39,8 @@ for limit in (20, 200, 0):
                                    ("sync_ms", "launch_kernel_ms", "kernel_ms", "readback_ms", "replay_ms")))
     print(f"   kernel clock {ghz:.2f} GHz; phases (% of total cycles): " +
           "  ".join(f"{k}={100 * pr[k] / tot:.1f}" for k in
-                    ("init", "lists", "pdb", "fork", "hint", "scan", "add", "commit", "revert")))
+                    ("init", "lists", "pdb", "fork", "bulk", "prep", "hint", "win", "loadchk", "skyb", "scan", "add",
+                     "commit", "revert")))
     print(f"   blocks scanned {pr['blocks']}  skip windows {pr['windows']}  helper hand-offs {pr.get('handoffs', 0)}",
           flush=True)
     m.close()

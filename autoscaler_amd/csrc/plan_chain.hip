@@ -40,7 +40,8 @@ constexpr int32_t PC_MVBUF = 512;             // moves staged in LDS between glo
 constexpr int PC_MAX_WAVES = 8;               // the chain wave + up to 7 helper waves (VGPR budget: 2 waves / SIMD)
 // shader-clock counters of the chain's phases (info[4 + k]; CASIM_PROF builds only)
 enum { PC_INIT, PC_LISTS, PC_PDB, PC_FORK, PC_HINT, PC_SCAN, PC_ADD, PC_COMMIT, PC_REVERT, PC_TOTAL, PC_BLOCKS,
-       PC_WINDOWS, PC_HANDOFFS, PC_BULK, PC_PREP, PC_WIN, PC_LOADCHK, PC_SKYB, PC_NPROF };
+       PC_WINDOWS, PC_HANDOFFS, PC_BULK, PC_PREP, PC_WIN, PC_LOADCHK, PC_SKYB,
+       PC_R_POD, PC_R_WIN, PC_R_BLK, PC_R_SKY, PC_R_ADD, PC_R_NPODS, PC_R_NBLK, PC_R_NWIN, PC_NPROF };
 constexpr int PC_INFO = 4 + PC_NPROF + 3;     // int64 words of the kernel's info record
 #ifdef CASIM_PROF
 #define PC_T0() uint64_t tp_ = clock64()
@@ -152,12 +153,16 @@ struct PcBlk {
 //     (stale-high: a scan that loads the block without a fit rebuilds it); a row that grows
 //     (the candidate's own RemovePods, a Revert) sets n = -1 (unknown: always loaded);
 //   * the candidate being simulated is excluded (its scans exclude it, and its row grew).
+// Stored point-major across blocks (c[i * nb + j]: point i of block j), so the window test —
+// lane q checks block q — reads every point with one conflict-free access per lane, all of
+// them issued at once.
 constexpr int PC_SKY = 8;
-struct PcSky {
-    int32_t n, pad;               // points stored (-1 = unknown)
-    int32_t c[PC_SKY], m[PC_SKY]; // cpu descending, memory ascending
+struct PcSkyV {
+    int32_t* n;                   // [nb] points stored (-1 = unknown)
+    int32_t* c;                   // [PC_SKY][nb] cpu, descending within a block
+    int32_t* m;                   // [PC_SKY][nb] memory (MiB, rounded up), ascending
+    int32_t nb;
 };
-static_assert(sizeof(PcSky) == 72, "PcSky");
 __host__ __device__ inline int32_t sky_c(int64_t v) {
     return v > INT32_MAX ? INT32_MAX : (v < INT32_MIN ? INT32_MIN : (int32_t)v);
 }
@@ -168,7 +173,7 @@ __host__ __device__ inline int32_t sky_m(int64_t v) {                 // ceil(v 
 
 // LDS image of one call (byte offsets; every array 16-B aligned)
 struct PcLayout {
-    size_t rc, rm, re, rp, exb, blk, sky, excnt, scratch, resbuf, mvbuf, ctx, help, total;
+    size_t rc, rm, re, rp, exb, blk, sky, excnt, scratch, resbuf, mvbuf, ctx, pdest, run, help, total;
 };
 
 __host__ __device__ inline PcLayout pc_layout(int32_t n, bool eph_cols) {
@@ -182,12 +187,14 @@ __host__ __device__ inline PcLayout pc_layout(int32_t n, bool eph_cols) {
     L.rp = take(4 * nn);
     L.exb = take(4 * (nn + 1));
     L.blk = take(sizeof(PcBlk) * nb);
-    L.sky = take(sizeof(PcSky) * nb);
+    L.sky = take(4 * nb * (1 + 2 * PC_SKY));
     L.excnt = take(2 * nn);
     L.scratch = take(4 * 64);
     L.resbuf = take(sizeof(ca_plan_result) * 64);       // results of the current 64 candidates
     L.mvbuf = take(sizeof(ca_plan_move) * PC_MVBUF);   // committed moves not yet written out
-    L.ctx = take(256);                                 // PcCtx
+    L.ctx = take(512);                                 // PcCtx
+    L.pdest = take(4 * PC_LIST);                       // destinations of a plain run's pods, by list index
+    L.run = take(128);                                 // PcRun
     L.help = take(256);                                // PcHelp (scan requests to the helper waves)
     L.total = o;
     return L;
@@ -201,6 +208,14 @@ __device__ inline PcRows pc_rows(unsigned char* pc_raw, const PcLayout& Y) {
     r.p = reinterpret_cast<int32_t*>(pc_raw + Y.rp);
     r.exb = reinterpret_cast<int32_t*>(pc_raw + Y.exb);
     return r;
+}
+__device__ inline PcSkyV pc_sky_view(unsigned char* pc_raw, const PcLayout& Y, int32_t nb) {
+    PcSkyV v;
+    v.n = reinterpret_cast<int32_t*>(pc_raw + Y.sky);
+    v.c = v.n + nb;
+    v.m = v.c + (size_t)PC_SKY * nb;
+    v.nb = nb;
+    return v;
 }
 
 extern "C" __device__ long long __ockl_wfred_add_i64(long long);
@@ -231,7 +246,7 @@ __device__ inline int64_t pc_uni64s(int64_t v) { return (int64_t)pc_uni64((uint6
 // largest (cpu, memory) key is a skyline point; every row with memory at most its memory is
 // dominated by it (its cpu is at most the point's); repeat on the rest.  C3 blocks hold
 // 4-5 points on average (p99 10), so a rebuild is a few wave reductions.
-__device__ void pc_sky_build(PcSky* sk, int64_t cc, int64_t cm, bool valid) {
+__device__ void pc_sky_build(const PcSkyV sk, int32_t j, int64_t cc, int64_t cm, bool valid) {
     const int lane = threadIdx.x & 63;
     const int32_t C = sky_c(cc), M = sky_m(cm);
     const int64_t key = ((int64_t)C << 32) | (int64_t)(uint32_t)(M ^ INT32_MIN);   // cpu, then memory
@@ -241,27 +256,31 @@ __device__ void pc_sky_build(PcSky* sk, int64_t cc, int64_t cm, bool valid) {
         if (!__ballot(alive)) break;
         const int64_t mx = __ockl_wfred_max_i64(alive ? key : INT64_MIN);
         const int32_t pm = (int32_t)((uint32_t)mx ^ (uint32_t)INT32_MIN);
-        if (lane == 0) { sk->c[k] = (int32_t)(mx >> 32); sk->m[k] = pm; }
+        if (lane == 0) { sk.c[k * sk.nb + j] = (int32_t)(mx >> 32); sk.m[k * sk.nb + j] = pm; }
         k++;
         alive = alive && M > pm;
     }
     if (k == PC_SKY - 1 && __ballot(alive)) {        // one point bounds the rest
         const int64_t mx = __ockl_wfred_max_i64(alive ? key : INT64_MIN);
         const int32_t mm = __ockl_wfred_max_i32(alive ? M : INT32_MIN);
-        if (lane == 0) { sk->c[k] = (int32_t)(mx >> 32); sk->m[k] = mm; }
+        if (lane == 0) { sk.c[k * sk.nb + j] = (int32_t)(mx >> 32); sk.m[k * sk.nb + j] = mm; }
         k++;
     }
-    if (lane == 0) sk->n = k;
+    if (lane == 0) sk.n[j] = k;
 }
 
 // May some row of the block fit a pod with these 32-bit images (sky_c / sky_m of its
 // requests; all_zero: only a visible row with a free slot is needed)?
-__device__ inline bool pc_sky_maybe(const PcSky& sk, int32_t pc, int32_t pm, bool all_zero) {
-    const int32_t k = sk.n;
+__device__ inline bool pc_sky_maybe(const PcSkyV sk, int32_t j, int32_t pc, int32_t pm, bool all_zero) {
+    const int32_t k = sk.n[j];
+    int32_t c[PC_SKY], m[PC_SKY];
+#pragma unroll
+    for (int i = 0; i < PC_SKY; i++) { c[i] = sk.c[i * sk.nb + j]; m[i] = sk.m[i * sk.nb + j]; }   // (all issued at once)
     if (k < 0) return true;
     if (all_zero) return k > 0;
     bool hit = false;
-    for (int32_t i = 0; i < k; i++) hit |= (pc <= sk.c[i]) & (pm <= sk.m[i]);
+#pragma unroll
+    for (int i = 0; i < PC_SKY; i++) hit |= (i < k) & (pc <= c[i]) & (pm <= m[i]);
     return hit;
 }
 
@@ -353,7 +372,7 @@ __device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) 
     int64_t* const re = R_.e;
     int32_t* const rp = R_.p;
     PcBlk* const blk = reinterpret_cast<PcBlk*>(pc_raw + Y.blk);
-    PcSky* const sky = reinterpret_cast<PcSky*>(pc_raw + Y.sky);
+    const PcSkyV sky = pc_sky_view(pc_raw, Y, (n + 63) >> 6);
     PcHelp* const q = reinterpret_cast<PcHelp*>(pc_raw + Y.help);
     int32_t seen = 0;
     for (;;) {
@@ -385,7 +404,7 @@ __device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) 
             const uint64_t cvis = pc_uni64(blk[j].vis);
             const uint64_t vw = cvis & inr & (j == jn ? ~nbit : ~0ull);
             if (!vw) continue;
-            if (!pc_sky_maybe(sky[j], pc32, pm32, all_zero)) continue;   // no row of the block can fit it
+            if (!pc_sky_maybe(sky, j, pc32, pm32, all_zero)) continue;   // no row of the block can fit it
             const int32_t x = j * 64 + lane;
             const bool in = x < n;
             const int64_t cc = in ? rc[x] : 0, cm = in ? rm[x] : 0;
@@ -408,7 +427,7 @@ __device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) 
             }
             const bool dj = j < 64 ? ((dirty0 >> j) & 1ull) : ((dirty1 >> (j - 64)) & 1ull);
             if (dj) {                                               // the exact skyline of the rows just read
-                pc_sky_build(&sky[j], cc, cm, ((cvis >> lane) & 1ull) && cp >= 1 && x != node);
+                pc_sky_build(sky, j, cc, cm, ((cvis >> lane) & 1ull) && cp >= 1 && x != node);
                 if (j < 64) refr0 |= 1ull << j; else refr1 |= 1ull << (j - 64);
             }
         }
@@ -420,15 +439,197 @@ __device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) 
     }
 }
 
+// A plain run's pod whose hint names a node it may not take (the candidate itself, or a
+// node outside podDestinations): findNodeWithHints still runs CheckPredicates on it
+// (hinting_simulator.go:91-108: one evaluation; its Hints.Set would store the same node)
+// and the pod goes on to the scan like an unhinted one.
+constexpr uint32_t PC_QF_HINT_EVAL = 0x80000000u;
+
+// Scalars a plain run (pc_plain_run) shares with the simulation, in LDS.
+struct PcRun {
+    int32_t Lw, adv, placed, failed;
+    int32_t node, moved, pad0, pad1;
+    uint64_t dirty0, dirty1, evals;
+    uint64_t prof[8];             // CASIM_PROF builds: PC_R_* (cycles by region, counts)
+};
+static_assert(sizeof(PcRun) <= 128, "PcRun");
+
+// A run of plain pods (no usable hint, no PreFilter names or failure, no NodeName or node
+// affinity) of one candidate, one pod after another: rotating first fit from lastIndex over
+// the committed rows (schedulerbased.go:114-131), the block skylines skipping blocks that
+// cannot fit the pod, AddPod of each placement (cluster.go:79).  Lane i holds pod t0 + i's
+// requests; destinations go to pdest[t0 + k] (LDS).  Out of line on purpose: the loop's
+// working set is small, and inside the simulation's register budget the scalar state it
+// needs was spilled to vector lanes around every step; one call per run pays the
+// save/restore once.  Stops at the first pod that fits nowhere (failed = 1) or after R pods.
+template <bool EPH_COLS>
+__device__ __attribute__((noinline)) void pc_plain_run(unsigned char* pc_raw, int32_t n_, int32_t t0_, int32_t R_,
+                                                       int64_t qc, int64_t qm, int64_t qe, uint32_t qf, int32_t qs,
+                                                       PcTabs tabs) {
+    const int lane = threadIdx.x & 63;
+    // (a device function's arguments arrive in vector registers as per-lane values: the
+    // uniform ones go back to scalars, else every loop and branch below is divergent)
+    const int32_t n = __builtin_amdgcn_readfirstlane(n_), t0 = __builtin_amdgcn_readfirstlane(t0_);
+    const int32_t R = __builtin_amdgcn_readfirstlane(R_);
+    const PcLayout Y = pc_layout(n, EPH_COLS);
+    const PcRows RW = pc_rows(pc_raw, Y);
+    int64_t* const rc = RW.c;
+    int64_t* const rm = RW.m;
+    int64_t* const re = RW.e;
+    int32_t* const rp = RW.p;
+    PcBlk* const blk = reinterpret_cast<PcBlk*>(pc_raw + Y.blk);
+    const PcSkyV sky = pc_sky_view(pc_raw, Y, (n + 63) >> 6);
+    int32_t* const pdest = reinterpret_cast<int32_t*>(pc_raw + Y.pdest);
+    PcRun* const rs = reinterpret_cast<PcRun*>(pc_raw + Y.run);
+    const int32_t nb = (n + 63) >> 6;
+    int32_t Lw = __builtin_amdgcn_readfirstlane(rs->Lw);
+    int32_t adv = __builtin_amdgcn_readfirstlane(rs->adv);
+    const int32_t node = __builtin_amdgcn_readfirstlane(rs->node);
+    uint64_t dirty0 = pc_uni64(rs->dirty0), dirty1 = pc_uni64(rs->dirty1);
+    const int32_t jn = node >> 6;
+    const uint64_t nbit = 1ull << (node & 63);
+    uint64_t evals = 0;
+    int32_t cj = -1;
+    int64_t cc = 0, cm = 0, ce = 0;
+    int32_t cp = 0;
+    uint64_t cvis = 0, cok = 0, ctaint = 0;
+    auto load_block = [&](int32_t j) {
+        const int32_t x = j * 64 + lane;
+        const bool in = x < n;
+        cc = in ? rc[x] : 0; cm = in ? rm[x] : 0; cp = in ? rp[x] : INT32_MIN;
+        ce = (EPH_COLS && in) ? re[x] : 0;
+        cvis = pc_uni64(blk[j].vis);
+        cok = EPH_COLS ? ~0ull : pc_uni64(blk[j].eph);
+        ctaint = pc_uni64(blk[j].taint);
+        cj = j;
+    };
+    int32_t k = 0, failed = 0;
+#ifdef CASIM_PROF
+    uint64_t rp_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t rt_ = clock64();
+#define PR_MARK(i) do { const uint64_t t_ = clock64(); rp_[i] += t_ - rt_; rt_ = t_; } while (0)
+#define PR_COUNT(i) (rp_[i]++)
+#else
+#define PR_MARK(i) do {} while (0)
+#define PR_COUNT(i) do {} while (0)
+#endif
+    for (; k < R; k++) {
+        PR_COUNT(5);
+        const int64_t pcpu = pc_rl64(qc, k), pmem = pc_rl64(qm, k);
+        const int64_t peph = EPH_COLS ? pc_rl64(qe, k) : 0;
+        const uint32_t pf = (uint32_t)pc_rl32((int32_t)qf, k);
+        const bool all_zero = (pf & PF_ALL_ZERO) != 0;
+        const bool taint_all = (pf & PF_TAINT_MASK_ALL) != 0;
+        if (pf & PC_QF_HINT_EVAL) evals += 1;        // the CheckPredicates of a hint it cannot take
+        const int32_t j0 = Lw >> 6, l0 = Lw & 63;
+        int32_t target = -1, wr = -1, my_nv = 0;
+        uint64_t passm = 0;
+        PR_MARK(0);
+        for (int32_t rr = 0; rr <= nb; rr++) {
+            if (rr == nb && l0 == 0) break;
+            int32_t j = j0 + rr;
+            if (j >= nb) j -= nb;
+            if (rr > 0 && rr < nb && j != cj) {
+                // 64 blocks at a time: a block passes when its skyline cannot fit the pod
+                if (wr < 0 || rr >= wr + 64) {
+                    const int32_t pc32 = sky_c(pcpu), pm32 = sky_m(pmem);   // (only scans that leave their block)
+                    const int32_t q = rr + lane;
+                    bool pass = false;
+                    my_nv = 0;
+                    if (q < nb) {
+                        int32_t jj = j0 + q;
+                        if (jj >= nb) jj -= nb;
+                        const uint64_t vw = blk[jj].vis & (jj == jn ? ~nbit : ~0ull);
+                        pass = !((vw != 0) && pc_sky_maybe(sky, jj, pc32, pm32, all_zero)) && jj != cj;
+                        my_nv = __popcll(vw);
+                    }
+                    passm = __ballot(pass);
+                    wr = rr;
+                    PR_COUNT(7);
+                }
+                const int32_t off = rr - wr;
+                const uint64_t stop = ~passm & (~0ull << off);
+                const int32_t kk = (stop ? __builtin_ctzll(stop) : 64) - off;
+                if (kk > 0) {
+                    evals += (uint64_t)__ockl_wfred_add_i32((lane >= off && lane < off + kk) ? my_nv : 0);
+                    rr += kk - 1;
+                    PR_MARK(1);
+                    continue;
+                }
+                PR_MARK(1);
+            }
+            if (j != cj) { load_block(j); PR_COUNT(6); }
+            const uint64_t inr = (rr == 0) ? (~0ull << l0) : (rr == nb ? ((1ull << l0) - 1) : ~0ull);
+            const uint64_t vism = cvis & inr & (j == jn ? ~nbit : ~0ull);
+            uint64_t fitm = vism & __ballot(cp >= 1);
+            if (!all_zero) {
+                fitm &= __ballot(pcpu <= cc) & __ballot(pmem <= cm);
+                fitm &= EPH_COLS ? __ballot(peph <= ce) : cok;
+            }
+            const uint64_t needm = taint_all ? 0ull : ctaint;
+            if (fitm & needm) {                              // TaintToleration where the node has taints
+                bool ok = true;
+                if (((fitm & needm) >> lane) & 1ull) ok = pc_static_fit(tabs, j * 64 + lane, pc_rl32(qs, k), pf);
+                fitm &= __ballot(ok);
+            }
+            if (fitm) {
+                const int f = __builtin_ctzll(fitm);
+                const uint64_t upto = (f == 63) ? ~0ull : ((2ull << f) - 1);
+                evals += (uint64_t)__popcll(vism & upto);
+                target = j * 64 + f;
+                PR_MARK(2);
+                break;
+            }
+            evals += (uint64_t)__popcll(vism);
+            PR_MARK(2);
+            // a block the skyline let through without a fit (a false positive): rebuild it.  Not
+            // the scan's first block — read regardless of its skyline, and usually the block of
+            // the previous placement: a rebuild there would buy nothing
+            const bool dj = rr > 0 && (j < 64 ? ((dirty0 >> j) & 1ull) : ((dirty1 >> (j - 64)) & 1ull));
+            if (dj) {
+                pc_sky_build(sky, j, cc, cm, ((cvis >> lane) & 1ull) && cp >= 1 && j * 64 + lane != node);
+                if (j < 64) dirty0 &= ~(1ull << j); else dirty1 &= ~(1ull << (j - 64));
+                PR_MARK(3);
+            }
+        }
+        if (target < 0) { failed = 1; break; }                                    // breakOnFailure
+        // ---- AddPod of the moved copy (:79): the row is the cached block's lane f ----
+        if (lane == (target & 63)) {
+            cc = wsub(cc, pcpu); cm = wsub(cm, pmem); cp -= 1;
+            rc[target] = cc; rm[target] = cm; rp[target] = cp;
+            if (EPH_COLS) { ce = wsub(ce, peph); re[target] = ce; }
+        }
+        const int32_t jt = target >> 6;
+        if (jt < 64) dirty0 |= 1ull << jt; else dirty1 |= 1ull << (jt - 64);
+        adv += (target >= Lw ? target - Lw : target + n - Lw) + 1;
+        Lw = target + 1 == n ? 0 : target + 1;                                   // schedulerbased.go:131
+        if (lane == 0) pdest[t0 + k] = target;
+        PR_MARK(4);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+        rs->Lw = Lw; rs->adv = adv; rs->dirty0 = dirty0; rs->dirty1 = dirty1; rs->evals = evals;
+        rs->placed = k; rs->failed = failed; rs->moved = k > 0 ? 1 : 0;
+#ifdef CASIM_PROF
+        for (int i = 0; i < 8; i++) rs->prof[i] = rp_[i];
+#endif
+    }
+#undef PR_MARK
+#undef PR_COUNT
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Per-call scalar state the candidate loop and the simulation share (LDS).
 struct PcCtx {
-    int32_t Lw, Lraw, nm, mv_n, mv_first, removed, pad0, pad1;
-    uint64_t dirty0, dirty1;              // blocks whose maxima may be stale-high
+    int32_t Lw, Lraw, nm, mv_n, mv_first, removed;
+    int32_t bulk_fail, bulk_skip;         // candidates whose first bulk step placed nothing; candidates to skip it
+    uint64_t dirty0, dirty1;              // blocks whose skylines may be stale-high
     ca_plan_result r;                     // the current candidate's result
 #ifdef CASIM_PROF
     uint64_t prof[PC_NPROF];
 #endif
 };
+static_assert(sizeof(PcCtx) <= 512, "PcCtx (pc_layout ctx)");
 
 __device__ inline void pc_flush_moves(const PcArgs& a, const ca_plan_move* mvbuf, PcCtx* ctx, int lane) {
     const int32_t k = __builtin_amdgcn_readfirstlane(ctx->mv_n), first = __builtin_amdgcn_readfirstlane(ctx->mv_first);
@@ -467,7 +668,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
     int64_t* const re = R_.e;
     int32_t* const rp = R_.p;
     PcBlk* const blk = reinterpret_cast<PcBlk*>(pc_raw + Y.blk);
-    PcSky* const sky = reinterpret_cast<PcSky*>(pc_raw + Y.sky);
+    const PcSkyV sky = pc_sky_view(pc_raw, Y, (n + 63) >> 6);
     uint16_t* const excnt = reinterpret_cast<uint16_t*>(pc_raw + Y.excnt);
     int32_t* const scratch = reinterpret_cast<int32_t*>(pc_raw + Y.scratch);
     ca_plan_move* const mvbuf = reinterpret_cast<ca_plan_move*>(pc_raw + Y.mvbuf);
@@ -518,7 +719,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             if (lane == 0) {
                 rc[node] = nc; rm[node] = nmm; rp[node] = np;
                 if (EPH_COLS) re[node] = ne2;
-                sky[jn].n = -1;             // a row that grows: the block's skyline is unknown
+                sky.n[jn] = -1;             // a row that grows: the block's skyline is unknown
             }
             if (jn == cj && lane == (node & 63)) { cc = nc; cm = nmm; ce = ne2; cp = np; }
             PC_MARK_DIRTY(jn);
@@ -528,7 +729,6 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
         int32_t placed = 0;
         int32_t d0 = -1, d1 = -1;                   // destinations of pods t = lane, 64 + lane
         int32_t hs0 = INT32_MIN, hs1 = INT32_MIN;   // Hints.Set of pods t = lane, 64 + lane
-        int32_t eb0 = 0, eb1 = 0;                   // ex_base of their destinations (loaded at AddPod)
         bool failed = false;
         // one pod (uniform values): hint check, then the rotating scan, then AddPod
         auto place = [&](const int32_t t, const int64_t pcpu, const int64_t pmem, const int64_t peph, const uint32_t pf,
@@ -604,7 +804,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                                 int32_t jj = j0 + q;
                                 if (jj >= nb) jj -= nb;
                                 const uint64_t vw = blk[jj].vis & (jj == jn ? ~nbit : ~0ull);
-                                const bool fitb = (vw != 0) && pc_sky_maybe(sky[jj], pc32, pm32, all_zero);
+                                const bool fitb = (vw != 0) && pc_sky_maybe(sky, jj, pc32, pm32, all_zero);
                                 pass = !fitb && jj != cj;
                                 my_nv = __popcll(vw);
                             }
@@ -700,10 +900,11 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                         break;
                     }
                     evals += (uint64_t)__popcll(vism);
-                    // the block passed: rebuild its skyline from the rows just read
-                    const bool dj = j < 64 ? ((dirty0 >> j) & 1ull) : ((dirty1 >> (j - 64)) & 1ull);
+                    // the block passed: rebuild its skyline from the rows just read (not the
+                    // scan's first block: read regardless of its skyline)
+                    const bool dj = rr > 0 && (j < 64 ? ((dirty0 >> j) & 1ull) : ((dirty1 >> (j - 64)) & 1ull));
                     if (dj) {
-                        pc_sky_build(&sky[j], cc, cm, ((cvis >> lane) & 1ull) && cp >= 1 && j * 64 + lane != node);
+                        pc_sky_build(sky, j, cc, cm, ((cvis >> lane) & 1ull) && cp >= 1 && j * 64 + lane != node);
                         if (j < 64) dirty0 &= ~(1ull << j); else dirty1 &= ~(1ull << (j - 64));
                         PC_SIM_MARK(PC_SKYB);
                     }
@@ -735,10 +936,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             }
             if ((target >> 6) == cj && lane == (target & 63)) { cc = nc; cm = nmm; ce = ne2; cp = np; }
             PC_MARK_DIRTY(target >> 6);
-            if (lane == tl) {
-                const int32_t eb = R_.exb[target];                                   // (used at Commit)
-                if (t >= 64) { d1 = target; eb1 = eb; } else { d0 = target; eb0 = eb; }
-            }
+            if (lane == tl) { if (t >= 64) d1 = target; else d0 = target; }
             PC_SIM_MARK(PC_ADD);
             return true;
         };
@@ -799,8 +997,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             const int32_t last = __builtin_amdgcn_readfirstlane(scratch[(tl0 + k - 1) & 63]);
             if (lane >= tl0 && lane < tl0 + k) {                                    // pods t0 .. t0+k-1
                 const int32_t v = scratch[lane];
-                const int32_t eb = R_.exb[v];                                        // (used at Commit)
-                if (hi) { d1 = v; hs1 = v; eb1 = eb; } else { d0 = v; hs0 = v; eb0 = eb; }   // :123 Set
+                if (hi) { d1 = v; hs1 = v; } else { d0 = v; hs0 = v; }                // :123 Set
             }
             __builtin_amdgcn_wave_barrier();
             PC_MARK_DIRTY(Lw >> 6);
@@ -812,18 +1009,92 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             cj = -1;                                                                 // rows changed
             return k;
         };
+        // plain pods of a half from t: the leading pods without a usable hint, PreFilter names or
+        // failure, NodeName or node affinity (lane i: pod t + i)
+        // (a hint to the candidate itself or to a node outside podDestinations cannot be taken:
+        // such a pod is plain but for the evaluation of the hint, PC_QF_HINT_EVAL)
+        auto hint_eval = [&](const int32_t hh) -> bool { return hh >= 0 && hh < n; };
+        auto hint_usable = [&](const int32_t hh) -> bool {
+            return hint_eval(hh) && hh != node && ((blk[hh >> 6].dest >> (hh & 63)) & 1ull);
+        };
+        auto plain_len = [&](const int32_t t0) -> int32_t {
+            const bool hi = t0 >= 64;
+            const int32_t hend = hi ? cnt : (cnt < 64 ? cnt : 64);
+            const int32_t src_i = ((t0 & 63) + lane) & 63;
+            const int32_t hh = __shfl(hi ? r1.hint : r0.hint, src_i, 64);
+            const uint32_t ff = (uint32_t)__shfl((int32_t)(hi ? r1.flags : r0.flags), src_i, 64);
+            const bool plain = t0 + lane < hend && !hint_usable(hh) &&
+                               !(ff & (PF_PREFILTER_FAIL | PF_PREFILTER_NAMES | PF_NODE_NAME | PF_AFFINITY));
+            const uint64_t pm = __ballot(plain);
+            return (~pm) ? __builtin_ctzll(~pm) : 64;
+        };
+        PcRun* const rs = reinterpret_cast<PcRun*>(pc_raw + Y.run);
+        int32_t* const pdest = reinterpret_cast<int32_t*>(pc_raw + Y.pdest);
         {
-            int32_t t = 0, cool = 0;
+            int32_t t = 0;
+            // the bulk step pays off in a loose cluster; in a tight one it keeps failing at the
+            // first pod: after 4 candidates in a row whose first bulk step placed nothing, the
+            // next 16 candidates start with the plain run
+            int32_t bfail = __builtin_amdgcn_readfirstlane(ctx->bulk_fail);
+            int32_t bskip = __builtin_amdgcn_readfirstlane(ctx->bulk_skip);
+            bool try_bulk = bskip == 0;
+            if (bskip > 0) bskip--;
+            bool first_bulk = true, bulk_hit = false;
             while (t < cnt && !failed) {
-                if (cool == 0 && n > 1) {
+                if (try_bulk && n > 1) {
                     const int32_t k = bulk(t);
                     PC_SIM_MARK(PC_BULK);
+                    if (first_bulk) {
+                        first_bulk = false;
+                        if (k > 0) bfail = 0;
+                        else if (++bfail >= 4) { bfail = 0; bskip = 16; }
+                    }
                     placed += k;
                     t += k;
-                    if (k > 0) continue;
-                    cool = 8;                                    // no plain run here: per pod for a while
+                    if (k > 0) { bulk_hit = true; continue; }
                 }
-                if (cool > 0) cool--;
+                try_bulk = false;
+                const int32_t R = plain_len(t);
+                if (R > 0) {
+                    // ---- a run of plain pods: the lean scan, out of line ----
+                    const bool hi = t >= 64;
+                    const int32_t src_i = ((t & 63) + lane) & 63;
+                    const int64_t qc = __shfl(hi ? r1.cpu : r0.cpu, src_i, 64);
+                    const int64_t qm = __shfl(hi ? r1.mem : r0.mem, src_i, 64);
+                    const int64_t qe = EPH_COLS ? __shfl(hi ? r1.eph : r0.eph, src_i, 64) : 0;
+                    const int32_t qh = __shfl(hi ? r1.hint : r0.hint, src_i, 64);
+                    const uint32_t qf = (uint32_t)__shfl((int32_t)(hi ? r1.flags : r0.flags), src_i, 64) |
+                                        (hint_eval(qh) ? PC_QF_HINT_EVAL : 0u);
+                    const int32_t qs = __shfl(hi ? r1.spec : r0.spec, src_i, 64);
+                    if (lane == 0) {
+                        rs->Lw = Lw; rs->adv = adv; rs->node = node; rs->dirty0 = dirty0; rs->dirty1 = dirty1;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    pc_plain_run<EPH_COLS>(pc_raw, n, t, R, qc, qm, qe, qf, qs, pc_tabs(a));
+                    Lw = __builtin_amdgcn_readfirstlane(rs->Lw);
+                    adv = __builtin_amdgcn_readfirstlane(rs->adv);
+                    dirty0 = pc_uni64(rs->dirty0);
+                    dirty1 = pc_uni64(rs->dirty1);
+                    evals += pc_uni64(rs->evals);
+                    const int32_t kp = __builtin_amdgcn_readfirstlane(rs->placed);
+                    const bool fl = __builtin_amdgcn_readfirstlane(rs->failed) != 0;
+#ifdef CASIM_PROF
+                    if (lane == 0) for (int i = 0; i < 8; i++) ctx->prof[PC_R_POD + i] += rs->prof[i];
+#endif
+                    if (kp > 0) moved_L = true;
+                    const int32_t tl0 = t & 63;
+                    if (lane >= tl0 && lane < tl0 + kp) {                         // :123 Set
+                        const int32_t v = pdest[(hi ? 64 : 0) + lane];
+                        if (hi) { d1 = v; hs1 = v; } else { d0 = v; hs0 = v; }
+                    }
+                    cj = -1;                                                      // rows changed
+                    placed += kp;
+                    t += kp;
+                    PC_SIM_MARK(PC_SCAN);
+                    if (fl) { failed = true; break; }
+                    try_bulk = bulk_hit;
+                    continue;
+                }
                 bool ok;
                 if (t < 64)
                     ok = place(t, pc_rl64(r0.cpu, t), pc_rl64(r0.mem, t), EPH_COLS ? pc_rl64(r0.eph, t) : 0,
@@ -835,7 +1106,9 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                 if (!ok) { failed = true; break; }
                 placed++;
                 t++;
+                try_bulk = bulk_hit;
             }
+            if (lane == 0) { ctx->bulk_fail = bfail; ctx->bulk_skip = bskip; }
         }
         r.n_placed = placed;
         r.evals = evals;
@@ -852,7 +1125,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                 const bool act = t < cnt;
                 const PcReg& q = half ? r1 : r0;
                 const int32_t f = half ? d1 : d0;
-                const int32_t fb = half ? eb1 : eb0;
+                const int32_t fb = act ? R_.exb[f] : 0;                              // the copies' slots of node f
                 const int32_t s = nm + t;
                 if (act) {
                     ca_plan_move mv;
@@ -938,7 +1211,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                 const int32_t t = half * 64 + lane;
                 if (t >= placed) continue;
                 const int32_t f = half ? d1 : d0, j = f >> 6;
-                sky[j].n = -1;
+                sky.n[j] = -1;
                 atomicOr(reinterpret_cast<unsigned long long*>(dmask + (j >> 6)), 1ull << (j & 63));
             }
             __builtin_amdgcn_wave_barrier();
@@ -947,7 +1220,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
             if (lane == 0) {
                 rc[node] = wsub(rc[node], sc); rm[node] = wsub(rm[node], sm); rp[node] -= cnt;
                 if (EPH_COLS) re[node] = wsub(re[node], se);
-                sky[jn].n = -1;             // (built without this candidate while it ran)
+                sky.n[jn] = -1;             // (built without this candidate while it ran)
             }
             PC_MARK_DIRTY(jn);
             cj = -1;                                                                 // rows changed
@@ -1018,7 +1291,7 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
                 if (lane == 0) {
                     blk[j].dest = dw; blk[j].vis = dw & ~uw; blk[j].usch = uw; blk[j].taint = tw;
                     if (!EPH_COLS) blk[j].eph = ew;
-                    reinterpret_cast<PcSky*>(pc_raw + Y.sky)[j].n = -1;     // unknown until a scan reads it
+                    reinterpret_cast<int32_t*>(pc_raw + Y.sky)[j] = -1;      // unknown until a scan reads it
                 }
             }
         }
@@ -1063,7 +1336,7 @@ __global__ void __launch_bounds__(PC_MAX_WAVES * 64) k_plan_chain(PcArgs a) {
         if (n > 0) { Lw = (int32_t)(a.L0 % n); if (Lw < 0) Lw += n; }
         ctx->Lw = Lw;
         ctx->Lraw = (int32_t)a.L0;                    // Go keeps the int until a scan succeeds
-        ctx->nm = 0; ctx->mv_n = 0; ctx->mv_first = 0; ctx->removed = 0;
+        ctx->nm = 0; ctx->mv_n = 0; ctx->mv_first = 0; ctx->removed = 0; ctx->bulk_fail = 0; ctx->bulk_skip = 0;
         ctx->dirty0 = ~0ull; ctx->dirty1 = ~0ull;
 #ifdef CASIM_PROF
         for (int k = 0; k < PC_NPROF; k++) ctx->prof[k] = 0;

@@ -25,10 +25,11 @@ def load(root: str, counter: str) -> dict:
     return out
 
 
-def main(root: str, steps: int, what: str = "scripts/pmc_step.py PMC_LEGS=all (C2 Estimate headline steps: 16-bit ids "
-                                           "published into page-locked memory, decoupled Go order; C5 "
-                                           "FilterOutSchedulable calls; fresh C3 sweeps; C3 planner loops "
-                                           "without a limit)") -> None:
+def main(root: str, steps: int, what: str = "scripts/pmc_step.py PMC_LEGS=all (C2 Estimate headline steps, "
+                                           "decoupled Go order, results left in HBM (PMC_MODE=device: under "
+                                           "--pmc the kernels are serialised, so the zero-copy publisher of "
+                                           "the timed step could not run); C5 FilterOutSchedulable calls; "
+                                           "fresh C3 sweeps; C3 planner loops without a limit)") -> None:
     fetch = load(root, "FETCH_SIZE")
     write = load(root, "WRITE_SIZE")
     res = {}

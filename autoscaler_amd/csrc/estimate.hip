@@ -39,6 +39,7 @@
 #include <functional>
 #include <chrono>
 #include <mutex>
+#include <thread>
 #include <cstdlib>
 
 namespace casim {
@@ -153,6 +154,12 @@ __device__ inline uint32_t static_sf(const PodHot& p, const ca_template& tp, boo
     if (p.flags & PF_PORTS) sf |= SF_PORTS;
     if (p.flags & (PF_HOSTNAME_DEP | PF_OUT_OF_SCOPE)) sf |= SF_UNSUP;
     return sf;
+}
+
+// the score class of every (group, pod) item, gathered from the podset's class column
+__global__ void __launch_bounds__(256) k_item_cls(const int32_t* __restrict__ pod_idx, const int32_t* __restrict__ cls,
+                                                 int32_t* __restrict__ out, int32_t n) {
+    for (int32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) out[i] = cls[pod_idx[i]];
 }
 
 // 1. score + static predicates + tile sort ----------------------------------
@@ -2643,37 +2650,86 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
         for (int i = 0; i < CA_MAX_SCALAR; i++)
             if (t.node.alloc_scalar[i] || t.used_scalar[i]) p->use_scalar = true;
     }
-    // (per-pod summaries of the podset: compact arrays instead of the 208-B records)
-    for (int32_t i = 0; i < p->total; i++) {
-        const int32_t pi = pod_idx[i];
-        if (pi < 0 || pi >= s->t.n_pods) return CA_EINVAL;
-    }
-    if (s->any_ports || s->any_scalar)
-        for (int32_t i = 0; i < p->total; i++) {
-            const uint8_t f = s->h_pflags[pod_idx[i]];
-            if (f & 1) p->use_ports = true;
-            if (f & 2) p->use_scalar = true;
-        }
-    p->decouple_ok = p->bucket && s->cls_uniform && groups_tie_free(s, pod_idx, p->h_meta, templates);
-    p->demand.assign(G, 0.0);
-    for (int32_t g = 0; g < G; g++) {
-        const GroupMeta& gm = p->h_meta[g];
-        double c = 0, mm = 0;
-        for (int32_t i = gm.off; i < gm.off + gm.count; i++) {
-            const int64_t* rq = &s->h_req[2 * (size_t)pod_idx[i]];
-            c += (double)rq[0];
-            mm += (double)rq[1];
-        }
-        double d = gm.tpods > 0 ? (double)gm.count / gm.tpods : 0.0;
-        if (gm.tcpu > 0) d = std::max(d, c / (double)gm.tcpu);
-        if (gm.tmem > 0) d = std::max(d, mm / (double)gm.tmem);
-        p->demand[g] = d;
-    }
     hipStream_t st = m->stream;
     int rc;
     const size_t tot = (size_t)std::max(p->total, 1);
+    // One pass over the lists (per-pod summaries of the podset: compact arrays instead of
+    // the 208-B records), split over host threads for big batches: index validation, the
+    // port / extended-resource flags and each group's summed requests for the demand
+    // order.  The lists travel to the device meanwhile (the main thread drives the copy);
+    // the item classes are gathered there from the podset's class column (k_item_cls).
+    {
+        const int32_t total = p->total;
+        const int32_t T = std::max(1, std::min(8, total / (1 << 17)));
+        struct Part { bool bad = false; uint8_t fl = 0; std::vector<double> c, mm; };
+        std::vector<Part> part((size_t)T);
+        const bool want_fl = s->any_ports || s->any_scalar;
+        auto work = [&](int32_t t) {
+            Part& pt = part[(size_t)t];
+            pt.c.assign((size_t)G, 0.0);
+            pt.mm.assign((size_t)G, 0.0);
+            const int32_t a = (int32_t)((int64_t)total * t / T), b = (int32_t)((int64_t)total * (t + 1) / T);
+            int32_t g = (int32_t)(std::upper_bound(group_off, group_off + G + 1, a) - group_off) - 1;
+            const int32_t np_ = s->t.n_pods;
+            const int64_t* req = s->h_req.data();
+            for (int32_t i = a; i < b && !pt.bad;) {
+                while (g < G - 1 && group_off[g + 1] <= i) g++;
+                const int32_t e = std::min(b, group_off[g + 1]);
+                double c0 = 0, c1 = 0, m0 = 0, m1 = 0;   // (two chains each: the adds pipeline)
+                bool bad = false;
+                int32_t k = i;
+                for (; k + 1 < e; k += 2) {
+                    const int32_t p0 = pod_idx[k], p1 = pod_idx[k + 1];
+                    bad |= (uint32_t)p0 >= (uint32_t)np_ || (uint32_t)p1 >= (uint32_t)np_;
+                    if (bad) break;
+                    c0 += (double)req[2 * (size_t)p0]; m0 += (double)req[2 * (size_t)p0 + 1];
+                    c1 += (double)req[2 * (size_t)p1]; m1 += (double)req[2 * (size_t)p1 + 1];
+                }
+                if (!bad && k < e) {
+                    const int32_t p0 = pod_idx[k];
+                    bad = (uint32_t)p0 >= (uint32_t)np_;
+                    if (!bad) { c0 += (double)req[2 * (size_t)p0]; m0 += (double)req[2 * (size_t)p0 + 1]; }
+                }
+                if (bad) { pt.bad = true; break; }
+                if (want_fl)
+                    for (int32_t q = i; q < e; q++) pt.fl |= s->h_pflags[pod_idx[q]];
+                pt.c[(size_t)g] += c0 + c1;
+                pt.mm[(size_t)g] += m0 + m1;
+                i = e;
+            }
+        };
+        std::vector<std::thread> th;
+        for (int32_t t = 1; t < T; t++) th.emplace_back(work, t);
+        hipError_t ce = hipSuccess;
+        if ((rc = p->d_pod_idx.reserve(sizeof(int32_t) * tot)) == CA_OK && total)
+            ce = hipMemcpyAsync(p->d_pod_idx.ptr, pod_idx, sizeof(int32_t) * total, hipMemcpyHostToDevice, st);
+        work(0);
+        for (auto& x : th) x.join();
+        if (rc != CA_OK) return rc;
+        CA_HIP_CHECK(ce);
+        bool bad = false;
+        p->demand.assign(G, 0.0);
+        std::vector<double> c((size_t)G, 0.0), mm((size_t)G, 0.0);
+        for (const Part& pt : part) {
+            bad |= pt.bad;
+            if (pt.fl & 1) p->use_ports = true;
+            if (pt.fl & 2) p->use_scalar = true;
+            for (int32_t g = 0; g < G; g++) { c[(size_t)g] += pt.c[(size_t)g]; mm[(size_t)g] += pt.mm[(size_t)g]; }
+        }
+        if (bad) {
+            CA_HIP_CHECK(hipStreamSynchronize(st));    // (the list copy may still read pod_idx)
+            return CA_EINVAL;
+        }
+        for (int32_t g = 0; g < G; g++) {
+            const GroupMeta& gm = p->h_meta[g];
+            double d = gm.tpods > 0 ? (double)gm.count / gm.tpods : 0.0;
+            if (gm.tcpu > 0) d = std::max(d, c[(size_t)g] / (double)gm.tcpu);
+            if (gm.tmem > 0) d = std::max(d, mm[(size_t)g] / (double)gm.tmem);
+            p->demand[g] = d;
+        }
+    }
+    p->decouple_ok = p->bucket && s->cls_uniform && groups_tie_free(s, pod_idx, p->h_meta, templates);
     if ((rc = p->d_meta.reserve(sizeof(GroupMeta) * (size_t)std::max(G, 1))) != CA_OK) return rc;
-    if ((rc = p->d_pod_idx.reserve(sizeof(int32_t) * tot)) != CA_OK) return rc;
     if ((rc = p->d_tmpl.reserve(sizeof(ca_template) * (size_t)std::max(G, 1))) != CA_OK) return rc;
     if ((rc = p->d_sortA.reserve(sizeof(SortItem) * tot)) != CA_OK) return rc;
     if ((rc = p->d_sortB.reserve(sizeof(SortItem) * tot)) != CA_OK) return rc;
@@ -2725,15 +2781,14 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
             return rc;
     }
     if (G) CA_HIP_CHECK(hipMemcpyAsync(p->d_meta.ptr, p->h_meta.data(), sizeof(GroupMeta) * G, hipMemcpyHostToDevice, st));
-    if (p->total) CA_HIP_CHECK(hipMemcpyAsync(p->d_pod_idx.ptr, pod_idx, sizeof(int32_t) * p->total, hipMemcpyHostToDevice, st));
-    std::vector<int32_t> item_cls;
     if (p->bucket && p->total > 0) {
         // the lists as (pod, class) pairs: the class of every item next to its pod index, so
         // the sorts and the run table read it in one coalesced load instead of two gathers
-        item_cls.resize((size_t)p->total);
-        for (int32_t i = 0; i < p->total; i++) item_cls[i] = s->h_cls[pod_idx[i]];
         if ((rc = p->d_item_cls.reserve(sizeof(int32_t) * (size_t)p->total)) != CA_OK) return rc;
-        CA_HIP_CHECK(hipMemcpyAsync(p->d_item_cls.ptr, item_cls.data(), sizeof(int32_t) * p->total, hipMemcpyHostToDevice, st));
+        const int32_t nb = (int32_t)std::min<int64_t>(4096, (p->total + 255) / 256);
+        hipLaunchKernelGGL(k_item_cls, dim3(nb), dim3(256), 0, st, p->d_pod_idx.as<int32_t>(),
+                           s->d_cls.as<int32_t>(), p->d_item_cls.as<int32_t>(), p->total);
+        CA_HIP_CHECK(hipGetLastError());
     }
     if (G) CA_HIP_CHECK(hipMemcpyAsync(p->d_tmpl.ptr, templates, sizeof(ca_template) * G, hipMemcpyHostToDevice, st));
     CA_HIP_CHECK(hipStreamSynchronize(st));

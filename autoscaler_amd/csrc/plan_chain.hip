@@ -41,7 +41,8 @@ constexpr int PC_MAX_WAVES = 8;               // the chain wave + up to 7 helper
 // shader-clock counters of the chain's phases (info[4 + k]; CASIM_PROF builds only)
 enum { PC_INIT, PC_LISTS, PC_PDB, PC_FORK, PC_HINT, PC_SCAN, PC_ADD, PC_COMMIT, PC_REVERT, PC_TOTAL, PC_BLOCKS,
        PC_WINDOWS, PC_HANDOFFS, PC_BULK, PC_PREP, PC_WIN, PC_LOADCHK, PC_SKYB,
-       PC_R_POD, PC_R_WIN, PC_R_BLK, PC_R_SKY, PC_R_ADD, PC_R_NPODS, PC_R_NBLK, PC_R_NWIN, PC_NPROF };
+       PC_R_POD, PC_R_WIN, PC_R_BLK, PC_R_SKY, PC_R_ADD, PC_R_NPODS, PC_R_NBLK, PC_R_NWIN, PC_R_NSKY, PC_R_NRUNS,
+       PC_NPROF };
 constexpr int PC_INFO = 4 + PC_NPROF + 3;     // int64 words of the kernel's info record
 #ifdef CASIM_PROF
 #define PC_T0() uint64_t tp_ = clock64()
@@ -493,14 +494,31 @@ __device__ __attribute__((noinline)) void pc_plain_run(unsigned char* pc_raw, in
     int64_t cc = 0, cm = 0, ce = 0;
     int32_t cp = 0;
     uint64_t cvis = 0, cok = 0, ctaint = 0;
+    uint64_t cd0 = 0, cd1 = 0;            // the cached block's dirty bit
+    bool cmod = false;                    // its rows in registers differ from LDS
+    // AddPods change the cached block's rows in registers only; they go back to LDS when
+    // another block is loaded and when the run ends (nothing else reads them meanwhile)
+    auto flush = [&]() {
+        if (cmod) {
+            const int32_t x = cj * 64 + lane;
+            if (x < n) {
+                rc[x] = cc; rm[x] = cm; rp[x] = cp;
+                if (EPH_COLS) re[x] = ce;
+            }
+            cmod = false;
+        }
+    };
     auto load_block = [&](int32_t j) {
+        flush();
         const int32_t x = j * 64 + lane;
         const bool in = x < n;
         cc = in ? rc[x] : 0; cm = in ? rm[x] : 0; cp = in ? rp[x] : INT32_MIN;
         ce = (EPH_COLS && in) ? re[x] : 0;
-        cvis = pc_uni64(blk[j].vis);
+        cvis = pc_uni64(blk[j].vis) & (j == jn ? ~nbit : ~0ull);   // (the candidate is never a destination)
         cok = EPH_COLS ? ~0ull : pc_uni64(blk[j].eph);
         ctaint = pc_uni64(blk[j].taint);
+        cd0 = j < 64 ? 1ull << j : 0ull;
+        cd1 = j < 64 ? 0ull : 1ull << (j - 64);
         cj = j;
     };
     int32_t k = 0, failed = 0;
@@ -509,7 +527,10 @@ __device__ __attribute__((noinline)) void pc_plain_run(unsigned char* pc_raw, in
     uint64_t rt_ = clock64();
 #define PR_MARK(i) do { const uint64_t t_ = clock64(); rp_[i] += t_ - rt_; rt_ = t_; } while (0)
 #define PR_COUNT(i) (rp_[i]++)
+#define PR_NSKY() (nsky_++)
+    int32_t nsky_ = 0;
 #else
+#define PR_NSKY() do {} while (0)
 #define PR_MARK(i) do {} while (0)
 #define PR_COUNT(i) do {} while (0)
 #endif
@@ -522,6 +543,77 @@ __device__ __attribute__((noinline)) void pc_plain_run(unsigned char* pc_raw, in
         const bool taint_all = (pf & PF_TAINT_MASK_ALL) != 0;
         if (pf & PC_QF_HINT_EVAL) evals += 1;        // the CheckPredicates of a hint it cannot take
         const int32_t j0 = Lw >> 6, l0 = Lw & 63;
+        // Fast path: a batch of pods whose first fits lie in the cached block (the block of the
+        // previous placement), each past the previous one's.  Within the batch every pod's scan
+        // starts past the rows the batch has taken (lastIndex = target + 1), so its fit test
+        // reads rows as they were when the batch began: the tests need no dependent updates,
+        // and the batch's AddPods, evaluations and lastIndex advance are applied once at its end.
+        if (j0 == cj && !all_zero) {
+            uint64_t P = 0;                       // rows the batch took (one pod each, ascending)
+            int32_t l = l0, kk = k, nhint = 0;
+            // (all uniform; said so, else the compiler keeps the loop state in vector lanes)
+            const uint64_t vis_ = pc_uni64(cvis), ok_ = pc_uni64(cok), taint_ = pc_uni64(ctaint);
+            const uint64_t free_ = vis_ & __ballot(cp >= 1) & (EPH_COLS ? ~0ull : ok_);
+            bool go = true;
+            while (go) {
+                l = __builtin_amdgcn_readfirstlane(l);
+                kk = __builtin_amdgcn_readfirstlane(kk);
+                P = pc_uni64(P);
+                // the fit masks of the next 4 pods first (independent of each other: their
+                // loads and compares overlap), then the dependent first-fit chain over them
+                uint64_t F[4];
+                uint32_t FL[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int32_t kq = kk + q < R ? kk + q : R - 1;
+                    FL[q] = (uint32_t)pc_rl32((int32_t)qf, kq);
+                    const int64_t c_ = pc_rl64(qc, kq), m_ = pc_rl64(qm, kq);
+                    uint64_t f_ = free_ & __ballot(c_ <= cc) & __ballot(m_ <= cm);
+                    if (EPH_COLS) f_ &= __ballot(pc_rl64(qe, kq) <= ce);
+                    F[q] = pc_uni64(f_);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)FL[q]);
+                    if (bf & PF_ALL_ZERO) { go = false; break; }                  // (pod k: not all_zero)
+                    const uint64_t fitm = F[q] & (~0ull << l);
+                    const uint64_t first = fitm & (0ull - fitm);
+                    if (!first || (first & ((bf & PF_TAINT_MASK_ALL) ? 0ull : taint_))) { go = false; break; }
+                    P |= first;
+                    if (kk > k && (bf & PC_QF_HINT_EVAL)) nhint++;               // (pod k's was counted above)
+                    l = __builtin_ctzll(first) + 1;
+                    if (++kk == R || l == 64) { go = false; break; }
+                }
+            }
+            if (P) {
+                const bool inP = (P >> lane) & 1ull;
+                const int32_t src = k + __popcll(P & pc_below(lane));    // the pod that took this row
+                const int32_t sa = (src & 63) * 4;
+                const int64_t sc = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int32_t)(qc >> 32)) << 32) |
+                                             (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int32_t)qc));
+                const int64_t sm = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int32_t)(qm >> 32)) << 32) |
+                                             (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int32_t)qm));
+                cc = inP ? wsub(cc, sc) : cc;
+                cm = inP ? wsub(cm, sm) : cm;
+                cp = inP ? cp - 1 : cp;
+                if (EPH_COLS) {
+                    const int64_t se = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int32_t)(qe >> 32)) << 32) |
+                                                 (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int32_t)qe));
+                    ce = inP ? wsub(ce, se) : ce;
+                }
+                if (inP) pdest[t0 + src] = cj * 64 + lane;
+                cmod = true;
+                dirty0 |= cd0; dirty1 |= cd1;
+                const int32_t tl = 63 - __builtin_clzll(P);              // the last pod's row
+                evals += (uint64_t)__popcll(cvis & (~0ull << l0) & (tl == 63 ? ~0ull : ((2ull << tl) - 1))) + nhint;
+                const int32_t nx = cj * 64 + tl + 1;
+                adv += nx - Lw;
+                Lw = nx == n ? 0 : nx;
+                k = kk - 1;
+                PR_MARK(4);
+                continue;
+            }
+        }
         int32_t target = -1, wr = -1, my_nv = 0;
         uint64_t passm = 0;
         PR_MARK(0);
@@ -560,7 +652,7 @@ __device__ __attribute__((noinline)) void pc_plain_run(unsigned char* pc_raw, in
             }
             if (j != cj) { load_block(j); PR_COUNT(6); }
             const uint64_t inr = (rr == 0) ? (~0ull << l0) : (rr == nb ? ((1ull << l0) - 1) : ~0ull);
-            const uint64_t vism = cvis & inr & (j == jn ? ~nbit : ~0ull);
+            const uint64_t vism = cvis & inr;
             uint64_t fitm = vism & __ballot(cp >= 1);
             if (!all_zero) {
                 fitm &= __ballot(pcpu <= cc) & __ballot(pmem <= cm);
@@ -589,33 +681,39 @@ __device__ __attribute__((noinline)) void pc_plain_run(unsigned char* pc_raw, in
             if (dj) {
                 pc_sky_build(sky, j, cc, cm, ((cvis >> lane) & 1ull) && cp >= 1 && j * 64 + lane != node);
                 if (j < 64) dirty0 &= ~(1ull << j); else dirty1 &= ~(1ull << (j - 64));
+                PR_NSKY();
                 PR_MARK(3);
             }
         }
         if (target < 0) { failed = 1; break; }                                    // breakOnFailure
         // ---- AddPod of the moved copy (:79): the row is the cached block's lane f ----
-        if (lane == (target & 63)) {
-            cc = wsub(cc, pcpu); cm = wsub(cm, pmem); cp -= 1;
-            rc[target] = cc; rm[target] = cm; rp[target] = cp;
-            if (EPH_COLS) { ce = wsub(ce, peph); re[target] = ce; }
+        {
+            const bool me = lane == (target & 63);
+            cc = me ? wsub(cc, pcpu) : cc;
+            cm = me ? wsub(cm, pmem) : cm;
+            cp = me ? cp - 1 : cp;
+            if (EPH_COLS) ce = me ? wsub(ce, peph) : ce;
+            cmod = true;
         }
-        const int32_t jt = target >> 6;
-        if (jt < 64) dirty0 |= 1ull << jt; else dirty1 |= 1ull << (jt - 64);
+        dirty0 |= cd0; dirty1 |= cd1;                                            // (target's block is cj)
         adv += (target >= Lw ? target - Lw : target + n - Lw) + 1;
         Lw = target + 1 == n ? 0 : target + 1;                                   // schedulerbased.go:131
         if (lane == 0) pdest[t0 + k] = target;
         PR_MARK(4);
     }
+    flush();
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
         rs->Lw = Lw; rs->adv = adv; rs->dirty0 = dirty0; rs->dirty1 = dirty1; rs->evals = evals;
         rs->placed = k; rs->failed = failed; rs->moved = k > 0 ? 1 : 0;
 #ifdef CASIM_PROF
         for (int i = 0; i < 8; i++) rs->prof[i] = rp_[i];
+        rs->pad0 = nsky_;
 #endif
     }
 #undef PR_MARK
 #undef PR_COUNT
+#undef PR_NSKY
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -1079,7 +1177,11 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                     const int32_t kp = __builtin_amdgcn_readfirstlane(rs->placed);
                     const bool fl = __builtin_amdgcn_readfirstlane(rs->failed) != 0;
 #ifdef CASIM_PROF
-                    if (lane == 0) for (int i = 0; i < 8; i++) ctx->prof[PC_R_POD + i] += rs->prof[i];
+                    if (lane == 0) {
+                        for (int i = 0; i < 8; i++) ctx->prof[PC_R_POD + i] += rs->prof[i];
+                        ctx->prof[PC_R_NSKY] += (uint64_t)rs->pad0;
+                        ctx->prof[PC_R_NRUNS] += 1;
+                    }
 #endif
                     if (kp > 0) moved_L = true;
                     const int32_t tl0 = t & 63;

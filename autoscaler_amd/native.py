@@ -523,7 +523,7 @@ class Mirror:
         k = self.lib.ca_plan_chain_profile(self.h, cyc.ctypes.data, 32, hm.ctypes.data)
         names = ["init", "lists", "pdb", "fork", "hint", "scan", "add", "commit", "revert", "total", "blocks",
                  "windows", "handoffs", "bulk", "prep", "win", "loadchk", "skyb", "r_pod", "r_win", "r_blk", "r_sky",
-                 "r_add", "r_npods", "r_nblk", "r_nwin"]
+                 "r_add", "r_npods", "r_nblk", "r_nwin", "r_nsky", "r_nruns"]
         out = {nm: int(v) for nm, v in zip(names, cyc[:max(k, 0)])}
         out.update({h: float(v) for h, v in zip(["sync_ms", "launch_kernel_ms", "kernel_ms", "readback_ms",
                                                    "replay_ms"], hm)})

@@ -44,7 +44,7 @@ for limit in (20, 200, 0):
     print(f"   blocks scanned {pr['blocks']}  skip windows {pr['windows']}  helper hand-offs {pr.get('handoffs', 0)}",
           flush=True)
     if pr.get("r_npods"):
-        print("   plain runs: pods {r_npods} blocks {r_nblk} windows {r_nwin}; cycles/pod: pod {a:.0f} win {b:.0f} blk {c:.0f} "
+        print("   plain runs: {r_nruns} runs, pods {r_npods} blocks {r_nblk} windows {r_nwin} sky rebuilds {r_nsky}; cycles/pod: pod {a:.0f} win {b:.0f} blk {c:.0f} "
               "sky {d:.0f} add {e:.0f}".format(a=pr["r_pod"] / pr["r_npods"], b=pr["r_win"] / pr["r_npods"],
                                               c=pr["r_blk"] / pr["r_npods"], d=pr["r_sky"] / pr["r_npods"],
                                               e=pr["r_add"] / pr["r_npods"], **pr), flush=True)

@@ -1347,20 +1347,12 @@ int ca_fits_matrix(ca_mirror* m, const ca_podset* s, uint8_t* out) {
     return CA_OK;
 }
 
-int ca_check_templates(ca_mirror* m, const ca_podset* s, const int32_t* samples, int32_t n_samples,
-                       const ca_template* templates, int32_t n_templates, ca_pred_result* out, uint8_t* out_ok) {
-    if (!m || !s || n_samples < 0 || n_templates < 0) return CA_EINVAL;
-    if (n_samples == 0 || n_templates == 0) return CA_OK;
-    if (!samples || !templates || (!out && !out_ok)) return CA_EINVAL;
-    for (int32_t e = 0; e < n_samples; e++)
-        if (samples[e] < 0 || samples[e] >= s->t.n_pods) return CA_EINVAL;
-    if (m->n_scope_blockers > 0) return CA_EUNSUPPORTED;
-    CA_HIP_CHECK(hipSetDevice(m->device));
-    // the test node: the template with its pods (NodeInfo of a fresh template copy)
-    std::vector<NodeHot> h(n_templates);
-    std::vector<NodeExt> x(n_templates);
-    std::vector<NodeStatic> st(n_templates);
-    for (int32_t g = 0; g < n_templates; g++) {
+}  // extern "C"
+
+namespace {
+// The test node of a node group (NodeInfo of a fresh template copy: the template with its pods)
+void template_test_rows(const ca_template* templates, int32_t G, NodeHot* h, NodeExt* x, NodeStatic* st) {
+    for (int32_t g = 0; g < G; g++) {
         const ca_template& tp = templates[g];
         const ca_node_spec& n = tp.node;
         h[g].cpu = wsub(n.alloc_milli_cpu, tp.used_milli_cpu);
@@ -1388,11 +1380,45 @@ int ca_check_templates(ca_mirror* m, const ca_podset* s, const int32_t* samples,
         st[g].int_valid = n.int_label_valid;
         st[g].name_id = n.name_id;
     }
+}
+
+int check_samples(const ca_mirror* m, const ca_podset* s, const int32_t* samples, int32_t n_samples) {
+    for (int32_t e = 0; e < n_samples; e++)
+        if (samples[e] < 0 || samples[e] >= s->t.n_pods) return CA_EINVAL;
+    if (m->n_scope_blockers > 0) return CA_EUNSUPPORTED;
+    return CA_OK;
+}
+}  // namespace
+
+// Node groups resident for ComputeExpansionOption checks (ca_expansion_plan_*): the
+// templates' test-node rows stay in HBM; a run passes samples and results through
+// page-locked memory the kernel reads and writes in place.
+struct ca_expansion_plan {
+    ca_mirror* m = nullptr;
+    int32_t G = 0;
+    casim::DevBuf rows;        // NodeHot[G] | NodeExt[G] | NodeStatic[G]
+    casim::HostBuf io;         // page-locked: samples | results | verdicts
+    float kernel_ms = 0;       // the last run's kernel (events)
+};
+
+extern "C" {
+
+int ca_check_templates(ca_mirror* m, const ca_podset* s, const int32_t* samples, int32_t n_samples,
+                       const ca_template* templates, int32_t n_templates, ca_pred_result* out, uint8_t* out_ok) {
+    if (!m || !s || n_samples < 0 || n_templates < 0) return CA_EINVAL;
+    if (n_samples == 0 || n_templates == 0) return CA_OK;
+    if (!samples || !templates || (!out && !out_ok)) return CA_EINVAL;
+    int rc;
+    if ((rc = check_samples(m, s, samples, n_samples)) != CA_OK) return rc;
+    CA_HIP_CHECK(hipSetDevice(m->device));
+    std::vector<NodeHot> h(n_templates);
+    std::vector<NodeExt> x(n_templates);
+    std::vector<NodeStatic> st(n_templates);
+    template_test_rows(templates, n_templates, h.data(), x.data(), st.data());
     const size_t nh = sizeof(NodeHot) * n_templates, nx = sizeof(NodeExt) * n_templates,
                  ns = sizeof(NodeStatic) * n_templates, nsm = sizeof(int32_t) * n_samples,
                  no = out ? sizeof(ca_pred_result) * (size_t)n_templates * (size_t)n_samples : 0,
                  nok = out_ok ? (size_t)n_templates * (size_t)n_samples : 0;
-    int rc;
     if ((rc = m->d_scratch2.reserve(nh + nx + ns + nsm + no + nok + 64)) != CA_OK) return rc;
     char* base = m->d_scratch2.as<char>();
     NodeHot* dh = reinterpret_cast<NodeHot*>(base);
@@ -1413,6 +1439,101 @@ int ca_check_templates(ca_mirror* m, const ca_podset* s, const int32_t* samples,
     if (out) CA_HIP_CHECK(hipMemcpyAsync(out, dout, no, hipMemcpyDeviceToHost, m->stream));
     if (out_ok) CA_HIP_CHECK(hipMemcpyAsync(out_ok, dok, nok, hipMemcpyDeviceToHost, m->stream));
     CA_HIP_CHECK(hipStreamSynchronize(m->stream));
+    return CA_OK;
+}
+
+int ca_expansion_plan_create(ca_mirror* m, const ca_template* templates, int32_t n_templates,
+                             ca_expansion_plan** out) {
+    if (!m || !out || n_templates < 0 || (n_templates > 0 && !templates)) return CA_EINVAL;
+    *out = nullptr;
+    CA_HIP_CHECK(hipSetDevice(m->device));
+    auto* p = new ca_expansion_plan();
+    p->m = m;
+    p->G = n_templates;
+    const size_t G = (size_t)std::max(n_templates, 1);
+    const size_t nh = sizeof(NodeHot) * G, nx = sizeof(NodeExt) * G, ns = sizeof(NodeStatic) * G;
+    int rc;
+    if ((rc = p->rows.reserve(nh + nx + ns)) != CA_OK) { delete p; return rc; }
+    if (n_templates > 0) {
+        std::vector<NodeHot> h(G);
+        std::vector<NodeExt> x(G);
+        std::vector<NodeStatic> st(G);
+        template_test_rows(templates, n_templates, h.data(), x.data(), st.data());
+        char* base = p->rows.as<char>();
+        if (hipMemcpyAsync(base, h.data(), nh, hipMemcpyHostToDevice, m->stream) != hipSuccess ||
+            hipMemcpyAsync(base + nh, x.data(), nx, hipMemcpyHostToDevice, m->stream) != hipSuccess ||
+            hipMemcpyAsync(base + nh + nx, st.data(), ns, hipMemcpyHostToDevice, m->stream) != hipSuccess ||
+            hipStreamSynchronize(m->stream) != hipSuccess) {
+            delete p;
+            set_last_error("ca_expansion_plan_create: template upload failed");
+            return CA_EDEVICE;
+        }
+    }
+    *out = p;
+    return CA_OK;
+}
+
+int ca_expansion_plan_run(ca_expansion_plan* p, const ca_podset* s, const int32_t* samples, int32_t n_samples,
+                          ca_pred_result* out, uint8_t* out_ok) {
+    if (!p || !s || s->m != p->m || n_samples < 0) return CA_EINVAL;
+    if (n_samples == 0 || p->G == 0) return CA_OK;
+    if (!samples || (!out && !out_ok)) return CA_EINVAL;
+    ca_mirror* m = p->m;
+    int rc;
+    if ((rc = check_samples(m, s, samples, n_samples)) != CA_OK) return rc;
+    CA_HIP_CHECK(hipSetDevice(m->device));
+    const size_t pairs = (size_t)p->G * (size_t)n_samples;
+    const size_t nsm = (sizeof(int32_t) * (size_t)n_samples + 63) & ~(size_t)63;
+    const size_t no = out ? ((sizeof(ca_pred_result) * pairs + 63) & ~(size_t)63) : 0;
+    const size_t nok = out_ok ? pairs : 0;
+    if ((rc = p->io.reserve(nsm + no + nok)) != CA_OK) return rc;
+    // the samples are read and the results written in page-locked memory through its
+    // device mapping: no copy-engine round trips for a call of a few kilobytes
+    char* hio = p->io.as<char>();
+    std::memcpy(hio, samples, sizeof(int32_t) * (size_t)n_samples);
+    void* dio_v = nullptr;
+    CA_HIP_CHECK(hipHostGetDevicePointer(&dio_v, p->io.ptr, 0));
+    char* dio = static_cast<char*>(dio_v);
+    // a page-locked output of the caller's (ca_host_alloc) takes the results straight from the kernel
+    auto mapped = [](void* h) -> char* {
+        hipPointerAttribute_t at;
+        if (h && hipPointerGetAttributes(&at, h) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer)
+            return static_cast<char*>(at.devicePointer);
+        (void)hipGetLastError();
+        return nullptr;
+    };
+    char* d_out = out ? mapped(out) : nullptr;
+    char* d_ok = out_ok ? mapped(out_ok) : nullptr;
+    const size_t G = (size_t)p->G;
+    const char* rows = p->rows.as<const char>();
+    CA_HIP_CHECK(hipEventRecord(m->ev0, m->stream));
+    hipLaunchKernelGGL(k_check_templates, dim3((n_samples + 255) / 256, p->G), dim3(256), 0, m->stream,
+                       reinterpret_cast<const NodeHot*>(rows),
+                       reinterpret_cast<const NodeExt*>(rows + sizeof(NodeHot) * G),
+                       reinterpret_cast<const NodeStatic*>(rows + (sizeof(NodeHot) + sizeof(NodeExt)) * G),
+                       reinterpret_cast<const int32_t*>(dio), n_samples, s->t.hot.as<PodHot>(),
+                       s->t.spec.as<ca_pod_spec>(), s->t.terms.as<ca_selector_term>(), s->t.reqs.as<ca_selector_req>(),
+                       out ? reinterpret_cast<ca_pred_result*>(d_out ? d_out : dio + nsm) : nullptr,
+                       out_ok ? reinterpret_cast<uint8_t*>(d_ok ? d_ok : dio + nsm + no) : nullptr);
+    CA_HIP_CHECK(hipGetLastError());
+    CA_HIP_CHECK(hipEventRecord(m->ev1, m->stream));
+    CA_HIP_CHECK(hipStreamSynchronize(m->stream));
+    CA_HIP_CHECK(hipEventElapsedTime(&p->kernel_ms, m->ev0, m->ev1));
+    if (out && !d_out) std::memcpy(out, hio + nsm, sizeof(ca_pred_result) * pairs);
+    if (out_ok && !d_ok) std::memcpy(out_ok, hio + nsm + no, pairs);
+    return CA_OK;
+}
+
+int ca_expansion_plan_kernel_ms(const ca_expansion_plan* p, float* kernel_ms) {
+    if (!p || !kernel_ms) return CA_EINVAL;
+    *kernel_ms = p->kernel_ms;
+    return CA_OK;
+}
+
+int ca_expansion_plan_destroy(ca_expansion_plan* p) {
+    if (!p) return CA_EINVAL;
+    if (p->m) (void)hipSetDevice(p->m->device);
+    delete p;
     return CA_OK;
 }
 

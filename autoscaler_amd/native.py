@@ -69,6 +69,10 @@ def load() -> C.CDLL:
         "ca_check_predicates": ([vp, vp, i32, i32, vp], C.c_int),
         "ca_fits_matrix": ([vp, vp, vp], C.c_int),
         "ca_check_templates": ([vp, vp, vp, i32, vp, i32, vp, vp], C.c_int),
+        "ca_expansion_plan_create": ([vp, vp, i32, p(vp)], C.c_int),
+        "ca_expansion_plan_run": ([vp, vp, vp, i32, vp, vp], C.c_int),
+        "ca_expansion_plan_destroy": ([vp], C.c_int),
+        "ca_expansion_plan_kernel_ms": ([vp, p(C.c_float)], C.c_int),
         "ca_estimate_batch": ([vp, vp, vp, vp, vp, i32, vp, p(i32), vp, vp, vp], C.c_int),
         "ca_estimate_plan_create": ([vp, vp, vp, vp, vp, i32, p(vp)], C.c_int),
         "ca_estimate_plan_run": ([vp, vp, p(i32), vp, vp, vp], C.c_int),
@@ -151,7 +155,8 @@ def exported_symbols() -> list[str]:
         "ca_mirror_remove_node", "ca_mirror_scope_blockers",
         "ca_mirror_fork", "ca_mirror_revert", "ca_mirror_commit", "ca_mirror_node_count", "ca_mirror_pod_node",
         "ca_mirror_node_pods", "ca_podset_create", "ca_podset_destroy", "ca_fits_any_node", "ca_check_predicates",
-        "ca_fits_matrix", "ca_check_templates", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
+        "ca_fits_matrix", "ca_check_templates", "ca_expansion_plan_create", "ca_expansion_plan_run",
+        "ca_expansion_plan_destroy", "ca_expansion_plan_kernel_ms", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
         "ca_estimate_plan_run_u16",
         "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_estimate_plan_timings",
         "ca_estimate_plan_set_phase_timing",
@@ -797,6 +802,58 @@ class EstimatePlan:
 
     def __exit__(self, *a):
         self.close()
+
+
+class ExpansionPlan:
+    """ComputeExpansionOption's check with the node groups resident (ca_expansion_plan_*,
+    include/casim.h; CA/core/scaleup/orchestrator/orchestrator.go:455-481): the templates'
+    test-node rows are uploaded once; run() checks a pod set's samples against all of them."""
+
+    def __init__(self, mirror: "Mirror", templates: np.ndarray):
+        self.lib = load()
+        self.mirror = mirror
+        self.templates = np.ascontiguousarray(templates, dtype=abi.TEMPLATE_DTYPE)
+        h = C.c_void_p()
+        _check(self.lib.ca_expansion_plan_create(mirror.h, ptr(self.templates), len(self.templates), C.byref(h)),
+               "ca_expansion_plan_create")
+        self.h = h
+
+    def run(self, podset: "PodSet", samples, verdict_only: bool = False, out=None) -> np.ndarray:
+        """[G][E] ca_pred_result (or with verdict_only a [G][E] uint8, 1 = fits), as
+        Mirror.check_templates returns it."""
+        sm = np.ascontiguousarray(samples, dtype=np.int32)
+        G = len(self.templates)
+        if out is None:
+            out = np.zeros((G, len(sm)), np.uint8 if verdict_only else abi.PRED_RESULT_DTYPE)
+        full, ok = (None, out) if verdict_only else (out, None)
+        _check(self.lib.ca_expansion_plan_run(self.h, podset.h, ptr(sm), len(sm),
+                                              ptr(full) if full is not None else None,
+                                              ptr(ok) if ok is not None else None), "ca_expansion_plan_run")
+        return out
+
+    @property
+    def kernel_ms(self) -> float:
+        """The last run's kernel time (HIP events)."""
+        v = C.c_float(0)
+        _check(self.lib.ca_expansion_plan_kernel_ms(self.h, C.byref(v)), "ca_expansion_plan_kernel_ms")
+        return v.value
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.ca_expansion_plan_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class UtilTable:

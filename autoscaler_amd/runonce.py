@@ -150,6 +150,37 @@ class DeviceUtil:
             self.rows = None
 
 
+class DeviceExpansion:
+    """The device's expansion-option step: the node groups' templates resident in one
+    ca_expansion_plan (re-created only when the caller's templates array changes), the
+    results written by the kernel into a page-locked buffer.  Like DeviceUtil's rows, the
+    returned array is overwritten by the next call."""
+
+    def __init__(self):
+        self.plan = None
+        self.templates = None
+        self.rows = None
+
+    def __call__(self, backend, podset, samples: np.ndarray, templates: np.ndarray) -> np.ndarray:
+        from . import native
+        if self.plan is None or self.templates is not templates or self.plan.mirror is not backend:
+            if self.plan is not None:
+                self.plan.close()
+            self.plan = native.ExpansionPlan(backend, templates)
+            self.templates = templates
+            self.rows = self.rows or native.PinnedRows()
+        out = self.rows.zeros("res", len(templates) * len(samples), abi.PRED_RESULT_DTYPE, zero=False)
+        return self.plan.run(podset, samples, out=out.reshape(len(templates), len(samples)))
+
+    def close(self):
+        if self.plan is not None:
+            self.plan.close()
+            self.plan = None
+        if self.rows is not None:
+            self.rows.close()
+            self.rows = None
+
+
 def _util_rows(w: RunOnceWorkload, placed_node: np.ndarray, zeros=_zeros):
     """ca_util_node / ca_util_pod rows of the snapshot after FilterOutSchedulable: each
     node's running pods, then the pods placed on it (NodeInfo.Pods order).  `zeros(key, n,
@@ -214,10 +245,12 @@ class UtilInput:
             self.nodes, self.off, self.pods, _ = _util_rows(w, placed_node, zeros)
 
 
-def run(backend, util_fn, w: RunOnceWorkload, timers=None, row_zeros=_zeros) -> RunOnceResult:
+def run(backend, util_fn, w: RunOnceWorkload, timers=None, row_zeros=_zeros, expand_fn=None) -> RunOnceResult:
     """One loop on `backend` (native.Mirror or pyoracle.OracleState, freshly loaded with
     W.load_filter) with `util_fn(UtilInput, now_ns) -> UTIL_INFO rows` (its attribute `want`,
-    default "full", picks the input form); `row_zeros` allocates full utilization rows."""
+    default "full", picks the input form); `row_zeros` allocates full utilization rows;
+    `expand_fn(backend, podset, samples, templates)` (e.g. DeviceExpansion) replaces the
+    backend's check_templates for step 2."""
     f = w.filt
     r = RunOnceResult()
     clock = time.perf_counter
@@ -237,7 +270,10 @@ def run(backend, util_fn, w: RunOnceWorkload, timers=None, row_zeros=_zeros) -> 
     groups = _equivalence_groups(f.pending.pods, unsched)
     samples = np.array([g[0] for g in groups], np.int32)
     t = clock()
-    res = backend.check_templates(f.pending, samples, w.templates, **kw)
+    if expand_fn is not None and ps is not None:
+        res = expand_fn(backend, ps, samples, w.templates)
+    else:
+        res = backend.check_templates(f.pending, samples, w.templates, **kw)
     r.ms["expansion"] = (clock() - t) * 1e3
     r.options = (res["type"] == 0).astype(np.uint8)
 

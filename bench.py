@@ -171,6 +171,23 @@ def expansion_leg(args, device: int, with_cpu: bool) -> dict:
             ms = float(np.median(ts) * 1e3)
             rec[f"{mode}_ms"] = ms
             rec[f"{mode}_pairs_per_s"] = len(samples) * len(w.templates) / (ms / 1e3)
+        # the same with the node groups resident (ca_expansion_plan): the samples in and the
+        # results out through page-locked memory the kernel reads and writes in place
+        res = res.copy()                                                   # (the resident runs reuse `full`)
+        with native.ExpansionPlan(m, w.templates) as plan:
+            for mode in ("verdicts", "with_reasons"):
+                call = (lambda: plan.run(podset, samples, verdict_only=True, out=ok)) if mode == "verdicts" else \
+                       (lambda: plan.run(podset, samples, out=full))
+                call()
+                ts, ks = [], []
+                for _ in range(max(args.steps, 5)):
+                    t = time.perf_counter()
+                    r2 = call()
+                    ts.append(time.perf_counter() - t)
+                    ks.append(plan.kernel_ms)
+                rec[f"resident_{mode}_ms"] = float(np.median(ts) * 1e3)
+                rec[f"resident_{mode}_kernel_ms"] = float(np.median(ks))
+            rec["resident_matches"] = bool(np.array_equal(r2, res))
         rec["feasible_pairs"] = int((res["type"] == 0).sum())
         rec["verdicts_match_results"] = bool(np.array_equal(ok.astype(bool), res["type"] == 0))
         res = res.copy()
@@ -187,6 +204,8 @@ def expansion_leg(args, device: int, with_cpu: bool) -> dict:
             cpu_ms = (time.perf_counter() - t) * 1e3
             rec.update({"cpu_ms": cpu_ms, "speedup_verdicts": cpu_ms / ms,
                         "speedup_with_reasons": cpu_ms / rec["with_reasons_ms"],
+                        "speedup_resident_verdicts": cpu_ms / rec["resident_verdicts_ms"],
+                        "speedup_resident_with_reasons": cpu_ms / rec["resident_with_reasons_ms"],
                         "parity": bool(np.array_equal(ro, res))})
         out[name] = rec
     podset.close()
@@ -430,11 +449,14 @@ def runonce_leg(args, device: int, with_cpu: bool) -> dict:
     # the utilization table holds the loop's starting snapshot resident (as the mirror does)
     # and receives the pods FilterOutSchedulable added (ca_util_table_set_added)
     util = runonce.DeviceUtil(device)
+    # the node groups' templates stay resident across loops (ca_expansion_plan)
+    expand = runonce.DeviceExpansion()
     runs = []
     for _ in range(1 + max(2, min(args.steps, 4))):
         m.fork()
-        runs.append(runonce.run(m, util, w))
+        runs.append(runonce.run(m, util, w, expand_fn=expand))
         m.revert()
+    expand.close()
     util.close()
     m.close()
     keys = list(runs[-1].ms)

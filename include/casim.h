@@ -360,6 +360,20 @@ int ca_fits_matrix(ca_mirror* m, const ca_podset* s, uint8_t* out);
 int ca_check_templates(ca_mirror* m, const ca_podset* s, const int32_t* samples, int32_t n_samples,
                        const ca_template* templates, int32_t n_templates, ca_pred_result* out,
                        uint8_t* out_ok);
+/* The same check with the node groups resident (a loop's node groups rarely change; the
+ * Estimate plan keeps its inputs the same way): _create uploads the templates' test-node
+ * rows once; _run takes the pod set and the samples of one loop and writes out / out_ok
+ * as ca_check_templates does, its samples and results passing through page-locked memory
+ * the kernel reads and writes in place (no copy-engine round trips).  s must belong to
+ * the plan's mirror. */
+typedef struct ca_expansion_plan ca_expansion_plan;
+int ca_expansion_plan_create(ca_mirror* m, const ca_template* templates, int32_t n_templates,
+                             ca_expansion_plan** out);
+int ca_expansion_plan_run(ca_expansion_plan* p, const ca_podset* s, const int32_t* samples, int32_t n_samples,
+                          ca_pred_result* out, uint8_t* out_ok);
+/* the last run's kernel time (HIP events) */
+int ca_expansion_plan_kernel_ms(const ca_expansion_plan* p, float* kernel_ms);
+int ca_expansion_plan_destroy(ca_expansion_plan* p);
 
 /* ---- estimator ---------------------------------------------------------------- */
 /* Estimate() for G node groups in order, sharing lastIndex as the reference's single

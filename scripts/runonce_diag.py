@@ -21,11 +21,12 @@ W.load_filter(m, w.filt)
 
 
 util = runonce.DeviceUtil(0)
+expand = runonce.DeviceExpansion()
 
 
 for rep in range(3):
     m.fork()
-    r = runonce.run(m, util, w)
+    r = runonce.run(m, util, w, expand_fn=expand)
     print({k: round(v, 2) for k, v in r.ms.items()}, flush=True)
     print("filter", m.filter_stats(), flush=True)
     print("sweep", m.removal_stats(), flush=True)

@@ -39,7 +39,16 @@ def test_runonce_gpu_parity(size, oracle_lib):
     W.load_filter(m, w.filt)
 
     util = runonce.DeviceUtil(0)
-    rg = runonce.run(m, util, w)
+    expand = runonce.DeviceExpansion()
+    rg = runonce.run(m, util, w, expand_fn=expand)
+    # the resident plan's results against the one-shot call's (full reason records)
+    ps = m.podset(w.filt.pending)
+    samples = np.array([g[0] for g in runonce._equivalence_groups(
+        w.filt.pending.pods, w.filt.order[rg.filter_node < 0])], np.int32)
+    assert expand(m, ps, samples, w.templates).tobytes() == \
+        m.check_templates(w.filt.pending, samples, w.templates, podset=ps).tobytes()
+    ps.close()
+    expand.close()
     # the full rows through one table, as a second form of the same step
     full = runonce.UtilInput(w, rg.filter_node, "full")
     t = native.UtilTable(0, full.nodes, full.off, full.pods)

@@ -110,6 +110,19 @@ def test_check_templates_gpu_matches_oracle(seed, oracle_lib):
     assert np.array_equal(outs[0], outs[1])
     v = b.check_templates(table, samples, tm, verdict_only=True)          # the one-byte verdicts
     assert np.array_equal(v.astype(bool), outs[0]["type"] == abi.CA_PRED_OK)
+    # the resident plan (ca_expansion_plan): pageable and page-locked outputs, two runs
+    ps = b.podset(table)
+    with native.ExpansionPlan(b, tm) as plan:
+        assert np.array_equal(plan.run(ps, samples), outs[0])
+        assert np.array_equal(plan.run(ps, samples, verdict_only=True), v)
+        pin = native.PinnedRows()
+        out = pin.zeros("r", len(tm) * len(samples), abi.PRED_RESULT_DTYPE).reshape(len(tm), len(samples))
+        assert np.array_equal(plan.run(ps, samples[::-1].copy(), out=out), outs[0][:, ::-1])
+        pin.close()
+        assert plan.run(ps, samples[:0]).shape == (len(tm), 0)
+        with pytest.raises(native.CasimError):
+            plan.run(ps, np.array([len(pods)], np.int32))                  # outside the pod set
+    ps.close()
 
 
 @pytest.mark.gpu

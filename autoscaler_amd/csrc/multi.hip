@@ -11,6 +11,7 @@
 // started at the input), and otherwise only has its lastIndex fields re-based.  No data
 // crosses devices: every block writes its own slice of the caller's result arrays.
 #include <thread>
+#include <chrono>
 
 #include "mirror.h"
 
@@ -84,6 +85,7 @@ struct ca_multi_removal_plan {
     std::vector<std::vector<int32_t>> hb;     // per block: the hints its run reads and writes
     int32_t reruns = 0;
     int32_t rerun_units = 0;                  // candidates in the re-run blocks of the last run
+    float phase_ms[5] = {0, 0, 0, 0, 0};      // last run (host wall): probe, map, compose, resolve, fix-up
     ~ca_multi_removal_plan() {
         for (auto* p : pl) if (p) ca_removal_plan_destroy(p);
     }
@@ -296,6 +298,13 @@ int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t 
     };
     p->reruns = 0;
     p->rerun_units = 0;
+    for (float& v : p->phase_ms) v = 0;
+    auto clk = std::chrono::steady_clock::now();
+    auto lap = [&](int i) {
+        const auto t = std::chrono::steady_clock::now();
+        p->phase_ms[i] = std::chrono::duration<float, std::milli>(t - clk).count();
+        clk = t;
+    };
     int rc;
     // ---- the ranges' lastIndex classes, composed on the host ----
     // 1. every range probes its candidates (guesses from the pods before it) and reports its
@@ -317,6 +326,7 @@ int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t 
             gb += removal_plan_sensitive_pods(p->pl[d]);
         }
         if ((rc = for_blocks(D, [&](int32_t d) { return run(d, L0, &ph[d]); })) != CA_OK) return rc;
+        lap(0);
         int64_t est = L0;
         std::vector<int32_t> mapped;                          // ranges whose output can depend on their input
         for (int32_t d = 0; d < D; d++) {
@@ -328,6 +338,7 @@ int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t 
         if ((rc = for_blocks((int32_t)mapped.size(), [&](int32_t i) { return run(mapped[i], L0, &ph[mapped[i]]); })) !=
             CA_OK)
             return rc;
+        lap(1);
         int64_t cur = L0;
         for (int32_t d = 0; d < D; d++) {
             if (ph[d].S == 0 || ph[d].succ == 0) {           // no scan can succeed: lastIndex passes through
@@ -350,6 +361,7 @@ int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t 
             lin_c[d] = (int32_t)cur;
             cur = mp[x];
         }
+        lap(2);
         for (int32_t d = 0; d < D; d++) ph[d].kind = SP_RESOLVE;
         std::vector<int32_t> todo;
         for (int32_t d = 0; d < D; d++) if (lin_c[d] != INT32_MIN) todo.push_back(d);
@@ -358,8 +370,10 @@ int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t 
                  return run(d, lin_c[d], &ph[d]);
              })) != CA_OK)
             return rc;
+        lap(3);
     } else {
         if ((rc = for_blocks(D, [&](int32_t d) { return run(d, L0, nullptr); })) != CA_OK) return rc;
+        lap(3);
     }
     int32_t cur = L0;
     bool cut = false;
@@ -396,6 +410,7 @@ int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t 
             }
     }
     *last_index = cur;
+    lap(4);
     return CA_OK;
 }
 
@@ -418,6 +433,12 @@ int ca_multi_removal_plan_rerun_units(const ca_multi_removal_plan* p, int32_t* c
     if (!p || !candidates_rerun) return CA_EINVAL;
     *candidates_rerun = p->rerun_units;
     return CA_OK;
+}
+
+int ca_multi_removal_plan_timings(const ca_multi_removal_plan* p, float* ms, int32_t cap) {
+    if (!p || (cap > 0 && !ms)) return CA_EINVAL;
+    for (int32_t i = 0; i < cap && i < 5; i++) ms[i] = p->phase_ms[i];
+    return 5;
 }
 
 int ca_multi_removal_plan_destroy(ca_multi_removal_plan* p) {

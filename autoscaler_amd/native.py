@@ -116,6 +116,7 @@ def load() -> C.CDLL:
         "ca_multi_removal_plan_run": ([vp, vp, i32, p(i32), vp, vp], C.c_int),
         "ca_multi_removal_plan_stats": ([vp, p(i32), p(i32), vp, i32], C.c_int),
         "ca_multi_removal_plan_rerun_units": ([vp, p(i32)], C.c_int),
+        "ca_multi_removal_plan_timings": ([vp, vp, i32], C.c_int),
         "ca_multi_removal_plan_destroy": ([vp], C.c_int),
         "ca_multi_find_nodes_to_remove": ([vp, vp, i32, vp, vp, vp, vp, vp, i32, p(i32), vp, vp], C.c_int),
         "ca_plan_removals": ([vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, i32, p(i32), vp, vp, i32, p(i32)], C.c_int),
@@ -171,7 +172,7 @@ def exported_symbols() -> list[str]:
         "ca_multi_estimate_plan_create", "ca_multi_estimate_plan_run",
         "ca_multi_estimate_plan_stats", "ca_multi_estimate_plan_rerun_units", "ca_multi_estimate_plan_destroy", "ca_multi_estimate_batch",
         "ca_multi_removal_plan_create", "ca_multi_removal_plan_run", "ca_multi_removal_plan_stats",
-        "ca_multi_removal_plan_rerun_units",
+        "ca_multi_removal_plan_rerun_units", "ca_multi_removal_plan_timings",
         "ca_multi_removal_plan_destroy", "ca_multi_find_nodes_to_remove",
         "ca_plan_removals", "ca_plan_last_moves", "ca_plan_stats", "ca_plan_last_path", "ca_plan_chain_profile",
     ]
@@ -1024,8 +1025,11 @@ class MultiRemovalPlan:
         self.lib.ca_multi_removal_plan_stats(self.h, C.byref(nb), C.byref(rr), ptr(first), len(first))
         ru = C.c_int32(0)
         self.lib.ca_multi_removal_plan_rerun_units(self.h, C.byref(ru))
+        tm = np.zeros(5, np.float32)
+        self.lib.ca_multi_removal_plan_timings(self.h, tm.ctypes.data, 5)
         return {"blocks": nb.value, "reruns": rr.value, "block_first_candidate": first[: nb.value + 1].tolist(),
-                "rerun_candidates": ru.value}
+                "rerun_candidates": ru.value,
+                "phase_ms": dict(zip(("probe", "map", "compose", "resolve", "fixup"), tm.tolist()))}
 
     def close(self) -> None:
         if self.h:

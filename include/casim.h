@@ -640,6 +640,9 @@ int ca_multi_removal_plan_stats(const ca_multi_removal_plan* p, int32_t* n_block
                                 int32_t* block_first_candidate, int32_t cap);
 /* candidates in the blocks the last run had to run again */
 int ca_multi_removal_plan_rerun_units(const ca_multi_removal_plan* p, int32_t* candidates_rerun);
+/* host wall time (ms) of the last run's phases: probe, map, compose, resolve, fix-up
+ * (the serial path reports its block runs as "resolve"); returns the count (5) */
+int ca_multi_removal_plan_timings(const ca_multi_removal_plan* p, float* ms, int32_t cap);
 int ca_multi_removal_plan_destroy(ca_multi_removal_plan* p);
 int ca_multi_find_nodes_to_remove(ca_multi* mm, const int32_t* candidates, int32_t n_candidates,
                                   const uint8_t* dest_mask, const int32_t* cand_status, const int32_t* move_off,

@@ -146,9 +146,9 @@ def test_multi_sweep_prefix_protocol(oracle):
 @pytest.mark.parametrize("replicas", [2, 4])
 def test_multi_sweep_c3_full(replicas, oracle):
     """BASELINE C3 at full size (5k nodes, 150k pods) on ca_multi_*: the fresh loop (every
-    block lastIndex-sensitive in a loose cluster: blocks after the first re-run) and the
-    hinted second loop (hint placements pass lastIndex through: no re-runs), against the
-    oracle; the re-run candidates are reported."""
+    block lastIndex-sensitive in a loose cluster: the blocks' lastIndex maps compose on the
+    host, so none waits for its predecessor or runs twice) and the hinted second loop (hint
+    placements pass lastIndex through), against the oracle, with no re-run candidates."""
     w = W.c3()
     args = (w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods)
     o = oracle.OracleState()

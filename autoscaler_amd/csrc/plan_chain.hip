@@ -242,29 +242,48 @@ __device__ inline uint64_t pc_uni64(uint64_t v) {
 }
 __device__ inline int64_t pc_uni64s(int64_t v) { return (int64_t)pc_uni64((uint64_t)v); }
 
+// Wave maximum of an unsigned value (0 = no value): DPP row shifts, then the row
+// broadcasts 15 / 31; lane 63 ends with the maximum.  Seven VALU steps, against ~35
+// instructions for the 64-bit __ockl reduction.
+__device__ inline uint32_t pc_wmax_u32(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // Rebuilds a block's skyline from its 64 rows as one wave holds them (lane i: row j*64 + i;
 // `valid`: visible, a free pod slot, not the candidate being simulated).  Extraction: the
 // largest (cpu, memory) key is a skyline point; every row with memory at most its memory is
-// dominated by it (its cpu is at most the point's); repeat on the rest.  C3 blocks hold
-// 4-5 points on average (p99 10), so a rebuild is a few wave reductions.
+// dominated by it (its cpu is at most the point's); repeat on the rest.  The key's maximum
+// is two 32-bit wave maxima (cpu, then memory among the rows at that cpu; values biased so
+// that unsigned order is signed order and 0 means none).  C3 blocks hold 4-5 points on
+// average (p99 10), so a rebuild is a few wave reductions.
 __device__ void pc_sky_build(const PcSkyV sk, int32_t j, int64_t cc, int64_t cm, bool valid) {
     const int lane = threadIdx.x & 63;
     const int32_t C = sky_c(cc), M = sky_m(cm);
-    const int64_t key = ((int64_t)C << 32) | (int64_t)(uint32_t)(M ^ INT32_MIN);   // cpu, then memory
+    const uint32_t Cu = (uint32_t)C ^ 0x80000000u, Mu = (uint32_t)M ^ 0x80000000u;
     bool alive = valid;
     int k = 0;
     while (k < PC_SKY - 1) {
         if (!__ballot(alive)) break;
-        const int64_t mx = __ockl_wfred_max_i64(alive ? key : INT64_MIN);
-        const int32_t pm = (int32_t)((uint32_t)mx ^ (uint32_t)INT32_MIN);
-        if (lane == 0) { sk.c[k * sk.nb + j] = (int32_t)(mx >> 32); sk.m[k * sk.nb + j] = pm; }
+        const uint32_t cmax = pc_wmax_u32(alive ? Cu : 0u);
+        const uint32_t mmax = pc_wmax_u32((alive && Cu == cmax) ? Mu : 0u);
+        const int32_t pm = (int32_t)(mmax ^ 0x80000000u);
+        if (lane == 0) { sk.c[k * sk.nb + j] = (int32_t)(cmax ^ 0x80000000u); sk.m[k * sk.nb + j] = pm; }
         k++;
         alive = alive && M > pm;
     }
     if (k == PC_SKY - 1 && __ballot(alive)) {        // one point bounds the rest
-        const int64_t mx = __ockl_wfred_max_i64(alive ? key : INT64_MIN);
-        const int32_t mm = __ockl_wfred_max_i32(alive ? M : INT32_MIN);
-        if (lane == 0) { sk.c[k * sk.nb + j] = (int32_t)(mx >> 32); sk.m[k * sk.nb + j] = mm; }
+        const uint32_t cmax = pc_wmax_u32(alive ? Cu : 0u);
+        const uint32_t mmax = pc_wmax_u32(alive ? Mu : 0u);
+        if (lane == 0) {
+            sk.c[k * sk.nb + j] = (int32_t)(cmax ^ 0x80000000u);
+            sk.m[k * sk.nb + j] = (int32_t)(mmax ^ 0x80000000u);
+        }
         k++;
     }
     if (lane == 0) sk.n[j] = k;
@@ -283,6 +302,18 @@ __device__ inline bool pc_sky_maybe(const PcSkyV sk, int32_t j, int32_t pc, int3
 #pragma unroll
     for (int i = 0; i < PC_SKY; i++) hit |= (i < k) & (pc <= c[i]) & (pm <= m[i]);
     return hit;
+}
+
+// The same test without branches (the window test: every lane's 18 loads in flight at once)
+__device__ inline bool pc_sky_maybe_bf(const PcSkyV sk, int32_t j, int32_t pc, int32_t pm, bool all_zero) {
+    const int32_t k = sk.n[j];
+    bool hit = false;
+#pragma unroll
+    for (int i = 0; i < PC_SKY; i++) {
+        const int32_t c = sk.c[i * sk.nb + j], m = sk.m[i * sk.nb + j];
+        hit |= (i < k) & (pc <= c) & (pm <= m);
+    }
+    return (k < 0) | (all_zero ? (k > 0) : hit);
 }
 
 // workgroup-coherent global loads: the PDB budgets the chain's own atomics updated
@@ -536,6 +567,15 @@ __device__ __attribute__((noinline)) void pc_plain_run(unsigned char* pc_raw, in
 #endif
     for (; k < R; k++) {
         PR_COUNT(5);
+        // (the loop state is uniform: said so at every pod, else a value the compiler cannot
+        // prove uniform turns the whole scan below into exec-masked vector code)
+        k = __builtin_amdgcn_readfirstlane(k);
+        Lw = __builtin_amdgcn_readfirstlane(Lw);
+        adv = __builtin_amdgcn_readfirstlane(adv);
+        cj = __builtin_amdgcn_readfirstlane(cj);
+        dirty0 = pc_uni64(dirty0); dirty1 = pc_uni64(dirty1);
+        cvis = pc_uni64(cvis); cok = pc_uni64(cok); ctaint = pc_uni64(ctaint);
+        cd0 = pc_uni64(cd0); cd1 = pc_uni64(cd1);
         const int64_t pcpu = pc_rl64(qc, k), pmem = pc_rl64(qm, k);
         const int64_t peph = EPH_COLS ? pc_rl64(qe, k) : 0;
         const uint32_t pf = (uint32_t)pc_rl32((int32_t)qf, k);
@@ -618,6 +658,10 @@ __device__ __attribute__((noinline)) void pc_plain_run(unsigned char* pc_raw, in
         uint64_t passm = 0;
         PR_MARK(0);
         for (int32_t rr = 0; rr <= nb; rr++) {
+            rr = __builtin_amdgcn_readfirstlane(rr);
+            wr = __builtin_amdgcn_readfirstlane(wr);
+            cj = __builtin_amdgcn_readfirstlane(cj);
+            passm = pc_uni64(passm);
             if (rr == nb && l0 == 0) break;
             int32_t j = j0 + rr;
             if (j >= nb) j -= nb;
@@ -626,15 +670,13 @@ __device__ __attribute__((noinline)) void pc_plain_run(unsigned char* pc_raw, in
                 if (wr < 0 || rr >= wr + 64) {
                     const int32_t pc32 = sky_c(pcpu), pm32 = sky_m(pmem);   // (only scans that leave their block)
                     const int32_t q = rr + lane;
-                    bool pass = false;
-                    my_nv = 0;
-                    if (q < nb) {
-                        int32_t jj = j0 + q;
-                        if (jj >= nb) jj -= nb;
-                        const uint64_t vw = blk[jj].vis & (jj == jn ? ~nbit : ~0ull);
-                        pass = !((vw != 0) && pc_sky_maybe(sky, jj, pc32, pm32, all_zero)) && jj != cj;
-                        my_nv = __popcll(vw);
-                    }
+                    const bool qin = q < nb;
+                    int32_t jj = j0 + (qin ? q : 0);             // (lanes past the ring read a valid block)
+                    if (jj >= nb) jj -= nb;
+                    const uint64_t vw = blk[jj].vis & (jj == jn ? ~nbit : ~0ull);
+                    const bool maybe = pc_sky_maybe_bf(sky, jj, pc32, pm32, all_zero);
+                    const bool pass = qin & !((vw != 0) & maybe) & (jj != cj);
+                    my_nv = qin ? __popcll(vw) : 0;
                     passm = __ballot(pass);
                     wr = rr;
                     PR_COUNT(7);

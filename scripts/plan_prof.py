@@ -33,7 +33,7 @@ for limit in (20, 200, 0):
         m.revert()
     tot = max(pr.get("total", 1), 1)
     ghz = tot / (pr["kernel_ms"] * 1e6) if pr["kernel_ms"] > 0 else 0
-    print(f"limit {limit}: {dt:.3f} ms path {st['path']} simulated {st['simulated']} "
+    print(f"limit {limit}: {dt:.3f} ms (library {st['total_ms']:.3f}) path {st['path']} simulated {st['simulated']} "
           f"evals {int(r.results['evals'].sum())} moves {len(r.moves)}", flush=True)
     print("   host: " + "  ".join(f"{k}={pr[k]:.3f}" for k in
                                    ("sync_ms", "launch_kernel_ms", "kernel_ms", "readback_ms", "replay_ms")))

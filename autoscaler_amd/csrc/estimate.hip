@@ -2656,11 +2656,11 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
     // One pass over the lists (per-pod summaries of the podset: compact arrays instead of
     // the 208-B records), split over host threads for big batches: index validation, the
     // port / extended-resource flags and each group's summed requests for the demand
-    // order.  The lists travel to the device meanwhile (the main thread drives the copy);
+    // order.  The lists travel to the device meanwhile (the caller's thread queues the copy);
     // the item classes are gathered there from the podset's class column (k_item_cls).
     {
         const int32_t total = p->total;
-        const int32_t T = std::max(1, std::min(8, total / (1 << 17)));
+        const int32_t T = std::max(1, std::min(7, total / (1 << 17)));
         struct Part { bool bad = false; uint8_t fl = 0; std::vector<double> c, mm; };
         std::vector<Part> part((size_t)T);
         const bool want_fl = s->any_ports || s->any_scalar;
@@ -2698,13 +2698,14 @@ int plan_prepare(ca_estimate_plan* p, ca_mirror* m, const ca_podset* s, const in
                 i = e;
             }
         };
-        std::vector<std::thread> th;
-        for (int32_t t = 1; t < T; t++) th.emplace_back(work, t);
         hipError_t ce = hipSuccess;
-        if ((rc = p->d_pod_idx.reserve(sizeof(int32_t) * tot)) == CA_OK && total)
-            ce = hipMemcpyAsync(p->d_pod_idx.ptr, pod_idx, sizeof(int32_t) * total, hipMemcpyHostToDevice, st);
-        work(0);
-        for (auto& x : th) x.join();
+        rc = CA_OK;
+        // task 0 (the caller's thread) queues the list upload, tasks 1..T walk the items
+        casim::parallel_run(T + 1, [&](int32_t t) {
+            if (t > 0) { work(t - 1); return; }
+            if ((rc = p->d_pod_idx.reserve(sizeof(int32_t) * tot)) == CA_OK && total)
+                ce = hipMemcpyAsync(p->d_pod_idx.ptr, pod_idx, sizeof(int32_t) * total, hipMemcpyHostToDevice, st);
+        });
         if (rc != CA_OK) return rc;
         CA_HIP_CHECK(ce);
         bool bad = false;

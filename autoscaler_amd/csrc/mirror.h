@@ -165,6 +165,12 @@ template <class T> class ChunkVec {
         n_ = n;
     }
     void clear() { resize(0); }                 // (the chunks stay mapped for the next load)
+    void resize_for_overwrite(size_t n) {       // grow without initialising: the caller writes every new row
+        static_assert(std::is_trivially_destructible<T>::value, "rows dropped without destructors");
+        if (n <= n_) { resize(n); return; }
+        reserve(n);
+        n_ = n;
+    }
 
   private:
     static constexpr size_t kHuge = (size_t)2 << 20;

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <condition_variable>
 #include <thread>
 #include <unordered_map>
 #include <algorithm>
@@ -151,6 +152,72 @@ void DevBuf::release() {
     }
     ptr = nullptr;
     bytes = 0;
+}
+
+namespace {
+class WorkerPool {
+  public:
+    explicit WorkerPool(int n) {
+        for (int i = 0; i < n; i++) th_.emplace_back([this, i] { loop(i + 1); });
+    }
+    ~WorkerPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void run(int32_t T, const std::function<void(int32_t)>& fn) {
+        std::lock_guard<std::mutex> region(run_mu_);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &fn;
+            njob_ = T;
+            left_ = (int32_t)th_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return left_ == 0; });
+    }
+    int32_t workers() const { return (int32_t)th_.size(); }
+
+  private:
+    void loop(int32_t id) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int32_t)>* f;
+            int32_t nj;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                f = job_;
+                nj = njob_;
+            }
+            if (id < nj) (*f)(id);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--left_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_, run_mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int32_t)>* job_ = nullptr;
+    int32_t njob_ = 0, left_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+}  // namespace
+
+void parallel_run(int32_t T, const std::function<void(int32_t)>& fn) {
+    if (T <= 1) { fn(0); return; }
+    static WorkerPool pool(7);
+    if (T > pool.workers() + 1) T = pool.workers() + 1;
+    pool.run(T, fn);
 }
 
 int HostBuf::reserve(size_t need) {
@@ -424,7 +491,7 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
     // walks the placements in order for its nodes, so every node sees its pods in order; the
     // journal entries of different nodes commute (Revert undoes each node's in reverse).
     const size_t base = pods.size();
-    pods.resize(base + (size_t)np);
+    pods.resize_for_overwrite(base + (size_t)np);                // (the threads write every record)
     if (dirty_flag.size() < nodes.size()) dirty_flag.resize(nodes.size(), 0);
     std::vector<int32_t> id_of((size_t)n, -1);
     for (int32_t k = 0, c = 0; k < n; k++)
@@ -437,7 +504,9 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
     };
     std::vector<Part> part((size_t)T);
     const bool journaled = depth > 0;
+    std::vector<double> tw((size_t)T * 3, 0.0);          // (CASIM_DEBUG_TIMING: per-thread start / records / AddPods)
     auto work = [&](int32_t w) {
+        if (dbg_t) tw[3 * w] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         Part& pt = part[w];
         const int32_t k0 = (int32_t)((int64_t)n * w / T), k1 = (int32_t)((int64_t)n * (w + 1) / T);
         for (int32_t k = k0; k < k1; k++) {             // the records of positions [k0, k1)
@@ -448,6 +517,7 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
             if (casim::pod_dev_flags(r.spec) & (casim::PF_PORTS | casim::PF_SCALAR_REQ | casim::PF_MOVED_SCALAR_REQ)) pt.ext++;
             if (r.spec.req_ephemeral != 0) pt.eph++;
         }
+        if (dbg_t) tw[3 * w + 1] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         for (int32_t k = 0; k < n; k++) {               // AddPod on my nodes, in order
             if (k + 32 < n) {                            // (rows are cache misses: fetch ahead)
                 const int32_t y = node[k + 32];
@@ -480,12 +550,14 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
                 pt.jr.push_back(e);
             }
         }
+        if (dbg_t) tw[3 * w + 2] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     };
-    std::vector<std::thread> th;
-    for (int32_t w = 1; w < T; w++) th.emplace_back(work, w);
-    work(0);
-    for (auto& x : th) x.join();
+    casim::parallel_run(T, work);
     tmark("threads");
+    if (dbg_t)
+        for (int32_t w = 0; w < T; w++)
+            fprintf(stderr, "[add_placed]   thread %d: start %.3f records %.3f addpods %.3f ms\n", w, tw[3 * w], tw[3 * w + 1],
+                    tw[3 * w + 2]);
     for (Part& pt : part) {
         n_ext_pods += pt.ext;
         n_eph_pods += pt.eph;

@@ -285,6 +285,11 @@ struct ca_mirror {
     void add_placed_batch(const ca_pod_table* t, const int32_t* idx, const int32_t* node, int32_t n,
                           int32_t* out_id, bool device_rows = false);
     int32_t store_moved_copy(int32_t pod);  // the copy findPlaceFor schedules (cluster.go:235-240)
+    // the planner's committed moves, candidate by candidate: RemovePod of each moved pod,
+    // then the copies (ids pods.size() + t, t-th move) AddPod'ed on their nodes; large
+    // batches on the worker pool, split by node (planner.hip).  CA_EDEVICE if mv[t].new_pod
+    // is not the id the copy gets.
+    int replay_moves(const ca_plan_move* mv, int32_t nm);
     void journal_push(int32_t kind, int32_t node, int32_t pod, int32_t slot, const uint64_t* ports);
     void fill_hot(int32_t i, casim::NodeHot& h) const;
     void fill_ext(int32_t i, casim::NodeExt& e) const;

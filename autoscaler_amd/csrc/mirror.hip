@@ -460,7 +460,9 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
     }
     reserve_more((size_t)np, depth > 0 ? (size_t)np : 0);
     tmark("reserved");
-    const int32_t T = plain ? std::min(8, np / 2048) : 1;
+    int32_t T = plain ? std::min(8, np / 2048) : 1;
+    T = T >= 8 ? 8 : T >= 4 ? 4 : T >= 2 ? 2 : 1;              // (a power of two: 64-node block & (T - 1) picks the thread)
+    const int32_t tmask = T - 1;
     // rows dirty before this batch stay dirty; the batch's own marks are dropped below where
     // the kernel's row equals fill_hot's
     const size_t dirty0 = dirty_rows.size();
@@ -487,7 +489,7 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
         keep_device_rows();
         return;
     }
-    // Threads own disjoint pod id ranges (the records) and disjoint node sets (node % T): each
+    // Threads own disjoint pod id ranges (the records) and disjoint node sets (64-node blocks: adjacent rows share cache lines): each
     // walks the placements in order for its nodes, so every node sees its pods in order; the
     // journal entries of different nodes commute (Revert undoes each node's in reverse).
     const size_t base = pods.size();
@@ -521,13 +523,13 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
         for (int32_t k = 0; k < n; k++) {               // AddPod on my nodes, in order
             if (k + 32 < n) {                            // (rows are cache misses: fetch ahead)
                 const int32_t y = node[k + 32];
-                if (y >= 0 && y % T == w) {
+                if (y >= 0 && ((y >> 6) & tmask) == w) {
                     __builtin_prefetch(&nodes[y], 1);
                     __builtin_prefetch(reinterpret_cast<const char*>(&nodes[y]) + 256, 1);
                 }
             }
             const int32_t x = node[k];
-            if (x < 0 || x % T != w) continue;
+            if (x < 0 || ((x >> 6) & tmask) != w) continue;
             const ca_pod_spec& p = t->pods[idx[k]];
             casim::NodeRow& nd = nodes[x];
             casim::JournalEntry e;

@@ -1825,22 +1825,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     moves_out.assign(hmoves, hmoves + nm);
     const auto t_read = std::chrono::steady_clock::now();
     // ---- replay the committed moves into the mirror (journaled at the caller's depth) ----
-    for (int32_t k = 0; k < nm;) {
-        const int32_t cand = moves_out[k].candidate;
-        int32_t e = k;
-        while (e < nm && moves_out[e].candidate == cand) e++;
-        for (int32_t t = k; t < e; t++)
-            if ((rc = ca_mirror_remove_pod(m, moves_out[t].pod)) != CA_OK) return rc;   // cluster.go:228-233
-        for (int32_t t = k; t < e; t++) {
-            const int32_t nid = m->store_moved_copy(moves_out[t].pod);
-            if (nid != moves_out[t].new_pod) {
-                set_last_error("plan chain: copy ids out of step with the mirror");
-                return CA_EDEVICE;
-            }
-            m->add_pod_to_node(nid, moves_out[t].node);                                   // AddPod (:79)
-        }
-        k = e;
-    }
+    if ((rc = m->replay_moves(moves_out.data(), nm)) != CA_OK) return rc;     // cluster.go:228-240, :79
     const auto t_end = std::chrono::steady_clock::now();
     {
         PlanStats& ps = m->plan;

@@ -97,6 +97,165 @@ int32_t ca_mirror::store_moved_copy(int32_t pod) {
     return (int32_t)pods.size() - 1;
 }
 
+int ca_mirror::replay_moves(const ca_plan_move* mv, int32_t nm) {
+    if (nm <= 0) return CA_OK;
+    const int32_t base = (int32_t)pods.size();
+    for (int32_t t = 0; t < nm; t++) {
+        if (mv[t].new_pod != base + t || mv[t].pod < 0 || mv[t].pod >= base + t || mv[t].node < 0 ||
+            mv[t].node >= (int32_t)nodes.size()) {
+            set_last_error("plan chain: copy ids out of step with the mirror");
+            return CA_EDEVICE;
+        }
+    }
+    int32_t T = std::min(8, nm / 4096);
+    T = T >= 8 ? 8 : T >= 4 ? 4 : T >= 2 ? 2 : 1;              // (a power of two: 64-node block & (T - 1) picks the thread)
+    const int32_t tm = T - 1;
+    if (T <= 1) {
+        for (int32_t k = 0; k < nm;) {
+            const int32_t cand = mv[k].candidate;
+            int32_t e = k;
+            while (e < nm && mv[e].candidate == cand) e++;
+            for (int32_t t = k; t < e; t++) {
+                const int rc = ca_mirror_remove_pod(this, mv[t].pod);                 // cluster.go:228-233
+                if (rc != CA_OK) return rc;
+            }
+            for (int32_t t = k; t < e; t++) add_pod_to_node(store_moved_copy(mv[t].pod), mv[t].node);   // AddPod (:79)
+            k = e;
+        }
+        return CA_OK;
+    }
+    const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
+    const auto tr0 = std::chrono::steady_clock::now();
+    auto tmark = [&](const char* what) {
+        if (dbg_t)
+            fprintf(stderr, "[replay] %-10s %8.3f ms\n", what,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count());
+    };
+    // Large batches (the loop without a limit: ~68k moves on C3).  The copies' records first:
+    // a copy of a copy is a copy of the original (moved_spec is idempotent), so record t
+    // derives from its root pod below `base` and every record is independent.  Then the row
+    // updates split by 64-node block (adjacent rows share cache lines): each thread walks the moves in order and applies the
+    // RemovePods / AddPods on its own nodes, so every node sees its pods in order; journal
+    // entries of different nodes commute (Revert undoes each node's in reverse).
+    std::vector<int32_t> root((size_t)nm), src_node((size_t)nm);
+    for (int32_t t = 0; t < nm; t++) {
+        const int32_t p = mv[t].pod;
+        root[t] = p < base ? p : root[p - base];
+        src_node[t] = p < base ? pods[p].node : mv[p - base].node;
+        if (src_node[t] < 0) return CA_ENOTFOUND;
+    }
+    pods.resize_for_overwrite((size_t)base + (size_t)nm);
+    if (dirty_flag.size() < nodes.size()) dirty_flag.resize(nodes.size(), 0);
+    if (depth > 0) reserve_more(0, 2 * (size_t)nm);
+    struct Part {
+        std::vector<JournalEntry> jr;
+        std::vector<int32_t> dirty;
+        int64_t ext = 0, eph = 0, blockers = 0;
+        int rc = CA_OK;
+    };
+    std::vector<Part> part((size_t)T);
+    const bool journaled = depth > 0;
+    tmark("prepared");
+    casim::parallel_run(T, [&](int32_t w) {
+        Part& pt = part[w];
+        const int32_t t0 = (int32_t)((int64_t)nm * w / T), t1 = (int32_t)((int64_t)nm * (w + 1) / T);
+        for (int32_t t = t0; t < t1; t++) {                     // the records of moves [t0, t1)
+            if (t + 8 < t1) __builtin_prefetch(&pods[root[t + 8]].spec);   // (random records: fetch ahead)
+            PodRow& r = pods[(size_t)base + t];
+            r.spec = moved_spec(pods[root[t]].spec);
+            r.node = -1;
+            if (pod_dev_flags(r.spec) & (PF_PORTS | PF_SCALAR_REQ | PF_MOVED_SCALAR_REQ)) pt.ext++;
+            if (r.spec.req_ephemeral != 0) pt.eph++;
+        }
+    });
+    tmark("records");
+    casim::parallel_run(T, [&](int32_t w) {
+        Part& pt = part[w];
+        if (journaled) pt.jr.reserve(2 * (size_t)nm / (size_t)T + 1024);
+        auto apply = [&](int32_t x, const ca_pod_spec& p, int sign) {
+            NodeRow& nd = nodes[x];
+            if (sign > 0) {
+                nd.req_cpu = wadd(nd.req_cpu, p.req_milli_cpu);
+                nd.req_mem = wadd(nd.req_mem, p.req_memory);
+                nd.req_eph = wadd(nd.req_eph, p.req_ephemeral);
+                for (int i = 0; i < CA_MAX_SCALAR; i++) nd.req_scalar[i] = wadd(nd.req_scalar[i], p.req_scalar[i]);
+                for (int q = 0; q < CA_PORT_WORDS; q++) nd.ports[q] |= p.port_use[q];
+            } else {
+                nd.req_cpu = wsub(nd.req_cpu, p.req_milli_cpu);
+                nd.req_mem = wsub(nd.req_mem, p.req_memory);
+                nd.req_eph = wsub(nd.req_eph, p.req_ephemeral);
+                for (int i = 0; i < CA_MAX_SCALAR; i++) nd.req_scalar[i] = wsub(nd.req_scalar[i], p.req_scalar[i]);
+                for (int q = 0; q < CA_PORT_WORDS; q++) nd.ports[q] &= ~p.port_use[q];
+            }
+            nd.npods += sign;
+            if (p.flags & CA_POD_REQUIRED_ANTI_AFFINITY) pt.blockers += sign;
+            if (!dirty_flag[x]) { dirty_flag[x] = 1; pt.dirty.push_back(x); }
+        };
+        auto journal = [&](int32_t kind, int32_t x, int32_t pod, int32_t slot, const uint64_t* before) {
+            if (!journaled) return;
+            JournalEntry e;
+            std::memset(&e, 0, sizeof e);
+            e.kind = kind; e.node = x; e.pod = pod; e.slot = slot;
+            std::memcpy(e.ports, before, sizeof e.ports);
+            pt.jr.push_back(e);
+        };
+        for (int32_t k = 0; k < nm && pt.rc == CA_OK;) {
+            const int32_t cand = mv[k].candidate;
+            int32_t e = k;
+            while (e < nm && mv[e].candidate == cand) e++;
+            for (int32_t t = k; t < e; t++) {                   // RemovePod (cluster.go:228-233)
+                if (t + 16 < nm && ((src_node[t + 16] >> 6) & tm) == w) {     // (random rows and records: fetch ahead)
+                    __builtin_prefetch(&pods[mv[t + 16].pod].spec);
+                    __builtin_prefetch(reinterpret_cast<const char*>(&pods[mv[t + 16].pod].spec) + 64);
+                    __builtin_prefetch(&nodes[src_node[t + 16]]);
+                }
+                const int32_t x = src_node[t];
+                if (((x >> 6) & tm) != w) continue;
+                const int32_t pod = mv[t].pod;
+                NodeRow& nd = nodes[x];
+                int32_t slot = -1;
+                for (size_t i = 0; i < nd.pods.size(); i++) if (nd.pods[i] == pod) { slot = (int32_t)i; break; }
+                if (slot < 0) { pt.rc = CA_ENOTFOUND; break; }
+                uint64_t before[CA_PORT_WORDS];
+                std::memcpy(before, nd.ports, sizeof before);
+                nd.pods[slot] = nd.pods.back();                 // swap-with-last (SF/types.go:660-663)
+                nd.pods.pop_back();
+                apply(x, pods[pod].spec, -1);
+                pods[pod].node = -1;
+                journal(J_REMOVE_POD, x, pod, slot, before);
+            }
+            for (int32_t t = k; t < e && pt.rc == CA_OK; t++) {    // AddPod of the copy (:79)
+                if (t + 16 < nm && ((mv[t + 16].node >> 6) & tm) == w) {
+                    __builtin_prefetch(&pods[(size_t)base + t + 16].spec);
+                    __builtin_prefetch(&nodes[mv[t + 16].node]);
+                }
+                const int32_t x = mv[t].node;
+                if (((x >> 6) & tm) != w) continue;
+                const int32_t nid = base + t;
+                NodeRow& nd = nodes[x];
+                uint64_t before[CA_PORT_WORDS];
+                std::memcpy(before, nd.ports, sizeof before);
+                apply(x, pods[nid].spec, +1);
+                nd.pods.push_back(nid);
+                pods[nid].node = x;
+                journal(J_ADD_POD, x, nid, (int32_t)nd.pods.size() - 1, before);
+            }
+            k = e;
+        }
+    });
+    tmark("rows");
+    for (Part& pt : part) {
+        if (pt.rc != CA_OK) return pt.rc;
+        n_ext_pods += pt.ext;
+        n_eph_pods += pt.eph;
+        n_scope_blockers += pt.blockers;
+        dirty_rows.insert(dirty_rows.end(), pt.dirty.begin(), pt.dirty.end());
+        if (journaled) journal.insert(journal.end(), pt.jr.begin(), pt.jr.end());
+    }
+    tmark("merged");
+    return CA_OK;
+}
+
 // plan_chain.hip: the whole loop as one device-resident chain (1 = ran, 0 = outside its scope)
 namespace casim {
 int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uint8_t* dest_mask,

@@ -160,8 +160,8 @@ struct PcBlk {
 constexpr int PC_SKY = 8;
 struct PcSkyV {
     int32_t* n;                   // [nb] points stored (-1 = unknown)
-    int32_t* c;                   // [PC_SKY][nb] cpu, descending within a block
-    int32_t* m;                   // [PC_SKY][nb] memory (MiB, rounded up), ascending
+    int32_t* c;                   // [PC_SKY][nb] cpu (points in no particular order)
+    int32_t* m;                   // [PC_SKY][nb] memory (MiB, rounded up)
     int32_t nb;
 };
 __host__ __device__ inline int32_t sky_c(int64_t v) {
@@ -256,35 +256,44 @@ __device__ inline uint32_t pc_wmax_u32(uint32_t v) {
 }
 
 // Rebuilds a block's skyline from its 64 rows as one wave holds them (lane i: row j*64 + i;
-// `valid`: visible, a free pod slot, not the candidate being simulated).  Extraction: the
-// largest (cpu, memory) key is a skyline point; every row with memory at most its memory is
-// dominated by it (its cpu is at most the point's); repeat on the rest.  The key's maximum
-// is two 32-bit wave maxima (cpu, then memory among the rows at that cpu; values biased so
-// that unsigned order is signed order and 0 means none).  C3 blocks hold 4-5 points on
-// average (p99 10), so a rebuild is a few wave reductions.
+// `valid`: visible, a free pod slot, not the candidate being simulated).  Extraction from
+// both ends of the staircase at once: the largest (cpu, memory) key is a skyline point (the
+// front), and so is the largest (memory, cpu) key (the back); every row with memory at most
+// the front's memory, or cpu at most the back's cpu, is dominated; repeat on the rest.  The
+// two ends' wave maxima are independent, so their latencies overlap: half the dependent
+// steps of a one-ended extraction.  Past PC_SKY - 1 exact points, one point bounds the
+// rest.  Keys are 32-bit images biased so that unsigned order is signed order (0: none).
+// C3 blocks hold 4-5 points on average (p99 10).
 __device__ void pc_sky_build(const PcSkyV sk, int32_t j, int64_t cc, int64_t cm, bool valid) {
     const int lane = threadIdx.x & 63;
     const int32_t C = sky_c(cc), M = sky_m(cm);
     const uint32_t Cu = (uint32_t)C ^ 0x80000000u, Mu = (uint32_t)M ^ 0x80000000u;
     bool alive = valid;
     int k = 0;
-    while (k < PC_SKY - 1) {
+    auto put = [&](int slot, uint32_t cu, uint32_t mu) {
+        if (lane == 0) { sk.c[slot * sk.nb + j] = (int32_t)(cu ^ 0x80000000u); sk.m[slot * sk.nb + j] = (int32_t)(mu ^ 0x80000000u); }
+    };
+    while (k <= PC_SKY - 3) {                        // room for two exact points and a bound
         if (!__ballot(alive)) break;
         const uint32_t cmax = pc_wmax_u32(alive ? Cu : 0u);
-        const uint32_t mmax = pc_wmax_u32((alive && Cu == cmax) ? Mu : 0u);
-        const int32_t pm = (int32_t)(mmax ^ 0x80000000u);
-        if (lane == 0) { sk.c[k * sk.nb + j] = (int32_t)(cmax ^ 0x80000000u); sk.m[k * sk.nb + j] = pm; }
-        k++;
-        alive = alive && M > pm;
+        const uint32_t mmax = pc_wmax_u32(alive ? Mu : 0u);
+        const uint32_t m_at = pc_wmax_u32((alive && Cu == cmax) ? Mu : 0u);   // front: (cmax, m_at)
+        const uint32_t c_at = pc_wmax_u32((alive && Mu == mmax) ? Cu : 0u);   // back: (c_at, mmax)
+        put(k++, cmax, m_at);
+        if (m_at != mmax) put(k++, c_at, mmax);      // (one point when the front is also the back)
+        alive = alive && Mu > m_at && Cu > c_at;
+    }
+    while (k < PC_SKY - 1) {                         // the last slots one point at a time
+        if (!__ballot(alive)) break;
+        const uint32_t cmax = pc_wmax_u32(alive ? Cu : 0u);
+        const uint32_t m_at = pc_wmax_u32((alive && Cu == cmax) ? Mu : 0u);
+        put(k++, cmax, m_at);
+        alive = alive && Mu > m_at;
     }
     if (k == PC_SKY - 1 && __ballot(alive)) {        // one point bounds the rest
         const uint32_t cmax = pc_wmax_u32(alive ? Cu : 0u);
         const uint32_t mmax = pc_wmax_u32(alive ? Mu : 0u);
-        if (lane == 0) {
-            sk.c[k * sk.nb + j] = (int32_t)(cmax ^ 0x80000000u);
-            sk.m[k * sk.nb + j] = (int32_t)(mmax ^ 0x80000000u);
-        }
-        k++;
+        put(k++, cmax, mmax);
     }
     if (lane == 0) sk.n[j] = k;
 }

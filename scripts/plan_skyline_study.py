@@ -107,6 +107,9 @@ def main():
                 e = int(v[: end + 1].sum())
                 ev += e
                 if len(idx):
+                    # blocks between the scan's first block and the fitting one
+                    d = (int(rot[idx[0]]) // 64 - int(rot[0]) // 64) % nb
+                    stats.setdefault("fit_block_dist", []).append(d)
                     tgt = int(rot[idx[0]])
                     L = (L + int(idx[0]) + 1) % N
                     stats["scan_ok"] += 1
@@ -135,6 +138,9 @@ def main():
         else:
             fc[:], fm[:], fp[:] = snap
     ss = np.array(stats.pop("sky_sizes"))
+    fd = np.array(stats.pop("fit_block_dist", [0]))
+    print("  fitting block distance (blocks after the scan's first): " +
+          "  ".join(f"{k}: {np.mean(fd == k):.3f}" for k in range(4)) + f"  >=4: {np.mean(fd >= 4):.3f}")
     print(f"C3 {N} nodes, limit {limit}: removed {removed}")
     for k, v in stats.items():
         print(f"  {k}: {v}")

@@ -148,6 +148,29 @@ int main(void) {
         CHECK(ca_estimate_plan_destroy(plan));
     }
 
+    /* ComputeExpansionOption: one-shot and with the node group resident (page-locked verdicts) */
+    {
+        int32_t samples[2] = {0, 999};
+        ca_template big = tmpl, small = tmpl;
+        small.node = node(400, 16 * GI, 110, -1001);        /* 400m free: a 500m pod does not fit */
+        ca_template ng[2] = {big, small};
+        uint8_t ok1[4];
+        CHECK(ca_check_templates(m, ps, samples, 2, ng, 2, NULL, ok1));
+        ca_expansion_plan* ep = NULL;
+        CHECK(ca_expansion_plan_create(m, ng, 2, &ep));
+        void* okb = NULL;
+        CHECK(ca_host_alloc(4, &okb));
+        uint8_t* ok2 = (uint8_t*)okb;
+        CHECK(ca_expansion_plan_run(ep, ps, samples, 2, NULL, ok2));
+        float kms = -1;
+        CHECK(ca_expansion_plan_kernel_ms(ep, &kms));
+        printf("expansion verdicts %d %d %d %d plan same %d\n", ok1[0], ok1[1], ok1[2], ok1[3],
+               memcmp(ok1, ok2, 4) == 0);
+        EXPECT(ok1[0] == 1 && ok1[1] == 1 && ok1[2] == 0 && ok1[3] == 0 && memcmp(ok1, ok2, 4) == 0 && kms >= 0);
+        CHECK(ca_host_free(okb));
+        CHECK(ca_expansion_plan_destroy(ep));
+    }
+
     /* kernel scope: a group with an out-of-scope pod stops the batch (prefix protocol) */
     pods[999].flags |= CA_POD_OUT_OF_SCOPE;
     ca_podset* ps2 = NULL;

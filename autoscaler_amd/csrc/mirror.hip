@@ -646,6 +646,16 @@ int ca_mirror::remap_hints_removed(int32_t pos, int32_t code, bool restore) {
 int ca_mirror::sync_nodes() {
     const size_t n = nodes.size();
     int rc;
+    static const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    struct Done {                                           // (CASIM_DEBUG_TIMING: the sync's size and time)
+        bool on; const std::chrono::steady_clock::time_point t0; size_t rows; bool full, stat;
+        ~Done() {
+            if (on)
+                fprintf(stderr, "[sync_nodes] %zu rows%s%s %.3f ms\n", rows, full ? " (full)" : "", stat ? " +static" : "",
+                        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        }
+    } done{dbg_t, t0, dirty_rows.size(), all_dirty, static_dirty};
     if (n > d_cap) {
         size_t cap = std::max<size_t>(n, std::max<size_t>(1024, d_cap * 2));
         if ((rc = d_hot.reserve(sizeof(NodeHot) * cap)) != CA_OK) return rc;
@@ -676,6 +686,9 @@ int ca_mirror::sync_nodes() {
         const size_t kcap = std::max<size_t>(k, std::max<size_t>(64, n / 4));   // the largest staged batch
         if ((rc = rs.h.reserve(sizeof(StagedRow) * kcap)) != CA_OK) return rc;
         if ((rc = rs.d.reserve(sizeof(StagedRow) * kcap)) != CA_OK) return rc;
+        if (dbg_t)
+            fprintf(stderr, "[sync_nodes]   staging reserved %.3f ms\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         StagedRow* sr = rs.h.as<StagedRow>();
         for (size_t j = 0; j < k; j++) {
             sr[j].row = dirty_rows[j];
@@ -686,6 +699,9 @@ int ca_mirror::sync_nodes() {
         hipLaunchKernelGGL(k_scatter_rows, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, stream,
                            rs.d.as<const StagedRow>(), (int32_t)k, d_hot.as<NodeHot>(), d_ext.as<NodeExt>());
         CA_HIP_CHECK(hipGetLastError());
+        if (dbg_t)
+            fprintf(stderr, "[sync_nodes]   staged + launched %.3f ms\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         CA_HIP_CHECK(hipStreamSynchronize(stream));        // the staging buffer is reused
     }
     if (static_dirty && n) {

@@ -388,7 +388,8 @@ def planner_leg(args, device: int, with_cpu: bool) -> dict:
         m = native.Mirror(device)                   # fresh: the copies' ids then match the port's
         W.load_sweep(m, w)
         ts, st, split = [], None, []
-        for _ in range(5):                          # the first run also uploads the snapshot
+        for _ in range(9):                          # the first run also uploads the snapshot; the median of
+                                                    # eight warm runs (a host stall of 10-40 ms hits one or two)
             m.fork()
             t = time.perf_counter()
             r = m.plan_removals(*args_, hints, 0, limit)
@@ -398,7 +399,8 @@ def planner_leg(args, device: int, with_cpu: bool) -> dict:
                 split.append(m.plan_chain_profile())
             m.revert()
             firsts.setdefault(limit, r)
-        out["runs"][str(limit)] = {"gpu_ms": float(np.median(ts[1:]) * 1e3), "path": st["path"], "rounds": st["rounds"],
+        out["runs"][str(limit)] = {"gpu_ms": float(np.median(ts[1:]) * 1e3), "min_ms": float(np.min(ts[1:]) * 1e3),
+                                   "path": st["path"], "rounds": st["rounds"],
                                    "conflicts": st["conflicts"], "simulated": st["simulated"],
                                    "removable": int(r.results["removable"].sum()),
                                    "candidates_run": int((r.results["reason"] != 101).sum()),
@@ -430,7 +432,7 @@ def planner_leg(args, device: int, with_cpu: bool) -> dict:
                                  and np.array_equal(ro.hints, g.hints) and ro.last_index == g.last_index)
         out["cpu_baseline"] = {"kind": "port", "cores": 1,
                                "sample": f"oracle/casim_oracle.c or_plan_removals, same loop, median of 3 runs (inside a "
-                                         f"reverted fork, as the GPU's median of 4), 1 thread of {cpu_model()}"}
+                                         f"reverted fork; the GPU's is the median of 8 warm runs), 1 thread of {cpu_model()}"}
     return out
 
 

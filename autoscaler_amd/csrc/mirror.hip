@@ -679,6 +679,11 @@ int ca_mirror::sync_nodes() {
         if (n) CA_HIP_CHECK(hipMemcpyAsync(d_hot.ptr, h, sizeof(NodeHot) * n, hipMemcpyHostToDevice, stream));
         if (n) CA_HIP_CHECK(hipMemcpyAsync(d_ext.ptr, e, sizeof(NodeExt) * n, hipMemcpyHostToDevice, stream));
         CA_HIP_CHECK(hipStreamSynchronize(stream));
+        // the staged path's buffers sized now, so the first partial sync (a revert's rows,
+        // the next loop) allocates nothing
+        const size_t kcap0 = std::max<size_t>(64, n / 4);
+        if ((rc = rs.h.reserve(sizeof(StagedRow) * kcap0)) != CA_OK) return rc;
+        if ((rc = rs.d.reserve(sizeof(StagedRow) * kcap0)) != CA_OK) return rc;
     } else if (!dirty_rows.empty()) {
         // few rows: stage them (row id + both columns) in pinned memory, one H2D copy, and
         // scatter them on the device

@@ -486,6 +486,12 @@ __device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) 
 // and the pod goes on to the scan like an unhinted one.
 constexpr uint32_t PC_QF_HINT_EVAL = 0x80000000u;
 
+#ifdef CASIM_PC_INLINE
+#define PC_PLAIN_RUN_ATTR __attribute__((always_inline)) inline
+#else
+#define PC_PLAIN_RUN_ATTR __attribute__((noinline))
+#endif
+
 // Scalars a plain run (pc_plain_run) shares with the simulation, in LDS.
 struct PcRun {
     int32_t Lw, adv, placed, failed;
@@ -504,7 +510,7 @@ static_assert(sizeof(PcRun) <= 128, "PcRun");
 // needs was spilled to vector lanes around every step; one call per run pays the
 // save/restore once.  Stops at the first pod that fits nowhere (failed = 1) or after R pods.
 template <bool EPH_COLS>
-__device__ __attribute__((noinline)) void pc_plain_run(unsigned char* pc_raw, int32_t n_, int32_t t0_, int32_t R_,
+__device__ PC_PLAIN_RUN_ATTR void pc_plain_run(unsigned char* pc_raw, int32_t n_, int32_t t0_, int32_t R_,
                                                        int64_t qc, int64_t qm, int64_t qe, uint32_t qf, int32_t qs,
                                                        PcTabs tabs) {
     const int lane = threadIdx.x & 63;

@@ -1647,6 +1647,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
                    int32_t* last_index, ca_plan_result* results, std::vector<ca_plan_move>& moves_out,
                    std::vector<std::pair<int32_t, int32_t>>& hint_sets, int32_t* simulated_out) {
     if (knob_env("CASIM_PLAN_SPECULATIVE")) return 0;
+    const auto t_entry = std::chrono::steady_clock::now();
     const int32_t N = (int32_t)m->nodes.size();
     if (N <= 0 || C <= 0) return 0;
     const int32_t M = move_off[C];
@@ -1726,6 +1727,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     const size_t o_mask = 4 * o;
     std::memcpy(reinterpret_cast<unsigned char*>(hw) + o_mask, dest_mask, (size_t)N);
     int32_t* const din = S.in.as<int32_t>();
+    const auto t_pack = std::chrono::steady_clock::now();
     CA_HIP_CHECK(hipMemcpyAsync(din, hw, o_mask + (size_t)N, hipMemcpyHostToDevice, st));
 
     // device work: the packed pods to move [M + 64], the copies [copy_cap]
@@ -1856,8 +1858,9 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
         ps.host_ms[3] = ms(t_kernel, t_read);    // moves, hints, budgets back
         ps.host_ms[4] = ms(t_read, t_end);       // replay into the mirror
         if (getenv("CASIM_DEBUG_TIMING"))
-            fprintf(stderr, "[plan chain] sync %.3f  launch+kernel %.3f (kernel %.3f)  readback %.3f  replay %.3f ms\n",
-                    ps.host_ms[0], ps.host_ms[1], ps.host_ms[2], ps.host_ms[3], ps.host_ms[4]);
+            fprintf(stderr, "[plan chain] checks %.3f  sync %.3f  pack %.3f  launch+kernel %.3f (kernel %.3f)  readback %.3f  "
+                    "replay %.3f ms (C %d, M %d, N %d)\n", ms(t_entry, t0), ps.host_ms[0], ms(t_sync, t_pack),
+                    ms(t_pack, t_kernel), ps.host_ms[2], ps.host_ms[3], ps.host_ms[4], C, M, N);
     }
     return 1;
 }

@@ -21,4 +21,6 @@ timeout -k 10 200 python -u scripts/plan_prof.py --prof > gpurun_out/plan_prof_b
 CASIM_LIB_PATH=$ALTP timeout -k 10 200 python -u scripts/plan_prof.py > gpurun_out/plan_prof_alt.log 2>&1 || { tail -20 gpurun_out/plan_prof_alt.log; exit 1; }
 echo "== prof base"; cat gpurun_out/plan_prof_base.log
 echo "== prof alt"; cat gpurun_out/plan_prof_alt.log
+CASIM_DEBUG_TIMING=1 timeout -k 10 200 python -u scripts/plan_prof.py > gpurun_out/plan_dbg.log 2>&1 || { tail -20 gpurun_out/plan_dbg.log; exit 1; }
+echo "== debug timing"; grep -E "^limit|plan chain|plan_args" gpurun_out/plan_dbg.log
 echo AB_OK

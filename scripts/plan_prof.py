@@ -48,4 +48,7 @@ for limit in (20, 200, 0):
               "sky {d:.0f} add {e:.0f}".format(a=pr["r_pod"] / pr["r_npods"], b=pr["r_win"] / pr["r_npods"],
                                               c=pr["r_blk"] / pr["r_npods"], d=pr["r_sky"] / pr["r_npods"],
                                               e=pr["r_add"] / pr["r_npods"], **pr), flush=True)
+    t = time.perf_counter()
+    native.plan_args(*args, hints)
+    print(f"   plan_args (the wrapper's marshalling) {(time.perf_counter() - t) * 1e3:.3f} ms", flush=True)
     m.close()

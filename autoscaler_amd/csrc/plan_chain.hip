@@ -486,10 +486,16 @@ __device__ void pc_helper(const PcArgs& a, unsigned char* pc_raw, int h, int H) 
 // and the pod goes on to the scan like an unhinted one.
 constexpr uint32_t PC_QF_HINT_EVAL = 0x80000000u;
 
-#ifdef CASIM_PC_INLINE
-#define PC_PLAIN_RUN_ATTR __attribute__((always_inline)) inline
-#else
+// The plain run is inlined: as a call, its entry waited for every memory operation in
+// flight (the ABI's s_waitcnt at function entry: the next candidate's prefetched pods, the
+// copies' records), its PcTabs argument went through scratch and its callee-saved registers
+// were saved and restored in scratch — ≈ 3.7k cycles per call, 13 % of the limit-200 kernel
+// (1.59 -> 1.38 ms) and 6 % without a limit (51.6 -> 48.4 ms).  CASIM_PC_NOINLINE builds
+// the call for comparison.
+#ifdef CASIM_PC_NOINLINE
 #define PC_PLAIN_RUN_ATTR __attribute__((noinline))
+#else
+#define PC_PLAIN_RUN_ATTR __attribute__((always_inline)) inline
 #endif
 
 // Scalars a plain run (pc_plain_run) shares with the simulation, in LDS.
@@ -505,10 +511,9 @@ static_assert(sizeof(PcRun) <= 128, "PcRun");
 // affinity) of one candidate, one pod after another: rotating first fit from lastIndex over
 // the committed rows (schedulerbased.go:114-131), the block skylines skipping blocks that
 // cannot fit the pod, AddPod of each placement (cluster.go:79).  Lane i holds pod t0 + i's
-// requests; destinations go to pdest[t0 + k] (LDS).  Out of line on purpose: the loop's
-// working set is small, and inside the simulation's register budget the scalar state it
-// needs was spilled to vector lanes around every step; one call per run pays the
-// save/restore once.  Stops at the first pod that fits nowhere (failed = 1) or after R pods.
+// requests; destinations go to pdest[t0 + k] (LDS).  Its state crosses in the PcRun record
+// (LDS) and its loop state is re-asserted uniform at every pod, so the inlined loop keeps
+// it in scalars.  Stops at the first pod that fits nowhere (failed = 1) or after R pods.
 template <bool EPH_COLS>
 __device__ PC_PLAIN_RUN_ATTR void pc_plain_run(unsigned char* pc_raw, int32_t n_, int32_t t0_, int32_t R_,
                                                        int64_t qc, int64_t qm, int64_t qe, uint32_t qf, int32_t qs,

@@ -112,6 +112,7 @@ def c4_leg(args, device: int, with_cpu: bool) -> dict:
             plan.run(w.max_nodes, 0, copy=False, device_results=True)
         ts = []
         for _ in range(max(args.steps, 5)):
+            r = None                  # (the previous result is freed outside the timing)
             t = time.perf_counter()
             r = plan.run(w.max_nodes, 0, copy=False, device_results=True)     # results in HBM, as the C2 line
             ts.append(time.perf_counter() - t)
@@ -124,6 +125,7 @@ def c4_leg(args, device: int, with_cpu: bool) -> dict:
         import pyoracle                                           # CPU baseline leg only
         o = pyoracle.OracleState()
         W.load_estimate(o, w)
+        ro = None                  # (the previous result is freed outside the timing)
         t = time.perf_counter()
         ro = o.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, 0)
         cpu_ms = (time.perf_counter() - t) * 1e3
@@ -165,6 +167,7 @@ def expansion_leg(args, device: int, with_cpu: bool) -> dict:
             call()                                                         # warm-up
             ts = []
             for _ in range(max(args.steps, 5)):
+                res = None                  # (the previous result is freed outside the timing)
                 t = time.perf_counter()
                 res = call()
                 ts.append(time.perf_counter() - t)
@@ -181,6 +184,7 @@ def expansion_leg(args, device: int, with_cpu: bool) -> dict:
                 call()
                 ts, ks = [], []
                 for _ in range(max(args.steps, 5)):
+                    r2 = None                  # (the previous result is freed outside the timing)
                     t = time.perf_counter()
                     r2 = call()
                     ts.append(time.perf_counter() - t)
@@ -199,6 +203,7 @@ def expansion_leg(args, device: int, with_cpu: bool) -> dict:
             import pyoracle                                           # CPU baseline leg only
             o = pyoracle.OracleState()
             W.load_estimate(o, w)
+            ro = None                  # (the previous result is freed outside the timing)
             t = time.perf_counter()
             ro = o.check_templates(w.table, samples, w.templates)
             cpu_ms = (time.perf_counter() - t) * 1e3
@@ -281,6 +286,7 @@ def filter_leg(args, device: int, with_cpu: bool) -> dict:
         ts, ks = [], []
         for rep in range(1 + max(3, min(args.steps, 5))):
             g.fork()
+            rg = None                  # (the previous result is freed outside the timing)
             t = time.perf_counter()
             rg = g.filter_out_schedulable(w.pending, w.order, w.class_owner, w.hints, 0)
             dt = (time.perf_counter() - t) * 1e3
@@ -300,6 +306,7 @@ def filter_leg(args, device: int, with_cpu: bool) -> dict:
             o = pyoracle.OracleState()
             W.load_filter(o, w)
             o.fork()
+            ro = None                  # (the previous result is freed outside the timing)
             t = time.perf_counter()
             ro = o.filter_out_schedulable(w.pending, w.order, w.class_owner, w.hints, 0)
             cpu_ms = (time.perf_counter() - t) * 1e3
@@ -337,6 +344,7 @@ def sweep_leg(args, device: int, with_cpu: bool) -> dict:
             for it in range(max(args.warmup, 3) + max(args.steps, 10)):
                 if mode == "fresh":
                     m.set_hints(fresh_h)
+                r = None                  # (the previous result is freed outside the timing)
                 t = time.perf_counter()
                 r = plan.run(0)
                 if it >= max(args.warmup, 3):
@@ -354,6 +362,7 @@ def sweep_leg(args, device: int, with_cpu: bool) -> dict:
         for mode in ("fresh", "hinted"):
             cts = []
             for _ in range(3):                                    # median, as on the GPU side
+                ro = None                  # (the previous result is freed outside the timing)
                 t = time.perf_counter()
                 ro = o.find_nodes_to_remove(*sweep_args, h, 0)
                 cts.append(time.perf_counter() - t)
@@ -391,6 +400,7 @@ def planner_leg(args, device: int, with_cpu: bool) -> dict:
         for _ in range(9):                          # the first run also uploads the snapshot; the median of
                                                     # eight warm runs (a host stall of 10-40 ms hits one or two)
             m.fork()
+            r = None                  # (the previous result is freed outside the timing)
             t = time.perf_counter()
             r = m.plan_removals(*args_, hints, 0, limit)
             ts.append(time.perf_counter() - t)
@@ -419,6 +429,7 @@ def planner_leg(args, device: int, with_cpu: bool) -> dict:
             cts, ro = [], None
             for _ in range(3):                                    # median, as on the GPU side
                 o.fork()
+                r1 = None                  # (the previous result is freed outside the timing)
                 t = time.perf_counter()
                 r1 = o.plan_removals(*args_, hints, 0, limit)
                 cts.append(time.perf_counter() - t)
@@ -514,6 +525,7 @@ def c2_unlimited_leg(args, device: int, with_cpu: bool) -> dict:
         plan.run(0, 0, want_nodes=False, copy=False)
         ts = []
         for _ in range(max(3, min(args.steps, 5))):
+            r = None                  # (the previous result is freed outside the timing)
             t = time.perf_counter()
             r = plan.run(0, 0, want_nodes=False, copy=False)
             ts.append(time.perf_counter() - t)
@@ -540,6 +552,7 @@ def c2_unlimited_leg(args, device: int, with_cpu: bool) -> dict:
         W.load_estimate(o, w)
         g = 3                                                     # bounded sample: the first groups
         off = w.group_off[: g + 1]
+        ro = None                  # (the previous result is freed outside the timing)
         t = time.perf_counter()
         ro = o.estimate(w.table, off, w.pod_idx[: off[-1]], w.templates[:g], 0, 0)
         cpu_s = time.perf_counter() - t

@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
 #include <cstdio>
@@ -89,6 +90,8 @@ struct PcArgs {
     PcPod* ex_pods;               // copies committed onto a node, as their later candidacy reads them
     ca_plan_result* res;          // (results, moves and info: page-locked host memory, written in place)
     ca_plan_move* moves;
+    int32_t* published;           // moves written out so far (page-locked): the host replays them
+                                  // into the mirror while the chain runs
     int64_t* info;                // [0] lastIndex, [1] moves, [2] removed, [3] candidates simulated,
                                   // [4..4+PC_NPROF) phase cycle counters (PC_* above), [4+PC_NPROF] the
                                   // first candidate not run (C: none; the host fills their results)
@@ -794,8 +797,14 @@ static_assert(sizeof(PcCtx) <= 512, "PcCtx (pc_layout ctx)");
 __device__ inline void pc_flush_moves(const PcArgs& a, const ca_plan_move* mvbuf, PcCtx* ctx, int lane) {
     const int32_t k = __builtin_amdgcn_readfirstlane(ctx->mv_n), first = __builtin_amdgcn_readfirstlane(ctx->mv_first);
     for (int32_t i = lane; i < k; i += 64) a.moves[first + i] = mvbuf[i];
+    // the records reach host memory before the count that publishes them (whole candidates:
+    // a flush follows a Commit)
+    __threadfence_system();
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0) { ctx->mv_first = first + k; ctx->mv_n = 0; }
+    if (lane == 0) {
+        ctx->mv_first = first + k; ctx->mv_n = 0;
+        __hip_atomic_store(a.published, first + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -1746,19 +1755,22 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     // outputs, written by the kernel straight into page-locked memory (no copies, one sync):
     // results [C], info [PC_INFO], moves [copy_cap], the caller's pods' hints by move index [M]
     const size_t out_bytes = sizeof(ca_plan_result) * C + PC_INFO * sizeof(int64_t) + sizeof(ca_plan_move) * copy_cap +
-                             sizeof(int32_t) * (size_t)std::max(M, 1);
+                             sizeof(int32_t) * (size_t)std::max(M, 1) + 64;
     if ((rc = S.h_out.reserve(out_bytes)) != CA_OK) return rc;
     ca_plan_result* const hres = S.h_out.as<ca_plan_result>();
     int64_t* const hinfo = reinterpret_cast<int64_t*>(hres + C);
     ca_plan_move* const hmoves = reinterpret_cast<ca_plan_move*>(hinfo + PC_INFO);
     int32_t* const hhout = reinterpret_cast<int32_t*>(hmoves + copy_cap);
     std::memcpy(hhout, hw + o_hm, sizeof(int32_t) * (size_t)M);     // unchanged unless Hints.Set
+    int32_t* const hpub = hhout + std::max(M, 1);                      // moves published so far
+    __atomic_store_n(hpub, 0, __ATOMIC_RELAXED);
     void* dout = nullptr;
     CA_HIP_CHECK(hipHostGetDevicePointer(&dout, S.h_out.ptr, 0));
     ca_plan_result* const dres = static_cast<ca_plan_result*>(dout);
     int64_t* const dinfo = reinterpret_cast<int64_t*>(dres + C);
     ca_plan_move* const dmoves = reinterpret_cast<ca_plan_move*>(dinfo + PC_INFO);
     int32_t* const dhout = reinterpret_cast<int32_t*>(dmoves + copy_cap);
+    int32_t* const dpub = dhout + std::max(M, 1);
 
     PcArgs A;
     A.hot = m->d_hot.as<NodeHot>();
@@ -1785,6 +1797,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     A.ex_pods = dex;
     A.res = dres;
     A.moves = dmoves;
+    A.published = dpub;
     A.info = dinfo;
     A.L0 = *last_index;
     A.copy_cap = copy_cap;
@@ -1813,6 +1826,32 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     CA_HIP_CHECK(hipGetLastError());
     CA_HIP_CHECK(hipEventRecord(m->ev1, st));
     if (P > 0) CA_HIP_CHECK(hipMemcpyAsync(hw + o_al, din + o_al, 4 * (size_t)P, hipMemcpyDeviceToHost, st));
+    // ---- replay the committed moves into the mirror (journaled at the caller's depth) while
+    // the chain runs: it publishes each flushed batch of whole candidates' moves through *hpub
+    // (cluster.go:228-240, :79) ----
+    int32_t replayed = 0;
+    float replay_ms = 0;
+    auto replay_upto = [&](int32_t upto) -> int {
+        const auto tr = std::chrono::steady_clock::now();
+        const int e = m->replay_moves(hmoves + replayed, upto - replayed);
+        replay_ms += std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - tr).count();
+        replayed = upto;
+        return e;
+    };
+    for (;;) {
+        const int32_t pub = __atomic_load_n(hpub, __ATOMIC_ACQUIRE);
+        if (pub > replayed && pub <= copy_cap) {
+            if ((rc = replay_upto(pub)) != CA_OK) {
+                (void)hipStreamSynchronize(st);           // (the chain still writes into the buffers)
+                return rc;
+            }
+            continue;
+        }
+        const hipError_t q = hipStreamQuery(st);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) CA_HIP_CHECK(q);
+        std::this_thread::yield();
+    }
     CA_HIP_CHECK(hipStreamSynchronize(st));
     const auto t_kernel = std::chrono::steady_clock::now();
     if (tr_env) {
@@ -1827,7 +1866,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     }
     const int32_t nm = (int32_t)hinfo[1];
     const int32_t stop_c = (int32_t)hinfo[4 + PC_NPROF];
-    if (nm < 0 || nm > copy_cap || stop_c < 0 || stop_c > C) {
+    if (nm < replayed || nm > copy_cap || stop_c < 0 || stop_c > C) {
         set_last_error("plan chain: move count out of range");
         return CA_EDEVICE;
     }
@@ -1844,11 +1883,11 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
         for (int32_t i = 0; i < move_off[stop_c]; i++)
             if (hhout[i] != hw[o_hm + i]) hint_sets.emplace_back(move_pods[i], hhout[i]);
     if (P > 0) std::memcpy(pdbs->allowed, hw + o_al, 4 * (size_t)P);
-    moves_out.assign(hmoves, hmoves + nm);
     const auto t_read = std::chrono::steady_clock::now();
-    // ---- replay the committed moves into the mirror (journaled at the caller's depth) ----
-    if ((rc = m->replay_moves(moves_out.data(), nm)) != CA_OK) return rc;     // cluster.go:228-240, :79
+    const float overlapped_ms = replay_ms;
+    if (nm > replayed && (rc = replay_upto(nm)) != CA_OK) return rc;        // the rest (the last flush)
     const auto t_end = std::chrono::steady_clock::now();
+    moves_out.assign(hmoves, hmoves + nm);
     {
         PlanStats& ps = m->plan;
         auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
@@ -1861,11 +1900,11 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
         ps.host_ms[1] = ms(t_sync, t_kernel);    // inputs, kernel, results back
         ps.host_ms[2] = kms;                     // the kernel (events)
         ps.host_ms[3] = ms(t_kernel, t_read);    // moves, hints, budgets back
-        ps.host_ms[4] = ms(t_read, t_end);       // replay into the mirror
+        ps.host_ms[4] = ms(t_read, t_end);       // replay into the mirror after the chain (the rest overlapped it)
         if (getenv("CASIM_DEBUG_TIMING"))
             fprintf(stderr, "[plan chain] checks %.3f  sync %.3f  pack %.3f  launch+kernel %.3f (kernel %.3f)  readback %.3f  "
-                    "replay %.3f ms (C %d, M %d, N %d)\n", ms(t_entry, t0), ps.host_ms[0], ms(t_sync, t_pack),
-                    ms(t_pack, t_kernel), ps.host_ms[2], ps.host_ms[3], ps.host_ms[4], C, M, N);
+                    "replay %.3f ms after the chain, %.3f ms beside it (C %d, M %d, N %d)\n", ms(t_entry, t0), ps.host_ms[0],
+                    ms(t_sync, t_pack), ms(t_pack, t_kernel), ps.host_ms[2], ps.host_ms[3], ps.host_ms[4], overlapped_ms, C, M, N);
     }
     return 1;
 }

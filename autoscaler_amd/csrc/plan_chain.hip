@@ -160,7 +160,10 @@ struct PcBlk {
 // Stored point-major across blocks (c[i * nb + j]: point i of block j), so the window test —
 // lane q checks block q — reads every point with one conflict-free access per lane, all of
 // them issued at once.
-constexpr int PC_SKY = 8;
+#ifndef CASIM_PC_SKY
+#define CASIM_PC_SKY 8
+#endif
+constexpr int PC_SKY = CASIM_PC_SKY;
 struct PcSkyV {
     int32_t* n;                   // [nb] points stored (-1 = unknown)
     int32_t* c;                   // [PC_SKY][nb] cpu (points in no particular order)
@@ -606,6 +609,7 @@ __device__ PC_PLAIN_RUN_ATTR void pc_plain_run(unsigned char* pc_raw, int32_t n_
         const bool taint_all = (pf & PF_TAINT_MASK_ALL) != 0;
         if (pf & PC_QF_HINT_EVAL) evals += 1;        // the CheckPredicates of a hint it cannot take
         const int32_t j0 = Lw >> 6, l0 = Lw & 63;
+        bool skip0 = false;                       // pod k fits no row of the cached block from l0 on
         // Fast path: a batch of pods whose first fits lie in the cached block (the block of the
         // previous placement), each past the previous one's.  Within the batch every pod's scan
         // starts past the rows the batch has taken (lastIndex = target + 1), so its fit test
@@ -640,6 +644,7 @@ __device__ PC_PLAIN_RUN_ATTR void pc_plain_run(unsigned char* pc_raw, int32_t n_
                     const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)FL[q]);
                     if (bf & PF_ALL_ZERO) { go = false; break; }                  // (pod k: not all_zero)
                     const uint64_t fitm = F[q] & (~0ull << l);
+                    if (kk == k && !fitm) skip0 = true;   // (the scan's first block: no fit, known)
                     const uint64_t first = fitm & (0ull - fitm);
                     if (!first || (first & ((bf & PF_TAINT_MASK_ALL) ? 0ull : taint_))) { go = false; break; }
                     P |= first;
@@ -680,7 +685,10 @@ __device__ PC_PLAIN_RUN_ATTR void pc_plain_run(unsigned char* pc_raw, int32_t n_
         int32_t target = -1, wr = -1, my_nv = 0;
         uint64_t passm = 0;
         PR_MARK(0);
-        for (int32_t rr = 0; rr <= nb; rr++) {
+        // the batch attempt already tested the scan's first block (the cached one) for pod k
+        skip0 = __builtin_amdgcn_readfirstlane((int)skip0) != 0;
+        if (skip0) evals += (uint64_t)__popcll(cvis & (~0ull << l0));
+        for (int32_t rr = skip0 ? 1 : 0; rr <= nb; rr++) {
             rr = __builtin_amdgcn_readfirstlane(rr);
             wr = __builtin_amdgcn_readfirstlane(wr);
             cj = __builtin_amdgcn_readfirstlane(cj);

@@ -1750,7 +1750,12 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     std::memcpy(reinterpret_cast<unsigned char*>(hw) + o_mask, dest_mask, (size_t)N);
     int32_t* const din = S.in.as<int32_t>();
     const auto t_pack = std::chrono::steady_clock::now();
+    const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
+    hipEvent_t dev[3] = {nullptr, nullptr, nullptr};            // (CASIM_DEBUG_TIMING: H2D and pack times)
+    if (dbg_t) for (auto& e : dev) if (hipEventCreate(&e) != hipSuccess) e = nullptr;
+    if (dev[0]) (void)hipEventRecord(dev[0], st);
     CA_HIP_CHECK(hipMemcpyAsync(din, hw, o_mask + (size_t)N, hipMemcpyHostToDevice, st));
+    if (dev[1]) (void)hipEventRecord(dev[1], st);
 
     // device work: the packed pods to move [M + 64], the copies [copy_cap]
     const size_t w_bytes = sizeof(PcPod) * ((size_t)M + 64) + sizeof(PcPod) * (size_t)copy_cap;
@@ -1760,6 +1765,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     hipLaunchKernelGGL(k_plan_pack, dim3((unsigned)((M + 64 + 255) / 256)), dim3(256), 0, st, din + o_mv, M,
                        m->d_pods.hot.as<PodHot>(), (const int32_t*)(din + o_hm), dpods);
     CA_HIP_CHECK(hipGetLastError());
+    if (dev[2]) (void)hipEventRecord(dev[2], st);
     // outputs, written by the kernel straight into page-locked memory (no copies, one sync):
     // results [C], info [PC_INFO], moves [copy_cap], the caller's pods' hints by move index [M]
     const size_t out_bytes = sizeof(ca_plan_result) * C + PC_INFO * sizeof(int64_t) + sizeof(ca_plan_move) * copy_cap +
@@ -1909,7 +1915,16 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
         ps.host_ms[2] = kms;                     // the kernel (events)
         ps.host_ms[3] = ms(t_kernel, t_read);    // moves, hints, budgets back
         ps.host_ms[4] = ms(t_read, t_end);       // replay into the mirror after the chain (the rest overlapped it)
-        if (getenv("CASIM_DEBUG_TIMING"))
+        if (dbg_t && dev[0] && dev[1] && dev[2]) {
+            float h2d = 0, pk = 0, gap = 0;
+            (void)hipEventElapsedTime(&h2d, dev[0], dev[1]);
+            (void)hipEventElapsedTime(&pk, dev[1], dev[2]);
+            (void)hipEventElapsedTime(&gap, dev[2], m->ev0);
+            fprintf(stderr, "[plan chain] device: H2D %.3f (%zu B)  pack %.3f  to the chain %.3f ms\n", h2d,
+                    o_mask + (size_t)N, pk, gap);
+        }
+        for (auto& e : dev) if (e) (void)hipEventDestroy(e);
+        if (dbg_t)
             fprintf(stderr, "[plan chain] checks %.3f  sync %.3f  pack %.3f  launch+kernel %.3f (kernel %.3f)  readback %.3f  "
                     "replay %.3f ms after the chain, %.3f ms beside it (C %d, M %d, N %d)\n", ms(t_entry, t0), ps.host_ms[0],
                     ms(t_sync, t_pack), ms(t_pack, t_kernel), ps.host_ms[2], ps.host_ms[3], ps.host_ms[4], overlapped_ms, C, M, N);

@@ -284,10 +284,13 @@ int plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const uint
     ps.rounds = ps.conflicts = ps.simulated = 0;
     ps.moves.clear();
     if (C > 0 && (move_off[0] != 0)) return CA_EINVAL;
-    for (int32_t c = 0; c < C; c++) {
+    for (int32_t c = 0; c < C; c++)
         if (move_off[c + 1] < move_off[c]) return CA_EINVAL;
-        for (int32_t i = move_off[c]; i < move_off[c + 1]; i++)
-            if (move_pods[i] < 0 || move_pods[i] >= n_pods) return CA_EINVAL;
+    {   // every pod to move names a mirror pod (one flat pass: the offsets ascend)
+        uint32_t bad = 0;
+        const int32_t M = C > 0 ? move_off[C] : 0;
+        for (int32_t i = 0; i < M; i++) bad |= (uint32_t)((uint32_t)move_pods[i] >= (uint32_t)n_pods);
+        if (bad) return CA_EINVAL;
     }
     {   // the planner walks unique node names (planner.go:261)
         std::vector<uint8_t> seen((size_t)std::max(N, 1), 0);

@@ -1043,7 +1043,7 @@ __global__ void __launch_bounds__(256) k_emit_bucket(const GroupMeta* __restrict
 
 // 4. the First-Fit-Decreasing chain -------------------------------------------
 #ifdef CASIM_PROF   // section cycle counters of k_ffd_chain (profiling build only)
-constexpr int NPROF = 12;
+constexpr int NPROF = 15;   // + [12] loop top (window moves, head reads), [13] epilogue, [14] before the loop
 __device__ unsigned long long g_chain_prof[1024][NPROF];
 #define PROF_T(v) const uint64_t v = clock64()
 #define PROF_ADD(i, t) prof[i] += clock64() - (t)
@@ -1601,7 +1601,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
 #endif
     uint32_t n_single = 0;
 #ifdef CASIM_PROF
-    uint64_t prof[NPROF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t prof[NPROF] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1709,7 +1709,11 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     };
 
     int32_t pos = 0;
+#ifdef CASIM_PROF
+    prof[14] = clock64() - t_cyc0;
+#endif
     while (pos < P && !stop) {
+        PROF_T(t_top);
         if (pos >= wbase + 64) {
             if (pend) {
                 so_pod[out_idx] = pos_out ? wbase + lane : cur.pod;
@@ -1739,6 +1743,10 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
         const int32_t pidx = rl32(cur.pod, sl);
         const uint32_t sf = (uint32_t)rl32((int32_t)cur.flags, sl);
         const bool zero = (sf & SF_ZERO) != 0;
+#ifdef CASIM_PROF
+        __builtin_amdgcn_s_waitcnt(0);       // (profiling: the head's loads land here, not in the run)
+#endif
+        PROF_ADD(12, t_top);
 
         // ---------------- a run of identical resource-only pods ----------------
         if (batch_runs && (sf & (SF_BATCH | SF_HEAD)) == (SF_BATCH | SF_HEAD)) {
@@ -2292,6 +2300,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
         progress();
         cbar<GROWS>();                        // the placement is visible to every wave
     }
+    PROF_T(t_epi);
     if (pend) {
         so_pod[out_idx] = pos_out ? wbase + lane : cur.pod;
         if (so_node) so_node[out_idx] = out_node;
@@ -2326,6 +2335,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     }
     if (tid == 0) {
 #ifdef CASIM_PROF
+        prof[13] = clock64() - t_epi;
         prof[5] = clock64() - t_cyc0;
         if (g < 1024) for (int i = 0; i < NPROF; i++) g_chain_prof[g][i] = prof[i];
 #endif
@@ -2888,6 +2898,15 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     if (sched16 && (sched_pod || sched_node || p->s->h_pods.size() > 65535)) return CA_EINVAL;
     p->pub_state = 0;
     const auto t_start = std::chrono::steady_clock::now();
+    // CASIM_STEP_TIMING (read once per process): host-side split of the steps, averaged over
+    // 20 calls — entry to the first launch, to the last launch, to the join, to the return,
+    // and the caller's time between a return and the next entry
+    static const bool step_timing = getenv("CASIM_STEP_TIMING") != nullptr;
+    static double st_acc[6] = {0, 0, 0, 0, 0, 0};
+    static int st_n = 0;
+    static std::chrono::steady_clock::time_point st_last_exit;
+    std::chrono::steady_clock::time_point st_t[4];
+    auto st_mark = [&](int k) { if (step_timing) st_t[k] = std::chrono::steady_clock::now(); };
     CA_HIP_CHECK(hipSetDevice(m->device));
     const int32_t n_base = (int32_t)m->nodes.size();
     if (G == 0) return CA_OK;
@@ -2984,6 +3003,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                    p->d_sortC.as<uint32_t>(), p->d_spod_go.as<int32_t>(),
                                    p->d_ids_ready.as<int32_t>(), p->ids_epoch, fold ? NP : 0)) != CA_OK)
             return rc0;
+        st_mark(0);
         // (ev_ids is recorded on st3 once the heavy chains are queued: the host's launches
         // ahead of them pace the step's start)
     }
@@ -3314,9 +3334,11 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         }
         if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_COMPACT], st));
         // (polling the events with hipEventQuery instead measured the same: 0.486 ms)
+        if (rounds == 1) st_mark(1);
         if (host_joins && pub_ran) CA_HIP_CHECK(hipEventSynchronize(p->ev_pub));   // (finishes last)
         CA_HIP_CHECK(hipEventSynchronize(p->ev_rb));
         if (light_pending) { CA_HIP_CHECK(hipEventSynchronize(p->ev_b)); light_pending = false; }
+        if (rounds == 1) st_mark(2);
         if (publish && p->h_qc.as<int32_t>()[2] != 0) pub_gave_up = true;
         float ms = 0;
         if (p->phase_events)
@@ -3464,6 +3486,26 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     p->stats.sort_ms = sort_ms;
     p->stats.total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     p->t_ms[6] = p->stats.total_ms;
+    if (step_timing) {
+        const auto t_exit = std::chrono::steady_clock::now();
+        auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return std::chrono::duration<double, std::micro>(b - a).count();
+        };
+        st_acc[0] += us(t_start, st_t[0]);
+        st_acc[1] += us(st_t[0], st_t[1]);
+        st_acc[2] += us(st_t[1], st_t[2]);
+        st_acc[3] += us(st_t[2], t_exit);
+        if (st_n > 0) st_acc[4] += us(st_last_exit, t_start);
+        st_acc[5] += us(t_start, t_exit);
+        st_last_exit = t_exit;
+        if (++st_n == 20) {
+            fprintf(stderr, "[step] us per call: to the sort launch %.1f, to the last launch %.1f, join wait %.1f, "
+                    "to the return %.1f, caller between calls %.1f, call %.1f\n", st_acc[0] / 20, st_acc[1] / 20,
+                    st_acc[2] / 20, st_acc[3] / 20, st_acc[4] / 19, st_acc[5] / 20);
+            for (double& v : st_acc) v = 0;
+            st_n = 0;
+        }
+    }
     return CA_OK;
 }
 

@@ -28,9 +28,9 @@ if os.environ.get("CASIM_LIB_PATH", "").endswith("libcasim_prof.so"):
     import ctypes as C
     lib = native.load()
     G = len(w.templates)
-    buf = np.zeros((G, 12), np.uint64)
+    buf = np.zeros((G, 15), np.uint64)
     lib.ca_debug_chain_prof(buf.ctypes.data_as(C.POINTER(C.c_uint64)), G)
-    names = ["run_end", "capa", "revol", "update", "open", "total", "n_rev", "n_runs", "prologue", "post_bar", "exhausted", "run_total"]
+    names = ["run_end", "capa", "revol", "update", "open", "total", "n_rev", "n_runs", "prologue", "post_bar", "exhausted", "run_total", "loop_top", "epilogue", "pre_loop"]
     for g in order[:6]:
         print(f"g{g:3d} " + " ".join(f"{n}={int(v)}" for n, v in zip(names, buf[g])))
 

@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(256) k_plan_pack(const int32_t* __restrict__ m
         const int32_t id = move_pods[i];
         const PodHot p = ph[id];
         r.cpu = p.cpu; r.mem = p.mem; r.eph = p.eph;
-        r.id = id; r.hint = hint_move[i]; r.spec = p.spec; r.orig = id;
+        r.id = id; r.hint = hint_move ? hint_move[i] : -1; r.spec = p.spec; r.orig = id;
         // moved-pod semantics (cluster.go:235-240 clears Spec.NodeName, tpu.go:57-79 the TPU requests)
         uint32_t f = p.flags & ~(PF_NODE_NAME | PF_ALL_ZERO | PF_SCALAR_REQ | PF_HAS_SCALAR_KEYS);
         if (p.flags & PF_MOVED_ALL_ZERO) f |= PF_ALL_ZERO;
@@ -1724,7 +1724,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     const size_t n_pdb_members = P > 0 ? (size_t)pdbs->pod_off[n_pods] : 0;
     const size_t in_words = (size_t)C + C + (C + 1) + std::max(M, 1) + (N + 1) + (P > 0 ? (size_t)n_pods + 1 : 1) +
                             std::max<size_t>(n_pdb_members, 1) + std::max(P, 1) + std::max(M, 1);
-    const size_t in_bytes = 4 * in_words + ((size_t)N + 15) / 16 * 16;
+    const size_t in_bytes = 4 * in_words + ((size_t)N + 15) / 16 * 16 + 16;      // (+ the hints' alignment)
     if ((rc = S.in.reserve(in_bytes)) != CA_OK) return rc;
     if ((rc = S.h_in.reserve(in_bytes)) != CA_OK) return rc;
     int32_t* hw = S.h_in.as<int32_t>();
@@ -1744,17 +1744,24 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     const size_t o_pof = put(P > 0 ? pdbs->pod_off : nullptr, P > 0 ? n_pods + 1 : 0, P > 0 ? (size_t)n_pods + 1 : 1);
     const size_t o_pp = put(P > 0 ? pdbs->pod_pdb : nullptr, n_pdb_members, std::max<size_t>(n_pdb_members, 1));
     const size_t o_al = put(P > 0 ? pdbs->allowed : nullptr, P, std::max(P, 1));
-    const size_t o_hm = put(nullptr, 0, std::max(M, 1));
-    for (int32_t i = 0; i < M; i++) hw[o_hm + i] = hints ? hints[move_pods[i]] : -1;
     const size_t o_mask = 4 * o;
     std::memcpy(reinterpret_cast<unsigned char*>(hw) + o_mask, dest_mask, (size_t)N);
+    // the hints by move index last: not uploaded when none is set (a fresh loop's)
+    const size_t o_hm = (o_mask + (size_t)N + 15) / 16 * 4;
+    int32_t any_hint = 0;
+    for (int32_t i = 0; i < M; i++) {
+        const int32_t h = hints ? hints[move_pods[i]] : -1;
+        hw[o_hm + i] = h;
+        any_hint |= h + 1;                      // (hints are >= -1)
+    }
+    const size_t up_bytes = any_hint ? 4 * (o_hm + (size_t)std::max(M, 1)) : o_mask + (size_t)N;
     int32_t* const din = S.in.as<int32_t>();
     const auto t_pack = std::chrono::steady_clock::now();
     const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
     hipEvent_t dev[3] = {nullptr, nullptr, nullptr};            // (CASIM_DEBUG_TIMING: H2D and pack times)
     if (dbg_t) for (auto& e : dev) if (hipEventCreate(&e) != hipSuccess) e = nullptr;
     if (dev[0]) (void)hipEventRecord(dev[0], st);
-    CA_HIP_CHECK(hipMemcpyAsync(din, hw, o_mask + (size_t)N, hipMemcpyHostToDevice, st));
+    CA_HIP_CHECK(hipMemcpyAsync(din, hw, up_bytes, hipMemcpyHostToDevice, st));
     if (dev[1]) (void)hipEventRecord(dev[1], st);
 
     // device work: the packed pods to move [M + 64], the copies [copy_cap]
@@ -1763,7 +1770,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     PcPod* const dpods = S.work.as<PcPod>();
     PcPod* const dex = dpods + M + 64;
     hipLaunchKernelGGL(k_plan_pack, dim3((unsigned)((M + 64 + 255) / 256)), dim3(256), 0, st, din + o_mv, M,
-                       m->d_pods.hot.as<PodHot>(), (const int32_t*)(din + o_hm), dpods);
+                       m->d_pods.hot.as<PodHot>(), any_hint ? (const int32_t*)(din + o_hm) : nullptr, dpods);
     CA_HIP_CHECK(hipGetLastError());
     if (dev[2]) (void)hipEventRecord(dev[2], st);
     // outputs, written by the kernel straight into page-locked memory (no copies, one sync):
@@ -1921,7 +1928,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
             (void)hipEventElapsedTime(&pk, dev[1], dev[2]);
             (void)hipEventElapsedTime(&gap, dev[2], m->ev0);
             fprintf(stderr, "[plan chain] device: H2D %.3f (%zu B)  pack %.3f  to the chain %.3f ms\n", h2d,
-                    o_mask + (size_t)N, pk, gap);
+                    up_bytes, pk, gap);
         }
         for (auto& e : dev) if (e) (void)hipEventDestroy(e);
         if (dbg_t)

@@ -1758,8 +1758,12 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     int32_t* const din = S.in.as<int32_t>();
     const auto t_pack = std::chrono::steady_clock::now();
     const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
-    hipEvent_t dev[3] = {nullptr, nullptr, nullptr};            // (CASIM_DEBUG_TIMING: H2D and pack times)
-    if (dbg_t) for (auto& e : dev) if (hipEventCreate(&e) != hipSuccess) e = nullptr;
+    struct DbgEvents {                                            // (CASIM_DEBUG_TIMING: H2D and pack times)
+        hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+        ~DbgEvents() { for (auto& x : e) if (x) (void)hipEventDestroy(x); }
+    } dbg_ev;
+    hipEvent_t* const dev = dbg_ev.e;                            // (destroyed on every return path)
+    if (dbg_t) for (int i = 0; i < 3; i++) if (hipEventCreate(&dev[i]) != hipSuccess) dev[i] = nullptr;
     if (dev[0]) (void)hipEventRecord(dev[0], st);
     CA_HIP_CHECK(hipMemcpyAsync(din, hw, up_bytes, hipMemcpyHostToDevice, st));
     if (dev[1]) (void)hipEventRecord(dev[1], st);
@@ -1930,7 +1934,6 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
             fprintf(stderr, "[plan chain] device: H2D %.3f (%zu B)  pack %.3f  to the chain %.3f ms\n", h2d,
                     up_bytes, pk, gap);
         }
-        for (auto& e : dev) if (e) (void)hipEventDestroy(e);
         if (dbg_t)
             fprintf(stderr, "[plan chain] checks %.3f  sync %.3f  pack %.3f  launch+kernel %.3f (kernel %.3f)  readback %.3f  "
                     "replay %.3f ms after the chain, %.3f ms beside it (C %d, M %d, N %d)\n", ms(t_entry, t0), ps.host_ms[0],

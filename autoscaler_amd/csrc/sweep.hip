@@ -844,6 +844,10 @@ __global__ void __launch_bounds__(64) k_sweep_table(
             while (!unknown) {
                 if (adv + steps >= n || work >= TB_SCAN) { lane_unknown = true; break; }
                 const int32_t b = pos >> 6;
+                // the node's row is requested with its block's summary: one global round trip
+                // per step, not two (a row read for a block that passes is wasted bandwidth only)
+                const NodeHot nh = hot[pos];
+                const uint8_t dm = dest_mask[pos];
                 if (skip_ok && b != okb) {
                     // the rest of a block whose maxima the pod fails: passed in one step (the
                     // lane's placements all lie behind it, so the committed rows are exact)
@@ -859,8 +863,6 @@ __global__ void __launch_bounds__(64) k_sweep_table(
                     okb = b;
                 }
                 work++;
-                const NodeHot nh = hot[pos];
-                const uint8_t dm = dest_mask[pos];
                 bool vis = (pos != node) & (dm != 0) & !(nh.flags & NF_UNSCHED);
                 if (vis && (p.flags & PF_PREFILTER_NAMES)) vis = in_prefilter(s, names, st[pos].name_id);
                 ev += vis ? 1u : 0u;

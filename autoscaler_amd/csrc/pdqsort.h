@@ -880,9 +880,6 @@ __device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, 
     // combined bits fs + k and 2fe - 1 - k + fs.  A run locates both ends once (binary
     // search of the combined prefix counts), then walks the bitmap, forwards on the left,
     // backwards on the right; four pairs per iteration (all loads, then all stores).
-#ifdef CASIM_PROF
-    int n_it = 0;
-#endif
     {
         const int P = c.fo[np];
         const int per = (P + NT - 1) / NT;
@@ -921,9 +918,6 @@ __device__ void wg_partition(const LdsStore& s, Ctl& c, uint32_t* __restrict__, 
             locate(fs + k, wl, bl, wbl);
             locate(2 * fe - 1 - k + fs, wr, br, wbr);
             for (;;) {
-#ifdef CASIM_PROF
-                n_it++;
-#endif
                 int pp[4], qq[4];
                 const int cnt = min(4, kend - k);
 #pragma unroll

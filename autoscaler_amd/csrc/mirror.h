@@ -60,6 +60,9 @@ struct SweepScratch {
     DevBuf chainl;                  // the host walk's serial exact chain: candidates in order
     DevBuf bmap;                    // a multi-device range's block map (k_walk_map)
     HostBuf h_in, h_tab, h_out, h_todo, h_lin, h_wl, h_tfp, h_ctab, h_l0, h_chainl, h_bmap;
+    // the host walk's side rows (windows just below and just above a re-centred row): [2][64][S]
+    // table values and [2][FPW][S] fit points, read only where built in this call
+    std::vector<int32_t> side_tab, side_fp;
     // the device pipeline of the last call shape, replayed as a graph (sweep.hip sweep_core)
     hipGraphExec_t gexec = nullptr;
     uint64_t gkey = 0, gseen = 0;

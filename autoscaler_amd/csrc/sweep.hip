@@ -1316,8 +1316,8 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     int32_t* const h_lin = sw.h_lin.as<int32_t>();
     uint8_t* const h_need = reinterpret_cast<uint8_t*>(h_lin + C);
     const size_t Sx = (size_t)std::max(S, 1);
-    if ((rc = sw.todo.reserve(sizeof(int32_t) * 4 * Sx)) != CA_OK) return rc;
-    if ((rc = sw.h_todo.reserve(sizeof(int32_t) * 4 * Sx)) != CA_OK) return rc;
+    if ((rc = sw.todo.reserve(sizeof(int32_t) * 12 * Sx)) != CA_OK) return rc;      // (a host round: 3 rows a candidate)
+    if ((rc = sw.h_todo.reserve(sizeof(int32_t) * 12 * Sx)) != CA_OK) return rc;
     if ((rc = sw.tab.reserve(sizeof(int32_t) * 64 * Sx)) != CA_OK) return rc;
     if ((rc = sw.h_tab.reserve(sizeof(int32_t) * 64 * Sx)) != CA_OK) return rc;
     if ((rc = sw.wl.reserve(sizeof(int32_t) * (64 * Sx + 64 * (size_t)std::max(nch, 1)))) != CA_OK) return rc;
@@ -1662,7 +1662,32 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         std::vector<int32_t> exact_lin((size_t)C, 0);
         std::vector<uint8_t> final_((size_t)C, 1);
         std::vector<uint8_t> have((size_t)S, 1);
-        std::vector<int32_t> todo, todo_ws, todo_k;
+        std::vector<int32_t> todo, todo_ws, todo_k, todo_slot;
+        // Side rows: a row whose estimate lies within 16 classes of its edge gets two more in the
+        // next round, the windows just below and just above it (overlapping it by 8 mean
+        // gaps), so an exact input that drifts a few positions past the edge still finds its
+        // class instead of costing another round (C5: most misses fell 2-21 positions outside
+        // the 64-wide windows).  Rows are not free: past ~500 a round's kernel grows.
+        const bool sides = !knob_env("CASIM_SWEEP_NO_SIDE_ROWS");
+        std::vector<uint8_t> have_side((size_t)S, 0), want_side((size_t)S, 0);
+        std::vector<int32_t> gapk((size_t)S, 1);
+        if (sides) {
+            if (sw.side_tab.size() < 2 * 64 * (size_t)S) sw.side_tab.resize(2 * 64 * (size_t)S);
+            if (sw.side_fp.size() < 2 * (size_t)FPW * S) sw.side_fp.resize(2 * (size_t)FPW * S);
+        }
+        int32_t* const stab = sides ? sw.side_tab.data() : nullptr;     // [2][64][S]
+        int32_t* const sfp = sides ? sw.side_fp.data() : nullptr;       // [2][FPW][S]
+        // the class of input L in candidate k's rows (main, then the sides), and its table
+        auto lookup = [&](int32_t k, int32_t L, const int32_t*& tb) -> int32_t {
+            tb = tab;
+            int32_t w = fp_class(h_tfp + k, S, n, L);
+            if (w >= 0 || !have_side[k]) return w;
+            for (int sd = 0; sd < 2; sd++) {
+                w = fp_class(sfp + (size_t)sd * FPW * S + k, S, n, L);
+                if (w >= 0) { tb = stab + (size_t)sd * 64 * S; return w; }
+            }
+            return -1;
+        };
         auto insensitive = [&](int32_t k) { return wlc[sens[k]] < 0; };
         // the device walk's re-runs already happened: only candidates from k0 on remain
         // each round looks LOOKAHEAD candidates ahead: the estimates drift with the distance
@@ -1715,10 +1740,20 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         while (k0 < S) {
             const auto t_round = std::chrono::steady_clock::now();
             const int32_t k_round = k0;
-            todo.clear(); todo_ws.clear(); todo_k.clear();
+            todo.clear(); todo_ws.clear(); todo_k.clear(); todo_slot.clear();
             const int32_t kend = std::min(S, k0 + LOOKAHEAD);
-            for (int32_t k = k0; k < kend; k++)
-                if (!have[k] && !insensitive(k)) { todo.push_back(sens[k]); todo_ws.push_back(ws[k]); todo_k.push_back(k); }
+            for (int32_t k = k0; k < kend; k++) {
+                if (insensitive(k)) continue;
+                if (!have[k]) { todo.push_back(sens[k]); todo_ws.push_back(ws[k]); todo_k.push_back(k); todo_slot.push_back(0); }
+                if (sides && want_side[k] && !have_side[k]) {
+                    const int64_t sh = 56 * (int64_t)gapk[k];
+                    todo.push_back(sens[k]); todo_ws.push_back(wrap((int64_t)ws[k] - sh, n)); todo_k.push_back(k);
+                    todo_slot.push_back(1);
+                    todo.push_back(sens[k]); todo_ws.push_back(wrap((int64_t)ws[k] + sh, n)); todo_k.push_back(k);
+                    todo_slot.push_back(2);
+                    want_side[k] = 0;
+                }
+            }
             if (!todo.empty()) {
                 rounds++;
                 const int32_t T = (int32_t)todo.size();
@@ -1763,17 +1798,19 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 CA_HIP_CHECK(hipStreamSynchronize(st));
                 tmark("table sync");
                 const int32_t* ctf = ct + 64 * (size_t)T;
-                // row by row: sequential reads, near-sequential writes (todo_k ascends)
+                // row by row: sequential reads, near-sequential writes (todo_k ascends); side
+                // rows to their own tables
+                int32_t* const tdst[3] = {tab, stab, stab ? stab + 64 * (size_t)S : nullptr};
+                int32_t* const fdst[3] = {h_tfp, sfp, sfp ? sfp + (size_t)FPW * S : nullptr};
                 for (int32_t w = 0; w < 64; w++) {
                     const int32_t* src = ct + (size_t)w * T;
-                    int32_t* dst = tab + (size_t)w * S;
-                    for (int32_t t = 0; t < T; t++) dst[todo_k[t]] = src[t];
+                    for (int32_t t = 0; t < T; t++) tdst[todo_slot[t]][(size_t)w * S + todo_k[t]] = src[t];
                 }
                 for (int32_t i = 0; i < FPW; i++) {
                     const int32_t* src = ctf + (size_t)i * T;
-                    int32_t* dst = h_tfp + (size_t)i * S;
-                    for (int32_t t = 0; t < T; t++) dst[todo_k[t]] = src[t];
+                    for (int32_t t = 0; t < T; t++) fdst[todo_slot[t]][(size_t)i * S + todo_k[t]] = src[t];
                 }
+                for (int32_t t = 0; t < T; t++) if (todo_slot[t] != 0) have_side[todo_k[t]] = 1;
                 float ms = 0;
                 (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
                 kms += ms;
@@ -1788,9 +1825,19 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 exact_lin[c] = (int32_t)cur;
                 if (wlv < 0) continue;                                             // lastIndex passes through
                 if (wrap(cur, n) == guess[c]) { cur = wlv; continue; }            // probed at the true value
-                const int32_t w = fp_class(h_tfp + k0, S, n, wrap(cur, n));
-                if (w < 0) break;
-                int32_t v = tab[(size_t)(w) * S + k0];
+                const int32_t* tb = tab;
+                const int32_t w = lookup(k0, wrap(cur, n), tb);
+                if (w < 0) {
+                    if (dbg_t) {                  // where the exact input fell against the row's window
+                        const int32_t* fp = h_tfp + k0;
+                        const int32_t lo = fp[0], hi = fp[(size_t)64 * S];
+                        const int32_t gap = std::max(1, wrap((int64_t)hi - lo, n) / 64);
+                        fprintf(stderr, "[sweep] miss at %d: input %d, window [%d, %d] (gap %d): %+d gaps from its start\n",
+                                k0, wrap(cur, n), lo, hi, gap, (int)(wrap((int64_t)wrap(cur, n) - lo + n / 2, n) - n / 2) / gap);
+                    }
+                    break;
+                }
+                int32_t v = tb[(size_t)(w) * S + k0];
                 if (v == TB_UNKNOWN) {
                     // hints / ports / long scans: exact kernel at the exact lastIndex, alone
                     std::memset(h_need, 0, (size_t)C);
@@ -1829,8 +1876,15 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
             for (int32_t k = k0; k < std::min(S, k0 + LOOKAHEAD); k++) {
                 if (insensitive(k)) continue;
                 const int32_t* fp = h_tfp + k;                      // column k of [FPW][S]
-                const int32_t w = fp_class(fp, S, n, wrap(est, n));
-                const int32_t v = w >= 0 ? tab[(size_t)(w) * S + k] : TB_UNKNOWN;
+                const int32_t* tb = tab;
+                const int32_t w = lookup(k, wrap(est, n), tb);
+                const int32_t v = w >= 0 ? tb[(size_t)(w) * S + k] : TB_UNKNOWN;
+                // an estimate within 16 classes of its row's edge: the next round adds the side
+                // rows (the exact input drifts a few positions past the edge now and then)
+                if (sides && w >= 0 && tb == tab && (w < 16 || w > 47) && !have_side[k]) {
+                    gapk[k] = std::max(1, wrap((int64_t)fp[(size_t)64 * S] - fp[0], n) / 64);
+                    want_side[k] = 1;
+                }
                 if (w >= 0 && v != TB_UNKNOWN) { est = v; continue; }
                 int64_t next = est + (move_off[sens[k] + 1] - move_off[sens[k]]);
                 int best = -1;              // known entry nearest the window centre
@@ -1842,7 +1896,9 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 if (w < 0) {                 // re-centre: 32 of the row's mean gaps before the estimate
                     const int32_t gap = std::max(1, wrap((int64_t)fp[(size_t)64 * S] - fp[0], n) / 64);
                     ws[k] = wrap(est - 32 * (int64_t)gap, n);
+                    gapk[k] = gap;
                     have[k] = 0;
+                    have_side[k] = 0;
                 }
                 est = wrap(next, n);
             }

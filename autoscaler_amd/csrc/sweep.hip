@@ -1663,13 +1663,19 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         std::vector<uint8_t> final_((size_t)C, 1);
         std::vector<uint8_t> have((size_t)S, 1);
         std::vector<int32_t> todo, todo_ws, todo_k, todo_slot;
-        // Side rows: a row whose estimate lies within 16 classes of its edge gets two more in the
-        // next round, the windows just below and just above it (overlapping it by 8 mean
-        // gaps), so an exact input that drifts a few positions past the edge still finds its
-        // class instead of costing another round (C5: most misses fell 2-21 positions outside
-        // the 64-wide windows).  Rows are not free: past ~500 a round's kernel grows.
+        // Side rows: a row whose estimate lies within SIDE_BAND classes of one of its edges gets
+        // the adjacent window on that side in the next round (overlapping it by 8 mean gaps),
+        // so an exact input that drifts a few positions past the edge still finds its class
+        // instead of costing another round (C5: most misses fell 2-28 positions outside the
+        // 64-wide windows).  Rows are not free — past ~500 a round's kernel grows — so one side
+        // per row, near-edge rows only (C5 RunOnce sweep: 16 / 24 / 32 classes read 2.85 /
+        // 2.6 / 3.0 ms, both sides at 16: 3.1, none: 3.5).
         const bool sides = !knob_env("CASIM_SWEEP_NO_SIDE_ROWS");
-        std::vector<uint8_t> have_side((size_t)S, 0), want_side((size_t)S, 0);
+#ifndef CASIM_SIDE_BAND
+#define CASIM_SIDE_BAND 24
+#endif
+        constexpr int32_t SIDE_BAND = CASIM_SIDE_BAND;
+        std::vector<uint8_t> have_side((size_t)S, 0), want_side((size_t)S, 0);   // want_side: bit 0 below, bit 1 above
         std::vector<int32_t> gapk((size_t)S, 1);
         if (sides) {
             if (sw.side_tab.size() < 2 * 64 * (size_t)S) sw.side_tab.resize(2 * 64 * (size_t)S);
@@ -1683,6 +1689,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
             int32_t w = fp_class(h_tfp + k, S, n, L);
             if (w >= 0 || !have_side[k]) return w;
             for (int sd = 0; sd < 2; sd++) {
+                if (!((have_side[k] >> sd) & 1)) continue;
                 w = fp_class(sfp + (size_t)sd * FPW * S + k, S, n, L);
                 if (w >= 0) { tb = stab + (size_t)sd * 64 * S; return w; }
             }
@@ -1747,11 +1754,11 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 if (!have[k]) { todo.push_back(sens[k]); todo_ws.push_back(ws[k]); todo_k.push_back(k); todo_slot.push_back(0); }
                 if (sides && want_side[k] && !have_side[k]) {
                     const int64_t sh = 56 * (int64_t)gapk[k];
-                    todo.push_back(sens[k]); todo_ws.push_back(wrap((int64_t)ws[k] - sh, n)); todo_k.push_back(k);
-                    todo_slot.push_back(1);
-                    todo.push_back(sens[k]); todo_ws.push_back(wrap((int64_t)ws[k] + sh, n)); todo_k.push_back(k);
-                    todo_slot.push_back(2);
-                    want_side[k] = 0;
+                    for (int sd = 0; sd < 2; sd++) {
+                        if (!((want_side[k] >> sd) & 1)) continue;
+                        todo.push_back(sens[k]); todo_ws.push_back(wrap((int64_t)ws[k] + (sd ? sh : -sh), n));
+                        todo_k.push_back(k); todo_slot.push_back(1 + sd);
+                    }
                 }
             }
             if (!todo.empty()) {
@@ -1810,7 +1817,8 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                     const int32_t* src = ctf + (size_t)i * T;
                     for (int32_t t = 0; t < T; t++) fdst[todo_slot[t]][(size_t)i * S + todo_k[t]] = src[t];
                 }
-                for (int32_t t = 0; t < T; t++) if (todo_slot[t] != 0) have_side[todo_k[t]] = 1;
+                for (int32_t t = 0; t < T; t++)
+                    if (todo_slot[t] != 0) { have_side[todo_k[t]] |= (uint8_t)(1 << (todo_slot[t] - 1)); want_side[todo_k[t]] = 0; }
                 float ms = 0;
                 (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
                 kms += ms;
@@ -1879,11 +1887,11 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 const int32_t* tb = tab;
                 const int32_t w = lookup(k, wrap(est, n), tb);
                 const int32_t v = w >= 0 ? tb[(size_t)(w) * S + k] : TB_UNKNOWN;
-                // an estimate within 16 classes of its row's edge: the next round adds the side
-                // rows (the exact input drifts a few positions past the edge now and then)
-                if (sides && w >= 0 && tb == tab && (w < 16 || w > 47) && !have_side[k]) {
+                // an estimate within SIDE_BAND classes of its row's edge: the next round adds the
+                // side row there (the exact input drifts a few positions past the edge now and then)
+                if (sides && w >= 0 && tb == tab && (w < SIDE_BAND || w > 63 - SIDE_BAND) && !have_side[k]) {
                     gapk[k] = std::max(1, wrap((int64_t)fp[(size_t)64 * S] - fp[0], n) / 64);
-                    want_side[k] = 1;
+                    want_side[k] = w < SIDE_BAND ? 1 : 2;
                 }
                 if (w >= 0 && v != TB_UNKNOWN) { est = v; continue; }
                 int64_t next = est + (move_off[sens[k] + 1] - move_off[sens[k]]);

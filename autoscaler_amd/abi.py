@@ -11,7 +11,7 @@ import ctypes as C
 
 import numpy as np
 
-CASIM_ABI_VERSION = 2
+CASIM_ABI_VERSION = 3
 
 # status codes
 CA_OK, CA_EINVAL, CA_ENOTFOUND, CA_EEXISTS, CA_EDEVICE, CA_ECAPACITY, CA_EUNSUPPORTED, CA_ESTATE, CA_ENOTRUN = range(9)
@@ -170,13 +170,21 @@ class PdbTableC(C.Structure):
     _fields_ = [("n_pdbs", C.c_int32), ("allowed", C.c_void_p), ("pod_off", C.c_void_p), ("pod_pdb", C.c_void_p)]
 
 
+# ca_sweep_phase: one block's record of the phased sweep (casim.h "one process per GPU")
+CA_SWEEP_PHASE_PROBE, CA_SWEEP_PHASE_MAP, CA_SWEEP_PHASE_RESOLVE = 1, 2, 3
+CA_SWEEP_MAP_INTS = 130
+CA_SWEEP_NOT_REACHED = -(2 ** 31)
+SWEEP_PHASE_DTYPE = np.dtype([("kind", np.int32), ("est_base", np.int32), ("guess_base", np.int64), ("adv", np.int64),
+                              ("succ", np.int32), ("n_sensitive", np.int32), ("map_ran", np.int32),
+                              ("map_ok", np.int32), ("map", np.int32, (CA_SWEEP_MAP_INTS,))])
+
 # sizes in ca_abi_struct_sizes order
 EXPECTED_SIZES = [
     NODE_DTYPE.itemsize, POD_DTYPE.itemsize, REQ_DTYPE.itemsize, TERM_DTYPE.itemsize,
     C.sizeof(PodTableC), C.sizeof(MatchSpecC), C.sizeof(PredResultC), TEMPLATE_DTYPE.itemsize,
     C.sizeof(LimiterC), ESTIMATE_RESULT_DTYPE.itemsize, REMOVAL_RESULT_DTYPE.itemsize,
     UTIL_NODE_DTYPE.itemsize, UTIL_POD_DTYPE.itemsize, UTIL_INFO_DTYPE.itemsize,
-    PLAN_RESULT_DTYPE.itemsize, PLAN_MOVE_DTYPE.itemsize,
+    PLAN_RESULT_DTYPE.itemsize, PLAN_MOVE_DTYPE.itemsize, SWEEP_PHASE_DTYPE.itemsize,
 ]
 
 

@@ -2901,7 +2901,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     // CASIM_STEP_TIMING (read once per process): host-side split of the steps, averaged over
     // 20 calls — entry to the first launch, to the last launch, to the join, to the return,
     // and the caller's time between a return and the next entry
-    static const bool step_timing = getenv("CASIM_STEP_TIMING") != nullptr;
+    static const bool step_timing = knob_env("CASIM_STEP_TIMING") != nullptr;
     static double st_acc[6] = {0, 0, 0, 0, 0, 0};
     static int st_n = 0;
     static std::chrono::steady_clock::time_point st_last_exit;
@@ -3528,6 +3528,14 @@ int32_t estimate_plan_rebase(const ca_estimate_plan* p, ca_estimate_result* resu
 }  // namespace casim
 
 extern "C" {
+
+int ca_estimate_plan_rebase(const ca_estimate_plan* p, ca_estimate_result* results, int32_t last_index_in,
+                            int32_t* last_index_out) {
+    if (!p || (p->G > 0 && !results)) return CA_EINVAL;
+    const int32_t lout = casim::estimate_plan_rebase(p, results, last_index_in);
+    if (last_index_out) *last_index_out = lout;
+    return CA_OK;
+}
 
 int ca_estimate_plan_create(ca_mirror* m, const ca_podset* s, const int32_t* group_off, const int32_t* pod_idx,
                             const ca_template* templates, int32_t n_groups, ca_estimate_plan** out) {

@@ -1401,7 +1401,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     if (!m || !t || n < 0 || n_classes < 0 || !last_index || (n > 0 && !out_node)) return CA_EINVAL;
     if (s && (s->m != m || s->t.n_pods != t->n_pods)) return CA_EINVAL;
     const auto t0 = std::chrono::steady_clock::now();
-    const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
+    const bool dbg_t = knob_env("CASIM_DEBUG_TIMING") != nullptr;
     auto tmark = [&](const char* what) {
         if (dbg_t)
             fprintf(stderr, "[filter] %-12s %8.3f ms\n", what,

@@ -207,17 +207,17 @@ namespace casim {
 //               pass — the tail of a normal call, host walk included, so it is always exact
 // Device state (probe outputs, guesses, tables, chunk maps) stays in the mirror's sweep
 // scratch between the calls; nothing else may use the mirror meanwhile.
-enum { SP_FULL = 0, SP_PROBE, SP_MAP, SP_RESOLVE };
-struct SweepPhase {
-    int kind = SP_FULL;
-    int64_t guess_base = 0;
-    int32_t est_base = 0;
-    int64_t adv = 0;              // SP_PROBE out
-    int32_t succ = 0;             // SP_PROBE out: candidates whose probe made a successful scan
-    int32_t S = 0;                // sensitive candidates of the range
-    int32_t map_ok = 0;           // SP_MAP out: the device walk ran (map valid)
-    int32_t map[64 + 65 + 1];     // SP_MAP out: k_walk_map's record (64 outputs, FPW fit points, mode)
-};
+enum { SP_FULL = 0, SP_PROBE = CA_SWEEP_PHASE_PROBE, SP_MAP = CA_SWEEP_PHASE_MAP, SP_RESOLVE = CA_SWEEP_PHASE_RESOLVE };
+// the map record k_walk_map writes (sweep.hip): 64 lastIndex-out values by class, then the
+// first row's SWEEP_FPW fit points, then the class mode flag
+constexpr int SWEEP_FPW = 65;
+constexpr int SWEEP_MAP_HEAD = 64;                     // offset of the fit points
+constexpr int SWEEP_MAP_MODE = 64 + SWEEP_FPW;         // offset of the mode flag
+constexpr int SWEEP_MAP_INTS = 64 + SWEEP_FPW + 1;
+static_assert(SWEEP_MAP_INTS == CA_SWEEP_MAP_INTS, "casim.h map record size");
+// the public record (casim.h ca_sweep_phase): kind, guess_base (PROBE in), est_base (MAP
+// in), adv / succ (PROBE out), n_sensitive, map_ran / map_ok / map (MAP out)
+using SweepPhase = ca_sweep_phase;
 
 int64_t removal_plan_sensitive_pods(const ca_removal_plan* p);
 bool removal_plan_phase_ok(const ca_removal_plan* p);             // no scope cut in the range

@@ -91,7 +91,7 @@ BlockCache& caller_cache() {
     return *c;
 }
 bool no_cache() {
-    static const bool off = getenv("CASIM_NO_ALLOC_CACHE") != nullptr;
+    static const bool off = knob_env("CASIM_NO_ALLOC_CACHE") != nullptr;
     return off;
 }
 // the synchronisation hipFree would have done, on the block's device
@@ -443,7 +443,7 @@ void ca_mirror::reserve_more(size_t n_pods_add, size_t n_journal_add) {
 
 void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, const int32_t* node, int32_t n,
                                  int32_t* out_id, bool device_rows) {
-    const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
+    const bool dbg_t = knob_env("CASIM_DEBUG_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     auto tmark = [&](const char* what) {
         if (dbg_t)
@@ -646,7 +646,7 @@ int ca_mirror::remap_hints_removed(int32_t pos, int32_t code, bool restore) {
 int ca_mirror::sync_nodes() {
     const size_t n = nodes.size();
     int rc;
-    static const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
+    static const bool dbg_t = knob_env("CASIM_DEBUG_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     struct Done {                                           // (CASIM_DEBUG_TIMING: the sync's size and time)
         bool on; const std::chrono::steady_clock::time_point t0; size_t rows; bool full, stat;
@@ -891,7 +891,8 @@ int ca_abi_struct_sizes(int32_t* out, int32_t cap) {
                          (int32_t)sizeof(ca_limiter), (int32_t)sizeof(ca_estimate_result),
                          (int32_t)sizeof(ca_removal_result), (int32_t)sizeof(ca_util_node),
                          (int32_t)sizeof(ca_util_pod), (int32_t)sizeof(ca_util_info),
-                         (int32_t)sizeof(ca_plan_result), (int32_t)sizeof(ca_plan_move)};
+                         (int32_t)sizeof(ca_plan_result), (int32_t)sizeof(ca_plan_move),
+                         (int32_t)sizeof(ca_sweep_phase)};
     const int32_t n = (int32_t)(sizeof s / sizeof s[0]);
     for (int32_t i = 0; i < n && i < cap; i++) out[i] = s[i];
     return n;

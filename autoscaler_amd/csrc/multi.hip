@@ -262,6 +262,44 @@ int ca_multi_removal_plan_create(ca_multi* mm, const int32_t* candidates, int32_
     return CA_OK;
 }
 
+// The blocks' lastIndex chain from their MAP records: a block without a
+// successful probe scan passes lastIndex through; otherwise the class of its input in its
+// first row's fit points picks its map entry, the next block's input.  The walk stops at the
+// first block whose map is missing or does not cover its input.
+int ca_sweep_compose(const ca_sweep_phase* ph, int32_t D, int32_t n, int32_t L0, int32_t* lin_c, int32_t* n_reached) {
+    if (D < 0 || (D > 0 && (!ph || !lin_c)) || n < 0) return CA_EINVAL;
+    for (int32_t d = 0; d < D; d++) lin_c[d] = CA_SWEEP_NOT_REACHED;
+    if (n_reached) *n_reached = 0;
+    if (n == 0) return CA_OK;
+    int64_t cur = L0;
+    int32_t reached = 0;
+    for (int32_t d = 0; d < D; d++) {
+        if (ph[d].n_sensitive == 0 || ph[d].succ == 0) {   // no scan can succeed: lastIndex passes through
+            lin_c[d] = (int32_t)cur;
+            reached++;
+            continue;
+        }
+        if (!ph[d].map_ok) break;
+        const int32_t* mp = ph[d].map;
+        const int32_t* head = mp + SWEEP_MAP_HEAD;
+        const int32_t Lw = (int32_t)(((cur % n) + n) % n);
+        int32_t x;
+        if (mp[SWEEP_MAP_MODE]) {
+            x = casim::sweep_fp_class(head, n, Lw);
+        } else {
+            x = Lw - head[1];
+            if (x < 0) x += n;
+            if (x >= 64) x = -1;
+        }
+        if (x < 0 || mp[x] < 0) break;
+        lin_c[d] = (int32_t)cur;
+        reached++;
+        cur = mp[x];
+    }
+    if (n_reached) *n_reached = reached;
+    return CA_OK;
+}
+
 int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t n_pods, int32_t* last_index,
                               ca_removal_result* results, int32_t* out_dest) {
     // (no resident-hint mode: a block re-run must start from the caller's hints again)
@@ -316,7 +354,7 @@ int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t 
     //    from the exact input, as before.
     bool phased = D > 1 && n > 0 && !knob_env("CASIM_MULTI_NO_MAP");
     for (int32_t d = 0; d < D && phased; d++) if (p->pl[d] && !removal_plan_phase_ok(p->pl[d])) phased = false;
-    std::vector<int32_t> lin_c((size_t)D, INT32_MIN);   // composed input of each range (INT32_MIN: not reached)
+    std::vector<int32_t> lin_c((size_t)D, CA_SWEEP_NOT_REACHED);   // composed input of each range
     if (phased) {
         std::vector<SweepPhase> ph((size_t)D);
         int64_t gb = L0;
@@ -333,38 +371,21 @@ int ca_multi_removal_plan_run(ca_multi_removal_plan* p, int32_t* hints, int32_t 
             ph[d].kind = SP_MAP;
             ph[d].est_base = (int32_t)(((est % n) + n) % n);
             est += ph[d].adv;
-            if (ph[d].S > 0 && ph[d].succ > 0) mapped.push_back(d);
+            // every range with sensitive candidates builds its tables here, including one whose
+            // probe made no successful scan (its lastIndex passes through the composition): its
+            // resolve walks the tables from the true input, so they must be this call's (a range
+            // left out would walk the tables and chunk maps of an earlier call)
+            if (ph[d].n_sensitive > 0) mapped.push_back(d);
         }
         if ((rc = for_blocks((int32_t)mapped.size(), [&](int32_t i) { return run(mapped[i], L0, &ph[mapped[i]]); })) !=
             CA_OK)
             return rc;
         lap(1);
-        int64_t cur = L0;
-        for (int32_t d = 0; d < D; d++) {
-            if (ph[d].S == 0 || ph[d].succ == 0) {           // no scan can succeed: lastIndex passes through
-                lin_c[d] = (int32_t)cur;
-                continue;
-            }
-            if (!ph[d].map_ok) break;
-            const int32_t* mp = ph[d].map;
-            const int32_t* head = mp + 64;
-            const int32_t Lw = (int32_t)(((cur % n) + n) % n);
-            int32_t x;
-            if (mp[64 + 65]) {
-                x = casim::sweep_fp_class(head, n, Lw);
-            } else {
-                x = Lw - head[1];
-                if (x < 0) x += n;
-                if (x >= 64) x = -1;
-            }
-            if (x < 0 || mp[x] < 0) break;
-            lin_c[d] = (int32_t)cur;
-            cur = mp[x];
-        }
+        ca_sweep_compose(ph.data(), D, n, L0, lin_c.data(), nullptr);
         lap(2);
         for (int32_t d = 0; d < D; d++) ph[d].kind = SP_RESOLVE;
         std::vector<int32_t> todo;
-        for (int32_t d = 0; d < D; d++) if (lin_c[d] != INT32_MIN) todo.push_back(d);
+        for (int32_t d = 0; d < D; d++) if (lin_c[d] != CA_SWEEP_NOT_REACHED) todo.push_back(d);
         if ((rc = for_blocks((int32_t)todo.size(), [&](int32_t i) {
                  const int32_t d = todo[i];
                  return run(d, lin_c[d], &ph[d]);

@@ -1757,7 +1757,7 @@ int plan_chain_run(ca_mirror* m, const int32_t* candidates, int32_t C, const uin
     const size_t up_bytes = any_hint ? 4 * (o_hm + (size_t)std::max(M, 1)) : o_mask + (size_t)N;
     int32_t* const din = S.in.as<int32_t>();
     const auto t_pack = std::chrono::steady_clock::now();
-    const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
+    const bool dbg_t = knob_env("CASIM_DEBUG_TIMING") != nullptr;
     struct DbgEvents {                                            // (CASIM_DEBUG_TIMING: H2D and pack times)
         hipEvent_t e[3] = {nullptr, nullptr, nullptr};
         ~DbgEvents() { for (auto& x : e) if (x) (void)hipEventDestroy(x); }

@@ -124,7 +124,7 @@ int ca_mirror::replay_moves(const ca_plan_move* mv, int32_t nm) {
         }
         return CA_OK;
     }
-    const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
+    const bool dbg_t = knob_env("CASIM_DEBUG_TIMING") != nullptr;
     const auto tr0 = std::chrono::steady_clock::now();
     auto tmark = [&](const char* what) {
         if (dbg_t)
@@ -244,8 +244,13 @@ int ca_mirror::replay_moves(const ca_plan_move* mv, int32_t nm) {
         }
     });
     tmark("rows");
+    // every part's changes are merged before an error is returned: a part that failed and the
+    // parts after it have already changed rows, pod lists and pods[].node, and the caller's
+    // revert-on-error (ca_plan_removals) can only undo what the journal holds and re-sync the
+    // rows dirty_rows names
+    int first_rc = CA_OK;
     for (Part& pt : part) {
-        if (pt.rc != CA_OK) return pt.rc;
+        if (first_rc == CA_OK) first_rc = pt.rc;
         n_ext_pods += pt.ext;
         n_eph_pods += pt.eph;
         n_scope_blockers += pt.blockers;
@@ -253,7 +258,7 @@ int ca_mirror::replay_moves(const ca_plan_move* mv, int32_t nm) {
         if (journaled) journal.insert(journal.end(), pt.jr.begin(), pt.jr.end());
     }
     tmark("merged");
-    return CA_OK;
+    return first_rc;
 }
 
 // plan_chain.hip: the whole loop as one device-resident chain (1 = ran, 0 = outside its scope)
@@ -361,7 +366,7 @@ int plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const uint
     std::vector<Own> own;
     std::vector<int32_t> list_tmp;
     bool done = false;
-    const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
+    const bool dbg_t = knob_env("CASIM_DEBUG_TIMING") != nullptr;
     const char* why = "";
 
     auto not_run = [&](int32_t from) {
@@ -581,7 +586,7 @@ int ca_plan_removals(ca_mirror* m, const int32_t* candidates, int32_t C, const u
     }
     const auto t_c = std::chrono::steady_clock::now();
     rc = ca_mirror_commit(m);
-    if (getenv("CASIM_DEBUG_TIMING"))
+    if (knob_env("CASIM_DEBUG_TIMING"))
         fprintf(stderr, "[plan] commit %.3f ms (journal %zu entries)\n",
                 std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_c).count(), m->journal.size());
     return rc;

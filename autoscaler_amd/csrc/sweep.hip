@@ -661,7 +661,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CASIM_S
 // row covers 64 fit points (DESIGN.md §4 sweep).  Rows whose first pod has PreFilter
 // node names, or a ring with fewer than 65 fit points, use 64 consecutive positions.
 // ---------------------------------------------------------------------------
-constexpr int FPW = 65;
+constexpr int FPW = SWEEP_FPW;
 
 // class of lastIndex L in a row (fp[k * fs], k = 0..64), or -1 outside it
 __host__ __device__ inline int32_t fp_class(const int32_t* fp, int32_t fs, int32_t n, int32_t L) {
@@ -1268,7 +1268,7 @@ int launch_exact(ca_mirror* m, hipStream_t st, const SweepCall& in, const int32_
 int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod_hints, int32_t* last_index,
                ca_removal_result* results, int32_t* out_dest, SweepPhase* ph = nullptr) {
     const auto t_start = std::chrono::steady_clock::now();
-    const bool dbg_t = getenv("CASIM_DEBUG_TIMING") != nullptr;
+    const bool dbg_t = knob_env("CASIM_DEBUG_TIMING") != nullptr;
     auto tmark = [&](const char* what) {
         if (dbg_t)
             fprintf(stderr, "[sweep] %-14s %8.3f ms\n", what,
@@ -1374,7 +1374,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     // -> mode[2]: the chain's input (k_sweep_est, k_walk_resolve); a range's SP_MAP centres
     // its windows on the estimate of its input instead
     sw.h_l0.as<int32_t>()[0] = n > 0 ? wrap(ph && ph->kind == SP_MAP ? (int64_t)ph->est_base : L0, n) : 0;
-    if (ph) ph->S = S;
+    if (ph) ph->n_sensitive = S;
     const bool use_ext = m->n_ext_pods > 0;
     if (use_ext && (rc = ensure_dyn_lds((const void*)k_sweep, sizeof(OverlayExt))) != CA_OK) return rc;
     const size_t wr_bytes = sizeof(int32_t) * (size_t)nch * (64 + FPW);
@@ -1472,7 +1472,9 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
             return CA_OK;
         }
         if (ph->kind == SP_MAP) {
+            ph->map_ran = 0;
             if (!(S > 0 && n > 0)) return CA_OK;
+            ph->map_ran = 1;
             CA_HIP_CHECK(hipMemcpyAsync(d_sens, ht, sizeof(int32_t) * S, hipMemcpyHostToDevice, st));
             CA_HIP_CHECK(hipMemcpyAsync(d_tdoff, ht + 2 * S, sizeof(int32_t) * S, hipMemcpyHostToDevice, st));
             hipLaunchKernelGGL(k_sweep_est, dim3(1), dim3(1024), 0, st, d_out.as<SweepOut>(), d_sens, S, n, d_ws, d_mode,
@@ -1493,16 +1495,22 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
             hipLaunchKernelGGL(k_walk_chunks, dim3(nch), dim3(64), 0, st, d_sens, d_ws, d_lin, d_wl, sw.tab.as<int32_t>(),
                                d_tfp, d_mode, S, n, d_cmap, d_traj);
             CA_HIP_CHECK(hipGetLastError());
-            if ((e = sw.bmap.reserve(sizeof(int32_t) * (64 + FPW + 1))) != CA_OK) return e;
-            if ((e = sw.h_bmap.reserve(sizeof(int32_t) * (64 + FPW + 1))) != CA_OK) return e;
+            if ((e = sw.bmap.reserve(sizeof(int32_t) * SWEEP_MAP_INTS)) != CA_OK) return e;
+            if ((e = sw.h_bmap.reserve(sizeof(int32_t) * SWEEP_MAP_INTS)) != CA_OK) return e;
             hipLaunchKernelGGL(k_walk_map, dim3(1), dim3(1024), wr_bytes, st, d_tfp, d_cmap, d_mode, S, n,
                                sw.bmap.as<int32_t>());
             CA_HIP_CHECK(hipGetLastError());
-            CA_HIP_CHECK(hipMemcpyAsync(sw.h_bmap.ptr, sw.bmap.ptr, sizeof(int32_t) * (64 + FPW + 1), hipMemcpyDeviceToHost,
+            CA_HIP_CHECK(hipMemcpyAsync(sw.h_bmap.ptr, sw.bmap.ptr, sizeof(int32_t) * SWEEP_MAP_INTS, hipMemcpyDeviceToHost,
                                         st));
             return CA_OK;
         }
-        // SP_RESOLVE: the tail of enqueue() from the true input (mode[2])
+        // SP_RESOLVE: the tail of enqueue() from the true input (mode[2]); it reads the
+        // tables and chunk maps this range's SP_MAP built (multi.hip maps every range with
+        // sensitive candidates), never an earlier call's
+        if (S > 0 && n > 0 && !ph->map_ran) {
+            set_last_error("sweep resolve phase without this call's map phase");
+            return CA_EINVAL;
+        }
         if (dev_walk) {
             // (the probe's results for the candidates the walk does not re-run stay in d_out;
             // d_lin was re-uploaded with the same guesses, need = 0 as the map phase left it)
@@ -1586,7 +1594,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         CA_HIP_CHECK(hipMemcpyAsync(sw.h_out.ptr, sw.out.ptr, d2h_bytes, hipMemcpyDeviceToHost, st));
         return CA_OK;
     };
-    static const bool no_graph = getenv("CASIM_NO_GRAPH") != nullptr;
+    static const bool no_graph = knob_env("CASIM_NO_GRAPH") != nullptr;
     CA_HIP_CHECK(hipEventRecord(m->ev0, st));
     const bool phased = ph && ph->kind != SP_FULL;
     if (phased) {
@@ -1632,7 +1640,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     }
     if (phased && ph->kind == SP_MAP) {
         ph->map_ok = (S > 0 && n > 0 && dev_walk) ? 1 : 0;
-        if (ph->map_ok) std::memcpy(ph->map, sw.h_bmap.ptr, sizeof(int32_t) * (64 + FPW + 1));
+        if (ph->map_ok) std::memcpy(ph->map, sw.h_bmap.ptr, sizeof(int32_t) * SWEEP_MAP_INTS);
         return CA_OK;
     }
     float kms = 0;
@@ -1943,7 +1951,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         const SweepOut& o = outs[c];
         if (o.status != CA_OK) { set_last_error("overlay capacity exceeded"); return o.status; }
         if (o.fa_success && wrap(o.lin, n) != wrap(Lrun, n)) {
-            if (getenv("CASIM_DEBUG"))
+            if (knob_env("CASIM_DEBUG"))
                 fprintf(stderr, "chain mismatch at candidate %d: o.lin=%d Lrun=%ld\n", c, o.lin, (long)Lrun);
             set_last_error("sweep lastIndex chain mismatch");
             return CA_EDEVICE;
@@ -2078,7 +2086,7 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     if ((rc = m->sync_nodes()) != CA_OK) return rc;
     const auto t_sync1 = std::chrono::steady_clock::now();
     if ((rc = m->sync_pods()) != CA_OK) return rc;
-    if (getenv("CASIM_DEBUG_TIMING"))
+    if (knob_env("CASIM_DEBUG_TIMING"))
         fprintf(stderr, "[sweep] sync           %8.3f ms (rows %zu dirty: %.3f ms; %zu pods)\n",
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_sync).count(), dirty,
                 std::chrono::duration<double, std::milli>(t_sync1 - t_sync).count(), m->pods.size());
@@ -2289,6 +2297,25 @@ int removal_plan_run_phase(ca_removal_plan* p, int32_t* hints, int32_t* last_ind
 }  // namespace casim
 
 extern "C" {
+
+int ca_removal_plan_sensitive_pods(const ca_removal_plan* p, int64_t* out) {
+    if (!p || !out) return CA_EINVAL;
+    *out = casim::removal_plan_sensitive_pods(p);
+    return CA_OK;
+}
+
+int ca_removal_plan_phased(const ca_removal_plan* p, int32_t* out) {
+    if (!p || !out) return CA_EINVAL;
+    *out = casim::removal_plan_phase_ok(p) ? 1 : 0;
+    return CA_OK;
+}
+
+int ca_removal_plan_run_phase(ca_removal_plan* p, ca_sweep_phase* ph, int32_t* hints, int32_t* last_index,
+                              ca_removal_result* results, int32_t* out_dest) {
+    if (!p || !ph || !hints) return CA_EINVAL;
+    if (ph->kind != SP_PROBE && ph->kind != SP_MAP && ph->kind != SP_RESOLVE) return CA_EINVAL;
+    return casim::removal_plan_run_phase(p, hints, last_index, results, out_dest, ph);
+}
 
 int ca_removal_plan_destroy(ca_removal_plan* p) {
     if (!p) return CA_EINVAL;

@@ -82,6 +82,7 @@ def load() -> C.CDLL:
         "ca_estimate_plan_device_results": ([vp, p(vp)], C.c_int),
         "ca_estimate_plan_stats": ([vp, p(i32), p(C.c_float), p(C.c_float), p(C.c_float)], C.c_int),
         "ca_estimate_plan_chain_info": ([vp, p(i32), p(i32)], C.c_int),
+        "ca_estimate_plan_rebase": ([vp, vp, i32, p(i32)], C.c_int),
         "ca_go_sort_ranks": ([i32, vp, i32, i32, i32, vp], C.c_int),
         "ca_estimate_plan_timings": ([vp, p(C.c_float), i32], C.c_int),
         "ca_estimate_plan_set_phase_timing": ([vp, i32], C.c_int),
@@ -91,6 +92,10 @@ def load() -> C.CDLL:
         "ca_removal_plan_create": ([vp, vp, i32, vp, vp, vp, vp, p(vp)], C.c_int),
         "ca_removal_plan_run": ([vp, vp, p(i32), vp, vp], C.c_int),
         "ca_removal_plan_destroy": ([vp], C.c_int),
+        "ca_removal_plan_sensitive_pods": ([vp, p(C.c_int64)], C.c_int),
+        "ca_removal_plan_phased": ([vp, p(i32)], C.c_int),
+        "ca_removal_plan_run_phase": ([vp, vp, vp, p(i32), vp, vp], C.c_int),
+        "ca_sweep_compose": ([vp, i32, i32, i32, vp, p(i32)], C.c_int),
         "ca_mirror_set_hints": ([vp, vp, i32], C.c_int),
         "ca_mirror_get_hints": ([vp, vp, i32], C.c_int),
         "ca_removal_candidate_ticks": ([vp, p(C.c_uint64), i32], C.c_int),
@@ -159,13 +164,15 @@ def exported_symbols() -> list[str]:
         "ca_fits_matrix", "ca_check_templates", "ca_expansion_plan_create", "ca_expansion_plan_run",
         "ca_expansion_plan_destroy", "ca_expansion_plan_kernel_ms", "ca_estimate_batch", "ca_estimate_plan_create", "ca_estimate_plan_run",
         "ca_estimate_plan_run_u16",
-        "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_estimate_plan_timings",
+        "ca_estimate_plan_destroy", "ca_estimate_plan_stats", "ca_estimate_plan_chain_info", "ca_estimate_plan_rebase",
+        "ca_estimate_plan_timings",
         "ca_estimate_plan_set_phase_timing",
         "ca_estimate_plan_group_ticks", "ca_estimate_plan_fetch", "ca_estimate_plan_device_results",
         "ca_go_sort_ranks",
         "ca_find_nodes_to_remove",
         "ca_removal_stats", "ca_removal_timings", "ca_removal_plan_create", "ca_removal_plan_run",
-        "ca_removal_plan_destroy", "ca_mirror_set_hints", "ca_mirror_get_hints",
+        "ca_removal_plan_destroy", "ca_removal_plan_sensitive_pods", "ca_removal_plan_phased",
+        "ca_removal_plan_run_phase", "ca_sweep_compose", "ca_mirror_set_hints", "ca_mirror_get_hints",
         "ca_removal_candidate_ticks", "ca_filter_out_schedulable", "ca_filter_stats",
         "ca_util_table_create", "ca_util_table_destroy", "ca_util_calculate", "ca_util_device_results",
         "ca_util_table_update", "ca_util_table_set_added", "ca_multi_create", "ca_multi_destroy",
@@ -187,6 +194,16 @@ def go_sort_ranks(ranks, store: int = 0, limit: int = 0, device: int = 0) -> np.
     if st != abi.CA_OK:
         raise CasimError(st, "go_sort_ranks")
     return perm[: len(r)]
+
+
+def sweep_compose(recs: np.ndarray, n_nodes: int, last_index: int) -> np.ndarray:
+    """ca_sweep_compose: every block's exact input lastIndex from the blocks' MAP records
+    (abi.CA_SWEEP_NOT_REACHED where the maps cannot carry the chain)."""
+    r = np.ascontiguousarray(recs, dtype=abi.SWEEP_PHASE_DTYPE)
+    lin = np.zeros(max(len(r), 1), np.int32)
+    _check(load().ca_sweep_compose(r.ctypes.data, len(r), n_nodes, last_index, lin.ctypes.data, None),
+           "ca_sweep_compose")
+    return lin[: len(r)]
 
 
 def device_count() -> int:
@@ -591,6 +608,32 @@ class RemovalPlan:
         return RemovalOutput(_fast_copy(self.results), dest[: len(self.moves)].copy() if dest is not None else None, h,
                              li.value)
 
+    # -- the phased sweep of one block (casim.h "one process per GPU"; shard.sweep_sharded) --
+    def sensitive_pods(self) -> int:
+        v = C.c_int64(0)
+        _check(self.lib.ca_removal_plan_sensitive_pods(self.h, C.byref(v)), "ca_removal_plan_sensitive_pods")
+        return v.value
+
+    def phased(self) -> bool:
+        v = C.c_int32(0)
+        _check(self.lib.ca_removal_plan_phased(self.h, C.byref(v)), "ca_removal_plan_phased")
+        return bool(v.value)
+
+    def run_phase(self, rec: np.ndarray, hints: np.ndarray, last_index: int, want_dest: bool = True):
+        """One phase (rec["kind"]) of this block; rec is a 1-element SWEEP_PHASE_DTYPE array,
+        updated in place; hints (int32, per mirror pod) read, and for RESOLVE updated for the
+        block's pods.  RESOLVE returns the block's RemovalOutput (dest: the block's moves)."""
+        assert rec.dtype == abi.SWEEP_PHASE_DTYPE and rec.flags["C_CONTIGUOUS"]
+        assert hints.dtype == np.int32 and hints.flags["C_CONTIGUOUS"]
+        li = C.c_int32(last_index)
+        dest = self._dest.array if want_dest else None
+        _check(self.lib.ca_removal_plan_run_phase(self.h, rec.ctypes.data, ptr(hints), C.byref(li), ptr(self.results),
+                                                  ptr(dest) if dest is not None else None), "ca_removal_plan_run_phase")
+        if int(rec["kind"][0]) != abi.CA_SWEEP_PHASE_RESOLVE:
+            return None
+        return RemovalOutput(_fast_copy(self.results), dest[: len(self.moves)].copy() if dest is not None else None,
+                             hints, li.value)
+
     def close(self) -> None:
         if self.h:
             self.lib.ca_removal_plan_destroy(self.h)
@@ -777,6 +820,14 @@ class EstimatePlan:
         sens, succ = C.c_int32(0), C.c_int32(0)
         self.lib.ca_estimate_plan_chain_info(self.h, C.byref(sens), C.byref(succ))
         return sens.value, succ.value
+
+    def rebase(self, results: np.ndarray, last_index_in: int) -> int:
+        """ca_estimate_plan_rebase: `results` (this plan's last run, a writable copy) re-based
+        in place to the exact input lastIndex; returns the batch's exact output."""
+        lo = C.c_int32(0)
+        _check(self.lib.ca_estimate_plan_rebase(self.h, ptr(results), last_index_in, C.byref(lo)),
+               "ca_estimate_plan_rebase")
+        return lo.value
 
     def group_ticks(self) -> np.ndarray:
         """Per group of the last run: (chain device time in us, single-pod steps)."""

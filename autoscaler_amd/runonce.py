@@ -152,22 +152,27 @@ class DeviceUtil:
 
 class DeviceExpansion:
     """The device's expansion-option step: the node groups' templates resident in one
-    ca_expansion_plan (re-created only when the caller's templates array changes), the
+    ca_expansion_plan (re-created when the caller's templates change, in place or not), the
     results written by the kernel into a page-locked buffer.  Like DeviceUtil's rows, the
     returned array is overwritten by the next call."""
 
     def __init__(self):
         self.plan = None
         self.templates = None
+        self.tbytes = None
         self.rows = None
 
     def __call__(self, backend, podset, samples: np.ndarray, templates: np.ndarray) -> np.ndarray:
         from . import native
-        if self.plan is None or self.templates is not templates or self.plan.mirror is not backend:
+        # the resident rows are re-uploaded when the node groups change: a new array, or the
+        # same array updated in place (ADVICE r5: keyed on the content, not only the identity)
+        tb = np.ascontiguousarray(templates).tobytes()
+        if self.plan is None or self.templates is not templates or self.tbytes != tb or self.plan.mirror is not backend:
             if self.plan is not None:
                 self.plan.close()
             self.plan = native.ExpansionPlan(backend, templates)
             self.templates = templates
+            self.tbytes = tb
             self.rows = self.rows or native.PinnedRows()
         out = self.rows.zeros("res", len(templates) * len(samples), abi.PRED_RESULT_DTYPE, zero=False)
         return self.plan.run(podset, samples, out=out.reshape(len(templates), len(samples)))
@@ -346,3 +351,49 @@ def compare(a: RunOnceResult, b: RunOnceResult) -> dict:
         "sweep": bool(np.array_equal(a.sweep_results, b.sweep_results) and np.array_equal(a.sweep_dest, b.sweep_dest)
                       and np.array_equal(a.sweep_hints, b.sweep_hints)),
     }
+
+
+class ShardedMirror:
+    """One rank's backend of a loop run with one process per GPU: every rank
+    holds a replica of the snapshot (``mirror``) and applies the loop's snapshot changes
+    itself (FilterOutSchedulable, the expansion check and the utilization step run on each
+    replica: they mutate or read the whole snapshot); the two batches whose units shard —
+    Estimate's node groups and FindNodesToRemove's candidates — run one contiguous block
+    per rank (shard.estimate_sharded / shard.sweep_sharded) and every rank receives the
+    whole batch's results by all-gather, so the replicas stay identical for the next step.
+    ``ex`` is the rank's shard.Exchange (RCCL or gloo all-gathers)."""
+
+    def __init__(self, mirror, ex, rank: int, world: int):
+        self.m = mirror
+        self.ex = ex
+        self.rank = rank
+        self.world = world
+        self.stats = {}
+
+    def __getattr__(self, k):                     # podset, filter_out_schedulable, h, lib, ...
+        return getattr(self.m, k)
+
+    def estimate(self, table, group_off, pod_idx, templates, max_nodes, last_index=0, want_nodes=False, podset=None):
+        from . import native, shard
+        off = np.ascontiguousarray(group_off, np.int32)
+        blocks = shard.split_blocks(np.diff(off), self.world)
+        a, b = blocks[self.rank], blocks[self.rank + 1]
+        with native.EstimatePlan(self.m, table, (off[a:b + 1] - off[a]).astype(np.int32), pod_idx[off[a]:off[b]],
+                                 templates[a:b], podset=podset) as plan:
+            res, sched, L, reruns = shard.estimate_sharded(plan, max_nodes, last_index, self.ex, self.rank, blocks, off)
+        self.stats["estimate_reruns"] = reruns
+        return native.EstimateOutput(res, sched, None, L)
+
+    def find_nodes_to_remove(self, candidates, dest_mask, cand_status, move_off, move_pods, hints, last_index=0):
+        from . import native, shard
+        off = np.ascontiguousarray(move_off, np.int32)
+        blocks = shard.split_blocks(np.diff(off), self.world)
+        a, b = blocks[self.rank], blocks[self.rank + 1]
+        h = np.array(hints, dtype=np.int32, copy=True)
+        with native.RemovalPlan(self.m, candidates[a:b], dest_mask, cand_status[a:b],
+                                (off[a:b + 1] - off[a]).astype(np.int32), move_pods[off[a]:off[b]]) as plan:
+            sb, ph = shard.sweep_setup(plan, self.ex, self.rank, a == b)
+            res, dest, L, st = shard.sweep_sharded(plan, last_index, h, len(dest_mask), self.ex, self.rank, blocks, off,
+                                                   move_pods, sb, ph)
+        self.stats["sweep"] = {k: v for k, v in st.items() if k in ("reached", "serial_blocks")}
+        return native.RemovalOutput(res, dest, h, L)

@@ -21,7 +21,18 @@ all ranks' evaluations / the slowest rank's time.  CASIM_BENCH_SCALING=strong sp
 same 100 groups over the N GPUs instead (rank 0 drives them through
 ca_multi_estimate_plan_run, or CASIM_BENCH_MULTI=rccl: one block per rank).
 
+At N > 1 the line also carries the configs that name several GPUs, every rank running one
+contiguous block of units on its own mirror replica (one process per GPU, RCCL all-gathers
+over xGMI): extra.c3_multi (BASELINE configs[2]: the C3 sweep's candidates, the blocks'
+lastIndex chain composed in the phases of casim.h "one process per GPU"), extra.c4_multi
+(configs[3]: the C4 Estimate batch's node groups) and extra.c5_runonce_multi (configs[4]:
+one C5 RunOnce, Estimate and the sweep sharded), each with results_identical_to_1gpu, the
+collective bytes and the CPU port's time.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (--gpus N > 1 without WORLD_SIZE starts N ranks under torch.distributed.run itself;
+       with WORLD_SIZE set it must equal N.  Fewer GPUs than ranks: the ranks share devices
+       and use gloo — a rehearsal, said so in config.devices)
        torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -491,6 +502,256 @@ def runonce_leg(args, device: int, with_cpu: bool) -> dict:
     return out
 
 
+class RankCtx:
+    """One rank of a --gpus N > 1 run: torch.distributed handle, rank, world, device,
+    collective device and the byte all-gather (RCCL over xGMI; gloo when ranks share a
+    device in a rehearsal)."""
+
+    def __init__(self, dist, rank, world, local, coll_dev, shared):
+        from autoscaler_amd import shard
+        self.dist, self.rank, self.world, self.local, self.coll_dev = dist, rank, world, local, coll_dev
+        self.shared = shared
+        self.gather = shard.torch_gather_bytes(dist, coll_dev)
+
+    def timed(self, fn, steps: int, warmup: int):
+        """fn() `warmup` times, then `steps` times between barrier + device syncs; returns
+        (max over ranks of the elapsed seconds, last output)."""
+        import torch
+        out = None
+        for _ in range(warmup):
+            out = fn()
+        self.dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = fn()
+        torch.cuda.synchronize()
+        self.dist.barrier()
+        el = time.perf_counter() - t0
+        t = torch.tensor([el], dtype=torch.float64, device=self.coll_dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t[0]), out
+
+
+def _devices_note(ctx) -> str:
+    return (f"{ctx.world} ranks sharing {native_device_count()} device(s) (rehearsal, gloo collectives)"
+            if ctx.shared else f"{ctx.world} ranks, one GPU each, RCCL all-gathers over xGMI")
+
+
+def c3_multi_leg(args, ctx) -> dict:
+    """BASELINE configs[2] at N > 1: the C3 FindNodesToRemove sweep (5k nodes, 150k pods)
+    with its candidates in N contiguous blocks, one per rank (cluster.go:130-137),
+    each rank on its own mirror replica; the blocks' lastIndex chain composed in three
+    phases (casim.h "one process per GPU": PROBE, MAP, ca_sweep_compose, RESOLVE) and one
+    all-gather of every block's results, destinations and hints (shard.sweep_sharded).
+    One step = one whole sweep, results and hints on every rank.  'fresh' = the first loop,
+    'hinted' = the next loop from the first loop's hints."""
+    from autoscaler_amd import native, shard
+    from autoscaler_amd import workloads as W
+    w = W.c3(n_nodes=args.sweep_nodes)
+    R, rank = ctx.world, ctx.rank
+    blocks = shard.split_blocks(np.diff(w.move_off), R)
+    a, b = blocks[rank], blocks[rank + 1]
+    m = native.Mirror(ctx.local)
+    W.load_sweep(m, w)
+    plan = native.RemovalPlan(m, w.candidates[a:b], w.dest_mask, w.cand_status[a:b],
+                              (w.move_off[a:b + 1] - w.move_off[a]).astype(np.int32),
+                              w.move_pods[w.move_off[a]:w.move_off[b]])
+    ex = shard.Exchange(ctx.gather)
+    sb, ph = shard.sweep_setup(plan, ex, rank, a == b)
+    n = len(w.nodes)
+    fresh = np.full(len(w.table), -1, np.int32)
+    steps = max(args.steps, 10)
+    out = {"workload": f"C3: {args.sweep_nodes} nodes, {len(w.table)} running pods, candidates = all nodes, "
+                       f"in {R} contiguous blocks (candidates {blocks})",
+           "devices": _devices_note(ctx), "scaling": "strong (the same sweep over N GPUs)"}
+    h_in, L_in = fresh, 0
+    runs = {}
+    for mode in ("fresh", "hinted"):
+        hh = {}
+
+        def step():
+            h = h_in.copy()
+            r = shard.sweep_sharded(plan, L_in, h, n, ex, rank, blocks, w.move_off, w.move_pods, sb, ph)
+            hh["h"] = h
+            return r
+        b0, c0 = ex.bytes, ex.calls
+        el, (res, dest, L, st) = ctx.timed(step, steps, max(args.warmup, 3))
+        per = steps + max(args.warmup, 3)
+        runs[mode] = (res, dest, L, hh["h"], h_in, L_in)
+        out[f"{mode}_ms"] = el / steps * 1e3
+        out[f"{mode}_blocks_composed"] = st["reached"]
+        out[f"{mode}_blocks_serial"] = st["serial_blocks"]
+        out[f"{mode}_collective_bytes_per_rank"] = (ex.bytes - b0) / per
+        out[f"{mode}_collectives"] = (ex.calls - c0) / per
+        out[f"{mode}_removable"] = int(res["removable"].sum())
+        h_in, L_in = hh["h"], L
+    plan.close()
+    if rank == 0:
+        # the same sweeps on one GPU (one plan over every candidate, this rank's mirror)
+        with native.RemovalPlan(m, w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods) as one:
+            same = True
+            for mode in ("fresh", "hinted"):
+                res, dest, L, h_out, h0, L0 = runs[mode]
+                ts = []
+                for _ in range(5):
+                    h = h0.copy()
+                    t0 = time.perf_counter()
+                    r1 = one.run(L0, hints=h, want_dest=True)
+                    ts.append(time.perf_counter() - t0)
+                out[f"{mode}_1gpu_ms"] = float(np.median(ts) * 1e3)
+                same &= bool(np.array_equal(r1.results, res) and np.array_equal(r1.dest, dest)
+                             and r1.last_index == L and np.array_equal(h, h_out))
+            out["results_identical_to_1gpu"] = same
+        if not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import pyoracle                                           # CPU baseline leg only
+            o = pyoracle.OracleState()
+            W.load_sweep(o, w)
+            par = True
+            for mode in ("fresh", "hinted"):
+                res, dest, L, h_out, h0, L0 = runs[mode]
+                t0 = time.perf_counter()
+                ro = o.find_nodes_to_remove(w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods, h0, L0)
+                out[f"{mode}_cpu_ms"] = (time.perf_counter() - t0) * 1e3
+                out[f"{mode}_speedup"] = out[f"{mode}_cpu_ms"] / out[f"{mode}_ms"]
+                par &= bool(np.array_equal(ro.results, res) and np.array_equal(ro.dest, dest) and ro.last_index == L
+                            and np.array_equal(ro.hints, h_out))
+            out["parity_vs_oracle"] = par
+            out["cpu_baseline"] = {"kind": "port", "cores": 1,
+                                   "sample": f"oracle/casim_oracle.c FindNodesToRemove, the same C3 sweeps, 1 thread of "
+                                             f"{cpu_model()}"}
+    m.close()
+    return out
+
+
+def c4_multi_leg(args, ctx) -> dict:
+    """BASELINE configs[3] at N > 1: the C4 Estimate batch (50k pods x 100 groups, taints,
+    labels, node affinity) with its node groups in N contiguous blocks balanced by items,
+    one per rank on its own mirror replica, the lastIndex chain by all-gathers of a 4-int
+    record (a sensitive block run from a wrong input runs again; others are re-based), then
+    two all-gathers bring every rank the per-group records and scheduled pods
+    (shard.estimate_sharded).  One step = the whole batch, results on every rank's host."""
+    from autoscaler_amd import native, shard
+    from autoscaler_amd import workloads as W
+    w = W.c4(n_pods=args.pods, n_groups=args.groups, n_existing=args.existing, max_nodes=args.max_nodes)
+    R, rank = ctx.world, ctx.rank
+    blocks = shard.split_blocks(np.diff(w.group_off), R)
+    a, b = blocks[rank], blocks[rank + 1]
+    off = w.group_off
+    m = native.Mirror(ctx.local)
+    W.load_estimate(m, w)
+    plan = native.EstimatePlan(m, w.table, (off[a:b + 1] - off[a]).astype(np.int32), w.pod_idx[off[a]:off[b]],
+                               w.templates[a:b])
+    ex = shard.Exchange(ctx.gather)
+    steps = max(args.steps, 5)
+    b0, c0 = ex.bytes, ex.calls
+    rr = {"n": 0}
+
+    def step():
+        r = shard.estimate_sharded(plan, w.max_nodes, 0, ex, rank, blocks, off)
+        rr["n"] += r[3]
+        return r
+    el, (res, sched, L, _) = ctx.timed(step, steps, 2)
+    per = steps + 2
+    items = int(off[-1])
+    evals = int(res["evals"].sum())
+    out = {"workload": f"C4: {args.pods} pods x {args.groups} groups, taints/labels/affinity, {items} (pod, group) "
+                       f"items, in {R} contiguous blocks (groups {blocks})",
+           "devices": _devices_note(ctx), "scaling": "strong (the same batch over N GPUs)",
+           "estimate_ms": el / steps * 1e3, "evals": evals, "evals_per_s": evals / (el / steps),
+           "reruns_rank0": rr["n"] / per,
+           "collective_bytes_per_rank": (ex.bytes - b0) / per, "collectives": (ex.calls - c0) / per}
+    reruns = ex.gather(np.array([rr["n"]], np.int64))
+    out["block_reruns_all_ranks"] = int(sum(int(v[0]) for v in reruns)) / per
+    plan.close()
+    if rank == 0:
+        with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as one:
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                o1 = one.run(w.max_nodes, 0, want_nodes=False)
+                ts.append(time.perf_counter() - t0)
+            out["estimate_1gpu_ms"] = float(np.median(ts) * 1e3)
+            out["results_identical_to_1gpu"] = bool(np.array_equal(o1.results, res) and o1.last_index == L and all(
+                np.array_equal(o1.sched_pod[off[g]:off[g] + int(o1.results[g]["n_scheduled"])],
+                               sched[off[g]:off[g] + int(o1.results[g]["n_scheduled"])]) for g in range(len(off) - 1)))
+        if not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import pyoracle                                           # CPU baseline leg only
+            o = pyoracle.OracleState()
+            W.load_estimate(o, w)
+            t0 = time.perf_counter()
+            ro = o.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, 0)
+            out["cpu_ms"] = (time.perf_counter() - t0) * 1e3
+            out["speedup"] = out["cpu_ms"] / out["estimate_ms"]
+            out["parity_vs_oracle"] = bool(np.array_equal(ro.results, res) and ro.last_index == L and all(
+                np.array_equal(ro.sched_pod[off[g]:off[g] + int(ro.results[g]["n_scheduled"])],
+                               sched[off[g]:off[g] + int(ro.results[g]["n_scheduled"])]) for g in range(len(off) - 1)))
+            out["cpu_baseline"] = {"kind": "port", "cores": 1,
+                                   "sample": f"oracle/casim_oracle.c, the same C4 batch, 1 thread of {cpu_model()}"}
+    m.close()
+    return out
+
+
+def c5_multi_leg(args, ctx) -> dict:
+    """BASELINE configs[4] at N > 1: one C5 RunOnce (15k nodes, 300k pods, 20k pending,
+    100 node groups) with one process per GPU (runonce.ShardedMirror): every rank applies
+    FilterOutSchedulable, the expansion check and the utilization step to its replica; the
+    Estimate of every option and FindNodesToRemove run one block of node groups /
+    candidates per rank, results all-gathered to every rank.  One step = one loop inside a
+    fork reverted after it."""
+    from autoscaler_amd import native, runonce, shard
+    from autoscaler_amd import workloads as W
+    w = runonce.c5_runonce()
+    m = native.Mirror(ctx.local)
+    W.load_filter(m, w.filt)
+    ex = shard.Exchange(ctx.gather)
+    sm = runonce.ShardedMirror(m, ex, ctx.rank, ctx.world)
+    util = runonce.DeviceUtil(ctx.local)
+    expand = runonce.DeviceExpansion()
+    loops = []
+
+    def step():
+        m.fork()
+        r = runonce.run(sm, util, w, expand_fn=expand)
+        m.revert()
+        loops.append(r)
+        return r
+    steps = max(2, min(args.steps, 4))
+    b0 = ex.bytes
+    el, r = ctx.timed(step, steps, 1)
+    keys = list(r.ms)
+    out = {"workload": "C5 RunOnce: 15000 nodes, 300000 running pods, 20000 pending, 100 node groups; Estimate and "
+                       f"FindNodesToRemove in {ctx.world} blocks (one per rank), the other legs on every replica",
+           "devices": _devices_note(ctx), "scaling": "strong (the same loop over N GPUs)",
+           "loop_ms": el / steps * 1e3,
+           "gpu_ms_rank0": {k: float(np.median([x.ms[k] for x in loops[1:]])) for k in keys},
+           "sizes": r.sizes, "sweep_blocks": sm.stats.get("sweep"),
+           "collective_bytes_per_rank_per_loop": (ex.bytes - b0) / (steps + 1)}
+    if ctx.rank == 0:
+        m.fork()
+        r1 = runonce.run(m, util, w, expand_fn=expand)           # the same loop on one GPU
+        m.revert()
+        out["gpu_ms_1gpu"] = r1.ms
+        out["results_identical_to_1gpu"] = runonce.compare(r1, r)
+        if not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import pyoracle                                           # CPU baseline leg only
+            o = pyoracle.OracleState()
+            W.load_filter(o, w.filt)
+            ro = runonce.run(o, pyoracle.runonce_cpu_util, w)
+            out["cpu_ms"] = ro.ms
+            out["speedup_total"] = ro.ms["total"] / out["loop_ms"]
+            out["parity_vs_oracle"] = runonce.compare(ro, r)
+            out["cpu_baseline"] = {"kind": "port", "cores": 1,
+                                   "sample": f"oracle/casim_oracle.c, the same loop step by step, 1 thread of {cpu_model()}"}
+    expand.close()
+    util.close()
+    m.close()
+    return out
+
+
 def split_groups(group_off, world: int) -> list:
     """Contiguous blocks of node groups, one per rank, balanced by (pod, group) items (the
     same split as ca_multi_estimate_plan, multi.hip:split_blocks)."""
@@ -670,14 +931,41 @@ def multi_main(args, world: int, rank: int, dist, coll_dev: str):
     return result
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """--gpus N > 1 without a launcher: start N ranks under torch.distributed.run as a child
+    process (nothing here has touched a GPU) and return its exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))         # --gpus is authoritative: N ranks, one per GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+              f"(torchrun --nproc-per-node {args.gpus} bench.py --gpus {args.gpus})", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal of the N>1 path on fewer GPUs (CASIM_BENCH_BACKEND=gloo: ranks share devices
-    # round-robin, collectives over gloo on host tensors); the driver's runs use RCCL
-    backend = os.environ.get("CASIM_BENCH_BACKEND", "nccl")
+    # RCCL when every rank has a GPU of its own; with fewer GPUs than ranks (a rehearsal of
+    # the N > 1 path on a one-GPU box) the ranks share devices round-robin and the collectives
+    # run over gloo on host tensors (CASIM_BENCH_BACKEND overrides)
+    shared = False
+    if world > 1:
+        import torch
+        shared = torch.cuda.device_count() < world
+    backend = os.environ.get("CASIM_BENCH_BACKEND", "gloo" if shared else "nccl")
     # N > 1: weak scaling by default — one Estimate batch of groups x N node groups, each
     # rank its own block of `groups` groups (rank 0's block is exactly the N = 1 workload),
     # the blocks chained through the checker's lastIndex by one all_gather of a 4-int record
@@ -688,8 +976,8 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        if backend != "nccl":
-            local = local % max(1, native_device_count())
+        if backend != "nccl" or shared:
+            local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         dist.init_process_group(backend)          # "nccl" is RCCL on ROCm
         if scaling == "strong" and os.environ.get("CASIM_BENCH_MULTI", "capi") != "rccl":
@@ -859,6 +1147,17 @@ def main():
                 traffic = rec.get("traffic_bytes_per_step", rec["traffic_bytes_per_launch"])
                 traffic_src = f"profiles/pmc_traffic.json ({tj.get('source', '')})"
 
+    # N > 1: configs 3-5 beside the C2 line, every rank taking part (one block each)
+    multi_legs = {}
+    if dist is not None:
+        ctx = RankCtx(dist, rank, world, local, coll_dev, shared)
+        if not args.no_sweep:
+            multi_legs["c3_multi"] = c3_multi_leg(args, ctx)
+        if not args.no_c4:
+            multi_legs["c4_multi"] = c4_multi_leg(args, ctx)
+        if not args.no_runonce:
+            multi_legs["c5_runonce_multi"] = c5_multi_leg(args, ctx)
+
     result = None
     if rank == 0:
         cpu = None
@@ -936,6 +1235,10 @@ def main():
                 "speedup_vs_cpu_baseline": (total_evals / elapsed) / cpu["value"] if cpu else None,
             },
         }
+        result["extra"].update(multi_legs)
+        if shared:
+            result["config"]["devices"] = f"{world} ranks sharing {torch.cuda.device_count()} GPU(s): a rehearsal " \
+                                          "of the N-GPU launch (gloo collectives), not an N-GPU measurement"
         if world == 1 and not args.no_sweep:
             result["extra"]["sweep"] = sweep_leg(args, local, not args.no_cpu_baseline)
         if world == 1 and not args.no_c4:

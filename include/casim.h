@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define CASIM_ABI_VERSION 2
+#define CASIM_ABI_VERSION 3
 
 /* ---- status codes (int return of every entry point) -------------------- */
 #define CA_OK            0
@@ -442,6 +442,13 @@ int ca_estimate_plan_set_phase_timing(ca_estimate_plan* p, int32_t on);
  * whether any FitsAnyNode call succeeded (if not, lastIndex passed through unchanged).
  * Used to chain batches sharded across GPUs. */
 int ca_estimate_plan_chain_info(const ca_estimate_plan* p, int32_t* lin_sensitive, int32_t* had_success);
+/* A run whose outputs do not depend on its input lastIndex (chain_info: not sensitive) but
+ * that started from a wrong one: rewrite its results' last_index_in / last_index_out fields
+ * for the exact input last_index_in (the run's own results[], in place) and return the
+ * batch's exact output in *last_index_out (may be NULL).  The one-process-per-GPU form of
+ * the node-group chain calls it on every rank after the walk. */
+int ca_estimate_plan_rebase(const ca_estimate_plan* p, ca_estimate_result* results, int32_t last_index_in,
+                            int32_t* last_index_out);
 /* Diagnostics of the last run's first chain launch, one entry per group: the chain's
  * device wall-clock ticks (100 MHz) in bits 0-31, the number of single-pod steps (pods
  * not placed by the closed-form run path) in bits 32-63.  Returns the group count. */
@@ -648,6 +655,56 @@ int ca_multi_find_nodes_to_remove(ca_multi* mm, const int32_t* candidates, int32
                                   const uint8_t* dest_mask, const int32_t* cand_status, const int32_t* move_off,
                                   const int32_t* move_pods, int32_t* hints, int32_t n_pods, int32_t* last_index,
                                   ca_removal_result* results, int32_t* out_dest);
+
+/* ---- one process per GPU: the sweep's phases ---------------------
+ * A caller with one process per GPU (each holding its own mirror replica and a removal plan
+ * over its contiguous block of candidates, blocks in candidate order) composes the blocks'
+ * lastIndex chain itself, exchanging one fixed-size ca_sweep_phase record per block per
+ * phase over its own transport (an RCCL all_gather over xGMI, or any all-gather) — the three
+ * phases ca_multi_removal_plan_run runs inside one process:
+ *   0. once per plan: ca_removal_plan_sensitive_pods; block d's guess_base = L0 + the sum
+ *      over the blocks before it (the probe's rough guess of its input);
+ *   1. PROBE   run_phase(kind = PROBE, guess_base): out adv (the block's lastIndex advance as
+ *              its successful scans saw it), succ, n_sensitive.  All-gather the records.
+ *   2. MAP     est_base = (L0 + the earlier blocks' adv) mod n_nodes; run_phase(kind = MAP):
+ *              every block with n_sensitive > 0 builds its tables and its map (lastIndex out
+ *              by class of its input).  All-gather the records.
+ *   3. ca_sweep_compose(all records, L0) -> each block's exact input lastIndex, or
+ *      CA_SWEEP_NOT_REACHED after the first block the maps cannot carry the chain through.
+ *   4. RESOLVE run_phase(kind = RESOLVE, *last_index = the composed input): the block's
+ *      results, out_dest and hints (Hints.Set of its candidates' pods), exact.  A block not
+ *      reached runs ca_removal_plan_run from its exact input once its predecessors are final.
+ * The chain is then the blocks' last_index outputs in order.  Between a plan's PROBE and its
+ * RESOLVE nothing else may use its mirror; hints must not be NULL (caller-held hints); a plan
+ * with a prefix-protocol cut (an out-of-scope candidate) runs whole calls only
+ * (ca_removal_plan_phased reports 0). */
+#define CA_SWEEP_PHASE_PROBE    1
+#define CA_SWEEP_PHASE_MAP      2
+#define CA_SWEEP_PHASE_RESOLVE  3
+#define CA_SWEEP_MAP_INTS       130           /* 64 outputs + 65 fit points + class mode */
+#define CA_SWEEP_NOT_REACHED    INT32_MIN
+
+typedef struct ca_sweep_phase {
+    int32_t kind;                             /* CA_SWEEP_PHASE_*                        */
+    int32_t est_base;                         /* MAP in: the estimate of the block's input */
+    int64_t guess_base;                       /* PROBE in                                */
+    int64_t adv;                              /* PROBE out                               */
+    int32_t succ;                             /* PROBE out: candidates with a successful scan */
+    int32_t n_sensitive;                      /* PROBE/MAP out: lastIndex-sensitive candidates */
+    int32_t map_ran;                          /* MAP out: tables built by this call      */
+    int32_t map_ok;                           /* MAP out: map[] valid                    */
+    int32_t map[CA_SWEEP_MAP_INTS];           /* MAP out                                 */
+} ca_sweep_phase;
+
+int ca_removal_plan_sensitive_pods(const ca_removal_plan* p, int64_t* out);
+int ca_removal_plan_phased(const ca_removal_plan* p, int32_t* out);
+/* hints[n_pods] caller-held (PROBE and MAP read them; RESOLVE updates the block's pods) */
+int ca_removal_plan_run_phase(ca_removal_plan* p, ca_sweep_phase* ph, int32_t* hints, int32_t* last_index,
+                              ca_removal_result* results, int32_t* out_dest);
+/* recs[D]: every block's MAP record, in block order; lin[D] = each block's input lastIndex
+ * or CA_SWEEP_NOT_REACHED; *n_reached (may be NULL) = the blocks reached. */
+int ca_sweep_compose(const ca_sweep_phase* recs, int32_t n_blocks, int32_t n_nodes, int32_t last_index,
+                     int32_t* lin, int32_t* n_reached);
 
 /* ---- planner: committing removal simulation ----------------------
  * Planner.categorizeNodes' simulation loop (CA/core/scaledown/planner/planner.go:252-296)

@@ -30,6 +30,7 @@ if "--bulk" in args:                    # (with --prof) fbcyc = mixed runs' chai
 if "--phases" in args:                  # host phase marks of every call on stderr (filter.hip tmark)
     args.remove("--phases")
     os.environ["CASIM_DEBUG_TIMING"] = "1"
+    os.environ["CASIM_KNOBS"] = "1"
 names = args or list(CFGS)
 for name in names:
     w = W.c5_filter(**CFGS[name])

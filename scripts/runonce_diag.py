@@ -13,6 +13,7 @@ from autoscaler_amd import workloads as W  # noqa: E402
 
 if "--phases" in sys.argv:
     os.environ["CASIM_DEBUG_TIMING"] = "1"
+    os.environ["CASIM_KNOBS"] = "1"
 w = runonce.c5_runonce()
 m = native.Mirror(0)
 W.load_filter(m, w.filt)

@@ -1,5 +1,6 @@
 """The C-ABI library loads, exports every symbol include/casim.h declares, and the
 Python binding's record layouts match the compiled structs (no compute calls)."""
+import numpy as np
 import ctypes as C
 import os
 import re
@@ -48,3 +49,27 @@ def test_no_device_here_fails_loudly():
         pytest.skip("a HIP device is present")
     with pytest.raises(native.CasimError):
         native.Mirror(0)
+
+
+def test_sweep_compose_host_rule():
+    """ca_sweep_compose (casim.h "one process per GPU"): a block without a successful probe
+    passes lastIndex through; a block with a map picks its entry by the class of its input
+    (consecutive-window mode: input - window start); the chain stops at a block without a
+    map or whose window misses the input."""
+    recs = np.zeros(4, abi.SWEEP_PHASE_DTYPE)
+    recs[0]["n_sensitive"] = 0                       # nothing sensitive: pass-through
+    recs[1]["n_sensitive"], recs[1]["succ"], recs[1]["map_ok"] = 3, 2, 1
+    recs[1]["map"][65] = 10                          # window [10, 74): class of L = L - 10
+    recs[1]["map"][:64] = 1000 + np.arange(64)
+    recs[2]["n_sensitive"], recs[2]["succ"], recs[2]["map_ok"] = 1, 1, 1
+    recs[2]["map"][65] = 2000                        # window [2000, 2064): the input 1017 misses
+    recs[3]["n_sensitive"], recs[3]["succ"] = 0, 0
+    lin = native.sweep_compose(recs, 5000, 17)
+    assert lin.tolist() == [17, 17, abi.CA_SWEEP_NOT_REACHED, abi.CA_SWEEP_NOT_REACHED]
+    recs[2]["map"][65] = 1000
+    recs[2]["map"][:64] = -1
+    recs[2]["map"][7] = 4321
+    lin = native.sweep_compose(recs, 5000, 17)
+    assert lin.tolist() == [17, 17, 1007, 4321]
+    recs[1]["map_ok"] = 0
+    assert native.sweep_compose(recs, 5000, 17).tolist()[1:] == [abi.CA_SWEEP_NOT_REACHED] * 3

@@ -192,3 +192,72 @@ def test_multi_estimate_c4_full(oracle):
         assert st["blocks"] == 2
     for m in ms:
         m.close()
+
+
+def test_multi_sweep_loops_reuse_plan(oracle):
+    """a range whose probe makes no successful scan but has sensitive candidates
+    must build this call's tables before it resolves (never walk an earlier call's).  One
+    plan on 4 replicas of a 300-node C3, loops in the order fresh, hinted, fresh from another
+    input, hinted again, and a second plan whose very first call is the hinted loop: every
+    call against the oracle."""
+    w = W.c3(n_nodes=300)
+    args = (w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods)
+    o = oracle.OracleState()
+    W.load_sweep(o, w)
+    fresh = np.full(len(w.table), -1, np.int32)
+    o1 = o.find_nodes_to_remove(*args, fresh, 7)
+    o2 = o.find_nodes_to_remove(*args, o1.hints, o1.last_index)
+    o3 = o.find_nodes_to_remove(*args, fresh, 123)
+    o4 = o.find_nodes_to_remove(*args, o1.hints, 45)
+    seq = [(fresh, 7, o1), (o1.hints, o1.last_index, o2), (fresh, 123, o3), (o1.hints, 45, o4), (o1.hints, 45, o4)]
+    ms = _replicas(4, lambda m: W.load_sweep(m, w))
+    with native.Multi(ms) as mm:
+        with native.MultiRemovalPlan(mm, *args) as plan:
+            for h, L, ro in seq:
+                g = plan.run(h.copy(), L)
+                assert np.array_equal(ro.results, g.results) and ro.last_index == g.last_index
+                assert np.array_equal(ro.dest, g.dest) and np.array_equal(ro.hints, g.hints)
+        with native.MultiRemovalPlan(mm, *args) as plan:           # first call: the hinted loop
+            for h, L, ro in seq[3:] + seq[:2]:
+                g = plan.run(h.copy(), L)
+                assert np.array_equal(ro.results, g.results) and ro.last_index == g.last_index
+                assert np.array_equal(ro.dest, g.dest) and np.array_equal(ro.hints, g.hints)
+    for m in ms:
+        m.close()
+
+
+@pytest.mark.parametrize("what", ["estimate", "sweep"])
+def test_multi_distinct_devices(what, oracle):
+    """Replicas on distinct devices (one per GPU): per-thread device binding, each device's
+    zero-copy publisher writing its slice of one page-locked buffer, events and streams per
+    device.  Same outputs as the oracle.  Skipped on a one-GPU box."""
+    if native.device_count() < 2:
+        pytest.skip("needs two or more GPUs: replicas on distinct devices")
+    D = min(native.device_count(), 4)
+    if what == "estimate":
+        w = W.c2(n_pods=6000, n_groups=16, n_existing=100)
+        o = oracle.OracleState()
+        W.load_estimate(o, w)
+        ro = o.estimate(w.table, w.group_off, w.pod_idx, w.templates, w.max_nodes, 3)
+        ms = [native.Mirror(d) for d in range(D)]
+        for m in ms:
+            W.load_estimate(m, w)
+        with native.Multi(ms) as mm, native.MultiEstimatePlan(mm, w.table, w.group_off, w.pod_idx, w.templates) as plan:
+            for _ in range(2):
+                g = plan.run(w.max_nodes, 3)
+                _eq_estimate(ro, g, w.group_off)
+    else:
+        w = W.c3(n_nodes=1500)
+        args = (w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods)
+        o = oracle.OracleState()
+        W.load_sweep(o, w)
+        o1 = o.find_nodes_to_remove(*args, np.full(len(w.table), -1, np.int32), 0)
+        ms = [native.Mirror(d) for d in range(D)]
+        for m in ms:
+            W.load_sweep(m, w)
+        with native.Multi(ms) as mm, native.MultiRemovalPlan(mm, *args) as plan:
+            g = plan.run(np.full(len(w.table), -1, np.int32), 0)
+            assert np.array_equal(o1.results, g.results) and o1.last_index == g.last_index
+            assert np.array_equal(o1.dest, g.dest) and np.array_equal(o1.hints, g.hints)
+    for m in ms:
+        m.close()

@@ -198,3 +198,94 @@ def test_sharded_sweep_gloo_world2(n_nodes, oracle_lib):
     res.sort()
     assert all(ok for _, ok, _ in res), res
     assert res[1][2] >= 1                       # rank 1 re-ran from rank 0's lastIndex
+
+
+def test_split_blocks_matches_library_rule():
+    from autoscaler_amd.shard import split_blocks
+    assert split_blocks([5, 5, 5, 5], 2) == [0, 2, 4]
+    assert split_blocks([1, 1, 1], 5) == [0, 1, 2, 3, 3, 3]
+    assert split_blocks([], 3) == [0, 0, 0, 0]
+    b = split_blocks([30] * 100, 8)
+    assert b[0] == 0 and b[-1] == 100 and len(b) == 9 and all(b[i] < b[i + 1] for i in range(8))
+
+
+class _OracleBlockPlan:
+    """A block's removal plan on the CPU restatement (test infrastructure): whole calls
+    only (phased() False), as a plan with a prefix-protocol cut runs."""
+
+    def __init__(self, o, w, a, b):
+        self.o, self.w = o, w
+        self.cand = w.candidates[a:b]
+        self.status = w.cand_status[a:b]
+        self.off = (w.move_off[a:b + 1] - w.move_off[a]).astype(np.int32)
+        self.moves = w.move_pods[w.move_off[a]:w.move_off[b]]
+
+    def sensitive_pods(self):
+        return 0
+
+    def phased(self):
+        return False
+
+    def run(self, lin, hints=None, want_dest=True):
+        from autoscaler_amd import native
+        ro = self.o.find_nodes_to_remove(self.cand, self.w.dest_mask, self.status, self.off, self.moves, hints.copy(),
+                                         lin)
+        hints[self.moves] = ro.hints[self.moves]
+        return native.RemovalOutput(ro.results, ro.dest, hints, ro.last_index)
+
+
+def _sweep_serial_worker(rank, world, port, n_nodes, q):
+    """shard.sweep_sharded's whole-call path (blocks in order, one all-gather each) and its
+    final exchange of results, destinations and hints, on the CPU restatement."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "oracle"), os.path.join(root, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    import pyoracle
+    from autoscaler_amd import shard
+    from autoscaler_amd import workloads as W
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w = W.c3(n_nodes=n_nodes)
+        blocks = shard.split_blocks(np.diff(w.move_off), world)
+        o = pyoracle.OracleState()
+        W.load_sweep(o, w)
+        plan = _OracleBlockPlan(o, w, blocks[rank], blocks[rank + 1])
+        ex = shard.Exchange(shard.torch_gather_bytes(dist, "cpu"))
+        sb, ph = shard.sweep_setup(plan, ex, rank, blocks[rank] == blocks[rank + 1])
+        ok = True
+        h_ref = np.full(len(w.table), -1, np.int32)
+        hints = h_ref.copy()
+        L = 11
+        for loop in range(2):
+            res, dest, final_L, st = shard.sweep_sharded(plan, L, hints, len(w.nodes), ex, rank, blocks, w.move_off,
+                                                         w.move_pods, sb, ph)
+            ref = o.find_nodes_to_remove(w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods, h_ref, L)
+            ok &= np.array_equal(res, ref.results) and np.array_equal(dest, ref.dest)
+            ok &= final_L == ref.last_index and np.array_equal(hints, ref.hints)
+            ok &= st["serial_blocks"] == world
+            h_ref, L = ref.hints.copy(), ref.last_index
+        q.put((rank, bool(ok), 0))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_sweep_exchange_gloo(world, oracle_lib):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sweep_serial_worker, args=(r, world, port, 200, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res), res

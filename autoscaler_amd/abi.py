@@ -185,6 +185,7 @@ EXPECTED_SIZES = [
     C.sizeof(LimiterC), ESTIMATE_RESULT_DTYPE.itemsize, REMOVAL_RESULT_DTYPE.itemsize,
     UTIL_NODE_DTYPE.itemsize, UTIL_POD_DTYPE.itemsize, UTIL_INFO_DTYPE.itemsize,
     PLAN_RESULT_DTYPE.itemsize, PLAN_MOVE_DTYPE.itemsize, SWEEP_PHASE_DTYPE.itemsize,
+    16, 24, 32, 24, 32,          # ca_str_pair, ca_taint_str, ca_toleration_str, ca_port_str, ca_requirement_str
 ]
 
 

@@ -892,7 +892,9 @@ int ca_abi_struct_sizes(int32_t* out, int32_t cap) {
                          (int32_t)sizeof(ca_removal_result), (int32_t)sizeof(ca_util_node),
                          (int32_t)sizeof(ca_util_pod), (int32_t)sizeof(ca_util_info),
                          (int32_t)sizeof(ca_plan_result), (int32_t)sizeof(ca_plan_move),
-                         (int32_t)sizeof(ca_sweep_phase)};
+                         (int32_t)sizeof(ca_sweep_phase), (int32_t)sizeof(ca_str_pair), (int32_t)sizeof(ca_taint_str),
+                         (int32_t)sizeof(ca_toleration_str), (int32_t)sizeof(ca_port_str),
+                         (int32_t)sizeof(ca_requirement_str)};
     const int32_t n = (int32_t)(sizeof s / sizeof s[0]);
     for (int32_t i = 0; i < n && i < cap; i++) out[i] = s[i];
     return n;

@@ -129,6 +129,22 @@ def load() -> C.CDLL:
         "ca_plan_stats": ([vp, p(i32), p(i32), p(i32), p(C.c_float)], C.c_int),
         "ca_plan_last_path": ([vp], C.c_int),
         "ca_plan_chain_profile": ([vp, vp, i32, vp], C.c_int),
+        "ca_interner_create": ([p(vp)], C.c_int),
+        "ca_interner_destroy": ([vp], C.c_int),
+        "ca_interner_size": ([vp, i32, p(i32), p(i32)], C.c_int),
+        "ca_is_scalar_resource": ([C.c_char_p], C.c_int),
+        "ca_intern_taint": ([vp, C.c_char_p, C.c_char_p, C.c_char_p, p(i32)], C.c_int),
+        "ca_intern_label_pair": ([vp, C.c_char_p, C.c_char_p, p(i32)], C.c_int),
+        "ca_intern_label_key": ([vp, C.c_char_p, p(i32)], C.c_int),
+        "ca_intern_int_key": ([vp, C.c_char_p, p(i32)], C.c_int),
+        "ca_intern_port": ([vp, C.c_char_p, C.c_char_p, i32, p(i32)], C.c_int),
+        "ca_intern_resource": ([vp, C.c_char_p, p(i32)], C.c_int),
+        "ca_intern_name": ([vp, C.c_char_p, p(i32)], C.c_int),
+        "ca_intern_encode_node": ([vp, vp, i32, vp, i32, vp], C.c_int),
+        "ca_intern_encode_tolerations": ([vp, vp, i32, vp, p(i32)], C.c_int),
+        "ca_intern_encode_ports": ([vp, vp, i32, vp, p(i32)], C.c_int),
+        "ca_intern_encode_node_selector": ([vp, vp, i32, vp, p(i32)], C.c_int),
+        "ca_intern_compile_term": ([vp, vp, i32, vp, i32, p(i32), p(i32)], C.c_int),
     }
     for name, (args, res) in sigs.items():
         if path != LIB_PATH and not hasattr(lib, name):
@@ -182,6 +198,10 @@ def exported_symbols() -> list[str]:
         "ca_multi_removal_plan_rerun_units", "ca_multi_removal_plan_timings",
         "ca_multi_removal_plan_destroy", "ca_multi_find_nodes_to_remove",
         "ca_plan_removals", "ca_plan_last_moves", "ca_plan_stats", "ca_plan_last_path", "ca_plan_chain_profile",
+        "ca_interner_create", "ca_interner_destroy", "ca_interner_size", "ca_is_scalar_resource", "ca_intern_taint",
+        "ca_intern_label_pair", "ca_intern_label_key", "ca_intern_int_key", "ca_intern_port", "ca_intern_resource",
+        "ca_intern_name", "ca_intern_encode_node", "ca_intern_encode_tolerations", "ca_intern_encode_ports",
+        "ca_intern_encode_node_selector", "ca_intern_compile_term",
     ]
 
 
@@ -1092,3 +1112,128 @@ class MultiRemovalPlan:
 
     def __exit__(self, *a):
         self.close()
+
+
+# ---- interning through the C ABI (casim.h "interning"; host-only, no device needed) ------
+
+class _StrPair(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("value", C.c_char_p)]
+
+
+class _TaintStr(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("value", C.c_char_p), ("effect", C.c_char_p)]
+
+
+class _TolerationStr(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("op", C.c_char_p), ("value", C.c_char_p), ("effect", C.c_char_p)]
+
+
+class _PortStr(C.Structure):
+    _fields_ = [("host_ip", C.c_char_p), ("protocol", C.c_char_p), ("host_port", C.c_int32), ("reserved", C.c_int32)]
+
+
+class _RequirementStr(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("op", C.c_char_p), ("values", C.POINTER(C.c_char_p)), ("n_values", C.c_int32),
+                ("is_field", C.c_int32)]
+
+
+def _b(x) -> bytes:
+    return (x or "").encode()
+
+
+class CInterner:
+    """``ca_interner``: the library's interning (what a cgo shim binds), driven with Python
+    strings.  Ids and encodings equal autoscaler_amd/intern.py's (tests/test_intern_c.py)."""
+
+    def __init__(self):
+        self.lib = load()
+        h = C.c_void_p()
+        _check(self.lib.ca_interner_create(C.byref(h)), "ca_interner_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.ca_interner_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _id(self, fn, *a) -> int:
+        i = C.c_int32(0)
+        _check(getattr(self.lib, fn)(self.h, *a, C.byref(i)), fn)
+        return i.value
+
+    def taint(self, k, v, e):
+        return self._id("ca_intern_taint", _b(k), _b(v), _b(e))
+
+    def label_pair(self, k, v):
+        return self._id("ca_intern_label_pair", _b(k), _b(v))
+
+    def label_key(self, k):
+        return self._id("ca_intern_label_key", _b(k))
+
+    def int_key(self, k):
+        return self._id("ca_intern_int_key", _b(k))
+
+    def port(self, ip, proto, port):
+        return self._id("ca_intern_port", _b(ip), _b(proto), int(port))
+
+    def resource(self, name):
+        return self._id("ca_intern_resource", _b(name))
+
+    def name(self, n):
+        return self._id("ca_intern_name", _b(n))
+
+    def size(self, universe: int) -> tuple:
+        n, o = C.c_int32(0), C.c_int32(0)
+        _check(self.lib.ca_interner_size(self.h, universe, C.byref(n), C.byref(o)), "ca_interner_size")
+        return n.value, o.value
+
+    def encode_node(self, labels: dict, taints, rec) -> None:
+        """labels {k: v}; taints [(key, value, effect)]; rec: an abi.NODE_DTYPE record (array of 1)."""
+        lb = (_StrPair * max(len(labels), 1))(*[_StrPair(_b(k), _b(v)) for k, v in labels.items()])
+        tt = (_TaintStr * max(len(taints), 1))(*[_TaintStr(_b(k), _b(v), _b(e)) for k, v, e in taints])
+        _check(self.lib.ca_intern_encode_node(self.h, lb, len(labels), tt, len(taints), rec.ctypes.data),
+               "ca_intern_encode_node")
+
+    def encode_tolerations(self, tols, rec) -> int:
+        """tols [(key, op, value, effect)]; rec: abi.POD_DTYPE array of 1.  Returns out_of_scope."""
+        tt = (_TolerationStr * max(len(tols), 1))(*[_TolerationStr(_b(k), _b(o), _b(v), _b(e)) for k, o, v, e in tols])
+        o = C.c_int32(0)
+        _check(self.lib.ca_intern_encode_tolerations(self.h, tt, len(tols), rec.ctypes.data, C.byref(o)),
+               "ca_intern_encode_tolerations")
+        return o.value
+
+    def encode_ports(self, ports, rec) -> int:
+        """ports [(host_ip, protocol, host_port)] of the pod's containers."""
+        pp = (_PortStr * max(len(ports), 1))(*[_PortStr(_b(i), _b(pr), int(pt), 0) for i, pr, pt in ports])
+        o = C.c_int32(0)
+        _check(self.lib.ca_intern_encode_ports(self.h, pp, len(ports), rec.ctypes.data, C.byref(o)),
+               "ca_intern_encode_ports")
+        return o.value
+
+    def encode_node_selector(self, sel: dict, rec) -> int:
+        ss = (_StrPair * max(len(sel), 1))(*[_StrPair(_b(k), _b(v)) for k, v in sel.items()])
+        o = C.c_int32(0)
+        _check(self.lib.ca_intern_encode_node_selector(self.h, ss, len(sel), rec.ctypes.data, C.byref(o)),
+               "ca_intern_encode_node_selector")
+        return o.value
+
+    def compile_term(self, reqs) -> tuple:
+        """reqs [(key, op, [values], is_field)] -> (abi.REQ_DTYPE rows, out_of_scope)."""
+        keep = []
+        rr = (_RequirementStr * max(len(reqs), 1))()
+        for i, (k, op, vals, f) in enumerate(reqs):
+            va = (C.c_char_p * max(len(vals), 1))(*[_b(v) for v in vals])
+            keep.append(va)
+            rr[i] = _RequirementStr(_b(k), _b(op), C.cast(va, C.POINTER(C.c_char_p)), len(vals), int(bool(f)))
+        out = np.zeros(max(len(reqs), 1), abi.REQ_DTYPE)
+        nr, o = C.c_int32(0), C.c_int32(0)
+        _check(self.lib.ca_intern_compile_term(self.h, rr, len(reqs), out.ctypes.data, len(out), C.byref(nr),
+                                               C.byref(o)), "ca_intern_compile_term")
+        del keep
+        return out[: nr.value], o.value

@@ -706,6 +706,83 @@ int ca_removal_plan_run_phase(ca_removal_plan* p, ca_sweep_phase* ph, int32_t* h
 int ca_sweep_compose(const ca_sweep_phase* recs, int32_t n_blocks, int32_t n_nodes, int32_t last_index,
                      int32_t* lin, int32_t* n_reached);
 
+/* ---- interning: API values -> the records' ids and bitsets --------
+ * What a cgo shim does before it fills ca_node_spec / ca_pod_spec / ca_selector_req
+ * records, here so the shim binds it instead of restating it:
+ *   taint classes   NoSchedule/NoExecute (key, value, effect) — other effects are not
+ *                   filter taints (V/k8s.io/component-helpers/scheduling/corev1/helpers.go:78-101)
+ *   label pairs     (key, value) referenced by nodeSelector / In / NotIn
+ *   label keys      keys referenced by Exists / DoesNotExist
+ *   int keys        keys referenced by Gt / Lt (node values parsed as strconv.ParseInt)
+ *   ports           (hostIP, protocol, hostPort), sanitised as HostPortInfo.sanitize
+ *                   (SF/types.go:923-931: "" -> 0.0.0.0 / TCP; hostPort <= 0 ignored)
+ *   scalars         IsScalarResourceName (scheduler/util/utils.go:158-161; fit.go:160-176)
+ *   names           node names (spec.nodeName, matchFields metadata.name, name_id)
+ * Protocol: intern every value of every object the call will see first (nodes, templates,
+ * pods — autoscaler_amd/intern.py:Interner.observe), then encode the records: port
+ * conflicts and toleration masks range over every value interned so far.  Universes have
+ * the records' fixed widths; a value past a width gets id -1 (remembered as overflow: a
+ * node taint past the width sets bit 63, which a pod's mask covers only when it tolerates
+ * every overflow taint), and an encoder reports *out_of_scope = 1 for a pod whose
+ * simulation would need such a value — the shim then sets CA_POD_OUT_OF_SCOPE (prefix
+ * protocol).  Quantities (MilliValue / Value), score sums, PreFilter NodeNames, scope and
+ * hostname flags stay with the shim (Go has them natively; intern.py shows each).  Pinned
+ * with autoscaler_amd/intern.py by tests/golden/intern_fixtures.json (tests/c_abi/
+ * intern_driver.c replays tests/golden/intern_calls.txt, generated from those cases). */
+typedef struct ca_interner ca_interner;
+#define CA_INTERN_NOT_INTERNED (-2)           /* not a value of the universe (effect, non-scalar, port <= 0) */
+#define CA_U_TAINTS       0
+#define CA_U_LABEL_PAIRS  1
+#define CA_U_LABEL_KEYS   2
+#define CA_U_INT_KEYS     3
+#define CA_U_PORTS        4
+#define CA_U_SCALARS      5
+#define CA_U_NAMES        6
+
+typedef struct ca_str_pair { const char* key; const char* value; } ca_str_pair;
+typedef struct ca_taint_str { const char* key; const char* value; const char* effect; } ca_taint_str;
+typedef struct ca_toleration_str {
+    const char* key; const char* op;          /* op: "", "Equal" or "Exists"             */
+    const char* value; const char* effect;
+} ca_toleration_str;
+typedef struct ca_port_str { const char* host_ip; const char* protocol; int32_t host_port; int32_t reserved; } ca_port_str;
+typedef struct ca_requirement_str {
+    const char* key;
+    const char* op;                           /* In NotIn Exists DoesNotExist Gt Lt      */
+    const char* const* values;
+    int32_t n_values;
+    int32_t is_field;                         /* 1: a matchFields requirement            */
+} ca_requirement_str;
+
+int ca_interner_create(ca_interner** out);
+int ca_interner_destroy(ca_interner* it);
+int ca_interner_size(const ca_interner* it, int32_t universe, int32_t* n, int32_t* n_overflow);
+int ca_is_scalar_resource(const char* name);  /* 1 / 0 */
+/* *id: the value's bit position, -1 past the width, or CA_INTERN_NOT_INTERNED */
+int ca_intern_taint(ca_interner* it, const char* key, const char* value, const char* effect, int32_t* id);
+int ca_intern_label_pair(ca_interner* it, const char* key, const char* value, int32_t* id);
+int ca_intern_label_key(ca_interner* it, const char* key, int32_t* id);
+int ca_intern_int_key(ca_interner* it, const char* key, int32_t* id);
+int ca_intern_port(ca_interner* it, const char* host_ip, const char* protocol, int32_t host_port, int32_t* id);
+int ca_intern_resource(ca_interner* it, const char* name, int32_t* id);
+int ca_intern_name(ca_interner* it, const char* name, int32_t* id);
+/* a node's taints (interned here), label_pairs, label_keys, int_label, int_label_valid */
+int ca_intern_encode_node(ca_interner* it, const ca_str_pair* labels, int32_t n_labels, const ca_taint_str* taints,
+                          int32_t n_taints, ca_node_spec* out);
+/* a pod's tolerated_taints and its CA_POD_TOLERATES_UNSCHED flag (other flags kept) */
+int ca_intern_encode_tolerations(const ca_interner* it, const ca_toleration_str* t, int32_t n, ca_pod_spec* out,
+                                 int32_t* out_of_scope);
+/* a pod's port_conflict / port_use over its containers' ports */
+int ca_intern_encode_ports(ca_interner* it, const ca_port_str* p, int32_t n, ca_pod_spec* out, int32_t* out_of_scope);
+/* a pod's node_selector bits */
+int ca_intern_encode_node_selector(ca_interner* it, const ca_str_pair* sel, int32_t n, ca_pod_spec* out,
+                                   int32_t* out_of_scope);
+/* one non-empty nodeSelectorTerm (expressions, then fields) -> rows out[cap]; *n_rows = the
+ * rows it needs (CA_ECAPACITY when cap is short).  An empty term matches nothing and is
+ * dropped by the caller (nodeaffinity.go:83-85). */
+int ca_intern_compile_term(ca_interner* it, const ca_requirement_str* reqs, int32_t n, ca_selector_req* out,
+                           int32_t cap, int32_t* n_rows, int32_t* out_of_scope);
+
 /* ---- planner: committing removal simulation ----------------------
  * Planner.categorizeNodes' simulation loop (CA/core/scaledown/planner/planner.go:252-296)
  * over a RemovalSimulator built with persistSuccessfulSimulations = true (planner.go:89):

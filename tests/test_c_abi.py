@@ -25,3 +25,14 @@ def test_driver_runs():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "abi_driver ok" in r.stdout
     assert "estimate node_count 125 n_scheduled 1000" in r.stdout
+
+
+def test_intern_driver_against_fixtures():
+    """The interning through casim.h alone, from C, against tests/golden/intern_calls.txt
+    (the calls and the ids / encodings tests/golden/intern_fixtures.json pins).  Host-only:
+    runs on the CPU."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    calls = os.path.join(os.path.dirname(HERE), "golden", "intern_calls.txt")
+    r = subprocess.run([os.path.join(HERE, "bin", "intern_driver"), calls], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "intern_driver ok" in r.stdout

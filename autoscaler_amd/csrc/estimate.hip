@@ -2975,20 +2975,25 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     const bool decoupled = go_order && p->decouple_ok && p->total > 0 &&
                            !(knob_env("CASIM_GO_DECOUPLE") && atoi(knob_env("CASIM_GO_DECOUPLE")) == 0);
     p->ran_decoupled = decoupled ? 1 : 0;
+    // Go's sort.Slice permutation of every group and its pod ids, on st3: its own class
+    // ranks, k_pdq_sort, ids into d_spod_go and per-group ready flags holding this run's
+    // epoch (no reset between runs; every run is synchronised before it returns).  The
+    // chains meanwhile run on the stable class order (same class at every position).  It
+    // is queued right after the heavy chains when the groups split (the heavy chains are the
+    // step's critical path; the sort only bounds when the publisher can start and ends well
+    // before them), else before anything else.
+    // (the run's epoch is set before anything is queued: every consumer launched below reads it)
     if (decoupled) {
-        // Go's sort.Slice permutation of every group and its pod ids, on st3 before anything
-        // else is queued (it bounds when the publisher can start): its own class ranks,
-        // k_pdq_sort, ids into d_spod_go and per-group ready flags holding this run's epoch
-        // (no reset between runs; every run is synchronised before it returns).  The chains
-        // meanwhile run on the stable class order (same class at every position).
-        const int32_t U = p->s->n_cls;
-        int32_t NP = 1;
-        while (NP < U) NP <<= 1;
         if (p->ids_epoch == INT32_MAX) {                  // (wrapped: start over from a clean table)
             CA_HIP_CHECK(hipMemsetAsync(p->d_ids_ready.ptr, 0, sizeof(int32_t) * (size_t)G, p->st3));
             p->ids_epoch = 0;
         }
         p->ids_epoch++;
+    }
+    auto launch_go_sort = [&]() -> int {
+        const int32_t U = p->s->n_cls;
+        int32_t NP = 1;
+        while (NP < U) NP <<= 1;
         // the class ranks inside the sort kernel when its LDS has room for the scratch
         const size_t npad = ((size_t)std::min(p->max_count, PDQ_LDS_N) + 63) & ~(size_t)63;
         const bool fold = 16 * (size_t)NP <= 3 * npad && 2 * (size_t)U <= npad / 8 && !knob_env("CASIM_NO_RANK_FOLD");
@@ -3004,9 +3009,11 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
                                    p->d_ids_ready.as<int32_t>(), p->ids_epoch, fold ? NP : 0)) != CA_OK)
             return rc0;
         st_mark(0);
-        // (ev_ids is recorded on st3 once the heavy chains are queued: the host's launches
-        // ahead of them pace the step's start)
-    }
+        return CA_OK;
+    };
+    bool go_sort_queued = !decoupled;
+    // (ev_ids is recorded on st3 once the heavy chains are queued: the host's launches ahead
+    // of them pace the step's start)
     bool ids_recorded = !decoupled;
     auto record_ids = [&]() -> int {
         if (!ids_recorded) { CA_HIP_CHECK(hipEventRecord(p->ev_ids, p->st3)); ids_recorded = true; }
@@ -3081,6 +3088,12 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         gmapB = gmapA + p->n_heavy;
     }
     const int32_t nA = split ? p->n_heavy : G, nB = split ? G - p->n_heavy : 0;
+    const bool sort_after_heavy = split && p->total > 0 && p->bucket && !knob_env("CASIM_SORT_FIRST");
+    if (!go_sort_queued && !sort_after_heavy) {
+        int rcs;
+        if ((rcs = launch_go_sort()) != CA_OK) return rcs;
+        go_sort_queued = true;
+    }
     // where the consumers (publisher, segment copies) read the stream's pod ids
     const int32_t* const ids_src = decoupled ? p->d_spod_go.as<int32_t>() : p->d_spod.as<int32_t>();
     std::function<int()> sort_light;        // split: the light groups' sort, queued after the heavy chains
@@ -3297,6 +3310,10 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
         int rc;
         if (rounds == 1 && split) {         // heavy groups on st as soon as their sort is done
             if ((rc = chain(st, gmapA, nA)) != CA_OK) return rc;
+            if (!go_sort_queued) {
+                if ((rc = launch_go_sort()) != CA_OK) return rc;
+                go_sort_queued = true;
+            }
             if ((rc = record_ids()) != CA_OK) return rc;
             if ((rc = sort_light()) != CA_OK) return rc;
             if ((rc = chain(p->st2, gmapB, nB)) != CA_OK) return rc;
@@ -3307,6 +3324,10 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             light_pending = host_joins;
         } else if ((rc = chain(st, nullptr, G)) != CA_OK) {
             return rc;
+        }
+        if (!go_sort_queued) {             // (a later round of a split run: queued in round 1)
+            if ((rc = launch_go_sort()) != CA_OK) return rc;
+            go_sort_queued = true;
         }
         if ((rc = record_ids()) != CA_OK) return rc;
         if (publish && round_tickets > 0 && !serial_now) {

@@ -922,7 +922,9 @@ int ca_host_alloc(size_t bytes, void** out) {
     void* p = no_cache() ? nullptr : caller_cache().take(want, -1, got);
     if (!p) {
         got = std::max<size_t>(want, 4096);
-        if (hipHostMalloc(&p, got, hipHostMallocNonCoherent) != hipSuccess) {
+        // portable: a caller's result buffer may be written by every device of a ca_multi
+        // (each block publishes its slice zero-copy), so it is mapped for all of them
+        if (hipHostMalloc(&p, got, hipHostMallocNonCoherent | hipHostMallocPortable) != hipSuccess) {
             set_last_error("hipHostMalloc failed");
             return CA_EDEVICE;
         }

@@ -16,6 +16,7 @@
 #include "casim_internal.h"
 
 #include <algorithm>
+#include <cstring>
 #include <vector>
 
 
@@ -25,19 +26,29 @@ struct ca_util_table {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_added = nullptr;       // the staging copy of the last set_added is done
     bool added_in_flight = false;
-    std::vector<int32_t> fill;           // counting-sort cursors
     int32_t n_nodes = 0, n_pods = 0;
     casim::DevBuf nodes, pod_off, pods, info;
-    // pods added since the rows were set (ca_util_table_set_added): CSR by node
+    // pods added since the rows were set (ca_util_table_set_added), in the caller's order:
+    // [node n_added][pad][pods n_added] in device memory, summed per node by atomics in
+    // ca_util_calculate (k_added_sums) into acc, which the node kernel reads and clears
     int32_t n_added = 0;
-    casim::DevBuf added;                 // [add_off n_nodes + 1][pad][add_pods n_added]
-    casim::HostBuf h_added;
+    casim::DevBuf added;
+    casim::HostBuf h_added;              // staging for pageable caller arrays
+    casim::DevBuf acc;                   // AddedSum per node, all zero between calls
 };
 
 namespace {
 
-// byte offset of the added pods behind their offsets in ca_util_table::added
-inline size_t added_pods_at(int32_t n_nodes) { return ((sizeof(int32_t) * ((size_t)n_nodes + 1)) + 63) & ~(size_t)63; }
+// byte offset of the added pods behind their node indices in ca_util_table::added
+inline size_t added_pods_at(int32_t n) { return ((sizeof(int32_t) * (size_t)std::max(n, 1)) + 63) & ~(size_t)63; }
+
+// the added pods' sums of one node (k_added_sums), consumed and cleared by k_node_utilization
+struct AddedSum {
+    unsigned long long req[3], dsm[3];       // int64 sums (two's complement adds)
+    int32_t drain, pad;
+    int64_t pad2;
+};
+static_assert(sizeof(AddedSum) == 64, "AddedSum");
 
 constexpr int kLanes = 16;                                    // lanes per node (C5: ~20 pods/node)
 constexpr int kThreads = 256;
@@ -55,11 +66,45 @@ __device__ inline int64_t seg_sum(int64_t v) {                // within a kLanes
     return v;
 }
 
+// one pod's share of its node's sums (info.go:100-124)
+__device__ inline void pod_share(const ca_util_pod& p, int32_t skip_ds, int32_t skip_mirror, int64_t now_ns,
+                                 int64_t (&req)[3], int64_t (&dsm)[3], int& drain) {
+    drain |= (int)(p.flags & (CA_UPOD_MOVABLE | CA_UPOD_BLOCKING));
+    const bool factored = (skip_ds && (p.flags & CA_UPOD_DAEMONSET)) || (skip_mirror && (p.flags & CA_UPOD_MIRROR));
+    // drain.IsPodLongTerminating (utils/drain/drain.go:294-306): deleted, and deletion +
+    // grace + 30 s strictly before now
+    const bool long_term = !factored && (p.flags & CA_UPOD_DELETED) &&
+                           p.deletion_ns + p.grace_s * kNsPerS + kLongTerminatingExtraNs < now_ns;
+    for (int r = 0; r < 3; r++) {
+        if (factored) dsm[r] += p.req_milli[r];
+        else if (!long_term) req[r] += p.req_milli[r];
+    }
+}
+
+// The pods added since the rows were set, one thread each, into their nodes' sums
+// (integer sums and flag ORs: the order of a node's pods does not matter).
+__global__ __launch_bounds__(kThreads) void k_added_sums(const int32_t* __restrict__ add_node,
+                                                         const ca_util_pod* __restrict__ add_pods, int32_t n,
+                                                         int32_t skip_ds, int32_t skip_mirror, int64_t now_ns,
+                                                         AddedSum* __restrict__ acc) {
+    const int32_t k = blockIdx.x * kThreads + threadIdx.x;
+    if (k >= n) return;
+    const int32_t x = add_node[k];
+    int64_t req[3] = {0, 0, 0}, dsm[3] = {0, 0, 0};
+    int drain = 0;
+    pod_share(add_pods[k], skip_ds, skip_mirror, now_ns, req, dsm, drain);
+    AddedSum& a = acc[x];
+    for (int r = 0; r < 3; r++) {
+        if (req[r]) atomicAdd(&a.req[r], (unsigned long long)req[r]);
+        if (dsm[r]) atomicAdd(&a.dsm[r], (unsigned long long)dsm[r]);
+    }
+    if (drain) atomicOr(&a.drain, drain);
+}
+
 __global__ __launch_bounds__(kThreads) void k_node_utilization(
     const ca_util_node* __restrict__ nodes, const int32_t* __restrict__ pod_off,
     const ca_util_pod* __restrict__ pods, int32_t n_nodes, int32_t skip_ds, int32_t skip_mirror,
-    int64_t now_ns, ca_util_info* __restrict__ out, const int32_t* __restrict__ add_off,
-    const ca_util_pod* __restrict__ add_pods, ca_util_info* __restrict__ out_host) {
+    int64_t now_ns, ca_util_info* __restrict__ out, AddedSum* __restrict__ acc, ca_util_info* __restrict__ out_host) {
     const int sub = threadIdx.x & (kLanes - 1);
     const int32_t node = blockIdx.x * (kThreads / kLanes) + (int32_t)(threadIdx.x / kLanes);
     if (node >= n_nodes) return;                                  // whole segments only
@@ -67,30 +112,20 @@ __global__ __launch_bounds__(kThreads) void k_node_utilization(
     const ca_util_node nd = nodes[node];                          // in flight during the pod loop
     int64_t req[3] = {0, 0, 0}, dsm[3] = {0, 0, 0};
     int drain = 0;
-    // the node's rows, then the pods added to it since (integer sums and flag ORs: the
-    // order of the pods does not matter)
-    const int32_t ab = add_off ? add_off[node] : 0, ae = add_off ? add_off[node + 1] : 0;
-    const int32_t tot = (e - b) + (ae - ab);
-    for (int32_t k = sub; k < tot; k += kLanes) {                 // info.go:100-124
-        const ca_util_pod p = k < e - b ? pods[b + k] : add_pods[ab + (k - (e - b))];
-        drain |= (int)(p.flags & (CA_UPOD_MOVABLE | CA_UPOD_BLOCKING));
-        const bool factored = (skip_ds && (p.flags & CA_UPOD_DAEMONSET)) ||
-                              (skip_mirror && (p.flags & CA_UPOD_MIRROR));
-        // drain.IsPodLongTerminating (utils/drain/drain.go:294-306): deleted, and
-        // deletion + grace + 30 s strictly before now
-        const bool long_term = !factored && (p.flags & CA_UPOD_DELETED) &&
-                               p.deletion_ns + p.grace_s * kNsPerS + kLongTerminatingExtraNs < now_ns;
-        for (int r = 0; r < 3; r++) {
-            if (factored) dsm[r] += p.req_milli[r];
-            else if (!long_term) req[r] += p.req_milli[r];
-        }
-    }
+    for (int32_t k = b + sub; k < e; k += kLanes)                 // info.go:100-124
+        pod_share(pods[k], skip_ds, skip_mirror, now_ns, req, dsm, drain);
     for (int r = 0; r < 3; r++) {
         req[r] = seg_sum(req[r]);
         dsm[r] = seg_sum(dsm[r]);
     }
     for (int o = kLanes / 2; o; o >>= 1) drain |= __shfl_xor(drain, o, kLanes);
     if (sub != 0) return;
+    if (acc) {                                                    // the added pods' sums, then cleared
+        AddedSum a = acc[node];
+        for (int r = 0; r < 3; r++) { req[r] += (int64_t)a.req[r]; dsm[r] += (int64_t)a.dsm[r]; }
+        drain |= a.drain;
+        if (a.drain | a.req[0] | a.req[1] | a.req[2] | a.dsm[0] | a.dsm[1] | a.dsm[2]) acc[node] = AddedSum{};
+    }
 
     ca_util_info o;
     o.cpu = o.mem = o.gpu = o.utilization = 0.0;
@@ -148,8 +183,11 @@ int ca_util_table_create(int32_t device, const ca_util_node* nodes, int32_t n_no
     if ((st = t->nodes.reserve(sizeof(ca_util_node) * (size_t)n_nodes + 1)) ||
         (st = t->pod_off.reserve(sizeof(int32_t) * ((size_t)n_nodes + 1))) ||
         (st = t->pods.reserve(sizeof(ca_util_pod) * (size_t)n_pods + 1)) ||
-        (st = t->info.reserve(sizeof(ca_util_info) * (size_t)n_nodes + 1)))
+        (st = t->info.reserve(sizeof(ca_util_info) * (size_t)n_nodes + 1)) ||
+        (st = t->acc.reserve(sizeof(AddedSum) * ((size_t)n_nodes + 1))))
         return fail(st);
+    if (hipMemsetAsync(t->acc.ptr, 0, sizeof(AddedSum) * ((size_t)n_nodes + 1), t->stream) != hipSuccess)
+        return fail(CA_EDEVICE);
     if (n_nodes > 0) {
         if (hipMemcpyAsync(t->nodes.ptr, nodes, sizeof(ca_util_node) * n_nodes, hipMemcpyHostToDevice,
                            t->stream) != hipSuccess ||
@@ -179,6 +217,13 @@ int ca_util_table_update(ca_util_table* t, const ca_util_node* nodes, int32_t n_
         (st = t->pods.reserve(sizeof(ca_util_pod) * (size_t)n_pods + 1)) ||
         (st = t->info.reserve(sizeof(ca_util_info) * (size_t)n_nodes + 1)))
         return st;
+    if (t->added_in_flight) {                                  // (a set_added copy may still read)
+        CA_HIP_CHECK(hipEventSynchronize(t->ev_added));
+        t->added_in_flight = false;
+    }
+    if ((st = t->acc.reserve_keep(sizeof(AddedSum) * ((size_t)n_nodes + 1), t->stream)) != CA_OK) return st;
+    // (a table that grows gets its new sums zeroed; the old ones are zero between calls)
+    CA_HIP_CHECK(hipMemsetAsync(t->acc.ptr, 0, sizeof(AddedSum) * ((size_t)n_nodes + 1), t->stream));
     if (n_nodes > 0) {
         CA_HIP_CHECK(hipMemcpyAsync(t->nodes.ptr, nodes, sizeof(ca_util_node) * n_nodes, hipMemcpyHostToDevice,
                                     t->stream));
@@ -197,8 +242,8 @@ int ca_util_table_update(ca_util_table* t, const ca_util_node* nodes, int32_t n_
 
 int ca_util_table_set_added(ca_util_table* t, const int32_t* node, const ca_util_pod* pods, int32_t n) {
     if (!t || n < 0 || (n > 0 && (!node || !pods))) return CA_EINVAL;
-    for (int32_t k = 0; k < n; k++)
-        if (node[k] < 0 || node[k] >= t->n_nodes) return CA_EINVAL;
+    for (int32_t k = 0; k < n; k++)                            // the kernel trusts the indices
+        if ((uint32_t)node[k] >= (uint32_t)t->n_nodes) return CA_EINVAL;
     CA_HIP_CHECK(hipSetDevice(t->device));
     if (t->added_in_flight) {                                  // the staging buffer is reused
         CA_HIP_CHECK(hipEventSynchronize(t->ev_added));
@@ -206,21 +251,31 @@ int ca_util_table_set_added(ca_util_table* t, const int32_t* node, const ca_util
     }
     t->n_added = 0;
     if (n == 0) return CA_OK;
-    // counting sort by node, straight into page-locked staging: [offsets][pods]
-    const size_t at = added_pods_at(t->n_nodes);
+    // one DMA per array into device memory (no sort: the sums are order-free); page-locked
+    // caller arrays (ca_host_alloc) are copied in place, others through page-locked staging
+    const size_t at = added_pods_at(n);
     const size_t bytes = at + sizeof(ca_util_pod) * (size_t)n;
     int st;
-    if ((st = t->added.reserve(bytes)) != CA_OK || (st = t->h_added.reserve(bytes)) != CA_OK) return st;
-    int32_t* off = t->h_added.as<int32_t>();
-    ca_util_pod* out = reinterpret_cast<ca_util_pod*>(t->h_added.as<unsigned char>() + at);
-    std::fill(off, off + t->n_nodes + 1, 0);
-    for (int32_t k = 0; k < n; k++) off[node[k] + 1]++;
-    for (int32_t i = 0; i < t->n_nodes; i++) off[i + 1] += off[i];
-    t->fill.assign(off, off + t->n_nodes);
-    int32_t* fill = t->fill.data();
-    for (int32_t k = 0; k < n; k++) out[fill[node[k]]++] = pods[k];
-    // stream-ordered before the next calculate; the next set_added waits for the copy
-    CA_HIP_CHECK(hipMemcpyAsync(t->added.ptr, t->h_added.ptr, bytes, hipMemcpyHostToDevice, t->stream));
+    if ((st = t->added.reserve(bytes)) != CA_OK) return st;
+    auto pinned = [](const void* h) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, h) == hipSuccess && a.type == hipMemoryTypeHost) return true;
+        (void)hipGetLastError();
+        return false;
+    };
+    const void* src_node = node;
+    const void* src_pods = pods;
+    if (!pinned(node) || !pinned(pods)) {
+        if ((st = t->h_added.reserve(bytes)) != CA_OK) return st;
+        std::memcpy(t->h_added.ptr, node, sizeof(int32_t) * (size_t)n);
+        std::memcpy(t->h_added.as<unsigned char>() + at, pods, sizeof(ca_util_pod) * (size_t)n);
+        src_node = t->h_added.ptr;
+        src_pods = t->h_added.as<unsigned char>() + at;
+    }
+    // stream-ordered before the next calculate; the next set_added waits for the copies
+    CA_HIP_CHECK(hipMemcpyAsync(t->added.ptr, src_node, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, t->stream));
+    CA_HIP_CHECK(hipMemcpyAsync(t->added.as<unsigned char>() + at, src_pods, sizeof(ca_util_pod) * (size_t)n,
+                                hipMemcpyHostToDevice, t->stream));
     CA_HIP_CHECK(hipEventRecord(t->ev_added, t->stream));
     t->added_in_flight = true;
     t->n_added = n;
@@ -237,6 +292,7 @@ int ca_util_table_destroy(ca_util_table* t) {
     t->info.release();
     t->added.release();
     t->h_added.release();
+    t->acc.release();
     if (t->ev0) (void)hipEventDestroy(t->ev0);
     if (t->ev1) (void)hipEventDestroy(t->ev1);
     if (t->ev_added) (void)hipEventDestroy(t->ev_added);
@@ -264,17 +320,21 @@ int ca_util_calculate(ca_util_table* t, int32_t skip_daemonset_pods, int32_t ski
             }
         }
         CA_HIP_CHECK(hipEventRecord(t->ev0, t->stream));
+        if (t->n_added > 0) {
+            hipLaunchKernelGGL(k_added_sums, dim3((t->n_added + kThreads - 1) / kThreads), dim3(kThreads), 0, t->stream,
+                               t->added.as<const int32_t>(),
+                               reinterpret_cast<const ca_util_pod*>(t->added.as<unsigned char>() + added_pods_at(t->n_added)),
+                               t->n_added, skip_daemonset_pods ? 1 : 0, skip_mirror_pods ? 1 : 0, now_ns,
+                               t->acc.as<AddedSum>());
+            CA_HIP_CHECK(hipGetLastError());
+        }
         constexpr int per_block = kThreads / kLanes;
         const int blocks = (t->n_nodes + per_block - 1) / per_block;
         hipLaunchKernelGGL(k_node_utilization, dim3(blocks), dim3(kThreads), 0, t->stream,
                            t->nodes.as<const ca_util_node>(), t->pod_off.as<const int32_t>(),
                            t->pods.as<const ca_util_pod>(), t->n_nodes, skip_daemonset_pods ? 1 : 0,
                            skip_mirror_pods ? 1 : 0, now_ns, t->info.as<ca_util_info>(),
-                           t->n_added > 0 ? t->added.as<const int32_t>() : nullptr,
-                           t->n_added > 0 ? reinterpret_cast<const ca_util_pod*>(
-                                                t->added.as<unsigned char>() + added_pods_at(t->n_nodes))
-                                          : nullptr,
-                           dst);
+                           t->n_added > 0 ? t->acc.as<AddedSum>() : nullptr, dst);
         CA_HIP_CHECK(hipGetLastError());
         CA_HIP_CHECK(hipEventRecord(t->ev1, t->stream));
         if (out && !zero_copy)

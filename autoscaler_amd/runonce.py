@@ -125,6 +125,14 @@ class DeviceUtil:
         self.base = None
         self.rows = None                 # page-locked result rows (native.PinnedRows), two in turn:
         self.turn = 0                    # a result stays valid until the call after the next
+        self.inputs = None               # page-locked added-pod arrays (UtilInput builds them)
+
+    def zeros(self, key: str, n: int, dtype) -> np.ndarray:
+        """Allocator of the loop's added-pod arrays: page-locked, so set_added copies them in
+        place (valid until the next loop's UtilInput)."""
+        from . import native
+        self.inputs = self.inputs or native.PinnedRows()
+        return self.inputs.zeros(key, n, dtype)
 
     def __call__(self, ui: "UtilInput", now_ns: int):
         from . import native
@@ -145,9 +153,10 @@ class DeviceUtil:
         if self.table is not None:
             self.table.close()
             self.table = None
-        if self.rows is not None:
-            self.rows.close()
-            self.rows = None
+        for r in (self.rows, self.inputs):
+            if r is not None:
+                r.close()
+        self.rows = self.inputs = None
 
 
 class DeviceExpansion:
@@ -223,16 +232,19 @@ def _util_base(w: RunOnceWorkload):
     return w._ubase
 
 
-def _util_added(w: RunOnceWorkload, placed_node: np.ndarray):
-    """(node, ca_util_pod row) of every pod FilterOutSchedulable placed, in placement order."""
+def _util_added(w: RunOnceWorkload, placed_node: np.ndarray, zeros=_zeros):
+    """(node, ca_util_pod row) of every pod FilterOutSchedulable placed, in placement order
+    (`zeros(key, n, dtype)` allocates the arrays: page-locked ones are copied in place)."""
     f = w.filt
     placed = np.nonzero(placed_node >= 0)[0]
     ids = f.order[placed]
-    pods = np.zeros(len(placed), abi.UTIL_POD_DTYPE)
+    pods = zeros("added_pods", len(placed), abi.UTIL_POD_DTYPE)
     pods["req_milli"][:, 0] = f.pending.pods["req_milli_cpu"][ids]
     pods["req_milli"][:, 1] = f.pending.pods["req_memory"][ids] * 1000
     pods["flags"] = abi.CA_UPOD_MOVABLE
-    return placed_node[placed].astype(np.int32), pods
+    node = zeros("added_node", len(placed), np.int32)
+    node[:] = placed_node[placed]
+    return node, pods
 
 
 class UtilInput:
@@ -245,7 +257,7 @@ class UtilInput:
         self.want = want
         if want == "added":
             self.base = _util_base(w)
-            self.added_node, self.added_pods = _util_added(w, placed_node)
+            self.added_node, self.added_pods = _util_added(w, placed_node, zeros)
         else:
             self.nodes, self.off, self.pods, _ = _util_rows(w, placed_node, zeros)
 
@@ -299,7 +311,7 @@ def run(backend, util_fn, w: RunOnceWorkload, timers=None, row_zeros=_zeros, exp
         ps.close()
 
     # 4. scale-down eligibility on the snapshot after step 1
-    ui = UtilInput(w, fo.node, getattr(util_fn, "want", "full"), row_zeros)
+    ui = UtilInput(w, fo.node, getattr(util_fn, "want", "full"), getattr(util_fn, "zeros", row_zeros))
     t = clock()
     r.util = util_fn(ui, w.now_ns)
     r.ms["utilization"] = (clock() - t) * 1e3

@@ -286,11 +286,13 @@ def filter_leg(args, device: int, with_cpu: bool) -> dict:
     running 300k pods, 20k pending pods in priority order, TrySchedulePods(ScheduleAnywhere,
     breakOnFailure=false) with hints and the similar-pods cache, one ca_filter_out_schedulable
     call per step inside a fork that is reverted after it (mirror resident in HBM).
-    'c5-c4' adds the C4 taint/label universe."""
+    'c5-c4' adds the C4 taint/label universe; 'loose' is the same cluster at 20-70 %
+    utilisation (nearly every pod fits its first node: the port does ~1 evaluation per pod,
+    the regime where the one-wavefront walk does not beat it)."""
     from autoscaler_amd import native
     from autoscaler_amd import workloads as W
     out = {}
-    for name, kw in (("c5", {}), ("c5-c4", {"taints": True})):
+    for name, kw in (("c5", {}), ("c5-c4", {"taints": True}), ("loose", {"util_low": (0.2, 0.4), "util_high": (0.5, 0.7)})):
         w = W.c5_filter(**kw)
         g = native.Mirror(device)
         W.load_filter(g, w)

@@ -585,10 +585,12 @@ int ca_util_table_destroy(ca_util_table* t);
 int ca_util_table_update(ca_util_table* t, const ca_util_node* nodes, int32_t n_nodes, const int32_t* pod_off,
                          const ca_util_pod* pods);
 /* Pods added to the snapshot since the rows were set (AddPod: FilterOutSchedulable's
- * placements, static_autoscaler.go:528): pods[k] now runs on node[k].  Replaces the previous
- * added set (n = 0 clears it; ca_util_table_update clears it too).  Calculate counts them
- * with the node's rows — only these records cross PCIe, not the node's whole pod list.
- * The copy is asynchronous: the next ca_util_calculate on t runs after it. */
+ * placements, static_autoscaler.go:528): pods[k] now runs on node[k], in any order.
+ * Replaces the previous added set (n = 0 clears it; ca_util_table_update clears it too).
+ * Calculate adds them to their nodes' sums — only these records cross PCIe, not the nodes'
+ * whole pod lists.  The copy is asynchronous and stream-ordered before the next
+ * ca_util_calculate; page-locked arrays (ca_host_alloc) are copied from in place, so keep
+ * them unchanged until that calculate returns. */
 int ca_util_table_set_added(ca_util_table* t, const int32_t* node, const ca_util_pod* pods, int32_t n);
 /* Calculate(nodeInfo, skipDaemonSetPods, skipMirrorPods, gpuConfig, currentTime) for every
  * node.  out NULL keeps the results in HBM (ca_util_device_results); otherwise out[n_nodes]

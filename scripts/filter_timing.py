@@ -27,6 +27,7 @@ if "--prof" in args:                    # CASIM_PROF build: the walk's cycle cou
 if "--bulk" in args:                    # (with --prof) fbcyc = mixed runs' chain / row loads / updates
     args.remove("--bulk")
     os.environ["CASIM_FB_PROF_BULK"] = "1"
+    os.environ["CASIM_KNOBS"] = "1"
 if "--phases" in args:                  # host phase marks of every call on stderr (filter.hip tmark)
     args.remove("--phases")
     os.environ["CASIM_DEBUG_TIMING"] = "1"

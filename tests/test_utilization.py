@@ -217,5 +217,17 @@ def test_gpu_added_pods_zero_copy(seed, n_nodes, ppn, n_add, oracle_lib):
         ref = oracle_lib.node_utilization(nodes, m_off, m_pods, sds, smp, now)
         assert _bits_equal(got, ref), (seed, sds, smp)
         assert _bits_equal(t.calculate(sds, smp, now), ref)       # pageable: the DMA path
+    # page-locked added arrays (copied in place), then an update: the per-node sums of the
+    # added pods are consumed by every calculate and nothing of them survives an update
+    pn = rows.zeros("add_node", n_add, np.int32)
+    pp = rows.zeros("add_pods", n_add, abi.UTIL_POD_DTYPE)
+    pn[:] = add_node
+    pp[:] = add
+    t.set_added(pn, pp)
+    out = rows.zeros("info", n_nodes, abi.UTIL_INFO_DTYPE)
+    assert _bits_equal(t.calculate(True, False, now, out=out), oracle_lib.node_utilization(nodes, m_off, m_pods, True,
+                                                                                            False, now))
+    t.update(nodes, off, pods)
+    assert _bits_equal(t.calculate(False, False, now), oracle_lib.node_utilization(nodes, off, pods, False, False, now))
     t.close()
     rows.close()

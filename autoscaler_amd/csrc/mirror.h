@@ -6,6 +6,7 @@
 #pragma once
 #include "casim_internal.h"
 #include <array>
+#include <deque>
 #include <cstdlib>
 #include <new>
 #include <sys/mman.h>
@@ -59,10 +60,10 @@ struct SweepScratch {
     DevBuf bsum;                    // per 64-node block: maxima of the visible rows (sweep.hip BlockSum)
     DevBuf chainl;                  // the host walk's serial exact chain: candidates in order
     DevBuf bmap;                    // a multi-device range's block map (k_walk_map)
-    HostBuf h_in, h_tab, h_out, h_todo, h_lin, h_wl, h_tfp, h_ctab, h_l0, h_chainl, h_bmap;
-    // the host walk's side rows (windows just below and just above a re-centred row): [2][64][S]
-    // table values and [2][FPW][S] fit points, read only where built in this call
-    std::vector<int32_t> side_tab, side_fp;
+    HostBuf h_in, h_tab, h_out, h_todo, h_lin, h_wl, h_tfp, h_l0, h_chainl, h_bmap;
+    // the host walk's table rounds: each round's compact rows (main and side rows), read in
+    // place by the walk for the rest of the call; pooled across calls
+    std::deque<HostBuf> rbuf;
     // the device pipeline of the last call shape, replayed as a graph (sweep.hip sweep_core)
     hipGraphExec_t gexec = nullptr;
     uint64_t gkey = 0, gseen = 0;

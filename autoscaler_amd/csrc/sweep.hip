@@ -1685,21 +1685,30 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         constexpr int32_t SIDE_BAND = CASIM_SIDE_BAND;
         std::vector<uint8_t> have_side((size_t)S, 0), want_side((size_t)S, 0);   // want_side: bit 0 below, bit 1 above
         std::vector<int32_t> gapk((size_t)S, 1);
-        if (sides) {
-            if (sw.side_tab.size() < 2 * 64 * (size_t)S) sw.side_tab.resize(2 * 64 * (size_t)S);
-            if (sw.side_fp.size() < 2 * (size_t)FPW * S) sw.side_fp.resize(2 * (size_t)FPW * S);
-        }
-        int32_t* const stab = sides ? sw.side_tab.data() : nullptr;     // [2][64][S]
-        int32_t* const sfp = sides ? sw.side_fp.data() : nullptr;       // [2][FPW][S]
-        // the class of input L in candidate k's rows (main, then the sides), and its table
-        auto lookup = [&](int32_t k, int32_t L, const int32_t*& tb) -> int32_t {
-            tb = tab;
-            int32_t w = fp_class(h_tfp + k, S, n, L);
+        // Where each candidate's rows are: the first pipeline's table ([64][S] values and
+        // [FPW][S] fit points, copied once), or the compact rows of the table round that
+        // rebuilt them, read in place in that round's page-locked buffer ([64][T], [FPW][T]:
+        // the kernel writes them there, zero-copy) — no scatter of every round's rows into
+        // one host table.  Slot 0: the main row, 1 / 2: the side rows below / above.
+        struct RowRef {
+            const int32_t* v;      // value of class w: v[w * s]
+            const int32_t* f;      // fit point i: f[i * s]
+            int32_t s;
+        };
+        std::vector<RowRef> rref((size_t)3 * S);
+        for (int32_t k = 0; k < S; k++) rref[k] = RowRef{tab + k, h_tfp + k, S};
+        RowRef* const mref = rref.data();
+        int32_t round_buf = 0;                     // this call's table rounds so far (sw.rbuf)
+        // the class of input L in candidate k's rows (main, then the sides), and that row
+        auto lookup = [&](int32_t k, int32_t L, const RowRef*& rr) -> int32_t {
+            rr = &mref[k];
+            int32_t w = fp_class(rr->f, rr->s, n, L);
             if (w >= 0 || !have_side[k]) return w;
             for (int sd = 0; sd < 2; sd++) {
                 if (!((have_side[k] >> sd) & 1)) continue;
-                w = fp_class(sfp + (size_t)sd * FPW * S + k, S, n, L);
-                if (w >= 0) { tb = stab + (size_t)sd * 64 * S; return w; }
+                const RowRef* q = &rref[(size_t)(1 + sd) * S + k];
+                w = fp_class(q->f, q->s, n, L);
+                if (w >= 0) { rr = q; return w; }
             }
             return -1;
         };
@@ -1776,10 +1785,16 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 std::memcpy(ht + T, todo_ws.data(), sizeof(int32_t) * T);
                 std::memcpy(ht + 2 * T, todo_k.data(), sizeof(int32_t) * T);
                 // zero-copy both ways: the kernel reads the rows to build from the page-locked
-                // staging and writes the compact rows straight into the host's buffer (no copy
-                // launches around a 40 µs kernel; the round trip is what a round costs)
-                if ((rc = sw.h_ctab.reserve(sizeof(int32_t) * (64 + FPW) * (size_t)T)) != CA_OK) return rc;
-                int32_t* const ct = sw.h_ctab.as<int32_t>();
+                // staging and writes the compact rows straight into this round's host buffer (no
+                // copy launches around a 40 µs kernel; the round trip is what a round costs).
+                // The round buffers are kept for the call (the walk reads the rows in place) and
+                // pooled across calls, each sized once for a full round (LOOKAHEAD main rows
+                // and their two side rows) so a later call never regrows one.
+                if ((int32_t)sw.rbuf.size() <= round_buf) sw.rbuf.emplace_back();
+                HostBuf& rbuf = sw.rbuf[round_buf++];
+                if ((rc = rbuf.reserve(sizeof(int32_t) * (64 + FPW) * (size_t)std::max(T, 3 * LOOKAHEAD))) != CA_OK)
+                    return rc;
+                int32_t* const ct = rbuf.as<int32_t>();
                 void *d_ht = nullptr, *d_ct = nullptr;
                 const bool zc = !knob_env("CASIM_SWEEP_COPY_ROUNDS") &&
                                 hipHostGetDevicePointer(&d_ht, ht, 0) == hipSuccess &&
@@ -1813,18 +1828,9 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 CA_HIP_CHECK(hipStreamSynchronize(st));
                 tmark("table sync");
                 const int32_t* ctf = ct + 64 * (size_t)T;
-                // row by row: sequential reads, near-sequential writes (todo_k ascends); side
-                // rows to their own tables
-                int32_t* const tdst[3] = {tab, stab, stab ? stab + 64 * (size_t)S : nullptr};
-                int32_t* const fdst[3] = {h_tfp, sfp, sfp ? sfp + (size_t)FPW * S : nullptr};
-                for (int32_t w = 0; w < 64; w++) {
-                    const int32_t* src = ct + (size_t)w * T;
-                    for (int32_t t = 0; t < T; t++) tdst[todo_slot[t]][(size_t)w * S + todo_k[t]] = src[t];
-                }
-                for (int32_t i = 0; i < FPW; i++) {
-                    const int32_t* src = ctf + (size_t)i * T;
-                    for (int32_t t = 0; t < T; t++) fdst[todo_slot[t]][(size_t)i * S + todo_k[t]] = src[t];
-                }
+                // the candidates' rows now live in this round's buffer (row t: column t)
+                for (int32_t t = 0; t < T; t++)
+                    rref[(size_t)todo_slot[t] * S + todo_k[t]] = RowRef{ct + t, ctf + t, T};
                 for (int32_t t = 0; t < T; t++)
                     if (todo_slot[t] != 0) { have_side[todo_k[t]] |= (uint8_t)(1 << (todo_slot[t] - 1)); want_side[todo_k[t]] = 0; }
                 float ms = 0;
@@ -1841,19 +1847,19 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 exact_lin[c] = (int32_t)cur;
                 if (wlv < 0) continue;                                             // lastIndex passes through
                 if (wrap(cur, n) == guess[c]) { cur = wlv; continue; }            // probed at the true value
-                const int32_t* tb = tab;
-                const int32_t w = lookup(k0, wrap(cur, n), tb);
+                const RowRef* rr = nullptr;
+                const int32_t w = lookup(k0, wrap(cur, n), rr);
                 if (w < 0) {
                     if (dbg_t) {                  // where the exact input fell against the row's window
-                        const int32_t* fp = h_tfp + k0;
-                        const int32_t lo = fp[0], hi = fp[(size_t)64 * S];
+                        const int32_t* fp = mref[k0].f;
+                        const int32_t lo = fp[0], hi = fp[(size_t)64 * mref[k0].s];
                         const int32_t gap = std::max(1, wrap((int64_t)hi - lo, n) / 64);
                         fprintf(stderr, "[sweep] miss at %d: input %d, window [%d, %d] (gap %d): %+d gaps from its start\n",
                                 k0, wrap(cur, n), lo, hi, gap, (int)(wrap((int64_t)wrap(cur, n) - lo + n / 2, n) - n / 2) / gap);
                     }
                     break;
                 }
-                int32_t v = tb[(size_t)(w) * S + k0];
+                int32_t v = rr->v[(size_t)w * rr->s];
                 if (v == TB_UNKNOWN) {
                     // hints / ports / long scans: exact kernel at the exact lastIndex, alone
                     std::memset(h_need, 0, (size_t)C);
@@ -1891,26 +1897,28 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
             int64_t est = cur;
             for (int32_t k = k0; k < std::min(S, k0 + LOOKAHEAD); k++) {
                 if (insensitive(k)) continue;
-                const int32_t* fp = h_tfp + k;                      // column k of [FPW][S]
-                const int32_t* tb = tab;
-                const int32_t w = lookup(k, wrap(est, n), tb);
-                const int32_t v = w >= 0 ? tb[(size_t)(w) * S + k] : TB_UNKNOWN;
+                const RowRef& mr = mref[k];                          // the main row
+                const int32_t* fp = mr.f;
+                const int32_t ms = mr.s;
+                const RowRef* rr = nullptr;
+                const int32_t w = lookup(k, wrap(est, n), rr);
+                const int32_t v = w >= 0 ? rr->v[(size_t)w * rr->s] : TB_UNKNOWN;
                 // an estimate within SIDE_BAND classes of its row's edge: the next round adds the
                 // side row there (the exact input drifts a few positions past the edge now and then)
-                if (sides && w >= 0 && tb == tab && (w < SIDE_BAND || w > 63 - SIDE_BAND) && !have_side[k]) {
-                    gapk[k] = std::max(1, wrap((int64_t)fp[(size_t)64 * S] - fp[0], n) / 64);
+                if (sides && w >= 0 && rr == &mr && (w < SIDE_BAND || w > 63 - SIDE_BAND) && !have_side[k]) {
+                    gapk[k] = std::max(1, wrap((int64_t)fp[(size_t)64 * ms] - fp[0], n) / 64);
                     want_side[k] = w < SIDE_BAND ? 1 : 2;
                 }
                 if (w >= 0 && v != TB_UNKNOWN) { est = v; continue; }
                 int64_t next = est + (move_off[sens[k] + 1] - move_off[sens[k]]);
                 int best = -1;              // known entry nearest the window centre
                 for (int d = 0; d <= 32 && best < 0; d++) {
-                    if (32 - d >= 0 && tab[(size_t)(32 - d) * S + k] != TB_UNKNOWN) best = 32 - d;
-                    else if (32 + d < 64 && tab[(size_t)(32 + d) * S + k] != TB_UNKNOWN) best = 32 + d;
+                    if (32 - d >= 0 && mr.v[(size_t)(32 - d) * ms] != TB_UNKNOWN) best = 32 - d;
+                    else if (32 + d < 64 && mr.v[(size_t)(32 + d) * ms] != TB_UNKNOWN) best = 32 + d;
                 }
-                if (best >= 0) next = est + wrap(tab[(size_t)(best) * S + k] - fp[(size_t)(1 + best) * S], n);
+                if (best >= 0) next = est + wrap(mr.v[(size_t)best * ms] - fp[(size_t)(1 + best) * ms], n);
                 if (w < 0) {                 // re-centre: 32 of the row's mean gaps before the estimate
-                    const int32_t gap = std::max(1, wrap((int64_t)fp[(size_t)64 * S] - fp[0], n) / 64);
+                    const int32_t gap = std::max(1, wrap((int64_t)fp[(size_t)64 * ms] - fp[0], n) / 64);
                     ws[k] = wrap(est - 32 * (int64_t)gap, n);
                     gapk[k] = gap;
                     have[k] = 0;

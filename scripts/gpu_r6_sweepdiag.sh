@@ -1,0 +1,9 @@
+#!/bin/bash
+# GPU-box job: the C5 RunOnce sweep's host / kernel split per table round (CASIM_DEBUG_TIMING).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u scripts/runonce_diag.py --phases > gpurun_out/rdiag.out 2> gpurun_out/rdiag.err || { tail -20 gpurun_out/rdiag.err; exit 1; }
+cat gpurun_out/rdiag.out
+grep "^\[sweep\]" gpurun_out/rdiag.err | tail -60

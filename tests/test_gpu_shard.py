@@ -143,3 +143,53 @@ def test_sharded_sweep_phases(world, n_nodes):
 def test_sharded_estimate_rebase(seed):
     res = _spawn(_estimate_worker, 3, seed)
     assert all(ok for _, ok, _ in res), res
+
+
+def _cut_worker(rank, world, port, n_nodes, q):
+    """An out-of-scope pod to move in a middle block: every plan runs whole calls (the
+    phases need every block free of a prefix-protocol cut), the cut candidate reports
+    OUT_OF_SCOPE and every later one NOT_RUN, as one mirror's call does."""
+    _paths()
+    import dataclasses
+    import torch.distributed as dist
+    from autoscaler_amd import abi, native, shard
+    from autoscaler_amd import workloads as W
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w = W.c3(n_nodes=n_nodes)
+        pods = w.table.pods.copy()
+        c_mid = len(w.candidates) // 2
+        pods["flags"][int(w.move_pods[w.move_off[c_mid]])] |= abi.CA_POD_OUT_OF_SCOPE
+        w = dataclasses.replace(w, table=abi.PodTable(pods))
+        blocks = shard.split_blocks(np.diff(w.move_off), world)
+        a, b = blocks[rank], blocks[rank + 1]
+        m = native.Mirror(0)
+        W.load_sweep(m, w)
+        ref = m.find_nodes_to_remove(w.candidates, w.dest_mask, w.cand_status, w.move_off, w.move_pods,
+                                     np.full(len(w.table), -1, np.int32), 5)
+        plan = native.RemovalPlan(m, w.candidates[a:b], w.dest_mask, w.cand_status[a:b],
+                                  (w.move_off[a:b + 1] - w.move_off[a]).astype(np.int32),
+                                  w.move_pods[w.move_off[a]:w.move_off[b]])
+        ex = shard.Exchange(shard.torch_gather_bytes(dist, "cpu"))
+        sb, ph = shard.sweep_setup(plan, ex, rank, a == b)
+        hints = np.full(len(w.table), -1, np.int32)
+        res, dest, L, st = shard.sweep_sharded(plan, 5, hints, len(w.nodes), ex, rank, blocks, w.move_off, w.move_pods,
+                                               sb, ph)
+        ok = np.array_equal(res, ref.results) and np.array_equal(dest, ref.dest) and L == ref.last_index
+        ok &= np.array_equal(hints, ref.hints)
+        ok &= int(res[c_mid]["reason"]) == abi.CA_UNREMOVABLE_OUT_OF_SCOPE
+        ok &= bool((res["reason"][c_mid + 1:] == abi.CA_UNREMOVABLE_NOT_RUN).all())
+        ok &= st["serial_blocks"] == world
+        plan.close()
+        m.close()
+        q.put((rank, bool(ok), st))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_sweep_prefix_cut():
+    res = _spawn(_cut_worker, 3, 600)
+    assert all(ok for _, ok, _ in res), res

@@ -272,6 +272,8 @@ struct ca_mirror {
     int ensure_pod_hints();                // grow to pods.size(), new entries -1
     int64_t n_ext_pods = 0;                // pods stored with host ports / extended requests
     int64_t n_eph_pods = 0;                // pods stored with ephemeral-storage requests
+    int64_t n_oos_pods = 0;                // pods stored with CA_POD_OUT_OF_SCOPE (never decremented:
+                                           // 0 lets the sweep's scope cut skip the per-pod check)
 
     int remap_hints_removed(int32_t pos, int32_t code, bool restore);   // resident hints around a RemoveNode
     int32_t removals = 0;                  // RemoveNode calls so far: hint codes of removed nodes

@@ -502,7 +502,7 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
     struct Part {
         std::vector<casim::JournalEntry> jr;
         std::vector<int32_t> dirty;
-        int64_t ext = 0, eph = 0, blockers = 0;
+        int64_t ext = 0, eph = 0, blockers = 0, oos = 0;
     };
     std::vector<Part> part((size_t)T);
     const bool journaled = depth > 0;
@@ -518,6 +518,7 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
             r.node = node[k];
             if (casim::pod_dev_flags(r.spec) & (casim::PF_PORTS | casim::PF_SCALAR_REQ | casim::PF_MOVED_SCALAR_REQ)) pt.ext++;
             if (r.spec.req_ephemeral != 0) pt.eph++;
+            if (r.spec.flags & CA_POD_OUT_OF_SCOPE) pt.oos++;
         }
         if (dbg_t) tw[3 * w + 1] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         for (int32_t k = 0; k < n; k++) {               // AddPod on my nodes, in order
@@ -563,6 +564,7 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
     for (Part& pt : part) {
         n_ext_pods += pt.ext;
         n_eph_pods += pt.eph;
+        n_oos_pods += pt.oos;
         n_scope_blockers += pt.blockers;
         dirty_rows.insert(dirty_rows.end(), pt.dirty.begin(), pt.dirty.end());
         if (journaled) journal.insert(journal.end(), pt.jr.begin(), pt.jr.end());
@@ -596,6 +598,7 @@ int32_t ca_mirror::store_pod(const ca_pod_table* t, int32_t idx, int32_t node) {
     }
     if (pod_dev_flags(row.spec) & (PF_PORTS | PF_SCALAR_REQ | PF_MOVED_SCALAR_REQ)) n_ext_pods++;
     if (row.spec.req_ephemeral != 0) n_eph_pods++;
+    if (row.spec.flags & CA_POD_OUT_OF_SCOPE) n_oos_pods++;
     pods.push_back(row);
     return (int32_t)pods.size() - 1;
 }
@@ -1003,6 +1006,7 @@ int ca_mirror_clear(ca_mirror* m) {
     if (!m) return CA_EINVAL;
     m->n_ext_pods = 0;
     m->n_eph_pods = 0;
+    m->n_oos_pods = 0;
     m->nodes.clear(); m->pods.clear(); m->terms.clear(); m->reqs.clear(); m->pf_names.clear();
     m->journal.clear(); m->depth = 0; m->removed_nodes.clear(); m->n_scope_blockers = 0;
     m->dirty_rows.clear(); m->dirty_flag.clear();
@@ -1499,6 +1503,17 @@ struct ca_expansion_plan {
     casim::DevBuf rows;        // NodeHot[G] | NodeExt[G] | NodeStatic[G]
     casim::HostBuf io;         // page-locked: samples | results | verdicts
     float kernel_ms = 0;       // the last run's kernel (events)
+    // The check reads only the plan's rows and the podset's tables, both immutable once
+    // their create call returned (each ends with a sync): it runs on a stream of its own, so
+    // it neither waits behind nor holds up work queued on the mirror's stream (after
+    // FilterOutSchedulable: the placed pods' record gather).
+    hipStream_t st = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    ~ca_expansion_plan() {
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (st) (void)hipStreamDestroy(st);
+    }
 };
 
 extern "C" {
@@ -1569,6 +1584,12 @@ int ca_expansion_plan_create(ca_mirror* m, const ca_template* templates, int32_t
             return CA_EDEVICE;
         }
     }
+    if (hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&p->ev0) != hipSuccess || hipEventCreate(&p->ev1) != hipSuccess) {
+        delete p;
+        set_last_error("ca_expansion_plan_create: stream / event creation failed");
+        return CA_EDEVICE;
+    }
     *out = p;
     return CA_OK;
 }
@@ -1578,6 +1599,7 @@ int ca_expansion_plan_run(ca_expansion_plan* p, const ca_podset* s, const int32_
     if (!p || !s || s->m != p->m || n_samples < 0) return CA_EINVAL;
     if (n_samples == 0 || p->G == 0) return CA_OK;
     if (!samples || (!out && !out_ok)) return CA_EINVAL;
+    const auto t_entry = std::chrono::steady_clock::now();
     ca_mirror* m = p->m;
     int rc;
     if ((rc = check_samples(m, s, samples, n_samples)) != CA_OK) return rc;
@@ -1606,8 +1628,8 @@ int ca_expansion_plan_run(ca_expansion_plan* p, const ca_podset* s, const int32_
     char* d_ok = out_ok ? mapped(out_ok) : nullptr;
     const size_t G = (size_t)p->G;
     const char* rows = p->rows.as<const char>();
-    CA_HIP_CHECK(hipEventRecord(m->ev0, m->stream));
-    hipLaunchKernelGGL(k_check_templates, dim3((n_samples + 255) / 256, p->G), dim3(256), 0, m->stream,
+    CA_HIP_CHECK(hipEventRecord(p->ev0, p->st));
+    hipLaunchKernelGGL(k_check_templates, dim3((n_samples + 255) / 256, p->G), dim3(256), 0, p->st,
                        reinterpret_cast<const NodeHot*>(rows),
                        reinterpret_cast<const NodeExt*>(rows + sizeof(NodeHot) * G),
                        reinterpret_cast<const NodeStatic*>(rows + (sizeof(NodeHot) + sizeof(NodeExt)) * G),
@@ -1616,9 +1638,16 @@ int ca_expansion_plan_run(ca_expansion_plan* p, const ca_podset* s, const int32_
                        out ? reinterpret_cast<ca_pred_result*>(d_out ? d_out : dio + nsm) : nullptr,
                        out_ok ? reinterpret_cast<uint8_t*>(d_ok ? d_ok : dio + nsm + no) : nullptr);
     CA_HIP_CHECK(hipGetLastError());
-    CA_HIP_CHECK(hipEventRecord(m->ev1, m->stream));
-    CA_HIP_CHECK(hipStreamSynchronize(m->stream));
-    CA_HIP_CHECK(hipEventElapsedTime(&p->kernel_ms, m->ev0, m->ev1));
+    CA_HIP_CHECK(hipEventRecord(p->ev1, p->st));
+    const auto t_launched = std::chrono::steady_clock::now();
+    CA_HIP_CHECK(hipStreamSynchronize(p->st));
+    CA_HIP_CHECK(hipEventElapsedTime(&p->kernel_ms, p->ev0, p->ev1));
+    if (knob_env("CASIM_DEBUG_TIMING")) {
+        const auto t_done = std::chrono::steady_clock::now();
+        fprintf(stderr, "[expansion] launched %.3f ms, synced %.3f ms, kernel %.3f ms (%d x %d)\n",
+                std::chrono::duration<double, std::milli>(t_launched - t_entry).count(),
+                std::chrono::duration<double, std::milli>(t_done - t_entry).count(), p->kernel_ms, p->G, n_samples);
+    }
     if (out && !d_out) std::memcpy(out, hio + nsm, sizeof(ca_pred_result) * pairs);
     if (out_ok && !d_ok) std::memcpy(out_ok, hio + nsm + no, pairs);
     return CA_OK;

@@ -93,6 +93,7 @@ int32_t ca_mirror::store_moved_copy(int32_t pod) {
     row.node = -1;
     if (pod_dev_flags(row.spec) & (PF_PORTS | PF_SCALAR_REQ | PF_MOVED_SCALAR_REQ)) n_ext_pods++;
     if (row.spec.req_ephemeral != 0) n_eph_pods++;
+    if (row.spec.flags & CA_POD_OUT_OF_SCOPE) n_oos_pods++;
     pods.push_back(row);
     return (int32_t)pods.size() - 1;
 }
@@ -150,7 +151,7 @@ int ca_mirror::replay_moves(const ca_plan_move* mv, int32_t nm) {
     struct Part {
         std::vector<JournalEntry> jr;
         std::vector<int32_t> dirty;
-        int64_t ext = 0, eph = 0, blockers = 0;
+        int64_t ext = 0, eph = 0, blockers = 0, oos = 0;
         int rc = CA_OK;
     };
     std::vector<Part> part((size_t)T);
@@ -166,6 +167,7 @@ int ca_mirror::replay_moves(const ca_plan_move* mv, int32_t nm) {
             r.node = -1;
             if (pod_dev_flags(r.spec) & (PF_PORTS | PF_SCALAR_REQ | PF_MOVED_SCALAR_REQ)) pt.ext++;
             if (r.spec.req_ephemeral != 0) pt.eph++;
+            if (r.spec.flags & CA_POD_OUT_OF_SCOPE) pt.oos++;
         }
     });
     tmark("records");
@@ -253,6 +255,7 @@ int ca_mirror::replay_moves(const ca_plan_move* mv, int32_t nm) {
         if (first_rc == CA_OK) first_rc = pt.rc;
         n_ext_pods += pt.ext;
         n_eph_pods += pt.eph;
+        n_oos_pods += pt.oos;
         n_scope_blockers += pt.blockers;
         dirty_rows.insert(dirty_rows.end(), pt.dirty.begin(), pt.dirty.end());
         if (journaled) journal.insert(journal.end(), pt.jr.begin(), pt.jr.end());

@@ -2016,6 +2016,7 @@ int32_t scope_cut(const ca_mirror* m, int32_t C, const int32_t* candidates, cons
         const int32_t nd = candidates[c];
         if (nd < 0 || nd >= n || !dest_mask[nd] || (status && status[c] != 0)) continue;
         if (move_off[c + 1] - move_off[c] > CA_MAX_MOVED_PODS) return c;
+        if (m->n_oos_pods == 0) continue;        // no out-of-scope record in the mirror: no per-pod reads
         for (int32_t i = move_off[c]; i < move_off[c + 1]; i++) {
             const int32_t id = move_pods[i];
             if (id >= 0 && id < np && (m->pods[id].spec.flags & CA_POD_OUT_OF_SCOPE)) return c;
@@ -2047,6 +2048,7 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
                             int32_t* hints, int32_t* last_index, ca_removal_result* results, int32_t* out_dest) {
     if (!m || (C > 0 && (!candidates || !dest_mask || !move_off || !results || !out_dest)) || !last_index || C < 0)
         return CA_EINVAL;
+    const auto t_entry = std::chrono::steady_clock::now();
     CA_HIP_CHECK(hipSetDevice(m->device));
     hipStream_t st = m->stream;
     const int32_t n = (int32_t)m->nodes.size();
@@ -2130,6 +2132,9 @@ int ca_find_nodes_to_remove(ca_mirror* m, const int32_t* candidates, int32_t C, 
     in.d_c = DevView{dptr}; in.d_status = DevView{dptr + C}; in.d_off = DevView{dptr + 2 * C};
     in.d_moves = DevView{dptr + 3 * C + 1}; in.d_hints = DevView{dptr + 3 * C + 1 + M};
     in.d_mask = DevView{dptr + in_ints};
+    if (knob_env("CASIM_DEBUG_TIMING"))
+        fprintf(stderr, "[sweep] entry to core %8.3f ms (C %d, M %d)\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_entry).count(), C, M);
     return sweep_core(m, in, hints, nullptr, last_index, results, out_dest);
 }
 

@@ -183,8 +183,10 @@ class DeviceExpansion:
             self.templates = templates
             self.tbytes = tb
             self.rows = self.rows or native.PinnedRows()
-        out = self.rows.zeros("res", len(templates) * len(samples), abi.PRED_RESULT_DTYPE, zero=False)
-        return self.plan.run(podset, samples, out=out.reshape(len(templates), len(samples)))
+        # the loop needs only the option set: one verdict byte per (group, sample) crosses PCIe
+        # instead of a 16-byte ca_pred_result
+        out = self.rows.zeros("ok", len(templates) * len(samples), np.uint8, zero=False)
+        return self.plan.run(podset, samples, verdict_only=True, out=out.reshape(len(templates), len(samples)))
 
     def close(self):
         if self.plan is not None:
@@ -292,7 +294,8 @@ def run(backend, util_fn, w: RunOnceWorkload, timers=None, row_zeros=_zeros, exp
     else:
         res = backend.check_templates(f.pending, samples, w.templates, **kw)
     r.ms["expansion"] = (clock() - t) * 1e3
-    r.options = (res["type"] == 0).astype(np.uint8)
+    # a [G][E] uint8 verdict (1 = fits, the device's verdict-only form) or ca_pred_result rows
+    r.options = res.astype(np.uint8) if res.dtype == np.uint8 else (res["type"] == 0).astype(np.uint8)
 
     # 3. Estimate of every option, one batch
     off, idx = [0], []

@@ -365,7 +365,11 @@ int ca_check_templates(ca_mirror* m, const ca_podset* s, const int32_t* samples,
  * rows once; _run takes the pod set and the samples of one loop and writes out / out_ok
  * as ca_check_templates does, its samples and results passing through page-locked memory
  * the kernel reads and writes in place (no copy-engine round trips).  s must belong to
- * the plan's mirror. */
+ * the plan's mirror.  _run reads only the plan's rows and the pod set (both fixed when
+ * their create calls return) and runs on the plan's own stream: it does not wait for
+ * work still queued on the mirror (e.g. FilterOutSchedulable's record gather).  Asking
+ * only for out_ok (one byte per pair instead of a 16-byte ca_pred_result) is the fast
+ * form when the caller needs only the option set. */
 typedef struct ca_expansion_plan ca_expansion_plan;
 int ca_expansion_plan_create(ca_mirror* m, const ca_template* templates, int32_t n_templates,
                              ca_expansion_plan** out);

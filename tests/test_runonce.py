@@ -45,13 +45,15 @@ def test_runonce_gpu_parity(size, oracle_lib):
     ps = m.podset(w.filt.pending)
     samples = np.array([g[0] for g in runonce._equivalence_groups(
         w.filt.pending.pods, w.filt.order[rg.filter_node < 0])], np.int32)
-    assert expand(m, ps, samples, w.templates).tobytes() == \
-        m.check_templates(w.filt.pending, samples, w.templates, podset=ps).tobytes()
+    ok = expand(m, ps, samples, w.templates)                # the loop's verdict-only form
+    full = expand.plan.run(ps, samples)                     # the same plan, full records
+    assert full.tobytes() == m.check_templates(w.filt.pending, samples, w.templates, podset=ps).tobytes()
+    assert ok.dtype == np.uint8 and np.array_equal(ok, (full["type"] == 0).astype(np.uint8))
     ps.close()
     expand.close()
     # the full rows through one table, as a second form of the same step
-    full = runonce.UtilInput(w, rg.filter_node, "full")
-    t = native.UtilTable(0, full.nodes, full.off, full.pods)
+    fullu = runonce.UtilInput(w, rg.filter_node, "full")
+    t = native.UtilTable(0, fullu.nodes, fullu.off, fullu.pods)
     assert t.calculate(False, False, w.now_ns).tobytes() == rg.util.tobytes()
     t.close()
     util.close()

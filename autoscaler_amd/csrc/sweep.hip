@@ -1685,6 +1685,9 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         constexpr int32_t SIDE_BAND = CASIM_SIDE_BAND;
         std::vector<uint8_t> have_side((size_t)S, 0), want_side((size_t)S, 0);   // want_side: bit 0 below, bit 1 above
         std::vector<int32_t> gapk((size_t)S, 1);
+        std::vector<int32_t> dbg_rc;                // (CASIM_DEBUG_TIMING) round that re-centred each row
+        int32_t dbg_first_rc = -1;                   // ... and the first row the last pass re-centred
+        if (dbg_t) dbg_rc.assign((size_t)S, 0);
         // Where each candidate's rows are: the first pipeline's table ([64][S] values and
         // [FPW][S] fit points, copied once), or the compact rows of the table round that
         // rebuilt them, read in place in that round's page-locked buffer ([64][T], [FPW][T]:
@@ -1716,7 +1719,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         // the device walk's re-runs already happened: only candidates from k0 on remain
         // each round looks LOOKAHEAD candidates ahead: the estimates drift with the distance
         // from the exact lastIndex, so rows further out would be re-centred again anyway
-        constexpr int32_t LOOKAHEAD = 512;
+        static const int32_t LOOKAHEAD = knob_env("CASIM_SWEEP_LOOKAHEAD") ? std::max(64, atoi(knob_env("CASIM_SWEEP_LOOKAHEAD"))) : 512;
         // Serial exact chain: when a table round resolves few candidates for its cost (late
         // planner windows over a nearly full cluster: long scans that no lane budget covers,
         // windows that miss again after every re-centring), the next candidates run exactly
@@ -1854,8 +1857,10 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                         const int32_t* fp = mref[k0].f;
                         const int32_t lo = fp[0], hi = fp[(size_t)64 * mref[k0].s];
                         const int32_t gap = std::max(1, wrap((int64_t)hi - lo, n) / 64);
-                        fprintf(stderr, "[sweep] miss at %d: input %d, window [%d, %d] (gap %d): %+d gaps from its start\n",
-                                k0, wrap(cur, n), lo, hi, gap, (int)(wrap((int64_t)wrap(cur, n) - lo + n / 2, n) - n / 2) / gap);
+                        fprintf(stderr, "[sweep] miss at %d: input %d, window [%d, %d] (gap %d): %+d gaps from its start"
+                                        " (row re-centred in round %d; %d rows after the last pass's first re-centred %d)\n",
+                                k0, wrap(cur, n), lo, hi, gap, (int)(wrap((int64_t)wrap(cur, n) - lo + n / 2, n) - n / 2) / gap,
+                                dbg_rc[k0], k0 - dbg_first_rc, dbg_first_rc);
                     }
                     break;
                 }
@@ -1895,6 +1900,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
             // re-centre the windows from k0 on: follow the tables where the estimate falls
             // inside a window, otherwise shift the nearest known entry
             int64_t est = cur;
+            dbg_first_rc = -1;
             for (int32_t k = k0; k < std::min(S, k0 + LOOKAHEAD); k++) {
                 if (insensitive(k)) continue;
                 const RowRef& mr = mref[k];                          // the main row
@@ -1921,6 +1927,10 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                     const int32_t gap = std::max(1, wrap((int64_t)fp[(size_t)64 * ms] - fp[0], n) / 64);
                     ws[k] = wrap(est - 32 * (int64_t)gap, n);
                     gapk[k] = gap;
+                    if (dbg_t) {
+                        dbg_rc[k] = rounds + 1;
+                        if (dbg_first_rc < 0) dbg_first_rc = k;
+                    }
                     have[k] = 0;
                     have_side[k] = 0;
                 }

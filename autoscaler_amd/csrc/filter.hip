@@ -1464,6 +1464,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
         h_order[k] = order ? order[k] : k;
         h_hints[k] = hints ? hints[k] : -1;
     }
+    tmark("inputs");
     if (class_owner) std::memcpy(hi + o_owner, class_owner, sizeof(int32_t) * n_classes);
     std::memcpy(hi + o_capped, capped.data(), (size_t)n_classes);
     FoCtl ctl0;
@@ -1479,6 +1480,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     // hints are in/out: the kernel writes into a copy in the output block
     int32_t* d_hints = reinterpret_cast<int32_t*>(dout + al(sizeof(int32_t) * n));
     CA_HIP_CHECK(hipMemcpyAsync(d_hints, di + o_hints, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, m->stream));
+    tmark("staged");
     FoArgs a;
     a.hot = m->d_hot.as<NodeHot>();
     a.ext = m->d_ext.as<NodeExt>();
@@ -1516,6 +1518,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     if (fb) {
         uint64_t taint_union = 0;
         for (const NodeRow& r : m->nodes) taint_union |= r.spec.taints;
+        tmark("taints");
         struct KeyHash {
             size_t operator()(const std::string& k) const { return std::hash<std::string>()(k); }
         };
@@ -1596,6 +1599,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
             fp.simcls = ps.similar_class;
             fp.flags = f;
         }
+        tmark("shapes");
         // Shapes that fit no node now never fit during the call (placements only take
         // resources away): their pods share one shape with an all-zero dyn row (requests no
         // node has), so only the live shapes count against the 64 lanes of the bit updates.
@@ -1636,6 +1640,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
                     }
                 }
             }
+            tmark("alive");
             bool any_dead = false;
             for (int32_t q = 0; q < S0; q++) any_dead |= !alive[q];
             if (any_dead) {

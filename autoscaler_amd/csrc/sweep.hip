@@ -1679,6 +1679,9 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         // per row, near-edge rows only (C5 RunOnce sweep: 16 / 24 / 32 classes read 2.85 /
         // 2.6 / 3.0 ms, both sides at 16: 3.1, none: 3.5).
         const bool sides = !knob_env("CASIM_SWEEP_NO_SIDE_ROWS");
+        // CASIM_SWEEP_RECENTRE_SIDES=1/2/3: a re-centred row gets its side row below / above /
+        // both in the same round as its main row (A/B of wider windows for the drifting estimates)
+        const int recentre_sides = knob_env("CASIM_SWEEP_RECENTRE_SIDES") ? atoi(knob_env("CASIM_SWEEP_RECENTRE_SIDES")) & 3 : 0;
 #ifndef CASIM_SIDE_BAND
 #define CASIM_SIDE_BAND 24
 #endif
@@ -1933,6 +1936,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                     }
                     have[k] = 0;
                     have_side[k] = 0;
+                    if (sides && recentre_sides) want_side[k] = (uint8_t)recentre_sides;   // (knob: A/B)
                 }
                 est = wrap(next, n);
             }

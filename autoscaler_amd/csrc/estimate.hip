@@ -1689,6 +1689,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     // publish the chunks whose outputs are all scheduled (wave 0 stores every result in
     // publishing mode: segments by thread 0, single placements by its lanes)
     int32_t tk_next = 0;
+    int32_t tk_bound = pch;         // (tk_next + 1) * pch: progress() divides only once it is reached
     // outputs [pure_from, nsched) all come from run segments with stream offset pure_off
     // (pure chunks: push_chunks); a single placement or a segment with another offset
     // restarts the range
@@ -1697,9 +1698,9 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
         if (src - dst != pure_off || dst < pure_from) { pure_from = dst; pure_off = src - dst; }
     };
     auto progress = [&]() {
-        if (!tickets || !w0) return;
+        if (!tickets || !w0 || nsched < tk_bound) return;
         const int32_t c1 = nsched / pch;
-        if (c1 <= tk_next) return;
+        tk_bound = (c1 + 1) * pch;
         if (pend) {                       // the pending single placement, stored now
             so_pod[out_idx] = pos_out ? wbase + lane : cur.pod;
             pend = false;
@@ -1781,6 +1782,10 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                     const int32_t rem = RN - done;
                     const int32_t len = n_base + k;
                     int32_t placed = 0;
+                    // last_node's used bit after this iteration: its bit now (every row is
+                    // visible here: a barrier ended the previous step) or a placement on it, so
+                    // the empty-node check below needs no barrier after the row updates
+                    bool last_used = last_node >= 0 && R[last_node].used;
                     if ((sf & SF_FA_OK) && k > 0) {
                         int32_t s0 = L;
                         if (s0 >= len) s0 = (int32_t)((uint32_t)s0 % (uint32_t)len);
@@ -1839,10 +1844,14 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                                     if (f0) {
                                         adm_w |= 1ull << ((b - lo) >> 6);
                                         s32 += acc(b, rec_copies_run(r0, dv, zero, rem, pcpu, pmem, peph), in0);
+                                    } else if (in0) {
+                                        CAPA[j] = 0;      // (read by the other waves' pick)
                                     }
                                     if (f1) {
                                         adm_w |= 1ull << ((b + 64 - lo) >> 6);
                                         s32 += acc(b + 64, rec_copies_run(r1, dv, zero, rem, pcpu, pmem, peph), in1);
+                                    } else if (in1) {
+                                        CAPA[j + 64] = 0;
                                     }
                                 }
                             } else {
@@ -1884,6 +1893,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                             if (L >= len) L -= len;
                             note_success();
                             placed = n_one;
+                            last_used |= one == last_node;
                         } else if (nalive > 1) {
                             const int32_t n = (int32_t)min(S, (int64_t)rem);
                             PROF_T(t_rv);
@@ -1911,25 +1921,21 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                                         if (t <= cw_) break;
                                         t -= cw_;
                                     }
-                                    if (wv == w) {
+                                    {   // every wave finds it in wave w's counts: no barrier
                                         int32_t lo, hi;
-                                        wave_rows(k, wv, lo, hi);
+                                        wave_rows(k, w, lo, hi);
                                         for (int32_t b = lo; b < hi; b += 64) {
-                                            if (!((adm_w >> ((b - lo) >> 6)) & 1ull)) continue;
                                             const int32_t j = b + lane;
                                             const uint64_t bm = __ballot(j < hi && CAPA[j] >= r);
                                             const int32_t pc = __builtin_popcountll(bm);
                                             if (t <= pc) {
                                                 const bool hit = ((bm >> lane) & 1ull) && mbcnt(bm) == t - 1;
-                                                const uint64_t hm2 = __ballot(hit);
-                                                if (lane == 0) cred.pick = b + __builtin_ctzll(hm2);
+                                                last = b + __builtin_ctzll(__ballot(hit));
                                                 break;
                                             }
                                             t -= pc;
                                         }
                                     }
-                                    cbar<GROWS>();
-                                    last = cred.pick;
                                     got = n;
                                     PROF_INC(6);
                                     break;
@@ -2049,6 +2055,12 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                                 }
                             }
                             PROF_ADD(3, t_up);
+                            if (last_node >= 0 && !last_used) {      // (the update's nj of last_node)
+                                const int32_t c = CAPA[last_node];
+                                int32_t rj = last_node - j0;
+                                if (rj < 0) rj += k;
+                                last_used = min(c, r - 1) + ((c >= r && rj <= rl) ? 1 : 0) > 0;
+                            }
                             L = n_base + last + 1;
                             if (L >= len) L -= len;
                             note_success();
@@ -2056,21 +2068,23 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                         }
                     }
                     PROF_T(t_pb);
-                    cbar<GROWS>();            // the run's row updates are visible to every wave
+                    // The row updates become visible to every wave at the next barrier: right
+                    // below when the run ends here, else the node opening's (its rows are new,
+                    // beyond every row read or written above)
                     if (tid == 0 && placed > 0) gseg[nseg] = Seg{nsched, pos + done, placed, 0};
                     if (placed > 0) note_segment(nsched, pos + done);
                     nseg += placed > 0 ? 1 : 0;
                     nsched += placed;
                     done += placed;
                     progress();
-                    if (done == RN) break;
+                    if (done == RN) { cbar<GROWS>(); break; }
                     exhausted = true;
                     // the next pod of the run fails FitsAnyNode: every new node visited
                     evals += kev * (uint64_t)k;
                     if (max_nodes > 0 && granted >= max_nodes) { stop = true; break; }
                     granted++;
                     PROF_ADD(9, t_pb);
-                    if (last_node >= 0 && !R[last_node].used) {
+                    if (last_node >= 0 && !last_used) {
                         // :114-116 — and every later pod of the run repeats this pod's fate
                         done++;
                         const int32_t q = RN - done;
@@ -2084,6 +2098,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                         evals += (uint64_t)q * kev * (uint64_t)k;
                         granted += q;
                         done = RN;
+                        cbar<GROWS>();
                         break;
                     }
                     if (k >= kcap) { res.status = CA_ECAPACITY; stop = true; break; }

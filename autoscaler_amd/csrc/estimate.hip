@@ -1574,7 +1574,9 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
 // placement's scan ends at unwrapped position (rev-1)*k + rank, so a batch costs
 // (r_last-1)*k + rank(last)+1 filter calls.  assign[pos] receives the new-node index of
 // every placed stream position (-1 = not scheduled).
-template <bool GROWS>
+// PS: the batch has pods with host ports or extended-resource requests (their columns and
+// checks compile out of the common instantiation)
+template <bool GROWS, bool PS>
 __global__ void __launch_bounds__(CT) k_ffd_chain(
     const GroupMeta* __restrict__ groups, const StreamPod* __restrict__ stream, const uint64_t* __restrict__ heads,
     const ca_template* __restrict__ tmpls, const ca_pod_spec* __restrict__ specs, const PodHot* __restrict__ ph,
@@ -1627,7 +1629,8 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
     int32_t* CAPA = reinterpret_cast<int32_t*>(SUM + nb_cap);                   // [kcap]
     int32_t* ALIVE = CAPA + kcap;                                               // [kcap]
     uint64_t* PORTS = reinterpret_cast<uint64_t*>(ALIVE + kcap);                // [kcap][CA_PORT_WORDS]
-    int64_t* SC = reinterpret_cast<int64_t*>(PORTS + (use_ports ? (size_t)CA_PORT_WORDS * kcap : 0));  // [8][kcap]
+    int64_t* SC = reinterpret_cast<int64_t*>(PORTS + (use_ports ? (size_t)CA_PORT_WORDS * kcap : 0));
+    if (!PS) use_ports = use_scalar = 0;  // [8][kcap]
 
     const ca_template& tp = tmpls[gm.tmpl];
     NodeRec trec;                 // a fresh template copy
@@ -2181,7 +2184,7 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
         uint64_t pconf[CA_PORT_WORDS] = {0, 0}, puse[CA_PORT_WORDS] = {0, 0};
         int64_t psc[CA_MAX_SCALAR];
         for (int i = 0; i < CA_MAX_SCALAR; i++) psc[i] = 0;
-        if (sf & (SF_PORTS | SF_SCALAR)) {
+        if (PS && (sf & (SF_PORTS | SF_SCALAR))) {
             const ca_pod_spec& s = specs[ph[pidx].spec];
             for (int w = 0; w < CA_PORT_WORDS; w++) { pconf[w] = s.port_conflict[w]; puse[w] = s.port_use[w]; }
             for (int i = 0; i < CA_MAX_SCALAR; i++) psc[i] = s.req_scalar[i];
@@ -2219,11 +2222,11 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
                         const bool valid = (j < k) & ((r != 0) | (j >= j0)) & ((r != nb) | (j < j0));
                         const NodeRec nr = R[j < k ? j : 0];
                         bool fit = valid & rec_fits(nr, pcpu, pmem, peph, zero);
-                        if (sf & SF_SCALAR) {
+                        if (PS && (sf & SF_SCALAR)) {
                             for (int i = 0; i < CA_MAX_SCALAR; i++)
                                 fit = fit & !((psc[i] != 0) & (j < k) && psc[i] > SC[(size_t)i * kcap + (j < k ? j : 0)]);
                         }
-                        if (sf & SF_PORTS) {
+                        if (PS && (sf & SF_PORTS)) {
                             uint64_t c = 0;
                             for (int w = 0; w < CA_PORT_WORDS; w++) c |= PORTS[(size_t)(j < k ? j : 0) * CA_PORT_WORDS + w] & pconf[w];
                             fit = fit & (c == 0);
@@ -2276,11 +2279,11 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
             bool ok = (sf & SF_CP_OK) != 0;
             if (ok) {
                 ok = rec_fits(trec, pcpu, pmem, peph, zero);
-                if (ok && (sf & SF_SCALAR)) {
+                if (PS && ok && (sf & SF_SCALAR)) {
                     for (int i = 0; i < CA_MAX_SCALAR; i++)
                         if (psc[i] != 0 && psc[i] > wsub(tp.node.alloc_scalar[i], tp.used_scalar[i])) ok = false;
                 }
-                if (ok && (sf & SF_PORTS)) {
+                if (PS && ok && (sf & SF_PORTS)) {
                     uint64_t c = 0;
                     for (int w = 0; w < CA_PORT_WORDS; w++) c |= tp.used_ports[w] & pconf[w];
                     ok = c == 0;
@@ -2301,13 +2304,13 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
             R[found] = r;
         }
         if (w0 && lane == sl) { out_node = found; out_idx = nsched; pend = true; }
-        if (sf & SF_SCALAR) {
+        if (PS && (sf & SF_SCALAR)) {
             if (tid < CA_MAX_SCALAR) {
                 const size_t ix = (size_t)tid * kcap + found;
                 SC[ix] = wsub(SC[ix], psc[tid]);
             }
         }
-        if (sf & SF_PORTS) {
+        if (PS && (sf & SF_PORTS)) {
             if (tid < CA_PORT_WORDS) PORTS[(size_t)found * CA_PORT_WORDS + tid] |= puse[tid];
         }
         nsched++;
@@ -3302,12 +3305,15 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
             CA_HIP_CHECK(hipEventRecord(p->ev_pub, st));
         }
         if (p->phase_events) CA_HIP_CHECK(hipEventRecord(p->ev[ca_estimate_plan::EV_CHAIN0], st));
+        const bool ps = p->use_ports || p->use_scalar;
+        auto chain_kernel = grows ? (ps ? k_ffd_chain<true, true> : k_ffd_chain<true, false>)
+                                  : (ps ? k_ffd_chain<false, true> : k_ffd_chain<false, false>);
         if (!grows) {
             int rcl;
-            if ((rcl = ensure_dyn_lds((const void*)k_ffd_chain<false>, lds)) != CA_OK) return rcl;
+            if ((rcl = ensure_dyn_lds((const void*)chain_kernel, lds)) != CA_OK) return rcl;
         }
         auto chain = [&](hipStream_t ss, const int32_t* gm, int32_t ng) -> int {
-            hipLaunchKernelGGL(grows ? k_ffd_chain<true> : k_ffd_chain<false>, dim3(ng), dim3(CT), lds, ss,
+            hipLaunchKernelGGL(chain_kernel, dim3(ng), dim3(CT), lds, ss,
                                p->d_meta.as<GroupMeta>(),
                                p->d_stream.as<StreamPod>(), p->d_heads.as<uint64_t>(), p->d_tmpl.as<ca_template>(),
                                p->s->t.spec.as<ca_pod_spec>(), p->s->t.hot.as<PodHot>(), p->d_lin.as<int32_t>(),

@@ -1431,6 +1431,7 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
     // ids_ready[g] holds this run's epoch — and the chains' single placements are stream positions
     __shared__ int32_t s_t, s_seg0;
     __shared__ int64_t s_tk;
+    __shared__ Seg s_segs[64];
     for (;;) {
         if (threadIdx.x == 0) {
             s_t = atomicAdd(&qctl[0], 1);
@@ -1523,23 +1524,47 @@ __global__ void __launch_bounds__(256) k_publish(const GroupMeta* __restrict__ g
         const int32_t* pr = reinterpret_cast<const int32_t*>(prog + tk);   // the group's progress at the push
         const int32_t nseg = ld_coh(pr);
         const int32_t ns = ld_coh(pr + 1);
-        if (threadIdx.x == 0) {                            // first segment ending after a
-            int32_t lo = 0, hi = nseg;
-            while (lo < hi) {
-                const int32_t mid = (lo + hi) >> 1;
-                const Seg sg = ld_seg(gs + mid);
-                if (sg.dst + sg.len <= a) lo = mid + 1; else hi = mid;
+        if (threadIdx.x < 64) {
+            // first segment ending after a (segments are in output order): wave 0 probes 64
+            // evenly spaced segments per step with coherent loads in flight together, so a
+            // search is one or two round trips to L2 instead of one per bisection step
+            const int lane = (int)threadIdx.x;
+            int32_t lo = 0, hi = nseg;                     // answer in [lo, hi]
+            while (hi - lo > 0) {
+                const int32_t span = hi - lo;
+                const int32_t step = (span + 63) / 64;
+                const int32_t i = lo + lane * step;
+                bool past = false;                         // segment i ends after a
+                if (i < hi) {
+                    const int32_t* q3 = reinterpret_cast<const int32_t*>(gs + i);
+                    past = ld_coh(q3) + ld_coh(q3 + 2) > a;
+                }
+                const uint64_t m = __ballot(past);
+                const int32_t f = m ? (int32_t)__builtin_ctzll(m) : -1;    // first probe past a
+                if (step == 1) { lo = f >= 0 ? lo + f : hi; break; }
+                const int32_t nlo = f > 0 ? lo + (f - 1) * step + 1 : (f == 0 ? lo : lo + ((span - 1) / step) * step + 1);
+                hi = f >= 0 ? lo + f * step : hi;
+                lo = nlo;
             }
-            s_seg0 = lo;
+            if (lane == 0) s_seg0 = lo;
         }
         lds_barrier();
         int32_t at = a, q = s_seg0;
         const int32_t end = min(b, ns);
+        int32_t q0 = 0, qn = 0;                           // segments [q0, q0 + qn) cached in LDS
         while (at < end) {
             int32_t lim = end, src_off = 0;
             bool from_seg = false;
+            if (q < nseg && (q < q0 || q >= q0 + qn)) {
+                // the next 64 segments, loaded together (one round trip instead of one per segment)
+                lds_barrier();                             // every thread is done with the old ones
+                if (threadIdx.x < 64 && q + (int32_t)threadIdx.x < nseg) s_segs[threadIdx.x] = ld_seg(gs + q + threadIdx.x);
+                q0 = q;
+                qn = min(64, nseg - q);
+                lds_barrier();
+            }
             if (q < nseg) {
-                const Seg sg = ld_seg(gs + q);
+                const Seg sg = s_segs[q - q0];
                 if (sg.dst <= at) {                            // inside segment q
                     from_seg = true;
                     src_off = sg.src - sg.dst;

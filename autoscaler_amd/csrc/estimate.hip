@@ -2373,7 +2373,11 @@ __global__ void __launch_bounds__(CT) k_ffd_chain(
             const bool ok = res.status == CA_OK;
             // a group that failed after publishing chunks: the host falls back to the copy
             if (!ok && tk_next > 0 && lane == 0) { atomicExch(&qctl[3], 1); hflags[3] = 1; }
-            push_chunks(g, tk_next, (P + pch - 1) / pch, nsub, tickets, qctl, prog, ok ? nseg : 0, ok ? nsched : 0, lane);
+            // every pod scheduled: the tail chunks are pure when one segment offset covers them
+            // (the publisher copies them straight from the stream's ids, no segment reads)
+            const bool all = ok && nsched == P;
+            push_chunks(g, tk_next, (P + pch - 1) / pch, nsub, tickets, qctl, prog, ok ? nseg : 0, ok ? nsched : 0, lane,
+                        all ? pch : 0, all ? pure_from : INT32_MAX, pure_off);
         }
     }
     if (tid == 0) {

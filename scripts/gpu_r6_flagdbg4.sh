@@ -1,0 +1,8 @@
+#!/bin/bash
+# GPU-box job: the sweep / planner GPU tests in one process with the row flags (system-scope row stores).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T="tests/test_gpu_parity.py tests/test_runonce.py tests/test_gpu_multi.py tests/test_gpu_shard.py tests/test_gpu_planner.py tests/test_scope.py"
+timeout -k 10 600 python -u -m pytest -q --timeout 300 --timeout-method thread $T -m gpu > gpurun_out/flagdbg4.log 2>&1; echo "flags rc=$?"; tail -4 gpurun_out/flagdbg4.log

@@ -2942,7 +2942,7 @@ int plan_run(ca_estimate_plan* p, const ca_limiter* lim, int32_t* last_index, ca
     const bool to_host = sched_pod != nullptr || sched16 != nullptr;
     if (!to_host && sched_node) return CA_EINVAL;
     // 16-bit results: pod ids of a podset of at most 65535 pods (0xFFFF: not scheduled)
-    if (sched16 && (sched_pod || sched_node || p->s->h_pods.size() > 65535)) return CA_EINVAL;
+    if (sched16 && (sched_pod || sched_node || p->s->n_host > 65535)) return CA_EINVAL;
     p->pub_state = 0;
     const auto t_start = std::chrono::steady_clock::now();
     // CASIM_STEP_TIMING (read once per process): host-side split of the steps, averaged over

@@ -1430,9 +1430,13 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     tmark("synced");
     const DevPodTable* dp = s ? &s->t : nullptr;
     if (!dp) {
-        if ((rc = fo.pods.upload(t->pods, t->n_pods, t->terms, t->n_terms, t->reqs, t->n_reqs, t->prefilter_names,
-                                 t->n_prefilter_names, m->stream)) != CA_OK)
+        // (queued: the shape preparation below runs while the records cross; the call's sync
+        // after the kernel ends them before the staging is reused)
+        if ((rc = fo.pods.upload_staged(t->pods, t->n_pods, t->terms, t->n_terms, t->reqs, t->n_reqs,
+                                        t->prefilter_names, t->n_prefilter_names, fo.h_pods, m->stream)) != CA_OK) {
+            (void)hipStreamSynchronize(m->stream);
             return rc;
+        }
         dp = &fo.pods;
     }
     // similar-pods classes: controllers with more than maxPodsPerOwnerRef classes can hit the cap

@@ -42,6 +42,11 @@ struct DevPodTable {
     int32_t n_pods = 0, n_terms = 0, n_reqs = 0, n_names = 0;
     int upload(const ca_pod_spec* pods, int32_t n, const ca_selector_term* terms, int32_t nt,
                const ca_selector_req* reqs, int32_t nr, const int32_t* names, int32_t nn, hipStream_t st);
+    // the same with the hot rows and records copied into the page-locked `stage` first (host
+    // threads) and the copies left queued on st: the caller syncs st before stage is reused
+    int upload_staged(const ca_pod_spec* pods, int32_t n, const ca_selector_term* terms, int32_t nt,
+                      const ca_selector_req* reqs, int32_t nr, const int32_t* names, int32_t nn, HostBuf& stage,
+                      hipStream_t st);
     // append pods [n_pods, n_pods + k) and the selector tables' new tails (the mirror's
     // tables only grow between Clear()s), keeping what is on the device
     int append(const ca_pod_spec* new_pods, int32_t k, const ca_selector_term* terms, int32_t nt,
@@ -82,6 +87,7 @@ struct FilterScratch {
     DevBuf in, zero, out;          // inputs (order, hints, class tables), zeroed state, outputs
     HostBuf h_in, h_out;
     DevPodTable pods;              // the pending table when the caller passes no podset
+    HostBuf h_pods;                // ... staged in page-locked memory (its copies run beside the preparation)
     DevBuf gather_idx;             // podset indices of the placed pods (mirror records gathered on the device)
     float kernel_ms = 0, total_ms = 0;
     int32_t phases = 0, steps = 0, ring_scans = 0, windows = 0;
@@ -266,6 +272,7 @@ struct ca_mirror {
     casim::FilterScratch fo;
     casim::PlanChainScratch pc;
     casim::RowStage rs;
+    casim::HostBuf podset_stage;           // ca_podset_create: the records' page-locked staging
     // resident HintingSimulator hints (hints.go:29-72): node per mirror pod, -1 = none
     casim::DevBuf d_pod_hints;
     size_t d_hints_n = 0;
@@ -305,7 +312,8 @@ struct ca_mirror {
 struct ca_podset {
     ca_mirror* m = nullptr;
     casim::DevPodTable t;
-    std::vector<ca_pod_spec> h_pods;   // host copy (flags, used for classification)
+    int32_t n_host = 0;                // pods in the set
+    bool any_oos = false;              // some pod carries CA_POD_OUT_OF_SCOPE (no host copy of the records)
     // Score classes: pods with equal (score_milli_cpu, score_memory) — the only inputs of
     // calculatePodScore (binpacking_estimator.go:164-193) — share a class, numbered in
     // first-occurrence order.  d_cls[pod] = class, d_cls_sc[c] = {score_milli_cpu,

@@ -280,6 +280,44 @@ int DevPodTable::upload(const ca_pod_spec* pods, int32_t n, const ca_selector_te
     return CA_OK;
 }
 
+int DevPodTable::upload_staged(const ca_pod_spec* pods, int32_t n, const ca_selector_term* tms, int32_t nt,
+                               const ca_selector_req* rqs, int32_t nr, const int32_t* nms, int32_t nn, HostBuf& stage,
+                               hipStream_t st) {
+    // [hot n][records n] in one page-locked block: the DMA reads it while the caller goes on
+    // (a pageable source is copied through the runtime's staging before the call returns)
+    const size_t hb = ((sizeof(PodHot) * (size_t)n + 255) & ~(size_t)255);
+    int rc;
+    CA_HIP_CHECK(hipStreamSynchronize(st));      // (an earlier call's copies out of stage are done)
+    if ((rc = stage.reserve(hb + sizeof(ca_pod_spec) * (size_t)std::max(n, 1))) != CA_OK) return rc;
+    PodHot* const h = stage.as<PodHot>();
+    ca_pod_spec* const rec = reinterpret_cast<ca_pod_spec*>(stage.as<unsigned char>() + hb);
+    const int32_t T = n >= 8192 ? 8 : 1;
+    parallel_run(T, [&](int32_t w) {
+        const int32_t a = (int32_t)((int64_t)n * w / T), b = (int32_t)((int64_t)n * (w + 1) / T);
+        std::memcpy(rec + a, pods + a, sizeof(ca_pod_spec) * (size_t)(b - a));
+        for (int32_t i = a; i < b; i++) {
+            h[i].cpu = pods[i].req_milli_cpu;
+            h[i].mem = pods[i].req_memory;
+            h[i].eph = pods[i].req_ephemeral;
+            h[i].flags = pod_dev_flags(pods[i]);
+            h[i].spec = i;
+        }
+    });
+    const size_t room = (size_t)n + (size_t)n / 4 + 1024;
+    if ((rc = hot.reserve(sizeof(PodHot) * room)) != CA_OK) return rc;
+    if ((rc = spec.reserve(sizeof(ca_pod_spec) * room)) != CA_OK) return rc;
+    if ((rc = terms.reserve(sizeof(ca_selector_term) * (size_t)(nt + 1))) != CA_OK) return rc;
+    if ((rc = reqs.reserve(sizeof(ca_selector_req) * (size_t)(nr + 1))) != CA_OK) return rc;
+    if ((rc = names.reserve(sizeof(int32_t) * (size_t)(nn + 1))) != CA_OK) return rc;
+    if (n) CA_HIP_CHECK(hipMemcpyAsync(hot.ptr, h, sizeof(PodHot) * n, hipMemcpyHostToDevice, st));
+    if (n) CA_HIP_CHECK(hipMemcpyAsync(spec.ptr, rec, sizeof(ca_pod_spec) * n, hipMemcpyHostToDevice, st));
+    if (nt) CA_HIP_CHECK(hipMemcpyAsync(terms.ptr, tms, sizeof(ca_selector_term) * nt, hipMemcpyHostToDevice, st));
+    if (nr) CA_HIP_CHECK(hipMemcpyAsync(reqs.ptr, rqs, sizeof(ca_selector_req) * nr, hipMemcpyHostToDevice, st));
+    if (nn) CA_HIP_CHECK(hipMemcpyAsync(names.ptr, nms, sizeof(int32_t) * nn, hipMemcpyHostToDevice, st));
+    n_pods = n; n_terms = nt; n_reqs = nr; n_names = nn;
+    return CA_OK;
+}
+
 int DevPodTable::append(const ca_pod_spec* np, int32_t k, const ca_selector_term* tms, int32_t nt,
                         const ca_selector_req* rqs, int32_t nr, const int32_t* nms, int32_t nn, hipStream_t st) {
     const int32_t n0 = n_pods, n = n_pods + k;
@@ -1225,13 +1263,21 @@ int ca_mirror_node_pods(const ca_mirror* m, int32_t node_pos, int32_t* out_ids, 
 int ca_podset_create(ca_mirror* m, const ca_pod_table* t, ca_podset** out) {
     if (!m || !t || !out || t->n_pods < 0) return CA_EINVAL;
     CA_HIP_CHECK(hipSetDevice(m->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    const bool dbg_t = knob_env("CASIM_DEBUG_TIMING") != nullptr;
+    auto tmark = [&](const char* what) {
+        if (dbg_t)
+            fprintf(stderr, "[podset] %-10s %8.3f ms\n", what,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    };
     ca_podset* s = new ca_podset();
     s->m = m;
-    s->h_pods.assign(t->pods, t->pods + t->n_pods);
+    s->n_host = t->n_pods;
     s->h_req.resize(2 * (size_t)t->n_pods);
     s->h_pflags.assign((size_t)t->n_pods, 0);
     for (int32_t i = 0; i < t->n_pods; i++) {
         const ca_pod_spec& ps = t->pods[i];
+        s->any_oos |= (ps.flags & CA_POD_OUT_OF_SCOPE) != 0;
         s->h_req[2 * (size_t)i] = ps.req_milli_cpu;
         s->h_req[2 * (size_t)i + 1] = ps.req_memory;
         const uint32_t f = pod_dev_flags(ps);
@@ -1240,9 +1286,13 @@ int ca_podset_create(ca_mirror* m, const ca_pod_table* t, ca_podset** out) {
         s->any_ports |= (b & 1) != 0;
         s->any_scalar |= (b & 2) != 0;
     }
-    int rc = s->t.upload(t->pods, t->n_pods, t->terms, t->n_terms, t->reqs, t->n_reqs, t->prefilter_names,
-                         t->n_prefilter_names, m->stream);
-    if (rc != CA_OK) { delete s; return rc; }
+    tmark("flags");
+    // the records' copies stay queued while the score classes are worked out below; the
+    // creation ends with one sync (a pod set is immutable and complete once created)
+    int rc = s->t.upload_staged(t->pods, t->n_pods, t->terms, t->n_terms, t->reqs, t->n_reqs, t->prefilter_names,
+                                t->n_prefilter_names, m->podset_stage, m->stream);
+    if (rc != CA_OK) { (void)hipStreamSynchronize(m->stream); delete s; return rc; }
+    tmark("uploaded");
     {   // score classes
         struct PairHash {
             size_t operator()(const std::pair<int64_t, int64_t>& k) const {
@@ -1279,11 +1329,11 @@ int ca_podset_create(ca_mirror* m, const ca_pod_table* t, ca_podset** out) {
         s->h_cls_sc = sc;
         std::vector<int32_t> rep((size_t)std::max(s->n_cls, 1), 0);
         for (int32_t i = t->n_pods - 1; i >= 0; i--) rep[cls[i]] = i;
-        if ((rc = s->d_cls_rep.reserve(sizeof(int32_t) * rep.size())) != CA_OK) { delete s; return rc; }
+        if ((rc = s->d_cls_rep.reserve(sizeof(int32_t) * rep.size())) != CA_OK) { (void)hipStreamSynchronize(m->stream); delete s; return rc; }
         CA_HIP_CHECK(hipMemcpyAsync(s->d_cls_rep.ptr, rep.data(), sizeof(int32_t) * rep.size(), hipMemcpyHostToDevice,
                                     m->stream));
         if ((rc = s->d_cls.reserve(sizeof(int32_t) * (cls.size() + 1))) != CA_OK ||
-            (rc = s->d_cls_sc.reserve(sizeof(int64_t) * (sc.size() + 2))) != CA_OK) { delete s; return rc; }
+            (rc = s->d_cls_sc.reserve(sizeof(int64_t) * (sc.size() + 2))) != CA_OK) { (void)hipStreamSynchronize(m->stream); delete s; return rc; }
         if (!cls.empty())
             CA_HIP_CHECK(hipMemcpyAsync(s->d_cls.ptr, cls.data(), sizeof(int32_t) * cls.size(), hipMemcpyHostToDevice,
                                         m->stream));
@@ -1292,6 +1342,7 @@ int ca_podset_create(ca_mirror* m, const ca_pod_table* t, ca_podset** out) {
                                         m->stream));
         CA_HIP_CHECK(hipStreamSynchronize(m->stream));
     }
+    tmark("classes");
     *out = s;
     return CA_OK;
 }
@@ -1437,7 +1488,7 @@ int ca_fits_matrix(ca_mirror* m, const ca_podset* s, uint8_t* out) {
     const int32_t n = (int32_t)m->nodes.size();
     const int32_t P = s->t.n_pods;
     if (m->n_scope_blockers > 0) return CA_EUNSUPPORTED;
-    for (const ca_pod_spec& ps : s->h_pods) if (ps.flags & CA_POD_OUT_OF_SCOPE) return CA_EUNSUPPORTED;
+    if (s->any_oos) return CA_EUNSUPPORTED;
     if (n == 0 || P == 0) return CA_OK;
     const size_t bytes = (size_t)n * (size_t)P;
     if ((rc = m->d_scratch2.reserve(bytes)) != CA_OK) return rc;

@@ -534,8 +534,17 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
     pods.resize_for_overwrite(base + (size_t)np);                // (the threads write every record)
     if (dirty_flag.size() < nodes.size()) dirty_flag.resize(nodes.size(), 0);
     std::vector<int32_t> id_of((size_t)n, -1);
+    // each thread's placements (its nodes' 64-node blocks), in order: a counting sort once
+    // instead of every thread stepping over all n positions
+    std::vector<int32_t> bk_off((size_t)T + 1, 0), bk((size_t)np);
     for (int32_t k = 0, c = 0; k < n; k++)
-        if (node[k] >= 0) id_of[k] = (int32_t)base + c++;
+        if (node[k] >= 0) { id_of[k] = (int32_t)base + c++; bk_off[((node[k] >> 6) & tmask) + 1]++; }
+    for (int32_t w = 0; w < T; w++) bk_off[w + 1] += bk_off[w];
+    {
+        std::vector<int32_t> fill(bk_off.begin(), bk_off.end() - 1);
+        for (int32_t k = 0; k < n; k++)
+            if (node[k] >= 0) bk[fill[(node[k] >> 6) & tmask]++] = k;
+    }
     tmark("resized");
     struct Part {
         std::vector<casim::JournalEntry> jr;
@@ -559,16 +568,16 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
             if (r.spec.flags & CA_POD_OUT_OF_SCOPE) pt.oos++;
         }
         if (dbg_t) tw[3 * w + 1] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        for (int32_t k = 0; k < n; k++) {               // AddPod on my nodes, in order
-            if (k + 32 < n) {                            // (rows are cache misses: fetch ahead)
-                const int32_t y = node[k + 32];
-                if (y >= 0 && ((y >> 6) & tmask) == w) {
-                    __builtin_prefetch(&nodes[y], 1);
-                    __builtin_prefetch(reinterpret_cast<const char*>(&nodes[y]) + 256, 1);
-                }
+        const int32_t b0 = bk_off[w], b1 = bk_off[w + 1];
+        if (journaled) pt.jr.reserve((size_t)(b1 - b0));
+        for (int32_t b = b0; b < b1; b++) {            // AddPod on my nodes, in order
+            if (b + 16 < b1) {                           // (rows are cache misses: fetch ahead)
+                const int32_t y = node[bk[b + 16]];
+                __builtin_prefetch(&nodes[y], 1);
+                __builtin_prefetch(reinterpret_cast<const char*>(&nodes[y]) + 256, 1);
             }
+            const int32_t k = bk[b];
             const int32_t x = node[k];
-            if (x < 0 || ((x >> 6) & tmask) != w) continue;
             const ca_pod_spec& p = t->pods[idx[k]];
             casim::NodeRow& nd = nodes[x];
             casim::JournalEntry e;

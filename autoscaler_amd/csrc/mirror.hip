@@ -547,12 +547,15 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
     }
     tmark("resized");
     struct Part {
-        std::vector<casim::JournalEntry> jr;
         std::vector<int32_t> dirty;
         int64_t ext = 0, eph = 0, blockers = 0, oos = 0;
     };
     std::vector<Part> part((size_t)T);
     const bool journaled = depth > 0;
+    // the journal grows by one entry per placement: thread w writes its placements' entries
+    // at jbase + bk_off[w] ... in place (no per-thread lists to merge)
+    const size_t jbase = journal.size();
+    if (journaled) journal.resize(jbase + (size_t)np);
     std::vector<double> tw((size_t)T * 3, 0.0);          // (CASIM_DEBUG_TIMING: per-thread start / records / AddPods)
     auto work = [&](int32_t w) {
         if (dbg_t) tw[3 * w] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -569,7 +572,6 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
         }
         if (dbg_t) tw[3 * w + 1] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         const int32_t b0 = bk_off[w], b1 = bk_off[w + 1];
-        if (journaled) pt.jr.reserve((size_t)(b1 - b0));
         for (int32_t b = b0; b < b1; b++) {            // AddPod on my nodes, in order
             if (b + 16 < b1) {                           // (rows are cache misses: fetch ahead)
                 const int32_t y = node[bk[b + 16]];
@@ -580,10 +582,10 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
             const int32_t x = node[k];
             const ca_pod_spec& p = t->pods[idx[k]];
             casim::NodeRow& nd = nodes[x];
-            casim::JournalEntry e;
             if (journaled) {
-                std::memset(&e, 0, sizeof e);
+                casim::JournalEntry& e = journal[jbase + (size_t)b];
                 e.kind = casim::J_ADD_POD; e.node = x; e.pod = id_of[k];
+                e.slot = (int32_t)nd.pods.size();                       // (the slot push_back below fills)
                 std::memcpy(e.ports, nd.ports, sizeof e.ports);
             }
             nd.req_cpu = casim::wadd(nd.req_cpu, p.req_milli_cpu);       // node_apply(+1)
@@ -595,10 +597,16 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
             if (p.flags & CA_POD_REQUIRED_ANTI_AFFINITY) pt.blockers++;
             if (!dirty_flag[x]) { dirty_flag[x] = 1; pt.dirty.push_back(x); }
             nd.pods.push_back(id_of[k]);
-            if (journaled) {
-                e.slot = (int32_t)nd.pods.size() - 1;
-                pt.jr.push_back(e);
+        }
+        if (device_rows) {                              // keep_device_rows on my own new marks
+            size_t o = 0;
+            for (const int32_t x : pt.dirty) {
+                const casim::NodeRow& nd = nodes[x];
+                const int64_t fp = nd.spec.alloc_pods - nd.npods;
+                if (fp >= INT32_MIN && fp + np <= INT32_MAX && (size_t)x < d_rows) { dirty_flag[x] = 0; continue; }
+                pt.dirty[o++] = x;
             }
+            pt.dirty.resize(o);
         }
         if (dbg_t) tw[3 * w + 2] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     };
@@ -614,11 +622,9 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
         n_oos_pods += pt.oos;
         n_scope_blockers += pt.blockers;
         dirty_rows.insert(dirty_rows.end(), pt.dirty.begin(), pt.dirty.end());
-        if (journaled) journal.insert(journal.end(), pt.jr.begin(), pt.jr.end());
     }
     if (out_id)
         for (int32_t k = 0; k < n; k++) out_id[k] = id_of[k];
-    keep_device_rows();
     tmark("merged");
 }
 

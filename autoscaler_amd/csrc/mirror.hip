@@ -1575,6 +1575,8 @@ struct ca_expansion_plan {
     // FilterOutSchedulable: the placed pods' record gather).
     hipStream_t st = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    void* io_host = nullptr;   // io.ptr when io_dev was looked up (a grown io re-queries)
+    char* io_dev = nullptr;    // io's device mapping
     ~ca_expansion_plan() {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -1679,19 +1681,27 @@ int ca_expansion_plan_run(ca_expansion_plan* p, const ca_podset* s, const int32_
     // device mapping: no copy-engine round trips for a call of a few kilobytes
     char* hio = p->io.as<char>();
     std::memcpy(hio, samples, sizeof(int32_t) * (size_t)n_samples);
-    void* dio_v = nullptr;
-    CA_HIP_CHECK(hipHostGetDevicePointer(&dio_v, p->io.ptr, 0));
-    char* dio = static_cast<char*>(dio_v);
-    // a page-locked output of the caller's (ca_host_alloc) takes the results straight from the kernel
-    auto mapped = [](void* h) -> char* {
+    if (p->io_host != p->io.ptr) {
+        void* dio_v = nullptr;
+        CA_HIP_CHECK(hipHostGetDevicePointer(&dio_v, p->io.ptr, 0));
+        p->io_dev = static_cast<char*>(dio_v);
+        p->io_host = p->io.ptr;
+    }
+    char* dio = p->io_dev;
+    // a page-locked output of the caller's (ca_host_alloc) takes large results straight from
+    // the kernel; below 256 KiB the results land in the plan's own buffer and one memcpy moves
+    // them (cheaper than the runtime's pointer lookup)
+    auto mapped = [](void* h, size_t bytes) -> char* {
+        if (!h || bytes < ((size_t)256 << 10)) return nullptr;
         hipPointerAttribute_t at;
-        if (h && hipPointerGetAttributes(&at, h) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer)
+        if (hipPointerGetAttributes(&at, h) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer)
             return static_cast<char*>(at.devicePointer);
         (void)hipGetLastError();
         return nullptr;
     };
-    char* d_out = out ? mapped(out) : nullptr;
-    char* d_ok = out_ok ? mapped(out_ok) : nullptr;
+    char* d_out = out ? mapped(out, sizeof(ca_pred_result) * pairs) : nullptr;
+    char* d_ok = out_ok ? mapped(out_ok, pairs) : nullptr;
+    const auto t_mapped = std::chrono::steady_clock::now();
     const size_t G = (size_t)p->G;
     const char* rows = p->rows.as<const char>();
     CA_HIP_CHECK(hipEventRecord(p->ev0, p->st));
@@ -1710,7 +1720,8 @@ int ca_expansion_plan_run(ca_expansion_plan* p, const ca_podset* s, const int32_
     CA_HIP_CHECK(hipEventElapsedTime(&p->kernel_ms, p->ev0, p->ev1));
     if (knob_env("CASIM_DEBUG_TIMING")) {
         const auto t_done = std::chrono::steady_clock::now();
-        fprintf(stderr, "[expansion] launched %.3f ms, synced %.3f ms, kernel %.3f ms (%d x %d)\n",
+        fprintf(stderr, "[expansion] mapped %.3f ms, launched %.3f ms, synced %.3f ms, kernel %.3f ms (%d x %d)\n",
+                std::chrono::duration<double, std::milli>(t_mapped - t_entry).count(),
                 std::chrono::duration<double, std::milli>(t_launched - t_entry).count(),
                 std::chrono::duration<double, std::milli>(t_done - t_entry).count(), p->kernel_ms, p->G, n_samples);
     }

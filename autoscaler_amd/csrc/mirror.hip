@@ -731,7 +731,15 @@ int ca_mirror::sync_nodes() {
         if ((rc = rs.full.reserve((sizeof(NodeHot) + sizeof(NodeExt)) * std::max<size_t>(n, 1))) != CA_OK) return rc;
         NodeHot* h = rs.full.as<NodeHot>();
         NodeExt* e = reinterpret_cast<NodeExt*>(h + n);
-        for (size_t i = 0; i < n; i++) { fill_hot((int32_t)i, h[i]); fill_ext((int32_t)i, e[i]); }
+        // (a revert's or a new snapshot's thousands of rows: filled by the host workers)
+        const int32_t T = (int32_t)std::max<size_t>(1, std::min<size_t>(8, n / 2048));
+        casim::parallel_run(T, [&](int32_t w) {
+            const size_t i0 = n * (size_t)w / (size_t)T, i1 = n * (size_t)(w + 1) / (size_t)T;
+            for (size_t i = i0; i < i1; i++) { fill_hot((int32_t)i, h[i]); fill_ext((int32_t)i, e[i]); }
+        });
+        if (dbg_t)
+            fprintf(stderr, "[sync_nodes]   filled %.3f ms\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         if (n) CA_HIP_CHECK(hipMemcpyAsync(d_hot.ptr, h, sizeof(NodeHot) * n, hipMemcpyHostToDevice, stream));
         if (n) CA_HIP_CHECK(hipMemcpyAsync(d_ext.ptr, e, sizeof(NodeExt) * n, hipMemcpyHostToDevice, stream));
         CA_HIP_CHECK(hipStreamSynchronize(stream));
@@ -767,7 +775,11 @@ int ca_mirror::sync_nodes() {
     }
     if (static_dirty && n) {
         std::vector<NodeStatic> s(n);
-        for (size_t i = 0; i < n; i++) fill_static((int32_t)i, s[i]);
+        const int32_t T = (int32_t)std::max<size_t>(1, std::min<size_t>(8, n / 2048));
+        casim::parallel_run(T, [&](int32_t w) {
+            const size_t i0 = n * (size_t)w / (size_t)T, i1 = n * (size_t)(w + 1) / (size_t)T;
+            for (size_t i = i0; i < i1; i++) fill_static((int32_t)i, s[i]);
+        });
         CA_HIP_CHECK(hipMemcpyAsync(d_static.ptr, s.data(), sizeof(NodeStatic) * n, hipMemcpyHostToDevice, stream));
         CA_HIP_CHECK(hipStreamSynchronize(stream));
     }

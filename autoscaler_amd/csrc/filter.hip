@@ -1520,8 +1520,33 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     bool fb = nn > 0 && !knob_env("CASIM_FO_WINDOW");
     const int32_t NW = (nn + 63) / 64;
     if (fb) {
+        // one pass over the node rows (host workers): the taints any node has, and the largest
+        // free cpu / memory / ephemeral of any node with a free pod slot (the dead-shape test below)
         uint64_t taint_union = 0;
-        for (const NodeRow& r : m->nodes) taint_union |= r.spec.taints;
+        int64_t mx_c = INT64_MIN, mx_m = INT64_MIN, mx_e = INT64_MIN;
+        {
+            const size_t N = m->nodes.size();
+            const int32_t T = (int32_t)std::max<size_t>(1, std::min<size_t>(8, N / 2048));
+            struct Part { uint64_t tu; int64_t c, mm, e; };
+            std::vector<Part> part((size_t)T, Part{0, INT64_MIN, INT64_MIN, INT64_MIN});
+            casim::parallel_run(T, [&](int32_t w) {
+                Part p{0, INT64_MIN, INT64_MIN, INT64_MIN};
+                const size_t i0 = N * (size_t)w / (size_t)T, i1 = N * (size_t)(w + 1) / (size_t)T;
+                for (size_t i = i0; i < i1; i++) {
+                    const NodeRow& nd = m->nodes[i];
+                    p.tu |= nd.spec.taints;
+                    if (clamp_i32(nd.spec.alloc_pods - nd.npods) < 1) continue;
+                    p.c = std::max(p.c, wsub(nd.spec.alloc_milli_cpu, nd.req_cpu));
+                    p.mm = std::max(p.mm, wsub(nd.spec.alloc_memory, nd.req_mem));
+                    p.e = std::max(p.e, wsub(nd.spec.alloc_ephemeral, nd.req_eph));
+                }
+                part[(size_t)w] = p;
+            });
+            for (const Part& p : part) {
+                taint_union |= p.tu;
+                mx_c = std::max(mx_c, p.c); mx_m = std::max(mx_m, p.mm); mx_e = std::max(mx_e, p.e);
+            }
+        }
         tmark("taints");
         struct KeyHash {
             size_t operator()(const std::string& k) const { return std::hash<std::string>()(k); }
@@ -1545,10 +1570,22 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
         fb_pods.resize((size_t)n);
         const ca_pod_spec* prev = nullptr;               // pods of one controller variant come in a row
         std::vector<int32_t> cls_seen((size_t)n_classes, -1);              // a similar class's first position
+        // which pods repeat the record before them (compared on the host workers first: the
+        // loop below then classifies only the first of each row)
+        std::vector<uint8_t> same((size_t)n, 0);
+        {
+            const int32_t T = std::max(1, std::min(8, n / 4096));
+            casim::parallel_run(T, [&](int32_t w) {
+                const int32_t k0 = (int32_t)((int64_t)n * w / T), k1 = (int32_t)((int64_t)n * (w + 1) / T);
+                for (int32_t k = std::max(k0, 1); k < k1; k++)
+                    same[(size_t)k] = std::memcmp(&t->pods[h_order[k - 1]], &t->pods[h_order[k]], sizeof(ca_pod_spec)) == 0;
+            });
+        }
         for (int32_t k = 0; k < n && fb; k++) {
             const ca_pod_spec& ps = t->pods[h_order[k]];
-            if (prev && std::memcmp(prev, &ps, sizeof ps) == 0) {          // the same record: same ids
+            if (prev && same[(size_t)k]) {                                 // the same record: same ids
                 fb_pods[k] = fb_pods[k - 1];
+                prev = &ps;
                 continue;
             }
             const int32_t sc = ps.similar_class;                           // (interleaved controllers)
@@ -1614,13 +1651,6 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
             // shapes beyond the largest free cpu / memory / ephemeral of any node with a free
             // pod slot fit no node: dead without the node walk below (RunOnce's backlog of
             // variants too large for every node would otherwise walk all nodes each)
-            int64_t mx_c = INT64_MIN, mx_m = INT64_MIN, mx_e = INT64_MIN;
-            for (const NodeRow& nd : m->nodes) {
-                if (clamp_i32(nd.spec.alloc_pods - nd.npods) < 1) continue;
-                mx_c = std::max(mx_c, wsub(nd.spec.alloc_milli_cpu, nd.req_cpu));
-                mx_m = std::max(mx_m, wsub(nd.spec.alloc_memory, nd.req_mem));
-                mx_e = std::max(mx_e, wsub(nd.spec.alloc_ephemeral, nd.req_eph));
-            }
             for (int32_t q = 0; q < S0; q++) {
                 const FbShape& sh = fb_shapes[q];
                 if (mx_c == INT64_MIN) continue;                               // no node has a slot

@@ -69,6 +69,8 @@ struct SweepScratch {
     // the host walk's table rounds: each round's compact rows (main and side rows), read in
     // place by the walk for the rest of the call; pooled across calls
     std::deque<HostBuf> rbuf;
+    // device mappings of h_todo and the round buffers (cleared whenever one of them moves)
+    std::vector<std::pair<void*, void*>> dmap;
     // the device pipeline of the last call shape, replayed as a graph (sweep.hip sweep_core)
     hipGraphExec_t gexec = nullptr;
     uint64_t gkey = 0, gseen = 0;

@@ -1317,7 +1317,11 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
     uint8_t* const h_need = reinterpret_cast<uint8_t*>(h_lin + C);
     const size_t Sx = (size_t)std::max(S, 1);
     if ((rc = sw.todo.reserve(sizeof(int32_t) * 12 * Sx)) != CA_OK) return rc;      // (a host round: 3 rows a candidate)
-    if ((rc = sw.h_todo.reserve(sizeof(int32_t) * 12 * Sx)) != CA_OK) return rc;
+    {
+        void* const was = sw.h_todo.ptr;
+        if ((rc = sw.h_todo.reserve(sizeof(int32_t) * 12 * Sx)) != CA_OK) return rc;
+        if (sw.h_todo.ptr != was) sw.dmap.clear();
+    }
     if ((rc = sw.tab.reserve(sizeof(int32_t) * 64 * Sx)) != CA_OK) return rc;
     if ((rc = sw.h_tab.reserve(sizeof(int32_t) * 64 * Sx)) != CA_OK) return rc;
     if ((rc = sw.wl.reserve(sizeof(int32_t) * (64 * Sx + 64 * (size_t)std::max(nch, 1)))) != CA_OK) return rc;
@@ -1798,13 +1802,22 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                 // and their two side rows) so a later call never regrows one.
                 if ((int32_t)sw.rbuf.size() <= round_buf) sw.rbuf.emplace_back();
                 HostBuf& rbuf = sw.rbuf[round_buf++];
+                void* const rb_was = rbuf.ptr;
                 if ((rc = rbuf.reserve(sizeof(int32_t) * (64 + FPW) * (size_t)std::max(T, 3 * LOOKAHEAD))) != CA_OK)
                     return rc;
+                if (rbuf.ptr != rb_was) sw.dmap.clear();
                 int32_t* const ct = rbuf.as<int32_t>();
                 void *d_ht = nullptr, *d_ct = nullptr;
-                const bool zc = !knob_env("CASIM_SWEEP_COPY_ROUNDS") &&
-                                hipHostGetDevicePointer(&d_ht, ht, 0) == hipSuccess &&
-                                hipHostGetDevicePointer(&d_ct, ct, 0) == hipSuccess;
+                // (the device mappings of the staging and of each pooled round buffer, looked
+                // up once per buffer: the runtime's lookup is a few µs per call)
+                auto dev_of = [&](void* h, void*& d) -> bool {
+                    for (const auto& e : sw.dmap)
+                        if (e.first == h) { d = e.second; return true; }
+                    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return false;
+                    sw.dmap.emplace_back(h, d);
+                    return true;
+                };
+                const bool zc = !knob_env("CASIM_SWEEP_COPY_ROUNDS") && dev_of(ht, d_ht) && dev_of(ct, d_ct);
                 if (!zc) {
                     (void)hipGetLastError();
                     CA_HIP_CHECK(hipMemcpyAsync(sw.todo.ptr, ht, sizeof(int32_t) * 3 * T, hipMemcpyHostToDevice, st));
@@ -1823,6 +1836,7 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
                                    (const int32_t*)d_mode, sw.bsum.as<BlockSum>());
                 CA_HIP_CHECK(hipGetLastError());
                 CA_HIP_CHECK(hipEventRecord(m->ev1, st));
+                tmark("table launched");
                 // compact rows (row t of this round): only they cross PCIe, then go to their
                 // places in the host copy, stored [lane][candidate] so the walk, whose class
                 // stays near the centre, reads it nearly sequentially

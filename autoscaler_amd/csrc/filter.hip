@@ -1407,16 +1407,17 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
             fprintf(stderr, "[filter] %-12s %8.3f ms\n", what,
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     };
+    // (one pass over the records: the arguments first, then the kernel scope)
+    bool oos = false;
     for (int32_t k = 0; k < n; k++) {
         const int32_t i = order ? order[k] : k;
         if (i < 0 || i >= t->n_pods) return CA_EINVAL;
         if (t->pods[i].similar_class >= n_classes) return CA_EINVAL;
+        oos |= (t->pods[i].flags & CA_POD_OUT_OF_SCOPE) != 0;
     }
     // casim.h kernel scope: an out-of-scope pending pod, or required anti-affinity in the
     // snapshot, sends the whole call to the Go path (nothing placed)
-    if (m->n_scope_blockers > 0) return CA_EUNSUPPORTED;
-    for (int32_t k = 0; k < n; k++)
-        if (t->pods[order ? order[k] : k].flags & CA_POD_OUT_OF_SCOPE) return CA_EUNSUPPORTED;
+    if (m->n_scope_blockers > 0 || oos) return CA_EUNSUPPORTED;
     if (n_overflowing) *n_overflowing = 0;
     if (n_placed) *n_placed = 0;
     FilterScratch& fo = m->fo;
@@ -1800,7 +1801,7 @@ int ca_filter_out_schedulable(ca_mirror* m, const ca_pod_table* t, const ca_pods
     const size_t pods0 = m->pods.size(), terms0 = m->terms.size(), reqs0 = m->reqs.size(), names0 = m->pf_names.size();
     const bool dev_in_sync = m->d_pods_synced == pods0 && (size_t)m->d_pods.n_pods == pods0 && m->d_terms_synced == terms0 &&
                              (size_t)m->d_pods.n_reqs == reqs0 && (size_t)m->d_pods.n_names == names0;
-    m->add_placed_batch(t, h_order, nodes_out, n, out_pod_id, fb);    // the walk flushed its rows to d_hot
+    m->add_placed_batch(t, h_order, nodes_out, n, out_pod_id, fb, s && !s->any_refs);   // the walk flushed its rows to d_hot
     // the new mirror records are the podset's records: gathered on the device instead of
     // crossing PCIe at the next sync (only when no selector tables had to be re-based)
     if (s && dev_in_sync && placed > 0 && m->pods.size() == pods0 + (size_t)placed && m->terms.size() == terms0 &&

@@ -298,7 +298,7 @@ struct ca_mirror {
     // device_rows: the caller's kernel already wrote the placed nodes' free resources to
     // d_hot (FilterOutSchedulable's bitmap walk), so they stay clean where fill_hot agrees
     void add_placed_batch(const ca_pod_table* t, const int32_t* idx, const int32_t* node, int32_t n,
-                          int32_t* out_id, bool device_rows = false);
+                          int32_t* out_id, bool device_rows = false, bool known_plain = false);
     int32_t store_moved_copy(int32_t pod);  // the copy findPlaceFor schedules (cluster.go:235-240)
     // the planner's committed moves, candidate by candidate: RemovePod of each moved pod,
     // then the copies (ids pods.size() + t, t-th move) AddPod'ed on their nodes; large
@@ -316,6 +316,7 @@ struct ca_podset {
     casim::DevPodTable t;
     int32_t n_host = 0;                // pods in the set
     bool any_oos = false;              // some pod carries CA_POD_OUT_OF_SCOPE (no host copy of the records)
+    bool any_refs = false;             // some pod references selector terms or PreFilter names
     // Score classes: pods with equal (score_milli_cpu, score_memory) — the only inputs of
     // calculatePodScore (binpacking_estimator.go:164-193) — share a class, numbered in
     // first-occurrence order.  d_cls[pod] = class, d_cls_sc[c] = {score_milli_cpu,

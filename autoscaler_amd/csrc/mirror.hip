@@ -480,7 +480,7 @@ void ca_mirror::reserve_more(size_t n_pods_add, size_t n_journal_add) {
 }
 
 void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, const int32_t* node, int32_t n,
-                                 int32_t* out_id, bool device_rows) {
+                                 int32_t* out_id, bool device_rows, bool known_plain) {
     const bool dbg_t = knob_env("CASIM_DEBUG_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     auto tmark = [&](const char* what) {
@@ -490,9 +490,11 @@ void ca_mirror::add_placed_batch(const ca_pod_table* t, const int32_t* idx, cons
     };
     int32_t np = 0;
     bool plain = true;                      // no selector tables or PreFilter names to re-base
+    // (known_plain: the caller's pod set holds no such references — no record reads here)
     for (int32_t k = 0; k < n; k++) {
         if (node[k] < 0) continue;
         np++;
+        if (known_plain) continue;
         const ca_pod_spec& ps = t->pods[idx[k]];
         if (ps.aff_term_count > 0 || ((ps.flags & CA_POD_PREFILTER_NAMES) && ps.prefilter_count > 0)) plain = false;
     }
@@ -1305,6 +1307,7 @@ int ca_podset_create(ca_mirror* m, const ca_pod_table* t, ca_podset** out) {
     for (int32_t i = 0; i < t->n_pods; i++) {
         const ca_pod_spec& ps = t->pods[i];
         s->any_oos |= (ps.flags & CA_POD_OUT_OF_SCOPE) != 0;
+        s->any_refs |= ps.aff_term_count > 0 || ((ps.flags & CA_POD_PREFILTER_NAMES) && ps.prefilter_count > 0);
         s->h_req[2 * (size_t)i] = ps.req_milli_cpu;
         s->h_req[2 * (size_t)i + 1] = ps.req_memory;
         const uint32_t f = pod_dev_flags(ps);

@@ -667,7 +667,14 @@ __global__ void __launch_bounds__(SQ_T) k_filter_out(FoArgs a) {
 constexpr int FB_MAX_SHAPES = 64;        // one lane per shape for the bit updates
 constexpr int FB_COLLECT_SHAPES = 1024;  // distinct shapes looked at before the dead ones are merged
 constexpr int FB_T = 64;                 // the walk is one wavefront
-constexpr int FB_ROWWISE_MAX = 24;       // mixed runs shorter than this update the bitmaps row by row
+#ifndef CASIM_FB_ROWWISE_MAX
+#define CASIM_FB_ROWWISE_MAX 24
+#endif
+#ifndef CASIM_FB_BACKOFF
+#define CASIM_FB_BACKOFF 1
+#endif
+constexpr int FB_ROWWISE_MAX = CASIM_FB_ROWWISE_MAX;   // mixed runs shorter than this update the bitmaps row by row
+constexpr int FB_BACKOFF = CASIM_FB_BACKOFF;           // pods a short mixed run (< 2 placed) skips before the next try
 constexpr size_t FB_LDS_MAX = 160 * 1024;
 
 struct alignas(16) FbPod {               // per pending position (the walk order)
@@ -1168,7 +1175,7 @@ __global__ void __launch_bounds__(FB_T) k_fb_walk(FbArgs a) {
 #endif
                     }
                 }
-                if (f < 2) bulk_from = base + j + 16;
+                if (f < 2) bulk_from = base + j + FB_BACKOFF;
                 if (f > 0) {
 #ifdef CASIM_PROF
                     prof_fb[2] += clock64() - pc0;

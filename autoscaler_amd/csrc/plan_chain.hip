@@ -161,7 +161,7 @@ struct PcBlk {
 // lane q checks block q — reads every point with one conflict-free access per lane, all of
 // them issued at once.
 #ifndef CASIM_PC_SKY
-#define CASIM_PC_SKY 8
+#define CASIM_PC_SKY 6
 #endif
 constexpr int PC_SKY = CASIM_PC_SKY;
 struct PcSkyV {
@@ -393,6 +393,15 @@ __device__ inline PcTabs pc_tabs(const PcArgs& a) { return PcTabs{a.st, a.specs,
 // their maxima were stale get the exact maxima (`refr` tells the chain which).  The chain
 // then takes the fit at `best` and counts the visible nodes before it as evaluations —
 // exactly the scan's outcome, in a fraction of its dependent steps.
+// the bulk step's back-off: after PC_BULK_FAILS candidates in a row whose first bulk step
+// placed nothing, the next PC_BULK_SKIP candidates start with the plain run
+#ifndef CASIM_PC_BULK_FAILS
+#define CASIM_PC_BULK_FAILS 3
+#endif
+#ifndef CASIM_PC_BULK_SKIP
+#define CASIM_PC_BULK_SKIP 32
+#endif
+constexpr int PC_BULK_FAILS = CASIM_PC_BULK_FAILS, PC_BULK_SKIP = CASIM_PC_BULK_SKIP;
 constexpr int PC_HELP_AFTER = 2;       // blocks the chain loads itself before handing off
 struct PcHelp {
     int32_t seq, quit, done, best;
@@ -1210,8 +1219,8 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
         {
             int32_t t = 0;
             // the bulk step pays off in a loose cluster; in a tight one it keeps failing at the
-            // first pod: after 4 candidates in a row whose first bulk step placed nothing, the
-            // next 16 candidates start with the plain run
+            // first pod: after PC_BULK_FAILS candidates in a row whose first bulk step placed nothing,
+            // the next PC_BULK_SKIP candidates start with the plain run
             int32_t bfail = __builtin_amdgcn_readfirstlane(ctx->bulk_fail);
             int32_t bskip = __builtin_amdgcn_readfirstlane(ctx->bulk_skip);
             bool try_bulk = bskip == 0;
@@ -1224,7 +1233,7 @@ __device__ __attribute__((always_inline)) inline void pc_simulate(const PcArgs& 
                     if (first_bulk) {
                         first_bulk = false;
                         if (k > 0) bfail = 0;
-                        else if (++bfail >= 4) { bfail = 0; bskip = 16; }
+                        else if (++bfail >= PC_BULK_FAILS) { bfail = 0; bskip = PC_BULK_SKIP; }
                     }
                     placed += k;
                     t += k;

@@ -1,6 +1,6 @@
 """A/B of two builds of the library on the C5 RunOnce loop's legs: alternating processes,
 each running 5 loops (fork, runonce.run, revert) and printing the median of the last 4 per
-leg.  Usage: python scripts/ab_runonce.py LIB_A LIB_B [rounds]"""
+leg.  Usage: python scripts/ab_runonce.py LIB_A LIB_B [LIB ...] [rounds]"""
 import json
 import os
 import subprocess
@@ -27,8 +27,9 @@ for _ in range(5):
 print(json.dumps({k: float(np.median([r.ms[k] for r in runs[1:]])) for k in runs[-1].ms}))
 """ % ROOT
 
-libs = sys.argv[1:3]
-rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+args = sys.argv[1:]
+rounds = int(args.pop()) if args and args[-1].isdigit() else 3
+libs = args
 res = {lib: [] for lib in libs}
 for r in range(rounds):
     for lib in libs:

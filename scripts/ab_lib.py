@@ -1,6 +1,6 @@
 """A/B of two builds of the library on the bench's headline step (C2, results on the host
 as 16-bit podset indices, phase events off): alternating processes, each timing 40 steps
-after warmup.  Usage: python scripts/ab_lib.py LIB_A LIB_B [rounds]"""
+after warmup.  Usage: python scripts/ab_lib.py LIB_A LIB_B [LIB ...] [rounds]"""
 import os
 import subprocess
 import sys
@@ -28,8 +28,9 @@ with native.EstimatePlan(m, w.table, w.group_off, w.pod_idx, w.templates) as pla
     print(ts[len(ts) // 2], ts[0])
 """ % ROOT
 
-libs = sys.argv[1:3]
-rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+args = sys.argv[1:]
+rounds = int(args.pop()) if args and args[-1].isdigit() else 3
+libs = args
 res = {lib: [] for lib in libs}
 for r in range(rounds):
     for lib in libs:

@@ -37,7 +37,10 @@ namespace casim {
 constexpr int PC_LIST = CA_MAX_MOVED_PODS;   // pods to move per candidate (larger: prefix cut)
 constexpr size_t PC_LDS_MAX = 163840;         // gfx950: one workgroup may own the CU's 160 KiB
 constexpr int32_t PC_MAX_NODES = 8192;        // two 64-bit words of per-block dirty bits
-constexpr int32_t PC_MVBUF = 512;             // moves staged in LDS between global writes
+#ifndef CASIM_PC_MVBUF
+#define CASIM_PC_MVBUF 512
+#endif
+constexpr int32_t PC_MVBUF = CASIM_PC_MVBUF;  // moves staged in LDS between global writes
 constexpr int PC_MAX_WAVES = 8;               // the chain wave + up to 7 helper waves (VGPR budget: 2 waves / SIMD)
 // shader-clock counters of the chain's phases (info[4 + k]; CASIM_PROF builds only)
 enum { PC_INIT, PC_LISTS, PC_PDB, PC_FORK, PC_HINT, PC_SCAN, PC_ADD, PC_COMMIT, PC_REVERT, PC_TOTAL, PC_BLOCKS,

@@ -1726,7 +1726,11 @@ int sweep_core(ca_mirror* m, const SweepCall& in, int32_t* hints, int32_t* d_pod
         // the device walk's re-runs already happened: only candidates from k0 on remain
         // each round looks LOOKAHEAD candidates ahead: the estimates drift with the distance
         // from the exact lastIndex, so rows further out would be re-centred again anyway
-        static const int32_t LOOKAHEAD = knob_env("CASIM_SWEEP_LOOKAHEAD") ? std::max(64, atoi(knob_env("CASIM_SWEEP_LOOKAHEAD"))) : 512;
+#ifndef CASIM_SWEEP_LOOKAHEAD_ROWS
+#define CASIM_SWEEP_LOOKAHEAD_ROWS 512
+#endif
+        static const int32_t LOOKAHEAD = knob_env("CASIM_SWEEP_LOOKAHEAD") ? std::max(64, atoi(knob_env("CASIM_SWEEP_LOOKAHEAD")))
+                                                                          : CASIM_SWEEP_LOOKAHEAD_ROWS;
         // Serial exact chain: when a table round resolves few candidates for its cost (late
         // planner windows over a nearly full cluster: long scans that no lane budget covers,
         // windows that miss again after every re-centring), the next candidates run exactly

@@ -9,4 +9,10 @@ export TMPDIR=/tmp
 timeout -k 10 900 python -u scripts/ab_planner.py autoscaler_amd/lib/libcasim.so autoscaler_amd/lib/mv1024/libcasim.so \
   autoscaler_amd/lib/mv2048/libcasim.so --rounds 4 > gpurun_out/ab_mv.txt 2>&1; rc=$?
 cat gpurun_out/ab_mv.txt
+[[ $rc -eq 0 ]] || exit $rc
+# (and the sweep's look-ahead rows per table round: 256 / 384 / 768 against 512, RunOnce legs;
+#  variant builds OUT=../lib/la<N> "EXTRA=-DCASIM_SWEEP_LOOKAHEAD_ROWS=<N>")
+timeout -k 10 900 python -u scripts/ab_runonce.py autoscaler_amd/lib/libcasim.so autoscaler_amd/lib/la256/libcasim.so \
+  autoscaler_amd/lib/la384/libcasim.so autoscaler_amd/lib/la768/libcasim.so 4 > gpurun_out/ab_la.txt 2>&1; rc=$?
+grep median gpurun_out/ab_la.txt
 exit $rc

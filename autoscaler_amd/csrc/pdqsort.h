@@ -517,7 +517,10 @@ template <class S> __device__ void w_sort(const S& s, int a, int b, int lf) {
 // ---------------------------------------------------------------------------------
 // workgroup steps
 // ---------------------------------------------------------------------------------
-constexpr int T_SMALL = 1024;        // frames up to this length wait for the wavefront phase
+#ifndef CASIM_PDQ_T_SMALL
+#define CASIM_PDQ_T_SMALL 2048
+#endif
+constexpr int T_SMALL = CASIM_PDQ_T_SMALL;   // frames up to this length wait for the wavefront phase
 
 struct Ctl {
     Frame f[MAXF];

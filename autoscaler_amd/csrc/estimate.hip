@@ -761,7 +761,10 @@ __host__ __device__ inline size_t pdq_lds_bytes(int32_t lds_n) {
     return (3 * np + np / 8 + 2 * (np / 64 + 1) + 15) & ~(size_t)15;
 }
 
-constexpr int PDQ_UB = 8;              // list positions per thread whose gathers are in flight together
+#ifndef CASIM_PDQ_UB
+#define CASIM_PDQ_UB 8
+#endif
+constexpr int PDQ_UB = CASIM_PDQ_UB;   // list positions per thread whose gathers are in flight together
 __global__ void __launch_bounds__(pdq::NT) k_pdq_sort(const GroupMeta* __restrict__ groups,
                                                      const int32_t* __restrict__ pod_idx,
                                                      const int32_t* __restrict__ pcls,

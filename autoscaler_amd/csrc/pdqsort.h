@@ -75,7 +75,10 @@ __device__ unsigned long long g_pdq_wg[3 * 128];
 
 constexpr int NT = 1024;             // threads of the workgroup
 constexpr int NW = NT / 64;          // wavefronts
-constexpr int MAXF = 96;             // frames per workgroup step
+#ifndef CASIM_PDQ_MAXF
+#define CASIM_PDQ_MAXF 96
+#endif
+constexpr int MAXF = CASIM_PDQ_MAXF; // frames per workgroup step
 constexpr int PIS_WAVE_MAX = 4096;   // LDS store: longer frames run partialInsertionSort on the workgroup
 constexpr int MAX_INSERTION = 12;    // pdqsort_func maxInsertion
 enum { HINT_UNKNOWN = 0, HINT_INC = 1, HINT_DEC = 2 };

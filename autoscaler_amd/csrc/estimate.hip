@@ -1374,7 +1374,10 @@ __device__ inline int32_t run_end_pf(const uint64_t* __restrict__ hm, int32_t po
 // chain's critical path.  Other chunks (single placements, a segment boundary with another
 // offset, the group's tail) go with the release and the progress record.
 constexpr int PCH = 4096;      // default chunk (CASIM_PUB_CHUNK overrides, for tests)
-constexpr int PCH_DECOUPLED = 8192;    // ... with the decoupled Go order (scripts/gpu_pubsweep2.sh)
+#ifndef CASIM_PCH_DECOUPLED
+#define CASIM_PCH_DECOUPLED 16384
+#endif
+constexpr int PCH_DECOUPLED = CASIM_PCH_DECOUPLED;   // ... with the decoupled Go order (scripts/gpu_pubsweep2.sh)
 __device__ inline void push_chunks(int32_t g, int32_t c0, int32_t c1, int32_t nsub, int64_t* tickets, int32_t* qctl,
                                    int2* prog, int32_t nseg, int32_t nsched, int lane, int32_t pch = 0,
                                    int32_t pure_from = INT32_MAX, int32_t pure_off = 0) {

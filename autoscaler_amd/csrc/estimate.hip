@@ -2922,11 +2922,15 @@ int launch_pdq_sort(ca_estimate_plan* p, hipStream_t ss, const int32_t* gm, int3
 int32_t pub_blocks(bool decoupled) {
     const char* e = knob_env("CASIM_PUB_BLOCKS");
     // scripts/pub_sweep.sh on C2: stable order 32 x 4096-output chunks; decoupled Go order
-    // 128 x 8192 (round 4: each group's ids are ready when its own sort ends, from ~0.17 ms
+    // 128 x 8192 in round 4 (each group's ids are ready when its own sort ends, from ~0.17 ms
     // on; more blocks in flight keep a block waiting on a late group from holding up the
     // ready ones — 0.474 against 0.478 ms for 64 x 16384, interleaved repeats,
-    // scripts/gpu_pubsweep2.sh)
-    return e ? std::max(1, atoi(e)) : (decoupled ? 128 : 32);
+    // scripts/gpu_pubsweep2.sh); with round 6's chains and sort, 64 x 16384 (A/Bs of variant
+    // builds: profiles/r06_pub_chunk_ab.txt, r06_pub_blocks_ab.txt)
+#ifndef CASIM_PUB_BLOCKS_DECOUPLED
+#define CASIM_PUB_BLOCKS_DECOUPLED 64
+#endif
+    return e ? std::max(1, atoi(e)) : (decoupled ? CASIM_PUB_BLOCKS_DECOUPLED : 32);
 }
 
 size_t chain_lds_bytes(int32_t kcap, bool use_ports, bool use_scalar) {
